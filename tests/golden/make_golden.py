@@ -1,0 +1,152 @@
+#!/usr/bin/env python3
+"""Generate golden vectors for the five hot-path tools by running the REFERENCE binaries
+(built from /root/reference sources by oracle/Makefile.ref into oracle/_ref/) over the
+fixtures in tests/golden/data/, in both input modes.
+
+Writes tests/golden/cases.json.gz: the case list, expected exit codes, sha256/length of
+stdout and stderr, and (base64) the raw bytes of outputs <= 16 KiB.
+Run from anywhere; all tools run with cwd=tests/golden and relative fixture paths so
+file names printed by the tools are stable.  argv[0] is the bare tool name.
+"""
+import base64
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = os.path.join(REPO, "oracle", "_ref")
+INLINE_MAX = 16 * 1024
+
+AF, RF, GQ, LD, VC = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query",
+                      "VCFX_ld_calculator", "VCFX_variant_counter")
+
+
+def fixtures():
+    names = sorted(os.listdir(os.path.join(HERE, "data")))
+    out = [os.path.join("data", n) for n in names if n.endswith(".vcf") or n.endswith(".gz")]
+    out += [os.path.join("data", "ref", n) for n in sorted(os.listdir(os.path.join(HERE, "data", "ref")))]
+    return out
+
+
+def build_cases():
+    cases = []
+
+    def add(tool, args, stdin=None, tag=None):
+        name = "%s__%s" % (tool[5:], tag or "_".join(a.replace("/", "-").replace(" ", "") for a in args) or "noargs")
+        name = "".join(c if c.isalnum() or c in "._-=+" else "_" for c in name)
+        if stdin:
+            name += "__stdin_" + os.path.basename(stdin)
+        base, k = name, 1
+        while any(c["name"] == name for c in cases):
+            k += 1
+            name = "%s_%d" % (base, k)
+        cases.append({"name": name, "tool": tool, "argv": [tool] + list(args), "stdin": stdin})
+
+    fx = fixtures()
+    vcfs = [f for f in fx if f.endswith(".vcf")]
+    big = {"data/synth_regular.vcf"}
+    # ---- allele_freq_calc
+    for f in vcfs:
+        add(AF, ["-i", f])
+        add(AF, [], stdin=f)
+        add(AF, ["-q", f])
+    for a in (["-h"], ["--help"], ["-v"], ["--version"], ["--bogus"], ["-x"], ["-i"], ["-i", "data/nope.vcf"]):
+        add(AF, a)
+    add(AF, [], stdin="data/empty.vcf", tag="empty_stdin")
+    add(AF, ["-q"], stdin="data/ties.vcf")
+    # ---- variant_counter
+    for f in vcfs + [g for g in fx if g.endswith(".gz")]:
+        if not f.endswith(".gz"):
+            add(VC, [f])
+            add(VC, ["--strict", f])
+        add(VC, [], stdin=f)
+        add(VC, ["-s"], stdin=f)
+    for a in (["-h"], ["-v"], ["--bogus"], ["data/nope.vcf"]):
+        add(VC, a)
+    # ---- genotype_query
+    queries = [["-g", "0/1"], ["-g", "1|1", "--strict"], ["-g", "0|1", "--strict"], ["-g", "1/0"], ["-g", "0/0"],
+               ["-g", "1/2"], ["-g", "2|1"], ["-g", "1/x"], ["-g", "x/1"], ["-g", "0"], ["-g", "./."],
+               ["-g", "10/1"], ["-g", "0/10"], ["-g", "00/1"], ["--genotype-query=1|1"], ["-g", "1/1", "-q"],
+               ["-g", "0/1", "--strict"], ["-g", "./.", "--strict"], ["-g", "1", "--strict"]]
+    for f in vcfs:
+        qs = queries if f not in big else queries[:4]
+        for q in qs:
+            add(GQ, q + ["-i", f])
+            add(GQ, q, stdin=f)
+        add(GQ, ["-g", "0/1", f])
+    for a in (["-h"], ["-v"], ["--vers"], [], ["-g"], ["-s", "-g", "0/1"], ["-g", "0/1", "-i", "data/nope.vcf"]):
+        add(GQ, a)
+    # ---- record_filter
+    filters = ["QUAL>=90", "AF>=0.2", "FILTER==PASS", "POS>=30000", "DP>=40", "DP>10", "QUAL<50", "FLAG==FLAG",
+               "FLAG>0", "AF!=0.1", "QUAL==0", "FILTER!=PASS", "POS>0x5", "AF>=0.01;DP<=100", "AF<0.05",
+               " QUAL > 20 ; FILTER == PASS ", "AF>=0.2;FILTER==PASS", "FILTER>PASS", "AF==nan", "DP==inf",
+               "AF>=0.0001", "QUAL>=1e2", "POS<=1500", "AF>.2", "AF>=-0"]
+    for f in vcfs:
+        fl = filters if f not in big else filters[:3]
+        for flt in fl:
+            add(RF, ["--filter", flt, "-i", f])
+            add(RF, ["-f", flt], stdin=f)
+        add(RF, ["--filter", "QUAL>=50;AF>=0.2", "--logic", "or", f])
+        add(RF, ["--filter", "QUAL>=50;AF>=0.2", "-l", "or"], stdin=f)
+    for a in ([], ["-h"], ["-v"], ["-q"], ["--filter", "QUAL"], ["--filter", "=5"], ["--filter", "QUAL>="],
+              ["--filter", "QUAL>1", "--logic", "xor"], ["--filter", ";;"], ["--filter", "QUAL>1", "data/nope.vcf"],
+              ["--filter", "QUAL>1", "-"]):
+        add(RF, a, stdin="data/ref/record_filter_input.vcf" if a[-1:] == ["-"] else None)
+    # ---- ld_calculator
+    ldsets = [["-w", "1000"], ["-w", "1"], ["-w", "3"], ["-t", "0.5"], ["-t", "0.2", "-w", "2"], ["-d", "150"],
+              ["-r", "1:100-1000"], ["-r", "21:9411239-9420000"], ["-m"], ["-m", "-r", "1:150-500"]]
+    for f in vcfs:
+        if f in big:
+            continue
+        for a in ldsets:
+            add(LD, a + ["-i", f])
+            add(LD, a, stdin=f)
+    for a in (["-h"], ["-v"], ["--versi"], ["-w", "x"], ["-t", "y"], ["-r", "bad"], ["-r", "1:9-2"], ["-t", "1e-400"],
+              ["-i", "data/empty.vcf"], ["-i", "data/nope.vcf"], ["-w", "-1", "-i", "data/synth_ld.vcf"],
+              ["-t", "2", "-i", "data/synth_ld.vcf"], ["-t", "nan", "-i", "data/synth_ld.vcf"], ["-n", "q"],
+              ["-d", "-5", "-i", "data/synth_ld.vcf"], ["-w", "0", "-i", "data/synth_ld.vcf"]):
+        add(LD, a)
+    return cases
+
+
+def run_case(c, exe_dir=REF):
+    exe = os.path.join(exe_dir, c["tool"])
+    stdin = open(os.path.join(HERE, c["stdin"]), "rb") if c["stdin"] else subprocess.DEVNULL
+    try:
+        p = subprocess.run(c["argv"], executable=exe, cwd=HERE, stdin=stdin, stdout=subprocess.PIPE,
+                           stderr=subprocess.PIPE, timeout=300)
+    finally:
+        if c["stdin"]:
+            stdin.close()
+    return p.stdout, p.stderr, p.returncode
+
+
+def digest(b):
+    return {"sha256": hashlib.sha256(b).hexdigest(), "len": len(b)}
+
+
+def main():
+    if not os.path.isdir(REF):
+        sys.exit("oracle/_ref missing: make -f oracle/Makefile.ref")
+    cases = build_cases()
+    for c in cases:
+        out, err, rc = run_case(c)
+        c["rc"] = rc
+        c["out"] = digest(out)
+        c["err"] = digest(err)
+        if len(out) <= INLINE_MAX:
+            c["out"]["b64"] = base64.b64encode(out).decode()
+        if len(err) <= INLINE_MAX:
+            c["err"]["b64"] = base64.b64encode(err).decode()
+    with gzip.GzipFile(os.path.join(HERE, "cases.json.gz"), "wb", mtime=0) as f:
+        f.write(json.dumps({"generator": "tests/golden/make_golden.py (reference binaries, oracle/Makefile.ref)",
+                            "cases": cases}, indent=0).encode())
+    print("%d cases" % len(cases))
+
+
+if __name__ == "__main__":
+    main()

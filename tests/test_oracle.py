@@ -1,0 +1,84 @@
+"""The C restatement oracle is pinned to the reference before anything is checked
+against it: (1) every golden vector produced by the reference binaries (built from
+/root/reference sources, tests/golden/make_golden.py) and (2) the reference's own
+committed expected outputs (copied as data into tests/golden/data/ref_expected/)."""
+import collections
+import os
+
+import pytest
+
+from tests._golden import GOLDEN, Oracle, case_stdin, load_cases, matches
+
+CASES = load_cases()
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return Oracle()
+
+
+def test_case_count():
+    tools = collections.Counter(c["tool"] for c in CASES)
+    assert len(tools) == 5 and min(tools.values()) > 40
+
+
+@pytest.mark.parametrize("tool", sorted({c["tool"] for c in CASES}))
+def test_oracle_matches_reference_goldens(oracle, tool):
+    bad = []
+    for c in CASES:
+        if c["tool"] != tool:
+            continue
+        out, err, rc = oracle.run(list(c["argv"]), case_stdin(c), cwd=GOLDEN)
+        if rc != c["rc"] or not matches(c["out"], out) or not matches(c["err"], err):
+            bad.append(c["name"])
+    assert not bad, "%d/%d mismatches, first: %s" % (len(bad), len(CASES), bad[:10])
+
+
+REF_EXP = [
+    # (reference test command, expected file) -- tests/test_allele_freq_calc.sh, test_record_filter.sh,
+    # test_variant_counter.sh in jorgeMFS/VCFX
+    (["VCFX_allele_freq_calc"], "ref/afc_simple.vcf", "afc_simple.tsv"),
+    (["VCFX_allele_freq_calc"], "ref/afc_multiallelic.vcf", "afc_multiallelic.tsv"),
+    (["VCFX_allele_freq_calc"], "ref/afc_missing.vcf", "afc_missing.tsv"),
+    (["VCFX_allele_freq_calc"], "ref/afc_phased.vcf", "afc_phased.tsv"),
+    (["VCFX_allele_freq_calc"], "ref/afc_complex.vcf", "afc_complex.tsv"),
+    (["VCFX_record_filter", "--filter", "QUAL>=90"], "ref/record_filter_input.vcf", "record_filter_qual.vcf"),
+    (["VCFX_record_filter", "--filter", "AF>=0.2"], "ref/record_filter_input.vcf", "record_filter_af.vcf"),
+    (["VCFX_record_filter", "--filter", "FILTER==PASS"], "ref/record_filter_input.vcf", "record_filter_pass.vcf"),
+    (["VCFX_record_filter", "--filter", "FILTER==PASS;AF>=0.2", "--logic", "and"], "ref/record_filter_input.vcf",
+     "record_filter_multiple_and.vcf"),
+    (["VCFX_record_filter", "--filter", "QUAL>=50;AF>=0.2", "--logic", "or"], "ref/record_filter_input.vcf",
+     "record_filter_multiple_or.vcf"),
+    (["VCFX_record_filter", "--filter", "POS>=30000", "data/ref/record_filter_input.vcf"], None,
+     "record_filter_pos.vcf"),
+    (["VCFX_record_filter", "--filter", "DP>=40", "data/ref/record_filter_input.vcf"], None, "record_filter_dp.vcf"),
+    (["VCFX_variant_counter"], "ref/variant_counter_normal.vcf", "variant_counter_normal.txt"),
+    (["VCFX_variant_counter"], "ref/variant_counter_large.vcf", "variant_counter_large.txt"),
+    (["VCFX_variant_counter"], "ref/variant_counter_empty.vcf", "variant_counter_empty.txt"),
+]
+
+
+@pytest.mark.parametrize("argv,stdin,expected", REF_EXP)
+def test_oracle_matches_reference_committed_expected(oracle, argv, stdin, expected):
+    if expected is None:
+        pytest.skip("no committed expected file")
+    data = open(os.path.join(GOLDEN, "data", stdin), "rb").read() if stdin else b""
+    out, err, rc = oracle.run(argv, data, cwd=GOLDEN)
+    want = open(os.path.join(GOLDEN, "data", "ref_expected", expected), "rb").read()
+    assert out == want
+
+
+def test_af_known_answers(oracle):
+    # test_allele_freq_calc.sh:219  verify_frequencies simple 0.5000 0.3333 0.3333 0.8333
+    data = open(os.path.join(GOLDEN, "data", "ref", "afc_simple.vcf"), "rb").read()
+    out, _, _ = oracle.run(["VCFX_allele_freq_calc"], data)
+    freqs = [l.split(b"\t")[-1] for l in out.splitlines()[1:]]
+    assert freqs == [b"0.5000", b"0.3333", b"0.3333", b"0.8333"]
+
+
+def test_af_tie_modes_differ(oracle):
+    # 1 ALT of 32 prints 0.0313 (mmap writeDouble4) vs 0.0312 (stdin printf)
+    data = open(os.path.join(GOLDEN, "data", "ties.vcf"), "rb").read()
+    out_s, _, _ = oracle.run(["VCFX_allele_freq_calc"], data)
+    out_m, _, _ = oracle.run(["VCFX_allele_freq_calc", "-q", "-i", "data/ties.vcf"], b"", cwd=GOLDEN)
+    assert out_s.splitlines()[1].endswith(b"0.0312") and out_m.splitlines()[1].endswith(b"0.0313")
