@@ -1,0 +1,54 @@
+# vcfx_amd build: HIP engine (libvcfx_gpu.so, gfx950), host core + tool binaries, synthetic
+# generator.  Outputs under build/ (git-ignored, shipped to the GPU box by gpurun).
+# The oracle (test infrastructure) has its own makefiles under oracle/.
+HIPCC ?= /opt/rocm/bin/hipcc
+CXX ?= g++
+CC ?= gcc
+ARCH ?= gfx950
+B := build
+GPU_SRC := vcfx_amd/csrc/gpu
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -I$(GPU_SRC)
+GPU_OBJS := $(B)/obj/vcfxg_kernels.o $(B)/obj/vcfxg_api.o
+
+TOOLS := VCFX_allele_freq_calc
+HOST_SRC := vcfx_amd/csrc/host
+TOOL_SRC := vcfx_amd/csrc/tools
+CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wno-unused-result -Iinclude -I$(HOST_SRC) -I$(TOOL_SRC)
+TOOL_OBJS := $(sort $(B)/obj/hostio.o $(patsubst $(TOOL_SRC)/%.cpp,$(B)/obj/%.o,$(wildcard $(TOOL_SRC)/tool_*.cpp)))
+TOOL_BINS := $(foreach t,$(TOOLS),$(B)/src/$(t)/$(t))
+
+all: $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so
+
+$(B)/obj/%.o: $(HOST_SRC)/%.cpp $(wildcard $(HOST_SRC)/*.h) include/vcfx_gpu.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c -o $@ $<
+
+$(B)/obj/%.o: $(TOOL_SRC)/%.cpp $(wildcard $(TOOL_SRC)/*.h) $(wildcard $(HOST_SRC)/*.h) include/vcfx_gpu.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c -o $@ $<
+
+$(B)/libvcfx_tools.so: $(TOOL_OBJS) $(B)/libvcfx_gpu.so
+	$(CXX) -shared -o $@ $(TOOL_OBJS) -L$(B) -lvcfx_gpu -Wl,-rpath,'$$ORIGIN'
+
+# drop-in executables at build/src/VCFX_<t>/VCFX_<t> (the reference test scripts' layout)
+$(B)/src/%: $(TOOL_SRC)/binary_main.cpp $(B)/libvcfx_tools.so
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -DVCFX_TOOL_NAME='"$(notdir $@)"' -o $@ $< -L$(B) -lvcfx_tools -lvcfx_gpu -Wl,-rpath,'$$ORIGIN/../..'
+
+$(B)/obj/vcfxg_%.o: $(GPU_SRC)/vcfxg_%.hip $(wildcard $(GPU_SRC)/*.h) include/vcfx_gpu.h
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(B)/libvcfx_gpu.so: $(GPU_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+$(B)/bin/vcfx_synth: vcfx_amd/csrc/synth/vcfx_synth.c
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -DVCFX_SYNTH_MAIN -o $@ $< -lpthread
+
+$(B)/libvcfx_synth.so: vcfx_amd/csrc/synth/vcfx_synth.c
+	$(CC) -O2 -fPIC -shared -o $@ $< -lpthread
+
+clean:
+	rm -rf $(B)
+.PHONY: all clean

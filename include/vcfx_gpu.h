@@ -1,0 +1,106 @@
+/*
+ * vcfx_gpu.h -- C ABI of the MI355X VCF record engine (libvcfx_gpu.so).
+ *
+ * The drop-in boundary for VCFX's per-line hot path.  The reference has no FFI for this
+ * path: its callers reach it through the VCFX_<tool> processes, whose
+ * main()s are re-implemented in vcfx_amd/csrc/tools/ on top of this ABI.  Each entry
+ * point below names the reference function(s) whose per-record work it replaces.
+ *
+ * Conventions: plain pointers and sizes; every function returns VCFXG_OK (0) or a
+ * negative vcfxg_status and never throws; buffers are caller-owned unless stated; one
+ * vcfxg_ctx per device, used by one host thread; all work is ordered on the context's
+ * HIP stream (vcfxg_stream()).  There is no CPU fallback: without a usable gfx950 device
+ * vcfxg_open() fails with VCFXG_E_NODEV.
+ */
+#ifndef VCFX_GPU_H
+#define VCFX_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct vcfxg_ctx vcfxg_ctx;
+
+enum vcfxg_status {
+    VCFXG_OK = 0,
+    VCFXG_E_NODEV = -1,   /* no HIP device / not gfx950 */
+    VCFXG_E_HIP = -2,     /* HIP runtime error (vcfxg_last_error has the text) */
+    VCFXG_E_ARG = -3,     /* bad argument */
+    VCFXG_E_NOMEM = -4,   /* device or host allocation failed */
+    VCFXG_E_STATE = -5,   /* call out of order (e.g. no input loaded / not indexed) */
+    VCFXG_E_CAP = -6      /* caller buffer too small */
+};
+
+/* input semantics of the reference tools: file = the mmap path, stdin = the getline path */
+enum vcfxg_mode { VCFXG_MODE_FILE = 0, VCFXG_MODE_STDIN = 1 };
+
+/* per-line status codes written by the record kernels (one byte per line of the indexed
+ * region) */
+enum vcfxg_line_status {
+    VCFXG_LINE_SKIP = 0,     /* empty, '#' header, or a data line the tool skips silently */
+    VCFXG_LINE_ROW = 1,      /* data line that produces output (AF row / kept record) */
+    VCFXG_LINE_DROP = 2,     /* data line evaluated and not kept (filters) */
+    VCFXG_LINE_WARN = 3,     /* data line the tool reports on stderr ("fewer than 9 fields") */
+    VCFXG_LINE_HEADER = 4    /* '#' line (pass-through tools print it) */
+};
+
+typedef struct {
+    uint64_t n_lines;      /* lines in the indexed region */
+    uint64_t rows;         /* output rows (AF) / kept records (filters) */
+    uint64_t data_lines;   /* data lines seen (AF "Processed V variants from L data lines") */
+    uint64_t warn_lines;   /* lines flagged VCFXG_LINE_WARN */
+    uint64_t text_bytes;   /* bytes of device-formatted output text (AF) */
+    uint64_t general_records; /* records that took the general (non fixed-stride) GT path */
+} vcfxg_summary;
+
+const char *vcfxg_version(void);
+int vcfxg_device_count(int *n);
+int vcfxg_open(int device, vcfxg_ctx **out);
+void vcfxg_close(vcfxg_ctx *ctx);
+const char *vcfxg_last_error(const vcfxg_ctx *ctx);
+/* the hipStream_t every call of this context is ordered on */
+void *vcfxg_stream(vcfxg_ctx *ctx);
+/* record HIP events around each kernel launch (see vcfxg_kernel_ms) */
+int vcfxg_set_profiling(vcfxg_ctx *ctx, int enable);
+/* elapsed ms of the last launch of the named kernel ("af_records", "line_index", ...) */
+int vcfxg_kernel_ms(vcfxg_ctx *ctx, const char *kernel, float *ms);
+/* accumulated event time and launch count of the named kernel since the last reset */
+int vcfxg_kernel_stats(vcfxg_ctx *ctx, const char *kernel, double *total_ms, uint64_t *launches);
+int vcfxg_reset_kernel_stats(vcfxg_ctx *ctx);
+
+/* ---- input ---------------------------------------------------------------------------
+ * The whole input (file or stdin bytes) is made device-resident once; record kernels read
+ * it straight from HBM.  Replaces MappedFile::open (VCFX_allele_freq_calc.cpp:47-70) and
+ * the std::getline loops' buffering. */
+int vcfxg_load_host(vcfxg_ctx *ctx, const char *host, size_t n);
+/* device copy of the loaded input (read-only view; valid until the next load) */
+const void *vcfxg_input_device_ptr(vcfxg_ctx *ctx);
+
+/* ---- K1: record index ------------------------------------------------------------------
+ * Newline scan over [data_start, n): line i spans [start_i, end_i) with end_i the offset
+ * of its '\n' (or n).  Replaces findNewlineSIMD (VCFX_allele_freq_calc.cpp:150-187,
+ * VCFX_record_filter.cpp:28-60, VCFX_genotype_query.cpp:139-171, VCFX_variant_counter.cpp:
+ * 46-89, VCFX_ld_calculator.cpp:91-137) and the line loops around them. */
+int vcfxg_index(vcfxg_ctx *ctx, size_t data_start, uint64_t *n_lines);
+/* copy line end offsets [first, first+count) to host */
+int vcfxg_line_ends(vcfxg_ctx *ctx, uint64_t first, uint64_t count, uint64_t *out);
+
+/* ---- K2: allele frequency --------------------------------------------------------------
+ * Per data line: FORMAT -> GT index, per-sample GT -> (ALT, total) allele counts, freq =
+ * alt/total (fp64, correctly rounded), formatted row "CHROM\tPOS\tID\tREF\tALT\t%.4f\n"
+ * with the mode's rounding rule.  Replaces processMmap (VCFX_allele_freq_calc.cpp:342-472)
+ * and processStdin (:477-557) per-record work: findGTIndex :298-316, extractGT :321-337,
+ * parseGenotypeAndCount :262-293, writeDouble4 :119-143 / setprecision(4) :553-555. */
+int vcfxg_allele_freq(vcfxg_ctx *ctx, int mode, vcfxg_summary *out);
+/* device-formatted output text (without the column header line) */
+int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);
+/* per-line results of the last record kernel: any pointer may be NULL */
+int vcfxg_fetch_lines(vcfxg_ctx *ctx, uint64_t first, uint64_t count, int32_t *alt, int32_t *total,
+                      uint8_t *status);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

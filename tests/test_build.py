@@ -1,0 +1,48 @@
+"""CPU checks of the product build: the C-ABI library loads and exports every symbol
+include/vcfx_gpu.h declares; tool entry points exist; no GPU is needed for these."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from vcfx_amd import BUILD, GPU_LIB, TOOLS, TOOLS_LIB, tool_binary
+from vcfx_amd import engine
+
+HDR = os.path.join(os.path.dirname(BUILD), "include", "vcfx_gpu.h")
+
+
+def declared_symbols():
+    txt = open(HDR).read()
+    return sorted(set(re.findall(r"\b(vcfxg_[a-z_]+)\s*\(", txt)))
+
+
+def test_gpu_lib_exports_header_symbols():
+    lib = ctypes.CDLL(GPU_LIB)
+    syms = declared_symbols()
+    assert len(syms) >= 15
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_ctypes_signatures_cover_header():
+    assert set(declared_symbols()) == set(engine.SIGNATURES)
+
+
+def test_open_without_gpu_fails_loudly():
+    n = ctypes.c_int(-1)
+    engine.lib().vcfxg_device_count(ctypes.byref(n))
+    if n.value > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(engine.EngineError):
+        engine.Engine(0)
+
+
+def test_tools_lib_exports():
+    lib = ctypes.CDLL(TOOLS_LIB)
+    assert hasattr(lib, "vcfx_tool_main")
+
+
+@pytest.mark.parametrize("tool", ["VCFX_allele_freq_calc"])
+def test_binaries_present(tool):
+    assert os.access(tool_binary(tool), os.X_OK)

@@ -1,0 +1,127 @@
+// VCFX_allele_freq_calc drop-in: the reference CLI (VCFX_allele_freq_calc.cpp:590-646)
+// on top of the vcfxg engine.  The host runs the '#CHROM' gate over the header prefix;
+// every record after it is counted and formatted on the GPU (vcfxg_allele_freq).
+#include <getopt.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "hostio.h"
+#include "tools.h"
+
+using namespace vcfxh;
+
+namespace {
+
+const char *kHelp =
+    "VCFX_allele_freq_calc v1.1 - High-performance allele frequency calculator\n\n"
+    "Usage:\n"
+    "  VCFX_allele_freq_calc [OPTIONS] [input.vcf]\n"
+    "  VCFX_allele_freq_calc [OPTIONS] < input.vcf > output.tsv\n\n"
+    "Options:\n"
+    "  -i, --input FILE   Input VCF file (uses memory-mapping for best performance)\n"
+    "  -q, --quiet        Suppress informational messages\n"
+    "  -h, --help         Display this help message and exit\n"
+    "  -v, --version      Show program version and exit\n\n"
+    "Description:\n"
+    "  Calculates allele frequency for each variant in a VCF file.\n"
+    "  Allele frequency is computed as (#ALT alleles) / (total #alleles),\n"
+    "  counting any non-zero numeric allele (1,2,3,...) as ALT.\n\n"
+    "Output Format:\n"
+    "  CHROM  POS  ID  REF  ALT  Allele_Frequency\n\n"
+    "Performance:\n"
+    "  - Memory-mapped I/O: Use -i flag for ~15-20x faster processing\n"
+    "  - SIMD acceleration for line/field scanning\n"
+    "  - Zero-copy parsing with string_view\n\n"
+    "Examples:\n"
+    "  VCFX_allele_freq_calc -i input.vcf > frequencies.tsv\n"
+    "  VCFX_allele_freq_calc < input.vcf > frequencies.tsv\n";
+
+const char *kWarnPre = "Warning: Data line encountered before #CHROM header. Skipping.\n";
+const char *kWarnFields = "Warning: Skipping invalid VCF line (fewer than 9 fields).\n";
+
+// returns false on a device error (already reported)
+bool run_af(const Input &in, int mode, bool quiet, Out &out, Out &err, uint64_t *variants, uint64_t *datalines) {
+    out.put("CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n");
+    *variants = *datalines = 0;
+    // '#CHROM' gate (processMmap :366-386 / processStdin :489-502) over the header prefix
+    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    size_t data_start = in.n;
+    while (next_line(p, end, ls, le)) {
+        const char *ae = le;
+        if (mode == VCFXG_MODE_FILE && ae > ls && ae[-1] == '\r') --ae;
+        if (ae == ls) continue;
+        if (*ls == '#') {
+            if (is_chrom_line(ls, (size_t)(ae - ls))) {
+                data_start = (size_t)(p - in.p);
+                break;
+            }
+            continue;
+        }
+        if (!quiet) err.put(kWarnPre);
+    }
+    if (data_start >= in.n) return true;
+    vcfxg_ctx *g = gpu(err.fd);
+    if (!g) return false;
+    err.flush();
+    if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd)) return false;
+    uint64_t nl = 0;
+    if (!gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd)) return false;
+    vcfxg_summary s;
+    if (!gpu_ok(g, vcfxg_allele_freq(g, mode, &s), "allele_freq", err.fd)) return false;
+    std::string text(s.text_bytes, '\0');
+    if (!gpu_ok(g, vcfxg_fetch_text(g, &text[0], text.size()), "fetch", err.fd)) return false;
+    out.put(text);
+    if (!quiet)
+        for (uint64_t k = 0; k < s.warn_lines; k++) err.put(kWarnFields);
+    *variants = s.rows;
+    *datalines = s.data_lines;
+    return true;
+}
+
+}  // namespace
+
+extern "C" int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int out_fd, int err_fd) {
+    Out out(out_fd), err(err_fd);
+    const char *input = nullptr;
+    bool quiet = false;
+    static struct option lo[] = {{"input", required_argument, nullptr, 'i'},
+                                 {"quiet", no_argument, nullptr, 'q'},
+                                 {"help", no_argument, nullptr, 'h'},
+                                 {"version", no_argument, nullptr, 'v'},
+                                 {nullptr, 0, nullptr, 0}};
+    GetoptStderr gs(err);
+    optind = 0;
+    int opt;
+    while ((opt = getopt_long(argc, argv, "i:qhv", lo, nullptr)) != -1) {
+        switch (opt) {
+        case 'i': input = optarg; break;
+        case 'q': quiet = true; break;
+        case 'h': out.put(kHelp); return 0;
+        case 'v': out.put("VCFX_allele_freq_calc v1.1\n"); return 0;
+        default: out.put(kHelp); return 1;
+        }
+    }
+    gs.done();
+    if (!input && optind < argc) input = argv[optind];
+    Input in;
+    uint64_t v = 0, l = 0;
+    if (input) {
+        if (!in.open_file(input)) {
+            err.put(std::string("Error: Cannot open file: ") + input + "\n");
+            return 1;
+        }
+        if (!quiet) err.put(std::string("Processing ") + input + " (" + std::to_string(in.n / (1024 * 1024)) + " MB)\n");
+        if (!run_af(in, VCFXG_MODE_FILE, quiet, out, err, &v, &l)) return 1;
+        if (!quiet) err.put("Processed " + std::to_string(v) + " variants from " + std::to_string(l) + " data lines\n");
+    } else {
+        in.read_fd(in_fd);
+        if (in.n == 0) {
+            out.put(kHelp);
+            return 1;
+        }
+        if (!run_af(in, VCFXG_MODE_STDIN, quiet, out, err, &v, &l)) return 1;
+    }
+    return 0;
+}

@@ -1,0 +1,11 @@
+// tool_dispatch.cpp -- name -> in-process tool entry.
+#include <string.h>
+
+#include "tools.h"
+
+extern "C" int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd) {
+    const char *t = strrchr(tool, '/');
+    t = t ? t + 1 : tool;
+    if (!strcmp(t, "VCFX_allele_freq_calc")) return vcfx_tool_allele_freq_calc(argc, argv, in_fd, out_fd, err_fd);
+    return -100;
+}

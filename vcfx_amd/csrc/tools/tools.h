@@ -1,0 +1,40 @@
+// tools.h -- in-process entry points of the VCFX_<tool> drop-ins (libvcfx_tools.so).
+// Each has the tool's exact CLI contract; binaries are thin main()s over these, and tests
+// call them in-process to reuse one GPU context across many cases.
+#pragma once
+#include <stdio.h>
+
+#include "hostio.h"
+
+extern "C" {
+int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd);
+}
+
+namespace vcfxh {
+// getopt_long prints its diagnostics on the C stderr stream; route them to the tool's
+// err fd (identical text to the reference's getopt messages).
+struct GetoptStderr {
+    Out &err;
+    FILE *saved = nullptr, *mem = nullptr;
+    char *buf = nullptr;
+    size_t len = 0;
+    explicit GetoptStderr(Out &e) : err(e) {
+        fflush(stderr);
+        mem = open_memstream(&buf, &len);
+        saved = stderr;
+        stderr = mem;
+    }
+    void done() {
+        if (!mem) return;
+        fflush(mem);
+        stderr = saved;
+        fclose(mem);
+        mem = nullptr;
+        if (len) err.put(buf, len);
+        free(buf);
+        buf = nullptr;
+    }
+    ~GetoptStderr() { done(); }
+};
+}  // namespace vcfxh

@@ -1,0 +1,163 @@
+"""ctypes binding of the C ABI in include/vcfx_gpu.h (libvcfx_gpu.so).
+
+This is plumbing for tests and bench.py; the CLI drop-ins call the same ABI from C++."""
+import ctypes
+import os
+
+from . import GPU_LIB
+
+VCFXG_OK = 0
+MODE_FILE, MODE_STDIN = 0, 1
+STATUS = {0: "skip", 1: "row", 2: "drop", 3: "warn", 4: "header"}
+
+
+class Summary(ctypes.Structure):
+    _fields_ = [("n_lines", ctypes.c_uint64), ("rows", ctypes.c_uint64), ("data_lines", ctypes.c_uint64),
+                ("warn_lines", ctypes.c_uint64), ("text_bytes", ctypes.c_uint64),
+                ("general_records", ctypes.c_uint64)]
+
+
+# every exported entry point: name -> (restype, argtypes)
+_P, _VP, _S, _U64, _I = ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int
+SIGNATURES = {
+    "vcfxg_version": (_P, []),
+    "vcfxg_device_count": (_I, [ctypes.POINTER(_I)]),
+    "vcfxg_open": (_I, [_I, ctypes.POINTER(_VP)]),
+    "vcfxg_close": (None, [_VP]),
+    "vcfxg_last_error": (_P, [_VP]),
+    "vcfxg_stream": (_VP, [_VP]),
+    "vcfxg_set_profiling": (_I, [_VP, _I]),
+    "vcfxg_kernel_ms": (_I, [_VP, _P, ctypes.POINTER(ctypes.c_float)]),
+    "vcfxg_kernel_stats": (_I, [_VP, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
+    "vcfxg_reset_kernel_stats": (_I, [_VP]),
+    "vcfxg_load_host": (_I, [_VP, _VP, _S]),
+    "vcfxg_input_device_ptr": (_VP, [_VP]),
+    "vcfxg_index": (_I, [_VP, _S, ctypes.POINTER(_U64)]),
+    "vcfxg_line_ends": (_I, [_VP, _U64, _U64, _VP]),
+    "vcfxg_allele_freq": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_fetch_text": (_I, [_VP, _VP, _S]),
+    "vcfxg_fetch_lines": (_I, [_VP, _U64, _U64, _VP, _VP, _VP]),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(GPU_LIB):
+            raise RuntimeError("libvcfx_gpu.so not built (run `make` or __graft_entry__.build())")
+        _lib = ctypes.CDLL(GPU_LIB)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(_lib, name)
+            f.restype = res
+            f.argtypes = args
+    return _lib
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+class Engine:
+    """One device context (vcfxg_ctx)."""
+
+    def __init__(self, device=0):
+        self.L = lib()
+        h = ctypes.c_void_p()
+        rc = self.L.vcfxg_open(device, ctypes.byref(h))
+        if rc != VCFXG_OK:
+            raise EngineError("vcfxg_open(%d) failed rc=%d: no usable gfx950 device" % (device, rc))
+        self.h = h
+        self._buf = None
+
+    def close(self):
+        if self.h:
+            self.L.vcfxg_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc != VCFXG_OK:
+            raise EngineError("%s failed rc=%d: %s" % (what, rc, self.L.vcfxg_last_error(self.h).decode()))
+
+    @property
+    def stream(self):
+        return self.L.vcfxg_stream(self.h)
+
+    def set_profiling(self, on=True):
+        self._chk(self.L.vcfxg_set_profiling(self.h, int(on)), "set_profiling")
+
+    def kernel_ms(self, name):
+        v = ctypes.c_float()
+        rc = self.L.vcfxg_kernel_ms(self.h, name.encode(), ctypes.byref(v))
+        return v.value if rc == VCFXG_OK else None
+
+    def kernel_stats(self, name):
+        """(total ms, launches) accumulated since reset_kernel_stats()."""
+        t = ctypes.c_double()
+        n = ctypes.c_uint64()
+        self._chk(self.L.vcfxg_kernel_stats(self.h, name.encode(), ctypes.byref(t), ctypes.byref(n)), "kernel_stats")
+        return t.value, n.value
+
+    def reset_kernel_stats(self):
+        self._chk(self.L.vcfxg_reset_kernel_stats(self.h), "reset_kernel_stats")
+
+    def load(self, data):
+        """data: bytes / bytearray / numpy uint8 array (kept alive until the next load)."""
+        import numpy as np
+        arr = np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data
+        self._buf = arr
+        self._chk(self.L.vcfxg_load_host(self.h, arr.ctypes.data, arr.size), "load_host")
+
+    def index(self, data_start):
+        n = ctypes.c_uint64()
+        self._chk(self.L.vcfxg_index(self.h, data_start, ctypes.byref(n)), "index")
+        return n.value
+
+    def allele_freq(self, mode=MODE_FILE):
+        s = Summary()
+        self._chk(self.L.vcfxg_allele_freq(self.h, mode, ctypes.byref(s)), "allele_freq")
+        return s
+
+    def text(self, nbytes):
+        b = ctypes.create_string_buffer(max(1, nbytes))
+        self._chk(self.L.vcfxg_fetch_text(self.h, b, nbytes), "fetch_text")
+        return b.raw[:nbytes]
+
+    def lines(self, n):
+        import numpy as np
+        alt = np.zeros(n, np.int32)
+        tot = np.zeros(n, np.int32)
+        st = np.zeros(n, np.uint8)
+        self._chk(self.L.vcfxg_fetch_lines(self.h, 0, n, alt.ctypes.data, tot.ctypes.data, st.ctypes.data),
+                  "fetch_lines")
+        return alt, tot, st
+
+    def line_ends(self, n):
+        import numpy as np
+        out = np.zeros(n, np.uint64)
+        self._chk(self.L.vcfxg_line_ends(self.h, 0, n, out.ctypes.data), "line_ends")
+        return out
+
+
+def data_start_of(buf, strip_cr=True):
+    """Byte offset just after the first '#CHROM' line (len(buf) if none)."""
+    p = 0
+    n = len(buf)
+    while p < n:
+        e = buf.find(b"\n", p)
+        e = n if e < 0 else e
+        line = buf[p:e]
+        if strip_cr and line.endswith(b"\r"):
+            line = line[:-1]
+        nxt = e + 1 if e < n else n
+        if line[:6] == b"#CHROM":
+            return nxt
+        p = nxt
+    return n

@@ -1,0 +1,47 @@
+"""In-process runs of the VCFX_<tool> drop-ins (libvcfx_tools.so).
+
+Mirrors the reference's Python wrapper contract (python/tools/base.py:51-75: argv + stdin
+bytes in, stdout/stderr/exit code out) without spawning a process per call, so one GPU
+context serves many calls."""
+import ctypes
+import os
+import tempfile
+
+from . import TOOLS_LIB
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(TOOLS_LIB):
+            raise RuntimeError("libvcfx_tools.so not built")
+        _lib = ctypes.CDLL(TOOLS_LIB)
+        _lib.vcfx_tool_main.restype = ctypes.c_int
+        _lib.vcfx_tool_main.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    return _lib
+
+
+def run(argv, stdin=None, cwd=None):
+    """Run tool argv[0] with argv; returns (stdout bytes, stderr bytes, exit code)."""
+    L = lib()
+    old = os.getcwd()
+    with tempfile.TemporaryFile() as fi, tempfile.TemporaryFile() as fo, tempfile.TemporaryFile() as fe:
+        if stdin:
+            fi.write(stdin)
+            fi.flush()
+            fi.seek(0)
+        arr = (ctypes.c_char_p * (len(argv) + 1))(*[a.encode() for a in argv], None)
+        if cwd:
+            os.chdir(cwd)
+        try:
+            rc = L.vcfx_tool_main(argv[0].encode(), len(argv), arr, fi.fileno(), fo.fileno(), fe.fileno())
+        finally:
+            os.chdir(old)
+        if rc == -100:
+            raise NotImplementedError(argv[0])
+        fo.seek(0)
+        fe.seek(0)
+        return fo.read(), fe.read(), rc
