@@ -94,6 +94,19 @@ int vcfxg_line_ends(vcfxg_ctx *ctx, uint64_t first, uint64_t count, uint64_t *ou
  * and processStdin (:477-557) per-record work: findGTIndex :298-316, extractGT :321-337,
  * parseGenotypeAndCount :262-293, writeDouble4 :119-143 / setprecision(4) :553-555. */
 int vcfxg_allele_freq(vcfxg_ctx *ctx, int mode, vcfxg_summary *out);
+/* ---- K2: genotype query ----------------------------------------------------------------
+ * Per line status (vcfxg_line_status): ROW = some sample's GT sub-field matches `query`
+ * (flexible: phase- and order-normalised diploid compare; strict: byte equality), DROP,
+ * WARN (fewer than 9 fields), HEADER ('#'), SKIP (empty).  The query is pre-parsed here
+ * exactly as main() does (parseDiploidAlleles incl. its partial assignment, then sort).
+ * strip_cr evaluates each line without a trailing '\r' (the line as VCFX_record_filter
+ * emits it, for the fused record_filter | genotype_query pipeline).  Replaces
+ * genotypeQueryMmap / genotypeQueryStream per-record work (VCFX_genotype_query.cpp:433-617):
+ * skipToField :223-230, findGTIndex :176-194, extractNthField :199-218,
+ * genotypeMatchesFast :275-316, checkAnySampleMatches :322-345. */
+int vcfxg_genotype_query(vcfxg_ctx *ctx, const char *query, size_t qlen, int strict, int strip_cr,
+                         vcfxg_summary *out);
+
 /* device-formatted output text (without the column header line) */
 int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);
 /* per-line results of the last record kernel: any pointer may be NULL */

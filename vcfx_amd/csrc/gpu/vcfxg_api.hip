@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
@@ -38,7 +39,8 @@ struct vcfxg_ctx {
     uint64_t n_lines = 0;
     bool indexed = false;
     // per-line results
-    DevBuf alt, tot, rowpre, status, rowlen, rowoff, text, counters;
+    DevBuf alt, tot, rowpre, status, rowlen, rowoff, text, counters, query;
+    std::string query_host;
     uint64_t text_bytes = 0;
     // profiling
     bool profiling = false;
@@ -163,7 +165,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
-                      &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters})
+                      &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query})
         if (b->p) (void)hipFree(b->p);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
@@ -325,6 +327,70 @@ int vcfxg_allele_freq(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
         out->warn_lines = host_tail[3];
         out->general_records = host_tail[4];
         out->text_bytes = text;
+    }
+    return VCFXG_OK;
+}
+
+// parseDiploidAlleles (VCFX_genotype_query.cpp:246-272) incl. its partial assignment on
+// failure, then the swap of main :641-645
+static void gq_parse_query(const char *q, size_t n, int &qa, int &qb) {
+    qa = qb = -1;
+    size_t sep = (size_t)-1;
+    for (size_t i = 0; i < n; i++)
+        if (q[i] == '|' || q[i] == '/') { sep = i; break; }
+    if (sep == (size_t)-1 || sep == 0 || sep == n - 1) return;
+    if (sep == 1 && q[0] == '.') return;
+    unsigned v = 0;
+    qa = 0;
+    bool ok = true;
+    for (size_t i = 0; i < sep && ok; i++) {
+        if (q[i] < '0' || q[i] > '9') ok = false;
+        else qa = (int)(v = v * 10u + (unsigned)(q[i] - '0'));
+    }
+    if (ok) {
+        if (!(n - sep - 1 == 1 && q[sep + 1] == '.')) {
+            v = 0;
+            qb = 0;
+            for (size_t i = sep + 1; i < n; i++) {
+                if (q[i] < '0' || q[i] > '9') break;
+                qb = (int)(v = v * 10u + (unsigned)(q[i] - '0'));
+            }
+        }
+    }
+    if (qa > qb) std::swap(qa, qb);
+}
+
+int vcfxg_genotype_query(vcfxg_ctx *c, const char *query, size_t qlen, int strict, int strip_cr, vcfxg_summary *out) {
+    if (!c || (!query && qlen)) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t L = c->n_lines;
+    int r = ensure(c, c->status, L + 1);
+    if (!r) r = ensure(c, c->query, qlen + 1);
+    if (r) return r;
+    int qa = -1, qb = -1;
+    if (!strict) gq_parse_query(query, qlen, qa, qb);
+    c->query_host.assign(query, qlen);
+    if (qlen)
+        HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), qlen, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    prof_begin(c, "gq_records");
+    HIPCHK(c, vcfxg::launch_gq_records(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
+                                       P<uint64_t>(c->d_nlines), L, strip_cr, P<char>(c->query), (int)qlen, strict,
+                                       qa, qb, P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "gq_records");
+    static thread_local uint64_t host_cnt[4];
+    HIPCHK(c, hipMemcpyAsync(host_cnt, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    c->text_bytes = 0;
+    if (out) {
+        out->n_lines = L;
+        out->rows = host_cnt[0];
+        out->data_lines = host_cnt[1];
+        out->warn_lines = host_cnt[2];
+        out->general_records = host_cnt[3];
+        out->text_bytes = 0;
     }
     return VCFXG_OK;
 }

@@ -64,6 +64,14 @@ __device__ __forceinline__ T wave_sum(T v) {
 template <typename T>
 __device__ __forceinline__ T wave_bcast(T v, int src) { return __shfl(v, src); }
 
+// a value known to be equal in all lanes, moved to scalar registers
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+    uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ int uniform32(int v) { return (int)__builtin_amdgcn_readfirstlane((uint32_t)v); }
+
 // j-th (0-based) set bit of m (m has > j bits set)
 __device__ __forceinline__ int nth_bit(uint32_t m, int j) {
     for (int k = 0; k < j; k++) m &= m - 1u;
@@ -100,7 +108,8 @@ __device__ __forceinline__ int head_tabs(const char *buf, int64_t ls, int64_t le
         nt += total;
     }
     if (nt > want) nt = want;
-    for (int k = 0; k < nt; k++) t[k] = lds[k];
+    // wave-uniform: keep the offsets in SGPRs
+    for (int k = 0; k < nt; k++) t[k] = uniform64(lds[k]);
     __builtin_amdgcn_wave_barrier();
     return nt;
 }

@@ -1,0 +1,287 @@
+// vcfxg_gt.h -- the per-record sample sweep shared by the GT reducers (allele counts,
+// genotype match, LD genotype codes).
+//
+// gt_fast: the fixed-stride path.  The sample region [S, E) of a record is tested for the
+// layout of single-digit diploid GT-only records -- N 4-byte units "a s b \t" (the last
+// without its tab), s the record's first separator ('/' or '|'), a, b in [0-9.] -- while
+// the reducer consumes it.  Sample dwords d = bytes [p, p+4), p = S + 4k, come from the
+// lane's 16 B block by v_alignbyte; per dword e = d ^ (0x09<<24 | '0'<<16 | s<<8 | '0'):
+// bytes 1 and 3 must be 0, bytes 0 and 2 a digit (0..9) or '.' (0x1E).  A record that
+// deviates anywhere returns false (wave-uniform) and the caller runs gt_general, which
+// restates the reference's per-sample loop exactly.
+#pragma once
+#include "vcfxg_device.h"
+
+namespace vcfxg {
+
+struct DwordView {
+    uint32_t d;    // canonical sample dword: byte0 = allele a, byte1 = sep, byte2 = allele b
+    uint32_t f;    // (d ^ exp) & 0x00FF00FF: allele digit values in 16-bit fields
+    uint32_t dig;  // bit 8 / bit 24 set where the allele is a digit
+};
+
+template <class Op>
+__device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_t &err, Op &op) {
+    uint32_t e = d ^ exp_xor;
+    err |= e & 0xFF00FF00u;
+    uint32_t f = e & 0x00FF00FFu;
+    uint32_t notdig = (f + 0x00F600F6u) & 0x01000100u;  // field >= 10
+    uint32_t notdot = ((f ^ 0x001E001Eu) + 0x00FF00FFu) & 0x01000100u;
+    err |= notdig & notdot;
+    DwordView v{d, f, notdig ^ 0x01000100u};
+    op.dword(v);
+}
+
+// returns false (uniformly) if the record is not fixed-stride
+template <class Op>
+__device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &op) {
+    int64_t L = E - S;
+    if (L < 3 || ((L + 1) & 3)) return false;
+    uint32_t sepc = byte_at(buf, S + 1);
+    if (sepc != '/' && sepc != '|') return false;
+    const uint32_t exp_xor = 0x09000000u | (sepc << 8) | 0x00300030u;
+    const uint32_t neutral = 0x092E002Eu | (sepc << 8);  // ". ." + tab: valid, reduces to nothing
+    op.begin(sepc, neutral);
+    const int s = (int)(S & 3);
+    const int64_t b0 = S & ~(int64_t)15;
+    uint32_t err = 0;
+    // kUnroll wave-steps per iteration: their loads are all issued before any is consumed
+    constexpr int kUnroll = 4;
+    for (int64_t w0 = b0; w0 < E; w0 += kUnroll * kWaveStep) {
+        uint4 v[kUnroll];
+        uint32_t x4[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            const int64_t blk = w0 + (int64_t)u * kWaveStep + (int64_t)lane() * kBlockBytes;
+            if (blk < E) {
+                v[u] = load16(buf, blk);
+                x4[u] = load4(buf, blk + 16);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            const int64_t w = w0 + (int64_t)u * kWaveStep;
+            const int64_t blk = w + (int64_t)lane() * kBlockBytes;
+            // interior step: every sample dword of every lane lies in [S, E) and is not the last
+            const bool interior = (w + s >= S) && (w + kWaveStep - 4 + s + 3 < E);
+            if (blk < E) {
+                uint32_t d[4] = {__builtin_amdgcn_alignbyte(v[u].y, v[u].x, s),
+                                 __builtin_amdgcn_alignbyte(v[u].z, v[u].y, s),
+                                 __builtin_amdgcn_alignbyte(v[u].w, v[u].z, s),
+                                 __builtin_amdgcn_alignbyte(x4[u], v[u].w, s)};
+                if (!interior) {
+#pragma unroll
+                    for (int i = 0; i < 4; i++) {
+                        int64_t p = blk + s + 4 * i;
+                        if (p < S || p + 3 > E) d[i] = neutral;
+                        else if (p + 3 == E) d[i] = (d[i] & 0x00FFFFFFu) | 0x09000000u;
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op);
+            }
+        }
+        if (op.done()) break;  // wave-uniform early exit (e.g. a match was found)
+    }
+    if (__any(err != 0u)) return false;
+    op.finish();
+    return true;
+}
+
+// general path: op.sample(st) for every sample start (S, and every tab+1 < E), one lane
+// per start in its 16 B block; op.finish() reduces across the wave.
+template <class Op>
+__device__ void gt_general(const char *__restrict__ buf, int64_t S, int64_t E, Op &op) {
+    for (int64_t w = S & ~(int64_t)15; w < E; w += kWaveStep) {
+        int64_t blk = w + (int64_t)lane() * kBlockBytes;
+        if (blk < E) {
+            uint32_t tm = eq_mask16(load16(buf, blk), kRepTab);
+            uint32_t starts = (tm << 1) & 0xFFFFu;
+            if (blk > 0 && byte_at(buf, blk - 1) == '\t') starts |= 1u;
+            starts &= range_mask16(blk, S + 1, E);
+            if (S >= blk && S < blk + 16) starts |= 1u << (S - blk);
+            while (starts) {
+                int j = __builtin_ctz(starts);
+                starts &= starts - 1u;
+                op.sample(blk + j);
+            }
+        }
+        if (op.done()) break;
+    }
+    op.finish();
+}
+
+// end of the sample starting at st: first '\t' at or after st, or E
+__device__ __forceinline__ int64_t sample_end(const char *__restrict__ buf, int64_t st, int64_t E) {
+    int64_t p = st;
+    while (p < E && byte_at(buf, p) != '\t') p++;
+    return p;
+}
+
+// ---------------------------------------------------------------------------------------
+// allele-count reducer: parseGenotypeAndCount (VCFX_allele_freq_calc.cpp:262-293) over
+// extractGT (:321-337)
+// ---------------------------------------------------------------------------------------
+struct AfOp {
+    const char *buf;
+    int64_t E;
+    int gi;
+    uint32_t alt = 0, tot = 0;
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() const { return false; }
+    __device__ void dword(const DwordView &v) {
+        tot += __popc(v.dig);
+        alt += __popc((v.f + 0x00FF00FFu) & v.dig);  // digit 1..9
+    }
+    __device__ void sample(int64_t st) {
+        int64_t p = st;
+        for (int k = 0; k < gi; k++) {  // skip gi colon fields
+            while (p < E) {
+                uint32_t c = byte_at(buf, p);
+                if (c == '\t' || c == ':') break;
+                p++;
+            }
+            if (p >= E || byte_at(buf, p) == '\t') return;
+            p++;
+        }
+        bool in_tok = false, first_dot = false, numeric = true, nonzero = false;
+        for (;; p++) {
+            uint32_t c = p < E ? byte_at(buf, p) : (uint32_t)'\t';
+            bool end = (c == '\t' || c == ':');
+            if (end || c == '/' || c == '|') {
+                if (in_tok && !first_dot && numeric) {
+                    tot++;
+                    if (nonzero) alt++;
+                }
+                in_tok = false;
+                if (end) break;
+                continue;
+            }
+            if (!in_tok) {
+                in_tok = true;
+                first_dot = (c == '.');
+                numeric = true;
+                nonzero = false;
+            }
+            if (c < '0' || c > '9') numeric = false;
+            else if (c != '0') nonzero = true;
+        }
+    }
+    __device__ void finish() {
+        alt = wave_sum(alt);
+        tot = wave_sum(tot);
+    }
+};
+
+// ---------------------------------------------------------------------------------------
+// genotype-match reducer: genotypeMatchesFast (VCFX_genotype_query.cpp:275-316) over
+// extractNthField (:199-218); "any sample matches" (checkAnySampleMatches :322-345)
+// ---------------------------------------------------------------------------------------
+struct GqQuery {
+    const char *q;  // query bytes (device)
+    int qlen;
+    int strict;
+    int qa, qb;     // parsed + sorted query alleles (host parse, partial-assignment semantics kept)
+};
+
+__device__ __forceinline__ bool is_digit(uint32_t c) { return c - '0' < 10u; }
+
+// parseDiploidAlleles (VCFX_genotype_query.cpp:246-272) on [g, g+n)
+__device__ __forceinline__ bool parse_diploid(const char *__restrict__ buf, int64_t g, int64_t n, int &a1, int &a2) {
+    int64_t sep = -1;
+    for (int64_t i = 0; i < n; i++) {
+        uint32_t c = byte_at(buf, g + i);
+        if (c == '|' || c == '/') { sep = i; break; }
+    }
+    if (sep <= 0 || sep == n - 1) return false;
+    if (sep == 1 && byte_at(buf, g) == '.') return false;
+    uint32_t v = 0;
+    for (int64_t i = 0; i < sep; i++) {
+        uint32_t c = byte_at(buf, g + i);
+        if (!is_digit(c)) return false;
+        v = v * 10u + (c - '0');
+    }
+    a1 = (int)v;
+    if (n - sep - 1 == 1 && byte_at(buf, g + sep + 1) == '.') return false;
+    v = 0;
+    for (int64_t i = sep + 1; i < n; i++) {
+        uint32_t c = byte_at(buf, g + i);
+        if (!is_digit(c)) return false;
+        v = v * 10u + (c - '0');
+    }
+    a2 = (int)v;
+    return true;
+}
+
+__device__ __forceinline__ bool gt_matches(const char *__restrict__ buf, int64_t g, int64_t n, const GqQuery &Q) {
+    if (Q.strict) {
+        if (n != Q.qlen) return false;
+        for (int64_t i = 0; i < n; i++)
+            if (byte_at(buf, g + i) != (uint32_t)(uint8_t)Q.q[i]) return false;
+        return true;
+    }
+    if (n == 3 && Q.qlen == 3) {
+        uint32_t s = byte_at(buf, g + 1);
+        if (s != '|' && s != '/') return false;
+        uint32_t g0 = byte_at(buf, g), g1 = byte_at(buf, g + 2);
+        if (!is_digit(g0) || !is_digit(g1)) return false;
+        int ga = (int)(g0 - '0'), gb = (int)(g1 - '0');
+        if (ga > gb) { int t = ga; ga = gb; gb = t; }
+        return ga == Q.qa && gb == Q.qb;
+    }
+    int a1 = 0, a2 = 0;
+    if (!parse_diploid(buf, g, n, a1, a2)) return false;
+    if (a1 > a2) { int t = a1; a1 = a2; a2 = t; }
+    return a1 == Q.qa && a2 == Q.qb;
+}
+
+struct GqOp {
+    const char *buf;
+    int64_t E;
+    int gi;
+    GqQuery Q;
+    uint32_t p1 = 0, p2 = 0, pmask = 0;  // fast-path dword pattern(s)
+    bool any = false;                    // this lane
+    bool found = false;                  // wave
+    __device__ void begin(uint32_t sepc, uint32_t) {
+        // on the fixed-stride layout a GT is "a s b"; flexible: match <=> a, b digits with
+        // sorted (a, b) == (qa, qb); strict: the 3 bytes equal the query
+        if (Q.strict) {
+            if (Q.qlen == 3) {
+                p1 = p2 = (uint32_t)(uint8_t)Q.q[0] | ((uint32_t)(uint8_t)Q.q[1] << 8) | ((uint32_t)(uint8_t)Q.q[2] << 16);
+                pmask = 0x00FFFFFFu;
+            } else pmask = 0;
+        } else if (Q.qa >= 0 && Q.qa <= 9 && Q.qb >= 0 && Q.qb <= 9) {
+            p1 = (uint32_t)('0' + Q.qa) | ((uint32_t)('0' + Q.qb) << 16);
+            p2 = (uint32_t)('0' + Q.qb) | ((uint32_t)('0' + Q.qa) << 16);
+            pmask = 0x00FF00FFu;
+        } else pmask = 0;
+        (void)sepc;
+    }
+    __device__ bool done() { return found = found || __any(any); }
+    __device__ void dword(const DwordView &v) {
+        uint32_t x = v.d & pmask;
+        any = any || (pmask && (x == p1 || x == p2));
+    }
+    __device__ void sample(int64_t st) {
+        if (any) return;
+        int64_t se = sample_end(buf, st, E);
+        // extractNthField(sample, gi)
+        int64_t p = st, fs = st;
+        int fi = 0;
+        for (;; p++) {
+            bool end = (p == se) || byte_at(buf, p) == ':';
+            if (end) {
+                if (fi == gi) break;
+                fi++;
+                fs = p + 1;
+                if (p == se) return;  // fewer fields: empty
+            }
+        }
+        int64_t n = p - fs;
+        if (n > 0 && gt_matches(buf, fs, n, Q)) any = true;
+    }
+    __device__ void finish() { found = __any(any); }
+};
+
+}  // namespace vcfxg

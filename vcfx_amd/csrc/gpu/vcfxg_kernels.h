@@ -12,6 +12,10 @@ hipError_t launch_nl_emit(const char *buf, int64_t lo, int64_t hi, const uint64_
 hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int mode, int32_t *alt, int32_t *tot, uint32_t *rowpre,
                              uint8_t *status, unsigned long long *counters, hipStream_t s);
+hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
+                             int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,
+                             hipStream_t s);
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, uint64_t *len, hipStream_t s);
 hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,

@@ -7,6 +7,7 @@
 //
 // Reference behaviour restated: VCFX_allele_freq_calc.cpp (citations per function).
 #include "vcfxg_device.h"
+#include "vcfxg_gt.h"
 #include "vcfxg_kernels.h"
 
 namespace vcfxg {
@@ -78,188 +79,96 @@ __global__ __launch_bounds__(kIdxThreads) void k_nl_emit(const char *__restrict_
 }
 
 // =======================================================================================
-// K2: allele frequency per record
+// K2: per-record GT reducers (allele counts, genotype match); one wave per line
 // =======================================================================================
-// Fast path: the sample region [S, E) is N fixed 4-byte units "a s b \t" (last one without
-// the tab), s == the record's first separator ('/' or '|'), a/b in [0-9.] -- the layout of
-// phased/unphased single-digit diploid GT-only records (1000 Genomes).  Any deviation makes
-// the record take af_general, which restates the reference loop per sample exactly.
-// Sample dwords d = bytes [p, p+4) for p = S + 4k, built with v_alignbyte from the lane's
-// 16 B block; per dword: e = d ^ (0x09 << 24 | sep << 8 | '0' << 16 | '0'):
-//   bytes 1 and 3 must be 0 (sep, tab); bytes 0 and 2 in 0..9 (digit) or 0x1E ('.').
-struct FastAcc {
-    uint32_t alt, tot, err;
+constexpr int kRecThreads = 256;
+constexpr int kRecWaves = kRecThreads / kWave;
+
+// block-reduced counters: one global atomic per block and counter
+struct BlockCounters {
+    uint32_t *lds;  // kNC entries
+    static constexpr int kNC = 4;
+    __device__ void add(int k, uint32_t v) {
+        if (lane() == 0 && v) atomicAdd(&lds[k], v);
+    }
 };
-
-__device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, FastAcc &a) {
-    uint32_t e = d ^ exp_xor;
-    a.err |= e & 0xFF00FF00u;
-    uint32_t f = e & 0x00FF00FFu;
-    uint32_t notdig = (f + 0x00F600F6u) & 0x01000100u;          // field >= 10
-    uint32_t dig = notdig ^ 0x01000100u;
-    uint32_t nz = (f + 0x00FF00FFu) & dig;                        // 1..9
-    uint32_t notdot = ((f ^ 0x001E001Eu) + 0x00FF00FFu) & 0x01000100u;
-    a.err |= notdig & notdot;
-    a.tot += __popc(dig);
-    a.alt += __popc(nz);
+__device__ __forceinline__ void flush_counters(uint32_t *lds, unsigned long long *g) {
+    __syncthreads();
+    if (threadIdx.x < BlockCounters::kNC && lds[threadIdx.x])
+        atomicAdd(&g[threadIdx.x], (unsigned long long)lds[threadIdx.x]);
 }
 
-// returns false (uniformly) if the record is not fixed-stride; otherwise alt/tot (uniform)
-__device__ bool af_fast(const char *__restrict__ buf, int64_t S, int64_t E, int &alt_o, int &tot_o) {
-    int64_t L = E - S;
-    if (L < 3 || ((L + 1) & 3)) return false;
-    uint32_t sepc = byte_at(buf, S + 1);
-    if (sepc != '/' && sepc != '|') return false;
-    const uint32_t exp_xor = 0x09000000u | (sepc << 8) | 0x00300030u;
-    const uint32_t neutral = 0x092E002Eu | (sepc << 8);  // ". ." with tab: counts 0, valid
-    const int s = (int)(S & 3);
-    const int64_t b0 = S & ~(int64_t)15;
-    FastAcc a = {0, 0, 0};
-    for (int64_t w = b0; w < E; w += kWaveStep) {
-        const int64_t blk = w + (int64_t)lane() * kBlockBytes;
-        // interior step: every sample dword of every lane lies in [S, E) and is not last
-        const bool interior = (w + s >= S) && (w + kWaveStep - 4 + s + 3 < E);
-        if (blk < E + 4) {
-            uint4 v = load16(buf, blk);
-            uint32_t x4 = load4(buf, blk + 16);
-            uint32_t d0 = __builtin_amdgcn_alignbyte(v.y, v.x, s);
-            uint32_t d1 = __builtin_amdgcn_alignbyte(v.z, v.y, s);
-            uint32_t d2 = __builtin_amdgcn_alignbyte(v.w, v.z, s);
-            uint32_t d3 = __builtin_amdgcn_alignbyte(x4, v.w, s);
-            if (!interior) {
-                uint32_t dd[4] = {d0, d1, d2, d3};
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    int64_t p = blk + s + 4 * i;
-                    if (p < S || p + 3 > E) dd[i] = neutral;
-                    else if (p + 3 == E) dd[i] = (dd[i] & 0x00FFFFFFu) | 0x09000000u;
-                }
-                d0 = dd[0]; d1 = dd[1]; d2 = dd[2]; d3 = dd[3];
-            }
-            fast_dword(d0, exp_xor, a);
-            fast_dword(d1, exp_xor, a);
-            fast_dword(d2, exp_xor, a);
-            fast_dword(d3, exp_xor, a);
-        }
-    }
-    if (__any(a.err != 0u)) return false;
-    alt_o = wave_sum((int)a.alt);
-    tot_o = wave_sum((int)a.tot);
-    return true;
+__device__ __forceinline__ void line_bounds(const uint64_t *__restrict__ line_end, int64_t data_start, uint64_t li,
+                                            int64_t &ls, int64_t &le) {
+    ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
+    le = (int64_t)line_end[li];
 }
 
-// parseGenotypeAndCount (VCFX_allele_freq_calc.cpp:262-293) over the GT sub-field
-// (extractGT :321-337) of the sample starting at st; the sample ends at '\t' or E.
-__device__ void af_sample(const char *__restrict__ buf, int64_t st, int64_t E, int gi, int &alt, int &tot) {
-    int64_t p = st;
-    // skip gi colon fields
-    for (int k = 0; k < gi; k++) {
-        while (p < E) {
-            uint32_t c = byte_at(buf, p);
-            if (c == '\t' || c == ':') break;
-            p++;
-        }
-        if (p >= E || byte_at(buf, p) == '\t') return;  // fewer sub-fields: empty GT
-        p++;                                            // skip ':'
-    }
-    // GT = [p, first of ':' '\t' E)
-    bool in_tok = false, first_dot = false, numeric = true, nonzero = false;
-    for (;; p++) {
-        uint32_t c = p < E ? byte_at(buf, p) : (uint32_t)'\t';
-        bool end = (c == '\t' || c == ':');
-        bool sep = end || c == '/' || c == '|';
-        if (sep) {
-            if (in_tok && !first_dot && numeric) {
-                tot++;
-                if (nonzero) alt++;
-            }
-            in_tok = false;
-            if (end) break;
-            continue;
-        }
-        if (!in_tok) {
-            in_tok = true;
-            first_dot = (c == '.');
-            numeric = true;
-            nonzero = false;
-        }
-        if (c < '0' || c > '9') numeric = false;
-        else if (c != '0') nonzero = true;
-    }
-}
-
-// general path: one lane per sample start (S, and every tab+1 < E) in its 16 B block
-__device__ void af_general(const char *__restrict__ buf, int64_t S, int64_t E, int gi, int &alt_o, int &tot_o) {
-    int alt = 0, tot = 0;
-    for (int64_t w = S & ~(int64_t)15; w < E; w += kWaveStep) {
-        int64_t blk = w + (int64_t)lane() * kBlockBytes;
-        if (blk < E) {
-            uint32_t tm = eq_mask16(load16(buf, blk), kRepTab);
-            uint32_t starts = (tm << 1) & 0xFFFFu;
-            if (blk > 0 && byte_at(buf, blk - 1) == '\t') starts |= 1u;
-            starts &= range_mask16(blk, S + 1, E);  // starts after tabs: S < st < E
-            if (S >= blk && S < blk + 16) starts |= 1u << (S - blk);
-            while (starts) {
-                int j = __builtin_ctz(starts);
-                starts &= starts - 1u;
-                af_sample(buf, blk + j, E, gi, alt, tot);
-            }
-        }
-    }
-    alt_o = wave_sum(alt);
-    tot_o = wave_sum(tot);
-}
-
-// one wave per line of the indexed region; writes per-line status/alt/tot/row prefix len
-__global__ __launch_bounds__(256) void k_af_records(const char *__restrict__ buf, int64_t data_start,
-                                                    const uint64_t *__restrict__ line_end, const uint64_t *n_lines_p,
-                                                    int mode, int32_t *__restrict__ alt_o, int32_t *__restrict__ tot_o,
-                                                    uint32_t *__restrict__ rowpre_o, uint8_t *__restrict__ status_o,
-                                                    unsigned long long *__restrict__ counters) {
-    __shared__ int64_t scratch[256 / kWave][16];
+// counters: 0 rows, 1 data lines, 2 warn lines, 3 general-path records
+__global__ __launch_bounds__(kRecThreads) void k_af_records(const char *__restrict__ buf, int64_t data_start,
+                                                            const uint64_t *__restrict__ line_end,
+                                                            const uint64_t *n_lines_p, int mode,
+                                                            int32_t *__restrict__ alt_o, int32_t *__restrict__ tot_o,
+                                                            uint32_t *__restrict__ rowpre_o,
+                                                            uint8_t *__restrict__ status_o,
+                                                            unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kRecWaves][16];
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
     int64_t *lds = scratch[threadIdx.x / kWave];
     const uint64_t n_lines = *n_lines_p;
-    const uint64_t wid = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
-    uint32_t c_rows = 0, c_data = 0, c_warn = 0, c_gen = 0;
     for (uint64_t li = wid; li < n_lines; li += nw) {
-        const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
-        const int64_t le = (int64_t)line_end[li];
+        int64_t ls, le;
+        line_bounds(line_end, data_start, li, ls, le);
         int64_t ae = le;
         if (mode == 0 && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;  // processMmap :362-364
         uint8_t st = 0;
-        int alt = 0, tot = 0;
-        uint32_t rowpre = 0;
+        uint32_t alt = 0, tot = 0, rowpre = 0;
         if (ae > ls && byte_at(buf, ls) != '#') {
-            c_data++;
+            bc.add(1, 1);
             int64_t t[10];
-            int nt = head_tabs(buf, ls, ae, 10, t, lds);
+            const int nt = head_tabs(buf, ls, ae, 10, t, lds);
             bool ok = true;
             int64_t fs = 0, fe = 0;
             if (mode == 0) {
-                // getField(8) non-empty (processMmap :391-401)
+                // getField(8) must be non-empty (processMmap :391-401)
                 if (nt < 8) ok = false;
                 else {
                     fs = t[7] + 1;
                     fe = nt >= 9 ? t[8] : ae;
-                    if (fe <= fs) ok = false;
+                    ok = fe > fs;
                 }
             } else {
-                // processStdin :509-523: fields = tabs + (last char != '\t')
-                int nf = nt + ((byte_at(buf, ae - 1) != '\t') ? 1 : 0);
-                if (nt >= 9) nf = 10;
-                if (nf < 9) { st = 3; ok = false; }
-                else { fs = t[7] + 1; fe = nt >= 9 ? t[8] : ae; }
+                // processStdin :509-523: #fields = tabs + (last char != '\t')
+                int nf = nt >= 9 ? 10 : nt + ((byte_at(buf, ae - 1) != '\t') ? 1 : 0);
+                if (nf < 9) {
+                    st = 3;
+                    ok = false;
+                } else {
+                    fs = t[7] + 1;
+                    fe = nt >= 9 ? t[8] : ae;
+                }
             }
             if (ok) {
-                int gi = gt_index(buf, fs, fe);
+                const int gi = gt_index(buf, fs, fe);
                 if (gi >= 0) {
                     if (nt >= 9) {
-                        int64_t S = t[8] + 1;
-                        bool fast = gi == 0 && af_fast(buf, S, ae, alt, tot);
-                        if (!fast) {
-                            af_general(buf, S, ae, gi, alt, tot);
-                            c_gen++;
+                        const int64_t S = t[8] + 1;
+                        AfOp op{buf, ae, gi};
+                        bool fast = gi == 0 && gt_fast(buf, S, ae, op);
+                        if (fast) {
+                            alt = op.alt;
+                            tot = op.tot;
+                        } else {
+                            AfOp g{buf, ae, gi};
+                            gt_general(buf, S, ae, g);
+                            alt = g.alt;
+                            tot = g.tot;
+                            bc.add(3, 1);
                         }
                     }
                     st = 1;
@@ -269,19 +178,75 @@ __global__ __launch_bounds__(256) void k_af_records(const char *__restrict__ buf
         }
         if (lane() == 0) {
             status_o[li] = st;
-            alt_o[li] = alt;
-            tot_o[li] = tot;
+            alt_o[li] = (int32_t)alt;
+            tot_o[li] = (int32_t)tot;
             rowpre_o[li] = rowpre;
         }
-        c_rows += st == 1;
-        c_warn += st == 3;
+        bc.add(0, st == 1);
+        bc.add(2, st == 3);
     }
-    if (lane() == 0 && (c_rows | c_data | c_warn | c_gen)) {
-        atomicAdd(&counters[0], (unsigned long long)c_rows);
-        atomicAdd(&counters[1], (unsigned long long)c_data);
-        atomicAdd(&counters[2], (unsigned long long)c_warn);
-        atomicAdd(&counters[3], (unsigned long long)c_gen);
+    flush_counters(cnt, counters);
+}
+
+// genotype_query per line: status 1 keep, 2 drop, 3 "<9 fields" warning, 4 header, 0 empty.
+// genotypeQueryMmap :450-516 / genotypeQueryStream :546-607 per data line; strip_cr = the
+// line as VCFX_record_filter emitted it (fused RF|GQ pipeline).
+__global__ __launch_bounds__(kRecThreads) void k_gq_records(const char *__restrict__ buf, int64_t data_start,
+                                                            const uint64_t *__restrict__ line_end,
+                                                            const uint64_t *n_lines_p, int strip_cr, GqQuery Q,
+                                                            uint8_t *__restrict__ status_o,
+                                                            unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kRecWaves][16];
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t li = wid; li < n_lines; li += nw) {
+        int64_t ls, le;
+        line_bounds(line_end, data_start, li, ls, le);
+        int64_t ae = le;
+        if (strip_cr && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;
+        uint8_t st = 0;
+        if (ae > ls) {
+            if (byte_at(buf, ls) == '#') st = 4;
+            else {
+                bc.add(1, 1);
+                int64_t t[10];
+                const int nt = head_tabs(buf, ls, ae, 10, t, lds);
+                // skipToField(8) (:223-230): NULL iff fewer than 8 tabs and the walk ends
+                // before the line end
+                const int64_t pn = nt ? t[(nt < 8 ? nt : 8) - 1] + 1 : ls;
+                st = 2;
+                if (nt < 8 && pn < ae) st = 3;
+                else if (nt >= 9) {
+                    const int gi = gt_index(buf, t[7] + 1, t[8]);
+                    if (gi >= 0) {
+                        const int64_t S = t[8] + 1;
+                        GqOp op{buf, ae, gi, Q};
+                        bool fast = gi == 0 && gt_fast(buf, S, ae, op);
+                        bool hit;
+                        if (fast) hit = op.found;
+                        else {
+                            GqOp g{buf, ae, gi, Q};
+                            gt_general(buf, S, ae, g);
+                            hit = g.found;
+                            bc.add(3, 1);
+                        }
+                        if (hit) st = 1;
+                    }
+                }
+                // nt == 8: FORMAT runs to the line end and there is no sample field -> drop
+            }
+        }
+        if (lane() == 0) status_o[li] = st;
+        bc.add(0, st == 1);
+        bc.add(2, st == 3);
     }
+    flush_counters(cnt, counters);
 }
 
 // =======================================================================================
@@ -376,9 +341,20 @@ hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t
                              uint64_t n_lines_host, int mode, int32_t *alt, int32_t *tot, uint32_t *rowpre,
                              uint8_t *status, unsigned long long *counters, hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
-    unsigned grid = grid_for((int64_t)n_lines_host, 4, 65536);
-    hipLaunchKernelGGL(k_af_records, dim3(grid), dim3(256), 0, s, buf, data_start, line_end, n_lines_dev, mode, alt,
+    unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
+    hipLaunchKernelGGL(k_af_records, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode, alt,
                        tot, rowpre, status, counters);
+    return hipGetLastError();
+}
+hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
+                             int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,
+                             hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    GqQuery Q{q_dev, qlen, strict, qa, qb};
+    unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
+    hipLaunchKernelGGL(k_gq_records, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                       strip_cr, Q, status, counters);
     return hipGetLastError();
 }
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,

@@ -5,6 +5,7 @@
 #pragma once
 #include <stddef.h>
 #include <stdint.h>
+#include <string.h>
 
 #include <string>
 
@@ -68,4 +69,15 @@ inline bool is_chrom_line(const char *s, size_t n) {
     return n >= 6 && s[0] == '#' && s[1] == 'C' && s[2] == 'H' && s[3] == 'R' && s[4] == 'O' && s[5] == 'M';
 }
 
+}  // namespace vcfxh
+
+#define VCFX_VERSION_STR "1.1.4"  // VCFX_VERSION of the reference build (CMakeLists.txt:4-9)
+
+namespace vcfxh {
+// vcfx::flag_present (vcfx_core.cpp:31-38)
+inline bool flag_present(int argc, char **argv, const char *l, const char *s) {
+    for (int i = 1; i < argc; ++i)
+        if (strcmp(argv[i], l) == 0 || (s && strcmp(argv[i], s) == 0)) return true;
+    return false;
+}
 }  // namespace vcfxh

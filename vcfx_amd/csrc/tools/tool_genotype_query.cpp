@@ -1,0 +1,177 @@
+// VCFX_genotype_query drop-in: the reference CLI (VCFX_genotype_query.cpp:350-428,
+// 624-661) on top of vcfxg_genotype_query.  The host handles the header prefix and the
+// ordered output; per-record GT matching runs on the GPU.
+#include <errno.h>
+#include <getopt.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "emit.h"
+#include "hostio.h"
+#include "tools.h"
+
+using namespace vcfxh;
+
+namespace {
+
+const char *kHelp =
+    "VCFX_genotype_query\n"
+    "Usage: VCFX_genotype_query [OPTIONS] [input.vcf]\n\n"
+    "Options:\n"
+    "  -g, --genotype-query GT  Genotype to query (e.g., \"0/1\", \"1|1\")\n"
+    "  -i, --input FILE         Input VCF file (uses fast memory-mapped I/O)\n"
+    "  --strict                 Exact string matching (no normalization)\n"
+    "  -q, --quiet              Suppress warning messages to stderr\n"
+    "  -h, --help               Display this help message and exit\n"
+    "  -v, --version            Show program version and exit\n\n"
+    "Description:\n"
+    "  Filters a VCF to retain only lines where at least one sample has the\n"
+    "  specified genotype in the 'GT' subfield.\n\n"
+    "  By default, phasing is unified (0|1 matches 0/1) and allele order is\n"
+    "  normalized (1/0 matches 0/1). Use --strict for exact matching.\n\n"
+    "Performance:\n"
+    "  File input mode (-i) uses memory-mapped I/O with SIMD optimization,\n"
+    "  providing 40-50x speedup over stdin mode for large files.\n\n"
+    "Examples:\n"
+    "  # Flexible matching (0/1 matches 0|1, 1/0, 1|0)\n"
+    "  VCFX_genotype_query -g \"0/1\" < input.vcf > het.vcf\n"
+    "  VCFX_genotype_query -g \"0/1\" -i input.vcf > het.vcf\n\n"
+    "  # Strict matching (only exact 0|1)\n"
+    "  VCFX_genotype_query -g \"0|1\" --strict < input.vcf > phased_het.vcf\n";
+
+struct Line {
+    const char *ls, *le;
+};
+
+// returns false on device error
+bool run_gq(const Input &in, bool stream_mode, const std::string &q, bool strict, bool quiet, int out_fd, Out &err) {
+    if (!stream_mode && in.n == 0) return true;  // genotypeQueryMmap :436
+    LineEmitter em(in.p, in.n, out_fd);
+    std::vector<Line> held;  // stream mode: header lines buffered until the next data line
+    auto header = [&](const char *ls, const char *le) {
+        if (stream_mode) held.push_back({ls, le});
+        else em.line(ls, le);
+    };
+    auto flush_held = [&]() {
+        for (auto &h : held) em.line(h.ls, h.le);
+        held.clear();
+    };
+    // header prefix up to and including '#CHROM' (mmap :450-478 / stream :546-563)
+    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    bool found = false;
+    size_t data_start = in.n;
+    while (next_line(p, end, ls, le)) {
+        if (le == ls) continue;
+        if (*ls == '#') {
+            header(ls, le);
+            if (is_chrom_line(ls, (size_t)(le - ls))) {
+                found = true;
+                data_start = (size_t)(p - in.p);
+                break;
+            }
+            continue;
+        }
+        if (!quiet) err.put("Error: No #CHROM header found before data lines.\n");
+        return true;
+    }
+    if (found && data_start < in.n) {
+        vcfxg_ctx *g = gpu(err.fd);
+        if (!g) return false;
+        uint64_t nl = 0;
+        vcfxg_summary s;
+        if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
+            !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
+            !gpu_ok(g, vcfxg_genotype_query(g, q.data(), q.size(), strict ? 1 : 0, 0, &s), "genotype_query", err.fd))
+            return false;
+        std::vector<uint64_t> ends(nl);
+        std::vector<uint8_t> st(nl);
+        if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||
+            !gpu_ok(g, vcfxg_fetch_lines(g, 0, nl, nullptr, nullptr, st.data()), "fetch_lines", err.fd))
+            return false;
+        uint64_t prev = data_start;
+        for (uint64_t i = 0; i < nl; i++) {
+            const char *a = in.p + prev, *b = in.p + ends[i];
+            prev = ends[i] + 1;
+            switch (st[i]) {
+            case VCFXG_LINE_HEADER: header(a, b); break;
+            case VCFXG_LINE_ROW: flush_held(); em.line(a, b); break;
+            case VCFXG_LINE_DROP: flush_held(); break;
+            case VCFXG_LINE_WARN:
+                flush_held();
+                if (!quiet) {
+                    if (stream_mode) {
+                        err.put("Warning: skipping line with <9 fields: ");
+                        err.put(a, (size_t)(b - a));
+                        err.put("\n");
+                    } else err.put("Warning: skipping line with <9 fields\n");
+                }
+                break;
+            default: break;
+            }
+        }
+    }
+    em.finish();
+    if (stream_mode && !found && !quiet) err.put("Error: No #CHROM line found in VCF.\n");
+    return true;
+}
+
+}  // namespace
+
+extern "C" int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int out_fd, int err_fd) {
+    Out out(out_fd), err(err_fd);
+    // vcfx::handle_common_flags (vcfx_core.h:57-62)
+    if (flag_present(argc, argv, "--help", "-h")) {
+        out.put(kHelp);
+        return 0;
+    }
+    if (flag_present(argc, argv, "--version", "-v")) {
+        out.put("VCFX_genotype_query version " VCFX_VERSION_STR "\n");
+        return 0;
+    }
+    std::string query, input;
+    bool strict = false, quiet = false, ok = true;
+    static struct option lo[] = {{"genotype-query", required_argument, nullptr, 'g'},
+                                 {"input", required_argument, nullptr, 'i'},
+                                 {"strict", no_argument, nullptr, 's'},
+                                 {"quiet", no_argument, nullptr, 'q'},
+                                 {"help", no_argument, nullptr, 'h'},
+                                 {"version", no_argument, nullptr, 'v'},
+                                 {nullptr, 0, nullptr, 0}};
+    GetoptStderr gs(err);
+    optind = 0;
+    int opt;
+    while ((opt = getopt_long(argc, argv, "g:i:qhv", lo, nullptr)) != -1) {
+        switch (opt) {
+        case 'g': query = optarg; break;
+        case 'i': input = optarg; break;
+        case 's': strict = true; break;
+        case 'q': quiet = true; break;
+        case 'h': gs.done(); out.put(kHelp); return 0;
+        case 'v': gs.done(); out.put("VCFX_genotype_query version 1.0\n"); return 0;
+        default: ok = false; break;
+        }
+        if (!ok) break;
+    }
+    gs.done();
+    if (ok && optind < argc && input.empty()) input = argv[optind];
+    if (!ok || query.empty()) {
+        err.put(std::string("Usage: ") + argv[0] + " -g \"0/1\" [--strict] [-i FILE] [-q]\n");
+        err.put("Use --help for usage.\n");
+        return 1;
+    }
+    Input in;
+    if (!input.empty()) {
+        if (!in.open_file(input.c_str())) {
+            err.put("Error: Cannot open file: " + input + "\n");
+            return 1;
+        }
+        out.flush();
+        return run_gq(in, false, query, strict, quiet, out_fd, err) ? 0 : 1;
+    }
+    in.read_fd(in_fd);
+    out.flush();
+    return run_gq(in, true, query, strict, quiet, out_fd, err) ? 0 : 1;
+}

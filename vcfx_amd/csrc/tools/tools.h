@@ -8,6 +8,7 @@
 
 extern "C" {
 int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int out_fd, int err_fd);
 int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd);
 }
 

@@ -35,6 +35,7 @@ SIGNATURES = {
     "vcfxg_index": (_I, [_VP, _S, ctypes.POINTER(_U64)]),
     "vcfxg_line_ends": (_I, [_VP, _U64, _U64, _VP]),
     "vcfxg_allele_freq": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_genotype_query": (_I, [_VP, _P, _S, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_fetch_text": (_I, [_VP, _VP, _S]),
     "vcfxg_fetch_lines": (_I, [_VP, _U64, _U64, _VP, _VP, _VP]),
 }
@@ -123,6 +124,13 @@ class Engine:
     def allele_freq(self, mode=MODE_FILE):
         s = Summary()
         self._chk(self.L.vcfxg_allele_freq(self.h, mode, ctypes.byref(s)), "allele_freq")
+        return s
+
+    def genotype_query(self, query, strict=False, strip_cr=False):
+        q = query.encode() if isinstance(query, str) else query
+        s = Summary()
+        self._chk(self.L.vcfxg_genotype_query(self.h, q, len(q), int(strict), int(strip_cr), ctypes.byref(s)),
+                  "genotype_query")
         return s
 
     def text(self, nbytes):
