@@ -8,9 +8,9 @@ ARCH ?= gfx950
 B := build
 GPU_SRC := vcfx_amd/csrc/gpu
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -I$(GPU_SRC)
-GPU_OBJS := $(B)/obj/vcfxg_kernels.o $(B)/obj/vcfxg_api.o
+GPU_OBJS := $(B)/obj/vcfxg_kernels.o $(B)/obj/vcfxg_rf.o $(B)/obj/vcfxg_api.o $(B)/obj/vcfxg_decimal.o
 
-TOOLS := VCFX_allele_freq_calc VCFX_genotype_query
+TOOLS := VCFX_allele_freq_calc VCFX_genotype_query VCFX_record_filter
 HOST_SRC := vcfx_amd/csrc/host
 TOOL_SRC := vcfx_amd/csrc/tools
 CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wno-unused-result -Iinclude -I$(HOST_SRC) -I$(TOOL_SRC)
@@ -38,6 +38,10 @@ $(B)/src/%: $(TOOL_SRC)/binary_main.cpp $(B)/libvcfx_tools.so
 $(B)/obj/vcfxg_%.o: $(GPU_SRC)/vcfxg_%.hip $(wildcard $(GPU_SRC)/*.h) include/vcfx_gpu.h
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(B)/obj/vcfxg_decimal.o: $(GPU_SRC)/vcfxg_decimal.cpp $(GPU_SRC)/vcfxg_decimal.h
+	@mkdir -p $(dir $@)
+	$(CXX) -O2 -std=c++17 -fPIC -Wall -c -o $@ $<
 
 $(B)/libvcfx_gpu.so: $(GPU_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^

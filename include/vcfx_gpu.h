@@ -107,6 +107,36 @@ int vcfxg_allele_freq(vcfxg_ctx *ctx, int mode, vcfxg_summary *out);
 int vcfxg_genotype_query(vcfxg_ctx *ctx, const char *query, size_t qlen, int strict, int strip_cr,
                          vcfxg_summary *out);
 
+/* ---- K3: record filter -----------------------------------------------------------------
+ * One compiled criterion of VCFX_record_filter (FilterCriterion, VCFX_record_filter.h:37-44,
+ * as produced by parseSingleCriterion :89-171): target = 0 POS, 1 QUAL, 2 FILTER, 3 INFO
+ * key; op = 0 >, 1 >=, 2 <, 3 <=, 4 ==, 5 !=; numeric = the value parsed fully by strtod
+ * (value = that double); key = the INFO key (field name); str = the string value. */
+typedef struct {
+    int target;
+    int op;
+    int numeric;
+    double value;
+    const char *key;
+    size_t key_len;
+    const char *str;
+    size_t str_len;
+} vcfxg_criterion;
+
+/* Per line status: ROW = data line passes (AND: all criteria, OR: any), DROP, HEADER ('#',
+ * printed without its '\r'), SKIP = empty after '\r' strip (printed as "\n").  Numeric
+ * comparisons are exact: strtod(field) is never approximated (see vcfxg_num.h).  Replaces
+ * evaluateLine / evaluateCriterion (VCFX_record_filter.cpp:333-401), extractField :207-229,
+ * extractInfoValue :234-267, parseDouble :273-299 per record. */
+int vcfxg_record_filter(vcfxg_ctx *ctx, const vcfxg_criterion *crit, int n, int and_logic, vcfxg_summary *out);
+
+/* Fused `VCFX_record_filter ... | VCFX_genotype_query ...`: the filter as above, then the
+ * genotype query on the lines the filter keeps, evaluated as the filter prints them ('\r'
+ * stripped).  Status of a filter-kept data line: ROW = query matches, 6 = no match, 7 =
+ * "<9 fields" warning; other lines keep the filter's status. */
+int vcfxg_filter_query(vcfxg_ctx *ctx, const vcfxg_criterion *crit, int n, int and_logic, const char *query,
+                       size_t qlen, int strict, vcfxg_summary *out);
+
 /* device-formatted output text (without the column header line) */
 int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);
 /* per-line results of the last record kernel: any pointer may be NULL */

@@ -11,7 +11,9 @@
 #include <vector>
 
 #include "vcfx_gpu.h"
+#include "vcfxg_decimal.h"
 #include "vcfxg_kernels.h"
+#include "vcfxg_rf.h"
 
 namespace {
 
@@ -39,8 +41,8 @@ struct vcfxg_ctx {
     uint64_t n_lines = 0;
     bool indexed = false;
     // per-line results
-    DevBuf alt, tot, rowpre, status, rowlen, rowoff, text, counters, query;
-    std::string query_host;
+    DevBuf alt, tot, rowpre, status, rowlen, rowoff, text, counters, query, crit, pool;
+    std::string query_host, crit_host, pool_host;  // host sources of in-flight async copies
     uint64_t text_bytes = 0;
     // profiling
     bool profiling = false;
@@ -165,7 +167,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
-                      &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query})
+                      &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool})
         if (b->p) (void)hipFree(b->p);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
@@ -377,7 +379,8 @@ int vcfxg_genotype_query(vcfxg_ctx *c, const char *query, size_t qlen, int stric
     prof_begin(c, "gq_records");
     HIPCHK(c, vcfxg::launch_gq_records(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
                                        P<uint64_t>(c->d_nlines), L, strip_cr, P<char>(c->query), (int)qlen, strict,
-                                       qa, qb, P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+                                       qa, qb, P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream,
+                                       nullptr));
     prof_end(c, "gq_records");
     static thread_local uint64_t host_cnt[4];
     HIPCHK(c, hipMemcpyAsync(host_cnt, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
@@ -391,6 +394,122 @@ int vcfxg_genotype_query(vcfxg_ctx *c, const char *query, size_t qlen, int stric
         out->warn_lines = host_cnt[2];
         out->general_records = host_cnt[3];
         out->text_bytes = 0;
+    }
+    return VCFXG_OK;
+}
+
+static vcfxg::DecRef put_dec(const vcfxg::DecHost &d, std::string &pool) {
+    vcfxg::DecRef r;
+    r.sign = d.sign;
+    r.exp = d.exp;
+    r.off = (uint32_t)pool.size();
+    r.n = (uint32_t)d.digits.size();
+    r.inf = d.inf;
+    pool += d.digits;
+    return r;
+}
+
+static int compile_criteria(vcfxg_ctx *c, const vcfxg_criterion *crit, int n) {
+    std::vector<vcfxg::RfCrit> dev((size_t)n);
+    std::string pool;
+    for (int i = 0; i < n; i++) {
+        const vcfxg_criterion &h = crit[i];
+        vcfxg::RfCrit &d = dev[(size_t)i];
+        std::memset(&d, 0, sizeof d);
+        d.target = h.target;
+        d.op = h.op;
+        d.numeric = h.numeric;
+        d.key_off = (uint32_t)pool.size();
+        d.key_len = (uint32_t)h.key_len;
+        pool.append(h.key ? h.key : "", h.key_len);
+        d.str_off = (uint32_t)pool.size();
+        d.str_len = (uint32_t)h.str_len;
+        pool.append(h.str ? h.str : "", h.str_len);
+        vcfxg::ThresholdHost th;
+        vcfxg::threshold_bounds(h.numeric ? h.value : 0.0, th);
+        d.T.t = h.numeric ? h.value : 0.0;
+        d.T.kind = th.kind;
+        d.T.lo = put_dec(th.lo, pool);
+        d.T.hi = put_dec(th.hi, pool);
+        d.T.lo_to_t = th.lo_to_t;
+        d.T.hi_to_t = th.hi_to_t;
+    }
+    int r = ensure(c, c->crit, sizeof(vcfxg::RfCrit) * (size_t)(n + 1));
+    if (!r) r = ensure(c, c->pool, pool.size() + 16);
+    if (r) return r;
+    c->crit_host.assign((const char *)dev.data(), sizeof(vcfxg::RfCrit) * (size_t)n);
+    c->pool_host = pool;
+    if (n)
+        HIPCHK(c, hipMemcpyAsync(c->crit.p, c->crit_host.data(), c->crit_host.size(), hipMemcpyHostToDevice, c->stream));
+    if (!pool.empty())
+        HIPCHK(c, hipMemcpyAsync(c->pool.p, c->pool_host.data(), pool.size(), hipMemcpyHostToDevice, c->stream));
+    return VCFXG_OK;
+}
+
+static int run_rf(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and_logic) {
+    int r = ensure(c, c->status, c->n_lines + 1);
+    if (!r) r = compile_criteria(c, crit, n);
+    if (r) return r;
+    prof_begin(c, "rf_records");
+    HIPCHK(c, vcfxg::launch_rf_records(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
+                                       P<uint64_t>(c->d_nlines), c->n_lines, P<vcfxg::RfCrit>(c->crit), n, and_logic,
+                                       P<char>(c->pool), P<uint8_t>(c->status), P<unsigned long long>(c->counters),
+                                       c->stream));
+    prof_end(c, "rf_records");
+    return VCFXG_OK;
+}
+
+int vcfxg_record_filter(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and_logic, vcfxg_summary *out) {
+    if (!c || n < 0 || (n && !crit)) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    int r = run_rf(c, crit, n, and_logic);
+    if (r) return r;
+    static thread_local uint64_t host_cnt[2];
+    HIPCHK(c, hipMemcpyAsync(host_cnt, c->counters.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    if (out) {
+        std::memset(out, 0, sizeof *out);
+        out->n_lines = c->n_lines;
+        out->rows = host_cnt[0];
+        out->data_lines = host_cnt[1];
+    }
+    return VCFXG_OK;
+}
+
+int vcfxg_filter_query(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and_logic, const char *query, size_t qlen,
+                       int strict, vcfxg_summary *out) {
+    if (!c || n < 0 || (n && !crit) || (!query && qlen)) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    int r = run_rf(c, crit, n, and_logic);
+    if (!r) r = ensure(c, c->query, qlen + 1);
+    if (r) return r;
+    int qa = -1, qb = -1;
+    if (!strict) gq_parse_query(query, qlen, qa, qb);
+    c->query_host.assign(query, qlen);
+    if (qlen)
+        HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), qlen, hipMemcpyHostToDevice, c->stream));
+    prof_begin(c, "gq_records");
+    HIPCHK(c, vcfxg::launch_gq_records(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
+                                       P<uint64_t>(c->d_nlines), c->n_lines, 1, P<char>(c->query), (int)qlen, strict,
+                                       qa, qb, P<uint8_t>(c->status), P<unsigned long long>(c->counters) + 4,
+                                       c->stream, P<uint8_t>(c->status)));
+    prof_end(c, "gq_records");
+    static thread_local uint64_t host_cnt[8];
+    HIPCHK(c, hipMemcpyAsync(host_cnt, c->counters.p, 64, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    if (out) {
+        std::memset(out, 0, sizeof *out);
+        out->n_lines = c->n_lines;
+        out->rows = host_cnt[4];        // kept by both stages
+        out->data_lines = host_cnt[0];  // kept by record_filter
+        out->warn_lines = host_cnt[6];
+        out->general_records = host_cnt[7];
     }
     return VCFXG_OK;
 }

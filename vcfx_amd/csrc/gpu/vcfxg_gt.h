@@ -18,17 +18,18 @@ struct DwordView {
     uint32_t d;    // canonical sample dword: byte0 = allele a, byte1 = sep, byte2 = allele b
     uint32_t f;    // (d ^ exp) & 0x00FF00FF: allele digit values in 16-bit fields
     uint32_t dig;  // bit 8 / bit 24 set where the allele is a digit
+    bool real;     // false: padding outside [S, E) (neutral ". ." bytes)
 };
 
 template <class Op>
-__device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_t &err, Op &op) {
+__device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_t &err, Op &op, bool real) {
     uint32_t e = d ^ exp_xor;
     err |= e & 0xFF00FF00u;
     uint32_t f = e & 0x00FF00FFu;
     uint32_t notdig = (f + 0x00F600F6u) & 0x01000100u;  // field >= 10
     uint32_t notdot = ((f ^ 0x001E001Eu) + 0x00FF00FFu) & 0x01000100u;
     err |= notdig & notdot;
-    DwordView v{d, f, notdig ^ 0x01000100u};
+    DwordView v{d, f, notdig ^ 0x01000100u, real};
     op.dword(v);
 }
 
@@ -69,16 +70,19 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
                                  __builtin_amdgcn_alignbyte(v[u].z, v[u].y, s),
                                  __builtin_amdgcn_alignbyte(v[u].w, v[u].z, s),
                                  __builtin_amdgcn_alignbyte(x4[u], v[u].w, s)};
+                bool real[4] = {true, true, true, true};
                 if (!interior) {
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
                         int64_t p = blk + s + 4 * i;
-                        if (p < S || p + 3 > E) d[i] = neutral;
-                        else if (p + 3 == E) d[i] = (d[i] & 0x00FFFFFFu) | 0x09000000u;
+                        if (p < S || p + 3 > E) {
+                            d[i] = neutral;
+                            real[i] = false;
+                        } else if (p + 3 == E) d[i] = (d[i] & 0x00FFFFFFu) | 0x09000000u;
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op);
+                for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op, real[i]);
             }
         }
         if (op.done()) break;  // wave-uniform early exit (e.g. a match was found)
@@ -261,7 +265,7 @@ struct GqOp {
     __device__ bool done() { return found = found || __any(any); }
     __device__ void dword(const DwordView &v) {
         uint32_t x = v.d & pmask;
-        any = any || (pmask && (x == p1 || x == p2));
+        any = any || (v.real && pmask && (x == p1 || x == p2));
     }
     __device__ void sample(int64_t st) {
         if (any) return;

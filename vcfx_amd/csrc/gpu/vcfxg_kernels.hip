@@ -195,7 +195,8 @@ __global__ __launch_bounds__(kRecThreads) void k_gq_records(const char *__restri
                                                             const uint64_t *__restrict__ line_end,
                                                             const uint64_t *n_lines_p, int strip_cr, GqQuery Q,
                                                             uint8_t *__restrict__ status_o,
-                                                            unsigned long long *__restrict__ counters) {
+                                                            unsigned long long *__restrict__ counters,
+                                                            const uint8_t *gate) {
     __shared__ int64_t scratch[kRecWaves][16];
     __shared__ uint32_t cnt[BlockCounters::kNC];
     if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
@@ -206,6 +207,8 @@ __global__ __launch_bounds__(kRecThreads) void k_gq_records(const char *__restri
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
     for (uint64_t li = wid; li < n_lines; li += nw) {
+        // gated (fused record_filter | genotype_query): only lines record_filter kept
+        if (gate && uniform32(gate[li]) != 1) continue;
         int64_t ls, le;
         line_bounds(line_end, data_start, li, ls, le);
         int64_t ae = le;
@@ -242,9 +245,10 @@ __global__ __launch_bounds__(kRecThreads) void k_gq_records(const char *__restri
                 // nt == 8: FORMAT runs to the line end and there is no sample field -> drop
             }
         }
-        if (lane() == 0) status_o[li] = st;
         bc.add(0, st == 1);
         bc.add(2, st == 3);
+        if (gate) st = st == 1 ? 1 : (st == 3 ? 7 : 6);  // kept-by-filter: match / warn / no match
+        if (lane() == 0) status_o[li] = st;
     }
     flush_counters(cnt, counters);
 }
@@ -349,12 +353,12 @@ hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
                              int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,
-                             hipStream_t s) {
+                             hipStream_t s, const uint8_t *gate) {
     if (!n_lines_host) return hipSuccess;
     GqQuery Q{q_dev, qlen, strict, qa, qb};
     unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
     hipLaunchKernelGGL(k_gq_records, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
-                       strip_cr, Q, status, counters);
+                       strip_cr, Q, status, counters, gate);
     return hipGetLastError();
 }
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,

@@ -1,0 +1,243 @@
+// VCFX_record_filter drop-in: the reference CLI (VCFXRecordFilter::run,
+// VCFX_record_filter.cpp:584-658, main :819-827) on top of vcfxg_record_filter.
+// Criteria are compiled on the host exactly as parseCriteria / parseSingleCriterion do
+// (:89-202); every data record is evaluated on the GPU; kept lines are written from the
+// host copy of the input.
+#include <getopt.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "emit.h"
+#include "hostio.h"
+#include "tools.h"
+
+using namespace vcfxh;
+
+namespace {
+
+const char *kHelp =
+    "VCFX_record_filter: Filter VCF data lines by multiple criteria.\n\n"
+    "Usage:\n"
+    "  VCFX_record_filter [options] --filter \"CRITERIA\" [input.vcf]\n"
+    "  VCFX_record_filter [options] --filter \"CRITERIA\" < input.vcf > output.vcf\n\n"
+    "Options:\n"
+    "  -f, --filter \"...\"   One or more criteria separated by semicolons, e.g.\n"
+    "                        \"POS>10000; QUAL>=30; AF<0.05; FILTER==PASS\"\n"
+    "                        Each criterion must use an operator among >,>=,<,<=,==,!=\n\n"
+    "  -l, --logic and|or    'and' => a line must pass all criteria (default)\n"
+    "                        'or'  => pass if any criterion is satisfied.\n"
+    "  -i <file>             Input file (uses memory-mapped I/O for speed)\n"
+    "  -q, --quiet           Suppress warnings\n"
+    "  -h, --help            Show this help.\n\n"
+    "Fields:\n"
+    "  POS => numeric, QUAL => numeric, FILTER => string.\n"
+    "  Others => assumed to be an INFO key. We try numeric parse if the criterion is numeric, else string.\n\n"
+    "Performance:\n"
+    "  Pass file directly for memory-mapped I/O (fastest).\n"
+    "  Uses SIMD-optimized parsing on x86_64.\n"
+    "  Zero-copy string_view parsing eliminates allocations.\n\n"
+    "Example:\n"
+    "  VCFX_record_filter --filter \"POS>=1000;FILTER==PASS;DP>10\" --logic and input.vcf\n"
+    "  VCFX_record_filter -f \"QUAL>=30\" < in.vcf > out.vcf\n";
+
+}  // namespace
+
+namespace vcfxh {
+
+static std::string trim_view(const std::string &s) {  // trimView :65-71 (spaces and tabs)
+    size_t a = 0, b = s.size();
+    while (a < b && (s[a] == ' ' || s[a] == '\t')) a++;
+    while (b > a && (s[b - 1] == ' ' || s[b - 1] == '\t')) b--;
+    return s.substr(a, b - a);
+}
+
+// parseCriteria / parseSingleCriterion (VCFX_record_filter.cpp:89-202)
+bool compile_filter(const std::string &all, std::vector<Criterion> &out, Out &err) {
+    static const char *ops[] = {">=", "<=", "==", "!=", ">", "<"};
+    static const int opv[] = {1, 3, 4, 5, 0, 2};  // vcfxg_criterion op codes
+    out.clear();
+    size_t start = 0;
+    while (start < all.size()) {
+        size_t end = all.find(';', start);
+        if (end == std::string::npos) end = all.size();
+        std::string tok = trim_view(all.substr(start, end - start));
+        if (!tok.empty()) {
+            size_t pos = std::string::npos, ol = 0;
+            int op = 0;
+            for (int i = 0; i < 6; i++) {
+                size_t p = tok.find(ops[i]);
+                if (p != std::string::npos) {
+                    pos = p;
+                    ol = strlen(ops[i]);
+                    op = opv[i];
+                    break;
+                }
+            }
+            if (pos == std::string::npos) {
+                err.put("Error: no operator found in '" + tok + "'.\n");
+                return false;
+            }
+            std::string name = trim_view(tok.substr(0, pos)), val = trim_view(tok.substr(pos + ol));
+            if (name.empty()) {
+                err.put("Error: empty field name in '" + tok + "'.\n");
+                return false;
+            }
+            if (val.empty()) {
+                err.put("Error: no value in '" + tok + "'.\n");
+                return false;
+            }
+            Criterion c;
+            c.name = name;
+            c.op = op;
+            c.target = name == "POS" ? 0 : name == "QUAL" ? 1 : name == "FILTER" ? 2 : 3;
+            char *ep = nullptr;
+            std::string tmp(val);  // strtod on a NUL-terminated copy (:143-158)
+            double d = strtod(tmp.c_str(), &ep);
+            c.numeric = ep == tmp.c_str() + tmp.size();
+            if (c.numeric) c.value = d;
+            else c.str = val;
+            out.push_back(c);
+        }
+        start = end + 1;
+    }
+    if (out.empty()) {
+        err.put("Error: no valid criteria in '" + all + "'.\n");
+        return false;
+    }
+    return true;
+}
+
+std::vector<vcfxg_criterion> to_abi(const std::vector<Criterion> &cs) {
+    std::vector<vcfxg_criterion> v;
+    for (auto &c : cs)
+        v.push_back({c.target, c.op, c.numeric ? 1 : 0, c.value, c.name.data(), c.name.size(), c.str.data(),
+                     c.str.size()});
+    return v;
+}
+
+}  // namespace vcfxh
+
+namespace {
+
+// processFileMmap (:406-493) / processStdin (:498-549)
+bool run_rf(const Input &in, bool stdin_mode, const std::vector<Criterion> &cs, bool and_logic, int out_fd,
+            Out &err) {
+    LineEmitter em(in.p, in.n, out_fd);
+    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    size_t data_start = in.n;
+    auto strip = [](const char *a, const char *b) { return (b > a && b[-1] == '\r') ? b - 1 : b; };
+    while (next_line(p, end, ls, le)) {
+        const char *ae = strip(ls, le);
+        if (ae == ls) {
+            em.raw("\n", 1);
+            continue;
+        }
+        if (*ls == '#') {
+            em.line(ls, ae);
+            if (is_chrom_line(ls, (size_t)(ae - ls))) {
+                data_start = (size_t)(p - in.p);
+                break;
+            }
+            continue;
+        }
+        if (stdin_mode) err.put("Warning: data line before #CHROM => skipping.\n");
+    }
+    if (data_start >= in.n) return true;
+    vcfxg_ctx *g = gpu(err.fd);
+    if (!g) return false;
+    uint64_t nl = 0;
+    vcfxg_summary s;
+    std::vector<vcfxg_criterion> abi = to_abi(cs);
+    if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
+        !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
+        !gpu_ok(g, vcfxg_record_filter(g, abi.data(), (int)abi.size(), and_logic ? 1 : 0, &s), "record_filter",
+                err.fd))
+        return false;
+    std::vector<uint64_t> ends(nl);
+    std::vector<uint8_t> st(nl);
+    if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||
+        !gpu_ok(g, vcfxg_fetch_lines(g, 0, nl, nullptr, nullptr, st.data()), "fetch_lines", err.fd))
+        return false;
+    uint64_t prev = data_start;
+    for (uint64_t i = 0; i < nl; i++) {
+        const char *a = in.p + prev, *b = in.p + ends[i];
+        prev = ends[i] + 1;
+        if (st[i] == VCFXG_LINE_SKIP) em.raw("\n", 1);
+        else if (st[i] == VCFXG_LINE_ROW || st[i] == VCFXG_LINE_HEADER) em.line(a, strip(a, b));
+    }
+    em.finish();
+    return true;
+}
+
+}  // namespace
+
+extern "C" int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out_fd, int err_fd) {
+    Out out(out_fd), err(err_fd);
+    if (flag_present(argc, argv, "--help", "-h")) {
+        out.put(kHelp);
+        return 0;
+    }
+    if (flag_present(argc, argv, "--version", "-v")) {
+        out.put("VCFX_record_filter version " VCFX_VERSION_STR "\n");
+        return 0;
+    }
+    std::string crit, logic = "and", input;
+    bool show = false;
+    static struct option lo[] = {{"help", no_argument, 0, 'h'},
+                                 {"filter", required_argument, 0, 'f'},
+                                 {"logic", required_argument, 0, 'l'},
+                                 {"quiet", no_argument, 0, 'q'},
+                                 {0, 0, 0, 0}};
+    GetoptStderr gs(err);
+    optind = 0;
+    for (;;) {
+        int c = getopt_long(argc, argv, "hf:l:i:q", lo, nullptr);
+        if (c == -1) break;
+        switch (c) {
+        case 'h': show = true; break;
+        case 'f': crit = optarg; break;
+        case 'l': logic = optarg; break;
+        case 'i': input = optarg; break;
+        case 'q': break;
+        default: show = true;
+        }
+    }
+    gs.done();
+    if (optind < argc && input.empty()) input = argv[optind];
+    if (show || argc == 1) {
+        out.put(kHelp);
+        return 0;
+    }
+    if (crit.empty()) {
+        err.put("Error: must provide --filter \"CRITERIA\".\n");
+        out.put(kHelp);
+        return 1;
+    }
+    bool and_logic;
+    if (logic == "and") and_logic = true;
+    else if (logic == "or") and_logic = false;
+    else {
+        err.put("Error: logic must be 'and' or 'or'.\n");
+        return 1;
+    }
+    std::vector<Criterion> cs;
+    if (!compile_filter(crit, cs, err)) {
+        err.put("Error: failed to parse criteria.\n");
+        return 1;
+    }
+    Input in;
+    out.flush();
+    if (!input.empty() && input != "-") {
+        if (!in.open_file(input.c_str())) {
+            err.put("Error: cannot open file '" + input + "'\n");
+            return 1;
+        }
+        if (in.n == 0) return 0;
+        return run_rf(in, false, cs, and_logic, out_fd, err) ? 0 : 1;
+    }
+    in.read_fd(in_fd);
+    return run_rf(in, true, cs, and_logic, out_fd, err) ? 0 : 1;
+}

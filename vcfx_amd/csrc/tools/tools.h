@@ -3,16 +3,38 @@
 // call them in-process to reuse one GPU context across many cases.
 #pragma once
 #include <stdio.h>
+#include <stdlib.h>
+
+#include <string>
+#include <vector>
 
 #include "hostio.h"
 
 extern "C" {
 int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int out_fd, int err_fd);
 int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_variant_counter(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out_fd, int err_fd);
 int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd);
+// fused `VCFX_record_filter --filter F --logic L [-i input] | VCFX_genotype_query -g Q
+// [--strict] [-q]` in one process (input = NULL: read in_fd)
+int vcfx_pipeline_filter_query(const char *filter, const char *logic, const char *input, const char *query, int strict,
+                               int gq_quiet, int in_fd, int out_fd, int err_fd);
 }
 
 namespace vcfxh {
+
+// compiled record_filter criterion (FilterCriterion, VCFX_record_filter.h:37-44)
+struct Criterion {
+    std::string name, str;
+    int op = 0, target = 0;
+    bool numeric = false;
+    double value = 0.0;
+};
+bool compile_filter(const std::string &all, std::vector<Criterion> &out, Out &err);
+std::vector<vcfxg_criterion> to_abi(const std::vector<Criterion> &cs);
+
 // getopt_long prints its diagnostics on the C stderr stream; route them to the tool's
 // err fd (identical text to the reference's getopt messages).
 struct GetoptStderr {

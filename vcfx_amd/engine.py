@@ -17,6 +17,17 @@ class Summary(ctypes.Structure):
                 ("general_records", ctypes.c_uint64)]
 
 
+class Criterion(ctypes.Structure):
+    _fields_ = [("target", ctypes.c_int), ("op", ctypes.c_int), ("numeric", ctypes.c_int), ("value", ctypes.c_double),
+                ("key", ctypes.c_char_p), ("key_len", ctypes.c_size_t), ("str", ctypes.c_char_p),
+                ("str_len", ctypes.c_size_t)]
+
+
+# record_filter criterion codes (vcfx_gpu.h vcfxg_criterion)
+POS, QUAL, FILTER, INFO = 0, 1, 2, 3
+GT, GE, LT, LE, EQ, NE = 0, 1, 2, 3, 4, 5
+
+
 # every exported entry point: name -> (restype, argtypes)
 _P, _VP, _S, _U64, _I = ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_int
 SIGNATURES = {
@@ -36,6 +47,8 @@ SIGNATURES = {
     "vcfxg_line_ends": (_I, [_VP, _U64, _U64, _VP]),
     "vcfxg_allele_freq": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
     "vcfxg_genotype_query": (_I, [_VP, _P, _S, _I, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_record_filter": (_I, [_VP, _VP, _I, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_filter_query": (_I, [_VP, _VP, _I, _I, _P, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_fetch_text": (_I, [_VP, _VP, _S]),
     "vcfxg_fetch_lines": (_I, [_VP, _U64, _U64, _VP, _VP, _VP]),
 }
@@ -131,6 +144,32 @@ class Engine:
         s = Summary()
         self._chk(self.L.vcfxg_genotype_query(self.h, q, len(q), int(strict), int(strip_cr), ctypes.byref(s)),
                   "genotype_query")
+        return s
+
+    def _criteria(self, crits):
+        """crits: list of (target, op, numeric, value, key, str) as vcfxg_criterion."""
+        arr = (Criterion * max(1, len(crits)))()
+        self._keep = []
+        for i, (target, op, numeric, value, key, sval) in enumerate(crits):
+            k = key.encode() if isinstance(key, str) else key
+            s = sval.encode() if isinstance(sval, str) else sval
+            self._keep += [k, s]
+            arr[i] = Criterion(target, op, int(numeric), float(value), k, len(k), s, len(s))
+        return arr
+
+    def record_filter(self, crits, and_logic=True):
+        s = Summary()
+        arr = self._criteria(crits)
+        self._chk(self.L.vcfxg_record_filter(self.h, ctypes.cast(arr, ctypes.c_void_p), len(crits), int(and_logic),
+                                             ctypes.byref(s)), "record_filter")
+        return s
+
+    def filter_query(self, crits, query, and_logic=True, strict=False):
+        s = Summary()
+        arr = self._criteria(crits)
+        q = query.encode() if isinstance(query, str) else query
+        self._chk(self.L.vcfxg_filter_query(self.h, ctypes.cast(arr, ctypes.c_void_p), len(crits), int(and_logic), q,
+                                            len(q), int(strict), ctypes.byref(s)), "filter_query")
         return s
 
     def text(self, nbytes):

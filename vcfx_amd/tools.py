@@ -45,3 +45,29 @@ def run(argv, stdin=None, cwd=None):
         fo.seek(0)
         fe.seek(0)
         return fo.read(), fe.read(), rc
+
+
+def pipeline_filter_query(filter_, query, input_path=None, stdin=None, logic="and", strict=False, gq_quiet=False,
+                          cwd=None):
+    """Fused `VCFX_record_filter --filter F --logic L [input] | VCFX_genotype_query -g Q`."""
+    L = lib()
+    f = L.vcfx_pipeline_filter_query
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                  ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    old = os.getcwd()
+    with tempfile.TemporaryFile() as fi, tempfile.TemporaryFile() as fo, tempfile.TemporaryFile() as fe:
+        if stdin:
+            fi.write(stdin)
+            fi.flush()
+            fi.seek(0)
+        if cwd:
+            os.chdir(cwd)
+        try:
+            rc = f(filter_.encode(), logic.encode(), input_path.encode() if input_path else None, query.encode(),
+                   int(strict), int(gq_quiet), fi.fileno(), fo.fileno(), fe.fileno())
+        finally:
+            os.chdir(old)
+        fo.seek(0)
+        fe.seek(0)
+        return fo.read(), fe.read(), rc
