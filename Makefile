@@ -10,7 +10,7 @@ GPU_SRC := vcfx_amd/csrc/gpu
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -I$(GPU_SRC)
 GPU_OBJS := $(B)/obj/vcfxg_kernels.o $(B)/obj/vcfxg_rf.o $(B)/obj/vcfxg_api.o $(B)/obj/vcfxg_decimal.o
 
-TOOLS := VCFX_allele_freq_calc VCFX_genotype_query VCFX_record_filter
+TOOLS := VCFX_allele_freq_calc VCFX_genotype_query VCFX_record_filter VCFX_variant_counter
 HOST_SRC := vcfx_amd/csrc/host
 TOOL_SRC := vcfx_amd/csrc/tools
 CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wno-unused-result -Iinclude -I$(HOST_SRC) -I$(TOOL_SRC)
@@ -28,7 +28,7 @@ $(B)/obj/%.o: $(TOOL_SRC)/%.cpp $(wildcard $(TOOL_SRC)/*.h) $(wildcard $(HOST_SR
 	$(CXX) $(CXXFLAGS) -c -o $@ $<
 
 $(B)/libvcfx_tools.so: $(TOOL_OBJS) $(B)/libvcfx_gpu.so
-	$(CXX) -shared -o $@ $(TOOL_OBJS) -L$(B) -lvcfx_gpu -Wl,-rpath,'$$ORIGIN'
+	$(CXX) -shared -o $@ $(TOOL_OBJS) -L$(B) -lvcfx_gpu -lz -Wl,-rpath,'$$ORIGIN'
 
 # drop-in executables at build/src/VCFX_<t>/VCFX_<t> (the reference test scripts' layout)
 $(B)/src/%: $(TOOL_SRC)/binary_main.cpp $(B)/libvcfx_tools.so

@@ -137,6 +137,13 @@ int vcfxg_record_filter(vcfxg_ctx *ctx, const vcfxg_criterion *crit, int n, int 
 int vcfxg_filter_query(vcfxg_ctx *ctx, const vcfxg_criterion *crit, int n, int and_logic, const char *query,
                        size_t qlen, int strict, vcfxg_summary *out);
 
+/* ---- variant counter -------------------------------------------------------------------
+ * Per line status: ROW = data line with >= 8 tab-separated columns (counted), WARN = fewer
+ * columns, SKIP = empty or '#'.  strip_cr: drop a trailing '\r' first (file path).
+ * Replaces countVariantsMmap / countVariants per-line work (VCFX_variant_counter.cpp:
+ * 182-202, 317-389) and hasEightColumnsFast :31-44.  rows = Total Variants. */
+int vcfxg_variant_count(vcfxg_ctx *ctx, int strip_cr, vcfxg_summary *out);
+
 /* device-formatted output text (without the column header line) */
 int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);
 /* per-line results of the last record kernel: any pointer may be NULL */

@@ -43,6 +43,6 @@ def test_tools_lib_exports():
     assert hasattr(lib, "vcfx_tool_main")
 
 
-@pytest.mark.parametrize("tool", ["VCFX_allele_freq_calc", "VCFX_genotype_query", "VCFX_record_filter"])
+@pytest.mark.parametrize("tool", ["VCFX_allele_freq_calc", "VCFX_genotype_query", "VCFX_record_filter", "VCFX_variant_counter"])
 def test_binaries_present(tool):
     assert os.access(tool_binary(tool), os.X_OK)

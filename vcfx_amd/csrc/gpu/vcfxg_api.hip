@@ -514,6 +514,31 @@ int vcfxg_filter_query(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and
     return VCFXG_OK;
 }
 
+int vcfxg_variant_count(vcfxg_ctx *c, int strip_cr, vcfxg_summary *out) {
+    if (!c) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    int r = ensure(c, c->status, c->n_lines + 1);
+    if (r) return r;
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    prof_begin(c, "vc_records");
+    HIPCHK(c, vcfxg::launch_vc_records(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
+                                       P<uint64_t>(c->d_nlines), c->n_lines, strip_cr, P<uint8_t>(c->status),
+                                       P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "vc_records");
+    static thread_local uint64_t host_cnt[2];
+    HIPCHK(c, hipMemcpyAsync(host_cnt, c->counters.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    if (out) {
+        std::memset(out, 0, sizeof *out);
+        out->n_lines = c->n_lines;
+        out->rows = host_cnt[0];
+        out->warn_lines = host_cnt[1];
+    }
+    return VCFXG_OK;
+}
+
 int vcfxg_fetch_text(vcfxg_ctx *c, char *host, size_t cap) {
     if (!c || (!host && c->text_bytes)) return VCFXG_E_ARG;
     if (cap < c->text_bytes) return VCFXG_E_CAP;

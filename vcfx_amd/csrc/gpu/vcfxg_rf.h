@@ -16,6 +16,9 @@ struct RfCrit {
     uint32_t str_off, str_len;  // string value in the pool
 };
 
+hipError_t launch_vc_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                             uint64_t n_lines_host, int strip_cr, uint8_t *status, unsigned long long *counters,
+                             hipStream_t s);
 hipError_t launch_rf_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, const RfCrit *crit, int ncrit, int and_logic, const char *pool,
                              uint8_t *status, unsigned long long *counters, hipStream_t s);

@@ -48,6 +48,7 @@ SIGNATURES = {
     "vcfxg_allele_freq": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
     "vcfxg_genotype_query": (_I, [_VP, _P, _S, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_record_filter": (_I, [_VP, _VP, _I, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_variant_count": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
     "vcfxg_filter_query": (_I, [_VP, _VP, _I, _I, _P, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_fetch_text": (_I, [_VP, _VP, _S]),
     "vcfxg_fetch_lines": (_I, [_VP, _U64, _U64, _VP, _VP, _VP]),
