@@ -144,6 +144,37 @@ int vcfxg_filter_query(vcfxg_ctx *ctx, const vcfxg_criterion *crit, int n, int a
  * 182-202, 317-389) and hasEightColumnsFast :31-44.  rows = Total Variants. */
 int vcfxg_variant_count(vcfxg_ctx *ctx, int strip_cr, vcfxg_summary *out);
 
+/* ---- K4: linkage disequilibrium ---------------------------------------------------------
+ * vcfxg_ld_prepare: every data line of the indexed region with >= 10 fields and an integer
+ * POS (and inside the region when has_region) becomes a variant: n_samples int8 genotype
+ * codes (0/1/2, -1 missing) from each sample's GT prefix, its sums and own variance, and a
+ * "CHROM\tPOS\tID" text prefix (ID "." -> "CHROM:POS" when id_dot_to_pos).  Replaces the
+ * per-record parse of computeLDStreamingMmap / computeLDMatrixMmap (VCFX_ld_calculator.cpp:
+ * 555-613, 697-759): fastParseInt :188-197, extractGT :177-185, parseGenotypeRaw :145-174,
+ * LDVariantOpt::computeStats :243-258. */
+int vcfxg_ld_prepare(vcfxg_ctx *ctx, int n_samples, int id_dot_to_pos, const char *region_chrom, size_t region_len,
+                     int has_region, int region_start, int region_end, int parse_mode, uint64_t *n_variants);
+/* parse_mode: 0 = fastParseInt POS + parseGenotypeRaw on the GT prefix (file paths, stdin
+ * streaming); 1 = the stdin matrix path's std::stoi POS + parseGenotype on the whole
+ * sample field (computeLD :1021-1045, parseGenotype :468-482). */
+/* the variants' "CHROM\tPOS\tID" prefixes (concatenated) and M+1 offsets */
+int vcfxg_ld_prefixes(vcfxg_ctx *ctx, char *text, size_t cap, uint64_t *offsets);
+/* Matrix mode body: 7*M*M bytes, row-major, cell (i, j) = "\t" + r^2 text ("1.0000" on the
+ * diagonal).  gate = computeRsqFast's own-variance gate (file path) vs computeRsq (stdin);
+ * printf4 = setprecision(4) (stdin) vs formatR2 (file).  Replaces the matrix loops of
+ * computeLDMatrixMmap :767-858 and computeLD :1050-1078. */
+int vcfxg_ld_matrix(vcfxg_ctx *ctx, int gate, int printf4, uint64_t *cell_bytes);
+/* Streaming-window pairs for new variants j in [j0, j1): every i with j - window <= i < j
+ * (pruned when max_dist > 0 and same CHROM with |POS_j - POS_i| > max_dist), r^2 exactly as
+ * computeRsqFast (:397-401 -> :352-393; int8 MFMA sums + correctly rounded fp64 epilogue),
+ * kept when r^2 >= threshold, formatted as the reference's output lines (formatR2 :200-211)
+ * in its order (j, then i ascending).  Text via vcfxg_fetch_text.  Replaces the window
+ * loop of computeLDStreamingMmap :616-646 / computeLDStreaming :954-983. */
+int vcfxg_ld_stream_chunk(vcfxg_ctx *ctx, uint64_t j0, uint64_t j1, uint64_t window, double threshold, int max_dist,
+                          uint64_t *n_pairs, uint64_t *text_bytes);
+/* checks the int8 MFMA operand layout the LD kernels assume (0 mismatches expected) */
+int vcfxg_selftest_mfma_i8(vcfxg_ctx *ctx, int *mismatches);
+
 /* device-formatted output text (without the column header line) */
 int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);
 /* per-line results of the last record kernel: any pointer may be NULL */

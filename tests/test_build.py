@@ -14,7 +14,7 @@ HDR = os.path.join(os.path.dirname(BUILD), "include", "vcfx_gpu.h")
 
 def declared_symbols():
     txt = open(HDR).read()
-    return sorted(set(re.findall(r"\b(vcfxg_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(vcfxg_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_gpu_lib_exports_header_symbols():
@@ -43,6 +43,6 @@ def test_tools_lib_exports():
     assert hasattr(lib, "vcfx_tool_main")
 
 
-@pytest.mark.parametrize("tool", ["VCFX_allele_freq_calc", "VCFX_genotype_query", "VCFX_record_filter", "VCFX_variant_counter"])
+@pytest.mark.parametrize("tool", ["VCFX_allele_freq_calc", "VCFX_genotype_query", "VCFX_record_filter", "VCFX_variant_counter", "VCFX_ld_calculator"])
 def test_binaries_present(tool):
     assert os.access(tool_binary(tool), os.X_OK)

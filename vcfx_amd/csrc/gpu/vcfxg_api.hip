@@ -13,6 +13,7 @@
 #include "vcfx_gpu.h"
 #include "vcfxg_decimal.h"
 #include "vcfxg_kernels.h"
+#include "vcfxg_ld.h"
 #include "vcfxg_rf.h"
 
 namespace {
@@ -43,6 +44,13 @@ struct vcfxg_ctx {
     // per-line results
     DevBuf alt, tot, rowpre, status, rowlen, rowoff, text, counters, query, crit, pool;
     std::string query_host, crit_host, pool_host;  // host sources of in-flight async copies
+    // LD
+    DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
+        ld_off, ld_pairs;
+    uint64_t ld_m = 0, ld_prefix_bytes = 0;
+    int ld_kpad = 64, ld_ns = 0;
+    bool ld_chrom_ids = false;
+    std::vector<uint32_t> ld_cid_host, ld_blocks_host;
     uint64_t text_bytes = 0;
     // profiling
     bool profiling = false;
@@ -167,7 +175,9 @@ void vcfxg_close(vcfxg_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
-                      &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool})
+                      &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
+                      &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs})
         if (b->p) (void)hipFree(b->p);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
@@ -536,6 +546,271 @@ int vcfxg_variant_count(vcfxg_ctx *c, int strip_cr, vcfxg_summary *out) {
         out->rows = host_cnt[0];
         out->warn_lines = host_cnt[1];
     }
+    return VCFXG_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// LD
+// ---------------------------------------------------------------------------------------
+struct U16ToU64 {
+    __host__ __device__ uint64_t operator()(const uint16_t &x) const { return x; }
+};
+
+int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char *rchrom, size_t rlen, int has_region,
+                     int rstart, int rend, int parse_mode, uint64_t *n_variants) {
+    if (!c || n_samples < 0 || (has_region && !rchrom && rlen)) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t L = c->n_lines;
+    const int kpad = n_samples > 0 ? ((n_samples + 63) / 64) * 64 : 64;  // MFMA k-steps of 32 B
+    int r = ensure(c, c->ld_G, (size_t)L * kpad + 64);
+    if (!r) r = ensure(c, c->ld_lines, sizeof(vcfxg::LdLine) * (L + 1));
+    if (!r) r = ensure(c, c->ld_vidx, 8 * (L + 1));
+    if (!r) r = ensure(c, c->ld_valid, 4 * (L + 1));
+    if (!r) r = ensure(c, c->query, rlen + 1);
+    if (r) return r;
+    c->query_host.assign(rchrom ? rchrom : "", rlen);
+    if (rlen)
+        HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), rlen, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->ld_G.p, 0xFF, (size_t)L * kpad + 64, c->stream));
+    vcfxg::LdParseArgs a{n_samples, kpad, has_region, rstart, rend, (int64_t)rlen, P<char>(c->query), parse_mode};
+    prof_begin(c, "ld_parse");
+    HIPCHK(c, vcfxg::launch_ld_parse(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
+                                     P<uint64_t>(c->d_nlines), L, a, P<int8_t>(c->ld_G), P<vcfxg::LdLine>(c->ld_lines),
+                                     c->stream));
+    prof_end(c, "ld_parse");
+    // compact order: exclusive scan of the valid flags (first member of LdLine)
+    struct ValidOf {
+        __host__ __device__ uint64_t operator()(const vcfxg::LdLine &x) const { return x.valid; }
+    };
+    hipcub::TransformInputIterator<uint64_t, ValidOf, const vcfxg::LdLine *> vin(P<vcfxg::LdLine>(c->ld_lines),
+                                                                                 ValidOf());
+    size_t tmp = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, vin, P<uint64_t>(c->ld_vidx), (int)L, c->stream));
+    r = ensure(c, c->scan_tmp, tmp);
+    if (r) return r;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, vin, P<uint64_t>(c->ld_vidx), (int)L, c->stream));
+    static thread_local uint64_t last[2];
+    static thread_local vcfxg::LdLine lastline;
+    if (L) {
+        HIPCHK(c, hipMemcpyAsync(&last[0], P<uint64_t>(c->ld_vidx) + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&lastline, P<vcfxg::LdLine>(c->ld_lines) + L - 1, sizeof lastline,
+                                 hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t M = L ? last[0] + lastline.valid : 0;
+    r = ensure(c, c->ld_Gc, (size_t)(M + 1) * kpad + 64);
+    if (!r) r = ensure(c, c->ld_vars, sizeof(vcfxg::LdVar) * (M + 1));
+    if (!r) r = ensure(c, c->ld_plen, 8 * (M + 2));
+    if (!r) r = ensure(c, c->ld_poff, 8 * (M + 2));
+    if (r) return r;
+    prof_begin(c, "ld_compact");
+    HIPCHK(c, vcfxg::launch_ld_compact(P<vcfxg::LdLine>(c->ld_lines), P<uint64_t>(c->ld_vidx), P<uint64_t>(c->d_nlines),
+                                       L, kpad, n_samples, P<int8_t>(c->ld_G), P<int8_t>(c->ld_Gc),
+                                       P<vcfxg::LdVar>(c->ld_vars), c->stream));
+    prof_end(c, "ld_compact");
+    // per-variant "chrom\tpos\tid" prefixes
+    HIPCHK(c, vcfxg::launch_ld_prefix(0, P<vcfxg::LdVar>(c->ld_vars), M, P<char>(c->input), id_dot_to_pos,
+                                      P<uint64_t>(c->ld_plen), nullptr, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->ld_plen) + M, 0, 8, c->stream));
+    r = exclusive_scan(c, P<uint64_t>(c->ld_plen), P<uint64_t>(c->ld_poff), (size_t)M + 1);
+    if (r) return r;
+    static thread_local uint64_t pbytes;
+    HIPCHK(c, hipMemcpyAsync(&pbytes, P<uint64_t>(c->ld_poff) + M, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    r = ensure(c, c->ld_prefix, pbytes + 16);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_ld_prefix(1, P<vcfxg::LdVar>(c->ld_vars), M, P<char>(c->input), id_dot_to_pos,
+                                      P<uint64_t>(c->ld_poff), P<char>(c->ld_prefix), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    c->ld_m = M;
+    c->ld_kpad = kpad;
+    c->ld_ns = n_samples;
+    c->ld_prefix_bytes = pbytes;
+    c->ld_chrom_ids = false;
+    if (n_variants) *n_variants = M;
+    return VCFXG_OK;
+}
+
+// exact chrom equality ids (for max_dist): strings are the first field of each prefix
+static int ld_chrom_ids(vcfxg_ctx *c) {
+    if (c->ld_chrom_ids) return VCFXG_OK;
+    const uint64_t M = c->ld_m;
+    std::vector<uint64_t> poff(M + 1);
+    std::string pre(c->ld_prefix_bytes, '\0');
+    HIPCHK(c, hipMemcpyAsync(poff.data(), c->ld_poff.p, 8 * (M + 1), hipMemcpyDeviceToHost, c->stream));
+    if (!pre.empty())
+        HIPCHK(c, hipMemcpyAsync(&pre[0], c->ld_prefix.p, pre.size(), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::map<std::string, uint32_t> ids;
+    std::vector<uint32_t> id(M + 1);
+    for (uint64_t v = 0; v < M; v++) {
+        size_t a = poff[v], tab = pre.find('\t', a);
+        auto ins = ids.emplace(pre.substr(a, tab - a), (uint32_t)ids.size());
+        id[v] = ins.first->second;
+    }
+    int r = ensure(c, c->ld_cid, 4 * (M + 1));
+    if (r) return r;
+    c->ld_cid_host.swap(id);
+    HIPCHK(c, hipMemcpyAsync(c->ld_cid.p, c->ld_cid_host.data(), 4 * M, hipMemcpyHostToDevice, c->stream));
+    c->ld_chrom_ids = true;
+    return VCFXG_OK;
+}
+
+int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t window, double threshold, int max_dist,
+                          uint64_t *n_pairs, uint64_t *text_bytes) {
+    if (!c) return VCFXG_E_ARG;
+    const uint64_t M = c->ld_m;
+    if (j1 > M) j1 = M;
+    if (j0 >= j1 || M < 2) {
+        c->text_bytes = 0;
+        if (n_pairs) *n_pairs = 0;
+        if (text_bytes) *text_bytes = 0;
+        return VCFXG_OK;
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t BM = vcfxg::kLdBlock;
+    if (max_dist > 0) {
+        int r = ld_chrom_ids(c);
+        if (r) return r;
+    }
+    // block list: row blocks J covering [j0, j1), column blocks I from the window start to J
+    std::vector<uint32_t> blocks;
+    uint64_t nb = 1;
+    for (uint64_t J = j0 / BM; J * BM < j1; J++) {
+        uint64_t jr0 = J * BM;
+        uint64_t I0 = jr0 > window ? (jr0 - window) / BM : 0;
+        nb = std::max<uint64_t>(nb, J - I0 + 1);
+        for (uint64_t I = I0; I <= J; I++) {
+            blocks.push_back((uint32_t)I);
+            blocks.push_back((uint32_t)J);
+        }
+    }
+    const uint32_t nbl = (uint32_t)(blocks.size() / 2);
+    const uint64_t rows = j1 - j0;
+    int r = ensure(c, c->ld_blocks, 4 * blocks.size() + 8);
+    if (!r) r = ensure(c, c->ld_cnt, 2 * rows * nb + 16);
+    if (!r) r = ensure(c, c->ld_off, 8 * (rows * nb + 1));
+    if (r) return r;
+    c->ld_blocks_host.swap(blocks);
+    HIPCHK(c, hipMemcpyAsync(c->ld_blocks.p, c->ld_blocks_host.data(), 4 * c->ld_blocks_host.size(),
+                             hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->ld_cnt.p, 0, 2 * rows * nb + 16, c->stream));
+    vcfxg::LdWindowArgs a{M, c->ld_kpad, c->ld_ns, window, threshold, max_dist, j0, j1, nb};
+    const uint32_t *cid = max_dist > 0 ? P<uint32_t>(c->ld_cid) : nullptr;
+    prof_begin(c, "ld_count");
+    HIPCHK(c, vcfxg::launch_ld_block(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a,
+                                     P<uint32_t>(c->ld_blocks), nbl, P<uint16_t>(c->ld_cnt), nullptr, nullptr,
+                                     c->stream));
+    prof_end(c, "ld_count");
+    hipcub::TransformInputIterator<uint64_t, U16ToU64, const uint16_t *> cin(P<uint16_t>(c->ld_cnt), U16ToU64());
+    const size_t ncnt = rows * nb + 1;  // +1: the zeroed pad entry gives the total
+    size_t tmp = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cin, P<uint64_t>(c->ld_off), (int)ncnt, c->stream));
+    r = ensure(c, c->scan_tmp, tmp);
+    if (r) return r;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, cin, P<uint64_t>(c->ld_off), (int)ncnt, c->stream));
+    static thread_local uint64_t tot;
+    HIPCHK(c, hipMemcpyAsync(&tot, P<uint64_t>(c->ld_off) + rows * nb, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t np = tot;
+    r = ensure(c, c->ld_pairs, sizeof(vcfxg::LdPair) * (np + 1));
+    if (!r) r = ensure(c, c->rowlen, 8 * (np + 1));
+    if (!r) r = ensure(c, c->rowoff, 8 * (np + 1));
+    if (r) return r;
+    prof_begin(c, "ld_emit");
+    HIPCHK(c, vcfxg::launch_ld_block(2, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a,
+                                     P<uint32_t>(c->ld_blocks), nbl, P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off),
+                                     P<vcfxg::LdPair>(c->ld_pairs), c->stream));
+    prof_end(c, "ld_emit");
+    HIPCHK(c, vcfxg::launch_ld_pairtext(0, P<vcfxg::LdPair>(c->ld_pairs), np, P<uint64_t>(c->ld_poff), nullptr,
+                                        P<uint64_t>(c->rowlen), nullptr, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->rowlen) + np, 0, 8, c->stream));
+    r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)np + 1);
+    if (r) return r;
+    static thread_local uint64_t tb;
+    HIPCHK(c, hipMemcpyAsync(&tb, P<uint64_t>(c->rowoff) + np, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    r = ensure(c, c->text, tb + 16);
+    if (r) return r;
+    prof_begin(c, "ld_text");
+    HIPCHK(c, vcfxg::launch_ld_pairtext(1, P<vcfxg::LdPair>(c->ld_pairs), np, P<uint64_t>(c->ld_poff),
+                                        P<char>(c->ld_prefix), P<uint64_t>(c->rowoff), P<char>(c->text), c->stream));
+    prof_end(c, "ld_text");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    c->text_bytes = tb;
+    if (n_pairs) *n_pairs = np;
+    if (text_bytes) *text_bytes = tb;
+    return VCFXG_OK;
+}
+
+int vcfxg_ld_prefixes(vcfxg_ctx *c, char *text, size_t cap, uint64_t *offsets) {
+    if (!c) return VCFXG_E_ARG;
+    if (cap < c->ld_prefix_bytes) return VCFXG_E_CAP;
+    if (c->ld_prefix_bytes && text)
+        HIPCHK(c, hipMemcpyAsync(text, c->ld_prefix.p, c->ld_prefix_bytes, hipMemcpyDeviceToHost, c->stream));
+    if (offsets)
+        HIPCHK(c, hipMemcpyAsync(offsets, c->ld_poff.p, 8 * (c->ld_m + 1), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VCFXG_OK;
+}
+
+int vcfxg_ld_matrix(vcfxg_ctx *c, int gate, int printf4, uint64_t *cell_bytes) {
+    if (!c) return VCFXG_E_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t M = c->ld_m, BM = vcfxg::kLdBlock;
+    std::vector<uint32_t> blocks;
+    for (uint64_t J = 0; J * BM < M; J++)
+        for (uint64_t I = 0; I <= J; I++) {
+            blocks.push_back((uint32_t)I);
+            blocks.push_back((uint32_t)J);
+        }
+    const uint64_t cells = 7ull * M * M;
+    int r = ensure(c, c->ld_blocks, 4 * blocks.size() + 8);
+    if (!r) r = ensure(c, c->text, cells + 16);
+    if (r) return r;
+    c->ld_blocks_host.swap(blocks);
+    HIPCHK(c, hipMemcpyAsync(c->ld_blocks.p, c->ld_blocks_host.data(), 4 * c->ld_blocks_host.size(),
+                             hipMemcpyHostToDevice, c->stream));
+    prof_begin(c, "ld_matrix");
+    HIPCHK(c, vcfxg::launch_ld_matrix(P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), M, c->ld_kpad, c->ld_ns, gate,
+                                      printf4, P<uint32_t>(c->ld_blocks), (uint32_t)(c->ld_blocks_host.size() / 2),
+                                      P<char>(c->text), c->stream));
+    prof_end(c, "ld_matrix");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    c->text_bytes = cells;
+    if (cell_bytes) *cell_bytes = cells;
+    return VCFXG_OK;
+}
+
+int vcfxg_selftest_mfma_i8(vcfxg_ctx *c, int *mismatches) {
+    if (!c || !mismatches) return VCFXG_E_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<int8_t> A(32 * 32), B(32 * 32);
+    for (int i = 0; i < 32 * 32; i++) {
+        A[i] = (int8_t)((i * 7 + 3) % 5 - 2);
+        B[i] = (int8_t)((i * 11 + 1) % 7 - 3);
+    }
+    int r = ensure(c, c->scan_tmp, 8192);
+    if (r) return r;
+    char *d = P<char>(c->scan_tmp);
+    HIPCHK(c, hipMemcpyAsync(d, A.data(), 1024, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d + 1024, B.data(), 1024, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, vcfxg::launch_mfma_i8_selftest((int8_t *)d, (int8_t *)(d + 1024), (int *)(d + 2048), c->stream));
+    std::vector<int> C(32 * 32);
+    HIPCHK(c, hipMemcpyAsync(C.data(), d + 2048, 4096, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int bad = 0;
+    for (int i = 0; i < 32; i++)
+        for (int j = 0; j < 32; j++) {
+            int s = 0;
+            for (int k = 0; k < 32; k++) s += A[i * 32 + k] * B[j * 32 + k];
+            bad += s != C[i * 32 + j];
+        }
+    *mismatches = bad;
     return VCFXG_OK;
 }
 

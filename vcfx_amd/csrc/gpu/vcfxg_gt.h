@@ -19,17 +19,19 @@ struct DwordView {
     uint32_t f;    // (d ^ exp) & 0x00FF00FF: allele digit values in 16-bit fields
     uint32_t dig;  // bit 8 / bit 24 set where the allele is a digit
     bool real;     // false: padding outside [S, E) (neutral ". ." bytes)
+    int64_t p;     // offset of the sample's first byte
 };
 
 template <class Op>
-__device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_t &err, Op &op, bool real) {
+__device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_t &err, Op &op, bool real,
+                                           int64_t p) {
     uint32_t e = d ^ exp_xor;
     err |= e & 0xFF00FF00u;
     uint32_t f = e & 0x00FF00FFu;
     uint32_t notdig = (f + 0x00F600F6u) & 0x01000100u;  // field >= 10
     uint32_t notdot = ((f ^ 0x001E001Eu) + 0x00FF00FFu) & 0x01000100u;
     err |= notdig & notdot;
-    DwordView v{d, f, notdig ^ 0x01000100u, real};
+    DwordView v{d, f, notdig ^ 0x01000100u, real, p};
     op.dword(v);
 }
 
@@ -82,7 +84,7 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op, real[i]);
+                for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op, real[i], blk + s + 4 * i);
             }
         }
         if (op.done()) break;  // wave-uniform early exit (e.g. a match was found)

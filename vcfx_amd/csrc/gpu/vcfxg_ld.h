@@ -1,0 +1,68 @@
+// vcfxg_ld.h -- device layouts and launchers of the LD kernels (vcfxg_ld.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vcfxg {
+
+struct LdParseArgs {
+    int ns;            // numSamples from the #CHROM line (tabs - 8 when >= 9 tabs)
+    int kpad;          // row stride of the genotype matrix (ns rounded up to 64)
+    int has_region;
+    int rstart, rend;
+    int64_t rlen;
+    const char *rchrom;  // device copy of the region chromosome
+    int stoi_mode;       // stdin matrix mode: std::stoi POS, parseGenotype on the whole field
+};
+
+struct LdLine {  // per indexed line
+    uint32_t valid;
+    int pos;
+    uint32_t cnt, sx, sx2;  // valid samples, sum x, sum x^2
+    uint32_t chrom_len, id_len;
+    uint64_t chrom, id;     // byte offsets in the input
+};
+
+struct LdVar {  // per variant (compact order)
+    int pos;
+    int cnt, sx, sx2;
+    double varx;            // own variance (computeStats) for computeRsqFast's gate
+    int complete;           // no missing genotype among the ns samples
+    uint32_t chrom_len, id_len;
+    uint64_t chrom, id, line;
+};
+
+struct LdPair {
+    uint32_t i, j;          // variant indices, i < j
+    double r2;
+};
+
+struct LdWindowArgs {
+    uint64_t m;             // variants
+    int kpad, ns;
+    uint64_t window;        // pairs (i, j) with j - window <= i < j
+    double threshold;
+    int max_dist;           // > 0: same-chrom pairs farther apart are skipped (mmap streaming)
+    uint64_t j_lo, j_hi;    // rows of this chunk
+    uint64_t nb;            // column blocks per row in the count table
+};
+
+hipError_t launch_ld_parse(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                           uint64_t n_lines_host, const LdParseArgs &a, int8_t *G, LdLine *lines, hipStream_t s);
+hipError_t launch_ld_compact(const LdLine *lines, const uint64_t *vidx, const uint64_t *n_lines_dev,
+                             uint64_t n_lines_host, int kpad, int ns, const int8_t *G, int8_t *Gc, LdVar *vars,
+                             hipStream_t s);
+hipError_t launch_ld_block(int pass, const int8_t *Gc, const LdVar *vars, const uint32_t *chrom_id,
+                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
+                           const uint64_t *off, LdPair *pairs, hipStream_t s);
+hipError_t launch_ld_prefix(int which, const LdVar *vars, uint64_t m, const char *buf, int id_dot_to_pos,
+                            uint64_t *len_or_off, char *out, hipStream_t s);
+hipError_t launch_ld_pairtext(int which, const LdPair *pairs, uint64_t np, const uint64_t *poff, const char *prefix,
+                              uint64_t *len_or_off, char *out, hipStream_t s);
+hipError_t launch_ld_matrix(const int8_t *Gc, const LdVar *vars, uint64_t m, int kpad, int ns, int gate, int printf4,
+                            const uint32_t *blocks, uint32_t nblocks, char *cells, hipStream_t s);
+hipError_t launch_mfma_i8_selftest(const int8_t *A, const int8_t *B, int *C, hipStream_t s);
+
+constexpr int kLdBlock = 64;
+
+}  // namespace vcfxg

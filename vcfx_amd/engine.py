@@ -49,6 +49,12 @@ SIGNATURES = {
     "vcfxg_genotype_query": (_I, [_VP, _P, _S, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_record_filter": (_I, [_VP, _VP, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_variant_count": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
+    "vcfxg_ld_prefixes": (_I, [_VP, _VP, _S, _VP]),
+    "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
+    "vcfxg_ld_stream_chunk": (_I, [_VP, _U64, _U64, _U64, ctypes.c_double, _I, ctypes.POINTER(_U64),
+                                   ctypes.POINTER(_U64)]),
+    "vcfxg_selftest_mfma_i8": (_I, [_VP, ctypes.POINTER(_I)]),
     "vcfxg_filter_query": (_I, [_VP, _VP, _I, _I, _P, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_fetch_text": (_I, [_VP, _VP, _S]),
     "vcfxg_fetch_lines": (_I, [_VP, _U64, _U64, _VP, _VP, _VP]),
@@ -172,6 +178,25 @@ class Engine:
         self._chk(self.L.vcfxg_filter_query(self.h, ctypes.cast(arr, ctypes.c_void_p), len(crits), int(and_logic), q,
                                             len(q), int(strict), ctypes.byref(s)), "filter_query")
         return s
+
+    def ld_prepare(self, n_samples, id_dot_to_pos=True, region=None):
+        n = ctypes.c_uint64()
+        rc, rs, re_ = (region[0].encode(), region[1], region[2]) if region else (b"", 0, 0)
+        self._chk(self.L.vcfxg_ld_prepare(self.h, n_samples, int(id_dot_to_pos), rc, len(rc), int(bool(region)), rs,
+                                          re_, 0, ctypes.byref(n)), "ld_prepare")
+        return n.value
+
+    def ld_stream_chunk(self, j0, j1, window, threshold, max_dist=0):
+        npairs = ctypes.c_uint64()
+        tb = ctypes.c_uint64()
+        self._chk(self.L.vcfxg_ld_stream_chunk(self.h, j0, j1, window, threshold, max_dist, ctypes.byref(npairs),
+                                               ctypes.byref(tb)), "ld_stream_chunk")
+        return npairs.value, tb.value
+
+    def selftest_mfma_i8(self):
+        m = ctypes.c_int()
+        self._chk(self.L.vcfxg_selftest_mfma_i8(self.h, ctypes.byref(m)), "selftest")
+        return m.value
 
     def text(self, nbytes):
         b = ctypes.create_string_buffer(max(1, nbytes))
