@@ -16,7 +16,7 @@ step() {  # step NAME SECONDS CMD...
 ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-    step pytest_gpu 900 python -m pytest tests -m gpu -x -q; rc=$?; ok_or_testfail $rc || exit $rc
+    step pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=10; rc=$?; ok_or_testfail $rc || exit $rc
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     step bench 600 python bench.py || exit $?

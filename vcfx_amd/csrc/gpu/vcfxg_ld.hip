@@ -304,7 +304,7 @@ __device__ __forceinline__ double rsq_epilogue(const LdVar &vi, const LdVar &vj,
 }
 
 // byte transforms of a 16-byte code vector (-1 = 0xFF missing): x' (missing -> 0), v, x'^2
-__device__ __forceinline__ uint32_t xprime(uint32_t c) { return c & ~((c & 0x80808080u) >> 7) * 0xFFu; }
+__device__ __forceinline__ uint32_t xprime(uint32_t c) { return c & ~(((c & 0x80808080u) >> 7) * 0xFFu); }
 __device__ __forceinline__ uint32_t vmask(uint32_t c) { return (~c & 0x80808080u) >> 7; }
 __device__ __forceinline__ uint32_t xsq(uint32_t xp) { return xp + (xp & 0x02020202u); }
 
@@ -316,7 +316,7 @@ struct TileSums {
 };
 
 __device__ __forceinline__ void tile_sums(const int8_t *__restrict__ Gc, const LdVar *__restrict__ vars, int64_t M,
-                                          int kpad, int64_t i0, int64_t j0, TileSums &T) {
+                                          int kpad, int ns, int64_t i0, int64_t j0, TileSums &T) {
     const int l = lane(), r = l & 31, h = l >> 5;
     // operand rows (clamped; out-of-range rows are masked in the epilogue)
     const int64_t ia = i0 + r < M ? i0 + r : M - 1, ja = j0 + r < M ? j0 + r : M - 1;
@@ -356,6 +356,8 @@ __device__ __forceinline__ void tile_sums(const int8_t *__restrict__ Gc, const L
             vx2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(avm, bx2, vx2, 0, 0, 0);
         }
     }
+    // complete rows hold -1 in the padding bytes [ns, kpad): (-1)(-1) per byte in X.X^T
+    if (comp) xx -= (kpad - ns);
     T.comp = comp;
     T.xx = xx;
     T.xv = xv;
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(256) void k_ld_block(const int8_t *__restrict__ Gc,
     const int l = lane(), r = l & 31, h = l >> 5;
     const int64_t M = (int64_t)a.m;
     TileSums T;
-    tile_sums(Gc, vars, M, a.kpad, i0, j0, T);
+    tile_sums(Gc, vars, M, a.kpad, a.ns, i0, j0, T);
     const bool comp = T.comp;
     const v16i &xx = T.xx, &xv = T.xv, &vx = T.vx, &vv = T.vv, &x2v = T.x2v, &vx2 = T.vx2;
     // epilogue: lane holds column j = j0 + r, rows i = i0 + (k&3) + 8*(k>>2) + 4*h
@@ -489,7 +491,7 @@ __global__ __launch_bounds__(256) void k_ld_matrix(const int8_t *__restrict__ Gc
     const int l = lane(), r = l & 31, h = l >> 5;
     const int64_t M = (int64_t)m;
     TileSums T;
-    tile_sums(Gc, vars, M, kpad, i0, j0, T);
+    tile_sums(Gc, vars, M, kpad, ns, i0, j0, T);
     const int64_t j = j0 + r;
     if (j >= M) return;
     const LdVar vj = vars[j];
