@@ -1,14 +1,25 @@
 #!/usr/bin/env python3
-"""bench.py -- VCFX_allele_freq_calc hot path on MI355X (BASELINE.json configs[1]; N>1 =
-configs[3], record-sharded, weak scaling).
+"""bench.py -- the VCFX per-record hot path on MI355X.
 
-A step = one pass of the hot path over one batch of synthetic input that is already
-resident in HBM: record index (K1) + per-record allele counts (K2) + device-formatted
-output rows (K5).  Each rank processes its own 427,409-record x 2,504-sample shard
-(≈4.3 GB, chr21-like layout; seed = 20251226 + rank).  value = records processed by all
-ranks / max-over-ranks wall time of the timed steps.
+Workloads (BASELINE.json configs; the default is the headline one):
+  af        configs[1] / configs[3]: VCFX_allele_freq_calc -i on a device-resident
+            427,409-record x 2,504-sample chr21-like shard per GPU.  A step = record index
+            (line_count + line_emit) + per-record allele counts (af_records) + device
+            formatted output rows (af_rows + af_format); for N > 1 ranks also all-reduce the
+            step's global counts (records, rows, alt/total alleles) over RCCL.
+  pipeline  configs[2]: VCFX_record_filter --filter "QUAL>=30;FILTER==PASS" |
+            VCFX_genotype_query --genotype-query "0|1" fused on the device (index + one
+            filter_query pass), same shard.
+  ld        configs[4]: VCFX_ld_calculator streaming, 100,000-variant window over a
+            100,000-variant x 2,504-sample shard (haplotype-block LD structure) with -t 0.8:
+            parse + int8-MFMA pair sums (count pass and emit pass) + pair text.
 
-Prints ONE JSON line on rank 0 (see the contract in the task / DESIGN.md §Measurement).
+value = units processed by all ranks / max-over-ranks wall time of the K timed steps
+(inputs already resident in HBM).  One process per GPU (torchrun), record-sharded with
+seed = base + rank: weak scaling.  Rank 0 prints ONE JSON line (contract: DESIGN.md
+§Measurement) carrying `roofline` for the dominant kernel (HIP-event timing on the engine's
+own stream, algorithmic bytes or ops per launch) and `cpu_baseline` (the oracle/ C
+restatement on a bounded sample, 1 core).
 """
 import argparse
 import json
@@ -21,7 +32,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "variant-records/sec (and GB/s vs HBM roofline), 427K var × 2504 samp"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+I8_PEAK_TOPS = 5000.0   # MI355X_MICROARCH.md: I8 MFMA = 2x the BF16 rate per clock, BF16 ~2.5 PF dense
+PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
 def parse():
@@ -29,33 +42,81 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--records", type=int, default=427409)
+    ap.add_argument("--workload", choices=("af", "pipeline", "ld"), default="af")
+    ap.add_argument("--records", type=int, default=None, help="records per GPU (default per workload)")
     ap.add_argument("--samples", type=int, default=2504)
+    ap.add_argument("--window", type=int, default=100000, help="ld: window in variants")
+    ap.add_argument("--threshold", type=float, default=0.8, help="ld: r^2 threshold")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.records is None:
+        a.records = 100000 if a.workload == "ld" else 427409
+    if a.workload == "ld" and a.steps == 20:
+        a.steps = 3
+    return a
 
 
-def cpu_baseline(arr, offs, n_records, budget_s):
-    """The C restatement oracle (oracle/, kind "port"), 1 thread, file (mmap) path of
-    VCFX_allele_freq_calc over a bounded prefix sample of this rank's synthetic input."""
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC pass (profiles/pmc_traffic.json,
+    written by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs,
+    FETCH_SIZE doubled per the gfx950 correction), or None."""
+    try:
+        with open(PMC_FILE) as f:
+            d = json.load(f)
+        return d[workload][kernel]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def _timed_oracle(argvs, budget_s):
+    """Run a chain of oracle tool invocations (stdout of one = stdin of the next) repeatedly."""
     from tests._golden import Oracle
-    sample_records = min(n_records, 20000)
-    sample = arr[:int(offs[sample_records])].tobytes()  # header + first sample_records records
     o = Oracle()
-    with tempfile.NamedTemporaryFile(suffix=".vcf", dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as f:
+    reps, t_total = 0, 0.0
+    while t_total < budget_s or reps == 0:
+        t0 = time.perf_counter()
+        data = b""
+        for argv in argvs:
+            out, err, rc = o.run(argv, data)
+            assert rc == 0, (argv, err[:200])
+            data = out
+        t_total += time.perf_counter() - t0
+        reps += 1
+    return reps, t_total
+
+
+def cpu_baseline(workload, arr, offs, a):
+    """The C restatement oracle (oracle/, kind "port"), 1 thread, over a bounded prefix sample
+    of this rank's synthetic input (the same byte layout as the GPU workload)."""
+    if workload == "ld":
+        nvar = min(a.records, 1500)
+    else:
+        nvar = min(a.records, 20000)
+    sample = arr[:int(offs[nvar])].tobytes()  # header + first nvar records
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    with tempfile.NamedTemporaryFile(suffix=".vcf", dir=shm) as f:
         f.write(sample)
         f.flush()
-        reps, t_total = 0, 0.0
-        while t_total < budget_s or reps == 0:
-            t0 = time.perf_counter()
-            out, err, rc = o.run(["VCFX_allele_freq_calc", "-q", "-i", f.name])
-            t_total += time.perf_counter() - t0
-            reps += 1
-            assert rc == 0
-    return {"value": sample_records * reps / t_total, "unit": "records/s", "cores": 1, "kind": "port",
-            "sample": "first %d records (%.1f MB) of the rank-0 shard, VCFX_allele_freq_calc -q -i (file path), "
-                      "%d reps, %.1f s" % (sample_records, len(sample) / 1e6, reps, t_total)}
+        if workload == "af":
+            argvs = [["VCFX_allele_freq_calc", "-q", "-i", f.name]]
+            desc = "VCFX_allele_freq_calc -q -i (file path)"
+        elif workload == "pipeline":
+            argvs = [["VCFX_record_filter", "--filter", "QUAL>=30;FILTER==PASS", "-i", f.name],
+                     ["VCFX_genotype_query", "--genotype-query", "0|1"]]
+            desc = "VCFX_record_filter -i | VCFX_genotype_query (stdin)"
+        else:
+            argvs = [["VCFX_ld_calculator", "-q", "-w", str(nvar), "-t", str(a.threshold), "-i", f.name]]
+            desc = "VCFX_ld_calculator -w %d -t %g -i (file path)" % (nvar, a.threshold)
+        reps, t = _timed_oracle(argvs, a.cpu_seconds)
+    if workload == "ld":
+        units = nvar * (nvar - 1) // 2
+        return {"value": units * reps / t, "unit": "r2-pairs/s", "cores": 1, "kind": "port",
+                "sample": "first %d variants (%.1f MB) of the rank-0 shard, all %d window pairs, %s, %d reps, "
+                          "%.1f s" % (nvar, len(sample) / 1e6, units, desc, reps, t)}
+    return {"value": nvar * reps / t, "unit": "records/s", "cores": 1, "kind": "port",
+            "sample": "first %d records (%.1f MB) of the rank-0 shard, %s, %d reps, %.1f s"
+                      % (nvar, len(sample) / 1e6, desc, reps, t)}
 
 
 def main():
@@ -63,33 +124,71 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
+    dist = torch = None
     if world > 1:
+        # torch first: its HIP runtime (same soname) then serves libvcfx_gpu.so too
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from vcfx_amd import engine, synth
 
-    arr, offs = synth.generate_array(a.records, a.samples, seed=20251226 + rank, rec_offsets=True)
-    head = arr[:1 << 20].tobytes()
-    ds = engine.data_start_of(head)
+    ld = a.workload == "ld"
+    arr, offs = synth.generate_array(a.records, a.samples, seed=20251226 + rank, hap_blocks=1 if ld else 0,
+                                     rec_offsets=True)
+    ds = engine.data_start_of(arr[:1 << 20].tobytes(), strip_cr=not ld)
     eng = engine.Engine(local)
     eng.load(arr)
     region_bytes = arr.size - ds
 
-    def step():
-        eng.index(ds)
-        return eng.allele_freq(engine.MODE_FILE)
+    red = None
+    if dist is not None:
+        red = torch.zeros(4, dtype=torch.int64, device="cuda")
+
+    def allreduce_counts(vals):
+        # global allele-count reduction over RCCL (configs[3]); per-rank outputs stay local
+        red.copy_(torch.tensor(vals, dtype=torch.int64))
+        dist.all_reduce(red)
+        return red
+
+    if a.workload == "af":
+        def step():
+            eng.index(ds)
+            s = eng.allele_freq(engine.MODE_FILE)
+            if red is not None:
+                allreduce_counts([s.n_lines, s.rows, s.data_lines, s.text_bytes])
+            return s
+        kern_names = ("line_count", "line_emit", "af_records", "af_rows", "af_format")
+    elif a.workload == "pipeline":
+        crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
+
+        def step():
+            eng.index(ds)
+            s = eng.filter_query(crits, "0|1", and_logic=True, strict=False)
+            if red is not None:
+                allreduce_counts([s.n_lines, s.rows, s.data_lines, s.warn_lines])
+            return s
+        kern_names = ("line_count", "line_emit", "rf_records", "gq_records")
+    else:
+        W = a.window
+
+        def step():
+            eng.index(ds)
+            m = eng.ld_prepare(a.samples)
+            np_, tb = eng.ld_stream_chunk(0, m, W, a.threshold)
+            if red is not None:
+                allreduce_counts([m, np_, tb, 0])
+            return m, np_, tb
+        kern_names = ("line_count", "line_emit", "ld_parse", "ld_compact", "ld_count", "ld_emit", "ld_text")
 
     s = None
     for _ in range(a.warmup):
         s = step()
-    assert s is None or s.rows == a.records, "unexpected row count %s" % (s and s.rows)
 
     def barrier():
         if dist is not None:
             dist.barrier()
+            torch.cuda.synchronize()
 
     eng.set_profiling(True)
     eng.reset_kernel_stats()
@@ -100,37 +199,71 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     eng.set_profiling(False)
-    assert s.rows == a.records and s.general_records == 0
 
     kernels = {}
-    for k in ("line_count", "line_emit", "af_records", "af_rows", "af_format"):
+    for k in kern_names:
         tot, n = eng.kernel_stats(k)
         if n:
             kernels[k] = tot / n
     if dist is not None:
-        import torch
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    records_total = a.records * world
-    value = records_total * a.steps / dt
+
+    if ld:
+        m, np_, tb = s
+        assert m == a.records, (m, a.records)
+        W = min(a.window, m)
+        pairs = (m * (m - 1) // 2) if W >= m - 1 else (W * (W - 1) // 2 + (m - W) * W)
+        units_total = pairs * world
+        unit, metric = "r2-pairs/s", "r2-pairs/sec (and int8 MFMA TOP/s vs peak), %dK var window x %d samp" % (
+            a.records // 1000, a.samples)
+    else:
+        assert s.rows > 0 and s.n_lines == a.records, (s.rows, s.n_lines)
+        if a.workload == "af":
+            assert s.rows == a.records and s.general_records == 0
+        units_total = a.records * world
+        unit, metric = "records/s", METRIC
+    value = units_total * a.steps / dt
 
     if rank == 0:
-        # dominant kernel + its algorithmic bytes per launch
-        L = s.n_lines
-        algo = {
-            "af_records": region_bytes + L * (8 + 13),   # record bytes + line_end read + per-line results
-            "line_count": region_bytes,
-            "line_emit": region_bytes + 8 * L,
-            "af_format": s.text_bytes + L * (8 + 8 + 13) + s.rows * 40,
-            "af_rows": L * (5 + 8 + 8 + 8),
-        }
-        dom = max(kernels, key=kernels.get)
-        ach = algo[dom] / (kernels[dom] * 1e-3) / 1e9
+        L = a.records
+        if ld:
+            # int8 MFMA: X.X^T over the window pairs (complete genotypes): 2 ops per sample per pair
+            algo = {"ld_count": 2.0 * a.samples * pairs, "ld_emit": 2.0 * a.samples * pairs}
+            dom = "ld_count"
+            ach = algo[dom] / (kernels[dom] * 1e-3) / 1e12
+            roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": I8_PEAK_TOPS, "unit": "TOP/s",
+                    "frac": ach / I8_PEAK_TOPS, "traffic": pmc_traffic("ld", dom),
+                    "algorithmic_ops_per_launch": algo[dom], "avg_launch_ms": kernels[dom]}
+        else:
+            tb = s.text_bytes
+            algo = {   # algorithmic bytes per launch
+                "line_count": region_bytes,
+                "line_emit": region_bytes + 8 * L,
+                "af_records": region_bytes + L * (8 + 13),      # record bytes + line_end + per-line results
+                "af_format": tb + L * (8 + 8 + 13) + s.rows * 40,
+                "af_rows": L * (5 + 8 + 8 + 8),
+                "rf_records": region_bytes + L * (8 + 1),
+                "gq_records": region_bytes + L * (8 + 2),
+            }
+            dom = max((k for k in kernels if k in algo), key=kernels.get)
+            ach = algo[dom] / (kernels[dom] * 1e-3) / 1e9
+            roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(a.workload, dom),
+                    "algorithmic_bytes_per_launch": int(algo[dom]), "avg_launch_ms": kernels[dom]}
+        workload = {
+            "af": "VCFX_allele_freq_calc -i (file path) on a device-resident %d x %d VCF shard per GPU: index + "
+                  "allele counts + formatted rows" % (a.records, a.samples),
+            "pipeline": "VCFX_record_filter --filter 'QUAL>=30;FILTER==PASS' | VCFX_genotype_query "
+                        "--genotype-query '0|1' fused, device-resident %d x %d shard per GPU" % (a.records, a.samples),
+            "ld": "VCFX_ld_calculator -w %d -t %g streaming on a device-resident %d x %d shard per GPU: parse + "
+                  "int8-MFMA pair sums (count + emit) + pair text" % (a.window, a.threshold, a.records, a.samples),
+        }[a.workload]
         out = {
-            "metric": METRIC,
+            "metric": metric,
             "value": value,
-            "unit": "records/s",
+            "unit": unit,
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
@@ -138,21 +271,22 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic: vcfx_synth seed 20251226+rank, chr21-like layout (FORMAT=GT, phased a|b, INFO=.)",
-            "config": {"workload": "VCFX_allele_freq_calc -i (file path) on a device-resident %d x %d VCF shard "
-                                   "per GPU: index + allele counts + formatted rows" % (a.records, a.samples),
-                       "records_per_gpu": a.records, "samples": a.samples, "bytes_per_gpu": int(arr.size),
-                       "parallelism": "record-sharded x%d (no data-path collective)" % world},
-            "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": ach / HBM_PEAK_GBS, "traffic": None,
-                         "algorithmic_bytes_per_launch": int(algo[dom]),
-                         "avg_launch_ms": kernels[dom]},
+            "dtype": "i8" if ld else "u8",
+            "data": "synthetic: vcfx_synth seed 20251226+rank, chr21-like layout (FORMAT=GT, phased a|b, INFO=.)"
+                    + (", founder-haplotype blocks" if ld else ""),
+            "config": {"workload": workload, "records_per_gpu": a.records, "samples": a.samples,
+                       "bytes_per_gpu": int(arr.size),
+                       "parallelism": "record-sharded x%d%s" % (world, ", RCCL all-reduce of global counts"
+                                                                if world > 1 else "")},
+            "roofline": roof,
             "kernels_ms": kernels,
             "pipeline_input_gbps": region_bytes * world * a.steps / dt / 1e9,
         }
+        if ld:
+            out["pairs_per_gpu"] = pairs
+            out["pairs_emitted"] = np_
         if not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(arr, offs, a.records, a.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(a.workload, arr, offs, a)
         print(json.dumps(out), flush=True)
     eng.close()
     if dist is not None:

@@ -1,6 +1,7 @@
 #!/bin/bash
-# One gpurun session: GPU tests, a bench run, and a rocprofv3 kernel-trace of the bench.
+# One gpurun session: GPU tests, bench runs, rocprofv3 kernel-trace summaries and PMC traffic passes.
 # Each GPU step has its own time limit; a fault/abort/timeout stops the script.
+#   bash gpu_job.sh [test|bench|prof|pmc|all] [workloads...]     (workloads: af pipeline ld)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -10,20 +11,37 @@ step() {  # step NAME SECONDS CMD...
     timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
     local rc=$?
     echo "=== $name rc=$rc"
-    tail -5 "gpurun_out/$name.log"
+    tail -3 "gpurun_out/$name.log" | cut -c1-400
     return $rc
 }
 ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 MODE=${1:-all}
+shift
+WLS=${*:-af pipeline ld}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
     step pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=10; rc=$?; ok_or_testfail $rc || exit $rc
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-    step bench 600 python bench.py || exit $?
-    cat gpurun_out/bench.log | tail -1 > gpurun_out/bench.json
+    for w in $WLS; do
+        step bench_$w 600 python bench.py --workload $w || exit $?
+        tail -1 gpurun_out/bench_$w.log > gpurun_out/bench_$w.json
+    done
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
-    step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-        python bench.py --steps 5 --warmup 1 --no-cpu-baseline || exit $?
+    for w in $WLS; do
+        step rocprof_$w 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$w -o run --output-format csv -- \
+            python bench.py --workload $w --steps 5 --warmup 1 --no-cpu-baseline || exit $?
+    done
+fi
+if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
+    for w in $WLS; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+            step pmc_${w}_$c 600 rocprofv3 --pmc $c -d gpurun_out/pmc_${w}_$c -o run --output-format csv -- \
+                python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline || exit $?
+        done
+        python tools/pmc_traffic.py $w $(find gpurun_out/pmc_${w}_FETCH_SIZE -name '*counter_collection.csv' | head -1) \
+            $(find gpurun_out/pmc_${w}_WRITE_SIZE -name '*counter_collection.csv' | head -1) gpurun_out/pmc_traffic.json \
+            > gpurun_out/pmc_$w.log 2>&1 || echo "pmc fold failed for $w"
+    done
 fi
 echo "=== done"

@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Fold rocprofv3 --pmc counter CSVs into profiles/pmc_traffic.json (HBM bytes per launch).
+
+usage: pmc_traffic.py WORKLOAD FETCH_CSV WRITE_CSV [OUT_JSON]
+
+FETCH_CSV / WRITE_CSV are the *_counter_collection.csv files of two SEPARATE runs
+(`rocprofv3 --pmc FETCH_SIZE ...` and `rocprofv3 --pmc WRITE_SIZE ...`; the two counters do
+not fit one pass on gfx950).  FETCH_SIZE / WRITE_SIZE are reported in KB (x1024 bytes);
+per MI355X_MICROARCH.md §HBM, FETCH_SIZE reports half of the bytes of a wide coalesced
+streaming read on gfx950, so it is doubled here.  Per kernel: mean over its dispatches.
+"""
+import csv
+import json
+import os
+import re
+import sys
+
+# engine profiling names (vcfxg_kernel_stats) -> device kernel symbol
+KERNELS = {
+    "line_count": r"vcfxg::k_nl_count\(",
+    "line_emit": r"vcfxg::k_nl_emit\(",
+    "af_records": r"vcfxg::k_af_records\(",
+    "af_format": r"vcfxg::k_af_format\(",
+    "rf_records": r"vcfxg::k_rf_records\(",
+    "gq_records": r"vcfxg::k_gq_records\(",
+    "ld_parse": r"vcfxg::k_ld_parse\(",
+    "ld_count": r"vcfxg::k_ld_block<1>\(",
+    "ld_emit": r"vcfxg::k_ld_block<2>\(",
+    "ld_matrix": r"vcfxg::k_ld_matrix\(",
+}
+
+
+def per_kernel(path, counter):
+    acc = {}
+    with open(path, newline="") as f:
+        for row in csv.DictReader(f):
+            if row.get("Counter_Name") != counter:
+                continue
+            name = row["Kernel_Name"]
+            for k, pat in KERNELS.items():
+                if re.search(pat, name):
+                    acc.setdefault(k, []).append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    workload, fcsv, wcsv = sys.argv[1:4]
+    out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+    fetch = per_kernel(fcsv, "FETCH_SIZE")
+    write = per_kernel(wcsv, "WRITE_SIZE")
+    try:
+        with open(out) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        d = {}
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        fb = fetch.get(k, 0.0) * 1024 * 2   # KB -> bytes, gfx950 streaming-read correction (x2)
+        wb = write.get(k, 0.0) * 1024
+        res[k] = {"fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb,
+                  "fetch_size_kb_raw": fetch.get(k), "write_size_kb_raw": write.get(k)}
+    d[workload] = res
+    d["_note"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; FETCH_SIZE doubled "
+                  "(gfx950 wide streaming reads, MI355X_MICROARCH.md HBM section); mean per dispatch")
+    with open(out, "w") as f:
+        json.dump(d, f, indent=1, sort_keys=True)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
