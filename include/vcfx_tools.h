@@ -1,0 +1,43 @@
+/*
+ * vcfx_tools.h -- in-process C entry points of the VCFX_<tool> drop-ins (libvcfx_tools.so).
+ *
+ * Each function runs one tool invocation exactly as the reference executable would with the
+ * same argv: argv[0] is the tool name, input comes from a file named in argv (the reference's
+ * mmap path) or from in_fd (its stdin path), output bytes go to out_fd, diagnostics to
+ * err_fd, and the return value is the process exit code.  The build's executables
+ * (build/src/VCFX_<t>/VCFX_<t>) are thin main()s over these; FFI callers (ctypes, cgo, JNI)
+ * bind them to run a tool without a process spawn while keeping one device context alive
+ * across calls.  They replace:
+ *   vcfx_tool_allele_freq_calc  main, VCFX_allele_freq_calc.cpp:590-646
+ *   vcfx_tool_record_filter     main/run, VCFX_record_filter.cpp:584-658, 819-827
+ *   vcfx_tool_genotype_query    main, VCFX_genotype_query.cpp:624-661
+ *   vcfx_tool_ld_calculator     run/main, VCFX_ld_calculator.cpp:1084-1225
+ *   vcfx_tool_variant_counter   run, VCFX_variant_counter.cpp:154-218
+ *   vcfx_tool_main              the `vcfx <tool> ...` dispatch (src/vcfx_wrapper/vcfx.cpp:177-187)
+ * Without a usable gfx950 device a tool that reaches the record loop writes
+ * "no usable MI355X" to err_fd and returns 1 (no CPU fallback).
+ */
+#ifndef VCFX_TOOLS_H
+#define VCFX_TOOLS_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_variant_counter(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+/* tool = "VCFX_<name>" (a leading path is ignored); -100 for an unknown tool */
+int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd);
+/* `VCFX_record_filter --filter F --logic L [-i input] | VCFX_genotype_query -g Q [--strict] [-q]`
+ * fused in one device pass (BASELINE config 3); input = NULL reads in_fd.  The return value is
+ * genotype_query's exit code; record_filter's stderr is written to err_fd first. */
+int vcfx_pipeline_filter_query(const char *filter, const char *logic, const char *input, const char *query, int strict,
+                               int gq_quiet, int in_fd, int out_fd, int err_fd);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -40,7 +40,11 @@ def test_open_without_gpu_fails_loudly():
 
 def test_tools_lib_exports():
     lib = ctypes.CDLL(TOOLS_LIB)
-    assert hasattr(lib, "vcfx_tool_main")
+    txt = open(os.path.join(os.path.dirname(BUILD), "include", "vcfx_tools.h")).read()
+    syms = sorted(set(re.findall(r"\b(vcfx_(?:tool|pipeline)_[a-z0-9_]+)\s*\(", txt)))
+    assert len(syms) == 7, syms
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
 
 
 @pytest.mark.parametrize("tool", ["VCFX_allele_freq_calc", "VCFX_genotype_query", "VCFX_record_filter", "VCFX_variant_counter", "VCFX_ld_calculator"])

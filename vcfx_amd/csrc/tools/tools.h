@@ -10,18 +10,7 @@
 
 #include "hostio.h"
 
-extern "C" {
-int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int out_fd, int err_fd);
-int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int out_fd, int err_fd);
-int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out_fd, int err_fd);
-int vcfx_tool_variant_counter(int argc, char **argv, int in_fd, int out_fd, int err_fd);
-int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out_fd, int err_fd);
-int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd);
-// fused `VCFX_record_filter --filter F --logic L [-i input] | VCFX_genotype_query -g Q
-// [--strict] [-q]` in one process (input = NULL: read in_fd)
-int vcfx_pipeline_filter_query(const char *filter, const char *logic, const char *input, const char *query, int strict,
-                               int gq_quiet, int in_fd, int out_fd, int err_fd);
-}
+#include "vcfx_tools.h"
 
 namespace vcfxh {
 
