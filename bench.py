@@ -11,7 +11,7 @@ Workloads (BASELINE.json configs; the default is the headline one):
             VCFX_genotype_query --genotype-query "0|1" fused on the device (index + one
             filter_query pass), same shard.
   ld        configs[4]: VCFX_ld_calculator streaming, 100,000-variant window over a
-            100,000-variant x 2,504-sample shard (haplotype-block LD structure) with -t 0.8:
+            100,000-variant x 2,504-sample shard (haplotype-block LD structure) with -t 0.5:
             parse + int8-MFMA pair sums (count pass and emit pass) + pair text.
 
 value = units processed by all ranks / max-over-ranks wall time of the K timed steps
@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--records", type=int, default=None, help="records per GPU (default per workload)")
     ap.add_argument("--samples", type=int, default=2504)
     ap.add_argument("--window", type=int, default=100000, help="ld: window in variants")
-    ap.add_argument("--threshold", type=float, default=0.8, help="ld: r^2 threshold")
+    ap.add_argument("--threshold", type=float, default=0.5, help="ld: r^2 threshold")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()

@@ -46,7 +46,8 @@ struct vcfxg_ctx {
     std::string query_host, crit_host, pool_host;  // host sources of in-flight async copies
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
-        ld_off, ld_pairs;
+        ld_off, ld_pairs, ld_fast, ld_gflag;
+    std::vector<uint8_t> ld_gflag_host;  // per 128-variant group: all complete
     uint64_t ld_m = 0, ld_prefix_bytes = 0;
     int ld_kpad = 64, ld_ns = 0;
     bool ld_chrom_ids = false;
@@ -177,7 +178,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag})
         if (b->p) (void)hipFree(b->p);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
@@ -601,14 +602,21 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
     const uint64_t M = L ? last[0] + lastline.valid : 0;
     r = ensure(c, c->ld_Gc, (size_t)(M + 1) * kpad + 64);
     if (!r) r = ensure(c, c->ld_vars, sizeof(vcfxg::LdVar) * (M + 1));
+    if (!r) r = ensure(c, c->ld_fast, sizeof(vcfxg::LdFast) * (M + 1));
+    if (!r) r = ensure(c, c->ld_gflag, M / vcfxg::kLdFastBlock + 2);
     if (!r) r = ensure(c, c->ld_plen, 8 * (M + 2));
     if (!r) r = ensure(c, c->ld_poff, 8 * (M + 2));
     if (r) return r;
     prof_begin(c, "ld_compact");
     HIPCHK(c, vcfxg::launch_ld_compact(P<vcfxg::LdLine>(c->ld_lines), P<uint64_t>(c->ld_vidx), P<uint64_t>(c->d_nlines),
                                        L, kpad, n_samples, P<int8_t>(c->ld_G), P<int8_t>(c->ld_Gc),
-                                       P<vcfxg::LdVar>(c->ld_vars), c->stream));
+                                       P<vcfxg::LdVar>(c->ld_vars), P<vcfxg::LdFast>(c->ld_fast), c->stream));
     prof_end(c, "ld_compact");
+    HIPCHK(c, vcfxg::launch_ld_groups(P<vcfxg::LdVar>(c->ld_vars), M, P<uint8_t>(c->ld_gflag), c->stream));
+    c->ld_gflag_host.assign(M / vcfxg::kLdFastBlock + 1, 0);
+    if (M)
+        HIPCHK(c, hipMemcpyAsync(c->ld_gflag_host.data(), c->ld_gflag.p, (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock,
+                                 hipMemcpyDeviceToHost, c->stream));
     // per-variant "chrom\tpos\tid" prefixes
     HIPCHK(c, vcfxg::launch_ld_prefix(0, P<vcfxg::LdVar>(c->ld_vars), M, P<char>(c->input), id_dot_to_pos,
                                       P<uint64_t>(c->ld_plen), nullptr, c->stream));
@@ -663,6 +671,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     if (!c) return VCFXG_E_ARG;
     const uint64_t M = c->ld_m;
     if (j1 > M) j1 = M;
+    if (window > M) window = M;  // a wider window holds the same pairs (and stays int64-safe)
     if (j0 >= j1 || M < 2) {
         c->text_bytes = 0;
         if (n_pairs) *n_pairs = 0;
@@ -675,19 +684,34 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
         int r = ld_chrom_ids(c);
         if (r) return r;
     }
-    // block list: row blocks J covering [j0, j1), column blocks I from the window start to J
+    // block lists.  Count-table columns are 64-blocks: row block J pairs with column blocks
+    // I0(J) = (J*64 - window)/64 .. J.  Pairs of 128-groups that are all complete go to the
+    // 128x128 X.X^T kernel (k_ld_fast); every other 64-block to the general kernel.
+    const uint64_t FB = vcfxg::kLdFastBlock;
+    auto ifirst = [&](uint64_t J) { const uint64_t jr0 = J * BM; return jr0 > window ? (jr0 - window) / BM : 0; };
+    const std::vector<uint8_t> &gf = c->ld_gflag_host;
+    auto gcomp = [&](uint64_t b64) { return gf[b64 / 2] != 0; };
     std::vector<uint32_t> blocks;
     uint64_t nb = 1;
-    for (uint64_t J = j0 / BM; J * BM < j1; J++) {
-        uint64_t jr0 = J * BM;
-        uint64_t I0 = jr0 > window ? (jr0 - window) / BM : 0;
-        nb = std::max<uint64_t>(nb, J - I0 + 1);
-        for (uint64_t I = I0; I <= J; I++) {
-            blocks.push_back((uint32_t)I);
-            blocks.push_back((uint32_t)J);
-        }
+    for (uint64_t J = j0 / FB; J * FB < j1; J++) {  // fast list first
+        if (!gf[J]) continue;
+        for (uint64_t I = ifirst(2 * J) / 2; I <= J; I++)
+            if (gf[I]) {
+                blocks.push_back((uint32_t)I);
+                blocks.push_back((uint32_t)J);
+            }
     }
-    const uint32_t nbl = (uint32_t)(blocks.size() / 2);
+    const uint32_t nfast = (uint32_t)(blocks.size() / 2);
+    for (uint64_t J = j0 / BM; J * BM < j1; J++) {
+        const uint64_t I0 = ifirst(J);
+        nb = std::max<uint64_t>(nb, J - I0 + 1);
+        for (uint64_t I = I0; I <= J; I++)
+            if (!(gcomp(I) && gcomp(J))) {
+                blocks.push_back((uint32_t)I);
+                blocks.push_back((uint32_t)J);
+            }
+    }
+    const uint32_t nbl = (uint32_t)(blocks.size() / 2) - nfast;
     const uint64_t rows = j1 - j0;
     int r = ensure(c, c->ld_blocks, 4 * blocks.size() + 8);
     if (!r) r = ensure(c, c->ld_cnt, 2 * rows * nb + 16);
@@ -697,13 +721,21 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     HIPCHK(c, hipMemcpyAsync(c->ld_blocks.p, c->ld_blocks_host.data(), 4 * c->ld_blocks_host.size(),
                              hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->ld_cnt.p, 0, 2 * rows * nb + 16, c->stream));
-    vcfxg::LdWindowArgs a{M, c->ld_kpad, c->ld_ns, window, threshold, max_dist, j0, j1, nb};
+    vcfxg::LdWindowArgs a{M, c->ld_kpad, c->ld_ns, window, threshold, max_dist, j0, j1, nb, 0.0, 0};
+    // prefilter margin: |fp64 r^2 - exact r^2| of the reference's sequence is < ~1.2e-14 * n
+    // (vx >= (n-1)/n^2 for a polymorphic complete variant); delta covers it 100-fold
+    a.tm = threshold - (1e-6 + 1e-10 * (double)c->ld_ns);
+    a.all_pass = a.tm <= 0.0;
     const uint32_t *cid = max_dist > 0 ? P<uint32_t>(c->ld_cid) : nullptr;
+    const uint32_t *fbl = P<uint32_t>(c->ld_blocks), *gbl = fbl + 2 * (size_t)nfast;
     prof_begin(c, "ld_count");
-    HIPCHK(c, vcfxg::launch_ld_block(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a,
-                                     P<uint32_t>(c->ld_blocks), nbl, P<uint16_t>(c->ld_cnt), nullptr, nullptr,
-                                     c->stream));
+    HIPCHK(c, vcfxg::launch_ld_fast(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
+                                    P<uint16_t>(c->ld_cnt), nullptr, nullptr, c->stream));
     prof_end(c, "ld_count");
+    prof_begin(c, "ld_count_gen");
+    HIPCHK(c, vcfxg::launch_ld_block(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,
+                                     P<uint16_t>(c->ld_cnt), nullptr, nullptr, c->stream));
+    prof_end(c, "ld_count_gen");
     hipcub::TransformInputIterator<uint64_t, U16ToU64, const uint16_t *> cin(P<uint16_t>(c->ld_cnt), U16ToU64());
     const size_t ncnt = rows * nb + 1;  // +1: the zeroed pad entry gives the total
     size_t tmp = 0;
@@ -720,10 +752,15 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     if (!r) r = ensure(c, c->rowoff, 8 * (np + 1));
     if (r) return r;
     prof_begin(c, "ld_emit");
-    HIPCHK(c, vcfxg::launch_ld_block(2, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a,
-                                     P<uint32_t>(c->ld_blocks), nbl, P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off),
-                                     P<vcfxg::LdPair>(c->ld_pairs), c->stream));
+    HIPCHK(c, vcfxg::launch_ld_fast(2, P<int8_t>(c->ld_Gc), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
+                                    P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off), P<vcfxg::LdPair>(c->ld_pairs),
+                                    c->stream));
     prof_end(c, "ld_emit");
+    prof_begin(c, "ld_emit_gen");
+    HIPCHK(c, vcfxg::launch_ld_block(2, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,
+                                     P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off), P<vcfxg::LdPair>(c->ld_pairs),
+                                     c->stream));
+    prof_end(c, "ld_emit_gen");
     HIPCHK(c, vcfxg::launch_ld_pairtext(0, P<vcfxg::LdPair>(c->ld_pairs), np, P<uint64_t>(c->ld_poff), nullptr,
                                         P<uint64_t>(c->rowlen), nullptr, c->stream));
     HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->rowlen) + np, 0, 8, c->stream));

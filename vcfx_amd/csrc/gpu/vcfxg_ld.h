@@ -32,6 +32,24 @@ struct LdVar {  // per variant (compact order)
     uint64_t chrom, id, line;
 };
 
+// complete-variant terms of computeRsqSIMD (:352-393) with n = ns, computed once per variant
+// with the reference's own operation order, plus the integer variance for the prefilter
+struct LdFast {
+    double mx;   // Sx / n
+    double vx;   // Sx2 / n - mx*mx  (== computeStats varX for a complete variant)
+    double sq;   // sqrt(vx)
+    double vxp;  // n*Sx2 - Sx^2 as double (> 0), +inf for a monomorphic variant
+    int sx, pos;
+};
+
+// r^2 of two complete variants from S_xy: the reference's fp64 sequence, bit-identical
+__device__ __forceinline__ double ld_fast_r2(const LdFast &fi, const LdFast &fj, int sxy, double dn) {
+    if (!(fi.vx > 0.0) || !(fj.vx > 0.0) || dn < 2.0) return 0.0;  // computeRsqFast gate / n < 2
+    const double cov = __dsub_rn(__ddiv_rn((double)sxy, dn), __dmul_rn(fi.mx, fj.mx));
+    const double r = __ddiv_rn(cov, __dmul_rn(fi.sq, fj.sq));
+    return __dmul_rn(r, r);
+}
+
 struct LdPair {
     uint32_t i, j;          // variant indices, i < j
     double r2;
@@ -45,13 +63,19 @@ struct LdWindowArgs {
     int max_dist;           // > 0: same-chrom pairs farther apart are skipped (mmap streaming)
     uint64_t j_lo, j_hi;    // rows of this chunk
     uint64_t nb;            // column blocks per row in the count table
+    double tm;              // prefilter: exact r^2 < tm cannot reach threshold (tm = threshold - delta)
+    int all_pass;           // tm <= 0: every pair is a candidate
 };
 
 hipError_t launch_ld_parse(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, const LdParseArgs &a, int8_t *G, LdLine *lines, hipStream_t s);
 hipError_t launch_ld_compact(const LdLine *lines, const uint64_t *vidx, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int kpad, int ns, const int8_t *G, int8_t *Gc, LdVar *vars,
-                             hipStream_t s);
+                             LdFast *fv, hipStream_t s);
+hipError_t launch_ld_fast(int pass, const int8_t *Gc, const LdFast *fv, const uint32_t *chrom_id,
+                          const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
+                          const uint64_t *off, LdPair *pairs, hipStream_t s);
+hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, uint8_t *gflag, hipStream_t s);
 hipError_t launch_ld_block(int pass, const int8_t *Gc, const LdVar *vars, const uint32_t *chrom_id,
                            const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
                            const uint64_t *off, LdPair *pairs, hipStream_t s);
@@ -64,5 +88,6 @@ hipError_t launch_ld_matrix(const int8_t *Gc, const LdVar *vars, uint64_t m, int
 hipError_t launch_mfma_i8_selftest(const int8_t *A, const int8_t *B, int *C, hipStream_t s);
 
 constexpr int kLdBlock = 64;
+constexpr int kLdFastBlock = 128;
 
 }  // namespace vcfxg

@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void k_ld_parse(const char *__restrict__ buf, 
 // gather valid variants into compact order; stats -> fp64 varX exactly as computeStats
 __global__ void k_ld_compact(const LdLine *__restrict__ lines, const uint64_t *__restrict__ vidx,
                              const uint64_t *n_lines_p, int kpad, int ns, const int8_t *__restrict__ G,
-                             int8_t *__restrict__ Gc, LdVar *__restrict__ vars) {
+                             int8_t *__restrict__ Gc, LdVar *__restrict__ vars, LdFast *__restrict__ fv) {
     const uint64_t n = *n_lines_p;
     // one block per line-chunk; each valid line copies its row (kpad bytes) with the block
     for (uint64_t li = blockIdx.x; li < n; li += gridDim.x) {
@@ -279,6 +279,22 @@ __global__ void k_ld_compact(const LdLine *__restrict__ lines, const uint64_t *_
             o.id_len = L.id_len;
             o.line = li;
             vars[v] = o;
+            LdFast f;
+            f.mx = 0.0;
+            f.vx = 0.0;
+            f.sq = 0.0;
+            f.vxp = __longlong_as_double(0x7FF0000000000000ll);  // +inf: never a prefilter candidate
+            if (L.cnt > 0) {
+                const double dn = (double)L.cnt;
+                f.mx = __ddiv_rn((double)L.sx, dn);
+                f.vx = __dsub_rn(__ddiv_rn((double)L.sx2, dn), __dmul_rn(f.mx, f.mx));
+                f.sq = f.vx > 0.0 ? __dsqrt_rn(f.vx) : 0.0;
+                const int64_t V = (int64_t)L.cnt * (int64_t)L.sx2 - (int64_t)L.sx * (int64_t)L.sx;
+                if (V > 0) f.vxp = (double)V;
+            }
+            f.sx = (int)L.sx;
+            f.pos = L.pos;
+            fv[v] = f;
         }
     }
 }
@@ -646,10 +662,10 @@ hipError_t launch_ld_parse(const char *buf, int64_t data_start, const uint64_t *
 }
 hipError_t launch_ld_compact(const LdLine *lines, const uint64_t *vidx, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int kpad, int ns, const int8_t *G, int8_t *Gc, LdVar *vars,
-                             hipStream_t s) {
+                             LdFast *fv, hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
     hipLaunchKernelGGL(k_ld_compact, dim3(gridfor(n_lines_host, 1, 65536)), dim3(256), 0, s, lines, vidx, n_lines_dev,
-                       kpad, ns, G, Gc, vars);
+                       kpad, ns, G, Gc, vars, fv);
     return hipGetLastError();
 }
 hipError_t launch_ld_block(int pass, const int8_t *Gc, const LdVar *vars, const uint32_t *chrom_id,

@@ -81,12 +81,14 @@ static size_t put_int(char *b, int64_t v) {
 static inline int allele_of(const vcfx_synth_opts *o, int64_t k, const rec_meta *m, int s, int h) {
     uint64_t r;
     if (o->hap_blocks) {
-        /* 100 founders; sample haplotype copies a founder chosen per 64-record block;
-         * founder alleles at this site drawn with p; 0.5% copying error */
+        /* 100 founders; a sample haplotype copies a founder chosen per 64-record block.
+         * Founder f carries the ALT allele at site k iff its per-block key is below the
+         * site's frequency, so the carrier sets of a block's sites are nested (strong LD
+         * between sites of similar frequency); 0.5% copying error */
         int64_t blk = k / 64;
         int f = (int)(rnd(o->seed, (uint64_t)blk, 1000 + (uint64_t)(2 * s + h)) % 100);
-        uint64_t fr = rnd(o->seed, (uint64_t)k, 5000 + (uint64_t)f);
-        int a = u01(fr) < (m->p < 0.05 ? 0.05 + m->p : m->p);
+        double key = u01(rnd(o->seed, (uint64_t)blk, 5000 + (uint64_t)f));
+        int a = key < (m->p < 0.05 ? 0.05 + m->p : m->p);
         if (u01(rnd(o->seed, (uint64_t)k, 9000000 + (uint64_t)(2 * s + h))) < 0.005) a ^= 1;
         return a;
     }

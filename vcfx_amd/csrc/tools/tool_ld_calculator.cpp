@@ -136,7 +136,7 @@ bool run_stream(const Input &in, bool mmap_mode, const LdOpts &o, const std::str
     const uint64_t W = std::min<uint64_t>(o.window, M ? M : 1);
     // chunk rows so that a chunk holds at most ~16M candidate pairs
     uint64_t R = (16ull << 20) / std::max<uint64_t>(W, 1);
-    R = std::max<uint64_t>(64, (R / 64) * 64);
+    R = std::max<uint64_t>(128, (R / 128) * 128);  // whole 128-variant fast blocks
     std::string text;
     for (uint64_t j0 = 0; j0 < M; j0 += R) {
         uint64_t np = 0, tb = 0;
