@@ -5,8 +5,8 @@ Workloads (BASELINE.json configs; the default is the headline one):
   af        configs[1] / configs[3]: VCFX_allele_freq_calc -i on a device-resident
             427,409-record x 2,504-sample chr21-like shard per GPU.  A step = record index
             (line_count + line_emit) + per-record allele counts (af_records) + device
-            formatted output rows (af_rows + af_format); for N > 1 ranks also all-reduce the
-            step's global counts (records, rows, alt/total alleles) over RCCL.
+            formatted output rows (af_rows + af_format), all through vcfxg_allele_freq_region;
+            for N > 1 ranks also all-reduce the step's global counts over RCCL.
   pipeline  configs[2]: VCFX_record_filter --filter "QUAL>=30;FILTER==PASS" |
             VCFX_genotype_query --genotype-query "0|1" fused on the device (index + one
             filter_query pass), same shard.
@@ -153,12 +153,11 @@ def main():
 
     if a.workload == "af":
         def step():
-            eng.index(ds)
-            s = eng.allele_freq(engine.MODE_FILE)
+            s = eng.allele_freq_region(ds, engine.MODE_FILE)  # index + counts + rows
             if red is not None:
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.text_bytes])
             return s
-        kern_names = ("line_count", "line_emit", "af_records", "af_rows", "af_format")
+        kern_names = ("line_count", "line_emit", "af_records", "af_fused", "af_rows", "af_format")
     elif a.workload == "pipeline":
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
@@ -242,6 +241,7 @@ def main():
                 "line_count": region_bytes,
                 "line_emit": region_bytes + 8 * L,
                 "af_records": region_bytes + L * (8 + 13),      # record bytes + line_end + per-line results
+                "af_fused": region_bytes + L * (8 + 13),        # one sweep: record bytes + line_end + results
                 "af_format": tb + L * (8 + 8 + 13) + s.rows * 40,
                 "af_rows": L * (5 + 8 + 8 + 8),
                 "rf_records": region_bytes + L * (8 + 1),

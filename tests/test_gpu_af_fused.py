@@ -1,0 +1,119 @@
+"""GPU parity of the fused one-sweep AF path (vcfxg_allele_freq_region: chunked line marks,
+decoupled look-back numbering, per-record counts in one kernel) against the two-pass path
+(vcfxg_index + vcfxg_allele_freq) and the C oracle: every per-line array and the output
+text must be identical, including inputs that put many line starts in one 16 KiB chunk
+(more than the kernel's per-pass mark list), lines that span several chunks, CRLF, empty
+lines, no trailing newline and chunk-boundary newlines."""
+import numpy as np
+import pytest
+
+from tests._golden import Oracle
+from vcfx_amd import engine, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    import os
+    old = os.environ.get("VCFXG_AF_FUSED")
+    os.environ["VCFXG_AF_FUSED"] = "1"  # read at vcfxg_open
+    try:
+        return engine.Engine(0)
+    finally:
+        if old is None:
+            del os.environ["VCFXG_AF_FUSED"]
+        else:
+            os.environ["VCFXG_AF_FUSED"] = old
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return Oracle()
+
+
+def _both(eng, buf, mode):
+    ds = engine.data_start_of(buf, strip_cr=(mode == engine.MODE_FILE))
+    eng.load(buf)
+    nl = eng.index(ds)
+    s2 = eng.allele_freq(mode)
+    two = (eng.line_ends(nl), eng.lines(nl), eng.text(s2.text_bytes), s2)
+    eng.load(buf)
+    s1 = eng.allele_freq_region(ds, mode)
+    nl1 = s1.n_lines
+    one = (eng.line_ends(nl1), eng.lines(nl1), eng.text(s1.text_bytes), s1)
+    return ds, two, one
+
+
+def _same(two, one):
+    e2, (a2, t2, st2), x2, s2 = two
+    e1, (a1, t1, st1), x1, s1 = one
+    assert s1.n_lines == s2.n_lines
+    np.testing.assert_array_equal(e1, e2)
+    np.testing.assert_array_equal(st1, st2)
+    rows = st2 == 1
+    np.testing.assert_array_equal(a1[rows], a2[rows])
+    np.testing.assert_array_equal(t1[rows], t2[rows])
+    assert x1 == x2
+    assert (s1.rows, s1.data_lines, s1.warn_lines, s1.general_records) == \
+        (s2.rows, s2.data_lines, s2.warn_lines, s2.general_records)
+
+
+SYNTH = [
+    # records, samples, seed, info, missing, hap, irregular, crlf
+    (3000, 2504, 11, 0, 0.0, 0, 0.0, 0),   # 10 KB lines spanning chunks
+    (2000, 997, 12, 1, 0.01, 0, 0.2, 0),
+    (4000, 3, 13, 0, 0.05, 0, 0.3, 1),     # ~60 B lines: > 256 starts per chunk, CRLF
+    (30000, 1, 14, 0, 0.0, 0, 0.0, 0),     # ~45 B lines: several mark passes per chunk
+]
+
+
+@pytest.mark.parametrize("cfg", SYNTH)
+@pytest.mark.parametrize("mode", [engine.MODE_FILE, engine.MODE_STDIN])
+def test_fused_matches_two_pass(eng, cfg, mode):
+    buf = synth.generate(*cfg)
+    _, two, one = _both(eng, buf, mode)
+    _same(two, one)
+
+
+def test_fused_edge_layouts(eng, oracle):
+    head = b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tA\tB\n"
+    row = b"1\t5\t.\tA\tG\t.\t.\t.\tGT\t0|1\t1|1\n"
+    cases = [
+        head + row * 3,                       # trailing newline
+        head + row * 3 + row[:-1],            # no trailing newline
+        head + b"\n\n" + row + b"\n" + row,   # empty lines
+        head + b"\n",                         # one empty data line
+        head + row[:-1],                      # a single unterminated record
+        head + b"#late header\n" + row,
+    ]
+    # a newline on the last byte of chunk 0, on the first byte of chunk 1, and just before
+    ds = len(head)
+    last0 = ((ds - 1) & ~15) + 16384 - 1
+    filler = b"1\t7\t.\tA\tG\t.\t.\t.\tGT\t0|0\t0|1\n"
+    for shift in (-1, 0, 1):
+        body = b""
+        while ds + len(body) + 2 * len(filler) + 64 < last0:
+            body += filler
+        tail = b"\tA\tG\t.\t.\t.\tGT\t0|0\t0|1\n"
+        k = last0 + shift - (ds + len(body)) - len(b"1\t7\t") - len(tail) + 1
+        line = b"1\t7\t" + b"x" * k + tail
+        assert ds + len(body) + len(line) - 1 == last0 + shift
+        cases.append(head + body + line + row * 5)
+    for buf in cases:
+        for mode in (engine.MODE_FILE, engine.MODE_STDIN):
+            _, two, one = _both(eng, buf, mode)
+            _same(two, one)
+
+
+def test_fused_text_matches_oracle(eng, oracle):
+    import tempfile
+    buf = synth.generate(1200, 401, 15, 1, 0.02, 0, 0.2, 0)
+    ds = engine.data_start_of(buf)
+    eng.load(buf)
+    s = eng.allele_freq_region(ds, engine.MODE_FILE)
+    with tempfile.NamedTemporaryFile(suffix=".vcf") as f:
+        f.write(buf)
+        f.flush()
+        want, _, _ = oracle.run(["VCFX_allele_freq_calc", "-q", "-i", f.name])
+    assert b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes) == want

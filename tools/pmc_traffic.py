@@ -20,12 +20,15 @@ KERNELS = {
     "line_count": r"vcfxg::k_nl_count\(",
     "line_emit": r"vcfxg::k_nl_emit\(",
     "af_records": r"vcfxg::k_af_records\(",
+    "af_fused": r"vcfxg::k_af_fused\(",
     "af_format": r"vcfxg::k_af_format\(",
     "rf_records": r"vcfxg::k_rf_records\(",
     "gq_records": r"vcfxg::k_gq_records\(",
     "ld_parse": r"vcfxg::k_ld_parse\(",
-    "ld_count": r"vcfxg::k_ld_block<1>\(",
-    "ld_emit": r"vcfxg::k_ld_block<2>\(",
+    "ld_count": r"vcfxg::k_ld_fast<1>\(",
+    "ld_emit": r"vcfxg::k_ld_fast<2>\(",
+    "ld_count_gen": r"vcfxg::k_ld_block<1>\(",
+    "ld_emit_gen": r"vcfxg::k_ld_block<2>\(",
     "ld_matrix": r"vcfxg::k_ld_matrix\(",
 }
 

@@ -11,7 +11,7 @@ import os
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD = os.path.join(REPO, "build")
-GPU_LIB = os.path.join(BUILD, "libvcfx_gpu.so")
+GPU_LIB = os.environ.get("VCFXG_GPU_LIB") or os.path.join(BUILD, "libvcfx_gpu.so")  # env: experiment builds
 TOOLS_LIB = os.path.join(BUILD, "libvcfx_tools.so")
 SYNTH_LIB = os.path.join(BUILD, "libvcfx_synth.so")
 TOOLS = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query", "VCFX_ld_calculator",

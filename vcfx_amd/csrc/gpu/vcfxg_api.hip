@@ -47,6 +47,11 @@ struct vcfxg_ctx {
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
         ld_off, ld_pairs, ld_fast, ld_gflag;
+    DevBuf fuse_state;          // fused AF: per-chunk look-back words
+    uint64_t af_line_cap = 0;   // fused AF: line capacity the last run needed
+    // one-sweep fused AF (k_af_fused) is opt-in until it beats the two-pass path
+    bool af_fused = getenv("VCFXG_AF_FUSED") && atoi(getenv("VCFXG_AF_FUSED")) != 0;
+    int fuse_dbg = getenv("VCFXG_FUSE_DEBUG") ? atoi(getenv("VCFXG_FUSE_DEBUG")) : 0;  // diagnostics only
     std::vector<uint8_t> ld_gflag_host;  // per 128-variant group: all complete
     uint64_t ld_m = 0, ld_prefix_bytes = 0;
     int ld_kpad = 64, ld_ns = 0;
@@ -178,7 +183,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->fuse_state})
         if (b->p) (void)hipFree(b->p);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
@@ -291,17 +296,24 @@ int vcfxg_line_ends(vcfxg_ctx *c, uint64_t first, uint64_t count, uint64_t *out)
     return VCFXG_OK;
 }
 
-int vcfxg_allele_freq(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
-    if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
-    if (!c->indexed) return VCFXG_E_STATE;
-    HIPCHK(c, hipSetDevice(c->device));
-    const uint64_t L = c->n_lines;
+static int af_buffers(vcfxg_ctx *c, uint64_t L) {
     int r = ensure(c, c->alt, 4 * (L + 1));
     if (!r) r = ensure(c, c->tot, 4 * (L + 1));
     if (!r) r = ensure(c, c->rowpre, 4 * (L + 1));
     if (!r) r = ensure(c, c->status, L + 1);
     if (!r) r = ensure(c, c->rowlen, 8 * (L + 1));
     if (!r) r = ensure(c, c->rowoff, 8 * (L + 1));
+    return r;
+}
+
+static int af_rows(vcfxg_ctx *c, int mode, vcfxg_summary *out);
+
+int vcfxg_allele_freq(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
+    if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t L = c->n_lines;
+    int r = af_buffers(c, L);
     if (r) return r;
     const char *buf = P<char>(c->input);
     const uint64_t *nl_dev = P<uint64_t>(c->d_nlines);
@@ -311,6 +323,60 @@ int vcfxg_allele_freq(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
                                        P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
                                        P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
     prof_end(c, "af_records");
+    return af_rows(c, mode, out);
+}
+
+int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
+    if (!c->loaded) return VCFXG_E_STATE;
+    if (data_start > c->n) data_start = c->n;
+    const uint64_t nc = c->af_fused ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
+    if (!nc) {  // the two-pass path (default; also no data lines or data_start == 0)
+        int r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    const char *buf = P<char>(c->input);
+    // line capacity: what the last run needed, else a 256 B/line estimate; a larger count
+    // reruns once with the exact capacity (the kernel counts every line regardless)
+    uint64_t cap = std::max<uint64_t>(c->af_line_cap, (c->n - data_start) / 256 + 4096);
+    for (int attempt = 0; attempt < 2; attempt++) {
+        int r = af_buffers(c, cap);
+        if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
+        if (!r) r = ensure(c, c->fuse_state, 8 * (nc + 1) + 64);
+        if (r) return r;
+        HIPCHK(c, hipMemsetAsync(c->fuse_state.p, 0, 8 * (nc + 1) + 64, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+        prof_begin(c, "af_fused");
+        HIPCHK(c, vcfxg::launch_af_fused(buf, (int64_t)data_start, (int64_t)c->n, mode,
+                                         P<unsigned long long>(c->fuse_state), P<uint64_t>(c->line_end),
+                                         P<uint64_t>(c->d_nlines), cap, P<int32_t>(c->alt), P<int32_t>(c->tot),
+                                         P<uint32_t>(c->rowpre), P<uint8_t>(c->status),
+                                         P<unsigned long long>(c->counters), c->stream, c->fuse_dbg));
+        prof_end(c, "af_fused");
+        static thread_local uint64_t nl, diag[8];
+        HIPCHK(c, hipMemcpyAsync(&nl, c->d_nlines.p, 8, hipMemcpyDeviceToHost, c->stream));
+        if (c->fuse_dbg & 2) HIPCHK(c, hipMemcpyAsync(diag, c->counters.p, 64, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->fuse_dbg & 2) fprintf(stderr, "af_fused: chunks %llu self-counted %llu\n", (unsigned long long)nc,
+                                     (unsigned long long)diag[5]);
+        c->data_start = data_start;
+        c->n_lines = nl;
+        c->indexed = true;
+        if (nl <= cap) {
+            c->af_line_cap = std::max<uint64_t>(c->af_line_cap, nl);
+            return af_rows(c, mode, out);
+        }
+        cap = nl;
+    }
+    return VCFXG_E_STATE;
+}
+
+static int af_rows(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
+    const uint64_t L = c->n_lines;
+    const char *buf = P<char>(c->input);
+    const uint64_t *nl_dev = P<uint64_t>(c->d_nlines);
+    int r;
     prof_begin(c, "af_rows");
     HIPCHK(c, vcfxg::launch_af_rowlen(P<uint32_t>(c->rowpre), P<uint8_t>(c->status), nl_dev, L, P<uint64_t>(c->rowlen),
                                       c->stream));

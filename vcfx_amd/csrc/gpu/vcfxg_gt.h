@@ -49,7 +49,10 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
     const int64_t b0 = S & ~(int64_t)15;
     uint32_t err = 0;
     // kUnroll wave-steps per iteration: their loads are all issued before any is consumed
-    constexpr int kUnroll = 4;
+#ifndef VCFXG_UNROLL
+#define VCFXG_UNROLL 4
+#endif
+    constexpr int kUnroll = VCFXG_UNROLL;
     for (int64_t w0 = b0; w0 < E; w0 += kUnroll * kWaveStep) {
         uint4 v[kUnroll];
         uint32_t x4[kUnroll];

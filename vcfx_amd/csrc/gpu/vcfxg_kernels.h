@@ -12,6 +12,11 @@ hipError_t launch_nl_emit(const char *buf, int64_t lo, int64_t hi, const uint64_
 hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int mode, int32_t *alt, int32_t *tot, uint32_t *rowpre,
                              uint8_t *status, unsigned long long *counters, hipStream_t s);
+// fused index + AF (one sweep): chunks for data_start / n (0 = use the two-pass path)
+uint64_t af_fused_chunks(int64_t ds, int64_t n);
+hipError_t launch_af_fused(const char *buf, int64_t ds, int64_t n, int mode, unsigned long long *state, uint64_t *line_end, uint64_t *n_lines_dev, uint64_t cap,
+                           int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
+                           unsigned long long *counters, hipStream_t s, int dbg = 0);
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
                              int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,

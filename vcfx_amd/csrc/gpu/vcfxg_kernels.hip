@@ -104,7 +104,72 @@ __device__ __forceinline__ void line_bounds(const uint64_t *__restrict__ line_en
     le = (int64_t)line_end[li];
 }
 
-// counters: 0 rows, 1 data lines, 2 warn lines, 3 general-path records
+// One AF data line [ls, le): processMmap :355-470 (mode 0) / processStdin :490-556 (mode 1).
+// Status 1 = output row, 3 = "<9 fields" warning (stdin), 0 = nothing.  Counters: 0 rows,
+// 1 data lines, 2 warn lines, 3 general-path records.
+__device__ __forceinline__ void af_line(const char *__restrict__ buf, int64_t ls, int64_t le, int mode, int64_t *lds,
+                                        BlockCounters &bc, uint8_t &st, uint32_t &alt, uint32_t &tot,
+                                        uint32_t &rowpre) {
+    int64_t ae = le;
+    if (mode == 0 && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;  // processMmap :362-364
+    st = 0;
+    alt = tot = rowpre = 0;
+    if (ae > ls && byte_at(buf, ls) != '#') {
+        bc.add(1, 1);
+        int64_t t[10];
+        const int nt = head_tabs(buf, ls, ae, 10, t, lds);
+        bool ok = true;
+        int64_t fs = 0, fe = 0;
+        if (mode == 0) {
+            // getField(8) must be non-empty (processMmap :391-401)
+            if (nt < 8) ok = false;
+            else {
+                fs = t[7] + 1;
+                fe = nt >= 9 ? t[8] : ae;
+                ok = fe > fs;
+            }
+        } else {
+            // processStdin :509-523: #fields = tabs + (last char != '\t')
+            int nf = nt >= 9 ? 10 : nt + ((byte_at(buf, ae - 1) != '\t') ? 1 : 0);
+            if (nf < 9) {
+                st = 3;
+                ok = false;
+            } else {
+                fs = t[7] + 1;
+                fe = nt >= 9 ? t[8] : ae;
+            }
+        }
+        if (ok) {
+            const int gi = gt_index(buf, fs, fe);
+            if (gi >= 0) {
+                if (nt >= 9) {
+                    const int64_t S = t[8] + 1;
+                    AfOp op{buf, ae, gi};
+                    bool fast = gi == 0 && gt_fast(buf, S, ae, op);
+                    if (fast) {
+                        alt = op.alt;
+                        tot = op.tot;
+                    } else {
+                        AfOp g{buf, ae, gi};
+                        gt_general(buf, S, ae, g);
+                        alt = g.alt;
+                        tot = g.tot;
+                        bc.add(3, 1);
+                    }
+                }
+                st = 1;
+                rowpre = (uint32_t)(t[4] - ls + 1);
+            }
+        }
+    }
+    bc.add(0, st == 1);
+    bc.add(2, st == 3);
+}
+
+// one wave per indexed line
+#ifdef VCFXG_AF_WAVES
+__attribute__((amdgpu_waves_per_eu(VCFXG_AF_WAVES, 8)))
+#endif
 __global__ __launch_bounds__(kRecThreads) void k_af_records(const char *__restrict__ buf, int64_t data_start,
                                                             const uint64_t *__restrict__ line_end,
                                                             const uint64_t *n_lines_p, int mode,
@@ -124,68 +189,178 @@ __global__ __launch_bounds__(kRecThreads) void k_af_records(const char *__restri
     for (uint64_t li = wid; li < n_lines; li += nw) {
         int64_t ls, le;
         line_bounds(line_end, data_start, li, ls, le);
-        int64_t ae = le;
-        if (mode == 0 && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;  // processMmap :362-364
-        uint8_t st = 0;
-        uint32_t alt = 0, tot = 0, rowpre = 0;
-        if (ae > ls && byte_at(buf, ls) != '#') {
-            bc.add(1, 1);
-            int64_t t[10];
-            const int nt = head_tabs(buf, ls, ae, 10, t, lds);
-            bool ok = true;
-            int64_t fs = 0, fe = 0;
-            if (mode == 0) {
-                // getField(8) must be non-empty (processMmap :391-401)
-                if (nt < 8) ok = false;
-                else {
-                    fs = t[7] + 1;
-                    fe = nt >= 9 ? t[8] : ae;
-                    ok = fe > fs;
-                }
-            } else {
-                // processStdin :509-523: #fields = tabs + (last char != '\t')
-                int nf = nt >= 9 ? 10 : nt + ((byte_at(buf, ae - 1) != '\t') ? 1 : 0);
-                if (nf < 9) {
-                    st = 3;
-                    ok = false;
-                } else {
-                    fs = t[7] + 1;
-                    fe = nt >= 9 ? t[8] : ae;
-                }
-            }
-            if (ok) {
-                const int gi = gt_index(buf, fs, fe);
-                if (gi >= 0) {
-                    if (nt >= 9) {
-                        const int64_t S = t[8] + 1;
-                        AfOp op{buf, ae, gi};
-                        bool fast = gi == 0 && gt_fast(buf, S, ae, op);
-                        if (fast) {
-                            alt = op.alt;
-                            tot = op.tot;
-                        } else {
-                            AfOp g{buf, ae, gi};
-                            gt_general(buf, S, ae, g);
-                            alt = g.alt;
-                            tot = g.tot;
-                            bc.add(3, 1);
-                        }
-                    }
-                    st = 1;
-                    rowpre = (uint32_t)(t[4] - ls + 1);
-                }
-            }
-        }
+        uint8_t st;
+        uint32_t alt, tot, rowpre;
+        af_line(buf, ls, le, mode, lds, bc, st, alt, tot, rowpre);
         if (lane() == 0) {
             status_o[li] = st;
             alt_o[li] = (int32_t)alt;
             tot_o[li] = (int32_t)tot;
             rowpre_o[li] = rowpre;
         }
-        bc.add(0, st == 1);
-        bc.add(2, st == 3);
     }
     flush_counters(cnt, counters);
+}
+
+// =======================================================================================
+// K12: fused index + AF, one HBM sweep.  The data region is cut into 16 KiB chunks, one per
+// one-wave block.  A block sweeps its chunk for line marks (the virtual
+// newline at data_start-1 and every '\n' of [data_start, N)), publishes its count of line
+// starts, and gets its first global line number by a decoupled look-back over the
+// predecessors' published counts.  It then runs af_line on every line starting after one
+// of its marks (the chunk it just swept is L2-resident; a line may run past the chunk) and
+// writes line_end / status / counts at global line numbers, so every later kernel sees the
+// same arrays as after vcfxg_index + k_af_records.
+// =======================================================================================
+constexpr int64_t kFuseChunk = 16 * 1024;
+constexpr int kFuseCap = 512;  // marks held per pass (more only for lines < 32 B on average)
+constexpr uint64_t kStAgg = 1ull << 62, kStIncl = 2ull << 62, kStVal = (1ull << 62) - 1;
+
+__device__ __forceinline__ void st_publish(unsigned long long *p, uint64_t v) {
+    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t st_peek(unsigned long long *p) {
+    return (uint64_t)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// marks of [cs, ce): returns their total; stores offsets (relative to cs) of ranks
+// [r_lo, r_lo + kFuseCap] into list
+__device__ int fuse_sweep(const char *__restrict__ buf, int64_t cs, int64_t ce, int64_t ds, int r_lo, int *list) {
+    int run = 0;
+    const int64_t lo = ds > cs ? ds : cs;
+    const int64_t vnl = ds - 1;  // the virtual newline ending the header
+    for (int64_t w0 = cs; w0 < ce; w0 += 4 * kWaveStep) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int64_t blk = w0 + u * kWaveStep + (int64_t)lane() * kBlockBytes;
+            if (blk < ce) v[u] = load16(buf, blk);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int64_t blk = w0 + u * kWaveStep + (int64_t)lane() * kBlockBytes;
+            uint32_t m = 0;
+            if (blk < ce) {
+                m = eq_mask16(v[u], kRepNl) & range_mask16(blk, lo, ce);
+                if (vnl >= blk && vnl < blk + 16 && vnl >= cs && vnl < ce) m |= 1u << (vnl - blk);
+            }
+            const int c = __popc(m);
+            const int incl = wave_incl_scan(c);
+            int rank = run + incl - c;
+            while (m) {
+                const int j = __builtin_ctz(m);
+                m &= m - 1u;
+                if (list && rank >= r_lo && rank <= r_lo + kFuseCap) list[rank - r_lo] = (int)(blk + j - cs);
+                rank++;
+            }
+            run += wave_bcast(incl, kWave - 1);
+        }
+    }
+    return run;
+}
+
+// line starts of chunk k (what its owner publishes): marks minus a final '\n' at n-1
+__device__ __forceinline__ int fuse_starts(const char *__restrict__ buf, int64_t base, int64_t n, int64_t ds,
+                                           uint64_t k, int *list, int *marks_o) {
+    const int64_t cs = base + (int64_t)k * kFuseChunk;
+    const int64_t ce = cs + kFuseChunk < n ? cs + kFuseChunk : n;
+    const int marks = fuse_sweep(buf, cs, ce, ds, 0, list);
+    if (marks_o) *marks_o = marks;
+    return marks - ((ce == n && n - 1 >= ds && byte_at(buf, n - 1) == '\n') ? 1 : 0);
+}
+
+__global__ __launch_bounds__(kWave) void k_af_fused(const char *__restrict__ buf, int64_t ds, int64_t n, int64_t base,
+                                                    uint64_t nchunks, int mode, unsigned long long *__restrict__ state,
+                                                    uint64_t *__restrict__ line_end, uint64_t *__restrict__ n_lines_o,
+                                                    uint64_t cap, int32_t *__restrict__ alt_o,
+                                                    int32_t *__restrict__ tot_o,
+                                                    uint32_t *__restrict__ rowpre_o, uint8_t *__restrict__ status_o,
+                                                    unsigned long long *__restrict__ counters, int dbg) {
+    __shared__ int64_t scratch[16];
+    __shared__ int list[kFuseCap + 1];
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (lane() < BlockCounters::kNC) cnt[lane()] = 0;
+    BlockCounters bc{cnt};
+    const uint64_t c = blockIdx.x;
+    const int64_t cs = base + (int64_t)c * kFuseChunk;
+    const int64_t ce = cs + kFuseChunk < n ? cs + kFuseChunk : n;
+    int marks = 0;
+    const int starts = fuse_starts(buf, base, n, ds, c, list, &marks);
+    // Decoupled look-back: exclusive count of line starts in chunks before c.  Wait-free: a
+    // predecessor that has not published after a short spin is counted here from its bytes
+    // (the same function its owner runs), so no block ever depends on another's progress
+    // and no dispatch order is assumed.
+    uint64_t excl = 0;
+    if (c == 0) {
+        if (lane() == 0) st_publish(&state[0], kStIncl | (uint64_t)starts);
+    } else {
+        if (lane() == 0) st_publish(&state[c], kStAgg | (uint64_t)starts);
+        int64_t pos = (int64_t)c - 1;
+        for (;;) {
+            const int64_t idx = pos - lane();
+            uint64_t v = idx >= 0 ? st_peek(&state[idx]) : kStIncl;
+            for (int spin = 0; spin < 32 && !__all(v != 0); spin++) {
+                __builtin_amdgcn_s_sleep(2);
+                if (v == 0) v = st_peek(&state[idx]);
+            }
+            const uint64_t incl = __ballot((v & ~kStVal) == kStIncl);
+            const int lim = incl ? __builtin_ctzll(incl) : kWave - 1;
+            uint64_t missing = __ballot(v == 0) & (lim == 63 ? ~0ull : ((2ull << lim) - 1ull));
+            while (missing) {
+                const int k = __builtin_ctzll(missing);
+                missing &= missing - 1ull;
+                const int sk = fuse_starts(buf, base, n, ds, (uint64_t)(pos - k), nullptr, nullptr);
+                if (lane() == 0) atomicAdd(&counters[5], 1ull);  // diagnostics: self-counted predecessors
+                if (lane() == k) v = kStAgg | (uint64_t)sk;
+            }
+            excl += wave_sum(lane() <= lim ? (v & kStVal) : 0ull);
+            if (incl) break;
+            pos -= kWave;
+        }
+        if (lane() == 0) st_publish(&state[c], kStIncl | (excl + (uint64_t)starts));
+    }
+    if (c == nchunks - 1 && lane() == 0) *n_lines_o = excl + (uint64_t)starts;
+    // end of the last line starting here when no later mark of this chunk ends it
+    int64_t nl_after = -1;
+    for (int r_lo = 0; r_lo < starts; r_lo += kFuseCap) {
+        if (dbg & 1) break;  // diagnostics: index part only
+        if (r_lo) marks = fuse_sweep(buf, cs, ce, ds, r_lo, list);  // > kFuseCap marks: next batch
+        const int r_hi = r_lo + kFuseCap < starts ? r_lo + kFuseCap : starts;
+        for (int k = r_lo; k < r_hi; k++) {
+            const int64_t ls = cs + list[k - r_lo] + 1;
+            int64_t le;
+            if (k + 1 < marks) le = cs + list[k + 1 - r_lo];
+            else {
+                if (nl_after < 0) {  // first '\n' at or after ce, else n
+                    nl_after = n;
+                    for (int64_t w = ce; w < n; w += kWaveStep) {
+                        const int64_t blk = w + (int64_t)lane() * kBlockBytes;
+                        uint32_t m = blk < n ? eq_mask16(load16(buf, blk), kRepNl) & range_mask16(blk, ce, n) : 0u;
+                        const uint64_t any = __ballot(m != 0);
+                        if (any) {
+                            const int src = __builtin_ctzll(any);
+                            const int64_t p = blk + (m ? __builtin_ctz(m) : 0);
+                            nl_after = __shfl(p, src);
+                            break;
+                        }
+                    }
+                }
+                le = nl_after;
+            }
+            const uint64_t li = excl + (uint64_t)k;
+            uint8_t st;
+            uint32_t alt, tot, rowpre;
+            af_line(buf, ls, le, mode, scratch, bc, st, alt, tot, rowpre);
+            if (lane() == 0 && li < cap) {
+                line_end[li] = (uint64_t)le;
+                status_o[li] = st;
+                alt_o[li] = (int32_t)alt;
+                tot_o[li] = (int32_t)tot;
+                rowpre_o[li] = rowpre;
+            }
+        }
+    }
+    if (lane() < BlockCounters::kNC && cnt[lane()]) atomicAdd(&counters[lane()], (unsigned long long)cnt[lane()]);
 }
 
 // genotype_query per line: status 1 keep, 2 drop, 3 "<9 fields" warning, 4 header, 0 empty.
@@ -348,6 +523,21 @@ hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t
     unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
     hipLaunchKernelGGL(k_af_records, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode, alt,
                        tot, rowpre, status, counters);
+    return hipGetLastError();
+}
+uint64_t af_fused_chunks(int64_t ds, int64_t n) {
+    if (ds < 1 || ds >= n) return 0;
+    const int64_t base = (ds - 1) & ~(int64_t)15;
+    return (uint64_t)((n - base + kFuseChunk - 1) / kFuseChunk);
+}
+hipError_t launch_af_fused(const char *buf, int64_t ds, int64_t n, int mode, unsigned long long *state, uint64_t *line_end, uint64_t *n_lines_dev, uint64_t cap,
+                           int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
+                           unsigned long long *counters, hipStream_t s, int dbg) {
+    const uint64_t nc = af_fused_chunks(ds, n);
+    if (!nc) return hipErrorInvalidValue;
+    const int64_t base = (ds - 1) & ~(int64_t)15;
+    hipLaunchKernelGGL(k_af_fused, dim3((unsigned)nc), dim3(kWave), 0, s, buf, ds, n, base, nc, mode, state,
+                       line_end, n_lines_dev, cap, alt, tot, rowpre, status, counters, dbg);
     return hipGetLastError();
 }
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,

@@ -66,10 +66,8 @@ bool run_af(const Input &in, int mode, bool quiet, Out &out, Out &err, uint64_t 
     if (!g) return false;
     err.flush();
     if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd)) return false;
-    uint64_t nl = 0;
-    if (!gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd)) return false;
-    vcfxg_summary s;
-    if (!gpu_ok(g, vcfxg_allele_freq(g, mode, &s), "allele_freq", err.fd)) return false;
+    vcfxg_summary s;  // index + counts + rows in one device sweep
+    if (!gpu_ok(g, vcfxg_allele_freq_region(g, data_start, mode, &s), "allele_freq", err.fd)) return false;
     std::string text(s.text_bytes, '\0');
     if (!gpu_ok(g, vcfxg_fetch_text(g, &text[0], text.size()), "fetch", err.fd)) return false;
     out.put(text);

@@ -46,6 +46,7 @@ SIGNATURES = {
     "vcfxg_index": (_I, [_VP, _S, ctypes.POINTER(_U64)]),
     "vcfxg_line_ends": (_I, [_VP, _U64, _U64, _VP]),
     "vcfxg_allele_freq": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_allele_freq_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_genotype_query": (_I, [_VP, _P, _S, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_record_filter": (_I, [_VP, _VP, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_variant_count": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
@@ -144,6 +145,12 @@ class Engine:
     def allele_freq(self, mode=MODE_FILE):
         s = Summary()
         self._chk(self.L.vcfxg_allele_freq(self.h, mode, ctypes.byref(s)), "allele_freq")
+        return s
+
+    def allele_freq_region(self, data_start, mode=MODE_FILE):
+        """index + allele counts + rows in one fused device sweep (vcfxg_allele_freq_region)."""
+        s = Summary()
+        self._chk(self.L.vcfxg_allele_freq_region(self.h, data_start, mode, ctypes.byref(s)), "allele_freq_region")
         return s
 
     def genotype_query(self, query, strict=False, strip_cr=False):
