@@ -17,7 +17,8 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wno-unused-result -Iinclude -I$(HOST_SRC
 TOOL_OBJS := $(sort $(B)/obj/hostio.o $(patsubst $(TOOL_SRC)/%.cpp,$(B)/obj/%.o,$(wildcard $(TOOL_SRC)/tool_*.cpp)))
 TOOL_BINS := $(foreach t,$(TOOLS),$(B)/src/$(t)/$(t))
 
-all: $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so
+all: $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so \
+     $(B)/libvcfx_core.so $(B)/libvcfx_core.a
 
 $(B)/obj/%.o: $(HOST_SRC)/%.cpp $(wildcard $(HOST_SRC)/*.h) include/vcfx_gpu.h
 	@mkdir -p $(dir $@)
@@ -26,6 +27,15 @@ $(B)/obj/%.o: $(HOST_SRC)/%.cpp $(wildcard $(HOST_SRC)/*.h) include/vcfx_gpu.h
 $(B)/obj/%.o: $(TOOL_SRC)/%.cpp $(wildcard $(TOOL_SRC)/*.h) $(wildcard $(HOST_SRC)/*.h) include/vcfx_gpu.h
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -c -o $@ $<
+
+# libvcfx_core: the host vcfx:: core API (include/vcfx_core.h, include/vcfx_io.h)
+$(B)/obj/core/vcfx_core.o: $(HOST_SRC)/vcfx_core.cpp include/vcfx_core.h include/vcfx_io.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -DVCFX_VERSION='"1.1.4"' -c -o $@ $<
+$(B)/libvcfx_core.so: $(B)/obj/core/vcfx_core.o
+	$(CXX) -shared -o $@ $< -lz
+$(B)/libvcfx_core.a: $(B)/obj/core/vcfx_core.o
+	ar rcs $@ $<
 
 $(B)/libvcfx_tools.so: $(TOOL_OBJS) $(B)/libvcfx_gpu.so
 	$(CXX) -shared -o $@ $(TOOL_OBJS) -L$(B) -lvcfx_gpu -lz -Wl,-rpath,'$$ORIGIN'
