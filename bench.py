@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--threshold", type=float, default=0.5, help="ld: r^2 threshold")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal on one GPU)")
     a = ap.parse_args()
     if a.records is None:
         a.records = 100000 if a.workload == "ld" else 427409
@@ -129,8 +130,13 @@ def main():
         # torch first: its HIP runtime (same soname) then serves libvcfx_gpu.so too
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.dist_backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:  # gloo rehearsal: ranks may share a GPU
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
     from vcfx_amd import engine, synth
 
     ld = a.workload == "ld"
@@ -143,7 +149,7 @@ def main():
 
     red = None
     if dist is not None:
-        red = torch.zeros(4, dtype=torch.int64, device="cuda")
+        red = torch.zeros(4, dtype=torch.int64, device="cuda" if a.dist_backend == "nccl" else "cpu")
 
     def allreduce_counts(vals):
         # global allele-count reduction over RCCL (configs[3]); per-rank outputs stay local
@@ -205,7 +211,7 @@ def main():
         if n:
             kernels[k] = tot / n
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 

@@ -44,4 +44,13 @@ if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
             > gpurun_out/pmc_$w.log 2>&1 || echo "pmc fold failed for $w"
     done
 fi
+
+if [ "$MODE" = rehearse ]; then
+    step rehearse_af 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29512 bench.py --gpus 2 --steps 3 --warmup 1 --records 50000 --dist-backend gloo \
+        --no-cpu-baseline || exit $?
+    step rehearse_ld 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29513 bench.py --gpus 2 --workload ld --records 20000 --window 20000 --steps 2 --warmup 1 \
+        --dist-backend gloo --no-cpu-baseline || exit $?
+fi
 echo "=== done"

@@ -1,0 +1,120 @@
+"""CPU coverage of the record-sharded multi-GPU path (vcfx_amd/shard.py):
+world_size-2 (and 3) gloo process groups over 127.0.0.1 run the sharded orchestration with
+the C oracle standing in for each rank's per-shard GPU run; the merged rank-0 output must
+equal the oracle's whole-file output byte for byte.  The cut logic is checked directly."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+from tests._golden import Oracle
+from vcfx_amd import shard, synth
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, cases, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o = Oracle()
+    try:
+        for argv in cases:
+            res = shard.run_sharded(argv, b"", dist, runner=lambda a, stdin: o.run(a, stdin))
+            if rank == 0:
+                q.put((argv, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_world(world, cases):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=300) for _ in cases]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    return got
+
+
+def _files(tmp):
+    paths = {}
+    head = b"##fileformat=VCFv4.2\n"
+    paths["synth"] = synth.generate(700, 37, 61, 1, 0.05, 0, 0.3, 0)
+    paths["crlf"] = synth.generate(300, 5, 62, 0, 0.0, 0, 0.2, 1)
+    bad = (head + b"1\t1\t.\tA\tG\t.\t.\t.\tGT\t0|1\n"  # data before #CHROM
+           + b"#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS1\n"
+           + b"".join(b"1\t%d\t.\tA\tG\t.\t.\t.\tGT\t%d|1\n" % (i, i % 2) for i in range(60))
+           + b"1\t99\t.\tA\n"  # short line
+           + b"".join(b"2\t%d\t.\tC\tT\t.\t.\t.\tGT\t1/1\n" % i for i in range(40))
+           + b"3\t5\tonly\tseven\tcols\t.\t.\n\n")
+    paths["bad"] = bad
+    paths["tiny"] = head + b"#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS1\n1\t1\t.\tA\tG\t.\t.\t.\tGT\t0|1\n"
+    out = {}
+    for k, b in paths.items():
+        p = os.path.join(tmp, k + ".vcf")
+        open(p, "wb").write(b)
+        out[k] = p
+    return out
+
+
+@pytest.fixture(scope="module")
+def files(tmp_path_factory):
+    return _files(str(tmp_path_factory.mktemp("shard")))
+
+
+def _cases(files):
+    cases = []
+    for k, p in files.items():
+        cases += [["VCFX_allele_freq_calc", "-i", p], ["VCFX_allele_freq_calc", "-q", "-i", p],
+                  ["VCFX_allele_freq_calc", p], ["VCFX_variant_counter", p]]
+    cases.append(["VCFX_variant_counter", "--strict", files["bad"]])
+    return cases
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_runs_match_whole_file(files, world):
+    cases = _cases(files)
+    o = Oracle()
+    got = _run_world(world, cases)
+    for argv, (out, err, rc) in got:
+        want = o.run(argv, b"")
+        assert (out, err, rc) == want, (argv, world)
+
+
+def test_record_cuts_cover_region_at_line_starts():
+    rng = np.random.default_rng(5)
+    for trial in range(30):
+        lines = [b"x" * int(rng.integers(0, 40)) for _ in range(int(rng.integers(0, 50)))]
+        buf = b"#H\n#CHROM\n" + b"\n".join(lines) + (b"\n" if rng.integers(0, 2) else b"")
+        ds = shard.header_end(buf)
+        assert ds == len(b"#H\n#CHROM\n") or ds == len(buf)
+        for world in range(1, 9):
+            cuts = shard.record_cuts(buf, ds, world)
+            assert len(cuts) == world + 1 and cuts[0] == ds and cuts[-1] == len(buf)
+            assert all(a <= b for a, b in zip(cuts, cuts[1:]))
+            for c in cuts[1:-1]:
+                assert c == ds or c == len(buf) or buf[c - 1:c] == b"\n"
+            # the shards' lines are exactly the region's lines, each once
+            region = buf[ds:]
+            joined = b"".join(buf[a:b] for a, b in zip(cuts, cuts[1:]))
+            assert joined == region
+
+
+def test_single_process_passthrough(files):
+    o = Oracle()
+    argv = ["VCFX_allele_freq_calc", "-i", files["synth"]]
+    assert shard.run_sharded(argv, b"", None, runner=lambda a, s: o.run(a, s)) == o.run(argv, b"")

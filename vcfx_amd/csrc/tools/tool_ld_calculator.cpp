@@ -78,6 +78,7 @@ namespace {
 
 struct LdOpts {
     bool matrix = false, quiet = false;
+    int shard_rank = 0, shard_world = 1;  // --shard r/N (multi-GPU extension, vcfx_amd/shard.py)
     size_t window = 1000;
     double thr = 0.0;
     int maxd = 0;
@@ -103,7 +104,7 @@ bool parse_region(const std::string &r, std::string &chrom, int &s, int &e) {
 bool run_stream(const Input &in, bool mmap_mode, const LdOpts &o, const std::string &rchrom, bool has_region, int rs,
                 int re, int out_fd, Out &err) {
     static const char kHead[] = "#VAR1_CHROM\tVAR1_POS\tVAR1_ID\tVAR2_CHROM\tVAR2_POS\tVAR2_ID\tR2\n";
-    write_all(out_fd, kHead, sizeof kHead - 1);
+    if (o.shard_rank == 0) write_all(out_fd, kHead, sizeof kHead - 1);
     const char *p = in.p, *end = in.p + in.n, *ls, *le;
     bool found = false;
     int ns = 0;
@@ -134,13 +135,34 @@ bool run_stream(const Input &in, bool mmap_mode, const LdOpts &o, const std::str
                 "ld_prepare", err.fd))
         return false;
     const uint64_t W = std::min<uint64_t>(o.window, M ? M : 1);
+    // this shard's rows: equal shares of the window pairs (row j pairs with min(j, W) rows)
+    uint64_t jb = 0, je = M;
+    if (o.shard_world > 1) {
+        auto cum = [&](uint64_t j) -> uint64_t {  // sum over rows k < j of min(k, W)
+            return j <= W ? j * (j - 1) / 2 : W * (W + 1) / 2 + (j - W - 1) * W;
+        };
+        auto cut = [&](int r) -> uint64_t {
+            if (r <= 0) return 0;
+            if (r >= o.shard_world) return M;
+            const long double target = (long double)cum(M) * r / o.shard_world;
+            uint64_t lo = 0, hi = M;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) / 2;
+                if ((long double)cum(mid) < target) lo = mid + 1;
+                else hi = mid;
+            }
+            return std::min<uint64_t>(M, (lo + 127) / 128 * 128);
+        };
+        jb = cut(o.shard_rank);
+        je = cut(o.shard_rank + 1);
+    }
     // chunk rows so that a chunk holds at most ~16M candidate pairs
     uint64_t R = (16ull << 20) / std::max<uint64_t>(W, 1);
     R = std::max<uint64_t>(128, (R / 128) * 128);  // whole 128-variant fast blocks
     std::string text;
-    for (uint64_t j0 = 0; j0 < M; j0 += R) {
+    for (uint64_t j0 = jb; j0 < je; j0 += R) {
         uint64_t np = 0, tb = 0;
-        if (!gpu_ok(g, vcfxg_ld_stream_chunk(g, j0, j0 + R, W, o.thr, mmap_mode ? o.maxd : 0, &np, &tb),
+        if (!gpu_ok(g, vcfxg_ld_stream_chunk(g, j0, std::min(j0 + R, je), W, o.thr, mmap_mode ? o.maxd : 0, &np, &tb),
                     "ld_stream_chunk", err.fd))
             return false;
         if (!tb) continue;
@@ -173,7 +195,8 @@ extern "C" int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out
                                  {"streaming", no_argument, 0, 's'},  {"matrix", no_argument, 0, 'm'},
                                  {"window", required_argument, 0, 'w'}, {"threshold", required_argument, 0, 't'},
                                  {"threads", required_argument, 0, 'n'}, {"max-distance", required_argument, 0, 'd'},
-                                 {"quiet", no_argument, 0, 'q'},       {0, 0, 0, 0}};
+                                 {"quiet", no_argument, 0, 'q'},       {"shard", required_argument, 0, 'S'},
+                                 {0, 0, 0, 0}};
     LdOpts o;
     bool show = false;
     GetoptStderr gs(err);
@@ -234,6 +257,14 @@ extern "C" int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out
             break;
         }
         case 'q': o.quiet = true; break;
+        case 'S':  // --shard r/N: rows of shard r of N (streaming); other shards print nothing else
+            if (sscanf(optarg, "%d/%d", &o.shard_rank, &o.shard_world) != 2 || o.shard_world < 1 ||
+                o.shard_rank < 0 || o.shard_rank >= o.shard_world) {
+                gs.done();
+                err.put(std::string("Error: Invalid shard '") + optarg + "'\n");
+                return 1;
+            }
+            break;
         default: show = true;
         }
     }
@@ -260,11 +291,13 @@ extern "C" int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out
             err.put("Error: cannot open file '" + o.input + "'\n");
             return 1;
         }
+        if (o.matrix && o.shard_rank > 0) return 0;  // matrix mode is not sharded: rank 0 writes it
         bool ok = o.matrix ? run_ld_matrix(in, true, o.quiet, rchrom, has_region, rs, re, out_fd, err)
                            : run_stream(in, true, o, rchrom, has_region, rs, re, out_fd, err);
         return ok ? 0 : 1;
     }
     in.read_fd(in_fd);
+    if (o.matrix && o.shard_rank > 0) return 0;
     bool ok = o.matrix ? run_ld_matrix(in, false, o.quiet, rchrom, has_region, rs, re, out_fd, err)
                        : run_stream(in, false, o, rchrom, has_region, rs, re, out_fd, err);
     return ok ? 0 : 1;
