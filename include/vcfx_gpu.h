@@ -94,11 +94,11 @@ int vcfxg_line_ends(vcfxg_ctx *ctx, uint64_t first, uint64_t count, uint64_t *ou
  * and processStdin (:477-557) per-record work: findGTIndex :298-316, extractGT :321-337,
  * parseGenotypeAndCount :262-293, writeDouble4 :119-143 / setprecision(4) :553-555. */
 int vcfxg_allele_freq(vcfxg_ctx *ctx, int mode, vcfxg_summary *out);
-/* vcfxg_index(data_start) + vcfxg_allele_freq(mode) in one call; same results and context
- * state as the two calls (the context is indexed afterwards).  With VCFXG_AF_FUSED=1 in the
- * environment at vcfxg_open it runs the one-sweep kernel instead: 16 KiB chunks whose line
- * starts are counted, numbered by a wait-free decoupled look-back and counted in the same
- * kernel (experimental: slower than the two-pass path today). */
+/* vcfxg_index(data_start) + vcfxg_allele_freq(mode) in one call, with the same results and
+ * context state as the two calls (the context is indexed afterwards).  VCFXG_AF_FUSED in the
+ * environment at vcfxg_open selects an alternative device schedule for measurement: 1 = a
+ * single sweep numbering 16 KiB chunks by a wait-free decoupled look-back, 2 = a chunk count
+ * then a chunk sweep counting records while L2-resident (both slower today). */
 int vcfxg_allele_freq_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
 /* ---- K2: genotype query ----------------------------------------------------------------
  * Per line status (vcfxg_line_status): ROW = some sample's GT sub-field matches `query`

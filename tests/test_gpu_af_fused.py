@@ -1,5 +1,5 @@
-"""GPU parity of the fused one-sweep AF path (vcfxg_allele_freq_region: chunked line marks,
-decoupled look-back numbering, per-record counts in one kernel) against the two-pass path
+"""GPU parity of vcfxg_allele_freq_region -- the default count + chunk-sweep path and the
+experimental one-sweep look-back kernel -- against the two-pass path
 (vcfxg_index + vcfxg_allele_freq) and the C oracle: every per-line array and the output
 text must be identical, including inputs that put many line starts in one 16 KiB chunk
 (more than the kernel's per-pass mark list), lines that span several chunks, CRLF, empty
@@ -13,11 +13,12 @@ from vcfx_amd import engine, synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def eng():
+@pytest.fixture(scope="module", params=["default", "fused", "chunks"])
+def eng(request):
+    """every region schedule: index + records (default), look-back single sweep, chunk sweep"""
     import os
     old = os.environ.get("VCFXG_AF_FUSED")
-    os.environ["VCFXG_AF_FUSED"] = "1"  # read at vcfxg_open
+    os.environ["VCFXG_AF_FUSED"] = {"default": "0", "fused": "1", "chunks": "2"}[request.param]  # read at vcfxg_open
     try:
         return engine.Engine(0)
     finally:

@@ -17,10 +17,11 @@ import sys
 
 # engine profiling names (vcfxg_kernel_stats) -> device kernel symbol
 KERNELS = {
-    "line_count": r"vcfxg::k_nl_count\(",
+    "line_count": r"vcfxg::k_(nl|fuse)_count\(",
     "line_emit": r"vcfxg::k_nl_emit\(",
     "af_records": r"vcfxg::k_af_records\(",
     "af_fused": r"vcfxg::k_af_fused\(",
+    "af_chunks": r"vcfxg::k_af_chunks\(",
     "af_format": r"vcfxg::k_af_format\(",
     "rf_records": r"vcfxg::k_rf_records\(",
     "gq_records": r"vcfxg::k_gq_records\(",

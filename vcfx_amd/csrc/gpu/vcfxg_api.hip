@@ -37,7 +37,7 @@ struct vcfxg_ctx {
     int last_byte = -1;  // input[n-1] (host copy), -1 if empty
     bool loaded = false;
     // index
-    DevBuf idx_counts, idx_offs, line_end, d_nlines, scan_tmp;
+    DevBuf idx_counts, idx_offs, idx_pos, line_end, d_nlines, scan_tmp;
     size_t data_start = 0;
     uint64_t n_lines = 0;
     bool indexed = false;
@@ -49,8 +49,10 @@ struct vcfxg_ctx {
         ld_off, ld_pairs, ld_fast, ld_gflag;
     DevBuf fuse_state;          // fused AF: per-chunk look-back words
     uint64_t af_line_cap = 0;   // fused AF: line capacity the last run needed
-    // one-sweep fused AF (k_af_fused) is opt-in until it beats the two-pass path
-    bool af_fused = getenv("VCFXG_AF_FUSED") && atoi(getenv("VCFXG_AF_FUSED")) != 0;
+    // region AF path: 0 = single-sweep index + k_af_records (default, fastest measured),
+    // 1 = one-sweep look-back kernel (k_af_fused), 2 = chunk count + chunk sweep
+    // (k_af_chunks); the alternatives stay selectable for measurement
+    int af_path = getenv("VCFXG_AF_FUSED") ? atoi(getenv("VCFXG_AF_FUSED")) : 0;
     int fuse_dbg = getenv("VCFXG_FUSE_DEBUG") ? atoi(getenv("VCFXG_FUSE_DEBUG")) : 0;  // diagnostics only
     std::vector<uint8_t> ld_gflag_host;  // per 128-variant group: all complete
     uint64_t ld_m = 0, ld_prefix_bytes = 0;
@@ -180,7 +182,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
+    for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
                       &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->fuse_state})
@@ -247,28 +249,40 @@ int vcfxg_index(vcfxg_ctx *c, size_t data_start, uint64_t *n_lines) {
     if (data_start > c->n) data_start = c->n;
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
-    const int64_t nc = vcfxg::idx_nchunks(lo, hi);
+    const int64_t nc = vcfxg::idx_wchunks(lo, hi);
     int r = ensure(c, c->idx_counts, sizeof(uint32_t) * (size_t)(nc + 1));
     if (!r) r = ensure(c, c->idx_offs, sizeof(uint64_t) * (size_t)(nc + 1));
+    if (!r) r = ensure(c, c->idx_pos, sizeof(uint64_t) * (size_t)nc * vcfxg::idx_pos_cap() + 64);
     if (r) return r;
     const char *buf = P<char>(c->input);
+    unsigned *overflow = reinterpret_cast<unsigned *>(P<uint64_t>(c->idx_pos) + (size_t)nc * vcfxg::idx_pos_cap());
+    HIPCHK(c, hipMemsetAsync(overflow, 0, 8, c->stream));
     prof_begin(c, "line_count");
-    HIPCHK(c, vcfxg::launch_nl_count(buf, lo, hi, P<uint32_t>(c->idx_counts), c->stream));
+    HIPCHK(c, vcfxg::launch_idx_count(buf, lo, hi, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_pos), overflow,
+                                      c->stream));
     prof_end(c, "line_count");
     HIPCHK(c, hipMemsetAsync(P<uint32_t>(c->idx_counts) + nc, 0, sizeof(uint32_t), c->stream));
     r = exclusive_scan(c, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_offs), (size_t)nc + 1);
     if (r) return r;
-    uint64_t total = 0;
+    static thread_local uint64_t total;
+    static thread_local unsigned ovf;
     HIPCHK(c, hipMemcpyAsync(&total, P<uint64_t>(c->idx_offs) + nc, sizeof total, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&ovf, overflow, sizeof ovf, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const bool tail = hi > lo && c->last_byte != '\n';
     const uint64_t nl = total + (tail ? 1 : 0);
     r = ensure(c, c->line_end, sizeof(uint64_t) * (size_t)(nl + 1));
     if (r) return r;
-    prof_begin(c, "line_emit");
-    HIPCHK(c, vcfxg::launch_nl_emit(buf, lo, hi, P<uint64_t>(c->idx_offs), P<uint64_t>(c->line_end), total,
-                                    c->stream));
-    prof_end(c, "line_emit");
+    if (ovf) {  // some chunk has more newlines than the scratch holds: the emit sweep
+        prof_begin(c, "line_emit");
+        HIPCHK(c, vcfxg::launch_idx_emit(buf, lo, hi, P<uint64_t>(c->idx_offs), P<uint64_t>(c->line_end), c->stream));
+        prof_end(c, "line_emit");
+    } else {
+        prof_begin(c, "line_compact");
+        HIPCHK(c, vcfxg::launch_nl_compact(lo, hi, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_offs),
+                                           P<uint64_t>(c->idx_pos), P<uint64_t>(c->line_end), c->stream));
+        prof_end(c, "line_compact");
+    }
     static thread_local uint64_t tail_end, nl_host;
     tail_end = (uint64_t)hi;
     nl_host = nl;
@@ -330,10 +344,42 @@ int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_su
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
-    const uint64_t nc = c->af_fused ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
-    if (!nc) {  // the two-pass path (default; also no data lines or data_start == 0)
+    const uint64_t nc = c->af_path ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
+    if (!nc) {  // default (also no data lines, or data_start == 0): index + record kernel
         int r = vcfxg_index(c, data_start, nullptr);
         return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    if (c->af_path == 2) {
+        // line starts counted per 16 KiB chunk (one sweep), scanned, then one sweep
+        // that writes line_end and counts every record while its chunk is L2-resident
+        HIPCHK(c, hipSetDevice(c->device));
+        const char *buf = P<char>(c->input);
+        int r = ensure(c, c->fuse_state, 16 * (nc + 2));
+        if (r) return r;
+        uint64_t *counts = P<uint64_t>(c->fuse_state), *offs = counts + nc + 1;
+        prof_begin(c, "line_count");
+        HIPCHK(c, vcfxg::launch_fuse_count(buf, (int64_t)data_start, (int64_t)c->n, counts, c->stream));
+        prof_end(c, "line_count");
+        HIPCHK(c, hipMemsetAsync(counts + nc, 0, 8, c->stream));
+        r = exclusive_scan(c, counts, offs, (size_t)nc + 1);
+        if (r) return r;
+        static thread_local uint64_t nl;
+        HIPCHK(c, hipMemcpyAsync(&nl, offs + nc, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->d_nlines.p, offs + nc, 8, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        r = af_buffers(c, nl);
+        if (!r) r = ensure(c, c->line_end, 8 * (nl + 1));
+        if (r) return r;
+        HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+        prof_begin(c, "af_chunks");
+        HIPCHK(c, vcfxg::launch_af_chunks(buf, (int64_t)data_start, (int64_t)c->n, offs, mode, P<uint64_t>(c->line_end),
+                                          nl, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                          P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+        prof_end(c, "af_chunks");
+        c->data_start = data_start;
+        c->n_lines = nl;
+        c->indexed = true;
+        return af_rows(c, mode, out);
     }
     HIPCHK(c, hipSetDevice(c->device));
     const char *buf = P<char>(c->input);

@@ -5,18 +5,32 @@
 
 namespace vcfxg {
 
-int64_t idx_nchunks(int64_t lo, int64_t hi);
-hipError_t launch_nl_count(const char *buf, int64_t lo, int64_t hi, uint32_t *counts, hipStream_t s);
-hipError_t launch_nl_emit(const char *buf, int64_t lo, int64_t hi, const uint64_t *offs, uint64_t *line_end,
-                          uint64_t cap, hipStream_t s);
+// single-sweep index over 16 KiB wave-chunks (idx_wchunks of them): counts + the first
+// idx_pos_cap() newline offsets per chunk, then a compaction into line_end (overflow != 0:
+// some chunk needs the emit sweep launch_idx_emit instead)
+int idx_pos_cap();
+int64_t idx_wchunks(int64_t lo, int64_t hi);
+hipError_t launch_idx_count(const char *buf, int64_t lo, int64_t hi, uint32_t *counts, uint64_t *pos,
+                            unsigned *overflow, hipStream_t s);
+hipError_t launch_idx_emit(const char *buf, int64_t lo, int64_t hi, const uint64_t *offs, uint64_t *line_end,
+                           hipStream_t s);
+hipError_t launch_nl_compact(int64_t lo, int64_t hi, const uint32_t *counts, const uint64_t *offs, const uint64_t *pos,
+                             uint64_t *line_end, hipStream_t s);
 hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int mode, int32_t *alt, int32_t *tot, uint32_t *rowpre,
                              uint8_t *status, unsigned long long *counters, hipStream_t s);
 // fused index + AF (one sweep): chunks for data_start / n (0 = use the two-pass path)
 uint64_t af_fused_chunks(int64_t ds, int64_t n);
-hipError_t launch_af_fused(const char *buf, int64_t ds, int64_t n, int mode, unsigned long long *state, uint64_t *line_end, uint64_t *n_lines_dev, uint64_t cap,
+hipError_t launch_af_fused(const char *buf, int64_t ds, int64_t n, int mode, unsigned long long *state,
+                           uint64_t *line_end, uint64_t *n_lines_dev, uint64_t cap,
                            int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
                            unsigned long long *counters, hipStream_t s, int dbg = 0);
+// default region path: per-16 KiB-chunk line-start counts, then (after a scan into offs) the
+// per-wave chunk sweep + record counts
+hipError_t launch_fuse_count(const char *buf, int64_t ds, int64_t n, uint64_t *counts, hipStream_t s);
+hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64_t *offs, int mode,
+                            uint64_t *line_end, uint64_t cap, int32_t *alt, int32_t *tot, uint32_t *rowpre,
+                            uint8_t *status, unsigned long long *counters, hipStream_t s);
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
                              int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,

@@ -1,11 +1,14 @@
 // vcfxg_kernels.hip -- record kernels of the MI355X VCF engine (gfx950).
 //
-// K1 line index  : two HBM sweeps (count, emit) -> line end offsets.
+// K1 line index  : one HBM sweep (per 16 KiB wave-chunk newline counts + offsets) -> scan ->
+//                  compaction into line end offsets (emit sweep only for very short lines).
 // K2 AF records  : one wave per record; fixed-stride "a|b\t" fast path (SWAR on 16 B per
 //                  lane, validated per record) with an exact general per-sample fallback.
 // K5 AF rows     : row length -> exclusive scan -> device-formatted text rows.
 //
 // Reference behaviour restated: VCFX_allele_freq_calc.cpp (citations per function).
+#include <algorithm>
+
 #include "vcfxg_device.h"
 #include "vcfxg_gt.h"
 #include "vcfxg_kernels.h"
@@ -16,66 +19,66 @@ namespace vcfxg {
 // K1: line index
 // =======================================================================================
 constexpr int kIdxThreads = 256;
-constexpr int64_t kIdxChunk = 64 * 1024;  // bytes per block
-constexpr int kIdxTile = kIdxThreads * kBlockBytes;
 
-__global__ __launch_bounds__(kIdxThreads) void k_nl_count(const char *__restrict__ buf, int64_t lo, int64_t hi,
-                                                           int64_t nchunks, uint32_t *__restrict__ counts) {
-    int64_t a0 = lo & ~(int64_t)15;
-    for (int64_t b = blockIdx.x; b < nchunks; b += gridDim.x) {
-        int64_t base = a0 + b * kIdxChunk;
-        uint32_t c = 0;
-#pragma unroll 4
-        for (int t = 0; t < kIdxChunk / kIdxTile; t++) {
-            int64_t blk = base + (int64_t)t * kIdxTile + (int64_t)threadIdx.x * kBlockBytes;
-            if (blk < hi) c += __popc(eq_mask16(load16(buf, blk), kRepNl) & range_mask16(blk, lo, hi));
+// Single-sweep index over 16 KiB wave-chunks: the count pass also keeps the first kPosCap
+// newline offsets of every chunk in a scratch table (wave-level ranks, no block barriers);
+// after the scan a small compaction copies them to line_end, so the emit sweep runs only
+// when some chunk holds more than kPosCap newlines (lines shorter than ~1 KiB on average).
+constexpr int kPosCap = 16;
+constexpr int64_t kWChunk = 16 * 1024;
+
+template <bool kEmit>
+__global__ __launch_bounds__(kIdxThreads) void k_idx_sweep(const char *__restrict__ buf, int64_t lo, int64_t hi,
+                                                            int64_t nchunks, uint32_t *__restrict__ counts,
+                                                            uint64_t *__restrict__ pos,
+                                                            unsigned *__restrict__ overflow,
+                                                            const uint64_t *__restrict__ offs,
+                                                            uint64_t *__restrict__ line_end) {
+    const int64_t a0 = lo & ~(int64_t)15;
+    const int64_t nw = (int64_t)gridDim.x * (kIdxThreads / kWave);
+    for (int64_t c = (int64_t)blockIdx.x * (kIdxThreads / kWave) + threadIdx.x / kWave; c < nchunks; c += nw) {
+        const int64_t base = a0 + c * kWChunk;
+        uint32_t run = 0;
+        uint64_t *slot = kEmit ? line_end + offs[c] : pos + (uint64_t)c * kPosCap;
+        constexpr int kSteps = (int)(kWChunk / kWaveStep), kU = 8;
+        for (int t0 = 0; t0 < kSteps; t0 += kU) {
+            uint4 v[kU];
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const int64_t blk = base + (int64_t)(t0 + u) * kWaveStep + (int64_t)lane() * kBlockBytes;
+                if (blk < hi) v[u] = load16(buf, blk);
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const int64_t blk = base + (int64_t)(t0 + u) * kWaveStep + (int64_t)lane() * kBlockBytes;
+                uint32_t m = blk < hi ? eq_mask16(v[u], kRepNl) & range_mask16(blk, lo, hi) : 0u;
+                const uint64_t any = __ballot(m != 0);
+                if (!any) continue;  // wave-uniform: no newline in this 1 KiB
+                const uint32_t c1 = __popc(m);
+                const uint32_t incl = wave_incl_scan(c1);
+                uint32_t idx = run + incl - c1;
+                while (m) {
+                    const int j = __builtin_ctz(m);
+                    m &= m - 1u;
+                    if (kEmit || idx < (uint32_t)kPosCap) slot[idx] = (uint64_t)(blk + j);
+                    idx++;
+                }
+                run += wave_bcast(incl, kWave - 1);
+            }
         }
-        c = wave_sum(c);
-        __shared__ uint32_t part[kIdxThreads / kWave];
-        if (lane() == 0) part[threadIdx.x / kWave] = c;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t s = 0;
-            for (int w = 0; w < kIdxThreads / kWave; w++) s += part[w];
-            counts[b] = s;
+        if (!kEmit && lane() == 0) {
+            counts[c] = run;
+            if (run > (uint32_t)kPosCap) atomicOr(overflow, 1u);
         }
-        __syncthreads();
     }
 }
 
-__global__ __launch_bounds__(kIdxThreads) void k_nl_emit(const char *__restrict__ buf, int64_t lo, int64_t hi,
-                                                          int64_t nchunks, const uint64_t *__restrict__ offs,
-                                                          uint64_t *__restrict__ line_end, uint64_t cap) {
-    __shared__ uint32_t wtot[kIdxThreads / kWave];
-    int64_t a0 = lo & ~(int64_t)15;
-    for (int64_t b = blockIdx.x; b < nchunks; b += gridDim.x) {
-        int64_t base = a0 + b * kIdxChunk;
-        uint64_t run = offs[b];
-        for (int t = 0; t < kIdxChunk / kIdxTile; t++) {
-            int64_t blk = base + (int64_t)t * kIdxTile + (int64_t)threadIdx.x * kBlockBytes;
-            uint32_t m = 0;
-            if (blk < hi) m = eq_mask16(load16(buf, blk), kRepNl) & range_mask16(blk, lo, hi);
-            uint32_t c = __popc(m);
-            uint32_t incl = wave_incl_scan(c);
-            if (lane() == kWave - 1) wtot[threadIdx.x / kWave] = incl;
-            __syncthreads();
-            uint32_t wbase = 0, btot = 0;
-            for (int w = 0; w < kIdxThreads / kWave; w++) {
-                uint32_t x = wtot[w];
-                if (w < (int)(threadIdx.x / kWave)) wbase += x;
-                btot += x;
-            }
-            uint64_t idx = run + wbase + (incl - c);
-            while (m) {
-                int j = __builtin_ctz(m);
-                m &= m - 1u;
-                if (idx < cap) line_end[idx] = (uint64_t)(blk + j);
-                idx++;
-            }
-            run += btot;
-            __syncthreads();
-        }
-    }
+__global__ void k_nl_compact(int64_t nchunks, const uint32_t *__restrict__ counts, const uint64_t *__restrict__ offs,
+                             const uint64_t *__restrict__ pos, uint64_t *__restrict__ line_end) {
+    const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint64_t b = i / kPosCap, k = i % kPosCap;
+    if ((int64_t)b >= nchunks || k >= counts[b]) return;
+    line_end[offs[b] + k] = pos[i];
 }
 
 // =======================================================================================
@@ -269,6 +272,53 @@ __device__ __forceinline__ int fuse_starts(const char *__restrict__ buf, int64_t
     return marks - ((ce == n && n - 1 >= ds && byte_at(buf, n - 1) == '\n') ? 1 : 0);
 }
 
+// count the records starting after the marks of chunk [cs, ce) (line numbers excl + k):
+// af_line per record, line_end and per-line results written at the global line number
+__device__ void fuse_process(const char *__restrict__ buf, int64_t cs, int64_t ce, int64_t n, int64_t ds, uint64_t excl,
+                             int starts, int marks, int *list, int mode, int64_t *scratch, BlockCounters &bc,
+                             uint64_t *__restrict__ line_end, uint64_t cap, int32_t *__restrict__ alt_o,
+                             int32_t *__restrict__ tot_o, uint32_t *__restrict__ rowpre_o,
+                             uint8_t *__restrict__ status_o) {
+    int64_t nl_after = -1;  // end of the last line starting here when no later mark ends it
+    for (int r_lo = 0; r_lo < starts; r_lo += kFuseCap) {
+        if (r_lo) marks = fuse_sweep(buf, cs, ce, ds, r_lo, list);  // > kFuseCap marks: next batch
+        const int r_hi = r_lo + kFuseCap < starts ? r_lo + kFuseCap : starts;
+        for (int k = r_lo; k < r_hi; k++) {
+            const int64_t ls = cs + list[k - r_lo] + 1;
+            int64_t le;
+            if (k + 1 < marks) le = cs + list[k + 1 - r_lo];
+            else {
+                if (nl_after < 0) {  // first '\n' at or after ce, else n
+                    nl_after = n;
+                    for (int64_t w = ce; w < n; w += kWaveStep) {
+                        const int64_t blk = w + (int64_t)lane() * kBlockBytes;
+                        uint32_t m = blk < n ? eq_mask16(load16(buf, blk), kRepNl) & range_mask16(blk, ce, n) : 0u;
+                        const uint64_t any = __ballot(m != 0);
+                        if (any) {
+                            const int src = __builtin_ctzll(any);
+                            const int64_t p = blk + (m ? __builtin_ctz(m) : 0);
+                            nl_after = __shfl(p, src);
+                            break;
+                        }
+                    }
+                }
+                le = nl_after;
+            }
+            const uint64_t li = excl + (uint64_t)k;
+            uint8_t st;
+            uint32_t alt, tot, rowpre;
+            af_line(buf, ls, le, mode, scratch, bc, st, alt, tot, rowpre);
+            if (lane() == 0 && li < cap) {
+                line_end[li] = (uint64_t)le;
+                status_o[li] = st;
+                alt_o[li] = (int32_t)alt;
+                tot_o[li] = (int32_t)tot;
+                rowpre_o[li] = rowpre;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kWave) void k_af_fused(const char *__restrict__ buf, int64_t ds, int64_t n, int64_t base,
                                                     uint64_t nchunks, int mode, unsigned long long *__restrict__ state,
                                                     uint64_t *__restrict__ line_end, uint64_t *__restrict__ n_lines_o,
@@ -320,47 +370,49 @@ __global__ __launch_bounds__(kWave) void k_af_fused(const char *__restrict__ buf
         if (lane() == 0) st_publish(&state[c], kStIncl | (excl + (uint64_t)starts));
     }
     if (c == nchunks - 1 && lane() == 0) *n_lines_o = excl + (uint64_t)starts;
-    // end of the last line starting here when no later mark of this chunk ends it
-    int64_t nl_after = -1;
-    for (int r_lo = 0; r_lo < starts; r_lo += kFuseCap) {
-        if (dbg & 1) break;  // diagnostics: index part only
-        if (r_lo) marks = fuse_sweep(buf, cs, ce, ds, r_lo, list);  // > kFuseCap marks: next batch
-        const int r_hi = r_lo + kFuseCap < starts ? r_lo + kFuseCap : starts;
-        for (int k = r_lo; k < r_hi; k++) {
-            const int64_t ls = cs + list[k - r_lo] + 1;
-            int64_t le;
-            if (k + 1 < marks) le = cs + list[k + 1 - r_lo];
-            else {
-                if (nl_after < 0) {  // first '\n' at or after ce, else n
-                    nl_after = n;
-                    for (int64_t w = ce; w < n; w += kWaveStep) {
-                        const int64_t blk = w + (int64_t)lane() * kBlockBytes;
-                        uint32_t m = blk < n ? eq_mask16(load16(buf, blk), kRepNl) & range_mask16(blk, ce, n) : 0u;
-                        const uint64_t any = __ballot(m != 0);
-                        if (any) {
-                            const int src = __builtin_ctzll(any);
-                            const int64_t p = blk + (m ? __builtin_ctz(m) : 0);
-                            nl_after = __shfl(p, src);
-                            break;
-                        }
-                    }
-                }
-                le = nl_after;
-            }
-            const uint64_t li = excl + (uint64_t)k;
-            uint8_t st;
-            uint32_t alt, tot, rowpre;
-            af_line(buf, ls, le, mode, scratch, bc, st, alt, tot, rowpre);
-            if (lane() == 0 && li < cap) {
-                line_end[li] = (uint64_t)le;
-                status_o[li] = st;
-                alt_o[li] = (int32_t)alt;
-                tot_o[li] = (int32_t)tot;
-                rowpre_o[li] = rowpre;
-            }
-        }
-    }
+    if (!(dbg & 1))  // dbg bit 0: index part only (diagnostics)
+        fuse_process(buf, cs, ce, n, ds, excl, starts, marks, list, mode, scratch, bc, line_end, cap, alt_o, tot_o,
+                     rowpre_o, status_o);
     if (lane() < BlockCounters::kNC && cnt[lane()]) atomicAdd(&counters[lane()], (unsigned long long)cnt[lane()]);
+}
+
+// K12b, the default one-pass-after-count path: line starts per 16 KiB chunk were counted by
+// k_fuse_count and scanned (offs), so every wave owns chunks independently (grid-stride, no
+// look-back, no barriers): it sweeps its chunk writing line_end, then counts the records
+// starting there while the chunk is L2-resident.
+__global__ __launch_bounds__(kWave) void k_fuse_count(const char *__restrict__ buf, int64_t ds, int64_t n,
+                                                      int64_t base, uint64_t nchunks, uint64_t *__restrict__ counts) {
+    for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+        const int st = fuse_starts(buf, base, n, ds, c, nullptr, nullptr);
+        if (lane() == 0) counts[c] = (uint64_t)st;
+    }
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_af_chunks(const char *__restrict__ buf, int64_t ds, int64_t n,
+                                                           int64_t base, uint64_t nchunks,
+                                                           const uint64_t *__restrict__ offs, int mode,
+                                                           uint64_t *__restrict__ line_end, uint64_t cap,
+                                                           int32_t *__restrict__ alt_o, int32_t *__restrict__ tot_o,
+                                                           uint32_t *__restrict__ rowpre_o,
+                                                           uint8_t *__restrict__ status_o,
+                                                           unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kRecWaves][16];
+    __shared__ int lists[kRecWaves][kFuseCap + 1];
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
+    const int w = threadIdx.x / kWave;
+    const uint64_t wid = (uint64_t)blockIdx.x * kRecWaves + w, nw = (uint64_t)gridDim.x * kRecWaves;
+    for (uint64_t c = wid; c < nchunks; c += nw) {
+        const int64_t cs = base + (int64_t)c * kFuseChunk;
+        const int64_t ce = cs + kFuseChunk < n ? cs + kFuseChunk : n;
+        int marks = 0;
+        const int starts = fuse_starts(buf, base, n, ds, c, lists[w], &marks);
+        fuse_process(buf, cs, ce, n, ds, offs[c], starts, marks, lists[w], mode, scratch[w], bc, line_end, cap, alt_o,
+                     tot_o, rowpre_o, status_o);
+    }
+    flush_counters(cnt, counters);
 }
 
 // genotype_query per line: status 1 keep, 2 drop, 3 "<9 fields" warning, 4 header, 0 empty.
@@ -492,28 +544,40 @@ __global__ void k_af_format(const char *__restrict__ buf, int64_t data_start, co
 // =======================================================================================
 // launchers
 // =======================================================================================
-int64_t idx_nchunks(int64_t lo, int64_t hi) {
-    int64_t a0 = lo & ~(int64_t)15;
-    return hi > lo ? (hi - a0 + kIdxChunk - 1) / kIdxChunk : 0;
-}
 static unsigned grid_for(int64_t n, int64_t per, unsigned cap) {
     int64_t g = (n + per - 1) / per;
     if (g < 1) g = 1;
     return (unsigned)(g > cap ? cap : g);
 }
 
-hipError_t launch_nl_count(const char *buf, int64_t lo, int64_t hi, uint32_t *counts, hipStream_t s) {
-    int64_t nc = idx_nchunks(lo, hi);
+int idx_pos_cap() { return kPosCap; }
+int64_t idx_wchunks(int64_t lo, int64_t hi) {
+    const int64_t a0 = lo & ~(int64_t)15;
+    return hi > lo ? (hi - a0 + kWChunk - 1) / kWChunk : 0;
+}
+hipError_t launch_idx_count(const char *buf, int64_t lo, int64_t hi, uint32_t *counts, uint64_t *pos,
+                            unsigned *overflow, hipStream_t s) {
+    const int64_t nc = idx_wchunks(lo, hi);
     if (!nc) return hipSuccess;
-    hipLaunchKernelGGL(k_nl_count, dim3(grid_for(nc, 1, 1u << 20)), dim3(kIdxThreads), 0, s, buf, lo, hi, nc, counts);
+    hipLaunchKernelGGL(k_idx_sweep<false>, dim3(grid_for(nc, kIdxThreads / kWave, 1u << 20)), dim3(kIdxThreads), 0,
+                       s, buf, lo, hi, nc, counts, pos, overflow, nullptr, nullptr);
     return hipGetLastError();
 }
-hipError_t launch_nl_emit(const char *buf, int64_t lo, int64_t hi, const uint64_t *offs, uint64_t *line_end,
-                          uint64_t cap, hipStream_t s) {
-    int64_t nc = idx_nchunks(lo, hi);
+hipError_t launch_idx_emit(const char *buf, int64_t lo, int64_t hi, const uint64_t *offs, uint64_t *line_end,
+                           hipStream_t s) {
+    const int64_t nc = idx_wchunks(lo, hi);
     if (!nc) return hipSuccess;
-    hipLaunchKernelGGL(k_nl_emit, dim3(grid_for(nc, 1, 1u << 20)), dim3(kIdxThreads), 0, s, buf, lo, hi, nc, offs,
-                       line_end, cap);
+    hipLaunchKernelGGL(k_idx_sweep<true>, dim3(grid_for(nc, kIdxThreads / kWave, 1u << 20)), dim3(kIdxThreads), 0,
+                       s, buf, lo, hi, nc, nullptr, nullptr, nullptr, offs, line_end);
+    return hipGetLastError();
+}
+hipError_t launch_nl_compact(int64_t lo, int64_t hi, const uint32_t *counts, const uint64_t *offs, const uint64_t *pos,
+                             uint64_t *line_end, hipStream_t s) {
+    const int64_t nc = idx_wchunks(lo, hi);
+    if (!nc) return hipSuccess;
+    const uint64_t n = (uint64_t)nc * kPosCap;
+    hipLaunchKernelGGL(k_nl_compact, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nc, counts, offs, pos,
+                       line_end);
     return hipGetLastError();
 }
 hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
@@ -538,6 +602,25 @@ hipError_t launch_af_fused(const char *buf, int64_t ds, int64_t n, int mode, uns
     const int64_t base = (ds - 1) & ~(int64_t)15;
     hipLaunchKernelGGL(k_af_fused, dim3((unsigned)nc), dim3(kWave), 0, s, buf, ds, n, base, nc, mode, state,
                        line_end, n_lines_dev, cap, alt, tot, rowpre, status, counters, dbg);
+    return hipGetLastError();
+}
+hipError_t launch_fuse_count(const char *buf, int64_t ds, int64_t n, uint64_t *counts, hipStream_t s) {
+    const uint64_t nc = af_fused_chunks(ds, n);
+    if (!nc) return hipErrorInvalidValue;
+    const int64_t base = (ds - 1) & ~(int64_t)15;
+    hipLaunchKernelGGL(k_fuse_count, dim3((unsigned)std::min<uint64_t>(nc, 65536)), dim3(kWave), 0, s, buf, ds, n,
+                       base, nc, counts);
+    return hipGetLastError();
+}
+hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64_t *offs, int mode,
+                            uint64_t *line_end, uint64_t cap, int32_t *alt, int32_t *tot, uint32_t *rowpre,
+                            uint8_t *status, unsigned long long *counters, hipStream_t s) {
+    const uint64_t nc = af_fused_chunks(ds, n);
+    if (!nc) return hipErrorInvalidValue;
+    const int64_t base = (ds - 1) & ~(int64_t)15;
+    const unsigned grid = (unsigned)std::min<uint64_t>((nc + kRecWaves - 1) / kRecWaves, 4096);
+    hipLaunchKernelGGL(k_af_chunks, dim3(grid), dim3(kRecThreads), 0, s, buf, ds, n, base, nc, offs, mode, line_end,
+                       cap, alt, tot, rowpre, status, counters);
     return hipGetLastError();
 }
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
