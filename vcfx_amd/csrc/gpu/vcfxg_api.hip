@@ -48,6 +48,7 @@ struct vcfxg_ctx {
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
         ld_off, ld_pairs, ld_fast, ld_gflag;
     DevBuf fuse_state;          // fused AF: per-chunk look-back words
+    DevBuf af_meta;             // AF head pass output (k_af_meta)
     uint64_t af_line_cap = 0;   // fused AF: line capacity the last run needed
     // region AF path: 0 = single-sweep index + k_af_records (default, fastest measured),
     // 1 = one-sweep look-back kernel (k_af_fused), 2 = chunk count + chunk sweep
@@ -185,7 +186,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->fuse_state})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->fuse_state, &c->af_meta})
         if (b->p) (void)hipFree(b->p);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
@@ -332,10 +333,12 @@ int vcfxg_allele_freq(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
     const char *buf = P<char>(c->input);
     const uint64_t *nl_dev = P<uint64_t>(c->d_nlines);
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (L + 1));
+    if (r) return r;
     prof_begin(c, "af_records");
-    HIPCHK(c, vcfxg::launch_af_records(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), nl_dev, L, mode,
-                                       P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    HIPCHK(c, vcfxg::launch_af_meta_sweep(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), nl_dev, L, mode,
+                                          c->af_meta.p, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                          P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
     prof_end(c, "af_records");
     return af_rows(c, mode, out);
 }

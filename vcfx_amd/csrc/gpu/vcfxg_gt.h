@@ -37,10 +37,11 @@ __device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_
 
 // returns false (uniformly) if the record is not fixed-stride
 template <class Op>
-__device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &op) {
+__device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &op, uint32_t sep_hint = 0) {
     int64_t L = E - S;
     if (L < 3 || ((L + 1) & 3)) return false;
-    uint32_t sepc = byte_at(buf, S + 1);
+    // sep_hint: the byte at S + 1 when the caller already has it (saves a dependent load)
+    uint32_t sepc = sep_hint ? sep_hint : byte_at(buf, S + 1);
     if (sepc != '/' && sepc != '|') return false;
     const uint32_t exp_xor = 0x09000000u | (sepc << 8) | 0x00300030u;
     const uint32_t neutral = 0x092E002Eu | (sepc << 8);  // ". ." + tab: valid, reduces to nothing

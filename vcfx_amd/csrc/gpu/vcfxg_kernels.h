@@ -19,6 +19,12 @@ hipError_t launch_nl_compact(int64_t lo, int64_t hi, const uint32_t *counts, con
 hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int mode, int32_t *alt, int32_t *tot, uint32_t *rowpre,
                              uint8_t *status, unsigned long long *counters, hipStream_t s);
+// AF head pass (k_af_meta, meta = af_meta_bytes() per line) + sample sweep (k_af_sweep)
+size_t af_meta_bytes();
+hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint64_t *line_end,
+                                const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, void *meta, int32_t *alt,
+                                int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
+                                hipStream_t s);
 // fused index + AF (one sweep): chunks for data_start / n (0 = use the two-pass path)
 uint64_t af_fused_chunks(int64_t ds, int64_t n);
 hipError_t launch_af_fused(const char *buf, int64_t ds, int64_t n, int mode, unsigned long long *state,

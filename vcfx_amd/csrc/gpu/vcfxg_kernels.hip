@@ -206,6 +206,186 @@ __global__ __launch_bounds__(kRecThreads) void k_af_records(const char *__restri
 }
 
 // =======================================================================================
+// K2a/K2b: AF as a head pass + a sweep pass.  k_af_meta (one lane per line) parses each
+// line's head out of its first 160 bytes: blank / '#' lines are settled, lines whose FORMAT
+// starts with the GT sub-field (gi == 0, the reference's findGTIndex) get their sample
+// region start S, the separator byte and the row prefix; anything else is left to the full
+// per-line path.  k_af_sweep (one wave per line) then runs only the sample sweep for those
+// lines, so a record's serial chain is one small metadata load + the sweep itself.
+// =======================================================================================
+constexpr uint8_t kAfPending = 0xFF;  // status of a kind-1 line whose fast sweep failed
+
+struct AfMeta {
+    uint64_t S;       // sample region start (kind 1)
+    uint32_t rowpre;  // bytes of "CHROM\tPOS\tID\tREF\tALT\t" (kind 1)
+    uint8_t kind;     // 0: no row, nothing counted; 1: GT-first data line; 2: full af_line
+    uint8_t sep;      // byte at S + 1 (kind 1)
+    uint8_t cr;       // mode 0 and the line ends in '\r' (stripped, processMmap :362-364)
+    uint8_t pad;
+};
+
+__global__ __launch_bounds__(256) void k_af_meta(const char *__restrict__ buf, int64_t data_start,
+                                                 const uint64_t *__restrict__ line_end, uint64_t n_lines, int mode,
+                                                 AfMeta *__restrict__ meta) {
+    const uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (li >= n_lines) return;
+    const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
+    const int64_t le = (int64_t)line_end[li];
+    AfMeta m{};
+    m.kind = 2;
+    if (le <= ls) {
+        m.kind = 0;
+        meta[li] = m;
+        return;
+    }
+    const int64_t a = ls & ~(int64_t)15;
+    constexpr int kB = 10;  // 160 bytes of head
+    uint4 v[kB];
+#pragma unroll
+    for (int b = 0; b < kB; b++) v[b] = load16(buf, a + 16 * b);
+    const uint32_t last = byte_at(buf, le - 1);
+    int64_t ae = le;
+    if (mode == 0 && last == '\r') {
+        ae--;
+        m.cr = 1;
+    }
+    const uint32_t first = byte_at(buf, ls);
+    if (ae <= ls || first == '#') {
+        m.kind = 0;
+        meta[li] = m;
+        return;
+    }
+    int nt = 0;
+    int64_t t4 = 0, t7 = 0, t8 = 0;
+#pragma unroll
+    for (int b = 0; b < kB; b++) {
+        uint32_t mk = eq_mask16(v[b], kRepTab) & range_mask16(a + 16 * b, ls, ae);
+        while (mk && nt < 9) {
+            const int j = __builtin_ctz(mk);
+            mk &= mk - 1u;
+            const int64_t p = a + 16 * b + j;
+            nt++;
+            if (nt == 5) t4 = p;
+            if (nt == 8) t7 = p;
+            if (nt == 9) t8 = p;
+        }
+    }
+    if (nt == 9 && t8 - t7 >= 3 && byte_at(buf, t7 + 1) == 'G' && byte_at(buf, t7 + 2) == 'T' &&
+        (t8 - t7 == 3 || byte_at(buf, t7 + 3) == ':')) {
+        m.kind = 1;
+        m.S = (uint64_t)(t8 + 1);
+        m.rowpre = (uint32_t)(t4 - ls + 1);
+        m.sep = t8 + 2 < ae ? (uint8_t)byte_at(buf, t8 + 2) : 0;
+    }
+    meta[li] = m;
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_af_sweep(const char *__restrict__ buf, int64_t data_start,
+                                                          const uint64_t *__restrict__ line_end,
+                                                          const uint64_t *n_lines_p, int mode,
+                                                          const AfMeta *__restrict__ meta,
+                                                          int32_t *__restrict__ alt_o, int32_t *__restrict__ tot_o,
+                                                          uint32_t *__restrict__ rowpre_o,
+                                                          uint8_t *__restrict__ status_o,
+                                                          unsigned long long *__restrict__ counters) {
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t li = wid; li < n_lines; li += nw) {
+        const AfMeta m = meta[li];
+        uint8_t st = 0;
+        uint32_t alt = 0, tot = 0, rowpre = 0;
+        if (m.kind == 1) {
+            const int64_t le = (int64_t)line_end[li], ae = le - m.cr;
+            bc.add(1, 1);
+            bc.add(0, 1);
+            AfOp op{buf, ae, 0};
+            if (gt_fast(buf, (int64_t)m.S, ae, op, m.sep)) {
+                alt = op.alt;
+                tot = op.tot;
+                st = 1;
+            } else {
+                st = kAfPending;  // not fixed-stride: k_af_complex runs the general sweep
+            }
+            rowpre = m.rowpre;
+        } else if (m.kind == 2) {
+            continue;  // k_af_complex
+        }
+        if (lane() == 0) {
+            status_o[li] = st;
+            alt_o[li] = (int32_t)alt;
+            tot_o[li] = (int32_t)tot;
+            rowpre_o[li] = rowpre;
+        }
+    }
+    flush_counters(cnt, counters);
+}
+
+// the lines k_af_meta left to the full per-line path (kind 2: FORMAT without a leading GT,
+// heads longer than 160 bytes, fewer than 9 tabs, ...) and the kind-1 lines whose
+// fixed-stride sweep failed (status kAfPending): the exact general per-sample sweep
+__global__ __launch_bounds__(kRecThreads) void k_af_complex(const char *__restrict__ buf, int64_t data_start,
+                                                            const uint64_t *__restrict__ line_end,
+                                                            const uint64_t *n_lines_p, int mode,
+                                                            const AfMeta *__restrict__ meta,
+                                                            int32_t *__restrict__ alt_o, int32_t *__restrict__ tot_o,
+                                                            uint32_t *__restrict__ rowpre_o,
+                                                            uint8_t *__restrict__ status_o,
+                                                            unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kRecWaves][16];
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    // a wave scans 64 lines' kinds per step and works only on the kind-2 ones
+    for (uint64_t l0 = wid * kWave; l0 < n_lines; l0 += nw * kWave) {
+        const uint64_t mine = l0 + lane();
+        const bool full = mine < n_lines && meta[mine].kind == 2;
+        const bool pend = mine < n_lines && !full && status_o[mine] == kAfPending;
+        uint64_t todo = __ballot(full || pend);
+        const uint64_t pendm = __ballot(pend);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1ull;
+            const uint64_t li = l0 + k;
+            if ((pendm >> k) & 1ull) {
+                const AfMeta m = meta[li];
+                const int64_t ae = (int64_t)line_end[li] - m.cr;
+                AfOp g{buf, ae, 0};
+                gt_general(buf, (int64_t)m.S, ae, g);
+                bc.add(3, 1);
+                if (lane() == 0) {
+                    status_o[li] = 1;
+                    alt_o[li] = (int32_t)g.alt;
+                    tot_o[li] = (int32_t)g.tot;
+                }
+                continue;
+            }
+            int64_t ls, le;
+            line_bounds(line_end, data_start, li, ls, le);
+            uint8_t st;
+            uint32_t alt, tot, rowpre;
+            af_line(buf, ls, le, mode, lds, bc, st, alt, tot, rowpre);
+            if (lane() == 0) {
+                status_o[li] = st;
+                alt_o[li] = (int32_t)alt;
+                tot_o[li] = (int32_t)tot;
+                rowpre_o[li] = rowpre;
+            }
+        }
+    }
+    flush_counters(cnt, counters);
+}
+
+// =======================================================================================
 // K12: fused index + AF, one HBM sweep.  The data region is cut into 16 KiB chunks, one per
 // one-wave block.  A block sweeps its chunk for line marks (the virtual
 // newline at data_start-1 and every '\n' of [data_start, N)), publishes its count of line
@@ -621,6 +801,22 @@ hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64
     const unsigned grid = (unsigned)std::min<uint64_t>((nc + kRecWaves - 1) / kRecWaves, 4096);
     hipLaunchKernelGGL(k_af_chunks, dim3(grid), dim3(kRecThreads), 0, s, buf, ds, n, base, nc, offs, mode, line_end,
                        cap, alt, tot, rowpre, status, counters);
+    return hipGetLastError();
+}
+size_t af_meta_bytes() { return sizeof(AfMeta); }
+hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint64_t *line_end,
+                                const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, void *meta, int32_t *alt,
+                                int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
+                                hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    hipLaunchKernelGGL(k_af_meta, dim3((unsigned)((n_lines_host + 255) / 256)), dim3(256), 0, s, buf, data_start,
+                       line_end, n_lines_host, mode, static_cast<AfMeta *>(meta));
+    unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
+    hipLaunchKernelGGL(k_af_sweep, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode,
+                       static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
+    unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
+    hipLaunchKernelGGL(k_af_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                       mode, static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
     return hipGetLastError();
 }
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
