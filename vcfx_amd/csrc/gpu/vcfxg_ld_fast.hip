@@ -28,6 +28,9 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int kFB = 128;        // block side (variants)
 constexpr int kBK = 64;         // k-slice bytes per stage
 constexpr int kStage = 2 * kFB * kBK;  // A rows then B rows: 16 KiB
+constexpr int kNBuf = 3;               // staging ring depth
+constexpr int kTileBytes = 4 * 64 * 64 * 4;
+static_assert(kNBuf * kStage <= kTileBytes, "staging ring must fit under the epilogue tiles");
 
 __device__ __forceinline__ void glds16(const int8_t *src, int8_t *lds_base) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
@@ -46,10 +49,12 @@ __global__ __launch_bounds__(256) void k_ld_fast(const int8_t *__restrict__ Gc, 
                                                  const uint32_t *__restrict__ blocks, uint32_t nblocks,
                                                  uint16_t *__restrict__ cnt, const uint64_t *__restrict__ off,
                                                  LdPair *__restrict__ pairs) {
-    // staging (2 x 16 KiB) during the k-loop, then the 4 waves' 64x64 int32 tiles (64 KiB)
-    __shared__ __attribute__((aligned(16))) int8_t lds[4 * 64 * 64 * 4];
-    __shared__ double rvx[kFB];
-    __shared__ int rsx[kFB];
+    // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
+    // ds_reads): 3 staging buffers (3 x 16 KiB) during the k-loop, then the 4 waves' 64x64
+    // int32 tiles (64 KiB) over them; the per-row prefilter terms after that
+    __shared__ __attribute__((aligned(16))) int8_t lds[kTileBytes + kFB * (8 + 4)];
+    double *rvx = reinterpret_cast<double *>(lds + kTileBytes);
+    int *rsx = reinterpret_cast<int *>(lds + kTileBytes + kFB * 8);
     const uint32_t b = xcd_remap(blockIdx.x, nblocks);
     const uint32_t I2 = blocks[2 * b], J2 = blocks[2 * b + 1];
     const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
@@ -99,11 +104,18 @@ __global__ __launch_bounds__(256) void k_ld_fast(const int8_t *__restrict__ Gc, 
 #pragma unroll
         for (int y = 0; y < 2; y++) acc[x][y] = v16i{};
     const int nk = kpad / kBK;
+    // 3-buffer ring, two stages in flight: at step ks a wave waits only for its own loads of
+    // stage ks (counted vmcnt: stage ks+1's 4 glds may stay outstanding), then a raw barrier
+    // (no __syncthreads: its fence would drain every glds) makes all waves' stage-ks bytes
+    // visible and frees buffer (ks+2)%3, last read at step ks-1
     stage(0, 0);
+    if (nk > 1) stage(1, 1);
     for (int ks = 0; ks < nk; ks++) {
-        __syncthreads();  // stage ks landed (vmcnt(0)); every wave is done with buffer (ks+1)&1
-        if (ks + 1 < nk) stage(ks + 1, (ks + 1) & 1);
-        const int8_t *base = lds + (ks & 1) * kStage;
+        if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (ks + 2 < nk) stage(ks + 2, (ks + 2) % kNBuf);
+        const int8_t *base = lds + (ks % kNBuf) * kStage;
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             v4i af[2], bf[2];
