@@ -808,12 +808,23 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     auto gcomp = [&](uint64_t b64) { return gf[b64 / 2] != 0; };
     std::vector<uint32_t> blocks;
     uint64_t nb = 1;
-    for (uint64_t J = j0 / FB; J * FB < j1; J++) {  // fast list first
-        if (!gf[J]) continue;
-        for (uint64_t I = ifirst(2 * J) / 2; I <= J; I++)
-            if (gf[I]) {
-                blocks.push_back((uint32_t)I);
-                blocks.push_back((uint32_t)J);
+    // fast list first, in 8 x 8 super-tiles (8 row blocks J x 8 column blocks I): the
+    // kernel maps contiguous list ranges to one XCD, so the ~64 blocks an XCD runs at once
+    // share 16 operand tiles (~5 MiB) through its L2 instead of streaming 128 distinct ones
+    constexpr uint64_t kSuper = 8;
+    const uint64_t Jb = j0 / FB, Je = (j1 + FB - 1) / FB;
+    for (uint64_t J0 = Jb; J0 < Je; J0 += kSuper) {
+        const uint64_t J1 = std::min(Je, J0 + kSuper);
+        const uint64_t Ilo = ifirst(2 * J0) / 2;
+        for (uint64_t I0 = Ilo; I0 < J1; I0 += kSuper)
+            for (uint64_t J = J0; J < J1; J++) {
+                if (!gf[J]) continue;
+                const uint64_t Imin = std::max(I0, ifirst(2 * J) / 2), Imax = std::min(I0 + kSuper, J + 1);
+                for (uint64_t I = Imin; I < Imax; I++)
+                    if (gf[I]) {
+                        blocks.push_back((uint32_t)I);
+                        blocks.push_back((uint32_t)J);
+                    }
             }
     }
     const uint32_t nfast = (uint32_t)(blocks.size() / 2);

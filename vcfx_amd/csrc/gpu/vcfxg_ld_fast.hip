@@ -28,7 +28,7 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 constexpr int kFB = 128;        // block side (variants)
 constexpr int kBK = 64;         // k-slice bytes per stage
 constexpr int kStage = 2 * kFB * kBK;  // A rows then B rows: 16 KiB
-constexpr int kNBuf = 3;               // staging ring depth
+constexpr int kNBuf = 4;               // staging ring depth (kNBuf - 1 stages in flight)
 constexpr int kTileBytes = 4 * 64 * 64 * 4;
 static_assert(kNBuf * kStage <= kTileBytes, "staging ring must fit under the epilogue tiles");
 
@@ -52,9 +52,10 @@ __global__ __launch_bounds__(256) void k_ld_fast(const int8_t *__restrict__ Gc, 
     // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
     // ds_reads): 3 staging buffers (3 x 16 KiB) during the k-loop, then the 4 waves' 64x64
     // int32 tiles (64 KiB) over them; the per-row prefilter terms after that
-    __shared__ __attribute__((aligned(16))) int8_t lds[kTileBytes + kFB * (8 + 4)];
+    __shared__ __attribute__((aligned(16))) int8_t lds[kTileBytes + kFB * (8 + 4 + 4)];
     double *rvx = reinterpret_cast<double *>(lds + kTileBytes);
     int *rsx = reinterpret_cast<int *>(lds + kTileBytes + kFB * 8);
+    float *rvxf = reinterpret_cast<float *>(lds + kTileBytes + kFB * 12);
     const uint32_t b = xcd_remap(blockIdx.x, nblocks);
     const uint32_t I2 = blocks[2 * b], J2 = blocks[2 * b + 1];
     const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
@@ -78,6 +79,7 @@ __global__ __launch_bounds__(256) void k_ld_fast(const int8_t *__restrict__ Gc, 
         const int64_t i = ibase + t < M ? ibase + t : M - 1;
         const LdFast f = fv[i];
         rvx[t] = f.vxp;
+        rvxf[t] = (float)f.vxp;
         rsx[t] = f.sx;
     }
     const int kpad = a.kpad;
@@ -104,17 +106,19 @@ __global__ __launch_bounds__(256) void k_ld_fast(const int8_t *__restrict__ Gc, 
 #pragma unroll
         for (int y = 0; y < 2; y++) acc[x][y] = v16i{};
     const int nk = kpad / kBK;
-    // 3-buffer ring, two stages in flight: at step ks a wave waits only for its own loads of
-    // stage ks (counted vmcnt: stage ks+1's 4 glds may stay outstanding), then a raw barrier
-    // (no __syncthreads: its fence would drain every glds) makes all waves' stage-ks bytes
-    // visible and frees buffer (ks+2)%3, last read at step ks-1
-    stage(0, 0);
-    if (nk > 1) stage(1, 1);
+    // kNBuf-buffer ring, kNBuf-1 stages in flight: at step ks a wave waits only for its own
+    // loads of stage ks (counted vmcnt: the later stages' glds may stay outstanding), then a
+    // raw barrier (no __syncthreads: its fence would drain every glds) makes all waves'
+    // stage-ks bytes visible and frees buffer (ks-1)%kNBuf, last read at step ks-1
+    for (int q = 0; q < kNBuf - 1 && q < nk; q++) stage(q, q);
     for (int ks = 0; ks < nk; ks++) {
-        if (ks + 1 < nk) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        // stages ks+1 .. ks+kNBuf-2 (4 glds each) may stay outstanding
+        const int ahead = nk - 1 - ks < kNBuf - 2 ? nk - 1 - ks : kNBuf - 2;
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (ks + 2 < nk) stage(ks + 2, (ks + 2) % kNBuf);
+        if (ks + kNBuf - 1 < nk) stage(ks + kNBuf - 1, (ks + kNBuf - 1) % kNBuf);
         const int8_t *base = lds + (ks % kNBuf) * kStage;
 #pragma unroll
         for (int s = 0; s < 2; s++) {
@@ -157,17 +161,27 @@ __global__ __launch_bounds__(256) void k_ld_fast(const int8_t *__restrict__ Gc, 
         fj = fv[j];
         const uint32_t cj = a.max_dist > 0 ? chrom_id[j] : 0u;
         const double rhs_j = a.all_pass ? 0.0 : a.tm * fj.vxp;
+        // fp32 form of the prefilter while n*Sxy and Sx*Sy fit int32 (n <= 23170): C exact in
+        // int32, C^2 and tm*Vx*Vy within ~1e-6 relative in fp32, so a further 1e-5 relative
+        // slack keeps every pair that can reach the threshold
+        const bool f32 = a.ns <= 23170;
+        const float rhs_jf = (float)(a.tm * (1.0 - 1e-5)) * (float)fj.vxp;
         const int64_t i0 = (int64_t)bI * kLdBlock;
         // rows i in [max(i0, j - window), min(i0 + 64, j))
-        const int64_t lo = j - (int64_t)a.window > i0 ? j - (int64_t)a.window - i0 : 0;
-        const int64_t hi = j - i0 < 64 ? j - i0 : 64;
-        for (int64_t row = lo; row < hi; row++) {
-            const int lr = wi * 64 + (int)row;
+        const int lo = (int)(j - (int64_t)a.window > i0 ? j - (int64_t)a.window - i0 : 0);
+        const int hi = (int)(j - i0 < 64 ? j - i0 : 64);
+        for (int row = lo; row < hi; row++) {
+            const int lr = wi * 64 + row;
             const int sxy = tile[row * 64 + l] - pad;
             if (!a.all_pass) {
-                const int64_t C = n * sxy - (int64_t)rsx[lr] * fj.sx;
-                const double c = (double)C;
-                if (!(c * c >= rvx[lr] * rhs_j)) continue;
+                if (f32) {
+                    const float c = (float)(a.ns * sxy - rsx[lr] * fj.sx);
+                    if (!(c * c >= rvxf[lr] * rhs_jf)) continue;
+                } else {
+                    const int64_t C = n * sxy - (int64_t)rsx[lr] * fj.sx;
+                    const double c = (double)C;
+                    if (!(c * c >= rvx[lr] * rhs_j)) continue;
+                }
             }
             const int64_t i = i0 + row;
             const LdFast fi = fv[i];
