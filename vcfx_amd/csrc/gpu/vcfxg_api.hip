@@ -495,6 +495,7 @@ int vcfxg_genotype_query(vcfxg_ctx *c, const char *query, size_t qlen, int stric
     const uint64_t L = c->n_lines;
     int r = ensure(c, c->status, L + 1);
     if (!r) r = ensure(c, c->query, qlen + 1);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (L + 1));
     if (r) return r;
     int qa = -1, qb = -1;
     if (!strict) gq_parse_query(query, qlen, qa, qb);
@@ -506,7 +507,7 @@ int vcfxg_genotype_query(vcfxg_ctx *c, const char *query, size_t qlen, int stric
     HIPCHK(c, vcfxg::launch_gq_records(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
                                        P<uint64_t>(c->d_nlines), L, strip_cr, P<char>(c->query), (int)qlen, strict,
                                        qa, qb, P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream,
-                                       nullptr));
+                                       nullptr, c->af_meta.p));
     prof_end(c, "gq_records");
     static thread_local uint64_t host_cnt[4];
     HIPCHK(c, hipMemcpyAsync(host_cnt, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
@@ -619,11 +620,13 @@ int vcfxg_filter_query(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and
     c->query_host.assign(query, qlen);
     if (qlen)
         HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), qlen, hipMemcpyHostToDevice, c->stream));
+    r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (c->n_lines + 1));
+    if (r) return r;
     prof_begin(c, "gq_records");
     HIPCHK(c, vcfxg::launch_gq_records(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
                                        P<uint64_t>(c->d_nlines), c->n_lines, 1, P<char>(c->query), (int)qlen, strict,
                                        qa, qb, P<uint8_t>(c->status), P<unsigned long long>(c->counters) + 4,
-                                       c->stream, P<uint8_t>(c->status)));
+                                       c->stream, P<uint8_t>(c->status), c->af_meta.p));
     prof_end(c, "gq_records");
     static thread_local uint64_t host_cnt[8];
     HIPCHK(c, hipMemcpyAsync(host_cnt, c->counters.p, 64, hipMemcpyDeviceToHost, c->stream));

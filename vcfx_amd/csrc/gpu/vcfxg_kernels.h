@@ -40,7 +40,7 @@ hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
                              int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,
-                             hipStream_t s, const uint8_t *gate);
+                             hipStream_t s, const uint8_t *gate, void *meta = nullptr);
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, uint64_t *len, hipStream_t s);
 hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,

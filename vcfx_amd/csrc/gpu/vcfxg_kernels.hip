@@ -215,26 +215,35 @@ __global__ __launch_bounds__(kRecThreads) void k_af_records(const char *__restri
 // =======================================================================================
 constexpr uint8_t kAfPending = 0xFF;  // status of a kind-1 line whose fast sweep failed
 
-struct AfMeta {
-    uint64_t S;       // sample region start (kind 1)
-    uint32_t rowpre;  // bytes of "CHROM\tPOS\tID\tREF\tALT\t" (kind 1)
-    uint8_t kind;     // 0: no row, nothing counted; 1: GT-first data line; 2: full af_line
-    uint8_t sep;      // byte at S + 1 (kind 1)
-    uint8_t cr;       // mode 0 and the line ends in '\r' (stripped, processMmap :362-364)
+enum : uint8_t { kMetaEmpty = 0, kMetaGt = 1, kMetaFull = 2, kMetaHeader = 3, kMetaGated = 4 };
+struct LineMeta {
+    uint64_t S;       // sample region start (kMetaGt)
+    uint32_t rowpre;  // bytes of "CHROM\tPOS\tID\tREF\tALT\t" (kMetaGt)
+    uint8_t kind;     // kMeta*: empty (after the '\r' strip), GT-first data line, full
+                      // per-line path, '#' line, gated out (fused RF|GQ: RF dropped it)
+    uint8_t sep;      // byte at S + 1 (kMetaGt)
+    uint8_t cr;       // a trailing '\r' was stripped
     uint8_t pad;
 };
+typedef LineMeta AfMeta;
 
-__global__ __launch_bounds__(256) void k_af_meta(const char *__restrict__ buf, int64_t data_start,
-                                                 const uint64_t *__restrict__ line_end, uint64_t n_lines, int mode,
-                                                 AfMeta *__restrict__ meta) {
+__global__ __launch_bounds__(256) void k_line_meta(const char *__restrict__ buf, int64_t data_start,
+                                                   const uint64_t *__restrict__ line_end, uint64_t n_lines,
+                                                   int strip_cr, const uint8_t *__restrict__ gate,
+                                                   LineMeta *__restrict__ meta) {
     const uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (li >= n_lines) return;
+    LineMeta m{};
+    if (gate && gate[li] != 1) {
+        m.kind = kMetaGated;
+        meta[li] = m;
+        return;
+    }
     const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
     const int64_t le = (int64_t)line_end[li];
-    AfMeta m{};
-    m.kind = 2;
+    m.kind = kMetaFull;
     if (le <= ls) {
-        m.kind = 0;
+        m.kind = kMetaEmpty;
         meta[li] = m;
         return;
     }
@@ -245,13 +254,13 @@ __global__ __launch_bounds__(256) void k_af_meta(const char *__restrict__ buf, i
     for (int b = 0; b < kB; b++) v[b] = load16(buf, a + 16 * b);
     const uint32_t last = byte_at(buf, le - 1);
     int64_t ae = le;
-    if (mode == 0 && last == '\r') {
+    if (strip_cr && last == '\r') {
         ae--;
         m.cr = 1;
     }
     const uint32_t first = byte_at(buf, ls);
     if (ae <= ls || first == '#') {
-        m.kind = 0;
+        m.kind = ae <= ls ? kMetaEmpty : kMetaHeader;
         meta[li] = m;
         return;
     }
@@ -272,7 +281,7 @@ __global__ __launch_bounds__(256) void k_af_meta(const char *__restrict__ buf, i
     }
     if (nt == 9 && t8 - t7 >= 3 && byte_at(buf, t7 + 1) == 'G' && byte_at(buf, t7 + 2) == 'T' &&
         (t8 - t7 == 3 || byte_at(buf, t7 + 3) == ':')) {
-        m.kind = 1;
+        m.kind = kMetaGt;
         m.S = (uint64_t)(t8 + 1);
         m.rowpre = (uint32_t)(t4 - ls + 1);
         m.sep = t8 + 2 < ae ? (uint8_t)byte_at(buf, t8 + 2) : 0;
@@ -299,7 +308,7 @@ __global__ __launch_bounds__(kRecThreads) void k_af_sweep(const char *__restrict
         const AfMeta m = meta[li];
         uint8_t st = 0;
         uint32_t alt = 0, tot = 0, rowpre = 0;
-        if (m.kind == 1) {
+        if (m.kind == kMetaGt) {
             const int64_t le = (int64_t)line_end[li], ae = le - m.cr;
             bc.add(1, 1);
             bc.add(0, 1);
@@ -312,7 +321,7 @@ __global__ __launch_bounds__(kRecThreads) void k_af_sweep(const char *__restrict
                 st = kAfPending;  // not fixed-stride: k_af_complex runs the general sweep
             }
             rowpre = m.rowpre;
-        } else if (m.kind == 2) {
+        } else if (m.kind == kMetaFull) {
             continue;  // k_af_complex
         }
         if (lane() == 0) {
@@ -348,7 +357,7 @@ __global__ __launch_bounds__(kRecThreads) void k_af_complex(const char *__restri
     // a wave scans 64 lines' kinds per step and works only on the kind-2 ones
     for (uint64_t l0 = wid * kWave; l0 < n_lines; l0 += nw * kWave) {
         const uint64_t mine = l0 + lane();
-        const bool full = mine < n_lines && meta[mine].kind == 2;
+        const bool full = mine < n_lines && meta[mine].kind == kMetaFull;
         const bool pend = mine < n_lines && !full && status_o[mine] == kAfPending;
         uint64_t todo = __ballot(full || pend);
         const uint64_t pendm = __ballot(pend);
@@ -595,6 +604,51 @@ __global__ __launch_bounds__(kRecThreads) void k_af_chunks(const char *__restric
     flush_counters(cnt, counters);
 }
 
+// one genotype_query data line [ls, le) -> status (1 keep, 2 drop, 3 warn, 4 header, 0 empty)
+__device__ __forceinline__ uint8_t gq_line(const char *__restrict__ buf, int64_t ls, int64_t le, int strip_cr,
+                                           const GqQuery &Q, int64_t *lds, BlockCounters &bc) {
+    int64_t ae = le;
+    if (strip_cr && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;
+    uint8_t st = 0;
+    if (ae > ls) {
+        if (byte_at(buf, ls) == '#') st = 4;
+        else {
+            bc.add(1, 1);
+            int64_t t[10];
+            const int nt = head_tabs(buf, ls, ae, 10, t, lds);
+            // skipToField(8) (:223-230): NULL iff fewer than 8 tabs and the walk ends
+            // before the line end
+            const int64_t pn = nt ? t[(nt < 8 ? nt : 8) - 1] + 1 : ls;
+            st = 2;
+            if (nt < 8 && pn < ae) st = 3;
+            else if (nt >= 9) {
+                const int gi = gt_index(buf, t[7] + 1, t[8]);
+                if (gi >= 0) {
+                    const int64_t S = t[8] + 1;
+                    GqOp op{buf, ae, gi, Q};
+                    bool fast = gi == 0 && gt_fast(buf, S, ae, op);
+                    bool hit;
+                    if (fast) hit = op.found;
+                    else {
+                        GqOp g{buf, ae, gi, Q};
+                        gt_general(buf, S, ae, g);
+                        hit = g.found;
+                        bc.add(3, 1);
+                    }
+                    if (hit) st = 1;
+                }
+            }
+            // nt == 8: FORMAT runs to the line end and there is no sample field -> drop
+        }
+    }
+    bc.add(0, st == 1);
+    bc.add(2, st == 3);
+    return st;
+}
+__device__ __forceinline__ uint8_t gq_gated(uint8_t st, const uint8_t *gate) {
+    return gate ? (st == 1 ? 1 : (st == 3 ? 7 : 6)) : st;  // kept-by-filter: match / warn / no match
+}
+
 // genotype_query per line: status 1 keep, 2 drop, 3 "<9 fields" warning, 4 header, 0 empty.
 // genotypeQueryMmap :450-516 / genotypeQueryStream :546-607 per data line; strip_cr = the
 // line as VCFX_record_filter emitted it (fused RF|GQ pipeline).
@@ -618,44 +672,96 @@ __global__ __launch_bounds__(kRecThreads) void k_gq_records(const char *__restri
         if (gate && uniform32(gate[li]) != 1) continue;
         int64_t ls, le;
         line_bounds(line_end, data_start, li, ls, le);
-        int64_t ae = le;
-        if (strip_cr && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;
-        uint8_t st = 0;
-        if (ae > ls) {
-            if (byte_at(buf, ls) == '#') st = 4;
-            else {
-                bc.add(1, 1);
-                int64_t t[10];
-                const int nt = head_tabs(buf, ls, ae, 10, t, lds);
-                // skipToField(8) (:223-230): NULL iff fewer than 8 tabs and the walk ends
-                // before the line end
-                const int64_t pn = nt ? t[(nt < 8 ? nt : 8) - 1] + 1 : ls;
-                st = 2;
-                if (nt < 8 && pn < ae) st = 3;
-                else if (nt >= 9) {
-                    const int gi = gt_index(buf, t[7] + 1, t[8]);
-                    if (gi >= 0) {
-                        const int64_t S = t[8] + 1;
-                        GqOp op{buf, ae, gi, Q};
-                        bool fast = gi == 0 && gt_fast(buf, S, ae, op);
-                        bool hit;
-                        if (fast) hit = op.found;
-                        else {
-                            GqOp g{buf, ae, gi, Q};
-                            gt_general(buf, S, ae, g);
-                            hit = g.found;
-                            bc.add(3, 1);
-                        }
-                        if (hit) st = 1;
-                    }
-                }
-                // nt == 8: FORMAT runs to the line end and there is no sample field -> drop
+        const uint8_t st = gq_gated(gq_line(buf, ls, le, strip_cr, Q, lds, bc), gate);
+        if (lane() == 0) status_o[li] = st;
+    }
+    flush_counters(cnt, counters);
+}
+
+// genotype_query as head pass (k_line_meta) + sweep: GT-first lines run only the sample
+// sweep (gt_fast with the GqOp early exit); full-path lines and fast-sweep failures go to
+// k_gq_complex (status kGqPending marks the latter)
+constexpr uint8_t kGqPending = 0xFE;
+
+__global__ __launch_bounds__(kRecThreads) void k_gq_sweep(const char *__restrict__ buf,
+                                                          const uint64_t *__restrict__ line_end,
+                                                          const uint64_t *n_lines_p, GqQuery Q,
+                                                          const LineMeta *__restrict__ meta,
+                                                          uint8_t *__restrict__ status_o,
+                                                          unsigned long long *__restrict__ counters,
+                                                          const uint8_t *gate) {
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t li = wid; li < n_lines; li += nw) {
+        const LineMeta m = meta[li];
+        uint8_t st;
+        if (m.kind == kMetaGated || m.kind == kMetaFull) continue;
+        if (m.kind == kMetaEmpty) st = 0;
+        else if (m.kind == kMetaHeader) st = 4;
+        else {
+            const int64_t ae = (int64_t)line_end[li] - m.cr;
+            bc.add(1, 1);
+            GqOp op{buf, ae, 0, Q};
+            if (gt_fast(buf, (int64_t)m.S, ae, op, m.sep)) {
+                st = op.found ? 1 : 2;
+                bc.add(0, st == 1);
+            } else {
+                if (lane() == 0) status_o[li] = kGqPending;
+                continue;
             }
         }
-        bc.add(0, st == 1);
-        bc.add(2, st == 3);
-        if (gate) st = st == 1 ? 1 : (st == 3 ? 7 : 6);  // kept-by-filter: match / warn / no match
-        if (lane() == 0) status_o[li] = st;
+        if (lane() == 0) status_o[li] = gq_gated(st, gate);
+    }
+    flush_counters(cnt, counters);
+}
+
+__global__ __launch_bounds__(kRecThreads) void k_gq_complex(const char *__restrict__ buf, int64_t data_start,
+                                                            const uint64_t *__restrict__ line_end,
+                                                            const uint64_t *n_lines_p, int strip_cr, GqQuery Q,
+                                                            const LineMeta *__restrict__ meta,
+                                                            uint8_t *__restrict__ status_o,
+                                                            unsigned long long *__restrict__ counters,
+                                                            const uint8_t *gate) {
+    __shared__ int64_t scratch[kRecWaves][16];
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t l0 = wid * kWave; l0 < n_lines; l0 += nw * kWave) {
+        const uint64_t mine = l0 + lane();
+        const bool full = mine < n_lines && meta[mine].kind == kMetaFull;
+        const bool pend = mine < n_lines && !full && meta[mine].kind == kMetaGt && status_o[mine] == kGqPending;
+        uint64_t todo = __ballot(full || pend);
+        const uint64_t pendm = __ballot(pend);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1ull;
+            const uint64_t li = l0 + k;
+            uint8_t st;
+            if ((pendm >> k) & 1ull) {
+                const LineMeta m = meta[li];
+                const int64_t ae = (int64_t)line_end[li] - m.cr;
+                GqOp g{buf, ae, 0, Q};
+                gt_general(buf, (int64_t)m.S, ae, g);
+                bc.add(3, 1);
+                st = g.found ? 1 : 2;
+                bc.add(0, st == 1);
+            } else {
+                int64_t ls, le;
+                line_bounds(line_end, data_start, li, ls, le);
+                st = gq_line(buf, ls, le, strip_cr, Q, lds, bc);
+            }
+            if (lane() == 0) status_o[li] = gq_gated(st, gate);
+        }
     }
     flush_counters(cnt, counters);
 }
@@ -809,8 +915,8 @@ hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint6
                                 int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
                                 hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
-    hipLaunchKernelGGL(k_af_meta, dim3((unsigned)((n_lines_host + 255) / 256)), dim3(256), 0, s, buf, data_start,
-                       line_end, n_lines_host, mode, static_cast<AfMeta *>(meta));
+    hipLaunchKernelGGL(k_line_meta, dim3((unsigned)((n_lines_host + 255) / 256)), dim3(256), 0, s, buf, data_start,
+                       line_end, n_lines_host, mode == 0 ? 1 : 0, nullptr, static_cast<AfMeta *>(meta));
     unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
     hipLaunchKernelGGL(k_af_sweep, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode,
                        static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
@@ -822,12 +928,23 @@ hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint6
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
                              int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,
-                             hipStream_t s, const uint8_t *gate) {
+                             hipStream_t s, const uint8_t *gate, void *meta) {
     if (!n_lines_host) return hipSuccess;
     GqQuery Q{q_dev, qlen, strict, qa, qb};
     unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
-    hipLaunchKernelGGL(k_gq_records, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
-                       strip_cr, Q, status, counters, gate);
+    if (!meta) {
+        hipLaunchKernelGGL(k_gq_records, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                           strip_cr, Q, status, counters, gate);
+        return hipGetLastError();
+    }
+    LineMeta *lm = static_cast<LineMeta *>(meta);
+    hipLaunchKernelGGL(k_line_meta, dim3((unsigned)((n_lines_host + 255) / 256)), dim3(256), 0, s, buf, data_start,
+                       line_end, n_lines_host, strip_cr, gate, lm);
+    hipLaunchKernelGGL(k_gq_sweep, dim3(grid), dim3(kRecThreads), 0, s, buf, line_end, n_lines_dev, Q, lm, status,
+                       counters, gate);
+    unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
+    hipLaunchKernelGGL(k_gq_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                       strip_cr, Q, lm, status, counters, gate);
     return hipGetLastError();
 }
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,
