@@ -4,10 +4,11 @@
 Workloads (BASELINE.json configs; the default is the headline one):
   af        configs[1] / configs[3]: VCFX_allele_freq_calc -i on a device-resident
             427,409-record x 2,504-sample chr21-like shard per GPU.  A step =
-            vcfxg_allele_freq_region: the line index in one sweep (line_count keeps each 64 KiB
+            vcfxg_allele_freq_region: the line index in one sweep (line_count keeps each 16 KiB
             chunk's newline offsets; line_compact places them), per-record allele counts
-            (af_records) and device formatted output rows (af_rows + af_format); for N > 1
-            ranks also all-reduce the step's global counts over RCCL.
+            (af_records = head pass + fixed-stride sample sweep + rare full-path lines) and
+            device formatted output rows (af_rows + af_format); for N > 1 ranks also all-reduce
+            the step's global counts over RCCL.
   pipeline  configs[2]: VCFX_record_filter --filter "QUAL>=30;FILTER==PASS" |
             VCFX_genotype_query --genotype-query "0|1" fused on the device (index + one
             filter_query pass), same shard.
@@ -164,8 +165,8 @@ def main():
             if red is not None:
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.text_bytes])
             return s
-        kern_names = ("line_count", "line_emit", "line_compact", "af_records", "af_chunks", "af_fused", "af_rows",
-                      "af_format")
+        kern_names = ("af_scan", "line_count", "line_emit", "line_compact", "af_records", "af_chunks", "af_fused",
+                      "af_rows", "af_format")
     elif a.workload == "pipeline":
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
@@ -249,6 +250,7 @@ def main():
             algo = {   # algorithmic bytes per launch
                 "line_count": region_bytes,
                 "line_emit": region_bytes + 8 * L,
+                "af_scan": region_bytes + L * 8,                # one sweep: every byte classified + newline offsets
                 "af_records": region_bytes + L * (8 + 13),      # record bytes + line_end + per-line results
                 "af_fused": region_bytes + L * (8 + 13),        # one sweep: record bytes + line_end + results
                 "af_chunks": region_bytes + L * (8 + 13),       # chunk sweep: record bytes + line_end + results

@@ -98,7 +98,8 @@ int vcfxg_allele_freq(vcfxg_ctx *ctx, int mode, vcfxg_summary *out);
  * context state as the two calls (the context is indexed afterwards).  VCFXG_AF_FUSED in the
  * environment at vcfxg_open selects an alternative device schedule for measurement: 1 = a
  * single sweep numbering 16 KiB chunks by a wait-free decoupled look-back, 2 = a chunk count
- * then a chunk sweep counting records while L2-resident (both slower today). */
+ * then a chunk sweep counting records while L2-resident, 4 = a single sweep accumulating
+ * byte-class counts per line segment (all slower today). */
 int vcfxg_allele_freq_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
 /* ---- K2: genotype query ----------------------------------------------------------------
  * Per line status (vcfxg_line_status): ROW = some sample's GT sub-field matches `query`

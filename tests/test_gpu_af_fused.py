@@ -1,5 +1,6 @@
-"""GPU parity of vcfxg_allele_freq_region -- the default count + chunk-sweep path and the
-experimental one-sweep look-back kernel -- against the two-pass path
+"""GPU parity of vcfxg_allele_freq_region -- every device schedule (default index + head
+pass + sweep, look-back single sweep, chunk sweep, byte-class single sweep) -- against the
+two-pass path
 (vcfxg_index + vcfxg_allele_freq) and the C oracle: every per-line array and the output
 text must be identical, including inputs that put many line starts in one 16 KiB chunk
 (more than the kernel's per-pass mark list), lines that span several chunks, CRLF, empty
@@ -13,12 +14,13 @@ from vcfx_amd import engine, synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["default", "fused", "chunks"])
+@pytest.fixture(scope="module", params=["default", "fused", "chunks", "scan"])
 def eng(request):
-    """every region schedule: index + records (default), look-back single sweep, chunk sweep"""
+    """every region schedule: index + head pass + sweep (default), look-back single sweep,
+    chunk sweep, byte-class single sweep"""
     import os
     old = os.environ.get("VCFXG_AF_FUSED")
-    os.environ["VCFXG_AF_FUSED"] = {"default": "0", "fused": "1", "chunks": "2"}[request.param]  # read at vcfxg_open
+    os.environ["VCFXG_AF_FUSED"] = {"default": "0", "fused": "1", "chunks": "2", "scan": "4"}[request.param]
     try:
         return engine.Engine(0)
     finally:
@@ -66,6 +68,9 @@ SYNTH = [
     (2000, 997, 12, 1, 0.01, 0, 0.2, 0),
     (4000, 3, 13, 0, 0.05, 0, 0.3, 1),     # ~60 B lines: > 256 starts per chunk, CRLF
     (30000, 1, 14, 0, 0.0, 0, 0.0, 0),     # ~45 B lines: several mark passes per chunk
+    (160, 5000, 16, 0, 0.01, 0, 0.1, 0),   # 20 KB lines: segments over 2-3 chunks
+    (120, 9000, 17, 1, 0.0, 0, 0.0, 1),    # 36 KB CRLF lines
+    (900, 2504, 18, 0, 0.0, 1, 0.0, 0),
 ]
 
 

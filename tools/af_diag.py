@@ -24,7 +24,7 @@ for name, fn in (("two-pass", lambda: (e.index(ds), e.allele_freq())), ("fused",
         fn()
     dt = (time.perf_counter() - t0) / 5
     ks = {}
-    for k in ("line_count", "line_emit", "af_records", "af_fused", "af_chunks"):
+    for k in ("line_count", "line_emit", "af_scan", "af_records", "af_fused", "af_chunks"):
         tot, n = e.kernel_stats(k)
         if n:
             ks[k] = round(tot / n, 3)

@@ -49,10 +49,13 @@ struct vcfxg_ctx {
         ld_off, ld_pairs, ld_fast, ld_gflag;
     DevBuf fuse_state;          // fused AF: per-chunk look-back words
     DevBuf af_meta;             // AF head pass output (k_af_meta)
+    DevBuf scan_seg, nl_chunk;  // AF one-sweep path: per-chunk segment counts, newline -> chunk
     uint64_t af_line_cap = 0;   // fused AF: line capacity the last run needed
-    // region AF path: 0 = single-sweep index + k_af_records (default, fastest measured),
-    // 1 = one-sweep look-back kernel (k_af_fused), 2 = chunk count + chunk sweep
-    // (k_af_chunks); the alternatives stay selectable for measurement
+    // region AF schedule: 0 = single-sweep index + head pass + fixed-stride sweep (default,
+    // fastest measured: two HBM sweeps), 1 = one-sweep look-back kernel (k_af_fused),
+    // 2 = chunk count + chunk sweep (k_af_chunks), 4 = one sweep with byte-class segment
+    // counts (k_af_scan); the single-sweep alternatives are correct and tested but slower
+    // today, kept selectable for measurement
     int af_path = getenv("VCFXG_AF_FUSED") ? atoi(getenv("VCFXG_AF_FUSED")) : 0;
     int fuse_dbg = getenv("VCFXG_FUSE_DEBUG") ? atoi(getenv("VCFXG_FUSE_DEBUG")) : 0;  // diagnostics only
     std::vector<uint8_t> ld_gflag_host;  // per 128-variant group: all complete
@@ -186,7 +189,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->fuse_state, &c->af_meta})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk})
         if (b->p) (void)hipFree(b->p);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
@@ -343,12 +346,77 @@ int vcfxg_allele_freq(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
     return af_rows(c, mode, out);
 }
 
+// default region path: ONE sweep of the input (k_af_scan: newline offsets + per-segment
+// byte-class counts), then compaction + per-line combine + the full/general rest
+static int af_region_scan(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
+    const int64_t nc = vcfxg::idx_wchunks(lo, hi);
+    if (!nc) {
+        int r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    const size_t cap = (size_t)vcfxg::af_scan_cap();
+    int r = ensure(c, c->idx_counts, sizeof(uint32_t) * (size_t)(nc + 1));
+    if (!r) r = ensure(c, c->idx_offs, sizeof(uint64_t) * (size_t)(nc + 1));
+    if (!r) r = ensure(c, c->idx_pos, sizeof(uint64_t) * (size_t)nc * cap + 64);
+    if (!r) r = ensure(c, c->scan_seg, vcfxg::af_scan_seg_bytes() * (size_t)nc);
+    if (r) return r;
+    const char *buf = P<char>(c->input);
+    unsigned *overflow = reinterpret_cast<unsigned *>(P<uint64_t>(c->idx_pos) + (size_t)nc * cap);
+    HIPCHK(c, hipMemsetAsync(overflow, 0, 8, c->stream));
+    prof_begin(c, "af_scan");
+    HIPCHK(c, vcfxg::launch_af_scan(buf, lo, hi, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_pos), c->scan_seg.p,
+                                    overflow, c->stream));
+    prof_end(c, "af_scan");
+    HIPCHK(c, hipMemsetAsync(P<uint32_t>(c->idx_counts) + nc, 0, sizeof(uint32_t), c->stream));
+    r = exclusive_scan(c, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_offs), (size_t)nc + 1);
+    if (r) return r;
+    static thread_local uint64_t total, tail_end, nl_host;
+    static thread_local unsigned ovf;
+    HIPCHK(c, hipMemcpyAsync(&total, P<uint64_t>(c->idx_offs) + nc, sizeof total, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&ovf, overflow, sizeof ovf, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ovf) {  // lines shorter than ~1 KiB somewhere: the index + per-line path
+        r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    const bool tail = hi > lo && c->last_byte != '\n';
+    const uint64_t nl = total + (tail ? 1 : 0);
+    r = ensure(c, c->line_end, 8 * (nl + 1));
+    if (!r) r = ensure(c, c->nl_chunk, 4 * (nl + 1));
+    if (!r) r = af_buffers(c, nl);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (nl + 1));
+    if (r) return r;
+    tail_end = (uint64_t)hi;
+    nl_host = nl;
+    if (tail)
+        HIPCHK(c, hipMemcpyAsync(P<uint64_t>(c->line_end) + total, &tail_end, 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_nlines.p, &nl_host, 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    prof_begin(c, "af_records");
+    HIPCHK(c, vcfxg::launch_af_combine(buf, lo, hi, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_offs),
+                                       P<uint64_t>(c->idx_pos), c->scan_seg.p, nl, total, mode,
+                                       P<uint64_t>(c->line_end), P<uint32_t>(c->nl_chunk), c->af_meta.p,
+                                       P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    HIPCHK(c, vcfxg::launch_af_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), nl, mode,
+                                       c->af_meta.p, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "af_records");
+    c->data_start = data_start;
+    c->n_lines = nl;
+    c->indexed = true;
+    return af_rows(c, mode, out);
+}
+
 int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
-    const uint64_t nc = c->af_path ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
-    if (!nc) {  // default (also no data lines, or data_start == 0): index + record kernel
+    if (c->af_path == 4) return af_region_scan(c, data_start, mode, out);
+    const uint64_t nc = (c->af_path == 1 || c->af_path == 2) ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
+    if (!nc) {  // default (also no data lines, or data_start == 0): index + record kernels
         int r = vcfxg_index(c, data_start, nullptr);
         return r ? r : vcfxg_allele_freq(c, mode, out);
     }

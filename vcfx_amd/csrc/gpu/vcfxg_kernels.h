@@ -5,6 +5,19 @@
 
 namespace vcfxg {
 
+// per-line head summary shared by the AF / GQ head passes (k_line_meta, k_af_combine)
+enum : uint8_t { kMetaEmpty = 0, kMetaGt = 1, kMetaFull = 2, kMetaHeader = 3, kMetaGated = 4 };
+struct LineMeta {
+    uint64_t S;       // sample region start (kMetaGt)
+    uint32_t rowpre;  // bytes of "CHROM\tPOS\tID\tREF\tALT\t" (kMetaGt)
+    uint8_t kind;     // kMeta*: empty (after the '\r' strip), GT-first data line, full
+                      // per-line path, '#' line, gated out (fused RF|GQ: RF dropped it)
+    uint8_t sep;      // byte at S + 1 (kMetaGt)
+    uint8_t cr;       // a trailing '\r' was stripped
+    uint8_t pad;
+};
+constexpr uint8_t kAfPending = 0xFF;  // AF status of a kMetaGt line whose fast sweep failed
+
 // single-sweep index over 16 KiB wave-chunks (idx_wchunks of them): counts + the first
 // idx_pos_cap() newline offsets per chunk, then a compaction into line_end (overflow != 0:
 // some chunk needs the emit sweep launch_idx_emit instead)
@@ -25,6 +38,20 @@ hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint6
                                 const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, void *meta, int32_t *alt,
                                 int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
                                 hipStream_t s);
+hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
+                             int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
+                             unsigned long long *counters, hipStream_t s);
+// AF in one sweep (vcfxg_af_scan.hip): per-chunk newline offsets + per-segment byte-class
+// counts, then compaction + per-line combine (+ launch_af_complex for the rest)
+size_t af_scan_seg_bytes();  // per chunk
+int af_scan_cap();           // newline slots per chunk
+hipError_t launch_af_scan(const char *buf, int64_t lo, int64_t hi, uint32_t *counts, uint64_t *pos, void *seg,
+                          unsigned *overflow, hipStream_t s);
+hipError_t launch_af_combine(const char *buf, int64_t lo, int64_t hi, const uint32_t *counts, const uint64_t *offs,
+                             const uint64_t *pos, const void *seg, uint64_t n_lines, uint64_t n_newlines, int mode,
+                             uint64_t *line_end, uint32_t *nl_chunk, void *meta, int32_t *alt, int32_t *tot,
+                             uint32_t *rowpre, uint8_t *status, unsigned long long *counters, hipStream_t s);
 // fused index + AF (one sweep): chunks for data_start / n (0 = use the two-pass path)
 uint64_t af_fused_chunks(int64_t ds, int64_t n);
 hipError_t launch_af_fused(const char *buf, int64_t ds, int64_t n, int mode, unsigned long long *state,

@@ -213,18 +213,7 @@ __global__ __launch_bounds__(kRecThreads) void k_af_records(const char *__restri
 // per-line path.  k_af_sweep (one wave per line) then runs only the sample sweep for those
 // lines, so a record's serial chain is one small metadata load + the sweep itself.
 // =======================================================================================
-constexpr uint8_t kAfPending = 0xFF;  // status of a kind-1 line whose fast sweep failed
 
-enum : uint8_t { kMetaEmpty = 0, kMetaGt = 1, kMetaFull = 2, kMetaHeader = 3, kMetaGated = 4 };
-struct LineMeta {
-    uint64_t S;       // sample region start (kMetaGt)
-    uint32_t rowpre;  // bytes of "CHROM\tPOS\tID\tREF\tALT\t" (kMetaGt)
-    uint8_t kind;     // kMeta*: empty (after the '\r' strip), GT-first data line, full
-                      // per-line path, '#' line, gated out (fused RF|GQ: RF dropped it)
-    uint8_t sep;      // byte at S + 1 (kMetaGt)
-    uint8_t cr;       // a trailing '\r' was stripped
-    uint8_t pad;
-};
 typedef LineMeta AfMeta;
 
 __global__ __launch_bounds__(256) void k_line_meta(const char *__restrict__ buf, int64_t data_start,
@@ -910,6 +899,16 @@ hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64
     return hipGetLastError();
 }
 size_t af_meta_bytes() { return sizeof(AfMeta); }
+hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
+                             int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
+                             unsigned long long *counters, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
+    hipLaunchKernelGGL(k_af_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                       mode, static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
+    return hipGetLastError();
+}
 hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint64_t *line_end,
                                 const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, void *meta, int32_t *alt,
                                 int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
