@@ -15,16 +15,19 @@ import os
 import re
 import sys
 
-# engine profiling names (vcfxg_kernel_stats) -> device kernel symbol
+# engine profiling names (vcfxg_kernel_stats) -> device kernel symbol(s); a name that times
+# several launches (af_records = head pass + sweep + full-path kernel) sums their traffic
 KERNELS = {
-    "line_count": r"vcfxg::k_(nl|fuse)_count\(",
-    "line_emit": r"vcfxg::k_nl_emit\(",
-    "af_records": r"vcfxg::k_af_records\(",
+    "line_count": r"vcfxg::k_idx_sweep<false>\(",
+    "line_emit": r"vcfxg::k_idx_sweep<true>\(",
+    "line_compact": r"vcfxg::k_nl_compact\(",
+    "af_records": r"vcfxg::k_(line_meta|af_sweep|af_complex)\(",
+    "af_scan": r"vcfxg::k_af_scan\(",
     "af_fused": r"vcfxg::k_af_fused\(",
     "af_chunks": r"vcfxg::k_af_chunks\(",
     "af_format": r"vcfxg::k_af_format\(",
     "rf_records": r"vcfxg::k_rf_records\(",
-    "gq_records": r"vcfxg::k_gq_records\(",
+    "gq_records": r"vcfxg::k_(line_meta|gq_sweep|gq_complex)\(",
     "ld_parse": r"vcfxg::k_ld_parse\(",
     "ld_count": r"vcfxg::k_ld_fast<1>\(",
     "ld_emit": r"vcfxg::k_ld_fast<2>\(",
@@ -35,7 +38,9 @@ KERNELS = {
 
 
 def per_kernel(path, counter):
-    acc = {}
+    """mean per timed step: sum over the matching dispatches / number of dispatches of the
+    most frequent matching symbol (one launch of each per step)"""
+    acc, calls = {}, {}
     with open(path, newline="") as f:
         for row in csv.DictReader(f):
             if row.get("Counter_Name") != counter:
@@ -43,8 +48,10 @@ def per_kernel(path, counter):
             name = row["Kernel_Name"]
             for k, pat in KERNELS.items():
                 if re.search(pat, name):
-                    acc.setdefault(k, []).append(float(row["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}
+                    acc[k] = acc.get(k, 0.0) + float(row["Counter_Value"])
+                    sym = name.split("(")[0]
+                    calls.setdefault(k, {})[sym] = calls.setdefault(k, {}).get(sym, 0) + 1
+    return {k: v / max(calls[k].values()) for k, v in acc.items()}
 
 
 def main():
