@@ -75,3 +75,33 @@ def test_ld_r2_values_bitexact(oracle):
     np_, tb = e.ld_stream_chunk(0, m, m, 0.0)
     assert np_ == m * (m - 1) // 2
     e.close()
+
+
+def _knock_out(buf, line_no):
+    """Make one genotype of data line `line_no` missing (its 256-group leaves the fast kernel)."""
+    lines = buf.split(b"\n")
+    data = [k for k, ln in enumerate(lines) if ln and not ln.startswith(b"#")]
+    k = data[line_no]
+    f = lines[k].split(b"\t")
+    f[9] = b".|."
+    lines[k] = b"\t".join(f)
+    return b"\n".join(lines)
+
+
+@pytest.mark.parametrize("knock", [None, 600])
+def test_ld_fast_blocks_across_groups(oracle, knock):
+    """Several 256-variant fast blocks (and, with a knocked-out genotype, a mix of fast and
+    general blocks): window edges inside and across blocks, thresholds that exercise the
+    fp32 candidate prefilter, threshold 0 (every pair a candidate) and the distance cap."""
+    buf = synth.generate(1100, 203, 58, 0, 0.0, 1, 0.0, 0)
+    if knock is not None:
+        buf = _knock_out(buf, knock)
+    with tempfile.NamedTemporaryFile(suffix=".vcf") as f:
+        f.write(buf)
+        f.flush()
+        for a in (["-w", "1100", "-t", "0.5"], ["-w", "300", "-t", "0.2"], ["-w", "257", "-t", "0.9"],
+                  ["-w", "511", "-t", "0.0"], ["-w", "700", "-t", "0.35", "-d", "5000"]):
+            argv = ["VCFX_ld_calculator"] + a + ["-i", f.name]
+            got = tools.run(argv, b"")
+            want = oracle.run(argv, b"")
+            assert got == want, (a, knock, len(got[0]), len(want[0]))

@@ -871,26 +871,31 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
         if (r) return r;
     }
     // block lists.  Count-table columns are 64-blocks: row block J pairs with column blocks
-    // I0(J) = (J*64 - window)/64 .. J.  Pairs of 128-groups that are all complete go to the
-    // 128x128 X.X^T kernel (k_ld_fast); every other 64-block to the general kernel.
+    // I0(J) = (J*64 - window)/64 .. J.  Pairs of 256-groups that are all complete go to the
+    // 256x256 X.X^T kernel (k_ld_fast); every other 64-block to the general kernel.
     const uint64_t FB = vcfxg::kLdFastBlock;
     auto ifirst = [&](uint64_t J) { const uint64_t jr0 = J * BM; return jr0 > window ? (jr0 - window) / BM : 0; };
     const std::vector<uint8_t> &gf = c->ld_gflag_host;
-    auto gcomp = [&](uint64_t b64) { return gf[b64 / 2] != 0; };
+    constexpr uint64_t kSub = vcfxg::kLdFastBlock / BM;  // 64-blocks per fast group
+    auto gcomp = [&](uint64_t b64) { return gf[b64 / kSub] != 0; };
     std::vector<uint32_t> blocks;
     uint64_t nb = 1;
-    // fast list first, in 8 x 8 super-tiles (8 row blocks J x 8 column blocks I): the
-    // kernel maps contiguous list ranges to one XCD, so the ~64 blocks an XCD runs at once
-    // share 16 operand tiles (~5 MiB) through its L2 instead of streaming 128 distinct ones
-    constexpr uint64_t kSuper = 8;
+    // fast list first, in kSuper x kSuper super-tiles (row blocks J x column blocks I): the
+    // kernel maps contiguous list ranges to one XCD, so the blocks an XCD runs at once share
+    // 2*kSuper operand tiles through its L2 instead of streaming distinct ones
+    static const uint64_t kSuper = [] {
+        const char *e = getenv("VCFXG_LD_SUPER");
+        const long v = e ? atol(e) : 0;
+        return (uint64_t)(v > 0 ? v : 4);
+    }();
     const uint64_t Jb = j0 / FB, Je = (j1 + FB - 1) / FB;
     for (uint64_t J0 = Jb; J0 < Je; J0 += kSuper) {
         const uint64_t J1 = std::min(Je, J0 + kSuper);
-        const uint64_t Ilo = ifirst(2 * J0) / 2;
+        const uint64_t Ilo = ifirst(kSub * J0) / kSub;
         for (uint64_t I0 = Ilo; I0 < J1; I0 += kSuper)
             for (uint64_t J = J0; J < J1; J++) {
                 if (!gf[J]) continue;
-                const uint64_t Imin = std::max(I0, ifirst(2 * J) / 2), Imax = std::min(I0 + kSuper, J + 1);
+                const uint64_t Imin = std::max(I0, ifirst(kSub * J) / kSub), Imax = std::min(I0 + kSuper, J + 1);
                 for (uint64_t I = Imin; I < Imax; I++)
                     if (gf[I]) {
                         blocks.push_back((uint32_t)I);

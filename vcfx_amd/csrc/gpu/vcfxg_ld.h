@@ -88,6 +88,6 @@ hipError_t launch_ld_matrix(const int8_t *Gc, const LdVar *vars, uint64_t m, int
 hipError_t launch_mfma_i8_selftest(const int8_t *A, const int8_t *B, int *C, hipStream_t s);
 
 constexpr int kLdBlock = 64;
-constexpr int kLdFastBlock = 128;
+constexpr int kLdFastBlock = 256;
 
 }  // namespace vcfxg

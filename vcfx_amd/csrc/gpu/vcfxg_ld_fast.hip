@@ -1,110 +1,247 @@
-// vcfxg_ld_fast.hip -- LD r^2 for 128x128 variant blocks whose genotypes are complete.
+// vcfxg_ld_fast.hip -- LD r^2 for 256x256 variant blocks whose genotypes are complete.
 //
 // The common case of VCFX_ld_calculator's pair loop (computeLDStreamingMmap :511-648 /
 // computeLDStreaming :864-987 calling computeRsqFast :397-401): with no missing genotype
 // among the ns samples, the pair sums need only S_xy = X.X^T (n = ns and Sx, Sx2 are
 // per-variant), so a block is one int8 GEMM tile:
-//   * operands: 128 rows of I and 128 rows of J, K = kpad bytes, staged in 64-byte k-slices
+//   * operands: 256 rows of I and 256 rows of J, K = kpad bytes, staged in 64-byte k-slices
 //     by global_load_lds (16 B/lane, lane-linear LDS image, XOR-swizzled 16 B slots via the
-//     SOURCE address so the ds_read_b128 fragment reads are bank-conflict free), double
-//     buffered, one barrier per k-slice;
-//   * 4 waves as 2x2, each a 64x64 output = 2x2 v_mfma_i32_32x32x32_i8 accumulators;
-//   * epilogue per pair: an exact integer prefilter (C = n*Sxy - Sx*Sy; r^2 = C^2/(Vx*Vy))
-//     rejects pairs whose exact r^2 is below threshold - delta without any fp64 division;
-//     candidates run the reference's fp64 operation sequence (correctly rounded __d*_rn
-//     ops, per-variant mean / variance / sqrt precomputed with the same ops), so the kept
-//     r^2 and the threshold decision are bit-identical to the reference;
-//   * each wave's 64x64 output is one 64-block of the count table (cnt[row j][column block])
+//     SOURCE address so the ds_read_b128 fragment reads are bank-conflict free) into a
+//     4-buffer ring with three stages in flight (counted vmcnt + raw s_barrier);
+//   * 8 waves as 4 (I) x 2 (J), each a 64x128 output = 2x4 v_mfma_i32_32x32x32_i8
+//     accumulators: per k-step a wave reads 6 fragments for 8 MFMAs, and the block loads
+//     32 KiB per 128 MFMAs (half the operand traffic per MFMA of a 128x128 block);
+//   * epilogue per 64x64 quarter of a wave's output (two per wave): the int32 tile goes to
+//     the wave's own LDS region and each lane walks one column: an exact integer prefilter
+//     (C = n*Sxy - Sx*Sy; r^2 = C^2/(Vx*Vy)) rejects pairs whose exact r^2 is below
+//     threshold - delta; candidates run the reference's fp64 operation sequence (correctly
+//     rounded __d*_rn ops, per-variant mean / variance / sqrt precomputed with the same
+//     ops), so the kept r^2 and the threshold decision are bit-identical to the reference;
+//   * every 64x64 quarter is one 64-block of the count table (cnt[row j][column block])
 //     shared with the general kernel (vcfxg_ld.hip k_ld_block), so pass 1 counts and pass 2
 //     writes pairs in the reference's (j, i) order; pass 2 skips blocks with no pair.
 #include "vcfxg_device.h"
 #include "vcfxg_ld.h"
+
+#include <type_traits>
+
+// VCFXG_LD_EXPT (diagnostic builds only, results invalid): bit 0 skips the epilogue, bit 1
+// the in-loop staging loads, bit 2 the LDS fragment reads
+#ifndef VCFXG_LD_EXPT
+#define VCFXG_LD_EXPT 0
+#endif
 
 namespace vcfxg {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int kFB = 128;        // block side (variants)
-constexpr int kBK = 64;         // k-slice bytes per stage
-constexpr int kStage = 2 * kFB * kBK;  // A rows then B rows: 16 KiB
+constexpr int kFB = kLdFastBlock;      // block side (variants): 256
+constexpr int kBK = 64;                // k-slice bytes per stage
+constexpr int kStage = 2 * kFB * kBK;  // A rows then B rows: 32 KiB
 constexpr int kNBuf = 4;               // staging ring depth (kNBuf - 1 stages in flight)
-constexpr int kTileBytes = 4 * 64 * 64 * 4;
-static_assert(kNBuf * kStage <= kTileBytes, "staging ring must fit under the epilogue tiles");
+constexpr int kWaves = 8;
+constexpr int kRing = kNBuf * kStage;  // 128 KiB
+constexpr int kQuarter = 64 * 64 * 4;  // one wave's 64x64 int32 epilogue tile
+static_assert(kWaves * kQuarter <= kRing, "epilogue tiles must fit in the staging ring");
+constexpr int kGlds = kStage / 1024 / kWaves;  // 1 KiB glds instructions per wave per stage
+static_assert(kGlds == 4, "the k-loop's vmcnt counts assume 4 glds per wave per stage");
 
 __device__ __forceinline__ void glds16(const int8_t *src, int8_t *lds_base) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                      (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
 }
 
-// bijective XCD-aware remap: consecutive list entries (sharing J rows) land on one XCD
+// bijective XCD-aware remap: consecutive list entries (one super-tile) land on one XCD
 __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
     const uint32_t q = n / 8, r = n % 8, x = b % 8, k = b / 8;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
 }
 
-template <int P>
-__global__ __launch_bounds__(256) void k_ld_fast(const int8_t *__restrict__ Gc, const LdFast *__restrict__ fv,
-                                                 const uint32_t *__restrict__ chrom_id, LdWindowArgs a,
-                                                 const uint32_t *__restrict__ blocks, uint32_t nblocks,
-                                                 uint16_t *__restrict__ cnt, const uint64_t *__restrict__ off,
-                                                 LdPair *__restrict__ pairs) {
-    // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
-    // ds_reads): 3 staging buffers (3 x 16 KiB) during the k-loop, then the 4 waves' 64x64
-    // int32 tiles (64 KiB) over them; the per-row prefilter terms after that
-    __shared__ __attribute__((aligned(16))) int8_t lds[kTileBytes + kFB * (8 + 4 + 4)];
-    double *rvx = reinterpret_cast<double *>(lds + kTileBytes);
-    int *rsx = reinterpret_cast<int *>(lds + kTileBytes + kFB * 8);
-    float *rvxf = reinterpret_cast<float *>(lds + kTileBytes + kFB * 12);
-    const uint32_t b = xcd_remap(blockIdx.x, nblocks);
-    const uint32_t I2 = blocks[2 * b], J2 = blocks[2 * b + 1];
-    const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
-    const int wi = w >> 1, wj = w & 1;
+// exact decision for one candidate pair (kept out of line: the rare path)
+__device__ __noinline__ int ld_exact_pass(const LdFast *__restrict__ fv, const uint32_t *__restrict__ chrom_id,
+                                          int max_dist, double threshold, int64_t i, int64_t j, int sxy,
+                                          double dn) {
+    const LdFast fi = fv[i], fj = fv[j];
+    if (max_dist > 0 && chrom_id[i] == chrom_id[j]) {
+        int d = fj.pos - fi.pos;
+        if (d < 0) d = -d;
+        if (d > max_dist) return 0;
+    }
+    return ld_fast_r2(fi, fj, sxy, dn) >= threshold ? 1 : 0;
+}
+
+// Count-pass epilogue straight from the accumulators (no LDS tile): lane (h, r) of a wave
+// holds, for each of its 4 column tiles y, column wj*128 + 32y + r and the 32 rows
+// 32x + 8g + 4h + e of the wave's 64-row block.  Prefilter per pair, branch-free:
+//   C = n*Sxy - Sx*Sy exact in int32 (24-bit multiplies; n <= 23170 keeps |C| <= 4n^2 < 2^31),
+//   candidate iff |C| >= u_i * v_j with u_i = sqrt(tm' Vx_i), v_j = sqrt(Vy_j) in fp32,
+// tm' = tm (1 - 1e-5): |C| >= sqrt(tm Vx Vy) survives the fp32 roundings (< 1e-6 relative),
+// so every pair whose exact r^2 can reach the threshold is a candidate; candidates (rare at
+// useful thresholds) run the exact fp64 r^2 of ld_fast_r2 -- the same decision the LDS-tile
+// epilogue and the general kernel make.  The two lanes of a column (h = 0, 1) sum their
+// counts with one cross-half swap.
+__device__ __forceinline__ void ld_count_regs(const v16i (&acc)[2][4], const LdWindowArgs &a,
+                                              const LdFast *__restrict__ fv, const uint32_t *__restrict__ chrom_id,
+                                              uint16_t *__restrict__ cnt, const float *ru, const int *rsx,
+                                              uint32_t I4, uint32_t J4, int wi, int wj, int h, int r) {
     const int64_t M = (int64_t)a.m;
-    const int64_t ibase = (int64_t)I2 * kFB, jbase = (int64_t)J2 * kFB;
-    // this wave's 64-block of the count table
-    const uint64_t bI = 2ull * I2 + wi, bJ = 2ull * J2 + wj;
-    const uint64_t jrow0 = bJ * kLdBlock;
-    const uint64_t ifirst = jrow0 > a.window ? (jrow0 - a.window) / kLdBlock : 0;
-    const bool slot_ok = bI >= ifirst && bI <= bJ;
-    const uint64_t slot = bI - ifirst;
-    if (P == 2) {  // emit pass: skip blocks without a counted pair
-        const int64_t jj = (int64_t)jrow0 + l;
-        uint32_t c = 0;
-        if (slot_ok && jj < M && jj >= (int64_t)a.j_lo && jj < (int64_t)a.j_hi)
-            c = cnt[(uint64_t)(jj - (int64_t)a.j_lo) * a.nb + slot];
-        if (!__syncthreads_or(c != 0)) return;
+    const int pad = a.kpad - a.ns;
+    const int ns = a.ns;
+    const double dn = (double)a.ns;
+    const uint64_t bI = 4ull * I4 + wi;
+    const int64_t i0 = (int64_t)bI * kLdBlock;
+    int64_t jv[4];
+    int nsx[4], lo[4], span[4], nc[4];
+    float vj[4];
+    bool full = true;
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+        const uint64_t bJ = 4ull * J4 + 2 * wj + (y >> 1);
+        const int64_t j = (int64_t)(bJ * kLdBlock) + 32 * (y & 1) + r;
+        jv[y] = j;
+        const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
+        const LdFast f = fv[jok ? j : 0];
+        nsx[y] = -f.sx;
+        vj[y] = sqrtf((float)f.vxp);
+        // valid rows [lo, hi) of the 64-block: i in [j - window, j)
+        const int64_t l0 = j - (int64_t)a.window - i0;
+        const int64_t h0 = j - i0;
+        const int l = (int)(l0 > 0 ? (l0 < 64 ? l0 : 64) : 0);
+        const int hh = (int)(h0 > 0 ? (h0 < 64 ? h0 : 64) : 0);
+        lo[y] = l;
+        span[y] = jok && hh > l ? hh - l : 0;
+        full = full && span[y] == 64;
+        nc[y] = 0;
+    }
+    const int nKp = -ns * pad;
+    auto body = [&](auto check) {
+#pragma unroll
+        for (int x = 0; x < 2; x++) {
+            int4 rs[4];
+            float4 ux[4];
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int lr = wi * 64 + 32 * x + 8 * g + 4 * h;
+                rs[g] = *reinterpret_cast<const int4 *>(rsx + lr);
+                ux[g] = *reinterpret_cast<const float4 *>(ru + lr);
+            }
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                auto cand = [&](int k) {
+                    const int g = k >> 2, e = k & 3;
+                    const int row = 32 * x + 8 * g + 4 * h + e;
+                    const int rsi = e == 0 ? rs[g].x : e == 1 ? rs[g].y : e == 2 ? rs[g].z : rs[g].w;
+                    const float ui = e == 0 ? ux[g].x : e == 1 ? ux[g].y : e == 2 ? ux[g].z : ux[g].w;
+                    const int C = __mul24(ns, acc[x][y][k]) + (__mul24(rsi, nsx[y]) + nKp);
+                    bool c = a.all_pass || fabsf((float)C) >= ui * vj[y];
+                    if (decltype(check)::value) c = c && (unsigned)(row - lo[y]) < (unsigned)span[y];
+                    return c;
+                };
+                // pass A: candidate test only (lane-mask OR, no branch per pair)
+                bool any = false;
+#pragma unroll
+                for (int k = 0; k < 16; k++) any |= cand(k);
+                // pass B, only for the rare lanes holding a candidate: exact fp64 r^2
+                if (any) {
+#pragma unroll
+                    for (int k = 0; k < 16; k++)
+                        if (cand(k))
+                            nc[y] += ld_exact_pass(fv, chrom_id, a.max_dist, a.threshold, i0 + 32 * x + 8 * (k >> 2) + 4 * h + (k & 3),
+                                                   jv[y], acc[x][y][k] - pad, dn);
+                }
+            }
+        }
+    };
+    if (__all(full)) body(std::integral_constant<bool, false>{});
+    else body(std::integral_constant<bool, true>{});
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+        const int tot = nc[y] + __shfl_xor(nc[y], 32);
+        const uint64_t bJ = 4ull * J4 + 2 * wj + (y >> 1);
+        const uint64_t jrow0 = bJ * kLdBlock;
+        const uint64_t ifirst = jrow0 > a.window ? (jrow0 - a.window) / kLdBlock : 0;
+        const int64_t j = jv[y];
+        const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
+        if (h == 0 && jok && bI >= ifirst && bI <= bJ)
+            cnt[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + (bI - ifirst)] = (uint16_t)tot;
+    }
+}
+
+template <int P>
+__global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__restrict__ Gc,
+                                                            const LdFast *__restrict__ fv,
+                                                            const uint32_t *__restrict__ chrom_id, LdWindowArgs a,
+                                                            const uint32_t *__restrict__ blocks, uint32_t nblocks,
+                                                            uint16_t *__restrict__ cnt,
+                                                            const uint64_t *__restrict__ off,
+                                                            LdPair *__restrict__ pairs) {
+    // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
+    // ds_reads): the staging ring during the k-loop, then the waves' epilogue tiles over it;
+    // the per-row prefilter terms after that
+    __shared__ __attribute__((aligned(16))) int8_t lds[kRing + kFB * (8 + 4 + 4 + 4)];
+    double *rvx = reinterpret_cast<double *>(lds + kRing);
+    int *rsx = reinterpret_cast<int *>(lds + kRing + kFB * 8);
+    float *rvxf = reinterpret_cast<float *>(lds + kRing + kFB * 12);
+    float *ru = reinterpret_cast<float *>(lds + kRing + kFB * 16);  // sqrt(tm' * Vx), register epilogue
+    const uint32_t b = xcd_remap(blockIdx.x, nblocks);
+    const uint32_t I4 = blocks[2 * b], J4 = blocks[2 * b + 1];
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
+    const int wi = w >> 1, wj = w & 1;  // output rows wi*64.., columns wj*128..
+    const int64_t M = (int64_t)a.m;
+    const int64_t ibase = (int64_t)I4 * kFB, jbase = (int64_t)J4 * kFB;
+    // count-table slot of 64-block pair (bI, bJ); false outside the window triangle
+    auto sub = [&](uint64_t bI, uint64_t bJ, uint64_t &slot) {
+        const uint64_t jrow0 = bJ * kLdBlock;
+        const uint64_t ifirst = jrow0 > a.window ? (jrow0 - a.window) / kLdBlock : 0;
+        slot = bI - ifirst;
+        return bI >= ifirst && bI <= bJ;
+    };
+    if (P == 2) {  // emit pass: skip blocks without a counted pair (16 quarters x 64 columns)
+        uint32_t any = 0;
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const int idx = t + e * kWaves * kWave;  // 0..1023
+            const int qi = idx >> 8, qj = (idx >> 6) & 3, col = idx & 63;
+            const uint64_t bI = 4ull * I4 + qi, bJ = 4ull * J4 + qj;
+            uint64_t slot;
+            const int64_t jj = (int64_t)(bJ * kLdBlock) + col;
+            if (sub(bI, bJ, slot) && jj < M && jj >= (int64_t)a.j_lo && jj < (int64_t)a.j_hi)
+                any |= cnt[(uint64_t)(jj - (int64_t)a.j_lo) * a.nb + slot];
+        }
+        if (!__syncthreads_or(any != 0)) return;
     }
     if (t < kFB) {
         const int64_t i = ibase + t < M ? ibase + t : M - 1;
         const LdFast f = fv[i];
         rvx[t] = f.vxp;
         rvxf[t] = (float)f.vxp;
+        ru[t] = sqrtf((float)(a.tm * (1.0 - 1e-5)) * (float)f.vxp);
         rsx[t] = f.sx;
     }
     const int kpad = a.kpad;
-    // staging: 16 wave-instructions of 1 KiB per stage, 4 per wave; instruction q of wave w
-    // fills LDS [(4w+q) KiB, +1 KiB) = 16 rows x 64 B; lane l -> row (l>>2), physical slot
-    // l&3 holding logical 16 B slot (l&3) ^ ((row>>2)&3)
-    const int8_t *src[4];
+    // staging: 32 wave-instructions of 1 KiB per stage, kGlds per wave; instruction q of
+    // wave w fills LDS [(kGlds*w+q) KiB, +1 KiB) = 16 rows x 64 B; lane l -> row (l>>2),
+    // physical slot l&3 holding logical 16 B slot (l&3) ^ ((row>>2)&3)
+    const int8_t *src[kGlds];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int idx = 4 * w + q;
-        const int lrow = (idx & 7) * 16 + (l >> 2);  // row within the A or B tile
-        int64_t g = (idx < 8 ? ibase : jbase) + lrow;
+    for (int q = 0; q < kGlds; q++) {
+        const int idx = kGlds * w + q;                // 0..31: A rows for 0..15, B rows after
+        const int lrow = (idx & 15) * 16 + (l >> 2);  // row within the A or B tile
+        int64_t g = (idx < 16 ? ibase : jbase) + lrow;
         if (g >= M) g = M - 1;
         const int logical = (l & 3) ^ ((lrow >> 2) & 3);
         src[q] = Gc + g * (int64_t)kpad + logical * 16;
     }
     auto stage = [&](int ks, int buf) {
 #pragma unroll
-        for (int q = 0; q < 4; q++) glds16(src[q] + ks * kBK, lds + buf * kStage + (4 * w + q) * 1024);
+        for (int q = 0; q < kGlds; q++) glds16(src[q] + ks * kBK, lds + buf * kStage + (kGlds * w + q) * 1024);
     };
-    v16i acc[2][2];
+    v16i acc[2][4];
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
-        for (int y = 0; y < 2; y++) acc[x][y] = v16i{};
+        for (int y = 0; y < 4; y++) acc[x][y] = v16i{};
     const int nk = kpad / kBK;
     // kNBuf-buffer ring, kNBuf-1 stages in flight: at step ks a wave waits only for its own
     // loads of stage ks (counted vmcnt: the later stages' glds may stay outstanding), then a
@@ -112,103 +249,128 @@ __global__ __launch_bounds__(256) void k_ld_fast(const int8_t *__restrict__ Gc, 
     // stage-ks bytes visible and frees buffer (ks-1)%kNBuf, last read at step ks-1
     for (int q = 0; q < kNBuf - 1 && q < nk; q++) stage(q, q);
     for (int ks = 0; ks < nk; ks++) {
-        // stages ks+1 .. ks+kNBuf-2 (4 glds each) may stay outstanding
-        const int ahead = nk - 1 - ks < kNBuf - 2 ? nk - 1 - ks : kNBuf - 2;
+        const int ahead = nk - 1 - ks < kNBuf - 2 ? nk - 1 - ks : kNBuf - 2;  // stages still loading
         if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (ks + kNBuf - 1 < nk) stage(ks + kNBuf - 1, (ks + kNBuf - 1) % kNBuf);
+        if (!(VCFXG_LD_EXPT & 2) && ks + kNBuf - 1 < nk) stage(ks + kNBuf - 1, (ks + kNBuf - 1) % kNBuf);
         const int8_t *base = lds + (ks % kNBuf) * kStage;
 #pragma unroll
         for (int s = 0; s < 2; s++) {
-            v4i af[2], bf[2];
+            const int lg = 2 * s + h;
+            v4i af[2], bf[4];
 #pragma unroll
             for (int x = 0; x < 2; x++) {
-                const int ra = wi * 64 + x * 32 + r, rb = wj * 64 + x * 32 + r;
-                const int lg = 2 * s + h;
+                const int ra = wi * 64 + x * 32 + r;
+                if (VCFXG_LD_EXPT & 4) { af[x] = v4i{ra, ks, s, x}; continue; }
                 af[x] = *reinterpret_cast<const v4i *>(base + ra * kBK + ((lg ^ ((ra >> 2) & 3)) << 4));
-                bf[x] = *reinterpret_cast<const v4i *>(base + kFB * kBK + rb * kBK + ((lg ^ ((rb >> 2) & 3)) << 4));
+            }
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                const int rb = wj * 128 + y * 32 + r;
+                if (VCFXG_LD_EXPT & 4) { bf[y] = v4i{rb, ks, s, y}; continue; }
+                bf[y] = *reinterpret_cast<const v4i *>(base + kFB * kBK + rb * kBK + ((lg ^ ((rb >> 2) & 3)) << 4));
             }
 #pragma unroll
             for (int x = 0; x < 2; x++)
 #pragma unroll
-                for (int y = 0; y < 2; y++)
+                for (int y = 0; y < 4; y++)
                     acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[x], bf[y], acc[x][y], 0, 0, 0);
         }
     }
-    // ---- epilogue.  The 4 waves' 64x64 int32 tiles go to LDS (over the staging buffers), so
-    // each lane then owns one column j of its wave's 64-block and walks its 64 rows with
-    // runtime indices (low register pressure, a 64-bit pass mask per column, no shuffles).
-    __syncthreads();  // every wave is done reading the staging buffers
-    int *tile = reinterpret_cast<int *>(lds) + w * 64 * 64;
+    if (VCFXG_LD_EXPT & 1) {
+        int z = 0;
 #pragma unroll
-    for (int x = 0; x < 2; x++)
+        for (int x = 0; x < 2; x++)
 #pragma unroll
-        for (int y = 0; y < 2; y++)
+            for (int y = 0; y < 4; y++)
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-                tile[(32 * x + (k & 3) + 8 * (k >> 2) + 4 * h) * 64 + 32 * y + r] = acc[x][y][k];
-    if (!slot_ok) return;  // wave-uniform: a sub-block outside the window triangle
+                for (int k = 0; k < 16; k++) z ^= acc[x][y][k];
+        if (z == 0x7fffffff) cnt[0] = 1;
+        return;
+    }
+    if (P == 1 && a.ns <= 23170) {
+        __syncthreads();  // the row terms written before the k-loop are visible to every wave
+        ld_count_regs(acc, a, fv, chrom_id, cnt, ru, rsx, I4, J4, wi, wj, h, r);
+        return;
+    }
+    __syncthreads();  // every wave is done reading the ring; the epilogue tiles reuse it
+    int *tile = reinterpret_cast<int *>(lds + w * kQuarter);
     const int pad = kpad - a.ns;
     const double dn = (double)a.ns;
     const int64_t n = a.ns;
-    const int64_t j = (int64_t)jrow0 + l;
-    const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
-    uint64_t mask = 0;
-    LdFast fj{};
-    if (jok) {
-        fj = fv[j];
-        const uint32_t cj = a.max_dist > 0 ? chrom_id[j] : 0u;
-        const double rhs_j = a.all_pass ? 0.0 : a.tm * fj.vxp;
-        // fp32 form of the prefilter while n*Sxy and Sx*Sy fit int32 (n <= 23170): C exact in
-        // int32, C^2 and tm*Vx*Vy within ~1e-6 relative in fp32, so a further 1e-5 relative
-        // slack keeps every pair that can reach the threshold
-        const bool f32 = a.ns <= 23170;
-        const float rhs_jf = (float)(a.tm * (1.0 - 1e-5)) * (float)fj.vxp;
-        const int64_t i0 = (int64_t)bI * kLdBlock;
-        // rows i in [max(i0, j - window), min(i0 + 64, j))
-        const int lo = (int)(j - (int64_t)a.window > i0 ? j - (int64_t)a.window - i0 : 0);
-        const int hi = (int)(j - i0 < 64 ? j - i0 : 64);
-        for (int row = lo; row < hi; row++) {
-            const int lr = wi * 64 + row;
-            const int sxy = tile[row * 64 + l] - pad;
-            if (!a.all_pass) {
-                if (f32) {
-                    const float c = (float)(a.ns * sxy - rsx[lr] * fj.sx);
-                    if (!(c * c >= rvxf[lr] * rhs_jf)) continue;
-                } else {
-                    const int64_t C = n * sxy - (int64_t)rsx[lr] * fj.sx;
-                    const double c = (double)C;
-                    if (!(c * c >= rvx[lr] * rhs_j)) continue;
-                }
-            }
-            const int64_t i = i0 + row;
-            const LdFast fi = fv[i];
-            if (a.max_dist > 0 && chrom_id[i] == cj) {
-                int d = fj.pos - fi.pos;
-                if (d < 0) d = -d;
-                if (d > a.max_dist) continue;
-            }
-            if (ld_fast_r2(fi, fj, sxy, dn) >= a.threshold) mask |= 1ull << row;
-        }
-    }
-    if (P == 1) {
-        if (jok) cnt[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot] = (uint16_t)__popcll(mask);
-        return;
-    }
-    if (!mask) return;
-    const uint64_t base = off[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot];
+    // fp32 form of the prefilter while n*Sxy and Sx*Sy fit int32 (n <= 23170): C exact in
+    // int32, C^2 and tm*Vx*Vy within ~1e-6 relative in fp32, so a further 1e-5 relative
+    // slack keeps every pair that can reach the threshold
+    const bool f32 = a.ns <= 23170;
+    const uint64_t bI = 4ull * I4 + wi;
     const int64_t i0 = (int64_t)bI * kLdBlock;
-    uint32_t rank = 0;
-    while (mask) {
-        const int row = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        LdPair pr;
-        pr.i = (uint32_t)(i0 + row);
-        pr.j = (uint32_t)j;
-        pr.r2 = ld_fast_r2(fv[i0 + row], fj, tile[row * 64 + l] - pad, dn);
-        pairs[base + rank++] = pr;
+#pragma unroll
+    for (int hy = 0; hy < 2; hy++) {  // the wave's two 64x64 quarters (columns hy*64..)
+        const uint64_t bJ = 4ull * J4 + 2 * wj + hy;
+        uint64_t slot;
+        if (!sub(bI, bJ, slot)) continue;  // wave-uniform: a quarter outside the window triangle
+        // the quarter's accumulators -> this wave's LDS tile [row][col] (no other wave uses
+        // it, and the wave's own lanes are in lockstep: no barrier between quarters)
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int yy = 0; yy < 2; yy++)
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    tile[(32 * x + (k & 3) + 8 * (k >> 2) + 4 * h) * 64 + 32 * yy + r] = acc[x][2 * hy + yy][k];
+        const int64_t j = (int64_t)(bJ * kLdBlock) + l;
+        const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
+        uint64_t mask = 0;
+        LdFast fj{};
+        if (jok) {
+            fj = fv[j];
+            const uint32_t cj = a.max_dist > 0 ? chrom_id[j] : 0u;
+            const double rhs_j = a.all_pass ? 0.0 : a.tm * fj.vxp;
+            const float rhs_jf = (float)(a.tm * (1.0 - 1e-5)) * (float)fj.vxp;
+            // rows i in [max(i0, j - window), min(i0 + 64, j))
+            const int lo = (int)(j - (int64_t)a.window > i0 ? j - (int64_t)a.window - i0 : 0);
+            const int hi = (int)(j - i0 < 64 ? j - i0 : 64);
+            for (int row = lo; row < hi; row++) {
+                const int lr = wi * 64 + row;
+                const int sxy = tile[row * 64 + l] - pad;
+                if (!a.all_pass) {
+                    if (f32) {
+                        const float c = (float)(a.ns * sxy - rsx[lr] * fj.sx);
+                        if (!(c * c >= rvxf[lr] * rhs_jf)) continue;
+                    } else {
+                        const int64_t C = n * sxy - (int64_t)rsx[lr] * fj.sx;
+                        const double c = (double)C;
+                        if (!(c * c >= rvx[lr] * rhs_j)) continue;
+                    }
+                }
+                const int64_t i = i0 + row;
+                const LdFast fi = fv[i];
+                if (a.max_dist > 0 && chrom_id[i] == cj) {
+                    int d = fj.pos - fi.pos;
+                    if (d < 0) d = -d;
+                    if (d > a.max_dist) continue;
+                }
+                if (ld_fast_r2(fi, fj, sxy, dn) >= a.threshold) mask |= 1ull << row;
+            }
+        }
+        if (P == 1) {
+            if (jok) cnt[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot] = (uint16_t)__popcll(mask);
+            continue;
+        }
+        if (!mask) continue;
+        const uint64_t pbase = off[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot];
+        uint32_t rank = 0;
+        while (mask) {
+            const int row = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            LdPair pr;
+            pr.i = (uint32_t)(i0 + row);
+            pr.j = (uint32_t)j;
+            pr.r2 = ld_fast_r2(fv[i0 + row], fj, tile[row * 64 + l] - pad, dn);
+            pairs[pbase + rank++] = pr;
+        }
     }
 }
 
@@ -218,15 +380,15 @@ hipError_t launch_ld_fast(int pass, const int8_t *Gc, const LdFast *fv, const ui
     if (!nblocks) return hipSuccess;
     if (a.kpad % kBK) return hipErrorInvalidValue;
     if (pass == 1)
-        hipLaunchKernelGGL(k_ld_fast<1>, dim3(nblocks), dim3(256), 0, s, Gc, fv, chrom_id, a, blocks, nblocks, cnt,
-                           off, pairs);
+        hipLaunchKernelGGL(k_ld_fast<1>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gc, fv, chrom_id, a, blocks,
+                           nblocks, cnt, off, pairs);
     else
-        hipLaunchKernelGGL(k_ld_fast<2>, dim3(nblocks), dim3(256), 0, s, Gc, fv, chrom_id, a, blocks, nblocks, cnt,
-                           off, pairs);
+        hipLaunchKernelGGL(k_ld_fast<2>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gc, fv, chrom_id, a, blocks,
+                           nblocks, cnt, off, pairs);
     return hipGetLastError();
 }
 
-// per 128-variant group: 1 if every variant of the group is complete
+// per kLdFastBlock-variant group: 1 if every variant of the group is complete
 __global__ void k_ld_groups(const LdVar *__restrict__ vars, uint64_t m, uint8_t *__restrict__ gflag) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x / 64 + threadIdx.x / 64;
     const uint64_t ng = (m + kFB - 1) / kFB;

@@ -151,14 +151,14 @@ bool run_stream(const Input &in, bool mmap_mode, const LdOpts &o, const std::str
                 if ((long double)cum(mid) < target) lo = mid + 1;
                 else hi = mid;
             }
-            return std::min<uint64_t>(M, (lo + 127) / 128 * 128);
+            return std::min<uint64_t>(M, (lo + 255) / 256 * 256);
         };
         jb = cut(o.shard_rank);
         je = cut(o.shard_rank + 1);
     }
     // chunk rows so that a chunk holds at most ~16M candidate pairs
     uint64_t R = (16ull << 20) / std::max<uint64_t>(W, 1);
-    R = std::max<uint64_t>(128, (R / 128) * 128);  // whole 128-variant fast blocks
+    R = std::max<uint64_t>(256, (R / 256) * 256);  // whole 256-variant fast blocks
     std::string text;
     for (uint64_t j0 = jb; j0 < je; j0 += R) {
         uint64_t np = 0, tb = 0;
