@@ -26,7 +26,8 @@
 #include <type_traits>
 
 // VCFXG_LD_EXPT (diagnostic builds only, results invalid): bit 0 skips the epilogue, bit 1
-// the in-loop staging loads, bit 2 the LDS fragment reads
+// the in-loop staging loads, bit 2 the LDS fragment reads; bit 3 stages k-slice 0 every step,
+// bit 4 reads rows 0..255 for every block
 #ifndef VCFXG_LD_EXPT
 #define VCFXG_LD_EXPT 0
 #endif
@@ -59,7 +60,7 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
 }
 
 // exact decision for one candidate pair (kept out of line: the rare path)
-__device__ __noinline__ int ld_exact_pass(const LdFast *__restrict__ fv, const uint32_t *__restrict__ chrom_id,
+__device__ __forceinline__ int ld_exact_pass(const LdFast *__restrict__ fv, const uint32_t *__restrict__ chrom_id,
                                           int max_dist, double threshold, int64_t i, int64_t j, int sxy,
                                           double dn) {
     const LdFast fi = fv[i], fj = fv[j];
@@ -73,27 +74,34 @@ __device__ __noinline__ int ld_exact_pass(const LdFast *__restrict__ fv, const u
 
 // Count-pass epilogue straight from the accumulators (no LDS tile): lane (h, r) of a wave
 // holds, for each of its 4 column tiles y, column wj*128 + 32y + r and the 32 rows
-// 32x + 8g + 4h + e of the wave's 64-row block.  Prefilter per pair, branch-free:
-//   C = n*Sxy - Sx*Sy exact in int32 (24-bit multiplies; n <= 23170 keeps |C| <= 4n^2 < 2^31),
-//   candidate iff |C| >= u_i * v_j with u_i = sqrt(tm' Vx_i), v_j = sqrt(Vy_j) in fp32,
-// tm' = tm (1 - 1e-5): |C| >= sqrt(tm Vx Vy) survives the fp32 roundings (< 1e-6 relative),
-// so every pair whose exact r^2 can reach the threshold is a candidate; candidates (rare at
+// 32x + 8g + 4h + e of the wave's 64-row block.  Candidate test per pair, branch-free and
+// two pairs per packed fp32 instruction:
+//   c = n*Sxy' + (-(Sx_i*Sy_j) - n*pad)   (Sxy' = accumulator incl. the padding bytes)
+//   candidate iff |c| >= u_i * v_j - E,   u_i = sqrt(tm' Vx_i), v_j = sqrt(Vy_j)
+// Every operand is an integer below 2^24 (exact in fp32) and each fma rounds once, so
+// |c - C| <= (8n^2 + 2e6) 2^-24 < E = (8n^2 + 4e6) 2^-23 for the exact C = n*Sxy - Sx*Sy;
+// tm' = tm (1 - 1e-5) absorbs the roundings of u, v (< 1e-6 relative): every pair whose
+// exact r^2 can reach the threshold (C^2 >= tm Vx Vy) is a candidate.  Candidates (rare at
 // useful thresholds) run the exact fp64 r^2 of ld_fast_r2 -- the same decision the LDS-tile
-// epilogue and the general kernel make.  The two lanes of a column (h = 0, 1) sum their
-// counts with one cross-half swap.
+// epilogue and the general kernel make.  tm <= 0 (all_pass): u = v = 0, E = +inf, every
+// pair in the window is a candidate.  The two lanes of a column (h = 0, 1) add their counts.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ void ld_count_regs(const v16i (&acc)[2][4], const LdWindowArgs &a,
                                               const LdFast *__restrict__ fv, const uint32_t *__restrict__ chrom_id,
-                                              uint16_t *__restrict__ cnt, const float *ru, const int *rsx,
+                                              uint16_t *__restrict__ cnt, const float *ru, const float *rsf,
                                               uint32_t I4, uint32_t J4, int wi, int wj, int h, int r) {
     const int64_t M = (int64_t)a.m;
     const int pad = a.kpad - a.ns;
-    const int ns = a.ns;
     const double dn = (double)a.ns;
     const uint64_t bI = 4ull * I4 + wi;
     const int64_t i0 = (int64_t)bI * kLdBlock;
+    const float nf = (float)a.ns;
+    const float nkp = -(float)a.ns * (float)pad;
+    const float negE = a.all_pass ? -INFINITY : -(float)((8.0 * a.ns * a.ns + 4e6) * (1.0 / 8388608.0));
     int64_t jv[4];
-    int nsx[4], lo[4], span[4], nc[4];
-    float vj[4];
+    int lo[4], span[4], nc[4];
+    float nsx[4], vj[4];
     bool full = true;
 #pragma unroll
     for (int y = 0; y < 4; y++) {
@@ -102,9 +110,9 @@ __device__ __forceinline__ void ld_count_regs(const v16i (&acc)[2][4], const LdW
         jv[y] = j;
         const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
         const LdFast f = fv[jok ? j : 0];
-        nsx[y] = -f.sx;
-        vj[y] = sqrtf((float)f.vxp);
-        // valid rows [lo, hi) of the 64-block: i in [j - window, j)
+        nsx[y] = -(float)f.sx;
+        vj[y] = a.all_pass ? 0.f : sqrtf((float)f.vxp);
+        // valid rows [lo, lo + span) of the 64-block: i in [j - window, j)
         const int64_t l0 = j - (int64_t)a.window - i0;
         const int64_t h0 = j - i0;
         const int l = (int)(l0 > 0 ? (l0 < 64 ? l0 : 64) : 0);
@@ -114,41 +122,60 @@ __device__ __forceinline__ void ld_count_regs(const v16i (&acc)[2][4], const LdW
         full = full && span[y] == 64;
         nc[y] = 0;
     }
-    const int nKp = -ns * pad;
     auto body = [&](auto check) {
 #pragma unroll
-        for (int x = 0; x < 2; x++) {
-            int4 rs[4];
-            float4 ux[4];
+        for (int y = 0; y < 4; y++) {
 #pragma unroll
-            for (int g = 0; g < 4; g++) {
-                const int lr = wi * 64 + 32 * x + 8 * g + 4 * h;
-                rs[g] = *reinterpret_cast<const int4 *>(rsx + lr);
-                ux[g] = *reinterpret_cast<const float4 *>(ru + lr);
-            }
+            for (int x = 0; x < 2; x++) {
+                float rs[16], uu[16];
 #pragma unroll
-            for (int y = 0; y < 4; y++) {
-                auto cand = [&](int k) {
-                    const int g = k >> 2, e = k & 3;
-                    const int row = 32 * x + 8 * g + 4 * h + e;
-                    const int rsi = e == 0 ? rs[g].x : e == 1 ? rs[g].y : e == 2 ? rs[g].z : rs[g].w;
-                    const float ui = e == 0 ? ux[g].x : e == 1 ? ux[g].y : e == 2 ? ux[g].z : ux[g].w;
-                    const int C = __mul24(ns, acc[x][y][k]) + (__mul24(rsi, nsx[y]) + nKp);
-                    bool c = a.all_pass || fabsf((float)C) >= ui * vj[y];
-                    if (decltype(check)::value) c = c && (unsigned)(row - lo[y]) < (unsigned)span[y];
-                    return c;
+                for (int g = 0; g < 4; g++) {
+                    const int lr = wi * 64 + 32 * x + 8 * g + 4 * h;
+                    const float4 a4 = *reinterpret_cast<const float4 *>(rsf + lr);
+                    const float4 u4 = *reinterpret_cast<const float4 *>(ru + lr);
+                    rs[4 * g] = a4.x, rs[4 * g + 1] = a4.y, rs[4 * g + 2] = a4.z, rs[4 * g + 3] = a4.w;
+                    uu[4 * g] = u4.x, uu[4 * g + 1] = u4.y, uu[4 * g + 2] = u4.z, uu[4 * g + 3] = u4.w;
+                }
+                auto cand2 = [&](int k, float sxj, float vjj, int a0, int a1, bool &c0, bool &c1) {
+                    const f2 af = {(float)a0, (float)a1};
+                    const f2 ct = __builtin_elementwise_fma(f2{rs[k], rs[k + 1]}, f2{sxj, sxj}, f2{nkp, nkp});
+                    const f2 c = __builtin_elementwise_fma(f2{nf, nf}, af, ct);
+                    const f2 tt = __builtin_elementwise_fma(f2{uu[k], uu[k + 1]}, f2{vjj, vjj}, f2{negE, negE});
+                    c0 = fabsf(c.x) >= tt.x;
+                    c1 = fabsf(c.y) >= tt.y;
+                    if (decltype(check)::value) {
+                        const int row = 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
+                        c0 = c0 & ((unsigned)(row - lo[y]) < (unsigned)span[y]);
+                        c1 = c1 & ((unsigned)(row + 1 - lo[y]) < (unsigned)span[y]);
+                    }
                 };
-                // pass A: candidate test only (lane-mask OR, no branch per pair)
                 bool any = false;
 #pragma unroll
-                for (int k = 0; k < 16; k++) any |= cand(k);
-                // pass B, only for the rare lanes holding a candidate: exact fp64 r^2
+                for (int k = 0; k < 16; k += 2) {
+                    bool c0, c1;
+                    cand2(k, nsx[y], vj[y], acc[x][y][k], acc[x][y][k + 1], c0, c1);
+                    any = any | c0 | c1;
+                    __builtin_amdgcn_sched_barrier(0);  // keep the pairs' temporaries short-lived
+                }
+                // only lanes holding a candidate: exact fp64 r^2 (out of line)
                 if (any) {
+                    // recomputed from laundered operands: sharing pass A's temporaries would
+                    // keep them live (and spilled) across pass A for this rare path
+                    float sxj = nsx[y], vjj = vj[y];
+                    asm volatile("" : "+v"(sxj), "+v"(vjj));
 #pragma unroll
-                    for (int k = 0; k < 16; k++)
-                        if (cand(k))
-                            nc[y] += ld_exact_pass(fv, chrom_id, a.max_dist, a.threshold, i0 + 32 * x + 8 * (k >> 2) + 4 * h + (k & 3),
-                                                   jv[y], acc[x][y][k] - pad, dn);
+                    for (int k = 0; k < 16; k += 2) {
+                        int a0 = acc[x][y][k], a1 = acc[x][y][k + 1];
+                        asm volatile("" : "+v"(a0), "+v"(a1));
+                        bool c[2];
+                        cand2(k, sxj, vjj, a0, a1, c[0], c[1]);
+#pragma unroll
+                        for (int e = 0; e < 2; e++)
+                            if (c[e])
+                                nc[y] += ld_exact_pass(fv, chrom_id, a.max_dist, a.threshold,
+                                                       i0 + 32 * x + 8 * ((k + e) >> 2) + 4 * h + ((k + e) & 3), jv[y],
+                                                       (e ? a1 : a0) - pad, dn);
+                    }
                 }
             }
         }
@@ -179,11 +206,12 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
     // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
     // ds_reads): the staging ring during the k-loop, then the waves' epilogue tiles over it;
     // the per-row prefilter terms after that
-    __shared__ __attribute__((aligned(16))) int8_t lds[kRing + kFB * (8 + 4 + 4 + 4)];
+    __shared__ __attribute__((aligned(16))) int8_t lds[kRing + kFB * (8 + 4 + 4 + 4 + 4)];
     double *rvx = reinterpret_cast<double *>(lds + kRing);
     int *rsx = reinterpret_cast<int *>(lds + kRing + kFB * 8);
     float *rvxf = reinterpret_cast<float *>(lds + kRing + kFB * 12);
-    float *ru = reinterpret_cast<float *>(lds + kRing + kFB * 16);  // sqrt(tm' * Vx), register epilogue
+    float *ru = reinterpret_cast<float *>(lds + kRing + kFB * 16);  // register epilogue: sqrt(tm' Vx)
+    float *rsf = reinterpret_cast<float *>(lds + kRing + kFB * 20);  // and Sx as fp32
     const uint32_t b = xcd_remap(blockIdx.x, nblocks);
     const uint32_t I4 = blocks[2 * b], J4 = blocks[2 * b + 1];
     const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
@@ -216,7 +244,8 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
         const LdFast f = fv[i];
         rvx[t] = f.vxp;
         rvxf[t] = (float)f.vxp;
-        ru[t] = sqrtf((float)(a.tm * (1.0 - 1e-5)) * (float)f.vxp);
+        ru[t] = a.all_pass ? 0.f : sqrtf((float)(a.tm * (1.0 - 1e-5)) * (float)f.vxp);
+        rsf[t] = (float)f.sx;
         rsx[t] = f.sx;
     }
     const int kpad = a.kpad;
@@ -228,14 +257,14 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
     for (int q = 0; q < kGlds; q++) {
         const int idx = kGlds * w + q;                // 0..31: A rows for 0..15, B rows after
         const int lrow = (idx & 15) * 16 + (l >> 2);  // row within the A or B tile
-        int64_t g = (idx < 16 ? ibase : jbase) + lrow;
+        int64_t g = (VCFXG_LD_EXPT & 16) ? lrow : (idx < 16 ? ibase : jbase) + lrow;
         if (g >= M) g = M - 1;
         const int logical = (l & 3) ^ ((lrow >> 2) & 3);
         src[q] = Gc + g * (int64_t)kpad + logical * 16;
     }
     auto stage = [&](int ks, int buf) {
 #pragma unroll
-        for (int q = 0; q < kGlds; q++) glds16(src[q] + ks * kBK, lds + buf * kStage + (kGlds * w + q) * 1024);
+        for (int q = 0; q < kGlds; q++) glds16(src[q] + ((VCFXG_LD_EXPT & 8) ? 0 : ks * kBK), lds + buf * kStage + (kGlds * w + q) * 1024);
     };
     v16i acc[2][4];
 #pragma unroll
@@ -292,7 +321,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
     }
     if (P == 1 && a.ns <= 23170) {
         __syncthreads();  // the row terms written before the k-loop are visible to every wave
-        ld_count_regs(acc, a, fv, chrom_id, cnt, ru, rsx, I4, J4, wi, wj, h, r);
+        ld_count_regs(acc, a, fv, chrom_id, cnt, ru, rsf, I4, J4, wi, wj, h, r);
         return;
     }
     __syncthreads();  // every wave is done reading the ring; the epilogue tiles reuse it
