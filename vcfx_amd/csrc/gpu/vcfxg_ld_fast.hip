@@ -7,7 +7,8 @@
 //   * operands: 256 rows of I and 256 rows of J, K = kpad bytes, staged in 64-byte k-slices
 //     by global_load_lds (16 B/lane, lane-linear LDS image, XOR-swizzled 16 B slots via the
 //     SOURCE address so the ds_read_b128 fragment reads are bank-conflict free) into a
-//     4-buffer ring with three stages in flight (counted vmcnt + raw s_barrier);
+//     4-buffer ring, fragments read one k-half ahead of the MFMAs (counted vmcnt + raw
+//     s_barrier between two MFMA groups);
 //   * 8 waves as 4 (I) x 2 (J), each a 64x128 output = 2x4 v_mfma_i32_32x32x32_i8
 //     accumulators: per k-step a wave reads 6 fragments for 8 MFMAs, and the block loads
 //     32 KiB per 128 MFMAs (half the operand traffic per MFMA of a 128x128 block);
@@ -25,9 +26,8 @@
 
 #include <type_traits>
 
-// VCFXG_LD_EXPT (diagnostic builds only, results invalid): bit 0 skips the epilogue, bit 1
-// the in-loop staging loads, bit 2 the LDS fragment reads; bit 3 stages k-slice 0 every step,
-// bit 4 reads rows 0..255 for every block
+// VCFXG_LD_EXPT (diagnostic builds only, results invalid): bit 0 skips the epilogue, bit 3
+// stages k-slice 0 every step, bit 4 reads rows 0..255 for every block
 #ifndef VCFXG_LD_EXPT
 #define VCFXG_LD_EXPT 0
 #endif
@@ -272,42 +272,66 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
 #pragma unroll
         for (int y = 0; y < 4; y++) acc[x][y] = v16i{};
     const int nk = kpad / kBK;
-    // kNBuf-buffer ring, kNBuf-1 stages in flight: at step ks a wave waits only for its own
-    // loads of stage ks (counted vmcnt: the later stages' glds may stay outstanding), then a
-    // raw barrier (no __syncthreads: its fence would drain every glds) makes all waves'
-    // stage-ks bytes visible and frees buffer (ks-1)%kNBuf, last read at step ks-1
-    for (int q = 0; q < kNBuf - 1 && q < nk; q++) stage(q, q);
-    for (int ks = 0; ks < nk; ks++) {
-        const int ahead = nk - 1 - ks < kNBuf - 2 ? nk - 1 - ks : kNBuf - 2;  // stages still loading
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (!(VCFXG_LD_EXPT & 2) && ks + kNBuf - 1 < nk) stage(ks + kNBuf - 1, (ks + kNBuf - 1) % kNBuf);
-        const int8_t *base = lds + (ks % kNBuf) * kStage;
+    // fragments of k-half s (32 k-bytes) of the k-slice in buffer `base`
+    auto frag = [&](const int8_t *base, int s, v4i(&fa)[2], v4i(&fb)[4]) {
+        const int lg = 2 * s + h;
 #pragma unroll
-        for (int s = 0; s < 2; s++) {
-            const int lg = 2 * s + h;
-            v4i af[2], bf[4];
-#pragma unroll
-            for (int x = 0; x < 2; x++) {
-                const int ra = wi * 64 + x * 32 + r;
-                if (VCFXG_LD_EXPT & 4) { af[x] = v4i{ra, ks, s, x}; continue; }
-                af[x] = *reinterpret_cast<const v4i *>(base + ra * kBK + ((lg ^ ((ra >> 2) & 3)) << 4));
-            }
-#pragma unroll
-            for (int y = 0; y < 4; y++) {
-                const int rb = wj * 128 + y * 32 + r;
-                if (VCFXG_LD_EXPT & 4) { bf[y] = v4i{rb, ks, s, y}; continue; }
-                bf[y] = *reinterpret_cast<const v4i *>(base + kFB * kBK + rb * kBK + ((lg ^ ((rb >> 2) & 3)) << 4));
-            }
-#pragma unroll
-            for (int x = 0; x < 2; x++)
-#pragma unroll
-                for (int y = 0; y < 4; y++)
-                    acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[x], bf[y], acc[x][y], 0, 0, 0);
+        for (int x = 0; x < 2; x++) {
+            const int ra = wi * 64 + x * 32 + r;
+            fa[x] = *reinterpret_cast<const v4i *>(base + ra * kBK + ((lg ^ ((ra >> 2) & 3)) << 4));
         }
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            const int rb = wj * 128 + y * 32 + r;
+            fb[y] = *reinterpret_cast<const v4i *>(base + kFB * kBK + rb * kBK + ((lg ^ ((rb >> 2) & 3)) << 4));
+        }
+    };
+    auto mfma8 = [&](const v4i(&fa)[2], const v4i(&fb)[4]) {
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+                acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[x], fb[y], acc[x][y], 0, 0, 0);
+    };
+    // Software pipeline over a kNBuf-buffer ring, fragments one k-half ahead of the MFMAs:
+    //   step ks: read F(ks, 1) | MFMAs (ks, 0) | wait stage ks+1, barrier, stage ks+3 into
+    //   buffer (ks-1)%kNBuf (last read by F(ks-1, 1), consumed before this barrier), read
+    //   F(ks+1, 0) | MFMAs (ks, 1)
+    // so every fragment read overlaps 8 MFMAs and the barrier sits between two MFMA groups;
+    // counted vmcnt + raw s_barrier (a __syncthreads fence would drain every glds)
+    for (int q = 0; q < kNBuf - 1; q++) stage(q < nk ? q : nk - 1, q);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    v4i a0[2], b0[4], a1[2], b1[4];
+    frag(lds, 0, a0, b0);
+    for (int ks = 0; ks < nk - 1; ks++) {  // (the last step peeled: no branch before MFMAs (ks, 1)
+        frag(lds + (ks % kNBuf) * kStage, 1, a1, b1);  // lets the compiler count lgkmcnt exactly)
+        mfma8(a0, b0);
+        // one MFMA first: the loop-header wait (lgkmcnt(0): the compiler merges the back-edge
+        // state) then covers only F(ks, 0), and F(ks, 1) loads behind the other 7
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
+        // stage ks+1 landed (stage ks+2 may still load); every step issues a stage -- past
+        // the end a re-read of the last (L2-hot) slice into the free buffer -- so the counts
+        // are constant and the loop body has no branch
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        frag(lds + ((ks + 1) % kNBuf) * kStage, 0, a0, b0);
+        stage(ks + kNBuf - 1 < nk ? ks + kNBuf - 1 : nk - 1, (ks + kNBuf - 1) % kNBuf);
+        mfma8(a1, b1);
+        // fragment reads, then the 4 staging loads spread between the MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+#pragma unroll
+        for (int q = 0; q < kGlds; q++) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8 - kGlds, 0);
     }
+    frag(lds + ((nk - 1) % kNBuf) * kStage, 1, a1, b1);
+    mfma8(a0, b0);
+    mfma8(a1, b1);
     if (VCFXG_LD_EXPT & 1) {
         int z = 0;
 #pragma unroll
