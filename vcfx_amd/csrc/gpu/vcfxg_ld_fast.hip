@@ -299,6 +299,10 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
     //   F(ks+1, 0) | MFMAs (ks, 1)
     // so every fragment read overlaps 8 MFMAs and the barrier sits between two MFMA groups;
     // counted vmcnt + raw s_barrier (a __syncthreads fence would drain every glds)
+    // the epilogue's pointer arguments, consumed here: left to itself the compiler hoists their
+    // scalar loads over the loop, and a pending SMEM load (out of order within lgkmcnt) turns
+    // every fragment wait in the loop into lgkmcnt(0)
+    asm volatile("" ::"s"(cnt), "s"(chrom_id), "s"(off), "s"(pairs));
     for (int q = 0; q < kNBuf - 1; q++) stage(q < nk ? q : nk - 1, q);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -307,8 +311,8 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
     for (int ks = 0; ks < nk - 1; ks++) {  // (the last step peeled: no branch before MFMAs (ks, 1)
         frag(lds + (ks % kNBuf) * kStage, 1, a1, b1);  // lets the compiler count lgkmcnt exactly)
         mfma8(a0, b0);
-        // one MFMA first: the loop-header wait (lgkmcnt(0): the compiler merges the back-edge
-        // state) then covers only F(ks, 0), and F(ks, 1) loads behind the other 7
+        // one MFMA first: the compiler's wait before it (always lgkmcnt(0) here) then covers
+        // only F(ks, 0), and F(ks, 1) loads behind the other 7
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
@@ -320,14 +324,16 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
         frag(lds + ((ks + 1) % kNBuf) * kStage, 0, a0, b0);
         stage(ks + kNBuf - 1 < nk ? ks + kNBuf - 1 : nk - 1, (ks + kNBuf - 1) % kNBuf);
         mfma8(a1, b1);
-        // fragment reads, then the 4 staging loads spread between the MFMAs
+        // again one MFMA first (the compiler's wait before it, lgkmcnt(0), then covers only
+        // the long-landed F(ks, 1)), the fragment reads, the staging loads between MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
 #pragma unroll
         for (int q = 0; q < kGlds; q++) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 8 - kGlds, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 7 - kGlds, 0);
     }
     frag(lds + ((nk - 1) % kNBuf) * kStage, 1, a1, b1);
     mfma8(a0, b0);
