@@ -181,6 +181,8 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *ctx, uint64_t j0, uint64_t j1, uint64_t win
                           uint64_t *n_pairs, uint64_t *text_bytes);
 /* checks the int8 MFMA operand layout the LD kernels assume (0 mismatches expected) */
 int vcfxg_selftest_mfma_i8(vcfxg_ctx *ctx, int *mismatches);
+/* checks the FP4 (e2m1, block-scaled) MFMA operand layout of the fast LD kernel */
+int vcfxg_selftest_mfma_fp4(vcfxg_ctx *ctx, int *mismatches);
 
 /* device-formatted output text (without the column header line) */
 int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);

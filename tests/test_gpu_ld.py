@@ -18,6 +18,7 @@ def oracle():
 def test_mfma_i8_layout():
     e = engine.Engine(0)
     assert e.selftest_mfma_i8() == 0
+    assert e.selftest_mfma_fp4() == 0
     e.close()
 
 

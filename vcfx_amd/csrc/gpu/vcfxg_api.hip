@@ -46,7 +46,7 @@ struct vcfxg_ctx {
     std::string query_host, crit_host, pool_host;  // host sources of in-flight async copies
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
-        ld_off, ld_pairs, ld_fast, ld_gflag;
+        ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp;
     DevBuf fuse_state;          // fused AF: per-chunk look-back words
     DevBuf af_meta;             // AF head pass output (k_af_meta)
     DevBuf scan_seg, nl_chunk;  // AF one-sweep path: per-chunk segment counts, newline -> chunk
@@ -60,7 +60,7 @@ struct vcfxg_ctx {
     int fuse_dbg = getenv("VCFXG_FUSE_DEBUG") ? atoi(getenv("VCFXG_FUSE_DEBUG")) : 0;  // diagnostics only
     std::vector<uint8_t> ld_gflag_host;  // per 128-variant group: all complete
     uint64_t ld_m = 0, ld_prefix_bytes = 0;
-    int ld_kpad = 64, ld_ns = 0;
+    int ld_kpad = 64, ld_ns = 0, ld_kp4 = 64;
     bool ld_chrom_ids = false;
     std::vector<uint32_t> ld_cid_host, ld_blocks_host;
     uint64_t text_bytes = 0;
@@ -189,7 +189,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk})
         if (b->p) (void)hipFree(b->p);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
@@ -789,6 +789,8 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
     r = ensure(c, c->ld_Gc, (size_t)(M + 1) * kpad + 64);
     if (!r) r = ensure(c, c->ld_vars, sizeof(vcfxg::LdVar) * (M + 1));
     if (!r) r = ensure(c, c->ld_fast, sizeof(vcfxg::LdFast) * (M + 1));
+    const int kp4 = vcfxg::ld_kp4(n_samples);
+    if (!r) r = ensure(c, c->ld_Gp, (size_t)(M + 1) * kp4 + 64);
     if (!r) r = ensure(c, c->ld_gflag, M / vcfxg::kLdFastBlock + 2);
     if (!r) r = ensure(c, c->ld_plen, 8 * (M + 2));
     if (!r) r = ensure(c, c->ld_poff, 8 * (M + 2));
@@ -797,6 +799,7 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
     HIPCHK(c, vcfxg::launch_ld_compact(P<vcfxg::LdLine>(c->ld_lines), P<uint64_t>(c->ld_vidx), P<uint64_t>(c->d_nlines),
                                        L, kpad, n_samples, P<int8_t>(c->ld_G), P<int8_t>(c->ld_Gc),
                                        P<vcfxg::LdVar>(c->ld_vars), P<vcfxg::LdFast>(c->ld_fast), c->stream));
+    HIPCHK(c, vcfxg::launch_ld_pack4(P<int8_t>(c->ld_Gc), M, kpad, n_samples, P<uint8_t>(c->ld_Gp), kp4, c->stream));
     prof_end(c, "ld_compact");
     HIPCHK(c, vcfxg::launch_ld_groups(P<vcfxg::LdVar>(c->ld_vars), M, P<uint8_t>(c->ld_gflag), c->stream));
     c->ld_gflag_host.assign(M / vcfxg::kLdFastBlock + 1, 0);
@@ -820,6 +823,7 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
     prof_collect(c);
     c->ld_m = M;
     c->ld_kpad = kpad;
+    c->ld_kp4 = kp4;
     c->ld_ns = n_samples;
     c->ld_prefix_bytes = pbytes;
     c->ld_chrom_ids = false;
@@ -928,10 +932,11 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     // (vx >= (n-1)/n^2 for a polymorphic complete variant); delta covers it 100-fold
     a.tm = threshold - (1e-6 + 1e-10 * (double)c->ld_ns);
     a.all_pass = a.tm <= 0.0;
+    a.kp4 = c->ld_kp4;
     const uint32_t *cid = max_dist > 0 ? P<uint32_t>(c->ld_cid) : nullptr;
     const uint32_t *fbl = P<uint32_t>(c->ld_blocks), *gbl = fbl + 2 * (size_t)nfast;
     prof_begin(c, "ld_count");
-    HIPCHK(c, vcfxg::launch_ld_fast(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
+    HIPCHK(c, vcfxg::launch_ld_fast(1, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
                                     P<uint16_t>(c->ld_cnt), nullptr, nullptr, c->stream));
     prof_end(c, "ld_count");
     prof_begin(c, "ld_count_gen");
@@ -954,7 +959,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     if (!r) r = ensure(c, c->rowoff, 8 * (np + 1));
     if (r) return r;
     prof_begin(c, "ld_emit");
-    HIPCHK(c, vcfxg::launch_ld_fast(2, P<int8_t>(c->ld_Gc), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
+    HIPCHK(c, vcfxg::launch_ld_fast(2, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
                                     P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off), P<vcfxg::LdPair>(c->ld_pairs),
                                     c->stream));
     prof_end(c, "ld_emit");
@@ -1048,6 +1053,40 @@ int vcfxg_selftest_mfma_i8(vcfxg_ctx *c, int *mismatches) {
             int s = 0;
             for (int k = 0; k < 32; k++) s += A[i * 32 + k] * B[j * 32 + k];
             bad += s != C[i * 32 + j];
+        }
+    *mismatches = bad;
+    return VCFXG_OK;
+}
+
+int vcfxg_selftest_mfma_fp4(vcfxg_ctx *c, int *mismatches) {
+    if (!c || !mismatches) return VCFXG_E_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    // dosages 0..2 in a 32x64 A and an asymmetric 32x64 B, packed e2m1 two per byte
+    std::vector<int> A(32 * 64), B(32 * 64);
+    for (int i = 0; i < 32 * 64; i++) {
+        A[i] = (i * 7 + 3) % 3;
+        B[i] = (i * 11 + i / 64 + 1) % 3;
+    }
+    std::vector<uint8_t> Ap(1024), Bp(1024);
+    for (int i = 0; i < 1024; i++) {
+        Ap[i] = (uint8_t)((2 * A[2 * i]) | ((2 * A[2 * i + 1]) << 4));
+        Bp[i] = (uint8_t)((2 * B[2 * i]) | ((2 * B[2 * i + 1]) << 4));
+    }
+    int r = ensure(c, c->scan_tmp, 8192);
+    if (r) return r;
+    char *d = P<char>(c->scan_tmp);
+    HIPCHK(c, hipMemcpyAsync(d, Ap.data(), 1024, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d + 1024, Bp.data(), 1024, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, vcfxg::launch_mfma_f4_selftest((uint8_t *)d, (uint8_t *)(d + 1024), (float *)(d + 2048), c->stream));
+    std::vector<float> C(32 * 32);
+    HIPCHK(c, hipMemcpyAsync(C.data(), d + 2048, 4096, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    int bad = 0;
+    for (int i = 0; i < 32; i++)
+        for (int j = 0; j < 32; j++) {
+            int sum = 0;
+            for (int k = 0; k < 64; k++) sum += A[i * 64 + k] * B[j * 64 + k];
+            bad += (float)sum != C[i * 32 + j];
         }
     *mismatches = bad;
     return VCFXG_OK;

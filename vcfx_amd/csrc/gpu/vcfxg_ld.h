@@ -65,6 +65,7 @@ struct LdWindowArgs {
     uint64_t nb;            // column blocks per row in the count table
     double tm;              // prefilter: exact r^2 < tm cannot reach threshold (tm = threshold - delta)
     int all_pass;           // tm <= 0: every pair is a candidate
+    int kp4;                // FP4 row bytes of the fast kernel's operand copy (multiple of 64)
 };
 
 hipError_t launch_ld_parse(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
@@ -72,10 +73,14 @@ hipError_t launch_ld_parse(const char *buf, int64_t data_start, const uint64_t *
 hipError_t launch_ld_compact(const LdLine *lines, const uint64_t *vidx, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int kpad, int ns, const int8_t *G, int8_t *Gc, LdVar *vars,
                              LdFast *fv, hipStream_t s);
-hipError_t launch_ld_fast(int pass, const int8_t *Gc, const LdFast *fv, const uint32_t *chrom_id,
+hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const uint32_t *chrom_id,
                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
                           const uint64_t *off, LdPair *pairs, hipStream_t s);
 hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, uint8_t *gflag, hipStream_t s);
+hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s);
+hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C, hipStream_t s);
+// FP4 row bytes for ns samples: two per byte, whole 64-byte k-slices
+inline int ld_kp4(int ns) { return ns > 0 ? ((ns + 127) / 128) * 64 : 64; }
 hipError_t launch_ld_block(int pass, const int8_t *Gc, const LdVar *vars, const uint32_t *chrom_id,
                            const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
                            const uint64_t *off, LdPair *pairs, hipStream_t s);

@@ -3,13 +3,17 @@
 // The common case of VCFX_ld_calculator's pair loop (computeLDStreamingMmap :511-648 /
 // computeLDStreaming :864-987 calling computeRsqFast :397-401): with no missing genotype
 // among the ns samples, the pair sums need only S_xy = X.X^T (n = ns and Sx, Sx2 are
-// per-variant), so a block is one int8 GEMM tile:
-//   * operands: 256 rows of I and 256 rows of J, K = kpad bytes, staged in 64-byte k-slices
+// per-variant), so a block is one GEMM tile over the dosages 0/1/2:
+//   * operands: FP4 (e2m1) rows -- 0, 1, 2 are exact e2m1 values and every product and
+//     partial sum is an integer below 2^24, so the fp32-accumulating block-scaled MFMA
+//     (scales 2^0) computes S_xy exactly at twice the int8 rate and half the operand bytes;
+//     zero padding needs no correction.  256 rows of I and 256 rows of J, K = kp4 bytes
+//     (2 dosages per byte), staged in 64-byte k-slices
 //     by global_load_lds (16 B/lane, lane-linear LDS image, XOR-swizzled 16 B slots via the
 //     SOURCE address so the ds_read_b128 fragment reads are bank-conflict free) into a
 //     4-buffer ring, fragments read one k-half ahead of the MFMAs (counted vmcnt + raw
 //     s_barrier between two MFMA groups);
-//   * 8 waves as 4 (I) x 2 (J), each a 64x128 output = 2x4 v_mfma_i32_32x32x32_i8
+//   * 8 waves as 4 (I) x 2 (J), each a 64x128 output = 2x4 v_mfma_scale_f32_32x32x64_f8f6f4
 //     accumulators: per k-step a wave reads 6 fragments for 8 MFMAs, and the block loads
 //     32 KiB per 128 MFMAs (half the operand traffic per MFMA of a 128x128 block);
 //   * epilogue per 64x64 quarter of a wave's output (two per wave): the int32 tile goes to
@@ -24,6 +28,7 @@
 #include "vcfxg_device.h"
 #include "vcfxg_ld.h"
 
+#include <algorithm>
 #include <type_traits>
 
 // VCFXG_LD_EXPT (diagnostic builds only, results invalid): bit 0 skips the epilogue, bit 3
@@ -35,7 +40,10 @@
 namespace vcfxg {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+constexpr int kFmtFp4 = 4;              // cbsz / blgp operand format: e2m1
+constexpr int kScaleOne = 0x7F7F7F7F;   // E8M0 block scales 2^0
 
 constexpr int kFB = kLdFastBlock;      // block side (variants): 256
 constexpr int kBK = 64;                // k-slice bytes per stage
@@ -48,7 +56,7 @@ static_assert(kWaves * kQuarter <= kRing, "epilogue tiles must fit in the stagin
 constexpr int kGlds = kStage / 1024 / kWaves;  // 1 KiB glds instructions per wave per stage
 static_assert(kGlds == 4, "the k-loop's vmcnt counts assume 4 glds per wave per stage");
 
-__device__ __forceinline__ void glds16(const int8_t *src, int8_t *lds_base) {
+__device__ __forceinline__ void glds16(const void *src, int8_t *lds_base) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
                                      (__attribute__((address_space(3))) void *)lds_base, 16, 0, 0);
 }
@@ -76,7 +84,7 @@ __device__ __forceinline__ int ld_exact_pass(const LdFast *__restrict__ fv, cons
 // holds, for each of its 4 column tiles y, column wj*128 + 32y + r and the 32 rows
 // 32x + 8g + 4h + e of the wave's 64-row block.  Candidate test per pair, branch-free and
 // two pairs per packed fp32 instruction:
-//   c = n*Sxy' + (-(Sx_i*Sy_j) - n*pad)   (Sxy' = accumulator incl. the padding bytes)
+//   c = n*Sxy + (-(Sx_i*Sy_j))            (Sxy = the exact fp32 accumulator)
 //   candidate iff |c| >= u_i * v_j - E,   u_i = sqrt(tm' Vx_i), v_j = sqrt(Vy_j)
 // Every operand is an integer below 2^24 (exact in fp32) and each fma rounds once, so
 // |c - C| <= (8n^2 + 2e6) 2^-24 < E = (8n^2 + 4e6) 2^-23 for the exact C = n*Sxy - Sx*Sy;
@@ -87,17 +95,16 @@ __device__ __forceinline__ int ld_exact_pass(const LdFast *__restrict__ fv, cons
 // pair in the window is a candidate.  The two lanes of a column (h = 0, 1) add their counts.
 typedef float f2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ void ld_count_regs(const v16i (&acc)[2][4], const LdWindowArgs &a,
+__device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdWindowArgs &a,
                                               const LdFast *__restrict__ fv, const uint32_t *__restrict__ chrom_id,
                                               uint16_t *__restrict__ cnt, const float *ru, const float *rsf,
                                               uint32_t I4, uint32_t J4, int wi, int wj, int h, int r) {
     const int64_t M = (int64_t)a.m;
-    const int pad = a.kpad - a.ns;
     const double dn = (double)a.ns;
     const uint64_t bI = 4ull * I4 + wi;
     const int64_t i0 = (int64_t)bI * kLdBlock;
     const float nf = (float)a.ns;
-    const float nkp = -(float)a.ns * (float)pad;
+    const float nkp = 0.f;
     const float negE = a.all_pass ? -INFINITY : -(float)((8.0 * a.ns * a.ns + 4e6) * (1.0 / 8388608.0));
     int64_t jv[4];
     int lo[4], span[4], nc[4];
@@ -174,7 +181,7 @@ __device__ __forceinline__ void ld_count_regs(const v16i (&acc)[2][4], const LdW
                             if (c[e])
                                 nc[y] += ld_exact_pass(fv, chrom_id, a.max_dist, a.threshold,
                                                        i0 + 32 * x + 8 * ((k + e) >> 2) + 4 * h + ((k + e) & 3), jv[y],
-                                                       (e ? a1 : a0) - pad, dn);
+                                                       (int)(e ? a1 : a0), dn);
                     }
                 }
             }
@@ -196,7 +203,7 @@ __device__ __forceinline__ void ld_count_regs(const v16i (&acc)[2][4], const LdW
 }
 
 template <int P>
-__global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__restrict__ Gc,
+__global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__restrict__ Gp,
                                                             const LdFast *__restrict__ fv,
                                                             const uint32_t *__restrict__ chrom_id, LdWindowArgs a,
                                                             const uint32_t *__restrict__ blocks, uint32_t nblocks,
@@ -248,11 +255,11 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
         rsf[t] = (float)f.sx;
         rsx[t] = f.sx;
     }
-    const int kpad = a.kpad;
+    const int kpad = a.kp4;  // FP4 row bytes
     // staging: 32 wave-instructions of 1 KiB per stage, kGlds per wave; instruction q of
     // wave w fills LDS [(kGlds*w+q) KiB, +1 KiB) = 16 rows x 64 B; lane l -> row (l>>2),
     // physical slot l&3 holding logical 16 B slot (l&3) ^ ((row>>2)&3)
-    const int8_t *src[kGlds];
+    const uint8_t *src[kGlds];
 #pragma unroll
     for (int q = 0; q < kGlds; q++) {
         const int idx = kGlds * w + q;                // 0..31: A rows for 0..15, B rows after
@@ -260,17 +267,17 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
         int64_t g = (VCFXG_LD_EXPT & 16) ? lrow : (idx < 16 ? ibase : jbase) + lrow;
         if (g >= M) g = M - 1;
         const int logical = (l & 3) ^ ((lrow >> 2) & 3);
-        src[q] = Gc + g * (int64_t)kpad + logical * 16;
+        src[q] = Gp + g * (int64_t)kpad + logical * 16;
     }
     auto stage = [&](int ks, int buf) {
 #pragma unroll
         for (int q = 0; q < kGlds; q++) glds16(src[q] + ((VCFXG_LD_EXPT & 8) ? 0 : ks * kBK), lds + buf * kStage + (kGlds * w + q) * 1024);
     };
-    v16i acc[2][4];
+    v16f acc[2][4];
 #pragma unroll
     for (int x = 0; x < 2; x++)
 #pragma unroll
-        for (int y = 0; y < 4; y++) acc[x][y] = v16i{};
+        for (int y = 0; y < 4; y++) acc[x][y] = v16f{};
     const int nk = kpad / kBK;
     // fragments of k-half s (32 k-bytes) of the k-slice in buffer `base`
     auto frag = [&](const int8_t *base, int s, v4i(&fa)[2], v4i(&fb)[4]) {
@@ -291,7 +298,10 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
         for (int x = 0; x < 2; x++)
 #pragma unroll
             for (int y = 0; y < 4; y++)
-                acc[x][y] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[x], fb[y], acc[x][y], 0, 0, 0);
+                acc[x][y] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                    v8i{fa[x].x, fa[x].y, fa[x].z, fa[x].w, 0, 0, 0, 0},
+                    v8i{fb[y].x, fb[y].y, fb[y].z, fb[y].w, 0, 0, 0, 0}, acc[x][y], kFmtFp4, kFmtFp4, 0, kScaleOne,
+                    0, kScaleOne);
     };
     // Software pipeline over a kNBuf-buffer ring, fragments one k-half ahead of the MFMAs:
     //   step ks: read F(ks, 1) | MFMAs (ks, 0) | wait stage ks+1, barrier, stage ks+3 into
@@ -345,7 +355,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
 #pragma unroll
             for (int y = 0; y < 4; y++)
 #pragma unroll
-                for (int k = 0; k < 16; k++) z ^= acc[x][y][k];
+                for (int k = 0; k < 16; k++) z ^= (int)acc[x][y][k];
         if (z == 0x7fffffff) cnt[0] = 1;
         return;
     }
@@ -356,7 +366,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
     }
     __syncthreads();  // every wave is done reading the ring; the epilogue tiles reuse it
     int *tile = reinterpret_cast<int *>(lds + w * kQuarter);
-    const int pad = kpad - a.ns;
+    const int pad = 0;  // FP4 rows are zero-padded
     const double dn = (double)a.ns;
     const int64_t n = a.ns;
     // fp32 form of the prefilter while n*Sxy and Sx*Sy fit int32 (n <= 23170): C exact in
@@ -378,7 +388,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
             for (int yy = 0; yy < 2; yy++)
 #pragma unroll
                 for (int k = 0; k < 16; k++)
-                    tile[(32 * x + (k & 3) + 8 * (k >> 2) + 4 * h) * 64 + 32 * yy + r] = acc[x][2 * hy + yy][k];
+                    tile[(32 * x + (k & 3) + 8 * (k >> 2) + 4 * h) * 64 + 32 * yy + r] = (int)acc[x][2 * hy + yy][k];
         const int64_t j = (int64_t)(bJ * kLdBlock) + l;
         const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
         uint64_t mask = 0;
@@ -433,17 +443,72 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const int8_t *__rest
     }
 }
 
-hipError_t launch_ld_fast(int pass, const int8_t *Gc, const LdFast *fv, const uint32_t *chrom_id,
+hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const uint32_t *chrom_id,
                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
                           const uint64_t *off, LdPair *pairs, hipStream_t s) {
     if (!nblocks) return hipSuccess;
-    if (a.kpad % kBK) return hipErrorInvalidValue;
+    if (a.kp4 % kBK || a.kp4 <= 0) return hipErrorInvalidValue;
     if (pass == 1)
-        hipLaunchKernelGGL(k_ld_fast<1>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gc, fv, chrom_id, a, blocks,
+        hipLaunchKernelGGL(k_ld_fast<1>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
                            nblocks, cnt, off, pairs);
     else
-        hipLaunchKernelGGL(k_ld_fast<2>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gc, fv, chrom_id, a, blocks,
+        hipLaunchKernelGGL(k_ld_fast<2>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
                            nblocks, cnt, off, pairs);
+    return hipGetLastError();
+}
+
+// FP4 (e2m1) copy of the compacted genotype rows for the fast kernel: dosage 0/1/2 ->
+// 0x0/0x2/0x4, two per byte (element 2b low nibble), zero from ns on; an incomplete row's
+// missing code packs as 0 (such rows never reach k_ld_fast)
+__global__ void k_ld_pack4(const int8_t *__restrict__ Gc, uint64_t m, int kpad, int ns, uint8_t *__restrict__ Gp,
+                           int kp4) {
+    const int per = kp4 / 16;  // 16 output bytes per thread
+    const uint64_t total = m * (uint64_t)per;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t v = t / per;
+        const int c = (int)(t - v * per);
+        const int8_t *row = Gc + v * (uint64_t)kpad;
+        uint32_t in[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 32 codes, 4 per dword
+        if (c * 32 + 32 <= kpad) {
+            const uint4 u0 = reinterpret_cast<const uint4 *>(row)[2 * c];
+            const uint4 u1 = reinterpret_cast<const uint4 *>(row)[2 * c + 1];
+            in[0] = u0.x, in[1] = u0.y, in[2] = u0.z, in[3] = u0.w;
+            in[4] = u1.x, in[5] = u1.y, in[6] = u1.z, in[7] = u1.w;
+        }
+        uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int e = 0; e < 32; e++) {
+            const int g = (int8_t)(in[e >> 2] >> (8 * (e & 3)));
+            const uint32_t code = c * 32 + e < ns ? (g == 1 ? 0x2u : g == 2 ? 0x4u : 0x0u) : 0x0u;
+            w[e >> 3] |= code << (4 * (e & 7));
+        }
+        reinterpret_cast<uint4 *>(Gp + v * (uint64_t)kp4)[c] = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
+hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s) {
+    if (!m) return hipSuccess;
+    if (kp4 % 64 || 2 * (int64_t)kp4 < ns) return hipErrorInvalidValue;
+    const uint64_t total = m * (uint64_t)(kp4 / 16);
+    const unsigned grid = (unsigned)std::min<uint64_t>((total + 255) / 256, 65536);
+    hipLaunchKernelGGL(k_ld_pack4, dim3(grid), dim3(256), 0, s, Gc, m, kpad, ns, Gp, kp4);
+    return hipGetLastError();
+}
+
+// self-test of the FP4 MFMA operand layout: C = A (32x64) . B^T over K = 64, dosages 0..2
+__global__ void k_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C) {
+    const int l = threadIdx.x, r = l & 31, h = l >> 5;
+    const v4i a = *reinterpret_cast<const v4i *>(A + r * 32 + 16 * h);
+    const v4i b = *reinterpret_cast<const v4i *>(B + r * 32 + 16 * h);
+    v16f c = {};
+    c = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(v8i{a.x, a.y, a.z, a.w, 0, 0, 0, 0},
+                                                        v8i{b.x, b.y, b.z, b.w, 0, 0, 0, 0}, c, kFmtFp4, kFmtFp4, 0,
+                                                        kScaleOne, 0, kScaleOne);
+    for (int k = 0; k < 16; k++) C[((k & 3) + 8 * (k >> 2) + 4 * h) * 32 + r] = c[k];
+}
+
+hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C, hipStream_t s) {
+    hipLaunchKernelGGL(k_mfma_f4_selftest, dim3(1), dim3(64), 0, s, A, B, C);
     return hipGetLastError();
 }
 

@@ -56,6 +56,7 @@ SIGNATURES = {
     "vcfxg_ld_stream_chunk": (_I, [_VP, _U64, _U64, _U64, ctypes.c_double, _I, ctypes.POINTER(_U64),
                                    ctypes.POINTER(_U64)]),
     "vcfxg_selftest_mfma_i8": (_I, [_VP, ctypes.POINTER(_I)]),
+    "vcfxg_selftest_mfma_fp4": (_I, [_VP, ctypes.POINTER(_I)]),
     "vcfxg_filter_query": (_I, [_VP, _VP, _I, _I, _P, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_fetch_text": (_I, [_VP, _VP, _S]),
     "vcfxg_fetch_lines": (_I, [_VP, _U64, _U64, _VP, _VP, _VP]),
@@ -203,6 +204,11 @@ class Engine:
     def selftest_mfma_i8(self):
         m = ctypes.c_int()
         self._chk(self.L.vcfxg_selftest_mfma_i8(self.h, ctypes.byref(m)), "selftest")
+        return m.value
+
+    def selftest_mfma_fp4(self):
+        m = ctypes.c_int()
+        self._chk(self.L.vcfxg_selftest_mfma_fp4(self.h, ctypes.byref(m)), "selftest")
         return m.value
 
     def text(self, nbytes):
