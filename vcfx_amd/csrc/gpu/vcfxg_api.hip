@@ -908,14 +908,27 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
             }
     }
     const uint32_t nfast = (uint32_t)(blocks.size() / 2);
+    // general list: every 64-block pair with an incomplete side -- for a complete row block J
+    // only the incomplete column blocks, found in the sorted list of them (no scan over the
+    // whole window triangle on the host)
+    const uint64_t Jlast = (j1 + BM - 1) / BM;
+    std::vector<uint32_t> inc;
+    for (uint64_t b = ifirst(j0 / BM); b < Jlast; b++)
+        if (!gcomp(b)) inc.push_back((uint32_t)b);
     for (uint64_t J = j0 / BM; J * BM < j1; J++) {
         const uint64_t I0 = ifirst(J);
         nb = std::max<uint64_t>(nb, J - I0 + 1);
-        for (uint64_t I = I0; I <= J; I++)
-            if (!(gcomp(I) && gcomp(J))) {
+        if (!gcomp(J)) {
+            for (uint64_t I = I0; I <= J; I++) {
                 blocks.push_back((uint32_t)I);
                 blocks.push_back((uint32_t)J);
             }
+            continue;
+        }
+        for (auto it = std::lower_bound(inc.begin(), inc.end(), (uint32_t)I0); it != inc.end() && *it <= J; ++it) {
+            blocks.push_back(*it);
+            blocks.push_back((uint32_t)J);
+        }
     }
     const uint32_t nbl = (uint32_t)(blocks.size() / 2) - nfast;
     const uint64_t rows = j1 - j0;

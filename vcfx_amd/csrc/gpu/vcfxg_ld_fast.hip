@@ -82,15 +82,15 @@ __device__ __forceinline__ int ld_exact_pass(const LdFast *__restrict__ fv, cons
 
 // Count-pass epilogue straight from the accumulators (no LDS tile): lane (h, r) of a wave
 // holds, for each of its 4 column tiles y, column wj*128 + 32y + r and the 32 rows
-// 32x + 8g + 4h + e of the wave's 64-row block.  Candidate test per pair, branch-free and
-// two pairs per packed fp32 instruction:
-//   c = n*Sxy + (-(Sx_i*Sy_j))            (Sxy = the exact fp32 accumulator)
-//   candidate iff |c| >= u_i * v_j - E,   u_i = sqrt(tm' Vx_i), v_j = sqrt(Vy_j)
-// Every operand is an integer below 2^24 (exact in fp32) and each fma rounds once, so
-// |c - C| <= (8n^2 + 2e6) 2^-24 < E = (8n^2 + 4e6) 2^-23 for the exact C = n*Sxy - Sx*Sy;
-// tm' = tm (1 - 1e-5) absorbs the roundings of u, v (< 1e-6 relative): every pair whose
-// exact r^2 can reach the threshold (C^2 >= tm Vx Vy) is a candidate.  Candidates (rare at
-// useful thresholds) run the exact fp64 r^2 of ld_fast_r2 -- the same decision the LDS-tile
+// 32x + 8g + 4h + e of the wave's 64-row block.  Candidate test per pair in C/n units, two
+// pairs per packed fp32 instruction and no conversion (the accumulator is already fp32):
+//   c' = Sxy + Sx_i * w_j               w_j = -Sy_j / n            (C' = C / n exactly)
+//   candidate iff |c'| >= u_i * v_j - E,  u_i = sqrt(tm' Vx_i) / n, v_j = sqrt(Vy_j)
+// Sxy and Sx_i are exact integers in fp32, w_j carries one rounding and the fma one more,
+// so |c' - C/n| <= 12 n 2^-24 < E = 32 n 2^-23 for the exact C = n*Sxy - Sx*Sy; tm' =
+// tm (1 - 1e-5) absorbs the roundings of u, v (< 1e-6 relative): every pair whose exact r^2
+// can reach the threshold (C^2 >= tm Vx Vy) is a candidate.  Candidates (rare at useful
+// thresholds) run the exact fp64 r^2 of ld_fast_r2 -- the same decision the LDS-tile
 // epilogue and the general kernel make.  tm <= 0 (all_pass): u = v = 0, E = +inf, every
 // pair in the window is a candidate.  The two lanes of a column (h = 0, 1) add their counts.
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -103,12 +103,10 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
     const double dn = (double)a.ns;
     const uint64_t bI = 4ull * I4 + wi;
     const int64_t i0 = (int64_t)bI * kLdBlock;
-    const float nf = (float)a.ns;
-    const float nkp = 0.f;
-    const float negE = a.all_pass ? -INFINITY : -(float)((8.0 * a.ns * a.ns + 4e6) * (1.0 / 8388608.0));
+    const float negE = a.all_pass ? -INFINITY : -(float)(32.0 * a.ns / 8388608.0);
     int64_t jv[4];
     int lo[4], span[4], nc[4];
-    float nsx[4], vj[4];
+    float wv[4], vj[4];
     bool full = true;
 #pragma unroll
     for (int y = 0; y < 4; y++) {
@@ -117,7 +115,7 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
         jv[y] = j;
         const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
         const LdFast f = fv[jok ? j : 0];
-        nsx[y] = -(float)f.sx;
+        wv[y] = -(float)f.sx / (float)a.ns;
         vj[y] = a.all_pass ? 0.f : sqrtf((float)f.vxp);
         // valid rows [lo, lo + span) of the 64-block: i in [j - window, j)
         const int64_t l0 = j - (int64_t)a.window - i0;
@@ -143,10 +141,8 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
                     rs[4 * g] = a4.x, rs[4 * g + 1] = a4.y, rs[4 * g + 2] = a4.z, rs[4 * g + 3] = a4.w;
                     uu[4 * g] = u4.x, uu[4 * g + 1] = u4.y, uu[4 * g + 2] = u4.z, uu[4 * g + 3] = u4.w;
                 }
-                auto cand2 = [&](int k, float sxj, float vjj, int a0, int a1, bool &c0, bool &c1) {
-                    const f2 af = {(float)a0, (float)a1};
-                    const f2 ct = __builtin_elementwise_fma(f2{rs[k], rs[k + 1]}, f2{sxj, sxj}, f2{nkp, nkp});
-                    const f2 c = __builtin_elementwise_fma(f2{nf, nf}, af, ct);
+                auto cand2 = [&](int k, float wjj, float vjj, float a0, float a1, bool &c0, bool &c1) {
+                    const f2 c = __builtin_elementwise_fma(f2{rs[k], rs[k + 1]}, f2{wjj, wjj}, f2{a0, a1});
                     const f2 tt = __builtin_elementwise_fma(f2{uu[k], uu[k + 1]}, f2{vjj, vjj}, f2{negE, negE});
                     c0 = fabsf(c.x) >= tt.x;
                     c1 = fabsf(c.y) >= tt.y;
@@ -160,7 +156,7 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
 #pragma unroll
                 for (int k = 0; k < 16; k += 2) {
                     bool c0, c1;
-                    cand2(k, nsx[y], vj[y], acc[x][y][k], acc[x][y][k + 1], c0, c1);
+                    cand2(k, wv[y], vj[y], acc[x][y][k], acc[x][y][k + 1], c0, c1);
                     any = any | c0 | c1;
                     __builtin_amdgcn_sched_barrier(0);  // keep the pairs' temporaries short-lived
                 }
@@ -168,14 +164,14 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
                 if (any) {
                     // recomputed from laundered operands: sharing pass A's temporaries would
                     // keep them live (and spilled) across pass A for this rare path
-                    float sxj = nsx[y], vjj = vj[y];
-                    asm volatile("" : "+v"(sxj), "+v"(vjj));
+                    float wjj = wv[y], vjj = vj[y];
+                    asm volatile("" : "+v"(wjj), "+v"(vjj));
 #pragma unroll
                     for (int k = 0; k < 16; k += 2) {
-                        int a0 = acc[x][y][k], a1 = acc[x][y][k + 1];
+                        float a0 = acc[x][y][k], a1 = acc[x][y][k + 1];
                         asm volatile("" : "+v"(a0), "+v"(a1));
                         bool c[2];
-                        cand2(k, sxj, vjj, a0, a1, c[0], c[1]);
+                        cand2(k, wjj, vjj, a0, a1, c[0], c[1]);
 #pragma unroll
                         for (int e = 0; e < 2; e++)
                             if (c[e])
@@ -217,7 +213,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
     double *rvx = reinterpret_cast<double *>(lds + kRing);
     int *rsx = reinterpret_cast<int *>(lds + kRing + kFB * 8);
     float *rvxf = reinterpret_cast<float *>(lds + kRing + kFB * 12);
-    float *ru = reinterpret_cast<float *>(lds + kRing + kFB * 16);  // register epilogue: sqrt(tm' Vx)
+    float *ru = reinterpret_cast<float *>(lds + kRing + kFB * 16);  // register epilogue: sqrt(tm' Vx) / n
     float *rsf = reinterpret_cast<float *>(lds + kRing + kFB * 20);  // and Sx as fp32
     const uint32_t b = xcd_remap(blockIdx.x, nblocks);
     const uint32_t I4 = blocks[2 * b], J4 = blocks[2 * b + 1];
@@ -251,7 +247,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
         const LdFast f = fv[i];
         rvx[t] = f.vxp;
         rvxf[t] = (float)f.vxp;
-        ru[t] = a.all_pass ? 0.f : sqrtf((float)(a.tm * (1.0 - 1e-5)) * (float)f.vxp);
+        ru[t] = a.all_pass ? 0.f : sqrtf((float)(a.tm * (1.0 - 1e-5)) * (float)f.vxp) / (float)a.ns;
         rsf[t] = (float)f.sx;
         rsx[t] = f.sx;
     }
