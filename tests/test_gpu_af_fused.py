@@ -1,5 +1,6 @@
 """GPU parity of vcfxg_allele_freq_region -- every device schedule (default index + head
-pass + sweep, look-back single sweep, chunk sweep, byte-class single sweep) -- against the
+pass + sweep, look-back single sweep, chunk sweep, byte-class single sweep, two-stream
+pipelined index + sweep) -- against the
 two-pass path
 (vcfxg_index + vcfxg_allele_freq) and the C oracle: every per-line array and the output
 text must be identical, including inputs that put many line starts in one 16 KiB chunk
@@ -14,20 +15,25 @@ from vcfx_amd import engine, synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["default", "fused", "chunks", "scan"])
+@pytest.fixture(scope="module", params=["default", "fused", "chunks", "scan", "pipe", "pipe1"])
 def eng(request):
     """every region schedule: index + head pass + sweep (default), look-back single sweep,
-    chunk sweep, byte-class single sweep"""
+    chunk sweep, byte-class single sweep, two-stream pipeline (pieces of 2 wave-chunks, so
+    the small inputs here span many pieces; and of 1)"""
     import os
-    old = os.environ.get("VCFXG_AF_FUSED")
-    os.environ["VCFXG_AF_FUSED"] = {"default": "0", "fused": "1", "chunks": "2", "scan": "4"}[request.param]
+    env = {"VCFXG_AF_FUSED": {"default": "0", "fused": "1", "chunks": "2", "scan": "4", "pipe": "5",
+                              "pipe1": "5"}[request.param],
+           "VCFXG_PIPE_CHUNKS": {"pipe1": "1"}.get(request.param, "2")}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return engine.Engine(0)
     finally:
-        if old is None:
-            del os.environ["VCFXG_AF_FUSED"]
-        else:
-            os.environ["VCFXG_AF_FUSED"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 @pytest.fixture(scope="module")

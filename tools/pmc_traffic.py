@@ -22,6 +22,7 @@ KERNELS = {
     "line_emit": r"vcfxg::k_idx_sweep<true>\(",
     "line_compact": r"vcfxg::k_nl_compact\(",
     "af_records": r"vcfxg::k_(line_meta|af_sweep|af_complex)\(",
+    "af_pipe": r"vcfxg::k_(idx_sweep<false>|nl_compact_piece|lines_tail|line_meta|af_sweep|af_complex)\(",
     "af_scan": r"vcfxg::k_af_scan\(",
     "af_fused": r"vcfxg::k_af_fused\(",
     "af_chunks": r"vcfxg::k_af_chunks\(",
@@ -37,9 +38,14 @@ KERNELS = {
 }
 
 
+# names whose kernels launch several times per step (one per pipelined piece): the per-step
+# divisor is the count of this once-per-step symbol instead
+ANCHOR = {"af_pipe": "vcfxg::k_af_complex"}
+
+
 def per_kernel(path, counter):
     """mean per timed step: sum over the matching dispatches / number of dispatches of the
-    most frequent matching symbol (one launch of each per step)"""
+    most frequent matching symbol (one launch of each per step), or of the ANCHOR symbol"""
     acc, calls = {}, {}
     with open(path, newline="") as f:
         for row in csv.DictReader(f):
@@ -51,7 +57,8 @@ def per_kernel(path, counter):
                     acc[k] = acc.get(k, 0.0) + float(row["Counter_Value"])
                     sym = name.split("(")[0]
                     calls.setdefault(k, {})[sym] = calls.setdefault(k, {}).get(sym, 0) + 1
-    return {k: v / max(calls[k].values()) for k, v in acc.items()}
+    return {k: v / (calls[k].get(ANCHOR[k], 0) if k in ANCHOR and calls[k].get(ANCHOR[k]) else max(calls[k].values()))
+            for k, v in acc.items()}
 
 
 def main():

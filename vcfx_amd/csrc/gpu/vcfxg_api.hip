@@ -30,6 +30,9 @@ struct DevBuf {
 struct vcfxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    hipStream_t stream2 = nullptr;           // pipelined AF: the record-sweep stream
+    std::vector<hipEvent_t> pipe_ev;         // pipelined AF: piece p indexed (stream -> stream2)
+    hipEvent_t pipe_done = nullptr;          // pipelined AF: stream2 drained
     std::string err;
     // input
     DevBuf input;
@@ -47,6 +50,7 @@ struct vcfxg_ctx {
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
         ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp;
+    DevBuf pipe_carry;          // pipelined AF: line number at the start of each piece
     DevBuf fuse_state;          // fused AF: per-chunk look-back words
     DevBuf af_meta;             // AF head pass output (k_af_meta)
     DevBuf scan_seg, nl_chunk;  // AF one-sweep path: per-chunk segment counts, newline -> chunk
@@ -58,6 +62,7 @@ struct vcfxg_ctx {
     // today, kept selectable for measurement
     int af_path = getenv("VCFXG_AF_FUSED") ? atoi(getenv("VCFXG_AF_FUSED")) : 0;
     int fuse_dbg = getenv("VCFXG_FUSE_DEBUG") ? atoi(getenv("VCFXG_FUSE_DEBUG")) : 0;  // diagnostics only
+    int64_t pipe_chunks = getenv("VCFXG_PIPE_CHUNKS") ? atol(getenv("VCFXG_PIPE_CHUNKS")) : 4096;  // 64 MiB pieces
     std::vector<uint8_t> ld_gflag_host;  // per 128-variant group: all complete
     uint64_t ld_m = 0, ld_prefix_bytes = 0;
     int ld_kpad = 64, ld_ns = 0, ld_kp4 = 64;
@@ -189,8 +194,12 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry})
         if (b->p) (void)hipFree(b->p);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
+    if (c->pipe_done) (void)hipEventDestroy(c->pipe_done);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
         (void)hipEventDestroy(kv.second.second);
@@ -410,11 +419,97 @@ static int af_region_scan(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     return af_rows(c, mode, out);
 }
 
+// Pipelined region path: the input is cut into pieces of whole 16 KiB wave-chunks.  On the
+// engine stream each piece is indexed (count sweep + in-kernel scan/compaction continuing
+// the line numbering from the previous piece, a device-side carry); on a second stream the
+// head pass and the fixed-stride sweep of that piece's lines follow as soon as its index is
+// published (one event per piece).  The sweep re-reads bytes the index sweep has just
+// pulled through the 256 MiB Infinity Cache, so the record pass is served largely on-die
+// while the index streams the next pieces from HBM.  No host synchronisation until the
+// end: line capacity is the hard bound 16 lines per chunk of the no-overflow case, and a
+// chunk with more newlines (lines under ~1 KiB) sends the whole call to the two-sweep path.
+static int af_region_pipe(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
+    const int64_t nc = vcfxg::idx_wchunks(lo, hi);
+    const int64_t piece = c->pipe_chunks;  // wave-chunks per piece
+    const int64_t np = (nc + piece - 1) / piece;
+    if (!nc || np < 2) {
+        int r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    const size_t pcap = (size_t)vcfxg::idx_pos_cap();
+    const uint64_t cap = (uint64_t)nc * pcap + 2;  // lines, when no chunk overflows
+    int r = ensure(c, c->idx_counts, sizeof(uint32_t) * (size_t)(nc + 1));
+    if (!r) r = ensure(c, c->idx_pos, sizeof(uint64_t) * (size_t)nc * pcap + 64);
+    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
+    if (!r) r = af_buffers(c, cap);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (cap + 1));
+    if (!r) r = ensure(c, c->pipe_carry, 8 * (size_t)(np + 2));
+    if (r) return r;
+    if (!c->stream2) HIPCHK(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    if (!c->pipe_done) HIPCHK(c, hipEventCreateWithFlags(&c->pipe_done, hipEventDisableTiming));
+    while ((int64_t)c->pipe_ev.size() < np) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->pipe_ev.push_back(e);
+    }
+    const char *buf = P<char>(c->input);
+    unsigned *overflow = reinterpret_cast<unsigned *>(P<uint64_t>(c->idx_pos) + (size_t)nc * pcap);
+    uint64_t *carry = P<uint64_t>(c->pipe_carry);
+    HIPCHK(c, hipMemsetAsync(overflow, 0, 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(carry, 0, 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    const bool tail = c->last_byte != '\n';
+    const int64_t a0 = lo & ~(int64_t)15, wb = vcfxg::idx_wchunk_bytes();
+    prof_begin(c, "af_pipe");
+    for (int64_t p = 0; p < np; p++) {
+        const int64_t c0 = p * piece, c1 = std::min(nc, c0 + piece);
+        const int64_t plo = p ? a0 + c0 * wb : lo, phi = std::min(hi, a0 + c1 * wb);
+        HIPCHK(c, vcfxg::launch_idx_count(buf, plo, phi, P<uint32_t>(c->idx_counts) + c0,
+                                          P<uint64_t>(c->idx_pos) + (size_t)c0 * pcap, overflow, c->stream));
+        HIPCHK(c, vcfxg::launch_nl_compact_piece(c1 - c0, P<uint32_t>(c->idx_counts) + c0,
+                                                 P<uint64_t>(c->idx_pos) + (size_t)c0 * pcap, carry + p, carry + p + 1,
+                                                 cap, P<uint64_t>(c->line_end), c->stream));
+        if (p == np - 1 && tail)
+            HIPCHK(c, vcfxg::launch_lines_tail(carry + p + 1, cap, hi, P<uint64_t>(c->line_end), c->stream));
+        HIPCHK(c, hipEventRecord(c->pipe_ev[p], c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->pipe_ev[p], 0));
+        HIPCHK(c, vcfxg::launch_af_meta_sweep_range(buf, lo, P<uint64_t>(c->line_end), carry + p,
+                                                    (uint64_t)(c1 - c0) * pcap + 2, mode, c->af_meta.p,
+                                                    P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                                    P<uint8_t>(c->status), P<unsigned long long>(c->counters),
+                                                    c->stream2));
+    }
+    HIPCHK(c, hipEventRecord(c->pipe_done, c->stream2));
+    HIPCHK(c, hipStreamWaitEvent(c->stream, c->pipe_done, 0));
+    HIPCHK(c, vcfxg::launch_af_complex(buf, lo, P<uint64_t>(c->line_end), carry + np, cap, mode, c->af_meta.p,
+                                       P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "af_pipe");
+    HIPCHK(c, hipMemcpyAsync(c->d_nlines.p, carry + np, 8, hipMemcpyDeviceToDevice, c->stream));
+    static thread_local uint64_t nl;
+    static thread_local unsigned ovf;
+    HIPCHK(c, hipMemcpyAsync(&nl, carry + np, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&ovf, overflow, sizeof ovf, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ovf) {  // some chunk holds more than idx_pos_cap() newlines: the two-sweep path
+        prof_collect(c);
+        r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    c->data_start = data_start;
+    c->n_lines = nl;
+    c->indexed = true;
+    return af_rows(c, mode, out);
+}
+
 int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
     if (c->af_path == 4) return af_region_scan(c, data_start, mode, out);
+    if (c->af_path == 5) return af_region_pipe(c, data_start, mode, out);
     const uint64_t nc = (c->af_path == 1 || c->af_path == 2) ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
     if (!nc) {  // default (also no data lines, or data_start == 0): index + record kernels
         int r = vcfxg_index(c, data_start, nullptr);

@@ -38,6 +38,15 @@ hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint6
                                 const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, void *meta, int32_t *alt,
                                 int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
                                 hipStream_t s);
+hipError_t launch_nl_compact_piece(int64_t nchunks, const uint32_t *counts, const uint64_t *pos,
+                                   const uint64_t *carry_in, uint64_t *carry_out, uint64_t cap, uint64_t *line_end,
+                                   hipStream_t s);
+hipError_t launch_lines_tail(uint64_t *carry, uint64_t cap, int64_t hi, uint64_t *line_end, hipStream_t s);
+hipError_t launch_af_meta_sweep_range(const char *buf, int64_t data_start, const uint64_t *line_end,
+                                      const uint64_t *range, uint64_t max_lines, int mode, void *meta, int32_t *alt,
+                                      int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
+                                      hipStream_t s);
+int64_t idx_wchunk_bytes();
 hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
                              int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,

@@ -81,6 +81,57 @@ __global__ void k_nl_compact(int64_t nchunks, const uint32_t *__restrict__ count
     line_end[offs[b] + k] = pos[i];
 }
 
+// Pipelined index (one piece of the input): the piece's chunk counts are scanned in place
+// -- each block sums the counts before its first chunk (a few thousand L2-resident words)
+// and scans its own 256 -- and the kept newline offsets land at line numbers continuing
+// from *carry_in; the last thread publishes *carry_out = *carry_in + the piece's lines.
+// Writes stop at `cap` (a chunk over kPosCap newlines sets the overflow flag in the count
+// sweep and the whole call falls back to the emit path, so clamped values are never used).
+constexpr int kCompactThreads = 256;
+__global__ __launch_bounds__(kCompactThreads) void k_nl_compact_piece(int64_t nchunks,
+                                                                      const uint32_t *__restrict__ counts,
+                                                                      const uint64_t *__restrict__ pos,
+                                                                      const uint64_t *carry_in, uint64_t *carry_out,
+                                                                      uint64_t cap, uint64_t *__restrict__ line_end) {
+    __shared__ uint64_t wsum[kCompactThreads / kWave];
+    __shared__ uint32_t wscan[kCompactThreads / kWave];
+    const int t = threadIdx.x, w = t / kWave;
+    const int64_t b0 = (int64_t)blockIdx.x * kCompactThreads;
+    uint64_t pre = 0;
+    for (int64_t k = t; k < b0; k += kCompactThreads) pre += counts[k];
+    pre = wave_sum(pre);
+    if (lane() == 0) wsum[w] = pre;
+    const int64_t c = b0 + t;
+    const uint32_t mine = c < nchunks ? counts[c] : 0u;
+    const uint32_t incl = wave_incl_scan(mine);
+    if (lane() == kWave - 1) wscan[w] = incl;
+    __syncthreads();
+    uint64_t before = 0;
+    uint32_t wbefore = 0;
+#pragma unroll
+    for (int k = 0; k < kCompactThreads / kWave; k++) {
+        before += wsum[k];
+        if (k < w) wbefore += wscan[k];
+    }
+    const uint64_t base = *carry_in + before + wbefore + incl - mine;
+    const uint32_t m = mine < (uint32_t)kPosCap ? mine : (uint32_t)kPosCap;
+    for (uint32_t k = 0; k < m; k++)
+        if (base + k < cap) line_end[base + k] = pos[(uint64_t)c * kPosCap + k];
+    if (blockIdx.x == gridDim.x - 1 && t == kCompactThreads - 1) {
+        const uint64_t end = base + mine;
+        *carry_out = end < cap ? end : cap;
+    }
+}
+
+// a last line without '\n' ends at hi: appended after the final piece
+__global__ void k_lines_tail(uint64_t *carry, uint64_t cap, int64_t hi, uint64_t *__restrict__ line_end) {
+    const uint64_t n = *carry;
+    if (n < cap) {
+        line_end[n] = (uint64_t)hi;
+        *carry = n + 1;
+    }
+}
+
 // =======================================================================================
 // K2: per-record GT reducers (allele counts, genotype match); one wave per line
 // =======================================================================================
@@ -216,12 +267,28 @@ __global__ __launch_bounds__(kRecThreads) void k_af_records(const char *__restri
 
 typedef LineMeta AfMeta;
 
+__device__ __forceinline__ void line_meta_one(const char *__restrict__ buf, int64_t data_start,
+                                              const uint64_t *__restrict__ line_end, uint64_t li, int strip_cr,
+                                              const uint8_t *__restrict__ gate, LineMeta *__restrict__ meta);
+
+// lines [0, n_lines), one thread each; with `range` (device [first, end), the pipelined AF
+// pieces) a grid-stride loop over [range[0], range[1]) instead
 __global__ __launch_bounds__(256) void k_line_meta(const char *__restrict__ buf, int64_t data_start,
                                                    const uint64_t *__restrict__ line_end, uint64_t n_lines,
                                                    int strip_cr, const uint8_t *__restrict__ gate,
-                                                   LineMeta *__restrict__ meta) {
-    const uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
-    if (li >= n_lines) return;
+                                                   LineMeta *__restrict__ meta, const uint64_t *range) {
+    const uint64_t gt = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (!range) {
+        if (gt < n_lines) line_meta_one(buf, data_start, line_end, gt, strip_cr, gate, meta);
+        return;
+    }
+    const uint64_t end = range[1], stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t li = range[0] + gt; li < end; li += stride) line_meta_one(buf, data_start, line_end, li, strip_cr, gate, meta);
+}
+
+__device__ __forceinline__ void line_meta_one(const char *__restrict__ buf, int64_t data_start,
+                                              const uint64_t *__restrict__ line_end, uint64_t li, int strip_cr,
+                                              const uint8_t *__restrict__ gate, LineMeta *__restrict__ meta) {
     LineMeta m{};
     if (gate && gate[li] != 1) {
         m.kind = kMetaGated;
@@ -285,15 +352,17 @@ __global__ __launch_bounds__(kRecThreads) void k_af_sweep(const char *__restrict
                                                           int32_t *__restrict__ alt_o, int32_t *__restrict__ tot_o,
                                                           uint32_t *__restrict__ rowpre_o,
                                                           uint8_t *__restrict__ status_o,
-                                                          unsigned long long *__restrict__ counters) {
+                                                          unsigned long long *__restrict__ counters,
+                                                          const uint64_t *first_p) {
     __shared__ uint32_t cnt[BlockCounters::kNC];
     if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
     __syncthreads();
     BlockCounters bc{cnt};
     const uint64_t n_lines = *n_lines_p;
+    const uint64_t first = first_p ? *first_p : 0;  // lines [first, n_lines)
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
-    for (uint64_t li = wid; li < n_lines; li += nw) {
+    for (uint64_t li = first + wid; li < n_lines; li += nw) {
         const AfMeta m = meta[li];
         uint8_t st = 0;
         uint32_t alt = 0, tot = 0, rowpre = 0;
@@ -826,6 +895,7 @@ static unsigned grid_for(int64_t n, int64_t per, unsigned cap) {
 }
 
 int idx_pos_cap() { return kPosCap; }
+int64_t idx_wchunk_bytes() { return kWChunk; }
 int64_t idx_wchunks(int64_t lo, int64_t hi) {
     const int64_t a0 = lo & ~(int64_t)15;
     return hi > lo ? (hi - a0 + kWChunk - 1) / kWChunk : 0;
@@ -899,6 +969,32 @@ hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64
     return hipGetLastError();
 }
 size_t af_meta_bytes() { return sizeof(AfMeta); }
+hipError_t launch_nl_compact_piece(int64_t nchunks, const uint32_t *counts, const uint64_t *pos,
+                                   const uint64_t *carry_in, uint64_t *carry_out, uint64_t cap, uint64_t *line_end,
+                                   hipStream_t s) {
+    if (nchunks <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_nl_compact_piece, dim3((unsigned)((nchunks + kCompactThreads - 1) / kCompactThreads)),
+                       dim3(kCompactThreads), 0, s, nchunks, counts, pos, carry_in, carry_out, cap, line_end);
+    return hipGetLastError();
+}
+hipError_t launch_lines_tail(uint64_t *carry, uint64_t cap, int64_t hi, uint64_t *line_end, hipStream_t s) {
+    hipLaunchKernelGGL(k_lines_tail, dim3(1), dim3(1), 0, s, carry, cap, hi, line_end);
+    return hipGetLastError();
+}
+// head pass + fixed-stride sweep over the device line range [range[0], range[1]) of one
+// pipelined piece (at most max_lines lines: sizes the grids)
+hipError_t launch_af_meta_sweep_range(const char *buf, int64_t data_start, const uint64_t *line_end,
+                                      const uint64_t *range, uint64_t max_lines, int mode, void *meta, int32_t *alt,
+                                      int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
+                                      hipStream_t s) {
+    if (!max_lines) return hipSuccess;
+    hipLaunchKernelGGL(k_line_meta, dim3(grid_for((int64_t)max_lines, 256, 2048)), dim3(256), 0, s, buf, data_start,
+                       line_end, (uint64_t)0, mode == 0 ? 1 : 0, nullptr, static_cast<AfMeta *>(meta), range);
+    unsigned grid = grid_for((int64_t)max_lines, kRecWaves, 4096);
+    hipLaunchKernelGGL(k_af_sweep, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, range + 1, mode,
+                       static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters, range);
+    return hipGetLastError();
+}
 hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
                              int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
@@ -915,10 +1011,10 @@ hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint6
                                 hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
     hipLaunchKernelGGL(k_line_meta, dim3((unsigned)((n_lines_host + 255) / 256)), dim3(256), 0, s, buf, data_start,
-                       line_end, n_lines_host, mode == 0 ? 1 : 0, nullptr, static_cast<AfMeta *>(meta));
+                       line_end, n_lines_host, mode == 0 ? 1 : 0, nullptr, static_cast<AfMeta *>(meta), nullptr);
     unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
     hipLaunchKernelGGL(k_af_sweep, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode,
-                       static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
+                       static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters, nullptr);
     unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
     hipLaunchKernelGGL(k_af_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
                        mode, static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
@@ -938,7 +1034,7 @@ hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t
     }
     LineMeta *lm = static_cast<LineMeta *>(meta);
     hipLaunchKernelGGL(k_line_meta, dim3((unsigned)((n_lines_host + 255) / 256)), dim3(256), 0, s, buf, data_start,
-                       line_end, n_lines_host, strip_cr, gate, lm);
+                       line_end, n_lines_host, strip_cr, gate, lm, nullptr);
     hipLaunchKernelGGL(k_gq_sweep, dim3(grid), dim3(kRecThreads), 0, s, buf, line_end, n_lines_dev, Q, lm, status,
                        counters, gate);
     unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
