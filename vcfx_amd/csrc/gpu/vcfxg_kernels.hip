@@ -362,12 +362,26 @@ __global__ __launch_bounds__(kRecThreads) void k_af_sweep(const char *__restrict
     const uint64_t first = first_p ? *first_p : 0;  // lines [first, n_lines)
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
-    for (uint64_t li = first + wid; li < n_lines; li += nw) {
-        const AfMeta m = meta[li];
+    // the next line's head record and end are loaded before this line's sweep (their
+    // latency hides behind it instead of opening every line)
+    uint64_t li = first + wid;
+    AfMeta mnext{};
+    uint64_t lenext = 0;
+    if (li < n_lines) {
+        mnext = meta[li];
+        lenext = line_end[li];
+    }
+    for (; li < n_lines; li += nw) {
+        const AfMeta m = mnext;
+        const uint64_t lecur = lenext;
+        if (li + nw < n_lines) {
+            mnext = meta[li + nw];
+            lenext = line_end[li + nw];
+        }
         uint8_t st = 0;
         uint32_t alt = 0, tot = 0, rowpre = 0;
         if (m.kind == kMetaGt) {
-            const int64_t le = (int64_t)line_end[li], ae = le - m.cr;
+            const int64_t le = (int64_t)lecur, ae = le - m.cr;
             bc.add(1, 1);
             bc.add(0, 1);
             AfOp op{buf, ae, 0};
