@@ -106,3 +106,22 @@ def test_ld_fast_blocks_across_groups(oracle, knock):
             got = tools.run(argv, b"")
             want = oracle.run(argv, b"")
             assert got == want, (a, knock, len(got[0]), len(want[0]))
+
+
+def test_ld_staging_overflow_falls_back(oracle):
+    """A staging area too small for the count pass's pairs: the emit pass recomputes them
+    (same bytes); and a roomy one: the scatter path."""
+    import os
+    buf = synth.generate(700, 150, 59, 0, 0.0, 1, 0.0, 0)
+    with tempfile.NamedTemporaryFile(suffix=".vcf") as f:
+        f.write(buf)
+        f.flush()
+        argv = ["VCFX_ld_calculator", "-w", "700", "-t", "0.2", "-i", f.name]
+        want = oracle.run(argv, b"")
+        for cap in ("7", "100000000"):
+            os.environ["VCFXG_LD_STAGE_CAP"] = cap
+            try:
+                got = tools.run(argv, b"")
+            finally:
+                del os.environ["VCFXG_LD_STAGE_CAP"]
+            assert got == want, cap

@@ -51,6 +51,10 @@ struct vcfxg_ctx {
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
         ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp;
     DevBuf pipe_carry;          // pipelined AF: line number at the start of each piece
+    DevBuf ld_temp, ld_quarters, ld_stage_ctr;  // LD: pairs staged by the count pass
+    uint64_t ld_temp_cap = 0;
+    // test hook: a fixed (small) staging capacity exercises the overflow -> emit-pass path
+    uint64_t ld_stage_cap_fixed = getenv("VCFXG_LD_STAGE_CAP") ? strtoull(getenv("VCFXG_LD_STAGE_CAP"), nullptr, 10) : 0;
     DevBuf fuse_state;          // fused AF: per-chunk look-back words
     DevBuf af_meta;             // AF head pass output (k_af_meta)
     DevBuf scan_seg, nl_chunk;  // AF one-sweep path: per-chunk segment counts, newline -> chunk
@@ -194,7 +198,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr})
         if (b->p) (void)hipFree(b->p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
@@ -1043,9 +1047,28 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     a.kp4 = c->ld_kp4;
     const uint32_t *cid = max_dist > 0 ? P<uint32_t>(c->ld_cid) : nullptr;
     const uint32_t *fbl = P<uint32_t>(c->ld_blocks), *gbl = fbl + 2 * (size_t)nfast;
+    // staging for the pairs the count pass finds (capacity: what the last chunk needed, at
+    // least 4 M pairs; a larger chunk overflows once and the emit pass recomputes)
+    vcfxg::LdStage stg;
+    {
+        const uint64_t qcap = 16ull * nfast + 16;
+        const uint64_t tcap = c->ld_stage_cap_fixed ? c->ld_stage_cap_fixed : std::max<uint64_t>(c->ld_temp_cap, 4ull << 20);
+        int r0 = ensure(c, c->ld_temp, sizeof(vcfxg::LdPair) * tcap);
+        if (!r0) r0 = ensure(c, c->ld_quarters, sizeof(vcfxg::LdQuarter) * qcap);
+        if (!r0) r0 = ensure(c, c->ld_stage_ctr, 64);
+        if (r0) return r0;
+        HIPCHK(c, hipMemsetAsync(c->ld_stage_ctr.p, 0, 64, c->stream));
+        // (the register count path, n <= 23170, is the one that stages)
+        stg.temp = c->ld_ns <= 23170 ? P<vcfxg::LdPair>(c->ld_temp) : nullptr;
+        stg.cap = tcap;
+        stg.quarters = P<vcfxg::LdQuarter>(c->ld_quarters);
+        stg.qcap = qcap;
+        stg.ctr = P<unsigned long long>(c->ld_stage_ctr);
+        stg.overflow = reinterpret_cast<unsigned *>(P<unsigned long long>(c->ld_stage_ctr) + 2);
+    }
     prof_begin(c, "ld_count");
     HIPCHK(c, vcfxg::launch_ld_fast(1, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
-                                    P<uint16_t>(c->ld_cnt), nullptr, nullptr, c->stream));
+                                    P<uint16_t>(c->ld_cnt), nullptr, nullptr, stg, c->stream));
     prof_end(c, "ld_count");
     prof_begin(c, "ld_count_gen");
     HIPCHK(c, vcfxg::launch_ld_block(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,
@@ -1058,18 +1081,26 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     r = ensure(c, c->scan_tmp, tmp);
     if (r) return r;
     HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, cin, P<uint64_t>(c->ld_off), (int)ncnt, c->stream));
-    static thread_local uint64_t tot;
+    static thread_local uint64_t tot, sctr[3];
     HIPCHK(c, hipMemcpyAsync(&tot, P<uint64_t>(c->ld_off) + rows * nb, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(sctr, c->ld_stage_ctr.p, 24, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const uint64_t np = tot;
+    const bool staged = stg.temp && (sctr[2] & 0xFFFFFFFFull) == 0;  // staged, no overflow
+    c->ld_temp_cap = std::max<uint64_t>(c->ld_temp_cap, sctr[0] + sctr[0] / 4);
     r = ensure(c, c->ld_pairs, sizeof(vcfxg::LdPair) * (np + 1));
     if (!r) r = ensure(c, c->rowlen, 8 * (np + 1));
     if (!r) r = ensure(c, c->rowoff, 8 * (np + 1));
     if (r) return r;
     prof_begin(c, "ld_emit");
-    HIPCHK(c, vcfxg::launch_ld_fast(2, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
-                                    P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off), P<vcfxg::LdPair>(c->ld_pairs),
-                                    c->stream));
+    if (staged)
+        HIPCHK(c, vcfxg::launch_ld_scatter(P<vcfxg::LdQuarter>(c->ld_quarters), P<unsigned long long>(c->ld_stage_ctr),
+                                           sctr[1], a, P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off),
+                                           P<vcfxg::LdPair>(c->ld_temp), P<vcfxg::LdPair>(c->ld_pairs), c->stream));
+    else
+        HIPCHK(c, vcfxg::launch_ld_fast(2, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
+                                        P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off), P<vcfxg::LdPair>(c->ld_pairs),
+                                        vcfxg::LdStage{}, c->stream));
     prof_end(c, "ld_emit");
     prof_begin(c, "ld_emit_gen");
     HIPCHK(c, vcfxg::launch_ld_block(2, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,

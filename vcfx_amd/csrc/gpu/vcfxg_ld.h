@@ -73,9 +73,26 @@ hipError_t launch_ld_parse(const char *buf, int64_t data_start, const uint64_t *
 hipError_t launch_ld_compact(const LdLine *lines, const uint64_t *vidx, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int kpad, int ns, const int8_t *G, int8_t *Gc, LdVar *vars,
                              LdFast *fv, hipStream_t s);
+// count pass of the fast kernel staging the pairs of every quarter that holds some
+// (quarters[] records where each went); overflow -> the emit pass recomputes them
+struct LdQuarter {
+    uint32_t bI, bJ;  // 64-blocks: column block (rows i) and row block (variants j)
+    uint64_t base;    // first staged pair
+};
+struct LdStage {
+    LdPair *temp = nullptr;               // nullptr: count only
+    uint64_t cap = 0;                     // staged-pair capacity
+    LdQuarter *quarters = nullptr;
+    uint64_t qcap = 0;
+    unsigned long long *ctr = nullptr;    // [0] staged pairs, [1] quarters
+    unsigned *overflow = nullptr;
+};
+hipError_t launch_ld_scatter(const LdQuarter *quarters, const unsigned long long *ctr, uint64_t nq_host,
+                             const LdWindowArgs &a, const uint16_t *cnt, const uint64_t *off, const LdPair *temp,
+                             LdPair *pairs, hipStream_t s);
 hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const uint32_t *chrom_id,
                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
-                          const uint64_t *off, LdPair *pairs, hipStream_t s);
+                          const uint64_t *off, LdPair *pairs, const LdStage &st, hipStream_t s);
 hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, uint8_t *gflag, hipStream_t s);
 hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s);
 hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C, hipStream_t s);

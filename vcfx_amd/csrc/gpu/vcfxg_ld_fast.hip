@@ -98,7 +98,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdWindowArgs &a,
                                               const LdFast *__restrict__ fv, const uint32_t *__restrict__ chrom_id,
                                               uint16_t *__restrict__ cnt, const float *ru, const float *rsf,
-                                              uint32_t I4, uint32_t J4, int wi, int wj, int h, int r) {
+                                              uint32_t I4, uint32_t J4, int wi, int wj, int h, int r,
+                                              int (&qtot)[2]) {
     const int64_t M = (int64_t)a.m;
     const double dn = (double)a.ns;
     const uint64_t bI = 4ull * I4 + wi;
@@ -195,7 +196,10 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
         const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
         if (h == 0 && jok && bI >= ifirst && bI <= bJ)
             cnt[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + (bI - ifirst)] = (uint16_t)tot;
+        nc[y] = h == 0 && jok && bI >= ifirst && bI <= bJ ? tot : 0;
     }
+    qtot[0] = wave_sum(nc[0] + nc[1]);  // quarter hy = columns of tiles 2hy, 2hy+1
+    qtot[1] = wave_sum(nc[2] + nc[3]);
 }
 
 template <int P>
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
                                                             const uint32_t *__restrict__ blocks, uint32_t nblocks,
                                                             uint16_t *__restrict__ cnt,
                                                             const uint64_t *__restrict__ off,
-                                                            LdPair *__restrict__ pairs) {
+                                                            LdPair *__restrict__ pairs, LdStage st) {
     // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
     // ds_reads): the staging ring during the k-loop, then the waves' epilogue tiles over it;
     // the per-row prefilter terms after that
@@ -355,13 +359,6 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
         if (z == 0x7fffffff) cnt[0] = 1;
         return;
     }
-    if (P == 1 && a.ns <= 23170) {
-        __syncthreads();  // the row terms written before the k-loop are visible to every wave
-        ld_count_regs(acc, a, fv, chrom_id, cnt, ru, rsf, I4, J4, wi, wj, h, r);
-        return;
-    }
-    __syncthreads();  // every wave is done reading the ring; the epilogue tiles reuse it
-    int *tile = reinterpret_cast<int *>(lds + w * kQuarter);
     const int pad = 0;  // FP4 rows are zero-padded
     const double dn = (double)a.ns;
     const int64_t n = a.ns;
@@ -371,11 +368,10 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
     const bool f32 = a.ns <= 23170;
     const uint64_t bI = 4ull * I4 + wi;
     const int64_t i0 = (int64_t)bI * kLdBlock;
-#pragma unroll
-    for (int hy = 0; hy < 2; hy++) {  // the wave's two 64x64 quarters (columns hy*64..)
-        const uint64_t bJ = 4ull * J4 + 2 * wj + hy;
-        uint64_t slot;
-        if (!sub(bI, bJ, slot)) continue;  // wave-uniform: a quarter outside the window triangle
+    int *tile = reinterpret_cast<int *>(lds + w * kQuarter);
+    // quarter hy (columns hy*64.. of the wave) through this wave's LDS tile: lane l walks
+    // column j's rows and returns the mask of the rows whose pair passes (exact decision)
+    auto walk = [&](int hy, int64_t j, bool jok, LdFast &fj) -> uint64_t {
         // the quarter's accumulators -> this wave's LDS tile [row][col] (no other wave uses
         // it, and the wave's own lanes are in lockstep: no barrier between quarters)
 #pragma unroll
@@ -385,10 +381,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
 #pragma unroll
                 for (int k = 0; k < 16; k++)
                     tile[(32 * x + (k & 3) + 8 * (k >> 2) + 4 * h) * 64 + 32 * yy + r] = (int)acc[x][2 * hy + yy][k];
-        const int64_t j = (int64_t)(bJ * kLdBlock) + l;
-        const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
         uint64_t mask = 0;
-        LdFast fj{};
         if (jok) {
             fj = fv[j];
             const uint32_t cj = a.max_dist > 0 ? chrom_id[j] : 0u;
@@ -420,12 +413,9 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
                 if (ld_fast_r2(fi, fj, sxy, dn) >= a.threshold) mask |= 1ull << row;
             }
         }
-        if (P == 1) {
-            if (jok) cnt[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot] = (uint16_t)__popcll(mask);
-            continue;
-        }
-        if (!mask) continue;
-        const uint64_t pbase = off[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot];
+        return mask;
+    };
+    auto write_pairs = [&](uint64_t mask, int64_t j, const LdFast &fj, LdPair *dst) {
         uint32_t rank = 0;
         while (mask) {
             const int row = __builtin_ctzll(mask);
@@ -434,22 +424,110 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
             pr.i = (uint32_t)(i0 + row);
             pr.j = (uint32_t)j;
             pr.r2 = ld_fast_r2(fv[i0 + row], fj, tile[row * 64 + l] - pad, dn);
-            pairs[pbase + rank++] = pr;
+            dst[rank++] = pr;
         }
+    };
+    if (P == 1 && a.ns <= 23170) {
+        __syncthreads();  // the row terms written before the k-loop are visible to every wave
+        int qt[2];
+        ld_count_regs(acc, a, fv, chrom_id, cnt, ru, rsf, I4, J4, wi, wj, h, r, qt);
+        if (!st.temp) return;
+        // quarters holding pairs: written now, column-major into a bump-allocated staging
+        // area (ld_scatter later moves each column's run to its ordered offset), so the
+        // emit pass needs no second MFMA sweep
+#pragma unroll
+        for (int hy = 0; hy < 2; hy++) {
+            if (!qt[hy]) continue;  // wave-uniform
+            const uint64_t bJ = 4ull * J4 + 2 * wj + hy;
+            const int64_t j = (int64_t)(bJ * kLdBlock) + l;
+            const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
+            LdFast fj{};
+            const uint64_t mask = walk(hy, j, jok, fj);
+            const uint32_t c = (uint32_t)__popcll(mask);
+            const uint32_t incl = wave_incl_scan(c);
+            const uint32_t total = wave_bcast(incl, kWave - 1);
+            unsigned long long base = 0;
+            if (l == 0) base = atomicAdd(st.ctr, (unsigned long long)total);
+            base = __shfl(base, 0);
+            if (base + total > st.cap) {
+                if (l == 0) atomicOr(st.overflow, 1u);
+                continue;
+            }
+            write_pairs(mask, j, fj, st.temp + base + (incl - c));
+            if (l == 0) {
+                const unsigned long long q = atomicAdd(st.ctr + 1, 1ull);
+                if (q < st.qcap) st.quarters[q] = LdQuarter{(uint32_t)bI, (uint32_t)bJ, (uint64_t)base};
+                else atomicOr(st.overflow, 1u);
+            }
+        }
+        return;
     }
+    __syncthreads();  // every wave is done reading the ring; the epilogue tiles reuse it
+#pragma unroll
+    for (int hy = 0; hy < 2; hy++) {  // the wave's two 64x64 quarters (columns hy*64..)
+        const uint64_t bJ = 4ull * J4 + 2 * wj + hy;
+        uint64_t slot;
+        if (!sub(bI, bJ, slot)) continue;  // wave-uniform: a quarter outside the window triangle
+        const int64_t j = (int64_t)(bJ * kLdBlock) + l;
+        const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
+        LdFast fj{};
+        const uint64_t mask = walk(hy, j, jok, fj);
+        if (P == 1) {
+            if (jok) cnt[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot] = (uint16_t)__popcll(mask);
+            continue;
+        }
+        if (!mask) continue;
+        write_pairs(mask, j, fj, pairs + off[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot]);
+    }
+}
+
+// staged pairs -> their ordered offsets: one wave per staged quarter, lane = column j; the
+// column's run starts after the runs of the quarter's earlier columns (the same wave scan
+// that laid them out) and goes to off[j][slot]
+__global__ __launch_bounds__(256) void k_ld_scatter(const LdQuarter *__restrict__ quarters,
+                                                    const unsigned long long *__restrict__ ctr, LdWindowArgs a,
+                                                    const uint16_t *__restrict__ cnt, const uint64_t *__restrict__ off,
+                                                    const LdPair *__restrict__ temp, LdPair *__restrict__ pairs) {
+    const uint64_t nq = ctr[1];
+    const int l = threadIdx.x & 63;
+    const int64_t M = (int64_t)a.m;
+    for (uint64_t q = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 64; q < nq;
+         q += (uint64_t)gridDim.x * blockDim.x / 64) {
+        const LdQuarter Q = quarters[q];
+        const uint64_t jrow0 = (uint64_t)Q.bJ * kLdBlock;
+        const uint64_t ifirst = jrow0 > a.window ? (jrow0 - a.window) / kLdBlock : 0;
+        const int64_t j = (int64_t)jrow0 + l;
+        const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
+        const uint64_t e = jok ? (uint64_t)(j - (int64_t)a.j_lo) * a.nb + (Q.bI - ifirst) : 0;
+        const uint32_t c = jok ? cnt[e] : 0u;
+        const uint32_t incl = wave_incl_scan(c);
+        const LdPair *src = temp + Q.base + (incl - c);
+        LdPair *dst = pairs + (jok ? off[e] : 0);
+        for (uint32_t k = 0; k < c; k++) dst[k] = src[k];
+    }
+}
+
+hipError_t launch_ld_scatter(const LdQuarter *quarters, const unsigned long long *ctr, uint64_t nq_host,
+                             const LdWindowArgs &a, const uint16_t *cnt, const uint64_t *off, const LdPair *temp,
+                             LdPair *pairs, hipStream_t s) {
+    if (!nq_host) return hipSuccess;
+    const uint64_t blocks = (nq_host + 3) / 4;
+    hipLaunchKernelGGL(k_ld_scatter, dim3((unsigned)std::min<uint64_t>(blocks, 65536)), dim3(256), 0, s, quarters, ctr,
+                       a, cnt, off, temp, pairs);
+    return hipGetLastError();
 }
 
 hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const uint32_t *chrom_id,
                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
-                          const uint64_t *off, LdPair *pairs, hipStream_t s) {
+                          const uint64_t *off, LdPair *pairs, const LdStage &st, hipStream_t s) {
     if (!nblocks) return hipSuccess;
     if (a.kp4 % kBK || a.kp4 <= 0) return hipErrorInvalidValue;
     if (pass == 1)
         hipLaunchKernelGGL(k_ld_fast<1>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
-                           nblocks, cnt, off, pairs);
+                           nblocks, cnt, off, pairs, st);
     else
         hipLaunchKernelGGL(k_ld_fast<2>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
-                           nblocks, cnt, off, pairs);
+                           nblocks, cnt, off, pairs, st);
     return hipGetLastError();
 }
 
