@@ -49,7 +49,7 @@ struct vcfxg_ctx {
     std::string query_host, crit_host, pool_host;  // host sources of in-flight async copies
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
-        ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp;
+        ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff;
     DevBuf pipe_carry;          // pipelined AF: line number at the start of each piece
     DevBuf ld_temp, ld_quarters, ld_stage_ctr;  // LD: pairs staged by the count pass
     uint64_t ld_temp_cap = 0;
@@ -198,7 +198,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff})
         if (b->p) (void)hipFree(b->p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
@@ -1033,12 +1033,13 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     const uint64_t rows = j1 - j0;
     int r = ensure(c, c->ld_blocks, 4 * blocks.size() + 8);
     if (!r) r = ensure(c, c->ld_cnt, 2 * rows * nb + 16);
-    if (!r) r = ensure(c, c->ld_off, 8 * (rows * nb + 1));
+    if (!r) r = ensure(c, c->ld_off, 4 * (rows * nb + 1));  // u32 offsets inside each row
+    if (!r) r = ensure(c, c->ld_rowoff, 16 * (rows + 1));      // row totals, then row starts
     if (r) return r;
     c->ld_blocks_host.swap(blocks);
     HIPCHK(c, hipMemcpyAsync(c->ld_blocks.p, c->ld_blocks_host.data(), 4 * c->ld_blocks_host.size(),
                              hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->ld_cnt.p, 0, 2 * rows * nb + 16, c->stream));
+    // (no clearing of ld_cnt: the count kernels write every window slot the row scan reads)
     vcfxg::LdWindowArgs a{M, c->ld_kpad, c->ld_ns, window, threshold, max_dist, j0, j1, nb, 0.0, 0};
     // prefilter margin: |fp64 r^2 - exact r^2| of the reference's sequence is < ~1.2e-14 * n
     // (vx >= (n-1)/n^2 for a polymorphic complete variant); delta covers it 100-fold
@@ -1068,21 +1069,24 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     }
     prof_begin(c, "ld_count");
     HIPCHK(c, vcfxg::launch_ld_fast(1, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
-                                    P<uint16_t>(c->ld_cnt), nullptr, nullptr, stg, c->stream));
+                                    P<uint16_t>(c->ld_cnt), vcfxg::LdOffsets{}, nullptr, stg, c->stream));
     prof_end(c, "ld_count");
     prof_begin(c, "ld_count_gen");
     HIPCHK(c, vcfxg::launch_ld_block(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,
-                                     P<uint16_t>(c->ld_cnt), nullptr, nullptr, c->stream));
+                                     P<uint16_t>(c->ld_cnt), vcfxg::LdOffsets{}, nullptr, c->stream));
     prof_end(c, "ld_count_gen");
-    hipcub::TransformInputIterator<uint64_t, U16ToU64, const uint16_t *> cin(P<uint16_t>(c->ld_cnt), U16ToU64());
-    const size_t ncnt = rows * nb + 1;  // +1: the zeroed pad entry gives the total
-    size_t tmp = 0;
-    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, cin, P<uint64_t>(c->ld_off), (int)ncnt, c->stream));
-    r = ensure(c, c->scan_tmp, tmp);
+    // ordered offsets: per-row scan of the count table (u32 inside a row), then the rows
+    uint64_t *rowtot = P<uint64_t>(c->ld_rowoff), *rowbase = rowtot + (rows + 1);
+    HIPCHK(c, vcfxg::launch_ld_rowscan(P<uint16_t>(c->ld_cnt), rows, nb, j0, window, P<uint32_t>(c->ld_off), rowtot,
+                                       c->stream));
+    HIPCHK(c, hipMemsetAsync(rowtot + rows, 0, 8, c->stream));
+    r = exclusive_scan(c, rowtot, rowbase, (size_t)rows + 1);
     if (r) return r;
-    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, cin, P<uint64_t>(c->ld_off), (int)ncnt, c->stream));
+    vcfxg::LdOffsets offs;
+    offs.row = rowbase;
+    offs.in_row = P<uint32_t>(c->ld_off);
     static thread_local uint64_t tot, sctr[3];
-    HIPCHK(c, hipMemcpyAsync(&tot, P<uint64_t>(c->ld_off) + rows * nb, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tot, rowbase + rows, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(sctr, c->ld_stage_ctr.p, 24, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const uint64_t np = tot;
@@ -1095,16 +1099,16 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     prof_begin(c, "ld_emit");
     if (staged)
         HIPCHK(c, vcfxg::launch_ld_scatter(P<vcfxg::LdQuarter>(c->ld_quarters), P<unsigned long long>(c->ld_stage_ctr),
-                                           sctr[1], a, P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off),
+                                           sctr[1], a, P<uint16_t>(c->ld_cnt), offs,
                                            P<vcfxg::LdPair>(c->ld_temp), P<vcfxg::LdPair>(c->ld_pairs), c->stream));
     else
         HIPCHK(c, vcfxg::launch_ld_fast(2, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
-                                        P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off), P<vcfxg::LdPair>(c->ld_pairs),
+                                        P<uint16_t>(c->ld_cnt), offs, P<vcfxg::LdPair>(c->ld_pairs),
                                         vcfxg::LdStage{}, c->stream));
     prof_end(c, "ld_emit");
     prof_begin(c, "ld_emit_gen");
     HIPCHK(c, vcfxg::launch_ld_block(2, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,
-                                     P<uint16_t>(c->ld_cnt), P<uint64_t>(c->ld_off), P<vcfxg::LdPair>(c->ld_pairs),
+                                     P<uint16_t>(c->ld_cnt), offs, P<vcfxg::LdPair>(c->ld_pairs),
                                      c->stream));
     prof_end(c, "ld_emit_gen");
     HIPCHK(c, vcfxg::launch_ld_pairtext(0, P<vcfxg::LdPair>(c->ld_pairs), np, P<uint64_t>(c->ld_poff), nullptr,

@@ -73,6 +73,18 @@ hipError_t launch_ld_parse(const char *buf, int64_t data_start, const uint64_t *
 hipError_t launch_ld_compact(const LdLine *lines, const uint64_t *vidx, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int kpad, int ns, const int8_t *G, int8_t *Gc, LdVar *vars,
                              LdFast *fv, hipStream_t s);
+// ordered output offset of pair slot (row j - j_lo, column block slot): the row's first
+// pair (exclusive scan over rows) + the slot's offset inside the row (per-row scan, u32)
+struct LdOffsets {
+    const uint64_t *row = nullptr;
+    const uint32_t *in_row = nullptr;
+    __device__ __forceinline__ uint64_t at(uint64_t jrel, uint64_t nb, uint64_t slot) const {
+        return row[jrel] + in_row[jrel * nb + slot];
+    }
+};
+hipError_t launch_ld_rowscan(const uint16_t *cnt, uint64_t rows, uint64_t nb, uint64_t j_lo, uint64_t window,
+                             uint32_t *in_row, uint64_t *rowtot, hipStream_t s);
+
 // count pass of the fast kernel staging the pairs of every quarter that holds some
 // (quarters[] records where each went); overflow -> the emit pass recomputes them
 struct LdQuarter {
@@ -88,11 +100,11 @@ struct LdStage {
     unsigned *overflow = nullptr;
 };
 hipError_t launch_ld_scatter(const LdQuarter *quarters, const unsigned long long *ctr, uint64_t nq_host,
-                             const LdWindowArgs &a, const uint16_t *cnt, const uint64_t *off, const LdPair *temp,
+                             const LdWindowArgs &a, const uint16_t *cnt, LdOffsets off, const LdPair *temp,
                              LdPair *pairs, hipStream_t s);
 hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const uint32_t *chrom_id,
                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
-                          const uint64_t *off, LdPair *pairs, const LdStage &st, hipStream_t s);
+                          LdOffsets off, LdPair *pairs, const LdStage &st, hipStream_t s);
 hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, uint8_t *gflag, hipStream_t s);
 hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s);
 hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C, hipStream_t s);
@@ -100,7 +112,7 @@ hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C,
 inline int ld_kp4(int ns) { return ns > 0 ? ((ns + 127) / 128) * 64 : 64; }
 hipError_t launch_ld_block(int pass, const int8_t *Gc, const LdVar *vars, const uint32_t *chrom_id,
                            const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
-                           const uint64_t *off, LdPair *pairs, hipStream_t s);
+                           LdOffsets off, LdPair *pairs, hipStream_t s);
 hipError_t launch_ld_prefix(int which, const LdVar *vars, uint64_t m, const char *buf, int id_dot_to_pos,
                             uint64_t *len_or_off, char *out, hipStream_t s);
 hipError_t launch_ld_pairtext(int which, const LdPair *pairs, uint64_t np, const uint64_t *poff, const char *prefix,

@@ -387,7 +387,7 @@ template <int P>  // P = 1: count pass, 2: emit pass
 __global__ __launch_bounds__(256) void k_ld_block(const int8_t *__restrict__ Gc, const LdVar *__restrict__ vars,
                                                   const uint32_t *__restrict__ chrom_id, LdWindowArgs a,
                                                   const uint32_t *__restrict__ blocks, uint16_t *__restrict__ cnt,
-                                                  const uint64_t *__restrict__ off, LdPair *__restrict__ pairs) {
+                                                  LdOffsets off, LdPair *__restrict__ pairs) {
     __shared__ uint32_t masks[kBM][kBM / 32];
     const int w = threadIdx.x / kWave;
     const int it = w >> 1, jt = w & 1;
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(256) void k_ld_block(const int8_t *__restrict__ Gc,
         return;
     }
     if (!jok || !bits) return;
-    const uint64_t base = off[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot_col];
+    const uint64_t base = off.at((uint64_t)(j - (int64_t)a.j_lo), a.nb, slot_col);
     const uint32_t above = it ? __popc(masks[jt * 32 + r][0]) : 0u;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -670,7 +670,7 @@ hipError_t launch_ld_compact(const LdLine *lines, const uint64_t *vidx, const ui
 }
 hipError_t launch_ld_block(int pass, const int8_t *Gc, const LdVar *vars, const uint32_t *chrom_id,
                            const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
-                           const uint64_t *off, LdPair *pairs, hipStream_t s) {
+                           LdOffsets off, LdPair *pairs, hipStream_t s) {
     if (!nblocks) return hipSuccess;
     if (pass == 1)
         hipLaunchKernelGGL(k_ld_block<1>, dim3(nblocks), dim3(256), 0, s, Gc, vars, chrom_id, a, blocks, cnt, off,

@@ -116,7 +116,7 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
         jv[y] = j;
         const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
         const LdFast f = fv[jok ? j : 0];
-        wv[y] = -(float)f.sx / (float)a.ns;
+        wv[y] = a.ns > 0 ? -(float)f.sx / (float)a.ns : 0.f;  // (n = 0: every r^2 is 0, no NaN)
         vj[y] = a.all_pass ? 0.f : sqrtf((float)f.vxp);
         // valid rows [lo, lo + span) of the 64-block: i in [j - window, j)
         const int64_t l0 = j - (int64_t)a.window - i0;
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
                                                             const uint32_t *__restrict__ chrom_id, LdWindowArgs a,
                                                             const uint32_t *__restrict__ blocks, uint32_t nblocks,
                                                             uint16_t *__restrict__ cnt,
-                                                            const uint64_t *__restrict__ off,
+                                                            LdOffsets off,
                                                             LdPair *__restrict__ pairs, LdStage st) {
     // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
     // ds_reads): the staging ring during the k-loop, then the waves' epilogue tiles over it;
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
     // the epilogue's pointer arguments, consumed here: left to itself the compiler hoists their
     // scalar loads over the loop, and a pending SMEM load (out of order within lgkmcnt) turns
     // every fragment wait in the loop into lgkmcnt(0)
-    asm volatile("" ::"s"(cnt), "s"(chrom_id), "s"(off), "s"(pairs));
+    asm volatile("" ::"s"(cnt), "s"(chrom_id), "s"(pairs));
     for (int q = 0; q < kNBuf - 1; q++) stage(q < nk ? q : nk - 1, q);
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
             continue;
         }
         if (!mask) continue;
-        write_pairs(mask, j, fj, pairs + off[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot]);
+        write_pairs(mask, j, fj, pairs + off.at((uint64_t)(j - (int64_t)a.j_lo), a.nb, slot));
     }
 }
 
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
 // that laid them out) and goes to off[j][slot]
 __global__ __launch_bounds__(256) void k_ld_scatter(const LdQuarter *__restrict__ quarters,
                                                     const unsigned long long *__restrict__ ctr, LdWindowArgs a,
-                                                    const uint16_t *__restrict__ cnt, const uint64_t *__restrict__ off,
+                                                    const uint16_t *__restrict__ cnt, LdOffsets off,
                                                     const LdPair *__restrict__ temp, LdPair *__restrict__ pairs) {
     const uint64_t nq = ctr[1];
     const int l = threadIdx.x & 63;
@@ -498,17 +498,17 @@ __global__ __launch_bounds__(256) void k_ld_scatter(const LdQuarter *__restrict_
         const uint64_t ifirst = jrow0 > a.window ? (jrow0 - a.window) / kLdBlock : 0;
         const int64_t j = (int64_t)jrow0 + l;
         const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
-        const uint64_t e = jok ? (uint64_t)(j - (int64_t)a.j_lo) * a.nb + (Q.bI - ifirst) : 0;
-        const uint32_t c = jok ? cnt[e] : 0u;
+        const uint64_t jrel = jok ? (uint64_t)(j - (int64_t)a.j_lo) : 0, slot = Q.bI - ifirst;
+        const uint32_t c = jok ? cnt[jrel * a.nb + slot] : 0u;
         const uint32_t incl = wave_incl_scan(c);
         const LdPair *src = temp + Q.base + (incl - c);
-        LdPair *dst = pairs + (jok ? off[e] : 0);
+        LdPair *dst = pairs + (jok ? off.at(jrel, a.nb, slot) : 0);
         for (uint32_t k = 0; k < c; k++) dst[k] = src[k];
     }
 }
 
 hipError_t launch_ld_scatter(const LdQuarter *quarters, const unsigned long long *ctr, uint64_t nq_host,
-                             const LdWindowArgs &a, const uint16_t *cnt, const uint64_t *off, const LdPair *temp,
+                             const LdWindowArgs &a, const uint16_t *cnt, LdOffsets off, const LdPair *temp,
                              LdPair *pairs, hipStream_t s) {
     if (!nq_host) return hipSuccess;
     const uint64_t blocks = (nq_host + 3) / 4;
@@ -519,7 +519,7 @@ hipError_t launch_ld_scatter(const LdQuarter *quarters, const unsigned long long
 
 hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const uint32_t *chrom_id,
                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
-                          const uint64_t *off, LdPair *pairs, const LdStage &st, hipStream_t s) {
+                          LdOffsets off, LdPair *pairs, const LdStage &st, hipStream_t s) {
     if (!nblocks) return hipSuccess;
     if (a.kp4 % kBK || a.kp4 <= 0) return hipErrorInvalidValue;
     if (pass == 1)
@@ -583,6 +583,41 @@ __global__ void k_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C)
 
 hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C, hipStream_t s) {
     hipLaunchKernelGGL(k_mfma_f4_selftest, dim3(1), dim3(64), 0, s, A, B, C);
+    return hipGetLastError();
+}
+
+// per-row scan of the pair-count table: one wave per output row j, the u16 counts of its
+// window slots (column blocks ifirst(J) .. J, every one written by the count kernels; the
+// table is not cleared) -> u32 offsets inside the row + the row's total
+__global__ __launch_bounds__(256) void k_ld_rowscan(const uint16_t *__restrict__ cnt, uint64_t rows, uint64_t nb,
+                                                    uint64_t j_lo, uint64_t window, uint32_t *__restrict__ in_row,
+                                                    uint64_t *__restrict__ rowtot) {
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const int l = threadIdx.x & 63;
+    for (uint64_t j = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 64; j < rows; j += nw) {
+        const uint64_t J = (j_lo + j) / kLdBlock, jr0 = J * kLdBlock;
+        const uint64_t I0 = jr0 > window ? (jr0 - window) / kLdBlock : 0;
+        const uint64_t ns = J - I0 + 1 < nb ? J - I0 + 1 : nb;
+        const uint16_t *c = cnt + j * nb;
+        uint32_t *o = in_row + j * nb;
+        uint32_t run = 0;
+        for (uint64_t s0 = 0; s0 < ns; s0 += 64) {
+            const uint64_t sl = s0 + l;
+            const uint32_t v = sl < ns ? c[sl] : 0u;
+            const uint32_t incl = wave_incl_scan(v);
+            if (sl < ns) o[sl] = run + incl - v;
+            run += wave_bcast(incl, 63);
+        }
+        if (l == 0) rowtot[j] = run;
+    }
+}
+
+hipError_t launch_ld_rowscan(const uint16_t *cnt, uint64_t rows, uint64_t nb, uint64_t j_lo, uint64_t window,
+                             uint32_t *in_row, uint64_t *rowtot, hipStream_t s) {
+    if (!rows) return hipSuccess;
+    const uint64_t blocks = (rows + 3) / 4;
+    hipLaunchKernelGGL(k_ld_rowscan, dim3((unsigned)std::min<uint64_t>(blocks, 65536)), dim3(256), 0, s, cnt, rows, nb,
+                       j_lo, window, in_row, rowtot);
     return hipGetLastError();
 }
 
