@@ -15,15 +15,17 @@ from vcfx_amd import engine, synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["default", "fused", "chunks", "scan", "pipe", "pipe1"])
+@pytest.fixture(scope="module", params=["default", "fused", "chunks", "scan", "pipe", "pipe1", "stream1", "stream3"])
 def eng(request):
     """every region schedule: index + head pass + sweep (default), look-back single sweep,
     chunk sweep, byte-class single sweep, two-stream pipeline (pieces of 2 wave-chunks, so
-    the small inputs here span many pieces; and of 1)"""
+    the small inputs here span many pieces; and of 1), one-sweep LDS-ring stream (grids of 1
+    and 3 persistent blocks, so the inputs span many chunks and block boundaries)"""
     import os
     env = {"VCFXG_AF_FUSED": {"default": "0", "fused": "1", "chunks": "2", "scan": "4", "pipe": "5",
-                              "pipe1": "5"}[request.param],
-           "VCFXG_PIPE_CHUNKS": {"pipe1": "1"}.get(request.param, "2")}
+                              "pipe1": "5", "stream1": "6", "stream3": "6"}[request.param],
+           "VCFXG_PIPE_CHUNKS": {"pipe1": "1"}.get(request.param, "2"),
+           "VCFXG_STREAM_GRID": {"stream1": "1", "stream3": "3"}.get(request.param, "0")}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -100,10 +102,12 @@ def test_fused_edge_layouts(eng, oracle):
         head + b"#late header\n" + row,
     ]
     # a newline on the last byte of chunk 0, on the first byte of chunk 1, and just before
+    # (16 KiB index chunks; 32 KiB one-sweep chunks)
     ds = len(head)
-    last0 = ((ds - 1) & ~15) + 16384 - 1
-    filler = b"1\t7\t.\tA\tG\t.\t.\t.\tGT\t0|0\t0|1\n"
-    for shift in (-1, 0, 1):
+    for last0, shift in [(((ds - 1) & ~15) + 16384 - 1, sh) for sh in (-1, 0, 1)] + \
+            [((ds & ~15) + 32768 - 1, sh) for sh in (-1, 0, 1)]:
+        # (long fillers on the 32 KiB grid: under the one-sweep kernel's lines-per-chunk cap)
+        filler = b"1\t7\t.\tA\tG\t.\t.\t" + (b"I" * 150 if last0 > 20000 else b".") + b"\tGT\t0|0\t0|1\n"
         body = b""
         while ds + len(body) + 2 * len(filler) + 64 < last0:
             body += filler

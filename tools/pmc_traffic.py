@@ -23,6 +23,7 @@ KERNELS = {
     "line_compact": r"vcfxg::k_nl_compact\(",
     "af_records": r"vcfxg::k_(line_meta|af_sweep|af_complex)\(",
     "af_pipe": r"vcfxg::k_(idx_sweep<false>|nl_compact_piece|lines_tail|line_meta|af_sweep|af_complex)\(",
+    "af_stream": r"vcfxg::k_(af_stream|af_stream_compact|af_complex)\(",
     "af_scan": r"vcfxg::k_af_scan\(",
     "af_fused": r"vcfxg::k_af_fused\(",
     "af_chunks": r"vcfxg::k_af_chunks\(",

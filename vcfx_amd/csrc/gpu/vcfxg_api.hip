@@ -51,6 +51,9 @@ struct vcfxg_ctx {
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
         ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff;
     DevBuf pipe_carry;          // pipelined AF: line number at the start of each piece
+    DevBuf st_le, st_alt, st_tot, st_rowpre, st_status, st_meta, st_bcount;  // one-sweep AF block regions
+    int n_cu = 0;
+    int stream_grid = getenv("VCFXG_STREAM_GRID") ? atoi(getenv("VCFXG_STREAM_GRID")) : 0;
     DevBuf ld_temp, ld_quarters, ld_stage_ctr;  // LD: pairs staged by the count pass
     uint64_t ld_temp_cap = 0;
     // test hook: a fixed (small) staging capacity exercises the overflow -> emit-pass path
@@ -198,7 +201,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->st_le, &c->st_alt, &c->st_tot, &c->st_rowpre, &c->st_status, &c->st_meta, &c->st_bcount})
         if (b->p) (void)hipFree(b->p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
@@ -423,6 +426,72 @@ static int af_region_scan(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     return af_rows(c, mode, out);
 }
 
+// One-sweep region path (default): k_af_stream reads every input byte once -- persistent
+// blocks stream 32 KiB chunks through an LDS ring, find the newlines, parse the heads and
+// sweep the sample regions of the lines ending in each chunk -- then the blocks' regions
+// are concatenated (k_af_stream_compact) and k_af_complex takes the lines left to the exact
+// per-line path.  Overflow (lines under ~512 B on average) -> the two-sweep schedule.
+static int af_region_stream(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
+    if (!c->n_cu) HIPCHK(c, hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
+    // (VCFXG_STREAM_GRID: a small persistent grid, so that the tests' small inputs still
+    // span several blocks of several chunks each)
+    const int G = c->stream_grid > 0 ? c->stream_grid : (c->n_cu > 0 ? c->n_cu : 256);
+    const int64_t nc = vcfxg::af_stream_chunks(lo, hi);
+    if (nc < (c->stream_grid > 0 ? 1 : 4 * (int64_t)G)) {  // small inputs: the two-sweep schedule
+        int r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    const uint64_t range = (uint64_t)((nc + G - 1) / G) * 32768;
+    const uint64_t cap_b = range / 512 + 1024, cap = cap_b * (uint64_t)G;
+    int r = ensure(c, c->st_le, 8 * cap);
+    if (!r) r = ensure(c, c->st_alt, 4 * cap);
+    if (!r) r = ensure(c, c->st_tot, 4 * cap);
+    if (!r) r = ensure(c, c->st_rowpre, 4 * cap);
+    if (!r) r = ensure(c, c->st_status, cap);
+    if (!r) r = ensure(c, c->st_meta, vcfxg::af_meta_bytes() * cap);
+    if (!r) r = ensure(c, c->st_bcount, 8 * (size_t)G + 64);
+    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
+    if (!r) r = af_buffers(c, cap);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (cap + 1));
+    if (r) return r;
+    const char *buf = P<char>(c->input);
+    unsigned *overflow = reinterpret_cast<unsigned *>(P<uint64_t>(c->st_bcount) + G);
+    HIPCHK(c, hipMemsetAsync(overflow, 0, 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    const int tail = c->last_byte != '\n' ? 1 : 0;
+    prof_begin(c, "af_stream");
+    HIPCHK(c, vcfxg::launch_af_stream(buf, lo, hi, (int64_t)c->n + 256, mode, tail, G, cap_b, P<uint64_t>(c->st_le),
+                                      P<int32_t>(c->st_alt), P<int32_t>(c->st_tot), P<uint32_t>(c->st_rowpre),
+                                      P<uint8_t>(c->st_status), c->st_meta.p, P<uint64_t>(c->st_bcount), overflow,
+                                      P<unsigned long long>(c->counters), c->stream));
+    HIPCHK(c, vcfxg::launch_af_stream_compact(G, cap_b, P<uint64_t>(c->st_bcount), P<uint64_t>(c->st_le),
+                                              P<int32_t>(c->st_alt), P<int32_t>(c->st_tot), P<uint32_t>(c->st_rowpre),
+                                              P<uint8_t>(c->st_status), c->st_meta.p, P<uint64_t>(c->line_end),
+                                              P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                              P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->d_nlines),
+                                              c->stream));
+    HIPCHK(c, vcfxg::launch_af_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
+                                       c->af_meta.p, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "af_stream");
+    static thread_local uint64_t nl;
+    static thread_local unsigned ovf;
+    HIPCHK(c, hipMemcpyAsync(&nl, c->d_nlines.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&ovf, overflow, sizeof ovf, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (ovf) {
+        prof_collect(c);
+        r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    c->data_start = data_start;
+    c->n_lines = nl;
+    c->indexed = true;
+    return af_rows(c, mode, out);
+}
+
 // Pipelined region path: the input is cut into pieces of whole 16 KiB wave-chunks.  On the
 // engine stream each piece is indexed (count sweep + in-kernel scan/compaction continuing
 // the line numbering from the previous piece, a device-side carry); on a second stream the
@@ -514,6 +583,7 @@ int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_su
     if (data_start > c->n) data_start = c->n;
     if (c->af_path == 4) return af_region_scan(c, data_start, mode, out);
     if (c->af_path == 5) return af_region_pipe(c, data_start, mode, out);
+    if (c->af_path == 6) return af_region_stream(c, data_start, mode, out);
     const uint64_t nc = (c->af_path == 1 || c->af_path == 2) ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
     if (!nc) {  // default (also no data lines, or data_start == 0): index + record kernels
         int r = vcfxg_index(c, data_start, nullptr);

@@ -47,6 +47,17 @@ hipError_t launch_af_meta_sweep_range(const char *buf, int64_t data_start, const
                                       int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
                                       hipStream_t s);
 int64_t idx_wchunk_bytes();
+// one-sweep AF record pass (vcfxg_af_stream.hip): persistent blocks over 32 KiB chunks
+int64_t af_stream_chunks(int64_t lo, int64_t hi);
+hipError_t launch_af_stream(const char *buf, int64_t lo, int64_t hi, int64_t n_alloc, int mode, int tail, int grid,
+                            uint64_t cap_b, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
+                            uint8_t *status_b, void *meta_b, uint64_t *bcount, unsigned *overflow,
+                            unsigned long long *counters, hipStream_t s);
+hipError_t launch_af_stream_compact(int grid, uint64_t cap_b, const uint64_t *bcount, const uint64_t *le_b,
+                                    const int32_t *alt_b, const int32_t *tot_b, const uint32_t *rowpre_b,
+                                    const uint8_t *status_b, const void *meta_b, uint64_t *line_end, int32_t *alt,
+                                    int32_t *tot, uint32_t *rowpre, uint8_t *status, void *meta, uint64_t *n_lines,
+                                    hipStream_t s);
 hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
                              int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,

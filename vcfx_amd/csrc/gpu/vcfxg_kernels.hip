@@ -11,6 +11,7 @@
 
 #include "vcfxg_device.h"
 #include "vcfxg_gt.h"
+#include "vcfxg_meta.h"
 #include "vcfxg_kernels.h"
 
 namespace vcfxg {
@@ -289,60 +290,15 @@ __global__ __launch_bounds__(256) void k_line_meta(const char *__restrict__ buf,
 __device__ __forceinline__ void line_meta_one(const char *__restrict__ buf, int64_t data_start,
                                               const uint64_t *__restrict__ line_end, uint64_t li, int strip_cr,
                                               const uint8_t *__restrict__ gate, LineMeta *__restrict__ meta) {
-    LineMeta m{};
     if (gate && gate[li] != 1) {
+        LineMeta m{};
         m.kind = kMetaGated;
         meta[li] = m;
         return;
     }
     const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
     const int64_t le = (int64_t)line_end[li];
-    m.kind = kMetaFull;
-    if (le <= ls) {
-        m.kind = kMetaEmpty;
-        meta[li] = m;
-        return;
-    }
-    const int64_t a = ls & ~(int64_t)15;
-    constexpr int kB = 10;  // 160 bytes of head
-    uint4 v[kB];
-#pragma unroll
-    for (int b = 0; b < kB; b++) v[b] = load16(buf, a + 16 * b);
-    const uint32_t last = byte_at(buf, le - 1);
-    int64_t ae = le;
-    if (strip_cr && last == '\r') {
-        ae--;
-        m.cr = 1;
-    }
-    const uint32_t first = byte_at(buf, ls);
-    if (ae <= ls || first == '#') {
-        m.kind = ae <= ls ? kMetaEmpty : kMetaHeader;
-        meta[li] = m;
-        return;
-    }
-    int nt = 0;
-    int64_t t4 = 0, t7 = 0, t8 = 0;
-#pragma unroll
-    for (int b = 0; b < kB; b++) {
-        uint32_t mk = eq_mask16(v[b], kRepTab) & range_mask16(a + 16 * b, ls, ae);
-        while (mk && nt < 9) {
-            const int j = __builtin_ctz(mk);
-            mk &= mk - 1u;
-            const int64_t p = a + 16 * b + j;
-            nt++;
-            if (nt == 5) t4 = p;
-            if (nt == 8) t7 = p;
-            if (nt == 9) t8 = p;
-        }
-    }
-    if (nt == 9 && t8 - t7 >= 3 && byte_at(buf, t7 + 1) == 'G' && byte_at(buf, t7 + 2) == 'T' &&
-        (t8 - t7 == 3 || byte_at(buf, t7 + 3) == ':')) {
-        m.kind = kMetaGt;
-        m.S = (uint64_t)(t8 + 1);
-        m.rowpre = (uint32_t)(t4 - ls + 1);
-        m.sep = t8 + 2 < ae ? (uint8_t)byte_at(buf, t8 + 2) : 0;
-    }
-    meta[li] = m;
+    meta[li] = head_meta(GlobalSrc{buf}, ls, le, strip_cr);
 }
 
 __global__ __launch_bounds__(kRecThreads) void k_af_sweep(const char *__restrict__ buf, int64_t data_start,
