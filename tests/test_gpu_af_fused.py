@@ -15,14 +15,16 @@ from vcfx_amd import engine, synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["default", "fused", "chunks", "scan", "pipe", "pipe1", "stream1", "stream3"])
+@pytest.fixture(scope="module", params=["default", "sync", "fused", "chunks", "scan", "pipe", "pipe1", "stream1",
+                                               "stream3"])
 def eng(request):
-    """every region schedule: index + head pass + sweep (default), look-back single sweep,
+    """every region schedule: index + head pass + sweep (default: one host synchronisation;
+    sync: the same kernels with the line count read back after the index), look-back single sweep,
     chunk sweep, byte-class single sweep, two-stream pipeline (pieces of 2 wave-chunks, so
     the small inputs here span many pieces; and of 1), one-sweep LDS-ring stream (grids of 1
     and 3 persistent blocks, so the inputs span many chunks and block boundaries)"""
     import os
-    env = {"VCFXG_AF_FUSED": {"default": "0", "fused": "1", "chunks": "2", "scan": "4", "pipe": "5",
+    env = {"VCFXG_AF_FUSED": {"default": "0", "sync": "3", "fused": "1", "chunks": "2", "scan": "4", "pipe": "5",
                               "pipe1": "5", "stream1": "6", "stream3": "6"}[request.param],
            "VCFXG_PIPE_CHUNKS": {"pipe1": "1"}.get(request.param, "2"),
            "VCFXG_STREAM_GRID": {"stream1": "1", "stream3": "3"}.get(request.param, "0")}

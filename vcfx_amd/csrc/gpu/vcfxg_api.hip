@@ -53,6 +53,7 @@ struct vcfxg_ctx {
     DevBuf pipe_carry;          // pipelined AF: line number at the start of each piece
     DevBuf st_le, st_alt, st_tot, st_rowpre, st_status, st_meta, st_bcount;  // one-sweep AF block regions
     int n_cu = 0;
+    DevBuf async_small;         // asynchronous AF path: line range {0, n}, failure flags, summary
     int stream_grid = getenv("VCFXG_STREAM_GRID") ? atoi(getenv("VCFXG_STREAM_GRID")) : 0;
     DevBuf ld_temp, ld_quarters, ld_stage_ctr;  // LD: pairs staged by the count pass
     uint64_t ld_temp_cap = 0;
@@ -201,7 +202,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->st_le, &c->st_alt, &c->st_tot, &c->st_rowpre, &c->st_status, &c->st_meta, &c->st_bcount})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->st_le, &c->st_alt, &c->st_tot, &c->st_rowpre, &c->st_status, &c->st_meta, &c->st_bcount, &c->async_small})
         if (b->p) (void)hipFree(b->p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
@@ -426,7 +427,108 @@ static int af_region_scan(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     return af_rows(c, mode, out);
 }
 
-// One-sweep region path (default): k_af_stream reads every input byte once -- persistent
+// Default region path, asynchronous: the two-sweep schedule (index sweep + scan +
+// compaction, head pass + fixed-stride sweep + the per-line rest, row lengths + scan) runs
+// with the line count kept on the device -- buffers sized by the count of the previous call
+// (else the no-overflow bound of idx_pos_cap() lines per 16 KiB chunk), compaction and
+// kernels guarded by it -- and ONE host synchronisation reads a small summary (lines, text
+// bytes, counters, failure) before the formatting kernel.  A failure (a chunk with more
+// newlines than the scratch keeps, or more lines than the capacity) reruns the call on the
+// synchronous path.
+static int af_region_async(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
+    const int64_t nc = vcfxg::idx_wchunks(lo, hi);
+    if (!nc) {
+        int r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    const size_t pcap = (size_t)vcfxg::idx_pos_cap();
+    const uint64_t bound = (uint64_t)nc * pcap + 2;
+    const uint64_t cap = c->af_line_cap ? std::min<uint64_t>(c->af_line_cap + 1, bound) : bound;
+    int r = ensure(c, c->idx_counts, sizeof(uint32_t) * (size_t)(nc + 1));
+    if (!r) r = ensure(c, c->idx_offs, sizeof(uint64_t) * (size_t)(nc + 1));
+    if (!r) r = ensure(c, c->idx_pos, sizeof(uint64_t) * (size_t)nc * pcap + 64);
+    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
+    if (!r) r = af_buffers(c, cap);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (cap + 1));
+    if (!r) r = ensure(c, c->async_small, 128);
+    if (r) return r;
+    const char *buf = P<char>(c->input);
+    uint64_t *small = P<uint64_t>(c->async_small);  // [0] 0, [1] n, [2] flags, [4..10] summary
+    unsigned *idx_ovf = reinterpret_cast<unsigned *>(small + 2), *failf = idx_ovf + 1;
+    HIPCHK(c, hipMemsetAsync(small, 0, 32, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    prof_begin(c, "line_count");
+    HIPCHK(c, vcfxg::launch_idx_count(buf, lo, hi, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_pos), idx_ovf,
+                                      c->stream));
+    prof_end(c, "line_count");
+    HIPCHK(c, hipMemsetAsync(P<uint32_t>(c->idx_counts) + nc, 0, sizeof(uint32_t), c->stream));
+    r = exclusive_scan(c, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_offs), (size_t)nc + 1);
+    if (r) return r;
+    prof_begin(c, "line_compact");
+    HIPCHK(c, vcfxg::launch_nl_compact_cap(lo, hi, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_offs),
+                                           P<uint64_t>(c->idx_pos), P<uint64_t>(c->line_end), cap, c->stream));
+    HIPCHK(c, vcfxg::launch_idx_finish(P<uint64_t>(c->idx_offs), nc, idx_ovf, c->last_byte != '\n' ? 1 : 0, hi, cap,
+                                       P<uint64_t>(c->line_end), small + 1, failf, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->d_nlines.p, small + 1, 8, hipMemcpyDeviceToDevice, c->stream));
+    prof_end(c, "line_compact");
+    prof_begin(c, "af_records");
+    HIPCHK(c, vcfxg::launch_af_meta_sweep_range(buf, lo, P<uint64_t>(c->line_end), small, cap, mode, c->af_meta.p,
+                                                P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                                P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    HIPCHK(c, vcfxg::launch_af_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
+                                       c->af_meta.p, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "af_records");
+    prof_begin(c, "af_rows");
+    HIPCHK(c, vcfxg::launch_af_rowlen(P<uint32_t>(c->rowpre), P<uint8_t>(c->status), P<uint64_t>(c->d_nlines), cap,
+                                      P<uint64_t>(c->rowlen), c->stream));
+    r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)cap + 1);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_af_summary(P<uint64_t>(c->d_nlines), P<uint64_t>(c->rowoff),
+                                       P<unsigned long long>(c->counters), failf, small + 4, c->stream));
+    prof_end(c, "af_rows");
+    static thread_local uint64_t sm[7];
+    HIPCHK(c, hipMemcpyAsync(sm, small + 4, sizeof sm, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (sm[6]) {  // rerun synchronously (and learn the exact line count)
+        prof_collect(c);
+        c->af_line_cap = 0;
+        r = vcfxg_index(c, data_start, nullptr);
+        if (!r) r = vcfxg_allele_freq(c, mode, out);
+        if (!r) c->af_line_cap = c->n_lines;
+        return r;
+    }
+    const uint64_t L = sm[0], text = sm[1];
+    c->af_line_cap = std::max<uint64_t>(c->af_line_cap, L);
+    r = ensure(c, c->text, text + 1);
+    if (r) return r;
+    prof_begin(c, "af_format");
+    HIPCHK(c, vcfxg::launch_af_format(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L, mode,
+                                      P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                      P<uint8_t>(c->status), P<uint64_t>(c->rowoff), P<char>(c->text), c->stream));
+    prof_end(c, "af_format");
+    if (c->profiling) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        prof_collect(c);
+    }
+    c->data_start = data_start;
+    c->n_lines = L;
+    c->indexed = true;
+    c->text_bytes = text;
+    if (out) {
+        out->n_lines = L;
+        out->rows = sm[2];
+        out->data_lines = sm[3];
+        out->warn_lines = sm[4];
+        out->general_records = sm[5];
+        out->text_bytes = text;
+    }
+    return VCFXG_OK;
+}
+
+// One-sweep region path: k_af_stream reads every input byte once -- persistent
 // blocks stream 32 KiB chunks through an LDS ring, find the newlines, parse the heads and
 // sweep the sample regions of the lines ending in each chunk -- then the blocks' regions
 // are concatenated (k_af_stream_compact) and k_af_complex takes the lines left to the exact
@@ -585,7 +687,8 @@ int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_su
     if (c->af_path == 5) return af_region_pipe(c, data_start, mode, out);
     if (c->af_path == 6) return af_region_stream(c, data_start, mode, out);
     const uint64_t nc = (c->af_path == 1 || c->af_path == 2) ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
-    if (!nc) {  // default (also no data lines, or data_start == 0): index + record kernels
+    if (c->af_path == 0) return af_region_async(c, data_start, mode, out);
+    if (!nc) {  // synchronous two-sweep schedule (VCFXG_AF_FUSED=3): index + record kernels
         int r = vcfxg_index(c, data_start, nullptr);
         return r ? r : vcfxg_allele_freq(c, mode, out);
     }

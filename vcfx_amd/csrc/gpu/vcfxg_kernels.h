@@ -88,6 +88,14 @@ hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
                              int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,
                              hipStream_t s, const uint8_t *gate, void *meta = nullptr);
+// asynchronous AF region path: capacity-guarded compaction, device-side line count and
+// a one-record summary for the single host synchronisation
+hipError_t launch_nl_compact_cap(int64_t lo, int64_t hi, const uint32_t *counts, const uint64_t *offs,
+                                 const uint64_t *pos, uint64_t *line_end, uint64_t cap, hipStream_t s);
+hipError_t launch_idx_finish(const uint64_t *offs, int64_t nchunks, const unsigned *idx_overflow, int tail, int64_t hi,
+                             uint64_t cap, uint64_t *line_end, uint64_t *n_lines, unsigned *fail, hipStream_t s);
+hipError_t launch_af_summary(const uint64_t *n_lines, const uint64_t *rowoff, const unsigned long long *counters,
+                             const unsigned *fail, uint64_t *out, hipStream_t s);
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, uint64_t *len, hipStream_t s);
 hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,

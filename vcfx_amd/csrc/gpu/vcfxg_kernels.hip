@@ -75,11 +75,40 @@ __global__ __launch_bounds__(kIdxThreads) void k_idx_sweep(const char *__restric
 }
 
 __global__ void k_nl_compact(int64_t nchunks, const uint32_t *__restrict__ counts, const uint64_t *__restrict__ offs,
-                             const uint64_t *__restrict__ pos, uint64_t *__restrict__ line_end) {
+                             const uint64_t *__restrict__ pos, uint64_t *__restrict__ line_end, uint64_t cap) {
     const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const uint64_t b = i / kPosCap, k = i % kPosCap;
-    if ((int64_t)b >= nchunks || k >= counts[b]) return;
+    if ((int64_t)b >= nchunks || k >= counts[b] || offs[b] + k >= cap) return;
     line_end[offs[b] + k] = pos[i];
+}
+
+// asynchronous index tail: line count (+ the unterminated last line) published on the
+// device; a chunk over kPosCap newlines or a count over `cap` publishes 0 lines and raises
+// *fail (the caller then reruns the synchronous index)
+__global__ void k_idx_finish(const uint64_t *__restrict__ offs, int64_t nchunks, const unsigned *idx_overflow,
+                             int tail, int64_t hi, uint64_t cap, uint64_t *__restrict__ line_end,
+                             uint64_t *n_lines, unsigned *fail) {
+    const uint64_t total = offs[nchunks];
+    const uint64_t n = total + (tail ? 1 : 0);
+    if (*idx_overflow || n > cap) {
+        *fail = 1u;
+        *n_lines = 0;
+        return;
+    }
+    if (tail) line_end[total] = (uint64_t)hi;
+    *n_lines = n;
+}
+
+// one small record for the host's single synchronisation of an AF call: line count, text
+// bytes (row offsets scanned over a capacity, read at the device count), counters, failure
+__global__ void k_af_summary(const uint64_t *n_lines, const uint64_t *__restrict__ rowoff,
+                             const unsigned long long *__restrict__ counters, const unsigned *fail,
+                             uint64_t *__restrict__ out) {
+    const uint64_t n = *n_lines;
+    out[0] = n;
+    out[1] = rowoff[n];
+    for (int k = 0; k < 4; k++) out[2 + k] = counters[k];
+    out[6] = *fail;
 }
 
 // Pipelined index (one piece of the input): the piece's chunk counts are scanned in place
@@ -892,7 +921,7 @@ hipError_t launch_nl_compact(int64_t lo, int64_t hi, const uint32_t *counts, con
     if (!nc) return hipSuccess;
     const uint64_t n = (uint64_t)nc * kPosCap;
     hipLaunchKernelGGL(k_nl_compact, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nc, counts, offs, pos,
-                       line_end);
+                       line_end, ~0ull);
     return hipGetLastError();
 }
 hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
@@ -1010,6 +1039,26 @@ hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t
     unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
     hipLaunchKernelGGL(k_gq_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
                        strip_cr, Q, lm, status, counters, gate);
+    return hipGetLastError();
+}
+hipError_t launch_nl_compact_cap(int64_t lo, int64_t hi, const uint32_t *counts, const uint64_t *offs,
+                                 const uint64_t *pos, uint64_t *line_end, uint64_t cap, hipStream_t s) {
+    const int64_t nc = idx_wchunks(lo, hi);
+    if (!nc) return hipSuccess;
+    const uint64_t n = (uint64_t)nc * kPosCap;
+    hipLaunchKernelGGL(k_nl_compact, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, nc, counts, offs, pos,
+                       line_end, cap);
+    return hipGetLastError();
+}
+hipError_t launch_idx_finish(const uint64_t *offs, int64_t nchunks, const unsigned *idx_overflow, int tail, int64_t hi,
+                             uint64_t cap, uint64_t *line_end, uint64_t *n_lines, unsigned *fail, hipStream_t s) {
+    hipLaunchKernelGGL(k_idx_finish, dim3(1), dim3(1), 0, s, offs, nchunks, idx_overflow, tail, hi, cap, line_end,
+                       n_lines, fail);
+    return hipGetLastError();
+}
+hipError_t launch_af_summary(const uint64_t *n_lines, const uint64_t *rowoff, const unsigned long long *counters,
+                             const unsigned *fail, uint64_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_af_summary, dim3(1), dim3(1), 0, s, n_lines, rowoff, counters, fail, out);
     return hipGetLastError();
 }
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,
