@@ -19,7 +19,7 @@ MODE=${1:-all}
 shift
 WLS=${*:-af pipeline ld}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-    step pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=10; rc=$?; ok_or_testfail $rc || exit $rc
+    step pytest_gpu 1000 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread; rc=$?; ok_or_testfail $rc || exit $rc
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
     for w in $WLS; do
