@@ -16,18 +16,22 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module", params=["default", "sync", "fused", "chunks", "scan", "pipe", "pipe1", "stream1",
-                                               "stream3"])
+                                               "stream3", "walk", "walk4k", "walk1k"])
 def eng(request):
     """every region schedule: index + head pass + sweep (default: one host synchronisation;
     sync: the same kernels with the line count read back after the index), look-back single sweep,
     chunk sweep, byte-class single sweep, two-stream pipeline (pieces of 2 wave-chunks, so
     the small inputs here span many pieces; and of 1), one-sweep LDS-ring stream (grids of 1
-    and 3 persistent blocks, so the inputs span many chunks and block boundaries)"""
+    and 3 persistent blocks, so the inputs span many chunks and block boundaries), walk
+    (no index sweep: predicted record ends validated by the sweep; chunks of 128 KiB, 4 KiB
+    and 1 KiB, so lines start in, span and skip over many walkers' chunks)"""
     import os
     env = {"VCFXG_AF_FUSED": {"default": "0", "sync": "3", "fused": "1", "chunks": "2", "scan": "4", "pipe": "5",
-                              "pipe1": "5", "stream1": "6", "stream3": "6"}[request.param],
+                              "pipe1": "5", "stream1": "6", "stream3": "6", "walk": "7", "walk4k": "7",
+                              "walk1k": "7"}[request.param],
            "VCFXG_PIPE_CHUNKS": {"pipe1": "1"}.get(request.param, "2"),
-           "VCFXG_STREAM_GRID": {"stream1": "1", "stream3": "3"}.get(request.param, "0")}
+           "VCFXG_STREAM_GRID": {"stream1": "1", "stream3": "3"}.get(request.param, "0"),
+           "VCFXG_WALK_CHUNK": {"walk4k": "4096", "walk1k": "1024"}.get(request.param, str(128 * 1024))}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -135,3 +139,58 @@ def test_fused_text_matches_oracle(eng, oracle):
         f.flush()
         want, _, _ = oracle.run(["VCFX_allele_freq_calc", "-q", "-i", f.name])
     assert b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes) == want
+
+
+def _walk_layouts(seed):
+    """long GT-only records whose ends the walk path predicts from the previous record:
+    varying sample counts, missing alleles, non-fixed-stride samples, CRLF records, '#' and
+    empty lines between records, and a short record followed by a line whose '\n' sits
+    exactly where the previous record's span predicts this one's end (the sweep must reject
+    the prediction and the '\n' search must find the true end)"""
+    rng = np.random.default_rng(seed)
+    ns = 300
+    head = b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + \
+        b"\t".join(b"S%d" % i for i in range(ns)) + b"\n"
+    toks = [b"0|0", b"0|1", b"1|0", b"1|1", b".|.", b"2|1"]
+
+    def rec(pos, n, bad=False, cr=False):
+        g = [toks[int(k)] for k in rng.integers(0, len(toks), n)]
+        if bad:
+            g[int(rng.integers(0, n))] = [b"0|1:7", b"0/1", b"10|1"][int(rng.integers(0, 3))]
+        return b"21\t%d\trs%d\tA\tG\t100\tPASS\t.\tGT\t" % (pos, pos) + b"\t".join(g) + (b"\r\n" if cr else b"\n")
+
+    body = []
+    pos = 100
+    for i in range(400):
+        pos += 1
+        r = rng.random()
+        if r < 0.05:
+            body.append(b"#interleaved header line\n")
+        elif r < 0.08:
+            body.append(b"\n")
+        elif r < 0.12:
+            body.append(rec(pos, ns, bad=True))
+        elif r < 0.16:
+            body.append(rec(pos, ns, cr=True))
+        elif r < 0.22:
+            body.append(rec(pos, int(rng.integers(200, 400))))
+        elif r < 0.26:
+            # a record 50 samples short, then a line whose '\n' is at the predicted end
+            body.append(rec(pos, ns))
+            short = rec(pos + 1, ns - 50)
+            body.append(short)
+            gap = 4 * ns - 1 - (4 * (ns - 50) - 1) - 1   # bytes of the next line before its '\n'
+            body.append(b"21\t%d\t" % (pos + 2) + b"x" * (gap - len(b"21\t%d\t" % (pos + 2))) + b"\n")
+            pos += 2
+        else:
+            body.append(rec(pos, ns))
+    tail = rec(pos + 1, ns)
+    return head + b"".join(body), head + b"".join(body) + tail[:-1]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_walk_predicted_ends(eng, seed):
+    for buf in _walk_layouts(seed):
+        for mode in (engine.MODE_FILE, engine.MODE_STDIN):
+            _, two, one = _both(eng, buf, mode)
+            _same(two, one)

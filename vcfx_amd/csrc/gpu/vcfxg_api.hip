@@ -61,6 +61,13 @@ struct vcfxg_ctx {
     uint64_t ld_stage_cap_fixed = getenv("VCFXG_LD_STAGE_CAP") ? strtoull(getenv("VCFXG_LD_STAGE_CAP"), nullptr, 10) : 0;
     DevBuf fuse_state;          // fused AF: per-chunk look-back words
     DevBuf af_meta;             // AF head pass output (k_af_meta)
+    // walk AF path (vcfxg_af_walk.hip): per-walker regions, counts, scan, flags
+    DevBuf wk_le, wk_alt, wk_tot, wk_rowpre, wk_status, wk_meta, wk_count, wk_offs, wk_gt, wk_small;
+    int64_t walk_chunk = getenv("VCFXG_WALK_CHUNK") ? atol(getenv("VCFXG_WALK_CHUNK")) : 128 * 1024;
+    bool walk_overflowed = false;  // the last walk run overflowed: two-sweep schedule
+    // host hints taken at load time from the first data line: its '\n' distance from the
+    // sample start (the walk's first prediction) and the mean length of the first lines
+    int64_t hint_span = 0, hint_line = 0;
     DevBuf scan_seg, nl_chunk;  // AF one-sweep path: per-chunk segment counts, newline -> chunk
     uint64_t af_line_cap = 0;   // fused AF: line capacity the last run needed
     // region AF schedule: 0 = single-sweep index + head pass + fixed-stride sweep (default,
@@ -202,7 +209,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->st_le, &c->st_alt, &c->st_tot, &c->st_rowpre, &c->st_status, &c->st_meta, &c->st_bcount, &c->async_small})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->st_le, &c->st_alt, &c->st_tot, &c->st_rowpre, &c->st_status, &c->st_meta, &c->st_bcount, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small})
         if (b->p) (void)hipFree(b->p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
@@ -247,6 +254,40 @@ int vcfxg_reset_kernel_stats(vcfxg_ctx *c) {
     return VCFXG_OK;
 }
 
+// the walk AF path's hints from the host copy: skip '#' lines, then the first data line's
+// '\n' distance from the byte after its 9th tab and the mean length of up to 256 lines
+static void load_hints(vcfxg_ctx *c, const char *h, size_t n) {
+    c->hint_span = 0;
+    c->hint_line = 0;
+    c->walk_overflowed = false;
+    size_t p = 0;
+    while (p < n && h[p] == '#') {
+        const void *q = memchr(h + p, '\n', n - p);
+        if (!q) return;
+        p = (size_t)((const char *)q - h) + 1;
+    }
+    const size_t first = p;
+    int lines = 0;
+    while (p < n && lines < 256) {
+        const char *q = (const char *)memchr(h + p, '\n', n - p);
+        const size_t e = q ? (size_t)(q - h) : n;
+        if (lines == 0) {
+            int tabs = 0;
+            size_t x = p;
+            while (x < e && tabs < 9) {
+                const char *t = (const char *)memchr(h + x, '\t', e - x);
+                if (!t) break;
+                x = (size_t)(t - h) + 1;
+                tabs++;
+            }
+            if (tabs == 9) c->hint_span = (int64_t)(e - x);
+        }
+        lines++;
+        p = e + 1;
+    }
+    if (lines) c->hint_line = (int64_t)((std::min(p, n) - first) / (size_t)lines);
+}
+
 int vcfxg_load_host(vcfxg_ctx *c, const char *host, size_t n) {
     if (!c || (!host && n)) return VCFXG_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -257,6 +298,7 @@ int vcfxg_load_host(vcfxg_ctx *c, const char *host, size_t n) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->n = n;
     c->last_byte = n ? (unsigned char)host[n - 1] : -1;
+    load_hints(c, host, n);
     c->loaded = true;
     c->indexed = false;
     return VCFXG_OK;
@@ -528,6 +570,108 @@ static int af_region_async(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summ
     return VCFXG_OK;
 }
 
+// Walk region path (default when the first data lines average >= 512 B): no separate
+// index sweep.  k_af_walk reads each chunk's lines once, predicting fixed-stride record
+// ends and validating them by the sample sweep itself; the walkers' regions are scanned
+// and concatenated (k_walk_compact), k_af_complex takes the lines left to the exact
+// per-line path, then row lengths + scan and ONE host synchronisation before formatting,
+// as in af_region_async.  A walker over its line capacity reruns the call on the
+// two-sweep schedule (and later calls on this input use it directly).
+static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
+    const int64_t C = c->walk_chunk;
+    const int64_t nw = vcfxg::af_walkers(lo, hi, C);
+    if (!nw) {
+        int r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_allele_freq(c, mode, out);
+    }
+    const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
+    const uint64_t cap = (uint64_t)nw * cap_w;
+    int r = ensure(c, c->wk_le, 8 * cap);
+    if (!r) r = ensure(c, c->wk_alt, 4 * cap);
+    if (!r) r = ensure(c, c->wk_tot, 4 * cap);
+    if (!r) r = ensure(c, c->wk_rowpre, 4 * cap);
+    if (!r) r = ensure(c, c->wk_status, cap);
+    if (!r) r = ensure(c, c->wk_meta, vcfxg::af_meta_bytes() * cap);
+    if (!r) r = ensure(c, c->wk_count, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_offs, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_gt, 4 * (size_t)nw);
+    if (!r) r = ensure(c, c->wk_small, 128);
+    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
+    if (!r) r = af_buffers(c, cap);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (cap + 1));
+    if (r) return r;
+    const char *buf = P<char>(c->input);
+    uint64_t *small = P<uint64_t>(c->wk_small);  // [0] overflow flag, [4..10] summary
+    unsigned *ovf = reinterpret_cast<unsigned *>(small);
+    HIPCHK(c, hipMemsetAsync(small, 0, 32, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->wk_count) + nw, 0, 8, c->stream));
+    prof_begin(c, "af_walk");
+    HIPCHK(c, vcfxg::launch_af_walk(buf, lo, hi, C, mode, c->hint_span, cap_w, P<uint64_t>(c->wk_le),
+                                    P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre),
+                                    P<uint8_t>(c->wk_status), c->wk_meta.p, P<uint64_t>(c->wk_count),
+                                    P<uint32_t>(c->wk_gt), ovf, c->stream));
+    prof_end(c, "af_walk");
+    prof_begin(c, "walk_compact");
+    r = exclusive_scan(c, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_offs), (size_t)nw + 1);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_walk_compact(nw, cap_w, P<uint64_t>(c->wk_offs), P<uint32_t>(c->wk_gt),
+                                         P<uint64_t>(c->wk_le), P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot),
+                                         P<uint32_t>(c->wk_rowpre), P<uint8_t>(c->wk_status), c->wk_meta.p,
+                                         P<uint64_t>(c->line_end), P<int32_t>(c->alt), P<int32_t>(c->tot),
+                                         P<uint32_t>(c->rowpre), P<uint8_t>(c->status), c->af_meta.p,
+                                         P<uint64_t>(c->d_nlines), P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "walk_compact");
+    prof_begin(c, "af_complex");
+    HIPCHK(c, vcfxg::launch_af_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
+                                       c->af_meta.p, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "af_complex");
+    prof_begin(c, "af_rows");
+    HIPCHK(c, vcfxg::launch_af_rowlen(P<uint32_t>(c->rowpre), P<uint8_t>(c->status), P<uint64_t>(c->d_nlines), cap,
+                                      P<uint64_t>(c->rowlen), c->stream));
+    r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)cap + 1);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_af_summary(P<uint64_t>(c->d_nlines), P<uint64_t>(c->rowoff),
+                                       P<unsigned long long>(c->counters), ovf, small + 4, c->stream));
+    prof_end(c, "af_rows");
+    static thread_local uint64_t sm[7];
+    HIPCHK(c, hipMemcpyAsync(sm, small + 4, sizeof sm, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (sm[6]) {  // a walker ran out of line slots (short lines): the two-sweep schedule
+        prof_collect(c);
+        c->walk_overflowed = true;
+        return af_region_async(c, data_start, mode, out);
+    }
+    const uint64_t L = sm[0], text = sm[1];
+    r = ensure(c, c->text, text + 1);
+    if (r) return r;
+    prof_begin(c, "af_format");
+    HIPCHK(c, vcfxg::launch_af_format(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L, mode,
+                                      P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                      P<uint8_t>(c->status), P<uint64_t>(c->rowoff), P<char>(c->text), c->stream));
+    prof_end(c, "af_format");
+    if (c->profiling) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        prof_collect(c);
+    }
+    c->data_start = data_start;
+    c->n_lines = L;
+    c->indexed = true;
+    c->text_bytes = text;
+    if (out) {
+        out->n_lines = L;
+        out->rows = sm[2];
+        out->data_lines = sm[3];
+        out->warn_lines = sm[4];
+        out->general_records = sm[5];
+        out->text_bytes = text;
+    }
+    return VCFXG_OK;
+}
+
 // One-sweep region path: k_af_stream reads every input byte once -- persistent
 // blocks stream 32 KiB chunks through an LDS ring, find the newlines, parse the heads and
 // sweep the sample regions of the lines ending in each chunk -- then the blocks' regions
@@ -686,6 +830,7 @@ int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_su
     if (c->af_path == 4) return af_region_scan(c, data_start, mode, out);
     if (c->af_path == 5) return af_region_pipe(c, data_start, mode, out);
     if (c->af_path == 6) return af_region_stream(c, data_start, mode, out);
+    if (c->af_path == 7) return af_region_walk(c, data_start, mode, out);
     const uint64_t nc = (c->af_path == 1 || c->af_path == 2) ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
     if (c->af_path == 0) return af_region_async(c, data_start, mode, out);
     if (!nc) {  // synchronous two-sweep schedule (VCFXG_AF_FUSED=3): index + record kernels

@@ -58,6 +58,19 @@ hipError_t launch_af_stream_compact(int grid, uint64_t cap_b, const uint64_t *bc
                                     const uint8_t *status_b, const void *meta_b, uint64_t *line_end, int32_t *alt,
                                     int32_t *tot, uint32_t *rowpre, uint8_t *status, void *meta, uint64_t *n_lines,
                                     hipStream_t s);
+// AF record pass without a separate index (vcfxg_af_walk.hip): one wave per `chunk` bytes
+// walks its lines (predicted fixed-stride ends validated by the sweep); per-walker regions
+// of cap_w lines, then k_walk_compact (offs = exclusive scan of wcount)
+int64_t af_walkers(int64_t lo, int64_t hi, int64_t chunk);
+hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int mode, int64_t span0,
+                          uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
+                          uint8_t *status_b, void *meta_b, uint64_t *wcount, uint32_t *wgt, unsigned *overflow,
+                          hipStream_t s);
+hipError_t launch_walk_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t *offs, const uint32_t *wgt,
+                               const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b,
+                               const uint32_t *rowpre_b, const uint8_t *status_b, const void *meta_b,
+                               uint64_t *line_end, int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
+                               void *meta, uint64_t *n_lines, unsigned long long *counters, hipStream_t s);
 hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
                              int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
