@@ -167,7 +167,7 @@ def main():
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.text_bytes])
             return s
         kern_names = ("af_scan", "line_count", "line_emit", "line_compact", "af_records", "af_chunks", "af_fused",
-                      "af_pipe", "af_stream", "af_rows", "af_format")
+                      "af_pipe", "af_stream", "af_walk", "walk_compact", "af_complex", "af_rows", "af_format")
     elif a.workload == "pipeline":
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
@@ -264,6 +264,12 @@ def main():
                 # once + per line: the block-region results written, read back and written
                 # dense (line_end 8, counts/prefix/status 13, head record 16, x3)
                 "af_stream": region_bytes + L * 3 * (8 + 13 + 16),
+                # walk (no index sweep): the record bytes once + per line its region results
+                # (line_end 8, counts/prefix/status 13, head record 16); the compaction reads
+                # and rewrites them dense; the per-line rest reads head record + status
+                "af_walk": region_bytes + L * (8 + 13 + 16),
+                "walk_compact": L * 2 * (8 + 13 + 16),
+                "af_complex": L * (16 + 1),
                 "af_format": tb + L * (8 + 8 + 13) + s.rows * 40,
                 "af_rows": L * (5 + 8 + 8 + 8),
                 "rf_records": region_bytes + L * (8 + 1),

@@ -16,9 +16,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module", params=["default", "sync", "fused", "chunks", "scan", "pipe", "pipe1", "stream1",
-                                               "stream3", "walk", "walk4k", "walk1k"])
+                                               "stream3", "walk", "walk4k", "walk1k", "twosweep"])
 def eng(request):
-    """every region schedule: index + head pass + sweep (default: one host synchronisation;
+    """every region schedule: default (the walk for long records, else the two-sweep
+    schedule), two-sweep = index + head pass + sweep with one host synchronisation;
     sync: the same kernels with the line count read back after the index), look-back single sweep,
     chunk sweep, byte-class single sweep, two-stream pipeline (pieces of 2 wave-chunks, so
     the small inputs here span many pieces; and of 1), one-sweep LDS-ring stream (grids of 1
@@ -28,7 +29,7 @@ def eng(request):
     import os
     env = {"VCFXG_AF_FUSED": {"default": "0", "sync": "3", "fused": "1", "chunks": "2", "scan": "4", "pipe": "5",
                               "pipe1": "5", "stream1": "6", "stream3": "6", "walk": "7", "walk4k": "7",
-                              "walk1k": "7"}[request.param],
+                              "walk1k": "7", "twosweep": "8"}[request.param],
            "VCFXG_PIPE_CHUNKS": {"pipe1": "1"}.get(request.param, "2"),
            "VCFXG_STREAM_GRID": {"stream1": "1", "stream3": "3"}.get(request.param, "0"),
            "VCFXG_WALK_CHUNK": {"walk4k": "4096", "walk1k": "1024"}.get(request.param, str(128 * 1024))}
@@ -143,7 +144,7 @@ def test_fused_text_matches_oracle(eng, oracle):
 
 def _walk_layouts(seed):
     """long GT-only records whose ends the walk path predicts from the previous record:
-    varying sample counts, missing alleles, non-fixed-stride samples, CRLF records, '#' and
+    heads longer than the head window, varying sample counts, missing alleles, non-fixed-stride samples, CRLF records, '#' and
     empty lines between records, and a short record followed by a line whose '\n' sits
     exactly where the previous record's span predicts this one's end (the sweep must reject
     the prediction and the '\n' search must find the true end)"""
@@ -153,11 +154,12 @@ def _walk_layouts(seed):
         b"\t".join(b"S%d" % i for i in range(ns)) + b"\n"
     toks = [b"0|0", b"0|1", b"1|0", b"1|1", b".|.", b"2|1"]
 
-    def rec(pos, n, bad=False, cr=False):
+    def rec(pos, n, bad=False, cr=False, info=b"."):
         g = [toks[int(k)] for k in rng.integers(0, len(toks), n)]
         if bad:
             g[int(rng.integers(0, n))] = [b"0|1:7", b"0/1", b"10|1"][int(rng.integers(0, 3))]
-        return b"21\t%d\trs%d\tA\tG\t100\tPASS\t.\tGT\t" % (pos, pos) + b"\t".join(g) + (b"\r\n" if cr else b"\n")
+        return b"21\t%d\trs%d\tA\tG\t100\tPASS\t%s\tGT\t" % (pos, pos, info) + b"\t".join(g) + \
+            (b"\r\n" if cr else b"\n")
 
     body = []
     pos = 100
@@ -174,7 +176,10 @@ def _walk_layouts(seed):
             body.append(rec(pos, ns, cr=True))
         elif r < 0.22:
             body.append(rec(pos, int(rng.integers(200, 400))))
-        elif r < 0.26:
+        elif r < 0.24:
+            # heads longer than the walk's 256 B window (and than 1 KiB)
+            body.append(rec(pos, ns, info=b"AF=0.5;X=" + b"y" * int(rng.integers(150, 1500))))
+        elif r < 0.28:
             # a record 50 samples short, then a line whose '\n' is at the predicted end
             body.append(rec(pos, ns))
             short = rec(pos + 1, ns - 50)

@@ -27,6 +27,9 @@ KERNELS = {
     "af_scan": r"vcfxg::k_af_scan\(",
     "af_fused": r"vcfxg::k_af_fused\(",
     "af_chunks": r"vcfxg::k_af_chunks\(",
+    "af_walk": r"vcfxg::k_af_walk\(",
+    "walk_compact": r"vcfxg::k_walk_compact\(",
+    "af_complex": r"vcfxg::k_af_complex\(",
     "af_format": r"vcfxg::k_af_format\(",
     "rf_records": r"vcfxg::k_rf_records\(",
     "gq_records": r"vcfxg::k_(line_meta|gq_sweep|gq_complex)\(",

@@ -42,21 +42,36 @@ namespace {
 
 constexpr int kWalkThreads = 256;
 constexpr int kWalkWaves = kWalkThreads / kWave;
+#ifndef VCFXG_WALK_UNROLL
+#define VCFXG_WALK_UNROLL 6
+#endif
+constexpr int kWalkUnroll = VCFXG_WALK_UNROLL;  // wave-steps (KiB) of a record in flight per sweep step
 
-// first '\n' in [p, hi), else hi (wave-uniform; 4 KiB per step)
+// bits j of a 16-byte block at relative offset b with lo <= b + j < hi (32-bit offsets)
+__device__ __forceinline__ uint32_t range16(int b, int lo, int hi) {
+    int a = lo - b, e = hi - b;
+    a = a < 0 ? 0 : (a > 16 ? 16 : a);
+    e = e < 0 ? 0 : (e > 16 ? 16 : e);
+    return e <= a ? 0u : ((1u << e) - 1u) & ~((1u << a) - 1u);
+}
+
+// first '\n' in [p, hi), else hi (wave-uniform; 4 KiB per step, lane offsets 32-bit)
 __device__ __forceinline__ int64_t scan_nl(const char *__restrict__ buf, int64_t p, int64_t hi) {
     constexpr int kU = 4;
+    const int lo16 = 16 * lane();
     for (int64_t w = p & ~(int64_t)15; w < hi; w += kU * kWaveStep) {
+        const char *__restrict__ wb = buf + w;
+        const int pr = (int)std::max<int64_t>(p - w, 0), hr = (int)std::min<int64_t>(hi - w, kU * kWaveStep);
         uint4 v[kU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const int64_t blk = w + (int64_t)u * kWaveStep + 16 * (int64_t)lane();
-            v[u] = blk < hi ? load16(buf, blk) : make_uint4(0, 0, 0, 0);
+        for (int u = 0; u < kU; u++) {  // branch-free: lanes past hi re-read the last block
+            const int b = u * kWaveStep + lo16;
+            v[u] = load16(wb, b < hr ? b : ((hr - 1) & ~15));
         }
 #pragma unroll
         for (int u = 0; u < kU; u++) {
-            const int64_t blk = w + (int64_t)u * kWaveStep + 16 * (int64_t)lane();
-            const uint32_t m = eq_mask16(v[u], kRepNl) & range_mask16(blk, p, hi);
+            const int b = u * kWaveStep + lo16;
+            const uint32_t m = eq_mask16(v[u], kRepNl) & range16(b, pr, hr);
             const uint64_t any = __ballot(m != 0u);
             if (any) {
                 const int k = __builtin_ctzll(any);
@@ -68,175 +83,260 @@ __device__ __forceinline__ int64_t scan_nl(const char *__restrict__ buf, int64_t
     return hi;
 }
 
-// dword `comp` (uniform) of a uint4
-__device__ __forceinline__ uint32_t comp4(const uint4 &v, int comp) {
-    return comp == 0 ? v.x : comp == 1 ? v.y : comp == 2 ? v.z : v.w;
-}
-// byte x of the window whose lane k holds [A + 16k, A + 16k + 16); A <= x < A + 1024
-__device__ __forceinline__ uint32_t win_byte(const uint4 &W, int64_t A, int64_t x) {
-    const int o = (int)(x - A);
-    const uint32_t d = (uint32_t)__shfl((int)comp4(W, (o >> 2) & 3), o >> 4);
-    return (d >> (8 * (o & 3))) & 0xFFu;
-}
 
-// the window at line start L: lane k holds [A + 16k, +16), A = L & ~15 (zeros past hi)
-__device__ __forceinline__ uint4 load_window(const char *__restrict__ buf, int64_t L, int64_t hi) {
-    const int64_t blk = (L & ~(int64_t)15) + 16 * (int64_t)lane();
-    return blk < hi ? load16(buf, blk) : make_uint4(0, 0, 0, 0);
-}
-
-// position of the tab with 0-based rank r (< total) given per-lane tab masks and their
-// exclusive per-lane counts (wave-uniform result)
-__device__ __forceinline__ int64_t tab_at(uint32_t tm, uint32_t excl, uint32_t c, int r, int64_t blk) {
+// relative position of the tab with 0-based rank r (< total) given per-lane tab masks and
+// their exclusive per-lane counts (wave-uniform result)
+__device__ __forceinline__ int tab_at(uint32_t tm, uint32_t excl, uint32_t c, int r, int b) {
     const bool mine = (uint32_t)r >= excl && (uint32_t)r < excl + c;
     const uint64_t who = __ballot(mine);
     const int k = __builtin_ctzll(who);
-    const int64_t p = mine ? blk + nth_bit(tm, r - (int)excl) : 0;
-    return uniform64(__shfl(p, k));
+    const int p = mine ? b + nth_bit(tm, r - (int)excl) : 0;
+    return __builtin_amdgcn_readfirstlane(__shfl(p, k));
 }
 
 }  // namespace
 
-__global__ __launch_bounds__(kWalkThreads) void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi,
-                                                          int64_t chunk, int64_t n_walkers, int mode, int64_t span0,
-                                                          uint64_t cap_w, uint64_t *__restrict__ le_o,
-                                                          int32_t *__restrict__ alt_o, int32_t *__restrict__ tot_o,
-                                                          uint32_t *__restrict__ rowpre_o,
-                                                          uint8_t *__restrict__ status_o,
-                                                          LineMeta *__restrict__ meta_o, uint64_t *__restrict__ wcount,
-                                                          uint32_t *__restrict__ wgt, unsigned *overflow) {
-    const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + threadIdx.x / kWave);
+// the window at A (16 B per lane) -> the wave's LDS slot by LDS-DMA: issued before the
+// current record's sweep, it lands while the sweep runs (lanes past hi re-read the last
+// block; those bytes are masked by the analysis)
+// The window is kWin bytes (the first kWin / 16 lanes; a line head is rarely longer and the
+// sweep re-reads the bytes after it from HBM anyway), or the full 1 KiB for a long head.
+constexpr int kWin = 256;
+__device__ __forceinline__ void prefetch_window(const char *__restrict__ buf, int64_t A, int64_t hi, uint4 *slot,
+                                                int bytes = kWin) {
+    if (16 * lane() >= bytes) return;
+    const int b = 16 * lane(), hr = (int)std::min<int64_t>(hi - A, bytes);
+    const char *src = buf + A + (b < hr ? b : ((hr - 1) & ~15));
+    // inline asm, so the compiler tracks no pending write for it: with the intrinsic it
+    // waited for the DMA (vmcnt(0)) before reusing the address registers inside the sweep.
+    // Nothing reads the slot before read_window / slot_check wait for vmcnt(0) themselves;
+    // the compiler's own counted waits only over-wait for this older load.
+    const uint32_t lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)slot);
+    uint32_t m0_saved;  // M0 is the DMA's LDS base; whatever the compiler kept there is restored
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(m0_saved)
+                 : "v"(src), "s"(lds)
+                 : "memory");
+}
+// the slot after its LDS-DMA landed (every earlier vector-memory op of this wave done)
+__device__ __forceinline__ uint4 read_window(const uint4 *slot) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return slot[lane()];
+}
+// byte at relative offset o (uniform) of a landed slot
+__device__ __forceinline__ uint32_t slot_byte(const uint4 *slot, int o) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<const uint8_t *>(slot)[o]);
+}
+
+__global__ __launch_bounds__(kWalkThreads)
+#ifdef VCFXG_WALK_MAXW
+__attribute__((amdgpu_waves_per_eu(1, VCFXG_WALK_MAXW)))
+#endif
+void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chunk, int64_t n_walkers, int mode,
+               int64_t span0, uint64_t cap_w, uint64_t *__restrict__ le_o, int32_t *__restrict__ alt_o,
+               int32_t *__restrict__ tot_o, uint32_t *__restrict__ rowpre_o, uint8_t *__restrict__ status_o,
+               LineMeta *__restrict__ meta_o, uint64_t *__restrict__ wcount, uint32_t *__restrict__ wgt,
+               unsigned *overflow) {
+    __shared__ uint4 win[kWalkWaves][2][kWave];  // two window slots per wave (double buffer)
+    const int wv = threadIdx.x / kWave;
+    const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + wv);
     if (wk >= n_walkers) return;
     const int strip_cr = mode == 0 ? 1 : 0;
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
     int64_t L = wk == 0 ? lo : scan_nl(buf, cs - 1, hi) + 1;
     int64_t span = span0;  // predicted '\n' distance from the sample start
+    uint8_t cr_prev = 0;   // and the '\r' state of that record
     uint64_t n = 0;
     uint32_t ngt = 0;
     const uint64_t base = (uint64_t)wk * cap_w;
-    uint4 W = make_uint4(0, 0, 0, 0);
-    if (L < ce) W = load_window(buf, L, hi);
+    // per-line results held by lane (n & 63), written out 64 lines at a time (no stores --
+    // and no waits for their completion -- on the per-record path)
+    uint64_t r_le = 0, r_S = 0;
+    uint32_t r_alt = 0, r_tot = 0, r_pre = 0, r_k = 0;  // r_k: kind | sep << 8 | cr << 16 | status << 24
+    auto flush = [&](uint64_t first, uint32_t cnt) {
+        if ((uint32_t)lane() < cnt) {
+            const uint64_t o = base + first + lane();
+            const uint8_t kind = (uint8_t)r_k;
+            LineMeta m{};
+            m.kind = kind;
+            m.cr = (uint8_t)(r_k >> 16);
+            if (kind == kMetaGt) {
+                m.S = r_S;
+                m.rowpre = r_pre;
+                m.sep = (uint8_t)(r_k >> 8);
+            }
+            le_o[o] = r_le;
+            alt_o[o] = (int32_t)r_alt;
+            tot_o[o] = (int32_t)r_tot;
+            rowpre_o[o] = kind == kMetaGt ? r_pre : 0u;
+            status_o[o] = (uint8_t)(r_k >> 24);
+            meta_o[o] = m;
+        }
+    };
+    int cur = 0;
+    int64_t A = L & ~(int64_t)15;  // window base of the current line (L - A < 32)
+    if (L < ce) prefetch_window(buf, A, hi, win[wv][cur]);
     while (L < ce) {
         if (n >= cap_w) {
             if (lane() == 0) atomicOr(overflow, 1u);
             break;
         }
-        // ---- 1. window analysis
-        const int64_t A = L & ~(int64_t)15;
-        const int64_t blk = A + 16 * (int64_t)lane();
-        const int64_t wend = std::min<int64_t>(A + kWaveStep, hi);
-        const uint32_t nlm = eq_mask16(W, kRepNl) & range_mask16(blk, L, hi);
-        const uint64_t anyn = __ballot(nlm != 0u);
-        int64_t N1 = -1;
-        if (anyn) {
-            const int k = __builtin_ctzll(anyn);
-            N1 = uniform64(A + 16 * k + __builtin_ctz((uint32_t)__shfl((int)nlm, k)));
+        // ---- 1. window analysis (offsets relative to A); a head that does not fit the short
+        // window (no '\n' and fewer than 9 tabs in it) gets the 1 KiB window
+        const int b = 16 * lane();
+        const int Lr = (int)(L - A);
+        const uint4 *cw = win[wv][cur];
+        int hr, N1r, r4 = 0, r7 = 0, r8 = 0;
+        uint32_t ntab, first;
+        auto analyze = [&](int ws) {
+            const uint4 W = read_window(cw);
+            hr = (int)std::min<int64_t>(hi - A, ws);
+            const uint32_t nlm = eq_mask16(W, kRepNl) & range16(b, Lr, hr);
+            const uint64_t anyn = __ballot(nlm != 0u);
+            N1r = -1;
+            if (anyn) {
+                const int k = __builtin_ctzll(anyn);
+                N1r = __builtin_amdgcn_readfirstlane(16 * k + __builtin_ctz((uint32_t)__shfl((int)nlm, k)));
+            }
+            const uint32_t tm = eq_mask16(W, kRepTab) & range16(b, Lr, N1r >= 0 ? N1r : hr);
+            const uint32_t tc = __popc(tm);
+            const uint32_t tinc = wave_incl_scan(tc);
+            ntab = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tinc, kWave - 1));
+            first = slot_byte(cw, Lr);
+            if (ntab >= 9) {
+                r4 = tab_at(tm, tinc - tc, tc, 4, b);
+                r7 = tab_at(tm, tinc - tc, tc, 7, b);
+                r8 = tab_at(tm, tinc - tc, tc, 8, b);
+            }
+        };
+        analyze(kWin);
+        if (N1r < 0 && ntab < 9 && first != '#' && hr == kWin) {  // (rare) a long head
+            prefetch_window(buf, A, hi, win[wv][cur], kWaveStep);
+            analyze(kWaveStep);
         }
-        const int64_t lim = N1 >= 0 ? N1 : wend;
-        const uint32_t tm = eq_mask16(W, kRepTab) & range_mask16(blk, L, lim);
-        const uint32_t tc = __popc(tm);
-        const uint32_t tinc = wave_incl_scan(tc);
-        const uint32_t ntab = (uint32_t)__shfl((int)tinc, kWave - 1);
-        const uint32_t first = win_byte(W, A, L);
-        int64_t t4 = -1, t7 = -1, t8 = -1;
+        const int64_t wend = A + hr;
+        int64_t t4 = -1, t8 = -1;
         bool gt_head = false, gt_only = false;
         if (ntab >= 9 && first != '#') {
-            t4 = tab_at(tm, tinc - tc, tc, 4, blk);
-            t7 = tab_at(tm, tinc - tc, tc, 7, blk);
-            t8 = tab_at(tm, tinc - tc, tc, 8, blk);
-            if (t8 - t7 >= 3 && win_byte(W, A, t7 + 1) == 'G' && win_byte(W, A, t7 + 2) == 'T') {
-                gt_only = t8 - t7 == 3;
-                gt_head = gt_only || win_byte(W, A, t7 + 3) == ':';
+            t4 = A + r4;
+            t8 = A + r8;
+            if (r8 - r7 >= 3 && slot_byte(cw, r7 + 1) == 'G' && slot_byte(cw, r7 + 2) == 'T') {
+                gt_only = r8 - r7 == 3;
+                gt_head = gt_only || slot_byte(cw, r7 + 3) == ':';
             }
         }
-        // ---- 2. line end
+        // ---- 2. line end (and its '\r' in file mode)
         int64_t E;
+        uint8_t cr = 0;
         bool predicted = false;
-        if (N1 >= 0) {
-            E = N1;
-        } else if (gt_only && span > 0) {
+        if (N1r >= 0) {
+            E = A + N1r;
+            cr = strip_cr && E > L && slot_byte(cw, N1r - 1) == '\r';
+        } else if (gt_only && span > 0 && t8 + 1 + span <= hi) {
+            // predicted from the previous fixed-stride record; its end bytes come with the
+            // next window (which starts at E - 1) and are checked after the sweep
             E = t8 + 1 + span;
-            const bool ok = E < hi ? byte_at(buf, E) == '\n' : E == hi;
-            if (ok) predicted = true;
-            else E = scan_nl(buf, wend, hi);
+            cr = cr_prev;
+            predicted = true;
         } else {
             E = scan_nl(buf, wend, hi);
+            cr = strip_cr && E > L && __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r';
         }
-        // the next line's window, loaded before this line's sweep
-        uint4 Wn = make_uint4(0, 0, 0, 0);
-        if (E + 1 < ce) Wn = load_window(buf, E + 1, hi);
+        // every read of the current slot happens before the next prefetch is issued (an LDS
+        // read after it would make the compiler wait for the LDS-DMA)
+        const uint32_t sep_w = gt_head && t8 + 2 < wend ? slot_byte(cw, (int)(t8 + 2 - A)) : 0u;
+        // the next window (the next line's head, and bytes E - 1 and E): issued right after
+        // the sweep's first loads (issued before them, the sweep loop's head wait would
+        // hold its loads back until the window landed)
+        const int nxt = cur ^ 1;
+        int64_t An = std::max<int64_t>(E - 1, 0) & ~(int64_t)15;
+        bool pending = true;  // the prefetch for An is still to be issued
+        auto pre = [&]() {
+            prefetch_window(buf, An, hi, win[wv][nxt]);
+            pending = false;
+        };
         // ---- 3. kind (head_meta) and the sweep
-        uint8_t st = 0, kind, cr = 0, sep = 0;
+        uint8_t st = 0, kind = 0, sep = 0;
         uint32_t alt = 0, tot = 0, rowpre = 0;
         int64_t S = 0;
-        for (int pass = 0;; pass++) {
-            int64_t ae = E;
-            cr = 0;
-            if (strip_cr && E > L && byte_at(buf, E - 1) == '\r') {
-                ae = E - 1;
-                cr = 1;
-            }
+        bool ok = false;
+        auto sweep = [&]() {
+            const int64_t ae = E - cr;
             if (ae <= L) kind = kMetaEmpty;
             else if (first == '#') kind = kMetaHeader;
             else if (gt_head && t8 < ae) kind = kMetaGt;
             else kind = kMetaFull;
-            if (kind != kMetaGt) {
-                st = 0;
-                break;
-            }
-            S = t8 + 1;
-            rowpre = (uint32_t)(t4 - L + 1);
-            sep = t8 + 2 < ae ? (uint8_t)byte_at(buf, t8 + 2) : 0;
-            AfOp op{buf, ae, 0};
-            if (gt_fast(buf, S, ae, op, sep)) {
-                st = 1;
+            ok = false;
+            if (kind == kMetaGt) {
+                S = t8 + 1;
+                rowpre = (uint32_t)(t4 - L + 1);
+                sep = t8 + 2 >= ae ? 0
+                      : t8 + 2 < wend ? (uint8_t)sep_w
+                                      : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
+                AfOp op{buf, ae, 0};
+                ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
                 alt = op.alt;
                 tot = op.tot;
-                span = E - S;
-                break;
             }
-            st = kAfPending;  // not fixed-stride: k_af_complex runs the general sweep
-            if (!predicted || pass > 0) break;
-            // a rejected prediction: the true end, then the line again with it
-            const int64_t Et = scan_nl(buf, wend, hi);
-            predicted = false;
-            if (Et == E) break;
-            E = Et;
-            Wn = make_uint4(0, 0, 0, 0);
-            if (E + 1 < ce) Wn = load_window(buf, E + 1, hi);
+        };
+        sweep();
+        if (pending) pre();  // (no sweep ran)
+        if (predicted) {
+            // the prediction holds iff the sweep accepted every byte of [S, ae) and the end
+            // bytes are the '\n' (or the input end) and the predicted '\r' state
+            const uint4 *nw = win[wv][nxt];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t be = slot_byte(nw, (int)(E - An)), be1 = slot_byte(nw, (int)(E - 1 - An));
+            const bool endok = (E < hi ? be == '\n' : true) && ((strip_cr && be1 == '\r') == (cr != 0));
+            if (!(ok && endok)) {
+                const int64_t Et = scan_nl(buf, wend, hi);
+                if (Et != E || !endok) {  // the line again with its true bounds
+                    E = Et;
+                    cr = strip_cr && E > L && __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r';
+                    An = std::max<int64_t>(E - 1, 0) & ~(int64_t)15;
+                    pending = true;
+                    sweep();
+                    if (pending) pre();
+                }
+                // else: true bounds, not fixed-stride
+            }
         }
-        // ---- 4. outputs
-        if (lane() == 0) {
-            const uint64_t o = base + n;
-            LineMeta m{};
-            m.kind = kind;
-            m.cr = cr;
-            if (kind == kMetaGt) {
-                m.S = (uint64_t)S;
-                m.rowpre = rowpre;
-                m.sep = sep;
+        if (kind == kMetaGt) {
+            if (ok) {
+                st = 1;
+                span = E - S;
+                cr_prev = cr;
+            } else {
+                st = kAfPending;  // not fixed-stride: k_af_complex runs the general sweep
             }
-            le_o[o] = (uint64_t)E;
-            alt_o[o] = (int32_t)alt;
-            tot_o[o] = (int32_t)tot;
-            rowpre_o[o] = kind == kMetaGt ? rowpre : 0u;
-            status_o[o] = st;
-            meta_o[o] = m;
+        }
+        // ---- 4. results into lane n & 63
+        if ((uint32_t)lane() == (uint32_t)(n & 63)) {
+            r_le = (uint64_t)E;
+            r_S = (uint64_t)S;
+            r_alt = alt;
+            r_tot = tot;
+            r_pre = rowpre;
+            r_k = (uint32_t)kind | ((uint32_t)sep << 8) | ((uint32_t)cr << 16) | ((uint32_t)st << 24);
         }
         ngt += kind == kMetaGt ? 1u : 0u;
         n++;
+        if ((n & 63) == 0) flush(n - 64, 64);
         L = E + 1;
-        W = Wn;
+        A = An;
+        cur = nxt;
     }
+    if (n & 63) flush(n & ~(uint64_t)63, (uint32_t)(n & 63));
     if (lane() == 0) {
         wcount[wk] = n;
         wgt[wk] = ngt;
     }
 }
 
-// walker regions -> dense per-line arrays in file order (offs = exclusive scan of wcount);
-// the rows / data-line counters (every GT-first record counts as both) are reduced per block
+// walker regions -> dense per-line arrays in file order (offs = exclusive scan of wcount):
+// one thread per region slot, grid-stride; the rows / data-line counters (every GT-first
+// record counts as both) are reduced per block
 __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_t cap_w,
                                                       const uint64_t *__restrict__ offs,
                                                       const uint32_t *__restrict__ wgt,
@@ -250,21 +350,20 @@ __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_
                                                       LineMeta *meta, uint64_t *n_lines,
                                                       unsigned long long *counters) {
     __shared__ uint32_t red[256 / kWave];
-    // one wave per walker, lanes over its lines
-    const int64_t nw = (int64_t)gridDim.x * (256 / kWave);
+    const uint64_t nslots = (uint64_t)n_walkers * cap_w, stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t g = 0;
-    for (int64_t w = (int64_t)blockIdx.x * (256 / kWave) + threadIdx.x / kWave; w < n_walkers; w += nw) {
-        const uint64_t d0 = offs[w], n = offs[w + 1] - d0, s0 = (uint64_t)w * cap_w;
-        for (uint64_t i = lane(); i < n; i += kWave) {
-            const uint64_t s = s0 + i, d = d0 + i;
-            line_end[d] = le_b[s];
-            alt[d] = alt_b[s];
-            tot[d] = tot_b[s];
-            rowpre[d] = rowpre_b[s];
-            status[d] = status_b[s];
-            meta[d] = meta_b[s];
-        }
-        if (lane() == 0) g += wgt[w];
+    for (uint64_t sl = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; sl < nslots; sl += stride) {
+        const uint64_t w = sl / cap_w, i = sl - w * cap_w;
+        const uint64_t d0 = offs[w];
+        if (i == 0) g += wgt[w];
+        if (i >= offs[w + 1] - d0) continue;
+        const uint64_t d = d0 + i;
+        line_end[d] = le_b[sl];
+        alt[d] = alt_b[sl];
+        tot[d] = tot_b[sl];
+        rowpre[d] = rowpre_b[sl];
+        status[d] = status_b[sl];
+        meta[d] = meta_b[sl];
     }
     g = wave_sum(g);
     if (lane() == 0) red[threadIdx.x / kWave] = g;
@@ -299,7 +398,7 @@ hipError_t launch_walk_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t
                                const uint32_t *rowpre_b, const uint8_t *status_b, const void *meta_b,
                                uint64_t *line_end, int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
                                void *meta, uint64_t *n_lines, unsigned long long *counters, hipStream_t s) {
-    const int64_t blocks = std::min<int64_t>((n_walkers + 3) / 4, 2048);
+    const int64_t blocks = std::min<int64_t>(((int64_t)(n_walkers * cap_w) + 255) / 256, 2048);
     hipLaunchKernelGGL(k_walk_compact, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s, n_walkers, cap_w,
                        offs, wgt, le_b, alt_b, tot_b, rowpre_b, status_b, static_cast<const LineMeta *>(meta_b),
                        line_end, alt, tot, rowpre, status, static_cast<LineMeta *>(meta), n_lines, counters);

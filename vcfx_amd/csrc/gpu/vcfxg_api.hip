@@ -70,11 +70,13 @@ struct vcfxg_ctx {
     int64_t hint_span = 0, hint_line = 0;
     DevBuf scan_seg, nl_chunk;  // AF one-sweep path: per-chunk segment counts, newline -> chunk
     uint64_t af_line_cap = 0;   // fused AF: line capacity the last run needed
-    // region AF schedule: 0 = single-sweep index + head pass + fixed-stride sweep (default,
-    // fastest measured: two HBM sweeps), 1 = one-sweep look-back kernel (k_af_fused),
+    // region AF schedule: 0 = default (the walk schedule 7 when the first records average
+    // >= 512 B, else 3 with one host synchronisation: single-sweep index + head pass +
+    // fixed-stride sweep), 1 = one-sweep look-back kernel (k_af_fused),
     // 2 = chunk count + chunk sweep (k_af_chunks), 4 = one sweep with byte-class segment
     // counts (k_af_scan); the single-sweep alternatives are correct and tested but slower
-    // today, kept selectable for measurement
+    // today, kept selectable for measurement; 7 = walk (k_af_walk: predicted
+    // record ends validated by the sweep, one HBM pass); 8 = the two-sweep schedule always
     int af_path = getenv("VCFXG_AF_FUSED") ? atoi(getenv("VCFXG_AF_FUSED")) : 0;
     int fuse_dbg = getenv("VCFXG_FUSE_DEBUG") ? atoi(getenv("VCFXG_FUSE_DEBUG")) : 0;  // diagnostics only
     int64_t pipe_chunks = getenv("VCFXG_PIPE_CHUNKS") ? atol(getenv("VCFXG_PIPE_CHUNKS")) : 4096;  // 64 MiB pieces
@@ -831,8 +833,13 @@ int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_su
     if (c->af_path == 5) return af_region_pipe(c, data_start, mode, out);
     if (c->af_path == 6) return af_region_stream(c, data_start, mode, out);
     if (c->af_path == 7) return af_region_walk(c, data_start, mode, out);
+    if (c->af_path == 8) return af_region_async(c, data_start, mode, out);
     const uint64_t nc = (c->af_path == 1 || c->af_path == 2) ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
-    if (c->af_path == 0) return af_region_async(c, data_start, mode, out);
+    if (c->af_path == 0) {
+        // records of >= 512 B on average (a GT-dense VCF): the walk schedule, no index sweep
+        if (c->hint_line >= 512 && !c->walk_overflowed) return af_region_walk(c, data_start, mode, out);
+        return af_region_async(c, data_start, mode, out);
+    }
     if (!nc) {  // synchronous two-sweep schedule (VCFXG_AF_FUSED=3): index + record kernels
         int r = vcfxg_index(c, data_start, nullptr);
         return r ? r : vcfxg_allele_freq(c, mode, out);

@@ -35,60 +35,78 @@ __device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_
     op.dword(v);
 }
 
-// returns false (uniformly) if the record is not fixed-stride
-template <class Op>
-__device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &op, uint32_t sep_hint = 0) {
+// returns false (uniformly) if the record is not fixed-stride.  S and E must be
+// wave-uniform.  Offsets inside the record are 32-bit, relative to b0 = S & ~15 (records
+// are far below 2 GiB): no per-lane 64-bit bounds arithmetic, nothing for the compiler to
+// hoist into dozens of loop-invariant 64-bit registers.
+#ifndef VCFXG_UNROLL
+#define VCFXG_UNROLL 4
+#endif
+struct NoPre {
+    __device__ void operator()() const {}
+};
+// pre(): called once, right after the record's first batch of loads is issued
+template <int kUnroll = VCFXG_UNROLL, class Op, class Pre = NoPre>
+__device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &op, uint32_t sep_hint = 0,
+                        Pre pre = Pre()) {
+    S = uniform64(S);
+    E = uniform64(E);
     int64_t L = E - S;
     if (L < 3 || ((L + 1) & 3)) return false;
     // sep_hint: the byte at S + 1 when the caller already has it (saves a dependent load)
     uint32_t sepc = sep_hint ? sep_hint : byte_at(buf, S + 1);
+    sepc = __builtin_amdgcn_readfirstlane(sepc);
     if (sepc != '/' && sepc != '|') return false;
     const uint32_t exp_xor = 0x09000000u | (sepc << 8) | 0x00300030u;
     const uint32_t neutral = 0x092E002Eu | (sepc << 8);  // ". ." + tab: valid, reduces to nothing
     op.begin(sepc, neutral);
     const int s = (int)(S & 3);
     const int64_t b0 = S & ~(int64_t)15;
+    const char *__restrict__ base = buf + b0;
+    const int Sr = (int)(S - b0), Er = (int)(E - b0);  // record bounds relative to b0
+    const int lastblk = (Er - 1) & ~15;                 // block holding the record's last byte
     uint32_t err = 0;
     // kUnroll wave-steps per iteration: their loads are all issued before any is consumed
-#ifndef VCFXG_UNROLL
-#define VCFXG_UNROLL 4
-#endif
-    constexpr int kUnroll = VCFXG_UNROLL;
-    for (int64_t w0 = b0; w0 < E; w0 += kUnroll * kWaveStep) {
+    const int lo16 = lane() * kBlockBytes;
+    for (int w0 = 0; w0 < Er; w0 += kUnroll * kWaveStep) {
         uint4 v[kUnroll];
         uint32_t x4[kUnroll];
+        // branch-free loads: a lane past the record re-reads the record's last block (its
+        // bytes are masked below), so the loads issue back to back in one basic block
+        // (per-lane branches around them made the compiler wait for each before the next)
 #pragma unroll
         for (int u = 0; u < kUnroll; u++) {
-            const int64_t blk = w0 + (int64_t)u * kWaveStep + (int64_t)lane() * kBlockBytes;
-            if (blk < E) {
-                v[u] = load16(buf, blk);
-                x4[u] = load4(buf, blk + 16);
-            }
+            const int blk = w0 + u * kWaveStep + lo16;
+            const int bl = blk < Er ? blk : lastblk;
+            v[u] = load16(base, bl);
+            x4[u] = load4(base, bl + 16);
         }
+        if (w0 == 0) pre();  // e.g. a prefetch that must not hold up these loads
 #pragma unroll
         for (int u = 0; u < kUnroll; u++) {
-            const int64_t w = w0 + (int64_t)u * kWaveStep;
-            const int64_t blk = w + (int64_t)lane() * kBlockBytes;
+            const int w = w0 + u * kWaveStep;
+            const int blk = w + lo16;
             // interior step: every sample dword of every lane lies in [S, E) and is not the last
-            const bool interior = (w + s >= S) && (w + kWaveStep - 4 + s + 3 < E);
-            if (blk < E) {
+            const bool interior = (w + s >= Sr) && (w + kWaveStep - 1 + s < Er);
+            if (blk < Er) {
                 uint32_t d[4] = {__builtin_amdgcn_alignbyte(v[u].y, v[u].x, s),
                                  __builtin_amdgcn_alignbyte(v[u].z, v[u].y, s),
                                  __builtin_amdgcn_alignbyte(v[u].w, v[u].z, s),
                                  __builtin_amdgcn_alignbyte(x4[u], v[u].w, s)};
                 bool real[4] = {true, true, true, true};
                 if (!interior) {
+                    const int q0 = blk + s - Sr, last = Er - Sr - 3;  // dword i starts at S + q0 + 4i
 #pragma unroll
                     for (int i = 0; i < 4; i++) {
-                        int64_t p = blk + s + 4 * i;
-                        if (p < S || p + 3 > E) {
+                        const int q = q0 + 4 * i;
+                        if (q < 0 || q > last) {
                             d[i] = neutral;
                             real[i] = false;
-                        } else if (p + 3 == E) d[i] = (d[i] & 0x00FFFFFFu) | 0x09000000u;
+                        } else if (q == last) d[i] = (d[i] & 0x00FFFFFFu) | 0x09000000u;
                     }
                 }
 #pragma unroll
-                for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op, real[i], blk + s + 4 * i);
+                for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op, real[i], b0 + blk + s + 4 * i);
             }
         }
         if (op.done()) break;  // wave-uniform early exit (e.g. a match was found)

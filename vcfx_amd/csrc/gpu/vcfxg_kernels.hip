@@ -330,7 +330,11 @@ __device__ __forceinline__ void line_meta_one(const char *__restrict__ buf, int6
     meta[li] = head_meta(GlobalSrc{buf}, ls, le, strip_cr);
 }
 
-__global__ __launch_bounds__(kRecThreads) void k_af_sweep(const char *__restrict__ buf, int64_t data_start,
+__global__ __launch_bounds__(kRecThreads)
+#ifdef VCFXG_SWEEP_MAXW
+__attribute__((amdgpu_waves_per_eu(1, VCFXG_SWEEP_MAXW)))
+#endif
+void k_af_sweep(const char *__restrict__ buf, int64_t data_start,
                                                           const uint64_t *__restrict__ line_end,
                                                           const uint64_t *n_lines_p, int mode,
                                                           const AfMeta *__restrict__ meta,
