@@ -172,12 +172,11 @@ def main():
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
         def step():
-            eng.index(ds)
-            s = eng.filter_query(crits, "0|1", and_logic=True, strict=False)
+            s = eng.filter_query_region(ds, crits, "0|1", and_logic=True, strict=False)  # index + RF + GQ
             if red is not None:
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.warn_lines])
             return s
-        kern_names = ("line_count", "line_emit", "line_compact", "rf_records", "gq_records")
+        kern_names = ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "rf_records", "gq_records")
     else:
         W = a.window
 
@@ -274,6 +273,11 @@ def main():
                 "af_rows": L * (5 + 8 + 8 + 8),
                 "rf_records": region_bytes + L * (8 + 1),
                 "gq_records": region_bytes + L * (8 + 2),
+                # filter / query walk (no index sweep): the record bytes once + per line its
+                # region results (line_end 8, status 1, head record 16); the rest compacts them
+                # (read + write) and reads status + head record once more
+                "fq_walk": region_bytes + L * (8 + 1 + 16),
+                "fq_rest": L * (2 * (8 + 1 + 16) + 16 + 1),
             }
             dom = max((k for k in kernels if k in algo), key=kernels.get)
             ach = algo[dom] / (kernels[dom] * 1e-3) / 1e9

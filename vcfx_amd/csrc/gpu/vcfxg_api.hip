@@ -78,6 +78,9 @@ struct vcfxg_ctx {
     // today, kept selectable for measurement; 7 = walk (k_af_walk: predicted
     // record ends validated by the sweep, one HBM pass); 8 = the two-sweep schedule always
     int af_path = getenv("VCFXG_AF_FUSED") ? atoi(getenv("VCFXG_AF_FUSED")) : 0;
+    // record_filter / genotype_query region schedule: 0 = the walk (vcfxg_fq_walk.hip) when
+    // the first records average >= 512 B, 1 = the walk always, -1 = index + per-tool kernels
+    int fq_path = getenv("VCFXG_FQ_WALK") ? atoi(getenv("VCFXG_FQ_WALK")) : 0;
     int fuse_dbg = getenv("VCFXG_FUSE_DEBUG") ? atoi(getenv("VCFXG_FUSE_DEBUG")) : 0;  // diagnostics only
     int64_t pipe_chunks = getenv("VCFXG_PIPE_CHUNKS") ? atol(getenv("VCFXG_PIPE_CHUNKS")) : 4096;  // 64 MiB pieces
     std::vector<uint8_t> ld_gflag_host;  // per 128-variant group: all complete
@@ -1045,7 +1048,11 @@ static int compile_criteria(vcfxg_ctx *c, const vcfxg_criterion *crit, int n) {
         d.str_len = (uint32_t)h.str_len;
         pool.append(h.str ? h.str : "", h.str_len);
         vcfxg::ThresholdHost th;
-        vcfxg::threshold_bounds(h.numeric ? h.value : 0.0, th);
+        // FILTER and string INFO criteria never compare numbers: no boundary digits (they
+        // would only lengthen the pool the filter walk keeps in registers)
+        const bool cmp_num = h.target != vcfxg::RF_FILTER && (h.target != vcfxg::RF_INFO || h.numeric);
+        vcfxg::threshold_bounds(cmp_num && h.numeric ? h.value : 0.0, th);
+        if (!cmp_num) th.lo.digits.clear(), th.hi.digits.clear();
         d.T.t = h.numeric ? h.value : 0.0;
         d.T.kind = th.kind;
         d.T.lo = put_dec(th.lo, pool);
@@ -1133,6 +1140,130 @@ int vcfxg_filter_query(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and
         out->general_records = host_cnt[7];
     }
     return VCFXG_OK;
+}
+
+// record_filter / genotype_query / the fused pipeline over the data region in one pass
+// (vcfxg_fq_walk.hip): k_fq_walk reads each chunk's lines once (no separate index sweep), the
+// walkers' regions are concatenated in file order (k_fq_compact), k_fq_finish filters the
+// lines whose head did not fit the walk's window and counts, k_gq_complex takes the query's
+// general lines; ONE host synchronisation reads the counters.  Short lines (the first lines
+// average under 512 B), an earlier walk overflow on this input, or VCFXG_FQ_WALK=-1:
+// vcfxg_index + the per-tool call, with identical results.
+static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_criterion *crit, int n, int and_logic,
+                     const char *query, size_t qlen, int strict, int gq_strip_cr, vcfxg_summary *out) {
+    if (!c || n < 0 || (n && !crit) || (!query && qlen)) return VCFXG_E_ARG;
+    if (!c->loaded) return VCFXG_E_STATE;
+    if (data_start > c->n) data_start = c->n;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n, C = c->walk_chunk;
+    const int64_t nw = vcfxg::af_walkers(lo, hi, C);
+    if (!nw || c->fq_path < 0 || c->walk_overflowed || (c->fq_path == 0 && c->hint_line < 512)) {
+        int r = vcfxg_index(c, data_start, nullptr);
+        if (r) return r;
+        if (what == vcfxg::kFqRF) return vcfxg_record_filter(c, crit, n, and_logic, out);
+        if (what == vcfxg::kFqGQ) return vcfxg_genotype_query(c, query, qlen, strict, gq_strip_cr, out);
+        return vcfxg_filter_query(c, crit, n, and_logic, query, qlen, strict, out);
+    }
+    const bool rf = (what & vcfxg::kFqRF) != 0, gq = (what & vcfxg::kFqGQ) != 0;
+    const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
+    const uint64_t cap = (uint64_t)nw * cap_w;
+    const size_t mb = vcfxg::af_meta_bytes();
+    int r = ensure(c, c->wk_le, 8 * cap);
+    if (!r) r = ensure(c, c->wk_status, cap);
+    if (!r && gq) r = ensure(c, c->wk_meta, mb * cap);
+    if (!r) r = ensure(c, c->wk_count, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_offs, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_small, 128);
+    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
+    if (!r) r = ensure(c, c->status, cap + 1);
+    if (!r && gq) r = ensure(c, c->af_meta, mb * (cap + 1));
+    if (!r && gq) r = ensure(c, c->query, qlen + 1);
+    if (!r && rf) r = compile_criteria(c, crit, n);
+    if (r) return r;
+    int qa = -1, qb = -1;
+    if (gq) {
+        if (!strict) gq_parse_query(query, qlen, qa, qb);
+        c->query_host.assign(query, qlen);
+        if (qlen)
+            HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), qlen, hipMemcpyHostToDevice, c->stream));
+    }
+    const char *buf = P<char>(c->input);
+    unsigned *ovf = P<unsigned>(c->wk_small);
+    unsigned long long *cnt = P<unsigned long long>(c->counters);
+    unsigned long long *gq_cnt = what == vcfxg::kFqBoth ? cnt + 4 : cnt;
+    const int strip_cr = rf ? 1 : gq_strip_cr;  // the pipeline's query sees record_filter's output
+    const int pool_len = (int)c->pool_host.size();
+    const vcfxg::RfArgs ra{P<vcfxg::RfCrit>(c->crit), n, and_logic ? 1 : 0, P<char>(c->pool), pool_len,
+                           (n * vcfxg::kCritWords <= 64 && pool_len <= vcfxg::kPoolRegBytes) ? 1 : 0};
+    HIPCHK(c, hipMemsetAsync(ovf, 0, 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(cnt, 0, 64, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->wk_count) + nw, 0, 8, c->stream));
+    prof_begin(c, "fq_walk");
+    HIPCHK(c, vcfxg::launch_fq_walk(what, buf, lo, hi, C, strip_cr, c->hint_span, cap_w, ra, P<char>(c->query),
+                                    (int)qlen, strict, qa, qb, P<uint64_t>(c->wk_le), P<uint8_t>(c->wk_status),
+                                    c->wk_meta.p, P<uint64_t>(c->wk_count), ovf, c->stream));
+    prof_end(c, "fq_walk");
+    prof_begin(c, "fq_rest");
+    r = exclusive_scan(c, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_offs), (size_t)nw + 1);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_fq_compact(what, nw, cap_w, P<uint64_t>(c->wk_offs), P<uint64_t>(c->wk_le),
+                                       P<uint8_t>(c->wk_status), c->wk_meta.p, P<uint64_t>(c->line_end),
+                                       P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->d_nlines), c->stream));
+    HIPCHK(c, vcfxg::launch_fq_finish(what, buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, ra,
+                                      P<uint8_t>(c->status), c->af_meta.p, cnt, gq_cnt, c->stream));
+    if (gq)
+        HIPCHK(c, vcfxg::launch_gq_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, strip_cr,
+                                           P<char>(c->query), (int)qlen, strict, qa, qb, c->af_meta.p,
+                                           P<uint8_t>(c->status), gq_cnt,
+                                           what == vcfxg::kFqBoth ? P<uint8_t>(c->status) : nullptr, c->stream));
+    prof_end(c, "fq_rest");
+    static thread_local uint64_t host[10];
+    HIPCHK(c, hipMemcpyAsync(host, cnt, 64, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(host + 8, c->d_nlines.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(host + 9, ovf, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    if (host[9]) {  // a walker ran out of line slots (short lines): index + the per-tool kernels
+        c->walk_overflowed = true;
+        return fq_region(c, data_start, what, crit, n, and_logic, query, qlen, strict, gq_strip_cr, out);
+    }
+    c->data_start = data_start;
+    c->n_lines = host[8];
+    c->indexed = true;
+    c->text_bytes = 0;
+    if (out) {
+        std::memset(out, 0, sizeof *out);
+        out->n_lines = host[8];
+        if (what == vcfxg::kFqBoth) {
+            out->rows = host[4];        // kept by both stages
+            out->data_lines = host[0];  // kept by record_filter
+            out->warn_lines = host[6];
+            out->general_records = host[7];
+        } else {
+            out->rows = host[0];
+            out->data_lines = host[1];
+            if (gq) {
+                out->warn_lines = host[2];
+                out->general_records = host[3];
+            }
+        }
+    }
+    return VCFXG_OK;
+}
+
+int vcfxg_record_filter_region(vcfxg_ctx *c, size_t data_start, const vcfxg_criterion *crit, int n, int and_logic,
+                               vcfxg_summary *out) {
+    return fq_region(c, data_start, vcfxg::kFqRF, crit, n, and_logic, nullptr, 0, 0, 0, out);
+}
+
+int vcfxg_genotype_query_region(vcfxg_ctx *c, size_t data_start, const char *query, size_t qlen, int strict,
+                                int strip_cr, vcfxg_summary *out) {
+    return fq_region(c, data_start, vcfxg::kFqGQ, nullptr, 0, 0, query, qlen, strict, strip_cr, out);
+}
+
+int vcfxg_filter_query_region(vcfxg_ctx *c, size_t data_start, const vcfxg_criterion *crit, int n, int and_logic,
+                              const char *query, size_t qlen, int strict, vcfxg_summary *out) {
+    return fq_region(c, data_start, vcfxg::kFqBoth, crit, n, and_logic, query, qlen, strict, 1, out);
 }
 
 int vcfxg_variant_count(vcfxg_ctx *c, int strip_cr, vcfxg_summary *out) {

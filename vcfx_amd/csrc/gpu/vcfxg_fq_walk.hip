@@ -1,0 +1,414 @@
+// vcfxg_fq_walk.hip -- VCFX_record_filter, VCFX_genotype_query and the fused
+// `record_filter | genotype_query` pipeline (BASELINE config 3) without a separate line
+// index: the walk of vcfxg_af_walk.hip (one wave per chunk walks the chunk's lines, a
+// line's head analysed out of an LDS window fetched while the previous line was swept) with
+// the per-line work of the two tools:
+//
+//   * record_filter (kRF): evaluateLine (VCFX_record_filter.cpp:383-401) over fields 0-7,
+//     evaluated wave-uniformly (scalar code) out of the window held in registers (rf_eval,
+//     vcfxg_rf.h) before the line's sample sweep.  A line whose first 8
+//     tabs are not inside the 1 KiB window (or criteria / pool too large for the registers)
+//     is left to k_fq_finish (status kRfPending, the thread-per-line rf_line).
+//   * genotype_query (kGQ): checkAnySampleMatches (VCFX_genotype_query.cpp:322-345) on a
+//     GT-first record as the fixed-stride sweep with the early exit at the first match
+//     (gt_fast + GqOp, vcfxg_gt.h); everything else goes to k_gq_complex (kGqPending: the
+//     general sweep of a GT-first record; kGqFull: gq_line, the whole per-line path).
+//
+// A GT-only record's end may be PREDICTED from the walker's previous fixed-stride record
+// (as in the AF walk).  The prediction holds iff the byte at E is the '\n' (or E is the
+// input end), the '\r' state matches, and no '\n' lies in [S, E): the sweep validates every
+// byte it examines, and after an early exit (a match) the unswept rest is scanned for '\n'.
+// A rejected prediction re-runs the line with the '\n' found by a scan.
+//
+// Final statuses (the same arrays vcfxg_index + vcfxg_record_filter / vcfxg_genotype_query /
+// vcfxg_filter_query produce): RF 0 empty, 4 header, 1 kept, 2 dropped; GQ 1 match, 2 no
+// match, 3 "<9 fields" warning, 4 header, 0 empty; the pipeline maps the GQ verdicts of the
+// lines RF kept to 1 / 6 / 7 (gq_gated).  strip_cr: record_filter (and so the pipeline)
+// strips a trailing '\r' (:454-456 / :509-511); genotype_query alone does not.
+#include "vcfxg_device.h"
+#include "vcfxg_gt.h"
+#include "vcfxg_kernels.h"
+#include "vcfxg_rf.h"
+#include "vcfxg_walk.h"
+
+namespace vcfxg {
+
+constexpr int kFqUnroll = 6;
+// where the filter runs (measurement builds): 1 = before the query sweep (default), 0 = right
+// after the sweep's first loads are issued (its scalar state then spills: 239 VGPRs), 2 = not
+// at all (diagnostic only: results invalid)
+#ifndef VCFXG_FQ_RF_MODE
+#define VCFXG_FQ_RF_MODE 1
+#endif
+
+// The filter runs wave-uniformly out of registers, so it compiles to scalar code with no
+// memory access: the window bytes (lane o >> 4 holds window bytes [16 (o >> 4), +16)), the
+// threshold / string pool (up to 1 KiB: 4 bytes per lane in each of 4 registers) and the
+// compiled criteria (one dword per lane) are read with v_readlane at uniform indices.
+struct WinRegs {
+    uint4 W;
+    int64_t A;
+    __device__ __forceinline__ uint32_t operator[](int64_t p) const {
+        const int o = (int)(p - A);
+        const int q = (o >> 2) & 3;
+        const uint32_t v = q == 0 ? W.x : (q == 1 ? W.y : (q == 2 ? W.z : W.w));
+        return ((uint32_t)__builtin_amdgcn_readlane((int)v, o >> 4) >> ((o & 3) * 8)) & 0xFFu;
+    }
+};
+struct PoolRegs {
+    uint32_t v[kPoolRegs];  // pool dword w in register w >> 6 of lane w & 63
+    __device__ __forceinline__ uint32_t operator[](int64_t j) const {
+        const int w = (int)(j >> 2), r = w >> 6;
+        const uint32_t x = r == 0 ? v[0] : (r == 1 ? v[1] : (r == 2 ? v[2] : v[3]));
+        return ((uint32_t)__builtin_amdgcn_readlane((int)x, w & 63) >> (((int)j & 3) * 8)) & 0xFFu;
+    }
+};
+static_assert(kPoolRegs == 4, "PoolRegs selects among 4 registers");
+struct CritRegs {
+    uint32_t v;
+    __device__ __forceinline__ RfCrit operator[](int k) const {
+        RfCrit c;
+        uint32_t *w = reinterpret_cast<uint32_t *>(&c);
+#pragma unroll
+        for (int i = 0; i < kCritWords; i++) w[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, k * kCritWords + i);
+        return c;
+    }
+};
+
+template <bool kRF, bool kGQ>
+__global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict__ buf, int64_t lo, int64_t hi,
+                                                          int64_t chunk, int64_t n_walkers, int strip_cr,
+                                                          int64_t span0, uint64_t cap_w, RfArgs rf, GqQuery Q,
+                                                          uint64_t *__restrict__ le_o, uint8_t *__restrict__ status_o,
+                                                          LineMeta *__restrict__ meta_o, uint64_t *__restrict__ wcount,
+                                                          unsigned *overflow) {
+    __shared__ uint4 win[kWalkWaves][2][kWave];  // two window slots per wave (double buffer)
+    const int wv = threadIdx.x / kWave;
+    const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + wv);
+    if (wk >= n_walkers) return;
+    const int64_t cs = lo + wk * chunk;
+    const int64_t ce = std::min<int64_t>(cs + chunk, hi);
+    uint32_t critv = 0;  // the criteria, one dword per lane
+    PoolRegs pool{};     // and the pool
+    if (kRF && rf.regs) {
+        if (lane() < rf.ncrit * kCritWords) critv = reinterpret_cast<const uint32_t *>(rf.crit)[lane()];
+#pragma unroll
+        for (int r = 0; r < kPoolRegs; r++)
+            if (4 * (64 * r + lane()) < rf.pool_len) pool.v[r] = reinterpret_cast<const uint32_t *>(rf.pool)[64 * r + lane()];
+    }
+    int64_t L = wk == 0 ? lo : scan_nl(buf, cs - 1, hi) + 1;
+    int64_t span = kGQ ? span0 : 0;  // predicted '\n' distance from the sample start
+    uint8_t cr_prev = 0;             // and the '\r' state of that record
+    uint64_t n = 0;
+    const uint64_t base = (uint64_t)wk * cap_w;
+    // per-line results held by lane (n & 63), written out 64 lines at a time
+    uint64_t r_le = 0, r_S = 0;
+    uint32_t r_k = 0;  // kind | sep << 8 | cr << 16 | status << 24
+    auto flush = [&](uint64_t first, uint32_t cnt) {
+        if ((uint32_t)lane() < cnt) {
+            const uint64_t o = base + first + lane();
+            le_o[o] = r_le;
+            status_o[o] = (uint8_t)(r_k >> 24);
+            if (kGQ) {
+                LineMeta m{};
+                m.kind = (uint8_t)r_k;
+                m.cr = (uint8_t)(r_k >> 16);
+                if (m.kind == kMetaGt) {
+                    m.S = r_S;
+                    m.sep = (uint8_t)(r_k >> 8);
+                }
+                meta_o[o] = m;
+            }
+        }
+    };
+    int cur = 0;
+    int64_t A = L & ~(int64_t)15;  // window base of the current line (L - A < 16)
+    if (L < ce) prefetch_window(buf, A, hi, win[wv][cur]);
+    while (L < ce) {
+        if (n >= cap_w) {
+            if (lane() == 0) atomicOr(overflow, 1u);
+            break;
+        }
+        // ---- 1. window analysis (offsets relative to A): the first '\n', the first 9 tabs
+        const int b = 16 * lane();
+        const int Lr = (int)(L - A);
+        const uint4 *cw = win[wv][cur];
+        int hr, N1r, rt[9];
+        uint32_t ntab, first;
+        uint4 W;  // this lane's 16 window bytes
+        auto analyze = [&](int ws) {
+            W = read_window(cw);
+            hr = (int)std::min<int64_t>(hi - A, ws);
+            const uint32_t nlm = eq_mask16(W, kRepNl) & range16(b, Lr, hr);
+            const uint64_t anyn = __ballot(nlm != 0u);
+            N1r = -1;
+            if (anyn) {
+                const int k = __builtin_ctzll(anyn);
+                N1r = __builtin_amdgcn_readfirstlane(16 * k + __builtin_ctz((uint32_t)__shfl((int)nlm, k)));
+            }
+            const uint32_t tm = eq_mask16(W, kRepTab) & range16(b, Lr, N1r >= 0 ? N1r : hr);
+            const uint32_t tc = __popc(tm);
+            const uint32_t tinc = wave_incl_scan(tc);
+            ntab = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tinc, kWave - 1));
+            first = slot_byte(cw, Lr);
+#pragma unroll
+            for (int r = kRF ? 0 : 7; r < 9; r++) rt[r] = (uint32_t)r < ntab ? tab_at(tm, tinc - tc, tc, r, b) : 0;
+        };
+        analyze(kWin);
+        if (N1r < 0 && ntab < 9 && first != '#' && hr == kWin) {  // (rare) a long head
+            prefetch_window(buf, A, hi, win[wv][cur], kWaveStep);
+            analyze(kWaveStep);
+        }
+        const int64_t wend = A + hr;
+        const int64_t t8 = ntab >= 9 ? A + rt[8] : -1;
+        bool gt_head = false, gt_only = false;
+        if (ntab >= 9 && first != '#') {
+            const int r7 = rt[7], r8 = rt[8];
+            if (r8 - r7 >= 3 && slot_byte(cw, r7 + 1) == 'G' && slot_byte(cw, r7 + 2) == 'T') {
+                gt_only = r8 - r7 == 3;
+                gt_head = gt_only || slot_byte(cw, r7 + 3) == ':';
+            }
+        }
+        // fields 0-7 inside the window: the whole line, or its first 8 tabs (and criteria and
+        // pool small enough for the registers)
+        const bool rf_here = (N1r >= 0 || ntab >= 8) && rf.regs;
+        // ---- 2. line end (and its '\r' when stripped)
+        int64_t E;
+        uint8_t cr = 0;
+        bool predicted = false;
+        if (N1r >= 0) {
+            E = A + N1r;
+            cr = strip_cr && E > L && slot_byte(cw, N1r - 1) == '\r';
+        } else if (kGQ && gt_only && span > 0 && t8 + 1 + span <= hi) {
+            E = t8 + 1 + span;  // checked after the sweep (its end bytes come with the next window)
+            cr = cr_prev;
+            predicted = true;
+        } else {
+            E = scan_nl(buf, wend, hi);
+            cr = strip_cr && E > L && __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r';
+        }
+        const uint32_t sep_w = gt_head && t8 + 2 < wend ? slot_byte(cw, (int)(t8 + 2 - A)) : 0u;
+        // ---- 3. kind, the filter (scalar, out of the registers) and the query sweep; the next
+        // window's prefetch is issued right after the sweep's first loads
+        const int nxt = cur ^ 1;
+        int64_t An = std::max<int64_t>(E - 1, 0) & ~(int64_t)15;
+        bool pending = true;  // pre() still to run
+        uint8_t kind = 0, sep = 0;
+        int64_t ae = E - cr, S = 0, swept = 0;
+        bool keep = true;
+        auto filter = [&]() {
+            int64_t t[8];
+            const int nt = ntab < 8 ? (int)ntab : 8;
+#pragma unroll
+            for (int k = 0; k < 8; k++) t[k] = A + rt[k];
+            keep = rf_eval(WinRegs{W, A}, t, nt, L, ae, CritRegs{critv}, rf.ncrit, rf.and_logic, pool);
+        };
+        if (VCFXG_FQ_RF_MODE == 1 && kRF && rf_here && ae > L && first != '#') filter();
+        auto pre = [&]() {
+            if (VCFXG_FQ_RF_MODE == 0 && kRF && rf_here && kind != kMetaEmpty && kind != kMetaHeader) filter();
+            prefetch_window(buf, An, hi, win[wv][nxt]);
+            pending = false;
+        };
+        bool ok = false, found = false;
+        auto sweep = [&]() {
+            ae = E - cr;
+            if (ae <= L) kind = kMetaEmpty;
+            else if (first == '#') kind = kMetaHeader;
+            else if (gt_head && t8 < ae) kind = kMetaGt;
+            else kind = kMetaFull;
+            ok = found = false;
+            swept = ae;
+            if (kGQ && kind == kMetaGt) {
+                S = t8 + 1;
+                sep = t8 + 2 >= ae ? 0
+                      : t8 + 2 < wend ? (uint8_t)sep_w
+                                      : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
+                GqOp op{buf, ae, 0, Q};
+                ok = gt_fast<kFqUnroll>(buf, S, ae, op, sep, pre, &swept);
+                found = op.found;
+            }
+            if (pending) pre();
+        };
+        sweep();
+        if (predicted) {
+            const uint4 *nw = win[wv][nxt];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t be = slot_byte(nw, (int)(E - An)), be1 = slot_byte(nw, (int)(E - 1 - An));
+            const bool endok = (E < hi ? be == '\n' : true) && ((strip_cr && be1 == '\r') == (cr != 0));
+            // after an early exit the bytes past the sweep hold no '\n' only once scanned
+            const bool good = ok && endok && (swept >= ae || scan_nl(buf, swept, E) == E);
+            if (!good) {
+                const int64_t Et = scan_nl(buf, wend, hi);
+                if (Et != E || !endok) {  // the line again with its true bounds
+                    E = Et;
+                    cr = strip_cr && E > L && __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r';
+                    An = std::max<int64_t>(E - 1, 0) & ~(int64_t)15;
+                    pending = true;
+                    sweep();
+                }
+                // else: true bounds, not fixed-stride
+            }
+        }
+        if (kGQ && kind == kMetaGt && ok) {  // the next prediction
+            span = E - S;
+            cr_prev = cr;
+        }
+        // ---- 4. status
+        uint8_t st;
+        if (kind == kMetaEmpty) st = 0;
+        else if (kind == kMetaHeader) st = 4;
+        else if (kRF && !rf_here) {
+            st = kRfPending;  // k_fq_finish evaluates the filter (then k_gq_complex the query)
+            kind = kMetaFull;
+        } else if (!keep) {
+            st = 2;
+            kind = kMetaGated;
+        } else if (!kGQ) st = 1;
+        else if (kind == kMetaGt && ok) st = found ? 1 : (kRF ? 6 : 2);
+        else st = kind == kMetaGt ? kGqPending : kGqFull;
+        if ((uint32_t)lane() == (uint32_t)(n & 63)) {
+            r_le = (uint64_t)E;
+            r_S = (uint64_t)S;
+            r_k = (uint32_t)kind | ((uint32_t)sep << 8) | ((uint32_t)cr << 16) | ((uint32_t)st << 24);
+        }
+        n++;
+        if ((n & 63) == 0) flush(n - 64, 64);
+        L = E + 1;
+        A = An;
+        cur = nxt;
+    }
+    if (n & 63) flush(n & ~(uint64_t)63, (uint32_t)(n & 63));
+    if (lane() == 0) wcount[wk] = n;
+}
+
+// walker regions -> dense per-line arrays in file order (offs = exclusive scan of wcount)
+template <bool kMeta>
+__global__ __launch_bounds__(256) void k_fq_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t *__restrict__ offs,
+                                                    const uint64_t *__restrict__ le_b,
+                                                    const uint8_t *__restrict__ status_b,
+                                                    const LineMeta *__restrict__ meta_b, uint64_t *line_end,
+                                                    uint8_t *status, LineMeta *meta, uint64_t *n_lines) {
+    const uint64_t nslots = (uint64_t)n_walkers * cap_w, stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t sl = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; sl < nslots; sl += stride) {
+        const uint64_t w = sl / cap_w, i = sl - w * cap_w;
+        const uint64_t d0 = offs[w];
+        if (i >= offs[w + 1] - d0) continue;
+        const uint64_t d = d0 + i;
+        line_end[d] = le_b[sl];
+        status[d] = status_b[sl];
+        if (kMeta) meta[d] = meta_b[sl];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *n_lines = offs[n_walkers];
+}
+
+// per dense line: the filter of the lines the walk left to it (kRfPending), then the counters
+// the tools report -- record_filter: kept, data lines; genotype_query: the GT-first lines it
+// matched and examined (k_gq_complex adds the ones it takes)
+template <bool kRF, bool kGQ>
+__global__ __launch_bounds__(256) void k_fq_finish(const char *__restrict__ buf, int64_t data_start,
+                                                   const uint64_t *__restrict__ line_end, const uint64_t *n_lines_p,
+                                                   RfArgs rf, uint8_t *__restrict__ status, LineMeta *__restrict__ meta,
+                                                   unsigned long long *rf_cnt, unsigned long long *gq_cnt) {
+    __shared__ uint32_t red[4][256 / kWave];
+    const uint64_t n = *n_lines_p;
+    uint32_t c[4] = {0, 0, 0, 0};  // rf kept, rf data lines, gq matched, gq data lines
+    for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < n; li += gridDim.x * (uint64_t)blockDim.x) {
+        uint8_t st = status[li];
+        if (kRF && st == kRfPending) {
+            const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
+            int64_t ae = (int64_t)line_end[li];
+            if (ae > ls && buf[ae - 1] == '\r') ae--;
+            if (!rf_line(buf, ls, ae, rf.crit, rf.ncrit, rf.and_logic, rf.pool)) {
+                st = 2;
+                if (kGQ) meta[li].kind = kMetaGated;
+            } else st = kGQ ? kGqFull : 1;
+            status[li] = st;
+        }
+        if (kRF) {
+            c[0] += st != 0 && st != 4 && st != 2;
+            c[1] += st != 0 && st != 4;
+        }
+        if (kGQ) {
+            const uint8_t kind = meta[li].kind;
+            c[2] += kind == kMetaGt && st == 1;
+            c[3] += kind == kMetaGt;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t s = wave_sum(c[k]);
+        if (lane() == 0) red[k][threadIdx.x / kWave] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        uint32_t t = 0;
+        for (int w = 0; w < 256 / kWave; w++) t += red[threadIdx.x][w];
+        unsigned long long *dst = threadIdx.x < 2 ? (kRF ? rf_cnt + threadIdx.x : nullptr)
+                                                  : (kGQ ? gq_cnt + (threadIdx.x - 2) : nullptr);
+        if (t && dst) atomicAdd(dst, (unsigned long long)t);
+    }
+}
+
+template <bool kRF, bool kGQ>
+static hipError_t fq_walk_launch(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int strip_cr, int64_t span0,
+                                 uint64_t cap_w, const RfArgs &rf, const GqQuery &Q, uint64_t *le_b,
+                                 uint8_t *status_b, LineMeta *meta_b, uint64_t *wcount, unsigned *overflow,
+                                 hipStream_t s) {
+    const int64_t nw = af_walkers(lo, hi, chunk);
+    const unsigned grid = (unsigned)((nw + kWalkWaves - 1) / kWalkWaves);
+    hipLaunchKernelGGL((k_fq_walk<kRF, kGQ>), dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, strip_cr,
+                       span0, cap_w, rf, Q, le_b, status_b, meta_b, wcount, overflow);
+    return hipGetLastError();
+}
+
+hipError_t launch_fq_walk(int what, const char *buf, int64_t lo, int64_t hi, int64_t chunk, int strip_cr,
+                          int64_t span0, uint64_t cap_w, const RfArgs &rf, const char *q_dev, int qlen, int strict,
+                          int qa, int qb, uint64_t *le_b, uint8_t *status_b, void *meta_b, uint64_t *wcount,
+                          unsigned *overflow, hipStream_t s) {
+    if (!af_walkers(lo, hi, chunk)) return hipErrorInvalidValue;
+    const GqQuery Q{q_dev, qlen, strict, qa, qb};
+    LineMeta *m = static_cast<LineMeta *>(meta_b);
+    if (what == kFqRF)
+        return fq_walk_launch<true, false>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m,
+                                           wcount, overflow, s);
+    if (what == kFqGQ)
+        return fq_walk_launch<false, true>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m,
+                                           wcount, overflow, s);
+    return fq_walk_launch<true, true>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m, wcount,
+                                      overflow, s);
+}
+
+hipError_t launch_fq_compact(int what, int64_t n_walkers, uint64_t cap_w, const uint64_t *offs, const uint64_t *le_b,
+                             const uint8_t *status_b, const void *meta_b, uint64_t *line_end, uint8_t *status,
+                             void *meta, uint64_t *n_lines, hipStream_t s) {
+    const int64_t blocks = std::max<int64_t>(std::min<int64_t>(((int64_t)(n_walkers * cap_w) + 255) / 256, 2048), 1);
+    const LineMeta *mb = static_cast<const LineMeta *>(meta_b);
+    LineMeta *m = static_cast<LineMeta *>(meta);
+    if (what == kFqRF)
+        hipLaunchKernelGGL(k_fq_compact<false>, dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs, le_b,
+                           status_b, mb, line_end, status, m, n_lines);
+    else
+        hipLaunchKernelGGL(k_fq_compact<true>, dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs, le_b,
+                           status_b, mb, line_end, status, m, n_lines);
+    return hipGetLastError();
+}
+
+hipError_t launch_fq_finish(int what, const char *buf, int64_t data_start, const uint64_t *line_end,
+                            const uint64_t *n_lines_dev, uint64_t n_lines_host, const RfArgs &rf, uint8_t *status,
+                            void *meta, unsigned long long *rf_cnt, unsigned long long *gq_cnt, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<uint64_t>((n_lines_host + 255) / 256, 1024);
+    LineMeta *m = static_cast<LineMeta *>(meta);
+    if (what == kFqRF)
+        hipLaunchKernelGGL((k_fq_finish<true, false>), dim3(grid), dim3(256), 0, s, buf, data_start, line_end,
+                           n_lines_dev, rf, status, m, rf_cnt, gq_cnt);
+    else if (what == kFqGQ)
+        hipLaunchKernelGGL((k_fq_finish<false, true>), dim3(grid), dim3(256), 0, s, buf, data_start, line_end,
+                           n_lines_dev, rf, status, m, rf_cnt, gq_cnt);
+    else
+        hipLaunchKernelGGL((k_fq_finish<true, true>), dim3(grid), dim3(256), 0, s, buf, data_start, line_end,
+                           n_lines_dev, rf, status, m, rf_cnt, gq_cnt);
+    return hipGetLastError();
+}
+
+}  // namespace vcfxg

@@ -45,10 +45,12 @@ __device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_
 struct NoPre {
     __device__ void operator()() const {}
 };
-// pre(): called once, right after the record's first batch of loads is issued
+// pre(): called once, right after the record's first batch of loads is issued.
+// swept (optional): the end of the bytes the sweep examined -- E, or on an early exit
+// (op.done()) the end of the last batch of loads
 template <int kUnroll = VCFXG_UNROLL, class Op, class Pre = NoPre>
 __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &op, uint32_t sep_hint = 0,
-                        Pre pre = Pre()) {
+                        Pre pre = Pre(), int64_t *swept = nullptr) {
     S = uniform64(S);
     E = uniform64(E);
     int64_t L = E - S;
@@ -66,6 +68,7 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
     const int Sr = (int)(S - b0), Er = (int)(E - b0);  // record bounds relative to b0
     const int lastblk = (Er - 1) & ~15;                 // block holding the record's last byte
     uint32_t err = 0;
+    if (swept) *swept = E;
     // kUnroll wave-steps per iteration: their loads are all issued before any is consumed
     const int lo16 = lane() * kBlockBytes;
     for (int w0 = 0; w0 < Er; w0 += kUnroll * kWaveStep) {
@@ -109,7 +112,10 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
                 for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op, real[i], b0 + blk + s + 4 * i);
             }
         }
-        if (op.done()) break;  // wave-uniform early exit (e.g. a match was found)
+        if (op.done()) {  // wave-uniform early exit (e.g. a match was found)
+            if (swept && b0 + w0 + kUnroll * kWaveStep < E) *swept = b0 + w0 + kUnroll * kWaveStep;
+            break;
+        }
     }
     if (__any(err != 0u)) return false;
     op.finish();

@@ -17,6 +17,9 @@ struct LineMeta {
     uint8_t pad;
 };
 constexpr uint8_t kAfPending = 0xFF;  // AF status of a kMetaGt line whose fast sweep failed
+constexpr uint8_t kGqPending = 0xFE;  // GQ: a kMetaGt line whose fast sweep failed (general sweep)
+constexpr uint8_t kRfPending = 0xFD;  // RF walk: head beyond the window (k_fq_finish filters it)
+constexpr uint8_t kGqFull = 0xFC;     // GQ walk: a kMetaFull line for k_gq_complex's gq_line
 
 // single-sweep index over 16 KiB wave-chunks (idx_wchunks of them): counts + the first
 // idx_pos_cap() newline offsets per chunk, then a compaction into line_end (overflow != 0:
@@ -101,6 +104,12 @@ hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
                              int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,
                              hipStream_t s, const uint8_t *gate, void *meta = nullptr);
+// k_gq_complex alone (the query's general lines after the filter / query walk): lines of
+// kind kMetaFull (gq_line) and kMetaGt lines with status kGqPending (general sweep)
+hipError_t launch_gq_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
+                             int qlen, int strict, int qa, int qb, const void *meta, uint8_t *status,
+                             unsigned long long *counters, const uint8_t *gate, hipStream_t s);
 // asynchronous AF region path: capacity-guarded compaction, device-side line count and
 // a one-record summary for the single host synchronisation
 hipError_t launch_nl_compact_cap(int64_t lo, int64_t hi, const uint32_t *counts, const uint64_t *offs,

@@ -742,7 +742,6 @@ __global__ __launch_bounds__(kRecThreads) void k_gq_records(const char *__restri
 // genotype_query as head pass (k_line_meta) + sweep: GT-first lines run only the sample
 // sweep (gt_fast with the GqOp early exit); full-path lines and fast-sweep failures go to
 // k_gq_complex (status kGqPending marks the latter)
-constexpr uint8_t kGqPending = 0xFE;
 
 __global__ __launch_bounds__(kRecThreads) void k_gq_sweep(const char *__restrict__ buf,
                                                           const uint64_t *__restrict__ line_end,
@@ -1043,6 +1042,17 @@ hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t
     unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
     hipLaunchKernelGGL(k_gq_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
                        strip_cr, Q, lm, status, counters, gate);
+    return hipGetLastError();
+}
+hipError_t launch_gq_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
+                             int qlen, int strict, int qa, int qb, const void *meta, uint8_t *status,
+                             unsigned long long *counters, const uint8_t *gate, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    GqQuery Q{q_dev, qlen, strict, qa, qb};
+    unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
+    hipLaunchKernelGGL(k_gq_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                       strip_cr, Q, static_cast<const LineMeta *>(meta), status, counters, gate);
     return hipGetLastError();
 }
 hipError_t launch_nl_compact_cap(int64_t lo, int64_t hi, const uint32_t *counts, const uint64_t *offs,

@@ -13,6 +13,8 @@
 // The accepted grammar is strtod's: leading isspace, sign, inf/infinity/nan/nan(...)
 // (case-insensitive), 0x hex with optional binary exponent, decimal with optional
 // exponent; anything left unconsumed makes the parse fail (criterion false).
+// Byte sources (B: the text, PB: the threshold digit pool) are anything indexable as
+// src[i] -> byte: a global pointer, or a wave's register copy (vcfxg_fq_walk.hip).
 #pragma once
 #include <stdint.h>
 
@@ -57,7 +59,8 @@ struct NumText {
     bool zero;
 };
 
-__device__ __forceinline__ bool ieq(const char *buf, int64_t p, int64_t e, const char *w) {
+template <class B>
+__device__ __forceinline__ bool ieq(const B &buf, int64_t p, int64_t e, const char *w) {
     int i = 0;
     for (; w[i]; i++)
         if (p + i >= e || lower((uint8_t)buf[p + i]) != (uint32_t)w[i]) return false;
@@ -65,7 +68,8 @@ __device__ __forceinline__ bool ieq(const char *buf, int64_t p, int64_t e, const
 }
 
 // exact hex-float value (round half to even), mantissa digits [p, e) after "0x"
-__device__ inline double hex_value(const char *buf, int64_t p, int64_t me, int64_t bexp) {
+template <class B>
+__device__ inline double hex_value(const B &buf, int64_t p, int64_t me, int64_t bexp) {
     // accumulate up to 64 significant bits; later nonzero bits -> sticky
     uint64_t m = 0;
     int shift = 0;   // binary exponent adjustment
@@ -133,7 +137,8 @@ __device__ inline double hex_value(const char *buf, int64_t p, int64_t me, int64
 }
 
 // parse text [p, e) with strtod's grammar; success only if everything is consumed
-__device__ inline NumText parse_number(const char *buf, int64_t p, int64_t e) {
+template <class B>
+__device__ inline NumText parse_number(const B &buf, int64_t p, int64_t e) {
     NumText r;
     r.kind = -1;
     r.v = 0;
@@ -278,7 +283,8 @@ __device__ inline NumText parse_number(const char *buf, int64_t p, int64_t e) {
 
 // compare |text| digits (from s0, skipping '.') with a pool digit string; both with the
 // same exponent.  -1 / 0 / +1
-__device__ inline int cmp_digits(const char *buf, int64_t s0, int64_t me, const char *pool, uint32_t off, uint32_t n) {
+template <class B, class PB>
+__device__ inline int cmp_digits(const B &buf, int64_t s0, int64_t me, const PB &pool, uint32_t off, uint32_t n) {
     int64_t k = s0;
     uint32_t j = 0;
     for (;;) {
@@ -304,7 +310,8 @@ __device__ inline int cmp_digits(const char *buf, int64_t s0, int64_t me, const 
 }
 
 // 3-way compare of the decimal text with a boundary
-__device__ inline int cmp_dec(const char *buf, const NumText &x, const DecRef &b, const char *pool) {
+template <class B, class PB>
+__device__ inline int cmp_dec(const B &buf, const NumText &x, const DecRef &b, const PB &pool) {
     if (b.inf) return b.sign > 0 ? -1 : 1;
     int sa = x.zero ? 0 : x.sign, sb = b.n == 0 ? 0 : b.sign;
     if (sa != sb) return sa < sb ? -1 : 1;
@@ -337,8 +344,9 @@ __device__ __forceinline__ bool cmp_double(double x, int op, double y) {
 }
 
 // parseDouble(text) && compareDouble(x, op, t); *parsed = parse success
-__device__ inline bool num_compare(const char *buf, int64_t p, int64_t e, const NumThreshold &T, int op, const char *pool,
-                            bool *parsed) {
+template <class B, class PB>
+__device__ inline bool num_compare(const B &buf, int64_t p, int64_t e, const NumThreshold &T, int op, const PB &pool,
+                                   bool *parsed) {
     NumText x = parse_number(buf, p, e);
     *parsed = x.kind >= 0;
     if (x.kind < 0) return false;

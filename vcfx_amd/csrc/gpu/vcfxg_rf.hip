@@ -11,81 +11,6 @@
 
 namespace vcfxg {
 
-struct Field {
-    int64_t p, e;
-};
-
-// extractField(line, i) for i <= 7 given the first nt (<= 8) tab offsets
-__device__ __forceinline__ Field field_of(const int64_t *t, int nt, int64_t ls, int64_t ae, int i) {
-    if (nt < i) return {ae, ae};  // "not enough fields" -> empty
-    int64_t p = i ? t[i - 1] + 1 : ls;
-    int64_t e = nt > i ? t[i] : ae;
-    return {p, e};
-}
-
-__device__ __forceinline__ bool bytes_eq(const char *buf, int64_t p, int64_t n, const char *pool, uint32_t off,
-                                         uint32_t len) {
-    if ((uint64_t)n != len) return false;
-    for (uint32_t k = 0; k < len; k++)
-        if (buf[p + k] != pool[off + k]) return false;
-    return true;
-}
-
-__device__ bool eval_crit(const char *__restrict__ buf, const int64_t *t, int nt, int64_t ls, int64_t ae,
-                          const RfCrit &c, const char *__restrict__ pool) {
-    bool parsed;
-    switch (c.target) {
-    case RF_POS: {
-        Field f = field_of(t, nt, ls, ae, 1);
-        if (f.e <= f.p) return false;
-        return num_compare(buf, f.p, f.e, c.T, c.op, pool, &parsed);
-    }
-    case RF_QUAL: {
-        Field f = field_of(t, nt, ls, ae, 5);
-        if (f.e <= f.p || (f.e - f.p == 1 && buf[f.p] == '.')) return cmp_double(0.0, c.op, c.T.t);
-        return num_compare(buf, f.p, f.e, c.T, c.op, pool, &parsed);
-    }
-    case RF_FILTER: {
-        if (c.numeric) return false;
-        Field f = field_of(t, nt, ls, ae, 6);
-        bool eq = bytes_eq(buf, f.p, f.e - f.p, pool, c.str_off, c.str_len);
-        return c.op == OPN_EQ ? eq : (c.op == OPN_NE ? !eq : false);
-    }
-    default: {
-        Field f = field_of(t, nt, ls, ae, 7);
-        if (f.e <= f.p || (f.e - f.p == 1 && buf[f.p] == '.')) return false;
-        // token scan
-        int64_t p = f.p;
-        int64_t vp = -1, ve = -1;
-        while (p < f.e) {
-            int64_t te = p;
-            while (te < f.e && buf[te] != ';') te++;
-            int64_t eq = p;
-            while (eq < te && buf[eq] != '=') eq++;
-            if (eq < te) {
-                if (bytes_eq(buf, p, eq - p, pool, c.key_off, c.key_len)) {
-                    vp = eq + 1;
-                    ve = te;
-                    break;
-                }
-            } else if (bytes_eq(buf, p, te - p, pool, c.key_off, c.key_len)) {
-                vp = p;
-                ve = te;
-                break;
-            }
-            p = te + 1;
-        }
-        if (vp < 0) return false;
-        if (c.numeric) {
-            if (ve <= vp) return false;
-            return num_compare(buf, vp, ve, c.T, c.op, pool, &parsed);
-        }
-        bool eq = bytes_eq(buf, vp, ve - vp, pool, c.str_off, c.str_len);
-        return c.op == OPN_EQ ? eq : (c.op == OPN_NE ? !eq : false);
-    }
-    }
-}
-
 // status: 0 empty (after '\r' strip; printed as "\n"), 4 header, 1 kept, 2 dropped
 __global__ __launch_bounds__(256) void k_rf_records(const char *__restrict__ buf, int64_t data_start,
                                                     const uint64_t *__restrict__ line_end, const uint64_t *n_lines_p,
@@ -106,18 +31,7 @@ __global__ __launch_bounds__(256) void k_rf_records(const char *__restrict__ buf
         else if (buf[ls] == '#') st = 4;
         else {
             data++;
-            int64_t t[8];
-            int nt = 0;
-            for (int64_t p = ls; p < ae && nt < 8; p++)
-                if (buf[p] == '\t') t[nt++] = p;
-            bool res;
-            if (and_logic) {
-                res = true;
-                for (int k = 0; k < ncrit && res; k++) res = eval_crit(buf, t, nt, ls, ae, crit[k], pool);
-            } else {
-                res = false;
-                for (int k = 0; k < ncrit && !res; k++) res = eval_crit(buf, t, nt, ls, ae, crit[k], pool);
-            }
+            const bool res = rf_line(buf, ls, ae, crit, ncrit, and_logic, pool);
             st = res ? 1 : 2;
             kept += res;
         }

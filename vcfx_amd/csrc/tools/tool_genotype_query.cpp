@@ -83,9 +83,10 @@ bool run_gq(const Input &in, bool stream_mode, const std::string &q, bool strict
         uint64_t nl = 0;
         vcfxg_summary s;
         if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
-            !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
-            !gpu_ok(g, vcfxg_genotype_query(g, q.data(), q.size(), strict ? 1 : 0, 0, &s), "genotype_query", err.fd))
+            !gpu_ok(g, vcfxg_genotype_query_region(g, data_start, q.data(), q.size(), strict ? 1 : 0, 0, &s),
+                    "genotype_query", err.fd))
             return false;
+        nl = s.n_lines;
         std::vector<uint64_t> ends(nl);
         std::vector<uint8_t> st(nl);
         if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||

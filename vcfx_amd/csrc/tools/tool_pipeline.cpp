@@ -63,12 +63,12 @@ extern "C" int vcfx_pipeline_filter_query(const char *filter, const char *logic,
         vcfxg_summary s;
         std::vector<vcfxg_criterion> abi = to_abi(cs);
         if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
-            !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
             !gpu_ok(g,
-                    vcfxg_filter_query(g, abi.data(), (int)abi.size(), and_logic ? 1 : 0, query, strlen(query),
-                                       strict, &s),
+                    vcfxg_filter_query_region(g, data_start, abi.data(), (int)abi.size(), and_logic ? 1 : 0, query,
+                                              strlen(query), strict, &s),
                     "filter_query", err.fd))
             return 1;
+        nl = s.n_lines;
         std::vector<uint64_t> ends(nl);
         std::vector<uint8_t> st(nl);
         if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||

@@ -152,10 +152,10 @@ bool run_rf(const Input &in, bool stdin_mode, const std::vector<Criterion> &cs, 
     vcfxg_summary s;
     std::vector<vcfxg_criterion> abi = to_abi(cs);
     if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
-        !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
-        !gpu_ok(g, vcfxg_record_filter(g, abi.data(), (int)abi.size(), and_logic ? 1 : 0, &s), "record_filter",
-                err.fd))
+        !gpu_ok(g, vcfxg_record_filter_region(g, data_start, abi.data(), (int)abi.size(), and_logic ? 1 : 0, &s),
+                "record_filter", err.fd))
         return false;
+    nl = s.n_lines;
     std::vector<uint64_t> ends(nl);
     std::vector<uint8_t> st(nl);
     if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||

@@ -58,6 +58,9 @@ SIGNATURES = {
     "vcfxg_selftest_mfma_i8": (_I, [_VP, ctypes.POINTER(_I)]),
     "vcfxg_selftest_mfma_fp4": (_I, [_VP, ctypes.POINTER(_I)]),
     "vcfxg_filter_query": (_I, [_VP, _VP, _I, _I, _P, _S, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_record_filter_region": (_I, [_VP, _S, _VP, _I, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_genotype_query_region": (_I, [_VP, _S, _P, _S, _I, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_filter_query_region": (_I, [_VP, _S, _VP, _I, _I, _P, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_fetch_text": (_I, [_VP, _VP, _S]),
     "vcfxg_fetch_lines": (_I, [_VP, _U64, _U64, _VP, _VP, _VP]),
 }
@@ -187,6 +190,32 @@ class Engine:
                                             len(q), int(strict), ctypes.byref(s)), "filter_query")
         return s
 
+    def record_filter_region(self, data_start, crits, and_logic=True):
+        """index + record_filter in one call (vcfxg_record_filter_region)."""
+        s = Summary()
+        arr = self._criteria(crits)
+        self._chk(self.L.vcfxg_record_filter_region(self.h, data_start, ctypes.cast(arr, ctypes.c_void_p), len(crits),
+                                                    int(and_logic), ctypes.byref(s)), "record_filter_region")
+        return s
+
+    def genotype_query_region(self, data_start, query, strict=False, strip_cr=False):
+        """index + genotype_query in one call (vcfxg_genotype_query_region)."""
+        q = query.encode() if isinstance(query, str) else query
+        s = Summary()
+        self._chk(self.L.vcfxg_genotype_query_region(self.h, data_start, q, len(q), int(strict), int(strip_cr),
+                                                     ctypes.byref(s)), "genotype_query_region")
+        return s
+
+    def filter_query_region(self, data_start, crits, query, and_logic=True, strict=False):
+        """index + the fused record_filter | genotype_query in one call (vcfxg_filter_query_region)."""
+        s = Summary()
+        arr = self._criteria(crits)
+        q = query.encode() if isinstance(query, str) else query
+        self._chk(self.L.vcfxg_filter_query_region(self.h, data_start, ctypes.cast(arr, ctypes.c_void_p), len(crits),
+                                                   int(and_logic), q, len(q), int(strict), ctypes.byref(s)),
+                  "filter_query_region")
+        return s
+
     def ld_prepare(self, n_samples, id_dot_to_pos=True, region=None):
         n = ctypes.c_uint64()
         rc, rs, re_ = (region[0].encode(), region[1], region[2]) if region else (b"", 0, 0)
@@ -224,6 +253,13 @@ class Engine:
         self._chk(self.L.vcfxg_fetch_lines(self.h, 0, n, alt.ctypes.data, tot.ctypes.data, st.ctypes.data),
                   "fetch_lines")
         return alt, tot, st
+
+    def statuses(self, n):
+        """per-line status bytes of the last call (no counts)."""
+        import numpy as np
+        st = np.zeros(max(n, 1), np.uint8)
+        self._chk(self.L.vcfxg_fetch_lines(self.h, 0, n, None, None, st.ctypes.data), "fetch_lines")
+        return st[:n]
 
     def line_ends(self, n):
         import numpy as np
