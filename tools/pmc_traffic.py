@@ -32,6 +32,8 @@ KERNELS = {
     "af_complex": r"vcfxg::k_af_complex\(",
     "af_format": r"vcfxg::k_af_format\(",
     "rf_records": r"vcfxg::k_rf_records\(",
+    "fq_walk": r"vcfxg::k_fq_walk<",
+    "fq_rest": r"vcfxg::k_(fq_compact<|fq_finish<|gq_complex\()",
     "gq_records": r"vcfxg::k_(line_meta|gq_sweep|gq_complex)\(",
     "ld_parse": r"vcfxg::k_ld_parse\(",
     "ld_count": r"vcfxg::k_ld_fast<1>\(",
@@ -40,6 +42,22 @@ KERNELS = {
     "ld_emit_gen": r"vcfxg::k_ld_block<2>\(",
     "ld_matrix": r"vcfxg::k_ld_matrix\(",
 }
+
+
+# the engine names bench.py times per workload (a symbol shared by two names, e.g.
+# k_af_complex, would otherwise leave a spurious entry under a workload that never times it)
+TIMED = {
+    "af": ("af_scan", "line_count", "line_emit", "line_compact", "af_records", "af_chunks", "af_fused",
+           "af_pipe", "af_stream", "af_walk", "walk_compact", "af_complex", "af_format"),
+    "pipeline": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "rf_records", "gq_records"),
+    "ld": ("line_count", "line_emit", "line_compact", "ld_parse", "ld_count", "ld_emit", "ld_count_gen",
+           "ld_emit_gen", "ld_matrix"),
+}
+
+
+# names that share a symbol with another name: kept only when their own primary kernel ran
+PRIMARY = {"af_records": "vcfxg::k_af_sweep", "af_pipe": "vcfxg::k_nl_compact_piece",
+           "af_stream": "vcfxg::k_af_stream", "gq_records": "vcfxg::k_gq_sweep", "fq_rest": "vcfxg::k_fq_compact<"}
 
 
 # names whose kernels launch several times per step (one per pipelined piece): the per-step
@@ -61,6 +79,7 @@ def per_kernel(path, counter):
                     acc[k] = acc.get(k, 0.0) + float(row["Counter_Value"])
                     sym = name.split("(")[0]
                     calls.setdefault(k, {})[sym] = calls.setdefault(k, {}).get(sym, 0) + 1
+    acc = {k: v for k, v in acc.items() if k not in PRIMARY or any(PRIMARY[k] in s for s in calls[k])}
     return {k: v / (calls[k].get(ANCHOR[k], 0) if k in ANCHOR and calls[k].get(ANCHOR[k]) else max(calls[k].values()))
             for k, v in acc.items()}
 
@@ -78,6 +97,8 @@ def main():
         d = {}
     res = {}
     for k in sorted(set(fetch) | set(write)):
+        if workload in TIMED and k not in TIMED[workload]:
+            continue
         fb = fetch.get(k, 0.0) * 1024 * 2   # KB -> bytes, gfx950 streaming-read correction (x2)
         wb = write.get(k, 0.0) * 1024
         res[k] = {"fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb,
