@@ -63,6 +63,7 @@ struct vcfxg_ctx {
     DevBuf af_meta;             // AF head pass output (k_af_meta)
     // walk AF path (vcfxg_af_walk.hip): per-walker regions, counts, scan, flags
     DevBuf wk_le, wk_alt, wk_tot, wk_rowpre, wk_status, wk_meta, wk_count, wk_offs, wk_gt, wk_small;
+    DevBuf wk_tabs, rf_tabs;    // filter / query walk: per-line tab offsets (per walker, dense)
     int64_t walk_chunk = getenv("VCFXG_WALK_CHUNK") ? atol(getenv("VCFXG_WALK_CHUNK")) : 128 * 1024;
     bool walk_overflowed = false;  // the last walk run overflowed: two-sweep schedule
     // host hints taken at load time from the first data line: its '\n' distance from the
@@ -214,7 +215,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->st_le, &c->st_alt, &c->st_tot, &c->st_rowpre, &c->st_status, &c->st_meta, &c->st_bcount, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->st_le, &c->st_alt, &c->st_tot, &c->st_rowpre, &c->st_status, &c->st_meta, &c->st_bcount, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs})
         if (b->p) (void)hipFree(b->p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
@@ -1171,6 +1172,8 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
     int r = ensure(c, c->wk_le, 8 * cap);
     if (!r) r = ensure(c, c->wk_status, cap);
     if (!r && gq) r = ensure(c, c->wk_meta, mb * cap);
+    if (!r && rf) r = ensure(c, c->wk_tabs, 16 * cap);
+    if (!r && rf) r = ensure(c, c->rf_tabs, 16 * (cap + 1));
     if (!r) r = ensure(c, c->wk_count, 8 * (size_t)(nw + 1));
     if (!r) r = ensure(c, c->wk_offs, 8 * (size_t)(nw + 1));
     if (!r) r = ensure(c, c->wk_small, 128);
@@ -1193,24 +1196,24 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
     unsigned long long *gq_cnt = what == vcfxg::kFqBoth ? cnt + 4 : cnt;
     const int strip_cr = rf ? 1 : gq_strip_cr;  // the pipeline's query sees record_filter's output
     const int pool_len = (int)c->pool_host.size();
-    const vcfxg::RfArgs ra{P<vcfxg::RfCrit>(c->crit), n, and_logic ? 1 : 0, P<char>(c->pool), pool_len,
-                           (n * vcfxg::kCritWords <= 64 && pool_len <= vcfxg::kPoolRegBytes) ? 1 : 0};
+    const vcfxg::RfArgs ra{P<vcfxg::RfCrit>(c->crit), n, and_logic ? 1 : 0, P<char>(c->pool), pool_len};
     HIPCHK(c, hipMemsetAsync(ovf, 0, 8, c->stream));
     HIPCHK(c, hipMemsetAsync(cnt, 0, 64, c->stream));
     HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->wk_count) + nw, 0, 8, c->stream));
     prof_begin(c, "fq_walk");
     HIPCHK(c, vcfxg::launch_fq_walk(what, buf, lo, hi, C, strip_cr, c->hint_span, cap_w, ra, P<char>(c->query),
                                     (int)qlen, strict, qa, qb, P<uint64_t>(c->wk_le), P<uint8_t>(c->wk_status),
-                                    c->wk_meta.p, P<uint64_t>(c->wk_count), ovf, c->stream));
+                                    c->wk_meta.p, c->wk_tabs.p, P<uint64_t>(c->wk_count), ovf, c->stream));
     prof_end(c, "fq_walk");
     prof_begin(c, "fq_rest");
     r = exclusive_scan(c, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_offs), (size_t)nw + 1);
     if (r) return r;
     HIPCHK(c, vcfxg::launch_fq_compact(what, nw, cap_w, P<uint64_t>(c->wk_offs), P<uint64_t>(c->wk_le),
-                                       P<uint8_t>(c->wk_status), c->wk_meta.p, P<uint64_t>(c->line_end),
-                                       P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->d_nlines), c->stream));
+                                       P<uint8_t>(c->wk_status), c->wk_meta.p, c->wk_tabs.p, P<uint64_t>(c->line_end),
+                                       P<uint8_t>(c->status), c->af_meta.p, c->rf_tabs.p, P<uint64_t>(c->d_nlines),
+                                       c->stream));
     HIPCHK(c, vcfxg::launch_fq_finish(what, buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, ra,
-                                      P<uint8_t>(c->status), c->af_meta.p, cnt, gq_cnt, c->stream));
+                                      P<uint8_t>(c->status), c->af_meta.p, c->rf_tabs.p, cnt, gq_cnt, c->stream));
     if (gq)
         HIPCHK(c, vcfxg::launch_gq_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, strip_cr,
                                            P<char>(c->query), (int)qlen, strict, qa, qb, c->af_meta.p,

@@ -4,11 +4,11 @@
 // line's head analysed out of an LDS window fetched while the previous line was swept) with
 // the per-line work of the two tools:
 //
-//   * record_filter (kRF): evaluateLine (VCFX_record_filter.cpp:383-401) over fields 0-7,
-//     evaluated wave-uniformly (scalar code) out of the window held in registers (rf_eval,
-//     vcfxg_rf.h) before the line's sample sweep.  A line whose first 8
-//     tabs are not inside the 1 KiB window (or criteria / pool too large for the registers)
-//     is left to k_fq_finish (status kRfPending, the thread-per-line rf_line).
+//   * record_filter (kRF): evaluateLine (VCFX_record_filter.cpp:383-401) over fields 0-7
+//     (rf_eval, vcfxg_rf.h), given the first 8 tabs found in the line's window, evaluated
+//     lane-parallel for a batch of 64 lines when the batch is flushed.  A line whose first
+//     8 tabs are not inside the 1 KiB window is left to k_fq_finish (status kRfPending, the
+//     thread-per-line rf_line).
 //   * genotype_query (kGQ): checkAnySampleMatches (VCFX_genotype_query.cpp:322-345) on a
 //     GT-first record as the fixed-stride sweep with the early exit at the first match
 //     (gt_fast + GqOp, vcfxg_gt.h); everything else goes to k_gq_complex (kGqPending: the
@@ -34,45 +34,29 @@
 namespace vcfxg {
 
 constexpr int kFqUnroll = 6;
-// where the filter runs (measurement builds): 1 = before the query sweep (default), 0 = right
-// after the sweep's first loads are issued (its scalar state then spills: 239 VGPRs), 2 = not
-// at all (diagnostic only: results invalid)
-#ifndef VCFXG_FQ_RF_MODE
-#define VCFXG_FQ_RF_MODE 1
-#endif
-
-// The filter runs wave-uniformly out of registers, so it compiles to scalar code with no
-// memory access: the window bytes (lane o >> 4 holds window bytes [16 (o >> 4), +16)), the
-// threshold / string pool (up to 1 KiB: 4 bytes per lane in each of 4 registers) and the
-// compiled criteria (one dword per lane) are read with v_readlane at uniform indices.
-struct WinRegs {
-    uint4 W;
-    int64_t A;
+// The filter does not run in the walk: the walk stores each data line's first 8 tab offsets
+// (u16 from the line start, 0xFFFF past the last tab) and k_fq_finish evaluates rf_eval
+// thread-per-line from them (the bytes through a 16-byte block cache per thread).  Evaluated
+// in the walk itself, wave-uniformly, the filter's scalar code serialised every line behind
+// it (and its state spilled the walk's SGPRs).
+struct BlockBytes {  // byte source: the 16-byte aligned block of the last byte read (per lane)
+    const char *__restrict__ buf;
+    mutable int64_t base;
+    mutable uint4 v;
     __device__ __forceinline__ uint32_t operator[](int64_t p) const {
-        const int o = (int)(p - A);
-        const int q = (o >> 2) & 3;
-        const uint32_t v = q == 0 ? W.x : (q == 1 ? W.y : (q == 2 ? W.z : W.w));
-        return ((uint32_t)__builtin_amdgcn_readlane((int)v, o >> 4) >> ((o & 3) * 8)) & 0xFFu;
+        const int64_t b = p & ~(int64_t)15;
+        if (b != base) {  // the input is padded, so the block is always readable
+            v = *reinterpret_cast<const uint4 *>(buf + b);
+            base = b;
+        }
+        const int o = (int)(p & 15), q = o >> 2;
+        const uint32_t w = q == 0 ? v.x : (q == 1 ? v.y : (q == 2 ? v.z : v.w));
+        return (w >> ((o & 3) * 8)) & 0xFFu;
     }
 };
-struct PoolRegs {
-    uint32_t v[kPoolRegs];  // pool dword w in register w >> 6 of lane w & 63
-    __device__ __forceinline__ uint32_t operator[](int64_t j) const {
-        const int w = (int)(j >> 2), r = w >> 6;
-        const uint32_t x = r == 0 ? v[0] : (r == 1 ? v[1] : (r == 2 ? v[2] : v[3]));
-        return ((uint32_t)__builtin_amdgcn_readlane((int)x, w & 63) >> (((int)j & 3) * 8)) & 0xFFu;
-    }
-};
-static_assert(kPoolRegs == 4, "PoolRegs selects among 4 registers");
-struct CritRegs {
-    uint32_t v;
-    __device__ __forceinline__ RfCrit operator[](int k) const {
-        RfCrit c;
-        uint32_t *w = reinterpret_cast<uint32_t *>(&c);
-#pragma unroll
-        for (int i = 0; i < kCritWords; i++) w[i] = (uint32_t)__builtin_amdgcn_readlane((int)v, k * kCritWords + i);
-        return c;
-    }
+struct PoolBytes {
+    const char *__restrict__ p;
+    __device__ __forceinline__ uint32_t operator[](int64_t i) const { return (uint8_t)p[i]; }
 };
 
 template <bool kRF, bool kGQ>
@@ -80,22 +64,14 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
                                                           int64_t chunk, int64_t n_walkers, int strip_cr,
                                                           int64_t span0, uint64_t cap_w, RfArgs rf, GqQuery Q,
                                                           uint64_t *__restrict__ le_o, uint8_t *__restrict__ status_o,
-                                                          LineMeta *__restrict__ meta_o, uint64_t *__restrict__ wcount,
-                                                          unsigned *overflow) {
+                                                          LineMeta *__restrict__ meta_o, uint4 *__restrict__ tabs_o,
+                                                          uint64_t *__restrict__ wcount, unsigned *overflow) {
     __shared__ uint4 win[kWalkWaves][2][kWave];  // two window slots per wave (double buffer)
     const int wv = threadIdx.x / kWave;
     const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + wv);
     if (wk >= n_walkers) return;
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
-    uint32_t critv = 0;  // the criteria, one dword per lane
-    PoolRegs pool{};     // and the pool
-    if (kRF && rf.regs) {
-        if (lane() < rf.ncrit * kCritWords) critv = reinterpret_cast<const uint32_t *>(rf.crit)[lane()];
-#pragma unroll
-        for (int r = 0; r < kPoolRegs; r++)
-            if (4 * (64 * r + lane()) < rf.pool_len) pool.v[r] = reinterpret_cast<const uint32_t *>(rf.pool)[64 * r + lane()];
-    }
     int64_t L = wk == 0 ? lo : scan_nl(buf, cs - 1, hi) + 1;
     int64_t span = kGQ ? span0 : 0;  // predicted '\n' distance from the sample start
     uint8_t cr_prev = 0;             // and the '\r' state of that record
@@ -104,11 +80,13 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
     // per-line results held by lane (n & 63), written out 64 lines at a time
     uint64_t r_le = 0, r_S = 0;
     uint32_t r_k = 0;  // kind | sep << 8 | cr << 16 | status << 24
+    uint32_t r_t[4] = {0, 0, 0, 0};  // kRF: tabs 0-7, u16 offsets from the line start
     auto flush = [&](uint64_t first, uint32_t cnt) {
         if ((uint32_t)lane() < cnt) {
             const uint64_t o = base + first + lane();
             le_o[o] = r_le;
             status_o[o] = (uint8_t)(r_k >> 24);
+            if (kRF) tabs_o[o] = make_uint4(r_t[0], r_t[1], r_t[2], r_t[3]);
             if (kGQ) {
                 LineMeta m{};
                 m.kind = (uint8_t)r_k;
@@ -171,7 +149,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
         }
         // fields 0-7 inside the window: the whole line, or its first 8 tabs (and criteria and
         // pool small enough for the registers)
-        const bool rf_here = (N1r >= 0 || ntab >= 8) && rf.regs;
+        const bool rf_here = N1r >= 0 || ntab >= 8;
         // ---- 2. line end (and its '\r' when stripped)
         int64_t E;
         uint8_t cr = 0;
@@ -188,24 +166,14 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
             cr = strip_cr && E > L && __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r';
         }
         const uint32_t sep_w = gt_head && t8 + 2 < wend ? slot_byte(cw, (int)(t8 + 2 - A)) : 0u;
-        // ---- 3. kind, the filter (scalar, out of the registers) and the query sweep; the next
+        // ---- 3. kind and the query sweep; the next
         // window's prefetch is issued right after the sweep's first loads
         const int nxt = cur ^ 1;
         int64_t An = std::max<int64_t>(E - 1, 0) & ~(int64_t)15;
         bool pending = true;  // pre() still to run
         uint8_t kind = 0, sep = 0;
         int64_t ae = E - cr, S = 0, swept = 0;
-        bool keep = true;
-        auto filter = [&]() {
-            int64_t t[8];
-            const int nt = ntab < 8 ? (int)ntab : 8;
-#pragma unroll
-            for (int k = 0; k < 8; k++) t[k] = A + rt[k];
-            keep = rf_eval(WinRegs{W, A}, t, nt, L, ae, CritRegs{critv}, rf.ncrit, rf.and_logic, pool);
-        };
-        if (VCFXG_FQ_RF_MODE == 1 && kRF && rf_here && ae > L && first != '#') filter();
         auto pre = [&]() {
-            if (VCFXG_FQ_RF_MODE == 0 && kRF && rf_here && kind != kMetaEmpty && kind != kMetaHeader) filter();
             prefetch_window(buf, An, hi, win[wv][nxt]);
             pending = false;
         };
@@ -260,16 +228,22 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
         else if (kRF && !rf_here) {
             st = kRfPending;  // k_fq_finish evaluates the filter (then k_gq_complex the query)
             kind = kMetaFull;
-        } else if (!keep) {
-            st = 2;
-            kind = kMetaGated;
-        } else if (!kGQ) st = 1;
+        } else if (!kGQ) st = 1;  // (k_fq_finish drops the lines the filter rejects)
         else if (kind == kMetaGt && ok) st = found ? 1 : (kRF ? 6 : 2);
         else st = kind == kMetaGt ? kGqPending : kGqFull;
         if ((uint32_t)lane() == (uint32_t)(n & 63)) {
             r_le = (uint64_t)E;
             r_S = (uint64_t)S;
             r_k = (uint32_t)kind | ((uint32_t)sep << 8) | ((uint32_t)cr << 16) | ((uint32_t)st << 24);
+            if (kRF) {
+                const int Lr = (int)(L - A);
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const uint32_t a0 = (uint32_t)(2 * k) < ntab ? (uint32_t)(rt[2 * k] - Lr) : 0xFFFFu;
+                    const uint32_t a1 = (uint32_t)(2 * k + 1) < ntab ? (uint32_t)(rt[2 * k + 1] - Lr) : 0xFFFFu;
+                    r_t[k] = a0 | a1 << 16;
+                }
+            }
         }
         n++;
         if ((n & 63) == 0) flush(n - 64, 64);
@@ -282,12 +256,13 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
 }
 
 // walker regions -> dense per-line arrays in file order (offs = exclusive scan of wcount)
-template <bool kMeta>
+template <bool kMeta, bool kTabs>
 __global__ __launch_bounds__(256) void k_fq_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t *__restrict__ offs,
                                                     const uint64_t *__restrict__ le_b,
                                                     const uint8_t *__restrict__ status_b,
-                                                    const LineMeta *__restrict__ meta_b, uint64_t *line_end,
-                                                    uint8_t *status, LineMeta *meta, uint64_t *n_lines) {
+                                                    const LineMeta *__restrict__ meta_b,
+                                                    const uint4 *__restrict__ tabs_b, uint64_t *line_end,
+                                                    uint8_t *status, LineMeta *meta, uint4 *tabs, uint64_t *n_lines) {
     const uint64_t nslots = (uint64_t)n_walkers * cap_w, stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t sl = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; sl < nslots; sl += stride) {
         const uint64_t w = sl / cap_w, i = sl - w * cap_w;
@@ -297,18 +272,21 @@ __global__ __launch_bounds__(256) void k_fq_compact(int64_t n_walkers, uint64_t 
         line_end[d] = le_b[sl];
         status[d] = status_b[sl];
         if (kMeta) meta[d] = meta_b[sl];
+        if (kTabs) tabs[d] = tabs_b[sl];
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *n_lines = offs[n_walkers];
 }
 
-// per dense line: the filter of the lines the walk left to it (kRfPending), then the counters
-// the tools report -- record_filter: kept, data lines; genotype_query: the GT-first lines it
-// matched and examined (k_gq_complex adds the ones it takes)
+// per dense line: the filter (from the tabs the walk stored, or with its own tab scan for the
+// lines whose head outgrew the window: kRfPending), then the counters the tools report --
+// record_filter: kept, data lines; genotype_query: the GT-first lines it matched and examined
+// (k_gq_complex adds the ones it takes)
 template <bool kRF, bool kGQ>
 __global__ __launch_bounds__(256) void k_fq_finish(const char *__restrict__ buf, int64_t data_start,
                                                    const uint64_t *__restrict__ line_end, const uint64_t *n_lines_p,
                                                    RfArgs rf, uint8_t *__restrict__ status, LineMeta *__restrict__ meta,
-                                                   unsigned long long *rf_cnt, unsigned long long *gq_cnt) {
+                                                   const uint4 *__restrict__ tabs, unsigned long long *rf_cnt,
+                                                   unsigned long long *gq_cnt) {
     __shared__ uint32_t red[4][256 / kWave];
     const uint64_t n = *n_lines_p;
     uint32_t c[4] = {0, 0, 0, 0};  // rf kept, rf data lines, gq matched, gq data lines
@@ -323,6 +301,26 @@ __global__ __launch_bounds__(256) void k_fq_finish(const char *__restrict__ buf,
                 if (kGQ) meta[li].kind = kMetaGated;
             } else st = kGQ ? kGqFull : 1;
             status[li] = st;
+        } else if (kRF && st != 0 && st != 4) {  // a data line with its 8 tabs (or all of them) stored
+            const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
+            int64_t ae = (int64_t)line_end[li];
+            const BlockBytes B{buf, -1, {}};
+            if (ae > ls && B[ae - 1] == '\r') ae--;
+            const uint4 tv = tabs[li];
+            const uint32_t tw[4] = {tv.x, tv.y, tv.z, tv.w};
+            int64_t t[8];
+            int nt = 0;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint32_t o = (tw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                t[k] = ls + o;
+                nt += o != 0xFFFFu;
+            }
+            if (!rf_eval(B, t, nt, ls, ae, rf.crit, rf.ncrit, rf.and_logic, PoolBytes{rf.pool})) {
+                st = 2;
+                if (kGQ) meta[li].kind = kMetaGated;
+                status[li] = st;
+            }
         }
         if (kRF) {
             c[0] += st != 0 && st != 4 && st != 2;
@@ -352,62 +350,70 @@ __global__ __launch_bounds__(256) void k_fq_finish(const char *__restrict__ buf,
 template <bool kRF, bool kGQ>
 static hipError_t fq_walk_launch(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int strip_cr, int64_t span0,
                                  uint64_t cap_w, const RfArgs &rf, const GqQuery &Q, uint64_t *le_b,
-                                 uint8_t *status_b, LineMeta *meta_b, uint64_t *wcount, unsigned *overflow,
-                                 hipStream_t s) {
+                                 uint8_t *status_b, LineMeta *meta_b, uint4 *tabs_b, uint64_t *wcount,
+                                 unsigned *overflow, hipStream_t s) {
     const int64_t nw = af_walkers(lo, hi, chunk);
     const unsigned grid = (unsigned)((nw + kWalkWaves - 1) / kWalkWaves);
     hipLaunchKernelGGL((k_fq_walk<kRF, kGQ>), dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, strip_cr,
-                       span0, cap_w, rf, Q, le_b, status_b, meta_b, wcount, overflow);
+                       span0, cap_w, rf, Q, le_b, status_b, meta_b, tabs_b, wcount, overflow);
     return hipGetLastError();
 }
 
 hipError_t launch_fq_walk(int what, const char *buf, int64_t lo, int64_t hi, int64_t chunk, int strip_cr,
                           int64_t span0, uint64_t cap_w, const RfArgs &rf, const char *q_dev, int qlen, int strict,
-                          int qa, int qb, uint64_t *le_b, uint8_t *status_b, void *meta_b, uint64_t *wcount,
-                          unsigned *overflow, hipStream_t s) {
+                          int qa, int qb, uint64_t *le_b, uint8_t *status_b, void *meta_b, void *tabs_b,
+                          uint64_t *wcount, unsigned *overflow, hipStream_t s) {
     if (!af_walkers(lo, hi, chunk)) return hipErrorInvalidValue;
     const GqQuery Q{q_dev, qlen, strict, qa, qb};
     LineMeta *m = static_cast<LineMeta *>(meta_b);
+    uint4 *t = static_cast<uint4 *>(tabs_b);
     if (what == kFqRF)
-        return fq_walk_launch<true, false>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m,
+        return fq_walk_launch<true, false>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m, t,
                                            wcount, overflow, s);
     if (what == kFqGQ)
-        return fq_walk_launch<false, true>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m,
+        return fq_walk_launch<false, true>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m, t,
                                            wcount, overflow, s);
-    return fq_walk_launch<true, true>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m, wcount,
+    return fq_walk_launch<true, true>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m, t, wcount,
                                       overflow, s);
 }
 
 hipError_t launch_fq_compact(int what, int64_t n_walkers, uint64_t cap_w, const uint64_t *offs, const uint64_t *le_b,
-                             const uint8_t *status_b, const void *meta_b, uint64_t *line_end, uint8_t *status,
-                             void *meta, uint64_t *n_lines, hipStream_t s) {
+                             const uint8_t *status_b, const void *meta_b, const void *tabs_b, uint64_t *line_end,
+                             uint8_t *status, void *meta, void *tabs, uint64_t *n_lines, hipStream_t s) {
     const int64_t blocks = std::max<int64_t>(std::min<int64_t>(((int64_t)(n_walkers * cap_w) + 255) / 256, 2048), 1);
     const LineMeta *mb = static_cast<const LineMeta *>(meta_b);
     LineMeta *m = static_cast<LineMeta *>(meta);
+    const uint4 *tb = static_cast<const uint4 *>(tabs_b);
+    uint4 *t = static_cast<uint4 *>(tabs);
     if (what == kFqRF)
-        hipLaunchKernelGGL(k_fq_compact<false>, dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs, le_b,
-                           status_b, mb, line_end, status, m, n_lines);
+        hipLaunchKernelGGL((k_fq_compact<false, true>), dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs,
+                           le_b, status_b, mb, tb, line_end, status, m, t, n_lines);
+    else if (what == kFqGQ)
+        hipLaunchKernelGGL((k_fq_compact<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs,
+                           le_b, status_b, mb, tb, line_end, status, m, t, n_lines);
     else
-        hipLaunchKernelGGL(k_fq_compact<true>, dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs, le_b,
-                           status_b, mb, line_end, status, m, n_lines);
+        hipLaunchKernelGGL((k_fq_compact<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs,
+                           le_b, status_b, mb, tb, line_end, status, m, t, n_lines);
     return hipGetLastError();
 }
 
 hipError_t launch_fq_finish(int what, const char *buf, int64_t data_start, const uint64_t *line_end,
                             const uint64_t *n_lines_dev, uint64_t n_lines_host, const RfArgs &rf, uint8_t *status,
-                            void *meta, unsigned long long *rf_cnt, unsigned long long *gq_cnt, hipStream_t s) {
+                            void *meta, const void *tabs, unsigned long long *rf_cnt, unsigned long long *gq_cnt,
+                            hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
     const unsigned grid = (unsigned)std::min<uint64_t>((n_lines_host + 255) / 256, 1024);
     LineMeta *m = static_cast<LineMeta *>(meta);
+    const uint4 *t = static_cast<const uint4 *>(tabs);
     if (what == kFqRF)
         hipLaunchKernelGGL((k_fq_finish<true, false>), dim3(grid), dim3(256), 0, s, buf, data_start, line_end,
-                           n_lines_dev, rf, status, m, rf_cnt, gq_cnt);
+                           n_lines_dev, rf, status, m, t, rf_cnt, gq_cnt);
     else if (what == kFqGQ)
         hipLaunchKernelGGL((k_fq_finish<false, true>), dim3(grid), dim3(256), 0, s, buf, data_start, line_end,
-                           n_lines_dev, rf, status, m, rf_cnt, gq_cnt);
+                           n_lines_dev, rf, status, m, t, rf_cnt, gq_cnt);
     else
         hipLaunchKernelGGL((k_fq_finish<true, true>), dim3(grid), dim3(256), 0, s, buf, data_start, line_end,
-                           n_lines_dev, rf, status, m, rf_cnt, gq_cnt);
+                           n_lines_dev, rf, status, m, t, rf_cnt, gq_cnt);
     return hipGetLastError();
 }
 

@@ -133,20 +133,18 @@ struct RfArgs {
     int ncrit, and_logic;
     const char *pool;
     int pool_len;
-    int regs;  // criteria and pool fit one VGPR each (the walk evaluates from registers)
 };
-constexpr int kCritWords = (int)(sizeof(RfCrit) / 4);
-constexpr int kPoolRegs = 4, kPoolRegBytes = kPoolRegs * 64 * 4;  // the walk's register copy of the pool
-static_assert(sizeof(RfCrit) % 4 == 0, "RfCrit is read as dwords");
 hipError_t launch_fq_walk(int what, const char *buf, int64_t lo, int64_t hi, int64_t chunk, int strip_cr,
                           int64_t span0, uint64_t cap_w, const RfArgs &rf, const char *q_dev, int qlen, int strict,
-                          int qa, int qb, uint64_t *le_b, uint8_t *status_b, void *meta_b, uint64_t *wcount,
-                          unsigned *overflow, hipStream_t s);
+                          int qa, int qb, uint64_t *le_b, uint8_t *status_b, void *meta_b, void *tabs_b,
+                          uint64_t *wcount, unsigned *overflow, hipStream_t s);
+// tabs: per line 16 B, the first 8 tab offsets (u16 from the line start, 0xFFFF = none)
 hipError_t launch_fq_compact(int what, int64_t n_walkers, uint64_t cap_w, const uint64_t *offs, const uint64_t *le_b,
-                             const uint8_t *status_b, const void *meta_b, uint64_t *line_end, uint8_t *status,
-                             void *meta, uint64_t *n_lines, hipStream_t s);
+                             const uint8_t *status_b, const void *meta_b, const void *tabs_b, uint64_t *line_end,
+                             uint8_t *status, void *meta, void *tabs, uint64_t *n_lines, hipStream_t s);
 hipError_t launch_fq_finish(int what, const char *buf, int64_t data_start, const uint64_t *line_end,
                             const uint64_t *n_lines_dev, uint64_t n_lines_host, const RfArgs &rf, uint8_t *status,
-                            void *meta, unsigned long long *rf_cnt, unsigned long long *gq_cnt, hipStream_t s);
+                            void *meta, const void *tabs, unsigned long long *rf_cnt, unsigned long long *gq_cnt,
+                            hipStream_t s);
 
 }  // namespace vcfxg
