@@ -251,8 +251,9 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
 }
 
 // walker regions -> dense per-line arrays in file order (offs = exclusive scan of wcount):
-// one thread per region slot, grid-stride; the rows / data-line counters (every GT-first
-// record counts as both) are reduced per block
+// one wave per walker region at a time (its lanes copy the region's lines, 64 at a time), so
+// no slot division and no work for the unused slots; the rows / data-line counters (every
+// GT-first record counts as both) are reduced per block (few blocks: few atomics)
 __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_t cap_w,
                                                       const uint64_t *__restrict__ offs,
                                                       const uint32_t *__restrict__ wgt,
@@ -266,20 +267,20 @@ __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_
                                                       LineMeta *meta, uint64_t *n_lines,
                                                       unsigned long long *counters) {
     __shared__ uint32_t red[256 / kWave];
-    const uint64_t nslots = (uint64_t)n_walkers * cap_w, stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t g = 0;
-    for (uint64_t sl = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; sl < nslots; sl += stride) {
-        const uint64_t w = sl / cap_w, i = sl - w * cap_w;
-        const uint64_t d0 = offs[w];
-        if (i == 0) g += wgt[w];
-        if (i >= offs[w + 1] - d0) continue;
-        const uint64_t d = d0 + i;
-        line_end[d] = le_b[sl];
-        alt[d] = alt_b[sl];
-        tot[d] = tot_b[sl];
-        rowpre[d] = rowpre_b[sl];
-        status[d] = status_b[sl];
-        meta[d] = meta_b[sl];
+    const int64_t nwaves = (int64_t)gridDim.x * (256 / kWave);
+    for (int64_t w = (int64_t)blockIdx.x * (256 / kWave) + threadIdx.x / kWave; w < n_walkers; w += nwaves) {
+        const uint64_t d0 = offs[w], cnt = offs[w + 1] - d0, s0 = (uint64_t)w * cap_w;
+        g += lane() == 0 ? wgt[w] : 0u;
+        for (uint64_t i = lane(); i < cnt; i += kWave) {
+            const uint64_t sl = s0 + i, d = d0 + i;
+            line_end[d] = le_b[sl];
+            alt[d] = alt_b[sl];
+            tot[d] = tot_b[sl];
+            rowpre[d] = rowpre_b[sl];
+            status[d] = status_b[sl];
+            meta[d] = meta_b[sl];
+        }
     }
     g = wave_sum(g);
     if (lane() == 0) red[threadIdx.x / kWave] = g;
@@ -314,7 +315,7 @@ hipError_t launch_walk_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t
                                const uint32_t *rowpre_b, const uint8_t *status_b, const void *meta_b,
                                uint64_t *line_end, int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
                                void *meta, uint64_t *n_lines, unsigned long long *counters, hipStream_t s) {
-    const int64_t blocks = std::min<int64_t>(((int64_t)(n_walkers * cap_w) + 255) / 256, 2048);
+    const int64_t blocks = std::min<int64_t>((n_walkers + 256 / kWave - 1) / (256 / kWave), 512);
     hipLaunchKernelGGL(k_walk_compact, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s, n_walkers, cap_w,
                        offs, wgt, le_b, alt_b, tot_b, rowpre_b, status_b, static_cast<const LineMeta *>(meta_b),
                        line_end, alt, tot, rowpre, status, static_cast<LineMeta *>(meta), n_lines, counters);

@@ -90,6 +90,7 @@ struct vcfxg_ctx {
     bool ld_chrom_ids = false;
     std::vector<uint32_t> ld_cid_host, ld_blocks_host;
     uint64_t text_bytes = 0;
+    uint64_t text_hint = 0;  // AF walk: text bytes of the previous call (the next call's capacity)
     // profiling
     bool profiling = false;
     std::map<std::string, std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -643,6 +644,18 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     HIPCHK(c, vcfxg::launch_af_summary(P<uint64_t>(c->d_nlines), P<uint64_t>(c->rowoff),
                                        P<unsigned long long>(c->counters), ovf, small + 4, c->stream));
     prof_end(c, "af_rows");
+    // the rows go out before the host has seen their total: into the text capacity of the
+    // previous call (rows past it are skipped, and all are written again below once it has
+    // grown), so the call synchronises with the host once
+    const uint64_t tcap = std::max<uint64_t>(c->text_hint, 1u << 16);
+    r = ensure(c, c->text, tcap + 1);
+    if (r) return r;
+    prof_begin(c, "af_format");
+    HIPCHK(c, vcfxg::launch_af_format(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
+                                      P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                      P<uint8_t>(c->status), P<uint64_t>(c->rowoff), P<char>(c->text), c->stream,
+                                      tcap));
+    prof_end(c, "af_format");
     static thread_local uint64_t sm[7];
     HIPCHK(c, hipMemcpyAsync(sm, small + 4, sizeof sm, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -652,13 +665,17 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
         return af_region_async(c, data_start, mode, out);
     }
     const uint64_t L = sm[0], text = sm[1];
-    r = ensure(c, c->text, text + 1);
-    if (r) return r;
-    prof_begin(c, "af_format");
-    HIPCHK(c, vcfxg::launch_af_format(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L, mode,
-                                      P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                      P<uint8_t>(c->status), P<uint64_t>(c->rowoff), P<char>(c->text), c->stream));
-    prof_end(c, "af_format");
+    c->text_hint = text;
+    if (text > tcap) {  // the text outgrew the previous capacity: all rows again
+        r = ensure(c, c->text, text + 1);
+        if (r) return r;
+        prof_begin(c, "af_format");
+        HIPCHK(c, vcfxg::launch_af_format(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L, mode,
+                                          P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
+                                          P<uint8_t>(c->status), P<uint64_t>(c->rowoff), P<char>(c->text),
+                                          c->stream));
+        prof_end(c, "af_format");
+    }
     if (c->profiling) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         prof_collect(c);

@@ -33,7 +33,10 @@
 
 namespace vcfxg {
 
-constexpr int kFqUnroll = 6;
+#ifndef VCFXG_FQ_UNROLL
+#define VCFXG_FQ_UNROLL 6
+#endif
+constexpr int kFqUnroll = VCFXG_FQ_UNROLL;
 // The filter does not run in the walk: the walk stores each data line's first 8 tab offsets
 // (u16 from the line start, 0xFFFF past the last tab) and k_fq_finish evaluates rf_eval
 // thread-per-line from them (the bytes through a 16-byte block cache per thread).  Evaluated
@@ -255,7 +258,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
     if (lane() == 0) wcount[wk] = n;
 }
 
-// walker regions -> dense per-line arrays in file order (offs = exclusive scan of wcount)
+// walker regions -> dense per-line arrays in file order (offs = exclusive scan of wcount),
+// one wave per walker region
 template <bool kMeta, bool kTabs>
 __global__ __launch_bounds__(256) void k_fq_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t *__restrict__ offs,
                                                     const uint64_t *__restrict__ le_b,
@@ -263,16 +267,16 @@ __global__ __launch_bounds__(256) void k_fq_compact(int64_t n_walkers, uint64_t 
                                                     const LineMeta *__restrict__ meta_b,
                                                     const uint4 *__restrict__ tabs_b, uint64_t *line_end,
                                                     uint8_t *status, LineMeta *meta, uint4 *tabs, uint64_t *n_lines) {
-    const uint64_t nslots = (uint64_t)n_walkers * cap_w, stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t sl = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; sl < nslots; sl += stride) {
-        const uint64_t w = sl / cap_w, i = sl - w * cap_w;
-        const uint64_t d0 = offs[w];
-        if (i >= offs[w + 1] - d0) continue;
-        const uint64_t d = d0 + i;
-        line_end[d] = le_b[sl];
-        status[d] = status_b[sl];
-        if (kMeta) meta[d] = meta_b[sl];
-        if (kTabs) tabs[d] = tabs_b[sl];
+    const int64_t w = (int64_t)blockIdx.x * (256 / kWave) + threadIdx.x / kWave;  // one wave per walker
+    if (w < n_walkers) {
+        const uint64_t d0 = offs[w], cnt = offs[w + 1] - d0, s0 = (uint64_t)w * cap_w;
+        for (uint64_t i = lane(); i < cnt; i += kWave) {
+            const uint64_t sl = s0 + i, d = d0 + i;
+            line_end[d] = le_b[sl];
+            status[d] = status_b[sl];
+            if (kMeta) meta[d] = meta_b[sl];
+            if (kTabs) tabs[d] = tabs_b[sl];
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) *n_lines = offs[n_walkers];
 }
@@ -380,7 +384,7 @@ hipError_t launch_fq_walk(int what, const char *buf, int64_t lo, int64_t hi, int
 hipError_t launch_fq_compact(int what, int64_t n_walkers, uint64_t cap_w, const uint64_t *offs, const uint64_t *le_b,
                              const uint8_t *status_b, const void *meta_b, const void *tabs_b, uint64_t *line_end,
                              uint8_t *status, void *meta, void *tabs, uint64_t *n_lines, hipStream_t s) {
-    const int64_t blocks = std::max<int64_t>(std::min<int64_t>(((int64_t)(n_walkers * cap_w) + 255) / 256, 2048), 1);
+    const int64_t blocks = std::max<int64_t>((n_walkers + 256 / kWave - 1) / (256 / kWave), 1);
     const LineMeta *mb = static_cast<const LineMeta *>(meta_b);
     LineMeta *m = static_cast<LineMeta *>(meta);
     const uint4 *tb = static_cast<const uint4 *>(tabs_b);

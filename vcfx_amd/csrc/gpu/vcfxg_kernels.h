@@ -120,9 +120,10 @@ hipError_t launch_af_summary(const uint64_t *n_lines, const uint64_t *rowoff, co
                              const unsigned *fail, uint64_t *out, hipStream_t s);
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, uint64_t *len, hipStream_t s);
+// text_cap: rows whose end passes it are not written (the caller checks the total)
 hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, int mode, const int32_t *alt, const int32_t *tot,
                             const uint32_t *rowpre, const uint8_t *status, const uint64_t *off, char *out,
-                            hipStream_t s);
+                            hipStream_t s, uint64_t text_cap = ~0ull);
 
 }  // namespace vcfxg

@@ -864,10 +864,10 @@ __global__ void k_af_format(const char *__restrict__ buf, int64_t data_start, co
                             const uint64_t *n_lines_p, int mode, const int32_t *__restrict__ alt,
                             const int32_t *__restrict__ tot, const uint32_t *__restrict__ rowpre,
                             const uint8_t *__restrict__ status, const uint64_t *__restrict__ off,
-                            char *__restrict__ out) {
+                            char *__restrict__ out, uint64_t cap) {
     const uint64_t n = *n_lines_p;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += gridDim.x * (uint64_t)blockDim.x) {
-        if (status[i] != 1) continue;
+        if (status[i] != 1 || off[i + 1] > cap) continue;
         const int64_t ls = i ? (int64_t)line_end[i - 1] + 1 : data_start;
         char *o = out + off[i];
         const uint32_t pl = rowpre[i];
@@ -1085,10 +1085,10 @@ hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const
 hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, int mode, const int32_t *alt, const int32_t *tot,
                             const uint32_t *rowpre, const uint8_t *status, const uint64_t *off, char *out,
-                            hipStream_t s) {
+                            hipStream_t s, uint64_t text_cap) {
     if (!n_lines_host) return hipSuccess;
     hipLaunchKernelGGL(k_af_format, dim3(grid_for((int64_t)n_lines_host, 256, 4096)), dim3(256), 0, s, buf, data_start,
-                       line_end, n_lines_dev, mode, alt, tot, rowpre, status, off, out);
+                       line_end, n_lines_dev, mode, alt, tot, rowpre, status, off, out, text_cap);
     return hipGetLastError();
 }
 

@@ -9,7 +9,10 @@
 
 namespace vcfxg {
 
-constexpr int kWalkThreads = 256;
+#ifndef VCFXG_WALK_THREADS
+#define VCFXG_WALK_THREADS 256
+#endif
+constexpr int kWalkThreads = VCFXG_WALK_THREADS;  // walkers (waves) per block x 64
 constexpr int kWalkWaves = kWalkThreads / kWave;
 
 // bits j of a 16-byte block at relative offset b with lo <= b + j < hi (32-bit offsets)
