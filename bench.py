@@ -274,10 +274,10 @@ def main():
                 "rf_records": region_bytes + L * (8 + 1),
                 "gq_records": region_bytes + L * (8 + 2),
                 # filter / query walk (no index sweep): the record bytes once + per line its
-                # region results (line_end 8, status 1, head record 16); the rest compacts them
-                # (read + write) and reads status + head record once more
-                "fq_walk": region_bytes + L * (8 + 1 + 16),
-                "fq_rest": L * (2 * (8 + 1 + 16) + 16 + 1),
+                # region results (line_end 8, status 1, head record 16, tab offsets 16); the rest
+                # compacts them (read + write) and reads status + head record + tabs once more
+                "fq_walk": region_bytes + L * (8 + 1 + 16 + 16),
+                "fq_rest": L * (2 * (8 + 1 + 16 + 16) + 16 + 1 + 16),
             }
             dom = max((k for k in kernels if k in algo), key=kernels.get)
             ach = algo[dom] / (kernels[dom] * 1e-3) / 1e9

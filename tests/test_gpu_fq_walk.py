@@ -95,3 +95,65 @@ def test_walk_overflow_falls_back(eng):
     long_part = synth.generate(300, 2504, 55, 1, 0.0, 0, 0.0, 0)
     short = b"".join(b"21\t%d\t.\tA\tG\t%d\tPASS\tAF=0.5\tGT\t0|1\n" % (10 ** 8 + i, i % 60) for i in range(40000))
     _all(eng, long_part + short)
+
+
+def _rf_edge_vcf(seed):
+    """record heads the filter must read exactly from the tab offsets the walk stores: lines
+    with under 8 fields, empty fields, QUAL '.', a leading space, hex / inf / long decimal
+    values, INFO flags and keys that are prefixes of other keys, non-ASCII FILTER bytes, CRLF,
+    empty and '#' lines, and INFO fields long enough to push the first 8 tabs out of the
+    walk's window (those lines take k_fq_finish's own tab scan)"""
+    rng = np.random.default_rng(seed)
+    ns = 40
+    head = b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + \
+        b"\t".join(b"S%d" % i for i in range(ns)) + b"\n"
+    toks = [b"0|0", b"0|1", b"1|0", b"1|1"]
+
+    def gts():
+        return b"\t".join(toks[int(k)] for k in rng.integers(0, 4, ns))
+
+    quals = [b"30", b"29.9999999999999999", b"30.0000000000000001", b".", b"", b" 31", b"0x1F", b"inf",
+             b"-inf", b"nan", b"1e2", b"3e1", b"29", b"abc", b"+30", b"00030"]
+    filters = [b"PASS", b"LowQual", b"", b".", b"P\xc3\xa9SS", b"PASS;q10", b"pass"]
+    infos = [b".", b"AF=0.5", b"AF=0.01;DP=3", b"DB;AF=0.009", b"AFX=0.5;AF=0.02", b"AF", b"AF=", b"AF=0x1p-6",
+             b"DP=7;AF=1e-2", b"AF=0.2;" + b"X=" + b"y" * 1500]
+    body = []
+    for i in range(2500):
+        pos = 9411239 + i
+        r = rng.random()
+        q, f, inf = (quals[int(rng.integers(0, len(quals)))], filters[int(rng.integers(0, len(filters)))],
+                     infos[int(rng.integers(0, len(infos)))])
+        if r < 0.03:
+            body.append(b"\n")
+        elif r < 0.05:
+            body.append(b"#interleaved\n")
+        elif r < 0.10:  # under 8 fields
+            k = int(rng.integers(1, 8))
+            body.append(b"\t".join([b"21", b"%d" % pos, b"rs", b"A", b"C", q, f][:k]) + b"\n")
+        elif r < 0.13:
+            body.append(b"\t" * int(rng.integers(1, 12)) + b"\n")
+        else:
+            line = b"21\t%d\trs%d\tA\tC\t%s\t%s\t%s\tGT\t%s" % (pos, i, q, f, inf, gts())
+            body.append(line + (b"\r\n" if rng.random() < 0.1 else b"\n"))
+    return head + b"".join(body)
+
+
+EDGE_CRITS = [
+    ([(engine.QUAL, engine.GE, 1, 30.0, "", "")], True),
+    ([(engine.QUAL, engine.LT, 1, 30.0, "", ""), (engine.FILTER, engine.NE, 0, 0.0, "", "PASS")], False),
+    ([(engine.FILTER, engine.EQ, 0, 0.0, "", b"P\xc3\xa9SS")], True),
+    ([(engine.INFO, engine.GE, 1, 0.01, "AF", "")], True),
+    ([(engine.INFO, engine.EQ, 0, 0.0, "DB", "DB"), (engine.POS, engine.LE, 1, 9412000.0, "", "")], True),
+    ([(engine.INFO, engine.NE, 0, 0.0, "AF", "0.5"), (engine.QUAL, engine.GT, 1, 29.5, "", "")], False),
+]
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_walk_filter_edge_heads(eng, seed):
+    buf = _rf_edge_vcf(seed)
+    ds = engine.data_start_of(buf)
+    for crits, logic in EDGE_CRITS:
+        _check(eng, buf, ds, lambda: eng.record_filter_region(ds, crits, logic),
+               lambda: eng.record_filter(crits, logic), ("rf-edge", crits, logic))
+        _check(eng, buf, ds, lambda: eng.filter_query_region(ds, crits, "0|1", logic, False),
+               lambda: eng.filter_query(crits, "0|1", logic, False), ("pipe-edge", crits, logic))
