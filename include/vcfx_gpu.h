@@ -152,9 +152,9 @@ int vcfxg_filter_query(vcfxg_ctx *ctx, const vcfxg_criterion *crit, int n, int a
 /* vcfxg_index(data_start) followed by vcfxg_record_filter / vcfxg_genotype_query /
  * vcfxg_filter_query, in one call: the same per-line statuses, line ends, summary and context
  * state (the context is indexed afterwards).  For inputs whose first records average >= 512 B
- * the device walks the records without a separate index sweep (one HBM pass: the filter is
- * evaluated out of each record's head window, the query's fixed-stride sweep validates the
- * record ends it predicts); VCFXG_FQ_WALK=1 / -1 in the environment at vcfxg_open forces /
+ * the device walks the records without a separate index sweep (one HBM pass: the walk keeps
+ * each record's first 8 tab offsets for the filter, the query's fixed-stride sweep validates
+ * the record ends it predicts); VCFXG_FQ_WALK=1 / -1 in the environment at vcfxg_open forces /
  * disables that schedule.  Replace the per-record loops of processFileMmap / processStdin
  * (VCFX_record_filter.cpp:406-549) and genotypeQueryMmap / genotypeQueryStream
  * (VCFX_genotype_query.cpp:433-617) including their line splitting. */

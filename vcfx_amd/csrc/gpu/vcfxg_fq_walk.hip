@@ -296,35 +296,40 @@ __global__ __launch_bounds__(256) void k_fq_finish(const char *__restrict__ buf,
     uint32_t c[4] = {0, 0, 0, 0};  // rf kept, rf data lines, gq matched, gq data lines
     for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < n; li += gridDim.x * (uint64_t)blockDim.x) {
         uint8_t st = status[li];
-        if (kRF && st == kRfPending) {
-            const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
-            int64_t ae = (int64_t)line_end[li];
-            if (ae > ls && buf[ae - 1] == '\r') ae--;
-            if (!rf_line(buf, ls, ae, rf.crit, rf.ncrit, rf.and_logic, rf.pool)) {
-                st = 2;
-                if (kGQ) meta[li].kind = kMetaGated;
-            } else st = kGQ ? kGqFull : 1;
-            status[li] = st;
-        } else if (kRF && st != 0 && st != 4) {  // a data line with its 8 tabs (or all of them) stored
+        if (kRF && st != 0 && st != 4) {  // a data line: its 8 tabs stored by the walk, or
+            // (kRfPending: a head longer than the walk's window) found here
             const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
             int64_t ae = (int64_t)line_end[li];
             const BlockBytes B{buf, -1, {}};
             if (ae > ls && B[ae - 1] == '\r') ae--;
-            const uint4 tv = tabs[li];
-            const uint32_t tw[4] = {tv.x, tv.y, tv.z, tv.w};
             int64_t t[8];
             int nt = 0;
+            if (st == kRfPending) {
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint32_t o = (tw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
-                t[k] = ls + o;
-                nt += o != 0xFFFFu;
+                for (int k = 0; k < 8; k++) t[k] = 0;
+                for (int64_t p = ls; p < ae && nt < 8; p++)
+                    if (B[p] == '\t') {  // (register selects: no scratch array)
+#pragma unroll
+                        for (int k = 0; k < 8; k++) t[k] = k == nt ? p : t[k];
+                        nt++;
+                    }
+            } else {
+                const uint4 tv = tabs[li];
+                const uint32_t tw[4] = {tv.x, tv.y, tv.z, tv.w};
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t o = (tw[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                    t[k] = ls + o;
+                    nt += o != 0xFFFFu;
+                }
             }
-            if (!rf_eval(B, t, nt, ls, ae, rf.crit, rf.ncrit, rf.and_logic, PoolBytes{rf.pool})) {
+            const bool keep = rf_eval(B, t, nt, ls, ae, rf.crit, rf.ncrit, rf.and_logic, PoolBytes{rf.pool});
+            const uint8_t st0 = st;
+            if (!keep) {
                 st = 2;
                 if (kGQ) meta[li].kind = kMetaGated;
-                status[li] = st;
-            }
+            } else if (st == kRfPending) st = kGQ ? kGqFull : 1;
+            if (st != st0) status[li] = st;
         }
         if (kRF) {
             c[0] += st != 0 && st != 4 && st != 2;
