@@ -31,6 +31,7 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     for w in $WLS; do
         step rocprof_$w 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$w -o run --output-format csv -- \
             python bench.py --workload $w --steps 5 --warmup 1 --no-cpu-baseline || exit $?
+        grep '^{' gpurun_out/rocprof_$w.log > gpurun_out/rocprof_bench_$w.json  # the bench line of the traced run
     done
 fi
 if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
