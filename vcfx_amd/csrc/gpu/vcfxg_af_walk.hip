@@ -60,7 +60,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     const int strip_cr = mode == 0 ? 1 : 0;
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
-    int64_t L = wk == 0 ? lo : scan_nl(buf, cs - 1, hi) + 1;
+    int64_t L = wk == 0 ? lo : scan_nl<kFirstScanU>(buf, cs - 1, hi) + 1;
     int64_t span = span0;  // predicted '\n' distance from the sample start
     uint8_t cr_prev = 0;   // and the '\r' state of that record
     uint64_t n = 0;

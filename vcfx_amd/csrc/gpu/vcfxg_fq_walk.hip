@@ -75,7 +75,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
     if (wk >= n_walkers) return;
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
-    int64_t L = wk == 0 ? lo : scan_nl(buf, cs - 1, hi) + 1;
+    int64_t L = wk == 0 ? lo : scan_nl<kFirstScanU>(buf, cs - 1, hi) + 1;
     int64_t span = kGQ ? span0 : 0;  // predicted '\n' distance from the sample start
     uint8_t cr_prev = 0;             // and the '\r' state of that record
     uint64_t n = 0;

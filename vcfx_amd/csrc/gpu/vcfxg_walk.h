@@ -14,6 +14,12 @@ namespace vcfxg {
 #endif
 constexpr int kWalkThreads = VCFXG_WALK_THREADS;  // walkers (waves) per block x 64
 constexpr int kWalkWaves = kWalkThreads / kWave;
+// a walker's search for its first line start reads the tail of the previous chunk's last
+// line, which that chunk's walker reads too (much later, so from HBM again): small steps
+#ifndef VCFXG_FIRST_SCAN_U
+#define VCFXG_FIRST_SCAN_U 4
+#endif
+constexpr int kFirstScanU = VCFXG_FIRST_SCAN_U;
 
 // bits j of a 16-byte block at relative offset b with lo <= b + j < hi (32-bit offsets)
 __device__ __forceinline__ uint32_t range16(int b, int lo, int hi) {
@@ -23,9 +29,9 @@ __device__ __forceinline__ uint32_t range16(int b, int lo, int hi) {
     return e <= a ? 0u : ((1u << e) - 1u) & ~((1u << a) - 1u);
 }
 
-// first '\n' in [p, hi), else hi (wave-uniform; 4 KiB per step, lane offsets 32-bit)
+// first '\n' in [p, hi), else hi (wave-uniform; kU KiB per step, lane offsets 32-bit)
+template <int kU = 4>
 __device__ __forceinline__ int64_t scan_nl(const char *__restrict__ buf, int64_t p, int64_t hi) {
-    constexpr int kU = 4;
     const int lo16 = 16 * lane();
     for (int64_t w = p & ~(int64_t)15; w < hi; w += kU * kWaveStep) {
         const char *__restrict__ wb = buf + w;
@@ -66,7 +72,10 @@ __device__ __forceinline__ int tab_at(uint32_t tm, uint32_t excl, uint32_t c, in
 // block; those bytes are masked by the analysis)
 // The window is kWin bytes (the first kWin / 16 lanes; a line head is rarely longer and the
 // sweep re-reads the bytes after it from HBM anyway), or the full 1 KiB for a long head.
-constexpr int kWin = 256;
+#ifndef VCFXG_WALK_WIN
+#define VCFXG_WALK_WIN 256
+#endif
+constexpr int kWin = VCFXG_WALK_WIN;
 __device__ __forceinline__ void prefetch_window(const char *__restrict__ buf, int64_t A, int64_t hi, uint4 *slot,
                                                 int bytes = kWin) {
     if (16 * lane() >= bytes) return;
