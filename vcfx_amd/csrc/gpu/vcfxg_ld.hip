@@ -204,15 +204,26 @@ __global__ __launch_bounds__(256) void k_ld_parse(const char *__restrict__ buf, 
             bool ok = nt >= 9;
             int pos = 0;
             if (ok && !a.stoi_mode) {  // fastParseInt(field 1)
-                int64_t p0 = t[0] + 1, p1 = t[1];
+                const int64_t p0 = t[0] + 1, p1 = t[1];
                 ok = p1 > p0;
-                uint32_t v = 0;
-                for (int64_t p = p0; ok && p < p1; p++) {
-                    uint32_t c = byte_at(buf, p);
-                    if (c - '0' >= 10u) ok = false;
-                    else v = v * 10u + (c - '0');
+                if (ok && p1 - p0 <= kWave) {
+                    // lane k holds digit k: one round of loads instead of a dependent byte
+                    // chain; sum of d_k * 10^(len-1-k) mod 2^32 = the wrapping Horner loop
+                    const int len = (int)(p1 - p0), k = lane();
+                    const uint32_t c = k < len ? byte_at(buf, p0 + k) : (uint32_t)'0';
+                    ok = !__any(c - '0' >= 10u);
+                    uint32_t pw = 1u;
+                    for (int e = k; e < len - 1; e++) pw *= 10u;
+                    pos = (int)wave_sum(k < len ? (c - '0') * pw : 0u);
+                } else if (ok) {
+                    uint32_t v = 0;
+                    for (int64_t p = p0; ok && p < p1; p++) {
+                        uint32_t c = byte_at(buf, p);
+                        if (c - '0' >= 10u) ok = false;
+                        else v = v * 10u + (c - '0');
+                    }
+                    pos = (int)v;
                 }
-                pos = (int)v;
             } else if (ok) {  // std::stoi(fields[1]) (computeLD :1026)
                 ok = cxx_stoi(buf, t[0] + 1, t[1], &pos);
             }
@@ -226,7 +237,7 @@ __global__ __launch_bounds__(256) void k_ld_parse(const char *__restrict__ buf, 
                 const int64_t S = t[8] + 1;
                 LdStats st;
                 LdOp op{row, S, a.ns};
-                if (gt_fast(buf, S, le, op)) st = op.st;
+                if (gt_fast<6>(buf, S, le, op)) st = op.st;  // (six 1 KiB steps in flight, as the walks)
                 else {
                     // rewrite the row: the failed fast sweep may have stored codes
                     for (int k = lane(); k < a.kpad; k += kWave) row[k] = -1;
