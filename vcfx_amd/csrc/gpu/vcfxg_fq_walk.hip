@@ -301,10 +301,10 @@ __global__ __launch_bounds__(256) void k_fq_finish(const char *__restrict__ buf,
             const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
             int64_t ae = (int64_t)line_end[li];
             const BlockBytes B{buf, -1, {}};
-            if (ae > ls && B[ae - 1] == '\r') ae--;
             int64_t t[8];
             int nt = 0;
             if (st == kRfPending) {
+                if (ae > ls && B[ae - 1] == '\r') ae--;
 #pragma unroll
                 for (int k = 0; k < 8; k++) t[k] = 0;
                 for (int64_t p = ls; p < ae && nt < 8; p++)
@@ -322,6 +322,8 @@ __global__ __launch_bounds__(256) void k_fq_finish(const char *__restrict__ buf,
                     t[k] = ls + o;
                     nt += o != 0xFFFFu;
                 }
+                // the line end only bounds a field past the last tab (fewer than 8 tabs)
+                if (nt < 8 && ae > ls && B[ae - 1] == '\r') ae--;
             }
             const bool keep = rf_eval(B, t, nt, ls, ae, rf.crit, rf.ncrit, rf.and_logic, PoolBytes{rf.pool});
             const uint8_t st0 = st;
