@@ -875,6 +875,228 @@ static int gq_main(int argc, char **argv, const char *in, size_t inn, ob_t *out,
 }
 
 /* ==================================================================================== */
+/* VCFX_nonref_filter (a per-sample GT reducer on the same path)     */
+/* ==================================================================================== */
+static void nr_help(ob_t *o) {  /* displayHelp, VCFX_nonref_filter.cpp:386-417 */
+    ob_puts(o,
+        "VCFX_nonref_filter: Exclude variants if all samples are homozygous reference.\n\n"
+        "Usage:\n"
+        "  VCFX_nonref_filter [options] [input.vcf]\n"
+        "  VCFX_nonref_filter [options] < input.vcf > output.vcf\n\n"
+        "Options:\n"
+        "  -h, --help          Show this help message\n"
+        "  -i, --input FILE    Input VCF file (uses fast memory-mapped I/O)\n\n"
+        "Description:\n"
+        "  Reads VCF lines. For each variant, we check each sample's genotype. If a\n"
+        "  genotype is polyploid, all alleles must be '0'. If a genotype is missing\n"
+        "  or partial, we consider it not guaranteed hom-ref => keep variant.\n"
+        "  If we find at least one sample not hom-ref, we print the variant. Otherwise,\n"
+        "  we skip it.\n\n"
+        "Performance:\n"
+        "  File input (-i) uses memory-mapped I/O for 100-1000x faster processing\n"
+        "  compared to stdin. Features include:\n"
+        "  - SIMD-optimized line scanning (AVX2/SSE2)\n"
+        "  - Zero-copy string parsing with string_view\n"
+        "  - 1MB output buffering\n"
+        "  - Direct GT field extraction (avoids full sample parsing)\n"
+        "  - Early termination on first non-homref sample\n\n"
+        "Examples:\n"
+        "  VCFX_nonref_filter -i input.vcf > filtered.vcf    # Fast (mmap)\n"
+        "  VCFX_nonref_filter input.vcf > filtered.vcf       # Fast (mmap)\n"
+        "  VCFX_nonref_filter < input.vcf > filtered.vcf     # Slower (stdin)\n\n");
+}
+/* allSamplesHomRefDirect's per-sample test (mmap), :286-300: "0s0" (s '/' or '|') at
+ * length 3, otherwise every byte '/', '|' or '0' */
+static int nr_homref_mmap(sv_t g) {
+    if (g.n == 3) return g.p[0] == '0' && (g.p[1] == '/' || g.p[1] == '|') && g.p[2] == '0';
+    if (!g.n) return 0;
+    for (size_t i = 0; i < g.n; i++)
+        if (g.p[i] != '/' && g.p[i] != '|' && g.p[i] != '0') return 0;
+    return 1;
+}
+/* isDefinitelyHomRef (stdin), :419-449 */
+static int nr_homref_stream(sv_t g) {
+    if (!g.n) return 0;
+    if (g.n == 3 && g.p[0] == '0' && (g.p[1] == '/' || g.p[1] == '|') && g.p[2] == '0') return 1;
+    for (size_t i = 0; i < g.n; i++)
+        if (g.p[i] != '/' && g.p[i] != '|' && g.p[i] != '0') return 0;
+    return 1;
+}
+/* skipToField :224-231: the byte after the n-th tab, or NULL */
+static const char *nr_skip(const char *p, const char *end, int n) {
+    int k = 0;
+    while (p < end && k < n) {
+        if (*p == '\t') k++;
+        p++;
+    }
+    return k == n ? p : NULL;
+}
+/* allSamplesHomRefDirect :248-312 (1 = every sample hom-ref: the line is dropped) */
+static int nr_all_homref_mmap(const char *ls, const char *le, int gi) {
+    if (!nr_skip(ls, le, 8)) return 0;
+    const char *p = nr_skip(ls, le, 9);
+    if (!p) return 0;
+    while (p < le) {
+        const char *se = (const char *)memchr(p, '\t', (size_t)(le - p));
+        if (!se) se = le;
+        sv_t smp = sv(p, (size_t)(se - p));
+        if (!smp.n) return 0;
+        sv_t g;
+        if (gi == 0) {
+            const char *c = (const char *)memchr(smp.p, ':', smp.n);
+            g = c ? sv(smp.p, (size_t)(c - smp.p)) : smp;
+        } else {
+            g = gq_nth(smp, gi);  /* extractNthField :179-197 (empty when absent) */
+        }
+        if (!nr_homref_mmap(g)) return 0;
+        p = se;
+        if (p < le && *p == '\t') p++;
+    }
+    return 1;
+}
+/* filterNonRefMmap :458-551 */
+static void nr_mmap(const char *d, size_t n, ob_t *out, ob_t *err) {
+    if (n == 0) return;
+    const char *p = d, *end = d + n;
+    int found = 0;
+    while (p < end) {
+        const char *le = (const char *)memchr(p, '\n', (size_t)(end - p));
+        if (!le) le = end;
+        const char *ae = le;
+        if (ae > p && ae[-1] == '\r') ae--;
+        size_t len = (size_t)(ae - p);
+        const char *next = le + 1;
+        if (len == 0) { ob_putc(out, '\n'); p = next; continue; }
+        if (p[0] == '#') {
+            ob_put(out, p, len);
+            ob_putc(out, '\n');
+            if (starts_chrom(p, len)) found = 1;
+            p = next;
+            continue;
+        }
+        if (!found) {
+            ob_puts(err, "Warning: VCF data line encountered before #CHROM. Passing line.\n");
+            ob_put(out, p, len);
+            ob_putc(out, '\n');
+            p = next;
+            continue;
+        }
+        const char *fs = nr_skip(p, ae, 8);
+        int keep = 1;
+        if (fs) {
+            const char *fe = (const char *)memchr(fs, '\t', (size_t)(ae - fs));
+            if (!fe) fe = ae;
+            int gi = gq_find_gt_index(sv(fs, (size_t)(fe - fs)));  /* findGTIndex :317-335 */
+            if (gi >= 0) keep = !nr_all_homref_mmap(p, ae, gi);
+        }
+        if (keep) { ob_put(out, p, len); ob_putc(out, '\n'); }
+        p = next;
+    }
+}
+/* std::getline(ss, tok, ':') over s: the k-th token (0-based), *ntok = tokens */
+static sv_t nr_getline_tok(sv_t s, int k, int *ntok) {
+    int t = 0;
+    sv_t r = {NULL, 0};
+    const char *p = s.p, *e = s.p + s.n;
+    while (p < e) {  /* getline yields no token for an empty remainder */
+        const char *c = (const char *)memchr(p, ':', (size_t)(e - p));
+        const char *te = c ? c : e;
+        if (t == k) r = sv(p, (size_t)(te - p));
+        t++;
+        p = c ? c + 1 : e;
+    }
+    *ntok = t;
+    return r;
+}
+/* filterNonRef (stdin) :553-636 */
+static void nr_stream(const char *d, size_t n, ob_t *out, ob_t *err) {
+    int found = 0;
+    lines_t it = {d, d + n};
+    const char *ls, *le;
+    while (next_line(&it, &ls, &le)) {
+        size_t len = (size_t)(le - ls);
+        if (len == 0) { ob_putc(out, '\n'); continue; }
+        if (ls[0] == '#') {
+            ob_put(out, ls, len);
+            ob_putc(out, '\n');
+            if (starts_chrom(ls, len)) found = 1;
+            continue;
+        }
+        if (!found) {
+            ob_puts(err, "Warning: VCF data line encountered before #CHROM. Passing line.\n");
+            ob_put(out, ls, len);
+            ob_putc(out, '\n');
+            continue;
+        }
+        /* vcfx::split_tabs: a trailing tab yields an empty last field */
+        size_t nf = 1;
+        for (const char *q = ls; q < le; q++) nf += *q == '\t';
+        int keep = 1;
+        if (nf >= 10) {
+            const char *fs = nr_skip(ls, le, 8);
+            const char *fe = (const char *)memchr(fs, '\t', (size_t)(le - fs));
+            sv_t fmt = sv(fs, (size_t)(fe - fs));
+            int gi = -1, nt = 0;
+            for (int k = 0;; k++) {
+                sv_t f = nr_getline_tok(fmt, k, &nt);
+                if (k >= nt) break;
+                if (f.n == 2 && f.p[0] == 'G' && f.p[1] == 'T') { gi = k; break; }
+            }
+            if (gi >= 0) {
+                int all = 1;
+                const char *p = fe + 1;
+                for (;;) {
+                    const char *se = (const char *)memchr(p, '\t', (size_t)(le - p));
+                    if (!se) se = le;
+                    int ntok;
+                    sv_t g = nr_getline_tok(sv(p, (size_t)(se - p)), gi, &ntok);
+                    if (gi >= ntok || !nr_homref_stream(g)) { all = 0; break; }
+                    if (se == le) break;
+                    p = se + 1;
+                }
+                keep = !all;
+            }
+        }
+        if (keep) { ob_put(out, ls, len); ob_putc(out, '\n'); }
+    }
+}
+/* run :340-384 + main :646-652 */
+static int nr_main(int argc, char **argv, const char *in, size_t inn, ob_t *out, ob_t *err) {
+    if (common_flags(argc, argv, "VCFX_nonref_filter", nr_help, out)) return 0;
+    const char *input = NULL;
+    int help = 0;
+    static struct option lo[] = {{"help", no_argument, NULL, 'h'},
+                                 {"input", required_argument, NULL, 'i'},
+                                 {NULL, 0, NULL, 0}};
+    optind = 0;
+    errcap_t ec;
+    errcap_begin(&ec);
+    int opt;
+    while ((opt = getopt_long(argc, argv, "hi:", lo, NULL)) != -1) {
+        if (opt == 'i') input = optarg;
+        else help = 1;
+    }
+    errcap_end(&ec, err);
+    if ((!input || !*input) && optind < argc) input = argv[optind];
+    if (help) {
+        nr_help(out);
+        return 0;
+    }
+    if (input && *input && strcmp(input, "-") != 0) {
+        char *d; size_t n;
+        if (read_file(input, &d, &n) < 0) {
+            ob_printf(err, "Error: Cannot open file: %s\n", input);
+            return 0;
+        }
+        nr_mmap(d, n, out, err);
+        free(d);
+    } else {
+        nr_stream(in, inn, out, err);
+    }
+    return 0;
+}
+
+/* ==================================================================================== */
 /* VCFX_record_filter                                                                   */
 /* ==================================================================================== */
 enum { OP_GT, OP_GE, OP_LT, OP_LE, OP_EQ, OP_NE };
@@ -1679,6 +1901,7 @@ int oracle_main(const char *tool, int argc, char **argv, const char *in, size_t 
     else if (strcmp(t, "VCFX_genotype_query") == 0) rc = gq_main(argc, argv, in, inn, &out, &err);
     else if (strcmp(t, "VCFX_record_filter") == 0) rc = rf_main(argc, argv, in, inn, &out, &err);
     else if (strcmp(t, "VCFX_ld_calculator") == 0) rc = ld_main(argc, argv, in, inn, &out, &err);
+    else if (strcmp(t, "VCFX_nonref_filter") == 0) rc = nr_main(argc, argv, in, inn, &out, &err);
     else return -1;
     res->out = out.p ? out.p : (char *)calloc(1, 1);
     res->out_len = out.n;

@@ -30,6 +30,41 @@ def rec(chrom, pos, rid, ref, alt, qual, filt, info, fmt, samples):
     return "\t".join([chrom, str(pos), rid, ref, alt, qual, filt, info, fmt] + samples) + "\n"
 
 
+def nonref_fixtures():
+    """VCFX_nonref_filter traps: hom-ref spellings the two input modes
+    judge differently ("000", "0", "/", polyploid, GT not first, missing subfields, empty
+    samples, trailing tabs), FORMAT without GT, short lines, CRLF, empty lines, '#' lines
+    between records and long all-hom-ref / one-non-ref records"""
+    H = "##fileformat=VCFv4.2\n"
+    body = H + "1\t1\tpre\tA\tC\t.\t.\t.\tGT\t0|0\n" + chrom_line(3)
+    gts = ["0|0", "0/0", "000", "0", "00", "/", "|", "0/0/0", "0|0|0", "0/1", "1|0", "./.", ".", ".|0", "0|.",
+           "0/0:5", "0:1", "", "0|0|1", "10/0", "0/00", "|0|", "0/0\t"]
+    pos = 100
+    for a in gts:
+        for b in ("0|0", "0/1"):
+            pos += 1
+            body += rec("1", pos, "g%d" % pos, "A", "C", "50", "PASS", ".", "GT", [a, b, "0|0"])
+    for fmt, samples in [("DP:GT", ["5:0|0", "7:0/0", "1:0|0"]), ("DP:GT", ["5:0|1", "7:0/0", "1:0|0"]),
+                         ("DP:GT", ["5", "7:0/0", "1:0|0"]), ("GT:DP", ["0|0:5", "0/0", ":3"]),
+                         ("DP", ["5", "6", "7"]), ("GTX:GT", ["1:0|0", "0:0|0", "0:0/0"]), ("", ["0|0", "0|0", "0|0"]),
+                         ("GT:", ["0|0", "0|0", "0|0"]), (":GT", ["x:0|0", "y:0|0", ":0/0"]),
+                         ("GT:GT", ["0|0:1|1", "0/0:1", "0|0"])]:
+        pos += 1
+        body += rec("1", pos, "f%d" % pos, "A", "C", "50", "PASS", ".", fmt, samples)
+    body += "1\t%d\tshort\tA\tC\t50\tPASS\t.\tGT\n" % (pos + 1)
+    body += "1\t%d\tshorter\tA\tC\t50\tPASS\n" % (pos + 2)
+    body += "1\t%d\ttrail\tA\tC\t50\tPASS\t.\tGT\t0|0\t0|0\t\n" % (pos + 3)
+    body += "1\t%d\tnine_tabs\tA\tC\t50\tPASS\t.\tGT\t\n" % (pos + 4)
+    body += "\n#interleaved\n\n"
+    long_ref = ["0|0"] * 3000
+    body += rec("1", pos + 5, "allref", "A", "C", "50", "PASS", ".", "GT", long_ref)
+    body += rec("1", pos + 6, "lastalt", "A", "C", "50", "PASS", ".", "GT", long_ref[:-1] + ["0|1"])
+    body += rec("1", pos + 7, "firstalt", "A", "C", "50", "PASS", ".", "GT", ["1/1"] + long_ref[1:])
+    body += rec("1", pos + 8, "missing", "A", "C", "50", "PASS", ".", "GT", long_ref[:1500] + ["./."] + long_ref[1501:])
+    w(os.path.join("ref_nonref", "nonref_traps.vcf"), body)
+    w(os.path.join("ref_nonref", "nonref_traps_crlf.vcf"), body.replace("\n", "\r\n"))
+
+
 def main():
     os.makedirs(DATA, exist_ok=True)
     # --- genotype zoo: every GT token shape the AF/GQ/LD parsers branch on
@@ -129,6 +164,7 @@ def main():
     for name, m, ns, seed, info, miss, hap, irr, crlf in slices:
         subprocess.check_call([synth, os.path.join(DATA, name), str(m), str(ns), str(seed), str(info),
                                repr(miss), str(hap), repr(irr), str(crlf)])
+    nonref_fixtures()
     print("fixtures written to", DATA)
 
 

@@ -23,6 +23,7 @@ INLINE_MAX = 16 * 1024
 
 AF, RF, GQ, LD, VC = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query",
                       "VCFX_ld_calculator", "VCFX_variant_counter")
+NR = "VCFX_nonref_filter"
 
 
 def fixtures():
@@ -110,6 +111,19 @@ def build_cases():
               ["-t", "2", "-i", "data/synth_ld.vcf"], ["-t", "nan", "-i", "data/synth_ld.vcf"], ["-n", "q"],
               ["-d", "-5", "-i", "data/synth_ld.vcf"], ["-w", "0", "-i", "data/synth_ld.vcf"]):
         add(LD, a)
+    # ---- nonref_filter: the shared fixtures, the reference's own nonref fixtures and traps
+    nr_dir = os.path.join(HERE, "data", "ref_nonref")
+    nr_files = vcfs + [os.path.join("data", "ref_nonref", n) for n in sorted(os.listdir(nr_dir))]
+    for f in nr_files:
+        add(NR, ["-i", f])
+        add(NR, [f])
+        add(NR, [], stdin=f)
+    add(NR, ["-"], stdin="data/ref_nonref/nonref_traps.vcf")
+    add(NR, ["--input", "data/ref_nonref/nonref_basic.vcf"])
+    for a in (["-h"], ["--help"], ["-v"], ["--version"], ["--bogus"], ["-x"], ["-i"], ["-i", "data/nope.vcf"],
+              ["data/nope.vcf"]):
+        add(NR, a)
+    add(NR, [], stdin="data/empty.vcf", tag="empty_stdin")
     return cases
 
 

@@ -19,7 +19,7 @@ def oracle():
 
 def test_case_count():
     tools = collections.Counter(c["tool"] for c in CASES)
-    assert len(tools) == 5 and min(tools.values()) > 40
+    assert len(tools) == 6 and min(tools.values()) > 40  # the five hot-path tools + nonref_filter (8(f))
 
 
 @pytest.mark.parametrize("tool", sorted({c["tool"] for c in CASES}))
@@ -55,6 +55,11 @@ REF_EXP = [
     (["VCFX_variant_counter"], "ref/variant_counter_normal.vcf", "variant_counter_normal.txt"),
     (["VCFX_variant_counter"], "ref/variant_counter_large.vcf", "variant_counter_large.txt"),
     (["VCFX_variant_counter"], "ref/variant_counter_empty.vcf", "variant_counter_empty.txt"),
+    # tests/test_nonref_filter.sh:31-34 (`$EXEC < input`, compared with `diff -b`)
+    (["VCFX_nonref_filter"], "ref_nonref/nonref_basic.vcf", "nonref_basic_out.vcf"),
+    (["VCFX_nonref_filter"], "ref_nonref/nonref_complex.vcf", "nonref_complex_out.vcf"),
+    (["VCFX_nonref_filter"], "ref_nonref/nonref_malformed.vcf", "nonref_malformed_out.vcf"),
+    (["VCFX_nonref_filter"], "ref_nonref/nonref_no_gt.vcf", "nonref_no_gt_out.vcf"),
 ]
 
 
@@ -65,7 +70,10 @@ def test_oracle_matches_reference_committed_expected(oracle, argv, stdin, expect
     data = open(os.path.join(GOLDEN, "data", stdin), "rb").read() if stdin else b""
     out, err, rc = oracle.run(argv, data, cwd=GOLDEN)
     want = open(os.path.join(GOLDEN, "data", "ref_expected", expected), "rb").read()
-    assert out == want
+    if argv[0] == "VCFX_nonref_filter":  # the reference script compares with diff -b
+        assert [l.split() for l in out.splitlines()] == [l.split() for l in want.splitlines()]
+    else:
+        assert out == want
 
 
 def test_af_known_answers(oracle):
