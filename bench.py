@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("af", "pipeline", "ld"), default="af")
+    ap.add_argument("--workload", choices=("af", "pipeline", "ld", "nonref"), default="af")
     ap.add_argument("--records", type=int, default=None, help="records per GPU (default per workload)")
     ap.add_argument("--samples", type=int, default=2504)
     ap.add_argument("--window", type=int, default=100000, help="ld: window in variants")
@@ -105,6 +105,9 @@ def cpu_baseline(workload, arr, offs, a):
         if workload == "af":
             argvs = [["VCFX_allele_freq_calc", "-q", "-i", f.name]]
             desc = "VCFX_allele_freq_calc -q -i (file path)"
+        elif workload == "nonref":
+            argvs = [["VCFX_nonref_filter", "-i", f.name]]
+            desc = "VCFX_nonref_filter -i (file path)"
         elif workload == "pipeline":
             argvs = [["VCFX_record_filter", "--filter", "QUAL>=30;FILTER==PASS", "-i", f.name],
                      ["VCFX_genotype_query", "--genotype-query", "0|1"]]
@@ -168,6 +171,14 @@ def main():
             return s
         kern_names = ("af_scan", "line_count", "line_emit", "line_compact", "af_records", "af_chunks", "af_fused",
                       "af_pipe", "af_stream", "af_walk", "walk_compact", "af_complex", "af_rows", "af_format")
+    elif a.workload == "nonref":
+        def step():
+            eng.index(ds)
+            s = eng.nonref_filter(engine.MODE_FILE)  # index + per-record "every sample hom-ref"
+            if red is not None:
+                allreduce_counts([s.n_lines, s.rows, s.data_lines, s.general_records])
+            return s
+        kern_names = ("line_count", "line_emit", "line_compact", "nr_records")
     elif a.workload == "pipeline":
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
@@ -276,6 +287,8 @@ def main():
                 # filter / query walk (no index sweep): the record bytes once + per line its
                 # region results (line_end 8, status 1, head record 16, tab offsets 16); the rest
                 # compacts them (read + write) and reads status + head record + tabs once more
+                # (nonref: nr_records stops at each record's first non-hom-ref sample, so its
+                # bytes are data-dependent; the roofline line is the index sweep's)
                 "fq_walk": region_bytes + L * (8 + 1 + 16 + 16),
                 "fq_rest": L * (2 * (8 + 1 + 16 + 16) + 16 + 1 + 16),
             }
@@ -289,6 +302,8 @@ def main():
                   "allele counts + formatted rows" % (a.records, a.samples),
             "pipeline": "VCFX_record_filter --filter 'QUAL>=30;FILTER==PASS' | VCFX_genotype_query "
                         "--genotype-query '0|1' fused, device-resident %d x %d shard per GPU" % (a.records, a.samples),
+            "nonref": "VCFX_nonref_filter -i (file path) on a device-resident %d x %d shard per GPU: index + "
+                      "per-record all-samples-hom-ref test" % (a.records, a.samples),
             "ld": "VCFX_ld_calculator -w %d -t %g streaming on a device-resident %d x %d shard per GPU: parse + "
                   "FP4-MFMA pair sums (count + emit) + pair text" % (a.window, a.threshold, a.records, a.samples),
         }[a.workload]

@@ -165,6 +165,15 @@ int vcfxg_genotype_query_region(vcfxg_ctx *ctx, size_t data_start, const char *q
 int vcfxg_filter_query_region(vcfxg_ctx *ctx, size_t data_start, const vcfxg_criterion *crit, int n, int and_logic,
                               const char *query, size_t qlen, int strict, vcfxg_summary *out);
 
+/* ---- VCFX_nonref_filter (a per-sample GT reducer on the same path) ----
+ * Over the indexed region: per line status 1 keep / 2 drop (every sample hom-ref), 4 '#'
+ * line, 0 empty; rows = kept lines, data_lines = evaluated lines, general_records = lines
+ * off the fixed-stride sweep.  mode VCFXG_MODE_FILE restates filterNonRefMmap +
+ * allSamplesHomRefDirect (VCFX_nonref_filter.cpp:458-551, 248-312; '\r' stripped),
+ * VCFXG_MODE_STDIN filterNonRef + isDefinitelyHomRef (:553-636, 419-449).  Data lines
+ * before '#CHROM' are the caller's (the tool warns and passes them through). */
+int vcfxg_nonref_filter(vcfxg_ctx *ctx, int mode, vcfxg_summary *out);
+
 /* ---- variant counter -------------------------------------------------------------------
  * Per line status: ROW = data line with >= 8 tab-separated columns (counted), WARN = fewer
  * columns, SKIP = empty or '#'.  strip_cr: drop a trailing '\r' first (file path).

@@ -1001,6 +1001,35 @@ static void gq_parse_query(const char *q, size_t n, int &qa, int &qb) {
     if (qa > qb) std::swap(qa, qb);
 }
 
+int vcfxg_nonref_filter(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
+    if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t L = c->n_lines;
+    int r = ensure(c, c->status, L + 1);
+    if (r) return r;
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    prof_begin(c, "nr_records");
+    HIPCHK(c, vcfxg::launch_nr_records(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
+                                       P<uint64_t>(c->d_nlines), L, mode, P<uint8_t>(c->status),
+                                       P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "nr_records");
+    static thread_local uint64_t host_cnt[4];
+    HIPCHK(c, hipMemcpyAsync(host_cnt, c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    c->text_bytes = 0;
+    if (out) {
+        out->n_lines = L;
+        out->rows = host_cnt[0];
+        out->data_lines = host_cnt[1];
+        out->warn_lines = 0;
+        out->general_records = host_cnt[3];
+        out->text_bytes = 0;
+    }
+    return VCFXG_OK;
+}
+
 int vcfxg_genotype_query(vcfxg_ctx *c, const char *query, size_t qlen, int strict, int strip_cr, vcfxg_summary *out) {
     if (!c || (!query && qlen)) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;

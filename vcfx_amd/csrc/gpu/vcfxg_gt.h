@@ -318,4 +318,56 @@ struct GqOp {
     __device__ void finish() { found = __any(any); }
 };
 
+// ---------------------------------------------------------------------------------------
+// nonref reducer (VCFX_nonref_filter): "some sample is not hom-ref".
+// Per sample the gi-th ':' subfield g (empty when absent) is hom-ref iff
+//   mmap  (allSamplesHomRefDirect :286-300): |g| = 3 ? g = "0s0" (s '/' or '|')
+//                                               : g non-empty of '0', '/', '|' only;
+//   stdin (isDefinitelyHomRef :419-449): g = "0s0", or g non-empty of '0', '/', '|' only.
+// An empty sample is not hom-ref in both modes.  On the fixed-stride layout (a, b digits or
+// '.') both rules are "a = b = '0'": the dword's digit fields are both 0.
+// ---------------------------------------------------------------------------------------
+struct NrOp {
+    const char *buf;
+    int64_t E;
+    int gi, mode;                // mode 0 mmap, 1 stdin
+    bool any = false;            // this lane saw a sample that is not hom-ref
+    bool found = false;          // wave
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() { return found = found || __any(any); }
+    __device__ void dword(const DwordView &v) { any = any || (v.real && v.f != 0u); }
+    __device__ void sample(int64_t st) {
+        if (any) return;
+        const int64_t se = sample_end(buf, st, E);
+        int64_t p = st, fs = st;
+        int fi = 0;
+        for (;; p++) {  // extractNthField(sample, gi) / the gi-th getline token
+            const bool end = (p == se) || byte_at(buf, p) == ':';
+            if (end) {
+                if (fi == gi) break;
+                fi++;
+                fs = p + 1;
+                if (p == se) {  // fewer subfields: not hom-ref
+                    any = true;
+                    return;
+                }
+            }
+        }
+        const int64_t n = p - fs;
+        bool hr = n > 0;
+        bool only = n > 0;  // every byte '0', '/' or '|'
+        for (int64_t k = fs; only && k < p; k++) {
+            const uint32_t c = byte_at(buf, k);
+            only = c == '0' || c == '/' || c == '|';
+        }
+        if (n == 3) {
+            const uint32_t c1 = byte_at(buf, fs + 1);
+            const bool pat = byte_at(buf, fs) == '0' && (c1 == '/' || c1 == '|') && byte_at(buf, fs + 2) == '0';
+            hr = pat || (mode == 1 && only);
+        } else hr = only;
+        if (!hr) any = true;
+    }
+    __device__ void finish() { found = __any(any); }
+};
+
 }  // namespace vcfxg

@@ -100,6 +100,11 @@ hipError_t launch_fuse_count(const char *buf, int64_t ds, int64_t n, uint64_t *c
 hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64_t *offs, int mode,
                             uint64_t *line_end, uint64_t cap, int32_t *alt, int32_t *tot, uint32_t *rowpre,
                             uint8_t *status, unsigned long long *counters, hipStream_t s);
+// VCFX_nonref_filter per line (mode 0 mmap, 1 stdin): status 1 keep / 2 drop / 4 '#' / 0 empty;
+// counters: [0] kept, [1] data lines, [3] lines off the fixed-stride sweep
+hipError_t launch_nr_records(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, uint8_t *status,
+                             unsigned long long *counters, hipStream_t s);
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int strip_cr, const char *q_dev,
                              int qlen, int strict, int qa, int qb, uint8_t *status, unsigned long long *counters,

@@ -739,6 +739,66 @@ __global__ __launch_bounds__(kRecThreads) void k_gq_records(const char *__restri
     flush_counters(cnt, counters);
 }
 
+// nonref_filter per line: status 1 keep, 2 drop, 4 '#' line, 0 empty.
+// filterNonRefMmap :458-551 (mode 0: '\r' stripped; FORMAT = field 8; keep when there is
+// no FORMAT, no GT in it or no 9th tab) / filterNonRef :553-636 (mode 1: keep under 10
+// fields or without GT; a trailing tab is an empty last sample, which keeps the line).
+// Data lines before '#CHROM' are the host's (warning + pass-through).
+__device__ uint8_t nr_line(const char *__restrict__ buf, int64_t ls, int64_t le, int mode, int64_t *lds,
+                           BlockCounters &bc) {
+    int64_t ae = le;
+    if (mode == 0 && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;
+    if (ae <= ls) return 0;
+    if (byte_at(buf, ls) == '#') return 4;
+    int64_t t[9];
+    const int nt = head_tabs(buf, ls, ae, 9, t, lds);
+    bool keep = true;
+    if (nt >= 8 && (mode == 0 || nt >= 9)) {
+        const int64_t fs = t[7] + 1, fe = nt >= 9 ? t[8] : ae;
+        const int gi = gt_index(buf, fs, fe);  // findGTIndex :317-335 (first "GT" getline token)
+        if (gi >= 0 && nt >= 9) {
+            const int64_t S = t[8] + 1;
+            if (S >= ae) keep = mode == 1;  // "...\tGT\t": mmap sees no sample, stdin an empty one
+            else if (mode == 1 && byte_at(buf, ae - 1) == '\t') keep = true;  // empty last sample
+            else {
+                NrOp op{buf, ae, gi, mode};
+                bool fast = gi == 0 && gt_fast<6>(buf, S, ae, op);
+                if (!fast) {
+                    bc.add(3, 1);
+                    NrOp g{buf, ae, gi, mode};
+                    gt_general(buf, S, ae, g);
+                    keep = g.found;
+                } else keep = op.found;
+            }
+        }
+    }
+    bc.add(0, keep);
+    bc.add(1, 1);
+    return keep ? 1 : 2;
+}
+__global__ __launch_bounds__(kRecThreads) void k_nr_records(const char *__restrict__ buf, int64_t data_start,
+                                                            const uint64_t *__restrict__ line_end,
+                                                            const uint64_t *n_lines_p, int mode,
+                                                            uint8_t *__restrict__ status_o,
+                                                            unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kRecWaves][16];
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t li = wid; li < n_lines; li += nw) {
+        int64_t ls, le;
+        line_bounds(line_end, data_start, li, ls, le);
+        const uint8_t st = nr_line(buf, ls, le, mode, lds, bc);
+        if (lane() == 0) status_o[li] = st;
+    }
+    flush_counters(cnt, counters);
+}
+
 // genotype_query as head pass (k_line_meta) + sweep: GT-first lines run only the sample
 // sweep (gt_fast with the GqOp early exit); full-path lines and fast-sweep failures go to
 // k_gq_complex (status kGqPending marks the latter)
@@ -1020,6 +1080,15 @@ hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint6
     unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
     hipLaunchKernelGGL(k_af_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
                        mode, static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
+    return hipGetLastError();
+}
+hipError_t launch_nr_records(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, uint8_t *status,
+                             unsigned long long *counters, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
+    hipLaunchKernelGGL(k_nr_records, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                       mode, status, counters);
     return hipGetLastError();
 }
 hipError_t launch_gq_records(const char *buf, int64_t data_start, const uint64_t *line_end,

@@ -1,0 +1,151 @@
+// VCFX_nonref_filter drop-in (a per-sample GT reducer on the record
+// path): the reference CLI (VCFX_nonref_filter.cpp:340-384, 646-652) on top of
+// vcfxg_nonref_filter.  The host handles the lines up to '#CHROM' (empty lines, headers, and
+// data lines before it, which are warned about and passed through) and the ordered output;
+// the per-record "every sample hom-ref" test runs on the GPU.
+#include <getopt.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "emit.h"
+#include "hostio.h"
+#include "tools.h"
+
+using namespace vcfxh;
+
+namespace {
+
+// displayHelp :386-417
+const char *kHelp =
+    "VCFX_nonref_filter: Exclude variants if all samples are homozygous reference.\n\n"
+    "Usage:\n"
+    "  VCFX_nonref_filter [options] [input.vcf]\n"
+    "  VCFX_nonref_filter [options] < input.vcf > output.vcf\n\n"
+    "Options:\n"
+    "  -h, --help          Show this help message\n"
+    "  -i, --input FILE    Input VCF file (uses fast memory-mapped I/O)\n\n"
+    "Description:\n"
+    "  Reads VCF lines. For each variant, we check each sample's genotype. If a\n"
+    "  genotype is polyploid, all alleles must be '0'. If a genotype is missing\n"
+    "  or partial, we consider it not guaranteed hom-ref => keep variant.\n"
+    "  If we find at least one sample not hom-ref, we print the variant. Otherwise,\n"
+    "  we skip it.\n\n"
+    "Performance:\n"
+    "  File input (-i) uses memory-mapped I/O for 100-1000x faster processing\n"
+    "  compared to stdin. Features include:\n"
+    "  - SIMD-optimized line scanning (AVX2/SSE2)\n"
+    "  - Zero-copy string parsing with string_view\n"
+    "  - 1MB output buffering\n"
+    "  - Direct GT field extraction (avoids full sample parsing)\n"
+    "  - Early termination on first non-homref sample\n\n"
+    "Examples:\n"
+    "  VCFX_nonref_filter -i input.vcf > filtered.vcf    # Fast (mmap)\n"
+    "  VCFX_nonref_filter input.vcf > filtered.vcf       # Fast (mmap)\n"
+    "  VCFX_nonref_filter < input.vcf > filtered.vcf     # Slower (stdin)\n\n";
+
+// returns false on device error.  filterNonRefMmap :458-551 (stream_mode false: '\r'
+// stripped from every line) / filterNonRef :553-636
+bool run_nr(const Input &in, bool stream_mode, int out_fd, Out &err) {
+    if (!stream_mode && in.n == 0) return true;
+    LineEmitter em(in.p, in.n, out_fd);
+    auto bare = [&](const char *ls, const char *le) {  // the line as the reference sees it
+        return (!stream_mode && le > ls && le[-1] == '\r') ? le - 1 : le;
+    };
+    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    bool found = false;
+    size_t data_start = in.n;
+    while (next_line(p, end, ls, le)) {
+        const char *ae = bare(ls, le);
+        if (ae == ls) {
+            em.line(ls, ls);
+            continue;
+        }
+        if (*ls == '#') {
+            em.line(ls, ae);
+            if (is_chrom_line(ls, (size_t)(ae - ls))) {
+                found = true;
+                data_start = (size_t)(p - in.p);
+                break;
+            }
+            continue;
+        }
+        err.put("Warning: VCF data line encountered before #CHROM. Passing line.\n");
+        em.line(ls, ae);
+    }
+    if (found && data_start < in.n) {
+        vcfxg_ctx *g = gpu(err.fd);
+        if (!g) return false;
+        uint64_t nl = 0;
+        vcfxg_summary s;
+        if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
+            !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
+            !gpu_ok(g, vcfxg_nonref_filter(g, stream_mode ? VCFXG_MODE_STDIN : VCFXG_MODE_FILE, &s), "nonref_filter",
+                    err.fd))
+            return false;
+        std::vector<uint64_t> ends(nl);
+        std::vector<uint8_t> st(nl);
+        if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||
+            !gpu_ok(g, vcfxg_fetch_lines(g, 0, nl, nullptr, nullptr, st.data()), "fetch_lines", err.fd))
+            return false;
+        uint64_t prev = data_start;
+        for (uint64_t i = 0; i < nl; i++) {
+            const char *a = in.p + prev, *b = in.p + ends[i];
+            prev = ends[i] + 1;
+            switch (st[i]) {
+            case VCFXG_LINE_SKIP: em.line(a, a); break;  // an empty line: "\n"
+            case VCFXG_LINE_HEADER:
+            case VCFXG_LINE_ROW: em.line(a, bare(a, b)); break;
+            default: break;  // VCFXG_LINE_DROP: every sample hom-ref
+            }
+        }
+    }
+    em.finish();
+    return true;
+}
+
+}  // namespace
+
+extern "C" int vcfx_tool_nonref_filter(int argc, char **argv, int in_fd, int out_fd, int err_fd) {
+    Out out(out_fd), err(err_fd);
+    // vcfx::handle_common_flags (vcfx_core.h:57-62)
+    if (flag_present(argc, argv, "--help", "-h")) {
+        out.put(kHelp);
+        return 0;
+    }
+    if (flag_present(argc, argv, "--version", "-v")) {
+        out.put("VCFX_nonref_filter version " VCFX_VERSION_STR "\n");
+        return 0;
+    }
+    std::string input;
+    bool help = false;
+    static struct option lo[] = {{"help", no_argument, nullptr, 'h'},
+                                 {"input", required_argument, nullptr, 'i'},
+                                 {nullptr, 0, nullptr, 0}};
+    GetoptStderr gs(err);
+    optind = 0;
+    int opt;
+    while ((opt = getopt_long(argc, argv, "hi:", lo, nullptr)) != -1) {
+        if (opt == 'i') input = optarg;
+        else help = true;  // -h and anything getopt rejects: the help text
+    }
+    gs.done();
+    if (input.empty() && optind < argc) input = argv[optind];
+    if (help) {
+        out.put(kHelp);
+        return 0;
+    }
+    Input in;
+    if (!input.empty() && input != "-") {
+        if (!in.open_file(input.c_str())) {
+            err.put("Error: Cannot open file: " + input + "\n");
+            return 0;
+        }
+        out.flush();
+        return run_nr(in, false, out_fd, err) ? 0 : 1;
+    }
+    in.read_fd(in_fd);
+    out.flush();
+    return run_nr(in, true, out_fd, err) ? 0 : 1;
+}

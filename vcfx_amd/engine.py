@@ -50,6 +50,7 @@ SIGNATURES = {
     "vcfxg_genotype_query": (_I, [_VP, _P, _S, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_record_filter": (_I, [_VP, _VP, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_variant_count": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_nonref_filter": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_prefixes": (_I, [_VP, _VP, _S, _VP]),
     "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
@@ -162,6 +163,12 @@ class Engine:
         s = Summary()
         self._chk(self.L.vcfxg_genotype_query(self.h, q, len(q), int(strict), int(strip_cr), ctypes.byref(s)),
                   "genotype_query")
+        return s
+
+    def nonref_filter(self, mode):
+        """VCFX_nonref_filter per line over the indexed region (mode MODE_FILE / MODE_STDIN)"""
+        s = Summary()
+        self._chk(self.L.vcfxg_nonref_filter(self.h, int(mode), ctypes.byref(s)), "nonref_filter")
         return s
 
     def _criteria(self, crits):
