@@ -173,12 +173,11 @@ def main():
                       "af_pipe", "af_stream", "af_walk", "walk_compact", "af_complex", "af_rows", "af_format")
     elif a.workload == "nonref":
         def step():
-            eng.index(ds)
-            s = eng.nonref_filter(engine.MODE_FILE)  # index + per-record "every sample hom-ref"
+            s = eng.nonref_filter_region(ds, engine.MODE_FILE)  # (the walk) per-record "every sample hom-ref"
             if red is not None:
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.general_records])
             return s
-        kern_names = ("line_count", "line_emit", "line_compact", "nr_records")
+        kern_names = ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "nr_records")
     elif a.workload == "pipeline":
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
@@ -287,9 +286,10 @@ def main():
                 # filter / query walk (no index sweep): the record bytes once + per line its
                 # region results (line_end 8, status 1, head record 16, tab offsets 16); the rest
                 # compacts them (read + write) and reads status + head record + tabs once more
-                # (nonref: nr_records stops at each record's first non-hom-ref sample, so its
-                # bytes are data-dependent; the roofline line is the index sweep's)
-                "fq_walk": region_bytes + L * (8 + 1 + 16 + 16),
+                # (nonref: the walk stops each record's sweep at its first non-hom-ref sample and
+                # scans the rest for the '\n' only when its end was predicted, so fq_walk's bytes are
+                # counted as the whole region, as for the query walk)
+                "fq_walk": region_bytes + L * (8 + 1 + 16 + (16 if a.workload == "pipeline" else 0)),
                 "fq_rest": L * (2 * (8 + 1 + 16 + 16) + 16 + 1 + 16),
             }
             dom = max((k for k in kernels if k in algo), key=kernels.get)
@@ -302,8 +302,8 @@ def main():
                   "allele counts + formatted rows" % (a.records, a.samples),
             "pipeline": "VCFX_record_filter --filter 'QUAL>=30;FILTER==PASS' | VCFX_genotype_query "
                         "--genotype-query '0|1' fused, device-resident %d x %d shard per GPU" % (a.records, a.samples),
-            "nonref": "VCFX_nonref_filter -i (file path) on a device-resident %d x %d shard per GPU: index + "
-                      "per-record all-samples-hom-ref test" % (a.records, a.samples),
+            "nonref": "VCFX_nonref_filter -i (file path) on a device-resident %d x %d shard per GPU: the walk "
+                      "with the per-record all-samples-hom-ref test" % (a.records, a.samples),
             "ld": "VCFX_ld_calculator -w %d -t %g streaming on a device-resident %d x %d shard per GPU: parse + "
                   "FP4-MFMA pair sums (count + emit) + pair text" % (a.window, a.threshold, a.records, a.samples),
         }[a.workload]

@@ -173,6 +173,9 @@ int vcfxg_filter_query_region(vcfxg_ctx *ctx, size_t data_start, const vcfxg_cri
  * VCFXG_MODE_STDIN filterNonRef + isDefinitelyHomRef (:553-636, 419-449).  Data lines
  * before '#CHROM' are the caller's (the tool warns and passes them through). */
 int vcfxg_nonref_filter(vcfxg_ctx *ctx, int mode, vcfxg_summary *out);
+/* The same over the data region from data_start without a separate index (the filter /
+ * query walk with the nonref reducer; index + vcfxg_nonref_filter for short records). */
+int vcfxg_nonref_filter_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
 
 /* ---- variant counter -------------------------------------------------------------------
  * Per line status: ROW = data line with >= 8 tab-separated columns (counted), WARN = fewer

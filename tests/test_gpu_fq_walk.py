@@ -76,6 +76,9 @@ def _all(eng, buf):
         for crits, logic in CRITS[:2]:
             _check(eng, buf, ds, lambda: eng.filter_query_region(ds, crits, q, logic, strict),
                    lambda: eng.filter_query(crits, q, logic, strict), ("pipe", crits, q, strict))
+    # VCFX_nonref_filter on the same walk (its own reducer), both input modes
+    for mode, d in ((engine.MODE_FILE, ds), (engine.MODE_STDIN, dsq)):
+        _check(eng, buf, d, lambda: eng.nonref_filter_region(d, mode), lambda: eng.nonref_filter(mode), ("nr", mode))
 
 
 @pytest.mark.parametrize("cfg", SYNTH)

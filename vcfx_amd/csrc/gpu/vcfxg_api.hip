@@ -1209,9 +1209,11 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
         if (r) return r;
         if (what == vcfxg::kFqRF) return vcfxg_record_filter(c, crit, n, and_logic, out);
         if (what == vcfxg::kFqGQ) return vcfxg_genotype_query(c, query, qlen, strict, gq_strip_cr, out);
+        if (what == vcfxg::kFqNR) return vcfxg_nonref_filter(c, gq_strip_cr ? VCFXG_MODE_FILE : VCFXG_MODE_STDIN, out);
         return vcfxg_filter_query(c, crit, n, and_logic, query, qlen, strict, out);
     }
-    const bool rf = (what & vcfxg::kFqRF) != 0, gq = (what & vcfxg::kFqGQ) != 0;
+    const bool nr = what == vcfxg::kFqNR;  // nonref_filter: the query's walk with its own reducer
+    const bool rf = !nr && (what & vcfxg::kFqRF) != 0, gq = nr || (what & vcfxg::kFqGQ) != 0;
     const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
     const uint64_t cap = (uint64_t)nw * cap_w;
     const size_t mb = vcfxg::af_meta_bytes();
@@ -1258,9 +1260,15 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
                                        P<uint8_t>(c->wk_status), c->wk_meta.p, c->wk_tabs.p, P<uint64_t>(c->line_end),
                                        P<uint8_t>(c->status), c->af_meta.p, c->rf_tabs.p, P<uint64_t>(c->d_nlines),
                                        c->stream));
-    HIPCHK(c, vcfxg::launch_fq_finish(what, buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, ra,
-                                      P<uint8_t>(c->status), c->af_meta.p, c->rf_tabs.p, cnt, gq_cnt, c->stream));
-    if (gq)
+    if (nr)
+        HIPCHK(c, vcfxg::launch_nr_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap,
+                                           strip_cr ? VCFXG_MODE_FILE : VCFXG_MODE_STDIN, P<uint8_t>(c->status), cnt,
+                                           c->stream));
+    else
+        HIPCHK(c, vcfxg::launch_fq_finish(what, buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap,
+                                          ra, P<uint8_t>(c->status), c->af_meta.p, c->rf_tabs.p, cnt, gq_cnt,
+                                          c->stream));
+    if (gq && !nr)
         HIPCHK(c, vcfxg::launch_gq_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, strip_cr,
                                            P<char>(c->query), (int)qlen, strict, qa, qb, c->af_meta.p,
                                            P<uint8_t>(c->status), gq_cnt,
@@ -1291,7 +1299,8 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
         } else {
             out->rows = host[0];
             out->data_lines = host[1];
-            if (gq) {
+            if (nr) out->general_records = host[3];
+            else if (gq) {
                 out->warn_lines = host[2];
                 out->general_records = host[3];
             }
@@ -1313,6 +1322,10 @@ int vcfxg_genotype_query_region(vcfxg_ctx *c, size_t data_start, const char *que
 int vcfxg_filter_query_region(vcfxg_ctx *c, size_t data_start, const vcfxg_criterion *crit, int n, int and_logic,
                               const char *query, size_t qlen, int strict, vcfxg_summary *out) {
     return fq_region(c, data_start, vcfxg::kFqBoth, crit, n, and_logic, query, qlen, strict, 1, out);
+}
+int vcfxg_nonref_filter_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    if (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN) return VCFXG_E_ARG;
+    return fq_region(c, data_start, vcfxg::kFqNR, nullptr, 0, 0, "", 0, 0, mode == VCFXG_MODE_FILE ? 1 : 0, out);
 }
 
 int vcfxg_variant_count(vcfxg_ctx *c, int strip_cr, vcfxg_summary *out) {

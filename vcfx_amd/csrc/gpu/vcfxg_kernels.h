@@ -102,6 +102,10 @@ hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64
                             uint8_t *status, unsigned long long *counters, hipStream_t s);
 // VCFX_nonref_filter per line (mode 0 mmap, 1 stdin): status 1 keep / 2 drop / 4 '#' / 0 empty;
 // counters: [0] kept, [1] data lines, [3] lines off the fixed-stride sweep
+// after the nonref walk: nr_line for the lines it left (kGqPending / kGqFull), counters as above
+hipError_t launch_nr_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, uint8_t *status,
+                             unsigned long long *counters, hipStream_t s);
 hipError_t launch_nr_records(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, uint8_t *status,
                              unsigned long long *counters, hipStream_t s);

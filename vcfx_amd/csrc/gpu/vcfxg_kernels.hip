@@ -799,6 +799,46 @@ __global__ __launch_bounds__(kRecThreads) void k_nr_records(const char *__restri
     flush_counters(cnt, counters);
 }
 
+// after the nonref walk: the lines it left (kGqPending: a GT-first record off the fixed-stride
+// sweep; kGqFull: everything else) through nr_line, one wave each, and the tool's counters
+// over all lines (lane per line, 64 lines per wave step)
+__global__ __launch_bounds__(kRecThreads) void k_nr_complex(const char *__restrict__ buf, int64_t data_start,
+                                                            const uint64_t *__restrict__ line_end,
+                                                            const uint64_t *n_lines_p, int mode,
+                                                            uint8_t *__restrict__ status,
+                                                            unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kRecWaves][16];
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    uint32_t kept = 0, data = 0;  // this lane's walk-decided lines (nr_line counts its own)
+    for (uint64_t g0 = wid * kWave; g0 < n_lines; g0 += nw * kWave) {
+        const uint64_t li = g0 + lane();
+        const uint8_t st = li < n_lines ? status[li] : 0;
+        const bool pend = st == kGqPending || st == kGqFull;
+        kept += !pend && st == 1;
+        data += !pend && (st == 1 || st == 2);
+        uint64_t todo = __ballot(pend);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint64_t lk = g0 + k;
+            int64_t ls, le;
+            line_bounds(line_end, data_start, lk, ls, le);
+            const uint8_t r = nr_line(buf, ls, le, mode, lds, bc);
+            if (lane() == 0) status[lk] = r;
+        }
+    }
+    bc.add(0, wave_sum(kept));
+    bc.add(1, wave_sum(data));
+    flush_counters(cnt, counters);
+}
+
 // genotype_query as head pass (k_line_meta) + sweep: GT-first lines run only the sample
 // sweep (gt_fast with the GqOp early exit); full-path lines and fast-sweep failures go to
 // k_gq_complex (status kGqPending marks the latter)
@@ -1080,6 +1120,15 @@ hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint6
     unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
     hipLaunchKernelGGL(k_af_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
                        mode, static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
+    return hipGetLastError();
+}
+hipError_t launch_nr_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
+                             const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, uint8_t *status,
+                             unsigned long long *counters, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    unsigned grid = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
+    hipLaunchKernelGGL(k_nr_complex, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                       mode, status, counters);
     return hipGetLastError();
 }
 hipError_t launch_nr_records(const char *buf, int64_t data_start, const uint64_t *line_end,

@@ -1,6 +1,6 @@
 // VCFX_nonref_filter drop-in (a per-sample GT reducer on the record
 // path): the reference CLI (VCFX_nonref_filter.cpp:340-384, 646-652) on top of
-// vcfxg_nonref_filter.  The host handles the lines up to '#CHROM' (empty lines, headers, and
+// vcfxg_nonref_filter_region (the walk for long records).  The host handles the lines up to '#CHROM' (empty lines, headers, and
 // data lines before it, which are warned about and passed through) and the ordered output;
 // the per-record "every sample hom-ref" test runs on the GPU.
 #include <getopt.h>
@@ -80,10 +80,10 @@ bool run_nr(const Input &in, bool stream_mode, int out_fd, Out &err) {
         uint64_t nl = 0;
         vcfxg_summary s;
         if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
-            !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
-            !gpu_ok(g, vcfxg_nonref_filter(g, stream_mode ? VCFXG_MODE_STDIN : VCFXG_MODE_FILE, &s), "nonref_filter",
-                    err.fd))
+            !gpu_ok(g, vcfxg_nonref_filter_region(g, data_start, stream_mode ? VCFXG_MODE_STDIN : VCFXG_MODE_FILE, &s),
+                    "nonref_filter", err.fd))
             return false;
+        nl = s.n_lines;
         std::vector<uint64_t> ends(nl);
         std::vector<uint8_t> st(nl);
         if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||

@@ -51,6 +51,7 @@ SIGNATURES = {
     "vcfxg_record_filter": (_I, [_VP, _VP, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_variant_count": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
     "vcfxg_nonref_filter": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_nonref_filter_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_prefixes": (_I, [_VP, _VP, _S, _VP]),
     "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
@@ -169,6 +170,13 @@ class Engine:
         """VCFX_nonref_filter per line over the indexed region (mode MODE_FILE / MODE_STDIN)"""
         s = Summary()
         self._chk(self.L.vcfxg_nonref_filter(self.h, int(mode), ctypes.byref(s)), "nonref_filter")
+        return s
+
+    def nonref_filter_region(self, data_start, mode):
+        """index + nonref_filter in one call (the walk for long records)"""
+        s = Summary()
+        self._chk(self.L.vcfxg_nonref_filter_region(self.h, data_start, int(mode), ctypes.byref(s)),
+                  "nonref_filter_region")
         return s
 
     def _criteria(self, crits):
