@@ -33,7 +33,8 @@ KERNELS = {
     "af_format": r"vcfxg::k_af_format\(",
     "rf_records": r"vcfxg::k_rf_records\(",
     "fq_walk": r"vcfxg::k_fq_walk<",
-    "fq_rest": r"vcfxg::k_(fq_compact<|fq_finish<|gq_complex\()",
+    "fq_rest": r"vcfxg::k_(fq_compact<|fq_finish<|gq_complex\(|nr_complex\()",
+    "nr_records": r"vcfxg::k_nr_records\(",
     "gq_records": r"vcfxg::k_(line_meta|gq_sweep|gq_complex)\(",
     "ld_parse": r"vcfxg::k_ld_parse\(",
     "ld_count": r"vcfxg::k_ld_fast<1>\(",
@@ -50,6 +51,7 @@ TIMED = {
     "af": ("af_scan", "line_count", "line_emit", "line_compact", "af_records", "af_chunks", "af_fused",
            "af_pipe", "af_stream", "af_walk", "walk_compact", "af_complex", "af_format"),
     "pipeline": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "rf_records", "gq_records"),
+    "nonref": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "nr_records"),
     "ld": ("line_count", "line_emit", "line_compact", "ld_parse", "ld_count", "ld_emit", "ld_count_gen",
            "ld_emit_gen", "ld_matrix"),
 }
