@@ -45,6 +45,8 @@ def test_two_rank_shards_match_single_gpu(tmp_path):
     open(p2, "wb").write(synth.generate(1500, 300, 72, 0, 0.01, 1, 0.0, 0))
     cases = [["VCFX_allele_freq_calc", "-i", p1], ["VCFX_allele_freq_calc", "-q", p1],
              ["VCFX_variant_counter", p1],
+             ["VCFX_record_filter", "--filter", "QUAL>=30;FILTER==PASS", "-i", p1],
+             ["VCFX_genotype_query", "-g", "0|1", "-i", p1], ["VCFX_nonref_filter", "-i", p1],
              ["VCFX_ld_calculator", "-i", p2, "-w", "300", "-t", "0.2"],
              ["VCFX_ld_calculator", "-i", p2, "-w", "5000"],
              ["VCFX_ld_calculator", "-i", p2, "-m", "-r", "21:9411239-9430000"]]

@@ -81,6 +81,9 @@ def _cases(files):
     for k, p in files.items():
         cases += [["VCFX_allele_freq_calc", "-i", p], ["VCFX_allele_freq_calc", "-q", "-i", p],
                   ["VCFX_allele_freq_calc", p], ["VCFX_variant_counter", p]]
+        cases += [["VCFX_record_filter", "--filter", "QUAL>=30;AF>=0.05", "-i", p],
+                  ["VCFX_genotype_query", "-g", "0/1", "-i", p], ["VCFX_genotype_query", "-g", "1|1", "--strict", p],
+                  ["VCFX_nonref_filter", "-i", p], ["VCFX_nonref_filter", p]]
     cases.append(["VCFX_variant_counter", "--strict", files["bad"]])
     return cases
 

@@ -11,6 +11,11 @@ share of ONE input file:
 * VCFX_variant_counter FILE: the whole file is cut the same way; "Total Variants" is
   all-reduced; warning line numbers are shifted to whole-file numbering; under --strict the
   earliest failing line of any rank wins.
+* VCFX_record_filter / VCFX_genotype_query / VCFX_nonref_filter with a file input: the
+  records are cut the same way; every rank runs the filter on header + its records, and
+  once more on the header alone to learn the header's own output (H, E), which it strips
+  from its outputs; rank 0 writes H and E once, then the ranks' kept lines and warnings in
+  rank order.  Files with data lines before '#CHROM' run unsharded.
 * VCFX_ld_calculator -i FILE (streaming): every rank parses the file and computes the pair
   rows of its `--shard r/N` share (equal window-pair counts); rank 0 writes the header and
   the ranks' pair lines in rank order.  Matrix mode runs on rank 0 only.
@@ -220,6 +225,48 @@ def run_vc(argv, comm, runner):
     return b"Total Variants: %d\n" % red[0], b"".join(errs), 0
 
 
+def _pre_header_data(buf, ds):
+    """a data line (not empty, not '#') before the '#CHROM' line"""
+    for line in bytes(buf[:ds]).split(b"\n"):
+        line = line[:-1] if line.endswith(b"\r") else line
+        if line and not line.startswith(b"#"):
+            return True
+    return False
+
+
+def run_filter(argv, comm, runner, path):
+    buf = np.memmap(path, np.uint8, mode="r") if os.path.getsize(path) else np.zeros(0, np.uint8)
+    ds = header_end(buf)
+    plain = ds < len(buf) and not _pre_header_data(buf, ds)
+    ok = comm.allreduce([1 if plain else 0], op="min")[0]
+    out = err = b""
+    rc = 0
+    if ok:
+        cuts = record_cuts(buf, ds, comm.world)
+        lo, hi = cuts[comm.rank], cuts[comm.rank + 1]
+        head = _write_shard([buf[:ds]])
+        shard = _write_shard([buf[:ds], buf[lo:hi]])
+        try:
+            H, E, _ = runner([a if a != path else head for a in argv], b"")
+            out, err, rc = runner([a if a != path else shard for a in argv], b"")
+        finally:
+            os.unlink(head)
+            os.unlink(shard)
+        good = out.startswith(H) and err.startswith(E)
+        ok = comm.allreduce([1 if good else 0], op="min")[0]
+        out, err = out[len(H):], err[len(E):]
+    if not ok:  # unsharded on rank 0
+        if comm.rank:
+            return b"", b"", 0
+        return runner(argv, b"")
+    outs = comm.gather_bytes(out)
+    errs = comm.gather_bytes(err)
+    rcs = comm.allreduce([rc])
+    if comm.rank:
+        return b"", b"", 0
+    return H + b"".join(outs), E + b"".join(errs), 1 if rcs[0] else 0
+
+
 def run_ld(argv, comm, runner):
     out, err, rc = runner(argv + ["--shard", "%d/%d" % (comm.rank, comm.world)], b"")
     outs = comm.gather_bytes(out)
@@ -245,6 +292,10 @@ def run_sharded(argv, stdin=b"", dist=None, runner=None):
             return run_vc(argv, comm, runner)
         if tool == "VCFX_ld_calculator" and _input_path(argv) and not ("-m" in argv or "--matrix" in argv):
             return run_ld(argv, comm, runner)
+        if tool in ("VCFX_record_filter", "VCFX_genotype_query", "VCFX_nonref_filter"):
+            path = _input_path(argv, positional=True)
+            if path:
+                return run_filter(argv, comm, runner, path)
     if comm.rank:
         return b"", b"", 0
     return runner(argv, stdin)
