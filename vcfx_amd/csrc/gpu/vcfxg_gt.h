@@ -42,6 +42,9 @@ __device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_
 #ifndef VCFXG_UNROLL
 #define VCFXG_UNROLL 4
 #endif
+#ifndef VCFXG_NT_SWEEP
+#define VCFXG_NT_SWEEP 0
+#endif
 struct NoPre {
     __device__ void operator()() const {}
 };
@@ -81,7 +84,15 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
         for (int u = 0; u < kUnroll; u++) {
             const int blk = w0 + u * kWaveStep + lo16;
             const int bl = blk < Er ? blk : lastblk;
+#if VCFXG_NT_SWEEP  // streaming (non-temporal) loads for the read-once sample bytes
+            {
+                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+                const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(base + bl));
+                v[u] = make_uint4(t.x, t.y, t.z, t.w);
+            }
+#else
             v[u] = load16(base, bl);
+#endif
             x4[u] = load4(base, bl + 16);
         }
         if (w0 == 0) pre();  // e.g. a prefetch that must not hold up these loads
