@@ -424,7 +424,9 @@ hipError_t launch_fq_finish(int what, const char *buf, int64_t data_start, const
                             void *meta, const void *tabs, unsigned long long *rf_cnt, unsigned long long *gq_cnt,
                             hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
-    const unsigned grid = (unsigned)std::min<uint64_t>((n_lines_host + 255) / 256, 1024);
+    // one line per thread: the filter is a latency chain (line end, tabs, field bytes), so
+    // every line gets its own thread rather than a grid-stride share
+    const unsigned grid = (unsigned)std::min<uint64_t>((n_lines_host + 255) / 256, 65535);
     LineMeta *m = static_cast<LineMeta *>(meta);
     const uint4 *t = static_cast<const uint4 *>(tabs);
     if (what == kFqRF)
