@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--threshold", type=float, default=0.5, help="ld: r^2 threshold")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end CLI timings")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal on one GPU)")
     a = ap.parse_args()
     if a.records is None:
@@ -124,6 +125,108 @@ def cpu_baseline(workload, arr, offs, a):
     return {"value": nvar * reps / t, "unit": "records/s", "cores": 1, "kind": "port",
             "sample": "first %d records (%.1f MB) of the rank-0 shard, %s, %d reps, %.1f s"
                       % (nvar, len(sample) / 1e6, desc, reps, t)}
+
+
+def output_check(workload, eng, s, a, rank):
+    """The last timed step's output against the REFERENCE's, on rank 0 at the BASELINE sizes:
+    the digests tests/golden/full_digests.json holds for this exact synthetic input (made by
+    running the reference binaries on it).  AF: sha256 of the formatted rows; pipeline /
+    nonref: sha256 of the kept-record bitmap; LD: the first 3,000 variants' pairs (their pairs
+    are the first lines of the stream at a window >= 3,000).  A mismatch raises."""
+    import hashlib
+    import numpy as np
+    try:
+        with open(os.path.join(REPO, "tests", "golden", "full_digests.json")) as f:
+            dig = json.load(f)
+    except OSError:
+        return {"checked": False, "why": "no tests/golden/full_digests.json"}
+    default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "ld": 100000}[workload]
+    if rank != 0 or a.records != default or a.samples != 2504 or (workload == "ld" and (a.window < 3000 or
+                                                                                         a.threshold != 0.5)):
+        return {"checked": False, "why": "no reference digest for this rank/configuration"}
+    if workload == "af":
+        c = dig["cases"]["af_file"]
+        got = hashlib.sha256(b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes)).hexdigest()
+        want, what = c["stdout"]["sha256"], "sha256 of the AF rows vs VCFX_allele_freq_calc -q -i (reference)"
+    elif workload in ("pipeline", "nonref"):
+        c = dig["cases"]["pipeline_bench" if workload == "pipeline" else "nonref_file"]
+        keep = (eng.statuses(s.n_lines) == 1).astype(np.uint8)
+        got = hashlib.sha256(np.packbits(keep).tobytes()).hexdigest()
+        want = c["keep_mask_sha256"]
+        what = "sha256 of the kept-record bitmap vs the reference's kept records (%s)" % " | ".join(
+            st[0] for st in c["stages"])
+    else:
+        c = dig["cases"]["ld3000_bench"]
+        head = b"#VAR1_CHROM\tVAR1_POS\tVAR1_ID\tVAR2_CHROM\tVAR2_POS\tVAR2_ID\tR2\n"
+        n = c["stdout"]["len"] - len(head)
+        text = eng.text(s[2])
+        got = hashlib.sha256(head + text[:n]).hexdigest()
+        want = c["stdout"]["sha256"]
+        what = "sha256 of the first 3,000 variants' pair lines vs VCFX_ld_calculator -w 100000 -t 0.5 (reference)"
+    if got != want:
+        raise AssertionError("bench output differs from the reference: %s (%s != %s)" % (what, got, want))
+    return {"checked": True, "match": True, "what": what}
+
+
+PCIE_H2D_GBS = 56.0  # pinned H2D measured on MI355X (tools/microbench/h2d_ingest.cpp; spec Gen5 x16 63 GB/s)
+
+
+def e2e_rates(workload, arr, a):
+    """End-to-end records/s of the drop-in CLI on this rank's synthetic file: page-cache-warm
+    file -> mmap -> H2D -> kernels -> rows -> stdout (/dev/null), wall clock of the whole process
+    (HIP runtime start included), best of 3; the same through a pipe (`cat F | tool`, the
+    streaming stdin ingest); and the in-process tool call with the device context already open
+    (libvcfx_tools, a long-running caller).  Never `value`: the device-resident rate is."""
+    import subprocess
+    from vcfx_amd import tool_binary, tools
+    if workload == "af":
+        tool, args = "VCFX_allele_freq_calc", ["-q"]
+    elif workload == "nonref":
+        tool, args = "VCFX_nonref_filter", []
+    elif workload == "pipeline":
+        tool, args = "VCFX_record_filter", ["--filter", "QUAL>=30;FILTER==PASS"]
+    else:
+        return None
+    fd, path = tempfile.mkstemp(suffix=".vcf")  # TMPDIR: a disk-backed file system, page cache warm
+    os.close(fd)
+    try:
+        arr.tofile(path)
+        exe = tool_binary(tool)
+        runs = {}
+        for name, cmd in (("process_file", [exe] + args + ["-i", path]),
+                          ("process_stdin_pipe", ["bash", "-o", "pipefail", "-c",
+                                                  "cat '%s' | '%s' %s" % (path, exe, " ".join("'%s'" % x for x in args))])):
+            walls = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=300)
+                walls.append(time.perf_counter() - t0)
+                assert r.returncode == 0, r.stderr[-500:]
+            runs[name] = {"value": a.records / min(walls), "wall_s": [round(w, 4) for w in walls]}
+        # in-process (libvcfx_tools' vcfx_tool_main, stdout -> /dev/null): the first call opens
+        # the context and is not counted
+        import ctypes
+        L = tools.lib()
+        argv = [tool] + args + ["-i", path]
+        carr = (ctypes.c_char_p * (len(argv) + 1))(*[x.encode() for x in argv], None)
+        dn = os.open(os.devnull, os.O_RDWR)
+        walls = []
+        try:
+            for _ in range(4):
+                t0 = time.perf_counter()
+                rc = L.vcfx_tool_main(tool.encode(), len(argv), carr, dn, dn, dn)
+                walls.append(time.perf_counter() - t0)
+                assert rc == 0, rc
+        finally:
+            os.close(dn)
+        runs["warm_context_file"] = {"value": a.records / min(walls[1:]), "wall_s": [round(w, 4) for w in walls[1:]],
+                                     "note": "in-process vcfx_tool_main with the device context already open"}
+        runs["pcie_ceiling"] = a.records / (arr.size / (PCIE_H2D_GBS * 1e9))
+        runs["unit"] = "records/s"
+        runs["cmd"] = "%s %s -i FILE > /dev/null (page-cache-warm %.2f GB file)" % (tool, " ".join(args), arr.size / 1e9)
+        return runs
+    finally:
+        os.unlink(path)
 
 
 def main():
@@ -332,6 +435,9 @@ def main():
         if ld:
             out["pairs_per_gpu"] = pairs
             out["pairs_emitted"] = np_
+        out["output_check"] = output_check(a.workload, eng, s, a, rank)
+        if world == 1 and not a.no_e2e:
+            out["e2e"] = e2e_rates(a.workload, arr, a)
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.workload, arr, offs, a)
         print(json.dumps(out), flush=True)

@@ -30,7 +30,7 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
     for w in $WLS; do
         step rocprof_$w 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$w -o run --output-format csv -- \
-            python bench.py --workload $w --steps 5 --warmup 1 --no-cpu-baseline || exit $?
+            python bench.py --workload $w --steps 5 --warmup 1 --no-cpu-baseline --no-e2e || exit $?
         grep '^{' gpurun_out/rocprof_$w.log > gpurun_out/rocprof_bench_$w.json  # the bench line of the traced run
     done
 fi
@@ -38,7 +38,7 @@ if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
     for w in $WLS; do
         for c in FETCH_SIZE WRITE_SIZE; do
             step pmc_${w}_$c 600 rocprofv3 --pmc $c -d gpurun_out/pmc_${w}_$c -o run --output-format csv -- \
-                python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline || exit $?
+                python bench.py --workload $w --steps 2 --warmup 1 --no-cpu-baseline --no-e2e || exit $?
         done
         python tools/pmc_traffic.py $w $(find gpurun_out/pmc_${w}_FETCH_SIZE -name '*counter_collection.csv' | head -1) \
             $(find gpurun_out/pmc_${w}_WRITE_SIZE -name '*counter_collection.csv' | head -1) gpurun_out/pmc_traffic.json \
@@ -49,9 +49,9 @@ fi
 if [ "$MODE" = rehearse ]; then
     step rehearse_af 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29512 bench.py --gpus 2 --steps 3 --warmup 1 --records 50000 --dist-backend gloo \
-        --no-cpu-baseline || exit $?
+        --no-cpu-baseline --no-e2e || exit $?
     step rehearse_ld 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29513 bench.py --gpus 2 --workload ld --records 20000 --window 20000 --steps 2 --warmup 1 \
-        --dist-backend gloo --no-cpu-baseline || exit $?
+        --dist-backend gloo --no-cpu-baseline --no-e2e || exit $?
 fi
 echo "=== done"

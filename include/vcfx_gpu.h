@@ -75,6 +75,22 @@ int vcfxg_reset_kernel_stats(vcfxg_ctx *ctx);
  * it straight from HBM.  Replaces MappedFile::open (VCFX_allele_freq_calc.cpp:47-70) and
  * the std::getline loops' buffering. */
 int vcfxg_load_host(vcfxg_ctx *ctx, const char *host, size_t n);
+/* Streaming form of the same (SURVEY 8(b) vcfxg_ingest; the pipe paths of processStdin,
+ * VCFX_allele_freq_calc.cpp:477-557, VCFX_record_filter.cpp:498-549, VCFX_genotype_query.cpp:
+ * 527-617): vcfxg_ingest_begin starts a new input (size_hint = expected bytes, may be 0);
+ * each vcfxg_ingest appends n bytes with an asynchronous H2D copy, so the caller's next read
+ * overlaps the transfer; the device buffer grows as needed.  The call with is_final_chunk
+ * set completes the input, which is then loaded exactly as by vcfxg_load_host.  Every
+ * chunk's host bytes must stay valid until that final call returns.
+ * vcfxg_load_host(h, n) == vcfxg_ingest_begin(n) + vcfxg_ingest(h, n, 1). */
+int vcfxg_ingest_begin(vcfxg_ctx *ctx, size_t size_hint);
+int vcfxg_ingest(vcfxg_ctx *ctx, const char *host, size_t n, int is_final_chunk);
+/* wait until the copies of the ingested bytes [0, upto) have completed (their host buffers
+ * may then be reused: a pinned staging ring) */
+int vcfxg_ingest_wait(vcfxg_ctx *ctx, size_t upto);
+/* page-locked host memory (H2D at the full PCIe rate, asynchronous), for staging rings */
+int vcfxg_host_alloc(vcfxg_ctx *ctx, size_t n, void **out);
+void vcfxg_host_free(vcfxg_ctx *ctx, void *p);
 /* device copy of the loaded input (read-only view; valid until the next load) */
 const void *vcfxg_input_device_ptr(vcfxg_ctx *ctx);
 

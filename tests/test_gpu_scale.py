@@ -1,0 +1,171 @@
+"""Parity at BASELINE scale (configs 2, 3 and 5 at their full sizes).
+
+The drop-in binaries run on the deterministic synthetic inputs of BASELINE.json (427,409 x
+2,504 chr21-like and annotated shards, LD at N = 2,504 over complete and knocked-out
+256-variant groups, the first 3,000 variants of the bench's LD shard) and their stdout must
+hash to the digests the REFERENCE binaries produced on the same bytes
+(tests/golden/full_digests.json, made by tests/golden/make_full_digests.py, where the C
+oracle was checked against the reference on the same inputs).  These exercise what the
+small cases cannot: walker line capacity at 32 K walkers, the compaction, the text
+re-format path, the streaming stdin ingest (pipes of > 128 MiB), the FP4 LD ring wrapping
+over 20 k-slices across many tiles.  The region API's kept-record bitmaps (the bench's own
+calls) are checked against the reference's kept records as well.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from tests._golden import GOLDEN
+from vcfx_amd import engine, synth, tool_binary
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+with open(os.path.join(GOLDEN, "full_digests.json")) as _f:
+    DIG = json.load(_f)
+
+
+class Inputs:
+    """Synthetic inputs written once per module to a temp dir (page-cache warm)."""
+
+    def __init__(self):
+        self.dir = tempfile.mkdtemp(prefix="vcfx_scale_")
+        self.files = {}
+
+    def path(self, name):
+        if name not in self.files:
+            arr = synth.generate_array(**DIG["inputs"][name])
+            p = os.path.join(self.dir, name + ".vcf")
+            arr.tofile(p)
+            self.files[name] = (p, arr)
+        return self.files[name][0]
+
+    def array(self, name):
+        self.path(name)
+        return self.files[name][1]
+
+    def drop(self, name):
+        if name in self.files:
+            os.unlink(self.files.pop(name)[0])
+
+    def close(self):
+        for n in list(self.files):
+            self.drop(n)
+        os.rmdir(self.dir)
+
+
+@pytest.fixture(scope="module")
+def inputs():
+    i = Inputs()
+    yield i
+    i.close()
+
+
+def _hash_cmd(cmd, stdin_path=None):
+    """Run a shell pipeline; sha256/len/lines of its stdout, streamed (outputs reach ~4 GB)."""
+    h = hashlib.sha256()
+    n = lines = 0
+    fin = open(stdin_path, "rb") if stdin_path else subprocess.DEVNULL
+    try:
+        p = subprocess.Popen(["bash", "-o", "pipefail", "-c", cmd], stdin=fin, stdout=subprocess.PIPE,
+                             stderr=subprocess.PIPE)
+        while True:
+            b = p.stdout.read(1 << 24)
+            if not b:
+                break
+            h.update(b)
+            n += len(b)
+            lines += b.count(b"\n")
+        err = p.stderr.read()
+        rc = p.wait(timeout=300)
+    finally:
+        if stdin_path:
+            fin.close()
+    return {"sha256": h.hexdigest(), "len": n, "lines": lines}, rc, err
+
+
+def _cmd(stages, path):
+    parts = []
+    for st in stages:
+        argv = [tool_binary(st[0])] + [a.replace("{F}", path) for a in st[1:]]
+        parts.append(" ".join("'%s'" % a for a in argv))
+    return " | ".join(parts)
+
+
+def _check(case, inputs, stdin="none"):
+    c = DIG["cases"][case]
+    path = inputs.path(c["input"])
+    cmd = _cmd(c["stages"], path)
+    stdin_path = None
+    first_reads_stdin = not any("{F}" in a for a in c["stages"][0])
+    if first_reads_stdin:
+        if stdin == "pipe":
+            cmd = "cat '%s' | %s" % (path, cmd)   # a pipe: the streaming ingest path
+        else:
+            stdin_path = path                     # `< file`: the mapped stdin path
+    got, rc, err = _hash_cmd(cmd, stdin_path)
+    assert rc == 0, err[-2000:]
+    assert got == c["stdout"], (case, got, c["stdout"], err[-2000:])
+
+
+@pytest.mark.parametrize("case,stdin", [("af_file", "none"), ("af_stdin", "pipe"), ("af_stdin", "file"),
+                                        ("nonref_file", "none"), ("pipeline_bench", "none")])
+def test_chr21_shard_matches_reference(inputs, case, stdin):
+    _check(case, inputs, stdin)
+
+
+@pytest.mark.parametrize("case", ["pipeline_annot", "gq_strict_annot"])
+def test_annotated_shard_matches_reference(inputs, case):
+    _check(case, inputs)
+    if case == "gq_strict_annot":
+        inputs.drop("annot")
+
+
+@pytest.mark.parametrize("case", ["ld1500_t02", "ld1500_t0", "ld1500_w300_t0", "ld3000_bench"])
+def test_ld_matches_reference(inputs, case):
+    _check(case, inputs)
+
+
+def _mask_sha(st, n_records):
+    keep = (st == 1).astype(np.uint8)  # VCFXG_LINE_ROW: kept
+    assert keep.size == n_records
+    return hashlib.sha256(np.packbits(keep).tobytes()).hexdigest()
+
+
+def test_region_api_at_full_size(inputs):
+    """The bench's own calls on the full chr21 shard: AF rows text, the fused RF|GQ and the nonref
+    walk's per-record decisions against the reference's outputs."""
+    arr = inputs.array("chr21")
+    n_rec = DIG["inputs"]["chr21"]["n_records"]
+    ds = engine.data_start_of(arr[:1 << 20].tobytes())
+    eng = engine.Engine(0)
+    want_af = DIG["cases"]["af_file"]["stdout"]["sha256"]
+    try:
+        # the streaming ingest on a fresh context: unequal chunks (records cut mid-line), the
+        # device buffer grown from nothing
+        cuts = [0, 1000, 77 << 20, 1 << 30, arr.size]
+        eng.ingest([arr[a:b] for a, b in zip(cuts, cuts[1:])])
+        s = eng.allele_freq_region(ds, engine.MODE_FILE)
+        text = b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes)
+        assert hashlib.sha256(text).hexdigest() == want_af
+        eng.load(arr)
+        s = eng.allele_freq_region(ds, engine.MODE_FILE)
+        assert s.rows == n_rec and s.general_records == 0
+        text = b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes)
+        assert hashlib.sha256(text).hexdigest() == want_af
+        crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
+        s = eng.filter_query_region(ds, crits, "0|1", and_logic=True, strict=False)
+        assert s.n_lines == n_rec
+        c = DIG["cases"]["pipeline_bench"]
+        assert s.rows == c["kept"]
+        assert _mask_sha(eng.statuses(s.n_lines), n_rec) == c["keep_mask_sha256"]
+        s = eng.nonref_filter_region(ds, engine.MODE_FILE)
+        c = DIG["cases"]["nonref_file"]
+        assert s.rows == c["kept"]
+        assert _mask_sha(eng.statuses(s.n_lines), n_rec) == c["keep_mask_sha256"]
+    finally:
+        eng.close()

@@ -39,6 +39,11 @@ struct vcfxg_ctx {
     size_t n = 0;
     int last_byte = -1;  // input[n-1] (host copy), -1 if empty
     bool loaded = false;
+    bool ingesting = false;               // between vcfxg_ingest_begin and the final chunk
+    const char *ingest_first = nullptr;   // the first ingested chunk (load-time hints)
+    size_t ingest_first_n = 0;
+    std::vector<std::pair<size_t, hipEvent_t>> ingest_ev;  // (input bytes copied once it fires, event)
+    std::vector<hipEvent_t> ingest_ev_free;
     // index
     DevBuf idx_counts, idx_offs, idx_pos, line_end, d_nlines, scan_tmp;
     size_t data_start = 0;
@@ -219,6 +224,8 @@ void vcfxg_close(vcfxg_ctx *c) {
                       &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->st_le, &c->st_alt, &c->st_tot, &c->st_rowpre, &c->st_status, &c->st_meta, &c->st_bcount, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs})
         if (b->p) (void)hipFree(b->p);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
+    for (hipEvent_t e : c->ingest_ev_free) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
     if (c->pipe_done) (void)hipEventDestroy(c->pipe_done);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
@@ -297,18 +304,96 @@ static void load_hints(vcfxg_ctx *c, const char *h, size_t n) {
 
 int vcfxg_load_host(vcfxg_ctx *c, const char *host, size_t n) {
     if (!c || (!host && n)) return VCFXG_E_ARG;
+    int r = vcfxg_ingest_begin(c, n);
+    if (!r) r = vcfxg_ingest(c, host, n, 1);
+    return r;
+}
+
+int vcfxg_ingest_begin(vcfxg_ctx *c, size_t size_hint) {
+    if (!c) return VCFXG_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    int r = ensure(c, c->input, n + kPad);
+    int r = ensure(c, c->input, size_hint + kPad);
     if (r) return r;
-    if (n) HIPCHK(c, hipMemcpyAsync(c->input.p, host, n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(static_cast<char *>(c->input.p) + n, 0, kPad, c->stream));
+    c->loaded = false;
+    c->indexed = false;
+    c->n = 0;
+    c->ingesting = true;
+    c->ingest_first = nullptr;
+    c->ingest_first_n = 0;
+    return VCFXG_OK;
+}
+
+int vcfxg_ingest(vcfxg_ctx *c, const char *host, size_t n, int is_final_chunk) {
+    if (!c || (!host && n)) return VCFXG_E_ARG;
+    if (!c->ingesting) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->n + n + kPad > c->input.cap) {
+        // grow: a larger buffer, the bytes so far copied on the device
+        size_t nc = std::max(c->input.cap * 2, c->n + n + kPad);
+        void *np = nullptr;
+        HIPCHK(c, hipMalloc(&np, nc));
+        if (c->n) HIPCHK(c, hipMemcpyAsync(np, c->input.p, c->n, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(c->input.p));
+        c->input.p = np;
+        c->input.cap = nc;
+    }
+    // pageable host memory: the runtime's staged DMA runs at the PCIe rate (measured
+    // 50-56 GB/s on MI355X, tools/microbench/h2d_ingest.cpp), asynchronous to the caller
+    // up to its staging depth
+    if (n) HIPCHK(c, hipMemcpyAsync(static_cast<char *>(c->input.p) + c->n, host, n, hipMemcpyHostToDevice, c->stream));
+    if (n && !is_final_chunk) {  // completion marker for vcfxg_ingest_wait
+        hipEvent_t e = nullptr;
+        if (!c->ingest_ev_free.empty()) {
+            e = c->ingest_ev_free.back();
+            c->ingest_ev_free.pop_back();
+        } else {
+            HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        HIPCHK(c, hipEventRecord(e, c->stream));
+        c->ingest_ev.push_back({c->n + n, e});
+    }
+    if (n && !c->ingest_first) {
+        c->ingest_first = host;
+        c->ingest_first_n = n;
+    }
+    c->n += n;
+    if (n) c->last_byte = (unsigned char)host[n - 1];
+    if (!is_final_chunk) return VCFXG_OK;
+    if (!c->n) c->last_byte = -1;
+    HIPCHK(c, hipMemsetAsync(static_cast<char *>(c->input.p) + c->n, 0, kPad, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->n = n;
-    c->last_byte = n ? (unsigned char)host[n - 1] : -1;
-    load_hints(c, host, n);
+    for (auto &pe : c->ingest_ev) c->ingest_ev_free.push_back(pe.second);
+    c->ingest_ev.clear();
+    load_hints(c, c->ingest_first, c->ingest_first_n);
+    c->ingest_first = nullptr;
+    c->ingesting = false;
     c->loaded = true;
     c->indexed = false;
     return VCFXG_OK;
+}
+
+int vcfxg_ingest_wait(vcfxg_ctx *c, size_t upto) {
+    if (!c) return VCFXG_E_ARG;
+    size_t k = 0;
+    while (k < c->ingest_ev.size() && c->ingest_ev[k].first <= upto) k++;
+    if (k == 0) return VCFXG_OK;
+    HIPCHK(c, hipEventSynchronize(c->ingest_ev[k - 1].second));
+    for (size_t i = 0; i < k; i++) c->ingest_ev_free.push_back(c->ingest_ev[i].second);
+    c->ingest_ev.erase(c->ingest_ev.begin(), c->ingest_ev.begin() + (long)k);
+    return VCFXG_OK;
+}
+
+int vcfxg_host_alloc(vcfxg_ctx *c, size_t n, void **out) {
+    if (!c || !out) return VCFXG_E_ARG;
+    *out = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipHostMalloc(out, n ? n : 1, hipHostMallocDefault));
+    return VCFXG_OK;
+}
+
+void vcfxg_host_free(vcfxg_ctx *c, void *p) {
+    if (c && p) (void)hipHostFree(p);
 }
 
 const void *vcfxg_input_device_ptr(vcfxg_ctx *c) { return c && c->loaded ? c->input.p : nullptr; }

@@ -9,12 +9,131 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <mutex>
+#include <thread>
+
+#ifndef MADV_POPULATE_WRITE
+#define MADV_POPULATE_WRITE 23  // Linux 5.14
+#endif
+#ifndef MADV_POPULATE_READ
+#define MADV_POPULATE_READ 22  // Linux 5.14
+#endif
+static constexpr int kMadvPopulateWrite = MADV_POPULATE_WRITE;
+static constexpr int kMadvPopulateRead = MADV_POPULATE_READ;
+
 namespace vcfxh {
 
 const void *memchr_(const char *p, const char *end) { return memchr(p, '\n', (size_t)(end - p)); }
 
+bool g_process_exit_fast = false;
+
+namespace {
+const std::chrono::steady_clock::time_point t_start = std::chrono::steady_clock::now();
+const bool timing_on = getenv("VCFX_TIMING") && atoi(getenv("VCFX_TIMING")) > 0;
+
+// inputs from this size on open the GPU context on a background thread as soon as they are
+// seen, so the HIP runtime start (~0.2 s on MI355X) overlaps reading / mapping the input
+constexpr size_t kPrefetchBytes = (size_t)1 << 20;
+// the pipe path streams to the device in chunks of this size once this much has arrived
+constexpr size_t kStreamChunk = (size_t)64 << 20;
+}  // namespace
+
+void phase(const char *what) {
+    if (!timing_on) return;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    char b[160];
+    int k = snprintf(b, sizeof b, "[vcfx-timing] %s %.2f ms\n", what, ms);
+    if (k > 0) write_all(2, b, (size_t)std::min<int>(k, (int)sizeof b - 1));
+}
+
+// ---- the process-wide device context --------------------------------------------------
+namespace {
+std::mutex g_mu;
+vcfxg_ctx *g_ctx = nullptr;
+bool g_tried = false;
+std::atomic<bool> g_open_done{false};  // the open (successful or not) has finished
+int g_rc = 0;
+int g_dev = 0;
+struct Opener {
+    std::thread t;
+    ~Opener() {
+        if (t.joinable()) t.join();
+    }
+} g_opener;
+
+void open_locked() {
+    if (g_tried) return;
+    g_tried = true;
+    g_dev = 0;
+    if (const char *e = getenv("VCFX_DEVICE")) g_dev = atoi(e);
+    phase("gpu open begin");
+    g_rc = vcfxg_open(g_dev, &g_ctx);
+    phase("gpu open end");
+    if (g_rc != VCFXG_OK) g_ctx = nullptr;
+    g_open_done.store(true, std::memory_order_release);
+}
+
+void join_opener() {
+    std::thread t;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!g_opener.t.joinable() || g_opener.t.get_id() == std::this_thread::get_id()) return;
+        t = std::move(g_opener.t);
+    }
+    t.join();
+}
+}  // namespace
+
+void gpu_join() { join_opener(); }
+
+void gpu_prefetch() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_tried || g_opener.t.joinable()) return;
+    g_opener.t = std::thread([] {
+        std::lock_guard<std::mutex> l2(g_mu);
+        open_locked();
+    });
+}
+
+vcfxg_ctx *gpu_quiet() {
+    join_opener();
+    std::lock_guard<std::mutex> lk(g_mu);
+    open_locked();
+    return g_ctx;
+}
+
+vcfxg_ctx *gpu(int err_fd) {
+    vcfxg_ctx *c = gpu_quiet();
+    if (!c)
+        write_str(err_fd, std::string("Error: vcfx_amd: no usable MI355X (gfx950) device ") + std::to_string(g_dev) +
+                              " (vcfxg_open rc=" + std::to_string(g_rc) + "); this build has no CPU path.\n");
+    return c;
+}
+
+bool gpu_ok(vcfxg_ctx *c, int rc, const char *what, int err_fd) {
+    if (rc == VCFXG_OK) return true;
+    write_str(err_fd, std::string("Error: vcfx_amd: ") + what + " failed (rc=" + std::to_string(rc) + "): " +
+                          vcfxg_last_error(c) + "\n");
+    return false;
+}
+
+// ---- input ----------------------------------------------------------------------------
+void Input::join_populate() const {
+    for (auto &t : populating) t.join();
+    populating.clear();
+}
+
 Input::~Input() {
-    if (mapped && p && n) munmap(const_cast<char *>(p), n);
+    join_populate();
+    if (g_process_exit_fast) return;  // the process ends next: let exit() drop the mappings
+    if (ring_ctx)
+        for (void *r : ring) vcfxg_host_free(ring_ctx, r);
+    if (map_base && map_len) munmap(map_base, map_len);
 }
 
 bool Input::open_file(const char *path) {
@@ -25,39 +144,257 @@ bool Input::open_file(const char *path) {
         ::close(fd);
         return false;
     }
-    n = (size_t)st.st_size;
+    n = host_n = (size_t)st.st_size;
     if (n == 0) {
         ::close(fd);
         p = "";
         return true;
     }
+    if (n >= kPrefetchBytes) gpu_prefetch();
     void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
     ::close(fd);
     if (m == MAP_FAILED) {
-        n = 0;
+        n = host_n = 0;
         return false;
     }
-    madvise(m, n, MADV_SEQUENTIAL | MADV_WILLNEED);
+    // the reference's advice (MappedFile, VCFX_allele_freq_calc.cpp:52-63); a large input is
+    // populated by helper threads instead of read-ahead (WILLNEED walks every cached page
+    // on this thread first: ~30 ms at 4 GB)
+    madvise(m, n, n < ((size_t)64 << 20) ? (MADV_SEQUENTIAL | MADV_WILLNEED) : MADV_SEQUENTIAL);
     p = (const char *)m;
     mapped = true;
+    map_base = m;
+    map_len = n;
+    populate(m, n);
     return true;
 }
 
-void Input::read_fd(int fd) {
-    heap.clear();
-    size_t cap = 1 << 20;
-    heap.resize(cap);
+// map a large input's page-cache pages into the page table on a few threads, while the
+// context opens: the H2D copy then runs without page faults (load_input joins them)
+void Input::populate(void *m, size_t len) {
+    if (len < ((size_t)64 << 20)) return;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int T = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
+    const size_t kStripe = (size_t)32 << 20;
+    for (int t = 0; t < T; t++)
+        populating.emplace_back([=] {
+            for (size_t o = (size_t)t * kStripe; o < len; o += (size_t)T * kStripe)
+                if (madvise((char *)m + o, std::min(kStripe, len - o), kMadvPopulateRead) != 0) return;
+        });
+}
+
+namespace {
+// true when [p, p+n) holds a complete line starting with "#CHROM" (the '#CHROM' gate of
+// every tool ends there)
+bool has_chrom_line(const char *p, size_t n) {
+    const char *s = p, *e = p + n;
+    while (s < e) {
+        const char *nl = (const char *)memchr(s, '\n', (size_t)(e - s));
+        if (!nl) return false;
+        if (is_chrom_line(s, (size_t)(nl - s))) return true;
+        s = nl + 1;
+    }
+    return false;
+}
+
+ssize_t read_full(int fd, char *dst, size_t want) {
     size_t got = 0;
+    while (got < want) {
+        ssize_t k = ::read(fd, dst + got, want - got);
+        if (k < 0 && errno == EINTR) continue;
+        if (k < 0) return got ? (ssize_t)got : -1;
+        if (k == 0) break;
+        got += (size_t)k;
+    }
+    return (ssize_t)got;
+}
+}  // namespace
+
+void Input::read_fd(int fd, bool host_copy) {
+    p = "";
+    n = host_n = 0;
+    struct stat st;
+    if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+        // `< file`: map the rest of the file (the bytes a read loop would return)
+        off_t pos = lseek(fd, 0, SEEK_CUR);
+        if (pos >= 0 && (off_t)st.st_size > pos) {
+            const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+            const size_t lo = (size_t)pos & ~(pg - 1);
+            const size_t len = (size_t)st.st_size - lo;
+            if ((size_t)st.st_size - (size_t)pos >= kPrefetchBytes) gpu_prefetch();
+            void *m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, (off_t)lo);
+            if (m != MAP_FAILED) {
+                madvise(m, len, len < ((size_t)64 << 20) ? (MADV_SEQUENTIAL | MADV_WILLNEED) : MADV_SEQUENTIAL);
+                populate(m, len);
+                map_base = m;
+                map_len = len;
+                p = (const char *)m + ((size_t)pos - lo);
+                n = host_n = (size_t)st.st_size - (size_t)pos;
+                lseek(fd, st.st_size, SEEK_SET);  // consumed, as by a read loop
+                return;
+            }
+        } else if (pos >= 0) {
+            return;  // at EOF
+        }
+    }
+#ifdef F_SETPIPE_SZ
+    if (fcntl(fd, F_GETPIPE_SZ) > 0) (void)fcntl(fd, F_SETPIPE_SZ, 1 << 20);  // fewer, larger reads
+#endif
+    // reserved address space (not memory): the bytes never move, so chunks already handed
+    // to the device copy stay valid while the read continues
+    size_t cap = 0;
+    void *m = MAP_FAILED;
+    for (int sh : {40, 36, 32, 30}) {
+        cap = (size_t)1 << sh;
+        m = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+        if (m != MAP_FAILED) break;
+    }
+    if (m == MAP_FAILED) return;
+    madvise(m, cap, MADV_HUGEPAGE);
+    char *const base = (char *)m;
+    map_base = m;
+    map_len = cap;
+    p = base;
+
+    // the head of the stream (up to 2 chunks) always lands in host memory: the '#CHROM' gate
+    // runs on it, and small inputs never reach the device
+    ssize_t k0 = read_full(fd, base, kPrefetchBytes);
+    size_t got = k0 > 0 ? (size_t)k0 : 0;
+    if (got == kPrefetchBytes) {
+        gpu_prefetch();  // a large input: the HIP runtime starts while the rest arrives
+        // the head keeps arriving into host memory while the context opens (a read that
+        // waited for the open would stall the writer for ~0.2 s)
+        for (;;) {
+            const bool enough = got >= 2 * kStreamChunk;
+            if (enough && (host_copy || g_open_done.load(std::memory_order_acquire))) break;
+            if (got >= ((size_t)8 << 30) || cap - got < ((size_t)8 << 20)) break;
+            ssize_t k = ::read(fd, base + got, (size_t)8 << 20);
+            if (k < 0 && errno == EINTR) continue;
+            if (k <= 0) {
+                n = host_n = got;
+                return;  // EOF: everything is on the host
+            }
+            got += (size_t)k;
+        }
+    }
+    if (got < 2 * kStreamChunk) {
+        n = host_n = got;
+        return;
+    }
+    if (!host_copy && has_chrom_line(base, got)) {
+        // the caller needs only the header on the host (VCFX_allele_freq_calc): the rest goes
+        // straight to the device through a pinned staging ring -- no host copy, no page faults
+        vcfxg_ctx *g = gpu_quiet();
+        if (g && vcfxg_ingest_begin(g, (size_t)1 << 30) == VCFXG_OK && vcfxg_ingest(g, base, got, 0) == VCFXG_OK) {
+            host_n = got;
+            stream_ctx = g;
+            ring_ctx = g;
+            constexpr int kSlots = 4;
+            constexpr size_t kSlot = (size_t)32 << 20;
+            bool ok = true;
+            for (int i = 0; i < kSlots && ok; i++) {
+                void *r = nullptr;
+                ok = vcfxg_host_alloc(g, kSlot, &r) == VCFXG_OK;
+                if (ok) ring.push_back(r);
+            }
+            size_t total = got;
+            std::vector<size_t> slot_end(kSlots, 0);  // input offset where the slot's last chunk ended
+            for (int k = 0; ok; k = (k + 1) % kSlots) {
+                ok = vcfxg_ingest_wait(g, slot_end[k]) == VCFXG_OK;
+                if (!ok) break;
+                ssize_t r = read_full(fd, (char *)ring[k], kSlot);
+                if (r <= 0) break;
+                ok = vcfxg_ingest(g, (const char *)ring[k], (size_t)r, 0) == VCFXG_OK;
+                total += (size_t)r;
+                slot_end[k] = total;
+                if ((size_t)r < kSlot) break;
+            }
+            n = total;
+            streamed = ok ? total : 0;  // a failure is reported when the input is used
+            phase("stdin streamed to the device");
+            return;
+        }
+    }
+    n = host_n = got;
+
+    // a helper thread faults the region in ahead of the reader (on another core), so read()
+    // lands on populated pages; without MADV_POPULATE_WRITE (Linux < 5.14) it just stops
+    std::atomic<size_t> rd{got};
+    std::atomic<bool> done{false};
+    const size_t kStep = (size_t)32 << 20, kAhead = (size_t)256 << 20;
+    std::thread pre([&] {
+        size_t pop = got;
+        while (!done.load(std::memory_order_acquire)) {
+            if (pop < rd.load(std::memory_order_acquire) + kAhead && pop + kStep <= cap) {
+                if (madvise(base + pop, kStep, kMadvPopulateWrite) != 0) return;
+                pop += kStep;
+            } else {
+                std::this_thread::sleep_for(std::chrono::microseconds(50));
+            }
+        }
+    });
+    // device ingest of complete chunks on its own thread, overlapping the pipe read (the
+    // context comes from the background open; a failed open here is silent)
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t avail = got;  // bytes read so far, published to the ingest thread
+    bool eof = false;
+    std::thread ing([&] {
+        vcfxg_ctx *g = gpu_quiet();
+        if (!g) return;
+        size_t at = 0;
+        bool ok = vcfxg_ingest_begin(g, (size_t)1 << 30) == VCFXG_OK;
+        for (;;) {
+            size_t upto;
+            bool fin;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return eof || avail - at >= kStreamChunk; });
+                fin = eof;
+                upto = fin ? avail : at + (avail - at) / kStreamChunk * kStreamChunk;
+            }
+            if (ok && upto > at) ok = vcfxg_ingest(g, base + at, upto - at, 0) == VCFXG_OK;
+            at = upto;
+            if (fin) break;
+        }
+        stream_ctx = g;
+        streamed = ok ? at : 0;
+    });
     for (;;) {
-        if (got == heap.size()) heap.resize(heap.size() * 2);
-        ssize_t k = ::read(fd, &heap[got], heap.size() - got);
+        if (cap - got < ((size_t)8 << 20)) break;  // reservation exhausted (> 1 TiB of stdin)
+        ssize_t k = ::read(fd, base + got, (size_t)8 << 20);
         if (k < 0 && errno == EINTR) continue;
         if (k <= 0) break;
         got += (size_t)k;
+        rd.store(got, std::memory_order_release);
+        std::lock_guard<std::mutex> lk(mu);
+        avail = got;
+        cv.notify_one();
     }
-    heap.resize(got);
-    p = heap.data();
-    n = got;
+    done.store(true, std::memory_order_release);
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        avail = got;
+        eof = true;
+        cv.notify_one();
+    }
+    ing.join();
+    pre.join();
+    n = host_n = got;
+}
+
+bool load_input(vcfxg_ctx *g, const Input &in, int err_fd) {
+    in.join_populate();
+    if (in.stream_ctx == g && in.streamed == in.n) {
+        // the bytes are on the device already (streamed while stdin was read); complete it
+        return gpu_ok(g, vcfxg_ingest(g, nullptr, 0, 1), "ingest", err_fd);
+    }
+    if (in.host_n != in.n) {  // a device-only stream whose ingest failed: nothing to redo
+        write_str(err_fd, "Error: vcfx_amd: streaming stdin to the device failed: " +
+                              std::string(vcfxg_last_error(in.stream_ctx ? in.stream_ctx : g)) + "\n");
+        return false;
+    }
+    return gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err_fd);
 }
 
 void write_all(int fd, const char *p, size_t n) {
@@ -68,28 +405,6 @@ void write_all(int fd, const char *p, size_t n) {
         p += k;
         n -= (size_t)k;
     }
-}
-
-static vcfxg_ctx *g_ctx = nullptr;
-
-vcfxg_ctx *gpu(int err_fd) {
-    if (g_ctx) return g_ctx;
-    int dev = 0;
-    if (const char *e = getenv("VCFX_DEVICE")) dev = atoi(e);
-    int rc = vcfxg_open(dev, &g_ctx);
-    if (rc != VCFXG_OK) {
-        write_str(err_fd, std::string("Error: vcfx_amd: no usable MI355X (gfx950) device ") + std::to_string(dev) +
-                              " (vcfxg_open rc=" + std::to_string(rc) + "); this build has no CPU path.\n");
-        g_ctx = nullptr;
-    }
-    return g_ctx;
-}
-
-bool gpu_ok(vcfxg_ctx *c, int rc, const char *what, int err_fd) {
-    if (rc == VCFXG_OK) return true;
-    write_str(err_fd, std::string("Error: vcfx_amd: ") + what + " failed (rc=" + std::to_string(rc) + "): " +
-                          vcfxg_last_error(c) + "\n");
-    return false;
 }
 
 }  // namespace vcfxh

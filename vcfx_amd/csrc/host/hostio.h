@@ -8,22 +8,58 @@
 #include <string.h>
 
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "vcfx_gpu.h"
 
 namespace vcfxh {
 
 struct Input {
+    // the input bytes [p, p + host_n) on the host; n = all input bytes.  host_n < n only for
+    // a stdin pipe read with host_copy = false: the bytes past the header then exist only on
+    // the device (already ingested; see load_input).
     const char *p = nullptr;
     size_t n = 0;
+    size_t host_n = 0;
     bool mapped = false;
-    std::string heap;  // stdin bytes
+    // mapping to release: [map_base, map_base + map_len)
+    void *map_base = nullptr;
+    size_t map_len = 0;
+    // pipe path: bytes [0, streamed) were appended to stream_ctx's device input while stdin
+    // was read (vcfxg_ingest, final chunk outstanding); see load_input
+    vcfxg_ctx *stream_ctx = nullptr;
+    size_t streamed = 0;
+    std::vector<void *> ring;  // pinned staging slots of a device-only stream (freed with ring_ctx)
+    vcfxg_ctx *ring_ctx = nullptr;
+    Input() = default;
+    Input(const Input &) = delete;
+    Input &operator=(const Input &) = delete;
     ~Input();
     // MappedFile::open semantics (VCFX_allele_freq_calc.cpp:52-63): false if open/stat
-    // fails; a 0-byte file is a successful empty map.
+    // fails; a 0-byte file is a successful empty map.  Inputs of 1 MiB and more start the
+    // GPU context opening on a background thread (gpu_prefetch).
     bool open_file(const char *path);
-    void read_fd(int fd);
+    // All of fd's remaining bytes (the stream path's input).  A regular file (`< file`) is
+    // mapped from the current offset, with no copy.  A pipe is read into a reserved,
+    // transparently-huge-page region that a helper thread pre-faults ahead of the reader,
+    // while a second thread streams each complete 64 MiB to the device (vcfxg_ingest): the
+    // H2D copy overlaps the read.  host_copy = false (a tool that needs only the header on
+    // the host): once the head holds the '#CHROM' line the rest of the pipe is read into a
+    // pinned staging ring and copied to the device from there, never kept on the host.
+    void read_fd(int fd, bool host_copy = true);
+    // mapped inputs of 64 MiB and more: page-table population running on helper threads
+    mutable std::vector<std::thread> populating;
+    void populate(void *m, size_t len);
+    void join_populate() const;
 };
+
+// VCFX_TIMING=1 in the environment: "[vcfx-timing] <what> <ms since process start>" on
+// stderr (fd 2) at each phase of a tool run -- e2e breakdowns; silent otherwise.
+void phase(const char *what);
+// set by the drop-in executables (binary_main.cpp): the process exits right after the tool
+// returns, so inputs skip unmapping (the kernel drops the mappings at exit anyway)
+extern bool g_process_exit_fast;
 
 void write_all(int fd, const char *p, size_t n);
 inline void write_str(int fd, const std::string &s) { write_all(fd, s.data(), s.size()); }
@@ -50,8 +86,18 @@ struct Out {
 // The process-wide device context (device 0, or $VCFX_DEVICE).  On failure prints
 // "Error: vcfx_amd: ..." to err_fd and returns nullptr -- there is no CPU fallback.
 vcfxg_ctx *gpu(int err_fd);
+// start opening that context on a background thread (the HIP runtime start then overlaps
+// the caller's input reading); gpu() / gpu_quiet() wait for it
+void gpu_prefetch();
+// wait for a background open started by gpu_prefetch (before the process ends)
+void gpu_join();
+// the same context, opened without a diagnostic (nullptr when there is no device)
+vcfxg_ctx *gpu_quiet();
 // run a vcfxg_* call; on failure prints the context error and returns false
 bool gpu_ok(vcfxg_ctx *c, int rc, const char *what, int err_fd);
+// make in's bytes the device-resident input of g: completes the ingest started while stdin
+// was read, or copies the whole input (vcfxg_load_host)
+bool load_input(vcfxg_ctx *g, const Input &in, int err_fd);
 
 const void *memchr_(const char *p, const char *end);
 

@@ -46,7 +46,8 @@ bool run_af(const Input &in, int mode, bool quiet, Out &out, Out &err, uint64_t 
     out.put("CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n");
     *variants = *datalines = 0;
     // '#CHROM' gate (processMmap :366-386 / processStdin :489-502) over the header prefix
-    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    // (for a device-only stdin stream the host holds the header part: host_n <= n)
+    const char *p = in.p, *end = in.p + in.host_n, *ls, *le;
     size_t data_start = in.n;
     while (next_line(p, end, ls, le)) {
         const char *ae = le;
@@ -61,15 +62,19 @@ bool run_af(const Input &in, int mode, bool quiet, Out &out, Out &err, uint64_t 
         }
         if (!quiet) err.put(kWarnPre);
     }
+    phase("header gate");
     if (data_start >= in.n) return true;
     vcfxg_ctx *g = gpu(err.fd);
     if (!g) return false;
     err.flush();
-    if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd)) return false;
+    if (!load_input(g, in, err.fd)) return false;
+    phase("input resident in HBM");
     vcfxg_summary s;  // index + counts + rows in one device sweep
     if (!gpu_ok(g, vcfxg_allele_freq_region(g, data_start, mode, &s), "allele_freq", err.fd)) return false;
+    phase("allele_freq_region");
     std::string text(s.text_bytes, '\0');
     if (!gpu_ok(g, vcfxg_fetch_text(g, &text[0], text.size()), "fetch", err.fd)) return false;
+    phase("rows fetched");
     out.put(text);
     if (!quiet)
         for (uint64_t k = 0; k < s.warn_lines; k++) err.put(kWarnFields);
@@ -106,6 +111,7 @@ extern "C" int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int 
     Input in;
     uint64_t v = 0, l = 0;
     if (input) {
+        phase("start");
         if (!in.open_file(input)) {
             err.put(std::string("Error: Cannot open file: ") + input + "\n");
             return 1;
@@ -114,7 +120,9 @@ extern "C" int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int 
         if (!run_af(in, VCFXG_MODE_FILE, quiet, out, err, &v, &l)) return 1;
         if (!quiet) err.put("Processed " + std::to_string(v) + " variants from " + std::to_string(l) + " data lines\n");
     } else {
-        in.read_fd(in_fd);
+        phase("start");
+        in.read_fd(in_fd, /*host_copy=*/false);  // only the header is needed on the host
+        phase("stdin read");
         if (in.n == 0) {
             out.put(kHelp);
             return 1;

@@ -82,7 +82,7 @@ bool run_gq(const Input &in, bool stream_mode, const std::string &q, bool strict
         if (!g) return false;
         uint64_t nl = 0;
         vcfxg_summary s;
-        if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
+        if (!load_input(g, in, err.fd) ||
             !gpu_ok(g, vcfxg_genotype_query_region(g, data_start, q.data(), q.size(), strict ? 1 : 0, 0, &s),
                     "genotype_query", err.fd))
             return false;
@@ -173,6 +173,7 @@ extern "C" int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int ou
         return run_gq(in, false, query, strict, quiet, out_fd, err) ? 0 : 1;
     }
     in.read_fd(in_fd);
+    phase("stdin read");
     out.flush();
     return run_gq(in, true, query, strict, quiet, out_fd, err) ? 0 : 1;
 }

@@ -129,7 +129,7 @@ bool run_stream(const Input &in, bool mmap_mode, const LdOpts &o, const std::str
     vcfxg_ctx *g = gpu(err.fd);
     if (!g) return false;
     uint64_t nl = 0, M = 0;
-    if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
+    if (!load_input(g, in, err.fd) ||
         !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
         !gpu_ok(g, vcfxg_ld_prepare(g, ns, 1, rchrom.data(), rchrom.size(), has_region ? 1 : 0, rs, re, 0, &M),
                 "ld_prepare", err.fd))

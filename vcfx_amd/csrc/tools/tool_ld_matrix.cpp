@@ -47,7 +47,7 @@ bool run_ld_matrix(const Input &in, bool mmap_mode, bool quiet, const std::strin
         g = gpu(err.fd);
         if (!g) return false;
         uint64_t nl = 0;
-        if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
+        if (!load_input(g, in, err.fd) ||
             !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
             !gpu_ok(g,
                     vcfxg_ld_prepare(g, ns, 0, rchrom.data(), rchrom.size(), has_region ? 1 : 0, rs, re,

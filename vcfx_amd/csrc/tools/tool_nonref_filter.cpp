@@ -79,7 +79,7 @@ bool run_nr(const Input &in, bool stream_mode, int out_fd, Out &err) {
         if (!g) return false;
         uint64_t nl = 0;
         vcfxg_summary s;
-        if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
+        if (!load_input(g, in, err.fd) ||
             !gpu_ok(g, vcfxg_nonref_filter_region(g, data_start, stream_mode ? VCFXG_MODE_STDIN : VCFXG_MODE_FILE, &s),
                     "nonref_filter", err.fd))
             return false;
@@ -146,6 +146,7 @@ extern "C" int vcfx_tool_nonref_filter(int argc, char **argv, int in_fd, int out
         return run_nr(in, false, out_fd, err) ? 0 : 1;
     }
     in.read_fd(in_fd);
+    phase("stdin read");
     out.flush();
     return run_nr(in, true, out_fd, err) ? 0 : 1;
 }

@@ -62,7 +62,7 @@ extern "C" int vcfx_pipeline_filter_query(const char *filter, const char *logic,
         uint64_t nl = 0;
         vcfxg_summary s;
         std::vector<vcfxg_criterion> abi = to_abi(cs);
-        if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
+        if (!load_input(g, in, err.fd) ||
             !gpu_ok(g,
                     vcfxg_filter_query_region(g, data_start, abi.data(), (int)abi.size(), and_logic ? 1 : 0, query,
                                               strlen(query), strict, &s),

@@ -151,10 +151,11 @@ bool run_rf(const Input &in, bool stdin_mode, const std::vector<Criterion> &cs, 
     uint64_t nl = 0;
     vcfxg_summary s;
     std::vector<vcfxg_criterion> abi = to_abi(cs);
-    if (!gpu_ok(g, vcfxg_load_host(g, in.p, in.n), "load", err.fd) ||
+    if (!load_input(g, in, err.fd) ||
         !gpu_ok(g, vcfxg_record_filter_region(g, data_start, abi.data(), (int)abi.size(), and_logic ? 1 : 0, &s),
                 "record_filter", err.fd))
         return false;
+    phase("record_filter_region");
     nl = s.n_lines;
     std::vector<uint64_t> ends(nl);
     std::vector<uint8_t> st(nl);
@@ -169,6 +170,7 @@ bool run_rf(const Input &in, bool stdin_mode, const std::vector<Criterion> &cs, 
         else if (st[i] == VCFXG_LINE_ROW || st[i] == VCFXG_LINE_HEADER) em.line(a, strip(a, b));
     }
     em.finish();
+    phase("records written");
     return true;
 }
 
@@ -239,5 +241,6 @@ extern "C" int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out
         return run_rf(in, false, cs, and_logic, out_fd, err) ? 0 : 1;
     }
     in.read_fd(in_fd);
+    phase("stdin read");
     return run_rf(in, true, cs, and_logic, out_fd, err) ? 0 : 1;
 }

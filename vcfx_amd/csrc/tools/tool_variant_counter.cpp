@@ -64,7 +64,7 @@ long count_lines(const char *p, size_t n, bool strip_cr, bool strict, Out &err) 
 
 // countVariantsGzip's decode: bytes whose lines the reference processes, and whether the
 // stream failed (then only complete lines count and the error follows their warnings)
-bool gunzip_like_reference(const std::string &in, std::string &out, bool &failed) {
+bool gunzip_like_reference(const char *in_p, size_t in_n, std::string &out, bool &failed) {
     const size_t CHUNK = 65536;
     z_stream st;
     memset(&st, 0, sizeof st);
@@ -74,9 +74,9 @@ bool gunzip_like_reference(const std::string &in, std::string &out, bool &failed
     size_t ip = 0;
     int ret = Z_OK;
     do {
-        size_t take = std::min(CHUNK, in.size() - ip);
+        size_t take = std::min(CHUNK, in_n - ip);
         st.avail_in = (uInt)take;
-        st.next_in = (Bytef *)(in.data() + ip);
+        st.next_in = (Bytef *)(in_p + ip);
         ip += take;
         if (take == 0) break;
         do {
@@ -136,7 +136,7 @@ extern "C" int vcfx_tool_variant_counter(int argc, char **argv, int in_fd, int o
         if (in.n >= 2 && (unsigned char)in.p[0] == 0x1f && (unsigned char)in.p[1] == 0x8b) {
             std::string dec;
             bool failed = false;
-            if (!gunzip_like_reference(in.heap, dec, failed)) {
+            if (!gunzip_like_reference(in.p, in.n, dec, failed)) {
                 err.put("Error: inflateInit2 failed.\n");
                 return 1;
             }

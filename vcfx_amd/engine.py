@@ -42,6 +42,11 @@ SIGNATURES = {
     "vcfxg_kernel_stats": (_I, [_VP, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
     "vcfxg_reset_kernel_stats": (_I, [_VP]),
     "vcfxg_load_host": (_I, [_VP, _VP, _S]),
+    "vcfxg_ingest_begin": (_I, [_VP, _S]),
+    "vcfxg_ingest": (_I, [_VP, _VP, _S, _I]),
+    "vcfxg_ingest_wait": (_I, [_VP, _S]),
+    "vcfxg_host_alloc": (_I, [_VP, _S, ctypes.POINTER(_VP)]),
+    "vcfxg_host_free": (None, [_VP, _VP]),
     "vcfxg_input_device_ptr": (_VP, [_VP]),
     "vcfxg_index": (_I, [_VP, _S, ctypes.POINTER(_U64)]),
     "vcfxg_line_ends": (_I, [_VP, _U64, _U64, _VP]),
@@ -142,6 +147,17 @@ class Engine:
         arr = np.frombuffer(data, np.uint8) if not isinstance(data, np.ndarray) else data
         self._buf = arr
         self._chk(self.L.vcfxg_load_host(self.h, arr.ctypes.data, arr.size), "load_host")
+
+    def ingest(self, chunks):
+        """Streaming load: vcfxg_ingest_begin + one vcfxg_ingest per chunk (the last is final)."""
+        import numpy as np
+        arrs = [np.frombuffer(c, np.uint8) if not isinstance(c, np.ndarray) else c for c in chunks]
+        self._buf = arrs
+        self._chk(self.L.vcfxg_ingest_begin(self.h, 0), "ingest_begin")
+        if not arrs:
+            self._chk(self.L.vcfxg_ingest(self.h, None, 0, 1), "ingest")
+        for i, a in enumerate(arrs):
+            self._chk(self.L.vcfxg_ingest(self.h, a.ctypes.data, a.size, int(i == len(arrs) - 1)), "ingest")
 
     def index(self, data_start):
         n = ctypes.c_uint64()
