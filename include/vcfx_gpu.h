@@ -91,6 +91,10 @@ int vcfxg_ingest_wait(vcfxg_ctx *ctx, size_t upto);
 /* page-locked host memory (H2D at the full PCIe rate, asynchronous), for staging rings */
 int vcfxg_host_alloc(vcfxg_ctx *ctx, size_t n, void **out);
 void vcfxg_host_free(vcfxg_ctx *ctx, void *p);
+/* copy input bytes [offset, offset + n) of the loaded input back to host memory (pass-through
+ * tools whose stdin was streamed to the device without a host copy write kept records from
+ * these) */
+int vcfxg_input_fetch(vcfxg_ctx *ctx, uint64_t offset, size_t n, void *host);
 /* device copy of the loaded input (read-only view; valid until the next load) */
 const void *vcfxg_input_device_ptr(vcfxg_ctx *ctx);
 

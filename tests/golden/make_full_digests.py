@@ -62,6 +62,9 @@ CASES = {
     "pipeline_annot": ("annot", [[RF, "--filter", "FILTER==PASS;AF>=0.01", "-i", "{F}"],
                                  [GQ, "-g", "0/1"]], True),
     "gq_strict_annot": ("annot", [[GQ, "-g", "1|1", "--strict", "-i", "{F}"]], True),
+    # the stream (stdin) paths of the pass-through tools: fed through a pipe by the tests
+    "nonref_stdin": ("chr21", [[NR]], True),
+    "rf_stdin_annot": ("annot", [[RF, "--filter", "FILTER==PASS;AF>=0.01"]], True),
     "ld1500_t02": ("ld1500", [[LD, "-q", "-w", "1500", "-t", "0.2", "-i", "{F}"]], False),
     "ld1500_t0": ("ld1500", [[LD, "-q", "-w", "1500", "-t", "0", "-i", "{F}"]], False),
     "ld1500_w300_t0": ("ld1500", [[LD, "-q", "-w", "300", "-t", "0", "-i", "{F}"]], False),

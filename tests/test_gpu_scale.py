@@ -113,14 +113,16 @@ def _check(case, inputs, stdin="none"):
 
 
 @pytest.mark.parametrize("case,stdin", [("af_file", "none"), ("af_stdin", "pipe"), ("af_stdin", "file"),
-                                        ("nonref_file", "none"), ("pipeline_bench", "none")])
+                                        ("nonref_file", "none"), ("pipeline_bench", "none"),
+                                        ("nonref_stdin", "pipe"), ("nonref_stdin", "file")])
 def test_chr21_shard_matches_reference(inputs, case, stdin):
     _check(case, inputs, stdin)
 
 
-@pytest.mark.parametrize("case", ["pipeline_annot", "gq_strict_annot"])
-def test_annotated_shard_matches_reference(inputs, case):
-    _check(case, inputs)
+@pytest.mark.parametrize("case,stdin", [("pipeline_annot", "none"), ("rf_stdin_annot", "pipe"),
+                                        ("gq_strict_annot", "none")])
+def test_annotated_shard_matches_reference(inputs, case, stdin):
+    _check(case, inputs, stdin)
     if case == "gq_strict_annot":
         inputs.drop("annot")
 

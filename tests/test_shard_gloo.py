@@ -1,7 +1,11 @@
 """CPU coverage of the record-sharded multi-GPU path (vcfx_amd/shard.py):
-world_size-2 (and 3) gloo process groups over 127.0.0.1 run the sharded orchestration with
+world_size-2, 3 and 8 gloo process groups over 127.0.0.1 run the sharded orchestration with
 the C oracle standing in for each rank's per-shard GPU run; the merged rank-0 output must
-equal the oracle's whole-file output byte for byte.  The cut logic is checked directly."""
+equal the oracle's whole-file output byte for byte, and every case meant to shard must have
+reached every rank as a view of its own records.  The stand-in runner applies the view the
+tools take from VCFX_INPUT_VIEW (header + record range) by writing it to a file, and the
+VCFX_VIEW_SKIP_HEADER rule by stripping the header-only run's output.  The cut logic and the
+getopt-style operand detection are checked directly."""
 import os
 import socket
 import tempfile
@@ -21,6 +25,33 @@ def _free_port():
     return p
 
 
+def oracle_view_runner(o, calls):
+    """the C oracle as a rank's tool, honouring the shard view like the drop-ins do"""
+    def run(argv, stdin, view=None, skip_header=False):
+        calls.append((list(argv), view, skip_header))
+        if view is None:
+            return o.run(argv, stdin)
+        tool = os.path.basename(argv[0])
+        path = shard.input_path(tool, argv)
+        with open(path, "rb") as f:
+            data = f.read()
+        h, lo, hi = view
+        with tempfile.NamedTemporaryFile(suffix=".vcf") as fv, tempfile.NamedTemporaryFile(suffix=".vcf") as fh:
+            fv.write(data[:h] + data[lo:hi])
+            fv.flush()
+            out, err, rc = o.run([fv.name if a == path else a for a in argv], stdin)
+            if skip_header:
+                fh.write(data[:h])
+                fh.flush()
+                H, E, _ = o.run([fh.name if a == path else a for a in argv], stdin)
+                assert out.startswith(H)
+                out = out[len(H):]
+                if err.startswith(E):
+                    err = err[len(E):]
+        return out, err, rc
+    return run
+
+
 def _worker(rank, world, port, cases, q):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -28,9 +59,9 @@ def _worker(rank, world, port, cases, q):
     o = Oracle()
     try:
         for argv in cases:
-            res = shard.run_sharded(argv, b"", dist, runner=lambda a, stdin: o.run(a, stdin))
-            if rank == 0:
-                q.put((argv, res))
+            calls = []
+            res = shard.run_sharded(argv, b"", dist, runner=oracle_view_runner(o, calls))
+            q.put((rank, argv, res, calls))
     finally:
         dist.destroy_process_group()
 
@@ -43,7 +74,7 @@ def _run_world(world, cases):
     procs = [ctx.Process(target=_worker, args=(r, world, port, cases, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=300) for _ in cases]
+    got = [q.get(timeout=300) for _ in range(len(cases) * world)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
@@ -88,14 +119,35 @@ def _cases(files):
     return cases
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_runs_match_whole_file(files, world):
     cases = _cases(files)
     o = Oracle()
     got = _run_world(world, cases)
-    for argv, (out, err, rc) in got:
-        want = o.run(argv, b"")
-        assert (out, err, rc) == want, (argv, world)
+    views = {}
+    for rank, argv, res, calls in got:
+        views.setdefault(tuple(argv), {})[rank] = calls
+        if rank == 0:
+            want = o.run(argv, b"")
+            assert res == want, (argv, world)
+        else:
+            assert res == (b"", b"", 0)
+    for argv in cases:
+        by_rank = views[tuple(argv)]
+        assert set(by_rank) == set(range(world))
+        meant = shard.plan(argv) in ("af", "vc", "filter") and not (
+            argv[0] in ("VCFX_record_filter", "VCFX_genotype_query", "VCFX_nonref_filter") and "bad" in argv[-1])
+        if not meant:
+            continue
+        # every rank ran its own view (no silent fallback to an unsharded rank-0 run)
+        spans = []
+        for r in range(world):
+            calls = [c for c in by_rank[r] if c[1] is not None]
+            assert len(calls) == 1, (argv, r, by_rank[r])
+            _, (h, lo, hi), skip = calls[0]
+            assert skip == (r > 0) or argv[0] == "VCFX_variant_counter"
+            spans.append((lo, hi))
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))  # contiguous, in rank order
 
 
 def test_record_cuts_cover_region_at_line_starts():
@@ -120,4 +172,26 @@ def test_record_cuts_cover_region_at_line_starts():
 def test_single_process_passthrough(files):
     o = Oracle()
     argv = ["VCFX_allele_freq_calc", "-i", files["synth"]]
-    assert shard.run_sharded(argv, b"", None, runner=lambda a, s: o.run(a, s)) == o.run(argv, b"")
+    assert shard.run_sharded(argv, b"", None, runner=oracle_view_runner(o, [])) == o.run(argv, b"")
+
+
+def test_input_operand_found_like_getopt(files):
+    """option values are never taken for the input operand (`-g 1|1 --strict in.vcf`)"""
+    p = files["synth"]
+    ip = shard.input_path
+    assert ip("VCFX_genotype_query", ["VCFX_genotype_query", "-g", "1|1", "--strict", p]) == p
+    assert ip("VCFX_genotype_query", ["VCFX_genotype_query", "-g", p, "--strict"]) is None  # p is the query
+    assert ip("VCFX_genotype_query", ["VCFX_genotype_query", "--genotype-query=0/1", p]) == p
+    assert ip("VCFX_record_filter", ["VCFX_record_filter", "--filter", p, "-l", "or"]) is None
+    assert ip("VCFX_record_filter", ["VCFX_record_filter", "-fQUAL>1", p]) == p
+    assert ip("VCFX_record_filter", ["VCFX_record_filter", "-f", "QUAL>1", "-i", p]) == p
+    assert ip("VCFX_allele_freq_calc", ["VCFX_allele_freq_calc", "-q", p]) == p
+    assert ip("VCFX_allele_freq_calc", ["VCFX_allele_freq_calc", "-i" + p]) == p
+    assert ip("VCFX_allele_freq_calc", ["VCFX_allele_freq_calc", "--input=" + p]) == p
+    assert ip("VCFX_nonref_filter", ["VCFX_nonref_filter", "--", p]) == p
+    assert ip("VCFX_ld_calculator", ["VCFX_ld_calculator", "-w", "10", p]) is None  # LD takes -i only
+    assert ip("VCFX_ld_calculator", ["VCFX_ld_calculator", "-w", "10", "-i", p]) == p
+    assert ip("VCFX_variant_counter", ["VCFX_variant_counter", "-s", p]) == p
+    assert shard.plan(["VCFX_genotype_query", "-g", "1|1", "--strict", p]) == "filter"
+    assert shard.plan(["VCFX_allele_freq_calc", "-h", p]) is None
+    assert shard.plan(["VCFX_ld_calculator", "-m", "-i", p]) is None

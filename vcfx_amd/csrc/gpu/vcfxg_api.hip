@@ -396,6 +396,17 @@ void vcfxg_host_free(vcfxg_ctx *c, void *p) {
     if (c && p) (void)hipHostFree(p);
 }
 
+int vcfxg_input_fetch(vcfxg_ctx *c, uint64_t offset, size_t n, void *host) {
+    if (!c || (!host && n)) return VCFXG_E_ARG;
+    if (!c->loaded) return VCFXG_E_STATE;
+    if (offset > c->n || n > c->n - offset) return VCFXG_E_ARG;
+    if (!n) return VCFXG_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(host, static_cast<const char *>(c->input.p) + offset, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VCFXG_OK;
+}
+
 const void *vcfxg_input_device_ptr(vcfxg_ctx *c) { return c && c->loaded ? c->input.p : nullptr; }
 
 int vcfxg_index(vcfxg_ctx *c, size_t data_start, uint64_t *n_lines) {

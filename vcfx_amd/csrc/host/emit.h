@@ -38,6 +38,12 @@ struct LineEmitter {
         close_run();
         drain();
     }
+    // write everything pending, then take a new base buffer (a moved input window)
+    void rebase(const char *b, size_t n) {
+        finish();
+        base = b;
+        end = b + n;
+    }
 
    private:
     void extend(const char *s, const char *e) {
@@ -73,6 +79,63 @@ struct LineEmitter {
             }
         }
         iov.clear();
+    }
+};
+
+// Host pointers to the lines of an input's data region, in order, for the pass-through tools.
+// A host-resident input (file mapping, `< file`, a host-copied pipe) is addressed in place.
+// A device-only stdin stream (Input::host_n < n: the bytes past the header were streamed to
+// the device without a host copy) is read back through a pinned window of >= 64 MiB
+// (vcfxg_input_fetch, ~50 GB/s; window_bytes()); the emitter writes out what it holds before the window
+// moves, so every pointer it keeps stays valid.
+struct LineSource {
+    const Input &in;
+    vcfxg_ctx *g;
+    LineEmitter &em;
+    char *win = nullptr;
+    size_t win_cap = 0;
+    uint64_t w0 = 0, w1 = 0;  // window = input bytes [w0, w1)
+    bool ok = true;
+    LineSource(const Input &i, vcfxg_ctx *ctx, LineEmitter &e) : in(i), g(ctx), em(e) {}
+    ~LineSource() {
+        if (!win) return;
+        em.finish();  // the emitter may still point into the window
+        vcfxg_host_free(g, win);
+    }
+    bool device_only() const { return in.host_n < in.n && !in.tail; }
+    bool in_tail = false;
+    // bytes [a, b) of the input, plus the byte at b when b < n (the line's newline)
+    const char *at(uint64_t a, uint64_t b) {
+        if (in.tail && a >= in.host_n) {  // a shard view: the record range elsewhere in the mapping
+            if (!in_tail) {
+                em.rebase(in.tail, in.n - in.host_n);
+                in_tail = true;
+            }
+            return in.tail + (a - in.host_n);
+        }
+        if (!device_only()) return in.p + a;
+        const uint64_t need = std::min<uint64_t>(b + 1, in.n);
+        if (a >= w0 && need <= w1 && win) return win + (a - w0);
+        const size_t want = (size_t)std::max<uint64_t>(window_bytes(), need - a);
+        em.finish();  // the emitter may point into the old window: write it out first
+        if (want > win_cap) {
+            if (win) vcfxg_host_free(g, win);
+            win = nullptr;
+            if (vcfxg_host_alloc(g, want, (void **)&win) != VCFXG_OK) {
+                ok = false;
+                win = nullptr;
+                win_cap = 0;
+                static const char z[1] = {0};
+                return z;
+            }
+            win_cap = want;
+        }
+        const uint64_t e = std::min<uint64_t>(in.n, a + win_cap);
+        if (vcfxg_input_fetch(g, a, (size_t)(e - a), win) != VCFXG_OK) ok = false;
+        w0 = a;
+        w1 = e;
+        em.rebase(win, (size_t)(e - a));
+        return win;
     }
 };
 

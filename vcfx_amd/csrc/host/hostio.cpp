@@ -36,12 +36,25 @@ namespace {
 const std::chrono::steady_clock::time_point t_start = std::chrono::steady_clock::now();
 const bool timing_on = getenv("VCFX_TIMING") && atoi(getenv("VCFX_TIMING")) > 0;
 
-// inputs from this size on open the GPU context on a background thread as soon as they are
-// seen, so the HIP runtime start (~0.2 s on MI355X) overlaps reading / mapping the input
-constexpr size_t kPrefetchBytes = (size_t)1 << 20;
-// the pipe path streams to the device in chunks of this size once this much has arrived
-constexpr size_t kStreamChunk = (size_t)64 << 20;
+size_t env_bytes(const char *name, size_t def) {
+    const char *e = getenv(name);
+    if (!e || !*e) return def;
+    const unsigned long long v = strtoull(e, nullptr, 10);
+    return v ? (size_t)v : def;
+}
 }  // namespace
+
+// Sizes of the input paths.  The environment overrides exist for tests (tiny values push
+// small inputs through the streaming and windowed paths).
+// inputs from prefetch_bytes() on open the GPU context on a background thread as soon as
+// they are seen, so the HIP runtime start (~0.2 s on MI355X) overlaps reading the input
+size_t prefetch_bytes() { return env_bytes("VCFX_PREFETCH_BYTES", (size_t)1 << 20); }
+// the pipe path streams to the device in chunks of this size
+size_t stream_chunk() { return env_bytes("VCFX_STREAM_CHUNK", (size_t)64 << 20); }
+// pinned staging slots of a device-only stream (4 of them)
+size_t ring_slot() { return env_bytes("VCFX_RING_SLOT", (size_t)32 << 20); }
+// the host window through which pass-through tools read a device-only input back
+size_t window_bytes() { return env_bytes("VCFX_WINDOW_BYTES", (size_t)64 << 20); }
 
 void phase(const char *what) {
     if (!timing_on) return;
@@ -150,7 +163,7 @@ bool Input::open_file(const char *path) {
         p = "";
         return true;
     }
-    if (n >= kPrefetchBytes) gpu_prefetch();
+    if (n >= prefetch_bytes()) gpu_prefetch();
     void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
     ::close(fd);
     if (m == MAP_FAILED) {
@@ -165,14 +178,38 @@ bool Input::open_file(const char *path) {
     mapped = true;
     map_base = m;
     map_len = n;
-    populate(m, n);
+    apply_view();
     return true;
+}
+
+bool view_skip_header() {
+    const char *e = getenv("VCFX_VIEW_SKIP_HEADER");
+    return e && atoi(e) > 0;
+}
+
+void Input::apply_view() {
+    const char *v = getenv("VCFX_INPUT_VIEW");
+    unsigned long long h = 0, lo = 0, hi = 0;
+    if (!v || sscanf(v, "%llu:%llu:%llu", &h, &lo, &hi) != 3 || h > lo || lo > hi || hi > n) {
+        populate(map_base, map_len);
+        return;
+    }
+    if (h == 0) {  // no header part: the view is one contiguous range
+        p += lo;
+        n = host_n = (size_t)(hi - lo);
+        populate((void *)p, n);
+        return;
+    }
+    tail = p + lo;
+    host_n = (size_t)h;
+    n = (size_t)(h + (hi - lo));
+    populate((void *)tail, (size_t)(hi - lo));
 }
 
 // map a large input's page-cache pages into the page table on a few threads, while the
 // context opens: the H2D copy then runs without page faults (load_input joins them)
 void Input::populate(void *m, size_t len) {
-    if (len < ((size_t)64 << 20)) return;
+    if (!m || len < ((size_t)64 << 20)) return;
     const unsigned hw = std::thread::hardware_concurrency();
     const int T = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
     const size_t kStripe = (size_t)32 << 20;
@@ -184,19 +221,6 @@ void Input::populate(void *m, size_t len) {
 }
 
 namespace {
-// true when [p, p+n) holds a complete line starting with "#CHROM" (the '#CHROM' gate of
-// every tool ends there)
-bool has_chrom_line(const char *p, size_t n) {
-    const char *s = p, *e = p + n;
-    while (s < e) {
-        const char *nl = (const char *)memchr(s, '\n', (size_t)(e - s));
-        if (!nl) return false;
-        if (is_chrom_line(s, (size_t)(nl - s))) return true;
-        s = nl + 1;
-    }
-    return false;
-}
-
 ssize_t read_full(int fd, char *dst, size_t want) {
     size_t got = 0;
     while (got < want) {
@@ -221,7 +245,7 @@ void Input::read_fd(int fd, bool host_copy) {
             const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
             const size_t lo = (size_t)pos & ~(pg - 1);
             const size_t len = (size_t)st.st_size - lo;
-            if ((size_t)st.st_size - (size_t)pos >= kPrefetchBytes) gpu_prefetch();
+            if ((size_t)st.st_size - (size_t)pos >= prefetch_bytes()) gpu_prefetch();
             void *m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, (off_t)lo);
             if (m != MAP_FAILED) {
                 madvise(m, len, len < ((size_t)64 << 20) ? (MADV_SEQUENTIAL | MADV_WILLNEED) : MADV_SEQUENTIAL);
@@ -258,17 +282,33 @@ void Input::read_fd(int fd, bool host_copy) {
 
     // the head of the stream (up to 2 chunks) always lands in host memory: the '#CHROM' gate
     // runs on it, and small inputs never reach the device
-    ssize_t k0 = read_full(fd, base, kPrefetchBytes);
+    const size_t kPre = prefetch_bytes(), kChunk = stream_chunk();
+    ssize_t k0 = read_full(fd, base, kPre);
     size_t got = k0 > 0 ? (size_t)k0 : 0;
-    if (got == kPrefetchBytes) {
+    bool chrom = false;  // the head holds the complete '#CHROM' line
+    size_t scanned = 0;
+    auto scan = [&] {
+        while (!chrom && scanned < got) {
+            const char *s0 = base + scanned;
+            const char *nl = (const char *)memchr(s0, '\n', got - scanned);
+            if (!nl) break;
+            chrom = is_chrom_line(s0, (size_t)(nl - s0));
+            scanned = (size_t)(nl - base) + 1;
+        }
+    };
+    if (got == kPre) {
         gpu_prefetch();  // a large input: the HIP runtime starts while the rest arrives
         // the head keeps arriving into host memory while the context opens (a read that
-        // waited for the open would stall the writer for ~0.2 s)
+        // waited for the open would stall the writer for ~0.2 s); a device-only stream also
+        // needs the whole header in it
+        const size_t head_cap = std::max<size_t>(2 * kChunk, (size_t)256 << 20);
         for (;;) {
-            const bool enough = got >= 2 * kStreamChunk;
-            if (enough && (host_copy || g_open_done.load(std::memory_order_acquire))) break;
+            if (!host_copy) scan();
+            const bool enough = got >= 2 * kChunk &&
+                                (host_copy || ((chrom || got >= head_cap) && g_open_done.load(std::memory_order_acquire)));
+            if (enough) break;
             if (got >= ((size_t)8 << 30) || cap - got < ((size_t)8 << 20)) break;
-            ssize_t k = ::read(fd, base + got, (size_t)8 << 20);
+            ssize_t k = ::read(fd, base + got, std::min<size_t>((size_t)8 << 20, std::max(kChunk, kPre)));
             if (k < 0 && errno == EINTR) continue;
             if (k <= 0) {
                 n = host_n = got;
@@ -277,11 +317,11 @@ void Input::read_fd(int fd, bool host_copy) {
             got += (size_t)k;
         }
     }
-    if (got < 2 * kStreamChunk) {
+    if (got < 2 * kChunk) {
         n = host_n = got;
         return;
     }
-    if (!host_copy && has_chrom_line(base, got)) {
+    if (!host_copy && chrom) {
         // the caller needs only the header on the host (VCFX_allele_freq_calc): the rest goes
         // straight to the device through a pinned staging ring -- no host copy, no page faults
         vcfxg_ctx *g = gpu_quiet();
@@ -290,7 +330,7 @@ void Input::read_fd(int fd, bool host_copy) {
             stream_ctx = g;
             ring_ctx = g;
             constexpr int kSlots = 4;
-            constexpr size_t kSlot = (size_t)32 << 20;
+            const size_t kSlot = ring_slot();
             bool ok = true;
             for (int i = 0; i < kSlots && ok; i++) {
                 void *r = nullptr;
@@ -349,9 +389,9 @@ void Input::read_fd(int fd, bool host_copy) {
             bool fin;
             {
                 std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return eof || avail - at >= kStreamChunk; });
+                cv.wait(lk, [&] { return eof || avail - at >= kChunk; });
                 fin = eof;
-                upto = fin ? avail : at + (avail - at) / kStreamChunk * kStreamChunk;
+                upto = fin ? avail : at + (avail - at) / kChunk * kChunk;
             }
             if (ok && upto > at) ok = vcfxg_ingest(g, base + at, upto - at, 0) == VCFXG_OK;
             at = upto;
@@ -385,6 +425,12 @@ void Input::read_fd(int fd, bool host_copy) {
 
 bool load_input(vcfxg_ctx *g, const Input &in, int err_fd) {
     in.join_populate();
+    if (in.tail) {  // a shard view: header + record range, straight from the mapping
+        int rc = vcfxg_ingest_begin(g, in.n);
+        if (!rc) rc = vcfxg_ingest(g, in.p, in.host_n, 0);
+        if (!rc) rc = vcfxg_ingest(g, in.tail, in.n - in.host_n, 1);
+        return gpu_ok(g, rc, "load view", err_fd);
+    }
     if (in.stream_ctx == g && in.streamed == in.n) {
         // the bytes are on the device already (streamed while stdin was read); complete it
         return gpu_ok(g, vcfxg_ingest(g, nullptr, 0, 1), "ingest", err_fd);

@@ -22,6 +22,9 @@ struct Input {
     const char *p = nullptr;
     size_t n = 0;
     size_t host_n = 0;
+    // a shard view (VCFX_INPUT_VIEW): input bytes [host_n, n) are at tail[0, n - host_n) on the
+    // host (another part of the same mapping), not after p
+    const char *tail = nullptr;
     bool mapped = false;
     // mapping to release: [map_base, map_base + map_len)
     void *map_base = nullptr;
@@ -40,6 +43,12 @@ struct Input {
     // fails; a 0-byte file is a successful empty map.  Inputs of 1 MiB and more start the
     // GPU context opening on a background thread (gpu_prefetch).
     bool open_file(const char *path);
+    // VCFX_INPUT_VIEW="H:LO:HI" in the environment (set by the multi-GPU runner,
+    // vcfx_amd/shard.py): the input is the file's header bytes [0, H) followed by its records
+    // [LO, HI) -- one rank's shard, without a copy.  The device input is ingested from those
+    // two host ranges (load_input); host-side line access goes through LineSource.
+    // VCFX_VIEW_SKIP_HEADER=1: the tool writes nothing for the header part (ranks > 0).
+    void apply_view();
     // All of fd's remaining bytes (the stream path's input).  A regular file (`< file`) is
     // mapped from the current offset, with no copy.  A pipe is read into a reserved,
     // transparently-huge-page region that a helper thread pre-faults ahead of the reader,
@@ -54,12 +63,21 @@ struct Input {
     void join_populate() const;
 };
 
+// sizes of the input paths (VCFX_PREFETCH_BYTES, VCFX_STREAM_CHUNK, VCFX_RING_SLOT,
+// VCFX_WINDOW_BYTES override them; tests use tiny values)
+size_t prefetch_bytes();
+size_t stream_chunk();
+size_t ring_slot();
+size_t window_bytes();
+
 // VCFX_TIMING=1 in the environment: "[vcfx-timing] <what> <ms since process start>" on
 // stderr (fd 2) at each phase of a tool run -- e2e breakdowns; silent otherwise.
 void phase(const char *what);
 // set by the drop-in executables (binary_main.cpp): the process exits right after the tool
 // returns, so inputs skip unmapping (the kernel drops the mappings at exit anyway)
 extern bool g_process_exit_fast;
+// VCFX_VIEW_SKIP_HEADER=1: a shard rank other than the first (its header output is rank 0's)
+bool view_skip_header();
 
 void write_all(int fd, const char *p, size_t n);
 inline void write_str(int fd, const std::string &s) { write_all(fd, s.data(), s.size()); }

@@ -43,7 +43,7 @@ const char *kWarnFields = "Warning: Skipping invalid VCF line (fewer than 9 fiel
 
 // returns false on a device error (already reported)
 bool run_af(const Input &in, int mode, bool quiet, Out &out, Out &err, uint64_t *variants, uint64_t *datalines) {
-    out.put("CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n");
+    if (!view_skip_header()) out.put("CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n");
     *variants = *datalines = 0;
     // '#CHROM' gate (processMmap :366-386 / processStdin :489-502) over the header prefix
     // (for a device-only stdin stream the host holds the header part: host_n <= n)

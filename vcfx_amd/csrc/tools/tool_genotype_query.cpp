@@ -43,30 +43,36 @@ const char *kHelp =
     "  VCFX_genotype_query -g \"0|1\" --strict < input.vcf > phased_het.vcf\n";
 
 struct Line {
-    const char *ls, *le;
+    std::string s;  // a held header line (a copy: a device-read window may move on)
 };
 
 // returns false on device error
 bool run_gq(const Input &in, bool stream_mode, const std::string &q, bool strict, bool quiet, int out_fd, Out &err) {
     if (!stream_mode && in.n == 0) return true;  // genotypeQueryMmap :436
-    LineEmitter em(in.p, in.n, out_fd);
+    LineEmitter em(in.p, in.host_n, out_fd);
     std::vector<Line> held;  // stream mode: header lines buffered until the next data line
     auto header = [&](const char *ls, const char *le) {
-        if (stream_mode) held.push_back({ls, le});
+        if (stream_mode) held.push_back({std::string(ls, (size_t)(le - ls))});
         else em.line(ls, le);
     };
     auto flush_held = [&]() {
-        for (auto &h : held) em.line(h.ls, h.le);
+        if (held.empty()) return;
+        for (auto &h : held) {
+            em.raw(h.s.data(), h.s.size());
+            em.raw("\n", 1);
+        }
+        em.finish();  // before the held strings go
         held.clear();
     };
     // header prefix up to and including '#CHROM' (mmap :450-478 / stream :546-563)
-    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    const char *p = in.p, *end = in.p + in.host_n, *ls, *le;
+    const bool skip_head = view_skip_header();  // a shard rank > 0: rank 0 writes the header part
     bool found = false;
     size_t data_start = in.n;
     while (next_line(p, end, ls, le)) {
         if (le == ls) continue;
         if (*ls == '#') {
-            header(ls, le);
+            if (!skip_head) header(ls, le);
             if (is_chrom_line(ls, (size_t)(le - ls))) {
                 found = true;
                 data_start = (size_t)(p - in.p);
@@ -92,11 +98,17 @@ bool run_gq(const Input &in, bool stream_mode, const std::string &q, bool strict
         if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||
             !gpu_ok(g, vcfxg_fetch_lines(g, 0, nl, nullptr, nullptr, st.data()), "fetch_lines", err.fd))
             return false;
+        LineSource src(in, g, em);
         uint64_t prev = data_start;
         for (uint64_t i = 0; i < nl; i++) {
-            const char *a = in.p + prev, *b = in.p + ends[i];
+            const uint8_t v = st[i];
+            const char *a = nullptr, *b = nullptr;
+            if (v == VCFXG_LINE_HEADER || v == VCFXG_LINE_ROW || v == VCFXG_LINE_WARN) {
+                a = src.at(prev, ends[i]);
+                b = a + (ends[i] - prev);
+            }
             prev = ends[i] + 1;
-            switch (st[i]) {
+            switch (v) {
             case VCFXG_LINE_HEADER: header(a, b); break;
             case VCFXG_LINE_ROW: flush_held(); em.line(a, b); break;
             case VCFXG_LINE_DROP: flush_held(); break;
@@ -112,6 +124,10 @@ bool run_gq(const Input &in, bool stream_mode, const std::string &q, bool strict
                 break;
             default: break;
             }
+        }
+        if (!src.ok) {
+            em.finish();
+            return gpu_ok(g, VCFXG_E_HIP, "input_fetch", err.fd);
         }
     }
     em.finish();
@@ -172,7 +188,7 @@ extern "C" int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int ou
         out.flush();
         return run_gq(in, false, query, strict, quiet, out_fd, err) ? 0 : 1;
     }
-    in.read_fd(in_fd);
+    in.read_fd(in_fd, /*host_copy=*/false);  // kept records are read back from the device
     phase("stdin read");
     out.flush();
     return run_gq(in, true, query, strict, quiet, out_fd, err) ? 0 : 1;

@@ -49,21 +49,22 @@ const char *kHelp =
 // stripped from every line) / filterNonRef :553-636
 bool run_nr(const Input &in, bool stream_mode, int out_fd, Out &err) {
     if (!stream_mode && in.n == 0) return true;
-    LineEmitter em(in.p, in.n, out_fd);
+    LineEmitter em(in.p, in.host_n, out_fd);
     auto bare = [&](const char *ls, const char *le) {  // the line as the reference sees it
         return (!stream_mode && le > ls && le[-1] == '\r') ? le - 1 : le;
     };
-    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    const char *p = in.p, *end = in.p + in.host_n, *ls, *le;
+    const bool skip_head = view_skip_header();  // a shard rank > 0: rank 0 writes the header part
     bool found = false;
     size_t data_start = in.n;
     while (next_line(p, end, ls, le)) {
         const char *ae = bare(ls, le);
         if (ae == ls) {
-            em.line(ls, ls);
+            if (!skip_head) em.line(ls, ls);
             continue;
         }
         if (*ls == '#') {
-            em.line(ls, ae);
+            if (!skip_head) em.line(ls, ae);
             if (is_chrom_line(ls, (size_t)(ae - ls))) {
                 found = true;
                 data_start = (size_t)(p - in.p);
@@ -89,16 +90,20 @@ bool run_nr(const Input &in, bool stream_mode, int out_fd, Out &err) {
         if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||
             !gpu_ok(g, vcfxg_fetch_lines(g, 0, nl, nullptr, nullptr, st.data()), "fetch_lines", err.fd))
             return false;
+        LineSource src(in, g, em);
         uint64_t prev = data_start;
         for (uint64_t i = 0; i < nl; i++) {
-            const char *a = in.p + prev, *b = in.p + ends[i];
+            const uint8_t v = st[i];
+            if (v == VCFXG_LINE_SKIP) em.raw("\n", 1);  // an empty line
+            else if (v == VCFXG_LINE_HEADER || v == VCFXG_LINE_ROW) {
+                const char *a = src.at(prev, ends[i]), *b = a + (ends[i] - prev);
+                em.line(a, bare(a, b));
+            }  // VCFXG_LINE_DROP: every sample hom-ref
             prev = ends[i] + 1;
-            switch (st[i]) {
-            case VCFXG_LINE_SKIP: em.line(a, a); break;  // an empty line: "\n"
-            case VCFXG_LINE_HEADER:
-            case VCFXG_LINE_ROW: em.line(a, bare(a, b)); break;
-            default: break;  // VCFXG_LINE_DROP: every sample hom-ref
-            }
+        }
+        if (!src.ok) {
+            em.finish();
+            return gpu_ok(g, VCFXG_E_HIP, "input_fetch", err.fd);
         }
     }
     em.finish();
@@ -145,7 +150,7 @@ extern "C" int vcfx_tool_nonref_filter(int argc, char **argv, int in_fd, int out
         out.flush();
         return run_nr(in, false, out_fd, err) ? 0 : 1;
     }
-    in.read_fd(in_fd);
+    in.read_fd(in_fd, /*host_copy=*/false);  // kept records are read back from the device
     phase("stdin read");
     out.flush();
     return run_nr(in, true, out_fd, err) ? 0 : 1;

@@ -31,22 +31,28 @@ extern "C" int vcfx_pipeline_filter_query(const char *filter, const char *logic,
             err.put(std::string("Error: cannot open file '") + input + "'\n");
             return 1;
         }
-    } else in.read_fd(in_fd);
-    LineEmitter em(in.p, in.n, out_fd);
-    struct L {
-        const char *a, *b;
+    } else in.read_fd(in_fd, /*host_copy=*/false);  // kept records are read back from the device
+    LineEmitter em(in.p, in.host_n, out_fd);
+    std::vector<std::string> held;  // genotype_query's buffered header lines (copies)
+    auto flush_held = [&]() {
+        if (held.empty()) return;
+        for (auto &h : held) {
+            em.raw(h.data(), h.size());
+            em.raw("\n", 1);
+        }
+        em.finish();
+        held.clear();
     };
-    std::vector<L> held;  // genotype_query's buffered header lines
     bool found = false;
     auto strip = [](const char *a, const char *b) { return (b > a && b[-1] == '\r') ? b - 1 : b; };
     // the filter's header prefix as the query sees it
-    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    const char *p = in.p, *end = in.p + in.host_n, *ls, *le;
     size_t data_start = in.n;
     while (next_line(p, end, ls, le)) {
         const char *ae = strip(ls, le);
         if (ae == ls) continue;  // filter prints "\n"; the query skips empty lines
         if (*ls == '#') {
-            held.push_back({ls, ae});
+            held.emplace_back(ls, (size_t)(ae - ls));
             if (is_chrom_line(ls, (size_t)(ae - ls))) {
                 found = true;
                 data_start = (size_t)(p - in.p);
@@ -74,15 +80,19 @@ extern "C" int vcfx_pipeline_filter_query(const char *filter, const char *logic,
         if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||
             !gpu_ok(g, vcfxg_fetch_lines(g, 0, nl, nullptr, nullptr, st.data()), "fetch_lines", err.fd))
             return 1;
+        LineSource src(in, g, em);
         uint64_t prev = data_start;
         for (uint64_t i = 0; i < nl; i++) {
-            const char *a = in.p + prev, *b = in.p + ends[i];
-            prev = ends[i] + 1;
             const uint8_t v = st[i];
-            if (v == VCFXG_LINE_HEADER) held.push_back({a, strip(a, b)});
+            const char *a = nullptr, *b = nullptr;
+            if (v == VCFXG_LINE_HEADER || v == VCFXG_LINE_ROW || v == 7) {
+                a = src.at(prev, ends[i]);
+                b = a + (ends[i] - prev);
+            }
+            prev = ends[i] + 1;
+            if (v == VCFXG_LINE_HEADER) held.emplace_back(a, (size_t)(strip(a, b) - a));
             else if (v == VCFXG_LINE_ROW || v == 6 || v == 7) {
-                for (auto &h : held) em.line(h.a, h.b);
-                held.clear();
+                flush_held();
                 if (v == VCFXG_LINE_ROW) em.line(a, strip(a, b));
                 else if (v == 7 && !gq_quiet) {
                     err.put("Warning: skipping line with <9 fields: ");

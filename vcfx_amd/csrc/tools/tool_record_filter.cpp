@@ -125,18 +125,19 @@ namespace {
 // processFileMmap (:406-493) / processStdin (:498-549)
 bool run_rf(const Input &in, bool stdin_mode, const std::vector<Criterion> &cs, bool and_logic, int out_fd,
             Out &err) {
-    LineEmitter em(in.p, in.n, out_fd);
-    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    LineEmitter em(in.p, in.host_n, out_fd);
+    const char *p = in.p, *end = in.p + in.host_n, *ls, *le;
     size_t data_start = in.n;
     auto strip = [](const char *a, const char *b) { return (b > a && b[-1] == '\r') ? b - 1 : b; };
+    const bool skip_head = view_skip_header();  // a shard rank > 0: rank 0 writes the header part
     while (next_line(p, end, ls, le)) {
         const char *ae = strip(ls, le);
         if (ae == ls) {
-            em.raw("\n", 1);
+            if (!skip_head) em.raw("\n", 1);
             continue;
         }
         if (*ls == '#') {
-            em.line(ls, ae);
+            if (!skip_head) em.line(ls, ae);
             if (is_chrom_line(ls, (size_t)(ae - ls))) {
                 data_start = (size_t)(p - in.p);
                 break;
@@ -162,14 +163,19 @@ bool run_rf(const Input &in, bool stdin_mode, const std::vector<Criterion> &cs, 
     if (!gpu_ok(g, vcfxg_line_ends(g, 0, nl, ends.data()), "line_ends", err.fd) ||
         !gpu_ok(g, vcfxg_fetch_lines(g, 0, nl, nullptr, nullptr, st.data()), "fetch_lines", err.fd))
         return false;
+    LineSource src(in, g, em);
     uint64_t prev = data_start;
     for (uint64_t i = 0; i < nl; i++) {
-        const char *a = in.p + prev, *b = in.p + ends[i];
+        const uint8_t v = st[i];
+        if (v == VCFXG_LINE_SKIP) em.raw("\n", 1);
+        else if (v == VCFXG_LINE_ROW || v == VCFXG_LINE_HEADER) {
+            const char *a = src.at(prev, ends[i]), *b = a + (ends[i] - prev);
+            em.line(a, strip(a, b));
+        }
         prev = ends[i] + 1;
-        if (st[i] == VCFXG_LINE_SKIP) em.raw("\n", 1);
-        else if (st[i] == VCFXG_LINE_ROW || st[i] == VCFXG_LINE_HEADER) em.line(a, strip(a, b));
     }
     em.finish();
+    if (!src.ok) return gpu_ok(g, VCFXG_E_HIP, "input_fetch", err.fd);
     phase("records written");
     return true;
 }
@@ -240,7 +246,7 @@ extern "C" int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out
         if (in.n == 0) return 0;
         return run_rf(in, false, cs, and_logic, out_fd, err) ? 0 : 1;
     }
-    in.read_fd(in_fd);
+    in.read_fd(in_fd, /*host_copy=*/false);  // kept records are read back from the device
     phase("stdin read");
     return run_rf(in, true, cs, and_logic, out_fd, err) ? 0 : 1;
 }

@@ -48,6 +48,7 @@ SIGNATURES = {
     "vcfxg_host_alloc": (_I, [_VP, _S, ctypes.POINTER(_VP)]),
     "vcfxg_host_free": (None, [_VP, _VP]),
     "vcfxg_input_device_ptr": (_VP, [_VP]),
+    "vcfxg_input_fetch": (_I, [_VP, _U64, _S, _VP]),
     "vcfxg_index": (_I, [_VP, _S, ctypes.POINTER(_U64)]),
     "vcfxg_line_ends": (_I, [_VP, _U64, _U64, _VP]),
     "vcfxg_allele_freq": (_I, [_VP, _I, ctypes.POINTER(Summary)]),

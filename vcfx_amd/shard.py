@@ -1,38 +1,42 @@
 """Record-sharded multi-GPU runs of the drop-in tools.
 
 One process per GPU (torchrun); rank r opens the engine on LOCAL_RANK and runs the tool on its
-share of ONE input file:
+share of ONE input file.  A share is a VIEW of the file, not a copy: the tool maps the file
+and takes the header bytes [0, H) plus its records [LO, HI) (VCFX_INPUT_VIEW="H:LO:HI",
+hostio.cpp Input::apply_view); the device input is ingested straight from those two ranges of
+the mapping and kept records are written from the mapping.
 
 * VCFX_allele_freq_calc -i FILE: the data region (after the '#CHROM' line) is cut at
   i*size/N and each cut advanced past the next '\\n' (the reference's own sharding pattern,
-  VCFX_allele_counter.cpp:889-901).  Rank r runs the tool on header + its records; rank 0
-  writes the header row and every rank's rows in rank order; the stderr totals
-  ("Processed V variants from L data lines") are all-reduced.
+  VCFX_allele_counter.cpp:889-901).  Rank r runs the tool on header + its records; ranks > 0
+  write no header row (VCFX_VIEW_SKIP_HEADER=1); the stderr totals ("Processed V variants
+  from L data lines") are all-reduced.
 * VCFX_variant_counter FILE: the whole file is cut the same way; "Total Variants" is
-  all-reduced; warning line numbers are shifted to whole-file numbering; under --strict the
-  earliest failing line of any rank wins.
+  all-reduced; warning line numbers are shifted to whole-file numbering (each rank counts its
+  own shard's lines only when some rank warned); under --strict the earliest failing line of
+  any rank wins.
 * VCFX_record_filter / VCFX_genotype_query / VCFX_nonref_filter with a file input: the
-  records are cut the same way; every rank runs the filter on header + its records, and
-  once more on the header alone to learn the header's own output (H, E), which it strips
-  from its outputs; rank 0 writes H and E once, then the ranks' kept lines and warnings in
-  rank order.  Files with data lines before '#CHROM' run unsharded.
+  records are cut the same way; rank 0's view writes the header part once, ranks > 0 skip it.
+  Files with data lines before '#CHROM' run unsharded.
 * VCFX_ld_calculator -i FILE (streaming): every rank parses the file and computes the pair
-  rows of its `--shard r/N` share (equal window-pair counts); rank 0 writes the header and
-  the ranks' pair lines in rank order.  Matrix mode runs on rank 0 only.
+  rows of its `--shard r/N` share (equal window-pair counts); with a window as large as the
+  file (BASELINE config 5) every row range needs every variant, so there is nothing to cut.
+  Matrix mode runs on rank 0 only.
 
-Per-rank outputs are gathered to rank 0 (the only writer of stdout/stderr, so pipes work);
-the only reductions are the global counts.  Other invocations (stdin input, other tools)
-run unsharded on rank 0.  The collectives go through torch.distributed, so the same code
-runs over RCCL (nccl backend, device tensors) on MI355X nodes and over gloo in the CPU tests.
+Outputs move to rank 0 only -- the only writer of stdout/stderr, so pipes work -- as chunked
+point-to-point sends in rank order (64 MiB per message); rank 0 streams each chunk to the sink
+as it arrives, so no rank ever holds another rank's output.  The only reductions are the
+global counts.  Other invocations (stdin input, other tools) run unsharded on rank 0.  The
+collectives go through torch.distributed: RCCL (nccl backend, device tensors) on MI355X nodes,
+gloo in the CPU tests.
 """
 import os
 import re
 import sys
-import tempfile
 
 import numpy as np
 
-_SHM = "/dev/shm" if os.path.isdir("/dev/shm") else None
+CHUNK = 64 << 20  # bytes per point-to-point message
 
 
 # ---------------------------------------------------------------------------------------
@@ -83,12 +87,79 @@ def record_cuts(buf, lo, world):
     return cuts
 
 
-def _write_shard(parts):
-    f = tempfile.NamedTemporaryFile(prefix="vcfx_shard_", suffix=".vcf", dir=_SHM, delete=False)
-    for p in parts:
-        f.write(memoryview(p))
-    f.close()
-    return f.name
+# ---------------------------------------------------------------------------------------
+# argv: the input operand, found as each tool's getopt_long finds it
+# ---------------------------------------------------------------------------------------
+# options that take a value, per tool (the optstrings / long options of the drop-ins, which
+# are the reference's: VCFX_allele_freq_calc.cpp:590-646, VCFX_record_filter.cpp:584-658,
+# VCFX_genotype_query.cpp:379-428, VCFX_nonref_filter.cpp:646-652, VCFX_ld_calculator.cpp:
+# 1084-1209, VCFX_variant_counter.cpp:154-218)
+_VALUE_OPTS = {
+    "VCFX_allele_freq_calc": ({"-i"}, {"--input"}),
+    "VCFX_record_filter": ({"-f", "-l", "-i"}, {"--filter", "--logic"}),
+    "VCFX_genotype_query": ({"-g", "-i"}, {"--genotype-query", "--input"}),
+    "VCFX_nonref_filter": ({"-i"}, {"--input"}),
+    "VCFX_ld_calculator": ({"-i", "-r", "-w", "-t", "-n", "-d"},
+                           {"--input", "--region", "--window", "--threshold", "--threads", "--max-distance",
+                            "--shard"}),
+    "VCFX_variant_counter": (set(), set()),
+}
+
+
+def parse_args(tool, argv):
+    """(options, operands) of argv[1:] the GNU getopt_long way: options may follow operands,
+    "--" ends them, a value-taking option consumes the next argument (or its attached /
+    '='-joined value).  options: list of (name, value or None)."""
+    short_v, long_v = _VALUE_OPTS.get(tool, (set(), set()))
+    opts, operands = [], []
+    i, args = 0, argv[1:]
+    while i < len(args):
+        a = args[i]
+        if a == "--":
+            operands += args[i + 1:]
+            break
+        if a.startswith("--") and len(a) > 2:
+            name, eq, val = a.partition("=")
+            if name in long_v and not eq:
+                val = args[i + 1] if i + 1 < len(args) else None
+                i += 1
+            opts.append((name, val if (eq or name in long_v) else None))
+        elif a.startswith("-") and len(a) > 1:
+            # a cluster of short options; a value-taking one eats the rest or the next arg
+            for k in range(1, len(a)):
+                o = "-" + a[k]
+                if o in short_v:
+                    if k + 1 < len(a):
+                        opts.append((o, a[k + 1:]))
+                    else:
+                        opts.append((o, args[i + 1] if i + 1 < len(args) else None))
+                        i += 1
+                    break
+                opts.append((o, None))
+        else:
+            operands.append(a)
+        i += 1
+    return opts, operands
+
+
+def input_path(tool, argv):
+    """The input file the tool reads (-i/--input, else the first operand where the tool takes
+    one); None when it reads stdin or the path is not a regular file."""
+    opts, operands = parse_args(tool, argv)
+    path = None
+    for name, val in opts:
+        if name in ("-i", "--input"):
+            path = val
+    if path is None and tool != "VCFX_ld_calculator" and operands:
+        path = operands[0]
+    if path == "-":
+        return None
+    return path if path and os.path.isfile(path) else None
+
+
+def _has_flag(tool, argv, *names):
+    opts, _ = parse_args(tool, argv)
+    return any(n in names for n, _ in opts)
 
 
 # ---------------------------------------------------------------------------------------
@@ -113,116 +184,154 @@ class Comm:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN if op == "min" else self.dist.ReduceOp.SUM)
         return [int(x) for x in t.cpu().tolist()]
 
-    def gather_bytes(self, b):
-        """every rank's bytes, in rank order, on every rank (all_gather of padded tensors)."""
+    def sizes(self, n):
+        """every rank's int64 n, in rank order."""
         if self.dist is None:
-            return [b]
+            return [n]
+        t = self.torch.tensor([n], dtype=self.torch.int64, device=self.dev)
+        out = [self.torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t)
+        return [int(x.item()) for x in out]
+
+    def to_root(self, b, sink):
+        """Rank-ordered concatenation of every rank's bytes `b` into sink (a callable taking
+        bytes) on rank 0: rank 0's own first, then each rank's in CHUNK-sized point-to-point
+        messages, written as they arrive.  Ranks > 0 only send; nothing is all-gathered."""
+        if self.dist is None:
+            sink(b)
+            return
         torch = self.torch
-        n = torch.tensor([len(b)], dtype=torch.int64, device=self.dev)
-        sizes = [torch.zeros_like(n) for _ in range(self.world)]
-        self.dist.all_gather(sizes, n)
-        sizes = [int(s.item()) for s in sizes]
-        m = max(1, max(sizes))
-        mine = torch.zeros(m, dtype=torch.uint8)
-        if b:
-            mine[:len(b)] = torch.frombuffer(bytearray(b), dtype=torch.uint8)
-        mine = mine.to(self.dev)
-        out = [torch.empty(m, dtype=torch.uint8, device=self.dev) for _ in range(self.world)]
-        self.dist.all_gather(out, mine)
-        return [bytes(o[:s].cpu().numpy().tobytes()) for o, s in zip(out, sizes)]
+        sizes = self.sizes(len(b))
+        if self.rank == 0:
+            sink(b)
+            buf = None
+            for r in range(1, self.world):
+                for off in range(0, sizes[r], CHUNK):
+                    k = min(CHUNK, sizes[r] - off)
+                    if buf is None or buf.numel() < k:
+                        buf = torch.empty(min(CHUNK, max(sizes[1:])), dtype=torch.uint8, device=self.dev)
+                    self.dist.recv(buf[:k], src=r)
+                    sink(buf[:k].cpu().numpy().tobytes())
+        else:
+            mv = memoryview(b)
+            for off in range(0, len(b), CHUNK):
+                piece = torch.frombuffer(bytearray(mv[off:off + CHUNK]), dtype=torch.uint8).to(self.dev)
+                self.dist.send(piece, dst=0)
 
 
 # ---------------------------------------------------------------------------------------
-# per-tool sharded runs; runner(argv, stdin) -> (stdout, stderr, rc)
+# per-tool sharded runs
+#   runner(argv, stdin, view=None, skip_header=False) -> (stdout, stderr, rc):
+#   view = (H, LO, HI): the tool's input is the file's bytes [0, H) + [LO, HI)
 # ---------------------------------------------------------------------------------------
-def _input_path(argv, short="-i", long_="--input", positional=False):
-    """the input file named by -i/--input (or, with positional, the first operand); None
-    unless it is a regular file"""
-    path = None
-    i = 1
-    while i < len(argv):
-        a = argv[i]
-        if a in (short, long_) and i + 1 < len(argv):
-            path = argv[i + 1]
-            break
-        if a.startswith(long_ + "="):
-            path = a.split("=", 1)[1]
-            break
-        if positional and not a.startswith("-") and path is None:
-            path = a
-        i += 1
-    return path if path and os.path.isfile(path) else None
+def tool_runner(argv, stdin, view=None, skip_header=False):
+    """The in-process drop-in (libvcfx_tools) with the shard view passed in its environment."""
+    from . import tools
+    keys = ("VCFX_INPUT_VIEW", "VCFX_VIEW_SKIP_HEADER")
+    saved = {k: os.environ.get(k) for k in keys}
+    try:
+        if view is not None:
+            os.environ["VCFX_INPUT_VIEW"] = "%d:%d:%d" % view
+        if skip_header:
+            os.environ["VCFX_VIEW_SKIP_HEADER"] = "1"
+        return tools.run(argv, stdin)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 _AF_PROCESSED = re.compile(rb"^Processed (\d+) variants from (\d+) data lines\n", re.M)
+_AF_PROCESSING = re.compile(rb"^Processing .* \(\d+ MB\)\n", re.M)
 _AF_HEAD = b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n"
 _AF_PRE = b"Warning: Data line encountered before #CHROM header. Skipping.\n"
-_AF_FIELDS = b"Warning: Skipping invalid VCF line (fewer than 9 fields).\n"
 
 
-def run_af(argv, comm, runner):
-    path = _input_path(argv, positional=True)
-    quiet = "-q" in argv or "--quiet" in argv
-    buf = np.memmap(path, np.uint8, mode="r") if os.path.getsize(path) else np.zeros(0, np.uint8)
+def _memmap(path):
+    return np.memmap(path, np.uint8, mode="r") if os.path.getsize(path) else np.zeros(0, np.uint8)
+
+
+class _Sink:
+    """rank 0's stdout: a callable sink, or collected bytes"""
+
+    def __init__(self, write=None):
+        self.write = write
+        self.parts = []
+
+    def __call__(self, b):
+        if not b:
+            return
+        if self.write is not None:
+            self.write(b)
+        else:
+            self.parts.append(bytes(b))
+
+    def value(self):
+        return b"".join(self.parts)
+
+
+def run_af(argv, comm, runner, path, sink):
+    quiet = _has_flag("VCFX_allele_freq_calc", argv, "-q", "--quiet")
+    buf = _memmap(path)
     ds = header_end(buf)
     cuts = record_cuts(buf, ds, comm.world)
     lo, hi = cuts[comm.rank], cuts[comm.rank + 1]
-    shard = _write_shard([buf[:ds], buf[lo:hi]])
-    try:
-        sargv = [a if a != path else shard for a in argv]
-        out, err, rc = runner(sargv, b"")
-    finally:
-        os.unlink(shard)
+    out, err, rc = runner(argv, b"", view=(ds, lo, hi), skip_header=comm.rank > 0)
     m = _AF_PROCESSED.search(err)
     v, lines = (int(m.group(1)), int(m.group(2))) if m else (0, 0)
     tot = comm.allreduce([v, lines, rc])
-    outs = comm.gather_bytes(out[len(_AF_HEAD):] if out.startswith(_AF_HEAD) else out)
-    warns = comm.gather_bytes(_AF_FIELDS * err.count(_AF_FIELDS))
+    comm.to_root(out, sink)
+    # per-rank stderr without the lines rank 0 rewrites (the header part's warnings are
+    # rank 0's: its view holds the header)
+    err = _AF_PROCESSED.sub(b"", _AF_PROCESSING.sub(b"", err))
+    if comm.rank:
+        err = err.replace(_AF_PRE, b"")
+    errs = _Sink()
+    comm.to_root(err, errs)
     if comm.rank:
         return b"", b"", 0
     rc = 1 if tot[2] else 0
-    stdout = _AF_HEAD + b"".join(outs)
     if quiet:
-        return stdout, b"", rc
-    size_mb = len(buf) // (1024 * 1024)
-    stderr = ("Processing %s (%d MB)\n" % (path, size_mb)).encode() + _AF_PRE * err.count(_AF_PRE) + b"".join(warns)
+        return None, errs.value(), rc
+    stderr = ("Processing %s (%d MB)\n" % (path, len(buf) // (1024 * 1024))).encode() + errs.value()
     stderr += b"Processed %d variants from %d data lines\n" % (tot[0], tot[1])
-    return stdout, stderr, rc
+    return None, stderr, rc
 
 
 _VC_WARN = re.compile(rb"^(Warning: skipping line |Error: line )(\d+)( .*\n)", re.M)
 
 
-def run_vc(argv, comm, runner):
-    path = _input_path(argv, "", "", positional=True)
-    buf = np.memmap(path, np.uint8, mode="r") if os.path.getsize(path) else np.zeros(0, np.uint8)
+def run_vc(argv, comm, runner, path, sink):
+    buf = _memmap(path)
     if len(buf) >= 2 and buf[0] == 0x1F and buf[1] == 0x8B:
         if comm.rank:
             return b"", b"", 0
         return runner(argv, b"")  # gzip input: not shardable by bytes
     cuts = record_cuts(buf, 0, comm.world)
     lo, hi = cuts[comm.rank], cuts[comm.rank + 1]
-    before = int(np.count_nonzero(buf[:lo] == 10))  # lines of earlier shards
-    shard = _write_shard([buf[lo:hi]])
-    try:
-        out, err, rc = runner([a if a != path else shard for a in argv], b"")
-    finally:
-        os.unlink(shard)
-    err = _VC_WARN.sub(lambda m: m.group(1) + str(int(m.group(2)) + before).encode() + m.group(3), err)
+    out, err, rc = runner(argv, b"", view=(0, lo, hi))
+    if comm.allreduce([1 if _VC_WARN.search(err) else 0])[0]:
+        # whole-file line numbers: lines of the earlier shards (each rank counts its own)
+        mine = int(np.count_nonzero(buf[lo:hi] == 10)) + (1 if hi > lo and buf[hi - 1] != 10 else 0)
+        before = sum(comm.sizes(mine)[:comm.rank])
+        err = _VC_WARN.sub(lambda m: m.group(1) + str(int(m.group(2)) + before).encode() + m.group(3), err)
     m = re.search(rb"Total Variants: (\d+)", out)
     total = int(m.group(1)) if m else 0
     first_err = int(_VC_WARN.search(err).group(2)) if rc and _VC_WARN.search(err) else (1 << 62)
     red = comm.allreduce([total])
     fe = comm.allreduce([first_err], op="min")[0]
-    errs = comm.gather_bytes(err if not rc else b"")
-    fails = comm.gather_bytes(err if rc else b"")
+    # --strict: the earliest failing line of any rank; its rank's stderr ends the output
+    fail_rank = comm.allreduce([comm.rank if first_err == fe and fe < (1 << 62) else comm.world], op="min")[0]
+    errs = _Sink()
+    comm.to_root(err if (fe == (1 << 62) or comm.rank <= fail_rank) else b"", errs)
     if comm.rank:
         return b"", b"", 0
-    if fe < (1 << 62):  # --strict: the earliest failing line of any rank, nothing on stdout
-        for r, f in enumerate(fails):
-            if f and int(_VC_WARN.search(f).group(2)) == fe:
-                return b"", b"".join(errs[:r]) + f, 1
-    return b"Total Variants: %d\n" % red[0], b"".join(errs), 0
+    if fe < (1 << 62):
+        return b"", errs.value(), 1
+    sink(b"Total Variants: %d\n" % red[0])
+    return None, errs.value(), 0
 
 
 def _pre_header_data(buf, ds):
@@ -234,71 +343,96 @@ def _pre_header_data(buf, ds):
     return False
 
 
-def run_filter(argv, comm, runner, path):
-    buf = np.memmap(path, np.uint8, mode="r") if os.path.getsize(path) else np.zeros(0, np.uint8)
+def run_filter(argv, comm, runner, path, sink):
+    buf = _memmap(path)
     ds = header_end(buf)
     plain = ds < len(buf) and not _pre_header_data(buf, ds)
-    ok = comm.allreduce([1 if plain else 0], op="min")[0]
-    out = err = b""
-    rc = 0
-    if ok:
-        cuts = record_cuts(buf, ds, comm.world)
-        lo, hi = cuts[comm.rank], cuts[comm.rank + 1]
-        head = _write_shard([buf[:ds]])
-        shard = _write_shard([buf[:ds], buf[lo:hi]])
-        try:
-            H, E, _ = runner([a if a != path else head for a in argv], b"")
-            out, err, rc = runner([a if a != path else shard for a in argv], b"")
-        finally:
-            os.unlink(head)
-            os.unlink(shard)
-        good = out.startswith(H) and err.startswith(E)
-        ok = comm.allreduce([1 if good else 0], op="min")[0]
-        out, err = out[len(H):], err[len(E):]
-    if not ok:  # unsharded on rank 0
+    if not comm.allreduce([1 if plain else 0], op="min")[0]:  # unsharded on rank 0
         if comm.rank:
             return b"", b"", 0
         return runner(argv, b"")
-    outs = comm.gather_bytes(out)
-    errs = comm.gather_bytes(err)
+    cuts = record_cuts(buf, ds, comm.world)
+    lo, hi = cuts[comm.rank], cuts[comm.rank + 1]
+    out, err, rc = runner(argv, b"", view=(ds, lo, hi), skip_header=comm.rank > 0)
+    comm.to_root(out, sink)
+    errs = _Sink()
+    comm.to_root(err, errs)
     rcs = comm.allreduce([rc])
     if comm.rank:
         return b"", b"", 0
-    return H + b"".join(outs), E + b"".join(errs), 1 if rcs[0] else 0
+    return None, errs.value(), 1 if rcs[0] else 0
 
 
-def run_ld(argv, comm, runner):
+def run_ld(argv, comm, runner, sink):
     out, err, rc = runner(argv + ["--shard", "%d/%d" % (comm.rank, comm.world)], b"")
-    outs = comm.gather_bytes(out)
-    errs = comm.gather_bytes(err)
+    comm.to_root(out, sink)
+    errs = _Sink()
+    comm.to_root(err, errs)
     rcs = comm.allreduce([rc])
     if comm.rank:
         return b"", b"", 0
-    return b"".join(outs), b"".join(errs), 1 if rcs[0] else 0
+    return None, errs.value(), 1 if rcs[0] else 0
 
 
-def run_sharded(argv, stdin=b"", dist=None, runner=None):
+SHARDED = ("VCFX_allele_freq_calc", "VCFX_variant_counter", "VCFX_ld_calculator", "VCFX_record_filter",
+           "VCFX_genotype_query", "VCFX_nonref_filter")
+
+
+def plan(argv):
+    """'af' / 'vc' / 'filter' / 'ld' when argv runs sharded at world > 1, else None (stdin
+    input, help/version, LD matrix mode, other tools)."""
+    tool = os.path.basename(argv[0])
+    if tool not in SHARDED:
+        return None
+    if _has_flag(tool, argv, "-h", "--help", "-v", "--version"):
+        return None
+    path = input_path(tool, argv)
+    if path is None:
+        return None
+    if tool == "VCFX_allele_freq_calc":
+        return "af"
+    if tool == "VCFX_variant_counter":
+        return "vc"
+    if tool == "VCFX_ld_calculator":
+        return None if _has_flag(tool, argv, "-m", "--matrix") else "ld"
+    return "filter"
+
+
+def run_sharded(argv, stdin=b"", dist=None, runner=None, write=None):
     """Run one tool invocation across the ranks of `dist` (None = single process).  Returns
-    (stdout, stderr, rc) on rank 0 and empty results on the other ranks."""
-    if runner is None:
-        from . import tools
-        runner = tools.run
+    (stdout, stderr, rc) on rank 0 and empty results on the other ranks; with `write` (a
+    callable) rank 0's stdout is streamed into it instead and returned as b""."""
+    runner = runner or tool_runner
     comm = Comm(dist)
     tool = os.path.basename(argv[0])
-    if comm.world > 1 and not any(a in ("-h", "--help", "-v", "--version") for a in argv[1:]):
-        if tool == "VCFX_allele_freq_calc" and _input_path(argv, positional=True):
-            return run_af(argv, comm, runner)
-        if tool == "VCFX_variant_counter" and _input_path(argv, "", "", positional=True):
-            return run_vc(argv, comm, runner)
-        if tool == "VCFX_ld_calculator" and _input_path(argv) and not ("-m" in argv or "--matrix" in argv):
-            return run_ld(argv, comm, runner)
-        if tool in ("VCFX_record_filter", "VCFX_genotype_query", "VCFX_nonref_filter"):
-            path = _input_path(argv, positional=True)
-            if path:
-                return run_filter(argv, comm, runner, path)
+    how = plan(argv) if comm.world > 1 else None
+    if how is None:
+        if comm.rank:
+            return b"", b"", 0
+        out, err, rc = runner(argv, stdin)
+        if write is not None:
+            write(out)
+            out = b""
+        return out, err, rc
+    sink = _Sink(write)
+    path = input_path(tool, argv)
+    if how == "af":
+        res = run_af(argv, comm, runner, path, sink)
+    elif how == "vc":
+        res = run_vc(argv, comm, runner, path, sink)
+    elif how == "ld":
+        res = run_ld(argv, comm, runner, sink)
+    else:
+        res = run_filter(argv, comm, runner, path, sink)
     if comm.rank:
         return b"", b"", 0
-    return runner(argv, stdin)
+    out, err, rc = res
+    if out is None:  # streamed through the sink
+        out = sink.value() if write is None else b""
+    elif write is not None:
+        write(out)
+        out = b""
+    return out, err, rc
 
 
 def main():
@@ -323,9 +457,13 @@ def main():
             engine.lib().vcfxg_device_count(ctypes.byref(n))
             local = local % max(1, n.value)
         os.environ["VCFX_DEVICE"] = str(local)
-    stdin = b"" if dist is not None and dist.get_rank() else (sys.stdin.buffer.read() if not sys.stdin.isatty()
-                                                              and not _input_path(argv) else b"")
-    out, err, rc = run_sharded(argv, stdin, dist)
+    rank0 = dist is None or dist.get_rank() == 0
+    tool = os.path.basename(argv[0]) if argv else ""
+    # stdin only when the tool reads it (no input file) -- never under an inherited pipe the
+    # tool would not read -- and only on rank 0, which runs such invocations
+    stdin = sys.stdin.buffer.read() if rank0 and argv and input_path(tool, argv) is None and \
+        not sys.stdin.isatty() and not _has_flag(tool, argv, "-h", "--help", "-v", "--version") else b""
+    out, err, rc = run_sharded(argv, stdin, dist, write=sys.stdout.buffer.write if rank0 else None)
     if dist is not None:
         dist.destroy_process_group()
     sys.stdout.buffer.write(out)

@@ -47,6 +47,44 @@ def run(argv, stdin=None, cwd=None):
         return fo.read(), fe.read(), rc
 
 
+def run_pipe(argv, stdin=b"", cwd=None):
+    """run() with stdin as a pipe (the tools' streaming stdin path: not a regular file, so it is
+    read, not mapped).  A writer thread feeds the pipe while the tool runs."""
+    import threading
+    L = lib()
+    old = os.getcwd()
+    rfd, wfd = os.pipe()
+
+    def feed():
+        try:
+            mv = memoryview(stdin or b"")
+            while mv:
+                k = os.write(wfd, mv[:1 << 20])
+                mv = mv[k:]
+        except OSError:
+            pass
+        finally:
+            os.close(wfd)
+
+    th = threading.Thread(target=feed, daemon=True)
+    th.start()
+    with tempfile.TemporaryFile() as fo, tempfile.TemporaryFile() as fe:
+        arr = (ctypes.c_char_p * (len(argv) + 1))(*[a.encode() for a in argv], None)
+        if cwd:
+            os.chdir(cwd)
+        try:
+            rc = L.vcfx_tool_main(argv[0].encode(), len(argv), arr, rfd, fo.fileno(), fe.fileno())
+        finally:
+            os.chdir(old)
+            os.close(rfd)  # a tool that stops early: the writer sees EPIPE
+            th.join()
+        if rc == -100:
+            raise NotImplementedError(argv[0])
+        fo.seek(0)
+        fe.seek(0)
+        return fo.read(), fe.read(), rc
+
+
 def pipeline_filter_query(filter_, query, input_path=None, stdin=None, logic="and", strict=False, gq_quiet=False,
                           cwd=None):
     """Fused `VCFX_record_filter --filter F --logic L [input] | VCFX_genotype_query -g Q`."""
