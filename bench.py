@@ -272,8 +272,8 @@ def main():
             if red is not None:
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.text_bytes])
             return s
-        kern_names = ("af_scan", "line_count", "line_emit", "line_compact", "af_records", "af_chunks", "af_fused",
-                      "af_pipe", "af_stream", "af_walk", "walk_compact", "af_complex", "af_rows", "af_format")
+        kern_names = ("line_count", "line_emit", "line_compact", "af_records", "af_walk", "walk_compact", "af_complex",
+                      "af_rows", "af_format")
     elif a.workload == "nonref":
         def step():
             s = eng.nonref_filter_region(ds, engine.MODE_FILE)  # (the walk) per-record "every sample hom-ref"
@@ -364,18 +364,7 @@ def main():
             algo = {   # algorithmic bytes per launch
                 "line_count": region_bytes,
                 "line_emit": region_bytes + 8 * L,
-                "af_scan": region_bytes + L * 8,                # one sweep: every byte classified + newline offsets
                 "af_records": region_bytes + L * (8 + 13),      # record bytes + line_end + per-line results
-                "af_fused": region_bytes + L * (8 + 13),        # one sweep: record bytes + line_end + results
-                "af_chunks": region_bytes + L * (8 + 13),       # chunk sweep: record bytes + line_end + results
-                # two-stream pipeline (index sweep + record sweep overlapped per 64 MiB piece):
-                # the record bytes once from HBM -- the second read is served by the Infinity
-                # Cache -- + line_end written and read + per-line results
-                "af_pipe": region_bytes + L * (8 + 8 + 13),
-                # one sweep (k_af_stream + compaction + the per-line rest): the record bytes
-                # once + per line: the block-region results written, read back and written
-                # dense (line_end 8, counts/prefix/status 13, head record 16, x3)
-                "af_stream": region_bytes + L * 3 * (8 + 13 + 16),
                 # walk (no index sweep): the record bytes once + per line its region results
                 # (line_end 8, counts/prefix/status 13, head record 16); the compaction reads
                 # and rewrites them dense; the per-line rest reads head record + status

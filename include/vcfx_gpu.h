@@ -120,11 +120,8 @@ int vcfxg_allele_freq(vcfxg_ctx *ctx, int mode, vcfxg_summary *out);
  * wave walks the records of one chunk, predicting a record's end from the previous record
  * and validating it by the sample sweep itself); otherwise the index sweep + head pass +
  * sample sweep.  VCFXG_AF_FUSED in the environment at vcfxg_open selects a schedule for
- * measurement: 1 = a single sweep numbering 16 KiB chunks by a wait-free decoupled
- * look-back, 2 = a chunk count then a chunk sweep, 3 = the two-sweep schedule with the line
- * count read back, 4 = byte-class counts per line segment, 5 = two-stream pipelined index +
- * sweep, 6 = LDS-ring stream, 7 = the walk, 8 = the two-sweep schedule with one host
- * synchronisation (all results identical). */
+ * measurement: 3 = the two-sweep schedule with the line count read back, 7 = the walk, 8 = the
+ * two-sweep schedule with one host synchronisation (all results identical). */
 int vcfxg_allele_freq_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
 /* ---- K2: genotype query ----------------------------------------------------------------
  * Per line status (vcfxg_line_status): ROW = some sample's GT sub-field matches `query`

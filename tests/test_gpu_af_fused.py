@@ -1,6 +1,5 @@
-"""GPU parity of vcfxg_allele_freq_region -- every device schedule (default index + head
-pass + sweep, look-back single sweep, chunk sweep, byte-class single sweep, two-stream
-pipelined index + sweep) -- against the
+"""GPU parity of vcfxg_allele_freq_region -- every device schedule (the walk, the two-sweep
+schedule with one host synchronisation, the synchronous two-sweep schedule) -- against the
 two-pass path
 (vcfxg_index + vcfxg_allele_freq) and the C oracle: every per-line array and the output
 text must be identical, including inputs that put many line starts in one 16 KiB chunk
@@ -15,23 +14,16 @@ from vcfx_amd import engine, synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["default", "sync", "fused", "chunks", "scan", "pipe", "pipe1", "stream1",
-                                               "stream3", "walk", "walk4k", "walk1k", "twosweep"])
+@pytest.fixture(scope="module", params=["default", "sync", "walk", "walk4k", "walk1k", "twosweep"])
 def eng(request):
     """every region schedule: default (the walk for long records, else the two-sweep
     schedule), two-sweep = index + head pass + sweep with one host synchronisation;
-    sync: the same kernels with the line count read back after the index), look-back single sweep,
-    chunk sweep, byte-class single sweep, two-stream pipeline (pieces of 2 wave-chunks, so
-    the small inputs here span many pieces; and of 1), one-sweep LDS-ring stream (grids of 1
-    and 3 persistent blocks, so the inputs span many chunks and block boundaries), walk
-    (no index sweep: predicted record ends validated by the sweep; chunks of 128 KiB, 4 KiB
-    and 1 KiB, so lines start in, span and skip over many walkers' chunks)"""
+    sync: the same kernels with the line count read back after the index; walk (no index
+    sweep: predicted record ends validated by the sweep; chunks of 128 KiB, 4 KiB and 1 KiB,
+    so lines start in, span and skip over many walkers' chunks)"""
     import os
-    env = {"VCFXG_AF_FUSED": {"default": "0", "sync": "3", "fused": "1", "chunks": "2", "scan": "4", "pipe": "5",
-                              "pipe1": "5", "stream1": "6", "stream3": "6", "walk": "7", "walk4k": "7",
-                              "walk1k": "7", "twosweep": "8"}[request.param],
-           "VCFXG_PIPE_CHUNKS": {"pipe1": "1"}.get(request.param, "2"),
-           "VCFXG_STREAM_GRID": {"stream1": "1", "stream3": "3"}.get(request.param, "0"),
+    env = {"VCFXG_AF_FUSED": {"default": "0", "sync": "3", "walk": "7", "walk4k": "7", "walk1k": "7",
+                              "twosweep": "8"}[request.param],
            "VCFXG_WALK_CHUNK": {"walk4k": "4096", "walk1k": "1024"}.get(request.param, str(128 * 1024))}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)

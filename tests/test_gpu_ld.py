@@ -1,5 +1,6 @@
-"""GPU parity for VCFX_ld_calculator: int8-MFMA pair sums + fp64 epilogue against the C
-oracle's computeRsqFast / computeRsq, streaming and matrix modes, both input paths."""
+"""GPU parity for VCFX_ld_calculator: MFMA pair sums (block-scaled FP4 for complete 256-variant
+groups, int8 for groups with missing calls) + the exact fp64 epilogue against the C oracle's
+computeRsqFast / computeRsq, streaming and matrix modes, both input paths."""
 import tempfile
 
 import pytest

@@ -22,11 +22,6 @@ KERNELS = {
     "line_emit": r"vcfxg::k_idx_sweep<true>\(",
     "line_compact": r"vcfxg::k_nl_compact\(",
     "af_records": r"vcfxg::k_(line_meta|af_sweep|af_complex)\(",
-    "af_pipe": r"vcfxg::k_(idx_sweep<false>|nl_compact_piece|lines_tail|line_meta|af_sweep|af_complex)\(",
-    "af_stream": r"vcfxg::k_(af_stream|af_stream_compact|af_complex)\(",
-    "af_scan": r"vcfxg::k_af_scan\(",
-    "af_fused": r"vcfxg::k_af_fused\(",
-    "af_chunks": r"vcfxg::k_af_chunks\(",
     "af_walk": r"vcfxg::k_af_walk\(",
     "walk_compact": r"vcfxg::k_walk_compact\(",
     "af_complex": r"vcfxg::k_af_complex\(",
@@ -48,8 +43,8 @@ KERNELS = {
 # the engine names bench.py times per workload (a symbol shared by two names, e.g.
 # k_af_complex, would otherwise leave a spurious entry under a workload that never times it)
 TIMED = {
-    "af": ("af_scan", "line_count", "line_emit", "line_compact", "af_records", "af_chunks", "af_fused",
-           "af_pipe", "af_stream", "af_walk", "walk_compact", "af_complex", "af_format"),
+    "af": ("line_count", "line_emit", "line_compact", "af_records", "af_walk", "walk_compact", "af_complex",
+           "af_format"),
     "pipeline": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "rf_records", "gq_records"),
     "nonref": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "nr_records"),
     "ld": ("line_count", "line_emit", "line_compact", "ld_parse", "ld_count", "ld_emit", "ld_count_gen",
@@ -58,13 +53,12 @@ TIMED = {
 
 
 # names that share a symbol with another name: kept only when their own primary kernel ran
-PRIMARY = {"af_records": "vcfxg::k_af_sweep", "af_pipe": "vcfxg::k_nl_compact_piece",
-           "af_stream": "vcfxg::k_af_stream", "gq_records": "vcfxg::k_gq_sweep", "fq_rest": "vcfxg::k_fq_compact<"}
+PRIMARY = {"af_records": "vcfxg::k_af_sweep", "gq_records": "vcfxg::k_gq_sweep", "fq_rest": "vcfxg::k_fq_compact<"}
 
 
 # names whose kernels launch several times per step (one per pipelined piece): the per-step
 # divisor is the count of this once-per-step symbol instead
-ANCHOR = {"af_pipe": "vcfxg::k_af_complex"}
+ANCHOR = {}
 
 
 def per_kernel(path, counter):

@@ -30,9 +30,6 @@ struct DevBuf {
 struct vcfxg_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t stream2 = nullptr;           // pipelined AF: the record-sweep stream
-    std::vector<hipEvent_t> pipe_ev;         // pipelined AF: piece p indexed (stream -> stream2)
-    hipEvent_t pipe_done = nullptr;          // pipelined AF: stream2 drained
     std::string err;
     // input
     DevBuf input;
@@ -55,16 +52,12 @@ struct vcfxg_ctx {
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
         ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff;
-    DevBuf pipe_carry;          // pipelined AF: line number at the start of each piece
-    DevBuf st_le, st_alt, st_tot, st_rowpre, st_status, st_meta, st_bcount;  // one-sweep AF block regions
     int n_cu = 0;
     DevBuf async_small;         // asynchronous AF path: line range {0, n}, failure flags, summary
-    int stream_grid = getenv("VCFXG_STREAM_GRID") ? atoi(getenv("VCFXG_STREAM_GRID")) : 0;
     DevBuf ld_temp, ld_quarters, ld_stage_ctr;  // LD: pairs staged by the count pass
     uint64_t ld_temp_cap = 0;
     // test hook: a fixed (small) staging capacity exercises the overflow -> emit-pass path
     uint64_t ld_stage_cap_fixed = getenv("VCFXG_LD_STAGE_CAP") ? strtoull(getenv("VCFXG_LD_STAGE_CAP"), nullptr, 10) : 0;
-    DevBuf fuse_state;          // fused AF: per-chunk look-back words
     DevBuf af_meta;             // AF head pass output (k_af_meta)
     // walk AF path (vcfxg_af_walk.hip): per-walker regions, counts, scan, flags
     DevBuf wk_le, wk_alt, wk_tot, wk_rowpre, wk_status, wk_meta, wk_count, wk_offs, wk_gt, wk_small;
@@ -74,8 +67,7 @@ struct vcfxg_ctx {
     // host hints taken at load time from the first data line: its '\n' distance from the
     // sample start (the walk's first prediction) and the mean length of the first lines
     int64_t hint_span = 0, hint_line = 0;
-    DevBuf scan_seg, nl_chunk;  // AF one-sweep path: per-chunk segment counts, newline -> chunk
-    uint64_t af_line_cap = 0;   // fused AF: line capacity the last run needed
+    uint64_t af_line_cap = 0;   // two-sweep AF: line capacity the last run needed
     // region AF schedule: 0 = default (the walk schedule 7 when the first records average
     // >= 512 B, else 3 with one host synchronisation: single-sweep index + head pass +
     // fixed-stride sweep), 1 = one-sweep look-back kernel (k_af_fused),
@@ -87,8 +79,6 @@ struct vcfxg_ctx {
     // record_filter / genotype_query region schedule: 0 = the walk (vcfxg_fq_walk.hip) when
     // the first records average >= 512 B, 1 = the walk always, -1 = index + per-tool kernels
     int fq_path = getenv("VCFXG_FQ_WALK") ? atoi(getenv("VCFXG_FQ_WALK")) : 0;
-    int fuse_dbg = getenv("VCFXG_FUSE_DEBUG") ? atoi(getenv("VCFXG_FUSE_DEBUG")) : 0;  // diagnostics only
-    int64_t pipe_chunks = getenv("VCFXG_PIPE_CHUNKS") ? atol(getenv("VCFXG_PIPE_CHUNKS")) : 4096;  // 64 MiB pieces
     std::vector<uint8_t> ld_gflag_host;  // per 128-variant group: all complete
     uint64_t ld_m = 0, ld_prefix_bytes = 0;
     int ld_kpad = 64, ld_ns = 0, ld_kp4 = 64;
@@ -221,14 +211,10 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->fuse_state, &c->af_meta, &c->scan_seg, &c->nl_chunk, &c->pipe_carry, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->st_le, &c->st_alt, &c->st_tot, &c->st_rowpre, &c->st_status, &c->st_meta, &c->st_bcount, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs})
         if (b->p) (void)hipFree(b->p);
-    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
     for (hipEvent_t e : c->ingest_ev_free) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->pipe_ev) (void)hipEventDestroy(e);
-    if (c->pipe_done) (void)hipEventDestroy(c->pipe_done);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     for (auto &kv : c->ev) {
         (void)hipEventDestroy(kv.second.first);
         (void)hipEventDestroy(kv.second.second);
@@ -508,69 +494,6 @@ int vcfxg_allele_freq(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
     return af_rows(c, mode, out);
 }
 
-// default region path: ONE sweep of the input (k_af_scan: newline offsets + per-segment
-// byte-class counts), then compaction + per-line combine + the full/general rest
-static int af_region_scan(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
-    HIPCHK(c, hipSetDevice(c->device));
-    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
-    const int64_t nc = vcfxg::idx_wchunks(lo, hi);
-    if (!nc) {
-        int r = vcfxg_index(c, data_start, nullptr);
-        return r ? r : vcfxg_allele_freq(c, mode, out);
-    }
-    const size_t cap = (size_t)vcfxg::af_scan_cap();
-    int r = ensure(c, c->idx_counts, sizeof(uint32_t) * (size_t)(nc + 1));
-    if (!r) r = ensure(c, c->idx_offs, sizeof(uint64_t) * (size_t)(nc + 1));
-    if (!r) r = ensure(c, c->idx_pos, sizeof(uint64_t) * (size_t)nc * cap + 64);
-    if (!r) r = ensure(c, c->scan_seg, vcfxg::af_scan_seg_bytes() * (size_t)nc);
-    if (r) return r;
-    const char *buf = P<char>(c->input);
-    unsigned *overflow = reinterpret_cast<unsigned *>(P<uint64_t>(c->idx_pos) + (size_t)nc * cap);
-    HIPCHK(c, hipMemsetAsync(overflow, 0, 8, c->stream));
-    prof_begin(c, "af_scan");
-    HIPCHK(c, vcfxg::launch_af_scan(buf, lo, hi, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_pos), c->scan_seg.p,
-                                    overflow, c->stream));
-    prof_end(c, "af_scan");
-    HIPCHK(c, hipMemsetAsync(P<uint32_t>(c->idx_counts) + nc, 0, sizeof(uint32_t), c->stream));
-    r = exclusive_scan(c, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_offs), (size_t)nc + 1);
-    if (r) return r;
-    static thread_local uint64_t total, tail_end, nl_host;
-    static thread_local unsigned ovf;
-    HIPCHK(c, hipMemcpyAsync(&total, P<uint64_t>(c->idx_offs) + nc, sizeof total, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&ovf, overflow, sizeof ovf, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (ovf) {  // lines shorter than ~1 KiB somewhere: the index + per-line path
-        r = vcfxg_index(c, data_start, nullptr);
-        return r ? r : vcfxg_allele_freq(c, mode, out);
-    }
-    const bool tail = hi > lo && c->last_byte != '\n';
-    const uint64_t nl = total + (tail ? 1 : 0);
-    r = ensure(c, c->line_end, 8 * (nl + 1));
-    if (!r) r = ensure(c, c->nl_chunk, 4 * (nl + 1));
-    if (!r) r = af_buffers(c, nl);
-    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (nl + 1));
-    if (r) return r;
-    tail_end = (uint64_t)hi;
-    nl_host = nl;
-    if (tail)
-        HIPCHK(c, hipMemcpyAsync(P<uint64_t>(c->line_end) + total, &tail_end, 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemcpyAsync(c->d_nlines.p, &nl_host, 8, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
-    prof_begin(c, "af_records");
-    HIPCHK(c, vcfxg::launch_af_combine(buf, lo, hi, P<uint32_t>(c->idx_counts), P<uint64_t>(c->idx_offs),
-                                       P<uint64_t>(c->idx_pos), c->scan_seg.p, nl, total, mode,
-                                       P<uint64_t>(c->line_end), P<uint32_t>(c->nl_chunk), c->af_meta.p,
-                                       P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
-    HIPCHK(c, vcfxg::launch_af_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), nl, mode,
-                                       c->af_meta.p, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
-    prof_end(c, "af_records");
-    c->data_start = data_start;
-    c->n_lines = nl;
-    c->indexed = true;
-    return af_rows(c, mode, out);
-}
 
 // Default region path, asynchronous: the two-sweep schedule (index sweep + scan +
 // compaction, head pass + fixed-stride sweep + the per-line rest, row lengths + scan) runs
@@ -791,243 +714,21 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     return VCFXG_OK;
 }
 
-// One-sweep region path: k_af_stream reads every input byte once -- persistent
-// blocks stream 32 KiB chunks through an LDS ring, find the newlines, parse the heads and
-// sweep the sample regions of the lines ending in each chunk -- then the blocks' regions
-// are concatenated (k_af_stream_compact) and k_af_complex takes the lines left to the exact
-// per-line path.  Overflow (lines under ~512 B on average) -> the two-sweep schedule.
-static int af_region_stream(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
-    HIPCHK(c, hipSetDevice(c->device));
-    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
-    if (!c->n_cu) HIPCHK(c, hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, c->device));
-    // (VCFXG_STREAM_GRID: a small persistent grid, so that the tests' small inputs still
-    // span several blocks of several chunks each)
-    const int G = c->stream_grid > 0 ? c->stream_grid : (c->n_cu > 0 ? c->n_cu : 256);
-    const int64_t nc = vcfxg::af_stream_chunks(lo, hi);
-    if (nc < (c->stream_grid > 0 ? 1 : 4 * (int64_t)G)) {  // small inputs: the two-sweep schedule
-        int r = vcfxg_index(c, data_start, nullptr);
-        return r ? r : vcfxg_allele_freq(c, mode, out);
-    }
-    const uint64_t range = (uint64_t)((nc + G - 1) / G) * 32768;
-    const uint64_t cap_b = range / 512 + 1024, cap = cap_b * (uint64_t)G;
-    int r = ensure(c, c->st_le, 8 * cap);
-    if (!r) r = ensure(c, c->st_alt, 4 * cap);
-    if (!r) r = ensure(c, c->st_tot, 4 * cap);
-    if (!r) r = ensure(c, c->st_rowpre, 4 * cap);
-    if (!r) r = ensure(c, c->st_status, cap);
-    if (!r) r = ensure(c, c->st_meta, vcfxg::af_meta_bytes() * cap);
-    if (!r) r = ensure(c, c->st_bcount, 8 * (size_t)G + 64);
-    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
-    if (!r) r = af_buffers(c, cap);
-    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (cap + 1));
-    if (r) return r;
-    const char *buf = P<char>(c->input);
-    unsigned *overflow = reinterpret_cast<unsigned *>(P<uint64_t>(c->st_bcount) + G);
-    HIPCHK(c, hipMemsetAsync(overflow, 0, 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
-    const int tail = c->last_byte != '\n' ? 1 : 0;
-    prof_begin(c, "af_stream");
-    HIPCHK(c, vcfxg::launch_af_stream(buf, lo, hi, (int64_t)c->n + 256, mode, tail, G, cap_b, P<uint64_t>(c->st_le),
-                                      P<int32_t>(c->st_alt), P<int32_t>(c->st_tot), P<uint32_t>(c->st_rowpre),
-                                      P<uint8_t>(c->st_status), c->st_meta.p, P<uint64_t>(c->st_bcount), overflow,
-                                      P<unsigned long long>(c->counters), c->stream));
-    HIPCHK(c, vcfxg::launch_af_stream_compact(G, cap_b, P<uint64_t>(c->st_bcount), P<uint64_t>(c->st_le),
-                                              P<int32_t>(c->st_alt), P<int32_t>(c->st_tot), P<uint32_t>(c->st_rowpre),
-                                              P<uint8_t>(c->st_status), c->st_meta.p, P<uint64_t>(c->line_end),
-                                              P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                              P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->d_nlines),
-                                              c->stream));
-    HIPCHK(c, vcfxg::launch_af_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
-                                       c->af_meta.p, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
-    prof_end(c, "af_stream");
-    static thread_local uint64_t nl;
-    static thread_local unsigned ovf;
-    HIPCHK(c, hipMemcpyAsync(&nl, c->d_nlines.p, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&ovf, overflow, sizeof ovf, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (ovf) {
-        prof_collect(c);
-        r = vcfxg_index(c, data_start, nullptr);
-        return r ? r : vcfxg_allele_freq(c, mode, out);
-    }
-    c->data_start = data_start;
-    c->n_lines = nl;
-    c->indexed = true;
-    return af_rows(c, mode, out);
-}
 
-// Pipelined region path: the input is cut into pieces of whole 16 KiB wave-chunks.  On the
-// engine stream each piece is indexed (count sweep + in-kernel scan/compaction continuing
-// the line numbering from the previous piece, a device-side carry); on a second stream the
-// head pass and the fixed-stride sweep of that piece's lines follow as soon as its index is
-// published (one event per piece).  The sweep re-reads bytes the index sweep has just
-// pulled through the 256 MiB Infinity Cache, so the record pass is served largely on-die
-// while the index streams the next pieces from HBM.  No host synchronisation until the
-// end: line capacity is the hard bound 16 lines per chunk of the no-overflow case, and a
-// chunk with more newlines (lines under ~1 KiB) sends the whole call to the two-sweep path.
-static int af_region_pipe(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
-    HIPCHK(c, hipSetDevice(c->device));
-    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
-    const int64_t nc = vcfxg::idx_wchunks(lo, hi);
-    const int64_t piece = c->pipe_chunks;  // wave-chunks per piece
-    const int64_t np = (nc + piece - 1) / piece;
-    if (!nc || np < 2) {
-        int r = vcfxg_index(c, data_start, nullptr);
-        return r ? r : vcfxg_allele_freq(c, mode, out);
-    }
-    const size_t pcap = (size_t)vcfxg::idx_pos_cap();
-    const uint64_t cap = (uint64_t)nc * pcap + 2;  // lines, when no chunk overflows
-    int r = ensure(c, c->idx_counts, sizeof(uint32_t) * (size_t)(nc + 1));
-    if (!r) r = ensure(c, c->idx_pos, sizeof(uint64_t) * (size_t)nc * pcap + 64);
-    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
-    if (!r) r = af_buffers(c, cap);
-    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (cap + 1));
-    if (!r) r = ensure(c, c->pipe_carry, 8 * (size_t)(np + 2));
-    if (r) return r;
-    if (!c->stream2) HIPCHK(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-    if (!c->pipe_done) HIPCHK(c, hipEventCreateWithFlags(&c->pipe_done, hipEventDisableTiming));
-    while ((int64_t)c->pipe_ev.size() < np) {
-        hipEvent_t e;
-        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        c->pipe_ev.push_back(e);
-    }
-    const char *buf = P<char>(c->input);
-    unsigned *overflow = reinterpret_cast<unsigned *>(P<uint64_t>(c->idx_pos) + (size_t)nc * pcap);
-    uint64_t *carry = P<uint64_t>(c->pipe_carry);
-    HIPCHK(c, hipMemsetAsync(overflow, 0, 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(carry, 0, 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
-    const bool tail = c->last_byte != '\n';
-    const int64_t a0 = lo & ~(int64_t)15, wb = vcfxg::idx_wchunk_bytes();
-    prof_begin(c, "af_pipe");
-    for (int64_t p = 0; p < np; p++) {
-        const int64_t c0 = p * piece, c1 = std::min(nc, c0 + piece);
-        const int64_t plo = p ? a0 + c0 * wb : lo, phi = std::min(hi, a0 + c1 * wb);
-        HIPCHK(c, vcfxg::launch_idx_count(buf, plo, phi, P<uint32_t>(c->idx_counts) + c0,
-                                          P<uint64_t>(c->idx_pos) + (size_t)c0 * pcap, overflow, c->stream));
-        HIPCHK(c, vcfxg::launch_nl_compact_piece(c1 - c0, P<uint32_t>(c->idx_counts) + c0,
-                                                 P<uint64_t>(c->idx_pos) + (size_t)c0 * pcap, carry + p, carry + p + 1,
-                                                 cap, P<uint64_t>(c->line_end), c->stream));
-        if (p == np - 1 && tail)
-            HIPCHK(c, vcfxg::launch_lines_tail(carry + p + 1, cap, hi, P<uint64_t>(c->line_end), c->stream));
-        HIPCHK(c, hipEventRecord(c->pipe_ev[p], c->stream));
-        HIPCHK(c, hipStreamWaitEvent(c->stream2, c->pipe_ev[p], 0));
-        HIPCHK(c, vcfxg::launch_af_meta_sweep_range(buf, lo, P<uint64_t>(c->line_end), carry + p,
-                                                    (uint64_t)(c1 - c0) * pcap + 2, mode, c->af_meta.p,
-                                                    P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                                    P<uint8_t>(c->status), P<unsigned long long>(c->counters),
-                                                    c->stream2));
-    }
-    HIPCHK(c, hipEventRecord(c->pipe_done, c->stream2));
-    HIPCHK(c, hipStreamWaitEvent(c->stream, c->pipe_done, 0));
-    HIPCHK(c, vcfxg::launch_af_complex(buf, lo, P<uint64_t>(c->line_end), carry + np, cap, mode, c->af_meta.p,
-                                       P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
-    prof_end(c, "af_pipe");
-    HIPCHK(c, hipMemcpyAsync(c->d_nlines.p, carry + np, 8, hipMemcpyDeviceToDevice, c->stream));
-    static thread_local uint64_t nl;
-    static thread_local unsigned ovf;
-    HIPCHK(c, hipMemcpyAsync(&nl, carry + np, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&ovf, overflow, sizeof ovf, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (ovf) {  // some chunk holds more than idx_pos_cap() newlines: the two-sweep path
-        prof_collect(c);
-        r = vcfxg_index(c, data_start, nullptr);
-        return r ? r : vcfxg_allele_freq(c, mode, out);
-    }
-    c->data_start = data_start;
-    c->n_lines = nl;
-    c->indexed = true;
-    return af_rows(c, mode, out);
-}
 
 int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
-    if (c->af_path == 4) return af_region_scan(c, data_start, mode, out);
-    if (c->af_path == 5) return af_region_pipe(c, data_start, mode, out);
-    if (c->af_path == 6) return af_region_stream(c, data_start, mode, out);
     if (c->af_path == 7) return af_region_walk(c, data_start, mode, out);
     if (c->af_path == 8) return af_region_async(c, data_start, mode, out);
-    const uint64_t nc = (c->af_path == 1 || c->af_path == 2) ? vcfxg::af_fused_chunks((int64_t)data_start, (int64_t)c->n) : 0;
-    if (c->af_path == 0) {
-        // records of >= 512 B on average (a GT-dense VCF): the walk schedule, no index sweep
-        if (c->hint_line >= 512 && !c->walk_overflowed) return af_region_walk(c, data_start, mode, out);
-        return af_region_async(c, data_start, mode, out);
-    }
-    if (!nc) {  // synchronous two-sweep schedule (VCFXG_AF_FUSED=3): index + record kernels
+    if (c->af_path == 3) {  // synchronous two-sweep schedule: index + record kernels
         int r = vcfxg_index(c, data_start, nullptr);
         return r ? r : vcfxg_allele_freq(c, mode, out);
     }
-    if (c->af_path == 2) {
-        // line starts counted per 16 KiB chunk (one sweep), scanned, then one sweep
-        // that writes line_end and counts every record while its chunk is L2-resident
-        HIPCHK(c, hipSetDevice(c->device));
-        const char *buf = P<char>(c->input);
-        int r = ensure(c, c->fuse_state, 16 * (nc + 2));
-        if (r) return r;
-        uint64_t *counts = P<uint64_t>(c->fuse_state), *offs = counts + nc + 1;
-        prof_begin(c, "line_count");
-        HIPCHK(c, vcfxg::launch_fuse_count(buf, (int64_t)data_start, (int64_t)c->n, counts, c->stream));
-        prof_end(c, "line_count");
-        HIPCHK(c, hipMemsetAsync(counts + nc, 0, 8, c->stream));
-        r = exclusive_scan(c, counts, offs, (size_t)nc + 1);
-        if (r) return r;
-        static thread_local uint64_t nl;
-        HIPCHK(c, hipMemcpyAsync(&nl, offs + nc, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->d_nlines.p, offs + nc, 8, hipMemcpyDeviceToDevice, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        r = af_buffers(c, nl);
-        if (!r) r = ensure(c, c->line_end, 8 * (nl + 1));
-        if (r) return r;
-        HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
-        prof_begin(c, "af_chunks");
-        HIPCHK(c, vcfxg::launch_af_chunks(buf, (int64_t)data_start, (int64_t)c->n, offs, mode, P<uint64_t>(c->line_end),
-                                          nl, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                          P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
-        prof_end(c, "af_chunks");
-        c->data_start = data_start;
-        c->n_lines = nl;
-        c->indexed = true;
-        return af_rows(c, mode, out);
-    }
-    HIPCHK(c, hipSetDevice(c->device));
-    const char *buf = P<char>(c->input);
-    // line capacity: what the last run needed, else a 256 B/line estimate; a larger count
-    // reruns once with the exact capacity (the kernel counts every line regardless)
-    uint64_t cap = std::max<uint64_t>(c->af_line_cap, (c->n - data_start) / 256 + 4096);
-    for (int attempt = 0; attempt < 2; attempt++) {
-        int r = af_buffers(c, cap);
-        if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
-        if (!r) r = ensure(c, c->fuse_state, 8 * (nc + 1) + 64);
-        if (r) return r;
-        HIPCHK(c, hipMemsetAsync(c->fuse_state.p, 0, 8 * (nc + 1) + 64, c->stream));
-        HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
-        prof_begin(c, "af_fused");
-        HIPCHK(c, vcfxg::launch_af_fused(buf, (int64_t)data_start, (int64_t)c->n, mode,
-                                         P<unsigned long long>(c->fuse_state), P<uint64_t>(c->line_end),
-                                         P<uint64_t>(c->d_nlines), cap, P<int32_t>(c->alt), P<int32_t>(c->tot),
-                                         P<uint32_t>(c->rowpre), P<uint8_t>(c->status),
-                                         P<unsigned long long>(c->counters), c->stream, c->fuse_dbg));
-        prof_end(c, "af_fused");
-        static thread_local uint64_t nl, diag[8];
-        HIPCHK(c, hipMemcpyAsync(&nl, c->d_nlines.p, 8, hipMemcpyDeviceToHost, c->stream));
-        if (c->fuse_dbg & 2) HIPCHK(c, hipMemcpyAsync(diag, c->counters.p, 64, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (c->fuse_dbg & 2) fprintf(stderr, "af_fused: chunks %llu self-counted %llu\n", (unsigned long long)nc,
-                                     (unsigned long long)diag[5]);
-        c->data_start = data_start;
-        c->n_lines = nl;
-        c->indexed = true;
-        if (nl <= cap) {
-            c->af_line_cap = std::max<uint64_t>(c->af_line_cap, nl);
-            return af_rows(c, mode, out);
-        }
-        cap = nl;
-    }
-    return VCFXG_E_STATE;
+    // records of >= 512 B on average (a GT-dense VCF): the walk schedule, no index sweep
+    if (c->hint_line >= 512 && !c->walk_overflowed) return af_region_walk(c, data_start, mode, out);
+    return af_region_async(c, data_start, mode, out);
 }
 
 static int af_rows(vcfxg_ctx *c, int mode, vcfxg_summary *out) {

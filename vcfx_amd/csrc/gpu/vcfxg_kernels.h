@@ -41,26 +41,11 @@ hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint6
                                 const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, void *meta, int32_t *alt,
                                 int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
                                 hipStream_t s);
-hipError_t launch_nl_compact_piece(int64_t nchunks, const uint32_t *counts, const uint64_t *pos,
-                                   const uint64_t *carry_in, uint64_t *carry_out, uint64_t cap, uint64_t *line_end,
-                                   hipStream_t s);
-hipError_t launch_lines_tail(uint64_t *carry, uint64_t cap, int64_t hi, uint64_t *line_end, hipStream_t s);
 hipError_t launch_af_meta_sweep_range(const char *buf, int64_t data_start, const uint64_t *line_end,
                                       const uint64_t *range, uint64_t max_lines, int mode, void *meta, int32_t *alt,
                                       int32_t *tot, uint32_t *rowpre, uint8_t *status, unsigned long long *counters,
                                       hipStream_t s);
 int64_t idx_wchunk_bytes();
-// one-sweep AF record pass (vcfxg_af_stream.hip): persistent blocks over 32 KiB chunks
-int64_t af_stream_chunks(int64_t lo, int64_t hi);
-hipError_t launch_af_stream(const char *buf, int64_t lo, int64_t hi, int64_t n_alloc, int mode, int tail, int grid,
-                            uint64_t cap_b, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
-                            uint8_t *status_b, void *meta_b, uint64_t *bcount, unsigned *overflow,
-                            unsigned long long *counters, hipStream_t s);
-hipError_t launch_af_stream_compact(int grid, uint64_t cap_b, const uint64_t *bcount, const uint64_t *le_b,
-                                    const int32_t *alt_b, const int32_t *tot_b, const uint32_t *rowpre_b,
-                                    const uint8_t *status_b, const void *meta_b, uint64_t *line_end, int32_t *alt,
-                                    int32_t *tot, uint32_t *rowpre, uint8_t *status, void *meta, uint64_t *n_lines,
-                                    hipStream_t s);
 // AF record pass without a separate index (vcfxg_af_walk.hip): one wave per `chunk` bytes
 // walks its lines (predicted fixed-stride ends validated by the sweep); per-walker regions
 // of cap_w lines, then k_walk_compact (offs = exclusive scan of wcount)
@@ -78,28 +63,6 @@ hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
                              int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
                              unsigned long long *counters, hipStream_t s);
-// AF in one sweep (vcfxg_af_scan.hip): per-chunk newline offsets + per-segment byte-class
-// counts, then compaction + per-line combine (+ launch_af_complex for the rest)
-size_t af_scan_seg_bytes();  // per chunk
-int af_scan_cap();           // newline slots per chunk
-hipError_t launch_af_scan(const char *buf, int64_t lo, int64_t hi, uint32_t *counts, uint64_t *pos, void *seg,
-                          unsigned *overflow, hipStream_t s);
-hipError_t launch_af_combine(const char *buf, int64_t lo, int64_t hi, const uint32_t *counts, const uint64_t *offs,
-                             const uint64_t *pos, const void *seg, uint64_t n_lines, uint64_t n_newlines, int mode,
-                             uint64_t *line_end, uint32_t *nl_chunk, void *meta, int32_t *alt, int32_t *tot,
-                             uint32_t *rowpre, uint8_t *status, unsigned long long *counters, hipStream_t s);
-// fused index + AF (one sweep): chunks for data_start / n (0 = use the two-pass path)
-uint64_t af_fused_chunks(int64_t ds, int64_t n);
-hipError_t launch_af_fused(const char *buf, int64_t ds, int64_t n, int mode, unsigned long long *state,
-                           uint64_t *line_end, uint64_t *n_lines_dev, uint64_t cap,
-                           int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
-                           unsigned long long *counters, hipStream_t s, int dbg = 0);
-// default region path: per-16 KiB-chunk line-start counts, then (after a scan into offs) the
-// per-wave chunk sweep + record counts
-hipError_t launch_fuse_count(const char *buf, int64_t ds, int64_t n, uint64_t *counts, hipStream_t s);
-hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64_t *offs, int mode,
-                            uint64_t *line_end, uint64_t cap, int32_t *alt, int32_t *tot, uint32_t *rowpre,
-                            uint8_t *status, unsigned long long *counters, hipStream_t s);
 // VCFX_nonref_filter per line (mode 0 mmap, 1 stdin): status 1 keep / 2 drop / 4 '#' / 0 empty;
 // counters: [0] kept, [1] data lines, [3] lines off the fixed-stride sweep
 // after the nonref walk: nr_line for the lines it left (kGqPending / kGqFull), counters as above

@@ -111,56 +111,6 @@ __global__ void k_af_summary(const uint64_t *n_lines, const uint64_t *__restrict
     out[6] = *fail;
 }
 
-// Pipelined index (one piece of the input): the piece's chunk counts are scanned in place
-// -- each block sums the counts before its first chunk (a few thousand L2-resident words)
-// and scans its own 256 -- and the kept newline offsets land at line numbers continuing
-// from *carry_in; the last thread publishes *carry_out = *carry_in + the piece's lines.
-// Writes stop at `cap` (a chunk over kPosCap newlines sets the overflow flag in the count
-// sweep and the whole call falls back to the emit path, so clamped values are never used).
-constexpr int kCompactThreads = 256;
-__global__ __launch_bounds__(kCompactThreads) void k_nl_compact_piece(int64_t nchunks,
-                                                                      const uint32_t *__restrict__ counts,
-                                                                      const uint64_t *__restrict__ pos,
-                                                                      const uint64_t *carry_in, uint64_t *carry_out,
-                                                                      uint64_t cap, uint64_t *__restrict__ line_end) {
-    __shared__ uint64_t wsum[kCompactThreads / kWave];
-    __shared__ uint32_t wscan[kCompactThreads / kWave];
-    const int t = threadIdx.x, w = t / kWave;
-    const int64_t b0 = (int64_t)blockIdx.x * kCompactThreads;
-    uint64_t pre = 0;
-    for (int64_t k = t; k < b0; k += kCompactThreads) pre += counts[k];
-    pre = wave_sum(pre);
-    if (lane() == 0) wsum[w] = pre;
-    const int64_t c = b0 + t;
-    const uint32_t mine = c < nchunks ? counts[c] : 0u;
-    const uint32_t incl = wave_incl_scan(mine);
-    if (lane() == kWave - 1) wscan[w] = incl;
-    __syncthreads();
-    uint64_t before = 0;
-    uint32_t wbefore = 0;
-#pragma unroll
-    for (int k = 0; k < kCompactThreads / kWave; k++) {
-        before += wsum[k];
-        if (k < w) wbefore += wscan[k];
-    }
-    const uint64_t base = *carry_in + before + wbefore + incl - mine;
-    const uint32_t m = mine < (uint32_t)kPosCap ? mine : (uint32_t)kPosCap;
-    for (uint32_t k = 0; k < m; k++)
-        if (base + k < cap) line_end[base + k] = pos[(uint64_t)c * kPosCap + k];
-    if (blockIdx.x == gridDim.x - 1 && t == kCompactThreads - 1) {
-        const uint64_t end = base + mine;
-        *carry_out = end < cap ? end : cap;
-    }
-}
-
-// a last line without '\n' ends at hi: appended after the final piece
-__global__ void k_lines_tail(uint64_t *carry, uint64_t cap, int64_t hi, uint64_t *__restrict__ line_end) {
-    const uint64_t n = *carry;
-    if (n < cap) {
-        line_end[n] = (uint64_t)hi;
-        *carry = n + 1;
-    }
-}
 
 // =======================================================================================
 // K2: per-record GT reducers (allele counts, genotype match); one wave per line
@@ -451,216 +401,6 @@ __global__ __launch_bounds__(kRecThreads) void k_af_complex(const char *__restri
                 rowpre_o[li] = rowpre;
             }
         }
-    }
-    flush_counters(cnt, counters);
-}
-
-// =======================================================================================
-// K12: fused index + AF, one HBM sweep.  The data region is cut into 16 KiB chunks, one per
-// one-wave block.  A block sweeps its chunk for line marks (the virtual
-// newline at data_start-1 and every '\n' of [data_start, N)), publishes its count of line
-// starts, and gets its first global line number by a decoupled look-back over the
-// predecessors' published counts.  It then runs af_line on every line starting after one
-// of its marks (the chunk it just swept is L2-resident; a line may run past the chunk) and
-// writes line_end / status / counts at global line numbers, so every later kernel sees the
-// same arrays as after vcfxg_index + k_af_records.
-// =======================================================================================
-constexpr int64_t kFuseChunk = 16 * 1024;
-constexpr int kFuseCap = 512;  // marks held per pass (more only for lines < 32 B on average)
-constexpr uint64_t kStAgg = 1ull << 62, kStIncl = 2ull << 62, kStVal = (1ull << 62) - 1;
-
-__device__ __forceinline__ void st_publish(unsigned long long *p, uint64_t v) {
-    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t st_peek(unsigned long long *p) {
-    return (uint64_t)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// marks of [cs, ce): returns their total; stores offsets (relative to cs) of ranks
-// [r_lo, r_lo + kFuseCap] into list
-__device__ int fuse_sweep(const char *__restrict__ buf, int64_t cs, int64_t ce, int64_t ds, int r_lo, int *list) {
-    int run = 0;
-    const int64_t lo = ds > cs ? ds : cs;
-    const int64_t vnl = ds - 1;  // the virtual newline ending the header
-    for (int64_t w0 = cs; w0 < ce; w0 += 4 * kWaveStep) {
-        uint4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int64_t blk = w0 + u * kWaveStep + (int64_t)lane() * kBlockBytes;
-            if (blk < ce) v[u] = load16(buf, blk);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int64_t blk = w0 + u * kWaveStep + (int64_t)lane() * kBlockBytes;
-            uint32_t m = 0;
-            if (blk < ce) {
-                m = eq_mask16(v[u], kRepNl) & range_mask16(blk, lo, ce);
-                if (vnl >= blk && vnl < blk + 16 && vnl >= cs && vnl < ce) m |= 1u << (vnl - blk);
-            }
-            const int c = __popc(m);
-            const int incl = wave_incl_scan(c);
-            int rank = run + incl - c;
-            while (m) {
-                const int j = __builtin_ctz(m);
-                m &= m - 1u;
-                if (list && rank >= r_lo && rank <= r_lo + kFuseCap) list[rank - r_lo] = (int)(blk + j - cs);
-                rank++;
-            }
-            run += wave_bcast(incl, kWave - 1);
-        }
-    }
-    return run;
-}
-
-// line starts of chunk k (what its owner publishes): marks minus a final '\n' at n-1
-__device__ __forceinline__ int fuse_starts(const char *__restrict__ buf, int64_t base, int64_t n, int64_t ds,
-                                           uint64_t k, int *list, int *marks_o) {
-    const int64_t cs = base + (int64_t)k * kFuseChunk;
-    const int64_t ce = cs + kFuseChunk < n ? cs + kFuseChunk : n;
-    const int marks = fuse_sweep(buf, cs, ce, ds, 0, list);
-    if (marks_o) *marks_o = marks;
-    return marks - ((ce == n && n - 1 >= ds && byte_at(buf, n - 1) == '\n') ? 1 : 0);
-}
-
-// count the records starting after the marks of chunk [cs, ce) (line numbers excl + k):
-// af_line per record, line_end and per-line results written at the global line number
-__device__ void fuse_process(const char *__restrict__ buf, int64_t cs, int64_t ce, int64_t n, int64_t ds, uint64_t excl,
-                             int starts, int marks, int *list, int mode, int64_t *scratch, BlockCounters &bc,
-                             uint64_t *__restrict__ line_end, uint64_t cap, int32_t *__restrict__ alt_o,
-                             int32_t *__restrict__ tot_o, uint32_t *__restrict__ rowpre_o,
-                             uint8_t *__restrict__ status_o) {
-    int64_t nl_after = -1;  // end of the last line starting here when no later mark ends it
-    for (int r_lo = 0; r_lo < starts; r_lo += kFuseCap) {
-        if (r_lo) marks = fuse_sweep(buf, cs, ce, ds, r_lo, list);  // > kFuseCap marks: next batch
-        const int r_hi = r_lo + kFuseCap < starts ? r_lo + kFuseCap : starts;
-        for (int k = r_lo; k < r_hi; k++) {
-            const int64_t ls = cs + list[k - r_lo] + 1;
-            int64_t le;
-            if (k + 1 < marks) le = cs + list[k + 1 - r_lo];
-            else {
-                if (nl_after < 0) {  // first '\n' at or after ce, else n
-                    nl_after = n;
-                    for (int64_t w = ce; w < n; w += kWaveStep) {
-                        const int64_t blk = w + (int64_t)lane() * kBlockBytes;
-                        uint32_t m = blk < n ? eq_mask16(load16(buf, blk), kRepNl) & range_mask16(blk, ce, n) : 0u;
-                        const uint64_t any = __ballot(m != 0);
-                        if (any) {
-                            const int src = __builtin_ctzll(any);
-                            const int64_t p = blk + (m ? __builtin_ctz(m) : 0);
-                            nl_after = __shfl(p, src);
-                            break;
-                        }
-                    }
-                }
-                le = nl_after;
-            }
-            const uint64_t li = excl + (uint64_t)k;
-            uint8_t st;
-            uint32_t alt, tot, rowpre;
-            af_line(buf, ls, le, mode, scratch, bc, st, alt, tot, rowpre);
-            if (lane() == 0 && li < cap) {
-                line_end[li] = (uint64_t)le;
-                status_o[li] = st;
-                alt_o[li] = (int32_t)alt;
-                tot_o[li] = (int32_t)tot;
-                rowpre_o[li] = rowpre;
-            }
-        }
-    }
-}
-
-__global__ __launch_bounds__(kWave) void k_af_fused(const char *__restrict__ buf, int64_t ds, int64_t n, int64_t base,
-                                                    uint64_t nchunks, int mode, unsigned long long *__restrict__ state,
-                                                    uint64_t *__restrict__ line_end, uint64_t *__restrict__ n_lines_o,
-                                                    uint64_t cap, int32_t *__restrict__ alt_o,
-                                                    int32_t *__restrict__ tot_o,
-                                                    uint32_t *__restrict__ rowpre_o, uint8_t *__restrict__ status_o,
-                                                    unsigned long long *__restrict__ counters, int dbg) {
-    __shared__ int64_t scratch[16];
-    __shared__ int list[kFuseCap + 1];
-    __shared__ uint32_t cnt[BlockCounters::kNC];
-    if (lane() < BlockCounters::kNC) cnt[lane()] = 0;
-    BlockCounters bc{cnt};
-    const uint64_t c = blockIdx.x;
-    const int64_t cs = base + (int64_t)c * kFuseChunk;
-    const int64_t ce = cs + kFuseChunk < n ? cs + kFuseChunk : n;
-    int marks = 0;
-    const int starts = fuse_starts(buf, base, n, ds, c, list, &marks);
-    // Decoupled look-back: exclusive count of line starts in chunks before c.  Wait-free: a
-    // predecessor that has not published after a short spin is counted here from its bytes
-    // (the same function its owner runs), so no block ever depends on another's progress
-    // and no dispatch order is assumed.
-    uint64_t excl = 0;
-    if (c == 0) {
-        if (lane() == 0) st_publish(&state[0], kStIncl | (uint64_t)starts);
-    } else {
-        if (lane() == 0) st_publish(&state[c], kStAgg | (uint64_t)starts);
-        int64_t pos = (int64_t)c - 1;
-        for (;;) {
-            const int64_t idx = pos - lane();
-            uint64_t v = idx >= 0 ? st_peek(&state[idx]) : kStIncl;
-            for (int spin = 0; spin < 32 && !__all(v != 0); spin++) {
-                __builtin_amdgcn_s_sleep(2);
-                if (v == 0) v = st_peek(&state[idx]);
-            }
-            const uint64_t incl = __ballot((v & ~kStVal) == kStIncl);
-            const int lim = incl ? __builtin_ctzll(incl) : kWave - 1;
-            uint64_t missing = __ballot(v == 0) & (lim == 63 ? ~0ull : ((2ull << lim) - 1ull));
-            while (missing) {
-                const int k = __builtin_ctzll(missing);
-                missing &= missing - 1ull;
-                const int sk = fuse_starts(buf, base, n, ds, (uint64_t)(pos - k), nullptr, nullptr);
-                if (lane() == 0) atomicAdd(&counters[5], 1ull);  // diagnostics: self-counted predecessors
-                if (lane() == k) v = kStAgg | (uint64_t)sk;
-            }
-            excl += wave_sum(lane() <= lim ? (v & kStVal) : 0ull);
-            if (incl) break;
-            pos -= kWave;
-        }
-        if (lane() == 0) st_publish(&state[c], kStIncl | (excl + (uint64_t)starts));
-    }
-    if (c == nchunks - 1 && lane() == 0) *n_lines_o = excl + (uint64_t)starts;
-    if (!(dbg & 1))  // dbg bit 0: index part only (diagnostics)
-        fuse_process(buf, cs, ce, n, ds, excl, starts, marks, list, mode, scratch, bc, line_end, cap, alt_o, tot_o,
-                     rowpre_o, status_o);
-    if (lane() < BlockCounters::kNC && cnt[lane()]) atomicAdd(&counters[lane()], (unsigned long long)cnt[lane()]);
-}
-
-// K12b, the default one-pass-after-count path: line starts per 16 KiB chunk were counted by
-// k_fuse_count and scanned (offs), so every wave owns chunks independently (grid-stride, no
-// look-back, no barriers): it sweeps its chunk writing line_end, then counts the records
-// starting there while the chunk is L2-resident.
-__global__ __launch_bounds__(kWave) void k_fuse_count(const char *__restrict__ buf, int64_t ds, int64_t n,
-                                                      int64_t base, uint64_t nchunks, uint64_t *__restrict__ counts) {
-    for (uint64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-        const int st = fuse_starts(buf, base, n, ds, c, nullptr, nullptr);
-        if (lane() == 0) counts[c] = (uint64_t)st;
-    }
-}
-
-__global__ __launch_bounds__(kRecThreads) void k_af_chunks(const char *__restrict__ buf, int64_t ds, int64_t n,
-                                                           int64_t base, uint64_t nchunks,
-                                                           const uint64_t *__restrict__ offs, int mode,
-                                                           uint64_t *__restrict__ line_end, uint64_t cap,
-                                                           int32_t *__restrict__ alt_o, int32_t *__restrict__ tot_o,
-                                                           uint32_t *__restrict__ rowpre_o,
-                                                           uint8_t *__restrict__ status_o,
-                                                           unsigned long long *__restrict__ counters) {
-    __shared__ int64_t scratch[kRecWaves][16];
-    __shared__ int lists[kRecWaves][kFuseCap + 1];
-    __shared__ uint32_t cnt[BlockCounters::kNC];
-    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    BlockCounters bc{cnt};
-    const int w = threadIdx.x / kWave;
-    const uint64_t wid = (uint64_t)blockIdx.x * kRecWaves + w, nw = (uint64_t)gridDim.x * kRecWaves;
-    for (uint64_t c = wid; c < nchunks; c += nw) {
-        const int64_t cs = base + (int64_t)c * kFuseChunk;
-        const int64_t ce = cs + kFuseChunk < n ? cs + kFuseChunk : n;
-        int marks = 0;
-        const int starts = fuse_starts(buf, base, n, ds, c, lists[w], &marks);
-        fuse_process(buf, cs, ce, n, ds, offs[c], starts, marks, lists[w], mode, scratch[w], bc, line_end, cap, alt_o,
-                     tot_o, rowpre_o, status_o);
     }
     flush_counters(cnt, counters);
 }
@@ -1036,53 +776,7 @@ hipError_t launch_af_records(const char *buf, int64_t data_start, const uint64_t
                        tot, rowpre, status, counters);
     return hipGetLastError();
 }
-uint64_t af_fused_chunks(int64_t ds, int64_t n) {
-    if (ds < 1 || ds >= n) return 0;
-    const int64_t base = (ds - 1) & ~(int64_t)15;
-    return (uint64_t)((n - base + kFuseChunk - 1) / kFuseChunk);
-}
-hipError_t launch_af_fused(const char *buf, int64_t ds, int64_t n, int mode, unsigned long long *state, uint64_t *line_end, uint64_t *n_lines_dev, uint64_t cap,
-                           int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
-                           unsigned long long *counters, hipStream_t s, int dbg) {
-    const uint64_t nc = af_fused_chunks(ds, n);
-    if (!nc) return hipErrorInvalidValue;
-    const int64_t base = (ds - 1) & ~(int64_t)15;
-    hipLaunchKernelGGL(k_af_fused, dim3((unsigned)nc), dim3(kWave), 0, s, buf, ds, n, base, nc, mode, state,
-                       line_end, n_lines_dev, cap, alt, tot, rowpre, status, counters, dbg);
-    return hipGetLastError();
-}
-hipError_t launch_fuse_count(const char *buf, int64_t ds, int64_t n, uint64_t *counts, hipStream_t s) {
-    const uint64_t nc = af_fused_chunks(ds, n);
-    if (!nc) return hipErrorInvalidValue;
-    const int64_t base = (ds - 1) & ~(int64_t)15;
-    hipLaunchKernelGGL(k_fuse_count, dim3((unsigned)std::min<uint64_t>(nc, 65536)), dim3(kWave), 0, s, buf, ds, n,
-                       base, nc, counts);
-    return hipGetLastError();
-}
-hipError_t launch_af_chunks(const char *buf, int64_t ds, int64_t n, const uint64_t *offs, int mode,
-                            uint64_t *line_end, uint64_t cap, int32_t *alt, int32_t *tot, uint32_t *rowpre,
-                            uint8_t *status, unsigned long long *counters, hipStream_t s) {
-    const uint64_t nc = af_fused_chunks(ds, n);
-    if (!nc) return hipErrorInvalidValue;
-    const int64_t base = (ds - 1) & ~(int64_t)15;
-    const unsigned grid = (unsigned)std::min<uint64_t>((nc + kRecWaves - 1) / kRecWaves, 4096);
-    hipLaunchKernelGGL(k_af_chunks, dim3(grid), dim3(kRecThreads), 0, s, buf, ds, n, base, nc, offs, mode, line_end,
-                       cap, alt, tot, rowpre, status, counters);
-    return hipGetLastError();
-}
 size_t af_meta_bytes() { return sizeof(AfMeta); }
-hipError_t launch_nl_compact_piece(int64_t nchunks, const uint32_t *counts, const uint64_t *pos,
-                                   const uint64_t *carry_in, uint64_t *carry_out, uint64_t cap, uint64_t *line_end,
-                                   hipStream_t s) {
-    if (nchunks <= 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_nl_compact_piece, dim3((unsigned)((nchunks + kCompactThreads - 1) / kCompactThreads)),
-                       dim3(kCompactThreads), 0, s, nchunks, counts, pos, carry_in, carry_out, cap, line_end);
-    return hipGetLastError();
-}
-hipError_t launch_lines_tail(uint64_t *carry, uint64_t cap, int64_t hi, uint64_t *line_end, hipStream_t s) {
-    hipLaunchKernelGGL(k_lines_tail, dim3(1), dim3(1), 0, s, carry, cap, hi, line_end);
-    return hipGetLastError();
-}
 // head pass + fixed-stride sweep over the device line range [range[0], range[1]) of one
 // pipelined piece (at most max_lines lines: sizes the grids)
 hipError_t launch_af_meta_sweep_range(const char *buf, int64_t data_start, const uint64_t *line_end,
