@@ -21,8 +21,10 @@ value = units processed by all ranks / max-over-ranks wall time of the K timed s
 (inputs already resident in HBM).  One process per GPU (torchrun), record-sharded with
 seed = base + rank: weak scaling.  Rank 0 prints ONE JSON line (contract: DESIGN.md
 §Measurement) carrying `roofline` for the dominant kernel (HIP-event timing on the engine's
-own stream, algorithmic bytes or ops per launch) and `cpu_baseline` (the oracle/ C
-restatement on a bounded sample, 1 core).
+own stream, algorithmic bytes or ops per launch), `cpu_baseline` (the reference's own tools
+compiled from its sources, else the oracle/ C restatement, on a bounded sample, 1 core),
+`output_check` (the last step's output against the reference's digests) and `e2e` (the
+drop-in CLI end to end: file / pipe / warm context).
 """
 import argparse
 import json
@@ -74,16 +76,28 @@ def pmc_traffic(workload, kernel):
         return None
 
 
-def _timed_oracle(argvs, budget_s):
-    """Run a chain of oracle tool invocations (stdout of one = stdin of the next) repeatedly."""
-    from tests._golden import Oracle
-    o = Oracle()
+REF_DIR = os.path.join(REPO, "oracle", "_ref")
+
+
+def _timed_chain(argvs, budget_s, reference):
+    """Run a chain of tool invocations (stdout of one = stdin of the next) repeatedly: the
+    reference binaries built from /root/reference sources (oracle/_ref, kind "reference") as
+    processes, or the C restatement in-process (kind "port")."""
+    import subprocess
+    o = None
+    if not reference:
+        from tests._golden import Oracle
+        o = Oracle()
     reps, t_total = 0, 0.0
     while t_total < budget_s or reps == 0:
         t0 = time.perf_counter()
         data = b""
         for argv in argvs:
-            out, err, rc = o.run(argv, data)
+            if reference:
+                r = subprocess.run([os.path.join(REF_DIR, argv[0])] + argv[1:], input=data, capture_output=True)
+                out, err, rc = r.stdout, r.stderr, r.returncode
+            else:
+                out, err, rc = o.run(argv, data)
             assert rc == 0, (argv, err[:200])
             data = out
         t_total += time.perf_counter() - t0
@@ -92,8 +106,10 @@ def _timed_oracle(argvs, budget_s):
 
 
 def cpu_baseline(workload, arr, offs, a):
-    """The C restatement oracle (oracle/, kind "port"), 1 thread, over a bounded prefix sample
-    of this rank's synthetic input (the same byte layout as the GPU workload)."""
+    """The reference's own tools (oracle/_ref, compiled here from /root/reference sources by
+    oracle/Makefile.ref; kind "reference"), else the C restatement (oracle/, kind "port"), 1
+    thread, over a bounded prefix sample of this rank's synthetic input (the same byte layout
+    as the GPU workload)."""
     if workload == "ld":
         nvar = min(a.records, 1500)
     else:
@@ -116,13 +132,15 @@ def cpu_baseline(workload, arr, offs, a):
         else:
             argvs = [["VCFX_ld_calculator", "-q", "-w", str(nvar), "-t", str(a.threshold), "-i", f.name]]
             desc = "VCFX_ld_calculator -w %d -t %g -i (file path)" % (nvar, a.threshold)
-        reps, t = _timed_oracle(argvs, a.cpu_seconds)
+        reference = all(os.access(os.path.join(REF_DIR, v[0]), os.X_OK) for v in argvs)
+        reps, t = _timed_chain(argvs, a.cpu_seconds, reference)
+    kind = "reference" if reference else "port"
     if workload == "ld":
         units = nvar * (nvar - 1) // 2
-        return {"value": units * reps / t, "unit": "r2-pairs/s", "cores": 1, "kind": "port",
+        return {"value": units * reps / t, "unit": "r2-pairs/s", "cores": 1, "kind": kind,
                 "sample": "first %d variants (%.1f MB) of the rank-0 shard, all %d window pairs, %s, %d reps, "
                           "%.1f s" % (nvar, len(sample) / 1e6, units, desc, reps, t)}
-    return {"value": nvar * reps / t, "unit": "records/s", "cores": 1, "kind": "port",
+    return {"value": nvar * reps / t, "unit": "records/s", "cores": 1, "kind": kind,
             "sample": "first %d records (%.1f MB) of the rank-0 shard, %s, %d reps, %.1f s"
                       % (nvar, len(sample) / 1e6, desc, reps, t)}
 
