@@ -40,6 +40,7 @@ METRIC = "variant-records/sec (and GB/s vs HBM roofline), 427K var × 2504 samp"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 FP4_PEAK_TOPS = 10000.0  # MI355X_MICROARCH.md: block-scaled FP4 MFMA = 4x the BF16 rate per clock, ~10 PF dense
 PMC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
+MFMA_FILE = os.path.join(REPO, "profiles", "r02_ld_mfma.json")  # tools/pmc_mfma.py over a --pmc pass
 
 
 def parse():
@@ -377,6 +378,13 @@ def main():
             roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP4_PEAK_TOPS, "unit": "TOP/s",
                     "frac": ach / FP4_PEAK_TOPS, "traffic": pmc_traffic("ld", dom),
                     "algorithmic_ops_per_launch": algo[dom], "avg_launch_ms": kernels[dom]}
+            try:  # MFMA-busy fraction of the SIMD cycles (committed PMC pass, profiles/)
+                with open(MFMA_FILE) as f:
+                    m = json.load(f)["mean"]
+                roof["mfma_util_pmc"] = {"util": m["mfma_util"], "clock_ghz": m["clock_ghz"],
+                                         "source": os.path.relpath(MFMA_FILE, REPO)}
+            except (OSError, KeyError, ValueError):
+                pass
         else:
             tb = s.text_bytes
             algo = {   # algorithmic bytes per launch

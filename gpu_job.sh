@@ -55,3 +55,11 @@ if [ "$MODE" = rehearse ]; then
         --dist-backend gloo --no-cpu-baseline --no-e2e || exit $?
 fi
 echo "=== done"
+
+if [ "$MODE" = mfma ]; then
+    # LD MFMA utilisation: MFMA-busy cycles, wave activity and the GPU clock, one pass
+    timeout -k 5 60 rocprofv3 -L > gpurun_out/rocprof_counters.txt 2>&1 || true
+    step pmc_ld_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
+        -d gpurun_out/pmc_ld_mfma -o run --output-format csv -- \
+        python bench.py --workload ld --steps 2 --warmup 1 --no-cpu-baseline --no-e2e || exit $?
+fi
