@@ -19,7 +19,7 @@ TOOL_OBJS := $(sort $(B)/obj/hostio.o $(patsubst $(TOOL_SRC)/%.cpp,$(B)/obj/%.o,
 TOOL_BINS := $(foreach t,$(TOOLS),$(B)/src/$(t)/$(t))
 
 all: $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so \
-     $(B)/libvcfx_core.so $(B)/libvcfx_core.a
+     $(B)/libvcfx_core.so $(B)/libvcfx_core.a $(B)/libvcfx_record_filter.so $(B)/libvcfx_genotype_query.so
 
 $(B)/obj/%.o: $(HOST_SRC)/%.cpp $(wildcard $(HOST_SRC)/*.h) include/vcfx_gpu.h
 	@mkdir -p $(dir $@)
@@ -40,6 +40,15 @@ $(B)/libvcfx_core.a: $(B)/obj/core/vcfx_core.o
 
 $(B)/libvcfx_tools.so: $(TOOL_OBJS) $(B)/libvcfx_gpu.so
 	$(CXX) -shared -o $@ $(TOOL_OBJS) -L$(B) -lvcfx_gpu -lz -Wl,-rpath,'$$ORIGIN'
+
+# the reference's per-tool library interfaces (include/vcfx_record_filter.h,
+# include/vcfx_genotype_query.h): one library each, as each declares its own printHelp()
+API_SRC := vcfx_amd/csrc/api
+$(B)/obj/api_%.o: $(API_SRC)/%_api.cpp include/vcfx_%.h $(wildcard $(TOOL_SRC)/*.h) $(wildcard $(HOST_SRC)/*.h)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c -o $@ $<
+$(B)/libvcfx_%.so: $(B)/obj/api_%.o $(B)/libvcfx_tools.so
+	$(CXX) -shared -o $@ $< -L$(B) -lvcfx_tools -lvcfx_gpu -Wl,-rpath,'$$ORIGIN'
 
 # drop-in executables at build/src/VCFX_<t>/VCFX_<t> (the reference test scripts' layout)
 $(B)/src/%: $(TOOL_SRC)/binary_main.cpp $(B)/libvcfx_tools.so

@@ -43,7 +43,8 @@ enum vcfxg_line_status {
     VCFXG_LINE_ROW = 1,      /* data line that produces output (AF row / kept record) */
     VCFXG_LINE_DROP = 2,     /* data line evaluated and not kept (filters) */
     VCFXG_LINE_WARN = 3,     /* data line the tool reports on stderr ("fewer than 9 fields") */
-    VCFXG_LINE_HEADER = 4    /* '#' line (pass-through tools print it) */
+    VCFXG_LINE_HEADER = 4,   /* '#' line (pass-through tools print it) */
+    VCFXG_LINE_RECHECK = 5   /* vcfxg_record_filter_ex: the line needs strtod's prefix value (host) */
 };
 
 typedef struct {
@@ -158,6 +159,15 @@ typedef struct {
  * evaluateLine / evaluateCriterion (VCFX_record_filter.cpp:333-401), extractField :207-229,
  * extractInfoValue :234-267, parseDouble :273-299 per record. */
 int vcfxg_record_filter(vcfxg_ctx *ctx, const vcfxg_criterion *crit, int n, int and_logic, vcfxg_summary *out);
+/* The same with the legacy free-function semantics available (VCFX_record_filter.h:99-102,
+ * .cpp:668-805, which no tool calls): flags VCFXG_RF_KEEP_CR evaluates each line with its
+ * trailing '\r' (processVCF reads with std::getline); criterion target 4 is QUAL as recordPasses
+ * treats it in OR mode (an unparsable QUAL compares as whatever strtod made of it: such lines
+ * get status VCFXG_LINE_RECHECK for the caller to decide); a numeric FILTER criterion is passed
+ * by the caller as the string criterion recordPasses makes of it. */
+#define VCFXG_RF_KEEP_CR 1
+int vcfxg_record_filter_ex(vcfxg_ctx *ctx, const vcfxg_criterion *crit, int n, int and_logic, int flags,
+                           vcfxg_summary *out);
 
 /* Fused `VCFX_record_filter ... | VCFX_genotype_query ...`: the filter as above, then the
  * genotype query on the lines the filter keeps, evaluated as the filter prints them ('\r'

@@ -916,7 +916,7 @@ static int compile_criteria(vcfxg_ctx *c, const vcfxg_criterion *crit, int n) {
     return VCFXG_OK;
 }
 
-static int run_rf(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and_logic) {
+static int run_rf(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and_logic, int keep_cr = 0) {
     int r = ensure(c, c->status, c->n_lines + 1);
     if (!r) r = compile_criteria(c, crit, n);
     if (r) return r;
@@ -924,17 +924,24 @@ static int run_rf(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and_logi
     HIPCHK(c, vcfxg::launch_rf_records(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
                                        P<uint64_t>(c->d_nlines), c->n_lines, P<vcfxg::RfCrit>(c->crit), n, and_logic,
                                        P<char>(c->pool), P<uint8_t>(c->status), P<unsigned long long>(c->counters),
-                                       c->stream));
+                                       c->stream, keep_cr));
     prof_end(c, "rf_records");
     return VCFXG_OK;
 }
 
 int vcfxg_record_filter(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and_logic, vcfxg_summary *out) {
-    if (!c || n < 0 || (n && !crit)) return VCFXG_E_ARG;
+    return vcfxg_record_filter_ex(c, crit, n, and_logic, 0, out);
+}
+
+int vcfxg_record_filter_ex(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and_logic, int flags,
+                           vcfxg_summary *out) {
+    if (!c || n < 0 || (n && !crit) || (flags & ~VCFXG_RF_KEEP_CR)) return VCFXG_E_ARG;
+    for (int k = 0; k < n; k++)
+        if (crit[k].target < 0 || crit[k].target > vcfxg::RF_QUAL_LENIENT) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
-    int r = run_rf(c, crit, n, and_logic);
+    int r = run_rf(c, crit, n, and_logic, (flags & VCFXG_RF_KEEP_CR) ? 1 : 0);
     if (r) return r;
     static thread_local uint64_t host_cnt[2];
     HIPCHK(c, hipMemcpyAsync(host_cnt, c->counters.p, 16, hipMemcpyDeviceToHost, c->stream));

@@ -7,7 +7,11 @@
 
 namespace vcfxg {
 
-enum { RF_POS = 0, RF_QUAL = 1, RF_FILTER = 2, RF_INFO = 3 };
+// RF_QUAL_LENIENT: the legacy free function recordPasses in OR mode (VCFX_record_filter.cpp:
+// 736-739) compares whatever strtod made of an unparsable QUAL; the device flags such lines
+// for the host (vcfxg_record_filter_ex status VCFXG_LINE_RECHECK) instead of restating strtod's
+// prefix rules
+enum { RF_POS = 0, RF_QUAL = 1, RF_FILTER = 2, RF_INFO = 3, RF_QUAL_LENIENT = 4 };
 
 struct RfCrit {
     int target, op, numeric;
@@ -40,7 +44,7 @@ __device__ __forceinline__ bool bytes_eq(const B &buf, int64_t p, int64_t n, con
 
 template <class B, class PB>
 __device__ inline bool eval_crit(const B &buf, const int64_t *t, int nt, int64_t ls, int64_t ae, const RfCrit &c,
-                                 const PB &pool) {
+                                 const PB &pool, bool *recheck = nullptr) {
     bool parsed;
     switch (c.target) {
     case RF_POS: {
@@ -48,10 +52,13 @@ __device__ inline bool eval_crit(const B &buf, const int64_t *t, int nt, int64_t
         if (f.e <= f.p) return false;
         return num_compare(buf, f.p, f.e, c.T, c.op, pool, &parsed);
     }
-    case RF_QUAL: {
+    case RF_QUAL:
+    case RF_QUAL_LENIENT: {
         Field f = field_of(t, nt, ls, ae, 5);
         if (f.e <= f.p || (f.e - f.p == 1 && buf[f.p] == '.')) return cmp_double(0.0, c.op, c.T.t);
-        return num_compare(buf, f.p, f.e, c.T, c.op, pool, &parsed);
+        const bool res = num_compare(buf, f.p, f.e, c.T, c.op, pool, &parsed);
+        if (c.target == RF_QUAL_LENIENT && !parsed && recheck) *recheck = true;
+        return res;
     }
     case RF_FILTER: {
         if (c.numeric) return false;
@@ -100,30 +107,31 @@ __device__ inline bool eval_crit(const B &buf, const int64_t *t, int nt, int64_t
 // RfCrit), B / PB: byte sources as in vcfxg_num.h
 template <class B, class CS, class PB>
 __device__ inline bool rf_eval(const B &buf, const int64_t *t, int nt, int64_t ls, int64_t ae, const CS &crit,
-                               int ncrit, int and_logic, const PB &pool) {
+                               int ncrit, int and_logic, const PB &pool, bool *recheck = nullptr) {
     bool res = and_logic ? true : false;
     for (int k = 0; k < ncrit && res == (bool)and_logic; k++) {
         const RfCrit c = crit[k];
-        res = eval_crit(buf, t, nt, ls, ae, c, pool);
+        res = eval_crit(buf, t, nt, ls, ae, c, pool, recheck);
     }
     return res;
 }
 // the same for the data line [ls, ae) ('\r' already stripped): one thread, byte loop
 __device__ inline bool rf_line(const char *__restrict__ buf, int64_t ls, int64_t ae, const RfCrit *__restrict__ crit,
-                               int ncrit, int and_logic, const char *__restrict__ pool) {
+                               int ncrit, int and_logic, const char *__restrict__ pool, bool *recheck = nullptr) {
     int64_t t[8];
     int nt = 0;
     for (int64_t p = ls; p < ae && nt < 8; p++)
         if (buf[p] == '\t') t[nt++] = p;
-    return rf_eval(buf, t, nt, ls, ae, crit, ncrit, and_logic, pool);
+    return rf_eval(buf, t, nt, ls, ae, crit, ncrit, and_logic, pool, recheck);
 }
 
 hipError_t launch_vc_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int strip_cr, uint8_t *status, unsigned long long *counters,
                              hipStream_t s);
+// keep_cr: evaluate each line with its trailing '\r' (the legacy processVCF's getline lines)
 hipError_t launch_rf_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, const RfCrit *crit, int ncrit, int and_logic, const char *pool,
-                             uint8_t *status, unsigned long long *counters, hipStream_t s);
+                             uint8_t *status, unsigned long long *counters, hipStream_t s, int keep_cr = 0);
 
 // ---- the filter / query walk (vcfxg_fq_walk.hip): record_filter (kFqRF), genotype_query
 // (kFqGQ) or the fused pipeline (kFqBoth) in one pass without a separate line index

@@ -11,12 +11,13 @@
 
 namespace vcfxg {
 
-// status: 0 empty (after '\r' strip; printed as "\n"), 4 header, 1 kept, 2 dropped
+// status: 0 empty (after '\r' strip; printed as "\n"), 4 header, 1 kept, 2 dropped, 5 to be
+// decided on the host (an RF_QUAL_LENIENT criterion met an unparsable QUAL)
 __global__ __launch_bounds__(256) void k_rf_records(const char *__restrict__ buf, int64_t data_start,
                                                     const uint64_t *__restrict__ line_end, const uint64_t *n_lines_p,
                                                     const RfCrit *__restrict__ crit, int ncrit, int and_logic,
                                                     const char *__restrict__ pool, uint8_t *__restrict__ status,
-                                                    unsigned long long *__restrict__ counters) {
+                                                    unsigned long long *__restrict__ counters, int keep_cr) {
     __shared__ uint32_t cnt[2];
     if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -25,15 +26,16 @@ __global__ __launch_bounds__(256) void k_rf_records(const char *__restrict__ buf
     for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < n; li += gridDim.x * (uint64_t)blockDim.x) {
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
         int64_t ae = (int64_t)line_end[li];
-        if (ae > ls && buf[ae - 1] == '\r') ae--;  // :454-456 / :509-511
+        if (!keep_cr && ae > ls && buf[ae - 1] == '\r') ae--;  // :454-456 / :509-511
         uint8_t st;
         if (ae == ls) st = 0;
         else if (buf[ls] == '#') st = 4;
         else {
             data++;
-            const bool res = rf_line(buf, ls, ae, crit, ncrit, and_logic, pool);
-            st = res ? 1 : 2;
-            kept += res;
+            bool recheck = false;
+            const bool res = rf_line(buf, ls, ae, crit, ncrit, and_logic, pool, &recheck);
+            st = recheck ? 5 : (res ? 1 : 2);
+            kept += res && !recheck;
         }
         status[li] = st;
     }
@@ -96,12 +98,12 @@ hipError_t launch_vc_records(const char *buf, int64_t data_start, const uint64_t
 
 hipError_t launch_rf_records(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, const RfCrit *crit, int ncrit, int and_logic, const char *pool,
-                             uint8_t *status, unsigned long long *counters, hipStream_t s) {
+                             uint8_t *status, unsigned long long *counters, hipStream_t s, int keep_cr) {
     if (!n_lines_host) return hipSuccess;
     int64_t g = ((int64_t)n_lines_host + 255) / 256;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_rf_records, dim3((unsigned)g), dim3(256), 0, s, buf, data_start, line_end, n_lines_dev, crit,
-                       ncrit, and_logic, pool, status, counters);
+                       ncrit, and_logic, pool, status, counters, keep_cr);
     return hipGetLastError();
 }
 

@@ -137,6 +137,10 @@ bool run_gq(const Input &in, bool stream_mode, const std::string &q, bool strict
 
 }  // namespace
 
+namespace vcfxh {
+const char *gq_help_text() { return kHelp; }
+}  // namespace vcfxh
+
 extern "C" int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int out_fd, int err_fd) {
     Out out(out_fd), err(err_fd);
     // vcfx::handle_common_flags (vcfx_core.h:57-62)

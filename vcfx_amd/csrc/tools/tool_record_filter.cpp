@@ -182,6 +182,10 @@ bool run_rf(const Input &in, bool stdin_mode, const std::vector<Criterion> &cs, 
 
 }  // namespace
 
+namespace vcfxh {
+const char *rf_help_text() { return kHelp; }
+}  // namespace vcfxh
+
 extern "C" int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out_fd, int err_fd) {
     Out out(out_fd), err(err_fd);
     if (flag_present(argc, argv, "--help", "-h")) {

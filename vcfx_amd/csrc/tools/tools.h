@@ -22,6 +22,9 @@ struct Criterion {
     double value = 0.0;
 };
 bool compile_filter(const std::string &all, std::vector<Criterion> &out, Out &err);
+// the drop-ins' help texts (the library interfaces' printHelp)
+const char *rf_help_text();
+const char *gq_help_text();
 std::vector<vcfxg_criterion> to_abi(const std::vector<Criterion> &cs);
 
 // getopt_long prints its diagnostics on the C stderr stream; route them to the tool's

@@ -55,6 +55,7 @@ SIGNATURES = {
     "vcfxg_allele_freq_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_genotype_query": (_I, [_VP, _P, _S, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_record_filter": (_I, [_VP, _VP, _I, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_record_filter_ex": (_I, [_VP, _VP, _I, _I, _I, ctypes.POINTER(Summary)]),
     "vcfxg_variant_count": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
     "vcfxg_nonref_filter": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
     "vcfxg_nonref_filter_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
