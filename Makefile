@@ -15,10 +15,10 @@ TOOLS := VCFX_allele_freq_calc VCFX_genotype_query VCFX_record_filter VCFX_varia
 HOST_SRC := vcfx_amd/csrc/host
 TOOL_SRC := vcfx_amd/csrc/tools
 CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wno-unused-result -Iinclude -I$(HOST_SRC) -I$(TOOL_SRC)
-TOOL_OBJS := $(sort $(B)/obj/hostio.o $(patsubst $(TOOL_SRC)/%.cpp,$(B)/obj/%.o,$(wildcard $(TOOL_SRC)/tool_*.cpp)))
+TOOL_OBJS := $(sort $(B)/obj/hostio.o $(B)/obj/gz.o $(patsubst $(TOOL_SRC)/%.cpp,$(B)/obj/%.o,$(wildcard $(TOOL_SRC)/tool_*.cpp)))
 TOOL_BINS := $(foreach t,$(TOOLS),$(B)/src/$(t)/$(t))
 
-all: $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so \
+all: $(B)/bin/vcfx_bgzf $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so \
      $(B)/libvcfx_core.so $(B)/libvcfx_core.a $(B)/libvcfx_record_filter.so $(B)/libvcfx_genotype_query.so
 
 $(B)/obj/%.o: $(HOST_SRC)/%.cpp $(wildcard $(HOST_SRC)/*.h) include/vcfx_gpu.h
@@ -69,6 +69,10 @@ $(B)/libvcfx_gpu.so: $(GPU_OBJS)
 $(B)/bin/vcfx_synth: vcfx_amd/csrc/synth/vcfx_synth.c
 	@mkdir -p $(dir $@)
 	$(CC) -O2 -DVCFX_SYNTH_MAIN -o $@ $< -lpthread
+
+$(B)/bin/vcfx_bgzf: vcfx_amd/csrc/synth/vcfx_bgzf.c
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -o $@ $< -lz -lpthread
 
 $(B)/libvcfx_synth.so: vcfx_amd/csrc/synth/vcfx_synth.c
 	$(CC) -O2 -fPIC -shared -o $@ $< -lpthread

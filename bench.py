@@ -240,6 +240,22 @@ def e2e_rates(workload, arr, a):
             os.close(dn)
         runs["warm_context_file"] = {"value": a.records / min(walls[1:]), "wall_s": [round(w, 4) for w in walls[1:]],
                                      "note": "in-process vcfx_tool_main with the device context already open"}
+        # the BGZF (.vcf.gz) form of the same file: inflated on the host threads, then the device path
+        bgz = path + ".bgz"
+        subprocess.check_call([os.path.join(REPO, "build", "bin", "vcfx_bgzf"), path, bgz, "16", "1"])
+        try:
+            walls = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                r = subprocess.run([exe] + args + ["-i", bgz], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                   timeout=300)
+                walls.append(time.perf_counter() - t0)
+                assert r.returncode == 0, r.stderr[-500:]
+            runs["process_file_bgzf"] = {"value": a.records / min(walls), "wall_s": [round(w, 4) for w in walls],
+                                         "compressed_bytes": os.path.getsize(bgz),
+                                         "note": "BGZF level 1 (build/bin/vcfx_bgzf); inflate on <= 16 host threads"}
+        finally:
+            os.unlink(bgz)
         runs["pcie_ceiling"] = a.records / (arr.size / (PCIE_H2D_GBS * 1e9))
         runs["unit"] = "records/s"
         runs["cmd"] = "%s %s -i FILE > /dev/null (page-cache-warm %.2f GB file)" % (tool, " ".join(args), arr.size / 1e9)

@@ -50,7 +50,10 @@ class Inputs:
 
     def drop(self, name):
         if name in self.files:
-            os.unlink(self.files.pop(name)[0])
+            p = self.files.pop(name)[0]
+            os.unlink(p)
+            if os.path.exists(p + ".bgz"):
+                os.unlink(p + ".bgz")
 
     def close(self):
         for n in list(self.files):
@@ -125,6 +128,21 @@ def test_annotated_shard_matches_reference(inputs, case, stdin):
     _check(case, inputs, stdin)
     if case == "gq_strict_annot":
         inputs.drop("annot")
+
+
+@pytest.mark.parametrize("case", ["af_file", "pipeline_bench"])
+def test_bgzf_chr21_matches_reference(inputs, case):
+    """the same shard as BGZF (.vcf.gz, made by build/bin/vcfx_bgzf): inflated on the host
+    threads, then the device path; output identical to the reference's on the plain bytes"""
+    from vcfx_amd import BUILD
+    plain = inputs.path("chr21")
+    bgz = plain + ".bgz"
+    if not os.path.exists(bgz):
+        subprocess.check_call([os.path.join(BUILD, "bin", "vcfx_bgzf"), plain, bgz, "16", "1"])
+    c = DIG["cases"][case]
+    got, rc, err = _hash_cmd(_cmd(c["stages"], bgz))
+    assert rc == 0, err[-2000:]
+    assert got == c["stdout"], (case, got, err[-2000:])
 
 
 @pytest.mark.parametrize("case", ["ld1500_t02", "ld1500_t0", "ld1500_w300_t0", "ld3000_bench"])

@@ -1,6 +1,8 @@
 // hostio.cpp -- see hostio.h
 #include "hostio.h"
 
+#include "gz.h"
+
 #include <errno.h>
 #include <fcntl.h>
 #include <stdlib.h>
@@ -178,7 +180,63 @@ bool Input::open_file(const char *path) {
     mapped = true;
     map_base = m;
     map_len = n;
+    source_n = n;
+    if (gzip_ok && is_gzip(p, n) && gzip_enabled()) return true;  // decompress() takes it from here
     apply_view();
+    return true;
+}
+
+bool gzip_enabled() {
+    const char *e = getenv("VCFX_GZIP");
+    return !(e && e[0] == '0');
+}
+
+namespace {
+// an anonymous region of reserved address space (not memory), transparent huge pages
+void *reserve_region(size_t *cap) {
+    for (int sh : {40, 36, 32, 30}) {
+        *cap = (size_t)1 << sh;
+        void *m = mmap(nullptr, *cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+        if (m != MAP_FAILED) {
+            madvise(m, *cap, MADV_HUGEPAGE);
+            return m;
+        }
+    }
+    *cap = 0;
+    return nullptr;
+}
+}  // namespace
+
+bool Input::decompress(int err_fd) {
+    if (!gzip_ok || gz || host_n != n || !is_gzip(p, n) || !gzip_enabled()) return true;
+    join_populate();
+    size_t cap = 0;
+    void *m = reserve_region(&cap);
+    if (!m) {
+        write_str(err_fd, "Error: vcfx_amd: no address space for the decompressed input\n");
+        return false;
+    }
+    unsigned hw = std::thread::hardware_concurrency();
+    int threads = (int)std::max(1u, std::min(16u, hw ? hw : 1u));
+    if (const char *e = getenv("VCFX_THREADS")) threads = std::max(1, atoi(e));
+    phase("gzip inflate begin");
+    const GzResult r = gz_inflate(p, n, (char *)m, cap, threads);
+    phase(r.bgzf ? "gzip inflate end (BGZF, parallel)" : "gzip inflate end (sequential)");
+    if (!r.ok) {
+        write_str(err_fd, "Error: vcfx_amd: the gzip input is truncated or corrupt (" + std::to_string(r.n) +
+                              " bytes inflated)\n");
+        munmap(m, cap);
+        return false;
+    }
+    if (map_base && map_len) munmap(map_base, map_len);  // the compressed bytes
+    map_base = m;
+    map_len = cap;
+    p = (const char *)m;
+    n = host_n = r.n;
+    mapped = false;
+    gz = true;
+    tail = nullptr;
+    if (n >= prefetch_bytes()) gpu_prefetch();
     return true;
 }
 
@@ -253,7 +311,7 @@ void Input::read_fd(int fd, bool host_copy) {
                 map_base = m;
                 map_len = len;
                 p = (const char *)m + ((size_t)pos - lo);
-                n = host_n = (size_t)st.st_size - (size_t)pos;
+                n = host_n = source_n = (size_t)st.st_size - (size_t)pos;
                 lseek(fd, st.st_size, SEEK_SET);  // consumed, as by a read loop
                 return;
             }
@@ -285,6 +343,18 @@ void Input::read_fd(int fd, bool host_copy) {
     const size_t kPre = prefetch_bytes(), kChunk = stream_chunk();
     ssize_t k0 = read_full(fd, base, kPre);
     size_t got = k0 > 0 ? (size_t)k0 : 0;
+    if (gzip_ok && is_gzip(base, got) && gzip_enabled()) {
+        // compressed: all of it to the host (decompress() inflates it)
+        for (;;) {
+            if (cap - got < ((size_t)8 << 20)) break;
+            ssize_t k = ::read(fd, base + got, (size_t)8 << 20);
+            if (k < 0 && errno == EINTR) continue;
+            if (k <= 0) break;
+            got += (size_t)k;
+        }
+        n = host_n = source_n = got;
+        return;
+    }
     bool chrom = false;  // the head holds the complete '#CHROM' line
     size_t scanned = 0;
     auto scan = [&] {

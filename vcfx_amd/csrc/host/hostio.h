@@ -35,6 +35,12 @@ struct Input {
     size_t streamed = 0;
     std::vector<void *> ring;  // pinned staging slots of a device-only stream (freed with ring_ctx)
     vcfxg_ctx *ring_ctx = nullptr;
+    // compressed input: set by the tools that read .vcf.gz (the record
+    // tools; not VCFX_variant_counter, whose own gzip handling is the reference's) before
+    // open_file / read_fd; decompress() then inflates gzip / BGZF input in place
+    bool gzip_ok = false;
+    bool gz = false;          // the input was inflated
+    size_t source_n = 0;      // bytes of the file / stream as read (compressed size for gz)
     Input() = default;
     Input(const Input &) = delete;
     Input &operator=(const Input &) = delete;
@@ -57,6 +63,10 @@ struct Input {
     // the host): once the head holds the '#CHROM' line the rest of the pipe is read into a
     // pinned staging ring and copied to the device from there, never kept on the host.
     void read_fd(int fd, bool host_copy = true);
+    // gzip / BGZF input (magic 1f 8b) and gzip_ok, unless VCFX_GZIP=0: inflate it (BGZF members
+    // on every host thread) into a reserved region that becomes the input.  false (after an
+    // "Error: ..." line on err_fd) when the stream is truncated or corrupt.
+    bool decompress(int err_fd);
     // mapped inputs of 64 MiB and more: page-table population running on helper threads
     mutable std::vector<std::thread> populating;
     void populate(void *m, size_t len);
@@ -78,6 +88,8 @@ void phase(const char *what);
 extern bool g_process_exit_fast;
 // VCFX_VIEW_SKIP_HEADER=1: a shard rank other than the first (its header output is rank 0's)
 bool view_skip_header();
+// VCFX_GZIP=0 turns compressed-input support off (the reference's tools read .gz bytes as text)
+bool gzip_enabled();
 
 void write_all(int fd, const char *p, size_t n);
 inline void write_str(int fd, const std::string &s) { write_all(fd, s.data(), s.size()); }

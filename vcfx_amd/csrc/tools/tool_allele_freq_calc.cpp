@@ -109,6 +109,7 @@ extern "C" int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int 
     gs.done();
     if (!input && optind < argc) input = argv[optind];
     Input in;
+    in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
     uint64_t v = 0, l = 0;
     if (input) {
         phase("start");
@@ -116,12 +117,14 @@ extern "C" int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int 
             err.put(std::string("Error: Cannot open file: ") + input + "\n");
             return 1;
         }
-        if (!quiet) err.put(std::string("Processing ") + input + " (" + std::to_string(in.n / (1024 * 1024)) + " MB)\n");
+        if (!quiet) err.put(std::string("Processing ") + input + " (" + std::to_string(in.source_n / (1024 * 1024)) + " MB)\n");
+        if (!in.decompress(err.fd)) return 1;
         if (!run_af(in, VCFXG_MODE_FILE, quiet, out, err, &v, &l)) return 1;
         if (!quiet) err.put("Processed " + std::to_string(v) + " variants from " + std::to_string(l) + " data lines\n");
     } else {
         phase("start");
         in.read_fd(in_fd, /*host_copy=*/false);  // only the header is needed on the host
+        if (!in.decompress(err.fd)) return 1;
         phase("stdin read");
         if (in.n == 0) {
             out.put(kHelp);

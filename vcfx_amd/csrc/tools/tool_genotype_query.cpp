@@ -184,15 +184,18 @@ extern "C" int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int ou
         return 1;
     }
     Input in;
+    in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
     if (!input.empty()) {
         if (!in.open_file(input.c_str())) {
             err.put("Error: Cannot open file: " + input + "\n");
             return 1;
         }
+        if (!in.decompress(err.fd)) return 1;
         out.flush();
         return run_gq(in, false, query, strict, quiet, out_fd, err) ? 0 : 1;
     }
     in.read_fd(in_fd, /*host_copy=*/false);  // kept records are read back from the device
+    if (!in.decompress(err.fd)) return 1;
     phase("stdin read");
     out.flush();
     return run_gq(in, true, query, strict, quiet, out_fd, err) ? 0 : 1;

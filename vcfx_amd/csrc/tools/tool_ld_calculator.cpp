@@ -286,17 +286,20 @@ extern "C" int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out
     }
     out.flush();
     Input in;
+    in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
     if (!o.input.empty()) {
         if (!in.open_file(o.input.c_str()) || in.n == 0) {
             err.put("Error: cannot open file '" + o.input + "'\n");
             return 1;
         }
+        if (!in.decompress(err.fd)) return 1;
         if (o.matrix && o.shard_rank > 0) return 0;  // matrix mode is not sharded: rank 0 writes it
         bool ok = o.matrix ? run_ld_matrix(in, true, o.quiet, rchrom, has_region, rs, re, out_fd, err)
                            : run_stream(in, true, o, rchrom, has_region, rs, re, out_fd, err);
         return ok ? 0 : 1;
     }
     in.read_fd(in_fd);
+    if (!in.decompress(err.fd)) return 1;
     if (o.matrix && o.shard_rank > 0) return 0;
     bool ok = o.matrix ? run_ld_matrix(in, false, o.quiet, rchrom, has_region, rs, re, out_fd, err)
                        : run_stream(in, false, o, rchrom, has_region, rs, re, out_fd, err);

@@ -142,15 +142,18 @@ extern "C" int vcfx_tool_nonref_filter(int argc, char **argv, int in_fd, int out
         return 0;
     }
     Input in;
+    in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
     if (!input.empty() && input != "-") {
         if (!in.open_file(input.c_str())) {
             err.put("Error: Cannot open file: " + input + "\n");
             return 0;
         }
+        if (!in.decompress(err.fd)) return 1;
         out.flush();
         return run_nr(in, false, out_fd, err) ? 0 : 1;
     }
     in.read_fd(in_fd, /*host_copy=*/false);  // kept records are read back from the device
+    if (!in.decompress(err.fd)) return 1;
     phase("stdin read");
     out.flush();
     return run_nr(in, true, out_fd, err) ? 0 : 1;

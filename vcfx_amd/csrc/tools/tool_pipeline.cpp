@@ -25,6 +25,7 @@ extern "C" int vcfx_pipeline_filter_query(const char *filter, const char *logic,
     }
     const bool and_logic = strcmp(logic, "or") != 0;
     Input in;
+    in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
     bool stdin_mode = !input;
     if (input) {
         if (!in.open_file(input)) {
@@ -32,6 +33,7 @@ extern "C" int vcfx_pipeline_filter_query(const char *filter, const char *logic,
             return 1;
         }
     } else in.read_fd(in_fd, /*host_copy=*/false);  // kept records are read back from the device
+    if (!in.decompress(err.fd)) return 1;
     LineEmitter em(in.p, in.host_n, out_fd);
     std::vector<std::string> held;  // genotype_query's buffered header lines (copies)
     auto flush_held = [&]() {

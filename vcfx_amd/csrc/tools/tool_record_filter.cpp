@@ -241,16 +241,19 @@ extern "C" int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out
         return 1;
     }
     Input in;
+    in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
     out.flush();
     if (!input.empty() && input != "-") {
         if (!in.open_file(input.c_str())) {
             err.put("Error: cannot open file '" + input + "'\n");
             return 1;
         }
+        if (!in.decompress(err.fd)) return 1;
         if (in.n == 0) return 0;
         return run_rf(in, false, cs, and_logic, out_fd, err) ? 0 : 1;
     }
     in.read_fd(in_fd, /*host_copy=*/false);  // kept records are read back from the device
+    if (!in.decompress(err.fd)) return 1;
     phase("stdin read");
     return run_rf(in, true, cs, and_logic, out_fd, err) ? 0 : 1;
 }
