@@ -1891,6 +1891,210 @@ static int ld_main(int argc, char **argv, const char *in, size_t inn, ob_t *out,
 }
 
 /* ==================================================================================== */
+/* ==================================================================================== */
+/* VCFX_hwe_tester                                                 */
+/* ==================================================================================== */
+/* chi2_pvalue_1df, VCFX_hwe_tester.cpp:278-287 (Abramowitz-Stegun erfc, libm exp/sqrt) */
+double oracle_hwe_pvalue(int homRef, int het, int homAlt) {
+    /* calculateHWE_chisq :290-315 */
+    int N = homRef + het + homAlt;
+    if (N < 1) return 1.0;
+    double p = (2.0 * homRef + het) / (2.0 * N);
+    double q = 1.0 - p;
+    if (p <= 0.0 || p >= 1.0) return 1.0;
+    double eh = N * p * p, ee = N * 2.0 * p * q, ea = N * q * q;
+    double obs[3] = {homRef, het, homAlt}, ex[3] = {eh, ee, ea}, chi2 = 0.0;
+    for (int k = 0; k < 3; k++) {
+        double t = 0.0;
+        if (ex[k] > 0.0) {
+            double diff = fabs(obs[k] - ex[k]) - 0.5;
+            if (diff < 0.0) diff = 0.0;
+            t = (diff * diff) / ex[k];
+        }
+        chi2 = k == 0 ? t : chi2 + t;
+    }
+    if (chi2 <= 0.0) return 1.0;
+    if (chi2 > 700.0) return 0.0;
+    double x = sqrt(chi2 * 0.5);
+    double t = 1.0 / (1.0 + 0.3275911 * x);
+    double y = t * (0.254829592 + t * (-0.284496736 + t * (1.421413741 + t * (-1.453152027 + t * 1.061405429))));
+    return y * exp(-x * x);
+}
+/* OutputBuffer::appendDouble, VCFX_hwe_tester.cpp:236-268: truncated 6-digit fraction */
+size_t oracle_hwe_fmt_mmap(double val, char *buf) {
+    size_t k = 0;
+    if (val < 0) { buf[k++] = '-'; val = -val; }
+    long long ip = (long long)val;
+    double frac = val - ip;
+    char t[24]; int i = 0;
+    if (ip == 0) t[i++] = '0';
+    else while (ip > 0) { t[i++] = (char)('0' + ip % 10); ip /= 10; }
+    while (i > 0) buf[k++] = t[--i];
+    buf[k++] = '.';
+    for (int d = 0; d < 6; d++) {
+        frac *= 10.0;
+        int digit = (int)frac;
+        buf[k++] = (char)('0' + digit);
+        frac -= digit;
+    }
+    return k;
+}
+/* parseGenotypeForHWE :339-378: 0 homRef, 1 het, 2 homAlt, -1 otherwise */
+static int hwe_parse(const char *p, const char *end) {
+    if (p >= end) return -1;
+    const char *c = (const char *)memchr(p, ':', (size_t)(end - p));
+    if (c) end = c;
+    while (p < end && (*p == ' ' || *p == '\r')) p++;
+    if (p >= end || *p == '.') return -1;
+    if (*p < '0' || *p > '9') return -1;
+    int a1 = 0;
+    while (p < end && *p >= '0' && *p <= '9') { a1 = a1 * 10 + (*p - '0'); p++; }
+    if (p >= end || (*p != '/' && *p != '|')) return -1;
+    p++;
+    if (p >= end || *p == '.') return -1;
+    if (*p < '0' || *p > '9') return -1;
+    int a2 = 0;
+    while (p < end && *p >= '0' && *p <= '9') { a2 = a2 * 10 + (*p - '0'); p++; }
+    if (a1 > 1 || a2 > 1) return -1;
+    if (a1 == 0 && a2 == 0) return 0;
+    if (a1 == 1 && a2 == 1) return 2;
+    return 1;
+}
+/* skipToField / getField :321-336 (findTabSIMD = first '\t' in [p, end)) */
+static const char *hwe_skip(const char *p, const char *le, int idx) {
+    for (int i = 0; i < idx && p < le; i++) {
+        const char *t = (const char *)memchr(p, '\t', (size_t)(le - p));
+        if (!t) return NULL;
+        p = t + 1;
+    }
+    return p < le ? p : NULL;
+}
+static sv_t hwe_field(const char *ls, const char *le, int idx) {
+    const char *p = hwe_skip(ls, le, idx);
+    if (!p) return sv(NULL, 0);
+    const char *t = (const char *)memchr(p, '\t', (size_t)(le - p));
+    return sv(p, (size_t)((t ? t : le) - p));
+}
+static void hwe_count(const char *sp, const char *le, int *c) {
+    c[0] = c[1] = c[2] = 0;
+    while (sp < le) {
+        const char *nt = (const char *)memchr(sp, '\t', (size_t)(le - sp));
+        if (!nt) nt = le;
+        int g = hwe_parse(sp, nt);
+        if (g >= 0) c[g]++;
+        sp = nt + 1;
+    }
+}
+/* performHWE_Mmap :455-559 */
+static void hwe_mmap(const char *d, size_t n, ob_t *out) {
+    if (n == 0) return;
+    ob_puts(out, "CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n");
+    const char *p = d, *end = d + n;
+    while (p < end) {
+        const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
+        const char *le = nl ? nl : end;
+        size_t len = (size_t)(le - p);
+        if (len > 0 && p[len - 1] == '\r') len--;
+        const char *ae = p + len;
+        if (len == 0 || *p == '#') { p = le + 1; continue; }
+        sv_t f[5];
+        for (int k = 0; k < 5; k++) f[k] = hwe_field(p, ae, k);
+        sv_t fmt = hwe_field(p, ae, 8);
+        const char *ss = hwe_skip(p, ae, 9);
+        if (f[0].n == 0 || f[1].n == 0 || f[4].n == 0 || memchr(f[4].p, ',', f[4].n) ||
+            fmt.n < 2 || memcmp(fmt.p, "GT", 2) != 0 || !ss) { p = le + 1; continue; }
+        int c[3];
+        hwe_count(ss, ae, c);
+        for (int k = 0; k < 5; k++) { ob_put(out, f[k].p, f[k].n); ob_putc(out, '\t'); }
+        char b[40];
+        ob_put(out, b, oracle_hwe_fmt_mmap(oracle_hwe_pvalue(c[0], c[1], c[2]), b));
+        ob_putc(out, '\n');
+        p = le + 1;
+    }
+}
+/* performHWE_Stdin :565-608 (split_tabs: a trailing tab is an empty last field) */
+static void hwe_stdin(const char *d, size_t n, ob_t *out) {
+    ob_puts(out, "CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n");
+    lines_t it = {d, d + n};
+    const char *ls, *le;
+    while (next_line(&it, &ls, &le)) {
+        if (le == ls) continue;
+        if (le[-1] == '\r') le--;
+        if (le == ls || *ls == '#') continue;
+        sv_t f[10];
+        size_t nf = 0;
+        const char *q = ls;
+        for (;;) {
+            const char *t = (const char *)memchr(q, '\t', (size_t)(le - q));
+            if (nf < 10) f[nf] = sv(q, (size_t)((t ? t : le) - q));
+            nf++;
+            if (!t) break;
+            q = t + 1;
+        }
+        if (nf < 10 || memchr(f[4].p, ',', f[4].n) || f[8].n < 2 || memcmp(f[8].p, "GT", 2) != 0) continue;
+        int c[3] = {0, 0, 0};
+        hwe_count(f[9].p, le, c);
+        if (f[9].p == le) c[0] = c[1] = c[2] = 0;  /* a lone empty sample field */
+        for (int k = 0; k < 5; k++) { ob_put(out, f[k].p, f[k].n); ob_putc(out, '\t'); }
+        ob_printf(out, "%.6f\n", oracle_hwe_pvalue(c[0], c[1], c[2]));
+    }
+}
+static void hwe_help(ob_t *o) {  /* displayHelp :394-412 */
+    ob_puts(o,
+        "VCFX_hwe_tester: Perform Hardy-Weinberg Equilibrium (HWE) tests on a biallelic VCF.\n\n"
+        "Usage:\n"
+        "  VCFX_hwe_tester [options] [input.vcf]\n"
+        "  VCFX_hwe_tester [options] < input.vcf\n\n"
+        "Options:\n"
+        "  -i, --input FILE   Input VCF file (uses memory-mapping for best performance)\n"
+        "  -q, --quiet        Suppress informational messages\n"
+        "  -h, --help         Show this help.\n\n"
+        "Description:\n"
+        "  Reads each variant line, ignoring multi-allelic calls. For biallelic lines,\n"
+        "  collects genotypes as 0/0, 0/1, 1/1, then uses chi-square test with Yates'\n"
+        "  continuity correction to produce a p-value for HWE.\n\n"
+        "Performance:\n"
+        "  Uses memory-mapped I/O and SIMD for ~20x speedup over stdin mode.\n\n"
+        "Example:\n"
+        "  VCFX_hwe_tester -i input.vcf > results.txt\n"
+        "  VCFX_hwe_tester < input.vcf > results.txt\n");
+}
+/* main :688-694 -> VCFXHWETester::run :614-641, parseArgs :414-449 */
+static int hwe_main(int argc, char **argv, const char *in, size_t inn, ob_t *out, ob_t *err) {
+    if (common_flags(argc, argv, "VCFX_hwe_tester", hwe_help, out)) return 0;
+    const char *input = NULL;
+    int quiet = 0, help = 0;
+    static struct option lo[] = {{"help", no_argument, NULL, 'h'},
+                                 {"input", required_argument, NULL, 'i'},
+                                 {"quiet", no_argument, NULL, 'q'},
+                                 {NULL, 0, NULL, 0}};
+    optind = 0;
+    errcap_t ec;
+    errcap_begin(&ec);
+    int opt;
+    while ((opt = getopt_long(argc, argv, "hi:q", lo, NULL)) != -1) {
+        if (opt == 'i') input = optarg;
+        else if (opt == 'q') quiet = 1;
+        else help = 1;
+    }
+    errcap_end(&ec, err);
+    if (!input && optind < argc) input = argv[optind];
+    if (help) { hwe_help(out); return 0; }
+    if (input) {
+        char *d; size_t n;
+        if (read_file(input, &d, &n) < 0) {
+            ob_printf(err, "Error: Cannot open file: %s\n", input);
+            return 1;
+        }
+        if (!quiet) ob_printf(err, "Processing %s (%zu bytes)...\n", input, n);
+        hwe_mmap(d, n, out);
+        free(d);
+    } else {
+        hwe_stdin(in, inn, out);
+    }
+    return 0;
+}
+
 int oracle_main(const char *tool, int argc, char **argv, const char *in, size_t inn, oracle_result *res) {
     ob_t out = {0}, err = {0};
     int rc;
@@ -1902,6 +2106,7 @@ int oracle_main(const char *tool, int argc, char **argv, const char *in, size_t 
     else if (strcmp(t, "VCFX_record_filter") == 0) rc = rf_main(argc, argv, in, inn, &out, &err);
     else if (strcmp(t, "VCFX_ld_calculator") == 0) rc = ld_main(argc, argv, in, inn, &out, &err);
     else if (strcmp(t, "VCFX_nonref_filter") == 0) rc = nr_main(argc, argv, in, inn, &out, &err);
+    else if (strcmp(t, "VCFX_hwe_tester") == 0) rc = hwe_main(argc, argv, in, inn, &out, &err);
     else return -1;
     res->out = out.p ? out.p : (char *)calloc(1, 1);
     res->out_len = out.n;

@@ -54,6 +54,11 @@ int oracle_ld_parse_gt_raw(const char *s, size_t len);
 size_t oracle_fmt_fixed4(double v, char *buf);
 size_t oracle_fmt_double4(double v, char *buf);
 
+/* VCFX_hwe_tester: calculateHWE_chisq (VCFX_hwe_tester.cpp:290-315, libm exp/sqrt) and the
+ * mmap path's 6-digit truncating appendDouble (:236-268). */
+double oracle_hwe_pvalue(int homRef, int het, int homAlt);
+size_t oracle_hwe_fmt_mmap(double v, char *buf);
+
 #ifdef __cplusplus
 }
 #endif

@@ -24,6 +24,7 @@ INLINE_MAX = 16 * 1024
 AF, RF, GQ, LD, VC = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query",
                       "VCFX_ld_calculator", "VCFX_variant_counter")
 NR = "VCFX_nonref_filter"
+HWE = "VCFX_hwe_tester"
 
 
 def fixtures():
@@ -124,6 +125,16 @@ def build_cases():
               ["data/nope.vcf"]):
         add(NR, a)
     add(NR, [], stdin="data/empty.vcf", tag="empty_stdin")
+    # ---- hwe_tester: the shared fixtures, the reference's own hwe fixtures, the traps
+    hwe_dir = os.path.join(HERE, "data", "ref_hwe")
+    for f in vcfs + [os.path.join("data", "ref_hwe", n) for n in sorted(os.listdir(hwe_dir))]:
+        add(HWE, ["-i", f])
+        add(HWE, ["-q", f])
+        add(HWE, [], stdin=f)
+    for a in (["-h"], ["--help"], ["-v"], ["--version"], ["--bogus"], ["-x"], ["-i"], ["-i", "data/nope.vcf"],
+              ["data/nope.vcf"], ["-i", "data/empty.vcf"]):
+        add(HWE, a)
+    add(HWE, [], stdin="data/empty.vcf", tag="empty_stdin")
     return cases
 
 

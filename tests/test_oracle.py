@@ -19,7 +19,8 @@ def oracle():
 
 def test_case_count():
     tools = collections.Counter(c["tool"] for c in CASES)
-    assert len(tools) == 6 and min(tools.values()) > 40  # the five hot-path tools + nonref_filter (8(f))
+    # the five hot-path tools + nonref_filter and hwe_tester (8(f) rank 2)
+    assert len(tools) == 7 and min(tools.values()) > 40
 
 
 @pytest.mark.parametrize("tool", sorted({c["tool"] for c in CASES}))
@@ -74,6 +75,22 @@ def test_oracle_matches_reference_committed_expected(oracle, argv, stdin, expect
         assert [l.split() for l in out.splitlines()] == [l.split() for l in want.splitlines()]
     else:
         assert out == want
+
+
+# tests/test_hwe_tester.sh:46-80: `$EXEC < input` against the inline expected text (echo -e adds
+# the final newline); the inputs are the files the script writes (tests/data/hwe_tester/)
+HWE_KNOWN = [("basic_hwe", b"CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n1\t100\trs1\tA\tG\t1.000000\n"),
+             ("multi_allelic", b"CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n"),
+             ("missing_genotypes", b"CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n1\t100\trs1\tA\tG\t1.000000\n"),
+             ("genotype_formats", b"CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n1\t100\trs1\tA\tG\t1.000000\n"),
+             ("no_gt_field", b"CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n")]
+
+
+@pytest.mark.parametrize("name,want", HWE_KNOWN)
+def test_hwe_known_answers(oracle, name, want):
+    data = open(os.path.join(GOLDEN, "data", "ref_hwe", name + ".vcf"), "rb").read()
+    out, _, rc = oracle.run(["VCFX_hwe_tester"], data)
+    assert (out, rc) == (want, 0)
 
 
 def test_af_known_answers(oracle):
