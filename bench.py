@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("af", "pipeline", "ld", "nonref"), default="af")
+    ap.add_argument("--workload", choices=("af", "pipeline", "ld", "nonref", "hwe"), default="af")
     ap.add_argument("--records", type=int, default=None, help="records per GPU (default per workload)")
     ap.add_argument("--samples", type=int, default=2504)
     ap.add_argument("--window", type=int, default=100000, help="ld: window in variants")
@@ -126,6 +126,9 @@ def cpu_baseline(workload, arr, offs, a):
         elif workload == "nonref":
             argvs = [["VCFX_nonref_filter", "-i", f.name]]
             desc = "VCFX_nonref_filter -i (file path)"
+        elif workload == "hwe":
+            argvs = [["VCFX_hwe_tester", "-q", "-i", f.name]]
+            desc = "VCFX_hwe_tester -q -i (file path)"
         elif workload == "pipeline":
             argvs = [["VCFX_record_filter", "--filter", "QUAL>=30;FILTER==PASS", "-i", f.name],
                      ["VCFX_genotype_query", "--genotype-query", "0|1"]]
@@ -159,7 +162,7 @@ def output_check(workload, eng, s, a, rank):
             dig = json.load(f)
     except OSError:
         return {"checked": False, "why": "no tests/golden/full_digests.json"}
-    default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "ld": 100000}[workload]
+    default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "hwe": 427409, "ld": 100000}[workload]
     if rank != 0 or a.records != default or a.samples != 2504 or (workload == "ld" and (a.window < 3000 or
                                                                                          a.threshold != 0.5)):
         return {"checked": False, "why": "no reference digest for this rank/configuration"}
@@ -167,6 +170,14 @@ def output_check(workload, eng, s, a, rank):
         c = dig["cases"]["af_file"]
         got = hashlib.sha256(b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes)).hexdigest()
         want, what = c["stdout"]["sha256"], "sha256 of the AF rows vs VCFX_allele_freq_calc -q -i (reference)"
+    elif workload == "hwe":
+        if "hwe_file" not in dig["cases"]:
+            return {"checked": False, "why": "no hwe_file digest"}
+        c = dig["cases"]["hwe_file"]
+        if eng.hwe_rechecks():
+            return {"checked": False, "why": "rows left to the host p-value (not in the device text)"}
+        got = hashlib.sha256(b"CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n" + eng.text(s.text_bytes)).hexdigest()
+        want, what = c["stdout"]["sha256"], "sha256 of the HWE rows vs VCFX_hwe_tester -q -i (reference)"
     elif workload in ("pipeline", "nonref"):
         c = dig["cases"]["pipeline_bench" if workload == "pipeline" else "nonref_file"]
         keep = (eng.statuses(s.n_lines) == 1).astype(np.uint8)
@@ -202,6 +213,8 @@ def e2e_rates(workload, arr, a):
         tool, args = "VCFX_allele_freq_calc", ["-q"]
     elif workload == "nonref":
         tool, args = "VCFX_nonref_filter", []
+    elif workload == "hwe":
+        tool, args = "VCFX_hwe_tester", ["-q"]
     elif workload == "pipeline":
         tool, args = "VCFX_record_filter", ["--filter", "QUAL>=30;FILTER==PASS"]
     else:
@@ -316,6 +329,14 @@ def main():
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.general_records])
             return s
         kern_names = ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "nr_records")
+    elif a.workload == "hwe":
+        def step():
+            s = eng.hwe_region(ds, engine.MODE_FILE)  # (the walk) genotype classes + row rules + rows
+            if red is not None:
+                allreduce_counts([s.n_lines, s.rows, s.text_bytes, s.general_records])
+            return s
+        kern_names = ("hwe_walk", "walk_compact", "hwe_lines", "hwe_rows", "hwe_format", "line_count", "line_emit",
+                      "line_compact")
     elif a.workload == "pipeline":
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
@@ -379,6 +400,8 @@ def main():
         assert s.rows > 0 and s.n_lines == a.records, (s.rows, s.n_lines)
         if a.workload == "af":
             assert s.rows == a.records and s.general_records == 0
+        if a.workload == "hwe":
+            assert s.general_records == 0
         units_total = a.records * world
         unit, metric = "records/s", METRIC
     value = units_total * a.steps / dt
@@ -411,6 +434,8 @@ def main():
                 # (line_end 8, counts/prefix/status 13, head record 16); the compaction reads
                 # and rewrites them dense; the per-line rest reads head record + status
                 "af_walk": region_bytes + L * (8 + 13 + 16),
+                # HWE: the same walk with three class counts per line (8 + 17 + 16)
+                "hwe_walk": region_bytes + L * (8 + 17 + 16),
                 "walk_compact": L * 2 * (8 + 13 + 16),
                 "af_complex": L * (16 + 1),
                 "af_format": tb + L * (8 + 8 + 13) + s.rows * 40,
@@ -438,6 +463,8 @@ def main():
                         "--genotype-query '0|1' fused, device-resident %d x %d shard per GPU" % (a.records, a.samples),
             "nonref": "VCFX_nonref_filter -i (file path) on a device-resident %d x %d shard per GPU: the walk "
                       "with the per-record all-samples-hom-ref test" % (a.records, a.samples),
+            "hwe": "VCFX_hwe_tester -i (file path) on a device-resident %d x %d shard per GPU: the walk with the "
+                   "genotype-class reducer + HWE chi-square p-value rows" % (a.records, a.samples),
             "ld": "VCFX_ld_calculator -w %d -t %g streaming on a device-resident %d x %d shard per GPU: parse + "
                   "FP4-MFMA pair sums (count + emit) + pair text" % (a.window, a.threshold, a.records, a.samples),
         }[a.workload]

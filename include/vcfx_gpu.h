@@ -204,6 +204,29 @@ int vcfxg_nonref_filter(vcfxg_ctx *ctx, int mode, vcfxg_summary *out);
  * query walk with the nonref reducer; index + vcfxg_nonref_filter for short records). */
 int vcfxg_nonref_filter_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
 
+/* ---- VCFX_hwe_tester (a per-sample GT reducer on the same path) -------
+ * Over the data region from data_start (the caller passes the end of the leading '#' lines,
+ * as performHWE_Mmap's header loop :466-472 skips them): per data line the genotype classes
+ * of parseGenotypeForHWE (VCFX_hwe_tester.cpp:339-378) over every sample, the row rules of
+ * performHWE_Mmap (:475-558, mode VCFXG_MODE_FILE) or performHWE_Stdin (:572-607, mode
+ * VCFXG_MODE_STDIN), and the rows "CHROM\tPOS\tID\tREF\tALT\t<p>\n" with the p-value of
+ * calculateHWE_chisq (:278-315) as appendDouble's truncated 6 digits (:236-268, file) or
+ * setprecision(6) (stdin).  Text via vcfxg_fetch_text (without the column header line);
+ * rows = output rows, general_records = lines off the fixed-stride sweep.  For long records the
+ * device walks them as for the allele frequencies (one HBM pass).
+ * The p-value's exp() is the device's: a row whose 6 digits it cannot settle (the values a few
+ * ulps either side print differently; practically never) is listed by vcfxg_hwe_rechecks, and
+ * the caller writes the 8 bytes at text_offset from the host libm's value of the same counts. */
+typedef struct {
+    uint64_t text_offset; /* offset of the row's 8 p-value bytes in the fetched text */
+    int32_t hom_ref, het, hom_alt;
+    int32_t reserved;
+} vcfxg_hwe_recheck;
+int vcfxg_hwe_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
+/* rows of the last vcfxg_hwe_region call that need the host's p-value: *n = their number,
+ * the first min(*n, cap) copied to out (any order) */
+int vcfxg_hwe_rechecks(vcfxg_ctx *ctx, vcfxg_hwe_recheck *out, uint64_t cap, uint64_t *n);
+
 /* ---- variant counter -------------------------------------------------------------------
  * Per line status: ROW = data line with >= 8 tab-separated columns (counted), WARN = fewer
  * columns, SKIP = empty or '#'.  strip_cr: drop a trailing '\r' first (file path).

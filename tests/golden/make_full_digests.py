@@ -48,8 +48,8 @@ INPUTS = {
     "ld3000": dict(n_records=3000, n_samples=2504, seed=20251226, hap_blocks=1),
 }
 
-AF, RF, GQ, LD, NR = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query", "VCFX_ld_calculator",
-                      "VCFX_nonref_filter")
+AF, RF, GQ, LD, NR, HWE = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query",
+                           "VCFX_ld_calculator", "VCFX_nonref_filter", "VCFX_hwe_tester")
 
 # name -> (input, [stage argv ...] with "{F}" for the file; the first stage reads stdin when
 # it has no {F}), keep-mask flag
@@ -57,6 +57,8 @@ CASES = {
     "af_file": ("chr21", [[AF, "-q", "-i", "{F}"]], False),
     "af_stdin": ("chr21", [[AF, "-q"]], False),
     "nonref_file": ("chr21", [[NR, "-i", "{F}"]], True),
+    "hwe_file": ("chr21", [[HWE, "-q", "-i", "{F}"]], False),
+    "hwe_stdin": ("chr21", [[HWE]], False),
     "pipeline_bench": ("chr21", [[RF, "--filter", "QUAL>=30;FILTER==PASS", "-i", "{F}"],
                                  [GQ, "--genotype-query", "0|1"]], True),
     "pipeline_annot": ("annot", [[RF, "--filter", "FILTER==PASS;AF>=0.01", "-i", "{F}"],

@@ -44,15 +44,41 @@ namespace vcfxg {
 #endif
 constexpr int kWalkUnroll = VCFXG_WALK_UNROLL;  // wave-steps (KiB) of a record in flight per sweep step
 
+// the walk's per-record reducer: AF allele counts (alt, total) or, for VCFX_hwe_tester, the
+// genotype classes (hom-ref, het, hom-alt; the third in aux_o)
+template <class Op>
+struct WalkRed;
+template <>
+struct WalkRed<AfOp> {
+    static constexpr bool kAux = false;
+    __device__ static AfOp make(const char *buf, int64_t ae) { return AfOp{buf, ae, 0}; }
+    __device__ static void out(const AfOp &op, uint32_t &a, uint32_t &b, uint32_t &) {
+        a = op.alt;
+        b = op.tot;
+    }
+};
+template <>
+struct WalkRed<HweOp> {
+    static constexpr bool kAux = true;
+    __device__ static HweOp make(const char *buf, int64_t ae) { return HweOp{buf, ae}; }
+    __device__ static void out(const HweOp &op, uint32_t &a, uint32_t &b, uint32_t &c) {
+        a = op.c0;
+        b = op.c1;
+        c = op.c2;
+    }
+};
+
+template <class Op>
 __global__ __launch_bounds__(kWalkThreads)
 #ifdef VCFXG_WALK_MAXW
 __attribute__((amdgpu_waves_per_eu(1, VCFXG_WALK_MAXW)))
 #endif
 void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chunk, int64_t n_walkers, int mode,
                int64_t span0, uint64_t cap_w, uint64_t *__restrict__ le_o, int32_t *__restrict__ alt_o,
-               int32_t *__restrict__ tot_o, uint32_t *__restrict__ rowpre_o, uint8_t *__restrict__ status_o,
-               LineMeta *__restrict__ meta_o, uint64_t *__restrict__ wcount, uint32_t *__restrict__ wgt,
-               unsigned *overflow) {
+               int32_t *__restrict__ tot_o, int32_t *__restrict__ aux_o, uint32_t *__restrict__ rowpre_o,
+               uint8_t *__restrict__ status_o, LineMeta *__restrict__ meta_o, uint64_t *__restrict__ wcount,
+               uint32_t *__restrict__ wgt, unsigned *overflow) {
+    typedef WalkRed<Op> R;
     __shared__ uint4 win[kWalkWaves][2][kWave];  // two window slots per wave (double buffer)
     const int wv = threadIdx.x / kWave;
     const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + wv);
@@ -69,7 +95,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     // per-line results held by lane (n & 63), written out 64 lines at a time (no stores --
     // and no waits for their completion -- on the per-record path)
     uint64_t r_le = 0, r_S = 0;
-    uint32_t r_alt = 0, r_tot = 0, r_pre = 0, r_k = 0;  // r_k: kind | sep << 8 | cr << 16 | status << 24
+    uint32_t r_alt = 0, r_tot = 0, r_aux = 0, r_pre = 0, r_k = 0;  // r_k: kind | sep << 8 | cr << 16 | status << 24
     auto flush = [&](uint64_t first, uint32_t cnt) {
         if ((uint32_t)lane() < cnt) {
             const uint64_t o = base + first + lane();
@@ -85,6 +111,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             le_o[o] = r_le;
             alt_o[o] = (int32_t)r_alt;
             tot_o[o] = (int32_t)r_tot;
+            if (R::kAux) aux_o[o] = (int32_t)r_aux;
             rowpre_o[o] = kind == kMetaGt ? r_pre : 0u;
             status_o[o] = (uint8_t)(r_k >> 24);
             meta_o[o] = m;
@@ -174,7 +201,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         };
         // ---- 3. kind (head_meta) and the sweep
         uint8_t st = 0, kind = 0, sep = 0;
-        uint32_t alt = 0, tot = 0, rowpre = 0;
+        uint32_t alt = 0, tot = 0, aux = 0, rowpre = 0;
         int64_t S = 0;
         bool ok = false;
         auto sweep = [&]() {
@@ -190,10 +217,9 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                 sep = t8 + 2 >= ae ? 0
                       : t8 + 2 < wend ? (uint8_t)sep_w
                                       : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
-                AfOp op{buf, ae, 0};
+                Op op = R::make(buf, ae);
                 ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
-                alt = op.alt;
-                tot = op.tot;
+                R::out(op, alt, tot, aux);
             }
         };
         sweep();
@@ -233,6 +259,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             r_S = (uint64_t)S;
             r_alt = alt;
             r_tot = tot;
+            r_aux = aux;
             r_pre = rowpre;
             r_k = (uint32_t)kind | ((uint32_t)sep << 8) | ((uint32_t)cr << 16) | ((uint32_t)st << 24);
         }
@@ -260,11 +287,12 @@ __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_
                                                       const uint64_t *__restrict__ le_b,
                                                       const int32_t *__restrict__ alt_b,
                                                       const int32_t *__restrict__ tot_b,
+                                                      const int32_t *__restrict__ aux_b,
                                                       const uint32_t *__restrict__ rowpre_b,
                                                       const uint8_t *__restrict__ status_b,
                                                       const LineMeta *__restrict__ meta_b, uint64_t *line_end,
-                                                      int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
-                                                      LineMeta *meta, uint64_t *n_lines,
+                                                      int32_t *alt, int32_t *tot, int32_t *aux, uint32_t *rowpre,
+                                                      uint8_t *status, LineMeta *meta, uint64_t *n_lines,
                                                       unsigned long long *counters) {
     __shared__ uint32_t red[256 / kWave];
     uint32_t g = 0;
@@ -277,6 +305,7 @@ __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_
             line_end[d] = le_b[sl];
             alt[d] = alt_b[sl];
             tot[d] = tot_b[sl];
+            if (aux_b) aux[d] = aux_b[sl];
             rowpre[d] = rowpre_b[sl];
             status[d] = status_b[sl];
             meta[d] = meta_b[sl];
@@ -301,12 +330,18 @@ int64_t af_walkers(int64_t lo, int64_t hi, int64_t chunk) { return hi > lo ? (hi
 hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int mode, int64_t span0,
                           uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
                           uint8_t *status_b, void *meta_b, uint64_t *wcount, uint32_t *wgt, unsigned *overflow,
-                          hipStream_t s) {
+                          hipStream_t s, int32_t *hwe_aux_b) {
     const int64_t nw = af_walkers(lo, hi, chunk);
     if (!nw) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((nw + kWalkWaves - 1) / kWalkWaves);
-    hipLaunchKernelGGL(k_af_walk, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, mode, span0, cap_w,
-                       le_b, alt_b, tot_b, rowpre_b, status_b, static_cast<LineMeta *>(meta_b), wcount, wgt, overflow);
+    if (hwe_aux_b)
+        hipLaunchKernelGGL(k_af_walk<HweOp>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, mode, span0,
+                           cap_w, le_b, alt_b, tot_b, hwe_aux_b, rowpre_b, status_b, static_cast<LineMeta *>(meta_b),
+                           wcount, wgt, overflow);
+    else
+        hipLaunchKernelGGL(k_af_walk<AfOp>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, mode, span0,
+                           cap_w, le_b, alt_b, tot_b, nullptr, rowpre_b, status_b, static_cast<LineMeta *>(meta_b),
+                           wcount, wgt, overflow);
     return hipGetLastError();
 }
 
@@ -314,11 +349,12 @@ hipError_t launch_walk_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t
                                const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b,
                                const uint32_t *rowpre_b, const uint8_t *status_b, const void *meta_b,
                                uint64_t *line_end, int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
-                               void *meta, uint64_t *n_lines, unsigned long long *counters, hipStream_t s) {
+                               void *meta, uint64_t *n_lines, unsigned long long *counters, hipStream_t s,
+                               const int32_t *aux_b, int32_t *aux) {
     const int64_t blocks = std::min<int64_t>((n_walkers + 256 / kWave - 1) / (256 / kWave), 512);
     hipLaunchKernelGGL(k_walk_compact, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s, n_walkers, cap_w,
-                       offs, wgt, le_b, alt_b, tot_b, rowpre_b, status_b, static_cast<const LineMeta *>(meta_b),
-                       line_end, alt, tot, rowpre, status, static_cast<LineMeta *>(meta), n_lines, counters);
+                       offs, wgt, le_b, alt_b, tot_b, aux_b, rowpre_b, status_b, static_cast<const LineMeta *>(meta_b),
+                       line_end, alt, tot, aux, rowpre, status, static_cast<LineMeta *>(meta), n_lines, counters);
     return hipGetLastError();
 }
 

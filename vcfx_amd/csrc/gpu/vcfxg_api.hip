@@ -62,6 +62,12 @@ struct vcfxg_ctx {
     // walk AF path (vcfxg_af_walk.hip): per-walker regions, counts, scan, flags
     DevBuf wk_le, wk_alt, wk_tot, wk_rowpre, wk_status, wk_meta, wk_count, wk_offs, wk_gt, wk_small;
     DevBuf wk_tabs, rf_tabs;    // filter / query walk: per-line tab offsets (per walker, dense)
+    // VCFX_hwe_tester: hom-alt counts (dense, per walker), the host-recheck list and its length
+    DevBuf hwe_aux, wk_aux, hwe_rc;
+    uint64_t hwe_rc_n = 0;
+    // ulps either side of the device p-value that must print the same digits (test hook: a
+    // huge value sends every exp()-derived row to the host)
+    int64_t hwe_ulps = getenv("VCFXG_HWE_ULPS") ? atoll(getenv("VCFXG_HWE_ULPS")) : 16;
     int64_t walk_chunk = getenv("VCFXG_WALK_CHUNK") ? atol(getenv("VCFXG_WALK_CHUNK")) : 128 * 1024;
     bool walk_overflowed = false;  // the last walk run overflowed: two-sweep schedule
     // host hints taken at load time from the first data line: its '\n' distance from the
@@ -211,7 +217,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc})
         if (b->p) (void)hipFree(b->p);
     for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
     for (hipEvent_t e : c->ingest_ev_free) (void)hipEventDestroy(e);
@@ -1130,6 +1136,166 @@ int vcfxg_filter_query_region(vcfxg_ctx *c, size_t data_start, const vcfxg_crite
 int vcfxg_nonref_filter_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
     if (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN) return VCFXG_E_ARG;
     return fq_region(c, data_start, vcfxg::kFqNR, nullptr, 0, 0, "", 0, 0, mode == VCFXG_MODE_FILE ? 1 : 0, out);
+}
+
+// VCFX_hwe_tester over [data_start, n).  walk: the AF walk with the HWE reducer (records of
+// >= 512 B on average), its compaction and k_hwe_lines for the lines it left; else the line
+// index and k_hwe_lines on every line.  Then the row rules + lengths, the scan, the rows into
+// the previous call's text capacity and ONE host synchronisation (as af_region_walk); rows
+// past the capacity are formatted again once it has grown.  A walker over its line capacity
+// reruns the call without the walk.
+static int hwe_region_impl(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out, bool walk) {
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
+    const int64_t C = c->walk_chunk;
+    const int64_t nw = walk ? vcfxg::af_walkers(lo, hi, C) : 0;
+    walk = walk && nw > 0;
+    const char *buf = P<char>(c->input);
+    int r = ensure(c, c->wk_small, 128);
+    if (r) return r;
+    uint64_t *small = P<uint64_t>(c->wk_small);  // [0] overflow flag, [4..10] summary, [11] rechecks
+    unsigned *ovf = reinterpret_cast<unsigned *>(small);
+    uint64_t cap = 0;
+    if (walk) {
+        const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
+        cap = (uint64_t)nw * cap_w;
+        r = ensure(c, c->wk_le, 8 * cap);
+        if (!r) r = ensure(c, c->wk_alt, 4 * cap);
+        if (!r) r = ensure(c, c->wk_tot, 4 * cap);
+        if (!r) r = ensure(c, c->wk_aux, 4 * cap);
+        if (!r) r = ensure(c, c->wk_rowpre, 4 * cap);
+        if (!r) r = ensure(c, c->wk_status, cap);
+        if (!r) r = ensure(c, c->wk_meta, vcfxg::af_meta_bytes() * cap);
+        if (!r) r = ensure(c, c->wk_count, 8 * (size_t)(nw + 1));
+        if (!r) r = ensure(c, c->wk_offs, 8 * (size_t)(nw + 1));
+        if (!r) r = ensure(c, c->wk_gt, 4 * (size_t)nw);
+        if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
+        if (!r) r = af_buffers(c, cap);
+        if (!r) r = ensure(c, c->hwe_aux, 4 * (cap + 1));
+        if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (cap + 1));
+        if (!r) r = ensure(c, c->hwe_rc, sizeof(vcfxg_hwe_recheck) * (cap + 1));
+        if (r) return r;
+        HIPCHK(c, hipMemsetAsync(small, 0, 96, c->stream));
+        HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->wk_count) + nw, 0, 8, c->stream));
+        prof_begin(c, "hwe_walk");
+        // mode 0: both HWE modes strip the trailing '\r' before the record is parsed
+        HIPCHK(c, vcfxg::launch_af_walk(buf, lo, hi, C, 0, c->hint_span, cap_w, P<uint64_t>(c->wk_le),
+                                        P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre),
+                                        P<uint8_t>(c->wk_status), c->wk_meta.p, P<uint64_t>(c->wk_count),
+                                        P<uint32_t>(c->wk_gt), ovf, c->stream, P<int32_t>(c->wk_aux)));
+        prof_end(c, "hwe_walk");
+        prof_begin(c, "walk_compact");
+        r = exclusive_scan(c, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_offs), (size_t)nw + 1);
+        if (r) return r;
+        HIPCHK(c, vcfxg::launch_walk_compact(nw, cap_w, P<uint64_t>(c->wk_offs), P<uint32_t>(c->wk_gt),
+                                             P<uint64_t>(c->wk_le), P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot),
+                                             P<uint32_t>(c->wk_rowpre), P<uint8_t>(c->wk_status), c->wk_meta.p,
+                                             P<uint64_t>(c->line_end), P<int32_t>(c->alt), P<int32_t>(c->tot),
+                                             P<uint32_t>(c->rowpre), P<uint8_t>(c->status), c->af_meta.p,
+                                             P<uint64_t>(c->d_nlines), P<unsigned long long>(c->counters), c->stream,
+                                             P<int32_t>(c->wk_aux), P<int32_t>(c->hwe_aux)));
+        prof_end(c, "walk_compact");
+    } else {
+        uint64_t L = 0;
+        r = vcfxg_index(c, data_start, &L);
+        if (r) return r;
+        cap = L;
+        r = af_buffers(c, cap);
+        if (!r) r = ensure(c, c->hwe_aux, 4 * (cap + 1));
+        if (!r) r = ensure(c, c->hwe_rc, sizeof(vcfxg_hwe_recheck) * (cap + 1));
+        if (r) return r;
+        HIPCHK(c, hipMemsetAsync(small, 0, 96, c->stream));
+    }
+    // (the walk's compaction counts GT lines for AF in counters[0..1]: rows are counted below)
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    prof_begin(c, "hwe_lines");
+    HIPCHK(c, vcfxg::launch_hwe_lines(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
+                                      walk ? c->af_meta.p : nullptr, P<int32_t>(c->alt), P<int32_t>(c->tot),
+                                      P<int32_t>(c->hwe_aux), P<uint32_t>(c->rowpre), P<uint8_t>(c->status),
+                                      P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "hwe_lines");
+    prof_begin(c, "hwe_rows");
+    HIPCHK(c, vcfxg::launch_hwe_rowlen(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
+                                       P<uint32_t>(c->rowpre), P<uint8_t>(c->status), P<uint64_t>(c->rowlen),
+                                       P<unsigned long long>(c->counters), c->stream));
+    r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)cap + 1);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_af_summary(P<uint64_t>(c->d_nlines), P<uint64_t>(c->rowoff),
+                                       P<unsigned long long>(c->counters), ovf, small + 4, c->stream));
+    prof_end(c, "hwe_rows");
+    const uint64_t tcap = std::max<uint64_t>(c->text_hint, 1u << 16);
+    r = ensure(c, c->text, tcap + 1);
+    if (r) return r;
+    unsigned long long *rc_n = reinterpret_cast<unsigned long long *>(small + 11);
+    prof_begin(c, "hwe_format");
+    HIPCHK(c, vcfxg::launch_hwe_format(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
+                                       P<int32_t>(c->alt), P<int32_t>(c->tot), P<int32_t>(c->hwe_aux),
+                                       P<uint32_t>(c->rowpre), P<uint8_t>(c->status), P<uint64_t>(c->rowoff),
+                                       P<char>(c->text), tcap, c->hwe_ulps, c->hwe_rc.p, rc_n, cap + 1, c->stream));
+    prof_end(c, "hwe_format");
+    static thread_local uint64_t sm[8];
+    HIPCHK(c, hipMemcpyAsync(sm, small + 4, sizeof sm, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (walk && sm[6]) {  // a walker ran out of line slots (short lines): no walk
+        prof_collect(c);
+        c->walk_overflowed = true;
+        return hwe_region_impl(c, data_start, mode, out, false);
+    }
+    const uint64_t L = sm[0], text = sm[1];
+    c->text_hint = text;
+    if (text > tcap) {  // the text outgrew the previous capacity: all rows again
+        r = ensure(c, c->text, text + 1);
+        if (r) return r;
+        HIPCHK(c, hipMemsetAsync(rc_n, 0, 8, c->stream));
+        prof_begin(c, "hwe_format");
+        HIPCHK(c, vcfxg::launch_hwe_format(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L, mode,
+                                           P<int32_t>(c->alt), P<int32_t>(c->tot), P<int32_t>(c->hwe_aux),
+                                           P<uint32_t>(c->rowpre), P<uint8_t>(c->status), P<uint64_t>(c->rowoff),
+                                           P<char>(c->text), ~0ull, c->hwe_ulps, c->hwe_rc.p, rc_n, cap + 1,
+                                           c->stream));
+        prof_end(c, "hwe_format");
+        HIPCHK(c, hipMemcpyAsync(&sm[7], rc_n, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (c->profiling) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        prof_collect(c);
+    }
+    c->data_start = data_start;
+    c->n_lines = L;
+    c->indexed = true;
+    c->text_bytes = text;
+    c->hwe_rc_n = sm[7];
+    if (out) {
+        out->n_lines = L;
+        out->rows = sm[2];
+        out->data_lines = 0;
+        out->warn_lines = 0;
+        out->general_records = sm[5];
+        out->text_bytes = text;
+    }
+    return VCFXG_OK;
+}
+
+int vcfxg_hwe_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
+    if (!c->loaded) return VCFXG_E_STATE;
+    if (data_start > c->n) data_start = c->n;
+    // the AF schedule knob selects here too: 3 / 8 = no walk, 7 = the walk
+    const bool walk = c->af_path == 7 || (c->af_path != 3 && c->af_path != 8 && c->hint_line >= 512 &&
+                                          !c->walk_overflowed);
+    return hwe_region_impl(c, data_start, mode, out, walk);
+}
+
+int vcfxg_hwe_rechecks(vcfxg_ctx *c, vcfxg_hwe_recheck *out, uint64_t cap, uint64_t *n) {
+    if (!c || !n || (!out && cap)) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    *n = c->hwe_rc_n;
+    const uint64_t k = std::min(cap, c->hwe_rc_n);
+    if (!k) return VCFXG_OK;
+    HIPCHK(c, hipMemcpyAsync(out, c->hwe_rc.p, k * sizeof(vcfxg_hwe_recheck), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VCFXG_OK;
 }
 
 int vcfxg_variant_count(vcfxg_ctx *c, int strip_cr, vcfxg_summary *out) {

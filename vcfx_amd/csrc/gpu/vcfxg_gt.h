@@ -381,4 +381,66 @@ struct NrOp {
     __device__ void finish() { found = __any(any); }
 };
 
+// ---------------------------------------------------------------------------------------
+// HWE genotype-class reducer (VCFX_hwe_tester): per sample
+// parseGenotypeForHWE (VCFX_hwe_tester.cpp:339-378) -> 0 hom-ref, 1 het, 2 hom-alt, or
+// invalid (not counted).  The sample's first ':' sub-field, leading ' ' / '\r' skipped, two
+// '/'- or '|'-separated integers (digits after the second are ignored), both <= 1.  On the
+// fixed-stride layout a sample counts iff both fields are digits <= 1; the class is a + b.
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int hwe_parse(const char *__restrict__ buf, int64_t p, int64_t end) {
+    if (p >= end) return -1;
+    for (int64_t k = p; k < end; k++)  // memchr(':')
+        if (byte_at(buf, k) == ':') {
+            end = k;
+            break;
+        }
+    while (p < end && (byte_at(buf, p) == ' ' || byte_at(buf, p) == '\r')) p++;
+    if (p >= end || !is_digit(byte_at(buf, p))) return -1;  // also '.'
+    // int accumulation as the reference's (two's-complement wrap on absurdly long numbers)
+    uint32_t a1 = 0, a2 = 0;
+    while (p < end && is_digit(byte_at(buf, p))) {
+        a1 = a1 * 10u + (byte_at(buf, p) - '0');
+        p++;
+    }
+    if (p >= end || (byte_at(buf, p) != '/' && byte_at(buf, p) != '|')) return -1;
+    p++;
+    if (p >= end || !is_digit(byte_at(buf, p))) return -1;
+    while (p < end && is_digit(byte_at(buf, p))) {
+        a2 = a2 * 10u + (byte_at(buf, p) - '0');
+        p++;
+    }
+    if ((int32_t)a1 > 1 || (int32_t)a2 > 1) return -1;
+    if (a1 == 0u && a2 == 0u) return 0;
+    if (a1 == 1u && a2 == 1u) return 2;
+    return 1;
+}
+
+struct HweOp {
+    const char *buf;
+    int64_t E;
+    uint32_t c0 = 0, c1 = 0, c2 = 0;  // hom-ref, het, hom-alt
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() const { return false; }
+    __device__ void dword(const DwordView &v) {
+        // both fields digits (neutral padding ". ." is not) and both 0 or 1
+        const bool ok = v.dig == 0x01000100u && (v.f & 0x00FE00FEu) == 0u;
+        const uint32_t s = (v.f & 1u) + ((v.f >> 16) & 1u);
+        c0 += ok && s == 0u;
+        c1 += ok && s == 1u;
+        c2 += ok && s == 2u;
+    }
+    __device__ void sample(int64_t st) {
+        const int g = hwe_parse(buf, st, sample_end(buf, st, E));
+        c0 += g == 0;
+        c1 += g == 1;
+        c2 += g == 2;
+    }
+    __device__ void finish() {
+        c0 = wave_sum(c0);
+        c1 = wave_sum(c1);
+        c2 = wave_sum(c2);
+    }
+};
+
 }  // namespace vcfxg

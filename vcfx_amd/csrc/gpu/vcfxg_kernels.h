@@ -53,12 +53,13 @@ int64_t af_walkers(int64_t lo, int64_t hi, int64_t chunk);
 hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int mode, int64_t span0,
                           uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
                           uint8_t *status_b, void *meta_b, uint64_t *wcount, uint32_t *wgt, unsigned *overflow,
-                          hipStream_t s);
+                          hipStream_t s, int32_t *hwe_aux_b = nullptr);
 hipError_t launch_walk_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t *offs, const uint32_t *wgt,
                                const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b,
                                const uint32_t *rowpre_b, const uint8_t *status_b, const void *meta_b,
                                uint64_t *line_end, int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
-                               void *meta, uint64_t *n_lines, unsigned long long *counters, hipStream_t s);
+                               void *meta, uint64_t *n_lines, unsigned long long *counters, hipStream_t s,
+                               const int32_t *aux_b = nullptr, int32_t *aux = nullptr);
 hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
                              int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
@@ -92,6 +93,20 @@ hipError_t launch_af_summary(const uint64_t *n_lines, const uint64_t *rowoff, co
                              const unsigned *fail, uint64_t *out, hipStream_t s);
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, uint64_t *len, hipStream_t s);
+// VCFX_hwe_tester (vcfxg_hwe.hip): the exact per-line pass (meta == nullptr: every line;
+// else the walk's kMetaFull / kAfPending lines), the CHROM..ALT row rules + row lengths
+// (counters[0] += rows), and the rows (rechecks: vcfxg_hwe_recheck entries, *rc_n counted)
+hipError_t launch_hwe_lines(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                            uint64_t n_lines_host, int mode, const void *meta, int32_t *c0, int32_t *c1, int32_t *c2,
+                            uint32_t *rowpre, uint8_t *status, unsigned long long *counters, hipStream_t s);
+hipError_t launch_hwe_rowlen(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                             uint64_t n_lines_host, int mode, const uint32_t *rowpre, uint8_t *status, uint64_t *len,
+                             unsigned long long *counters, hipStream_t s);
+hipError_t launch_hwe_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                             uint64_t n_lines_host, int mode, const int32_t *c0, const int32_t *c1, const int32_t *c2,
+                             const uint32_t *rowpre, const uint8_t *status, const uint64_t *off, char *out,
+                             uint64_t text_cap, int64_t ulps, void *rc, unsigned long long *rc_n, uint64_t rc_cap,
+                             hipStream_t s);
 // text_cap: rows whose end passes it are not written (the caller checks the total)
 hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, int mode, const int32_t *alt, const int32_t *tot,

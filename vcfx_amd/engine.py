@@ -59,6 +59,8 @@ SIGNATURES = {
     "vcfxg_variant_count": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
     "vcfxg_nonref_filter": (_I, [_VP, _I, ctypes.POINTER(Summary)]),
     "vcfxg_nonref_filter_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_hwe_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_hwe_rechecks": (_I, [_VP, _VP, _U64, ctypes.POINTER(_U64)]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_prefixes": (_I, [_VP, _VP, _S, _VP]),
     "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
@@ -196,6 +198,22 @@ class Engine:
         self._chk(self.L.vcfxg_nonref_filter_region(self.h, data_start, int(mode), ctypes.byref(s)),
                   "nonref_filter_region")
         return s
+
+    def hwe_region(self, data_start, mode):
+        """VCFX_hwe_tester over [data_start, n): counts, row rules and rows (vcfxg_hwe_region)"""
+        s = Summary()
+        self._chk(self.L.vcfxg_hwe_region(self.h, data_start, int(mode), ctypes.byref(s)), "hwe_region")
+        return s
+
+    def hwe_rechecks(self):
+        """the last hwe_region's rows left to the host: [(text_offset, hom_ref, het, hom_alt)]"""
+        import numpy as np
+        n = ctypes.c_uint64()
+        self._chk(self.L.vcfxg_hwe_rechecks(self.h, None, 0, ctypes.byref(n)), "hwe_rechecks")
+        a = np.zeros((max(n.value, 1), 3), np.uint64)  # 24 B per vcfxg_hwe_recheck
+        self._chk(self.L.vcfxg_hwe_rechecks(self.h, a.ctypes.data, n.value, ctypes.byref(n)), "hwe_rechecks")
+        v = a[:n.value].view(np.uint32).reshape(-1, 6)
+        return [(int(r[0]) | (int(r[1]) << 32), int(r[2]), int(r[3]), int(r[4])) for r in v]
 
     def _criteria(self, crits):
         """crits: list of (target, op, numeric, value, key, str) as vcfxg_criterion."""
