@@ -86,7 +86,7 @@ def test_hwe_recheck_path(oracle, mode, tmp_path):
     import ctypes
     buf = synth.generate(1200, 301, 77, 0, 0.01, 0, 0.1, 0)
     s, text, rc = _engine_text(buf, mode, {"VCFXG_HWE_ULPS": str(1 << 50)})
-    assert len(rc) > 500  # most rows go through exp()
+    assert len(rc) > 200  # the rows whose p-value went through exp()
     lib = oracle.lib
     lib.oracle_hwe_pvalue.restype = ctypes.c_double
     lib.oracle_hwe_pvalue.argtypes = [ctypes.c_int] * 3

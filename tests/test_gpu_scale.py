@@ -117,7 +117,8 @@ def _check(case, inputs, stdin="none"):
 
 @pytest.mark.parametrize("case,stdin", [("af_file", "none"), ("af_stdin", "pipe"), ("af_stdin", "file"),
                                         ("nonref_file", "none"), ("pipeline_bench", "none"),
-                                        ("nonref_stdin", "pipe"), ("nonref_stdin", "file")])
+                                        ("nonref_stdin", "pipe"), ("nonref_stdin", "file"),
+                                        ("hwe_file", "none"), ("hwe_stdin", "pipe"), ("hwe_stdin", "file")])
 def test_chr21_shard_matches_reference(inputs, case, stdin):
     _check(case, inputs, stdin)
 
@@ -130,7 +131,7 @@ def test_annotated_shard_matches_reference(inputs, case, stdin):
         inputs.drop("annot")
 
 
-@pytest.mark.parametrize("case", ["af_file", "pipeline_bench"])
+@pytest.mark.parametrize("case", ["af_file", "pipeline_bench", "hwe_file"])
 def test_bgzf_chr21_matches_reference(inputs, case):
     """the same shard as BGZF (.vcf.gz, made by build/bin/vcfx_bgzf): inflated on the host
     threads, then the device path; output identical to the reference's on the plain bytes"""
@@ -187,5 +188,10 @@ def test_region_api_at_full_size(inputs):
         c = DIG["cases"]["nonref_file"]
         assert s.rows == c["kept"]
         assert _mask_sha(eng.statuses(s.n_lines), n_rec) == c["keep_mask_sha256"]
+        s = eng.hwe_region(ds, engine.MODE_FILE)
+        c = DIG["cases"]["hwe_file"]
+        assert s.rows == c["stdout"]["lines"] - 1 and s.general_records == 0 and not eng.hwe_rechecks()
+        text = b"CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n" + eng.text(s.text_bytes)
+        assert hashlib.sha256(text).hexdigest() == c["stdout"]["sha256"]
     finally:
         eng.close()
