@@ -96,6 +96,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     // and no waits for their completion -- on the per-record path)
     uint64_t r_le = 0, r_S = 0;
     uint32_t r_alt = 0, r_tot = 0, r_aux = 0, r_pre = 0, r_k = 0;  // r_k: kind | sep << 8 | cr << 16 | status << 24
+    uint32_t r_h = 0;  // HWE: the CHROM..ALT flags (LineMeta::pad)
     auto flush = [&](uint64_t first, uint32_t cnt) {
         if ((uint32_t)lane() < cnt) {
             const uint64_t o = base + first + lane();
@@ -103,6 +104,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             LineMeta m{};
             m.kind = kind;
             m.cr = (uint8_t)(r_k >> 16);
+            m.pad = R::kAux ? (uint8_t)r_h : 0;
             if (kind == kMetaGt) {
                 m.S = r_S;
                 m.rowpre = r_pre;
@@ -131,7 +133,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         const int Lr = (int)(L - A);
         const uint4 *cw = win[wv][cur];
         int hr, N1r, r4 = 0, r7 = 0, r8 = 0;
-        uint32_t ntab, first;
+        uint32_t ntab, first, hflags = 0;
         auto analyze = [&](int ws) {
             const uint4 W = read_window(cw);
             hr = (int)std::min<int64_t>(hi - A, ws);
@@ -151,6 +153,13 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                 r4 = tab_at(tm, tinc - tc, tc, 4, b);
                 r7 = tab_at(tm, tinc - tc, tc, 7, b);
                 r8 = tab_at(tm, tinc - tc, tc, 8, b);
+                if (R::kAux) {  // HWE row rules on CHROM..ALT (VCFX_hwe_tester.cpp:497-506)
+                    const int r0 = tab_at(tm, tinc - tc, tc, 0, b), r1 = tab_at(tm, tinc - tc, tc, 1, b),
+                              r3 = tab_at(tm, tinc - tc, tc, 3, b);
+                    const bool comma = __ballot((eq_mask16(W, 0x2C2C2C2Cu) & range16(b, r3 + 1, r4)) != 0u) != 0ull;
+                    const bool empty = r0 == Lr || r1 == r0 + 1 || r4 == r3 + 1;
+                    hflags = (comma ? kHweAltComma : 0u) | (empty ? kHweEmptyField : 0u);
+                }
             }
         };
         analyze(kWin);
@@ -260,6 +269,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             r_alt = alt;
             r_tot = tot;
             r_aux = aux;
+            r_h = hflags;
             r_pre = rowpre;
             r_k = (uint32_t)kind | ((uint32_t)sep << 8) | ((uint32_t)cr << 16) | ((uint32_t)st << 24);
         }

@@ -1215,7 +1215,7 @@ static int hwe_region_impl(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summ
                                       P<unsigned long long>(c->counters), c->stream));
     prof_end(c, "hwe_lines");
     prof_begin(c, "hwe_rows");
-    HIPCHK(c, vcfxg::launch_hwe_rowlen(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
+    HIPCHK(c, vcfxg::launch_hwe_rowlen(P<uint64_t>(c->d_nlines), cap, mode, walk ? c->af_meta.p : nullptr,
                                        P<uint32_t>(c->rowpre), P<uint8_t>(c->status), P<uint64_t>(c->rowlen),
                                        P<unsigned long long>(c->counters), c->stream));
     r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)cap + 1);

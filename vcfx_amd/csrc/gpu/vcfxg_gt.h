@@ -419,16 +419,17 @@ __device__ __forceinline__ int hwe_parse(const char *__restrict__ buf, int64_t p
 struct HweOp {
     const char *buf;
     int64_t E;
-    uint32_t c0 = 0, c1 = 0, c2 = 0;  // hom-ref, het, hom-alt
+    uint32_t c0 = 0, c1 = 0, c2 = 0;  // hom-ref, het, hom-alt (after finish())
+    // fixed-stride accumulators: (valid samples << 16) + ALT alleles of the valid ones, and
+    // the hom-alt count (a lane sees < 65536 dwords of a record)
+    uint32_t nv_alt = 0, two = 0;
     __device__ void begin(uint32_t, uint32_t) {}
     __device__ bool done() const { return false; }
     __device__ void dword(const DwordView &v) {
-        // both fields digits (neutral padding ". ." is not) and both 0 or 1
-        const bool ok = v.dig == 0x01000100u && (v.f & 0x00FE00FEu) == 0u;
-        const uint32_t s = (v.f & 1u) + ((v.f >> 16) & 1u);
-        c0 += ok && s == 0u;
-        c1 += ok && s == 1u;
-        c2 += ok && s == 2u;
+        // both fields 0 or 1 (no other field value, '.' included, passes)
+        const bool ok = (v.f & 0x00FE00FEu) == 0u;
+        nv_alt += ok ? (uint32_t)__popc(v.f) + 0x10000u : 0u;
+        two += v.f == 0x00010001u;
     }
     __device__ void sample(int64_t st) {
         const int g = hwe_parse(buf, st, sample_end(buf, st, E));
@@ -437,6 +438,10 @@ struct HweOp {
         c2 += g == 2;
     }
     __device__ void finish() {
+        const uint32_t nv = nv_alt >> 16, alt = nv_alt & 0xFFFFu;
+        c2 += two;
+        c1 += alt - 2u * two;
+        c0 += nv - (alt - two);
         c0 = wave_sum(c0);
         c1 = wave_sum(c1);
         c2 = wave_sum(c2);

@@ -4,8 +4,8 @@
 // Counting: the AF walk (vcfxg_af_walk.hip) with the HweOp reducer gives each fixed-stride
 // GT record its (hom-ref, het, hom-alt) counts in the same single HBM pass; k_hwe_lines runs
 // hwe_line, the exact per-line restatement, on everything else (and on every line of the
-// two-sweep schedule for short records).  k_hwe_rowlen applies the row rules that only need
-// the CHROM..ALT prefix, a scan gives row offsets, and k_hwe_format writes the rows
+// two-sweep schedule for short records).  The row rules on CHROM..ALT come from the walk's head
+// window (or hwe_line), k_hwe_rowlen + a scan give row offsets, and k_hwe_format writes the rows
 // "CHROM\tPOS\tID\tREF\tALT\t<p>\n" with <p> in the mode's 6-digit format.
 //
 // Exactness: the p-value (calculateHWE_chisq / chi2_pvalue_1df, VCFX_hwe_tester.cpp:278-315)
@@ -28,7 +28,7 @@ constexpr int kHweThreads = 256;
 constexpr int kHweWaves = kHweThreads / kWave;
 
 // One line [ls, le) in mode 0 (performHWE_Mmap :475-558) or 1 (performHWE_Stdin :572-607):
-// status 1 = candidate row (the CHROM/POS/ALT rules are k_hwe_rowlen's), 0 = skipped.
+// status 1 = row, 0 = skipped.
 // Both modes drop one trailing '\r' and skip empty and '#' lines.  Both need >= 9 tabs
 // (mmap: getField(8) + skipToField(9); stdin: >= 10 split_tabs fields) and a FORMAT that
 // starts with "GT"; mmap also a non-empty sample region.  Every tab-separated sample of
@@ -48,6 +48,12 @@ __device__ __forceinline__ void hwe_line(const char *__restrict__ buf, int64_t l
     if (t[8] - t[7] - 1 < 2 || byte_at(buf, t[7] + 1) != 'G' || byte_at(buf, t[7] + 2) != 'T') return;
     const int64_t S = t[8] + 1;
     if (mode == 0 && S >= ae) return;
+    // CHROM..ALT: ALT without ',' (both modes); CHROM, POS, ALT non-empty (mmap :497)
+    if (mode == 0 && (t[0] == ls || t[1] == t[0] + 1 || t[4] == t[3] + 1)) return;
+    for (int64_t w = t[3] + 1; w < t[4]; w += kWave) {
+        const int64_t p = w + lane();
+        if (__ballot(p < t[4] && byte_at(buf, p) == ',')) return;
+    }
     HweOp op{buf, ae};
     if (!gt_fast(buf, S, ae, op)) {
         HweOp g{buf, ae};
@@ -105,42 +111,41 @@ __global__ __launch_bounds__(kHweThreads) void k_hwe_lines(const char *__restric
     if (lane() == 0 && ngen) atomicAdd(&counters[3], (unsigned long long)ngen);
 }
 
-// The rules on CHROM..ALT (prefix = rowpre bytes, 5 fields each followed by its tab): ALT has
-// no ',' (isBiallelic :380-382, both modes); mmap also CHROM, POS and ALT non-empty (:497).
-// len = row bytes (prefix + 8 digits + '\n') or 0; a rejected line's status becomes 0.
-__global__ void k_hwe_rowlen(const char *__restrict__ buf, int64_t data_start, const uint64_t *__restrict__ line_end,
-                             const uint64_t *n_lines_p, int mode, const uint32_t *__restrict__ rowpre,
-                             uint8_t *__restrict__ status, uint64_t *__restrict__ len,
-                             unsigned long long *__restrict__ counters) {
+// Row lengths (prefix + 8 digits + '\n', or 0).  The rules on CHROM..ALT were applied by
+// hwe_line, or for the walk's kMetaGt lines (meta != nullptr) come as the flags the walk took
+// from its head window: ALT holds a ',' (isBiallelic :380-382, both modes) or CHROM, POS or ALT
+// is empty (mmap :497).  A rejected line's status becomes 0; counters[0] += rows.
+__global__ void k_hwe_rowlen(const uint64_t *n_lines_p, int mode, const LineMeta *__restrict__ meta,
+                             const uint32_t *__restrict__ rowpre, uint8_t *__restrict__ status,
+                             uint64_t *__restrict__ len, unsigned long long *__restrict__ counters) {
     const uint64_t n = *n_lines_p;
     uint32_t rows = 0;
+    const uint8_t reject = mode == 0 ? (kHweAltComma | kHweEmptyField) : kHweAltComma;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += gridDim.x * (uint64_t)blockDim.x) {
         uint64_t l = 0;
         if (status[i] == 1) {
-            const int64_t ls = i ? (int64_t)line_end[i - 1] + 1 : data_start;
-            const uint32_t pl = rowpre[i];
-            int tabs = 0;
-            uint32_t t0 = 0;
-            bool comma = false;
-            for (uint32_t k = 0; k < pl; k++) {
-                const uint32_t ch = byte_at(buf, ls + k);
-                if (ch == '\t') {
-                    if (tabs == 0) t0 = k;
-                    tabs++;
-                } else if (tabs == 4 && ch == ',') comma = true;
+            bool ok = true;
+            if (meta) {
+                const LineMeta m = meta[i];
+                ok = m.kind != kMetaGt || (m.pad & reject) == 0;
             }
-            bool ok = !comma;
-            if (mode == 0)
-                ok = ok && t0 > 0 && byte_at(buf, ls + t0 + 1) != '\t' && byte_at(buf, ls + pl - 2) != '\t';
             if (ok) {
-                l = (uint64_t)pl + 9u;
+                l = (uint64_t)rowpre[i] + 9u;
                 rows++;
             } else status[i] = 0;
         }
         len[i] = l;
     }
+    // one atomic per block (same-address atomics serialise in L2: one per wave cost ~80 us)
+    __shared__ uint32_t red[256 / kWave];
     rows = wave_sum(rows);
-    if (lane() == 0 && rows) atomicAdd(&counters[0], (unsigned long long)rows);
+    if (lane() == 0) red[threadIdx.x / kWave] = rows;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < 256 / kWave; k++) t += red[k];
+        if (t) atomicAdd(&counters[0], (unsigned long long)t);
+    }
 }
 
 // calculateHWE_chisq (:290-315) + chi2_pvalue_1df (:278-287): the reference's operation
@@ -291,12 +296,12 @@ hipError_t launch_hwe_lines(const char *buf, int64_t data_start, const uint64_t 
     return hipGetLastError();
 }
 
-hipError_t launch_hwe_rowlen(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
-                             uint64_t n_lines_host, int mode, const uint32_t *rowpre, uint8_t *status, uint64_t *len,
-                             unsigned long long *counters, hipStream_t s) {
+hipError_t launch_hwe_rowlen(const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
+                             const uint32_t *rowpre, uint8_t *status, uint64_t *len, unsigned long long *counters,
+                             hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
-    hipLaunchKernelGGL(k_hwe_rowlen, dim3(grid_of((int64_t)n_lines_host, 256, 4096)), dim3(256), 0, s, buf, data_start,
-                       line_end, n_lines_dev, mode, rowpre, status, len, counters);
+    hipLaunchKernelGGL(k_hwe_rowlen, dim3(grid_of((int64_t)n_lines_host, 256, 1024)), dim3(256), 0, s, n_lines_dev,
+                       mode, static_cast<const LineMeta *>(meta), rowpre, status, len, counters);
     return hipGetLastError();
 }
 

@@ -20,6 +20,8 @@ constexpr uint8_t kAfPending = 0xFF;  // AF status of a kMetaGt line whose fast 
 constexpr uint8_t kGqPending = 0xFE;  // GQ: a kMetaGt line whose fast sweep failed (general sweep)
 constexpr uint8_t kRfPending = 0xFD;  // RF walk: head beyond the window (k_fq_finish filters it)
 constexpr uint8_t kGqFull = 0xFC;     // GQ walk: a kMetaFull line for k_gq_complex's gq_line
+// HWE walk: LineMeta::pad of a kMetaGt line -- ALT holds a ',' / CHROM, POS or ALT is empty
+constexpr uint8_t kHweAltComma = 1, kHweEmptyField = 2;
 
 // single-sweep index over 16 KiB wave-chunks (idx_wchunks of them): counts + the first
 // idx_pos_cap() newline offsets per chunk, then a compaction into line_end (overflow != 0:
@@ -94,14 +96,14 @@ hipError_t launch_af_summary(const uint64_t *n_lines, const uint64_t *rowoff, co
 hipError_t launch_af_rowlen(const uint32_t *rowpre, const uint8_t *status, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, uint64_t *len, hipStream_t s);
 // VCFX_hwe_tester (vcfxg_hwe.hip): the exact per-line pass (meta == nullptr: every line;
-// else the walk's kMetaFull / kAfPending lines), the CHROM..ALT row rules + row lengths
-// (counters[0] += rows), and the rows (rechecks: vcfxg_hwe_recheck entries, *rc_n counted)
+// else the walk's kMetaFull / kAfPending lines), the row lengths (the walk's CHROM..ALT flags
+// applied when meta != nullptr; counters[0] += rows), and the rows (rechecks: vcfxg_hwe_recheck entries, *rc_n counted)
 hipError_t launch_hwe_lines(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, int mode, const void *meta, int32_t *c0, int32_t *c1, int32_t *c2,
                             uint32_t *rowpre, uint8_t *status, unsigned long long *counters, hipStream_t s);
-hipError_t launch_hwe_rowlen(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
-                             uint64_t n_lines_host, int mode, const uint32_t *rowpre, uint8_t *status, uint64_t *len,
-                             unsigned long long *counters, hipStream_t s);
+hipError_t launch_hwe_rowlen(const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
+                             const uint32_t *rowpre, uint8_t *status, uint64_t *len, unsigned long long *counters,
+                             hipStream_t s);
 hipError_t launch_hwe_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int mode, const int32_t *c0, const int32_t *c1, const int32_t *c2,
                              const uint32_t *rowpre, const uint8_t *status, const uint64_t *off, char *out,
