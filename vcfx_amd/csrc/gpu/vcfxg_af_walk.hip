@@ -77,7 +77,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                int64_t span0, uint64_t cap_w, uint64_t *__restrict__ le_o, int32_t *__restrict__ alt_o,
                int32_t *__restrict__ tot_o, int32_t *__restrict__ aux_o, uint32_t *__restrict__ rowpre_o,
                uint8_t *__restrict__ status_o, LineMeta *__restrict__ meta_o, uint64_t *__restrict__ wcount,
-               uint32_t *__restrict__ wgt, unsigned *overflow) {
+               uint32_t *__restrict__ wgt, unsigned *overflow, WalkTail tail) {
     typedef WalkRed<Op> R;
     __shared__ uint4 win[kWalkWaves][2][kWave];  // two window slots per wave (double buffer)
     const int wv = threadIdx.x / kWave;
@@ -87,6 +87,8 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
     int64_t L = wk == 0 ? lo : scan_nl<kFirstScanU>(buf, cs - 1, hi) + 1;
+    const int64_t L0 = L;
+    uint64_t wtext = 0;  // region tail (tail.wtext): bytes of this walker's GT-line rows
     int64_t span = span0;  // predicted '\n' distance from the sample start
     uint8_t cr_prev = 0;   // and the '\r' state of that record
     uint64_t n = 0;
@@ -274,6 +276,17 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             r_k = (uint32_t)kind | ((uint32_t)sep << 8) | ((uint32_t)cr << 16) | ((uint32_t)st << 24);
         }
         ngt += kind == kMetaGt ? 1u : 0u;
+        if (tail.wtext) {
+            // the row (CHROM..ALT + "\t" + 4 digits... "x.xxxx\n") of a GT line; lines off the
+            // fixed-stride sweep go to the leftover list (rare: one atomic each)
+            if (kind == kMetaGt) wtext += (uint64_t)rowpre + 7u;
+            if (kind == kMetaFull || (kind == kMetaGt && !ok)) {
+                if (lane() == 0) {
+                    const unsigned long long e = atomicAdd(tail.cx_n, 1ull);
+                    if (e < tail.cx_cap) tail.cx_list[e] = base + n;
+                }
+            }
+        }
         n++;
         if ((n & 63) == 0) flush(n - 64, 64);
         L = E + 1;
@@ -283,6 +296,10 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     if (n & 63) flush(n & ~(uint64_t)63, (uint32_t)(n & 63));
     if (lane() == 0) {
         wcount[wk] = n;
+        if (tail.wtext) {
+            tail.wtext[wk] = wtext;
+            tail.wstart[wk] = (uint64_t)L0;
+        }
         wgt[wk] = ngt;
     }
 }
@@ -303,12 +320,14 @@ __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_
                                                       const LineMeta *__restrict__ meta_b, uint64_t *line_end,
                                                       int32_t *alt, int32_t *tot, int32_t *aux, uint32_t *rowpre,
                                                       uint8_t *status, LineMeta *meta, uint64_t *n_lines,
-                                                      unsigned long long *counters) {
+                                                      unsigned long long *counters, const uint64_t *__restrict__ bpre) {
     __shared__ uint32_t red[256 / kWave];
     uint32_t g = 0;
     const int64_t nwaves = (int64_t)gridDim.x * (256 / kWave);
     for (int64_t w = (int64_t)blockIdx.x * (256 / kWave) + threadIdx.x / kWave; w < n_walkers; w += nwaves) {
-        const uint64_t d0 = offs[w], cnt = offs[w + 1] - d0, s0 = (uint64_t)w * cap_w;
+        // (bpre: block-local offsets of k_walker_scan)
+        const uint64_t d0 = offs[w] + (bpre ? bpre[w / kWalkerScanBlock] : 0),
+                       cnt = offs[w + 1] + (bpre ? bpre[(w + 1) / kWalkerScanBlock] : 0) - d0, s0 = (uint64_t)w * cap_w;
         g += lane() == 0 ? wgt[w] : 0u;
         for (uint64_t i = lane(); i < cnt; i += kWave) {
             const uint64_t sl = s0 + i, d = d0 + i;
@@ -331,7 +350,7 @@ __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_
             atomicAdd(&counters[0], (unsigned long long)t);
             atomicAdd(&counters[1], (unsigned long long)t);
         }
-        if (blockIdx.x == 0) *n_lines = offs[n_walkers];
+        if (blockIdx.x == 0) *n_lines = offs[n_walkers] + (bpre ? bpre[n_walkers / kWalkerScanBlock] : 0);
     }
 }
 
@@ -340,18 +359,19 @@ int64_t af_walkers(int64_t lo, int64_t hi, int64_t chunk) { return hi > lo ? (hi
 hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int mode, int64_t span0,
                           uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
                           uint8_t *status_b, void *meta_b, uint64_t *wcount, uint32_t *wgt, unsigned *overflow,
-                          hipStream_t s, int32_t *hwe_aux_b) {
+                          hipStream_t s, int32_t *hwe_aux_b, const WalkTail *tail) {
+    const WalkTail t = tail ? *tail : WalkTail{};
     const int64_t nw = af_walkers(lo, hi, chunk);
     if (!nw) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((nw + kWalkWaves - 1) / kWalkWaves);
     if (hwe_aux_b)
         hipLaunchKernelGGL(k_af_walk<HweOp>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, mode, span0,
                            cap_w, le_b, alt_b, tot_b, hwe_aux_b, rowpre_b, status_b, static_cast<LineMeta *>(meta_b),
-                           wcount, wgt, overflow);
+                           wcount, wgt, overflow, t);
     else
         hipLaunchKernelGGL(k_af_walk<AfOp>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, mode, span0,
                            cap_w, le_b, alt_b, tot_b, nullptr, rowpre_b, status_b, static_cast<LineMeta *>(meta_b),
-                           wcount, wgt, overflow);
+                           wcount, wgt, overflow, t);
     return hipGetLastError();
 }
 
@@ -360,11 +380,11 @@ hipError_t launch_walk_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t
                                const uint32_t *rowpre_b, const uint8_t *status_b, const void *meta_b,
                                uint64_t *line_end, int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
                                void *meta, uint64_t *n_lines, unsigned long long *counters, hipStream_t s,
-                               const int32_t *aux_b, int32_t *aux) {
+                               const int32_t *aux_b, int32_t *aux, const uint64_t *bpre) {
     const int64_t blocks = std::min<int64_t>((n_walkers + 256 / kWave - 1) / (256 / kWave), 512);
     hipLaunchKernelGGL(k_walk_compact, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s, n_walkers, cap_w,
                        offs, wgt, le_b, alt_b, tot_b, aux_b, rowpre_b, status_b, static_cast<const LineMeta *>(meta_b),
-                       line_end, alt, tot, aux, rowpre, status, static_cast<LineMeta *>(meta), n_lines, counters);
+                       line_end, alt, tot, aux, rowpre, status, static_cast<LineMeta *>(meta), n_lines, counters, bpre);
     return hipGetLastError();
 }
 

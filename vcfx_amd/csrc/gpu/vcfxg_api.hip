@@ -62,6 +62,12 @@ struct vcfxg_ctx {
     // walk AF path (vcfxg_af_walk.hip): per-walker regions, counts, scan, flags
     DevBuf wk_le, wk_alt, wk_tot, wk_rowpre, wk_status, wk_meta, wk_count, wk_offs, wk_gt, wk_small;
     DevBuf wk_tabs, rf_tabs;    // filter / query walk: per-line tab offsets (per walker, dense)
+    // AF walk region tail: per walker row bytes, text offsets, first line start; leftover list
+    DevBuf wk_text, wk_toff, wk_start, wk_cx, wk_bs, scratch_small;
+    // the last AF walk left its per-line results in walker regions only (ensure_dense)
+    bool dense_pending = false;
+    int64_t dense_nw = 0;
+    uint64_t dense_cap_w = 0;
     // VCFX_hwe_tester: hom-alt counts (dense, per walker), the host-recheck list and its length
     DevBuf hwe_aux, wk_aux, hwe_rc;
     uint64_t hwe_rc_n = 0;
@@ -175,6 +181,14 @@ int exclusive_scan(vcfxg_ctx *c, const InT *in, uint64_t *out, size_t n) {
 
 }  // namespace
 
+static int ensure_dense(vcfxg_ctx *c);
+// per-line calls on the indexed context read the dense arrays
+#define DENSE(c)                       \
+    do {                               \
+        int rd_ = ensure_dense(c);     \
+        if (rd_) return rd_;           \
+    } while (0)
+
 extern "C" {
 
 const char *vcfxg_version(void) { return "vcfx_amd 0.1 (gfx950)"; }
@@ -217,7 +231,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
         if (b->p) (void)hipFree(b->p);
     for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
     for (hipEvent_t e : c->ingest_ev_free) (void)hipEventDestroy(e);
@@ -302,6 +316,7 @@ int vcfxg_load_host(vcfxg_ctx *c, const char *host, size_t n) {
 }
 
 int vcfxg_ingest_begin(vcfxg_ctx *c, size_t size_hint) {
+    if (c) c->dense_pending = false;  // a new index / regions replace the pending ones
     if (!c) return VCFXG_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     int r = ensure(c, c->input, size_hint + kPad);
@@ -402,6 +417,7 @@ int vcfxg_input_fetch(vcfxg_ctx *c, uint64_t offset, size_t n, void *host) {
 const void *vcfxg_input_device_ptr(vcfxg_ctx *c) { return c && c->loaded ? c->input.p : nullptr; }
 
 int vcfxg_index(vcfxg_ctx *c, size_t data_start, uint64_t *n_lines) {
+    if (c) c->dense_pending = false;  // a new index / regions replace the pending ones
     if (!c) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
@@ -460,6 +476,7 @@ int vcfxg_index(vcfxg_ctx *c, size_t data_start, uint64_t *n_lines) {
 int vcfxg_line_ends(vcfxg_ctx *c, uint64_t first, uint64_t count, uint64_t *out) {
     if (!c || (!out && count)) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     if (first + count > c->n_lines) return VCFXG_E_ARG;
     if (!count) return VCFXG_OK;
     HIPCHK(c, hipMemcpyAsync(out, P<uint64_t>(c->line_end) + first, count * sizeof(uint64_t), hipMemcpyDeviceToHost,
@@ -483,6 +500,7 @@ static int af_rows(vcfxg_ctx *c, int mode, vcfxg_summary *out);
 int vcfxg_allele_freq(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     HIPCHK(c, hipSetDevice(c->device));
     const uint64_t L = c->n_lines;
     int r = af_buffers(c, L);
@@ -510,6 +528,7 @@ int vcfxg_allele_freq(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
 // newlines than the scratch keeps, or more lines than the capacity) reruns the call on the
 // synchronous path.
 static int af_region_async(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    if (c) c->dense_pending = false;  // a new index / regions replace the pending ones
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
     const int64_t nc = vcfxg::idx_wchunks(lo, hi);
@@ -603,13 +622,17 @@ static int af_region_async(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summ
 }
 
 // Walk region path (default when the first data lines average >= 512 B): no separate
-// index sweep.  k_af_walk reads each chunk's lines once, predicting fixed-stride record
-// ends and validating them by the sample sweep itself; the walkers' regions are scanned
-// and concatenated (k_walk_compact), k_af_complex takes the lines left to the exact
-// per-line path, then row lengths + scan and ONE host synchronisation before formatting,
-// as in af_region_async.  A walker over its line capacity reruns the call on the
-// two-sweep schedule (and later calls on this input use it directly).
+// index sweep.  k_af_walk reads each chunk's lines once, predicting fixed-stride record ends
+// and validating them by the sample sweep itself, and leaves per walker its lines' results,
+// its rows' bytes and a list of the lines for the exact per-line path.  The tail works on the
+// walkers' regions directly: k_af_cx (the listed lines), k_walker_scan (one block: walker line
+// and text offsets + the call summary), k_af_format_w (rows, into the previous call's text
+// capacity), then ONE host synchronisation.  The dense per-line arrays (line ends, counts,
+// statuses) are compacted from the regions only when a later call asks for them
+// (ensure_dense).  A walker over its line capacity, or an overlong leftover list, reruns the
+// call on the two-sweep schedule (and later calls on this input use it directly).
 static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    if (c) c->dense_pending = false;  // a new index / regions replace the pending ones
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
     const int64_t C = c->walk_chunk;
@@ -629,45 +652,45 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     if (!r) r = ensure(c, c->wk_count, 8 * (size_t)(nw + 1));
     if (!r) r = ensure(c, c->wk_offs, 8 * (size_t)(nw + 1));
     if (!r) r = ensure(c, c->wk_gt, 4 * (size_t)nw);
+    if (!r) r = ensure(c, c->wk_text, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_toff, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_start, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_cx, 8 * cap);
+    const int64_t nbs = (nw + vcfxg::kWalkerScanBlock - 1) / vcfxg::kWalkerScanBlock;
+    if (!r) r = ensure(c, c->wk_bs, 8 * (size_t)(5 * nbs + 4));
     if (!r) r = ensure(c, c->wk_small, 128);
-    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
-    if (!r) r = af_buffers(c, cap);
-    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (cap + 1));
     if (r) return r;
     const char *buf = P<char>(c->input);
-    uint64_t *small = P<uint64_t>(c->wk_small);  // [0] overflow flag, [4..10] summary
+    // [0] walk overflow flag (u32), [1] leftover count, [2..5] counters, [6] walker-scan
+    // arrivals (u32), [8..14] call summary
+    uint64_t *bpre_a = P<uint64_t>(c->wk_bs), *bpre_b = bpre_a + nbs + 1, *bsum = bpre_b + nbs + 1;
+    uint64_t *small = P<uint64_t>(c->wk_small);
     unsigned *ovf = reinterpret_cast<unsigned *>(small);
-    HIPCHK(c, hipMemsetAsync(small, 0, 32, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
-    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->wk_count) + nw, 0, 8, c->stream));
+    unsigned long long *cx_n = reinterpret_cast<unsigned long long *>(small + 1);
+    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(small + 2);
+    HIPCHK(c, hipMemsetAsync(small, 0, 128, c->stream));
+    vcfxg::WalkTail tail;
+    tail.wtext = P<uint64_t>(c->wk_text);
+    tail.wstart = P<uint64_t>(c->wk_start);
+    tail.cx_list = P<uint64_t>(c->wk_cx);
+    tail.cx_n = cx_n;
+    tail.cx_cap = cap;
     prof_begin(c, "af_walk");
     HIPCHK(c, vcfxg::launch_af_walk(buf, lo, hi, C, mode, c->hint_span, cap_w, P<uint64_t>(c->wk_le),
                                     P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre),
                                     P<uint8_t>(c->wk_status), c->wk_meta.p, P<uint64_t>(c->wk_count),
-                                    P<uint32_t>(c->wk_gt), ovf, c->stream));
+                                    P<uint32_t>(c->wk_gt), ovf, c->stream, nullptr, &tail));
     prof_end(c, "af_walk");
-    prof_begin(c, "walk_compact");
-    r = exclusive_scan(c, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_offs), (size_t)nw + 1);
-    if (r) return r;
-    HIPCHK(c, vcfxg::launch_walk_compact(nw, cap_w, P<uint64_t>(c->wk_offs), P<uint32_t>(c->wk_gt),
-                                         P<uint64_t>(c->wk_le), P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot),
-                                         P<uint32_t>(c->wk_rowpre), P<uint8_t>(c->wk_status), c->wk_meta.p,
-                                         P<uint64_t>(c->line_end), P<int32_t>(c->alt), P<int32_t>(c->tot),
-                                         P<uint32_t>(c->rowpre), P<uint8_t>(c->status), c->af_meta.p,
-                                         P<uint64_t>(c->d_nlines), P<unsigned long long>(c->counters), c->stream));
-    prof_end(c, "walk_compact");
     prof_begin(c, "af_complex");
-    HIPCHK(c, vcfxg::launch_af_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
-                                       c->af_meta.p, P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                       P<uint8_t>(c->status), P<unsigned long long>(c->counters), c->stream));
+    HIPCHK(c, vcfxg::launch_af_cx(buf, mode, cap_w, tail.cx_list, cx_n, cap, cap, tail.wstart, P<uint64_t>(c->wk_le),
+                                  c->wk_meta.p, P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot),
+                                  P<uint32_t>(c->wk_rowpre), P<uint8_t>(c->wk_status), tail.wtext, cnt, c->stream));
     prof_end(c, "af_complex");
     prof_begin(c, "af_rows");
-    HIPCHK(c, vcfxg::launch_af_rowlen(P<uint32_t>(c->rowpre), P<uint8_t>(c->status), P<uint64_t>(c->d_nlines), cap,
-                                      P<uint64_t>(c->rowlen), c->stream));
-    r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)cap + 1);
-    if (r) return r;
-    HIPCHK(c, vcfxg::launch_af_summary(P<uint64_t>(c->d_nlines), P<uint64_t>(c->rowoff),
-                                       P<unsigned long long>(c->counters), ovf, small + 4, c->stream));
+    HIPCHK(c, vcfxg::launch_walker_scan(nw, P<uint64_t>(c->wk_count), tail.wtext, P<uint32_t>(c->wk_gt),
+                                        P<uint64_t>(c->wk_offs), P<uint64_t>(c->wk_toff), bpre_a, bpre_b, bsum,
+                                        reinterpret_cast<unsigned *>(small + 6), cnt, ovf, P<uint64_t>(c->d_nlines),
+                                        small + 8, c->stream));
     prof_end(c, "af_rows");
     // the rows go out before the host has seen their total: into the text capacity of the
     // previous call (rows past it are skipped, and all are written again below once it has
@@ -676,13 +699,14 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     r = ensure(c, c->text, tcap + 1);
     if (r) return r;
     prof_begin(c, "af_format");
-    HIPCHK(c, vcfxg::launch_af_format(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, mode,
-                                      P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                      P<uint8_t>(c->status), P<uint64_t>(c->rowoff), P<char>(c->text), c->stream,
-                                      tcap));
+    HIPCHK(c, vcfxg::launch_af_format_w(buf, mode, nw, cap_w, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_toff),
+                                        bpre_b, tail.wstart, P<uint64_t>(c->wk_le), P<int32_t>(c->wk_alt),
+                                        P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre), P<uint8_t>(c->wk_status),
+                                        P<char>(c->text), tcap, c->stream));
     prof_end(c, "af_format");
-    static thread_local uint64_t sm[7];
-    HIPCHK(c, hipMemcpyAsync(sm, small + 4, sizeof sm, hipMemcpyDeviceToHost, c->stream));
+    // (the leftover list holds every slot at most once: it cannot overflow its capacity)
+    static thread_local uint64_t sm[7];  // lines, text bytes, counters[0..3], walk overflow
+    HIPCHK(c, hipMemcpyAsync(sm, small + 8, sizeof sm, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (sm[6]) {  // a walker ran out of line slots (short lines): the two-sweep schedule
         prof_collect(c);
@@ -695,10 +719,10 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
         r = ensure(c, c->text, text + 1);
         if (r) return r;
         prof_begin(c, "af_format");
-        HIPCHK(c, vcfxg::launch_af_format(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L, mode,
-                                          P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
-                                          P<uint8_t>(c->status), P<uint64_t>(c->rowoff), P<char>(c->text),
-                                          c->stream));
+        HIPCHK(c, vcfxg::launch_af_format_w(buf, mode, nw, cap_w, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_toff),
+                                            bpre_b, tail.wstart, P<uint64_t>(c->wk_le), P<int32_t>(c->wk_alt),
+                                            P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre),
+                                            P<uint8_t>(c->wk_status), P<char>(c->text), ~0ull, c->stream));
         prof_end(c, "af_format");
     }
     if (c->profiling) {
@@ -709,6 +733,9 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     c->n_lines = L;
     c->indexed = true;
     c->text_bytes = text;
+    c->dense_nw = nw;  // the dense arrays come from the regions on demand
+    c->dense_cap_w = cap_w;
+    c->dense_pending = true;
     if (out) {
         out->n_lines = L;
         out->rows = sm[2];
@@ -720,7 +747,26 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     return VCFXG_OK;
 }
 
-
+// the dense per-line arrays (line_end, alt, tot, rowpre, status, meta) of the last walk
+// region call, compacted from its walker regions (k_walk_compact; counters discarded)
+static int ensure_dense(vcfxg_ctx *c) {
+    if (!c->dense_pending) return VCFXG_OK;
+    c->dense_pending = false;
+    const uint64_t L = c->n_lines;
+    int r = ensure(c, c->line_end, 8 * (L + 1));
+    if (!r) r = af_buffers(c, L);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (L + 1));
+    if (!r) r = ensure(c, c->scratch_small, 64);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_walk_compact(c->dense_nw, c->dense_cap_w, P<uint64_t>(c->wk_offs), P<uint32_t>(c->wk_gt),
+                                         P<uint64_t>(c->wk_le), P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot),
+                                         P<uint32_t>(c->wk_rowpre), P<uint8_t>(c->wk_status), c->wk_meta.p,
+                                         P<uint64_t>(c->line_end), P<int32_t>(c->alt), P<int32_t>(c->tot),
+                                         P<uint32_t>(c->rowpre), P<uint8_t>(c->status), c->af_meta.p,
+                                         P<uint64_t>(c->d_nlines), P<unsigned long long>(c->scratch_small),
+                                         c->stream, nullptr, nullptr, P<uint64_t>(c->wk_bs)));
+    return VCFXG_OK;
+}
 
 int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
@@ -807,6 +853,7 @@ static void gq_parse_query(const char *q, size_t n, int &qa, int &qb) {
 int vcfxg_nonref_filter(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     HIPCHK(c, hipSetDevice(c->device));
     const uint64_t L = c->n_lines;
     int r = ensure(c, c->status, L + 1);
@@ -836,6 +883,7 @@ int vcfxg_nonref_filter(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
 int vcfxg_genotype_query(vcfxg_ctx *c, const char *query, size_t qlen, int strict, int strip_cr, vcfxg_summary *out) {
     if (!c || (!query && qlen)) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     HIPCHK(c, hipSetDevice(c->device));
     const uint64_t L = c->n_lines;
     int r = ensure(c, c->status, L + 1);
@@ -945,6 +993,7 @@ int vcfxg_record_filter_ex(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int
     for (int k = 0; k < n; k++)
         if (crit[k].target < 0 || crit[k].target > vcfxg::RF_QUAL_LENIENT) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
     int r = run_rf(c, crit, n, and_logic, (flags & VCFXG_RF_KEEP_CR) ? 1 : 0);
@@ -966,6 +1015,7 @@ int vcfxg_filter_query(vcfxg_ctx *c, const vcfxg_criterion *crit, int n, int and
                        int strict, vcfxg_summary *out) {
     if (!c || n < 0 || (n && !crit) || (!query && qlen)) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
     int r = run_rf(c, crit, n, and_logic);
@@ -1010,6 +1060,7 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
                      const char *query, size_t qlen, int strict, int gq_strip_cr, vcfxg_summary *out) {
     if (!c || n < 0 || (n && !crit) || (!query && qlen)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
+    c->dense_pending = false;  // its own index replaces pending regions
     if (data_start > c->n) data_start = c->n;
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n, C = c->walk_chunk;
@@ -1145,6 +1196,7 @@ int vcfxg_nonref_filter_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_
 // past the capacity are formatted again once it has grown.  A walker over its line capacity
 // reruns the call without the walk.
 static int hwe_region_impl(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out, bool walk) {
+    if (c) c->dense_pending = false;  // a new index / regions replace the pending ones
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
     const int64_t C = c->walk_chunk;
@@ -1290,6 +1342,7 @@ int vcfxg_hwe_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *o
 int vcfxg_hwe_rechecks(vcfxg_ctx *c, vcfxg_hwe_recheck *out, uint64_t cap, uint64_t *n) {
     if (!c || !n || (!out && cap)) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     *n = c->hwe_rc_n;
     const uint64_t k = std::min(cap, c->hwe_rc_n);
     if (!k) return VCFXG_OK;
@@ -1301,6 +1354,7 @@ int vcfxg_hwe_rechecks(vcfxg_ctx *c, vcfxg_hwe_recheck *out, uint64_t cap, uint6
 int vcfxg_variant_count(vcfxg_ctx *c, int strip_cr, vcfxg_summary *out) {
     if (!c) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     HIPCHK(c, hipSetDevice(c->device));
     int r = ensure(c, c->status, c->n_lines + 1);
     if (r) return r;
@@ -1334,6 +1388,7 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
                      int rstart, int rend, int parse_mode, uint64_t *n_variants) {
     if (!c || n_samples < 0 || (has_region && !rchrom && rlen)) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     HIPCHK(c, hipSetDevice(c->device));
     const uint64_t L = c->n_lines;
     const int kpad = n_samples > 0 ? ((n_samples + 63) / 64) * 64 : 64;  // MFMA k-steps of 32 B
@@ -1735,6 +1790,7 @@ int vcfxg_fetch_text(vcfxg_ctx *c, char *host, size_t cap) {
 int vcfxg_fetch_lines(vcfxg_ctx *c, uint64_t first, uint64_t count, int32_t *alt, int32_t *total, uint8_t *status) {
     if (!c) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
     if (first + count > c->n_lines) return VCFXG_E_ARG;
     if (!count) return VCFXG_OK;
     if (alt) HIPCHK(c, hipMemcpyAsync(alt, P<int32_t>(c->alt) + first, 4 * count, hipMemcpyDeviceToHost, c->stream));

@@ -52,16 +52,48 @@ int64_t idx_wchunk_bytes();
 // walks its lines (predicted fixed-stride ends validated by the sweep); per-walker regions
 // of cap_w lines, then k_walk_compact (offs = exclusive scan of wcount)
 int64_t af_walkers(int64_t lo, int64_t hi, int64_t chunk);
+// the AF walk's region tail (all null: the walk only fills its regions): per walker its row
+// bytes (GT lines) and first line start, and the list of region slots left to the exact
+// per-line path (kMetaFull lines, GT lines off the fixed-stride sweep)
+struct WalkTail {
+    uint64_t *wtext = nullptr;
+    uint64_t *wstart = nullptr;
+    uint64_t *cx_list = nullptr;
+    unsigned long long *cx_n = nullptr;
+    uint64_t cx_cap = 0;
+};
 hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int mode, int64_t span0,
                           uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
                           uint8_t *status_b, void *meta_b, uint64_t *wcount, uint32_t *wgt, unsigned *overflow,
-                          hipStream_t s, int32_t *hwe_aux_b = nullptr);
+                          hipStream_t s, int32_t *hwe_aux_b = nullptr, const WalkTail *tail = nullptr);
+// AF region tail without the dense per-line arrays (vcfxg_kernels.hip):
+//   launch_af_cx       the walk's leftover slots: af_line / the general sweep, new rows' bytes
+//                      added to their walker's total (counters as k_af_complex)
+//   launch_walker_scan one block: exclusive scans of the walkers' line counts and row bytes,
+//                      GT-line totals into counters[0..1], the line count to *n_lines and the
+//                      7-value call summary (lines, text bytes, counters[0..3], *fail)
+//   launch_af_format_w one wave per walker region: rows into out (rows ending past cap skipped)
+hipError_t launch_af_cx(const char *buf, int mode, uint64_t cap_w, const uint64_t *list, const unsigned long long *list_n,
+                        uint64_t list_cap, uint64_t list_cap_host, const uint64_t *wstart, const uint64_t *le_b,
+                        const void *meta_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b, uint8_t *status_b,
+                        uint64_t *wtext, unsigned long long *counters, hipStream_t s);
+// walker offsets are block-local: woff[w] + bpre[w / kWalkerScanBlock] (bsum: 3 per block,
+// bpre_*: blocks + 1 entries; *done zero before the launch)
+constexpr int kWalkerScanBlock = 1024;
+hipError_t launch_walker_scan(int64_t nw, const uint64_t *wcount, const uint64_t *wtext, const uint32_t *wgt,
+                              uint64_t *woff, uint64_t *wtoff, uint64_t *bpre_a, uint64_t *bpre_b, uint64_t *bsum,
+                              unsigned *done, unsigned long long *counters, const unsigned *fail, uint64_t *n_lines,
+                              uint64_t *summary, hipStream_t s);
+hipError_t launch_af_format_w(const char *buf, int mode, int64_t nw, uint64_t cap_w, const uint64_t *wcount,
+                              const uint64_t *wtoff, const uint64_t *bpre_b, const uint64_t *wstart,
+                              const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b, const uint32_t *rowpre_b,
+                              const uint8_t *status_b, char *out, uint64_t cap, hipStream_t s);
 hipError_t launch_walk_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t *offs, const uint32_t *wgt,
                                const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b,
                                const uint32_t *rowpre_b, const uint8_t *status_b, const void *meta_b,
                                uint64_t *line_end, int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
                                void *meta, uint64_t *n_lines, unsigned long long *counters, hipStream_t s,
-                               const int32_t *aux_b = nullptr, int32_t *aux = nullptr);
+                               const int32_t *aux_b = nullptr, int32_t *aux = nullptr, const uint64_t *bpre = nullptr);
 hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t *line_end,
                              const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, const void *meta,
                              int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,

@@ -728,6 +728,202 @@ __global__ void k_af_format(const char *__restrict__ buf, int64_t data_start, co
 }
 
 // =======================================================================================
+// AF region tail straight from the walk's regions (no dense per-line arrays)
+// =======================================================================================
+// the walk's leftover slots: kMetaFull lines run af_line (the exact per-line path), GT lines
+// whose fixed-stride sweep failed the general sweep (their row bytes are already counted);
+// a kMetaFull line that becomes a row adds its bytes to its walker's total
+__global__ __launch_bounds__(kRecThreads) void k_af_cx(const char *__restrict__ buf, int mode, uint64_t cap_w,
+                                                       const uint64_t *__restrict__ list,
+                                                       const unsigned long long *list_n, uint64_t list_cap,
+                                                       const uint64_t *__restrict__ wstart,
+                                                       const uint64_t *__restrict__ le_b,
+                                                       const LineMeta *__restrict__ meta_b, int32_t *__restrict__ alt_b,
+                                                       int32_t *__restrict__ tot_b, uint32_t *__restrict__ rowpre_b,
+                                                       uint8_t *__restrict__ status_b, uint64_t *__restrict__ wtext,
+                                                       unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kRecWaves][16];
+    __shared__ uint32_t cnt[BlockCounters::kNC];
+    if (threadIdx.x < BlockCounters::kNC) cnt[threadIdx.x] = 0;
+    __syncthreads();
+    BlockCounters bc{cnt};
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    const uint64_t n = std::min<uint64_t>(*list_n, list_cap);
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t e = wid; e < n; e += nw) {
+        const uint64_t sl = (uint64_t)uniform64((int64_t)list[e]);
+        const uint64_t w = sl / cap_w, i = sl - w * cap_w;
+        const int64_t le = (int64_t)le_b[sl];
+        const LineMeta m = meta_b[sl];
+        if (m.kind == kMetaGt) {
+            const int64_t ae = le - m.cr;
+            AfOp g{buf, ae, 0};
+            gt_general(buf, (int64_t)m.S, ae, g);
+            bc.add(3, 1);
+            if (lane() == 0) {
+                status_b[sl] = 1;
+                alt_b[sl] = (int32_t)g.alt;
+                tot_b[sl] = (int32_t)g.tot;
+            }
+            continue;
+        }
+        const int64_t ls = i ? (int64_t)le_b[sl - 1] + 1 : (int64_t)wstart[w];
+        uint8_t st;
+        uint32_t alt, tot, rowpre;
+        af_line(buf, ls, le, mode, lds, bc, st, alt, tot, rowpre);
+        if (lane() == 0) {
+            status_b[sl] = st;
+            alt_b[sl] = (int32_t)alt;
+            tot_b[sl] = (int32_t)tot;
+            rowpre_b[sl] = rowpre;
+            if (st == 1) atomicAdd(reinterpret_cast<unsigned long long *>(&wtext[w]), (unsigned long long)rowpre + 7ull);
+        }
+    }
+    flush_counters(cnt, counters);
+}
+
+// exclusive scans of the walkers' line counts and row bytes, 1024 walkers per block: each
+// block writes block-local offsets and its totals; the last block to finish scans the block
+// totals into bpre_* (entry k = the offsets before block k; bpre[nb] = the grand totals), so a
+// walker's offset is woff[w] + bpre[w >> 10] with no second pass.  The last block also adds
+// the GT-line total to counters[0..1] (rows, data lines) and writes the line count to *n_lines
+// and the call summary (lines, text bytes, counters[0..3], *fail).
+constexpr int kWScan = kWalkerScanBlock;
+__device__ __forceinline__ void block_scan2(uint64_t &a, uint64_t &b, uint64_t *sa, uint64_t *sb) {
+    // inclusive: wave scans, then the 16 wave totals by one wave
+    const int t = threadIdx.x, wv = t / kWave;
+    a = wave_incl_scan(a);
+    b = wave_incl_scan(b);
+    if (lane() == kWave - 1) {
+        sa[wv] = a;
+        sb[wv] = b;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        uint64_t x = lane() < kWScan / kWave ? sa[lane()] : 0, y = lane() < kWScan / kWave ? sb[lane()] : 0;
+        x = wave_incl_scan(x);
+        y = wave_incl_scan(y);
+        if (lane() < kWScan / kWave) {
+            sa[lane()] = x;
+            sb[lane()] = y;
+        }
+    }
+    __syncthreads();
+    if (wv) {
+        a += sa[wv - 1];
+        b += sb[wv - 1];
+    }
+}
+__global__ __launch_bounds__(kWScan) void k_walker_scan(int64_t nw, const uint64_t *__restrict__ wcount,
+                                                        const uint64_t *__restrict__ wtext,
+                                                        const uint32_t *__restrict__ wgt, uint64_t *__restrict__ woff,
+                                                        uint64_t *__restrict__ wtoff, uint64_t *bpre_a, uint64_t *bpre_b,
+                                                        uint64_t *bsum, unsigned *done,
+                                                        unsigned long long *counters, const unsigned *fail,
+                                                        uint64_t *n_lines, uint64_t *__restrict__ summary) {
+    __shared__ uint64_t sa[kWScan / kWave], sb[kWScan / kWave];
+    __shared__ bool last;
+    const int t = threadIdx.x;
+    const int64_t nb = (nw + kWScan - 1) / kWScan;
+    const int64_t w = (int64_t)blockIdx.x * kWScan + t;
+    const uint64_t a0 = w < nw ? wcount[w] : 0, b0 = w < nw ? wtext[w] : 0;
+    uint32_t g = w < nw ? wgt[w] : 0u;
+    uint64_t a = a0, b = b0;
+    block_scan2(a, b, sa, sb);
+    if (w <= nw) {  // (w == nw: the block total, the end offset within this block)
+        woff[w] = a - a0;
+        wtoff[w] = b - b0;
+    }
+    g = wave_sum(g);
+    __syncthreads();
+    __shared__ uint32_t sg[kWScan / kWave];
+    if (lane() == 0) sg[t / kWave] = g;
+    __syncthreads();
+    if (t == kWScan - 1) {
+        uint64_t G = 0;
+        for (int k = 0; k < kWScan / kWave; k++) G += sg[k];
+        // block totals -> bsum[3 * blk], published before the arrival count (device scope)
+        __hip_atomic_store(&bsum[3 * blockIdx.x], a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bsum[3 * blockIdx.x + 1], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&bsum[3 * blockIdx.x + 2], G, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned prev = __hip_atomic_fetch_add(done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        last = prev == (unsigned)nb - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    // the last block: prefix of the block totals (atomic loads: other CUs' stores)
+    if (t == 0) {
+        uint64_t ra = 0, rb = 0, G = 0;
+        for (int64_t k = 0; k < nb; k++) {
+            bpre_a[k] = ra;
+            bpre_b[k] = rb;
+            ra += __hip_atomic_load(&bsum[3 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            rb += __hip_atomic_load(&bsum[3 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            G += __hip_atomic_load(&bsum[3 * k + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        bpre_a[nb] = ra;
+        bpre_b[nb] = rb;
+        if (nw % kWScan == 0) {  // no thread stood at w == nw
+            woff[nw] = 0;
+            wtoff[nw] = 0;
+        }
+        *done = 0;  // ready for the next launch
+        counters[0] += G;
+        counters[1] += G;
+        *n_lines = ra;
+        summary[0] = ra;
+        summary[1] = rb;
+        for (int k = 0; k < 4; k++) summary[2 + k] = counters[k];
+        summary[6] = *fail;
+    }
+}
+
+// one wave per walker region: row offsets = the walker's text offset + a wave scan of its
+// rows' lengths; each lane writes its line's row (rows ending past cap are skipped)
+__global__ __launch_bounds__(256) void k_af_format_w(const char *__restrict__ buf, int mode, int64_t nw, uint64_t cap_w,
+                                                     const uint64_t *__restrict__ wcount,
+                                                     const uint64_t *__restrict__ wtoff,
+                                                     const uint64_t *__restrict__ bpre_b,
+                                                     const uint64_t *__restrict__ wstart,
+                                                     const uint64_t *__restrict__ le_b, const int32_t *__restrict__ alt_b,
+                                                     const int32_t *__restrict__ tot_b,
+                                                     const uint32_t *__restrict__ rowpre_b,
+                                                     const uint8_t *__restrict__ status_b, char *__restrict__ out,
+                                                     uint64_t cap) {
+    const int64_t nwv = (int64_t)gridDim.x * (256 / kWave);
+    for (int64_t w = (int64_t)blockIdx.x * (256 / kWave) + threadIdx.x / kWave; w < nw; w += nwv) {
+        const uint64_t n = wcount[w], s0 = (uint64_t)w * cap_w;
+        uint64_t run = wtoff[w] + bpre_b[w / kWScan];
+        for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
+            const uint64_t i = i0 + lane(), sl = s0 + i;
+            const bool in = i < n;
+            const uint32_t pl = in ? rowpre_b[sl] : 0u;
+            const uint32_t len = in && status_b[sl] == 1 ? pl + 7u : 0u;
+            const uint32_t incl = wave_incl_scan(len);
+            const uint64_t off = run + incl - len;
+            run += wave_bcast(incl, kWave - 1);
+            if (!len || off + len > cap) continue;
+            const int64_t ls = i ? (int64_t)le_b[sl - 1] + 1 : (int64_t)wstart[w];
+            char *o = out + off;
+            for (uint32_t k = 0; k < pl; k++) o[k] = buf[ls + k];
+            const int a = alt_b[sl], t = tot_b[sl];
+            const double f = t > 0 ? __ddiv_rn((double)a, (double)t) : 0.0;
+            const uint32_t k4 = mode == 0 ? fixed4_mmap(f) : fixed4_printf(f);
+            const uint32_t ip = k4 / 10000u, fp = k4 % 10000u;
+            o += pl;
+            o[0] = (char)('0' + ip);
+            o[1] = '.';
+            o[2] = (char)('0' + fp / 1000u);
+            o[3] = (char)('0' + (fp / 100u) % 10u);
+            o[4] = (char)('0' + (fp / 10u) % 10u);
+            o[5] = (char)('0' + fp % 10u);
+            o[6] = '\n';
+        }
+    }
+}
+
+// =======================================================================================
 // launchers
 // =======================================================================================
 static unsigned grid_for(int64_t n, int64_t per, unsigned cap) {
@@ -901,6 +1097,35 @@ hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t 
     if (!n_lines_host) return hipSuccess;
     hipLaunchKernelGGL(k_af_format, dim3(grid_for((int64_t)n_lines_host, 256, 4096)), dim3(256), 0, s, buf, data_start,
                        line_end, n_lines_dev, mode, alt, tot, rowpre, status, off, out, text_cap);
+    return hipGetLastError();
+}
+
+hipError_t launch_af_cx(const char *buf, int mode, uint64_t cap_w, const uint64_t *list, const unsigned long long *list_n,
+                        uint64_t list_cap, uint64_t list_cap_host, const uint64_t *wstart, const uint64_t *le_b,
+                        const void *meta_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b, uint8_t *status_b,
+                        uint64_t *wtext, unsigned long long *counters, hipStream_t s) {
+    // the list is short (the walk's leftovers); a wave per entry, grid-stride
+    const unsigned grid = grid_for((int64_t)std::max<uint64_t>(list_cap_host, 1), kRecWaves, 2048);
+    hipLaunchKernelGGL(k_af_cx, dim3(grid), dim3(kRecThreads), 0, s, buf, mode, cap_w, list, list_n, list_cap, wstart,
+                       le_b, static_cast<const LineMeta *>(meta_b), alt_b, tot_b, rowpre_b, status_b, wtext, counters);
+    return hipGetLastError();
+}
+hipError_t launch_walker_scan(int64_t nw, const uint64_t *wcount, const uint64_t *wtext, const uint32_t *wgt,
+                              uint64_t *woff, uint64_t *wtoff, uint64_t *bpre_a, uint64_t *bpre_b, uint64_t *bsum,
+                              unsigned *done, unsigned long long *counters, const unsigned *fail, uint64_t *n_lines,
+                              uint64_t *summary, hipStream_t s) {
+    const int64_t nb = std::max<int64_t>((nw + kWScan - 1) / kWScan, 1);
+    hipLaunchKernelGGL(k_walker_scan, dim3((unsigned)nb), dim3(kWScan), 0, s, nw, wcount, wtext, wgt, woff, wtoff,
+                       bpre_a, bpre_b, bsum, done, counters, fail, n_lines, summary);
+    return hipGetLastError();
+}
+hipError_t launch_af_format_w(const char *buf, int mode, int64_t nw, uint64_t cap_w, const uint64_t *wcount,
+                              const uint64_t *wtoff, const uint64_t *bpre_b, const uint64_t *wstart,
+                              const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b, const uint32_t *rowpre_b,
+                              const uint8_t *status_b, char *out, uint64_t cap, hipStream_t s) {
+    if (nw <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_af_format_w, dim3(grid_for(nw, 256 / kWave, 16384)), dim3(256), 0, s, buf, mode, nw, cap_w,
+                       wcount, wtoff, bpre_b, wstart, le_b, alt_b, tot_b, rowpre_b, status_b, out, cap);
     return hipGetLastError();
 }
 
