@@ -54,6 +54,10 @@ constexpr int kRing = kNBuf * kStage;  // 128 KiB
 constexpr int kQuarter = 64 * 64 * 4;  // one wave's 64x64 int32 epilogue tile
 static_assert(kWaves * kQuarter <= kRing, "epilogue tiles must fit in the staging ring");
 constexpr int kGlds = kStage / 1024 / kWaves;  // 1 KiB glds instructions per wave per stage
+constexpr int kFvBytes = kFB * 40;             // one side's LdFast records (40 B each)
+constexpr int kFvGlds = kFvBytes / 1024;       // 1 KiB pieces of them
+static_assert(kFvBytes % 1024 == 0, "the records are DMA'd in whole 1 KiB pieces");
+static_assert(sizeof(LdFast) == 40, "LdFast layout");
 static_assert(kGlds == 4, "the k-loop's vmcnt counts assume 4 glds per wave per stage");
 
 __device__ __forceinline__ void glds16(const void *src, int8_t *lds_base) {
@@ -98,8 +102,8 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdWindowArgs &a,
                                               const LdFast *__restrict__ fv, const uint32_t *__restrict__ chrom_id,
                                               uint16_t *__restrict__ cnt, const float *ru, const float *rsf,
-                                              uint32_t I4, uint32_t J4, int wi, int wj, int h, int r,
-                                              int (&qtot)[2]) {
+                                              const float *cw, const float *cv, uint32_t I4, uint32_t J4, int wi,
+                                              int wj, int h, int r, int (&qtot)[2]) {
     const int64_t M = (int64_t)a.m;
     const double dn = (double)a.ns;
     const uint64_t bI = 4ull * I4 + wi;
@@ -115,9 +119,9 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
         const int64_t j = (int64_t)(bJ * kLdBlock) + 32 * (y & 1) + r;
         jv[y] = j;
         const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
-        const LdFast f = fv[jok ? j : 0];
-        wv[y] = a.ns > 0 ? -(float)f.sx / (float)a.ns : 0.f;  // (n = 0: every r^2 is 0, no NaN)
-        vj[y] = a.all_pass ? 0.f : sqrtf((float)f.vxp);
+        const int cj = (2 * wj + (y >> 1)) * kLdBlock + 32 * (y & 1) + r;  // column within the tile
+        wv[y] = cw[cj];
+        vj[y] = cv[cj];
         // valid rows [lo, lo + span) of the 64-block: i in [j - window, j)
         const int64_t l0 = j - (int64_t)a.window - i0;
         const int64_t h0 = j - i0;
@@ -213,12 +217,18 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
     // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
     // ds_reads): the staging ring during the k-loop, then the waves' epilogue tiles over it;
     // the per-row prefilter terms after that
-    __shared__ __attribute__((aligned(16))) int8_t lds[kRing + kFB * (8 + 4 + 4 + 4 + 4)];
+    // ... and the tile's raw per-variant records (rows I, columns J), DMA'd in with the first
+    // stages so no global-load latency sits before the k-loop or the epilogue
+    __shared__ __attribute__((aligned(16))) int8_t lds[kRing + kFB * (8 + 4 + 4 + 4 + 4 + 4 + 4) + 2 * kFvBytes];
     double *rvx = reinterpret_cast<double *>(lds + kRing);
     int *rsx = reinterpret_cast<int *>(lds + kRing + kFB * 8);
     float *rvxf = reinterpret_cast<float *>(lds + kRing + kFB * 12);
     float *ru = reinterpret_cast<float *>(lds + kRing + kFB * 16);  // register epilogue: sqrt(tm' Vx) / n
     float *rsf = reinterpret_cast<float *>(lds + kRing + kFB * 20);  // and Sx as fp32
+    float *cw = reinterpret_cast<float *>(lds + kRing + kFB * 24);   // columns: -Sy / n
+    float *cv = reinterpret_cast<float *>(lds + kRing + kFB * 28);   // and sqrt(Vy)
+    const LdFast *fI = reinterpret_cast<const LdFast *>(lds + kRing + kFB * 32);
+    const LdFast *fJ = reinterpret_cast<const LdFast *>(lds + kRing + kFB * 32 + kFvBytes);
     const uint32_t b = xcd_remap(blockIdx.x, nblocks);
     const uint32_t I4 = blocks[2 * b], J4 = blocks[2 * b + 1];
     const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
@@ -246,14 +256,14 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
         }
         if (!__syncthreads_or(any != 0)) return;
     }
-    if (t < kFB) {
-        const int64_t i = ibase + t < M ? ibase + t : M - 1;
-        const LdFast f = fv[i];
-        rvx[t] = f.vxp;
-        rvxf[t] = (float)f.vxp;
-        ru[t] = a.all_pass ? 0.f : sqrtf((float)(a.tm * (1.0 - 1e-5)) * (float)f.vxp) / (float)a.ns;
-        rsf[t] = (float)f.sx;
-        rsx[t] = f.sx;
+    {  // the I and J records: kFvBytes each, 1 KiB per wave-instruction (lanes past the array
+        // re-read its last 16 B: those rows / columns are outside the matrix and never used)
+        const char *fv_end = reinterpret_cast<const char *>(fv + M) - 16;
+        for (int q = w; q < 2 * kFvGlds; q += kWaves) {
+            const int side = q / kFvGlds, part = q - side * kFvGlds;
+            const char *s = reinterpret_cast<const char *>(fv + (side ? jbase : ibase)) + part * 1024 + l * 16;
+            glds16(s < fv_end ? s : fv_end, lds + kRing + kFB * 32 + side * kFvBytes + part * 1024);
+        }
     }
     const int kpad = a.kp4;  // FP4 row bytes
     // staging: 32 wave-instructions of 1 KiB per stage, kGlds per wave; instruction q of
@@ -359,6 +369,21 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
         if (z == 0x7fffffff) cnt[0] = 1;
         return;
     }
+    // the row and column terms from the DMA'd records (every wave's loads done, then visible)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t < kFB) {
+        const LdFast f = fI[t];
+        rvx[t] = f.vxp;
+        rvxf[t] = (float)f.vxp;
+        ru[t] = a.all_pass ? 0.f : sqrtf((float)(a.tm * (1.0 - 1e-5)) * (float)f.vxp) / (float)a.ns;
+        rsf[t] = (float)f.sx;
+        rsx[t] = f.sx;
+    } else {
+        const LdFast f = fJ[t - kFB];
+        cw[t - kFB] = a.ns > 0 ? -(float)f.sx / (float)a.ns : 0.f;  // (n = 0: every r^2 is 0, no NaN)
+        cv[t - kFB] = a.all_pass ? 0.f : sqrtf((float)f.vxp);
+    }
     const int pad = 0;  // FP4 rows are zero-padded
     const double dn = (double)a.ns;
     const int64_t n = a.ns;
@@ -428,9 +453,9 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
         }
     };
     if (P == 1 && a.ns <= 23170) {
-        __syncthreads();  // the row terms written before the k-loop are visible to every wave
+        __syncthreads();  // the row and column terms are visible to every wave
         int qt[2];
-        ld_count_regs(acc, a, fv, chrom_id, cnt, ru, rsf, I4, J4, wi, wj, h, r, qt);
+        ld_count_regs(acc, a, fv, chrom_id, cnt, ru, rsf, cw, cv, I4, J4, wi, wj, h, r, qt);
         if (!st.temp) return;
         // quarters holding pairs: written now, column-major into a bump-allocated staging
         // area (ld_scatter later moves each column's run to its ordered offset), so the
