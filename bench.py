@@ -53,6 +53,11 @@ def parse():
     ap.add_argument("--samples", type=int, default=2504)
     ap.add_argument("--window", type=int, default=100000, help="ld: window in variants")
     ap.add_argument("--threshold", type=float, default=0.5, help="ld: r^2 threshold")
+    ap.add_argument("--format", choices=("gt", "gt:ad:dp"), default="gt",
+                    help="FORMAT of the synthetic records: GT (fixed-stride) or GT:AD:DP (the general GT path)")
+    ap.add_argument("--missing-rate", type=float, default=0.0, help="per-sample './.' probability")
+    ap.add_argument("--irregular-rate", type=float, default=0.0,
+                    help="fraction of records in a general-path shape (GT:DP, DP:GT, '/', haploid, multi-digit)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end CLI timings")
@@ -163,6 +168,8 @@ def output_check(workload, eng, s, a, rank):
     except OSError:
         return {"checked": False, "why": "no tests/golden/full_digests.json"}
     default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "hwe": 427409, "ld": 100000}[workload]
+    if a.format != "gt" or a.missing_rate > 0 or a.irregular_rate > 0:
+        return {"checked": False, "why": "no reference digest for the general-path data"}
     if rank != 0 or a.records != default or a.samples != 2504 or (workload == "ld" and (a.window < 3000 or
                                                                                          a.threshold != 0.5)):
         return {"checked": False, "why": "no reference digest for this rank/configuration"}
@@ -297,8 +304,10 @@ def main():
     from vcfx_amd import engine, synth
 
     ld = a.workload == "ld"
+    general = a.format != "gt" or a.missing_rate > 0 or a.irregular_rate > 0
     arr, offs = synth.generate_array(a.records, a.samples, seed=20251226 + rank, hap_blocks=1 if ld else 0,
-                                     rec_offsets=True)
+                                     rec_offsets=True, missing_rate=a.missing_rate, irregular_rate=a.irregular_rate,
+                                     format_mode=1 if a.format == "gt:ad:dp" else 0)
     ds = engine.data_start_of(arr[:1 << 20].tobytes(), strip_cr=not ld)
     eng = engine.Engine(local)
     eng.load(arr)
@@ -398,9 +407,9 @@ def main():
             a.records // 1000, a.samples)
     else:
         assert s.rows > 0 and s.n_lines == a.records, (s.rows, s.n_lines)
-        if a.workload == "af":
+        if a.workload == "af" and not general:
             assert s.rows == a.records and s.general_records == 0
-        if a.workload == "hwe":
+        if a.workload == "hwe" and not general:
             assert s.general_records == 0
         units_total = a.records * world
         unit, metric = "records/s", METRIC
@@ -437,7 +446,9 @@ def main():
                 # HWE: the same walk with three class counts per line (8 + 17 + 16)
                 "hwe_walk": region_bytes + L * (8 + 17 + 16),
                 "walk_compact": L * 2 * (8 + 13 + 16),
-                "af_complex": L * (16 + 1),
+                # the per-line rest: its lines' record bytes when the data are off the fixed-stride
+                # layout (every line a GT:AD:DP record), else the head record + status per line
+                "af_complex": (region_bytes if a.format != "gt" else 0) + L * (16 + 1),
                 "af_format": tb + L * (8 + 8 + 13) + s.rows * 40,
                 "af_rows": L * (5 + 8 + 8 + 8),
                 "rf_records": region_bytes + L * (8 + 1),
@@ -456,6 +467,11 @@ def main():
             roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(a.workload, dom),
                     "algorithmic_bytes_per_launch": int(algo[dom]), "avg_launch_ms": kernels[dom]}
+        if general:
+            extra = " [data: FORMAT=%s, missing rate %g, irregular rate %g: the general GT path]" % (
+                a.format.upper(), a.missing_rate, a.irregular_rate)
+        else:
+            extra = ""
         workload = {
             "af": "VCFX_allele_freq_calc -i (file path) on a device-resident %d x %d VCF shard per GPU: index + "
                   "allele counts + formatted rows" % (a.records, a.samples),
@@ -467,7 +483,7 @@ def main():
                    "genotype-class reducer + HWE chi-square p-value rows" % (a.records, a.samples),
             "ld": "VCFX_ld_calculator -w %d -t %g streaming on a device-resident %d x %d shard per GPU: parse + "
                   "FP4-MFMA pair sums (count + emit) + pair text" % (a.window, a.threshold, a.records, a.samples),
-        }[a.workload]
+        }[a.workload] + extra
         out = {
             "metric": metric,
             "value": value,
@@ -480,8 +496,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp4(e2m1)->f32" if ld else "u8",
-            "data": "synthetic: vcfx_synth seed 20251226+rank, chr21-like layout (FORMAT=GT, phased a|b, INFO=.)"
-                    + (", founder-haplotype blocks" if ld else ""),
+            "data": "synthetic: vcfx_synth seed 20251226+rank, chr21-like layout (FORMAT=%s, phased a|b, INFO=.)"
+                    % a.format.upper() + (", founder-haplotype blocks" if ld else ""),
             "config": {"workload": workload, "records_per_gpu": a.records, "samples": a.samples,
                        "bytes_per_gpu": int(arr.size),
                        "parallelism": "record-sharded x%d%s" % (world, ", RCCL all-reduce of global counts"
@@ -494,7 +510,7 @@ def main():
             out["pairs_per_gpu"] = pairs
             out["pairs_emitted"] = np_
         out["output_check"] = output_check(a.workload, eng, s, a, rank)
-        if world == 1 and not a.no_e2e:
+        if world == 1 and not a.no_e2e and not general:
             out["e2e"] = e2e_rates(a.workload, arr, a)
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.workload, arr, offs, a)

@@ -84,3 +84,24 @@ def test_af_cli_binary_end_to_end(tmp_path):
     r = subprocess.run([tool_binary("VCFX_allele_freq_calc")], input=buf, capture_output=True, timeout=300)
     want, werr, wrc = o.run(["VCFX_allele_freq_calc"], buf)
     assert (r.stdout, r.stderr, r.returncode) == (want, werr, wrc)
+
+
+@pytest.mark.parametrize("cfg", [dict(n_records=1200, n_samples=2504, seed=31, missing_rate=0.001, format_mode=1),
+                                 dict(n_records=700, n_samples=301, seed=32, missing_rate=0.05, irregular_rate=0.2,
+                                      crlf=1, format_mode=1)])
+def test_af_gt_ad_dp_region_matches_oracle(eng, oracle, cfg, tmp_path):
+    """FORMAT=GT:AD:DP (variable-width samples: every record off the fixed-stride sweep) through
+    the region path (walk + leftover lines) and the drop-in tool, both modes"""
+    buf = synth.generate(**cfg)
+    for mode in (engine.MODE_FILE, engine.MODE_STDIN):
+        ds = engine.data_start_of(buf, strip_cr=(mode == engine.MODE_FILE))
+        eng.load(buf)
+        s = eng.allele_freq_region(ds, mode)
+        assert s.general_records == cfg["n_records"]
+        p = tmp_path / "in.vcf"
+        p.write_bytes(buf)
+        argv = ["VCFX_allele_freq_calc", "-q"] + (["-i", str(p)] if mode == engine.MODE_FILE else [])
+        stdin = b"" if mode == engine.MODE_FILE else buf
+        want = oracle.run(argv, stdin)
+        assert b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes) == want[0]
+        assert tools.run(argv, stdin) == want

@@ -118,3 +118,15 @@ def test_hwe_recheck_path(oracle, mode, tmp_path):
     else:
         got = subprocess.run([BIN], input=buf, capture_output=True, env=env, timeout=120)
     assert got.returncode == 0 and got.stdout == want
+
+
+@pytest.mark.parametrize("cfg", [dict(n_records=900, n_samples=2504, seed=78, missing_rate=0.002, format_mode=1),
+                                 dict(n_records=600, n_samples=97, seed=79, irregular_rate=0.3, crlf=1,
+                                      format_mode=1)])
+def test_hwe_gt_ad_dp_matches_oracle(oracle, cfg, tmp_path):
+    """FORMAT=GT:AD:DP records (the per-line path) in both modes"""
+    buf = synth.generate(**cfg)
+    path = tmp_path / "in.vcf"
+    path.write_bytes(buf)
+    for argv, stdin in ((["VCFX_hwe_tester", "-i", str(path)], b""), (["VCFX_hwe_tester"], buf)):
+        assert tools.run(argv, stdin) == oracle.run(argv, stdin), argv[1:2]

@@ -164,6 +164,100 @@ __device__ __forceinline__ int64_t sample_end(const char *__restrict__ buf, int6
 }
 
 // ---------------------------------------------------------------------------------------
+// gt_first: records whose FORMAT starts with GT and has more sub-fields ("GT:AD:DP", ...), so
+// samples have any width.  One pass over [S, hi) finds the line end E (the first '\n', or hi;
+// cr = its '\r' when strip_cr, ae = E - cr) and, for every sample start p in [S, ae) (S and
+// each tab + 1), takes the bytes c0..c3 at p: a "quick" GT is c0 s c2 with s '/' or '|', c0
+// and c2 not a separator, ':', tab, space or '\r', and c3 ':' or tab or p + 3 == ae -- the
+// GT sub-field of exactly 3 bytes, whose tokens are c0 and c2 alone: op.gt3(c0, c2).  Any
+// other sample makes the result false (wave-uniform): the caller runs gt_general with the
+// end it now knows.  pre(E) is called once, as soon as E is known (the next line's prefetch).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool gt_special(uint32_t c) {
+    return c == '/' || c == '|' || c == ':' || c == '\t' || c == ' ' || c == '\r';
+}
+template <int kU, class Op, class Pre>
+__device__ bool gt_first(const char *__restrict__ buf, int64_t S, int64_t hi, int strip_cr, Op &op, Pre pre,
+                         int64_t &E_out, uint8_t &cr_out) {
+    S = uniform64(S);
+    int64_t E = hi, ae = hi;
+    bool found = false, bad = false;
+    uint32_t carry = 0;  // byte 15 of the previous wave-step's last lane
+    const int64_t b0 = S & ~(int64_t)15;
+    const int lo16 = lane() * kBlockBytes;
+    for (int64_t w0 = b0; w0 < hi && !found; w0 += kU * kWaveStep) {
+        uint4 v[kU];
+        uint32_t x4[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {  // branch-free: lanes past hi re-read the last block
+            const int64_t blk = w0 + u * kWaveStep + lo16;
+            const int64_t bl = blk < hi ? blk : ((hi - 1) & ~(int64_t)15);
+            v[u] = load16(buf, bl);
+            x4[u] = load4(buf, bl + 16);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            if (found) break;
+            const int64_t blk = w0 + u * kWaveStep + lo16;
+            const uint32_t nlm = blk < hi ? eq_mask16(v[u], kRepNl) & range_mask16(blk, S, hi) : 0u;
+            const uint64_t anyn = __ballot(nlm != 0u);
+            if (anyn) {
+                const int k = __builtin_ctzll(anyn);
+                E = uniform64(w0 + u * kWaveStep + 16 * k + __builtin_ctz((uint32_t)__shfl((int)nlm, k)));
+                found = true;
+                const uint32_t cr = strip_cr && E > S ? __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r' : 0u;
+                cr_out = (uint8_t)cr;
+                ae = E - cr;
+                pre(E);
+            }
+            // sample starts: S, and the byte after every tab, in [S, ae)
+            const uint32_t tm = eq_mask16(v[u], kRepTab);
+            const uint32_t last = (uint32_t)__shfl_up((int)(v[u].w >> 24), 1);
+            const uint32_t prev = lane() ? last : carry;
+            carry = (uint32_t)__shfl((int)(v[u].w >> 24), kWave - 1);
+            uint32_t starts = ((tm << 1) & 0xFFFFu) | (prev == '\t' ? 1u : 0u);
+            if (S >= blk && S < blk + 16) starts |= 1u << (S - blk);
+            starts &= range_mask16(blk, S, ae);
+            const uint32_t wd[5] = {v[u].x, v[u].y, v[u].z, v[u].w, x4[u]};
+            while (starts) {
+                const int o = __builtin_ctz(starts);
+                starts &= starts - 1u;
+                const int q = o >> 2;
+                const uint32_t lo = q == 0 ? wd[0] : q == 1 ? wd[1] : q == 2 ? wd[2] : wd[3];
+                const uint32_t hw = q == 0 ? wd[1] : q == 1 ? wd[2] : q == 2 ? wd[3] : wd[4];
+                const uint32_t d = __builtin_amdgcn_alignbyte(hw, lo, (uint32_t)(o & 3));
+                const uint32_t c0 = d & 0xFFu, c1 = (d >> 8) & 0xFFu, c2 = (d >> 16) & 0xFFu, c3 = d >> 24;
+                const int64_t p3 = blk + o + 3;
+                const bool quick = (c1 == '/' || c1 == '|') && !gt_special(c0) && !gt_special(c2) &&
+                                   (p3 == ae || (p3 < ae && (c3 == ':' || c3 == '\t')));
+                if (quick) op.gt3(c0, c2);
+                else bad = true;
+            }
+        }
+    }
+    if (!found) {
+        E = hi;
+        const uint32_t cr = strip_cr && E > S ? __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r' : 0u;
+        cr_out = (uint8_t)cr;
+        pre(E);
+    }
+    E_out = E;
+    if (__any(bad)) return false;
+    op.finish();
+    return true;
+}
+struct NoPreE {
+    __device__ void operator()(int64_t) const {}
+};
+// the GT-first sweep over a sample region [S, ae) of known end (no '\n' inside)
+template <int kU = 4, class Op>
+__device__ __forceinline__ bool gt_first_known(const char *__restrict__ buf, int64_t S, int64_t ae, Op &op) {
+    int64_t e;
+    uint8_t cr;
+    return gt_first<kU>(buf, S, ae, 0, op, NoPreE(), e, cr);
+}
+
+// ---------------------------------------------------------------------------------------
 // allele-count reducer: parseGenotypeAndCount (VCFX_allele_freq_calc.cpp:262-293) over
 // extractGT (:321-337)
 // ---------------------------------------------------------------------------------------
@@ -177,6 +271,11 @@ struct AfOp {
     __device__ void dword(const DwordView &v) {
         tot += __popc(v.dig);
         alt += __popc((v.f + 0x00FF00FFu) & v.dig);  // digit 1..9
+    }
+    // a 3-byte GT "c0 s c2" (gt_first): each single-byte token counts if it is a digit
+    __device__ void gt3(uint32_t c0, uint32_t c2) {
+        tot += (c0 - '0' < 10u) + (c2 - '0' < 10u);
+        alt += (c0 - '1' < 9u) + (c2 - '1' < 9u);
     }
     __device__ void sample(int64_t st) {
         int64_t p = st;
@@ -431,6 +530,14 @@ struct HweOp {
         nv_alt += ok ? (uint32_t)__popc(v.f) + 0x10000u : 0u;
         two += v.f == 0x00010001u;
     }
+    __device__ void gt3(uint32_t c0, uint32_t c2) {  // both '0' or '1': the class a + b
+        const bool ok = (c0 - '0' < 2u) && (c2 - '0' < 2u);
+        const uint32_t s = (c0 - '0') + (c2 - '0');
+        c0_ += ok && s == 0u;
+        c1_ += ok && s == 1u;
+        c2_ += ok && s == 2u;
+    }
+    uint32_t c0_ = 0, c1_ = 0, c2_ = 0;  // gt_first's counts (folded in finish())
     __device__ void sample(int64_t st) {
         const int g = hwe_parse(buf, st, sample_end(buf, st, E));
         c0 += g == 0;
@@ -439,9 +546,9 @@ struct HweOp {
     }
     __device__ void finish() {
         const uint32_t nv = nv_alt >> 16, alt = nv_alt & 0xFFFFu;
-        c2 += two;
-        c1 += alt - 2u * two;
-        c0 += nv - (alt - two);
+        c2 += two + c2_;
+        c1 += alt - 2u * two + c1_;
+        c0 += nv - (alt - two) + c0_;
         c0 = wave_sum(c0);
         c1 = wave_sum(c1);
         c2 = wave_sum(c2);

@@ -56,9 +56,11 @@ __device__ __forceinline__ void hwe_line(const char *__restrict__ buf, int64_t l
     }
     HweOp op{buf, ae};
     if (!gt_fast(buf, S, ae, op)) {
-        HweOp g{buf, ae};
-        gt_general(buf, S, ae, g);
-        op = g;
+        op = HweOp{buf, ae};
+        if (!gt_first_known(buf, S, ae, op)) {  // (every sample's first sub-field is its GT)
+            op = HweOp{buf, ae};
+            gt_general(buf, S, ae, op);
+        }
         general = true;
     }
     st = 1;

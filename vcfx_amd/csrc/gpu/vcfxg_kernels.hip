@@ -180,6 +180,10 @@ __device__ __forceinline__ void af_line(const char *__restrict__ buf, int64_t ls
                     const int64_t S = t[8] + 1;
                     AfOp op{buf, ae, gi};
                     bool fast = gi == 0 && gt_fast(buf, S, ae, op);
+                    if (!fast && gi == 0) {  // GT-first, variable-width samples
+                        op = AfOp{buf, ae, gi};
+                        fast = gt_first_known(buf, S, ae, op);
+                    }
                     if (fast) {
                         alt = op.alt;
                         tot = op.tot;
@@ -380,7 +384,10 @@ __global__ __launch_bounds__(kRecThreads) void k_af_complex(const char *__restri
                 const AfMeta m = meta[li];
                 const int64_t ae = (int64_t)line_end[li] - m.cr;
                 AfOp g{buf, ae, 0};
-                gt_general(buf, (int64_t)m.S, ae, g);
+                if (!gt_first_known(buf, (int64_t)m.S, ae, g)) {
+                    g = AfOp{buf, ae, 0};
+                    gt_general(buf, (int64_t)m.S, ae, g);
+                }
                 bc.add(3, 1);
                 if (lane() == 0) {
                     status_o[li] = 1;
@@ -759,7 +766,10 @@ __global__ __launch_bounds__(kRecThreads) void k_af_cx(const char *__restrict__ 
         if (m.kind == kMetaGt) {
             const int64_t ae = le - m.cr;
             AfOp g{buf, ae, 0};
-            gt_general(buf, (int64_t)m.S, ae, g);
+            if (!gt_first_known(buf, (int64_t)m.S, ae, g)) {
+                g = AfOp{buf, ae, 0};
+                gt_general(buf, (int64_t)m.S, ae, g);
+            }
             bc.add(3, 1);
             if (lane() == 0) {
                 status_b[sl] = 1;

@@ -256,13 +256,15 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
         }
         if (!__syncthreads_or(any != 0)) return;
     }
-    {  // the I and J records: kFvBytes each, 1 KiB per wave-instruction (lanes past the array
-        // re-read its last 16 B: those rows / columns are outside the matrix and never used)
-        const char *fv_end = reinterpret_cast<const char *>(fv + M) - 16;
+    {  // the I and J records: kFvBytes each, 1 KiB per wave-instruction.  A lane whose 16 B
+        // start past the array re-reads its last 16 B (rows / columns outside the matrix, never
+        // used); a lane straddling the end reads < 16 B past it, inside the M + 1 records the
+        // array is allocated with (vcfxg_ld_prepare)
+        const char *fv_end = reinterpret_cast<const char *>(fv + M);
         for (int q = w; q < 2 * kFvGlds; q += kWaves) {
             const int side = q / kFvGlds, part = q - side * kFvGlds;
             const char *s = reinterpret_cast<const char *>(fv + (side ? jbase : ibase)) + part * 1024 + l * 16;
-            glds16(s < fv_end ? s : fv_end, lds + kRing + kFB * 32 + side * kFvBytes + part * 1024);
+            glds16(s < fv_end ? s : fv_end - 16, lds + kRing + kFB * 32 + side * kFvBytes + part * 1024);
         }
     }
     const int kpad = a.kp4;  // FP4 row bytes

@@ -27,6 +27,7 @@ typedef struct {
     int32_t hap_blocks;      /* 1: founder-haplotype blocks (LD structure) */
     double irregular_rate;   /* fraction of records in a general-path shape */
     int32_t crlf;            /* 1: "\r\n" line endings */
+    int32_t format_mode;     /* 0: FORMAT=GT; 1: the regular records as GT:AD:DP ("a|b:x,y:x+y") */
 } vcfx_synth_opts;
 
 static inline uint64_t smix(uint64_t x) {
@@ -130,13 +131,15 @@ static size_t emit_record(const vcfx_synth_opts *o, int64_t k, const rec_meta *m
     }
     int shape = 0;
     if (m->irregular) shape = 1 + (int)(rnd(o->seed, (uint64_t)k, 6) % 5);
-    if (!b && shape == 0) {
+    const int fmt3 = o->format_mode == 1 && shape == 0;
+    if (!b && shape == 0 && !fmt3) {
         /* regular record: "\tGT" + N x "\ta|b" (missing ".|." has the same width) */
         n += 3 + 4 * (size_t)o->n_samples + (o->crlf ? 2 : 1);
         return n;
     }
     if (shape == 1) PUTS("\tGT:DP", 6);
     else if (shape == 5) PUTS("\tDP:GT", 6);
+    else if (fmt3) PUTS("\tGT:AD:DP", 9);
     else PUTS("\tGT", 3);
     for (int s = 0; s < o->n_samples; s++) {
         PUT('\t');
@@ -153,6 +156,12 @@ static size_t emit_record(const vcfx_synth_opts *o, int64_t k, const rec_meta *m
             PUT((char)('0' + a1));
         }
         if (shape == 1) { PUT(':'); l = put_int(nb, (int64_t)(rs % 60)); PUTS(nb, l); }
+        if (fmt3) {  /* AD (two read depths < 31) and DP = their sum */
+            const uint64_t r3 = rnd(o->seed, (uint64_t)k, 40000000 + (uint64_t)s);
+            const int64_t d0 = (int64_t)(r3 % 31), d1 = (int64_t)((r3 >> 8) % 31);
+            PUT(':'); l = put_int(nb, d0); PUTS(nb, l); PUT(','); l = put_int(nb, d1); PUTS(nb, l);
+            PUT(':'); l = put_int(nb, d0 + d1); PUTS(nb, l);
+        }
     }
     if (o->crlf) PUT('\r');
     PUT('\n');
@@ -175,6 +184,7 @@ static size_t emit_header(const vcfx_synth_opts *o, char *b) {
     }
     PUTS("##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">"); PUTS(eol);
     PUTS("##FORMAT=<ID=DP,Number=1,Type=Integer,Description=\"Read Depth\">"); PUTS(eol);
+    if (o->format_mode == 1) { PUTS("##FORMAT=<ID=AD,Number=R,Type=Integer,Description=\"Allelic depths\">"); PUTS(eol); }
     PUTS("#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT");
     for (int s = 0; s < o->n_samples; s++) {
         snprintf(line, sizeof line, "\tS%05d", s + 1);
@@ -258,13 +268,14 @@ int main(int argc, char **argv) {
         fprintf(stderr, "usage: vcfx_synth OUT N_RECORDS N_SAMPLES [seed info_mode missing hap irregular crlf]\n");
         return 2;
     }
-    vcfx_synth_opts o = {20251226ull, atoll(argv[2]), atoi(argv[3]), 0, 0.0, 0, 0.0, 0};
+    vcfx_synth_opts o = {20251226ull, atoll(argv[2]), atoi(argv[3]), 0, 0.0, 0, 0.0, 0, 0};
     if (argc > 4) o.seed = strtoull(argv[4], NULL, 10);
     if (argc > 5) o.info_mode = atoi(argv[5]);
     if (argc > 6) o.missing_rate = atof(argv[6]);
     if (argc > 7) o.hap_blocks = atoi(argv[7]);
     if (argc > 8) o.irregular_rate = atof(argv[8]);
     if (argc > 9) o.crlf = atoi(argv[9]);
+    if (argc > 10) o.format_mode = atoi(argv[10]);
     size_t n = vcfx_synth_size(&o);
     char *buf = (char *)malloc(n);
     vcfx_synth_fill(&o, buf, n, 8, NULL);

@@ -11,7 +11,7 @@ from . import SYNTH_LIB
 class Opts(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("n_records", ctypes.c_int64), ("n_samples", ctypes.c_int32),
                 ("info_mode", ctypes.c_int32), ("missing_rate", ctypes.c_double), ("hap_blocks", ctypes.c_int32),
-                ("irregular_rate", ctypes.c_double), ("crlf", ctypes.c_int32)]
+                ("irregular_rate", ctypes.c_double), ("crlf", ctypes.c_int32), ("format_mode", ctypes.c_int32)]
 
 
 _lib = None
@@ -30,9 +30,10 @@ def lib():
 
 
 def generate_array(n_records, n_samples, seed=20251226, info_mode=0, missing_rate=0.0, hap_blocks=0,
-                   irregular_rate=0.0, crlf=0, threads=None, rec_offsets=False):
-    """numpy uint8 array of the VCF bytes (and optionally int64 record offsets)."""
-    o = Opts(seed, n_records, n_samples, info_mode, missing_rate, hap_blocks, irregular_rate, crlf)
+                   irregular_rate=0.0, crlf=0, threads=None, rec_offsets=False, format_mode=0):
+    """numpy uint8 array of the VCF bytes (and optionally int64 record offsets).  format_mode 1:
+    the regular records carry FORMAT=GT:AD:DP (variable-width samples: the general GT path)."""
+    o = Opts(seed, n_records, n_samples, info_mode, missing_rate, hap_blocks, irregular_rate, crlf, format_mode)
     L = lib()
     n = L.vcfx_synth_size(ctypes.byref(o))
     arr = np.empty(n, np.uint8)
