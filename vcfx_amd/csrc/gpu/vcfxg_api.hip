@@ -79,6 +79,9 @@ struct vcfxg_ctx {
     // host hints taken at load time from the first data line: its '\n' distance from the
     // sample start (the walk's first prediction) and the mean length of the first lines
     int64_t hint_span = 0, hint_line = 0;
+    // the first data line's FORMAT is exactly "GT" (fixed-stride records: the walk's predicted
+    // ends pay; "GT:AD:DP"-like records are scanned faster by the index sweep)
+    bool hint_gt_only = false;
     uint64_t af_line_cap = 0;   // two-sweep AF: line capacity the last run needed
     // region AF schedule: 0 = default (the walk schedule 7 when the first records average
     // >= 512 B, else 3 with one host synchronisation: single-sweep index + head pass +
@@ -279,6 +282,7 @@ int vcfxg_reset_kernel_stats(vcfxg_ctx *c) {
 static void load_hints(vcfxg_ctx *c, const char *h, size_t n) {
     c->hint_span = 0;
     c->hint_line = 0;
+    c->hint_gt_only = false;
     c->walk_overflowed = false;
     size_t p = 0;
     while (p < n && h[p] == '#') {
@@ -293,12 +297,14 @@ static void load_hints(vcfxg_ctx *c, const char *h, size_t n) {
         const size_t e = q ? (size_t)(q - h) : n;
         if (lines == 0) {
             int tabs = 0;
-            size_t x = p;
+            size_t x = p, f8 = 0;
             while (x < e && tabs < 9) {
                 const char *t = (const char *)memchr(h + x, '\t', e - x);
                 if (!t) break;
+                if (tabs == 8) c->hint_gt_only = (size_t)(t - h) - f8 == 2 && h[f8] == 'G' && h[f8 + 1] == 'T';
                 x = (size_t)(t - h) + 1;
                 tabs++;
+                if (tabs == 8) f8 = x;
             }
             if (tabs == 9) c->hint_span = (int64_t)(e - x);
         }
@@ -779,7 +785,7 @@ int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_su
         return r ? r : vcfxg_allele_freq(c, mode, out);
     }
     // records of >= 512 B on average (a GT-dense VCF): the walk schedule, no index sweep
-    if (c->hint_line >= 512 && !c->walk_overflowed) return af_region_walk(c, data_start, mode, out);
+    if (c->hint_line >= 512 && c->hint_gt_only && !c->walk_overflowed) return af_region_walk(c, data_start, mode, out);
     return af_region_async(c, data_start, mode, out);
 }
 
@@ -1334,7 +1340,7 @@ int vcfxg_hwe_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *o
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
     // the AF schedule knob selects here too: 3 / 8 = no walk, 7 = the walk
-    const bool walk = c->af_path == 7 || (c->af_path != 3 && c->af_path != 8 && c->hint_line >= 512 &&
+    const bool walk = c->af_path == 7 || (c->af_path != 3 && c->af_path != 8 && c->hint_line >= 512 && c->hint_gt_only &&
                                           !c->walk_overflowed);
     return hwe_region_impl(c, data_start, mode, out, walk);
 }

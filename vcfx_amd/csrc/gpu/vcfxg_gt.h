@@ -127,6 +127,7 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
             if (swept && b0 + w0 + kUnroll * kWaveStep < E) *swept = b0 + w0 + kUnroll * kWaveStep;
             break;
         }
+        if (__any(err != 0u)) return false;  // not fixed-stride: stop reading the record
     }
     if (__any(err != 0u)) return false;
     op.finish();
@@ -250,7 +251,7 @@ struct NoPreE {
     __device__ void operator()(int64_t) const {}
 };
 // the GT-first sweep over a sample region [S, ae) of known end (no '\n' inside)
-template <int kU = 4, class Op>
+template <int kU = 8, class Op>
 __device__ __forceinline__ bool gt_first_known(const char *__restrict__ buf, int64_t S, int64_t ae, Op &op) {
     int64_t e;
     uint8_t cr;

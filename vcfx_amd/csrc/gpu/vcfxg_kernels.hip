@@ -1002,7 +1002,7 @@ hipError_t launch_af_complex(const char *buf, int64_t data_start, const uint64_t
                              int32_t *alt, int32_t *tot, uint32_t *rowpre, uint8_t *status,
                              unsigned long long *counters, hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
-    unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
+    unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 2048);
     hipLaunchKernelGGL(k_af_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
                        mode, static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
     return hipGetLastError();
@@ -1017,7 +1017,7 @@ hipError_t launch_af_meta_sweep(const char *buf, int64_t data_start, const uint6
     unsigned grid = grid_for((int64_t)n_lines_host, kRecWaves, 4096);
     hipLaunchKernelGGL(k_af_sweep, dim3(grid), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode,
                        static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters, nullptr);
-    unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 1024);
+    unsigned gridc = grid_for((int64_t)((n_lines_host + kWave - 1) / kWave), kRecWaves, 2048);
     hipLaunchKernelGGL(k_af_complex, dim3(gridc), dim3(kRecThreads), 0, s, buf, data_start, line_end, n_lines_dev,
                        mode, static_cast<const AfMeta *>(meta), alt, tot, rowpre, status, counters);
     return hipGetLastError();
