@@ -1,7 +1,7 @@
 #!/bin/bash
 # One gpurun session: GPU tests, bench runs, rocprofv3 kernel-trace summaries and PMC traffic passes.
 # Each GPU step has its own time limit; a fault/abort/timeout stops the script.
-#   bash gpu_job.sh [test|bench|prof|pmc|all] [workloads...]     (workloads: af pipeline ld nonref)
+#   bash gpu_job.sh [test|bench|prof|pmc|all] [workloads...]     (workloads: af pipeline ld nonref hwe)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -17,7 +17,7 @@ step() {  # step NAME SECONDS CMD...
 ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 MODE=${1:-all}
 shift
-WLS=${*:-af pipeline ld nonref}
+WLS=${*:-af pipeline ld nonref hwe}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
     step pytest_gpu 1000 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread; rc=$?; ok_or_testfail $rc || exit $rc
 fi

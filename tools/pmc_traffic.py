@@ -22,10 +22,15 @@ KERNELS = {
     "line_emit": r"vcfxg::k_idx_sweep<true>\(",
     "line_compact": r"vcfxg::k_nl_compact\(",
     "af_records": r"vcfxg::k_(line_meta|af_sweep|af_complex)\(",
-    "af_walk": r"vcfxg::k_af_walk\(",
+    "af_walk": r"vcfxg::k_af_walk<vcfxg::AfOp>\(",
+    "hwe_walk": r"vcfxg::k_af_walk<vcfxg::HweOp>\(",
     "walk_compact": r"vcfxg::k_walk_compact\(",
-    "af_complex": r"vcfxg::k_af_complex\(",
-    "af_format": r"vcfxg::k_af_format\(",
+    "af_complex": r"vcfxg::k_af_(complex|cx)\(",
+    "af_rows": r"vcfxg::k_(walker_scan|af_rowlen|af_summary)\(",
+    "af_format": r"vcfxg::k_af_format(_w)?\(",
+    "hwe_lines": r"vcfxg::k_hwe_lines\(",
+    "hwe_rows": r"vcfxg::k_hwe_rowlen\(",
+    "hwe_format": r"vcfxg::k_hwe_format\(",
     "rf_records": r"vcfxg::k_rf_records\(",
     "fq_walk": r"vcfxg::k_fq_walk<",
     "fq_rest": r"vcfxg::k_(fq_compact<|fq_finish<|gq_complex\(|nr_complex\()",
@@ -44,7 +49,9 @@ KERNELS = {
 # k_af_complex, would otherwise leave a spurious entry under a workload that never times it)
 TIMED = {
     "af": ("line_count", "line_emit", "line_compact", "af_records", "af_walk", "walk_compact", "af_complex",
-           "af_format"),
+           "af_rows", "af_format"),
+    "hwe": ("hwe_walk", "walk_compact", "hwe_lines", "hwe_rows", "hwe_format", "line_count", "line_emit",
+            "line_compact"),
     "pipeline": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "rf_records", "gq_records"),
     "nonref": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "nr_records"),
     "ld": ("line_count", "line_emit", "line_compact", "ld_parse", "ld_count", "ld_emit", "ld_count_gen",
