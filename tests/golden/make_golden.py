@@ -25,6 +25,7 @@ AF, RF, GQ, LD, VC = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genot
                       "VCFX_ld_calculator", "VCFX_variant_counter")
 NR = "VCFX_nonref_filter"
 HWE = "VCFX_hwe_tester"
+DOSE = "VCFX_dosage_calculator"
 
 
 def fixtures():
@@ -135,6 +136,18 @@ def build_cases():
               ["data/nope.vcf"], ["-i", "data/empty.vcf"]):
         add(HWE, a)
     add(HWE, [], stdin="data/empty.vcf", tag="empty_stdin")
+    # ---- dosage_calculator: the shared fixtures, the reference test script's fixtures
+    # (tests/golden/extract_sh_fixtures.py), the traps
+    ddir = os.path.join(HERE, "data", "ref_dosage")
+    for f in vcfs + [os.path.join("data", "ref_dosage", n) for n in sorted(os.listdir(ddir)) if n.endswith(".vcf")]:
+        add(DOSE, ["-i", f])
+        add(DOSE, ["-q", f])
+        add(DOSE, [], stdin=f)
+        add(DOSE, ["-q"], stdin=f)
+    for a in (["-h"], ["--help"], ["-v"], ["--version"], ["--bogus"], ["-x"], ["-i"], ["-i", "data/nope.vcf"],
+              ["data/nope.vcf"], ["-i", "data/empty.vcf"]):
+        add(DOSE, a)
+    add(DOSE, [], stdin="data/empty.vcf", tag="empty_stdin")
     return cases
 
 

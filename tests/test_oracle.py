@@ -19,8 +19,8 @@ def oracle():
 
 def test_case_count():
     tools = collections.Counter(c["tool"] for c in CASES)
-    # the five hot-path tools + nonref_filter and hwe_tester (8(f) rank 2)
-    assert len(tools) == 7 and min(tools.values()) > 40
+    # the five hot-path tools + nonref_filter, hwe_tester and dosage_calculator (8(f) rank 2)
+    assert len(tools) == 8 and min(tools.values()) > 40
 
 
 @pytest.mark.parametrize("tool", sorted({c["tool"] for c in CASES}))
@@ -91,6 +91,26 @@ def test_hwe_known_answers(oracle, name, want):
     data = open(os.path.join(GOLDEN, "data", "ref_hwe", name + ".vcf"), "rb").read()
     out, _, rc = oracle.run(["VCFX_hwe_tester"], data)
     assert (out, rc) == (want, 0)
+
+
+# tests/test_dosage_calculator.sh: `$DOSAGE_TOOL < X.vcf` (and -i) against the script's expected_X.txt
+# (both extracted as data by tests/golden/extract_sh_fixtures.py)
+DOSE_KNOWN = ["basic", "multi_allelic", "phased", "missing", "malformed", "missing_gt", "single", "gt_not_first"]
+
+
+@pytest.mark.parametrize("name", DOSE_KNOWN)
+def test_dosage_known_answers(oracle, name):
+    d = os.path.join(GOLDEN, "data", "ref_dosage")
+    data = open(os.path.join(d, name + ".vcf"), "rb").read()
+    want = open(os.path.join(d, "expected_%s.txt" % name), "rb").read()
+    assert oracle.run(["VCFX_dosage_calculator"], data)[0] == want
+    assert oracle.run(["VCFX_dosage_calculator", "-i", "data/ref_dosage/%s.vcf" % name], cwd=GOLDEN)[0] == want
+
+
+def test_dosage_missing_header_error(oracle):
+    data = open(os.path.join(GOLDEN, "data", "ref_dosage", "missing_header.vcf"), "rb").read()
+    out, err, rc = oracle.run(["VCFX_dosage_calculator"], data)
+    assert (out, err, rc) == (b"", b"Error: VCF header (#CHROM) not found before variant records.\n", 0)
 
 
 def test_af_known_answers(oracle):
