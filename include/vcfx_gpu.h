@@ -227,6 +227,19 @@ int vcfxg_hwe_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary 
  * the first min(*n, cap) copied to out (any order) */
 int vcfxg_hwe_rechecks(vcfxg_ctx *ctx, vcfxg_hwe_recheck *out, uint64_t cap, uint64_t *n);
 
+/* ---- VCFX_dosage_calculator (a per-sample GT map on the same path) ---
+ * Over the data lines from data_start (the byte after the '#CHROM' line; data lines before
+ * it are the caller's error): per line the row "CHROM\tPOS\tID\tREF\tALT\t" + one dosage
+ * per sample (number of non-zero alleles of a diploid GT, or "NA"), comma separated, "NA" for
+ * the record when FORMAT has no GT, of processFileMmap (VCFX_dosage_calculator.cpp:375-588,
+ * mode VCFXG_MODE_FILE: '\r' stripped) or calculateDosage (:209-360, mode VCFXG_MODE_STDIN);
+ * findGTIndexRaw :160-178, extractGTFromSample :182-203, parseDosageInline :111-156 per
+ * sample.  Text via vcfxg_fetch_text (without the column header); rows = output rows,
+ * warn_lines = lines with fewer than 10 fields (the caller prints the warning),
+ * general_records = lines off the fixed-stride sweep; per-line statuses via
+ * vcfxg_fetch_lines (1 row, 3 warning, 0 skipped). */
+int vcfxg_dosage_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
+
 /* ---- variant counter -------------------------------------------------------------------
  * Per line status: ROW = data line with >= 8 tab-separated columns (counted), WARN = fewer
  * columns, SKIP = empty or '#'.  strip_cr: drop a trailing '\r' first (file path).

@@ -50,6 +50,7 @@ INPUTS = {
 
 AF, RF, GQ, LD, NR, HWE = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query",
                            "VCFX_ld_calculator", "VCFX_nonref_filter", "VCFX_hwe_tester")
+DOSE = "VCFX_dosage_calculator"
 
 # name -> (input, [stage argv ...] with "{F}" for the file; the first stage reads stdin when
 # it has no {F}), keep-mask flag
@@ -59,6 +60,7 @@ CASES = {
     "nonref_file": ("chr21", [[NR, "-i", "{F}"]], True),
     "hwe_file": ("chr21", [[HWE, "-q", "-i", "{F}"]], False),
     "hwe_stdin": ("chr21", [[HWE]], False),
+    "dose_file": ("chr21", [[DOSE, "-q", "-i", "{F}"]], False),
     "pipeline_bench": ("chr21", [[RF, "--filter", "QUAL>=30;FILTER==PASS", "-i", "{F}"],
                                  [GQ, "--genotype-query", "0|1"]], True),
     "pipeline_annot": ("annot", [[RF, "--filter", "FILTER==PASS;AF>=0.01", "-i", "{F}"],

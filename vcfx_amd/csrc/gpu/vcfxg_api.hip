@@ -1357,6 +1357,57 @@ int vcfxg_hwe_rechecks(vcfxg_ctx *c, vcfxg_hwe_recheck *out, uint64_t cap, uint6
     return VCFXG_OK;
 }
 
+// VCFX_dosage_calculator over [data_start, n): the line index, the row lengths, a scan, the
+// rows (one host synchronisation for the text size)
+int vcfxg_dosage_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
+    if (!c->loaded) return VCFXG_E_STATE;
+    if (data_start > c->n) data_start = c->n;
+    uint64_t L = 0;
+    int r = vcfxg_index(c, data_start, &L);
+    if (r) return r;
+    HIPCHK(c, hipSetDevice(c->device));
+    r = af_buffers(c, L);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::dose_meta_bytes() * (L + 1));
+    if (r) return r;
+    const char *buf = P<char>(c->input);
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->rowlen) + L, 0, 8, c->stream));
+    prof_begin(c, "dose_len");
+    HIPCHK(c, vcfxg::launch_dose_len(buf, (int64_t)data_start, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L,
+                                     mode, P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->af_meta.p,
+                                     P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "dose_len");
+    prof_begin(c, "dose_rows");
+    r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)L + 1);
+    if (r) return r;
+    prof_end(c, "dose_rows");
+    static thread_local uint64_t tail[5];
+    HIPCHK(c, hipMemcpyAsync(&tail[0], P<uint64_t>(c->rowoff) + L, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tail[1], c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t text = tail[0];
+    r = ensure(c, c->text, text + 1);
+    if (r) return r;
+    prof_begin(c, "dose_fmt");
+    HIPCHK(c, vcfxg::launch_dose_fmt(buf, (int64_t)data_start, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L,
+                                     P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
+                                     ~0ull, c->stream));
+    prof_end(c, "dose_fmt");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    c->text_bytes = text;
+    if (out) {
+        out->n_lines = L;
+        out->rows = tail[1];
+        out->data_lines = tail[1] + tail[3];
+        out->warn_lines = tail[3];
+        out->general_records = tail[4];
+        out->text_bytes = text;
+    }
+    return VCFXG_OK;
+}
+
 int vcfxg_variant_count(vcfxg_ctx *c, int strip_cr, vcfxg_summary *out) {
     if (!c) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;

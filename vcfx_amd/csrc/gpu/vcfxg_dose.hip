@@ -1,0 +1,325 @@
+// vcfxg_dose.hip -- VCFX_dosage_calculator's per-record pass (a per-sample
+// GT map on the record path).
+//
+// Output per data record: "CHROM\tPOS\tID\tREF\tALT\t" + one dosage per sample ('0' / '1' /
+// '2', or "NA"), comma separated, + '\n' -- about 2 bytes per sample, so the output is half
+// the input.  Two passes over the indexed lines, one wave per line:
+//   k_dose_len  the record's head (tabs, the FORMAT's GT index) and its row length: on the
+//               fixed-stride layout (GT-only, single-digit diploid) the sweep counts the NA
+//               samples (gt_fast); GT-first records of any width go through gt_first;
+//               anything else through the exact per-sample parse (gt_general);
+//   k_dose_fmt  after a scan of the row lengths: the prefix and the dosages, each lane's
+//               samples placed by a wave scan of their output bytes (the fixed-stride sweep
+//               on fixed-stride records, a lane per sample start otherwise).
+// Semantics (VCFX_dosage_calculator.cpp): processFileMmap :426-577 (mode 0: '\r' stripped) /
+// calculateDosage :229-353 (mode 1: no strip); fields split up to 10 (< 10: the warning);
+// findGTIndexRaw :160-178 (GT not in FORMAT: "NA" for the record); extractGTFromSample
+// :182-203 and parseDosageInline :111-156 per sample (samples run to the line end: a
+// trailing tab adds no sample).
+#include <algorithm>
+
+#include "vcfxg_device.h"
+#include "vcfxg_gt.h"
+#include "vcfxg_kernels.h"
+
+namespace vcfxg {
+
+constexpr int kDoseThreads = 256;
+constexpr int kDoseWaves = kDoseThreads / kWave;
+
+// parseDosageInline on [g, g + n): -1 NA, else the dosage (an allele counts when its number,
+// accumulated modulo 2^32, is non-zero: the reference build's `> 0` on a non-negative int)
+__device__ __forceinline__ int dose_parse(const char *__restrict__ buf, int64_t g, int64_t n) {
+    if (n <= 0) return -1;
+    int dose = 0, count = 0;
+    int64_t p = g, e = g + n;
+    while (p < e) {
+        while (p < e && (byte_at(buf, p) == '/' || byte_at(buf, p) == '|')) p++;
+        if (p >= e) break;
+        if (byte_at(buf, p) == '.') return -1;
+        uint32_t a = 0;
+        bool dig = false;
+        while (p < e && is_digit(byte_at(buf, p))) {
+            a = a * 10u + (byte_at(buf, p) - '0');
+            dig = true;
+            p++;
+        }
+        if (!dig) return -1;
+        dose += a != 0u;
+        if (++count > 2) return -1;
+    }
+    return count == 2 ? dose : -1;
+}
+
+// extractGTFromSample(gi) + parseDosageInline for the sample starting at st (ends at the next
+// tab or E)
+__device__ __forceinline__ int dose_sample(const char *__restrict__ buf, int64_t st, int64_t E, int gi) {
+    const int64_t se = sample_end(buf, st, E);
+    int cur = 0;
+    int64_t fs = st;
+    for (int64_t q = st; q <= se; q++) {
+        if (q == se || byte_at(buf, q) == ':') {
+            if (cur == gi) return dose_parse(buf, fs, q - fs);
+            cur++;
+            fs = q + 1;
+        }
+    }
+    return -1;
+}
+
+// pass-1 reducer: samples and NA samples (NA = 2 output bytes)
+struct DoseCountOp {
+    const char *buf;
+    int64_t E;
+    int gi;
+    uint32_t ns = 0, na = 0;
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() const { return false; }
+    __device__ void dword(const DwordView &v) {  // "a s b": NA unless both are digits
+        ns += v.real;
+        na += v.real && v.dig != 0x01000100u;
+    }
+    __device__ void gt3(uint32_t c0, uint32_t c2) {
+        ns++;
+        na += !(c0 - '0' < 10u && c2 - '0' < 10u);
+    }
+    __device__ void sample(int64_t st) {
+        ns++;
+        na += dose_sample(buf, st, E, gi) < 0;
+    }
+    __device__ void finish() {
+        ns = wave_sum(ns);
+        na = wave_sum(na);
+    }
+};
+
+enum : uint8_t { kDoseSkip = 0, kDoseRow = 1, kDoseWarn = 3 };
+enum : uint8_t { kDoseFast = 1, kDoseGeneral = 2, kDoseNA = 3, kDoseNoSamples = 4 };
+
+// per line: status, row length, and how pass 2 writes it (kind, GT index, sample start)
+struct DoseMeta {
+    uint64_t S;     // sample region start
+    uint32_t pre;   // bytes of "CHROM\t..ALT\t"
+    uint32_t ae;    // line end (after the mode's '\r' strip) - S
+    int32_t gi;     // GT index in FORMAT
+    uint8_t kind;   // kDose*
+    uint8_t pad[3];
+};
+
+__global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restrict__ buf, int64_t data_start,
+                                                           const uint64_t *__restrict__ line_end,
+                                                           const uint64_t *n_lines_p, int mode,
+                                                           uint8_t *__restrict__ status, uint64_t *__restrict__ len,
+                                                           DoseMeta *__restrict__ meta,
+                                                           unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kDoseWaves][16];
+    __shared__ uint32_t red[3][kDoseWaves];
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    uint32_t rows = 0, warns = 0, gen = 0;  // (wave-uniform)
+    for (uint64_t li = wid; li < n_lines; li += nw) {
+        const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
+        int64_t ae = le;
+        if (mode == 0 && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;
+        uint8_t st = kDoseSkip;
+        uint64_t L = 0;
+        DoseMeta m{};
+        if (ae > ls && byte_at(buf, ls) != '#') {
+            int64_t t[10];
+            const int nt = head_tabs(buf, ls, ae, 10, t, lds);
+            if (nt < 9) st = kDoseWarn;
+            else {
+                st = kDoseRow;
+                m.pre = (uint32_t)(t[4] - ls + 1);
+                m.S = (uint64_t)(t[8] + 1);
+                m.ae = (uint32_t)(ae - (t[8] + 1));
+                const int gi = gt_index(buf, t[7] + 1, t[8]);
+                if (gi < 0) {
+                    m.kind = kDoseNA;
+                    L = m.pre + 3u;  // "NA\n"
+                } else if (t[8] + 1 >= ae) {
+                    m.kind = kDoseNoSamples;
+                    L = m.pre + 1u;  // "\n"
+                } else {
+                    m.gi = gi;
+                    const int64_t S = t[8] + 1;
+                    DoseCountOp op{buf, ae, gi};
+                    bool fast = gi == 0 && gt_fast(buf, S, ae, op);
+                    m.kind = kDoseFast;
+                    if (!fast) {
+                        m.kind = kDoseGeneral;
+                        op = DoseCountOp{buf, ae, gi};
+                        if (!(gi == 0 && gt_first_known(buf, S, ae, op))) {
+                            op = DoseCountOp{buf, ae, gi};
+                            gt_general(buf, S, ae, op);
+                        }
+                        gen++;
+                    }
+                    L = (uint64_t)m.pre + 2u * op.ns + op.na;  // dosages + separators / '\n'
+                }
+            }
+        }
+        rows += st == kDoseRow;
+        warns += st == kDoseWarn;
+        if (lane() == 0) {
+            status[li] = st;
+            len[li] = L;
+            meta[li] = m;
+        }
+    }
+    // one atomic per block and counter (same-address atomics serialise in L2)
+    if (lane() == 0) {
+        red[0][threadIdx.x / kWave] = rows;
+        red[1][threadIdx.x / kWave] = warns;
+        red[2][threadIdx.x / kWave] = gen;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint32_t t = 0;
+        for (int k = 0; k < kDoseWaves; k++) t += red[threadIdx.x][k];
+        const int slot = threadIdx.x == 0 ? 0 : threadIdx.x == 1 ? 2 : 3;
+        if (t) atomicAdd(&counters[slot], (unsigned long long)t);
+    }
+}
+
+__device__ __forceinline__ void put_dose(char *o, int d, bool last) {
+    if (d < 0) {
+        o[0] = 'N';
+        o[1] = 'A';
+        o[2] = last ? '\n' : ',';
+    } else {
+        o[0] = (char)('0' + d);
+        o[1] = last ? '\n' : ',';
+    }
+}
+
+__global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restrict__ buf, int64_t data_start,
+                                                           const uint64_t *__restrict__ line_end,
+                                                           const uint64_t *n_lines_p,
+                                                           const uint8_t *__restrict__ status,
+                                                           const DoseMeta *__restrict__ meta,
+                                                           const uint64_t *__restrict__ off, char *__restrict__ out,
+                                                           uint64_t cap) {
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t li = wid; li < n_lines; li += nw) {
+        if (status[li] != kDoseRow || off[li + 1] > cap) continue;  // (wave-uniform)
+        const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
+        const DoseMeta m = meta[li];
+        char *o = out + off[li];
+        for (uint32_t k = lane(); k < m.pre; k += kWave) o[k] = buf[ls + k];
+        o += m.pre;
+        if (m.kind == kDoseNA) {
+            if (lane() == 0) {
+                o[0] = 'N';
+                o[1] = 'A';
+                o[2] = '\n';
+            }
+            continue;
+        }
+        if (m.kind == kDoseNoSamples) {
+            if (lane() == 0) o[0] = '\n';
+            continue;
+        }
+        const int64_t S = (int64_t)uniform64((int64_t)m.S), E = S + (int64_t)m.ae;
+        // the samples' output bytes (pass 1's row length less the prefix): the sample whose
+        // bytes end there is the last, and ends with '\n' instead of ','
+        const uint64_t tot = off[li + 1] - off[li] - m.pre;
+        uint64_t run = 0;  // output bytes of the samples before this wave-step
+        if (m.kind == kDoseFast) {
+            // the fixed-stride layout: samples "a s b\t" on the 4-byte grid from S, the last
+            // without its tab; lane l of a wave-step takes 4 consecutive samples
+            const int64_t ns = (E - S + 1) / 4;
+            for (int64_t k0 = 0; k0 < ns; k0 += 4 * kWave) {
+                const int64_t k = k0 + 4 * lane();
+                int d[4];
+                uint32_t bytes = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    d[i] = 0;
+                    if (k + i < ns) {
+                        const int64_t p = S + 4 * (k + i);
+                        const uint32_t a = byte_at(buf, p), b = byte_at(buf, p + 2);
+                        d[i] = (is_digit(a) && is_digit(b)) ? (a != '0') + (b != '0') : -1;
+                        bytes += d[i] < 0 ? 3u : 2u;
+                    }
+                }
+                const uint32_t incl = wave_incl_scan(bytes);
+                uint64_t pos = run + incl - bytes;
+#pragma unroll
+                for (int i = 0; i < 4; i++)
+                    if (k + i < ns) {
+                        const uint32_t nb = d[i] < 0 ? 3u : 2u;
+                        put_dose(o + pos, d[i], pos + nb == tot);
+                        pos += nb;
+                    }
+                run += wave_bcast(incl, kWave - 1);
+            }
+            continue;
+        }
+        // any other layout: a lane per 16 B block, its sample starts in order
+        const int gi = m.gi;
+        for (int64_t w = S & ~(int64_t)15; w < E; w += kWaveStep) {
+            const int64_t blk = w + (int64_t)lane() * kBlockBytes;
+            uint32_t starts = 0;
+            if (blk < E) {
+                const uint32_t tm = eq_mask16(load16(buf, blk), kRepTab);
+                starts = (tm << 1) & 0xFFFFu;
+                if (blk > 0 && byte_at(buf, blk - 1) == '\t') starts |= 1u;
+                starts &= range_mask16(blk, S + 1, E);
+                if (S >= blk && S < blk + 16) starts |= 1u << (S - blk);
+            }
+            int8_t dd[16];
+            uint32_t bytes = 0, mm = starts;
+            for (int c = 0; mm; c++) {
+                const int j = __builtin_ctz(mm);
+                mm &= mm - 1u;
+                dd[c] = (int8_t)dose_sample(buf, blk + j, E, gi);
+                bytes += dd[c] < 0 ? 3u : 2u;
+            }
+            const uint32_t incl = wave_incl_scan(bytes);
+            uint64_t pos = run + incl - bytes;
+            mm = starts;
+            for (int c = 0; mm; c++) {
+                mm &= mm - 1u;
+                const uint32_t nb = dd[c] < 0 ? 3u : 2u;
+                put_dose(o + pos, dd[c], pos + nb == tot);
+                pos += nb;
+            }
+            run += wave_bcast(incl, kWave - 1);
+        }
+    }
+}
+
+static unsigned dose_grid(int64_t n, int64_t per, unsigned cap) {
+    int64_t g = (n + per - 1) / per;
+    if (g < 1) g = 1;
+    return (unsigned)(g > cap ? cap : g);
+}
+
+size_t dose_meta_bytes() { return sizeof(DoseMeta); }
+
+hipError_t launch_dose_len(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                           uint64_t n_lines_host, int mode, uint8_t *status, uint64_t *len, void *meta,
+                           unsigned long long *counters, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    hipLaunchKernelGGL(k_dose_len, dim3(dose_grid((int64_t)n_lines_host, kDoseWaves, 2048)), dim3(kDoseThreads), 0, s,
+                       buf, data_start, line_end, n_lines_dev, mode, status, len, static_cast<DoseMeta *>(meta),
+                       counters);
+    return hipGetLastError();
+}
+
+hipError_t launch_dose_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                           uint64_t n_lines_host, const uint8_t *status, const void *meta, const uint64_t *off,
+                           char *out, uint64_t cap, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    hipLaunchKernelGGL(k_dose_fmt, dim3(dose_grid((int64_t)n_lines_host, kDoseWaves, 2048)), dim3(kDoseThreads), 0, s,
+                       buf, data_start, line_end, n_lines_dev, status, static_cast<const DoseMeta *>(meta), off, out,
+                       cap);
+    return hipGetLastError();
+}
+
+}  // namespace vcfxg

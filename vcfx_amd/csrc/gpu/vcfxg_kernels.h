@@ -141,6 +141,16 @@ hipError_t launch_hwe_format(const char *buf, int64_t data_start, const uint64_t
                              const uint32_t *rowpre, const uint8_t *status, const uint64_t *off, char *out,
                              uint64_t text_cap, int64_t ulps, void *rc, unsigned long long *rc_n, uint64_t rc_cap,
                              hipStream_t s);
+// VCFX_dosage_calculator (vcfxg_dose.hip) over the indexed lines: per line status (1 row,
+// 3 "< 10 fields", 0 skip), row length and meta (dose_meta_bytes() each; counters[0] rows,
+// [2] warnings, [3] lines off the fixed-stride sweep); then the rows at their offsets
+size_t dose_meta_bytes();
+hipError_t launch_dose_len(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                           uint64_t n_lines_host, int mode, uint8_t *status, uint64_t *len, void *meta,
+                           unsigned long long *counters, hipStream_t s);
+hipError_t launch_dose_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                           uint64_t n_lines_host, const uint8_t *status, const void *meta, const uint64_t *off,
+                           char *out, uint64_t cap, hipStream_t s);
 // text_cap: rows whose end passes it are not written (the caller checks the total)
 hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, int mode, const int32_t *alt, const int32_t *tot,

@@ -13,5 +13,6 @@ extern "C" int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd
     if (!strcmp(t, "VCFX_ld_calculator")) return vcfx_tool_ld_calculator(argc, argv, in_fd, out_fd, err_fd);
     if (!strcmp(t, "VCFX_nonref_filter")) return vcfx_tool_nonref_filter(argc, argv, in_fd, out_fd, err_fd);
     if (!strcmp(t, "VCFX_hwe_tester")) return vcfx_tool_hwe_tester(argc, argv, in_fd, out_fd, err_fd);
+    if (!strcmp(t, "VCFX_dosage_calculator")) return vcfx_tool_dosage_calculator(argc, argv, in_fd, out_fd, err_fd);
     return -100;
 }

@@ -61,6 +61,7 @@ SIGNATURES = {
     "vcfxg_nonref_filter_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_hwe_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_hwe_rechecks": (_I, [_VP, _VP, _U64, ctypes.POINTER(_U64)]),
+    "vcfxg_dosage_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_prefixes": (_I, [_VP, _VP, _S, _VP]),
     "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
@@ -203,6 +204,12 @@ class Engine:
         """VCFX_hwe_tester over [data_start, n): counts, row rules and rows (vcfxg_hwe_region)"""
         s = Summary()
         self._chk(self.L.vcfxg_hwe_region(self.h, data_start, int(mode), ctypes.byref(s)), "hwe_region")
+        return s
+
+    def dosage_region(self, data_start, mode):
+        """VCFX_dosage_calculator rows over the data lines from data_start (vcfxg_dosage_region)"""
+        s = Summary()
+        self._chk(self.L.vcfxg_dosage_region(self.h, data_start, int(mode), ctypes.byref(s)), "dosage_region")
         return s
 
     def hwe_rechecks(self):
