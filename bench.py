@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("af", "pipeline", "ld", "nonref", "hwe"), default="af")
+    ap.add_argument("--workload", choices=("af", "pipeline", "ld", "nonref", "hwe", "dose"), default="af")
     ap.add_argument("--records", type=int, default=None, help="records per GPU (default per workload)")
     ap.add_argument("--samples", type=int, default=2504)
     ap.add_argument("--window", type=int, default=100000, help="ld: window in variants")
@@ -134,6 +134,9 @@ def cpu_baseline(workload, arr, offs, a):
         elif workload == "hwe":
             argvs = [["VCFX_hwe_tester", "-q", "-i", f.name]]
             desc = "VCFX_hwe_tester -q -i (file path)"
+        elif workload == "dose":
+            argvs = [["VCFX_dosage_calculator", "-q", "-i", f.name]]
+            desc = "VCFX_dosage_calculator -q -i (file path)"
         elif workload == "pipeline":
             argvs = [["VCFX_record_filter", "--filter", "QUAL>=30;FILTER==PASS", "-i", f.name],
                      ["VCFX_genotype_query", "--genotype-query", "0|1"]]
@@ -167,7 +170,7 @@ def output_check(workload, eng, s, a, rank):
             dig = json.load(f)
     except OSError:
         return {"checked": False, "why": "no tests/golden/full_digests.json"}
-    default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "hwe": 427409, "ld": 100000}[workload]
+    default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "hwe": 427409, "dose": 427409, "ld": 100000}[workload]
     if a.format != "gt" or a.missing_rate > 0 or a.irregular_rate > 0:
         return {"checked": False, "why": "no reference digest for the general-path data"}
     if rank != 0 or a.records != default or a.samples != 2504 or (workload == "ld" and (a.window < 3000 or
@@ -177,6 +180,10 @@ def output_check(workload, eng, s, a, rank):
         c = dig["cases"]["af_file"]
         got = hashlib.sha256(b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes)).hexdigest()
         want, what = c["stdout"]["sha256"], "sha256 of the AF rows vs VCFX_allele_freq_calc -q -i (reference)"
+    elif workload == "dose":
+        c = dig["cases"]["dose_file"]
+        got = hashlib.sha256(b"CHROM\tPOS\tID\tREF\tALT\tDosages\n" + eng.text(s.text_bytes)).hexdigest()
+        want, what = c["stdout"]["sha256"], "sha256 of the dosage rows vs VCFX_dosage_calculator -q -i (reference)"
     elif workload == "hwe":
         if "hwe_file" not in dig["cases"]:
             return {"checked": False, "why": "no hwe_file digest"}
@@ -222,6 +229,8 @@ def e2e_rates(workload, arr, a):
         tool, args = "VCFX_nonref_filter", []
     elif workload == "hwe":
         tool, args = "VCFX_hwe_tester", ["-q"]
+    elif workload == "dose":
+        tool, args = "VCFX_dosage_calculator", ["-q"]
     elif workload == "pipeline":
         tool, args = "VCFX_record_filter", ["--filter", "QUAL>=30;FILTER==PASS"]
     else:
@@ -346,6 +355,13 @@ def main():
             return s
         kern_names = ("hwe_walk", "walk_compact", "hwe_lines", "hwe_rows", "hwe_format", "line_count", "line_emit",
                       "line_compact")
+    elif a.workload == "dose":
+        def step():
+            s = eng.dosage_region(ds, engine.MODE_FILE)  # index + per-sample dosages + rows
+            if red is not None:
+                allreduce_counts([s.n_lines, s.rows, s.text_bytes, s.general_records])
+            return s
+        kern_names = ("line_count", "line_emit", "line_compact", "dose_len", "dose_rows", "dose_fmt")
     elif a.workload == "pipeline":
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
@@ -445,6 +461,10 @@ def main():
                 "af_walk": region_bytes + L * (8 + 13 + 16),
                 # HWE: the same walk with three class counts per line (8 + 17 + 16)
                 "hwe_walk": region_bytes + L * (8 + 17 + 16),
+                # dosage: pass 1 reads the records (+ line end, status, length, meta per line);
+                # pass 2 reads them again and writes the rows (2 bytes per sample)
+                "dose_len": region_bytes + L * (8 + 1 + 8 + 24),
+                "dose_fmt": region_bytes + tb + L * (8 + 1 + 8 + 24),
                 "walk_compact": L * 2 * (8 + 13 + 16),
                 # the per-line rest: its lines' record bytes when the data are off the fixed-stride
                 # layout (every line a GT:AD:DP record), else the head record + status per line
@@ -481,6 +501,8 @@ def main():
                       "with the per-record all-samples-hom-ref test" % (a.records, a.samples),
             "hwe": "VCFX_hwe_tester -i (file path) on a device-resident %d x %d shard per GPU: the walk with the "
                    "genotype-class reducer + HWE chi-square p-value rows" % (a.records, a.samples),
+            "dose": "VCFX_dosage_calculator -i (file path) on a device-resident %d x %d shard per GPU: index + "
+                    "per-sample dosage rows (2 output bytes per sample)" % (a.records, a.samples),
             "ld": "VCFX_ld_calculator -w %d -t %g streaming on a device-resident %d x %d shard per GPU: parse + "
                   "FP4-MFMA pair sums (count + emit) + pair text" % (a.window, a.threshold, a.records, a.samples),
         }[a.workload] + extra

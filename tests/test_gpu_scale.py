@@ -118,7 +118,8 @@ def _check(case, inputs, stdin="none"):
 @pytest.mark.parametrize("case,stdin", [("af_file", "none"), ("af_stdin", "pipe"), ("af_stdin", "file"),
                                         ("nonref_file", "none"), ("pipeline_bench", "none"),
                                         ("nonref_stdin", "pipe"), ("nonref_stdin", "file"),
-                                        ("hwe_file", "none"), ("hwe_stdin", "pipe"), ("hwe_stdin", "file")])
+                                        ("hwe_file", "none"), ("hwe_stdin", "pipe"), ("hwe_stdin", "file"),
+                                        ("dose_file", "none")])
 def test_chr21_shard_matches_reference(inputs, case, stdin):
     _check(case, inputs, stdin)
 
