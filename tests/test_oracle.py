@@ -19,8 +19,9 @@ def oracle():
 
 def test_case_count():
     tools = collections.Counter(c["tool"] for c in CASES)
-    # the five hot-path tools + nonref_filter, hwe_tester and dosage_calculator (8(f) rank 2)
-    assert len(tools) == 8 and min(tools.values()) > 40
+    # the five hot-path tools + nonref_filter, hwe_tester, dosage_calculator, allele_counter and
+    # missing_detector (8(f) rank 2)
+    assert len(tools) == 10 and min(tools.values()) > 40
 
 
 @pytest.mark.parametrize("tool", sorted({c["tool"] for c in CASES}))
@@ -61,18 +62,28 @@ REF_EXP = [
     (["VCFX_nonref_filter"], "ref_nonref/nonref_complex.vcf", "nonref_complex_out.vcf"),
     (["VCFX_nonref_filter"], "ref_nonref/nonref_malformed.vcf", "nonref_malformed_out.vcf"),
     (["VCFX_nonref_filter"], "ref_nonref/nonref_no_gt.vcf", "nonref_no_gt_out.vcf"),
+    # tests/test_allele_counter.sh:37-62 (`-q < A`, `-q --samples "Y" < B`, and the -i / positional forms)
+    (["VCFX_allele_counter", "-q"], "ref_ac/allele_counter_A.vcf", "allele_counter_A_out.tsv"),
+    (["VCFX_allele_counter", "-q", "--samples", "Y"], "ref_ac/allele_counter_B.vcf", "allele_counter_B_out.tsv"),
+    (["VCFX_allele_counter", "-q", "-i", "data/ref_ac/allele_counter_A.vcf"], None, "allele_counter_A_out.tsv"),
+    (["VCFX_allele_counter", "-q", "data/ref_ac/allele_counter_A.vcf"], None, "allele_counter_A_out.tsv"),
+    (["VCFX_allele_counter", "-q", "-s", "Y", "-i", "data/ref_ac/allele_counter_B.vcf"], None,
+     "allele_counter_B_out.tsv"),
+    # tests/test_missing_detector.sh:65-87 (`$EXEC < input`, trailing whitespace stripped, diff -w -B)
+    (["VCFX_missing_detector"], "ref_md/md_basic.vcf", "md_basic_out.vcf"),
+    (["VCFX_missing_detector"], "ref_md/md_malformed.vcf", "md_malformed_out.vcf"),
+    (["VCFX_missing_detector"], "ref_md/md_empty.vcf", "md_empty_out.vcf"),
+    (["VCFX_missing_detector", "--help"], None, "md_help_message.txt"),
 ]
 
 
 @pytest.mark.parametrize("argv,stdin,expected", REF_EXP)
 def test_oracle_matches_reference_committed_expected(oracle, argv, stdin, expected):
-    if expected is None:
-        pytest.skip("no committed expected file")
     data = open(os.path.join(GOLDEN, "data", stdin), "rb").read() if stdin else b""
     out, err, rc = oracle.run(argv, data, cwd=GOLDEN)
     want = open(os.path.join(GOLDEN, "data", "ref_expected", expected), "rb").read()
-    if argv[0] == "VCFX_nonref_filter":  # the reference script compares with diff -b
-        assert [l.split() for l in out.splitlines()] == [l.split() for l in want.splitlines()]
+    if argv[0] in ("VCFX_nonref_filter", "VCFX_missing_detector"):  # the scripts compare with diff -b / -w -B
+        assert [l.split() for l in out.splitlines() if l.strip()] == [l.split() for l in want.splitlines() if l.strip()]
     else:
         assert out == want
 
