@@ -240,6 +240,21 @@ int vcfxg_hwe_rechecks(vcfxg_ctx *ctx, vcfxg_hwe_recheck *out, uint64_t cap, uin
  * vcfxg_fetch_lines (1 row, 3 warning, 0 skipped). */
 int vcfxg_dosage_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
 
+/* ---- VCFX_missing_detector (a per-sample GT predicate on the same path) -
+ * Over the lines from data_start (the caller passes the end of the leading '#' lines): per
+ * line status 0 empty (after the file mode's '\r' strip), 4 '#' line, 1 data line kept as it
+ * is, VCFXG_LINE_MISSING a data line with a missing genotype -- some sample's first ':' sub-
+ * field holds a '.' that starts or ends it or touches '/' or '|' (hasMissingGenotypeInSamples,
+ * VCFX_missing_detector.cpp:290-336).  vcfxg_fetch_lines gives the statuses and, as alt /
+ * total, a flagged line's INFO field [start, end) relative to the line start (the caller
+ * writes "MISSING_GENOTYPES=1" into it).  mode VCFXG_MODE_FILE: processMmapZeroCopy
+ * (:450-589, '\r' dropped); VCFXG_MODE_STDIN: detectMissingGenotypes (:860-911).
+ * data_lines = data lines, rows = flagged lines, general_records = lines ending in '\n' whose
+ * sample columns hold any '.' (0: the file mode's pre-scan, sampleColumnsHaveAnyDots
+ * :371-445, passes the input through unchanged). */
+#define VCFXG_LINE_MISSING 6
+int vcfxg_missing_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
+
 /* ---- variant counter -------------------------------------------------------------------
  * Per line status: ROW = data line with >= 8 tab-separated columns (counted), WARN = fewer
  * columns, SKIP = empty or '#'.  strip_cr: drop a trailing '\r' first (file path).

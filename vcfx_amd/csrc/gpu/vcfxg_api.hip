@@ -1408,6 +1408,37 @@ int vcfxg_dosage_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary
     return VCFXG_OK;
 }
 
+// VCFX_missing_detector over [data_start, n): the line index and one per-line pass
+int vcfxg_missing_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
+    if (!c->loaded) return VCFXG_E_STATE;
+    if (data_start > c->n) data_start = c->n;
+    uint64_t L = 0;
+    int r = vcfxg_index(c, data_start, &L);
+    if (r) return r;
+    HIPCHK(c, hipSetDevice(c->device));
+    r = af_buffers(c, L);
+    if (r) return r;
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    prof_begin(c, "md_lines");
+    HIPCHK(c, vcfxg::launch_md_lines(P<char>(c->input), (int64_t)data_start, (int64_t)c->n, P<uint64_t>(c->line_end),
+                                     P<uint64_t>(c->d_nlines), L, mode, P<uint8_t>(c->status), P<int32_t>(c->alt),
+                                     P<int32_t>(c->tot), P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "md_lines");
+    static thread_local uint64_t cnt[3];
+    HIPCHK(c, hipMemcpyAsync(cnt, c->counters.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    if (out) {
+        std::memset(out, 0, sizeof *out);
+        out->n_lines = L;
+        out->data_lines = cnt[0];
+        out->rows = cnt[1];
+        out->general_records = cnt[2];
+    }
+    return VCFXG_OK;
+}
+
 int vcfxg_variant_count(vcfxg_ctx *c, int strip_cr, vcfxg_summary *out) {
     if (!c) return VCFXG_E_ARG;
     if (!c->indexed) return VCFXG_E_STATE;

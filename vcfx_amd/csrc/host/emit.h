@@ -30,6 +30,8 @@ struct LineEmitter {
             push((const char *)"\n", 1);
         }
     }
+    // [s, e) as it is (no newline added)
+    void bytes(const char *s, const char *e) { extend(s, e); }
     void raw(const char *p, size_t n) {
         close_run();
         push(p, n);

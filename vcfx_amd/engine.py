@@ -62,6 +62,7 @@ SIGNATURES = {
     "vcfxg_hwe_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_hwe_rechecks": (_I, [_VP, _VP, _U64, ctypes.POINTER(_U64)]),
     "vcfxg_dosage_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_missing_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_prefixes": (_I, [_VP, _VP, _S, _VP]),
     "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
@@ -210,6 +211,12 @@ class Engine:
         """VCFX_dosage_calculator rows over the data lines from data_start (vcfxg_dosage_region)"""
         s = Summary()
         self._chk(self.L.vcfxg_dosage_region(self.h, data_start, int(mode), ctypes.byref(s)), "dosage_region")
+        return s
+
+    def missing_region(self, data_start, mode):
+        """VCFX_missing_detector's per-line test over the lines from data_start (vcfxg_missing_region)"""
+        s = Summary()
+        self._chk(self.L.vcfxg_missing_region(self.h, data_start, int(mode), ctypes.byref(s)), "missing_region")
         return s
 
     def hwe_rechecks(self):
