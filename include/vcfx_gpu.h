@@ -255,6 +255,34 @@ int vcfxg_dosage_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summa
 #define VCFXG_LINE_MISSING 6
 int vcfxg_missing_region(vcfxg_ctx *ctx, size_t data_start, int mode, vcfxg_summary *out);
 
+/* ---- VCFX_allele_counter (a per-sample GT reducer, a row per sample) ----
+ * Over the indexed lines [first_line, last_line): per data line (non-empty, not '#'; no '\r'
+ * handling, as in the reference) the REF / ALT allele counts of parseGenotypeRaw
+ * (VCFX_allele_counter.cpp:267-294: digit runs of the sample's GT, 0 counting as REF) for each
+ * output slot's sample, formatted as the reference does:
+ *   kind 0: "CHROM\tPOS\tID\tREF\tALT\t<name>\t<ref>\t<alt>\n" per slot,
+ *   kind 1: "CHROM\tPOS\tID\tREF\tALT\t<sum ref>\t<sum alt>\t<rows>\n" per record,
+ *   kind 2: the two counts as int8 bytes per slot.
+ * seq 0 = countAllelesMmapMT / processChunk (:550-642, 786-950): every slot a row, a sample past
+ * the record's last tab counts 0 / 0, counts printed as int8_t; seq 1 = countAllelesUnified
+ * (:1266-1468) / countAllelesStream (:1122-1260): a forward-only cursor (a slot reads the
+ * largest index so far), rows stop at the first sample that starts at or past the line end.
+ * Text (without the column header) via vcfxg_fetch_text / vcfxg_fetch_text_range; per-line
+ * statuses via vcfxg_fetch_lines (1 data line, 4 '#CHROM' line, 0 other).  rows = output rows,
+ * data_lines = data lines, warn_lines = '#CHROM' lines in the range (countAllelesStream
+ * re-selects at each: the caller splits the range there), general_records = lines off the
+ * fixed-stride sweep. */
+typedef struct {
+    const uint32_t *sample;   /* per output slot: the sample's index (sampleIndices) */
+    uint64_t m;               /* output slots */
+    const char *names;        /* the slots' sample names, concatenated */
+    const uint64_t *name_off; /* m + 1 offsets into names */
+    int seq;                  /* selection semantics (above) */
+    int kind;                 /* 0 text, 1 aggregate, 2 binary */
+} vcfxg_ac_params;
+int vcfxg_allele_counter(vcfxg_ctx *ctx, uint64_t first_line, uint64_t last_line, const vcfxg_ac_params *params,
+                         vcfxg_summary *out);
+
 /* ---- variant counter -------------------------------------------------------------------
  * Per line status: ROW = data line with >= 8 tab-separated columns (counted), WARN = fewer
  * columns, SKIP = empty or '#'.  strip_cr: drop a trailing '\r' first (file path).
@@ -297,6 +325,8 @@ int vcfxg_selftest_mfma_fp4(vcfxg_ctx *ctx, int *mismatches);
 
 /* device-formatted output text (without the column header line) */
 int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);
+/* bytes [offset, offset + n) of that text (outputs larger than one host buffer) */
+int vcfxg_fetch_text_range(vcfxg_ctx *ctx, uint64_t offset, size_t n, void *host);
 /* per-line results of the last record kernel: any pointer may be NULL */
 int vcfxg_fetch_lines(vcfxg_ctx *ctx, uint64_t first, uint64_t count, int32_t *alt, int32_t *total,
                       uint8_t *status);

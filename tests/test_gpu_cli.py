@@ -8,7 +8,8 @@ from vcfx_amd import tools
 pytestmark = pytest.mark.gpu
 
 IMPLEMENTED = ["VCFX_allele_freq_calc", "VCFX_genotype_query", "VCFX_record_filter", "VCFX_variant_counter", "VCFX_ld_calculator",
-               "VCFX_nonref_filter", "VCFX_hwe_tester", "VCFX_dosage_calculator", "VCFX_missing_detector"]
+               "VCFX_nonref_filter", "VCFX_hwe_tester", "VCFX_dosage_calculator", "VCFX_missing_detector",
+               "VCFX_allele_counter"]
 CASES = load_cases()
 
 

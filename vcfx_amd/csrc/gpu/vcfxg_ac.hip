@@ -1,0 +1,464 @@
+// vcfxg_ac.hip -- VCFX_allele_counter's per-record, per-sample pass (a
+// per-sample GT reducer on the record path whose output is a row per (record, sample)).
+//
+// Output per data record (no '\r' handling anywhere, as in the reference), for the selected
+// samples in selection order:
+//   text:      "CHROM\tPOS\tID\tREF\tALT\t" + name + "\t" + ref + "\t" + alt + "\n" per sample
+//   aggregate: "CHROM\tPOS\tID\tREF\tALT\t" + Σref + "\t" + Σalt + "\t" + rows + "\n"
+//   binary:    the two counts as int8 bytes per sample
+// Two selection semantics (VCFX_allele_counter.cpp):
+//   all (countAllelesMmapMT / processChunk :550-642): every selected sample gets a row; a sample
+//       index past the record's last tab counts 0 / 0; the counts print as int8_t;
+//   seq (countAllelesUnified :1371-1465, countAllelesStream :1188-1246): a forward-only cursor
+//       (slot i reads the running maximum of the indices so far), rows stop at the first slot
+//       whose sample starts at or past the line end; counts print as int.
+// parseGenotypeRaw :267-294 per GT (the sample up to its first ':' or tab): digit runs count,
+// 0 (modulo 2^32) as REF and anything else as ALT.
+//
+// Two passes, one wave per indexed line:
+//   k_ac_len  head (prefix length, sample start), then either the fixed-stride sweep (gt_fast:
+//             every GT is "a s b", so every count is one digit and a sample's bytes sit at
+//             S + 4k) or the general path (the line's sample starts into a per-wave table in
+//             global scratch, then a lane per output slot parses its sample); the row bytes;
+//   k_ac_fmt  after a scan of the row bytes: the rows.  Fixed-stride text rows are composed
+//             64 at a time in LDS (a lane per row) and written out as aligned 16 B stores.
+#include "vcfxg_device.h"
+#include "vcfxg_gt.h"
+#include "vcfxg_kernels.h"
+
+namespace vcfxg {
+
+constexpr int kAcThreads = 256;
+constexpr int kAcWaves = kAcThreads / kWave;
+constexpr int kAcTile = 4096;  // LDS bytes per wave for one tile of 64 text rows
+constexpr int kAcPre = 256;    // LDS bytes per wave for the record's prefix
+
+enum : uint8_t { kAcFast = 1, kAcGeneral = 2 };
+
+struct AcMeta {
+    uint64_t S;        // sample region start
+    uint64_t sr, sa;   // aggregate: Σref, Σalt
+    uint32_t P;        // prefix bytes ("CHROM\t..ALT\t", missing fields as empty)
+    uint32_t rows;     // output rows
+    uint32_t ns;       // fast: samples in the record
+    uint32_t lim;      // prefix bytes taken from the line (the rest are tabs)
+    uint8_t kind;
+    uint8_t pad[7];
+};
+
+struct AcArgs {
+    const uint32_t *eff;   // per slot: the sample index it reads
+    const uint64_t *noff;  // per slot: name offsets (m + 1)
+    const char *names;
+    uint32_t *scratch;     // per wave: scap sample starts (relative to S)
+    uint32_t m, scap;      // slots; sample starts a line needs (max index + 1)
+    int seq, kind;
+};
+
+struct AcNullOp {
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() const { return false; }
+    __device__ void dword(const DwordView &) {}
+    __device__ void finish() {}
+};
+
+__device__ __forceinline__ uint32_t dec_digits(uint64_t v) {
+    uint32_t d = 1;
+    while (v >= 10) {
+        v /= 10;
+        d++;
+    }
+    return d;
+}
+__device__ __forceinline__ uint32_t int_bytes(int64_t v) { return v < 0 ? 1u + dec_digits((uint64_t)(-v)) : dec_digits((uint64_t)v); }
+
+// parseGenotypeRaw over [g, e)
+__device__ __forceinline__ void ac_parse(const char *__restrict__ buf, int64_t g, int64_t e, int &r, int &a) {
+    r = a = 0;
+    uint32_t v = 0;
+    bool dig = false;
+    for (int64_t p = g; p <= e; p++) {
+        const uint32_t c = p < e ? byte_at(buf, p) : (uint32_t)'/';
+        if (c - '0' < 10u) {
+            v = v * 10u + (c - '0');
+            dig = true;
+        } else {
+            if (dig) {
+                if (v == 0u) r++;
+                else a++;
+            }
+            dig = false;
+            v = 0u;
+        }
+    }
+}
+
+// the GT of the sample starting at st: up to its first ':' or tab (or the line end)
+__device__ __forceinline__ void ac_sample(const char *__restrict__ buf, int64_t st, int64_t le, int &r, int &a) {
+    int64_t e = st;
+    while (e < le) {
+        const uint32_t c = byte_at(buf, e);
+        if (c == ':' || c == '\t') break;
+        e++;
+    }
+    ac_parse(buf, st, e, r, a);
+}
+
+// the line's sample starts in [S, le] into the wave's table: tab[k] = start of sample k - S
+// for k < min(ns, scap), sample 0 at S and one after every tab (a trailing tab's sample starts
+// at le); returns ns capped at scap
+__device__ __forceinline__ uint32_t ac_starts(const char *__restrict__ buf, int64_t S, int64_t le, uint32_t *tab,
+                                              uint32_t scap) {
+    if (lane() == 0) tab[0] = 0u;
+    uint32_t cnt = 0;  // tabs seen (wave-uniform)
+    for (int64_t w = S & ~(int64_t)15; w < le && cnt + 1 < scap; w += kWaveStep) {
+        const int64_t blk = w + (int64_t)lane() * kBlockBytes;
+        uint32_t tm = blk < le ? eq_mask16(load16(buf, blk), kRepTab) & range_mask16(blk, S, le) : 0u;
+        const uint32_t c = (uint32_t)__popc(tm);
+        const uint32_t incl = wave_incl_scan(c);
+        uint32_t k = cnt + incl - c + 1;
+        while (tm) {
+            const int j = __builtin_ctz(tm);
+            tm &= tm - 1u;
+            if (k < scap) tab[k] = (uint32_t)(blk + j + 1 - S);
+            k++;
+        }
+        cnt += wave_bcast(incl, kWave - 1);
+    }
+    // the table is read back by other lanes of the wave (through a fresh L1)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t ns = cnt + 1;
+    return ns < scap ? ns : scap;
+}
+
+// slot counts on the general path for sample e (ns = ac_starts' count): valid = the slot
+// produces a row (seq: its sample starts before the line end; all: always, 0 / 0 past the
+// last sample)
+__device__ __forceinline__ void ac_slot_general(const char *__restrict__ buf, int64_t S, int64_t le, const uint32_t *tab,
+                                                uint32_t ns, uint32_t e, bool seq, bool &valid, int &r, int &a) {
+    r = a = 0;
+    const bool has = e < ns;
+    const int64_t st = has ? S + tab[e] : le;
+    valid = seq ? st < le : true;
+    if (has) ac_sample(buf, st, le, r, a);
+}
+
+// slot counts on the fixed-stride path: sample e's GT is the 3 bytes at S + 4e
+__device__ __forceinline__ void ac_slot_fast(const char *__restrict__ buf, int64_t S, uint32_t ns, uint32_t e, int &r,
+                                             int &a) {
+    r = a = 0;
+    if (e < ns) {
+        const uint32_t c0 = byte_at(buf, S + 4 * (int64_t)e), c2 = byte_at(buf, S + 4 * (int64_t)e + 2);
+        r = (c0 == '0') + (c2 == '0');
+        a = (c0 - '1' < 9u) + (c2 - '1' < 9u);
+    }
+}
+
+__global__ __launch_bounds__(kAcThreads) void k_ac_len(const char *__restrict__ buf, int64_t data_start,
+                                                       const uint64_t *__restrict__ line_end, uint64_t l0, uint64_t l1,
+                                                       AcArgs A, uint8_t *__restrict__ status, uint64_t *__restrict__ len,
+                                                       AcMeta *__restrict__ meta,
+                                                       unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kAcWaves][16];
+    __shared__ unsigned long long red[4][kAcWaves];
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    uint32_t *tab = A.scratch + wid * (uint64_t)A.scap;
+    unsigned long long rows_all = 0;
+    uint32_t data = 0, chrom = 0, gen = 0;  // (wave-uniform)
+    for (uint64_t li = l0 + wid; li < l1; li += nw) {
+        const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
+        uint8_t st = 0;
+        uint64_t L = 0;
+        AcMeta m{};
+        if (le > ls) {
+            if (byte_at(buf, ls) == '#') {
+                const bool c = le - ls >= 6 && byte_at(buf, ls + 1) == 'C' && byte_at(buf, ls + 2) == 'H' &&
+                               byte_at(buf, ls + 3) == 'R' && byte_at(buf, ls + 4) == 'O' && byte_at(buf, ls + 5) == 'M';
+                st = c ? 4 : 0;
+                chrom += c;
+            } else {
+                st = 1;
+                data++;
+                int64_t t[9];
+                const int nt = head_tabs(buf, ls, le, 9, t, lds);
+                m.P = nt >= 5 ? (uint32_t)(t[4] - ls + 1) : (uint32_t)(le - ls) + (uint32_t)(5 - nt);
+                m.lim = nt >= 5 ? m.P : (uint32_t)(le - ls);
+                const int64_t S = nt >= 9 ? t[8] + 1 : le;
+                m.S = (uint64_t)S;
+                AcNullOp nop;
+                const bool fast = S < le && gt_fast(buf, S, le, nop);
+                uint32_t rows = 0;
+                uint64_t text = 0, sr = 0, sa = 0;
+                if (fast) {
+                    m.kind = kAcFast;
+                    const uint32_t ns = (uint32_t)((le - S + 1) / 4);
+                    m.ns = ns;
+                    uint32_t cnt = 0;
+                    for (uint32_t i = lane(); i < A.m; i += kWave) {
+                        const uint32_t e = A.eff[i];
+                        const bool valid = !A.seq || e < ns;
+                        cnt += valid;
+                        if (A.kind == 1 && valid) {
+                            int r, a;
+                            ac_slot_fast(buf, S, ns, e, r, a);
+                            sr += (uint64_t)r;
+                            sa += (uint64_t)a;
+                        }
+                    }
+                    rows = wave_sum(cnt);
+                    if (A.kind == 0) text = (uint64_t)rows * (m.P + 5u) + A.noff[rows];
+                } else {
+                    m.kind = kAcGeneral;
+                    gen++;
+                    const uint32_t nsa = ac_starts(buf, S, le, tab, A.scap);
+                    uint32_t cnt = 0;
+                    for (uint32_t i = lane(); i < A.m; i += kWave) {
+                        const uint32_t e = A.eff[i];
+                        bool valid;
+                        int r, a;
+                        ac_slot_general(buf, S, le, tab, nsa, e, A.seq, valid, r, a);
+                        if (!valid) continue;
+                        cnt++;
+                        if (A.kind == 0) {
+                            const int pr = A.seq ? r : (int)(int8_t)r, pa = A.seq ? a : (int)(int8_t)a;
+                            text += m.P + (A.noff[i + 1] - A.noff[i]) + 3u + int_bytes(pr) + int_bytes(pa);
+                        } else if (A.kind == 1) {
+                            sr += (uint64_t)r;
+                            sa += (uint64_t)a;
+                        }
+                    }
+                    rows = wave_sum(cnt);
+                    text = wave_sum(text);
+                }
+                m.rows = rows;
+                if (A.kind == 1) {
+                    sr = wave_sum(sr);
+                    sa = wave_sum(sa);
+                    m.sr = sr;
+                    m.sa = sa;
+                    text = m.P + dec_digits(sr) + dec_digits(sa) + dec_digits(rows) + 3u;
+                } else if (A.kind == 2)
+                    text = 2ull * rows;
+                L = text;
+                rows_all += A.kind == 1 ? 1u : rows;
+            }
+        }
+        if (lane() == 0) {
+            status[li] = st;
+            len[li - l0] = L;
+            meta[li] = m;
+        }
+    }
+    if (lane() == 0) {
+        red[0][threadIdx.x / kWave] = rows_all;
+        red[1][threadIdx.x / kWave] = data;
+        red[2][threadIdx.x / kWave] = chrom;
+        red[3][threadIdx.x / kWave] = gen;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        unsigned long long t = 0;
+        for (int k = 0; k < kAcWaves; k++) t += red[threadIdx.x][k];
+        if (t) atomicAdd(&counters[threadIdx.x], t);
+    }
+}
+
+// writes the decimal text of v (bytes already known) at o
+__device__ __forceinline__ void put_int(char *o, int64_t v, uint32_t nb) {
+    uint64_t x = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
+    if (v < 0) o[0] = '-';
+    for (uint32_t k = nb; k-- > (v < 0 ? 1u : 0u);) {
+        o[k] = (char)('0' + x % 10);
+        x /= 10;
+    }
+}
+
+__global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ buf, int64_t data_start,
+                                                       const uint64_t *__restrict__ line_end, uint64_t l0, uint64_t l1,
+                                                       AcArgs A, const uint8_t *__restrict__ status,
+                                                       const AcMeta *__restrict__ meta, const uint64_t *__restrict__ off,
+                                                       char *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char tile_all[kAcWaves][kAcTile + 16];
+    __shared__ char pre_all[kAcWaves][kAcPre];
+    char *tile = tile_all[threadIdx.x / kWave];
+    char *pre = pre_all[threadIdx.x / kWave];
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    uint32_t *tab = A.scratch + wid * (uint64_t)A.scap;
+    for (uint64_t li = l0 + wid; li < l1; li += nw) {
+        if (status[li] != 1) continue;  // (wave-uniform)
+        const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
+        const AcMeta m = meta[li];
+        char *o = out + off[li - l0];
+        const int64_t S = (int64_t)m.S;
+        const uint32_t P = m.P;
+        auto pre_byte = [&](uint32_t k) -> char { return k < m.lim ? buf[ls + k] : '\t'; };
+        if (A.kind == 1) {  // aggregate: one row
+            if (lane() == 0) {
+                for (uint32_t k = 0; k < P; k++) o[k] = pre_byte(k);
+                uint32_t p = P, nb = dec_digits(m.sr);
+                put_int(o + p, (int64_t)m.sr, nb);
+                p += nb;
+                o[p++] = '\t';
+                nb = dec_digits(m.sa);
+                put_int(o + p, (int64_t)m.sa, nb);
+                p += nb;
+                o[p++] = '\t';
+                nb = dec_digits(m.rows);
+                put_int(o + p, (int64_t)m.rows, nb);
+                p += nb;
+                o[p] = '\n';
+            }
+            continue;
+        }
+        const uint32_t nsa = m.kind == kAcGeneral ? ac_starts(buf, S, le, tab, A.scap) : 0u;
+        if (A.kind == 2) {  // binary: two int8 bytes per row
+            for (uint32_t i = lane(); i < m.rows; i += kWave) {
+                int r, a;
+                bool valid;
+                if (m.kind == kAcFast) ac_slot_fast(buf, S, m.ns, A.eff[i], r, a);
+                else ac_slot_general(buf, S, le, tab, nsa, A.eff[i], A.seq, valid, r, a);
+                o[2 * i] = (char)(int8_t)r;
+                o[2 * i + 1] = (char)(int8_t)a;
+            }
+            continue;
+        }
+        if (m.kind == kAcGeneral || P > kAcPre) {
+            // any layout: a lane per row, rows placed by a wave scan of their bytes
+            uint64_t run = 0;
+            for (uint32_t i0 = 0; i0 < m.rows; i0 += kWave) {
+                const uint32_t i = i0 + lane();
+                int r = 0, a = 0;
+                uint32_t nb = 0, br = 0, ba = 0;
+                if (i < m.rows) {
+                    bool valid;
+                    if (m.kind == kAcFast) ac_slot_fast(buf, S, m.ns, A.eff[i], r, a);
+                    else ac_slot_general(buf, S, le, tab, nsa, A.eff[i], A.seq, valid, r, a);
+                    if (!A.seq) {
+                        r = (int8_t)r;
+                        a = (int8_t)a;
+                    }
+                    br = int_bytes(r);
+                    ba = int_bytes(a);
+                    nb = P + (uint32_t)(A.noff[i + 1] - A.noff[i]) + 3u + br + ba;
+                }
+                const uint64_t incl = wave_incl_scan((uint64_t)nb);
+                if (i < m.rows) {
+                    char *q = o + run + incl - nb;
+                    for (uint32_t k = 0; k < P; k++) q[k] = pre_byte(k);
+                    q += P;
+                    for (uint64_t k = A.noff[i]; k < A.noff[i + 1]; k++) *q++ = A.names[k];
+                    *q++ = '\t';
+                    put_int(q, r, br);
+                    q += br;
+                    *q++ = '\t';
+                    put_int(q, a, ba);
+                    q[ba] = '\n';
+                }
+                run += wave_bcast(incl, kWave - 1);
+            }
+            continue;
+        }
+        // fixed-stride text rows: P + name + 5 bytes each; the prefix staged once in LDS
+        for (uint32_t k = lane(); k < P; k += kWave) pre[k] = pre_byte(k);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint64_t rl = P + 5u;
+        for (uint32_t i0 = 0; i0 < m.rows; i0 += kWave) {
+            const uint32_t i1 = min(m.rows, i0 + (uint32_t)kWave);
+            const uint64_t g0 = (uint64_t)i0 * rl + A.noff[i0];                // tile start in the line's text
+            const uint64_t B = (uint64_t)(i1 - i0) * rl + A.noff[i1] - A.noff[i0];  // tile bytes
+            const uint32_t i = i0 + lane();
+            int r = 0, a = 0;
+            if (i < i1) ac_slot_fast(buf, S, m.ns, A.eff[i], r, a);
+            const uint64_t ga = (uint64_t)(o - out) + g0;  // absolute text offset of the tile
+            if (B + 16 > (uint64_t)kAcTile) {             // long names: straight to global memory
+                if (i < i1) {
+                    char *q = o + (uint64_t)i * rl + A.noff[i];
+                    for (uint32_t k = 0; k < P; k++) q[k] = pre[k];
+                    q += P;
+                    for (uint64_t k = A.noff[i]; k < A.noff[i + 1]; k++) *q++ = A.names[k];
+                    q[0] = '\t';
+                    q[1] = (char)('0' + r);
+                    q[2] = '\t';
+                    q[3] = (char)('0' + a);
+                    q[4] = '\n';
+                }
+                continue;
+            }
+            const uint32_t sh = (uint32_t)(ga & 15);  // LDS position = text position mod 16
+            if (i < i1) {
+                char *q = tile + sh + ((uint64_t)i * rl + A.noff[i] - g0);
+                for (uint32_t k = 0; k < P; k++) q[k] = pre[k];
+                q += P;
+                for (uint64_t k = A.noff[i]; k < A.noff[i + 1]; k++) *q++ = A.names[k];
+                q[0] = '\t';
+                q[1] = (char)('0' + r);
+                q[2] = '\t';
+                q[3] = (char)('0' + a);
+                q[4] = '\n';
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // copy out: aligned 16 B blocks of [ga, ga + B)
+            const uint64_t a0 = ga & ~(uint64_t)15, aend = ga + B;
+            for (uint64_t blk = a0 + 16ull * lane(); blk < aend; blk += 16ull * kWave) {
+                const char *src = tile + (blk - a0);
+                if (blk >= ga && blk + 16 <= aend)
+                    *reinterpret_cast<uint4 *>(out + blk) = *reinterpret_cast<const uint4 *>(src);
+                else
+                    for (int k = 0; k < 16; k++)
+                        if (blk + k >= ga && blk + k < aend) out[blk + k] = src[k];
+            }
+            __builtin_amdgcn_wave_barrier();  // the tile is rewritten by the next iteration
+        }
+    }
+}
+
+size_t ac_meta_bytes() { return sizeof(AcMeta); }
+
+static AcArgs ac_args(const uint32_t *eff, const uint64_t *noff, const char *names, uint32_t *scratch, uint32_t m,
+                      uint32_t scap, int seq, int kind) {
+    AcArgs A;
+    A.eff = eff;
+    A.noff = noff;
+    A.names = names;
+    A.scratch = scratch;
+    A.m = m;
+    A.scap = scap;
+    A.seq = seq;
+    A.kind = kind;
+    return A;
+}
+
+hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
+                         unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
+                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint8_t *status,
+                         uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s) {
+    if (l1 <= l0) return hipSuccess;
+    hipLaunchKernelGGL(k_ac_len, dim3(blocks), dim3(kAcThreads), 0, s, buf, data_start, line_end, l0, l1,
+                       ac_args(eff, noff, names, scratch, m, scap, seq, kind), status, len,
+                       static_cast<AcMeta *>(meta), counters);
+    return hipGetLastError();
+}
+
+hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
+                         unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
+                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, const uint8_t *status,
+                         const void *meta, const uint64_t *off, char *out, hipStream_t s) {
+    if (l1 <= l0) return hipSuccess;
+    hipLaunchKernelGGL(k_ac_fmt, dim3(blocks), dim3(kAcThreads), 0, s, buf, data_start, line_end, l0, l1,
+                       ac_args(eff, noff, names, scratch, m, scap, seq, kind), status,
+                       static_cast<const AcMeta *>(meta), off, out);
+    return hipGetLastError();
+}
+
+int ac_threads() { return kAcThreads; }
+
+}  // namespace vcfxg

@@ -70,6 +70,11 @@ struct vcfxg_ctx {
     uint64_t dense_cap_w = 0;
     // VCFX_hwe_tester: hom-alt counts (dense, per walker), the host-recheck list and its length
     DevBuf hwe_aux, wk_aux, hwe_rc;
+    // VCFX_allele_counter: slots' sample indices, name offsets and bytes, per-wave sample tables
+    DevBuf ac_eff, ac_noff, ac_names, ac_scratch;
+    std::vector<uint32_t> ac_eff_host;
+    std::vector<uint64_t> ac_noff_host;
+    std::string ac_names_host;
     uint64_t hwe_rc_n = 0;
     // ulps either side of the device p-value that must print the same digits (test hook: a
     // huge value sends every exp()-derived row to the host)
@@ -1408,6 +1413,84 @@ int vcfxg_dosage_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary
     return VCFXG_OK;
 }
 
+// VCFX_allele_counter over indexed lines [l0, l1): row bytes, a scan, the rows (one host
+// synchronisation for the text size)
+int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_params *p, vcfxg_summary *out) {
+    if (!c || !p || (p->m && (!p->sample || !p->name_off)) || p->kind < 0 || p->kind > 2 || p->m >= (1ull << 31))
+        return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
+    if (l0 > l1 || l1 > c->n_lines) return VCFXG_E_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t m = p->m, n = l1 - l0, L = c->n_lines;
+    // slot i reads eff[i]: the selection itself, or (seq) its running maximum
+    c->ac_eff_host.resize(m + 1);
+    c->ac_noff_host.assign(p->name_off, p->name_off + m + 1);
+    uint32_t run = 0, mx = 0;
+    for (uint64_t i = 0; i < m; i++) {
+        run = p->seq ? std::max(run, p->sample[i]) : p->sample[i];
+        c->ac_eff_host[i] = run;
+        mx = std::max(mx, run);
+    }
+    const uint64_t nb = p->name_off[m] - p->name_off[0];
+    if (p->name_off[0] != 0) return VCFXG_E_ARG;
+    c->ac_names_host.assign(p->names ? p->names : "", (size_t)nb);
+    const uint64_t scap = (uint64_t)mx + 1;
+    // grid: a wave per line up to 2048 blocks, and at most 1 GiB of per-wave sample tables
+    const uint64_t waves_per_block = (uint64_t)(vcfxg::ac_threads() / 64);
+    uint64_t blocks = std::min<uint64_t>((n + waves_per_block - 1) / waves_per_block, 2048);
+    blocks = std::max<uint64_t>(1, std::min<uint64_t>(blocks, (1ull << 30) / (4 * scap * waves_per_block)));
+    int r = ensure(c, c->ac_eff, 4 * (m + 1));
+    if (!r) r = ensure(c, c->ac_noff, 8 * (m + 1));
+    if (!r) r = ensure(c, c->ac_names, nb + 1);
+    if (!r) r = ensure(c, c->ac_scratch, 4 * scap * waves_per_block * blocks);
+    if (!r) r = af_buffers(c, L);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::ac_meta_bytes() * (L + 1));
+    if (r) return r;
+    HIPCHK(c, hipMemcpyAsync(c->ac_eff.p, c->ac_eff_host.data(), 4 * (m + 1), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->ac_noff.p, c->ac_noff_host.data(), 8 * (m + 1), hipMemcpyHostToDevice, c->stream));
+    if (nb) HIPCHK(c, hipMemcpyAsync(c->ac_names.p, c->ac_names_host.data(), nb, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->rowlen) + n, 0, 8, c->stream));
+    const char *buf = P<char>(c->input);
+    prof_begin(c, "ac_len");
+    HIPCHK(c, vcfxg::launch_ac_len(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, (unsigned)blocks,
+                                   P<uint32_t>(c->ac_eff), P<uint64_t>(c->ac_noff), P<char>(c->ac_names),
+                                   P<uint32_t>(c->ac_scratch), (uint32_t)m, (uint32_t)scap, p->seq, p->kind,
+                                   P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->af_meta.p,
+                                   P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "ac_len");
+    r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)n + 1);
+    if (r) return r;
+    static thread_local uint64_t tail[5];
+    HIPCHK(c, hipMemcpyAsync(&tail[0], P<uint64_t>(c->rowoff) + n, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tail[1], c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t text = tail[0];
+    r = ensure(c, c->text, text + 1);
+    if (r) return r;
+    prof_begin(c, "ac_fmt");
+    HIPCHK(c, vcfxg::launch_ac_fmt(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, (unsigned)blocks,
+                                   P<uint32_t>(c->ac_eff), P<uint64_t>(c->ac_noff), P<char>(c->ac_names),
+                                   P<uint32_t>(c->ac_scratch), (uint32_t)m, (uint32_t)scap, p->seq, p->kind,
+                                   P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
+                                   c->stream));
+    prof_end(c, "ac_fmt");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    c->text_bytes = text;
+    if (out) {
+        std::memset(out, 0, sizeof *out);
+        out->n_lines = n;
+        out->rows = tail[1];
+        out->data_lines = tail[2];
+        out->warn_lines = tail[3];
+        out->general_records = tail[4];
+        out->text_bytes = text;
+    }
+    return VCFXG_OK;
+}
+
 // VCFX_missing_detector over [data_start, n): the line index and one per-line pass
 int vcfxg_missing_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
@@ -1871,6 +1954,15 @@ int vcfxg_fetch_text(vcfxg_ctx *c, char *host, size_t cap) {
     if (cap < c->text_bytes) return VCFXG_E_CAP;
     if (!c->text_bytes) return VCFXG_OK;
     HIPCHK(c, hipMemcpyAsync(host, c->text.p, c->text_bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return VCFXG_OK;
+}
+
+int vcfxg_fetch_text_range(vcfxg_ctx *c, uint64_t offset, size_t n, void *host) {
+    if (!c || (!host && n)) return VCFXG_E_ARG;
+    if (offset > c->text_bytes || n > c->text_bytes - offset) return VCFXG_E_ARG;
+    if (!n) return VCFXG_OK;
+    HIPCHK(c, hipMemcpyAsync(host, P<char>(c->text) + offset, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return VCFXG_OK;
 }

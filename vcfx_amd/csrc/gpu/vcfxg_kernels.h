@@ -158,6 +158,20 @@ constexpr uint8_t kMdFlag = 6;
 hipError_t launch_md_lines(const char *buf, int64_t data_start, int64_t n_input, const uint64_t *line_end,
                            const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, uint8_t *status,
                            int32_t *info_s, int32_t *info_e, unsigned long long *counters, hipStream_t s);
+// VCFX_allele_counter (vcfxg_ac.hip) over indexed lines [l0, l1): per line status (1 data,
+// 4 '#CHROM', 0 other), row bytes (len[li - l0]) and meta (ac_meta_bytes() each); counters
+// [0] rows, [1] data lines, [2] '#CHROM' lines, [3] lines off the fixed-stride sweep.  eff:
+// per output slot the sample index it reads; scratch: ac_threads() / 64 * blocks * scap u32
+size_t ac_meta_bytes();
+int ac_threads();
+hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
+                         unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
+                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint8_t *status,
+                         uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s);
+hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
+                         unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
+                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, const uint8_t *status,
+                         const void *meta, const uint64_t *off, char *out, hipStream_t s);
 // text_cap: rows whose end passes it are not written (the caller checks the total)
 hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, int mode, const int32_t *alt, const int32_t *tot,

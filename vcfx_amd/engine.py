@@ -63,6 +63,8 @@ SIGNATURES = {
     "vcfxg_hwe_rechecks": (_I, [_VP, _VP, _U64, ctypes.POINTER(_U64)]),
     "vcfxg_dosage_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_missing_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
+    "vcfxg_allele_counter": (_I, [_VP, _U64, _U64, _VP, ctypes.POINTER(Summary)]),
+    "vcfxg_fetch_text_range": (_I, [_VP, _U64, _S, _VP]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_prefixes": (_I, [_VP, _VP, _S, _VP]),
     "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
