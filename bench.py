@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("af", "pipeline", "ld", "nonref", "hwe", "dose"), default="af")
+    ap.add_argument("--workload", choices=("af", "pipeline", "ld", "nonref", "hwe", "dose", "ac", "md"), default="af")
     ap.add_argument("--records", type=int, default=None, help="records per GPU (default per workload)")
     ap.add_argument("--samples", type=int, default=2504)
     ap.add_argument("--window", type=int, default=100000, help="ld: window in variants")
@@ -137,6 +137,12 @@ def cpu_baseline(workload, arr, offs, a):
         elif workload == "dose":
             argvs = [["VCFX_dosage_calculator", "-q", "-i", f.name]]
             desc = "VCFX_dosage_calculator -q -i (file path)"
+        elif workload == "ac":
+            argvs = [["VCFX_allele_counter", "-q", "-t", "1", "-i", f.name]]
+            desc = "VCFX_allele_counter -q -t 1 -i (file path, one thread)"
+        elif workload == "md":
+            argvs = [["VCFX_missing_detector", "-q", "-i", f.name]]
+            desc = "VCFX_missing_detector -q -i (file path)"
         elif workload == "pipeline":
             argvs = [["VCFX_record_filter", "--filter", "QUAL>=30;FILTER==PASS", "-i", f.name],
                      ["VCFX_genotype_query", "--genotype-query", "0|1"]]
@@ -157,7 +163,7 @@ def cpu_baseline(workload, arr, offs, a):
                       % (nvar, len(sample) / 1e6, desc, reps, t)}
 
 
-def output_check(workload, eng, s, a, rank):
+def output_check(workload, eng, s, a, rank, arr=None):
     """The last timed step's output against the REFERENCE's, on rank 0 at the BASELINE sizes:
     the digests tests/golden/full_digests.json holds for this exact synthetic input (made by
     running the reference binaries on it).  AF: sha256 of the formatted rows; pipeline /
@@ -170,7 +176,8 @@ def output_check(workload, eng, s, a, rank):
             dig = json.load(f)
     except OSError:
         return {"checked": False, "why": "no tests/golden/full_digests.json"}
-    default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "hwe": 427409, "dose": 427409, "ld": 100000}[workload]
+    default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "hwe": 427409, "dose": 427409, "ac": 427409,
+               "md": 427409, "ld": 100000}[workload]
     if a.format != "gt" or a.missing_rate > 0 or a.irregular_rate > 0:
         return {"checked": False, "why": "no reference digest for the general-path data"}
     if rank != 0 or a.records != default or a.samples != 2504 or (workload == "ld" and (a.window < 3000 or
@@ -184,6 +191,31 @@ def output_check(workload, eng, s, a, rank):
         c = dig["cases"]["dose_file"]
         got = hashlib.sha256(b"CHROM\tPOS\tID\tREF\tALT\tDosages\n" + eng.text(s.text_bytes)).hexdigest()
         want, what = c["stdout"]["sha256"], "sha256 of the dosage rows vs VCFX_dosage_calculator -q -i (reference)"
+    elif workload == "ac":
+        # every (record, sample) count of the shard: the binary form of the same call (one
+        # untimed extra call; the text rows' formatting is pinned by tests/test_gpu_scale.py)
+        c = dig["cases"].get("ac_bin_file")
+        if c is None:
+            return {"checked": False, "why": "no ac_bin_file digest"}
+        names = ["S%05d" % (k + 1) for k in range(a.samples)]
+        sb = eng.allele_counter(0, s.n_lines, list(range(a.samples)), names, seq=1, kind=2)
+        hdr = b"VCAC" + (1).to_bytes(4, "little") + a.samples.to_bytes(4, "little") + bytes(8)
+        h = hashlib.sha256(hdr)
+        for o in range(0, sb.text_bytes, 1 << 28):
+            h.update(eng.text_range(o, min(1 << 28, sb.text_bytes - o)))
+        got = h.hexdigest()
+        want, what = c["stdout"]["sha256"], ("sha256 of every (record, sample) REF/ALT count (the -b form of the "
+                                             "same call) vs VCFX_allele_counter -q -b -i (reference)")
+    elif workload == "md":
+        c = dig["cases"].get("md_file")
+        if c is None:
+            return {"checked": False, "why": "no md_file digest"}
+        # no '.' in the shard's samples (device counts): the tool then writes its input unchanged
+        got = "flagged %d, lines with a '.' %d" % (s.rows, s.general_records)
+        if s.rows == 0 and s.general_records == 0:
+            got = hashlib.sha256(arr).hexdigest()
+        want, what = c["stdout"]["sha256"], ("no record flagged and no '.' in any sample column, so the output is "
+                                             "the input: its sha256 vs VCFX_missing_detector -q -i (reference)")
     elif workload == "hwe":
         if "hwe_file" not in dig["cases"]:
             return {"checked": False, "why": "no hwe_file digest"}
@@ -231,6 +263,8 @@ def e2e_rates(workload, arr, a):
         tool, args = "VCFX_hwe_tester", ["-q"]
     elif workload == "dose":
         tool, args = "VCFX_dosage_calculator", ["-q"]
+    elif workload == "md":
+        tool, args = "VCFX_missing_detector", ["-q"]
     elif workload == "pipeline":
         tool, args = "VCFX_record_filter", ["--filter", "QUAL>=30;FILTER==PASS"]
     else:
@@ -362,6 +396,24 @@ def main():
                 allreduce_counts([s.n_lines, s.rows, s.text_bytes, s.general_records])
             return s
         kern_names = ("line_count", "line_emit", "line_compact", "dose_len", "dose_rows", "dose_fmt")
+    elif a.workload == "ac":
+        ac_names = ["S%05d" % (k + 1) for k in range(a.samples)]
+        ac_idx = list(range(a.samples))
+
+        def step():
+            L = eng.index(ds)
+            s = eng.allele_counter(0, L, ac_idx, ac_names, seq=0, kind=0)  # every (record, sample) row
+            if red is not None:
+                allreduce_counts([s.n_lines, s.rows, s.text_bytes, s.general_records])
+            return s
+        kern_names = ("line_count", "line_emit", "line_compact", "ac_len", "ac_fmt")
+    elif a.workload == "md":
+        def step():
+            s = eng.missing_region(ds, engine.MODE_FILE)  # index + per-record missing-genotype test
+            if red is not None:
+                allreduce_counts([s.n_lines, s.rows, s.data_lines, s.general_records])
+            return s
+        kern_names = ("line_count", "line_emit", "line_compact", "md_lines")
     elif a.workload == "pipeline":
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
@@ -465,6 +517,12 @@ def main():
                 # pass 2 reads them again and writes the rows (2 bytes per sample)
                 "dose_len": region_bytes + L * (8 + 1 + 8 + 24),
                 "dose_fmt": region_bytes + tb + L * (8 + 1 + 8 + 24),
+                # allele counter: pass 1 reads the records (+ line end, status, length, meta per
+                # line); pass 2 reads each selected sample's GT (the records again) and writes the rows
+                "ac_len": region_bytes + L * (8 + 1 + 8 + 48),
+                "ac_fmt": region_bytes + tb + L * (8 + 1 + 8 + 48),
+                # missing detector: the records once + line end, status and the INFO span per line
+                "md_lines": region_bytes + L * (8 + 1 + 8),
                 "walk_compact": L * 2 * (8 + 13 + 16),
                 # the per-line rest: its lines' record bytes when the data are off the fixed-stride
                 # layout (every line a GT:AD:DP record), else the head record + status per line
@@ -503,6 +561,11 @@ def main():
                    "genotype-class reducer + HWE chi-square p-value rows" % (a.records, a.samples),
             "dose": "VCFX_dosage_calculator -i (file path) on a device-resident %d x %d shard per GPU: index + "
                     "per-sample dosage rows (2 output bytes per sample)" % (a.records, a.samples),
+            "ac": "VCFX_allele_counter -i (file path, per-sample text rows) on a device-resident %d x %d shard per "
+                  "GPU: index + per-(record, sample) REF/ALT counts + %d rows per record" % (a.records, a.samples,
+                                                                                            a.samples),
+            "md": "VCFX_missing_detector -i (file path) on a device-resident %d x %d shard per GPU: index + the "
+                  "per-record missing-genotype test" % (a.records, a.samples),
             "ld": "VCFX_ld_calculator -w %d -t %g streaming on a device-resident %d x %d shard per GPU: parse + "
                   "FP4-MFMA pair sums (count + emit) + pair text" % (a.window, a.threshold, a.records, a.samples),
         }[a.workload] + extra
@@ -531,7 +594,7 @@ def main():
         if ld:
             out["pairs_per_gpu"] = pairs
             out["pairs_emitted"] = np_
-        out["output_check"] = output_check(a.workload, eng, s, a, rank)
+        out["output_check"] = output_check(a.workload, eng, s, a, rank, arr)
         if world == 1 and not a.no_e2e and not general:
             out["e2e"] = e2e_rates(a.workload, arr, a)
         if not a.no_cpu_baseline:

@@ -283,6 +283,25 @@ typedef struct {
 int vcfxg_allele_counter(vcfxg_ctx *ctx, uint64_t first_line, uint64_t last_line, const vcfxg_ac_params *params,
                          vcfxg_summary *out);
 
+/* ---- VCFX_haplotype_phaser (LD reuse in block phasing) ------------------
+ * Over the lines from data_start (the byte after the '#CHROM' line): per line status 1 variant,
+ * 4 '#' line, 3 "<10 fields", 7 invalid POS, 8 no GT in FORMAT, 0 empty (mode VCFXG_MODE_FILE:
+ * phaseHaplotypesMmap / ...MmapStreaming, '\r' stripped first; VCFXG_MODE_STDIN: phaseHaplotypes
+ * / ...Streaming, an empty line skipped before the strip), VCFX_haplotype_phaser.cpp:607-1259.
+ * Each variant's genotypes are parseGenotypeFast codes (:312-357, the GT sub-field's allele sum,
+ * -1 missing); for every variant v > 0 the device computes calculateLDFast (:366-470) of (v - 1,
+ * v) over the shorter sample list -- the pair groupVariants (:1275-1322) and the streaming loops
+ * test, since the block's last variant is always the previous one -- and the block rule:
+ * r^2 >= threshold (and r > 0 when v's CHROM is "1").  n_samples_hint: the header's sample
+ * count (the genotype row width; wider records are handled by a second pass).  rows = variants;
+ * the text (vcfxg_fetch_text) holds each variant's entry "v:(CHROM:POS)" back to back. */
+int vcfxg_haplotype_phaser(vcfxg_ctx *ctx, size_t data_start, int mode, double threshold, uint32_t n_samples_hint,
+                           vcfxg_summary *out);
+/* per variant of the last call: flags (bit 0 the pair with the previous variant passes the block
+ * rule, bit 1 both have the same CHROM; 0 for variant 0), r2 (may be NULL) and the entries'
+ * text offsets (n_variants + 1) */
+int vcfxg_phaser_variants(vcfxg_ctx *ctx, uint8_t *flags, double *r2, uint64_t *entry_offsets);
+
 /* ---- variant counter -------------------------------------------------------------------
  * Per line status: ROW = data line with >= 8 tab-separated columns (counted), WARN = fewer
  * columns, SKIP = empty or '#'.  strip_cr: drop a trailing '\r' first (file path).

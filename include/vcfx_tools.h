@@ -17,6 +17,7 @@
  *   vcfx_tool_dosage_calculator run/main, VCFX_dosage_calculator.cpp:52-102, 614-620
  *   vcfx_tool_missing_detector  run/main, VCFX_missing_detector.cpp:943-997, 1010-1013
  *   vcfx_tool_allele_counter    parseArguments/main, VCFX_allele_counter.cpp:352-395, 1473-1536
+ *   vcfx_tool_haplotype_phaser  run/main, VCFX_haplotype_phaser.cpp:478-569, 1336-1342
  *   vcfx_tool_variant_counter   run, VCFX_variant_counter.cpp:154-218
  *   vcfx_tool_main              the `vcfx <tool> ...` dispatch (src/vcfx_wrapper/vcfx.cpp:177-187)
  * Without a usable gfx950 device a tool that reaches the record loop writes
@@ -39,6 +40,7 @@ int vcfx_tool_hwe_tester(int argc, char **argv, int in_fd, int out_fd, int err_f
 int vcfx_tool_dosage_calculator(int argc, char **argv, int in_fd, int out_fd, int err_fd);
 int vcfx_tool_missing_detector(int argc, char **argv, int in_fd, int out_fd, int err_fd);
 int vcfx_tool_allele_counter(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+int vcfx_tool_haplotype_phaser(int argc, char **argv, int in_fd, int out_fd, int err_fd);
 /* tool = "VCFX_<name>" (a leading path is ignored); -100 for an unknown tool */
 int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd);
 /* `VCFX_record_filter --filter F --logic L [-i input] | VCFX_genotype_query -g Q [--strict] [-q]`

@@ -2905,6 +2905,353 @@ static int md_main(int argc, char **argv, const char *in, size_t inn, ob_t *out,
     return 0;
 }
 
+/* ==================================================================================== */
+/* VCFX_haplotype_phaser (consecutive-variant r^2 on the LD coding)     */
+/* ==================================================================================== */
+/* parseGenotypeFast, VCFX_haplotype_phaser.cpp:312-357: the allele sum as int8_t, -1 missing */
+static int ph_gt(const char *g, size_t n) {
+    if (n == 0) return -1;
+    if (n == 3 && (g[1] == '/' || g[1] == '|')) {
+        if (g[0] == '.' || g[2] == '.') return -1;
+        if (g[0] >= '0' && g[0] <= '9' && g[2] >= '0' && g[2] <= '9') return (int8_t)((g[0] - '0') + (g[2] - '0'));
+    }
+    size_t k = 0;
+    while (k < n && g[k] != '/' && g[k] != '|') k++;
+    if (k == n) return -1;
+    const char *a1 = g, *a2 = g + k + 1;
+    size_t n1 = k, n2 = n - k - 1;
+    if (!n1 || !n2 || a1[0] == '.' || a2[0] == '.') return -1;
+    uint32_t i1 = 0, i2 = 0;  /* (int accumulation; wraps as built) */
+    for (size_t j = 0; j < n1; j++) {
+        if (a1[j] < '0' || a1[j] > '9') return -1;
+        i1 = i1 * 10u + (uint32_t)(a1[j] - '0');
+    }
+    for (size_t j = 0; j < n2; j++) {
+        if (a2[j] < '0' || a2[j] > '9') return -1;
+        i2 = i2 * 10u + (uint32_t)(a2[j] - '0');
+    }
+    return (int8_t)(i1 + i2);
+}
+/* findGTIndex :289-307 */
+static int ph_gt_index(const char *f, size_t n) {
+    size_t st = 0;
+    int idx = 0;
+    for (size_t p = 0; p <= n; p++)
+        if (p == n || f[p] == ':') {
+            if (p - st == 2 && f[st] == 'G' && f[st + 1] == 'T') return idx;
+            idx++;
+            st = p + 1;
+        }
+    return -1;
+}
+/* extractNthField :265-284 */
+static sv_t ph_nth(const char *s, size_t n, int k) {
+    size_t st = 0;
+    int idx = 0;
+    for (size_t p = 0; p <= n; p++)
+        if (p == n || s[p] == ':') {
+            if (idx == k) return sv(s + st, p - st);
+            idx++;
+            st = p + 1;
+        }
+    return sv(s, 0);
+}
+/* calculateLDFast :366-470 (both builds: integer sums, then the same fp64 sequence) */
+void oracle_ph_ld(const int8_t *a, const int8_t *b, size_t n, double *r, double *r2) {
+    long long sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;
+    int vn = 0;
+    for (size_t i = 0; i < n; i++) {
+        int x = a[i], y = b[i];
+        if (x < 0 || y < 0) continue;
+        vn++;
+        sx += x; sy += y; sxy += x * y; sx2 += x * x; sy2 += y * y;
+    }
+    *r = *r2 = 0.0;
+    if (vn == 0) return;
+    double mx = (double)sx / vn, my = (double)sy / vn;
+    double cov = ((double)sxy / vn) - (mx * my);
+    double vx = ((double)sx2 / vn) - (mx * mx), vy = ((double)sy2 / vn) - (my * my);
+    if (vx <= 0.0 || vy <= 0.0) return;
+    *r = cov / (sqrt(vx) * sqrt(vy));
+    *r2 = *r * *r;
+}
+typedef struct {
+    sv_t chrom;
+    int pos;
+    size_t ns;
+    int8_t *g;
+} ph_var;
+enum { PH_OK = 0, PH_FEW = 1, PH_POS = 2, PH_NOGT = 3 };
+/* the record parse shared by the four paths: fields split on every tab, >= 10 fields, POS all
+ * digits (empty = 0), GT index of FORMAT, a genotype per field from the 10th */
+static int ph_parse(const char *ls, const char *le, ph_var *v) {
+    size_t nf = 1;
+    for (const char *p = ls; p < le; p++) nf += *p == '\t';
+    if (nf < 10) return PH_FEW;
+    const char *f[10];
+    const char *p = ls;
+    for (int k = 0; k < 10; k++) {
+        f[k] = p;
+        if (k < 9) p = (const char *)memchr(p, '\t', (size_t)(le - p)) + 1;
+    }
+    uint32_t pos = 0;
+    for (const char *q = f[1]; q < f[2] - 1; q++) {
+        if (*q < '0' || *q > '9') return PH_POS;
+        pos = pos * 10u + (uint32_t)(*q - '0');
+    }
+    int gi = ph_gt_index(f[8], (size_t)(f[9] - 1 - f[8]));
+    if (gi < 0) return PH_NOGT;
+    v->chrom = sv(ls, (size_t)(f[1] - 1 - ls));
+    v->pos = (int)pos;
+    v->ns = nf - 9;
+    v->g = (int8_t *)malloc(v->ns + 1);
+    const char *s = f[9];
+    for (size_t k = 0; k < v->ns; k++) {
+        const char *e = (const char *)memchr(s, '\t', (size_t)(le - s));
+        if (!e) e = le;
+        sv_t gt = ph_nth(s, (size_t)(e - s), gi);
+        v->g[k] = (int8_t)ph_gt(gt.p, gt.n);
+        s = e + 1;
+    }
+    return PH_OK;
+}
+static void ph_entry(ob_t *o, int idx, const ph_var *v) {
+    ob_printf(o, "%d:(", idx);
+    ob_put(o, v->chrom.p, v->chrom.n);
+    ob_printf(o, ":%d)", v->pos);
+}
+/* the block decision of groupVariants :1275-1322 / the streaming loops for variant b after a */
+static int ph_join(const ph_var *a, const ph_var *b, double thr) {
+    double r, r2;
+    oracle_ph_ld(a->g, b->g, a->ns < b->ns ? a->ns : b->ns, &r, &r2);
+    if (sv_eqs(b->chrom, "1")) return r2 >= thr && r > 0;
+    return r2 >= thr;
+}
+/* phaseHaplotypesMmap :607-751 (stdin_mode 0) / phaseHaplotypes :971-1081 (1); streaming:
+ * phaseHaplotypesMmapStreaming :757-965 / phaseHaplotypesStreaming :1086-1259 (a window
+ * of `win` variants, CircularVariantBuffer :153-203 restated over variant numbers) */
+static void ph_run(const char *d, size_t n, int stdin_mode, int streaming, double thr, size_t win, int quiet,
+                   ob_t *out, ob_t *err) {
+    lines_t it = {d, d + n};
+    const char *ls, *le;
+    int found = 0, marker = 0, blockno = 0;
+    ph_var *vs = NULL;
+    size_t nv = 0, capv = 0;
+    /* streaming: the circular buffer of variant numbers */
+    size_t cap = win + 1, head = 0, cnt = 0;
+    size_t *ring = streaming ? (size_t *)malloc((cap ? cap : 1) * sizeof(size_t)) : NULL;
+    sv_t cur = sv("", 0);
+    while (next_line(&it, &ls, &le)) {
+        if (stdin_mode && le == ls) continue;
+        if (le > ls && le[-1] == '\r') le--;
+        if (!stdin_mode && le == ls) continue;
+        char c0 = le > ls ? *ls : '\0';
+        if (c0 == '#') {
+            if (starts_chrom(ls, (size_t)(le - ls))) found = 1;
+            ob_put(out, ls, (size_t)(le - ls));
+            ob_putc(out, '\n');
+            continue;
+        }
+        if (!found) {
+            if (!stdin_mode) {
+                if (!quiet) ob_puts(err, "Warning: VCF data line before #CHROM\n");
+                continue;
+            }
+            if (!quiet) ob_puts(err, "Error: no #CHROM line found.\n");
+            goto done;
+        }
+        if (streaming && !marker) {
+            ob_puts(out, "#HAPLOTYPE_BLOCKS_START (streaming)\n");
+            marker = 1;
+        }
+        ph_var v;
+        int st = ph_parse(ls, le, &v);
+        if (st == PH_FEW) { if (!quiet) ob_puts(err, "Warning: skipping line with <10 fields\n"); continue; }
+        if (st == PH_POS) { if (!quiet) ob_puts(err, "Warning: invalid pos => skip\n"); continue; }
+        if (st == PH_NOGT) {
+            if (!quiet && !streaming) ob_puts(err, stdin_mode ? "Warning: no GT field\n" : "Warning: no GT field found\n");
+            continue;
+        }
+        if (nv == capv) { capv = capv ? 2 * capv : 64; vs = (ph_var *)realloc(vs, capv * sizeof *vs); }
+        vs[nv++] = v;
+        if (!streaming) continue;
+        size_t vi = nv - 1;
+#define PH_AT(i) ring[(head + (i)) % cap]
+#define PH_BLOCK(k)                                                      \
+    do {                                                                 \
+        ob_printf(out, "Block %d: ", ++blockno);                         \
+        for (size_t j = 0; j < (k); j++) {                               \
+            ph_entry(out, (int)PH_AT(j), &vs[PH_AT(j)]);                 \
+            if (j + 1 < (k)) ob_puts(out, ", ");                         \
+        }                                                                \
+        ob_putc(out, '\n');                                              \
+    } while (0)
+#define PH_PUSH(x)                                                       \
+    do {                                                                 \
+        ring[(head + cnt) % cap] = (x);                                  \
+        if (cnt < cap) cnt++;                                            \
+        else head = (head + 1) % cap;                                    \
+    } while (0)
+        if (cnt == 0) {
+            PH_PUSH(vi);
+            cur = v.chrom;
+            continue;
+        }
+        if (!(cur.n == v.chrom.n && memcmp(cur.p, v.chrom.p, cur.n) == 0)) {
+            PH_BLOCK(cnt);
+            head = cnt = 0;
+            PH_PUSH(vi);
+            cur = v.chrom;
+            continue;
+        }
+        if (ph_join(&vs[ring[(head + cnt - 1) % cap]], &v, thr)) {
+            PH_PUSH(vi);
+            if (cnt > win) {
+                size_t ev = cnt - win;
+                PH_BLOCK(ev);
+                for (size_t j = 0; j < ev; j++) if (cnt) { head = (head + 1) % cap; cnt--; }
+            }
+        } else {
+            PH_BLOCK(cnt);
+            head = cnt = 0;
+            PH_PUSH(vi);
+        }
+    }
+    if (streaming) {
+        if (cnt) PH_BLOCK(cnt);
+        if (marker) ob_puts(out, "#HAPLOTYPE_BLOCKS_END\n");
+        goto done;
+    }
+    if (nv == 0) {
+        if (!quiet) ob_puts(err, "Error: no variant data found.\n");
+        goto done;
+    }
+    ob_puts(out, "#HAPLOTYPE_BLOCKS_START\n");
+    for (size_t i = 0; i < nv; i++) {
+        int start = i == 0 || !sv_eq(vs[i].chrom, vs[i - 1].chrom.p, vs[i - 1].chrom.n) || !ph_join(&vs[i - 1], &vs[i], thr);
+        if (start) {
+            if (i) ob_putc(out, '\n');
+            ob_printf(out, "Block %d: ", ++blockno);
+        } else ob_puts(out, ", ");
+        ph_entry(out, (int)i, &vs[i]);
+    }
+    ob_puts(out, "\n#HAPLOTYPE_BLOCKS_END\n");
+done:
+#undef PH_AT
+#undef PH_BLOCK
+#undef PH_PUSH
+    for (size_t i = 0; i < nv; i++) free(vs[i].g);
+    free(vs);
+    free(ring);
+}
+static void ph_help(ob_t *o) {  /* displayHelp :571-601 */
+    ob_puts(o,
+        "VCFX_haplotype_phaser: Group variants into blocks by naive LD threshold.\n\n"
+        "Usage:\n"
+        "  VCFX_haplotype_phaser [options] [input.vcf]\n"
+        "  VCFX_haplotype_phaser [options] < input.vcf\n\n"
+        "Options:\n"
+        "  -h, --help               Show this help message\n"
+        "  -l, --ld-threshold <val> r^2 threshold [0..1], default 0.8\n"
+        "  -s, --streaming          Enable streaming mode with sliding window.\n"
+        "                           Uses O(window * samples) memory instead of O(variants * samples).\n"
+        "  -w, --window <N>         Window size for streaming mode (default: 1000)\n"
+        "  -i, --input FILE         Input VCF file (uses fast memory-mapped I/O)\n"
+        "  -q, --quiet              Suppress warning messages\n\n"
+        "Performance:\n"
+        "  File input (-i) uses memory-mapped I/O for 20-50x faster processing.\n"
+        "  Features include:\n"
+        "  - SIMD-optimized line scanning (AVX2/SSE2)\n"
+        "  - Zero-copy string parsing with string_view\n"
+        "  - 1MB output buffering\n"
+        "  - Circular buffer for O(1) streaming operations\n"
+        "  - FORMAT field caching\n"
+        "  - SIMD-optimized LD calculation\n\n"
+        "Modes:\n"
+        "  Default mode:   Loads all variants into memory, outputs blocks at end.\n"
+        "  Streaming mode: Uses sliding window, outputs blocks incrementally.\n"
+        "                  Enables processing of arbitrarily large files.\n\n"
+        "Examples:\n"
+        "  VCFX_haplotype_phaser -i input.vcf              # Fast (mmap)\n"
+        "  VCFX_haplotype_phaser input.vcf                 # Fast (mmap)\n"
+        "  VCFX_haplotype_phaser < input.vcf               # Slower (stdin)\n"
+        "  VCFX_haplotype_phaser --streaming -w 500 -i large.vcf\n");
+}
+/* std::stod / std::stoul: no conversion or ERANGE -> the error path */
+static int ph_stod(const char *s, double *v) {
+    char *e;
+    errno = 0;
+    *v = strtod(s, &e);
+    return e != s && errno != ERANGE;
+}
+static int ph_stoul(const char *s, unsigned long *v) {
+    char *e;
+    errno = 0;
+    *v = strtoul(s, &e, 10);
+    return e != s && errno != ERANGE;
+}
+/* main :1336-1342 (handle_common_flags) + run :478-569 */
+static int ph_main(int argc, char **argv, const char *in, size_t inn, ob_t *out, ob_t *err) {
+    if (common_flags(argc, argv, "VCFX_haplotype_phaser", ph_help, out)) return 0;
+    double thr = 0.8;
+    unsigned long win = 1000;
+    int streaming = 0, quiet = 0, help = 0;
+    const char *input = NULL;
+    static struct option lo[] = {{"help", no_argument, NULL, 'h'},      {"ld-threshold", required_argument, NULL, 'l'},
+                                 {"streaming", no_argument, NULL, 's'}, {"window", required_argument, NULL, 'w'},
+                                 {"input", required_argument, NULL, 'i'}, {"quiet", no_argument, NULL, 'q'},
+                                 {NULL, 0, NULL, 0}};
+    optind = 0;
+    errcap_t ec;
+    errcap_begin(&ec);
+    int opt, rc = -1;
+    while (rc < 0 && (opt = getopt_long(argc, argv, "hl:sw:i:q", lo, NULL)) != -1) {
+        switch (opt) {
+            case 'h': help = 1; break;
+            case 'l':
+                if (!ph_stod(optarg, &thr)) {
+                    errcap_end(&ec, err);
+                    ob_puts(err, "Error: invalid LD threshold.\n");
+                    ph_help(out);
+                    return 1;
+                }
+                break;
+            case 's': streaming = 1; break;
+            case 'w':
+                if (!ph_stoul(optarg, &win)) {
+                    errcap_end(&ec, err);
+                    ob_puts(err, "Error: invalid window size.\n");
+                    ph_help(out);
+                    return 1;
+                }
+                break;
+            case 'i': input = optarg; break;
+            case 'q': quiet = 1; break;
+            default: help = 1;
+        }
+    }
+    errcap_end(&ec, err);
+    if (!input && optind < argc) input = argv[optind];
+    if (help) { ph_help(out); return 0; }
+    if (thr < 0.0 || thr > 1.0) {
+        ob_puts(err, "Error: invalid LD threshold\n");
+        ph_help(out);
+        return 1;
+    }
+    if (input && strcmp(input, "-") != 0) {
+        char *d;
+        size_t n;
+        if (read_file(input, &d, &n) < 0) {
+            ob_printf(err, "Error: Cannot open file: %s\n", input);
+            return 0;
+        }
+        if (n) ph_run(d, n, 0, streaming, thr, (size_t)win, quiet, out, err);
+        free(d);
+    } else
+        ph_run(in, inn, 1, streaming, thr, (size_t)win, quiet, out, err);
+    return 0;
+}
+
 int oracle_main(const char *tool, int argc, char **argv, const char *in, size_t inn, oracle_result *res) {
     ob_t out = {0}, err = {0};
     int rc;
@@ -2920,6 +3267,7 @@ int oracle_main(const char *tool, int argc, char **argv, const char *in, size_t 
     else if (strcmp(t, "VCFX_dosage_calculator") == 0) rc = dose_main(argc, argv, in, inn, &out, &err);
     else if (strcmp(t, "VCFX_allele_counter") == 0) rc = ac_main(argc, argv, in, inn, &out, &err);
     else if (strcmp(t, "VCFX_missing_detector") == 0) rc = md_main(argc, argv, in, inn, &out, &err);
+    else if (strcmp(t, "VCFX_haplotype_phaser") == 0) rc = ph_main(argc, argv, in, inn, &out, &err);
     else return -1;
     res->out = out.p ? out.p : (char *)calloc(1, 1);
     res->out_len = out.n;

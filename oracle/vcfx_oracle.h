@@ -46,6 +46,8 @@ long oracle_af_counts(const char *buf, size_t n, int stdin_mode, int32_t *alt,
 /* r^2 of two int8 genotype vectors exactly as computeRsqFast (VCFX_ld_calculator.cpp:
  * 397-401 -> 352-393, x86 scalar body) computes it. */
 double oracle_ld_rsq_fast(const int8_t *g1, const int8_t *g2, size_t n);
+/* VCFX_haplotype_phaser calculateLDFast (VCFX_haplotype_phaser.cpp:366-470): r and r^2 */
+void oracle_ph_ld(const int8_t *a, const int8_t *b, size_t n, double *r, double *r2);
 /* parseGenotypeRaw (VCFX_ld_calculator.cpp:145-174). */
 int oracle_ld_parse_gt_raw(const char *s, size_t len);
 

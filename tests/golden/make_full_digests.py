@@ -46,11 +46,18 @@ INPUTS = {
     # config 5: the first 3,000 variants of the bench's LD shard (seed 20251226, hap blocks);
     # with a 100 K window their pairs are the first pairs of the bench's own output
     "ld3000": dict(n_records=3000, n_samples=2504, seed=20251226, hap_blocks=1),
+    # the chr21-like shard with sparse missing calls (".|." at rate 5e-4: about 70 % of the
+    # records carry one) for VCFX_missing_detector's flagging path
+    "chr21_miss": dict(n_records=427409, n_samples=2504, seed=20251226, missing_rate=5e-4),
 }
 
 AF, RF, GQ, LD, NR, HWE = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query",
                            "VCFX_ld_calculator", "VCFX_nonref_filter", "VCFX_hwe_tester")
 DOSE = "VCFX_dosage_calculator"
+AC, MD = "VCFX_allele_counter", "VCFX_missing_detector"
+# 50 sample names of the synthetic header (S00001..S02504) in a scrambled order: the MT path's
+# per-slot lookup and the stream path's forward-only cursor differ on it
+SEL50 = " ".join("S%05d" % (1 + (k * 1597) % 2504) for k in range(50))
 
 # name -> (input, [stage argv ...] with "{F}" for the file; the first stage reads stdin when
 # it has no {F}), keep-mask flag
@@ -72,6 +79,13 @@ CASES = {
     "ld1500_t02": ("ld1500", [[LD, "-q", "-w", "1500", "-t", "0.2", "-i", "{F}"]], False),
     "ld1500_t0": ("ld1500", [[LD, "-q", "-w", "1500", "-t", "0", "-i", "{F}"]], False),
     "ld1500_w300_t0": ("ld1500", [[LD, "-q", "-w", "300", "-t", "0", "-i", "{F}"]], False),
+    "ac_bin_file": ("chr21", [[AC, "-q", "-b", "-i", "{F}"]], False),
+    "ac_agg_file": ("chr21", [[AC, "-q", "-a", "-i", "{F}"]], False),
+    "ac_sel_file": ("chr21", [[AC, "-q", "-s", SEL50, "-i", "{F}"]], False),
+    "ac_sel_stdin": ("chr21", [[AC, "-q", "-s", SEL50]], False),
+    "md_file": ("chr21", [[MD, "-q", "-i", "{F}"]], False),
+    "md_file_miss": ("chr21_miss", [[MD, "-q", "-i", "{F}"]], False),
+    "md_stdin_miss": ("chr21_miss", [[MD]], False),
     "ld3000_bench": ("ld3000", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
 }
 

@@ -29,6 +29,7 @@ HWE = "VCFX_hwe_tester"
 DOSE = "VCFX_dosage_calculator"
 AC = "VCFX_allele_counter"
 MD = "VCFX_missing_detector"
+PH = "VCFX_haplotype_phaser"
 # the reference's parseGenotypeRaw loops forever on a GT byte other than a digit, '/', '|'
 # or '.' (a CRLF line's last sample, for one): such cases are left out (run_case -> None)
 HANG_S = 20
@@ -188,6 +189,25 @@ def build_cases():
               ["data/nope.vcf"], ["-i", "data/empty.vcf"], ["-t", "0", "-q", "-i", "data/ref_md/md_traps.vcf"]):
         add(MD, a)
     add(MD, [], stdin="data/empty.vcf", tag="empty_stdin")
+    # ---- haplotype_phaser: both modes (default / --streaming) in both input forms, the
+    # reference test script's fixtures (copied as data) and the traps
+    pdir = os.path.join(HERE, "data", "ref_ph")
+    for f in vcfs + [os.path.join("data", "ref_ph", n) for n in sorted(os.listdir(pdir))]:
+        for a in ([], ["-l", "0.5"], ["-s"], ["-s", "-w", "2"], ["-q"], ["-q", "-s", "-w", "1", "-l", "0.3"]):
+            add(PH, a + ["-i", f])
+            add(PH, a, stdin=f)
+        add(PH, [f])
+        if f not in big:
+            add(PH, ["-s", "-w", "0", "-i", f])
+            add(PH, ["-l", "0", "-i", f])
+            add(PH, ["-l", "1", "-s"], stdin=f)
+            add(PH, ["-l", "nan", "-i", f])
+    for a in (["-h"], ["--help"], ["-v"], ["--version"], ["--bogus"], ["-x"], ["-i"], ["-i", "data/nope.vcf"],
+              ["data/nope.vcf"], ["-i", "data/empty.vcf"], ["-l", "x"], ["-l", "1.5"], ["-l", "-0.1"], ["-l", "1e-400"],
+              ["-l", " 0.5", "-i", "data/ph_traps.vcf"], ["-w", "x"], ["-w", "-1", "-i", "data/ph_traps.vcf"],
+              ["--ld-threshold=0.7", "--window=3", "--streaming", "--input", "data/ph_traps.vcf"], ["-"]):
+        add(PH, a, stdin="data/ph_traps.vcf" if a[-1:] == ["-"] else None)
+    add(PH, [], stdin="data/empty.vcf", tag="empty_stdin")
     return cases
 
 

@@ -42,13 +42,13 @@ def test_tools_lib_exports():
     lib = ctypes.CDLL(TOOLS_LIB)
     txt = open(os.path.join(os.path.dirname(BUILD), "include", "vcfx_tools.h")).read()
     syms = sorted(set(re.findall(r"\b(vcfx_(?:tool|pipeline)_[a-z0-9_]+)\s*\(", txt)))
-    assert len(syms) == 12, syms  # main, 10 tools, the fused pipeline
+    assert len(syms) == 13, syms  # main, 11 tools, the fused pipeline
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
 
 
 @pytest.mark.parametrize("tool", ["VCFX_allele_freq_calc", "VCFX_genotype_query", "VCFX_record_filter", "VCFX_variant_counter", "VCFX_ld_calculator",
                                   "VCFX_nonref_filter", "VCFX_hwe_tester", "VCFX_dosage_calculator", "VCFX_missing_detector",
-                                  "VCFX_allele_counter"])
+                                  "VCFX_allele_counter", "VCFX_haplotype_phaser"])
 def test_binaries_present(tool):
     assert os.access(tool_binary(tool), os.X_OK)

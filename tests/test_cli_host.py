@@ -11,7 +11,7 @@ from vcfx_amd import tools
 
 IMPLEMENTED = {"VCFX_allele_freq_calc", "VCFX_genotype_query", "VCFX_record_filter", "VCFX_variant_counter", "VCFX_ld_calculator",
                "VCFX_nonref_filter", "VCFX_hwe_tester", "VCFX_dosage_calculator", "VCFX_missing_detector",
-               "VCFX_allele_counter"}
+               "VCFX_allele_counter", "VCFX_haplotype_phaser"}
 CASES = [c for c in load_cases() if c["tool"] in IMPLEMENTED]
 NODEV = b"no usable MI355X"
 

@@ -9,7 +9,7 @@ pytestmark = pytest.mark.gpu
 
 IMPLEMENTED = ["VCFX_allele_freq_calc", "VCFX_genotype_query", "VCFX_record_filter", "VCFX_variant_counter", "VCFX_ld_calculator",
                "VCFX_nonref_filter", "VCFX_hwe_tester", "VCFX_dosage_calculator", "VCFX_missing_detector",
-               "VCFX_allele_counter"]
+               "VCFX_allele_counter", "VCFX_haplotype_phaser"]
 CASES = load_cases()
 
 

@@ -119,7 +119,9 @@ def _check(case, inputs, stdin="none"):
                                         ("nonref_file", "none"), ("pipeline_bench", "none"),
                                         ("nonref_stdin", "pipe"), ("nonref_stdin", "file"),
                                         ("hwe_file", "none"), ("hwe_stdin", "pipe"), ("hwe_stdin", "file"),
-                                        ("dose_file", "none")])
+                                        ("dose_file", "none"), ("ac_bin_file", "none"), ("ac_agg_file", "none"),
+                                        ("ac_sel_file", "none"), ("ac_sel_stdin", "pipe"), ("ac_sel_stdin", "file"),
+                                        ("md_file", "none")])
 def test_chr21_shard_matches_reference(inputs, case, stdin):
     _check(case, inputs, stdin)
 
@@ -130,6 +132,15 @@ def test_annotated_shard_matches_reference(inputs, case, stdin):
     _check(case, inputs, stdin)
     if case == "gq_strict_annot":
         inputs.drop("annot")
+
+
+@pytest.mark.parametrize("case,stdin", [("md_file_miss", "none"), ("md_stdin_miss", "pipe"),
+                                        ("md_stdin_miss", "file")])
+def test_missing_shard_matches_reference(inputs, case, stdin):
+    """VCFX_missing_detector on the shard with sparse missing calls (most records flagged)"""
+    _check(case, inputs, stdin)
+    if case == "md_stdin_miss" and stdin == "file":
+        inputs.drop("chr21_miss")
 
 
 @pytest.mark.parametrize("case", ["af_file", "pipeline_bench", "hwe_file"])

@@ -20,8 +20,26 @@ def oracle():
 def test_case_count():
     tools = collections.Counter(c["tool"] for c in CASES)
     # the five hot-path tools + nonref_filter, hwe_tester, dosage_calculator, allele_counter and
-    # missing_detector (8(f) rank 2)
-    assert len(tools) == 10 and min(tools.values()) > 40
+    # missing_detector (8(f) rank 2), haplotype_phaser (8(f) rank 3)
+    assert len(tools) == 11 and min(tools.values()) > 40
+
+
+# tests/test_haplotype_phaser.sh (jorgeMFS/VCFX): the block lines its tests 1-3 grep for
+PH_EXP = [("basic.vcf", "0.8", [b"Block 1: 0:(1:100), 1:(1:150), 2:(1:200)", b"Block 2: 3:(1:250)"]),
+          ("basic.vcf", "0.99", [b"Block 1: 0:(1:100), 1:(1:150), 2:(1:200)", b"Block 2: 3:(1:250)"]),
+          ("low_ld.vcf", "0.5", [b"Block 1: 0:(1:100), 1:(1:150), 2:(1:200)", b"Block 2: 3:(1:250)",
+                                 b"Block 3: 4:(1:300)"])]
+
+
+@pytest.mark.parametrize("name,thr,want", PH_EXP)
+def test_oracle_phaser_reference_script(oracle, name, thr, want):
+    with open(os.path.join(GOLDEN, "data", "ref_ph", name), "rb") as f:
+        data = f.read()
+    out, _, rc = oracle.run(["VCFX_haplotype_phaser", "--ld-threshold", thr], data)
+    assert rc == 0
+    lines = out.split(b"\n")
+    for w in want:
+        assert w in lines, (w, out)
 
 
 @pytest.mark.parametrize("tool", sorted({c["tool"] for c in CASES}))

@@ -75,6 +75,9 @@ struct vcfxg_ctx {
     std::vector<uint32_t> ac_eff_host;
     std::vector<uint64_t> ac_noff_host;
     std::string ac_names_host;
+    // VCFX_haplotype_phaser: genotype rows (by line), per-line info, variant -> line, pair flags
+    DevBuf ph_G, ph_isvar, ph_info, ph_vnum, ph_vline, ph_flags, ph_r2;
+    uint64_t ph_nvar = 0;
     uint64_t hwe_rc_n = 0;
     // ulps either side of the device p-value that must print the same digits (test hook: a
     // huge value sends every exp()-derived row to the host)
@@ -1488,6 +1491,97 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
         out->general_records = tail[4];
         out->text_bytes = text;
     }
+    return VCFXG_OK;
+}
+
+// VCFX_haplotype_phaser over [data_start, n): index, the per-line parse into genotype rows, the
+// variant compaction (one host synchronisation for the variant count), the pair pass, a scan
+// and the entries (a second synchronisation)
+int vcfxg_haplotype_phaser(vcfxg_ctx *c, size_t data_start, int mode, double thr, uint32_t hint, vcfxg_summary *out) {
+    if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
+    if (!c->loaded) return VCFXG_E_STATE;
+    if (data_start > c->n) data_start = c->n;
+    uint64_t L = 0;
+    int r = vcfxg_index(c, data_start, &L);
+    if (r) return r;
+    HIPCHK(c, hipSetDevice(c->device));
+    const char *buf = P<char>(c->input);
+    uint64_t kpad = ((uint64_t)std::max<uint32_t>(hint, 16) + 15) & ~15ull;
+    static thread_local uint64_t h[2];
+    for (int pass = 0;; pass++) {
+        r = ensure(c, c->ph_G, L * kpad + 16);
+        if (!r) r = af_buffers(c, L);
+        if (!r) r = ensure(c, c->ph_isvar, 4 * (L + 1));
+        if (!r) r = ensure(c, c->ph_info, vcfxg::ph_line_bytes() * (L + 1));
+        if (!r) r = ensure(c, c->ph_vnum, 8 * (L + 1));
+        if (!r) r = ensure(c, c->ph_vline, 8 * (L + 1));
+        if (r) return r;
+        HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+        HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->counters) + 4, 0, 8, c->stream));
+        prof_begin(c, "ph_lines");
+        HIPCHK(c, vcfxg::launch_ph_lines(buf, (int64_t)data_start, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L,
+                                         mode, (uint32_t)kpad, P<int8_t>(c->ph_G), P<uint8_t>(c->status),
+                                         P<uint32_t>(c->ph_isvar), c->ph_info.p, P<unsigned long long>(c->counters),
+                                         c->stream));
+        prof_end(c, "ph_lines");
+        if (L) {
+            r = exclusive_scan(c, P<uint32_t>(c->ph_isvar), P<uint64_t>(c->ph_vnum), (size_t)L);
+            if (r) return r;
+            HIPCHK(c, vcfxg::launch_ph_compact(P<uint32_t>(c->ph_isvar), P<uint64_t>(c->ph_vnum), P<uint64_t>(c->d_nlines),
+                                               L, P<uint64_t>(c->ph_vline), P<uint64_t>(c->counters) + 4, c->stream));
+        }
+        HIPCHK(c, hipMemcpyAsync(h, P<uint64_t>(c->counters) + 3, 16, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (h[0] > kpad && pass == 0) {  // a record wider than the rows: once more with rows that fit
+            kpad = (h[0] + 15) & ~15ull;
+            continue;
+        }
+        break;
+    }
+    const uint64_t V = h[1];
+    r = ensure(c, c->ph_flags, V + 1);
+    if (!r) r = ensure(c, c->ph_r2, 8 * (V + 1));
+    if (!r) r = ensure(c, c->rowlen, 8 * (V + 1));
+    if (!r) r = ensure(c, c->rowoff, 8 * (V + 1));
+    if (r) return r;
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->rowlen) + V, 0, 8, c->stream));
+    prof_begin(c, "ph_pairs");
+    HIPCHK(c, vcfxg::launch_ph_pairs(buf, P<uint64_t>(c->ph_vline), P<uint64_t>(c->counters) + 4, V, c->ph_info.p,
+                                     P<int8_t>(c->ph_G), (uint32_t)kpad, thr, P<uint8_t>(c->ph_flags),
+                                     P<uint64_t>(c->rowlen), P<double>(c->ph_r2), c->stream));
+    prof_end(c, "ph_pairs");
+    r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)V + 1);
+    if (r) return r;
+    static thread_local uint64_t text;
+    HIPCHK(c, hipMemcpyAsync(&text, P<uint64_t>(c->rowoff) + V, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    r = ensure(c, c->text, text + 1);
+    if (r) return r;
+    prof_begin(c, "ph_fmt");
+    HIPCHK(c, vcfxg::launch_ph_fmt(buf, P<uint64_t>(c->ph_vline), P<uint64_t>(c->counters) + 4, V, c->ph_info.p,
+                                   P<uint64_t>(c->rowoff), P<char>(c->text), c->stream));
+    prof_end(c, "ph_fmt");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    c->text_bytes = text;
+    c->ph_nvar = V;
+    if (out) {
+        std::memset(out, 0, sizeof *out);
+        out->n_lines = L;
+        out->rows = V;
+        out->text_bytes = text;
+    }
+    return VCFXG_OK;
+}
+
+int vcfxg_phaser_variants(vcfxg_ctx *c, uint8_t *flags, double *r2, uint64_t *offs) {
+    if (!c) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    const uint64_t V = c->ph_nvar;
+    if (flags && V) HIPCHK(c, hipMemcpyAsync(flags, c->ph_flags.p, V, hipMemcpyDeviceToHost, c->stream));
+    if (r2 && V) HIPCHK(c, hipMemcpyAsync(r2, c->ph_r2.p, 8 * V, hipMemcpyDeviceToHost, c->stream));
+    if (offs) HIPCHK(c, hipMemcpyAsync(offs, c->rowoff.p, 8 * (V + 1), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return VCFXG_OK;
 }
 

@@ -172,6 +172,22 @@ hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *li
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
                          uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, const uint8_t *status,
                          const void *meta, const uint64_t *off, char *out, hipStream_t s);
+// VCFX_haplotype_phaser (vcfxg_ph.hip): per line status (kPh*), the variants' genotype codes
+// (row = line, kpad bytes; counters[3] = the largest sample count past kpad), the variant ->
+// line compaction, per variant the pair flags with its predecessor (bit 0 the block rule
+// passes, bit 1 same CHROM) + r^2 + entry length, and the entries "v:(chrom:pos)"
+enum : uint8_t { kPhSkip = 0, kPhVar = 1, kPhFew = 3, kPhHeader = 4, kPhPos = 7, kPhNoGt = 8 };
+size_t ph_line_bytes();
+hipError_t launch_ph_lines(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                           uint64_t n_lines_host, int mode, uint32_t kpad, int8_t *G, uint8_t *status, uint32_t *isvar,
+                           void *info, unsigned long long *counters, hipStream_t s);
+hipError_t launch_ph_compact(const uint32_t *isvar, const uint64_t *vnum, const uint64_t *n_lines_dev,
+                             uint64_t n_lines_host, uint64_t *vline, uint64_t *n_var, hipStream_t s);
+hipError_t launch_ph_pairs(const char *buf, const uint64_t *vline, const uint64_t *n_var_dev, uint64_t n_var_host,
+                           const void *info, const int8_t *G, uint32_t kpad, double thr, uint8_t *flags, uint64_t *len,
+                           double *r2, hipStream_t s);
+hipError_t launch_ph_fmt(const char *buf, const uint64_t *vline, const uint64_t *n_var_dev, uint64_t n_var_host,
+                         const void *info, const uint64_t *off, char *out, hipStream_t s);
 // text_cap: rows whose end passes it are not written (the caller checks the total)
 hipError_t launch_af_format(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                             uint64_t n_lines_host, int mode, const int32_t *alt, const int32_t *tot,

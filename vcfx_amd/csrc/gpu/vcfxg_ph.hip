@@ -1,0 +1,335 @@
+// vcfxg_ph.hip -- VCFX_haplotype_phaser's per-record parse and consecutive-variant LD (SURVEY
+// 8(f) rank 3: LD reuse in block phasing).
+//
+// The phaser groups variants into blocks by r^2 between a variant and the last variant of the
+// current block, which is always the variant before it (groupVariants, VCFX_haplotype_phaser.cpp
+// :1275-1322, and the streaming loops :757-965 / :1086-1259): so the device computes, for every
+// parsed variant v > 0, calculateLDFast (:366-470) of the pair (v - 1, v) and the decision the
+// reference takes on it (r^2 >= threshold, and r > 0 on chromosome "1"), plus whether the two
+// share CHROM.  The host assembles the block lines from these flags and the variants' entry
+// texts "idx:(chrom:pos)" formatted here.
+//
+//   k_ph_lines  wave per line: the line rules of both input modes (status), POS, the FORMAT's
+//               GT index and one genotype code per sample (parseGenotypeFast :312-357: the
+//               allele sum as int8, -1 missing) into row `line` of G (kpad bytes per row): the
+//               fixed-stride sweep (gt_fast) for GT-only records, else a lane per sample start;
+//   k_ph_pairs  wave per variant: the pair sums over min(ns) samples (valid = both >= 0), the
+//               reference's fp64 sequence in correctly rounded operations, the decision, the
+//               CHROM compare and the entry length;
+//   k_ph_fmt    the entries at their scanned offsets.
+#include "vcfxg_device.h"
+#include "vcfxg_gt.h"
+#include "vcfxg_kernels.h"
+
+namespace vcfxg {
+
+constexpr int kPhThreads = 256;
+constexpr int kPhWaves = kPhThreads / kWave;
+
+// parseGenotypeFast on [g, g + n)
+__device__ __forceinline__ int ph_gt(const char *__restrict__ buf, int64_t g, int64_t n) {
+    if (n <= 0) return -1;
+    if (n == 3) {
+        const uint32_t c0 = byte_at(buf, g), c1 = byte_at(buf, g + 1), c2 = byte_at(buf, g + 2);
+        if (c1 == '/' || c1 == '|') {
+            if (c0 == '.' || c2 == '.') return -1;
+            if (c0 - '0' < 10u && c2 - '0' < 10u) return (int)(int8_t)((c0 - '0') + (c2 - '0'));
+        }
+    }
+    int64_t k = 0;
+    while (k < n && byte_at(buf, g + k) != '/' && byte_at(buf, g + k) != '|') k++;
+    if (k == n) return -1;
+    const int64_t n1 = k, n2 = n - k - 1;
+    if (!n1 || !n2 || byte_at(buf, g) == '.' || byte_at(buf, g + k + 1) == '.') return -1;
+    uint32_t i1 = 0, i2 = 0;
+    for (int64_t j = 0; j < n1; j++) {
+        const uint32_t c = byte_at(buf, g + j);
+        if (c - '0' >= 10u) return -1;
+        i1 = i1 * 10u + (c - '0');
+    }
+    for (int64_t j = 0; j < n2; j++) {
+        const uint32_t c = byte_at(buf, g + k + 1 + j);
+        if (c - '0' >= 10u) return -1;
+        i2 = i2 * 10u + (c - '0');
+    }
+    return (int)(int8_t)(i1 + i2);
+}
+
+// the sample at st (ends at the next tab or E): its gi-th ':' sub-field (extractNthField)
+__device__ __forceinline__ int ph_sample(const char *__restrict__ buf, int64_t st, int64_t E, int gi) {
+    int cur = 0;
+    int64_t fs = st;
+    for (int64_t q = st;; q++) {
+        const uint32_t c = q < E ? byte_at(buf, q) : (uint32_t)'\t';
+        if (c == '\t' || c == ':') {
+            if (cur == gi) return ph_gt(buf, fs, q - fs);
+            if (c == '\t') return -1;
+            cur++;
+            fs = q + 1;
+        }
+    }
+}
+
+// fixed-stride reducer: the code of every sample into its row
+struct PhOp {
+    int8_t *row;
+    int64_t S;
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() const { return false; }
+    __device__ void dword(const DwordView &v) {
+        if (!v.real) return;
+        const uint32_t a = v.f & 0xFFu, b = (v.f >> 16) & 0xFFu;
+        row[(v.p - S) >> 2] = (int8_t)(v.dig == 0x01000100u ? (int)(a + b) : -1);
+    }
+    __device__ void finish() {}
+};
+
+struct PhLine {
+    uint64_t chrom;  // CHROM start
+    uint32_t clen;   // CHROM bytes
+    int32_t pos;
+    uint32_t ns;     // samples (fields after the 9th)
+    uint32_t pad;
+};
+
+__global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict__ buf, int64_t data_start,
+                                                         const uint64_t *__restrict__ line_end,
+                                                         const uint64_t *n_lines_p, int mode, uint32_t kpad,
+                                                         int8_t *__restrict__ G, uint8_t *__restrict__ status,
+                                                         uint32_t *__restrict__ isvar, PhLine *__restrict__ info,
+                                                         unsigned long long *__restrict__ counters) {
+    __shared__ int64_t scratch[kPhWaves][16];
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    const uint64_t n_lines = *n_lines_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t li = wid; li < n_lines; li += nw) {
+        const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
+        uint8_t st = kPhSkip;
+        PhLine m{};
+        if (!(mode == 1 && le == ls)) {  // stdin: an empty line before the '\r' strip
+            int64_t ae = le;
+            if (ae > ls && byte_at(buf, ae - 1) == '\r') ae--;
+            if (ae == ls) st = mode == 0 ? kPhSkip : kPhFew;  // (stdin: a lone '\r' is a 1-field line)
+            else if (byte_at(buf, ls) == '#') st = kPhHeader;
+            else {
+                int64_t t[9];
+                const int nt = head_tabs(buf, ls, ae, 9, t, lds);
+                if (nt < 9) st = kPhFew;
+                else {
+                    // POS: every byte a digit (an empty POS is 0), int accumulation
+                    bool ok = true;
+                    uint32_t pos = 0;
+                    for (int64_t q = t[0] + 1; q < t[1]; q++) {
+                        const uint32_t c = byte_at(buf, q);
+                        if (c - '0' >= 10u) {
+                            ok = false;
+                            break;
+                        }
+                        pos = pos * 10u + (c - '0');
+                    }
+                    const int gi = ok ? gt_index(buf, t[7] + 1, t[8]) : -1;
+                    if (!ok) st = kPhPos;
+                    else if (gi < 0) st = kPhNoGt;
+                    else {
+                        st = kPhVar;
+                        m.chrom = (uint64_t)ls;
+                        m.clen = (uint32_t)(t[0] - ls);
+                        m.pos = (int32_t)pos;
+                        const int64_t S = t[8] + 1;
+                        int8_t *row = G + li * (uint64_t)kpad;
+                        const int64_t L = ae - S;
+                        PhOp op{row, S};
+                        if (gi == 0 && L >= 3 && ((L + 1) & 3) == 0 && (uint64_t)((L + 1) / 4) <= kpad &&
+                            gt_fast(buf, S, ae, op))
+                            m.ns = (uint32_t)((L + 1) / 4);
+                        else {
+                            // a lane per sample start; sample k = its rank among the starts
+                            uint32_t cnt = 0;
+                            for (int64_t w = S & ~(int64_t)15; w <= ae; w += kWaveStep) {
+                                const int64_t blk = w + (int64_t)lane() * kBlockBytes;
+                                uint32_t starts = 0;
+                                if (blk <= ae) {
+                                    const uint32_t tm = eq_mask16(load16(buf, blk), kRepTab);
+                                    starts = (tm << 1) & 0xFFFFu;
+                                    if (blk > 0 && byte_at(buf, blk - 1) == '\t') starts |= 1u;
+                                    starts &= range_mask16(blk, S + 1, ae + 1);  // (a trailing tab: a sample at ae)
+                                    if (S >= blk && S < blk + 16) starts |= 1u << (S - blk);
+                                }
+                                const uint32_t c = (uint32_t)__popc(starts);
+                                const uint32_t incl = wave_incl_scan(c);
+                                uint32_t k = cnt + incl - c;
+                                while (starts) {
+                                    const int j = __builtin_ctz(starts);
+                                    starts &= starts - 1u;
+                                    if (k < kpad) row[k] = (int8_t)ph_sample(buf, blk + j, ae, gi);
+                                    k++;
+                                }
+                                cnt += wave_bcast(incl, kWave - 1);
+                            }
+                            m.ns = cnt;
+                            if (cnt > kpad && lane() == 0) atomicMax(&counters[3], (unsigned long long)cnt);
+                        }
+                    }
+                }
+            }
+        }
+        if (lane() == 0) {
+            status[li] = st;
+            isvar[li] = st == kPhVar;
+            info[li] = m;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t ph_digits(uint64_t v) {
+    uint32_t d = 1;
+    while (v >= 10) {
+        v /= 10;
+        d++;
+    }
+    return d;
+}
+__device__ __forceinline__ uint32_t ph_int_len(int64_t v) { return v < 0 ? 1u + ph_digits((uint64_t)-v) : ph_digits((uint64_t)v); }
+
+// per variant v: vline[v] = its line.  flags: bit 0 the pair (v - 1, v) passes the block rule,
+// bit 1 the two share CHROM.  len: bytes of the entry "v:(chrom:pos)".
+__global__ __launch_bounds__(kPhThreads) void k_ph_pairs(const char *__restrict__ buf, const uint64_t *__restrict__ vline,
+                                                         const uint64_t *n_var_p, const PhLine *__restrict__ info,
+                                                         const int8_t *__restrict__ G, uint32_t kpad, double thr,
+                                                         uint8_t *__restrict__ flags, uint64_t *__restrict__ len,
+                                                         double *__restrict__ r2_out) {
+    const uint64_t nv = *n_var_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t v = wid; v < nv; v += nw) {
+        const PhLine b = info[vline[v]];
+        uint8_t f = 0;
+        double r2v = 0.0;
+        if (v > 0) {
+            const PhLine a = info[vline[v - 1]];
+            const int8_t *ga = G + vline[v - 1] * (uint64_t)kpad, *gb = G + vline[v] * (uint64_t)kpad;
+            const uint32_t n = min(a.ns, b.ns);
+            int32_t vn = 0, sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;  // (int8 codes: no overflow below 2^31 / 127^2 samples per lane)
+            for (uint32_t k = lane(); k < n; k += kWave) {
+                const int x = ga[k], y = gb[k];
+                if (x < 0 || y < 0) continue;
+                vn++;
+                sx += x;
+                sy += y;
+                sxy += x * y;
+                sx2 += x * x;
+                sy2 += y * y;
+            }
+            const int64_t N = wave_sum((int64_t)vn), SX = wave_sum((int64_t)sx), SY = wave_sum((int64_t)sy),
+                          SXY = wave_sum((int64_t)sxy), SX2 = wave_sum((int64_t)sx2), SY2 = wave_sum((int64_t)sy2);
+            double r = 0.0;
+            if (N > 0) {
+                const double dn = (double)N;
+                const double mx = __ddiv_rn((double)SX, dn), my = __ddiv_rn((double)SY, dn);
+                const double cov = __dsub_rn(__ddiv_rn((double)SXY, dn), __dmul_rn(mx, my));
+                const double vx = __dsub_rn(__ddiv_rn((double)SX2, dn), __dmul_rn(mx, mx));
+                const double vy = __dsub_rn(__ddiv_rn((double)SY2, dn), __dmul_rn(my, my));
+                if (vx > 0.0 && vy > 0.0) {
+                    r = __ddiv_rn(cov, __dmul_rn(__dsqrt_rn(vx), __dsqrt_rn(vy)));
+                    r2v = __dmul_rn(r, r);
+                }
+            }
+            const bool one = b.clen == 1 && byte_at(buf, (int64_t)b.chrom) == '1';
+            const bool pass = one ? (r2v >= thr && r > 0.0) : (r2v >= thr);
+            bool same = a.clen == b.clen;
+            for (uint32_t k = 0; same && k < a.clen; k++) same = buf[a.chrom + k] == buf[b.chrom + k];
+            f = (uint8_t)((pass ? 1u : 0u) | (same ? 2u : 0u));
+        }
+        if (lane() == 0) {
+            flags[v] = f;
+            r2_out[v] = r2v;
+            len[v] = ph_digits(v) + 2u + b.clen + 1u + ph_int_len(b.pos) + 1u;
+        }
+    }
+}
+
+__device__ __forceinline__ void ph_put_int(char *o, int64_t v, uint32_t nb) {
+    uint64_t x = v < 0 ? (uint64_t)-v : (uint64_t)v;
+    if (v < 0) o[0] = '-';
+    for (uint32_t k = nb; k-- > (v < 0 ? 1u : 0u);) {
+        o[k] = (char)('0' + x % 10);
+        x /= 10;
+    }
+}
+
+__global__ __launch_bounds__(kPhThreads) void k_ph_fmt(const char *__restrict__ buf, const uint64_t *__restrict__ vline,
+                                                       const uint64_t *n_var_p, const PhLine *__restrict__ info,
+                                                       const uint64_t *__restrict__ off, char *__restrict__ out) {
+    const uint64_t nv = *n_var_p;
+    for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < nv; v += gridDim.x * (uint64_t)blockDim.x) {
+        const PhLine b = info[vline[v]];
+        char *o = out + off[v];
+        uint32_t nb = ph_digits(v);
+        ph_put_int(o, (int64_t)v, nb);
+        o += nb;
+        *o++ = ':';
+        *o++ = '(';
+        for (uint32_t k = 0; k < b.clen; k++) *o++ = buf[b.chrom + k];
+        *o++ = ':';
+        nb = ph_int_len(b.pos);
+        ph_put_int(o, b.pos, nb);
+        o += nb;
+        *o = ')';
+    }
+}
+
+// variant number -> line (the lines with isvar set, in order)
+__global__ void k_ph_compact(const uint32_t *__restrict__ isvar, const uint64_t *__restrict__ vnum,
+                             const uint64_t *n_lines_p, uint64_t *__restrict__ vline, uint64_t *__restrict__ n_var) {
+    const uint64_t n = *n_lines_p;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += gridDim.x * (uint64_t)blockDim.x) {
+        if (isvar[i]) vline[vnum[i]] = i;
+        if (i == n - 1) *n_var = vnum[i] + isvar[i];
+    }
+}
+
+size_t ph_line_bytes() { return sizeof(PhLine); }
+
+hipError_t launch_ph_lines(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
+                           uint64_t n_lines_host, int mode, uint32_t kpad, int8_t *G, uint8_t *status, uint32_t *isvar,
+                           void *info, unsigned long long *counters, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    int64_t g = ((int64_t)n_lines_host + kPhWaves - 1) / kPhWaves;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_ph_lines, dim3((unsigned)g), dim3(kPhThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                       mode, kpad, G, status, isvar, static_cast<PhLine *>(info), counters);
+    return hipGetLastError();
+}
+
+hipError_t launch_ph_compact(const uint32_t *isvar, const uint64_t *vnum, const uint64_t *n_lines_dev,
+                             uint64_t n_lines_host, uint64_t *vline, uint64_t *n_var, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    int64_t g = ((int64_t)n_lines_host + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_ph_compact, dim3((unsigned)g), dim3(256), 0, s, isvar, vnum, n_lines_dev, vline, n_var);
+    return hipGetLastError();
+}
+
+hipError_t launch_ph_pairs(const char *buf, const uint64_t *vline, const uint64_t *n_var_dev, uint64_t n_var_host,
+                           const void *info, const int8_t *G, uint32_t kpad, double thr, uint8_t *flags, uint64_t *len,
+                           double *r2, hipStream_t s) {
+    if (!n_var_host) return hipSuccess;
+    int64_t g = ((int64_t)n_var_host + kPhWaves - 1) / kPhWaves;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_ph_pairs, dim3((unsigned)g), dim3(kPhThreads), 0, s, buf, vline, n_var_dev,
+                       static_cast<const PhLine *>(info), G, kpad, thr, flags, len, r2);
+    return hipGetLastError();
+}
+
+hipError_t launch_ph_fmt(const char *buf, const uint64_t *vline, const uint64_t *n_var_dev, uint64_t n_var_host,
+                         const void *info, const uint64_t *off, char *out, hipStream_t s) {
+    if (!n_var_host) return hipSuccess;
+    int64_t g = ((int64_t)n_var_host + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_ph_fmt, dim3((unsigned)g), dim3(256), 0, s, buf, vline, n_var_dev,
+                       static_cast<const PhLine *>(info), off, out);
+    return hipGetLastError();
+}
+
+}  // namespace vcfxg

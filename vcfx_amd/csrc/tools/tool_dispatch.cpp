@@ -16,5 +16,6 @@ extern "C" int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd
     if (!strcmp(t, "VCFX_dosage_calculator")) return vcfx_tool_dosage_calculator(argc, argv, in_fd, out_fd, err_fd);
     if (!strcmp(t, "VCFX_missing_detector")) return vcfx_tool_missing_detector(argc, argv, in_fd, out_fd, err_fd);
     if (!strcmp(t, "VCFX_allele_counter")) return vcfx_tool_allele_counter(argc, argv, in_fd, out_fd, err_fd);
+    if (!strcmp(t, "VCFX_haplotype_phaser")) return vcfx_tool_haplotype_phaser(argc, argv, in_fd, out_fd, err_fd);
     return -100;
 }

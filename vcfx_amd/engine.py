@@ -17,6 +17,11 @@ class Summary(ctypes.Structure):
                 ("general_records", ctypes.c_uint64)]
 
 
+class AcParams(ctypes.Structure):
+    _fields_ = [("sample", ctypes.c_void_p), ("m", ctypes.c_uint64), ("names", ctypes.c_char_p),
+                ("name_off", ctypes.c_void_p), ("seq", ctypes.c_int), ("kind", ctypes.c_int)]
+
+
 class Criterion(ctypes.Structure):
     _fields_ = [("target", ctypes.c_int), ("op", ctypes.c_int), ("numeric", ctypes.c_int), ("value", ctypes.c_double),
                 ("key", ctypes.c_char_p), ("key_len", ctypes.c_size_t), ("str", ctypes.c_char_p),
@@ -65,6 +70,8 @@ SIGNATURES = {
     "vcfxg_missing_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_allele_counter": (_I, [_VP, _U64, _U64, _VP, ctypes.POINTER(Summary)]),
     "vcfxg_fetch_text_range": (_I, [_VP, _U64, _S, _VP]),
+    "vcfxg_haplotype_phaser": (_I, [_VP, _S, _I, ctypes.c_double, ctypes.c_uint32, ctypes.POINTER(Summary)]),
+    "vcfxg_phaser_variants": (_I, [_VP, _VP, _VP, _VP]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_prefixes": (_I, [_VP, _VP, _S, _VP]),
     "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
@@ -220,6 +227,43 @@ class Engine:
         s = Summary()
         self._chk(self.L.vcfxg_missing_region(self.h, data_start, int(mode), ctypes.byref(s)), "missing_region")
         return s
+
+    def allele_counter(self, l0, l1, samples, names, seq=0, kind=0):
+        """VCFX_allele_counter rows of indexed lines [l0, l1) for the output slots (sample index,
+        name) (vcfxg_allele_counter); seq 0 = the file path's every-slot semantics, 1 = the
+        forward cursor; kind 0 text, 1 aggregate, 2 binary"""
+        import numpy as np
+        idx = np.ascontiguousarray(samples, np.uint32)
+        nb = [x.encode() if isinstance(x, str) else bytes(x) for x in names]
+        assert len(nb) == len(idx)
+        off = np.zeros(len(nb) + 1, np.uint64)
+        off[1:] = np.cumsum([len(x) for x in nb])
+        p = AcParams(idx.ctypes.data, len(idx), b"".join(nb), off.ctypes.data, int(seq), int(kind))
+        s = Summary()
+        self._chk(self.L.vcfxg_allele_counter(self.h, l0, l1, ctypes.byref(p), ctypes.byref(s)), "allele_counter")
+        return s
+
+    def haplotype_phaser(self, data_start, mode, threshold, n_samples):
+        """VCFX_haplotype_phaser's parse + consecutive-variant LD (vcfxg_haplotype_phaser)"""
+        s = Summary()
+        self._chk(self.L.vcfxg_haplotype_phaser(self.h, data_start, int(mode), float(threshold), int(n_samples),
+                                                ctypes.byref(s)), "haplotype_phaser")
+        return s
+
+    def phaser_variants(self, n_var):
+        """(flags, r2, entry offsets) of the last haplotype_phaser call"""
+        import numpy as np
+        f = np.zeros(max(n_var, 1), np.uint8)
+        r2 = np.zeros(max(n_var, 1), np.float64)
+        off = np.zeros(n_var + 1, np.uint64)
+        self._chk(self.L.vcfxg_phaser_variants(self.h, f.ctypes.data, r2.ctypes.data, off.ctypes.data),
+                  "phaser_variants")
+        return f[:n_var], r2[:n_var], off
+
+    def text_range(self, offset, n):
+        b = ctypes.create_string_buffer(max(1, n))
+        self._chk(self.L.vcfxg_fetch_text_range(self.h, offset, n, b), "fetch_text_range")
+        return b.raw[:n]
 
     def hwe_rechecks(self):
         """the last hwe_region's rows left to the host: [(text_offset, hom_ref, het, hom_alt)]"""
