@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=("af", "pipeline", "ld", "nonref", "hwe", "dose", "ac", "md"), default="af")
+    ap.add_argument("--workload", choices=("af", "pipeline", "ld", "nonref", "hwe", "dose", "ac", "md", "ph"), default="af")
     ap.add_argument("--records", type=int, default=None, help="records per GPU (default per workload)")
     ap.add_argument("--samples", type=int, default=2504)
     ap.add_argument("--window", type=int, default=100000, help="ld: window in variants")
@@ -143,6 +143,9 @@ def cpu_baseline(workload, arr, offs, a):
         elif workload == "md":
             argvs = [["VCFX_missing_detector", "-q", "-i", f.name]]
             desc = "VCFX_missing_detector -q -i (file path)"
+        elif workload == "ph":
+            argvs = [["VCFX_haplotype_phaser", "-q", "-i", f.name]]
+            desc = "VCFX_haplotype_phaser -q -i (file path, default mode, threshold 0.8)"
         elif workload == "pipeline":
             argvs = [["VCFX_record_filter", "--filter", "QUAL>=30;FILTER==PASS", "-i", f.name],
                      ["VCFX_genotype_query", "--genotype-query", "0|1"]]
@@ -163,6 +166,32 @@ def cpu_baseline(workload, arr, offs, a):
                       % (nvar, len(sample) / 1e6, desc, reps, t)}
 
 
+def _ph_blocks_sha(arr, flags, off, text):
+    """sha256 of the phaser's default-mode output: the '#' lines, then the block lines assembled
+    from the per-variant flags (bit 0 pair passes, bit 1 same CHROM) and the entries"""
+    import hashlib
+    h = hashlib.sha256()
+    head = arr[:1 << 20].tobytes()
+    for line in head.split(b"\n"):
+        if not line.startswith(b"#"):
+            break
+        h.update(line.rstrip(b"\r") + b"\n")
+    h.update(b"#HAPLOTYPE_BLOCKS_START\n")
+    parts, blk = [], 0
+    for v in range(len(flags)):
+        if v == 0 or (flags[v] & 3) != 3:
+            if v:
+                parts.append(b"\n")
+            blk += 1
+            parts.append(b"Block %d: " % blk)
+        else:
+            parts.append(b", ")
+        parts.append(text[int(off[v]):int(off[v + 1])])
+    h.update(b"".join(parts))
+    h.update(b"\n#HAPLOTYPE_BLOCKS_END\n")
+    return h.hexdigest()
+
+
 def output_check(workload, eng, s, a, rank, arr=None):
     """The last timed step's output against the REFERENCE's, on rank 0 at the BASELINE sizes:
     the digests tests/golden/full_digests.json holds for this exact synthetic input (made by
@@ -177,7 +206,7 @@ def output_check(workload, eng, s, a, rank, arr=None):
     except OSError:
         return {"checked": False, "why": "no tests/golden/full_digests.json"}
     default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "hwe": 427409, "dose": 427409, "ac": 427409,
-               "md": 427409, "ld": 100000}[workload]
+               "md": 427409, "ph": 427409, "ld": 100000}[workload]
     if a.format != "gt" or a.missing_rate > 0 or a.irregular_rate > 0:
         return {"checked": False, "why": "no reference digest for the general-path data"}
     if rank != 0 or a.records != default or a.samples != 2504 or (workload == "ld" and (a.window < 3000 or
@@ -216,6 +245,15 @@ def output_check(workload, eng, s, a, rank, arr=None):
             got = hashlib.sha256(arr).hexdigest()
         want, what = c["stdout"]["sha256"], ("no record flagged and no '.' in any sample column, so the output is "
                                              "the input: its sha256 vs VCFX_missing_detector -q -i (reference)")
+    elif workload == "ph":
+        c = dig["cases"].get("ph_file")
+        if c is None:
+            return {"checked": False, "why": "no ph_file digest"}
+        # the block lines from the device's pair decisions and entries (the tool's assembly)
+        flags, _, off = eng.phaser_variants(s.rows)
+        text = eng.text(s.text_bytes)
+        got = _ph_blocks_sha(arr, flags, off, text)
+        want, what = c["stdout"]["sha256"], "sha256 of the header + block lines vs VCFX_haplotype_phaser -q -i (reference)"
     elif workload == "hwe":
         if "hwe_file" not in dig["cases"]:
             return {"checked": False, "why": "no hwe_file digest"}
@@ -265,6 +303,8 @@ def e2e_rates(workload, arr, a):
         tool, args = "VCFX_dosage_calculator", ["-q"]
     elif workload == "md":
         tool, args = "VCFX_missing_detector", ["-q"]
+    elif workload == "ph":
+        tool, args = "VCFX_haplotype_phaser", ["-q"]
     elif workload == "pipeline":
         tool, args = "VCFX_record_filter", ["--filter", "QUAL>=30;FILTER==PASS"]
     else:
@@ -414,6 +454,13 @@ def main():
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.general_records])
             return s
         kern_names = ("line_count", "line_emit", "line_compact", "md_lines")
+    elif a.workload == "ph":
+        def step():
+            s = eng.haplotype_phaser(ds, engine.MODE_FILE, 0.8, a.samples)  # parse + consecutive-variant LD
+            if red is not None:
+                allreduce_counts([s.n_lines, s.rows, s.text_bytes, 0])
+            return s
+        kern_names = ("line_count", "line_emit", "line_compact", "ph_lines", "ph_pairs", "ph_fmt")
     elif a.workload == "pipeline":
         crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
 
@@ -474,7 +521,7 @@ def main():
         unit, metric = "r2-pairs/s", "r2-pairs/sec (and MFMA TOP/s vs peak), %dK var window x %d samp" % (
             a.records // 1000, a.samples)
     else:
-        assert s.rows > 0 and s.n_lines == a.records, (s.rows, s.n_lines)
+        assert (s.rows > 0 or a.workload == "md") and s.n_lines == a.records, (s.rows, s.n_lines)
         if a.workload == "af" and not general:
             assert s.rows == a.records and s.general_records == 0
         if a.workload == "hwe" and not general:
@@ -523,6 +570,10 @@ def main():
                 "ac_fmt": region_bytes + tb + L * (8 + 1 + 8 + 48),
                 # missing detector: the records once + line end, status and the INFO span per line
                 "md_lines": region_bytes + L * (8 + 1 + 8),
+                # phaser: the records once + a genotype code per sample + line end, status, flag
+                # and the per-line record (24 B); the pairs read each code row twice
+                "ph_lines": region_bytes + L * (a.samples + 8 + 1 + 4 + 24),
+                "ph_pairs": L * (2 * a.samples + 2 * 8 + 2 * 24 + 1 + 8 + 8),
                 "walk_compact": L * 2 * (8 + 13 + 16),
                 # the per-line rest: its lines' record bytes when the data are off the fixed-stride
                 # layout (every line a GT:AD:DP record), else the head record + status per line
@@ -564,6 +615,8 @@ def main():
             "ac": "VCFX_allele_counter -i (file path, per-sample text rows) on a device-resident %d x %d shard per "
                   "GPU: index + per-(record, sample) REF/ALT counts + %d rows per record" % (a.records, a.samples,
                                                                                             a.samples),
+            "ph": "VCFX_haplotype_phaser -i (file path, default mode, -l 0.8) on a device-resident %d x %d shard "
+                  "per GPU: parse to genotype codes + consecutive-variant r^2 + entries" % (a.records, a.samples),
             "md": "VCFX_missing_detector -i (file path) on a device-resident %d x %d shard per GPU: index + the "
                   "per-record missing-genotype test" % (a.records, a.samples),
             "ld": "VCFX_ld_calculator -w %d -t %g streaming on a device-resident %d x %d shard per GPU: parse + "

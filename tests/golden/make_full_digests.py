@@ -54,7 +54,7 @@ INPUTS = {
 AF, RF, GQ, LD, NR, HWE = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query",
                            "VCFX_ld_calculator", "VCFX_nonref_filter", "VCFX_hwe_tester")
 DOSE = "VCFX_dosage_calculator"
-AC, MD = "VCFX_allele_counter", "VCFX_missing_detector"
+AC, MD, PH = "VCFX_allele_counter", "VCFX_missing_detector", "VCFX_haplotype_phaser"
 # 50 sample names of the synthetic header (S00001..S02504) in a scrambled order: the MT path's
 # per-slot lookup and the stream path's forward-only cursor differ on it
 SEL50 = " ".join("S%05d" % (1 + (k * 1597) % 2504) for k in range(50))
@@ -86,6 +86,9 @@ CASES = {
     "md_file": ("chr21", [[MD, "-q", "-i", "{F}"]], False),
     "md_file_miss": ("chr21_miss", [[MD, "-q", "-i", "{F}"]], False),
     "md_stdin_miss": ("chr21_miss", [[MD]], False),
+    "ph_file": ("chr21", [[PH, "-q", "-i", "{F}"]], False),
+    "ph_stream_stdin": ("chr21", [[PH, "-q", "-s", "-w", "50", "-l", "0.5"]], False),
+    "ph_ld3000": ("ld3000", [[PH, "-l", "0.3", "-i", "{F}"]], False),
     "ld3000_bench": ("ld3000", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
 }
 

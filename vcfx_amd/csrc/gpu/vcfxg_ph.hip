@@ -211,15 +211,23 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_pairs(const char *__restrict_
             const int8_t *ga = G + vline[v - 1] * (uint64_t)kpad, *gb = G + vline[v] * (uint64_t)kpad;
             const uint32_t n = min(a.ns, b.ns);
             int32_t vn = 0, sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;  // (int8 codes: no overflow below 2^31 / 127^2 samples per lane)
-            for (uint32_t k = lane(); k < n; k += kWave) {
-                const int x = ga[k], y = gb[k];
-                if (x < 0 || y < 0) continue;
-                vn++;
-                sx += x;
-                sy += y;
-                sxy += x * y;
-                sx2 += x * x;
-                sy2 += y * y;
+            // 16 codes per lane per load (rows are 16-byte aligned; bytes past n are masked)
+            for (uint32_t k0 = 16u * lane(); k0 < n; k0 += 16u * kWave) {
+                const uint4 va = *reinterpret_cast<const uint4 *>(ga + k0);
+                const uint4 vb = *reinterpret_cast<const uint4 *>(gb + k0);
+                const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+                for (int j = 0; j < 16; j++) {
+                    const int x = (int)(int8_t)(wa[j >> 2] >> (8 * (j & 3)));
+                    const int y = (int)(int8_t)(wb[j >> 2] >> (8 * (j & 3)));
+                    if (k0 + j >= n || x < 0 || y < 0) continue;
+                    vn++;
+                    sx += x;
+                    sy += y;
+                    sxy += x * y;
+                    sx2 += x * x;
+                    sy2 += y * y;
+                }
             }
             const int64_t N = wave_sum((int64_t)vn), SX = wave_sum((int64_t)sx), SY = wave_sum((int64_t)sy),
                           SXY = wave_sum((int64_t)sxy), SX2 = wave_sum((int64_t)sx2), SY2 = wave_sum((int64_t)sy2);
