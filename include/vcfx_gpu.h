@@ -342,6 +342,14 @@ int vcfxg_selftest_mfma_i8(vcfxg_ctx *ctx, int *mismatches);
 /* checks the FP4 (e2m1, block-scaled) MFMA operand layout of the fast LD kernel */
 int vcfxg_selftest_mfma_fp4(vcfxg_ctx *ctx, int *mismatches);
 
+/* ---- multi-GPU shard plan (host-only, needs no device) ---------------
+ * world + 1 cut offsets over the data region [lo, n) of `data`: cut i is lo + i*(n - lo)/world
+ * advanced to the first line start at or after it (the reference's own split,
+ * VCFX_allele_counter.cpp:889-901); shard i = [cuts[i], cuts[i+1]) holds whole records.  The
+ * multi-GPU runner (vcfx_amd/shard.py, one process per GPU over torch.distributed / RCCL) hands
+ * each rank its shard as a zero-copy view (VCFX_INPUT_VIEW). */
+int vcfxg_shard_cuts(const char *data, size_t n, size_t lo, int world, uint64_t *cuts);
+
 /* device-formatted output text (without the column header line) */
 int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);
 /* bytes [offset, offset + n) of that text (outputs larger than one host buffer) */

@@ -2052,6 +2052,22 @@ int vcfxg_fetch_text(vcfxg_ctx *c, char *host, size_t cap) {
     return VCFXG_OK;
 }
 
+int vcfxg_shard_cuts(const char *data, size_t n, size_t lo, int world, uint64_t *cuts) {
+    if ((!data && n) || world < 1 || !cuts || lo > n) return VCFXG_E_ARG;
+    cuts[0] = lo;
+    for (int i = 1; i < world; i++) {
+        size_t p = lo + (size_t)((unsigned __int128)(n - lo) * (unsigned)i / (unsigned)world);
+        if (p < cuts[i - 1]) p = cuts[i - 1];
+        if (p > lo && p < n && data[p - 1] != '\n') {
+            const void *nl = memchr(data + p, '\n', n - p);
+            p = nl ? (size_t)((const char *)nl - data) + 1 : n;
+        }
+        cuts[i] = p < n ? p : n;
+    }
+    cuts[world] = n;
+    return VCFXG_OK;
+}
+
 int vcfxg_fetch_text_range(vcfxg_ctx *c, uint64_t offset, size_t n, void *host) {
     if (!c || (!host && n)) return VCFXG_E_ARG;
     if (offset > c->text_bytes || n > c->text_bytes - offset) return VCFXG_E_ARG;

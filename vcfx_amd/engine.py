@@ -70,6 +70,7 @@ SIGNATURES = {
     "vcfxg_missing_region": (_I, [_VP, _S, _I, ctypes.POINTER(Summary)]),
     "vcfxg_allele_counter": (_I, [_VP, _U64, _U64, _VP, ctypes.POINTER(Summary)]),
     "vcfxg_fetch_text_range": (_I, [_VP, _U64, _S, _VP]),
+    "vcfxg_shard_cuts": (_I, [_VP, _S, _S, _I, _VP]),
     "vcfxg_haplotype_phaser": (_I, [_VP, _S, _I, ctypes.c_double, ctypes.c_uint32, ctypes.POINTER(Summary)]),
     "vcfxg_phaser_variants": (_I, [_VP, _VP, _VP, _VP]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
@@ -377,6 +378,17 @@ class Engine:
         out = np.zeros(n, np.uint64)
         self._chk(self.L.vcfxg_line_ends(self.h, 0, n, out.ctypes.data), "line_ends")
         return out
+
+
+def shard_cuts(buf, lo, world):
+    """vcfxg_shard_cuts: world + 1 record-aligned cut offsets over [lo, len(buf)) (no device)"""
+    import numpy as np
+    arr = np.frombuffer(buf, np.uint8) if not isinstance(buf, np.ndarray) else buf
+    cuts = np.zeros(world + 1, np.uint64)
+    rc = lib().vcfxg_shard_cuts(arr.ctypes.data, arr.size, lo, world, cuts.ctypes.data)
+    if rc != VCFXG_OK:
+        raise EngineError("vcfxg_shard_cuts failed (%d)" % rc)
+    return [int(x) for x in cuts]
 
 
 def data_start_of(buf, strip_cr=True):

@@ -69,7 +69,13 @@ def header_end(buf, strip_cr=True):
 
 def record_cuts(buf, lo, world):
     """world+1 cut offsets over [lo, len(buf)): cut i at lo + i*size/world advanced to the
-    first line start at or after it; shard i = [cuts[i], cuts[i+1])."""
+    first line start at or after it; shard i = [cuts[i], cuts[i+1]).  The engine's C ABI
+    (vcfxg_shard_cuts) computes them; record_cuts_py is the same rule in numpy (its test)."""
+    from . import engine
+    return engine.shard_cuts(buf, lo, world)
+
+
+def record_cuts_py(buf, lo, world):
     arr = np.frombuffer(buf, np.uint8) if not isinstance(buf, np.ndarray) else buf
     n = arr.size
     cuts = [lo]
