@@ -47,7 +47,7 @@ def test_two_rank_shards_match_single_gpu(tmp_path):
              ["VCFX_variant_counter", p1],
              ["VCFX_record_filter", "--filter", "QUAL>=30;FILTER==PASS", "-i", p1],
              ["VCFX_genotype_query", "-g", "0|1", "-i", p1], ["VCFX_genotype_query", "-g", "1|1", "--strict", p1],
-             ["VCFX_nonref_filter", "-i", p1], ["VCFX_nonref_filter", p1],
+             ["VCFX_nonref_filter", "-i", p1], ["VCFX_nonref_filter", p1], ["VCFX_dosage_calculator", "-i", p1],
              ["VCFX_ld_calculator", "-i", p2, "-w", "300", "-t", "0.2"],
              ["VCFX_ld_calculator", "-i", p2, "-w", "5000"],
              ["VCFX_ld_calculator", "-i", p2, "-m", "-r", "21:9411239-9430000"]]

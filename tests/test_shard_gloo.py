@@ -114,7 +114,8 @@ def _cases(files):
                   ["VCFX_allele_freq_calc", p], ["VCFX_variant_counter", p]]
         cases += [["VCFX_record_filter", "--filter", "QUAL>=30;AF>=0.05", "-i", p],
                   ["VCFX_genotype_query", "-g", "0/1", "-i", p], ["VCFX_genotype_query", "-g", "1|1", "--strict", p],
-                  ["VCFX_nonref_filter", "-i", p], ["VCFX_nonref_filter", p]]
+                  ["VCFX_nonref_filter", "-i", p], ["VCFX_nonref_filter", p],
+                  ["VCFX_dosage_calculator", "-i", p], ["VCFX_dosage_calculator", "-q", p]]
     cases.append(["VCFX_variant_counter", "--strict", files["bad"]])
     return cases
 
@@ -136,7 +137,8 @@ def test_sharded_runs_match_whole_file(files, world):
         by_rank = views[tuple(argv)]
         assert set(by_rank) == set(range(world))
         meant = shard.plan(argv) in ("af", "vc", "filter") and not (
-            argv[0] in ("VCFX_record_filter", "VCFX_genotype_query", "VCFX_nonref_filter") and "bad" in argv[-1])
+            argv[0] in ("VCFX_record_filter", "VCFX_genotype_query", "VCFX_nonref_filter", "VCFX_dosage_calculator")
+            and "bad" in argv[-1])
         if not meant:
             continue
         # every rank ran its own view (no silent fallback to an unsharded rank-0 run)

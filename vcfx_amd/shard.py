@@ -15,8 +15,8 @@ the mapping and kept records are written from the mapping.
   all-reduced; warning line numbers are shifted to whole-file numbering (each rank counts its
   own shard's lines only when some rank warned); under --strict the earliest failing line of
   any rank wins.
-* VCFX_record_filter / VCFX_genotype_query / VCFX_nonref_filter with a file input: the
-  records are cut the same way; rank 0's view writes the header part once, ranks > 0 skip it.
+* VCFX_record_filter / VCFX_genotype_query / VCFX_nonref_filter / VCFX_dosage_calculator
+  with a file input: the records are cut the same way; rank 0's view writes the header part once, ranks > 0 skip it.
   Files with data lines before '#CHROM' run unsharded.
 * VCFX_ld_calculator -i FILE (streaming): every rank parses the file and computes the pair
   rows of its `--shard r/N` share (equal window-pair counts); with a window as large as the
@@ -109,6 +109,7 @@ _VALUE_OPTS = {
                            {"--input", "--region", "--window", "--threshold", "--threads", "--max-distance",
                             "--shard"}),
     "VCFX_variant_counter": (set(), set()),
+    "VCFX_dosage_calculator": ({"-i"}, {"--input"}),
 }
 
 
@@ -381,7 +382,7 @@ def run_ld(argv, comm, runner, sink):
 
 
 SHARDED = ("VCFX_allele_freq_calc", "VCFX_variant_counter", "VCFX_ld_calculator", "VCFX_record_filter",
-           "VCFX_genotype_query", "VCFX_nonref_filter")
+           "VCFX_genotype_query", "VCFX_nonref_filter", "VCFX_dosage_calculator")
 
 
 def plan(argv):
