@@ -285,7 +285,7 @@ def output_check(workload, eng, s, a, rank, arr=None):
 PCIE_H2D_GBS = 56.0  # pinned H2D measured on MI355X (tools/microbench/h2d_ingest.cpp; spec Gen5 x16 63 GB/s)
 
 
-def e2e_rates(workload, arr, a):
+def e2e_rates(workload, arr, a, offs=None):
     """End-to-end records/s of the drop-in CLI on this rank's synthetic file: page-cache-warm
     file -> mmap -> H2D -> kernels -> rows -> stdout (/dev/null), wall clock of the whole process
     (HIP runtime start included), best of 3; the same through a pipe (`cat F | tool`, the
@@ -359,6 +359,28 @@ def e2e_rates(workload, arr, a):
                                          "note": "BGZF level 1 (build/bin/vcfx_bgzf); inflate on <= 16 host threads"}
         finally:
             os.unlink(bgz)
+        # per-invocation start-up: the drop-in process on a small input (the first 100 records),
+        # the reference's own binary on the same bytes beside it (best of 5 each)
+        if offs is not None:
+            small = path + ".small.vcf"
+            arr[:int(offs[min(100, len(offs) - 1)])].tofile(small)
+            try:
+                lat = {}
+                for name, ex in (("drop_in", exe), ("reference", os.path.join(REF_DIR, tool))):
+                    if not os.access(ex, os.X_OK):
+                        continue
+                    walls = []
+                    for _ in range(5):
+                        t0 = time.perf_counter()
+                        r = subprocess.run([ex] + args + ["-i", small], stdout=subprocess.DEVNULL,
+                                           stderr=subprocess.PIPE, timeout=120)
+                        walls.append(time.perf_counter() - t0)
+                        assert r.returncode == 0, r.stderr[-500:]
+                    lat[name + "_s"] = round(min(walls), 4)
+                lat["input"] = "first 100 records (%.1f MB)" % (os.path.getsize(small) / 1e6)
+                runs["small_input_latency"] = lat
+            finally:
+                os.unlink(small)
         runs["pcie_ceiling"] = a.records / (arr.size / (PCIE_H2D_GBS * 1e9))
         runs["unit"] = "records/s"
         runs["cmd"] = "%s %s -i FILE > /dev/null (page-cache-warm %.2f GB file)" % (tool, " ".join(args), arr.size / 1e9)
@@ -649,7 +671,7 @@ def main():
             out["pairs_emitted"] = np_
         out["output_check"] = output_check(a.workload, eng, s, a, rank, arr)
         if world == 1 and not a.no_e2e and not general:
-            out["e2e"] = e2e_rates(a.workload, arr, a)
+            out["e2e"] = e2e_rates(a.workload, arr, a, offs)
         if not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.workload, arr, offs, a)
         print(json.dumps(out), flush=True)

@@ -100,6 +100,8 @@ def _cmd(stages, path):
 
 
 def _check(case, inputs, stdin="none"):
+    if case not in DIG["cases"]:
+        pytest.skip("no reference digest for %s (tests/golden/make_full_digests.py %s)" % (case, case))
     c = DIG["cases"][case]
     path = inputs.path(c["input"])
     cmd = _cmd(c["stages"], path)
