@@ -97,3 +97,15 @@ def test_allele_counter_stream_traps(oracle, k):
     T = "VCFX_allele_counter"
     _check(oracle, [T], STREAM_ONLY[k])
     _check(oracle, [T, "-q", "-s", "A"], STREAM_ONLY[k])
+
+
+def test_allele_counter_selection_in_global_memory(oracle, tmp_path, monkeypatch):
+    """the row writer with the selection read from global memory (too large for LDS)"""
+    monkeypatch.setenv("VCFXG_AC_SEL_GLOBAL", "1")
+    buf = synth.generate(n_records=200, n_samples=700, seed=106)
+    path = tmp_path / "in.vcf"
+    path.write_bytes(buf)
+    T = "VCFX_allele_counter"
+    for argv in ([T, "-q", "-i", str(path)], [T, "-q", "-l", "9", "-i", str(path)]):
+        _check(oracle, argv)
+    _check(oracle, [T, "-q"], buf)

@@ -53,6 +53,7 @@ struct AcArgs {
     uint32_t *scratch;     // per wave: scap sample starts (relative to S)
     uint32_t m, scap;      // slots; sample starts a line needs (max index + 1)
     int seq, kind;
+    uint32_t sel_lds;      // k_ac_fmt: the selection (eff, name offsets, names) copied to LDS (its bytes; 0: read from global memory)
 };
 
 struct AcNullOp {
@@ -284,6 +285,22 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
                                                        char *__restrict__ out) {
     __shared__ __attribute__((aligned(16))) char tile_all[kAcWaves][kAcTile + 16];
     __shared__ char pre_all[kAcWaves][kAcPre];
+    // the selection in LDS when it fits (the text rows read a slot's sample index, name offset and
+    // name bytes for every row: LDS reads instead of chains of dependent global loads)
+    extern __shared__ __attribute__((aligned(16))) char sel_all[];
+    uint32_t *s_eff = reinterpret_cast<uint32_t *>(sel_all), *s_noff = s_eff + A.m;
+    char *s_names = reinterpret_cast<char *>(s_noff + A.m + 1);
+    if (A.sel_lds) {
+        for (uint32_t k = threadIdx.x; k <= A.m; k += blockDim.x) {
+            if (k < A.m) s_eff[k] = A.eff[k];
+            s_noff[k] = (uint32_t)A.noff[k];
+        }
+        for (uint64_t k = threadIdx.x; k < A.noff[A.m]; k += blockDim.x) s_names[k] = A.names[k];
+        __syncthreads();
+    }
+    auto EFF = [&](uint32_t i) -> uint32_t { return A.sel_lds ? s_eff[i] : A.eff[i]; };
+    auto NOFF = [&](uint32_t i) -> uint64_t { return A.sel_lds ? (uint64_t)s_noff[i] : A.noff[i]; };
+    auto NAME = [&](uint64_t k) -> char { return A.sel_lds ? s_names[k] : A.names[k]; };
     char *tile = tile_all[threadIdx.x / kWave];
     char *pre = pre_all[threadIdx.x / kWave];
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
@@ -369,20 +386,23 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint64_t rl = P + 5u;
+        // the first tile's counts; each iteration loads the next tile's before writing its own
+        int rn = 0, an = 0;
+        if ((uint32_t)lane() < m.rows) ac_slot_fast(buf, S, m.ns, EFF(lane()), rn, an);
         for (uint32_t i0 = 0; i0 < m.rows; i0 += kWave) {
             const uint32_t i1 = min(m.rows, i0 + (uint32_t)kWave);
-            const uint64_t g0 = (uint64_t)i0 * rl + A.noff[i0];                // tile start in the line's text
-            const uint64_t B = (uint64_t)(i1 - i0) * rl + A.noff[i1] - A.noff[i0];  // tile bytes
+            const uint64_t g0 = (uint64_t)i0 * rl + NOFF(i0);                // tile start in the line's text
+            const uint64_t B = (uint64_t)(i1 - i0) * rl + NOFF(i1) - NOFF(i0);  // tile bytes
             const uint32_t i = i0 + lane();
-            int r = 0, a = 0;
-            if (i < i1) ac_slot_fast(buf, S, m.ns, A.eff[i], r, a);
+            const int r = rn, a = an;
+            if (i + kWave < m.rows) ac_slot_fast(buf, S, m.ns, EFF(i + kWave), rn, an);
             const uint64_t ga = (uint64_t)(o - out) + g0;  // absolute text offset of the tile
             if (B + 16 > (uint64_t)kAcTile) {             // long names: straight to global memory
                 if (i < i1) {
-                    char *q = o + (uint64_t)i * rl + A.noff[i];
+                    char *q = o + (uint64_t)i * rl + NOFF(i);
                     for (uint32_t k = 0; k < P; k++) q[k] = pre[k];
                     q += P;
-                    for (uint64_t k = A.noff[i]; k < A.noff[i + 1]; k++) *q++ = A.names[k];
+                    for (uint64_t k = NOFF(i); k < NOFF(i + 1); k++) *q++ = NAME(k);
                     q[0] = '\t';
                     q[1] = (char)('0' + r);
                     q[2] = '\t';
@@ -393,10 +413,10 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
             }
             const uint32_t sh = (uint32_t)(ga & 15);  // LDS position = text position mod 16
             if (i < i1) {
-                char *q = tile + sh + ((uint64_t)i * rl + A.noff[i] - g0);
+                char *q = tile + sh + ((uint64_t)i * rl + NOFF(i) - g0);
                 for (uint32_t k = 0; k < P; k++) q[k] = pre[k];
                 q += P;
-                for (uint64_t k = A.noff[i]; k < A.noff[i + 1]; k++) *q++ = A.names[k];
+                for (uint64_t k = NOFF(i), ke = NOFF(i + 1); k < ke; k++) *q++ = NAME(k);
                 q[0] = '\t';
                 q[1] = (char)('0' + r);
                 q[2] = '\t';
@@ -424,7 +444,7 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
 size_t ac_meta_bytes() { return sizeof(AcMeta); }
 
 static AcArgs ac_args(const uint32_t *eff, const uint64_t *noff, const char *names, uint32_t *scratch, uint32_t m,
-                      uint32_t scap, int seq, int kind) {
+                      uint32_t scap, int seq, int kind, uint32_t sel_lds = 0) {
     AcArgs A;
     A.eff = eff;
     A.noff = noff;
@@ -434,6 +454,7 @@ static AcArgs ac_args(const uint32_t *eff, const uint64_t *noff, const char *nam
     A.scap = scap;
     A.seq = seq;
     A.kind = kind;
+    A.sel_lds = sel_lds;
     return A;
 }
 
@@ -450,11 +471,11 @@ hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *li
 
 hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
-                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, const uint8_t *status,
-                         const void *meta, const uint64_t *off, char *out, hipStream_t s) {
+                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint32_t sel_lds,
+                         const uint8_t *status, const void *meta, const uint64_t *off, char *out, hipStream_t s) {
     if (l1 <= l0) return hipSuccess;
-    hipLaunchKernelGGL(k_ac_fmt, dim3(blocks), dim3(kAcThreads), 0, s, buf, data_start, line_end, l0, l1,
-                       ac_args(eff, noff, names, scratch, m, scap, seq, kind), status,
+    hipLaunchKernelGGL(k_ac_fmt, dim3(blocks), dim3(kAcThreads), sel_lds, s, buf, data_start, line_end, l0, l1,
+                       ac_args(eff, noff, names, scratch, m, scap, seq, kind, sel_lds), status,
                        static_cast<const AcMeta *>(meta), off, out);
     return hipGetLastError();
 }

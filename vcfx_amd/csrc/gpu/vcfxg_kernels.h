@@ -161,7 +161,8 @@ hipError_t launch_md_lines(const char *buf, int64_t data_start, int64_t n_input,
 // VCFX_allele_counter (vcfxg_ac.hip) over indexed lines [l0, l1): per line status (1 data,
 // 4 '#CHROM', 0 other), row bytes (len[li - l0]) and meta (ac_meta_bytes() each); counters
 // [0] rows, [1] data lines, [2] '#CHROM' lines, [3] lines off the fixed-stride sweep.  eff:
-// per output slot the sample index it reads; scratch: ac_threads() / 64 * blocks * scap u32
+// per output slot the sample index it reads; scratch: ac_threads() / 64 * blocks * scap u32;
+// sel_lds: LDS bytes for the selection in k_ac_fmt (4 m + 4 (m + 1) + name bytes), 0 = global
 size_t ac_meta_bytes();
 int ac_threads();
 hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
@@ -170,8 +171,8 @@ hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *li
                          uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s);
 hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
-                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, const uint8_t *status,
-                         const void *meta, const uint64_t *off, char *out, hipStream_t s);
+                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint32_t sel_lds,
+                         const uint8_t *status, const void *meta, const uint64_t *off, char *out, hipStream_t s);
 // VCFX_haplotype_phaser (vcfxg_ph.hip): per line status (kPh*), the variants' genotype codes
 // (row = line, kpad bytes; counters[3] = the largest sample count past kpad), the variant ->
 // line compaction, per variant the pair flags with its predecessor (bit 0 the block rule
