@@ -123,7 +123,7 @@ def _check(case, inputs, stdin="none"):
                                         ("hwe_file", "none"), ("hwe_stdin", "pipe"), ("hwe_stdin", "file"),
                                         ("dose_file", "none"), ("ac_bin_file", "none"), ("ac_agg_file", "none"),
                                         ("ac_sel_file", "none"), ("ac_sel_stdin", "pipe"), ("ac_sel_stdin", "file"),
-                                        ("md_file", "none")])
+                                        ("md_file", "none"), ("ph_file", "none"), ("ph_stream_stdin", "pipe")])
 def test_chr21_shard_matches_reference(inputs, case, stdin):
     _check(case, inputs, stdin)
 
@@ -160,7 +160,7 @@ def test_bgzf_chr21_matches_reference(inputs, case):
     assert got == c["stdout"], (case, got, err[-2000:])
 
 
-@pytest.mark.parametrize("case", ["ld1500_t02", "ld1500_t0", "ld1500_w300_t0", "ld3000_bench"])
+@pytest.mark.parametrize("case", ["ld1500_t02", "ld1500_t0", "ld1500_w300_t0", "ld3000_bench", "ph_ld3000"])
 def test_ld_matches_reference(inputs, case):
     _check(case, inputs)
 
