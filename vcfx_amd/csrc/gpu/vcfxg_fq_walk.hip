@@ -424,8 +424,10 @@ hipError_t launch_fq_finish(int what, const char *buf, int64_t data_start, const
                             void *meta, const void *tabs, unsigned long long *rf_cnt, unsigned long long *gq_cnt,
                             hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
-    // one line per thread: the filter is a latency chain (line end, tabs, field bytes), so
-    // every line gets its own thread rather than a grid-stride share
+    // up to one line per thread: the filter is a latency chain (line end, tabs, field bytes),
+    // so lines get their own threads rather than grid-stride shares; the kernel still grid-
+    // strides past 65535 * 256 lines (the loop keeps it correct at any count).  n_lines_host
+    // is the caller's line capacity, an upper bound of the count the kernel reads on the device
     const unsigned grid = (unsigned)std::min<uint64_t>((n_lines_host + 255) / 256, 65535);
     LineMeta *m = static_cast<LineMeta *>(meta);
     const uint4 *t = static_cast<const uint4 *>(tabs);
