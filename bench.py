@@ -475,7 +475,7 @@ def main():
             if red is not None:
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.general_records])
             return s
-        kern_names = ("line_count", "line_emit", "line_compact", "md_lines")
+        kern_names = ("line_count", "line_emit", "line_compact", "md_lines", "md_walk", "md_rest")
     elif a.workload == "ph":
         def step():
             s = eng.haplotype_phaser(ds, engine.MODE_FILE, 0.8, a.samples)  # parse + consecutive-variant LD
@@ -592,6 +592,9 @@ def main():
                 "ac_fmt": region_bytes + tb + L * (8 + 1 + 8 + 48),
                 # missing detector: the records once + line end, status and the INFO span per line
                 "md_lines": region_bytes + L * (8 + 1 + 8),
+                # its walk (long GT-only records): the record bytes once + line end, status and
+                # head record per line; the rest compacts them and reads status + line ends
+                "md_walk": region_bytes + L * (8 + 1 + 16),
                 # phaser: the records once + a genotype code per sample + line end, status, flag
                 # and the per-line record (24 B); the pairs read each code row twice
                 "ph_lines": region_bytes + L * (a.samples + 8 + 1 + 4 + 24),

@@ -74,3 +74,26 @@ def test_missing_engine_counts(oracle):
     assert s.data_lines == 1500 and s.rows == int((st == 6).sum()) and s.general_records >= s.rows > 0
     assert s.rows == oracle.run(["VCFX_missing_detector"], buf)[0].count(b"MISSING_GENOTYPES=1")
     eng.close()
+
+
+def test_missing_walk_and_index_paths_agree(oracle, monkeypatch):
+    """the walk (long GT-only records: VCFXG_FQ_WALK=1) and the index path (-1) give the same
+    per-line statuses, INFO spans and counts, and the counts the reference prints"""
+    import numpy as np
+    for cfg in (dict(n_records=900, n_samples=2504, seed=98, missing_rate=0.0003),
+                dict(n_records=700, n_samples=1200, seed=99, missing_rate=0.001, irregular_rate=0.1, crlf=1)):
+        buf = synth.generate(**cfg)
+        ds = engine.data_start_of(buf)
+        got = []
+        for walk in ("1", "-1"):
+            monkeypatch.setenv("VCFXG_FQ_WALK", walk)
+            eng = engine.Engine(0)
+            eng.load(buf)
+            s = eng.missing_region(ds, engine.MODE_FILE)
+            a, t, st = eng.lines(s.n_lines)
+            got.append(((s.n_lines, s.data_lines, s.rows, s.general_records), st.copy(), a.copy(), t.copy()))
+            eng.close()
+        assert got[0][0] == got[1][0]
+        for k in (1, 2, 3):
+            assert np.array_equal(got[0][k], got[1][k])
+        assert got[0][0][2] == oracle.run(["VCFX_missing_detector"], buf)[0].count(b"MISSING_GENOTYPES=1")

@@ -1589,11 +1589,81 @@ int vcfxg_phaser_variants(vcfxg_ctx *c, uint8_t *flags, double *r2, uint64_t *of
     return VCFXG_OK;
 }
 
-// VCFX_missing_detector over [data_start, n): the line index and one per-line pass
+// VCFX_missing_detector over [data_start, n): for long GT-only records the filter / query walk
+// with the missing-allele reducer (one HBM pass; k_md_lines then takes the lines it left and
+// the flagged lines' INFO spans), else the line index and k_md_lines on every line
+static int md_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+    c->dense_pending = false;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n, C = c->walk_chunk;
+    const int64_t nw = vcfxg::af_walkers(lo, hi, C);
+    const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
+    const uint64_t cap = (uint64_t)nw * cap_w;
+    const size_t mb = vcfxg::af_meta_bytes();
+    int r = ensure(c, c->wk_le, 8 * cap);
+    if (!r) r = ensure(c, c->wk_status, cap);
+    if (!r) r = ensure(c, c->wk_meta, mb * cap);
+    if (!r) r = ensure(c, c->wk_count, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_offs, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_small, 128);
+    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
+    if (!r) r = ensure(c, c->af_meta, mb * (cap + 1));
+    if (!r) r = af_buffers(c, cap);
+    if (r) return r;
+    const char *buf = P<char>(c->input);
+    unsigned *ovf = P<unsigned>(c->wk_small);
+    const vcfxg::RfArgs ra{nullptr, 0, 1, nullptr, 0};
+    HIPCHK(c, hipMemsetAsync(ovf, 0, 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->wk_count) + nw, 0, 8, c->stream));
+    prof_begin(c, "md_walk");
+    HIPCHK(c, vcfxg::launch_fq_walk(vcfxg::kFqMD, buf, lo, hi, C, mode == VCFXG_MODE_FILE ? 1 : 0, c->hint_span, cap_w, ra,
+                                    nullptr, 0, 0, -1, -1, P<uint64_t>(c->wk_le), P<uint8_t>(c->wk_status),
+                                    c->wk_meta.p, nullptr, P<uint64_t>(c->wk_count), ovf, c->stream));
+    prof_end(c, "md_walk");
+    prof_begin(c, "md_rest");
+    r = exclusive_scan(c, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_offs), (size_t)nw + 1);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_fq_compact(vcfxg::kFqMD, nw, cap_w, P<uint64_t>(c->wk_offs), P<uint64_t>(c->wk_le),
+                                       P<uint8_t>(c->wk_status), c->wk_meta.p, nullptr, P<uint64_t>(c->line_end),
+                                       P<uint8_t>(c->status), c->af_meta.p, nullptr, P<uint64_t>(c->d_nlines),
+                                       c->stream));
+    HIPCHK(c, vcfxg::launch_md_lines(buf, lo, (int64_t)c->n, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap,
+                                     mode, P<uint8_t>(c->status), P<int32_t>(c->alt), P<int32_t>(c->tot),
+                                     P<unsigned long long>(c->counters), c->stream, 1));
+    prof_end(c, "md_rest");
+    static thread_local uint64_t h[5];
+    HIPCHK(c, hipMemcpyAsync(h, c->counters.p, 24, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(h + 3, c->d_nlines.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(h + 4, ovf, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    if (h[4] & 0xFFFFFFFFu) {  // a walker ran out of line slots (short lines): no walk
+        c->walk_overflowed = true;
+        return vcfxg_missing_region(c, data_start, mode, out);
+    }
+    c->data_start = data_start;
+    c->n_lines = h[3];
+    c->indexed = true;
+    c->text_bytes = 0;
+    if (out) {
+        std::memset(out, 0, sizeof *out);
+        out->n_lines = h[3];
+        out->data_lines = h[0];
+        out->rows = h[1];
+        out->general_records = h[2];
+    }
+    return VCFXG_OK;
+}
+
 int vcfxg_missing_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
+    // the walk for long GT-only records (VCFXG_FQ_WALK: 1 always, -1 never), as the filter tools
+    if (vcfxg::af_walkers((int64_t)data_start, (int64_t)c->n, c->walk_chunk) && c->fq_path >= 0 && !c->walk_overflowed &&
+        (c->fq_path == 1 || (c->hint_line >= 512 && c->hint_gt_only)))
+        return md_region_walk(c, data_start, mode, out);
     uint64_t L = 0;
     int r = vcfxg_index(c, data_start, &L);
     if (r) return r;

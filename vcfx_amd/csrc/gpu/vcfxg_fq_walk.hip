@@ -63,8 +63,10 @@ struct PoolBytes {
 };
 
 // kNR (with kGQ, without kRF): VCFX_nonref_filter -- the same walk with NrOp ("some sample
-// is not hom-ref", early exit) in place of the query; k_nr_complex takes the rest
-template <bool kRF, bool kGQ, bool kNR = false>
+// is not hom-ref", early exit) in place of the query; k_nr_complex takes the rest.
+// kMD (with kGQ): VCFX_missing_detector -- MdOp ("some sample's GT has a '.' allele", early
+// exit): status kMdFlag / 1 on the fixed-stride records; k_md_lines takes the rest
+template <bool kRF, bool kGQ, bool kNR = false, bool kMD = false>
 __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict__ buf, int64_t lo, int64_t hi,
                                                           int64_t chunk, int64_t n_walkers, int strip_cr,
                                                           int64_t span0, uint64_t cap_w, RfArgs rf, GqQuery Q,
@@ -196,7 +198,11 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
                 sep = t8 + 2 >= ae ? 0
                       : t8 + 2 < wend ? (uint8_t)sep_w
                                       : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
-                if constexpr (kNR) {
+                if constexpr (kMD) {
+                    MdOp op{};
+                    ok = gt_fast<kFqUnroll>(buf, S, ae, op, sep, pre, &swept);
+                    found = op.found;
+                } else if constexpr (kNR) {
                     NrOp op{buf, ae, 0, strip_cr ? 0 : 1};
                     ok = gt_fast<kFqUnroll>(buf, S, ae, op, sep, pre, &swept);
                     found = op.found;
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
             st = kRfPending;  // k_fq_finish evaluates the filter (then k_gq_complex the query)
             kind = kMetaFull;
         } else if (!kGQ) st = 1;  // (k_fq_finish drops the lines the filter rejects)
-        else if (kind == kMetaGt && ok) st = found ? 1 : (kRF ? 6 : 2);
+        else if (kind == kMetaGt && ok) st = kMD ? (found ? kMdFlag : 1) : found ? 1 : (kRF ? 6 : 2);
         else st = kind == kMetaGt ? kGqPending : kGqFull;
         if ((uint32_t)lane() == (uint32_t)(n & 63)) {
             r_le = (uint64_t)E;
@@ -366,14 +372,14 @@ __global__ __launch_bounds__(256) void k_fq_finish(const char *__restrict__ buf,
     }
 }
 
-template <bool kRF, bool kGQ, bool kNR = false>
+template <bool kRF, bool kGQ, bool kNR = false, bool kMD = false>
 static hipError_t fq_walk_launch(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int strip_cr, int64_t span0,
                                  uint64_t cap_w, const RfArgs &rf, const GqQuery &Q, uint64_t *le_b,
                                  uint8_t *status_b, LineMeta *meta_b, uint4 *tabs_b, uint64_t *wcount,
                                  unsigned *overflow, hipStream_t s) {
     const int64_t nw = af_walkers(lo, hi, chunk);
     const unsigned grid = (unsigned)((nw + kWalkWaves - 1) / kWalkWaves);
-    hipLaunchKernelGGL((k_fq_walk<kRF, kGQ, kNR>), dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, strip_cr,
+    hipLaunchKernelGGL((k_fq_walk<kRF, kGQ, kNR, kMD>), dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, strip_cr,
                        span0, cap_w, rf, Q, le_b, status_b, meta_b, tabs_b, wcount, overflow);
     return hipGetLastError();
 }
@@ -395,6 +401,9 @@ hipError_t launch_fq_walk(int what, const char *buf, int64_t lo, int64_t hi, int
     if (what == kFqNR)
         return fq_walk_launch<false, true, true>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m,
                                                  t, wcount, overflow, s);
+    if (what == kFqMD)
+        return fq_walk_launch<false, true, false, true>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b,
+                                                        status_b, m, t, wcount, overflow, s);
     return fq_walk_launch<true, true>(buf, lo, hi, chunk, strip_cr, span0, cap_w, rf, Q, le_b, status_b, m, t, wcount,
                                       overflow, s);
 }
@@ -410,7 +419,7 @@ hipError_t launch_fq_compact(int what, int64_t n_walkers, uint64_t cap_w, const 
     if (what == kFqRF)
         hipLaunchKernelGGL((k_fq_compact<false, true>), dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs,
                            le_b, status_b, mb, tb, line_end, status, m, t, n_lines);
-    else if (what == kFqGQ || what == kFqNR)
+    else if (what == kFqGQ || what == kFqNR || what == kFqMD)
         hipLaunchKernelGGL((k_fq_compact<true, false>), dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs,
                            le_b, status_b, mb, tb, line_end, status, m, t, n_lines);
     else

@@ -482,6 +482,21 @@ struct NrOp {
 };
 
 // ---------------------------------------------------------------------------------------
+// missing-genotype reducer (VCFX_missing_detector) on the fixed-stride
+// layout: every sample is a 3-byte GT "a s b" between tabs, so a '.' allele is at its GT's
+// start or end -- the sample is missing (hasMissingGenotypeInSamples,
+// VCFX_missing_detector.cpp:290-336); early exit at the first one
+// ---------------------------------------------------------------------------------------
+struct MdOp {
+    bool any = false;    // this lane saw a '.' allele
+    bool found = false;  // wave
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() { return found = found || __any(any); }
+    __device__ void dword(const DwordView &v) { any = any || (v.real && v.dig != 0x01000100u); }
+    __device__ void finish() { found = __any(any); }
+};
+
+// ---------------------------------------------------------------------------------------
 // HWE genotype-class reducer (VCFX_hwe_tester): per sample
 // parseGenotypeForHWE (VCFX_hwe_tester.cpp:339-378) -> 0 hom-ref, 1 het, 2 hom-alt, or
 // invalid (not counted).  The sample's first ':' sub-field, leading ' ' / '\r' skipped, two

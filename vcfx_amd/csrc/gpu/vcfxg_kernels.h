@@ -153,11 +153,13 @@ hipError_t launch_dose_fmt(const char *buf, int64_t data_start, const uint64_t *
                            char *out, uint64_t cap, hipStream_t s);
 // VCFX_missing_detector (vcfxg_md.hip) over the indexed lines: per line status (0 empty, 4 '#',
 // 1 kept as is, kMdFlag flagged) and the flagged lines' INFO span relative to the line start;
-// counters [0] data lines, [1] flagged, [2] lines ending in '\n' with a '.' in their samples
+// counters [0] data lines, [1] flagged, [2] lines ending in '\n' with a '.' in their samples;
+// walk: the statuses hold the missing-detector walk's decisions (1 / kMdFlag taken as they are)
 constexpr uint8_t kMdFlag = 6;
 hipError_t launch_md_lines(const char *buf, int64_t data_start, int64_t n_input, const uint64_t *line_end,
                            const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, uint8_t *status,
-                           int32_t *info_s, int32_t *info_e, unsigned long long *counters, hipStream_t s);
+                           int32_t *info_s, int32_t *info_e, unsigned long long *counters, hipStream_t s,
+                           int walk = 0);
 // VCFX_allele_counter (vcfxg_ac.hip) over indexed lines [l0, l1): per line status (1 data,
 // 4 '#CHROM', 0 other), row bytes (len[li - l0]) and meta (ac_meta_bytes() each); counters
 // [0] rows, [1] data lines, [2] '#CHROM' lines, [3] lines off the fixed-stride sweep.  eff:

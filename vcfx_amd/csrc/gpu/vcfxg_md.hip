@@ -75,7 +75,7 @@ __device__ __forceinline__ void md_sweep(const char *__restrict__ buf, int64_t s
 
 __global__ __launch_bounds__(kMdThreads) void k_md_lines(const char *__restrict__ buf, int64_t data_start,
                                                          int64_t n_input, const uint64_t *__restrict__ line_end,
-                                                         const uint64_t *n_lines_p, int mode,
+                                                         const uint64_t *n_lines_p, int mode, int walk,
                                                          uint8_t *__restrict__ status, int32_t *__restrict__ info_s,
                                                          int32_t *__restrict__ info_e,
                                                          unsigned long long *__restrict__ counters) {
@@ -86,14 +86,26 @@ __global__ __launch_bounds__(kMdThreads) void k_md_lines(const char *__restrict_
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
     uint32_t data = 0, flagged = 0, dots = 0;  // (wave-uniform)
-    for (uint64_t li = wid; li < n_lines; li += nw) {
+    // one line with the whole wave
+    auto one = [&](uint64_t li) {
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
         int64_t ae = le;
         if (mode == 0 && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;
         uint8_t st = 0;
         int32_t is = 0, ie = 0;
         bool dot = false, miss = false;
-        if (ae > ls) {
+        const uint8_t ws = walk ? status[li] : (uint8_t)0xFF;
+        if (ws == kMdFlag) {  // the walk found a missing sample: the INFO span
+            int64_t t[9];
+            const int nt = head_tabs(buf, ls, ae, 9, t, lds);
+            (void)nt;  // (a fixed-stride record has its 9 tabs)
+            data++;
+            flagged++;
+            st = kMdFlag;
+            is = (int32_t)(t[6] + 1 - ls);
+            ie = (int32_t)(t[7] - ls);
+            dots += le < n_input;
+        } else if (ae > ls) {
             const bool hash = byte_at(buf, ls) == '#';
             int64_t t[9];
             // a '#' line is copied, but the file pre-scan looks at its "sample" bytes too
@@ -119,7 +131,28 @@ __global__ __launch_bounds__(kMdThreads) void k_md_lines(const char *__restrict_
             info_s[li] = is;
             info_e[li] = ie;
         }
-    }
+    };
+    if (walk) {
+        // 64 lines per step, a lane each: the walk's fixed-stride records without a '.' allele
+        // (status 1: no '.' at all) are counted by the lanes; the wave takes the others in turn
+        for (uint64_t b0 = wid * kWave; b0 < n_lines; b0 += nw * kWave) {
+            const uint64_t li = b0 + lane();
+            const uint8_t st = li < n_lines ? status[li] : (uint8_t)0;
+            const bool plain = li < n_lines && st == 1;
+            if (plain) {
+                info_s[li] = 0;
+                info_e[li] = 0;
+            }
+            data += (uint32_t)__popcll(__ballot(plain));
+            uint64_t todo = __ballot(li < n_lines && st != 1);
+            while (todo) {
+                const int j = __builtin_ctzll(todo);
+                todo &= todo - 1;
+                one(b0 + j);
+            }
+        }
+    } else
+        for (uint64_t li = wid; li < n_lines; li += nw) one(li);
     if (lane() == 0) {
         red[0][threadIdx.x / kWave] = data;
         red[1][threadIdx.x / kWave] = flagged;
@@ -135,12 +168,12 @@ __global__ __launch_bounds__(kMdThreads) void k_md_lines(const char *__restrict_
 
 hipError_t launch_md_lines(const char *buf, int64_t data_start, int64_t n_input, const uint64_t *line_end,
                            const uint64_t *n_lines_dev, uint64_t n_lines_host, int mode, uint8_t *status,
-                           int32_t *info_s, int32_t *info_e, unsigned long long *counters, hipStream_t s) {
+                           int32_t *info_s, int32_t *info_e, unsigned long long *counters, hipStream_t s, int walk) {
     if (!n_lines_host) return hipSuccess;
     int64_t g = ((int64_t)n_lines_host + kMdWaves - 1) / kMdWaves;
     if (g > 4096) g = 4096;
     hipLaunchKernelGGL(k_md_lines, dim3((unsigned)g), dim3(kMdThreads), 0, s, buf, data_start, n_input, line_end,
-                       n_lines_dev, mode, status, info_s, info_e, counters);
+                       n_lines_dev, mode, walk, status, info_s, info_e, counters);
     return hipGetLastError();
 }
 

@@ -135,7 +135,7 @@ hipError_t launch_rf_records(const char *buf, int64_t data_start, const uint64_t
 
 // ---- the filter / query walk (vcfxg_fq_walk.hip): record_filter (kFqRF), genotype_query
 // (kFqGQ) or the fused pipeline (kFqBoth) in one pass without a separate line index
-enum { kFqRF = 1, kFqGQ = 2, kFqBoth = 3, kFqNR = 4 };  // kFqNR: VCFX_nonref_filter
+enum { kFqRF = 1, kFqGQ = 2, kFqBoth = 3, kFqNR = 4, kFqMD = 5 };  // kFqNR: VCFX_nonref_filter, kFqMD: VCFX_missing_detector
 struct RfArgs {
     const RfCrit *crit;
     int ncrit, and_logic;
