@@ -103,7 +103,8 @@ struct DoseMeta {
     uint32_t ae;    // line end (after the mode's '\r' strip) - S
     int32_t gi;     // GT index in FORMAT
     uint8_t kind;   // kDose*
-    uint8_t pad[3];
+    uint8_t plain;  // kDoseFast without an "NA": 2 output bytes per sample
+    uint8_t pad[2];
 };
 
 __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restrict__ buf, int64_t data_start,
@@ -148,6 +149,7 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
                     DoseCountOp op{buf, ae, gi};
                     bool fast = gi == 0 && gt_fast(buf, S, ae, op);
                     m.kind = kDoseFast;
+                    m.plain = fast && op.na == 0;
                     if (!fast) {
                         m.kind = kDoseGeneral;
                         op = DoseCountOp{buf, ae, gi};
@@ -229,6 +231,75 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
         // bytes end there is the last, and ends with '\n' instead of ','
         const uint64_t tot = off[li + 1] - off[li] - m.pre;
         uint64_t run = 0;  // output bytes of the samples before this wave-step
+        if (m.kind == kDoseFast && m.plain) {
+            // fixed-stride, no "NA": sample k ("a s b\t" at S + 4k) is output bytes 2k, 2k + 1
+            // of the dosage text (the digit, then ',' or the final '\n').  Lane c takes samples
+            // 8c..8c+7 (32 input bytes, realigned from three 16 B loads by S mod 16) and builds
+            // the aligned 16 B output block that starts inside its 16 bytes' span: the previous
+            // lane's last (ob mod 16) bytes, then its own first ones -- one store per block
+            const int64_t ns = (E - S + 1) / 4;
+            const uint64_t ob = (uint64_t)(o - out), oe = ob + 2 * (uint64_t)ns;
+            const uint32_t ish = (uint32_t)(S & 15), osh = (uint32_t)(ob & 15);
+            const uint32_t iq = ish >> 2, ib = ish & 3, wq = (16u - osh) >> 2, wb = (16u - osh) & 3;
+            const int64_t nch = (ns + 7) / 8;  // chunks of 8 samples; chunk nch holds only the tail block
+            uint32_t carry[4] = {0u, 0u, 0u, 0u};  // the previous wave-step's last chunk
+            for (int64_t c0 = 0; c0 <= nch; c0 += kWave) {
+                const int64_t c = c0 + lane(), k0 = 8 * c;
+                uint32_t od[4] = {0u, 0u, 0u, 0u};
+                if (c < nch) {
+                    const char *ip = buf + ((S + 4 * k0) & ~(int64_t)15);
+                    const uint4 v0 = load16(ip, 0), v1 = load16(ip, 16), v2 = load16(ip, 32);
+                    const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
+                    uint32_t r[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {  // (iq wave-uniform)
+                        const uint32_t lo_ = iq == 0 ? w[i] : iq == 1 ? w[i + 1] : iq == 2 ? w[i + 2] : w[i + 3];
+                        const uint32_t hi_ = iq == 0 ? w[i + 1] : iq == 1 ? w[i + 2] : iq == 2 ? w[i + 3] : w[i + 4];
+                        r[i] = __builtin_amdgcn_alignbyte(hi_, lo_, ib);
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        uint32_t v = 0;
+#pragma unroll
+                        for (int h = 0; h < 2; h++) {
+                            const int t = 2 * j + h;
+                            const uint32_t a = r[t] & 0xFFu, b = (r[t] >> 16) & 0xFFu;
+                            const uint32_t d = (a != '0') + (b != '0');
+                            const uint32_t sep = k0 + t == ns - 1 ? (uint32_t)'\n' : (uint32_t)',';
+                            v |= (('0' + d) | (sep << 8)) << (16 * h);
+                        }
+                        od[j] = v;
+                    }
+                }
+                // the previous chunk's bytes: the lane before, or the carry for lane 0
+                uint32_t pv[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t up = (uint32_t)__shfl_up((int)od[j], 1);
+                    pv[j] = lane() ? up : carry[j];
+                    carry[j] = (uint32_t)__shfl((int)od[j], kWave - 1);
+                }
+                // the block = bytes [16 - osh, 32 - osh) of (pv ++ od)
+                const uint32_t X[9] = {pv[0], pv[1], pv[2], pv[3], od[0], od[1], od[2], od[3], 0u};
+                uint32_t bw[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {  // (wq wave-uniform)
+                    const uint32_t lo_ = wq == 0 ? X[i] : wq == 1 ? X[i + 1] : wq == 2 ? X[i + 2] : wq == 3 ? X[i + 3] : X[i + 4];
+                    const uint32_t hi_ = wq == 0 ? X[i + 1] : wq == 1 ? X[i + 2] : wq == 2 ? X[i + 3] : wq == 3 ? X[i + 4] : X[i + 5];
+                    bw[i] = __builtin_amdgcn_alignbyte(hi_, lo_, wb);
+                }
+                const uint64_t base = (ob & ~15ull) + 16ull * (uint64_t)c;
+                if (c <= nch && base < oe) {
+                    if (base >= ob && base + 16 <= oe)
+                        *reinterpret_cast<uint4 *>(out + base) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+                    else
+#pragma unroll
+                        for (int j = 0; j < 16; j++)
+                            if (base + j >= ob && base + j < oe) out[base + j] = (char)(bw[j >> 2] >> (8 * (j & 3)));
+                }
+            }
+            continue;
+        }
         if (m.kind == kDoseFast) {
             // the fixed-stride layout: samples "a s b\t" on the 4-byte grid from S, the last
             // without its tab; lane l of a wave-step takes 4 consecutive samples
