@@ -25,6 +25,8 @@ namespace vcfxg {
 
 constexpr int kPhThreads = 256;
 constexpr int kPhWaves = kPhThreads / kWave;
+constexpr int kPhLdsRow = 4096;
+constexpr int kPhUnroll = 4;     // k_ph_pairs: 16 B loads of each row in flight per lane  // samples per record composed in LDS (more: byte stores to HBM)
 
 // parseGenotypeFast on [g, g + n)
 __device__ __forceinline__ int ph_gt(const char *__restrict__ buf, int64_t g, int64_t n) {
@@ -84,6 +86,20 @@ struct PhOp {
     __device__ void finish() {}
 };
 
+// the same codes into the wave's LDS row (an LDS-address-space pointer: ds_write_b8, not flat)
+struct PhOpL {
+    __attribute__((address_space(3))) int8_t *row;
+    int64_t S;
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() const { return false; }
+    __device__ void dword(const DwordView &v) {
+        if (!v.real) return;
+        const uint32_t a = v.f & 0xFFu, b = (v.f >> 16) & 0xFFu;
+        row[(v.p - S) >> 2] = (int8_t)(v.dig == 0x01000100u ? (int)(a + b) : -1);
+    }
+    __device__ void finish() {}
+};
+
 struct PhLine {
     uint64_t chrom;  // CHROM start
     uint32_t clen;   // CHROM bytes
@@ -99,7 +115,12 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
                                                          uint32_t *__restrict__ isvar, PhLine *__restrict__ info,
                                                          unsigned long long *__restrict__ counters) {
     __shared__ int64_t scratch[kPhWaves][16];
+    // a GT-only fixed-stride record's codes are composed in the wave's LDS row (byte writes)
+    // and leave in 16 B stores: a byte store per sample to HBM would be 4 store instructions
+    // per lane per KiB of record
+    __shared__ __attribute__((aligned(16))) int8_t lrows[kPhWaves][kPhLdsRow];
     int64_t *lds = scratch[threadIdx.x / kWave];
+    int8_t *lrow = lrows[threadIdx.x / kWave];
     const uint64_t n_lines = *n_lines_p;
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
@@ -139,9 +160,31 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
                         const int64_t S = t[8] + 1;
                         int8_t *row = G + li * (uint64_t)kpad;
                         const int64_t L = ae - S;
-                        PhOp op{row, S};
-                        if (gi == 0 && L >= 3 && ((L + 1) & 3) == 0 && (uint64_t)((L + 1) / 4) <= kpad &&
-                            gt_fast(buf, S, ae, op))
+                        const bool fixed = gi == 0 && L >= 3 && ((L + 1) & 3) == 0 && (uint64_t)((L + 1) / 4) <= kpad;
+                        bool swept = false;
+                        if (fixed && (L + 1) / 4 <= kPhLdsRow) {
+                            PhOpL op{(__attribute__((address_space(3))) int8_t *)lrow, S};
+                            swept = gt_fast(buf, S, ae, op);
+                            if (swept) {
+                                const uint32_t ns = (uint32_t)((L + 1) / 4);
+                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                                __builtin_amdgcn_wave_barrier();
+                                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                                for (uint32_t o = (uint32_t)lane() * 16; o < ns; o += kWave * 16) {
+                                    if (o + 16 <= ns)
+                                        *reinterpret_cast<uint4 *>(row + o) = *reinterpret_cast<const uint4 *>(lrow + o);
+                                    else
+                                        for (uint32_t q = o; q < ns; q++) row[q] = lrow[q];
+                                }
+                                // the next line's byte writes must not pass these reads
+                                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                                __builtin_amdgcn_wave_barrier();
+                            }
+                        } else if (fixed) {
+                            PhOp op{row, S};
+                            swept = gt_fast(buf, S, ae, op);
+                        }
+                        if (swept)
                             m.ns = (uint32_t)((L + 1) / 4);
                         else {
                             // a lane per sample start; sample k = its rank among the starts
@@ -210,27 +253,53 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_pairs(const char *__restrict_
             const PhLine a = info[vline[v - 1]];
             const int8_t *ga = G + vline[v - 1] * (uint64_t)kpad, *gb = G + vline[v] * (uint64_t)kpad;
             const uint32_t n = min(a.ns, b.ns);
-            int32_t vn = 0, sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;  // (int8 codes: no overflow below 2^31 / 127^2 samples per lane)
-            // 16 codes per lane per load (rows are 16-byte aligned; bytes past n are masked)
-            for (uint32_t k0 = 16u * lane(); k0 < n; k0 += 16u * kWave) {
-                const uint4 va = *reinterpret_cast<const uint4 *>(ga + k0);
-                const uint4 vb = *reinterpret_cast<const uint4 *>(gb + k0);
-                const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
+            // per lane and pass: (valid, Sx) | (Sy, Sxy) | (Sx2, Sy2) as two 32-bit fields of
+            // one 64-bit word each, so a pass reduces three 64-bit sums instead of six (a pass
+            // covers 16 * 64 * kPhUnroll codes: a field stays below 127^2 * 4096 < 2^32)
+            int64_t N = 0, SX = 0, SY = 0, SXY = 0, SX2 = 0, SY2 = 0;
+            // 16 codes per lane per load, kPhUnroll loads of each row in flight (rows are 16-byte
+            // aligned and kpad long; bytes past n are masked, a load past the row re-reads its
+            // last 16 bytes)
+            for (uint32_t b0 = 0; b0 < n; b0 += 16u * kWave * kPhUnroll) {
+                uint4 va[kPhUnroll], vb[kPhUnroll];
 #pragma unroll
-                for (int j = 0; j < 16; j++) {
-                    const int x = (int)(int8_t)(wa[j >> 2] >> (8 * (j & 3)));
-                    const int y = (int)(int8_t)(wb[j >> 2] >> (8 * (j & 3)));
-                    if (k0 + j >= n || x < 0 || y < 0) continue;
-                    vn++;
-                    sx += x;
-                    sy += y;
-                    sxy += x * y;
-                    sx2 += x * x;
-                    sy2 += y * y;
+                for (int u = 0; u < kPhUnroll; u++) {
+                    uint32_t k0 = b0 + 16u * (lane() + kWave * u);
+                    k0 = k0 < kpad ? k0 : kpad - 16u;
+                    va[u] = *reinterpret_cast<const uint4 *>(ga + k0);
+                    vb[u] = *reinterpret_cast<const uint4 *>(gb + k0);
                 }
+                uint64_t p0 = 0, p1 = 0, p2 = 0;
+#pragma unroll
+                for (int u = 0; u < kPhUnroll; u++) {
+                    const uint32_t k0 = b0 + 16u * (lane() + kWave * u);
+                    const uint32_t wa[4] = {va[u].x, va[u].y, va[u].z, va[u].w}, wb[4] = {vb[u].x, vb[u].y, vb[u].z, vb[u].w};
+                    uint32_t vn = 0, sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;
+#pragma unroll
+                    for (int j = 0; j < 16; j++) {
+                        const int x = (int)(int8_t)(wa[j >> 2] >> (8 * (j & 3)));
+                        const int y = (int)(int8_t)(wb[j >> 2] >> (8 * (j & 3)));
+                        if (k0 + j >= n || x < 0 || y < 0) continue;
+                        vn++;
+                        sx += x;
+                        sy += y;
+                        sxy += x * y;
+                        sx2 += x * x;
+                        sy2 += y * y;
+                    }
+                    p0 += (uint64_t)vn | (uint64_t)sx << 32;
+                    p1 += (uint64_t)sy | (uint64_t)sxy << 32;
+                    p2 += (uint64_t)sx2 | (uint64_t)sy2 << 32;
+                }
+                const uint64_t q0 = (uint64_t)wave_sum((int64_t)p0), q1 = (uint64_t)wave_sum((int64_t)p1),
+                               q2 = (uint64_t)wave_sum((int64_t)p2);
+                N += (uint32_t)q0;
+                SX += q0 >> 32;
+                SY += (uint32_t)q1;
+                SXY += q1 >> 32;
+                SX2 += (uint32_t)q2;
+                SY2 += q2 >> 32;
             }
-            const int64_t N = wave_sum((int64_t)vn), SX = wave_sum((int64_t)sx), SY = wave_sum((int64_t)sy),
-                          SXY = wave_sum((int64_t)sxy), SX2 = wave_sum((int64_t)sx2), SY2 = wave_sum((int64_t)sy2);
             double r = 0.0;
             if (N > 0) {
                 const double dn = (double)N;
@@ -305,6 +374,7 @@ hipError_t launch_ph_lines(const char *buf, int64_t data_start, const uint64_t *
     if (!n_lines_host) return hipSuccess;
     int64_t g = ((int64_t)n_lines_host + kPhWaves - 1) / kPhWaves;
     if (g > 4096) g = 4096;
+    // (a record's sweep with 8 KiB-steps in flight per wave measured the same as 4: r02)
     hipLaunchKernelGGL(k_ph_lines, dim3((unsigned)g), dim3(kPhThreads), 0, s, buf, data_start, line_end, n_lines_dev,
                        mode, kpad, G, status, isvar, static_cast<PhLine *>(info), counters);
     return hipGetLastError();
