@@ -126,3 +126,29 @@ def test_ld_staging_overflow_falls_back(oracle):
             finally:
                 del os.environ["VCFXG_LD_STAGE_CAP"]
             assert got == want, cap
+
+
+def test_ld_pair_lines_long_and_short_fields(oracle):
+    """The pair-line writer composes 64 lines per wave in an 8 KiB LDS tile and writes it as
+    aligned 16 B stores; waves whose lines outgrow the tile write each line straight out.
+    IDs of 1..400 bytes (some records long enough to force the straight path, the rest short)
+    at threshold 0: every window pair's line, tile edges at every alignment."""
+    import random
+    buf = synth.generate(300, 60, 61, 0, 0.0, 1, 0.0, 0)
+    rnd = random.Random(61)
+    lines = buf.split(b"\n")
+    for k, ln in enumerate(lines):
+        if ln and not ln.startswith(b"#"):
+            f = ln.split(b"\t")
+            n = rnd.choice([1, 2, 7, 15, 16, 17, 33]) if rnd.random() < 0.8 else rnd.randint(100, 400)
+            f[2] = (b"rs%d_" % k + b"x" * n)
+            lines[k] = b"\t".join(f)
+    buf = b"\n".join(lines)
+    with tempfile.NamedTemporaryFile(suffix=".vcf") as f:
+        f.write(buf)
+        f.flush()
+        for a in (["-w", "300", "-t", "0.0"], ["-w", "40", "-t", "0.1"]):
+            argv = ["VCFX_ld_calculator"] + a + ["-i", f.name]
+            got = tools.run(argv, b"")
+            want = oracle.run(argv, b"")
+            assert got == want, (a, len(got[0]), len(want[0]))

@@ -630,18 +630,63 @@ __device__ void fmt_r2(char *o, double r2) {
     o[2] = (char)('0' + v % 10);
 }
 
-__global__ void k_ld_pairwrite(const LdPair *__restrict__ pairs, uint64_t np, const uint64_t *__restrict__ poff,
-                               const char *__restrict__ prefix, const uint64_t *__restrict__ toff,
-                               char *__restrict__ out) {
-    for (uint64_t p = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; p < np; p += gridDim.x * (uint64_t)blockDim.x) {
-        const LdPair x = pairs[p];
-        char *o = out + toff[p];
-        for (uint64_t k = poff[x.i]; k < poff[x.i + 1]; k++) *o++ = prefix[k];
-        *o++ = '\t';
-        for (uint64_t k = poff[x.j]; k < poff[x.j + 1]; k++) *o++ = prefix[k];
-        *o++ = '\t';
-        fmt_r2(o, x.r2);
-        o[6] = '\n';
+// pair lines, 64 per wave: the wave's lines are contiguous in the text, so they are composed
+// in the wave's LDS tile (at their text position mod 16) and leave as aligned 16 B stores (the
+// tile's partial first and last blocks byte by byte: their other bytes belong to the
+// neighbouring waves); a wave whose lines exceed the tile writes each line straight out
+constexpr int kPwTile = 8192;
+__global__ __launch_bounds__(256) void k_ld_pairwrite(const LdPair *__restrict__ pairs, uint64_t np,
+                                                      const uint64_t *__restrict__ poff,
+                                                      const char *__restrict__ prefix,
+                                                      const uint64_t *__restrict__ toff, char *__restrict__ out) {
+    __shared__ __attribute__((aligned(16))) char tile_all[4][kPwTile + 16];
+    char *tile = tile_all[threadIdx.x / kWave];
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / kWave);
+    for (uint64_t p0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave * kWave; p0 < np;
+         p0 += nw * kWave) {
+        const uint64_t p = p0 + lane();
+        const bool ok = p < np;
+        LdPair x{};
+        uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0, t = 0;
+        if (ok) {
+            x = pairs[p];
+            a0 = poff[x.i], a1 = poff[x.i + 1], b0 = poff[x.j], b1 = poff[x.j + 1];
+            t = toff[p];
+        }
+        const uint64_t len = ok ? (a1 - a0) + 1 + (b1 - b0) + 1 + 7 : 0;
+        const uint64_t g0 = wave_bcast(t, 0);
+        const int last = (int)(np - 1 - p0 < (uint64_t)kWave - 1 ? np - 1 - p0 : (uint64_t)kWave - 1);
+        const uint64_t B = wave_bcast(t + len, last) - g0;  // (the lines are contiguous)
+        auto line = [&](char *o) {
+            for (uint64_t k = a0; k < a1; k++) *o++ = prefix[k];
+            *o++ = '\t';
+            for (uint64_t k = b0; k < b1; k++) *o++ = prefix[k];
+            *o++ = '\t';
+            fmt_r2(o, x.r2);
+            o[6] = '\n';
+        };
+        if (B + 16 > (uint64_t)kPwTile) {  // (wave-uniform) long lines: straight out
+            if (ok) line(out + t);
+            continue;
+        }
+        const uint32_t sh = (uint32_t)(g0 & 15);  // tile byte sh + q = text byte g0 + q
+        if (ok) line(tile + sh + (t - g0));
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // text bytes [g0, g0 + B): aligned blocks [A0, A1) whole, the rest byte by byte
+        const uint64_t ge = g0 + B, A0 = (g0 + 15) & ~(uint64_t)15, A1 = ge & ~(uint64_t)15;
+        if (A0 >= A1) {
+            for (uint64_t q = g0 + lane(); q < ge; q += kWave) out[q] = tile[sh + (q - g0)];
+        } else {
+            for (uint64_t q = g0 + lane(); q < A0; q += kWave) out[q] = tile[sh + (q - g0)];
+            for (uint64_t q = A0 + 16u * lane(); q < A1; q += 16u * kWave)
+                *reinterpret_cast<uint4 *>(out + q) = *reinterpret_cast<const uint4 *>(tile + sh + (q - g0));
+            for (uint64_t q = A1 + lane(); q < ge; q += kWave) out[q] = tile[sh + (q - g0)];
+        }
+        // the next group's composition must not pass these reads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -708,7 +753,7 @@ hipError_t launch_ld_pairtext(int which, const LdPair *pairs, uint64_t np, const
     if (which == 0)
         hipLaunchKernelGGL(k_ld_pairlen, dim3(gridfor(np, 256, 8192)), dim3(256), 0, s, pairs, np, poff, len_or_off);
     else
-        hipLaunchKernelGGL(k_ld_pairwrite, dim3(gridfor(np, 256, 8192)), dim3(256), 0, s, pairs, np, poff, prefix,
+        hipLaunchKernelGGL(k_ld_pairwrite, dim3(gridfor(np, 256, 16384)), dim3(256), 0, s, pairs, np, poff, prefix,
                            len_or_off, out);
     return hipGetLastError();
 }
