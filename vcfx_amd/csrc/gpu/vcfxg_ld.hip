@@ -144,6 +144,29 @@ struct LdOp {
     __device__ void finish() {}
 };
 
+// the same codes into the wave's LDS row (an LDS-address-space pointer: ds_write_b8), written
+// out afterwards as 16 B stores
+struct LdOpL {
+    __attribute__((address_space(3))) int8_t *row;
+    int64_t S;
+    int ns;
+    LdStats st;
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() const { return false; }
+    __device__ void dword(const DwordView &v) {
+        if (!v.real) return;
+        int64_t k = (v.p - S) >> 2;
+        if (k >= ns) return;
+        uint32_t a = v.d & 0xFF, b = (v.d >> 16) & 0xFF;
+        int code = ((a - '0') < 2u && (b - '0') < 2u) ? (int)(a - '0' + b - '0') : -1;
+        row[k] = (int8_t)code;
+        st.add(code);
+    }
+    __device__ void sample(int64_t) {}
+    __device__ void finish() {}
+};
+constexpr int kLdLdsRow = 4096;  // samples per record composed in LDS (more: byte stores to HBM)
+
 // general path: samples numbered by a running count of starts (sampleIdx, :598-611)
 __device__ void ld_general(const char *__restrict__ buf, int64_t S, int64_t E, int ns, int8_t *row, LdStats &st,
                            int stoi_mode) {
@@ -189,7 +212,9 @@ __global__ __launch_bounds__(256) void k_ld_parse(const char *__restrict__ buf, 
                                                   const uint64_t *__restrict__ line_end, const uint64_t *n_lines_p,
                                                   LdParseArgs a, int8_t *__restrict__ G, LdLine *__restrict__ lines) {
     __shared__ int64_t scratch[4][16];
+    __shared__ __attribute__((aligned(16))) int8_t lrows[4][kLdLdsRow];
     int64_t *lds = scratch[threadIdx.x / kWave];
+    int8_t *lrow = lrows[threadIdx.x / kWave];
     const uint64_t n_lines = *n_lines_p;
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
@@ -236,9 +261,33 @@ __global__ __launch_bounds__(256) void k_ld_parse(const char *__restrict__ buf, 
                 int8_t *row = G + li * (uint64_t)a.kpad;
                 const int64_t S = t[8] + 1;
                 LdStats st;
-                LdOp op{row, S, a.ns};
-                if (gt_fast<6>(buf, S, le, op)) st = op.st;  // (six 1 KiB steps in flight, as the walks)
-                else {
+                bool fast;
+                if (a.ns <= kLdLdsRow) {  // codes composed in LDS, then 16 B stores
+                    LdOpL op{(__attribute__((address_space(3))) int8_t *)lrow, S, a.ns};
+                    fast = gt_fast<6>(buf, S, le, op);  // (six 1 KiB steps in flight, as the walks)
+                    if (fast) {
+                        st = op.st;
+                        const int64_t nr = (le - S + 1) / 4;
+                        const uint32_t nout = (uint32_t)(nr < a.ns ? nr : a.ns);
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                        for (uint32_t o = (uint32_t)lane() * 16; o < nout; o += kWave * 16) {
+                            if (o + 16 <= nout)
+                                *reinterpret_cast<uint4 *>(row + o) = *reinterpret_cast<const uint4 *>(lrow + o);
+                            else
+                                for (uint32_t q = o; q < nout; q++) row[q] = lrow[q];
+                        }
+                        // the next line's byte writes must not pass these reads
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                } else {
+                    LdOp op{row, S, a.ns};
+                    fast = gt_fast<6>(buf, S, le, op);
+                    if (fast) st = op.st;
+                }
+                if (!fast) {
                     // rewrite the row: the failed fast sweep may have stored codes
                     for (int k = lane(); k < a.kpad; k += kWave) row[k] = -1;
                     ld_general(buf, S, le, a.ns, row, st, a.stoi_mode);
