@@ -93,7 +93,7 @@ struct DoseCountOp {
     }
 };
 
-enum : uint8_t { kDoseSkip = 0, kDoseRow = 1, kDoseWarn = 3 };
+enum : uint8_t { kDoseSkip = 0, kDoseRow = 1, kDoseWarn = 3, kDosePend = 0xFE };
 enum : uint8_t { kDoseFast = 1, kDoseGeneral = 2, kDoseNA = 3, kDoseNoSamples = 4 };
 
 // per line: status, row length, and how pass 2 writes it (kind, GT index, sample start)
@@ -107,6 +107,10 @@ struct DoseMeta {
     uint8_t pad[2];
 };
 
+// kFast: the first pass -- fixed-stride records (and the head-only kinds) only; any other
+// record is left kDosePend for the second pass (kFast = false, which skips every other line),
+// so the first pass carries none of the general parsers' registers (occupancy)
+template <bool kFast>
 __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restrict__ buf, int64_t data_start,
                                                            const uint64_t *__restrict__ line_end,
                                                            const uint64_t *n_lines_p, int mode,
@@ -121,6 +125,7 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
     uint32_t rows = 0, warns = 0, gen = 0;  // (wave-uniform)
     for (uint64_t li = wid; li < n_lines; li += nw) {
+        if (!kFast && status[li] != kDosePend) continue;  // (wave-uniform)
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
         int64_t ae = le;
         if (mode == 0 && ae > ls && byte_at(buf, ae - 1) == '\r') ae--;
@@ -150,7 +155,8 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
                     bool fast = gi == 0 && gt_fast(buf, S, ae, op);
                     m.kind = kDoseFast;
                     m.plain = fast && op.na == 0;
-                    if (!fast) {
+                    if (kFast && !fast) st = kDosePend;
+                    else if (!fast) {
                         m.kind = kDoseGeneral;
                         op = DoseCountOp{buf, ae, gi};
                         if (!(gi == 0 && gt_first_known(buf, S, ae, op))) {
@@ -159,7 +165,7 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
                         }
                         gen++;
                     }
-                    L = (uint64_t)m.pre + 2u * op.ns + op.na;  // dosages + separators / '\n'
+                    if (st != kDosePend) L = (uint64_t)m.pre + 2u * op.ns + op.na;  // dosages + separators / '\n'
                 }
             }
         }
@@ -377,9 +383,11 @@ hipError_t launch_dose_len(const char *buf, int64_t data_start, const uint64_t *
                            uint64_t n_lines_host, int mode, uint8_t *status, uint64_t *len, void *meta,
                            unsigned long long *counters, hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
-    hipLaunchKernelGGL(k_dose_len, dim3(dose_grid((int64_t)n_lines_host, kDoseWaves, 2048)), dim3(kDoseThreads), 0, s,
-                       buf, data_start, line_end, n_lines_dev, mode, status, len, static_cast<DoseMeta *>(meta),
-                       counters);
+    const dim3 g(dose_grid((int64_t)n_lines_host, kDoseWaves, 2048));
+    hipLaunchKernelGGL(k_dose_len<true>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode,
+                       status, len, static_cast<DoseMeta *>(meta), counters);
+    hipLaunchKernelGGL(k_dose_len<false>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode,
+                       status, len, static_cast<DoseMeta *>(meta), counters);
     return hipGetLastError();
 }
 
