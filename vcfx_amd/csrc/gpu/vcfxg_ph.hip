@@ -108,6 +108,11 @@ struct PhLine {
     uint32_t pad;
 };
 
+// kFast: the first pass -- fixed-stride records composed in LDS (and every head-only status);
+// any other record is left kPhPend for the second pass (kFast = false, which skips every other
+// line), so the first pass carries none of the per-sample-start parser's registers
+constexpr uint8_t kPhPend = 0xFE;
+template <bool kFast>
 __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict__ buf, int64_t data_start,
                                                          const uint64_t *__restrict__ line_end,
                                                          const uint64_t *n_lines_p, int mode, uint32_t kpad,
@@ -125,6 +130,7 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
     for (uint64_t li = wid; li < n_lines; li += nw) {
+        if (!kFast && status[li] != kPhPend) continue;  // (wave-uniform)
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
         uint8_t st = kPhSkip;
         PhLine m{};
@@ -180,12 +186,14 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
                                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                                 __builtin_amdgcn_wave_barrier();
                             }
-                        } else if (fixed) {
+                        } else if (!kFast && fixed) {
                             PhOp op{row, S};
                             swept = gt_fast(buf, S, ae, op);
                         }
                         if (swept)
                             m.ns = (uint32_t)((L + 1) / 4);
+                        else if (kFast)
+                            st = kPhPend;
                         else {
                             // a lane per sample start; sample k = its rank among the starts
                             uint32_t cnt = 0;
@@ -375,8 +383,11 @@ hipError_t launch_ph_lines(const char *buf, int64_t data_start, const uint64_t *
     int64_t g = ((int64_t)n_lines_host + kPhWaves - 1) / kPhWaves;
     if (g > 4096) g = 4096;
     // (a record's sweep with 8 KiB-steps in flight per wave measured the same as 4: r02)
-    hipLaunchKernelGGL(k_ph_lines, dim3((unsigned)g), dim3(kPhThreads), 0, s, buf, data_start, line_end, n_lines_dev,
-                       mode, kpad, G, status, isvar, static_cast<PhLine *>(info), counters);
+    hipLaunchKernelGGL(k_ph_lines<true>, dim3((unsigned)g), dim3(kPhThreads), 0, s, buf, data_start, line_end,
+                       n_lines_dev, mode, kpad, G, status, isvar, static_cast<PhLine *>(info), counters);
+    hipLaunchKernelGGL(k_ph_lines<false>, dim3((unsigned)std::min<int64_t>(g, 2048)), dim3(kPhThreads), 0, s, buf,
+                       data_start, line_end, n_lines_dev, mode, kpad, G, status, isvar,
+                       static_cast<PhLine *>(info), counters);
     return hipGetLastError();
 }
 
