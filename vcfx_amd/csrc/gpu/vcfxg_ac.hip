@@ -28,7 +28,7 @@
 
 namespace vcfxg {
 
-constexpr int kAcThreads = 256;
+constexpr int kAcThreads = 512;  // 8 waves share one LDS copy of the selection (r02: 256 -> 512)
 constexpr int kAcWaves = kAcThreads / kWave;
 constexpr int kAcTile = 4096;  // LDS bytes per wave for one tile of 64 text rows
 constexpr int kAcPre = 256;    // LDS bytes per wave for the record's prefix
