@@ -30,7 +30,7 @@ namespace vcfxg {
 
 constexpr int kAcThreads = 512;  // 8 waves share one LDS copy of the selection (r02: 256 -> 512)
 constexpr int kAcWaves = kAcThreads / kWave;
-constexpr int kAcTile = 4096;  // LDS bytes per wave for one tile of 64 text rows
+constexpr int kAcTile = 3072;  // LDS bytes per wave for one tile of 64 text rows (longer: straight out)
 constexpr int kAcPre = 256;    // LDS bytes per wave for the record's prefix
 
 enum : uint8_t { kAcFast = 1, kAcGeneral = 2 };
@@ -54,6 +54,7 @@ struct AcArgs {
     uint32_t m, scap;      // slots; sample starts a line needs (max index + 1)
     int seq, kind;
     uint32_t sel_lds;      // k_ac_fmt: the selection (eff, name offsets, names) copied to LDS (its bytes; 0: read from global memory)
+    uint32_t ident;        // k_ac_fmt: eff[i] == i for every slot (no index array in LDS)
 };
 
 struct AcNullOp {
@@ -288,17 +289,17 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
     // the selection in LDS when it fits (the text rows read a slot's sample index, name offset and
     // name bytes for every row: LDS reads instead of chains of dependent global loads)
     extern __shared__ __attribute__((aligned(16))) char sel_all[];
-    uint32_t *s_eff = reinterpret_cast<uint32_t *>(sel_all), *s_noff = s_eff + A.m;
+    uint32_t *s_eff = reinterpret_cast<uint32_t *>(sel_all), *s_noff = s_eff + (A.ident ? 0u : A.m);
     char *s_names = reinterpret_cast<char *>(s_noff + A.m + 1);
     if (A.sel_lds) {
         for (uint32_t k = threadIdx.x; k <= A.m; k += blockDim.x) {
-            if (k < A.m) s_eff[k] = A.eff[k];
+            if (k < A.m && !A.ident) s_eff[k] = A.eff[k];
             s_noff[k] = (uint32_t)A.noff[k];
         }
         for (uint64_t k = threadIdx.x; k < A.noff[A.m]; k += blockDim.x) s_names[k] = A.names[k];
         __syncthreads();
     }
-    auto EFF = [&](uint32_t i) -> uint32_t { return A.sel_lds ? s_eff[i] : A.eff[i]; };
+    auto EFF = [&](uint32_t i) -> uint32_t { return A.ident ? i : A.sel_lds ? s_eff[i] : A.eff[i]; };
     auto NOFF = [&](uint32_t i) -> uint64_t { return A.sel_lds ? (uint64_t)s_noff[i] : A.noff[i]; };
     auto NAME = [&](uint64_t k) -> char { return A.sel_lds ? s_names[k] : A.names[k]; };
     char *tile = tile_all[threadIdx.x / kWave];
@@ -444,8 +445,9 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
 size_t ac_meta_bytes() { return sizeof(AcMeta); }
 
 static AcArgs ac_args(const uint32_t *eff, const uint64_t *noff, const char *names, uint32_t *scratch, uint32_t m,
-                      uint32_t scap, int seq, int kind, uint32_t sel_lds = 0) {
+                      uint32_t scap, int seq, int kind, uint32_t sel_lds = 0, int ident = 0) {
     AcArgs A;
+    A.ident = ident ? 1u : 0u;
     A.eff = eff;
     A.noff = noff;
     A.names = names;
@@ -472,10 +474,11 @@ hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *li
 hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
                          uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint32_t sel_lds,
-                         const uint8_t *status, const void *meta, const uint64_t *off, char *out, hipStream_t s) {
+                         int ident, const uint8_t *status, const void *meta, const uint64_t *off, char *out,
+                         hipStream_t s) {
     if (l1 <= l0) return hipSuccess;
     hipLaunchKernelGGL(k_ac_fmt, dim3(blocks), dim3(kAcThreads), sel_lds, s, buf, data_start, line_end, l0, l1,
-                       ac_args(eff, noff, names, scratch, m, scap, seq, kind, sel_lds), status,
+                       ac_args(eff, noff, names, scratch, m, scap, seq, kind, sel_lds, ident), status,
                        static_cast<const AcMeta *>(meta), off, out);
     return hipGetLastError();
 }

@@ -1441,7 +1441,10 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
     const uint64_t scap = (uint64_t)mx + 1;
     // the selection in k_ac_fmt's LDS when it fits in 40 KiB (the sample indices, 32-bit name
     // offsets and the names); VCFXG_AC_SEL_GLOBAL=1 keeps it in global memory (test hook)
-    const uint64_t sel_bytes = ((4 * m + 4 * (m + 1) + (p->name_off[m] - p->name_off[0]) + 15) / 16) * 16;
+    // an identity selection (slot i reads sample i: every sample, in order) keeps no index array
+    bool ident = true;
+    for (uint64_t i = 0; i < m && ident; i++) ident = c->ac_eff_host[i] == i;
+    const uint64_t sel_bytes = (((ident ? 0 : 4 * m) + 4 * (m + 1) + (p->name_off[m] - p->name_off[0]) + 15) / 16) * 16;
     const uint32_t sel_lds = sel_bytes <= 40960 && !getenv("VCFXG_AC_SEL_GLOBAL") ? (uint32_t)sel_bytes : 0u;
     // grid: a wave per line up to 2048 blocks, and at most 1 GiB of per-wave sample tables
     const uint64_t waves_per_block = (uint64_t)(vcfxg::ac_threads() / 64);
@@ -1480,7 +1483,8 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
     HIPCHK(c, vcfxg::launch_ac_fmt(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, (unsigned)blocks,
                                    P<uint32_t>(c->ac_eff), P<uint64_t>(c->ac_noff), P<char>(c->ac_names),
                                    P<uint32_t>(c->ac_scratch), (uint32_t)m, (uint32_t)scap, p->seq, p->kind, sel_lds,
-                                   P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
+                                   ident ? 1 : 0, P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->rowoff),
+                                   P<char>(c->text),
                                    c->stream));
     prof_end(c, "ac_fmt");
     HIPCHK(c, hipStreamSynchronize(c->stream));

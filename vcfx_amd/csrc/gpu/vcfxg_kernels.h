@@ -174,7 +174,8 @@ hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *li
 hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
                          uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint32_t sel_lds,
-                         const uint8_t *status, const void *meta, const uint64_t *off, char *out, hipStream_t s);
+                         int ident, const uint8_t *status, const void *meta, const uint64_t *off, char *out,
+                         hipStream_t s);
 // VCFX_haplotype_phaser (vcfxg_ph.hip): per line status (kPh*), the variants' genotype codes
 // (row = line, kpad bytes; counters[3] = the largest sample count past kpad), the variant ->
 // line compaction, per variant the pair flags with its predecessor (bit 0 the block rule
