@@ -109,3 +109,26 @@ def test_allele_counter_selection_in_global_memory(oracle, tmp_path, monkeypatch
     for argv in ([T, "-q", "-i", str(path)], [T, "-q", "-l", "9", "-i", str(path)]):
         _check(oracle, argv)
     _check(oracle, [T, "-q"], buf)
+
+
+def test_allele_counter_long_rows_and_identity_selection(oracle, tmp_path):
+    """Text rows composed in 3 KiB LDS tiles (64 rows of up to 48 bytes) next to records whose
+    rows are longer (IDs of 20..200 bytes: written straight out), under the identity selection
+    (every sample in order: no index array in LDS) and a reordered one (the index array)."""
+    import random
+    buf = synth.generate(n_records=160, n_samples=70, seed=106)
+    rnd = random.Random(106)
+    lines = buf.split(b"\n")
+    for k, ln in enumerate(lines):
+        if ln and not ln.startswith(b"#") and rnd.random() < 0.4:
+            f = ln.split(b"\t")
+            f[2] = b"id%d_" % k + b"y" * rnd.randint(20, 200)
+            lines[k] = b"\t".join(f)
+    buf = b"\n".join(lines)
+    path = tmp_path / "in.vcf"
+    path.write_bytes(buf)
+    p = str(path)
+    nm = _names(buf)
+    T = "VCFX_allele_counter"
+    for argv in ([T, "-q", "-i", p], [T, "-q", "-s", " ".join(nm[::-1]), "-i", p], [T, "-q", "-s", " ".join(nm), "-i", p]):
+        _check(oracle, argv)
