@@ -1400,7 +1400,7 @@ int vcfxg_dosage_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary
     prof_begin(c, "dose_fmt");
     HIPCHK(c, vcfxg::launch_dose_fmt(buf, (int64_t)data_start, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L,
                                      P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
-                                     ~0ull, c->stream));
+                                     ~0ull, tail[2], c->stream));
     prof_end(c, "dose_fmt");
     HIPCHK(c, hipStreamSynchronize(c->stream));
     prof_collect(c);

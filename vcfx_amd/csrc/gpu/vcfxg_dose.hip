@@ -118,12 +118,12 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
                                                            DoseMeta *__restrict__ meta,
                                                            unsigned long long *__restrict__ counters) {
     __shared__ int64_t scratch[kDoseWaves][16];
-    __shared__ uint32_t red[3][kDoseWaves];
+    __shared__ uint32_t red[4][kDoseWaves];
     int64_t *lds = scratch[threadIdx.x / kWave];
     const uint64_t n_lines = *n_lines_p;
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
-    uint32_t rows = 0, warns = 0, gen = 0;  // (wave-uniform)
+    uint32_t rows = 0, warns = 0, gen = 0, slow = 0;  // (wave-uniform; slow: rows not kDoseFast)
     for (uint64_t li = wid; li < n_lines; li += nw) {
         if (!kFast && status[li] != kDosePend) continue;  // (wave-uniform)
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
             }
         }
         rows += st == kDoseRow;
+        slow += st == kDoseRow && m.kind != kDoseFast;
         warns += st == kDoseWarn;
         if (lane() == 0) {
             status[li] = st;
@@ -182,12 +183,13 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
         red[0][threadIdx.x / kWave] = rows;
         red[1][threadIdx.x / kWave] = warns;
         red[2][threadIdx.x / kWave] = gen;
+        red[3][threadIdx.x / kWave] = slow;
     }
     __syncthreads();
-    if (threadIdx.x < 3) {
+    if (threadIdx.x < 4) {  // counters: rows, rows k_dose_fmt<false> writes, warnings, general
         uint32_t t = 0;
         for (int k = 0; k < kDoseWaves; k++) t += red[threadIdx.x][k];
-        const int slot = threadIdx.x == 0 ? 0 : threadIdx.x == 1 ? 2 : 3;
+        const int slot = threadIdx.x == 0 ? 0 : threadIdx.x == 1 ? 2 : threadIdx.x == 2 ? 3 : 1;
         if (t) atomicAdd(&counters[slot], (unsigned long long)t);
     }
 }
@@ -203,6 +205,9 @@ __device__ __forceinline__ void put_dose(char *o, int d, bool last) {
     }
 }
 
+// kFast: the fixed-stride records only (m.kind == kDoseFast); the other launch takes every
+// other row kind, so the fixed-stride pass carries none of the general placement's registers
+template <bool kFast>
 __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restrict__ buf, int64_t data_start,
                                                            const uint64_t *__restrict__ line_end,
                                                            const uint64_t *n_lines_p,
@@ -217,6 +222,7 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
         if (status[li] != kDoseRow || off[li + 1] > cap) continue;  // (wave-uniform)
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
         const DoseMeta m = meta[li];
+        if ((m.kind == kDoseFast) != kFast) continue;  // (wave-uniform)
         char *o = out + off[li];
         for (uint32_t k = lane(); k < m.pre; k += kWave) o[k] = buf[ls + k];
         o += m.pre;
@@ -393,11 +399,14 @@ hipError_t launch_dose_len(const char *buf, int64_t data_start, const uint64_t *
 
 hipError_t launch_dose_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, const uint8_t *status, const void *meta, const uint64_t *off,
-                           char *out, uint64_t cap, hipStream_t s) {
+                           char *out, uint64_t cap, uint64_t slow_rows, hipStream_t s) {
     if (!n_lines_host) return hipSuccess;
-    hipLaunchKernelGGL(k_dose_fmt, dim3(dose_grid((int64_t)n_lines_host, kDoseWaves, 2048)), dim3(kDoseThreads), 0, s,
-                       buf, data_start, line_end, n_lines_dev, status, static_cast<const DoseMeta *>(meta), off, out,
-                       cap);
+    const dim3 g(dose_grid((int64_t)n_lines_host, kDoseWaves, 2048));
+    hipLaunchKernelGGL(k_dose_fmt<true>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev, status,
+                       static_cast<const DoseMeta *>(meta), off, out, cap);
+    if (slow_rows)  // (k_dose_len counted them: no pass over every line for nothing)
+        hipLaunchKernelGGL(k_dose_fmt<false>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                           status, static_cast<const DoseMeta *>(meta), off, out, cap);
     return hipGetLastError();
 }
 

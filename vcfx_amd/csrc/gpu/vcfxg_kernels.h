@@ -150,7 +150,7 @@ hipError_t launch_dose_len(const char *buf, int64_t data_start, const uint64_t *
                            unsigned long long *counters, hipStream_t s);
 hipError_t launch_dose_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, const uint8_t *status, const void *meta, const uint64_t *off,
-                           char *out, uint64_t cap, hipStream_t s);
+                           char *out, uint64_t cap, uint64_t slow_rows, hipStream_t s);
 // VCFX_missing_detector (vcfxg_md.hip) over the indexed lines: per line status (0 empty, 4 '#',
 // 1 kept as is, kMdFlag flagged) and the flagged lines' INFO span relative to the line start;
 // counters [0] data lines, [1] flagged, [2] lines ending in '\n' with a '.' in their samples;
