@@ -81,3 +81,24 @@ $(B)/libvcfx_synth.so: vcfx_amd/csrc/synth/vcfx_synth.c
 clean:
 	rm -rf $(B)
 .PHONY: all clean
+
+# host sanitizer builds (SURVEY §5 race detection): the input layer (hostio.cpp, gz.cpp:
+# page-population, BGZF inflate, pipe reader threads) under ASan+UBSan and under TSan, and the
+# vcfx:: core API under ASan+UBSan; run by tests/test_sanitize.py.  Host code only -- no GPU
+# sanitizer on this pool.
+SAN := $(B)/san
+SANFLAGS := -O1 -g -fno-omit-frame-pointer -std=c++17 -Iinclude -I$(HOST_SRC)
+SAN_HOST_SRC := tests/host_san_test.cpp $(HOST_SRC)/hostio.cpp $(HOST_SRC)/gz.cpp
+sanitize: $(SAN)/host_san_asan $(SAN)/host_san_tsan $(SAN)/core_api_asan
+$(SAN)/host_san_asan: $(SAN_HOST_SRC) $(wildcard $(HOST_SRC)/*.h) $(B)/libvcfx_gpu.so
+	@mkdir -p $(dir $@)
+	$(CXX) $(SANFLAGS) -fsanitize=address,undefined -fno-sanitize-recover=undefined -o $@ $(SAN_HOST_SRC) \
+	    -L$(B) -lvcfx_gpu -lz -lpthread -Wl,-rpath,'$$ORIGIN/..'
+$(SAN)/host_san_tsan: $(SAN_HOST_SRC) $(wildcard $(HOST_SRC)/*.h) $(B)/libvcfx_gpu.so
+	@mkdir -p $(dir $@)
+	$(CXX) $(SANFLAGS) -fsanitize=thread -o $@ $(SAN_HOST_SRC) -L$(B) -lvcfx_gpu -lz -lpthread -Wl,-rpath,'$$ORIGIN/..'
+$(SAN)/core_api_asan: tests/core_api_test.cpp $(HOST_SRC)/vcfx_core.cpp include/vcfx_core.h include/vcfx_io.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(SANFLAGS) -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+	    -o $@ tests/core_api_test.cpp $(HOST_SRC)/vcfx_core.cpp -lz
+.PHONY: sanitize

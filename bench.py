@@ -9,9 +9,10 @@ Workloads (BASELINE.json configs; the default is the headline one):
             (af_records = head pass + fixed-stride sample sweep + rare full-path lines) and
             device formatted output rows (af_rows + af_format); for N > 1 ranks also all-reduce
             the step's global counts over RCCL.
-  pipeline  configs[2]: VCFX_record_filter --filter "QUAL>=30;FILTER==PASS" |
-            VCFX_genotype_query --genotype-query "0|1" fused on the device (index + one
-            filter_query pass), same shard.
+  pipeline  configs[2] as SURVEY §8(d) defines it: VCFX_record_filter --filter
+            "FILTER==PASS;AF>=0.01" | VCFX_genotype_query -g 0/1 fused on the device (one walk:
+            the filter's INFO key lookup + the genotype query), on the annotated shard
+            (INFO=AF=..;DP=.., seed 20251227+rank).
   ld        configs[4]: VCFX_ld_calculator streaming, 100,000-variant window over a
             100,000-variant x 2,504-sample shard (haplotype-block LD structure) with -t 0.5:
             parse + FP4-MFMA pair sums (exact for 0/1/2 dosages; count pass and emit pass) +
@@ -19,7 +20,8 @@ Workloads (BASELINE.json configs; the default is the headline one):
 
 value = units processed by all ranks / max-over-ranks wall time of the K timed steps
 (inputs already resident in HBM).  One process per GPU (torchrun), record-sharded with
-seed = base + rank: weak scaling.  Rank 0 prints ONE JSON line (contract: DESIGN.md
+seed = base + rank: weak scaling.  `--gpus N` without a torchrun environment launches the N
+ranks itself (torch.distributed.run, 127.0.0.1) before anything touches the GPU.  Rank 0 prints ONE JSON line (contract: DESIGN.md
 §Measurement) carrying `roofline` for the dominant kernel (HIP-event timing on the engine's
 own stream, algorithmic bytes or ops per launch), `cpu_baseline` (the reference's own tools
 compiled from its sources, else the oracle/ C restatement, on a bounded sample, 1 core),
@@ -70,6 +72,31 @@ def parse():
     return a
 
 
+def input_params(a, rank):
+    """vcfx_synth parameters of this rank's shard (the keys of full_digests.json "inputs")"""
+    p = dict(n_records=a.records, n_samples=a.samples, seed=20251226 + rank)
+    if a.workload == "pipeline":
+        p.update(seed=20251227 + rank, info_mode=1)  # the annotated shard: INFO AF=..;DP=..
+    if a.workload == "ld":
+        p["hap_blocks"] = 1
+    if a.missing_rate > 0:
+        p["missing_rate"] = a.missing_rate
+    if a.irregular_rate > 0:
+        p["irregular_rate"] = a.irregular_rate
+    if a.format == "gt:ad:dp":
+        p["format_mode"] = 1
+    return p
+
+
+_SYNTH_DEFAULTS = dict(seed=20251226, info_mode=0, missing_rate=0.0, hap_blocks=0, irregular_rate=0.0, crlf=0,
+                       format_mode=0)
+
+
+def _same_input(p, q):
+    full = lambda d: dict(_SYNTH_DEFAULTS, **d)  # noqa: E731
+    return full(p) == full(q)
+
+
 def pmc_traffic(workload, kernel):
     """HBM bytes per launch of `kernel` from the committed PMC pass (profiles/pmc_traffic.json,
     written by tools/pmc_traffic.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs,
@@ -83,6 +110,8 @@ def pmc_traffic(workload, kernel):
 
 
 REF_DIR = os.path.join(REPO, "oracle", "_ref")
+# configs[2] as SURVEY §8(d) states it
+PIPE_FILTER, PIPE_QUERY = "FILTER==PASS;AF>=0.01", "0/1"
 
 
 def _timed_chain(argvs, budget_s, reference):
@@ -147,8 +176,8 @@ def cpu_baseline(workload, arr, offs, a):
             argvs = [["VCFX_haplotype_phaser", "-q", "-i", f.name]]
             desc = "VCFX_haplotype_phaser -q -i (file path, default mode, threshold 0.8)"
         elif workload == "pipeline":
-            argvs = [["VCFX_record_filter", "--filter", "QUAL>=30;FILTER==PASS", "-i", f.name],
-                     ["VCFX_genotype_query", "--genotype-query", "0|1"]]
+            argvs = [["VCFX_record_filter", "--filter", PIPE_FILTER, "-i", f.name],
+                     ["VCFX_genotype_query", "-g", PIPE_QUERY]]
             desc = "VCFX_record_filter -i | VCFX_genotype_query (stdin)"
         else:
             argvs = [["VCFX_ld_calculator", "-q", "-w", str(nvar), "-t", str(a.threshold), "-i", f.name]]
@@ -192,12 +221,25 @@ def _ph_blocks_sha(arr, flags, off, text):
     return h.hexdigest()
 
 
+# per workload: the reference cases whose command is the bench step's (the first whose input
+# is this rank's shard is checked)
+_CHECK_CASES = {
+    "af": ("af_file", "af_file_miss", "af_file_irreg", "af_file_gtadp"),
+    "pipeline": ("pipeline_annot", "pipeline_annot_miss", "pipeline_annot_gtadp"),
+    "nonref": ("nonref_file",), "hwe": ("hwe_file",), "dose": ("dose_file",), "ac": ("ac_bin_file",),
+    "md": ("md_file",), "ph": ("ph_file",),
+    "ld": ("ld20k_bench", "ld3000_bench"),
+}
+
+
 def output_check(workload, eng, s, a, rank, arr=None):
-    """The last timed step's output against the REFERENCE's, on rank 0 at the BASELINE sizes:
-    the digests tests/golden/full_digests.json holds for this exact synthetic input (made by
-    running the reference binaries on it).  AF: sha256 of the formatted rows; pipeline /
-    nonref: sha256 of the kept-record bitmap; LD: the first 3,000 variants' pairs (their pairs
-    are the first lines of the stream at a window >= 3,000).  A mismatch raises."""
+    """The last timed step's output against the REFERENCE's, on rank 0: the digests
+    tests/golden/full_digests.json holds for this exact synthetic input (made by running the
+    reference binaries on it; every data shape bench.py can generate that has a digest: the
+    chr21-like shard, its missing-call, irregular-record and GT:AD:DP forms, the annotated
+    shard and its forms).  AF / DOSE / HWE: sha256 of the formatted rows; pipeline / nonref:
+    sha256 of the kept-record bitmap; LD: the first 20,000 variants' pairs (the first lines of
+    the stream at a window >= 20,000: 2.0e8 window pairs).  A mismatch raises."""
     import hashlib
     import numpy as np
     try:
@@ -205,15 +247,26 @@ def output_check(workload, eng, s, a, rank, arr=None):
             dig = json.load(f)
     except OSError:
         return {"checked": False, "why": "no tests/golden/full_digests.json"}
-    default = {"af": 427409, "pipeline": 427409, "nonref": 427409, "hwe": 427409, "dose": 427409, "ac": 427409,
-               "md": 427409, "ph": 427409, "ld": 100000}[workload]
-    if a.format != "gt" or a.missing_rate > 0 or a.irregular_rate > 0:
-        return {"checked": False, "why": "no reference digest for the general-path data"}
-    if rank != 0 or a.records != default or a.samples != 2504 or (workload == "ld" and (a.window < 3000 or
-                                                                                         a.threshold != 0.5)):
-        return {"checked": False, "why": "no reference digest for this rank/configuration"}
+    mine = input_params(a, rank)
+    case = None
+    for nm in _CHECK_CASES[workload]:
+        c = dig["cases"].get(nm)
+        if c is None:
+            continue
+        want_in = dict(dig["inputs"][c["input"]])
+        if workload == "ld":  # a prefix of the shard: its first n variants' pairs lead the stream
+            if want_in["n_records"] > a.records or a.window < want_in["n_records"] or a.threshold != 0.5:
+                continue
+            want_in["n_records"] = a.records
+        if _same_input(mine, want_in):
+            case = nm
+            break
+    if case is None:
+        return {"checked": False, "why": "no reference digest for this rank's input %s" % json.dumps(mine)}
+    if workload == "md" and case != "md_file":
+        return {"checked": False, "why": "md output assembly is host-side"}
     if workload == "af":
-        c = dig["cases"]["af_file"]
+        c = dig["cases"][case]
         got = hashlib.sha256(b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes)).hexdigest()
         want, what = c["stdout"]["sha256"], "sha256 of the AF rows vs VCFX_allele_freq_calc -q -i (reference)"
     elif workload == "dose":
@@ -263,23 +316,24 @@ def output_check(workload, eng, s, a, rank, arr=None):
         got = hashlib.sha256(b"CHROM\tPOS\tID\tREF\tALT\tHWE_pvalue\n" + eng.text(s.text_bytes)).hexdigest()
         want, what = c["stdout"]["sha256"], "sha256 of the HWE rows vs VCFX_hwe_tester -q -i (reference)"
     elif workload in ("pipeline", "nonref"):
-        c = dig["cases"]["pipeline_bench" if workload == "pipeline" else "nonref_file"]
+        c = dig["cases"][case]
         keep = (eng.statuses(s.n_lines) == 1).astype(np.uint8)
         got = hashlib.sha256(np.packbits(keep).tobytes()).hexdigest()
         want = c["keep_mask_sha256"]
         what = "sha256 of the kept-record bitmap vs the reference's kept records (%s)" % " | ".join(
             st[0] for st in c["stages"])
     else:
-        c = dig["cases"]["ld3000_bench"]
+        c = dig["cases"][case]
         head = b"#VAR1_CHROM\tVAR1_POS\tVAR1_ID\tVAR2_CHROM\tVAR2_POS\tVAR2_ID\tR2\n"
         n = c["stdout"]["len"] - len(head)
         text = eng.text(s[2])
         got = hashlib.sha256(head + text[:n]).hexdigest()
         want = c["stdout"]["sha256"]
-        what = "sha256 of the first 3,000 variants' pair lines vs VCFX_ld_calculator -w 100000 -t 0.5 (reference)"
+        what = "sha256 of the first %d variants' pair lines vs VCFX_ld_calculator -w 100000 -t 0.5 (reference)" % (
+            dig["inputs"][c["input"]]["n_records"])
     if got != want:
         raise AssertionError("bench output differs from the reference: %s (%s != %s)" % (what, got, want))
-    return {"checked": True, "match": True, "what": what}
+    return {"checked": True, "match": True, "case": case, "what": what}
 
 
 PCIE_H2D_GBS = 56.0  # pinned H2D measured on MI355X (tools/microbench/h2d_ingest.cpp; spec Gen5 x16 63 GB/s)
@@ -306,7 +360,7 @@ def e2e_rates(workload, arr, a, offs=None):
     elif workload == "ph":
         tool, args = "VCFX_haplotype_phaser", ["-q"]
     elif workload == "pipeline":
-        tool, args = "VCFX_record_filter", ["--filter", "QUAL>=30;FILTER==PASS"]
+        tool, args = "VCFX_record_filter", ["--filter", PIPE_FILTER]
     else:
         return None
     fd, path = tempfile.mkstemp(suffix=".vcf")  # TMPDIR: a disk-backed file system, page cache warm
@@ -389,9 +443,29 @@ def e2e_rates(workload, arr, a, offs=None):
         os.unlink(path)
 
 
+def launch_ranks(a):
+    """`--gpus N` outside torchrun: start the N ranks as children (torch.distributed.run on
+    127.0.0.1, one process per GPU) and return their exit code.  Nothing here has touched the
+    GPU, and the ranks are children, not an exec of this process."""
+    import socket
+    import subprocess
+    so = socket.socket()
+    so.bind(("127.0.0.1", 0))
+    port = so.getsockname()[1]
+    so.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%d\n" % (a.gpus, world))
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = torch = None
@@ -410,9 +484,7 @@ def main():
 
     ld = a.workload == "ld"
     general = a.format != "gt" or a.missing_rate > 0 or a.irregular_rate > 0
-    arr, offs = synth.generate_array(a.records, a.samples, seed=20251226 + rank, hap_blocks=1 if ld else 0,
-                                     rec_offsets=True, missing_rate=a.missing_rate, irregular_rate=a.irregular_rate,
-                                     format_mode=1 if a.format == "gt:ad:dp" else 0)
+    arr, offs = synth.generate_array(rec_offsets=True, **input_params(a, rank))
     ds = engine.data_start_of(arr[:1 << 20].tobytes(), strip_cr=not ld)
     eng = engine.Engine(local)
     eng.load(arr)
@@ -484,10 +556,11 @@ def main():
             return s
         kern_names = ("line_count", "line_emit", "line_compact", "ph_lines", "ph_pairs", "ph_fmt")
     elif a.workload == "pipeline":
-        crits = [(engine.QUAL, engine.GE, 1, 30.0, "QUAL", ""), (engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS")]
+        # FILTER==PASS;AF>=0.01 as VCFX_record_filter's parseCriteria compiles it
+        crits = [(engine.FILTER, engine.EQ, 0, 0.0, "FILTER", "PASS"), (engine.INFO, engine.GE, 1, 0.01, "AF", "")]
 
         def step():
-            s = eng.filter_query_region(ds, crits, "0|1", and_logic=True, strict=False)  # index + RF + GQ
+            s = eng.filter_query_region(ds, crits, PIPE_QUERY, and_logic=True, strict=False)  # RF + GQ
             if red is not None:
                 allreduce_counts([s.n_lines, s.rows, s.data_lines, s.warn_lines])
             return s
@@ -629,8 +702,8 @@ def main():
         workload = {
             "af": "VCFX_allele_freq_calc -i (file path) on a device-resident %d x %d VCF shard per GPU: index + "
                   "allele counts + formatted rows" % (a.records, a.samples),
-            "pipeline": "VCFX_record_filter --filter 'QUAL>=30;FILTER==PASS' | VCFX_genotype_query "
-                        "--genotype-query '0|1' fused, device-resident %d x %d shard per GPU" % (a.records, a.samples),
+            "pipeline": "VCFX_record_filter --filter '%s' | VCFX_genotype_query -g '%s' fused, device-resident "
+                        "%d x %d annotated shard per GPU" % (PIPE_FILTER, PIPE_QUERY, a.records, a.samples),
             "nonref": "VCFX_nonref_filter -i (file path) on a device-resident %d x %d shard per GPU: the walk "
                       "with the per-record all-samples-hom-ref test" % (a.records, a.samples),
             "hwe": "VCFX_hwe_tester -i (file path) on a device-resident %d x %d shard per GPU: the walk with the "
@@ -659,8 +732,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp4(e2m1)->f32" if ld else "u8",
-            "data": "synthetic: vcfx_synth seed 20251226+rank, chr21-like layout (FORMAT=%s, phased a|b, INFO=.)"
-                    % a.format.upper() + (", founder-haplotype blocks" if ld else ""),
+            "data": "synthetic: vcfx_synth seed %d+rank, chr21-like layout (FORMAT=%s, phased a|b, INFO=%s)"
+                    % (input_params(a, 0)["seed"], a.format.upper(),
+                       "AF=..;DP=.." if a.workload == "pipeline" else ".") + (", founder-haplotype blocks" if ld else ""),
             "config": {"workload": workload, "records_per_gpu": a.records, "samples": a.samples,
                        "bytes_per_gpu": int(arr.size),
                        "parallelism": "record-sharded x%d%s" % (world, ", RCCL all-reduce of global counts"
@@ -675,7 +749,7 @@ def main():
         out["output_check"] = output_check(a.workload, eng, s, a, rank, arr)
         if world == 1 and not a.no_e2e and not general:
             out["e2e"] = e2e_rates(a.workload, arr, a, offs)
-        if not a.no_cpu_baseline:
+        if world == 1 and not a.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(a.workload, arr, offs, a)
         print(json.dumps(out), flush=True)
     eng.close()
@@ -684,4 +758,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -49,6 +49,17 @@ INPUTS = {
     # the chr21-like shard with sparse missing calls (".|." at rate 5e-4: about 70 % of the
     # records carry one) for VCFX_missing_detector's flagging path
     "chr21_miss": dict(n_records=427409, n_samples=2504, seed=20251226, missing_rate=5e-4),
+    # config 5: the first 20,000 variants of the bench's LD shard (1.9995e8 window pairs, every
+    # tile row of the first 20 K rows: the staging and row offsets past 3 K rows, tiles far from
+    # the diagonal)
+    "ld20k": dict(n_records=20000, n_samples=2504, seed=20251226, hap_blocks=1),
+    # the general GT path at BASELINE scale: every record GT:AD:DP (bench.py --format gt:ad:dp)
+    "chr21_gtadp": dict(n_records=427409, n_samples=2504, seed=20251226, format_mode=1),
+    # 5 % of the records in a general-path shape (bench.py --irregular-rate 0.05)
+    "chr21_irreg": dict(n_records=427409, n_samples=2504, seed=20251226, irregular_rate=0.05),
+    # config 3's annotated shard with sparse missing calls
+    "annot_gtadp": dict(n_records=427409, n_samples=2504, seed=20251227, info_mode=1, format_mode=1),
+    "annot_miss": dict(n_records=427409, n_samples=2504, seed=20251227, info_mode=1, missing_rate=5e-4),
 }
 
 AF, RF, GQ, LD, NR, HWE = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query",
@@ -90,6 +101,16 @@ CASES = {
     "ph_stream_stdin": ("chr21", [[PH, "-q", "-s", "-w", "50", "-l", "0.5"]], False),
     "ph_ld3000": ("ld3000", [[PH, "-l", "0.3", "-i", "{F}"]], False),
     "ld3000_bench": ("ld3000", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
+    "ld20k_bench": ("ld20k", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
+    "af_file_miss": ("chr21_miss", [[AF, "-q", "-i", "{F}"]], False),
+    "af_stdin_miss": ("chr21_miss", [[AF, "-q"]], False),
+    "af_file_gtadp": ("chr21_gtadp", [[AF, "-q", "-i", "{F}"]], False),
+    "af_stdin_gtadp": ("chr21_gtadp", [[AF, "-q"]], False),
+    "af_file_irreg": ("chr21_irreg", [[AF, "-q", "-i", "{F}"]], False),
+    "pipeline_annot_miss": ("annot_miss", [[RF, "--filter", "FILTER==PASS;AF>=0.01", "-i", "{F}"],
+                                           [GQ, "-g", "0/1"]], True),
+    "pipeline_annot_gtadp": ("annot_gtadp", [[RF, "--filter", "FILTER==PASS;AF>=0.01", "-i", "{F}"],
+                                             [GQ, "-g", "0/1"]], True),
 }
 
 

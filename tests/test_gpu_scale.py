@@ -145,6 +145,37 @@ def test_missing_shard_matches_reference(inputs, case, stdin):
         inputs.drop("chr21_miss")
 
 
+@pytest.mark.parametrize("case,stdin", [("af_file_miss", "none"), ("af_stdin_miss", "pipe"), ("af_stdin_miss", "file")])
+def test_af_missing_shard_matches_reference(inputs, case, stdin):
+    """AF where ~70 % of the records carry a missing call ('.|.'): the walk's fixed-stride
+    sweep with missing alleles at BASELINE scale"""
+    _check(case, inputs, stdin)
+
+
+def test_af_irregular_shard_matches_reference(inputs):
+    """AF where 5 % of the records take the general GT path (GT:DP, DP:GT, '/', haploid,
+    multi-digit alleles): the walk's leftover lines through gt_first / gt_general"""
+    _check("af_file_irreg", inputs)
+    inputs.drop("chr21_irreg")
+
+
+@pytest.mark.parametrize("case,stdin", [("af_file_gtadp", "none"), ("af_stdin_gtadp", "file")])
+def test_af_gtadp_shard_matches_reference(inputs, case, stdin):
+    """AF on the 13.2 GB shard with every record GT:AD:DP (the general GT path: index sweep +
+    gt_first) at BASELINE scale"""
+    _check(case, inputs, stdin)
+    if stdin == "file":
+        inputs.drop("chr21_gtadp")
+
+
+@pytest.mark.parametrize("case,inp", [("pipeline_annot_miss", "annot_miss"), ("pipeline_annot_gtadp", "annot_gtadp")])
+def test_pipeline_general_shards_match_reference(inputs, case, inp):
+    """config 3's command (FILTER==PASS;AF>=0.01 | -g 0/1) on the annotated shard with sparse
+    missing calls, and on its GT:AD:DP form"""
+    _check(case, inputs)
+    inputs.drop(inp)
+
+
 @pytest.mark.parametrize("case", ["af_file", "pipeline_bench", "hwe_file"])
 def test_bgzf_chr21_matches_reference(inputs, case):
     """the same shard as BGZF (.vcf.gz, made by build/bin/vcfx_bgzf): inflated on the host
@@ -160,7 +191,8 @@ def test_bgzf_chr21_matches_reference(inputs, case):
     assert got == c["stdout"], (case, got, err[-2000:])
 
 
-@pytest.mark.parametrize("case", ["ld1500_t02", "ld1500_t0", "ld1500_w300_t0", "ld3000_bench", "ph_ld3000"])
+@pytest.mark.parametrize("case", ["ld1500_t02", "ld1500_t0", "ld1500_w300_t0", "ld3000_bench", "ph_ld3000",
+                                  "ld20k_bench"])
 def test_ld_matches_reference(inputs, case):
     _check(case, inputs)
 

@@ -6,9 +6,12 @@ reached every rank as a view of its own records.  The stand-in runner applies th
 tools take from VCFX_INPUT_VIEW (header + record range) by writing it to a file, and the
 VCFX_VIEW_SKIP_HEADER rule by stripping the header-only run's output.  The cut logic and the
 getopt-style operand detection are checked directly."""
+import gzip
 import os
 import socket
+import struct
 import tempfile
+import zlib
 
 import numpy as np
 import pytest
@@ -81,6 +84,15 @@ def _run_world(world, cases):
     return got
 
 
+def _bgzf_member(data):
+    """one BGZF member (RFC 1952 + the 'BC' extra subfield holding the member size - 1)"""
+    co = zlib.compressobj(6, zlib.DEFLATED, -15)
+    body = co.compress(data) + co.flush()
+    bsize = 18 + len(body) + 8
+    hdr = b"\x1f\x8b\x08\x04" + bytes(4) + b"\x00\xff" + struct.pack("<H", 6) + b"BC" + struct.pack("<HH", 2, bsize - 1)
+    return hdr + body + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data) & 0xFFFFFFFF)
+
+
 def _files(tmp):
     paths = {}
     head = b"##fileformat=VCFv4.2\n"
@@ -94,9 +106,15 @@ def _files(tmp):
            + b"3\t5\tonly\tseven\tcols\t.\t.\n\n")
     paths["bad"] = bad
     paths["tiny"] = head + b"#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS1\n1\t1\t.\tA\tG\t.\t.\t.\tGT\t0|1\n"
+    # compressed copies (byte cuts of a gzip file are not record cuts): one gzip
+    # member, and BGZF-style 64 KiB members with the BC extra field
+    paths["synth.gz"] = gzip.compress(paths["synth"], mtime=0)
+    raw = paths["synth"]
+    paths["synth.bgz"] = b"".join(_bgzf_member(raw[o:o + 65280]) for o in range(0, len(raw), 65280)) + \
+        _bgzf_member(b"")
     out = {}
     for k, b in paths.items():
-        p = os.path.join(tmp, k + ".vcf")
+        p = os.path.join(tmp, k if k.endswith("gz") else k + ".vcf")
         open(p, "wb").write(b)
         out[k] = p
     return out
@@ -136,6 +154,11 @@ def test_sharded_runs_match_whole_file(files, world):
     for argv in cases:
         by_rank = views[tuple(argv)]
         assert set(by_rank) == set(range(world))
+        if argv[-1].endswith("gz"):
+            # compressed input runs whole on rank 0 (no view), the other ranks run nothing
+            assert shard.plan(argv) is None, argv
+            assert [c[1] for c in by_rank[0]] == [None] and all(not by_rank[r] for r in range(1, world)), argv
+            continue
         meant = shard.plan(argv) in ("af", "vc", "filter") and not (
             argv[0] in ("VCFX_record_filter", "VCFX_genotype_query", "VCFX_nonref_filter", "VCFX_dosage_calculator")
             and "bad" in argv[-1])

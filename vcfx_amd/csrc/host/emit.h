@@ -106,7 +106,9 @@ struct LineSource {
     }
     bool device_only() const { return in.host_n < in.n && !in.tail; }
     bool in_tail = false;
-    // bytes [a, b) of the input, plus the byte at b when b < n (the line's newline)
+    // bytes [a, b) of the input, plus the byte at b when b < n (the line's newline); nullptr
+    // (and ok = false) when the pinned window cannot be allocated or filled: the caller stops
+    // at that line and reports the error, writing nothing from it
     const char *at(uint64_t a, uint64_t b) {
         if (in.tail && a >= in.host_n) {  // a shard view: the record range elsewhere in the mapping
             if (!in_tail) {
@@ -127,13 +129,17 @@ struct LineSource {
                 ok = false;
                 win = nullptr;
                 win_cap = 0;
-                static const char z[1] = {0};
-                return z;
+                w0 = w1 = 0;
+                return nullptr;
             }
             win_cap = want;
         }
         const uint64_t e = std::min<uint64_t>(in.n, a + win_cap);
-        if (vcfxg_input_fetch(g, a, (size_t)(e - a), win) != VCFXG_OK) ok = false;
+        if (vcfxg_input_fetch(g, a, (size_t)(e - a), win) != VCFXG_OK) {
+            ok = false;  // the window's bytes are stale: nothing may be written from them
+            w0 = w1 = 0;
+            return nullptr;
+        }
         w0 = a;
         w1 = e;
         em.rebase(win, (size_t)(e - a));

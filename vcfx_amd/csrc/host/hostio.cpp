@@ -192,9 +192,18 @@ bool gzip_enabled() {
 }
 
 namespace {
+// log2 of the largest address-space reservation tried first (1 TiB; VCFX_RESERVE_LOG2 lowers it
+// for hosts where faults in a huge reservation fail, e.g. under ThreadSanitizer's shadow map)
+int reserve_log2() {
+    const char *e = getenv("VCFX_RESERVE_LOG2");
+    const int v = e ? atoi(e) : 40;
+    return v >= 30 && v <= 40 ? v : 40;
+}
+
 // an anonymous region of reserved address space (not memory), transparent huge pages
 void *reserve_region(size_t *cap) {
     for (int sh : {40, 36, 32, 30}) {
+        if (sh > reserve_log2()) continue;
         *cap = (size_t)1 << sh;
         void *m = mmap(nullptr, *cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
         if (m != MAP_FAILED) {
@@ -208,6 +217,10 @@ void *reserve_region(size_t *cap) {
 }  // namespace
 
 bool Input::decompress(int err_fd) {
+    if (read_errno) {  // a failed read(2) is not the end of the input
+        write_str(err_fd, std::string("Error: vcfx_amd: reading the input failed: ") + strerror(read_errno) + "\n");
+        return false;
+    }
     if (!gzip_ok || gz || host_n != n || !is_gzip(p, n) || !gzip_enabled()) return true;
     join_populate();
     size_t cap = 0;
@@ -279,12 +292,16 @@ void Input::populate(void *m, size_t len) {
 }
 
 namespace {
-ssize_t read_full(int fd, char *dst, size_t want) {
+// want bytes (fewer at EOF); a read error stops it and leaves its errno in *err
+ssize_t read_full(int fd, char *dst, size_t want, int *err) {
     size_t got = 0;
     while (got < want) {
         ssize_t k = ::read(fd, dst + got, want - got);
         if (k < 0 && errno == EINTR) continue;
-        if (k < 0) return got ? (ssize_t)got : -1;
+        if (k < 0) {
+            *err = errno;
+            return got ? (ssize_t)got : -1;
+        }
         if (k == 0) break;
         got += (size_t)k;
     }
@@ -327,6 +344,7 @@ void Input::read_fd(int fd, bool host_copy) {
     size_t cap = 0;
     void *m = MAP_FAILED;
     for (int sh : {40, 36, 32, 30}) {
+        if (sh > reserve_log2()) continue;
         cap = (size_t)1 << sh;
         m = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
         if (m != MAP_FAILED) break;
@@ -340,8 +358,8 @@ void Input::read_fd(int fd, bool host_copy) {
 
     // the head of the stream (up to 2 chunks) always lands in host memory: the '#CHROM' gate
     // runs on it, and small inputs never reach the device
-    const size_t kPre = prefetch_bytes(), kChunk = stream_chunk();
-    ssize_t k0 = read_full(fd, base, kPre);
+    const size_t kPre = std::min(prefetch_bytes(), cap / 4), kChunk = stream_chunk();  // reads stay inside the region
+    ssize_t k0 = read_full(fd, base, kPre, &read_errno);
     size_t got = k0 > 0 ? (size_t)k0 : 0;
     if (gzip_ok && is_gzip(base, got) && gzip_enabled()) {
         // compressed: all of it to the host (decompress() inflates it)
@@ -349,6 +367,7 @@ void Input::read_fd(int fd, bool host_copy) {
             if (cap - got < ((size_t)8 << 20)) break;
             ssize_t k = ::read(fd, base + got, (size_t)8 << 20);
             if (k < 0 && errno == EINTR) continue;
+            if (k < 0) read_errno = errno;
             if (k <= 0) break;
             got += (size_t)k;
         }
@@ -380,6 +399,7 @@ void Input::read_fd(int fd, bool host_copy) {
             if (got >= ((size_t)8 << 30) || cap - got < ((size_t)8 << 20)) break;
             ssize_t k = ::read(fd, base + got, std::min<size_t>((size_t)8 << 20, std::max(kChunk, kPre)));
             if (k < 0 && errno == EINTR) continue;
+            if (k < 0) read_errno = errno;
             if (k <= 0) {
                 n = host_n = got;
                 return;  // EOF: everything is on the host
@@ -412,7 +432,7 @@ void Input::read_fd(int fd, bool host_copy) {
             for (int k = 0; ok; k = (k + 1) % kSlots) {
                 ok = vcfxg_ingest_wait(g, slot_end[k]) == VCFXG_OK;
                 if (!ok) break;
-                ssize_t r = read_full(fd, (char *)ring[k], kSlot);
+                ssize_t r = read_full(fd, (char *)ring[k], kSlot, &read_errno);
                 if (r <= 0) break;
                 ok = vcfxg_ingest(g, (const char *)ring[k], (size_t)r, 0) == VCFXG_OK;
                 total += (size_t)r;
@@ -432,8 +452,8 @@ void Input::read_fd(int fd, bool host_copy) {
     std::atomic<size_t> rd{got};
     std::atomic<bool> done{false};
     const size_t kStep = (size_t)32 << 20, kAhead = (size_t)256 << 20;
-    std::thread pre([&] {
-        size_t pop = got;
+    std::thread pre([&, got0 = got] {  // (got itself keeps changing on this thread: by value)
+        size_t pop = got0;
         while (!done.load(std::memory_order_acquire)) {
             if (pop < rd.load(std::memory_order_acquire) + kAhead && pop + kStep <= cap) {
                 if (madvise(base + pop, kStep, kMadvPopulateWrite) != 0) return;
@@ -474,6 +494,7 @@ void Input::read_fd(int fd, bool host_copy) {
         if (cap - got < ((size_t)8 << 20)) break;  // reservation exhausted (> 1 TiB of stdin)
         ssize_t k = ::read(fd, base + got, (size_t)8 << 20);
         if (k < 0 && errno == EINTR) continue;
+        if (k < 0) read_errno = errno;
         if (k <= 0) break;
         got += (size_t)k;
         rd.store(got, std::memory_order_release);

@@ -40,6 +40,7 @@ struct Input {
     // open_file / read_fd; decompress() then inflates gzip / BGZF input in place
     bool gzip_ok = false;
     bool gz = false;          // the input was inflated
+    int read_errno = 0;       // read_fd stopped on a read(2) error (decompress() reports it)
     size_t source_n = 0;      // bytes of the file / stream as read (compressed size for gz)
     Input() = default;
     Input(const Input &) = delete;
@@ -63,6 +64,7 @@ struct Input {
     // the host): once the head holds the '#CHROM' line the rest of the pipe is read into a
     // pinned staging ring and copied to the device from there, never kept on the host.
     void read_fd(int fd, bool host_copy = true);
+    // A read error of read_fd first: false after "Error: vcfx_amd: reading the input failed".
     // gzip / BGZF input (magic 1f 8b) and gzip_ok, unless VCFX_GZIP=0: inflate it (BGZF members
     // on every host thread) into a reserved region that becomes the input.  false (after an
     // "Error: ..." line on err_fd) when the stream is truncated or corrupt.

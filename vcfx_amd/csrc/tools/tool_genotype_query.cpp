@@ -105,6 +105,7 @@ bool run_gq(const Input &in, bool stream_mode, const std::string &q, bool strict
             const char *a = nullptr, *b = nullptr;
             if (v == VCFXG_LINE_HEADER || v == VCFXG_LINE_ROW || v == VCFXG_LINE_WARN) {
                 a = src.at(prev, ends[i]);
+                if (!a) break;
                 b = a + (ends[i] - prev);
             }
             prev = ends[i] + 1;

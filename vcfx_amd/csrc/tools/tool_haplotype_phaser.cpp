@@ -202,7 +202,9 @@ bool run_ph(const Input &in, Phaser &P) {
         for (uint64_t i = 0; i < nl; i++) {
             const uint8_t s = st[i];
             if (s == kHead) {
-                const char *a = src.at(prev, ends[i]), *b = a + (ends[i] - prev);
+                const char *a = src.at(prev, ends[i]);
+                if (!a) break;
+                const char *b = a + (ends[i] - prev);
                 if (b > a && b[-1] == '\r') --b;
                 P.header_line(a, b);
             } else if (s != 0) {

@@ -109,7 +109,9 @@ bool run_md(const Input &in, bool file, const char *path, bool quiet, int out_fd
         uint64_t prev = ds;
         for (uint64_t i = 0; i < nl; i++) {
             const uint8_t v = st[i];
-            const char *a = src.at(prev, ends[i]), *b = a + (ends[i] - prev);
+            const char *a = src.at(prev, ends[i]);
+            if (!a) break;
+            const char *b = a + (ends[i] - prev);
             if (v == VCFXG_LINE_MISSING) {
                 const char *ae = (file && b > a && b[-1] == '\r') ? b - 1 : b;
                 const char *i0 = a + is[i], *i1 = a + ie[i];

@@ -96,7 +96,9 @@ bool run_nr(const Input &in, bool stream_mode, int out_fd, Out &err) {
             const uint8_t v = st[i];
             if (v == VCFXG_LINE_SKIP) em.raw("\n", 1);  // an empty line
             else if (v == VCFXG_LINE_HEADER || v == VCFXG_LINE_ROW) {
-                const char *a = src.at(prev, ends[i]), *b = a + (ends[i] - prev);
+                const char *a = src.at(prev, ends[i]);
+                if (!a) break;
+                const char *b = a + (ends[i] - prev);
                 em.line(a, bare(a, b));
             }  // VCFXG_LINE_DROP: every sample hom-ref
             prev = ends[i] + 1;

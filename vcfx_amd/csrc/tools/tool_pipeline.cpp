@@ -89,6 +89,7 @@ extern "C" int vcfx_pipeline_filter_query(const char *filter, const char *logic,
             const char *a = nullptr, *b = nullptr;
             if (v == VCFXG_LINE_HEADER || v == VCFXG_LINE_ROW || v == 7) {
                 a = src.at(prev, ends[i]);
+                if (!a) break;
                 b = a + (ends[i] - prev);
             }
             prev = ends[i] + 1;
@@ -102,6 +103,10 @@ extern "C" int vcfx_pipeline_filter_query(const char *filter, const char *logic,
                     err.put("\n");
                 }
             }
+        }
+        if (!src.ok) {
+            em.finish();
+            return gpu_ok(g, VCFXG_E_HIP, "input_fetch", err.fd) ? 0 : 1;
         }
     }
     em.finish();

@@ -169,7 +169,9 @@ bool run_rf(const Input &in, bool stdin_mode, const std::vector<Criterion> &cs, 
         const uint8_t v = st[i];
         if (v == VCFXG_LINE_SKIP) em.raw("\n", 1);
         else if (v == VCFXG_LINE_ROW || v == VCFXG_LINE_HEADER) {
-            const char *a = src.at(prev, ends[i]), *b = a + (ends[i] - prev);
+            const char *a = src.at(prev, ends[i]);
+            if (!a) break;
+            const char *b = a + (ends[i] - prev);
             em.line(a, strip(a, b));
         }
         prev = ends[i] + 1;

@@ -164,6 +164,15 @@ def input_path(tool, argv):
     return path if path and os.path.isfile(path) else None
 
 
+def is_gzip(path):
+    """the gzip magic (1f 8b) at the start of the file: the tools inflate such input whole"""
+    try:
+        with open(path, "rb") as f:
+            return f.read(2) == b"\x1f\x8b"
+    except OSError:
+        return False
+
+
 def _has_flag(tool, argv, *names):
     opts, _ = parse_args(tool, argv)
     return any(n in names for n, _ in opts)
@@ -312,10 +321,6 @@ _VC_WARN = re.compile(rb"^(Warning: skipping line |Error: line )(\d+)( .*\n)", r
 
 def run_vc(argv, comm, runner, path, sink):
     buf = _memmap(path)
-    if len(buf) >= 2 and buf[0] == 0x1F and buf[1] == 0x8B:
-        if comm.rank:
-            return b"", b"", 0
-        return runner(argv, b"")  # gzip input: not shardable by bytes
     cuts = record_cuts(buf, 0, comm.world)
     lo, hi = cuts[comm.rank], cuts[comm.rank + 1]
     out, err, rc = runner(argv, b"", view=(0, lo, hi))
@@ -396,12 +401,17 @@ def plan(argv):
     path = input_path(tool, argv)
     if path is None:
         return None
+    if tool == "VCFX_ld_calculator":
+        # every rank parses the whole (inflated) input and takes a share of the pair rows
+        return None if _has_flag(tool, argv, "-m", "--matrix") else "ld"
+    if is_gzip(path):
+        # gzip / BGZF: the byte cuts of the compressed file are not record cuts, and the tool
+        # inflates its whole input before a view could apply -- run it unsharded on rank 0
+        return None
     if tool == "VCFX_allele_freq_calc":
         return "af"
     if tool == "VCFX_variant_counter":
         return "vc"
-    if tool == "VCFX_ld_calculator":
-        return None if _has_flag(tool, argv, "-m", "--matrix") else "ld"
     return "filter"
 
 
