@@ -228,7 +228,7 @@ _CHECK_CASES = {
     "pipeline": ("pipeline_annot", "pipeline_annot_miss", "pipeline_annot_gtadp"),
     "nonref": ("nonref_file",), "hwe": ("hwe_file",), "dose": ("dose_file",), "ac": ("ac_bin_file",),
     "md": ("md_file",), "ph": ("ph_file",),
-    "ld": ("ld20k_bench", "ld3000_bench"),
+    "ld": ("ld20k_bench", "ld3000_bench", "ld20k_miss_bench"),
 }
 
 
@@ -575,8 +575,8 @@ def main():
             if red is not None:
                 allreduce_counts([m, np_, tb, 0])
             return m, np_, tb
-        kern_names = ("line_count", "line_emit", "line_compact", "ld_parse", "ld_compact", "ld_count", "ld_emit",
-                      "ld_text")
+        kern_names = ("line_count", "line_emit", "line_compact", "ld_parse", "ld_compact", "ld_pack_vq", "ld_count",
+                      "ld_emit", "ld_count_mask", "ld_emit_mask", "ld_count_gen", "ld_emit_gen", "ld_text")
 
     s = None
     for _ in range(a.warmup):
@@ -630,13 +630,22 @@ def main():
         if ld:
             # X.X^T over the window pairs (complete genotypes) on the FP4 MFMA: 2 ops per sample
             # per pair, priced against the dense FP4 peak the kernel's instruction runs at
-            algo = {"ld_count": 2.0 * a.samples * pairs, "ld_emit": 2.0 * a.samples * pairs}
-            dom = "ld_count"
-            ach = algo[dom] / (kernels[dom] * 1e-3) / 1e12
+            # the count kernel of the data: k_ld_fast (complete 256-groups, X.X^T) or, with
+            # missing calls, k_ld_mask (the six masked sums: 6x the executed MFMA ops); the
+            # algorithmic ops are the same 2 N per window pair either way
+            dom = "ld_count_mask" if kernels.get("ld_count_mask", 0) > kernels.get("ld_count", 0) else "ld_count"
+            algo_ops = 2.0 * a.samples * pairs
+            ach = algo_ops / (kernels[dom] * 1e-3) / 1e12
             roof = {"bound": "mfma", "kernel": dom, "achieved": ach, "peak": FP4_PEAK_TOPS, "unit": "TOP/s",
                     "frac": ach / FP4_PEAK_TOPS, "traffic": pmc_traffic("ld", dom),
-                    "algorithmic_ops_per_launch": algo[dom], "avg_launch_ms": kernels[dom]}
-            try:  # MFMA-busy fraction of the SIMD cycles (committed PMC pass, profiles/)
+                    "algorithmic_ops_per_launch": algo_ops, "avg_launch_ms": kernels[dom]}
+            if dom == "ld_count_mask":
+                # executed: 6 products over the 128 x 128 tiles the kernel ran (whole tiles)
+                roof["executed_ops_per_launch"] = 6.0 * algo_ops
+                roof["executed_frac"] = 6.0 * algo_ops / (kernels[dom] * 1e-3) / 1e12 / FP4_PEAK_TOPS
+            try:  # MFMA-busy fraction of the SIMD cycles (committed PMC pass of k_ld_fast, profiles/)
+                if dom != "ld_count":
+                    raise KeyError(dom)
                 with open(MFMA_FILE) as f:
                     m = json.load(f)["mean"]
                 roof["mfma_util_pmc"] = {"util": m["mfma_util"], "clock_ghz": m["clock_ghz"],

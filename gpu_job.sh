@@ -47,12 +47,16 @@ if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
 fi
 
 if [ "$MODE" = rehearse ]; then
-    step rehearse_af 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-        --master-port 29512 bench.py --gpus 2 --steps 3 --warmup 1 --records 50000 --dist-backend gloo \
-        --no-cpu-baseline --no-e2e || exit $?
-    step rehearse_ld 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-        --master-port 29513 bench.py --gpus 2 --workload ld --records 20000 --window 20000 --steps 2 --warmup 1 \
+    # bench.py launches its own ranks for --gpus N (torch.distributed.run on 127.0.0.1); gloo:
+    # both ranks share the one GPU of this box
+    step rehearse_af 600 python bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo || exit $?
+    grep '^{' gpurun_out/rehearse_af.log > gpurun_out/rehearse_af.json
+    step rehearse_ld 600 python bench.py --gpus 2 --workload ld --records 20000 --window 20000 --steps 2 --warmup 1 \
         --dist-backend gloo --no-cpu-baseline --no-e2e || exit $?
+fi
+if [ "$MODE" = scale ]; then  # full-size reference digests (tests/test_gpu_scale.py), optionally -k filtered
+    step pytest_scale 1100 python -u -m pytest tests/test_gpu_scale.py -v -x --timeout 900 --timeout-method thread \
+        ${*:+-k "$*"} || exit $?
 fi
 echo "=== done"
 

@@ -53,6 +53,9 @@ INPUTS = {
     # tile row of the first 20 K rows: the staging and row offsets past 3 K rows, tiles far from
     # the diagonal)
     "ld20k": dict(n_records=20000, n_samples=2504, seed=20251226, hap_blocks=1),
+    # config 5 with missing calls (bench.py --workload ld --missing-rate 0.001: ~8 % of the
+    # variants complete, so nearly every tile takes the masked FP4 kernel)
+    "ld20k_miss": dict(n_records=20000, n_samples=2504, seed=20251226, hap_blocks=1, missing_rate=0.001),
     # the general GT path at BASELINE scale: every record GT:AD:DP (bench.py --format gt:ad:dp)
     "chr21_gtadp": dict(n_records=427409, n_samples=2504, seed=20251226, format_mode=1),
     # 5 % of the records in a general-path shape (bench.py --irregular-rate 0.05)
@@ -102,6 +105,7 @@ CASES = {
     "ph_ld3000": ("ld3000", [[PH, "-l", "0.3", "-i", "{F}"]], False),
     "ld3000_bench": ("ld3000", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
     "ld20k_bench": ("ld20k", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
+    "ld20k_miss_bench": ("ld20k_miss", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
     "af_file_miss": ("chr21_miss", [[AF, "-q", "-i", "{F}"]], False),
     "af_stdin_miss": ("chr21_miss", [[AF, "-q"]], False),
     "af_file_gtadp": ("chr21_gtadp", [[AF, "-q", "-i", "{F}"]], False),

@@ -1,6 +1,7 @@
-"""GPU parity for VCFX_ld_calculator: MFMA pair sums (block-scaled FP4 for complete 256-variant
-groups, int8 for groups with missing calls) + the exact fp64 epilogue against the C oracle's
-computeRsqFast / computeRsq, streaming and matrix modes, both input paths."""
+"""GPU parity for VCFX_ld_calculator: MFMA pair sums (block-scaled FP4: X.X^T for complete
+256-variant groups, the six masked sums for 128-variant tiles with missing calls) + the exact
+fp64 epilogue against the C oracle's computeRsqFast / computeRsq, streaming and matrix modes,
+both input paths."""
 import tempfile
 
 import pytest
@@ -152,3 +153,41 @@ def test_ld_pair_lines_long_and_short_fields(oracle):
             got = tools.run(argv, b"")
             want = oracle.run(argv, b"")
             assert got == want, (a, len(got[0]), len(want[0]))
+
+
+@pytest.mark.parametrize("rate", [0.001, 0.08])
+def test_ld_mask_tiles_missing_calls(oracle, rate):
+    """Missing calls in most variants (per-sample rate 0.1 %: ~8 % of the 2,504-sample variants
+    complete; 8 %: none): the 128 x 128 masked FP4 tiles (n, Sx, Sy, Sxx, Syy, Sxy per pair)
+    next to complete 256-groups, window edges inside and across tiles, thresholds that exercise
+    the fp32 prefilter, threshold 0 (every window pair a candidate) and the distance cap; the
+    same bytes through the previous int8 general kernel (VCFXG_LD_MASK=0, a fresh process)."""
+    import os
+    import subprocess
+    buf = synth.generate(1100, 2504 if rate < 0.01 else 517, 62, 0, rate, 1, 0.0, 0)
+    if rate < 0.01:  # two complete 256-groups among the incomplete ones
+        lines = buf.split(b"\n")
+        data = [k for k, ln in enumerate(lines) if ln and not ln.startswith(b"#")]
+        for k in data[256:768]:
+            f = lines[k].split(b"\t")
+            f[9:] = [b"0|0" if x[:1] == b"." or x[2:3] == b"." else x for x in f[9:]]
+            lines[k] = b"\t".join(f)
+        buf = b"\n".join(lines)
+    with tempfile.NamedTemporaryFile(suffix=".vcf") as f:
+        f.write(buf)
+        f.flush()
+        for a in (["-w", "1100", "-t", "0.5"], ["-w", "300", "-t", "0.2"], ["-w", "129", "-t", "0.0"],
+                  ["-w", "700", "-t", "0.35", "-d", "5000"], ["-w", "64", "-t", "0.05"]):
+            argv = ["VCFX_ld_calculator"] + a + ["-i", f.name]
+            got = tools.run(argv, b"")
+            want = oracle.run(argv, b"")
+            assert got == want, (a, rate, len(got[0]), len(want[0]))
+        argv = ["VCFX_ld_calculator", "-w", "1100", "-t", "0.3", "-i", f.name]
+        old = subprocess.run([tools_binary("VCFX_ld_calculator")] + argv[1:], capture_output=True,
+                             env=dict(os.environ, VCFXG_LD_MASK="0"), timeout=300)
+        assert (old.stdout, old.returncode) == (oracle.run(argv, b"")[0], 0)
+
+
+def tools_binary(t):
+    from vcfx_amd import tool_binary
+    return tool_binary(t)

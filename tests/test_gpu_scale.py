@@ -192,7 +192,7 @@ def test_bgzf_chr21_matches_reference(inputs, case):
 
 
 @pytest.mark.parametrize("case", ["ld1500_t02", "ld1500_t0", "ld1500_w300_t0", "ld3000_bench", "ph_ld3000",
-                                  "ld20k_bench"])
+                                  "ld20k_bench", "ld20k_miss_bench"])
 def test_ld_matches_reference(inputs, case):
     _check(case, inputs)
 

@@ -51,7 +51,8 @@ struct vcfxg_ctx {
     std::string query_host, crit_host, pool_host;  // host sources of in-flight async copies
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
-        ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff;
+        ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff, ld_Gv, ld_Gq;
+    bool ld_vq = false;  // ld_Gv / ld_Gq (valid-mask and squared-dosage FP4 planes) are current
     int n_cu = 0;
     DevBuf async_small;         // asynchronous AF path: line range {0, n}, failure flags, summary
     DevBuf ld_temp, ld_quarters, ld_stage_ctr;  // LD: pairs staged by the count pass
@@ -242,7 +243,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
         if (b->p) (void)hipFree(b->p);
     for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
     for (hipEvent_t e : c->ingest_ev_free) (void)hipEventDestroy(e);
@@ -1802,6 +1803,19 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
     HIPCHK(c, hipStreamSynchronize(c->stream));
     r = ensure(c, c->ld_prefix, pbytes + 16);
     if (r) return r;
+    // a group with a missing genotype: the valid-mask and squared-dosage planes of the
+    // missing-data kernel (k_ld_mask), next to the dosage plane ld_Gp
+    c->ld_vq = false;
+    for (uint64_t g = 0; g * vcfxg::kLdFastBlock < M && !c->ld_vq; g++) c->ld_vq = !c->ld_gflag_host[g];
+    if (c->ld_vq) {
+        r = ensure(c, c->ld_Gv, (size_t)(M + 1) * kp4 + 64);
+        if (!r) r = ensure(c, c->ld_Gq, (size_t)(M + 1) * kp4 + 64);
+        if (r) return r;
+        prof_begin(c, "ld_pack_vq");
+        HIPCHK(c, vcfxg::launch_ld_pack_vq(P<int8_t>(c->ld_Gc), M, kpad, n_samples, P<uint8_t>(c->ld_Gv),
+                                           P<uint8_t>(c->ld_Gq), kp4, c->stream));
+        prof_end(c, "ld_pack_vq");
+    }
     HIPCHK(c, vcfxg::launch_ld_prefix(1, P<vcfxg::LdVar>(c->ld_vars), M, P<char>(c->input), id_dot_to_pos,
                                       P<uint64_t>(c->ld_poff), P<char>(c->ld_prefix), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1915,7 +1929,29 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
             blocks.push_back((uint32_t)J);
         }
     }
-    const uint32_t nbl = (uint32_t)(blocks.size() / 2) - nfast;
+    uint32_t nbl = (uint32_t)(blocks.size() / 2) - nfast;
+    // the missing-data tiles (k_ld_mask, default): every 128 x 128 tile pair in the window
+    // whose 256-groups are not both complete (those are k_ld_fast's), replacing the 64-block
+    // general list (kept for VCFXG_LD_MASK=0)
+    static const bool use_mask = [] {
+        const char *e = getenv("VCFXG_LD_MASK");
+        return !(e && e[0] == '0');
+    }();
+    uint32_t nmask = 0;
+    if (use_mask && c->ld_vq) {
+        blocks.resize(2 * (size_t)nfast);
+        constexpr uint64_t TM = vcfxg::kLdMaskTile, kPerG = vcfxg::kLdFastBlock / vcfxg::kLdMaskTile;
+        for (uint64_t J2 = j0 / TM; J2 * TM < j1; J2++) {
+            const uint64_t I2lo = ifirst(J2 * (TM / BM)) / (TM / BM);  // the first 64-row's window start
+            for (uint64_t I2 = I2lo; I2 <= J2; I2++) {
+                if (gf[I2 / kPerG] && gf[J2 / kPerG]) continue;  // a complete group pair: k_ld_fast
+                blocks.push_back((uint32_t)I2);
+                blocks.push_back((uint32_t)J2);
+            }
+        }
+        nmask = (uint32_t)(blocks.size() / 2) - nfast;
+        nbl = 0;
+    }
     const uint64_t rows = j1 - j0;
     int r = ensure(c, c->ld_blocks, 4 * blocks.size() + 8);
     if (!r) r = ensure(c, c->ld_cnt, 2 * rows * nb + 16);
@@ -1961,6 +1997,11 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     HIPCHK(c, vcfxg::launch_ld_block(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,
                                      P<uint16_t>(c->ld_cnt), vcfxg::LdOffsets{}, nullptr, c->stream));
     prof_end(c, "ld_count_gen");
+    prof_begin(c, "ld_count_mask");
+    HIPCHK(c, vcfxg::launch_ld_mask(1, P<uint8_t>(c->ld_Gp), P<uint8_t>(c->ld_Gv), P<uint8_t>(c->ld_Gq),
+                                    P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nmask, P<uint16_t>(c->ld_cnt),
+                                    vcfxg::LdOffsets{}, nullptr, c->stream));
+    prof_end(c, "ld_count_mask");
     // ordered offsets: per-row scan of the count table (u32 inside a row), then the rows
     uint64_t *rowtot = P<uint64_t>(c->ld_rowoff), *rowbase = rowtot + (rows + 1);
     HIPCHK(c, vcfxg::launch_ld_rowscan(P<uint16_t>(c->ld_cnt), rows, nb, j0, window, P<uint32_t>(c->ld_off), rowtot,
@@ -1997,6 +2038,11 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
                                      P<uint16_t>(c->ld_cnt), offs, P<vcfxg::LdPair>(c->ld_pairs),
                                      c->stream));
     prof_end(c, "ld_emit_gen");
+    prof_begin(c, "ld_emit_mask");
+    HIPCHK(c, vcfxg::launch_ld_mask(2, P<uint8_t>(c->ld_Gp), P<uint8_t>(c->ld_Gv), P<uint8_t>(c->ld_Gq),
+                                    P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nmask, P<uint16_t>(c->ld_cnt), offs,
+                                    P<vcfxg::LdPair>(c->ld_pairs), c->stream));
+    prof_end(c, "ld_emit_mask");
     HIPCHK(c, vcfxg::launch_ld_pairtext(0, P<vcfxg::LdPair>(c->ld_pairs), np, P<uint64_t>(c->ld_poff), nullptr,
                                         P<uint64_t>(c->rowlen), nullptr, c->stream));
     HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->rowlen) + np, 0, 8, c->stream));

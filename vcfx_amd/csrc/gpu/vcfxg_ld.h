@@ -5,6 +5,10 @@
 
 namespace vcfxg {
 
+constexpr int kLdBlock = 64;       // count-table granularity (64-variant blocks)
+constexpr int kLdFastBlock = 256;  // complete-group tile of the X.X^T kernel (vcfxg_ld_fast.hip)
+constexpr int kLdMaskTile = 128;   // tile of the missing-data kernel (vcfxg_ld_mask.hip)
+
 struct LdParseArgs {
     int ns;            // numSamples from the #CHROM line (tabs - 8 when >= 9 tabs)
     int kpad;          // row stride of the genotype matrix (ns rounded up to 64)
@@ -110,6 +114,14 @@ hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8
 hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C, hipStream_t s);
 // FP4 row bytes for ns samples: two per byte, whole 64-byte k-slices
 inline int ld_kp4(int ns) { return ns > 0 ? ((ns + 127) / 128) * 64 : 64; }
+// tiles (128 x 128, list of (I, J) tile indices) where a side holds a missing genotype: the six
+// pair sums of computeRsqSIMD on the FP4 MFMA (Gx = the dosage plane = Gp, Gv the valid mask,
+// Gq the squared dosage; vcfxg_ld_mask.hip)
+hipError_t launch_ld_mask(int pass, const uint8_t *Gx, const uint8_t *Gv, const uint8_t *Gq, const LdVar *vars,
+                          const uint32_t *chrom_id, const LdWindowArgs &a, const uint32_t *tiles, uint32_t ntiles,
+                          uint16_t *cnt, LdOffsets off, LdPair *pairs, hipStream_t s);
+hipError_t launch_ld_pack_vq(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gv, uint8_t *Gq, int kp4,
+                             hipStream_t s);
 hipError_t launch_ld_block(int pass, const int8_t *Gc, const LdVar *vars, const uint32_t *chrom_id,
                            const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
                            LdOffsets off, LdPair *pairs, hipStream_t s);
@@ -121,7 +133,5 @@ hipError_t launch_ld_matrix(const int8_t *Gc, const LdVar *vars, uint64_t m, int
                             const uint32_t *blocks, uint32_t nblocks, char *cells, hipStream_t s);
 hipError_t launch_mfma_i8_selftest(const int8_t *A, const int8_t *B, int *C, hipStream_t s);
 
-constexpr int kLdBlock = 64;
-constexpr int kLdFastBlock = 256;
 
 }  // namespace vcfxg
