@@ -350,6 +350,19 @@ int vcfxg_selftest_mfma_fp4(vcfxg_ctx *ctx, int *mismatches);
  * each rank its shard as a zero-copy view (VCFX_INPUT_VIEW). */
 int vcfxg_shard_cuts(const char *data, size_t n, size_t lo, int world, uint64_t *cuts);
 
+/* ---- rank cliques (SURVEY 8(b) vcfxg_shard_run's RCCL lifetime; 8(e) the count all-reduce) ----
+ * A clique of n contexts, one per rank of an in-process multi-GPU run (vcfx_tool_main_sharded,
+ * include/vcfx_tools.h: one host thread per rank).  On n distinct devices the reductions run
+ * over RCCL (librccl loaded at run time; ncclCommInitAll + ncclAllReduce on each rank's stream,
+ * over xGMI); ranks sharing a device (a rehearsal on one GPU) reduce on the host.  VCFX_RCCL=0
+ * forces the host reduction.  vcfxg_comm_allreduce_u64: every rank calls it from its own
+ * thread with the same count (<= 64); on return vals holds the sums over all ranks. */
+typedef struct vcfxg_comm vcfxg_comm;
+int vcfxg_comm_init(vcfxg_ctx *const *ctxs, int n, vcfxg_comm **out);
+int vcfxg_comm_allreduce_u64(vcfxg_comm *comm, int rank, uint64_t *vals, size_t count);
+int vcfxg_comm_uses_rccl(const vcfxg_comm *comm);
+void vcfxg_comm_destroy(vcfxg_comm *comm);
+
 /* device-formatted output text (without the column header line) */
 int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);
 /* bytes [offset, offset + n) of that text (outputs larger than one host buffer) */

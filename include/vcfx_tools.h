@@ -25,6 +25,7 @@
  */
 #ifndef VCFX_TOOLS_H
 #define VCFX_TOOLS_H
+#include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
@@ -43,6 +44,20 @@ int vcfx_tool_allele_counter(int argc, char **argv, int in_fd, int out_fd, int e
 int vcfx_tool_haplotype_phaser(int argc, char **argv, int in_fd, int out_fd, int err_fd);
 /* tool = "VCFX_<name>" (a leading path is ignored); -100 for an unknown tool */
 int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd);
+/* The same invocation over ngpu device contexts in this process (one host thread per rank;
+ * SURVEY 8(b) vcfxg_shard_run, 8(e)): the record tools (allele_freq_calc, record_filter,
+ * genotype_query, nonref_filter, dosage_calculator, hwe_tester, missing_detector,
+ * allele_counter) on a file input run each rank on its record range of the file, cut at
+ * i*size/ngpu and advanced past the next '\n' (VCFX_allele_counter.cpp:889-901);
+ * ld_calculator (streaming) on its share of the pair rows.  Output bytes, stderr text and exit
+ * code are those of the single-context run; global counts are all-reduced over the rank clique
+ * (vcfxg_comm: RCCL on distinct devices).  Other invocations run as vcfx_tool_main.  The
+ * executables call it when VCFX_NGPU (a count, or "all") asks for more than one rank; more
+ * ranks than devices share devices round robin. */
+int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd, int ngpu);
+/* host-only plan of that run (no device): the ranks used (1 = unsharded), *kind 0 unsharded /
+ * 1 record views / 2 LD rows, and for kind 1 the world + 1 cut offsets into cuts */
+int vcfx_shard_plan(const char *tool, int argc, char **argv, int ngpu, uint64_t *cuts, int *kind);
 /* `VCFX_record_filter --filter F --logic L [-i input] | VCFX_genotype_query -g Q [--strict] [-q]`
  * fused in one device pass (BASELINE config 3); input = NULL reads in_fd.  The return value is
  * genotype_query's exit code; record_filter's stderr is written to err_fd first. */

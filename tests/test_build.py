@@ -41,8 +41,8 @@ def test_open_without_gpu_fails_loudly():
 def test_tools_lib_exports():
     lib = ctypes.CDLL(TOOLS_LIB)
     txt = open(os.path.join(os.path.dirname(BUILD), "include", "vcfx_tools.h")).read()
-    syms = sorted(set(re.findall(r"\b(vcfx_(?:tool|pipeline)_[a-z0-9_]+)\s*\(", txt)))
-    assert len(syms) == 13, syms  # main, 11 tools, the fused pipeline
+    syms = sorted(set(re.findall(r"\b(vcfx_(?:tool|pipeline|shard)_[a-z0-9_]+)\s*\(", txt)))
+    assert len(syms) == 15, syms  # main, 11 tools, the fused pipeline, the sharded main and its plan
     missing = [s for s in syms if not hasattr(lib, s)]
     assert not missing, missing
 

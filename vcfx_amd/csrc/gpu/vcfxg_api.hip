@@ -3,9 +3,13 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <dlfcn.h>
+
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <algorithm>
+#include <mutex>
 #include <map>
 #include <string>
 #include <vector>
@@ -2190,6 +2194,126 @@ int vcfxg_shard_cuts(const char *data, size_t n, size_t lo, int world, uint64_t 
     }
     cuts[world] = n;
     return VCFXG_OK;
+}
+
+// ---- rank cliques: the count all-reduce of the in-process multi-GPU drop-in ------------------
+// RCCL comes from librccl at run time (dlopen: a single-GPU process never loads it); its symbols
+// are the ones of rccl.h (ncclCommInitAll, ncclAllReduce, ncclCommDestroy).
+namespace {
+typedef void *nccl_comm_t;
+typedef int (*nccl_init_all_f)(nccl_comm_t *, int, const int *);
+typedef int (*nccl_allreduce_f)(const void *, void *, size_t, int, int, nccl_comm_t, hipStream_t);
+typedef int (*nccl_destroy_f)(nccl_comm_t);
+typedef const char *(*nccl_errstr_f)(int);
+constexpr int kNcclUint64 = 5, kNcclSum = 0;
+constexpr size_t kCommSlots = 64;  // u64 values per all-reduce
+}  // namespace
+
+struct vcfxg_comm {
+    int n = 0;
+    std::vector<vcfxg_ctx *> ctx;
+    // RCCL
+    void *lib = nullptr;
+    nccl_allreduce_f allreduce = nullptr;
+    nccl_destroy_f destroy = nullptr;
+    std::vector<nccl_comm_t> comms;
+    std::vector<uint64_t *> dbuf;  // per rank: kCommSlots u64 on its device
+    // host reduction (several ranks on one device)
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t gen = 0;
+    int arrived = 0;
+    std::vector<uint64_t> acc, result;
+};
+
+int vcfxg_comm_init(vcfxg_ctx *const *ctxs, int n, vcfxg_comm **out) {
+    if (!ctxs || n < 1 || !out) return VCFXG_E_ARG;
+    vcfxg_comm *c = new vcfxg_comm;
+    c->n = n;
+    c->ctx.assign(ctxs, ctxs + n);
+    std::vector<int> dev(n);
+    bool distinct = n > 1;
+    for (int r = 0; r < n; r++) {
+        if (!ctxs[r]) {
+            delete c;
+            return VCFXG_E_ARG;
+        }
+        dev[r] = ctxs[r]->device;
+        for (int q = 0; q < r; q++) distinct = distinct && dev[q] != dev[r];
+    }
+    const char *e = getenv("VCFX_RCCL");
+    if (distinct && !(e && e[0] == '0')) {
+        c->lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!c->lib) c->lib = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        nccl_init_all_f init = c->lib ? (nccl_init_all_f)dlsym(c->lib, "ncclCommInitAll") : nullptr;
+        c->allreduce = c->lib ? (nccl_allreduce_f)dlsym(c->lib, "ncclAllReduce") : nullptr;
+        c->destroy = c->lib ? (nccl_destroy_f)dlsym(c->lib, "ncclCommDestroy") : nullptr;
+        c->comms.assign(n, nullptr);
+        if (!init || !c->allreduce || !c->destroy || init(c->comms.data(), n, dev.data()) != 0) {
+            if (c->lib) dlclose(c->lib);
+            c->lib = nullptr;
+            c->allreduce = nullptr;
+            c->comms.clear();
+            ctxs[0]->err = "vcfxg_comm_init: RCCL clique over " + std::to_string(n) + " devices failed";
+            delete c;
+            return VCFXG_E_HIP;
+        }
+        c->dbuf.assign(n, nullptr);
+        for (int r = 0; r < n; r++) {
+            HIPCHK(ctxs[r], hipSetDevice(dev[r]));
+            HIPCHK(ctxs[r], hipMalloc((void **)&c->dbuf[r], kCommSlots * 8));
+        }
+    }
+    c->acc.assign(kCommSlots, 0);
+    c->result.assign(kCommSlots, 0);
+    *out = c;
+    return VCFXG_OK;
+}
+
+int vcfxg_comm_uses_rccl(const vcfxg_comm *c) { return c && c->allreduce ? 1 : 0; }
+
+int vcfxg_comm_allreduce_u64(vcfxg_comm *c, int rank, uint64_t *vals, size_t count) {
+    if (!c || rank < 0 || rank >= c->n || (!vals && count) || count > kCommSlots) return VCFXG_E_ARG;
+    if (c->allreduce) {  // RCCL over the devices (xGMI), on the rank's own stream
+        vcfxg_ctx *x = c->ctx[rank];
+        HIPCHK(x, hipSetDevice(x->device));
+        HIPCHK(x, hipMemcpyAsync(c->dbuf[rank], vals, 8 * count, hipMemcpyHostToDevice, x->stream));
+        if (c->allreduce(c->dbuf[rank], c->dbuf[rank], count, kNcclUint64, kNcclSum, c->comms[rank], x->stream) != 0) {
+            x->err = "ncclAllReduce failed";
+            return VCFXG_E_HIP;
+        }
+        HIPCHK(x, hipMemcpyAsync(vals, c->dbuf[rank], 8 * count, hipMemcpyDeviceToHost, x->stream));
+        HIPCHK(x, hipStreamSynchronize(x->stream));
+        return VCFXG_OK;
+    }
+    // host: the last rank to arrive publishes the sums of this generation
+    std::unique_lock<std::mutex> lk(c->mu);
+    const uint64_t g = c->gen;
+    for (size_t k = 0; k < count; k++) c->acc[k] += vals[k];
+    if (++c->arrived == c->n) {
+        c->result = c->acc;
+        std::fill(c->acc.begin(), c->acc.end(), 0);
+        c->arrived = 0;
+        c->gen++;
+        c->cv.notify_all();
+    } else {
+        c->cv.wait(lk, [&] { return c->gen != g; });
+    }
+    for (size_t k = 0; k < count; k++) vals[k] = c->result[k];
+    return VCFXG_OK;
+}
+
+void vcfxg_comm_destroy(vcfxg_comm *c) {
+    if (!c) return;
+    for (size_t r = 0; r < c->comms.size(); r++)
+        if (c->comms[r] && c->destroy) c->destroy(c->comms[r]);
+    for (size_t r = 0; r < c->dbuf.size(); r++)
+        if (c->dbuf[r]) {
+            (void)hipSetDevice(c->ctx[r]->device);
+            (void)hipFree(c->dbuf[r]);
+        }
+    // (librccl stays loaded: its teardown threads may still be unwinding)
+    delete c;
 }
 
 int vcfxg_fetch_text_range(vcfxg_ctx *c, uint64_t offset, size_t n, void *host) {

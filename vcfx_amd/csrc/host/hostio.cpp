@@ -107,6 +107,7 @@ void join_opener() {
 void gpu_join() { join_opener(); }
 
 void gpu_prefetch() {
+    if (t_shard) return;
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_tried || g_opener.t.joinable()) return;
     g_opener.t = std::thread([] {
@@ -116,6 +117,7 @@ void gpu_prefetch() {
 }
 
 vcfxg_ctx *gpu_quiet() {
+    if (t_shard) return t_shard->g;  // a rank of an in-process multi-GPU run: its own context
     join_opener();
     std::lock_guard<std::mutex> lk(g_mu);
     open_locked();
@@ -253,15 +255,32 @@ bool Input::decompress(int err_fd) {
     return true;
 }
 
+thread_local ShardRank *t_shard = nullptr;
+
+void shard_records_begin(Out &err) {
+    if (!t_shard) return;
+    err.flush();
+    const off_t at = lseek(t_shard->err_fd, 0, SEEK_CUR);
+    t_shard->err_mark = at < 0 ? 0 : (long long)at;
+}
+
+size_t reported_size(const Input &in) { return t_shard ? t_shard->whole_bytes : in.source_n; }
+
 bool view_skip_header() {
+    if (t_shard) return t_shard->rank > 0;
     const char *e = getenv("VCFX_VIEW_SKIP_HEADER");
     return e && atoi(e) > 0;
 }
 
 void Input::apply_view() {
-    const char *v = getenv("VCFX_INPUT_VIEW");
+    const char *v = t_shard ? nullptr : getenv("VCFX_INPUT_VIEW");
     unsigned long long h = 0, lo = 0, hi = 0;
-    if (!v || sscanf(v, "%llu:%llu:%llu", &h, &lo, &hi) != 3 || h > lo || lo > hi || hi > n) {
+    bool have = v && sscanf(v, "%llu:%llu:%llu", &h, &lo, &hi) == 3;
+    if (t_shard) {
+        h = t_shard->h, lo = t_shard->lo, hi = t_shard->hi;
+        have = true;
+    }
+    if (!have || h > lo || lo > hi || hi > n) {
         populate(map_base, map_len);
         return;
     }

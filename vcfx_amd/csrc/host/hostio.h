@@ -7,6 +7,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <functional>
 #include <string>
 #include <thread>
 #include <vector>
@@ -14,6 +15,8 @@
 #include "vcfx_gpu.h"
 
 namespace vcfxh {
+
+struct Out;
 
 struct Input {
     // the input bytes [p, p + host_n) on the host; n = all input bytes.  host_n < n only for
@@ -74,6 +77,29 @@ struct Input {
     void populate(void *m, size_t len);
     void join_populate() const;
 };
+
+// ---- one rank of an in-process multi-GPU run (tool_shard_main.cpp, VCFX_NGPU) -------------------
+// The driver runs the tool once per rank, each on its own host thread with its own device
+// context and its own view of the input file; these thread-local settings replace the
+// process-wide ones (gpu(), VCFX_INPUT_VIEW, VCFX_VIEW_SKIP_HEADER) on that thread.
+struct ShardRank {
+    int rank = 0, world = 1;
+    vcfxg_ctx *g = nullptr;                          // this rank's context
+    unsigned long long h = 0, lo = 0, hi = 0;        // view: header [0, h) + records [lo, hi)
+    size_t whole_bytes = 0;                          // the whole input file's size
+    int err_fd = -1;                                 // this rank's stderr (a memfd)
+    long long err_mark = -1;                         // its bytes before the record phase
+    // counters the driver sums over the ranks after the run (RCCL on distinct devices), and
+    // on rank 0 the summary lines made from the sums (written after every rank's stderr)
+    uint64_t cnt[8] = {};
+    std::function<std::string(const uint64_t *)> summary;
+};
+extern thread_local ShardRank *t_shard;
+// the stderr written so far is the argument / header phase, which every rank repeats: ranks
+// > 0 drop it (the driver copies their stderr from here on)
+void shard_records_begin(Out &err);
+// the input's size as the tools report it ("Processing F (X MB)"): the whole file for a rank
+size_t reported_size(const Input &in);
 
 // sizes of the input paths (VCFX_PREFETCH_BYTES, VCFX_STREAM_CHUNK, VCFX_RING_SLOT,
 // VCFX_WINDOW_BYTES override them; tests use tiny values)

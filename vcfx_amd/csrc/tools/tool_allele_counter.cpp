@@ -230,14 +230,16 @@ int run_file(const Args &A, int out_fd, Out &err) {
             nt = hw_threads();
             if (nt <= 0) nt = 4;
         }
-        const size_t dsz = in.n - ds;
+        const size_t dsz = reported_size(in) - ds;  // (a multi-GPU rank: the whole file's data)
         if (dsz < 10u * 1024 * 1024) nt = 1;
         else if (dsz < 100u * 1024 * 1024 && nt > 4) nt = 4;
         err.put("Info: Using " + std::to_string(nt) + " threads\n");
     }
     err.flush();
+    shard_records_begin(err);
     Sink sink(out_fd, A.gzip);
-    if (A.kind == kText) sink.put(kTextHdr, sizeof kTextHdr - 1);
+    if (view_skip_header()) {  // a multi-GPU rank > 0: rank 0 writes the header
+    } else if (A.kind == kText) sink.put(kTextHdr, sizeof kTextHdr - 1);
     else if (A.kind == kAgg) sink.put(kAggHdr, sizeof kAggHdr - 1);
     else {  // BinaryHeader :327-332: "VCAC", version 1, sample count, 8 reserved bytes
         unsigned char h[20] = {'V', 'C', 'A', 'C', 1, 0, 0, 0};

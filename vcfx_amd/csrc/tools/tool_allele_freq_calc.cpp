@@ -117,10 +117,18 @@ extern "C" int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int 
             err.put(std::string("Error: Cannot open file: ") + input + "\n");
             return 1;
         }
-        if (!quiet) err.put(std::string("Processing ") + input + " (" + std::to_string(in.source_n / (1024 * 1024)) + " MB)\n");
+        if (!quiet) err.put(std::string("Processing ") + input + " (" + std::to_string(reported_size(in) / (1024 * 1024)) + " MB)\n");
         if (!in.decompress(err.fd)) return 1;
+        shard_records_begin(err);
         if (!run_af(in, VCFXG_MODE_FILE, quiet, out, err, &v, &l)) return 1;
-        if (!quiet) err.put("Processed " + std::to_string(v) + " variants from " + std::to_string(l) + " data lines\n");
+        if (t_shard) {  // a rank of a multi-GPU run: the totals over every rank, after all stderr
+            t_shard->cnt[0] = v;
+            t_shard->cnt[1] = l;
+            if (!quiet && t_shard->rank == 0)
+                t_shard->summary = [](const uint64_t *c) {
+                    return "Processed " + std::to_string(c[0]) + " variants from " + std::to_string(c[1]) + " data lines\n";
+                };
+        } else if (!quiet) err.put("Processed " + std::to_string(v) + " variants from " + std::to_string(l) + " data lines\n");
     } else {
         phase("start");
         in.read_fd(in_fd, /*host_copy=*/false);  // only the header is needed on the host

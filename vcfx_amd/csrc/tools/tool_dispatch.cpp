@@ -3,6 +3,13 @@
 
 #include "tools.h"
 
+namespace vcfxh {
+std::recursive_mutex &getopt_mutex() {
+    static std::recursive_mutex m;
+    return m;
+}
+}  // namespace vcfxh
+
 extern "C" int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd) {
     const char *t = strrchr(tool, '/');
     t = t ? t + 1 : tool;

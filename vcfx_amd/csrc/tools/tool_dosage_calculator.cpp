@@ -130,6 +130,7 @@ extern "C" int vcfx_tool_dosage_calculator(int argc, char **argv, int in_fd, int
             return 1;
         }
         if (!in.decompress(err.fd)) return 1;
+        shard_records_begin(err);  // (a multi-GPU rank > 0 drops its stderr before this)
         rc = run_dose(in, VCFXG_MODE_FILE, quiet, out, err);
     } else {
         phase("start");

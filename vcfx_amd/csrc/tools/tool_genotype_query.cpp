@@ -192,6 +192,7 @@ extern "C" int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int ou
             return 1;
         }
         if (!in.decompress(err.fd)) return 1;
+        shard_records_begin(err);  // (a multi-GPU rank > 0 drops its stderr before this)
         out.flush();
         return run_gq(in, false, query, strict, quiet, out_fd, err) ? 0 : 1;
     }

@@ -167,9 +167,10 @@ extern "C" int vcfx_tool_hwe_tester(int argc, char **argv, int in_fd, int out_fd
             err.put(std::string("Error: Cannot open file: ") + input + "\n");
             return 1;
         }
-        if (!quiet) err.put(std::string("Processing ") + input + " (" + std::to_string(in.source_n) + " bytes)...\n");
+        if (!quiet) err.put(std::string("Processing ") + input + " (" + std::to_string(reported_size(in)) + " bytes)...\n");
         err.flush();
         if (!in.decompress(err.fd)) return 1;
+        shard_records_begin(err);
         return run_hwe(in, VCFXG_MODE_FILE, out, err) ? 0 : 1;
     }
     phase("start");

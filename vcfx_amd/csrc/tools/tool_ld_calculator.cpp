@@ -293,6 +293,7 @@ extern "C" int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out
             return 1;
         }
         if (!in.decompress(err.fd)) return 1;
+        shard_records_begin(err);  // (a multi-GPU rank > 0 drops its stderr before this)
         if (o.matrix && o.shard_rank > 0) return 0;  // matrix mode is not sharded: rank 0 writes it
         bool ok = o.matrix ? run_ld_matrix(in, true, o.quiet, rchrom, has_region, rs, re, out_fd, err)
                            : run_stream(in, true, o, rchrom, has_region, rs, re, out_fd, err);

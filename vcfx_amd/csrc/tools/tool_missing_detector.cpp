@@ -58,19 +58,34 @@ size_t leading_headers(const Input &in) {
     return ds;
 }
 
+// the file path's closing lines (processMmapZeroCopy :575-589): the pre-scan's fast path
+// (no '.' in any sample column) reports its line count, the per-line pass its flagged share
+std::string md_summary(bool fast, uint64_t lines, uint64_t data_lines, uint64_t flagged) {
+    if (fast)
+        return "Fast path: No '.' in sample columns (scan complete)\nProcessed " + std::to_string(lines) +
+               " variants, 0 with missing genotypes (0%)\n";
+    const double pct = data_lines ? 100.0 * (double)flagged / (double)data_lines : 0.0;
+    char b[160];
+    snprintf(b, sizeof b, "Processed %llu variants, %llu with missing genotypes (%g%%)\n",
+             (unsigned long long)data_lines, (unsigned long long)flagged, pct);
+    return b;
+}
+
 // file: processMmapZeroCopy :450-589; stdin: detectMissingGenotypes :860-911.  Returns false
 // on a device error (already reported).
 bool run_md(const Input &in, bool file, const char *path, bool quiet, int out_fd, Out &err) {
     if (file && !quiet) {
         char b[64];
-        snprintf(b, sizeof b, " (%zu MB)\n", in.source_n / (1024 * 1024));
+        snprintf(b, sizeof b, " (%zu MB)\n", reported_size(in) / (1024 * 1024));
         err.put(std::string("Processing ") + path + b);
         err.flush();
     }
+    shard_records_begin(err);
     LineEmitter em(in.p, in.host_n, out_fd);
     const size_t ds = leading_headers(in);
-    // the leading '#' lines: copied (file) / each followed by '\n' (stdin: getline)
-    if (file) em.bytes(in.p, in.p + ds);
+    // the leading '#' lines: copied (file) / each followed by '\n' (stdin: getline); a multi-GPU
+    // rank > 0 leaves them to rank 0
+    if (file && !view_skip_header()) em.bytes(in.p, in.p + ds);
     else {
         const char *p = in.p, *end = in.p + ds, *ls, *le;
         while (next_line(p, end, ls, le)) em.line(ls, le);
@@ -87,15 +102,24 @@ bool run_md(const Input &in, bool file, const char *path, bool quiet, int out_fd
             return false;
         nl = s.n_lines;
     }
+    // a multi-GPU rank: the summary over every rank (the fast path's message only when no rank
+    // saw a '.'; a rank's own fast path writes the same bytes as its per-line pass in file mode)
+    const bool last_nl = in.n && (in.tail ? in.tail[in.n - in.host_n - 1] : in.p[in.n - 1]) == '\n';
+    const uint64_t lines = nl - (nl && !last_nl ? 1 : 0);
+    if (file && t_shard) {
+        t_shard->cnt[0] = lines;
+        t_shard->cnt[1] = s.data_lines;
+        t_shard->cnt[2] = s.rows;
+        t_shard->cnt[3] = s.general_records;
+        if (!quiet && t_shard->rank == 0)
+            t_shard->summary = [](const uint64_t *c) { return md_summary(c[3] == 0, c[0], c[1], c[2]); };
+    }
     if (file && s.general_records == 0) {
         // the pre-scan saw no '.' in any sample column: the input as it is
-        if (!quiet) err.put("Fast path: No '.' in sample columns (scan complete)\n");
         em.bytes(in.p + ds, in.p + in.host_n);
         em.finish();
         if (in.tail) write_all(out_fd, in.tail, in.n - in.host_n);
-        const bool last_nl = in.n && (in.tail ? in.tail[in.n - in.host_n - 1] : in.p[in.n - 1]) == '\n';
-        const uint64_t lines = nl - (nl && !last_nl ? 1 : 0);
-        if (!quiet) err.put("Processed " + std::to_string(lines) + " variants, 0 with missing genotypes (0%)\n");
+        if (!quiet && !t_shard) err.put(md_summary(true, lines, 0, 0));
         return true;
     }
     if (nl) {
@@ -135,13 +159,7 @@ bool run_md(const Input &in, bool file, const char *path, bool quiet, int out_fd
         }
     }
     em.finish();
-    if (file && !quiet) {
-        const double pct = s.data_lines ? 100.0 * (double)s.rows / (double)s.data_lines : 0.0;
-        char b[160];
-        snprintf(b, sizeof b, "Processed %llu variants, %llu with missing genotypes (%g%%)\n",
-                 (unsigned long long)s.data_lines, (unsigned long long)s.rows, pct);
-        err.put(b);
-    }
+    if (file && !quiet && !t_shard) err.put(md_summary(false, lines, s.data_lines, s.rows));
     return true;
 }
 

@@ -151,6 +151,7 @@ extern "C" int vcfx_tool_nonref_filter(int argc, char **argv, int in_fd, int out
             return 0;
         }
         if (!in.decompress(err.fd)) return 1;
+        shard_records_begin(err);  // (a multi-GPU rank > 0 drops its stderr before this)
         out.flush();
         return run_nr(in, false, out_fd, err) ? 0 : 1;
     }

@@ -251,6 +251,7 @@ extern "C" int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out
             return 1;
         }
         if (!in.decompress(err.fd)) return 1;
+        shard_records_begin(err);  // (a multi-GPU rank > 0 drops its stderr before this)
         if (in.n == 0) return 0;
         return run_rf(in, false, cs, and_logic, out_fd, err) ? 0 : 1;
     }

@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -29,26 +30,32 @@ std::vector<vcfxg_criterion> to_abi(const std::vector<Criterion> &cs);
 
 // getopt_long prints its diagnostics on the C stderr stream; route them to the tool's
 // err fd (identical text to the reference's getopt messages).
+// getopt_long's state (optind, optarg) and the stderr swap are process-wide: the argument
+// phase of the tools is serialised (the ranks of an in-process multi-GPU run parse at once).
+std::recursive_mutex &getopt_mutex();
 struct GetoptStderr {
     Out &err;
+    std::unique_lock<std::recursive_mutex> lk;
     FILE *saved = nullptr, *mem = nullptr;
     char *buf = nullptr;
     size_t len = 0;
-    explicit GetoptStderr(Out &e) : err(e) {
+    explicit GetoptStderr(Out &e) : err(e), lk(getopt_mutex()) {
         fflush(stderr);
         mem = open_memstream(&buf, &len);
         saved = stderr;
         stderr = mem;
     }
     void done() {
-        if (!mem) return;
-        fflush(mem);
-        stderr = saved;
-        fclose(mem);
-        mem = nullptr;
-        if (len) err.put(buf, len);
-        free(buf);
-        buf = nullptr;
+        if (mem) {
+            fflush(mem);
+            stderr = saved;
+            fclose(mem);
+            mem = nullptr;
+            if (len) err.put(buf, len);
+            free(buf);
+            buf = nullptr;
+        }
+        if (lk.owns_lock()) lk.unlock();
     }
     ~GetoptStderr() { done(); }
 };

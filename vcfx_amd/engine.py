@@ -71,6 +71,10 @@ SIGNATURES = {
     "vcfxg_allele_counter": (_I, [_VP, _U64, _U64, _VP, ctypes.POINTER(Summary)]),
     "vcfxg_fetch_text_range": (_I, [_VP, _U64, _S, _VP]),
     "vcfxg_shard_cuts": (_I, [_VP, _S, _S, _I, _VP]),
+    "vcfxg_comm_init": (_I, [_VP, _I, ctypes.POINTER(_VP)]),
+    "vcfxg_comm_allreduce_u64": (_I, [_VP, _I, _VP, _S]),
+    "vcfxg_comm_uses_rccl": (_I, [_VP]),
+    "vcfxg_comm_destroy": (None, [_VP]),
     "vcfxg_haplotype_phaser": (_I, [_VP, _S, _I, ctypes.c_double, ctypes.c_uint32, ctypes.POINTER(Summary)]),
     "vcfxg_phaser_variants": (_I, [_VP, _VP, _VP, _VP]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),

@@ -21,11 +21,18 @@ def lib():
         _lib.vcfx_tool_main.restype = ctypes.c_int
         _lib.vcfx_tool_main.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                         ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        _lib.vcfx_tool_main_sharded.restype = ctypes.c_int
+        _lib.vcfx_tool_main_sharded.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        _lib.vcfx_shard_plan.restype = ctypes.c_int
+        _lib.vcfx_shard_plan.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int)]
     return _lib
 
 
-def run(argv, stdin=None, cwd=None):
-    """Run tool argv[0] with argv; returns (stdout bytes, stderr bytes, exit code)."""
+def run(argv, stdin=None, cwd=None, ngpu=1):
+    """Run tool argv[0] with argv; returns (stdout bytes, stderr bytes, exit code).  ngpu > 1:
+    the in-process multi-GPU run (vcfx_tool_main_sharded, ranks round robin over the devices)."""
     L = lib()
     old = os.getcwd()
     with tempfile.TemporaryFile() as fi, tempfile.TemporaryFile() as fo, tempfile.TemporaryFile() as fe:
@@ -37,7 +44,11 @@ def run(argv, stdin=None, cwd=None):
         if cwd:
             os.chdir(cwd)
         try:
-            rc = L.vcfx_tool_main(argv[0].encode(), len(argv), arr, fi.fileno(), fo.fileno(), fe.fileno())
+            if ngpu > 1:
+                rc = L.vcfx_tool_main_sharded(argv[0].encode(), len(argv), arr, fi.fileno(), fo.fileno(), fe.fileno(),
+                                              ngpu)
+            else:
+                rc = L.vcfx_tool_main(argv[0].encode(), len(argv), arr, fi.fileno(), fo.fileno(), fe.fileno())
         finally:
             os.chdir(old)
         if rc == -100:
@@ -45,6 +56,16 @@ def run(argv, stdin=None, cwd=None):
         fo.seek(0)
         fe.seek(0)
         return fo.read(), fe.read(), rc
+
+
+def shard_plan(argv, ngpu):
+    """(ranks, kind, cuts) of the in-process multi-GPU run of argv at ngpu (host only)"""
+    L = lib()
+    arr = (ctypes.c_char_p * (len(argv) + 1))(*[a.encode() for a in argv], None)
+    cuts = (ctypes.c_uint64 * (ngpu + 1))()
+    kind = ctypes.c_int(0)
+    w = L.vcfx_shard_plan(argv[0].encode(), len(argv), arr, ngpu, cuts, ctypes.byref(kind))
+    return w, kind.value, list(cuts[:w + 1]) if kind.value == 1 else None
 
 
 def run_pipe(argv, stdin=b"", cwd=None):
