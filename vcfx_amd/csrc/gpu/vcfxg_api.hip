@@ -1911,50 +1911,49 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
             }
     }
     const uint32_t nfast = (uint32_t)(blocks.size() / 2);
-    // general list: every 64-block pair with an incomplete side -- for a complete row block J
-    // only the incomplete column blocks, found in the sorted list of them (no scan over the
-    // whole window triangle on the host)
-    const uint64_t Jlast = (j1 + BM - 1) / BM;
-    std::vector<uint32_t> inc;
-    for (uint64_t b = ifirst(j0 / BM); b < Jlast; b++)
-        if (!gcomp(b)) inc.push_back((uint32_t)b);
-    for (uint64_t J = j0 / BM; J * BM < j1; J++) {
-        const uint64_t I0 = ifirst(J);
-        nb = std::max<uint64_t>(nb, J - I0 + 1);
-        if (!gcomp(J)) {
-            for (uint64_t I = I0; I <= J; I++) {
-                blocks.push_back((uint32_t)I);
-                blocks.push_back((uint32_t)J);
-            }
-            continue;
-        }
-        for (auto it = std::lower_bound(inc.begin(), inc.end(), (uint32_t)I0); it != inc.end() && *it <= J; ++it) {
-            blocks.push_back(*it);
-            blocks.push_back((uint32_t)J);
-        }
-    }
-    uint32_t nbl = (uint32_t)(blocks.size() / 2) - nfast;
     // the missing-data tiles (k_ld_mask, default): every 128 x 128 tile pair in the window
-    // whose 256-groups are not both complete (those are k_ld_fast's), replacing the 64-block
-    // general list (kept for VCFXG_LD_MASK=0)
+    // whose 256-groups are not both complete (those are k_ld_fast's); VCFXG_LD_MASK=0 keeps the
+    // previous int8 kernel (k_ld_block) over every 64-block pair with an incomplete side
     static const bool use_mask = [] {
         const char *e = getenv("VCFXG_LD_MASK");
         return !(e && e[0] == '0');
     }();
-    uint32_t nmask = 0;
+    for (uint64_t J = j0 / BM; J * BM < j1; J++) nb = std::max<uint64_t>(nb, J - ifirst(J) + 1);
+    uint32_t nmask = 0, nbl = 0;
     if (use_mask && c->ld_vq) {
-        blocks.resize(2 * (size_t)nfast);
         constexpr uint64_t TM = vcfxg::kLdMaskTile, kPerG = vcfxg::kLdFastBlock / vcfxg::kLdMaskTile;
         for (uint64_t J2 = j0 / TM; J2 * TM < j1; J2++) {
             const uint64_t I2lo = ifirst(J2 * (TM / BM)) / (TM / BM);  // the first 64-row's window start
+            const bool jc = gf[J2 / kPerG] != 0;
             for (uint64_t I2 = I2lo; I2 <= J2; I2++) {
-                if (gf[I2 / kPerG] && gf[J2 / kPerG]) continue;  // a complete group pair: k_ld_fast
+                if (jc && gf[I2 / kPerG]) continue;  // a complete group pair: k_ld_fast
                 blocks.push_back((uint32_t)I2);
                 blocks.push_back((uint32_t)J2);
             }
         }
         nmask = (uint32_t)(blocks.size() / 2) - nfast;
-        nbl = 0;
+    } else {
+        // for a complete row block J only the incomplete column blocks, found in the sorted list
+        // of them (no scan over the whole window triangle on the host)
+        const uint64_t Jlast = (j1 + BM - 1) / BM;
+        std::vector<uint32_t> inc;
+        for (uint64_t b = ifirst(j0 / BM); b < Jlast; b++)
+            if (!gcomp(b)) inc.push_back((uint32_t)b);
+        for (uint64_t J = j0 / BM; J * BM < j1; J++) {
+            const uint64_t I0 = ifirst(J);
+            if (!gcomp(J)) {
+                for (uint64_t I = I0; I <= J; I++) {
+                    blocks.push_back((uint32_t)I);
+                    blocks.push_back((uint32_t)J);
+                }
+                continue;
+            }
+            for (auto it = std::lower_bound(inc.begin(), inc.end(), (uint32_t)I0); it != inc.end() && *it <= J; ++it) {
+                blocks.push_back(*it);
+                blocks.push_back((uint32_t)J);
+            }
+        }
+        nbl = (uint32_t)(blocks.size() / 2) - nfast;
     }
     const uint64_t rows = j1 - j0;
     int r = ensure(c, c->ld_blocks, 4 * blocks.size() + 8);

@@ -85,8 +85,9 @@ bool run_md(const Input &in, bool file, const char *path, bool quiet, int out_fd
     const size_t ds = leading_headers(in);
     // the leading '#' lines: copied (file) / each followed by '\n' (stdin: getline); a multi-GPU
     // rank > 0 leaves them to rank 0
-    if (file && !view_skip_header()) em.bytes(in.p, in.p + ds);
-    else {
+    if (file) {
+        if (!view_skip_header()) em.bytes(in.p, in.p + ds);
+    } else {
         const char *p = in.p, *end = in.p + ds, *ls, *le;
         while (next_line(p, end, ls, le)) em.line(ls, le);
     }
