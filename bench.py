@@ -529,7 +529,8 @@ def main():
             if red is not None:
                 allreduce_counts([s.n_lines, s.rows, s.text_bytes, s.general_records])
             return s
-        kern_names = ("line_count", "line_emit", "line_compact", "dose_len", "dose_rows", "dose_fmt")
+        kern_names = ("dose_walk", "walk_compact", "line_count", "line_emit", "line_compact", "dose_len", "dose_rows",
+                      "dose_fmt")
     elif a.workload == "ac":
         ac_names = ["S%05d" % (k + 1) for k in range(a.samples)]
         ac_idx = list(range(a.samples))
@@ -667,6 +668,9 @@ def main():
                 # dosage: pass 1 reads the records (+ line end, status, length, meta per line);
                 # pass 2 reads them again and writes the rows (2 bytes per sample)
                 "dose_len": region_bytes + L * (8 + 1 + 8 + 24),
+                # the dosage walk (records of >= 512 B): the record bytes once + per line its
+                # region results (line end 8, samples / NA 8, status 1, head record 16)
+                "dose_walk": region_bytes + L * (8 + 8 + 1 + 16),
                 "dose_fmt": region_bytes + tb + L * (8 + 1 + 8 + 24),
                 # allele counter: pass 1 reads the records (+ line end, status, length, meta per
                 # line); pass 2 reads each selected sample's GT (the records again) and writes the rows
@@ -701,7 +705,9 @@ def main():
             dom = max((k for k in kernels if k in algo), key=kernels.get)
             ach = algo[dom] / (kernels[dom] * 1e-3) / 1e9
             roof = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": pmc_traffic(a.workload, dom),
+                    "frac": ach / HBM_PEAK_GBS,
+                    # (the committed PMC pass is of the default data: none for the general-path shapes)
+                    "traffic": None if general else pmc_traffic(a.workload, dom),
                     "algorithmic_bytes_per_launch": int(algo[dom]), "avg_launch_ms": kernels[dom]}
         if general:
             extra = " [data: FORMAT=%s, missing rate %g, irregular rate %g: the general GT path]" % (

@@ -46,7 +46,7 @@ CASES = [
     ["VCFX_missing_detector", "-i", "{mixed}"], ["VCFX_missing_detector", "-i", "{gt}"],
     ["VCFX_missing_detector", "-q", "-i", "{crlf}"],
     ["VCFX_allele_counter", "-i", "{gt}"], ["VCFX_allele_counter", "-a", "-i", "{mixed}"],
-    ["VCFX_allele_counter", "-b", "-i", "{gt}"], ["VCFX_allele_counter", "-s", "S3 S1", "-i", "{mixed}"],
+    ["VCFX_allele_counter", "-b", "-i", "{gt}"], ["VCFX_allele_counter", "-s", "S00003 S00001", "-i", "{mixed}"],
     ["VCFX_ld_calculator", "-w", "60", "-t", "0.2", "-i", "{ld}"],
     ["VCFX_ld_calculator", "-w", "400", "-t", "0.5", "-q", "-i", "{ld}"],
 ]

@@ -12,7 +12,11 @@ step() {
     tail -4 "gpurun_out/$name.log" | cut -c1-600
     return $rc
 }
-bash tools/r03_latency.sh && step ngpu_tests 900 python -u -m pytest tests/test_gpu_ngpu.py -x -v --timeout 300 --timeout-method thread || exit $?
+step ngpu_tests 900 python -u -m pytest tests/test_gpu_ngpu.py -x -v --timeout 300 --timeout-method thread || exit $?
+step dose_tests 600 python -u -m pytest tests/test_gpu_dose.py -x -v --timeout 300 --timeout-method thread || exit $?
+step bench_dose 600 python -u bench.py --workload dose --no-e2e || exit $?
+step af_tests 600 python -u -m pytest tests/test_gpu_af.py -x -v --timeout 300 --timeout-method thread || exit $?
+step bench_af_gtadp 600 python -u bench.py --format gt:ad:dp --steps 5 --warmup 2 --no-e2e || exit $?
 step bench_ld_miss2 600 python -u bench.py --workload ld --missing-rate 0.001 --steps 3 --warmup 1 --no-cpu-baseline || exit $?
 
 # A/B: the AF walk sweep over raw blocks (gt_fast_bytes) vs gt_fast, same box, alternating

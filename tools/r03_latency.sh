@@ -22,3 +22,6 @@ done
 echo "== reference" >> $out
 for i in 1 2 3; do s=$(date +%s%N); oracle/_ref/VCFX_allele_freq_calc -q -i /tmp/small.vcf > /dev/null; e=$(date +%s%N); echo "ref wall $(( (e - s) / 1000000 )) ms" >> $out; done
 cat $out
+echo "== runtime start-up without / with the engine's fat binary" >> $out
+for b in plain vcfx plain vcfx; do timeout -k 5 60 tools/microbench/hip_init_$b >> $out 2>&1 || exit 1; done
+cat $out | tail -20

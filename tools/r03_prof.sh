@@ -25,6 +25,9 @@ SQ="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_AN
 step pmc_af_sq 300 rocprofv3 --pmc $SQ -d gpurun_out/pmc_af_sq -o run --output-format csv -- \
     python bench.py --steps 2 --warmup 1 $B || exit $?
 python tools/pmc_sq.py $(find gpurun_out/pmc_af_sq -name '*counter_collection.csv' | head -1) 'k_af_walk' gpurun_out/pmc_af_walk_sq.json
+step pmc_gtadp_sq 300 rocprofv3 --pmc $SQ -d gpurun_out/pmc_gtadp_sq -o run --output-format csv -- \
+    python bench.py --format gt:ad:dp --steps 1 --warmup 1 $B || exit $?
+python tools/pmc_sq.py $(find gpurun_out/pmc_gtadp_sq -name '*counter_collection.csv' | head -1) 'k_af_walk' gpurun_out/pmc_gtadp_walk_sq.json
 MF="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"
 step pmc_ldmiss_mfma 300 rocprofv3 --pmc $MF -d gpurun_out/pmc_ldmiss_mfma -o run --output-format csv -- \
     python bench.py --workload ld --missing-rate 0.001 --steps 1 --warmup 1 $B || exit $?

@@ -73,7 +73,21 @@ struct WalkRed<HweOp> {
     }
 };
 
-template <class Op>
+template <>
+struct WalkRed<DoseWalkOp> {  // samples and "NA" samples of the record (alt_o / tot_o)
+    static constexpr bool kAux = false;
+    __device__ static DoseWalkOp make(const char *buf, int64_t ae) { return DoseWalkOp{buf, ae}; }
+    __device__ static void out(const DoseWalkOp &op, uint32_t &a, uint32_t &b, uint32_t &) {
+        a = op.ns;
+        b = op.na;
+    }
+};
+
+// kGF: the GT-first walk (records "GT:AD:DP"-like, no fixed stride to predict): a GT-first
+// record whose '\n' is past the window is swept by gt_first from its sample start, which finds
+// the record's end in the same pass (and issues the next window as soon as it does); a separate
+// instantiation, so the GT-only walk keeps its registers
+template <class Op, bool kGF = false>
 __global__ __launch_bounds__(kWalkThreads)
 #ifdef VCFXG_WALK_MAXW
 __attribute__((amdgpu_waves_per_eu(1, VCFXG_WALK_MAXW)))
@@ -97,7 +111,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     int64_t span = span0;  // predicted '\n' distance from the sample start
     uint8_t cr_prev = 0;   // and the '\r' state of that record
     uint64_t n = 0;
-    uint32_t ngt = 0;
+    uint32_t ngt = 0, ngf = 0;  // GT-first lines; of them, swept whole by gt_first (kGF)
     const uint64_t base = (uint64_t)wk * cap_w;
     // per-line results held by lane (n & 63), written out 64 lines at a time (no stores --
     // and no waits for their completion -- on the per-record path)
@@ -189,9 +203,12 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         int64_t E;
         uint8_t cr = 0;
         bool predicted = false;
+        const bool gf = kGF && N1r < 0 && gt_head && !gt_only;  // the end comes with the sweep
         if (N1r >= 0) {
             E = A + N1r;
             cr = strip_cr && E > L && slot_byte(cw, N1r - 1) == '\r';
+        } else if (gf) {
+            E = hi;  // (until gt_first finds the '\n')
         } else if (gt_only && span > 0 && t8 + 1 + span <= hi) {
             // predicted from the previous fixed-stride record; its end bytes come with the
             // next window (which starts at E - 1) and are checked after the sweep
@@ -221,6 +238,32 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         int64_t S = 0;
         bool ok = false;
         auto sweep = [&]() {
+            if constexpr (kGF) {
+              if (gf) {  // gt_first from the sample start: the counts and the record end
+                S = t8 + 1;
+                Op op = R::make(buf, hi);
+                int64_t Eo = hi;
+                uint8_t cro = 0;
+                auto pre_e = [&](int64_t e) {
+                    An = std::max<int64_t>(e - 1, 0) & ~(int64_t)15;
+                    pre();
+                };
+                ok = gt_first<kWalkUnroll>(buf, S, hi, strip_cr, op, pre_e, Eo, cro);
+                E = Eo;
+                cr = cro;
+                const int64_t ae = E - cr;
+                kind = t8 < ae ? kMetaGt : kMetaFull;
+                ok = ok && kind == kMetaGt;
+                if (kind == kMetaGt) {
+                    rowpre = (uint32_t)(t4 - L + 1);
+                    sep = t8 + 2 >= ae ? 0
+                          : t8 + 2 < wend ? (uint8_t)sep_w
+                                          : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
+                    R::out(op, alt, tot, aux);
+                }
+                return;
+              }
+            }
             const int64_t ae = E - cr;
             if (ae <= L) kind = kMetaEmpty;
             else if (first == '#') kind = kMetaHeader;
@@ -285,6 +328,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             r_k = (uint32_t)kind | ((uint32_t)sep << 8) | ((uint32_t)cr << 16) | ((uint32_t)st << 24);
         }
         ngt += kind == kMetaGt ? 1u : 0u;
+        if constexpr (kGF) ngf += gf && kind == kMetaGt && ok ? 1u : 0u;
         if (tail.wtext) {
             // the row (CHROM..ALT + "\t" + 4 digits... "x.xxxx\n") of a GT line; lines off the
             // fixed-stride sweep go to the leftover list (rare: one atomic each)
@@ -309,7 +353,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             tail.wtext[wk] = wtext;
             tail.wstart[wk] = (uint64_t)L0;
         }
-        wgt[wk] = ngt;
+        wgt[wk] = ngt | (ngf << 16);
     }
 }
 
@@ -337,7 +381,7 @@ __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_
         // (bpre: block-local offsets of k_walker_scan)
         const uint64_t d0 = offs[w] + (bpre ? bpre[w / kWalkerScanBlock] : 0),
                        cnt = offs[w + 1] + (bpre ? bpre[(w + 1) / kWalkerScanBlock] : 0) - d0, s0 = (uint64_t)w * cap_w;
-        g += lane() == 0 ? wgt[w] : 0u;
+        g += lane() == 0 ? (wgt[w] & 0xFFFFu) : 0u;
         for (uint64_t i = lane(); i < cnt; i += kWave) {
             const uint64_t sl = s0 + i, d = d0 + i;
             line_end[d] = le_b[sl];
@@ -368,12 +412,20 @@ int64_t af_walkers(int64_t lo, int64_t hi, int64_t chunk) { return hi > lo ? (hi
 hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int mode, int64_t span0,
                           uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
                           uint8_t *status_b, void *meta_b, uint64_t *wcount, uint32_t *wgt, unsigned *overflow,
-                          hipStream_t s, int32_t *hwe_aux_b, const WalkTail *tail) {
+                          hipStream_t s, int32_t *hwe_aux_b, const WalkTail *tail, bool dose, bool gt_first_walk) {
     const WalkTail t = tail ? *tail : WalkTail{};
     const int64_t nw = af_walkers(lo, hi, chunk);
     if (!nw) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)((nw + kWalkWaves - 1) / kWalkWaves);
-    if (hwe_aux_b)
+    if (gt_first_walk)
+        hipLaunchKernelGGL(HIP_KERNEL_NAME(k_af_walk<AfOp, true>), dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi,
+                           chunk, nw, mode, span0, cap_w, le_b, alt_b, tot_b, nullptr, rowpre_b, status_b,
+                           static_cast<LineMeta *>(meta_b), wcount, wgt, overflow, t);
+    else if (dose)
+        hipLaunchKernelGGL(k_af_walk<DoseWalkOp>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, mode,
+                           span0, cap_w, le_b, alt_b, tot_b, nullptr, rowpre_b, status_b, static_cast<LineMeta *>(meta_b),
+                           wcount, wgt, overflow, t);
+    else if (hwe_aux_b)
         hipLaunchKernelGGL(k_af_walk<HweOp>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, mode, span0,
                            cap_w, le_b, alt_b, tot_b, hwe_aux_b, rowpre_b, status_b, static_cast<LineMeta *>(meta_b),
                            wcount, wgt, overflow, t);

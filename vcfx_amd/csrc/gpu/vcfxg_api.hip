@@ -55,7 +55,7 @@ struct vcfxg_ctx {
     std::string query_host, crit_host, pool_host;  // host sources of in-flight async copies
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
-        ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff, ld_Gv, ld_Gq;
+        ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff, ld_Gv, ld_Gq, dose_meta;
     bool ld_vq = false;  // ld_Gv / ld_Gq (valid-mask and squared-dosage FP4 planes) are current
     int n_cu = 0;
     DevBuf async_small;         // asynchronous AF path: line range {0, n}, failure flags, summary
@@ -95,6 +95,9 @@ struct vcfxg_ctx {
     // the first data line's FORMAT is exactly "GT" (fixed-stride records: the walk's predicted
     // ends pay; "GT:AD:DP"-like records are scanned faster by the index sweep)
     bool hint_gt_only = false;
+    // ... or starts with "GT:" (GT:AD:DP-like records: the GT-first walk, gt_first finding each
+    // record's end in its one sweep)
+    bool hint_gt_first = false;
     uint64_t af_line_cap = 0;   // two-sweep AF: line capacity the last run needed
     // region AF schedule: 0 = default (the walk schedule 7 when the first records average
     // >= 512 B, else 3 with one host synchronisation: single-sweep index + head pass +
@@ -247,7 +250,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
         if (b->p) (void)hipFree(b->p);
     for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
     for (hipEvent_t e : c->ingest_ev_free) (void)hipEventDestroy(e);
@@ -296,6 +299,7 @@ static void load_hints(vcfxg_ctx *c, const char *h, size_t n) {
     c->hint_span = 0;
     c->hint_line = 0;
     c->hint_gt_only = false;
+    c->hint_gt_first = false;
     c->walk_overflowed = false;
     size_t p = 0;
     while (p < n && h[p] == '#') {
@@ -314,7 +318,10 @@ static void load_hints(vcfxg_ctx *c, const char *h, size_t n) {
             while (x < e && tabs < 9) {
                 const char *t = (const char *)memchr(h + x, '\t', e - x);
                 if (!t) break;
-                if (tabs == 8) c->hint_gt_only = (size_t)(t - h) - f8 == 2 && h[f8] == 'G' && h[f8 + 1] == 'T';
+                if (tabs == 8) {
+                    c->hint_gt_only = (size_t)(t - h) - f8 == 2 && h[f8] == 'G' && h[f8 + 1] == 'T';
+                    c->hint_gt_first = (size_t)(t - h) - f8 > 3 && h[f8] == 'G' && h[f8 + 1] == 'T' && h[f8 + 2] == ':';
+                }
                 x = (size_t)(t - h) + 1;
                 tabs++;
                 if (tabs == 8) f8 = x;
@@ -650,7 +657,7 @@ static int af_region_async(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summ
 // statuses) are compacted from the regions only when a later call asks for them
 // (ensure_dense).  A walker over its line capacity, or an overlong leftover list, reruns the
 // call on the two-sweep schedule (and later calls on this input use it directly).
-static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
+static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out, bool gf = false) {
     if (c) c->dense_pending = false;  // a new index / regions replace the pending ones
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
@@ -698,7 +705,7 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     HIPCHK(c, vcfxg::launch_af_walk(buf, lo, hi, C, mode, c->hint_span, cap_w, P<uint64_t>(c->wk_le),
                                     P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre),
                                     P<uint8_t>(c->wk_status), c->wk_meta.p, P<uint64_t>(c->wk_count),
-                                    P<uint32_t>(c->wk_gt), ovf, c->stream, nullptr, &tail));
+                                    P<uint32_t>(c->wk_gt), ovf, c->stream, nullptr, &tail, false, gf));
     prof_end(c, "af_walk");
     prof_begin(c, "af_complex");
     HIPCHK(c, vcfxg::launch_af_cx(buf, mode, cap_w, tail.cx_list, cx_n, cap, cap, tail.wstart, P<uint64_t>(c->wk_le),
@@ -797,8 +804,15 @@ int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_su
         int r = vcfxg_index(c, data_start, nullptr);
         return r ? r : vcfxg_allele_freq(c, mode, out);
     }
-    // records of >= 512 B on average (a GT-dense VCF): the walk schedule, no index sweep
+    // records of >= 512 B on average (a GT-dense VCF): the walk schedule, no index sweep; the
+    // GT-first walk for "GT:..." records (VCFXG_AF_GF_WALK=0: the index sweep + per-line sweep)
     if (c->hint_line >= 512 && c->hint_gt_only && !c->walk_overflowed) return af_region_walk(c, data_start, mode, out);
+    static const bool gf_ok = [] {
+        const char *e = getenv("VCFXG_AF_GF_WALK");
+        return !(e && e[0] == '0');
+    }();
+    if (gf_ok && c->hint_line >= 512 && c->hint_gt_first && !c->walk_overflowed)
+        return af_region_walk(c, data_start, mode, out, true);
     return af_region_async(c, data_start, mode, out);
 }
 
@@ -1370,26 +1384,114 @@ int vcfxg_hwe_rechecks(vcfxg_ctx *c, vcfxg_hwe_recheck *out, uint64_t cap, uint6
     return VCFXG_OK;
 }
 
+// the dosage walk: line ends + per fixed-stride record its samples / "NA" samples, compacted to
+// the dense per-line arrays (line_end, alt = ns, tot = na, status, af_meta = LineMeta); the
+// context is indexed afterwards.  *overflow: a walker ran out of line slots (short lines)
+static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *L_out, bool *overflow) {
+    c->dense_pending = false;
+    HIPCHK(c, hipSetDevice(c->device));
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
+    const int64_t C = c->walk_chunk;
+    const int64_t nw = vcfxg::af_walkers(lo, hi, C);
+    const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
+    const uint64_t cap = (uint64_t)nw * cap_w;
+    int r = ensure(c, c->wk_le, 8 * cap);
+    if (!r) r = ensure(c, c->wk_alt, 4 * cap);
+    if (!r) r = ensure(c, c->wk_tot, 4 * cap);
+    if (!r) r = ensure(c, c->wk_rowpre, 4 * cap);
+    if (!r) r = ensure(c, c->wk_status, cap);
+    if (!r) r = ensure(c, c->wk_meta, vcfxg::af_meta_bytes() * cap);
+    if (!r) r = ensure(c, c->wk_count, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_offs, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->wk_gt, 4 * (size_t)nw);
+    if (!r) r = ensure(c, c->wk_small, 128);
+    if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
+    if (!r) r = af_buffers(c, cap);
+    if (!r) r = ensure(c, c->af_meta, vcfxg::af_meta_bytes() * (cap + 1));
+    if (r) return r;
+    const char *buf = P<char>(c->input);
+    uint64_t *small = P<uint64_t>(c->wk_small);
+    HIPCHK(c, hipMemsetAsync(small, 0, 16, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->wk_count) + nw, 0, 8, c->stream));
+    prof_begin(c, "dose_walk");
+    HIPCHK(c, vcfxg::launch_af_walk(buf, lo, hi, C, mode, c->hint_span, cap_w, P<uint64_t>(c->wk_le),
+                                    P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre),
+                                    P<uint8_t>(c->wk_status), c->wk_meta.p, P<uint64_t>(c->wk_count),
+                                    P<uint32_t>(c->wk_gt), reinterpret_cast<unsigned *>(small), c->stream, nullptr,
+                                    nullptr, true));
+    prof_end(c, "dose_walk");
+    prof_begin(c, "walk_compact");
+    r = exclusive_scan(c, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_offs), (size_t)nw + 1);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_walk_compact(nw, cap_w, P<uint64_t>(c->wk_offs), P<uint32_t>(c->wk_gt),
+                                         P<uint64_t>(c->wk_le), P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot),
+                                         P<uint32_t>(c->wk_rowpre), P<uint8_t>(c->wk_status), c->wk_meta.p,
+                                         P<uint64_t>(c->line_end), P<int32_t>(c->alt), P<int32_t>(c->tot),
+                                         P<uint32_t>(c->rowpre), P<uint8_t>(c->status), c->af_meta.p,
+                                         P<uint64_t>(c->d_nlines), P<unsigned long long>(c->counters), c->stream));
+    prof_end(c, "walk_compact");
+    static thread_local uint64_t h[2];  // overflow flag, lines
+    HIPCHK(c, hipMemcpyAsync(&h[0], small, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&h[1], c->d_nlines.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *overflow = (h[0] & 0xFFFFFFFFull) != 0;
+    if (*overflow) {
+        c->walk_overflowed = true;
+        return VCFXG_OK;
+    }
+    c->data_start = data_start;
+    c->n_lines = h[1];
+    c->indexed = true;
+    *L_out = h[1];
+    return VCFXG_OK;
+}
+
 // VCFX_dosage_calculator over [data_start, n): the line index, the row lengths, a scan, the
-// rows (one host synchronisation for the text size)
+// rows (one host synchronisation for the text size).  Records of >= 512 B (a GT-dense VCF): the
+// walk reads each record once for its line end and (fixed-stride records) its samples and "NA"
+// samples -- no index sweep, no row-length pass over the records; the other lines take the
+// exact row-length pass; VCFXG_DOSE_WALK=0 keeps the index + two-pass schedule
+static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *L_out, bool *overflow);
+
 int vcfxg_dosage_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
+    static const bool walk_ok = [] {
+        const char *e = getenv("VCFXG_DOSE_WALK");
+        return !(e && e[0] == '0');
+    }();
+    const bool walk = walk_ok && c->af_path != 3 && c->af_path != 8 && c->hint_line >= 512 && c->hint_gt_only &&
+                      !c->walk_overflowed && vcfxg::af_walkers((int64_t)data_start, (int64_t)c->n, c->walk_chunk) > 0;
     uint64_t L = 0;
-    int r = vcfxg_index(c, data_start, &L);
-    if (r) return r;
+    int r;
+    bool walked = false;
+    if (walk) {
+        bool ovf = false;
+        r = dose_walk_index(c, data_start, mode, &L, &ovf);
+        if (r) return r;
+        walked = !ovf;
+    }
+    if (!walked) {
+        r = vcfxg_index(c, data_start, &L);
+        if (r) return r;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     r = af_buffers(c, L);
-    if (!r) r = ensure(c, c->af_meta, vcfxg::dose_meta_bytes() * (L + 1));
+    if (!r) r = ensure(c, c->dose_meta, vcfxg::dose_meta_bytes() * (L + 1));
     if (r) return r;
     const char *buf = P<char>(c->input);
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
     HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->rowlen) + L, 0, 8, c->stream));
     prof_begin(c, "dose_len");
+    if (walked)
+        HIPCHK(c, vcfxg::launch_dose_from_walk(P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L, c->af_meta.p,
+                                               P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint8_t>(c->status),
+                                               P<uint64_t>(c->rowlen), c->dose_meta.p,
+                                               P<unsigned long long>(c->counters), c->stream));
     HIPCHK(c, vcfxg::launch_dose_len(buf, (int64_t)data_start, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L,
-                                     mode, P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->af_meta.p,
-                                     P<unsigned long long>(c->counters), c->stream));
+                                     mode, P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->dose_meta.p,
+                                     P<unsigned long long>(c->counters), c->stream, walked));
     prof_end(c, "dose_len");
     prof_begin(c, "dose_rows");
     r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)L + 1);
@@ -1404,7 +1506,7 @@ int vcfxg_dosage_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary
     if (r) return r;
     prof_begin(c, "dose_fmt");
     HIPCHK(c, vcfxg::launch_dose_fmt(buf, (int64_t)data_start, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L,
-                                     P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
+                                     P<uint8_t>(c->status), c->dose_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
                                      ~0ull, tail[2], c->stream));
     prof_end(c, "dose_fmt");
     HIPCHK(c, hipStreamSynchronize(c->stream));

@@ -385,13 +385,62 @@ static unsigned dose_grid(int64_t n, int64_t per, unsigned cap) {
 
 size_t dose_meta_bytes() { return sizeof(DoseMeta); }
 
+// the walk's lines -> dose statuses (thread per line): a fixed-stride GT-only record (walk
+// status 1) is a kDoseFast row of pre + 2 ns + na bytes; '#' / empty lines are skipped; the
+// rest (fewer than 9 tabs, other FORMATs, GT records off the fixed-stride layout) pending
+__global__ void k_dose_from_walk(const uint64_t *__restrict__ line_end, const uint64_t *n_lines_p,
+                                 const LineMeta *__restrict__ wm, const int32_t *__restrict__ ns,
+                                 const int32_t *__restrict__ na, uint8_t *__restrict__ status,
+                                 uint64_t *__restrict__ len, DoseMeta *__restrict__ meta,
+                                 unsigned long long *__restrict__ counters) {
+    const uint64_t n_lines = *n_lines_p;
+    uint32_t rows = 0;
+    for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < n_lines;
+         li += (uint64_t)gridDim.x * blockDim.x) {
+        const LineMeta w = wm[li];
+        DoseMeta m{};
+        uint8_t st = kDosePend;
+        uint64_t L = 0;
+        if (w.kind == kMetaEmpty || w.kind == kMetaHeader) st = kDoseSkip;
+        else if (w.kind == kMetaGt && status[li] == 1) {
+            const uint64_t ae = line_end[li] - w.cr;
+            m.S = w.S;
+            m.pre = w.rowpre;
+            m.ae = (uint32_t)(ae - w.S);
+            m.gi = 0;
+            m.kind = kDoseFast;
+            m.plain = na[li] == 0;
+            st = kDoseRow;
+            L = (uint64_t)m.pre + 2u * (uint64_t)ns[li] + (uint64_t)na[li];
+            rows++;
+        }
+        status[li] = st;
+        len[li] = L;
+        meta[li] = m;
+    }
+    rows = wave_sum(rows);
+    if (lane() == 0 && rows) atomicAdd(&counters[0], (unsigned long long)rows);
+}
+
+hipError_t launch_dose_from_walk(const uint64_t *line_end, const uint64_t *n_lines_dev, uint64_t n_lines_host,
+                                 const void *walk_meta, const int32_t *ns, const int32_t *na, uint8_t *status,
+                                 uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s) {
+    if (!n_lines_host) return hipSuccess;
+    const unsigned g = (unsigned)std::min<uint64_t>((n_lines_host + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_dose_from_walk, dim3(g), dim3(256), 0, s, line_end, n_lines_dev,
+                       static_cast<const LineMeta *>(walk_meta), ns, na, status, len, static_cast<DoseMeta *>(meta),
+                       counters);
+    return hipGetLastError();
+}
+
 hipError_t launch_dose_len(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, int mode, uint8_t *status, uint64_t *len, void *meta,
-                           unsigned long long *counters, hipStream_t s) {
+                           unsigned long long *counters, hipStream_t s, bool pending_only) {
     if (!n_lines_host) return hipSuccess;
     const dim3 g(dose_grid((int64_t)n_lines_host, kDoseWaves, 2048));
-    hipLaunchKernelGGL(k_dose_len<true>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode,
-                       status, len, static_cast<DoseMeta *>(meta), counters);
+    if (!pending_only)
+        hipLaunchKernelGGL(k_dose_len<true>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode,
+                           status, len, static_cast<DoseMeta *>(meta), counters);
     hipLaunchKernelGGL(k_dose_len<false>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev, mode,
                        status, len, static_cast<DoseMeta *>(meta), counters);
     return hipGetLastError();

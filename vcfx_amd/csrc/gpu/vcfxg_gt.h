@@ -596,6 +596,24 @@ __device__ __forceinline__ int hwe_parse(const char *__restrict__ buf, int64_t p
     return 1;
 }
 
+// VCFX_dosage_calculator's row-length pass on the walk (fixed-stride records): samples and the
+// samples that print "NA" (not both alleles digits), as k_dose_len's DoseCountOp on gt_fast
+struct DoseWalkOp {
+    const char *buf;
+    int64_t E;
+    uint32_t ns = 0, na = 0;
+    __device__ void begin(uint32_t, uint32_t) {}
+    __device__ bool done() const { return false; }
+    __device__ void dword(const DwordView &v) {
+        ns += v.real;
+        na += v.real && v.dig != 0x01000100u;
+    }
+    __device__ void finish() {
+        ns = wave_sum(ns);
+        na = wave_sum(na);
+    }
+};
+
 struct HweOp {
     const char *buf;
     int64_t E;

@@ -65,7 +65,8 @@ struct WalkTail {
 hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int mode, int64_t span0,
                           uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
                           uint8_t *status_b, void *meta_b, uint64_t *wcount, uint32_t *wgt, unsigned *overflow,
-                          hipStream_t s, int32_t *hwe_aux_b = nullptr, const WalkTail *tail = nullptr);
+                          hipStream_t s, int32_t *hwe_aux_b = nullptr, const WalkTail *tail = nullptr,
+                          bool dose = false, bool gt_first_walk = false);
 // AF region tail without the dense per-line arrays (vcfxg_kernels.hip):
 //   launch_af_cx       the walk's leftover slots: af_line / the general sweep, new rows' bytes
 //                      added to their walker's total (counters as k_af_complex)
@@ -147,7 +148,13 @@ hipError_t launch_hwe_format(const char *buf, int64_t data_start, const uint64_t
 size_t dose_meta_bytes();
 hipError_t launch_dose_len(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, int mode, uint8_t *status, uint64_t *len, void *meta,
-                           unsigned long long *counters, hipStream_t s);
+                           unsigned long long *counters, hipStream_t s, bool pending_only = false);
+// after the dosage walk (launch_af_walk dose, compacted): the walk's fixed-stride GT-only lines
+// become rows (ns = alt, na = tot), '#' / empty lines are skipped, every other line is left
+// pending for launch_dose_len(pending_only); status is rewritten in place, meta is the dose meta
+hipError_t launch_dose_from_walk(const uint64_t *line_end, const uint64_t *n_lines_dev, uint64_t n_lines_host,
+                                 const void *walk_meta, const int32_t *ns, const int32_t *na, uint8_t *status,
+                                 uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s);
 hipError_t launch_dose_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, const uint8_t *status, const void *meta, const uint64_t *off,
                            char *out, uint64_t cap, uint64_t slow_rows, hipStream_t s);

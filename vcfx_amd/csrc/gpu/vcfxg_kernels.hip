@@ -838,7 +838,9 @@ __global__ __launch_bounds__(kWScan) void k_walker_scan(int64_t nw, const uint64
     const int64_t nb = (nw + kWScan - 1) / kWScan;
     const int64_t w = (int64_t)blockIdx.x * kWScan + t;
     const uint64_t a0 = w < nw ? wcount[w] : 0, b0 = w < nw ? wtext[w] : 0;
-    uint32_t g = w < nw ? wgt[w] : 0u;
+    // wgt: GT-first lines (low 16 bits) | the GT-first walk's lines swept by gt_first (high 16)
+    const uint32_t gw = w < nw ? wgt[w] : 0u;
+    uint64_t g = (uint64_t)(gw & 0xFFFFu) | ((uint64_t)(gw >> 16) << 32);
     uint64_t a = a0, b = b0;
     block_scan2(a, b, sa, sb);
     if (w <= nw) {  // (w == nw: the block total, the end offset within this block)
@@ -847,7 +849,7 @@ __global__ __launch_bounds__(kWScan) void k_walker_scan(int64_t nw, const uint64
     }
     g = wave_sum(g);
     __syncthreads();
-    __shared__ uint32_t sg[kWScan / kWave];
+    __shared__ uint64_t sg[kWScan / kWave];
     if (lane() == 0) sg[t / kWave] = g;
     __syncthreads();
     if (t == kWScan - 1) {
@@ -879,8 +881,9 @@ __global__ __launch_bounds__(kWScan) void k_walker_scan(int64_t nw, const uint64
             wtoff[nw] = 0;
         }
         *done = 0;  // ready for the next launch
-        counters[0] += G;
-        counters[1] += G;
+        counters[0] += G & 0xFFFFFFFFull;
+        counters[1] += G & 0xFFFFFFFFull;
+        counters[3] += G >> 32;  // records of the general (gt_first) sweep
         *n_lines = ra;
         summary[0] = ra;
         summary[1] = rb;

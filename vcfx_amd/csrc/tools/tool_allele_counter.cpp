@@ -183,7 +183,8 @@ size_t file_header(const Input &in, std::vector<std::string> &names) {
         if (is_chrom_line(ls, (size_t)(le - ls))) chrom_names(ls, le, names);
         p = q;
     }
-    return in.n;
+    // a shard view (VCFX_INPUT_VIEW / a multi-GPU rank): its records follow the header part
+    return in.tail && p >= end ? in.host_n : in.n;
 }
 
 int hw_threads() {

@@ -107,7 +107,7 @@ extern "C" int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int 
         }
     }
     gs.done();
-    if (!input && optind < argc) input = argv[optind];
+    if (!input && gs.next < argc) input = argv[gs.next];
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
     uint64_t v = 0, l = 0;

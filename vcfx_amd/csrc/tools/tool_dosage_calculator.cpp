@@ -115,7 +115,7 @@ extern "C" int vcfx_tool_dosage_calculator(int argc, char **argv, int in_fd, int
         else help = true;
     }
     gs.done();
-    if (!input && optind < argc) input = argv[optind];
+    if (!input && gs.next < argc) input = argv[gs.next];
     if (help) {
         out.put(kHelp);
         return 0;

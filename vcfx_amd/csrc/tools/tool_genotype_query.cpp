@@ -178,7 +178,7 @@ extern "C" int vcfx_tool_genotype_query(int argc, char **argv, int in_fd, int ou
         if (!ok) break;
     }
     gs.done();
-    if (ok && optind < argc && input.empty()) input = argv[optind];
+    if (ok && gs.next < argc && input.empty()) input = argv[gs.next];
     if (!ok || query.empty()) {
         err.put(std::string("Usage: ") + argv[0] + " -g \"0/1\" [--strict] [-i FILE] [-q]\n");
         err.put("Use --help for usage.\n");

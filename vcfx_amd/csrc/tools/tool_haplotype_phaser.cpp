@@ -306,7 +306,7 @@ extern "C" int vcfx_tool_haplotype_phaser(int argc, char **argv, int in_fd, int 
         }
     }
     gs.done();
-    if (input.empty() && optind < argc) input = argv[optind];
+    if (input.empty() && gs.next < argc) input = argv[gs.next];
     if (help) {
         out.put(kHelp);
         return 0;

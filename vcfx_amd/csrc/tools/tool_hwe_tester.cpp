@@ -154,7 +154,7 @@ extern "C" int vcfx_tool_hwe_tester(int argc, char **argv, int in_fd, int out_fd
         else help = true;
     }
     gs.done();
-    if (!input && optind < argc) input = argv[optind];
+    if (!input && gs.next < argc) input = argv[gs.next];
     if (help) {
         out.put(kHelp);
         return 0;

@@ -269,7 +269,7 @@ extern "C" int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out
         }
     }
     gs.done();
-    if (optind < argc && o.input.empty()) o.input = argv[optind];
+    if (gs.next < argc && o.input.empty()) o.input = argv[gs.next];
     if (show) {
         out.put(kLdHelp);
         return 0;

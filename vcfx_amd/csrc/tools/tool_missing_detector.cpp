@@ -192,7 +192,7 @@ extern "C" int vcfx_tool_missing_detector(int argc, char **argv, int in_fd, int 
     }
     gs.done();
     if (rc >= 0) return rc;
-    if (!input && optind < argc) input = argv[optind];
+    if (!input && gs.next < argc) input = argv[gs.next];
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
     if (input) {

@@ -138,7 +138,7 @@ extern "C" int vcfx_tool_nonref_filter(int argc, char **argv, int in_fd, int out
         else help = true;  // -h and anything getopt rejects: the help text
     }
     gs.done();
-    if (input.empty() && optind < argc) input = argv[optind];
+    if (input.empty() && gs.next < argc) input = argv[gs.next];
     if (help) {
         out.put(kHelp);
         return 0;

@@ -220,7 +220,7 @@ extern "C" int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out
         }
     }
     gs.done();
-    if (optind < argc && input.empty()) input = argv[optind];
+    if (gs.next < argc && input.empty()) input = argv[gs.next];
     if (show || argc == 1) {
         out.put(kHelp);
         return 0;

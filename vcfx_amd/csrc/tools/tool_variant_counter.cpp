@@ -125,9 +125,9 @@ extern "C" int vcfx_tool_variant_counter(int argc, char **argv, int in_fd, int o
     }
     long total;
     Input in;
-    if (optind < argc) {
-        if (!in.open_file(argv[optind])) {
-            err.put(std::string("Error: cannot open file: ") + argv[optind] + "\n");
+    if (gs.next < argc) {
+        if (!in.open_file(argv[gs.next])) {
+            err.put(std::string("Error: cannot open file: ") + argv[gs.next] + "\n");
             return 1;
         }
         total = count_lines(in.p, in.n, true, strict, err);

@@ -5,6 +5,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <getopt.h>
+
 #include <mutex>
 #include <string>
 #include <vector>
@@ -45,7 +47,9 @@ struct GetoptStderr {
         saved = stderr;
         stderr = mem;
     }
+    int next = 0;  // optind when the argument phase ended (read it, not optind, afterwards)
     void done() {
+        if (lk.owns_lock()) next = optind;
         if (mem) {
             fflush(mem);
             stderr = saved;
