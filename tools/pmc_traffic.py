@@ -3,6 +3,9 @@
 
 usage: pmc_traffic.py WORKLOAD FETCH_CSV WRITE_CSV [OUT_JSON]
 
+The kernels found are merged into OUT_JSON[WORKLOAD] (a second input of the same workload,
+e.g. LD on data with missing calls, adds the masked-LD kernels beside the first run's).
+
 FETCH_CSV / WRITE_CSV are the *_counter_collection.csv files of two SEPARATE runs
 (`rocprofv3 --pmc FETCH_SIZE ...` and `rocprofv3 --pmc WRITE_SIZE ...`; the two counters do
 not fit one pass on gfx950).  FETCH_SIZE / WRITE_SIZE are reported in KB (x1024 bytes);
@@ -42,6 +45,9 @@ KERNELS = {
     "ld_count_gen": r"vcfxg::k_ld_block<1>\(",
     "ld_emit_gen": r"vcfxg::k_ld_block<2>\(",
     "ld_matrix": r"vcfxg::k_ld_matrix\(",
+    "ld_pack_vq": r"vcfxg::k_ld_pack_vq\(",
+    "ld_count_mask": r"vcfxg::k_ld_mask<1>\(",
+    "ld_emit_mask": r"vcfxg::k_ld_mask<2>\(",
 }
 
 
@@ -55,7 +61,7 @@ TIMED = {
     "pipeline": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "rf_records", "gq_records"),
     "nonref": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "nr_records"),
     "ld": ("line_count", "line_emit", "line_compact", "ld_parse", "ld_count", "ld_emit", "ld_count_gen",
-           "ld_emit_gen", "ld_matrix"),
+           "ld_emit_gen", "ld_matrix", "ld_pack_vq", "ld_count_mask", "ld_emit_mask"),
 }
 
 
@@ -98,7 +104,7 @@ def main():
             d = json.load(f)
     except (OSError, ValueError):
         d = {}
-    res = {}
+    res = dict(d.get(workload, {}))
     for k in sorted(set(fetch) | set(write)):
         if workload in TIMED and k not in TIMED[workload]:
             continue
@@ -111,7 +117,7 @@ def main():
                   "(gfx950 wide streaming reads, MI355X_MICROARCH.md HBM section); mean per dispatch")
     with open(out, "w") as f:
         json.dump(d, f, indent=1, sort_keys=True)
-    print(json.dumps(res, indent=1))
+    print(json.dumps({k: res[k] for k in sorted(set(fetch) | set(write)) if k in res}, indent=1))
 
 
 if __name__ == "__main__":

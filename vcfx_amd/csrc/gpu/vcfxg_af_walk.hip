@@ -43,11 +43,7 @@ namespace vcfxg {
 #ifndef VCFXG_WALK_UNROLL
 #define VCFXG_WALK_UNROLL 6
 #endif
-constexpr int kWalkUnroll = VCFXG_WALK_UNROLL;
-// 1: the AF walk's sweep reads raw blocks and rotates (gt_fast_bytes); 0: gt_fast
-#ifndef VCFXG_WALK_BYTES
-#define VCFXG_WALK_BYTES 0
-#endif  // wave-steps (KiB) of a record in flight per sweep step
+constexpr int kWalkUnroll = VCFXG_WALK_UNROLL;  // wave-steps (KiB) of a record in flight per sweep step
 
 // the walk's per-record reducer: AF allele counts (alt, total) or, for VCFX_hwe_tester, the
 // genotype classes (hom-ref, het, hom-alt; the third in aux_o)
@@ -277,11 +273,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                       : t8 + 2 < wend ? (uint8_t)sep_w
                                       : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
                 Op op = R::make(buf, ae);
-#if VCFXG_WALK_BYTES
-                if constexpr (std::is_same<Op, AfOp>::value) ok = gt_fast_bytes<kWalkUnroll>(buf, S, ae, op, sep, pre);
-                else
-#endif
-                    ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
+                ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
                 R::out(op, alt, tot, aux);
             }
         };

@@ -134,71 +134,6 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
     return true;
 }
 
-// gt_fast for reducers that take each allele byte on its own (Op::kPerByte: AF's allele
-// counts never pair the two alleles of a sample).  The same acceptance set as gt_fast -- every
-// byte of [S, E) checked against its position's class (allele, separator, tab) -- but read as
-// the raw 16 B blocks: a raw dword at D holds classes ((j - S) mod 4) at bytes j, so rotating it
-// by S mod 4 (v_alignbyte of the dword with itself) gives the canonical "a s b \t" layout
-// without the neighbouring 4 bytes (no second load per block, no cross-dword alignment); the
-// bytes outside [S, E) of the record's first and last dwords are replaced by the neutral
-// ". ." / separator / tab bytes.
-template <int kUnroll = VCFXG_UNROLL, class Op, class Pre = NoPre>
-__device__ bool gt_fast_bytes(const char *__restrict__ buf, int64_t S, int64_t E, Op &op, uint32_t sep_hint = 0,
-                              Pre pre = Pre()) {
-    S = uniform64(S);
-    E = uniform64(E);
-    const int64_t L = E - S;
-    if (L < 3 || ((L + 1) & 3)) return false;
-    uint32_t sepc = sep_hint ? sep_hint : byte_at(buf, S + 1);
-    sepc = __builtin_amdgcn_readfirstlane(sepc);
-    if (sepc != '/' && sepc != '|') return false;
-    const uint32_t exp_xor = 0x09000000u | (sepc << 8) | 0x00300030u;
-    const uint32_t neutral = 0x092E002Eu | (sepc << 8);
-    op.begin(sepc, neutral);
-    const int s = (int)(S & 3);
-    const int64_t b0 = S & ~(int64_t)15;
-    const char *__restrict__ base = buf + b0;
-    const int Sr = (int)(S - b0), Er = (int)(E - b0);
-    const int lastblk = (Er - 1) & ~15;
-    uint32_t err = 0;
-    const int lo16 = lane() * kBlockBytes;
-    for (int w0 = 0; w0 < Er; w0 += kUnroll * kWaveStep) {
-        uint4 v[kUnroll];
-#pragma unroll
-        for (int u = 0; u < kUnroll; u++) {  // branch-free: lanes past the record re-read its last block
-            const int blk = w0 + u * kWaveStep + lo16;
-            v[u] = load16(base, blk < Er ? blk : lastblk);
-        }
-        if (w0 == 0) pre();
-#pragma unroll
-        for (int u = 0; u < kUnroll; u++) {
-            const int w = w0 + u * kWaveStep;
-            const int blk = w + lo16;
-            const bool interior = w >= Sr && w + kWaveStep <= Er;  // every byte of the step in [S, E)
-            if (blk < Er) {
-                const uint32_t d[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    uint32_t r = __builtin_amdgcn_alignbyte(d[i], d[i], s);
-                    if (!interior) {  // raw bytes [lo, hi) of this dword lie in [S, E)
-                        const int D = blk + 4 * i;
-                        const int lo = min(max(Sr - D, 0), 4), hi = min(max(Er - D, 0), 4);
-                        const uint32_t below = lo >= 4 ? 0xFFFFFFFFu : (1u << (8 * lo)) - 1u;
-                        const uint32_t upto = hi >= 4 ? 0xFFFFFFFFu : (1u << (8 * hi)) - 1u;
-                        uint32_t keep = upto & ~below;
-                        keep = __builtin_amdgcn_alignbyte(keep, keep, s);
-                        r = (r & keep) | (neutral & ~keep);
-                    }
-                    fast_dword(r, exp_xor, err, op, true, 0);
-                }
-            }
-        }
-        if (__any(err != 0u)) return false;  // not fixed-stride: stop reading the record
-    }
-    op.finish();
-    return true;
-}
-
 // general path: op.sample(st) for every sample start (S, and every tab+1 < E), one lane
 // per start in its 16 B block; op.finish() reduces across the wave.
 template <class Op>
