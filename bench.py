@@ -332,6 +332,8 @@ def output_check(workload, eng, s, a, rank, arr=None):
         what = "sha256 of the first %d variants' pair lines vs VCFX_ld_calculator -w 100000 -t 0.5 (reference)" % (
             dig["inputs"][c["input"]]["n_records"])
     if got != want:
+        if os.environ.get("VCFX_BENCH_ABLATION"):  # diagnostic builds (results invalid by design)
+            return {"checked": True, "match": False, "case": case, "what": what}
         raise AssertionError("bench output differs from the reference: %s (%s != %s)" % (what, got, want))
     return {"checked": True, "match": True, "case": case, "what": what}
 
