@@ -55,7 +55,7 @@ struct vcfxg_ctx {
     std::string query_host, crit_host, pool_host;  // host sources of in-flight async copies
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
-        ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff, ld_Gv, ld_Gq, dose_meta, ld_terms;
+        ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff, ld_Gv, ld_Gq, dose_meta;
     bool ld_vq = false;  // ld_Gv / ld_Gq (valid-mask and squared-dosage FP4 planes) are current
     int n_cu = 0;
     DevBuf async_small;         // asynchronous AF path: line range {0, n}, failure flags, summary
@@ -250,7 +250,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->ld_terms, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
         if (b->p) (void)hipFree(b->p);
     for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
     for (hipEvent_t e : c->ingest_ev_free) (void)hipEventDestroy(e);
@@ -1981,8 +1981,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     }
     // block lists.  Count-table columns are 64-blocks: row block J pairs with column blocks
     // I0(J) = (J*64 - window)/64 .. J.  Pairs of 256-groups that are all complete go to the
-    // X.X^T kernel (k_ld_fast: 128-row x 256-column tiles); every other 64-block to the
-    // missing-data kernel.
+    // 256x256 X.X^T kernel (k_ld_fast); every other 64-block to the general kernel.
     const uint64_t FB = vcfxg::kLdFastBlock;
     auto ifirst = [&](uint64_t J) { const uint64_t jr0 = J * BM; return jr0 > window ? (jr0 - window) / BM : 0; };
     const std::vector<uint8_t> &gf = c->ld_gflag_host;
@@ -2007,12 +2006,10 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
                 if (!gf[J]) continue;
                 const uint64_t Imin = std::max(I0, ifirst(kSub * J) / kSub), Imax = std::min(I0 + kSuper, J + 1);
                 for (uint64_t I = Imin; I < Imax; I++)
-                    if (gf[I])
-                        for (uint64_t I2 = 2 * I; I2 < 2 * I + 2; I2++)  // the group's two 128-row tiles
-                            if (2 * I2 + 1 >= ifirst(kSub * J)) {        // (one wholly before the window: none)
-                                blocks.push_back((uint32_t)I2);
-                                blocks.push_back((uint32_t)J);
-                            }
+                    if (gf[I]) {
+                        blocks.push_back((uint32_t)I);
+                        blocks.push_back((uint32_t)J);
+                    }
             }
     }
     const uint32_t nfast = (uint32_t)(blocks.size() / 2);
@@ -2076,18 +2073,6 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     a.tm = threshold - (1e-6 + 1e-10 * (double)c->ld_ns);
     a.all_pass = a.tm <= 0.0;
     a.kp4 = c->ld_kp4;
-    // the complete-tile kernel's prefilter terms for this threshold (8 B per row and column)
-    vcfxg::LdTerms terms;
-    if (nfast) {
-        const uint64_t ng256 = (M + FB - 1) / FB + 1, ng128 = 2 * ng256;
-        r = ensure(c, c->ld_terms, 4 * (ng128 * 2 * vcfxg::kLdFastRows + ng256 * 2 * FB));
-        if (r) return r;
-        float *trow = P<float>(c->ld_terms), *tcol = trow + ng128 * 2 * vcfxg::kLdFastRows;
-        HIPCHK(c, vcfxg::launch_ld_terms(P<vcfxg::LdFast>(c->ld_fast), M, a.tm, a.ns, a.all_pass, trow, tcol,
-                                         c->stream));
-        terms.row = trow;
-        terms.col = tcol;
-    }
     const uint32_t *cid = max_dist > 0 ? P<uint32_t>(c->ld_cid) : nullptr;
     const uint32_t *fbl = P<uint32_t>(c->ld_blocks), *gbl = fbl + 2 * (size_t)nfast;
     // staging for the pairs the count pass finds (capacity: what the last chunk needed, at
@@ -2111,7 +2096,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     }
     prof_begin(c, "ld_count");
     HIPCHK(c, vcfxg::launch_ld_fast(1, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
-                                    P<uint16_t>(c->ld_cnt), vcfxg::LdOffsets{}, nullptr, stg, terms, c->stream));
+                                    P<uint16_t>(c->ld_cnt), vcfxg::LdOffsets{}, nullptr, stg, c->stream));
     prof_end(c, "ld_count");
     prof_begin(c, "ld_count_gen");
     HIPCHK(c, vcfxg::launch_ld_block(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,
@@ -2151,7 +2136,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     else
         HIPCHK(c, vcfxg::launch_ld_fast(2, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
                                         P<uint16_t>(c->ld_cnt), offs, P<vcfxg::LdPair>(c->ld_pairs),
-                                        vcfxg::LdStage{}, terms, c->stream));
+                                        vcfxg::LdStage{}, c->stream));
     prof_end(c, "ld_emit");
     prof_begin(c, "ld_emit_gen");
     HIPCHK(c, vcfxg::launch_ld_block(2, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,

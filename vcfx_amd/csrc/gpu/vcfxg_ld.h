@@ -6,8 +6,7 @@
 namespace vcfxg {
 
 constexpr int kLdBlock = 64;       // count-table granularity (64-variant blocks)
-constexpr int kLdFastBlock = 256;  // complete-group side; the X.X^T kernel's tile columns (vcfxg_ld_fast.hip)
-constexpr int kLdFastRows = 128;   // the X.X^T kernel's tile rows
+constexpr int kLdFastBlock = 256;  // complete-group tile of the X.X^T kernel (vcfxg_ld_fast.hip)
 constexpr int kLdMaskTile = 128;   // tile of the missing-data kernel (vcfxg_ld_mask.hip)
 
 struct LdParseArgs {
@@ -107,18 +106,9 @@ struct LdStage {
 hipError_t launch_ld_scatter(const LdQuarter *quarters, const unsigned long long *ctr, uint64_t nq_host,
                              const LdWindowArgs &a, const uint16_t *cnt, LdOffsets off, const LdPair *temp,
                              LdPair *pairs, hipStream_t s);
-// per-call prefilter terms of the complete-tile kernel (k_ld_terms): per 128-row group
-// {u[128], Sx[128]}, per 256-column group {w[256], v[256]} (fp32)
-struct LdTerms {
-    const float *row = nullptr;
-    const float *col = nullptr;
-};
-hipError_t launch_ld_terms(const LdFast *fv, uint64_t m, double tm, int ns, int all_pass, float *row, float *col,
-                           hipStream_t s);
-// tiles: (I2, J4) = (128-row group, 256-column group) pairs
 hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const uint32_t *chrom_id,
                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
-                          LdOffsets off, LdPair *pairs, const LdStage &st, const LdTerms &tm, hipStream_t s);
+                          LdOffsets off, LdPair *pairs, const LdStage &st, hipStream_t s);
 hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, uint8_t *gflag, hipStream_t s);
 hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s);
 hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C, hipStream_t s);

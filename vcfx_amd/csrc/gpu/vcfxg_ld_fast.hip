@@ -1,34 +1,30 @@
-// vcfxg_ld_fast.hip -- LD r^2 for variant tiles whose genotypes are complete.
+// vcfxg_ld_fast.hip -- LD r^2 for 256x256 variant blocks whose genotypes are complete.
 //
 // The common case of VCFX_ld_calculator's pair loop (computeLDStreamingMmap :511-648 /
 // computeLDStreaming :864-987 calling computeRsqFast :397-401): with no missing genotype
 // among the ns samples, the pair sums need only S_xy = X.X^T (n = ns and Sx, Sx2 are
-// per-variant), so a tile is one GEMM tile over the dosages 0/1/2:
+// per-variant), so a block is one GEMM tile over the dosages 0/1/2:
 //   * operands: FP4 (e2m1) rows -- 0, 1, 2 are exact e2m1 values and every product and
 //     partial sum is an integer below 2^24, so the fp32-accumulating block-scaled MFMA
 //     (scales 2^0) computes S_xy exactly at twice the int8 rate and half the operand bytes;
-//     zero padding needs no correction.  K = kp4 bytes (2 dosages per byte), staged in
-//     64-byte k-slices by global_load_lds (16 B/lane, lane-linear LDS image, XOR-swizzled
-//     16 B slots via the SOURCE address so the ds_read_b128 fragment reads are bank-conflict
-//     free) into a 3-buffer ring, fragments read one k-half ahead of the MFMAs (counted
-//     vmcnt + raw s_barrier between two MFMA groups);
-//   * a tile is 128 rows (variants i) x 256 columns (variants j), 4 waves as 2 (I) x 2 (J),
-//     each a 64x128 output = 2x4 v_mfma_scale_f32_32x32x64_f8f6f4 accumulators (128
-//     registers), so per k-step a wave reads 6 fragments for 8 MFMAs;
-//   * TWO tiles per CU (76.8 KB of LDS and <= 256 registers per lane each): one tile's
-//     prologue (ring fill) and count epilogue (VALU) run while the other tile's waves issue
-//     MFMAs on the same SIMDs.  With one 256x256 tile per CU (r01-r03) the MFMAs sat idle
-//     through every tile's fill and epilogue (MFMA busy 43 %);
-//   * the per-variant prefilter terms are precomputed per call (k_ld_terms: 8 B per row /
-//     column) and DMA'd into LDS with the first stages;
-//   * count epilogue straight from the accumulators (ld_count_regs): an fp32 prefilter with
-//     an explicit error bound keeps every pair that can reach the threshold; candidates run
-//     the reference's fp64 operation sequence (correctly rounded __d*_rn ops, per-variant
-//     mean / variance / sqrt precomputed with the same ops), so the kept r^2 and the
-//     threshold decision are bit-identical to the reference;
+//     zero padding needs no correction.  256 rows of I and 256 rows of J, K = kp4 bytes
+//     (2 dosages per byte), staged in 64-byte k-slices
+//     by global_load_lds (16 B/lane, lane-linear LDS image, XOR-swizzled 16 B slots via the
+//     SOURCE address so the ds_read_b128 fragment reads are bank-conflict free) into a
+//     4-buffer ring, fragments read one k-half ahead of the MFMAs (counted vmcnt + raw
+//     s_barrier between two MFMA groups);
+//   * 8 waves as 4 (I) x 2 (J), each a 64x128 output = 2x4 v_mfma_scale_f32_32x32x64_f8f6f4
+//     accumulators: per k-step a wave reads 6 fragments for 8 MFMAs, and the block loads
+//     32 KiB per 128 MFMAs (half the operand traffic per MFMA of a 128x128 block);
+//   * epilogue per 64x64 quarter of a wave's output (two per wave): the int32 tile goes to
+//     the wave's own LDS region and each lane walks one column: an exact integer prefilter
+//     (C = n*Sxy - Sx*Sy; r^2 = C^2/(Vx*Vy)) rejects pairs whose exact r^2 is below
+//     threshold - delta; candidates run the reference's fp64 operation sequence (correctly
+//     rounded __d*_rn ops, per-variant mean / variance / sqrt precomputed with the same
+//     ops), so the kept r^2 and the threshold decision are bit-identical to the reference;
 //   * every 64x64 quarter is one 64-block of the count table (cnt[row j][column block])
-//     shared with the other LD kernels, so pass 1 counts (and stages the pairs of quarters
-//     holding some) and pass 2 writes pairs in the reference's (j, i) order.
+//     shared with the general kernel (vcfxg_ld.hip k_ld_block), so pass 1 counts and pass 2
+//     writes pairs in the reference's (j, i) order; pass 2 skips blocks with no pair.
 #include "vcfxg_device.h"
 #include "vcfxg_ld.h"
 
@@ -36,7 +32,7 @@
 #include <type_traits>
 
 // VCFXG_LD_EXPT (diagnostic builds only, results invalid): bit 0 skips the epilogue, bit 3
-// stages k-slice 0 every step, bit 4 reads rows 0..383 for every tile
+// stages k-slice 0 every step, bit 4 reads rows 0..255 for every block
 #ifndef VCFXG_LD_EXPT
 #define VCFXG_LD_EXPT 0
 #endif
@@ -49,20 +45,20 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr int kFmtFp4 = 4;              // cbsz / blgp operand format: e2m1
 constexpr int kScaleOne = 0x7F7F7F7F;   // E8M0 block scales 2^0
 
-constexpr int kTI = kLdFastRows;       // tile rows (variants i): 128
-constexpr int kTJ = kLdFastBlock;      // tile columns (variants j): 256
+constexpr int kFB = kLdFastBlock;      // block side (variants): 256
 constexpr int kBK = 64;                // k-slice bytes per stage
-constexpr int kStage = (kTI + kTJ) * kBK;  // A rows then B rows: 24 KiB
-constexpr int kNBuf = 3;               // staging ring depth (2 stages in flight + the one read)
-constexpr int kWaves = 4;
-constexpr int kRing = kNBuf * kStage;  // 72 KiB
+constexpr int kStage = 2 * kFB * kBK;  // A rows then B rows: 32 KiB
+constexpr int kNBuf = 4;               // staging ring depth (kNBuf - 1 stages in flight)
+constexpr int kWaves = 8;
+constexpr int kRing = kNBuf * kStage;  // 128 KiB
 constexpr int kQuarter = 64 * 64 * 4;  // one wave's 64x64 int32 epilogue tile
 static_assert(kWaves * kQuarter <= kRing, "epilogue tiles must fit in the staging ring");
 constexpr int kGlds = kStage / 1024 / kWaves;  // 1 KiB glds instructions per wave per stage
-static_assert(kGlds == 6, "the k-loop's vmcnt counts assume 6 glds per wave per stage");
-constexpr int kTermBytes = (kTI + kTJ) * 8;    // rows {u, Sx}, columns {w, v}: 3 KiB
-constexpr int kLdsBytes = kRing + kTermBytes;  // 76.8 KB: two tiles per CU
-static_assert(2 * kLdsBytes <= 160 * 1024, "two tiles must fit one CU's LDS");
+constexpr int kFvBytes = kFB * 40;             // one side's LdFast records (40 B each)
+constexpr int kFvGlds = kFvBytes / 1024;       // 1 KiB pieces of them
+static_assert(kFvBytes % 1024 == 0, "the records are DMA'd in whole 1 KiB pieces");
+static_assert(sizeof(LdFast) == 40, "LdFast layout");
+static_assert(kGlds == 4, "the k-loop's vmcnt counts assume 4 glds per wave per stage");
 
 __device__ __forceinline__ void glds16(const void *src, int8_t *lds_base) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
@@ -88,43 +84,9 @@ __device__ __forceinline__ int ld_exact_pass(const LdFast *__restrict__ fv, cons
     return ld_fast_r2(fi, fj, sxy, dn) >= threshold ? 1 : 0;
 }
 
-// Prefilter terms of one call (threshold-dependent), per 128-row group g:
-//   row[g*256 + t] = u_i = sqrt(tm' Vx_i) / n,  row[g*256 + 128 + t] = Sx_i (fp32)
-// and per 256-column group G:
-//   col[G*512 + t] = w_j = -Sy_j / n,           col[G*512 + 256 + t] = v_j = sqrt(Vy_j)
-// (Vx = n*Sx2 - Sx^2, +inf for a monomorphic variant; slots past M are 0)
-__global__ void k_ld_terms(const LdFast *__restrict__ fv, uint64_t m, double tm, int ns, int all_pass,
-                           float *__restrict__ row, float *__restrict__ col) {
-    const uint64_t mp = (m + kTJ - 1) / kTJ * kTJ;
-    for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < mp; v += (uint64_t)gridDim.x * blockDim.x) {
-        float u = 0.f, s = 0.f, w = 0.f, q = 0.f;
-        if (v < m) {
-            const LdFast f = fv[v];
-            u = all_pass ? 0.f : sqrtf((float)(tm * (1.0 - 1e-5)) * (float)f.vxp) / (float)ns;
-            s = (float)f.sx;
-            w = ns > 0 ? -(float)f.sx / (float)ns : 0.f;  // (n = 0: every r^2 is 0, no NaN)
-            q = all_pass ? 0.f : sqrtf((float)f.vxp);
-        }
-        const uint64_t g = v / kTI, t = v % kTI, G = v / kTJ, T = v % kTJ;
-        row[g * 2 * kTI + t] = u;
-        row[g * 2 * kTI + kTI + t] = s;
-        col[G * 2 * kTJ + T] = w;
-        col[G * 2 * kTJ + kTJ + T] = q;
-    }
-}
-
-hipError_t launch_ld_terms(const LdFast *fv, uint64_t m, double tm, int ns, int all_pass, float *row, float *col,
-                           hipStream_t s) {
-    if (!m) return hipSuccess;
-    const uint64_t mp = (m + kTJ - 1) / kTJ * kTJ;
-    hipLaunchKernelGGL(k_ld_terms, dim3((unsigned)std::min<uint64_t>((mp + 255) / 256, 4096)), dim3(256), 0, s, fv, m,
-                       tm, ns, all_pass, row, col);
-    return hipGetLastError();
-}
-
 // Count-pass epilogue straight from the accumulators (no LDS tile): lane (h, r) of a wave
 // holds, for each of its 4 column tiles y, column wj*128 + 32y + r and the 32 rows
-// 32x + 8g + 4h + e of the wave's 64-row block bI.  Candidate test per pair in C/n units, two
+// 32x + 8g + 4h + e of the wave's 64-row block.  Candidate test per pair in C/n units, two
 // pairs per packed fp32 instruction and no conversion (the accumulator is already fp32):
 //   c' = Sxy + Sx_i * w_j               w_j = -Sy_j / n            (C' = C / n exactly)
 //   candidate iff |c'| >= u_i * v_j - E,  u_i = sqrt(tm' Vx_i) / n, v_j = sqrt(Vy_j)
@@ -140,10 +102,11 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdWindowArgs &a,
                                               const LdFast *__restrict__ fv, const uint32_t *__restrict__ chrom_id,
                                               uint16_t *__restrict__ cnt, const float *ru, const float *rsf,
-                                              const float *cw, const float *cv, uint64_t bI, uint32_t J4, int wi,
+                                              const float *cw, const float *cv, uint32_t I4, uint32_t J4, int wi,
                                               int wj, int h, int r, int (&qtot)[2]) {
     const int64_t M = (int64_t)a.m;
     const double dn = (double)a.ns;
+    const uint64_t bI = 4ull * I4 + wi;
     const int64_t i0 = (int64_t)bI * kLdBlock;
     const float negE = a.all_pass ? -INFINITY : -(float)(32.0 * a.ns / 8388608.0);
     int64_t jv[4];
@@ -243,28 +206,35 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
     qtot[1] = wave_sum(nc[2] + nc[3]);
 }
 
-// tile list entry b: (I2, J4) = (128-row group of variants i, 256-column group of variants j)
 template <int P>
-__global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__restrict__ Gp,
-                                                               const LdFast *__restrict__ fv,
-                                                               const uint32_t *__restrict__ chrom_id, LdWindowArgs a,
-                                                               const uint32_t *__restrict__ blocks, uint32_t nblocks,
-                                                               uint16_t *__restrict__ cnt, LdOffsets off,
-                                                               LdPair *__restrict__ pairs, LdStage st, LdTerms tm) {
+__global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__restrict__ Gp,
+                                                            const LdFast *__restrict__ fv,
+                                                            const uint32_t *__restrict__ chrom_id, LdWindowArgs a,
+                                                            const uint32_t *__restrict__ blocks, uint32_t nblocks,
+                                                            uint16_t *__restrict__ cnt,
+                                                            LdOffsets off,
+                                                            LdPair *__restrict__ pairs, LdStage st) {
     // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
-    // ds_reads): the staging ring during the k-loop (the waves' epilogue tiles over it in the
-    // LDS-tile path), then the tile's prefilter terms, DMA'd in with the first stages
-    __shared__ __attribute__((aligned(16))) int8_t lds[kLdsBytes];
-    const float *ru = reinterpret_cast<const float *>(lds + kRing);  // rows: sqrt(tm' Vx) / n
-    const float *rsf = ru + kTI;                                       // and Sx as fp32
-    const float *cw = ru + 2 * kTI;                                    // columns: -Sy / n
-    const float *cv = cw + kTJ;                                        // and sqrt(Vy)
+    // ds_reads): the staging ring during the k-loop, then the waves' epilogue tiles over it;
+    // the per-row prefilter terms after that
+    // ... and the tile's raw per-variant records (rows I, columns J), DMA'd in with the first
+    // stages so no global-load latency sits before the k-loop or the epilogue
+    __shared__ __attribute__((aligned(16))) int8_t lds[kRing + kFB * (8 + 4 + 4 + 4 + 4 + 4 + 4) + 2 * kFvBytes];
+    double *rvx = reinterpret_cast<double *>(lds + kRing);
+    int *rsx = reinterpret_cast<int *>(lds + kRing + kFB * 8);
+    float *rvxf = reinterpret_cast<float *>(lds + kRing + kFB * 12);
+    float *ru = reinterpret_cast<float *>(lds + kRing + kFB * 16);  // register epilogue: sqrt(tm' Vx) / n
+    float *rsf = reinterpret_cast<float *>(lds + kRing + kFB * 20);  // and Sx as fp32
+    float *cw = reinterpret_cast<float *>(lds + kRing + kFB * 24);   // columns: -Sy / n
+    float *cv = reinterpret_cast<float *>(lds + kRing + kFB * 28);   // and sqrt(Vy)
+    const LdFast *fI = reinterpret_cast<const LdFast *>(lds + kRing + kFB * 32);
+    const LdFast *fJ = reinterpret_cast<const LdFast *>(lds + kRing + kFB * 32 + kFvBytes);
     const uint32_t b = xcd_remap(blockIdx.x, nblocks);
-    const uint32_t I2 = blocks[2 * b], J4 = blocks[2 * b + 1];
+    const uint32_t I4 = blocks[2 * b], J4 = blocks[2 * b + 1];
     const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
     const int wi = w >> 1, wj = w & 1;  // output rows wi*64.., columns wj*128..
     const int64_t M = (int64_t)a.m;
-    const int64_t ibase = (int64_t)I2 * kTI, jbase = (int64_t)J4 * kTJ;
+    const int64_t ibase = (int64_t)I4 * kFB, jbase = (int64_t)J4 * kFB;
     // count-table slot of 64-block pair (bI, bJ); false outside the window triangle
     auto sub = [&](uint64_t bI, uint64_t bJ, uint64_t &slot) {
         const uint64_t jrow0 = bJ * kLdBlock;
@@ -272,13 +242,13 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
         slot = bI - ifirst;
         return bI >= ifirst && bI <= bJ;
     };
-    if (P == 2) {  // emit pass: skip tiles without a counted pair (8 quarters x 64 columns)
+    if (P == 2) {  // emit pass: skip blocks without a counted pair (16 quarters x 64 columns)
         uint32_t any = 0;
 #pragma unroll
         for (int e = 0; e < 2; e++) {
-            const int idx = t + e * kWaves * kWave;  // 0..511
+            const int idx = t + e * kWaves * kWave;  // 0..1023
             const int qi = idx >> 8, qj = (idx >> 6) & 3, col = idx & 63;
-            const uint64_t bI = 2ull * I2 + qi, bJ = 4ull * J4 + qj;
+            const uint64_t bI = 4ull * I4 + qi, bJ = 4ull * J4 + qj;
             uint64_t slot;
             const int64_t jj = (int64_t)(bJ * kLdBlock) + col;
             if (sub(bI, bJ, slot) && jj < M && jj >= (int64_t)a.j_lo && jj < (int64_t)a.j_hi)
@@ -286,31 +256,34 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
         }
         if (!__syncthreads_or(any != 0)) return;
     }
-    // the tile's terms: rows {u, Sx} (1 KiB, wave 0), columns {w, v} (2 KiB, waves 1, 2)
-    if (w < 3)
-        glds16(w == 0 ? reinterpret_cast<const int8_t *>(tm.row + (uint64_t)I2 * 2 * kTI) + l * 16
-                      : reinterpret_cast<const int8_t *>(tm.col + (uint64_t)J4 * 2 * kTJ) + (w - 1) * 1024 + l * 16,
-               lds + kRing + w * 1024);
+    {  // the I and J records: kFvBytes each, 1 KiB per wave-instruction.  A lane whose 16 B
+        // start past the array re-reads its last 16 B (rows / columns outside the matrix, never
+        // used); a lane straddling the end reads < 16 B past it, inside the M + 1 records the
+        // array is allocated with (vcfxg_ld_prepare)
+        const char *fv_end = reinterpret_cast<const char *>(fv + M);
+        for (int q = w; q < 2 * kFvGlds; q += kWaves) {
+            const int side = q / kFvGlds, part = q - side * kFvGlds;
+            const char *s = reinterpret_cast<const char *>(fv + (side ? jbase : ibase)) + part * 1024 + l * 16;
+            glds16(s < fv_end ? s : fv_end - 16, lds + kRing + kFB * 32 + side * kFvBytes + part * 1024);
+        }
+    }
     const int kpad = a.kp4;  // FP4 row bytes
-    // staging: 24 wave-instructions of 1 KiB per stage, kGlds per wave; instruction q of
-    // wave w fills LDS [(kGlds*w+q) KiB, +1 KiB) = 16 rows x 64 B (A rows for 0..7, B rows
-    // after); lane l -> row (l>>2), physical slot l&3 holding logical 16 B slot
-    // (l&3) ^ ((row>>2)&3)
+    // staging: 32 wave-instructions of 1 KiB per stage, kGlds per wave; instruction q of
+    // wave w fills LDS [(kGlds*w+q) KiB, +1 KiB) = 16 rows x 64 B; lane l -> row (l>>2),
+    // physical slot l&3 holding logical 16 B slot (l&3) ^ ((row>>2)&3)
     const uint8_t *src[kGlds];
 #pragma unroll
     for (int q = 0; q < kGlds; q++) {
-        const int idx = kGlds * w + q;  // 0..23
-        const bool isA = idx < kTI / 16;
-        const int lrow = (isA ? idx : idx - kTI / 16) * 16 + (l >> 2);  // row within the A or B tile
-        int64_t g = (VCFXG_LD_EXPT & 16) ? idx * 16 + (l >> 2) : (isA ? ibase : jbase) + lrow;
+        const int idx = kGlds * w + q;                // 0..31: A rows for 0..15, B rows after
+        const int lrow = (idx & 15) * 16 + (l >> 2);  // row within the A or B tile
+        int64_t g = (VCFXG_LD_EXPT & 16) ? lrow : (idx < 16 ? ibase : jbase) + lrow;
         if (g >= M) g = M - 1;
         const int logical = (l & 3) ^ ((lrow >> 2) & 3);
         src[q] = Gp + g * (int64_t)kpad + logical * 16;
     }
     auto stage = [&](int ks, int buf) {
 #pragma unroll
-        for (int q = 0; q < kGlds; q++)
-            glds16(src[q] + ((VCFXG_LD_EXPT & 8) ? 0 : ks * kBK), lds + buf * kStage + (kGlds * w + q) * 1024);
+        for (int q = 0; q < kGlds; q++) glds16(src[q] + ((VCFXG_LD_EXPT & 8) ? 0 : ks * kBK), lds + buf * kStage + (kGlds * w + q) * 1024);
     };
     v16f acc[2][4];
 #pragma unroll
@@ -329,7 +302,7 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
 #pragma unroll
         for (int y = 0; y < 4; y++) {
             const int rb = wj * 128 + y * 32 + r;
-            fb[y] = *reinterpret_cast<const v4i *>(base + kTI * kBK + rb * kBK + ((lg ^ ((rb >> 2) & 3)) << 4));
+            fb[y] = *reinterpret_cast<const v4i *>(base + kFB * kBK + rb * kBK + ((lg ^ ((rb >> 2) & 3)) << 4));
         }
     };
     auto mfma8 = [&](const v4i(&fa)[2], const v4i(&fb)[4]) {
@@ -342,19 +315,18 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
                     v8i{fb[y].x, fb[y].y, fb[y].z, fb[y].w, 0, 0, 0, 0}, acc[x][y], kFmtFp4, kFmtFp4, 0, kScaleOne,
                     0, kScaleOne);
     };
-    // Software pipeline over the 3-buffer ring, fragments one k-half ahead of the MFMAs:
-    //   step ks: read F(ks, 1) | MFMAs (ks, 0) | wait stage ks+1 and the F(ks, 1) reads,
-    //   barrier, stage ks+3 into buffer ks%3 (every wave's reads of it retired before the
-    //   barrier), read F(ks+1, 0) | MFMAs (ks, 1)
-    // so every fragment read overlaps 8 MFMAs, two stages stay in flight and the barrier sits
-    // between two MFMA groups; counted vmcnt + raw s_barrier (a __syncthreads fence would
-    // drain every glds)
+    // Software pipeline over a kNBuf-buffer ring, fragments one k-half ahead of the MFMAs:
+    //   step ks: read F(ks, 1) | MFMAs (ks, 0) | wait stage ks+1, barrier, stage ks+3 into
+    //   buffer (ks-1)%kNBuf (last read by F(ks-1, 1), consumed before this barrier), read
+    //   F(ks+1, 0) | MFMAs (ks, 1)
+    // so every fragment read overlaps 8 MFMAs and the barrier sits between two MFMA groups;
+    // counted vmcnt + raw s_barrier (a __syncthreads fence would drain every glds)
     // the epilogue's pointer arguments, consumed here: left to itself the compiler hoists their
     // scalar loads over the loop, and a pending SMEM load (out of order within lgkmcnt) turns
     // every fragment wait in the loop into lgkmcnt(0)
     asm volatile("" ::"s"(cnt), "s"(chrom_id), "s"(pairs));
-    for (int q = 0; q < kNBuf; q++) stage(q < nk ? q : nk - 1, q);
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // stage 0 (and the terms) landed
+    for (int q = 0; q < kNBuf - 1; q++) stage(q < nk ? q : nk - 1, q);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     v4i a0[2], b0[4], a1[2], b1[4];
     frag(lds, 0, a0, b0);
@@ -366,15 +338,13 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 7, 0);
-        // stage ks+1 landed (stage ks+2 may still load) and this wave's F(ks, 1) reads are
-        // done, so after the barrier buffer ks%3 is free; every step issues a stage -- past
+        // stage ks+1 landed (stage ks+2 may still load); every step issues a stage -- past
         // the end a re-read of the last (L2-hot) slice into the free buffer -- so the counts
         // are constant and the loop body has no branch
-        __builtin_amdgcn_sched_barrier(0);  // (after all 8 MFMAs: the reads had them to land)
-        asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         frag(lds + ((ks + 1) % kNBuf) * kStage, 0, a0, b0);
-        stage(ks + kNBuf < nk ? ks + kNBuf : nk - 1, ks % kNBuf);
+        stage(ks + kNBuf - 1 < nk ? ks + kNBuf - 1 : nk - 1, (ks + kNBuf - 1) % kNBuf);
         mfma8(a1, b1);
         // again one MFMA first (the compiler's wait before it, lgkmcnt(0), then covers only
         // the long-landed F(ks, 1)), the fragment reads, the staging loads between MFMAs
@@ -399,21 +369,96 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
 #pragma unroll
                 for (int k = 0; k < 16; k++) z ^= (int)acc[x][y][k];
         if (z == 0x7fffffff) cnt[0] = 1;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         return;
     }
-    // the re-read stages past the end land before the ring is reused or the tile ends
+    // the row and column terms from the DMA'd records (every wave's loads done, then visible)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t < kFB) {
+        const LdFast f = fI[t];
+        rvx[t] = f.vxp;
+        rvxf[t] = (float)f.vxp;
+        ru[t] = a.all_pass ? 0.f : sqrtf((float)(a.tm * (1.0 - 1e-5)) * (float)f.vxp) / (float)a.ns;
+        rsf[t] = (float)f.sx;
+        rsx[t] = f.sx;
+    } else {
+        const LdFast f = fJ[t - kFB];
+        cw[t - kFB] = a.ns > 0 ? -(float)f.sx / (float)a.ns : 0.f;  // (n = 0: every r^2 is 0, no NaN)
+        cv[t - kFB] = a.all_pass ? 0.f : sqrtf((float)f.vxp);
+    }
+    const int pad = 0;  // FP4 rows are zero-padded
     const double dn = (double)a.ns;
     const int64_t n = a.ns;
-    const uint64_t bI = 2ull * I2 + wi;
+    // fp32 form of the prefilter while n*Sxy and Sx*Sy fit int32 (n <= 23170): C exact in
+    // int32, C^2 and tm*Vx*Vy within ~1e-6 relative in fp32, so a further 1e-5 relative
+    // slack keeps every pair that can reach the threshold
+    const bool f32 = a.ns <= 23170;
+    const uint64_t bI = 4ull * I4 + wi;
     const int64_t i0 = (int64_t)bI * kLdBlock;
-    if (P == 1 && a.ns <= 23170) {  // (the terms are visible since the prologue's barrier)
+    int *tile = reinterpret_cast<int *>(lds + w * kQuarter);
+    // quarter hy (columns hy*64.. of the wave) through this wave's LDS tile: lane l walks
+    // column j's rows and returns the mask of the rows whose pair passes (exact decision)
+    auto walk = [&](int hy, int64_t j, bool jok, LdFast &fj) -> uint64_t {
+        // the quarter's accumulators -> this wave's LDS tile [row][col] (no other wave uses
+        // it, and the wave's own lanes are in lockstep: no barrier between quarters)
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int yy = 0; yy < 2; yy++)
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    tile[(32 * x + (k & 3) + 8 * (k >> 2) + 4 * h) * 64 + 32 * yy + r] = (int)acc[x][2 * hy + yy][k];
+        uint64_t mask = 0;
+        if (jok) {
+            fj = fv[j];
+            const uint32_t cj = a.max_dist > 0 ? chrom_id[j] : 0u;
+            const double rhs_j = a.all_pass ? 0.0 : a.tm * fj.vxp;
+            const float rhs_jf = (float)(a.tm * (1.0 - 1e-5)) * (float)fj.vxp;
+            // rows i in [max(i0, j - window), min(i0 + 64, j))
+            const int lo = (int)(j - (int64_t)a.window > i0 ? j - (int64_t)a.window - i0 : 0);
+            const int hi = (int)(j - i0 < 64 ? j - i0 : 64);
+            for (int row = lo; row < hi; row++) {
+                const int lr = wi * 64 + row;
+                const int sxy = tile[row * 64 + l] - pad;
+                if (!a.all_pass) {
+                    if (f32) {
+                        const float c = (float)(a.ns * sxy - rsx[lr] * fj.sx);
+                        if (!(c * c >= rvxf[lr] * rhs_jf)) continue;
+                    } else {
+                        const int64_t C = n * sxy - (int64_t)rsx[lr] * fj.sx;
+                        const double c = (double)C;
+                        if (!(c * c >= rvx[lr] * rhs_j)) continue;
+                    }
+                }
+                const int64_t i = i0 + row;
+                const LdFast fi = fv[i];
+                if (a.max_dist > 0 && chrom_id[i] == cj) {
+                    int d = fj.pos - fi.pos;
+                    if (d < 0) d = -d;
+                    if (d > a.max_dist) continue;
+                }
+                if (ld_fast_r2(fi, fj, sxy, dn) >= a.threshold) mask |= 1ull << row;
+            }
+        }
+        return mask;
+    };
+    auto write_pairs = [&](uint64_t mask, int64_t j, const LdFast &fj, LdPair *dst) {
+        uint32_t rank = 0;
+        while (mask) {
+            const int row = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            LdPair pr;
+            pr.i = (uint32_t)(i0 + row);
+            pr.j = (uint32_t)j;
+            pr.r2 = ld_fast_r2(fv[i0 + row], fj, tile[row * 64 + l] - pad, dn);
+            dst[rank++] = pr;
+        }
+    };
+    if (P == 1 && a.ns <= 23170) {
+        __syncthreads();  // the row and column terms are visible to every wave
         int qt[2];
-        ld_count_regs(acc, a, fv, chrom_id, cnt, ru, rsf, cw, cv, bI, J4, wi, wj, h, r, qt);
+        ld_count_regs(acc, a, fv, chrom_id, cnt, ru, rsf, cw, cv, I4, J4, wi, wj, h, r, qt);
         if (!st.temp) return;
-        __syncthreads();  // every wave is done reading the ring; the quarter tiles reuse it
-        int *tile = reinterpret_cast<int *>(lds + w * kQuarter);
         // quarters holding pairs: written now, column-major into a bump-allocated staging
         // area (ld_scatter later moves each column's run to its ordered offset), so the
         // emit pass needs no second MFMA sweep
@@ -423,38 +468,8 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
             const uint64_t bJ = 4ull * J4 + 2 * wj + hy;
             const int64_t j = (int64_t)(bJ * kLdBlock) + l;
             const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
-#pragma unroll
-            for (int x = 0; x < 2; x++)
-#pragma unroll
-                for (int yy = 0; yy < 2; yy++)
-#pragma unroll
-                    for (int k = 0; k < 16; k++)
-                        tile[(32 * x + (k & 3) + 8 * (k >> 2) + 4 * h) * 64 + 32 * yy + r] = (int)acc[x][2 * hy + yy][k];
-            uint64_t mask = 0;
             LdFast fj{};
-            if (jok) {
-                fj = fv[j];
-                const uint32_t cj = a.max_dist > 0 ? chrom_id[j] : 0u;
-                const int lo = (int)(j - (int64_t)a.window > i0 ? j - (int64_t)a.window - i0 : 0);
-                const int hi = (int)(j - i0 < 64 ? j - i0 : 64);
-                for (int row = lo; row < hi; row++) {
-                    const int64_t i = i0 + row;
-                    const int sxy = tile[row * 64 + l];
-                    const int lr = wi * 64 + row;
-                    // the register epilogue's candidate test, then the exact decision
-                    const float c = fmaf(rsf[lr], cw[(int)(j - jbase)], (float)sxy);
-                    if (!(fabsf(c) >= fmaf(ru[lr], cv[(int)(j - jbase)],
-                                           a.all_pass ? -INFINITY : -(float)(32.0 * a.ns / 8388608.0))))
-                        continue;
-                    const LdFast fi = fv[i];
-                    if (a.max_dist > 0 && chrom_id[i] == cj) {
-                        int d = fj.pos - fi.pos;
-                        if (d < 0) d = -d;
-                        if (d > a.max_dist) continue;
-                    }
-                    if (ld_fast_r2(fi, fj, sxy, dn) >= a.threshold) mask |= 1ull << row;
-                }
-            }
+            const uint64_t mask = walk(hy, j, jok, fj);
             const uint32_t c = (uint32_t)__popcll(mask);
             const uint32_t incl = wave_incl_scan(c);
             const uint32_t total = wave_bcast(incl, kWave - 1);
@@ -465,13 +480,7 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
                 if (l == 0) atomicOr(st.overflow, 1u);
                 continue;
             }
-            LdPair *dst = st.temp + base + (incl - c);
-            uint32_t rank = 0;
-            while (mask) {
-                const int row = __builtin_ctzll(mask);
-                mask &= mask - 1;
-                dst[rank++] = LdPair{(uint32_t)(i0 + row), (uint32_t)j, ld_fast_r2(fv[i0 + row], fj, tile[row * 64 + l], dn)};
-            }
+            write_pairs(mask, j, fj, st.temp + base + (incl - c));
             if (l == 0) {
                 const unsigned long long q = atomicAdd(st.ctr + 1, 1ull);
                 if (q < st.qcap) st.quarters[q] = LdQuarter{(uint32_t)bI, (uint32_t)bJ, (uint64_t)base};
@@ -480,10 +489,7 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
         }
         return;
     }
-    // LDS-tile path (emit pass, or n > 23170 where n*Sxy overflows the fp32 prefilter's
-    // exactness): each quarter through the wave's LDS tile, lane l walking column j
     __syncthreads();  // every wave is done reading the ring; the epilogue tiles reuse it
-    int *tile = reinterpret_cast<int *>(lds + w * kQuarter);
 #pragma unroll
     for (int hy = 0; hy < 2; hy++) {  // the wave's two 64x64 quarters (columns hy*64..)
         const uint64_t bJ = 4ull * J4 + 2 * wj + hy;
@@ -491,51 +497,14 @@ __global__ __launch_bounds__(kWaves * kWave, 2) void k_ld_fast(const uint8_t *__
         if (!sub(bI, bJ, slot)) continue;  // wave-uniform: a quarter outside the window triangle
         const int64_t j = (int64_t)(bJ * kLdBlock) + l;
         const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
-#pragma unroll
-        for (int x = 0; x < 2; x++)
-#pragma unroll
-            for (int yy = 0; yy < 2; yy++)
-#pragma unroll
-                for (int k = 0; k < 16; k++)
-                    tile[(32 * x + (k & 3) + 8 * (k >> 2) + 4 * h) * 64 + 32 * yy + r] = (int)acc[x][2 * hy + yy][k];
-        uint64_t mask = 0;
         LdFast fj{};
-        if (jok) {
-            fj = fv[j];
-            const uint32_t cj = a.max_dist > 0 ? chrom_id[j] : 0u;
-            const double rhs_j = a.all_pass ? 0.0 : a.tm * fj.vxp;
-            // rows i in [max(i0, j - window), min(i0 + 64, j))
-            const int lo = (int)(j - (int64_t)a.window > i0 ? j - (int64_t)a.window - i0 : 0);
-            const int hi = (int)(j - i0 < 64 ? j - i0 : 64);
-            for (int row = lo; row < hi; row++) {
-                const int64_t i = i0 + row;
-                const int sxy = tile[row * 64 + l];
-                const LdFast fi = fv[i];
-                if (!a.all_pass) {  // exact integer C in int64, its square against tm Vx Vy in fp64
-                    const int64_t C = n * sxy - (int64_t)fi.sx * fj.sx;
-                    const double cd = (double)C;
-                    if (!(cd * cd >= fi.vxp * rhs_j * (1.0 - 1e-9))) continue;
-                }
-                if (a.max_dist > 0 && chrom_id[i] == cj) {
-                    int d = fj.pos - fi.pos;
-                    if (d < 0) d = -d;
-                    if (d > a.max_dist) continue;
-                }
-                if (ld_fast_r2(fi, fj, sxy, dn) >= a.threshold) mask |= 1ull << row;
-            }
-        }
+        const uint64_t mask = walk(hy, j, jok, fj);
         if (P == 1) {
             if (jok) cnt[(uint64_t)(j - (int64_t)a.j_lo) * a.nb + slot] = (uint16_t)__popcll(mask);
             continue;
         }
         if (!mask) continue;
-        LdPair *dst = pairs + off.at((uint64_t)(j - (int64_t)a.j_lo), a.nb, slot);
-        uint32_t rank = 0;
-        while (mask) {
-            const int row = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            dst[rank++] = LdPair{(uint32_t)(i0 + row), (uint32_t)j, ld_fast_r2(fv[i0 + row], fj, tile[row * 64 + l], dn)};
-        }
+        write_pairs(mask, j, fj, pairs + off.at((uint64_t)(j - (int64_t)a.j_lo), a.nb, slot));
     }
 }
 
@@ -577,15 +546,15 @@ hipError_t launch_ld_scatter(const LdQuarter *quarters, const unsigned long long
 
 hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const uint32_t *chrom_id,
                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
-                          LdOffsets off, LdPair *pairs, const LdStage &st, const LdTerms &tm, hipStream_t s) {
+                          LdOffsets off, LdPair *pairs, const LdStage &st, hipStream_t s) {
     if (!nblocks) return hipSuccess;
     if (a.kp4 % kBK || a.kp4 <= 0) return hipErrorInvalidValue;
     if (pass == 1)
         hipLaunchKernelGGL(k_ld_fast<1>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
-                           nblocks, cnt, off, pairs, st, tm);
+                           nblocks, cnt, off, pairs, st);
     else
         hipLaunchKernelGGL(k_ld_fast<2>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
-                           nblocks, cnt, off, pairs, st, tm);
+                           nblocks, cnt, off, pairs, st);
     return hipGetLastError();
 }
 
@@ -682,12 +651,12 @@ hipError_t launch_ld_rowscan(const uint16_t *cnt, uint64_t rows, uint64_t nb, ui
 // per kLdFastBlock-variant group: 1 if every variant of the group is complete
 __global__ void k_ld_groups(const LdVar *__restrict__ vars, uint64_t m, uint8_t *__restrict__ gflag) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x / 64 + threadIdx.x / 64;
-    const uint64_t ng = (m + kTJ - 1) / kTJ;
+    const uint64_t ng = (m + kFB - 1) / kFB;
     if (g >= ng) return;
     const int l = threadIdx.x & 63;
     bool ok = true;
-    for (int k = l; k < kTJ; k += 64) {
-        const uint64_t v = g * kTJ + k;
+    for (int k = l; k < kFB; k += 64) {
+        const uint64_t v = g * kFB + k;
         if (v < m) ok = ok && vars[v].complete;
     }
     ok = __all(ok);
@@ -695,7 +664,7 @@ __global__ void k_ld_groups(const LdVar *__restrict__ vars, uint64_t m, uint8_t 
 }
 
 hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, uint8_t *gflag, hipStream_t s) {
-    const uint64_t ng = (m + kTJ - 1) / kTJ;
+    const uint64_t ng = (m + kFB - 1) / kFB;
     if (!ng) return hipSuccess;
     hipLaunchKernelGGL(k_ld_groups, dim3((unsigned)((ng + 3) / 4)), dim3(256), 0, s, vars, m, gflag);
     return hipGetLastError();
