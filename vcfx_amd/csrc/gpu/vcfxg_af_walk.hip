@@ -273,7 +273,8 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                       : t8 + 2 < wend ? (uint8_t)sep_w
                                       : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
                 Op op = R::make(buf, ae);
-                ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
+                if constexpr (std::is_same<Op, AfOp>::value) ok = af_fixed<kWalkUnroll>(buf, S, ae, op, sep, pre);
+                else ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
                 R::out(op, alt, tot, aux);
             }
         };

@@ -36,6 +36,14 @@ __device__ __forceinline__ uint32_t range_mask16(int64_t base, int64_t lo, int64
     return ((1u << b) - 1u) & ~((1u << a) - 1u);
 }
 
+// bits j of a 16-byte block at relative offset b with lo <= b + j < hi (32-bit offsets)
+__device__ __forceinline__ uint32_t range16(int b, int lo, int hi) {
+    int a = lo - b, e = hi - b;
+    a = a < 0 ? 0 : (a > 16 ? 16 : a);
+    e = e < 0 ? 0 : (e > 16 ? 16 : e);
+    return e <= a ? 0u : ((1u << e) - 1u) & ~((1u << a) - 1u);
+}
+
 __device__ __forceinline__ uint4 load16(const char *buf, int64_t off) {
     return *reinterpret_cast<const uint4 *>(buf + off);
 }

@@ -318,6 +318,104 @@ struct AfOp {
     }
 };
 
+// bytes of a 4-bit mask (bit j -> byte j = 0xFF)
+__device__ __forceinline__ uint32_t nib_bytes(uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu; }
+
+// ---------------------------------------------------------------------------------------
+// af_fixed: gt_fast + AfOp (the same record test and the same counts) on the raw 16 B
+// blocks, without realigning them to the sample grid.  In a fixed-stride record every byte's
+// role -- allele, separator or tab -- is (offset - S) mod 4, so a raw aligned dword holds the
+// canonical unit "0 s 0 \t" rotated left by 8 (S mod 4) bits, whichever samples its bytes
+// belong to (the allele counts do not care).  Per raw dword, against that rotated expectation:
+//   e = d ^ exp:  a record whose alleles are all '0' / '1' has e = 0 except bit 0 of its
+//   allele bytes, so  err |= e & rot(0xFFFEFFFE)  and  alt += popc(e)  are the whole test and
+//   count (3 VALU per 4 bytes; tot = 2 x units), where gt_fast spends ~15 per sample and an
+//   extra 4-byte load per lane for the realignment;
+// a wave-step that fails that (some allele neither '0' nor '1') is counted again, from the
+// same registers, with gt_fast's per-allele rules (digit: counts, 1..9: ALT, '.': not counted,
+// anything else: not fixed-stride).  Bytes outside [S, E) read as the expected '0'-allele
+// bytes (the last sample's byte at E -- its '\n' -- as its tab), so they neither count nor fail.
+// Returns false (wave-uniform) where gt_fast returns false; op.alt / op.tot as gt_fast leaves
+// them after op.finish().
+// ---------------------------------------------------------------------------------------
+template <int kUnroll, class Pre>
+__device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfOp &op, uint32_t sep_hint, Pre pre) {
+    S = uniform64(S);
+    E = uniform64(E);
+    const int64_t L = E - S;
+    if (L < 3 || ((L + 1) & 3)) return false;
+    uint32_t sepc = sep_hint ? sep_hint : byte_at(buf, S + 1);
+    sepc = __builtin_amdgcn_readfirstlane(sepc);
+    if (sepc != '/' && sepc != '|') return false;
+    const uint32_t sh = 8u * (uint32_t)(S & 3);
+    auto rot = [&](uint32_t x) { return sh ? (x << sh) | (x >> (32u - sh)) : x; };
+    const uint32_t exp = rot(0x09300030u | (sepc << 8));  // '0' s '0' \t
+    const uint32_t mbin = rot(0xFFFEFFFEu);               // separator / tab bytes whole, allele bits 1..7
+    const uint32_t msep = rot(0xFF00FF00u);               // separator / tab bytes
+    const uint32_t fsh = (S & 1) ? 8u : 0u;               // allele bytes -> bytes 0 and 2
+    const int64_t b0 = S & ~(int64_t)15;
+    const char *__restrict__ base = buf + b0;
+    const int Sr = (int)(S - b0), Er = (int)(E - b0);  // record bounds relative to b0
+    const int lastblk = (Er - 1) & ~15;
+    const int lo16 = lane() * kBlockBytes;
+    uint32_t alt = 0, dots = 0, err = 0;
+    for (int w0 = 0; w0 < Er; w0 += kUnroll * kWaveStep) {
+        uint4 v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {  // branch-free: lanes past the record re-read its last block
+            const int blk = w0 + u * kWaveStep + lo16;
+            v[u] = load16(base, blk < Er ? blk : lastblk);
+        }
+        if (w0 == 0) pre();
+        // the step's dwords, bytes outside [S, E) replaced by the expected ones (edge steps only)
+        auto dwords = [&](int u, const uint4 &x, uint32_t(&d)[4]) {
+            d[0] = x.x, d[1] = x.y, d[2] = x.z, d[3] = x.w;
+            const int w = w0 + u * kWaveStep;
+            if (!(w >= Sr && w + kWaveStep <= Er)) {  // wave-uniform
+                const int blk = w + lo16;
+                const uint32_t rm = blk < Er ? range16(blk, Sr, Er) : 0u;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t bm = nib_bytes((rm >> (4 * i)) & 0xFu);
+                    d[i] = (d[i] & bm) | (exp & ~bm);
+                }
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            uint32_t d[4];
+            dwords(u, v[u], d);
+            uint32_t berr = 0, balt = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t e = d[i] ^ exp;
+                berr |= e & mbin;
+                balt += __popc(e);
+            }
+            if (!__any(berr != 0u)) {
+                alt += balt;
+                continue;
+            }
+            // some allele of the step is neither '0' nor '1': gt_fast's per-allele rules
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t e = d[i] ^ exp;
+                err |= e & msep;
+                const uint32_t f = (e >> fsh) & 0x00FF00FFu;
+                const uint32_t notdig = (f + 0x00F600F6u) & 0x01000100u;  // field >= 10
+                const uint32_t notdot = ((f ^ 0x001E001Eu) + 0x00FF00FFu) & 0x01000100u;
+                err |= notdig & notdot;
+                dots += __popc(notdig);  // (valid: not a digit = '.')
+                alt += __popc((f + 0x00FF00FFu) & (notdig ^ 0x01000100u));  // digit 1..9
+            }
+        }
+        if (__any(err != 0u)) return false;  // not fixed-stride: stop reading the record
+    }
+    op.alt = wave_sum(alt);
+    op.tot = (uint32_t)(2 * ((L + 1) >> 2)) - wave_sum(dots);
+    return true;
+}
+
 // ---------------------------------------------------------------------------------------
 // genotype-match reducer: genotypeMatchesFast (VCFX_genotype_query.cpp:275-316) over
 // extractNthField (:199-218); "any sample matches" (checkAnySampleMatches :322-345)

@@ -179,7 +179,7 @@ __device__ __forceinline__ void af_line(const char *__restrict__ buf, int64_t ls
                 if (nt >= 9) {
                     const int64_t S = t[8] + 1;
                     AfOp op{buf, ae, gi};
-                    bool fast = gi == 0 && gt_fast(buf, S, ae, op);
+                    bool fast = gi == 0 && af_fixed<VCFXG_UNROLL>(buf, S, ae, op, 0u, NoPre());
                     if (!fast && gi == 0) {  // GT-first, variable-width samples
                         op = AfOp{buf, ae, gi};
                         fast = gt_first_known(buf, S, ae, op);
@@ -328,7 +328,7 @@ void k_af_sweep(const char *__restrict__ buf, int64_t data_start,
             bc.add(1, 1);
             bc.add(0, 1);
             AfOp op{buf, ae, 0};
-            if (gt_fast(buf, (int64_t)m.S, ae, op, m.sep)) {
+            if (af_fixed<VCFXG_UNROLL>(buf, (int64_t)m.S, ae, op, m.sep, NoPre())) {
                 alt = op.alt;
                 tot = op.tot;
                 st = 1;

@@ -21,14 +21,6 @@ constexpr int kWalkWaves = kWalkThreads / kWave;
 #endif
 constexpr int kFirstScanU = VCFXG_FIRST_SCAN_U;
 
-// bits j of a 16-byte block at relative offset b with lo <= b + j < hi (32-bit offsets)
-__device__ __forceinline__ uint32_t range16(int b, int lo, int hi) {
-    int a = lo - b, e = hi - b;
-    a = a < 0 ? 0 : (a > 16 ? 16 : a);
-    e = e < 0 ? 0 : (e > 16 ? 16 : e);
-    return e <= a ? 0u : ((1u << e) - 1u) & ~((1u << a) - 1u);
-}
-
 // first '\n' in [p, hi), else hi (wave-uniform; kU KiB per step, lane offsets 32-bit)
 template <int kU = 4>
 __device__ __forceinline__ int64_t scan_nl(const char *__restrict__ buf, int64_t p, int64_t hi) {
