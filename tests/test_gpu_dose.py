@@ -49,3 +49,49 @@ def test_dosage_engine_statuses(oracle):
     want = oracle.run(["VCFX_dosage_calculator"], buf)[0]
     assert b"CHROM\tPOS\tID\tREF\tALT\tDosages\n" + eng.text(s.text_bytes) == want
     eng.close()
+
+
+def _mutate(buf, rec, sample, new):
+    """replace sample `sample` of data record `rec` (fixed-stride "a|b" units) by `new` bytes"""
+    lines = buf.split(b"\n")
+    k = next(i for i, l in enumerate(lines) if l.startswith(b"#CHROM")) + 1 + rec
+    f = lines[k].split(b"\t")
+    f[9 + sample] = new
+    lines[k] = b"\t".join(f)
+    return b"\n".join(lines)
+
+
+# the head walk (DoseHeadOp) takes a record on its predicted '\n' alone; k_dose_fmt's check of
+# every sample byte must catch each way such a record can differ, and the call must be redone
+# with the sweeping walk: an "NA" ('.'), a non-digit allele, another separator, a sample of the
+# same width in another shape, and a '\n' inside a record of the predicted length (two lines)
+MUTATIONS = [
+    (7, 100, b".|0"), (300, 2503, b"0|."), (11, 0, b"x|1"), (12, 5, b"1/0"), (13, 9, b"11|"),
+    (14, 1000, b"0\n0"),
+]
+
+
+@pytest.mark.parametrize("rec,sample,new", MUTATIONS)
+def test_dosage_head_walk_fallback(oracle, rec, sample, new):
+    buf = _mutate(synth.generate(600, 2504, 88, 0, 0.0, 0, 0.0, 0), rec, sample, new)
+    want = oracle.run(["VCFX_dosage_calculator"], buf)[0]
+    ds = engine.data_start_of(buf)
+    eng = engine.Engine(0)
+    eng.load(buf)
+    for _ in range(2):  # the failed head attempt, then the input's remembered sweeping walk
+        s = eng.dosage_region(ds, engine.MODE_FILE)
+        assert b"CHROM\tPOS\tID\tREF\tALT\tDosages\n" + eng.text(s.text_bytes) == want
+    eng.close()
+
+
+def test_dosage_head_walk_clean(oracle):
+    # a clean fixed-stride input: the head walk's rows all pass, every record a fixed-stride row
+    buf = synth.generate(900, 2504, 89, 0, 0.0, 0, 0.0, 0)
+    ds = engine.data_start_of(buf)
+    eng = engine.Engine(0)
+    eng.load(buf)
+    s = eng.dosage_region(ds, engine.MODE_FILE)
+    assert s.rows == 900 and s.general_records == 0
+    assert b"CHROM\tPOS\tID\tREF\tALT\tDosages\n" + eng.text(s.text_bytes) == \
+        oracle.run(["VCFX_dosage_calculator"], buf)[0]
+    eng.close()

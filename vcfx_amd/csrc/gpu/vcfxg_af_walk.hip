@@ -79,6 +79,11 @@ struct WalkRed<DoseWalkOp> {  // samples and "NA" samples of the record (alt_o /
     }
 };
 
+template <>
+struct WalkRed<DoseHeadOp> : WalkRed<DoseWalkOp> {
+    __device__ static DoseHeadOp make(const char *buf, int64_t ae) { return DoseHeadOp{{buf, ae}}; }
+};
+
 // kGF: the GT-first walk (records "GT:AD:DP"-like, no fixed stride to predict): a GT-first
 // record whose '\n' is past the window is swept by gt_first from its sample start, which finds
 // the record's end in the same pass (and issues the next window as soon as it does); a separate
@@ -233,6 +238,8 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         uint32_t alt = 0, tot = 0, aux = 0, rowpre = 0;
         int64_t S = 0;
         bool ok = false;
+        // DoseHeadOp: a predicted GT-only record is not swept (k_dose_fmt checks its bytes)
+        bool skip = std::is_same<Op, DoseHeadOp>::value && predicted;
         auto sweep = [&]() {
             if constexpr (kGF) {
               if (gf) {  // gt_first from the sample start: the counts and the record end
@@ -274,7 +281,15 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                                       : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
                 Op op = R::make(buf, ae);
                 if constexpr (std::is_same<Op, AfOp>::value) ok = af_fixed<kWalkUnroll>(buf, S, ae, op, sep, pre);
-                else ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
+                else if constexpr (std::is_same<Op, DoseHeadOp>::value) {
+                    if (skip) {  // samples (ae - S + 1) / 4, none "NA" (checked by k_dose_fmt)
+                        ok = (sep == '/' || sep == '|') && ae - S >= 3 && ((ae - S + 1) & 3) == 0;
+                        op.ns = ok ? (uint32_t)((ae - S + 1) >> 2) : 0u;
+                        op.na = 0;
+                    } else {
+                        ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
+                    }
+                } else ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
                 R::out(op, alt, tot, aux);
             }
         };
@@ -290,6 +305,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             if (!(ok && endok)) {
                 const int64_t Et = scan_nl(buf, wend, hi);
                 if (Et != E || !endok) {  // the line again with its true bounds
+                    skip = false;
                     E = Et;
                     cr = strip_cr && E > L && __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r';
                     An = std::max<int64_t>(E - 1, 0) & ~(int64_t)15;
@@ -405,7 +421,8 @@ int64_t af_walkers(int64_t lo, int64_t hi, int64_t chunk) { return hi > lo ? (hi
 hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int mode, int64_t span0,
                           uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
                           uint8_t *status_b, void *meta_b, uint64_t *wcount, uint32_t *wgt, unsigned *overflow,
-                          hipStream_t s, int32_t *hwe_aux_b, const WalkTail *tail, bool dose, bool gt_first_walk) {
+                          hipStream_t s, int32_t *hwe_aux_b, const WalkTail *tail, bool dose, bool gt_first_walk,
+                          bool dose_head) {
     const WalkTail t = tail ? *tail : WalkTail{};
     const int64_t nw = af_walkers(lo, hi, chunk);
     if (!nw) return hipErrorInvalidValue;
@@ -414,6 +431,10 @@ hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk
         hipLaunchKernelGGL(HIP_KERNEL_NAME(k_af_walk<AfOp, true>), dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi,
                            chunk, nw, mode, span0, cap_w, le_b, alt_b, tot_b, nullptr, rowpre_b, status_b,
                            static_cast<LineMeta *>(meta_b), wcount, wgt, overflow, t);
+    else if (dose && dose_head)
+        hipLaunchKernelGGL(k_af_walk<DoseHeadOp>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, mode,
+                           span0, cap_w, le_b, alt_b, tot_b, nullptr, rowpre_b, status_b, static_cast<LineMeta *>(meta_b),
+                           wcount, wgt, overflow, t);
     else if (dose)
         hipLaunchKernelGGL(k_af_walk<DoseWalkOp>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, mode,
                            span0, cap_w, le_b, alt_b, tot_b, nullptr, rowpre_b, status_b, static_cast<LineMeta *>(meta_b),

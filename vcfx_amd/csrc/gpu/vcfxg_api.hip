@@ -89,6 +89,7 @@ struct vcfxg_ctx {
     int64_t hwe_ulps = getenv("VCFXG_HWE_ULPS") ? atoll(getenv("VCFXG_HWE_ULPS")) : 16;
     int64_t walk_chunk = getenv("VCFXG_WALK_CHUNK") ? atol(getenv("VCFXG_WALK_CHUNK")) : 128 * 1024;
     bool walk_overflowed = false;  // the last walk run overflowed: two-sweep schedule
+    bool dose_head_failed = false;  // a dosage head walk's rows failed the check (this input)
     // host hints taken at load time from the first data line: its '\n' distance from the
     // sample start (the walk's first prediction) and the mean length of the first lines
     int64_t hint_span = 0, hint_line = 0;
@@ -301,6 +302,7 @@ static void load_hints(vcfxg_ctx *c, const char *h, size_t n) {
     c->hint_gt_only = false;
     c->hint_gt_first = false;
     c->walk_overflowed = false;
+    c->dose_head_failed = false;
     size_t p = 0;
     while (p < n && h[p] == '#') {
         const void *q = memchr(h + p, '\n', n - p);
@@ -1387,7 +1389,8 @@ int vcfxg_hwe_rechecks(vcfxg_ctx *c, vcfxg_hwe_recheck *out, uint64_t cap, uint6
 // the dosage walk: line ends + per fixed-stride record its samples / "NA" samples, compacted to
 // the dense per-line arrays (line_end, alt = ns, tot = na, status, af_meta = LineMeta); the
 // context is indexed afterwards.  *overflow: a walker ran out of line slots (short lines)
-static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *L_out, bool *overflow) {
+static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *L_out, bool *overflow,
+                           bool head) {
     c->dense_pending = false;
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
@@ -1418,7 +1421,7 @@ static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *
                                     P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre),
                                     P<uint8_t>(c->wk_status), c->wk_meta.p, P<uint64_t>(c->wk_count),
                                     P<uint32_t>(c->wk_gt), reinterpret_cast<unsigned *>(small), c->stream, nullptr,
-                                    nullptr, true));
+                                    nullptr, true, false, head));
     prof_end(c, "dose_walk");
     prof_begin(c, "walk_compact");
     r = exclusive_scan(c, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_offs), (size_t)nw + 1);
@@ -1451,12 +1454,33 @@ static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *
 // walk reads each record once for its line end and (fixed-stride records) its samples and "NA"
 // samples -- no index sweep, no row-length pass over the records; the other lines take the
 // exact row-length pass; VCFXG_DOSE_WALK=0 keeps the index + two-pass schedule
-static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *L_out, bool *overflow);
+//
+// On such input the first attempt is the HEAD walk (DoseHeadOp): a GT-only record whose '\n' is
+// where the previous fixed-stride record predicts it is taken as a fixed-stride row without
+// "NA" and its samples are not read by the walk -- only the record heads are -- so the input is
+// read about once in all (by k_dose_fmt, which checks every sample byte of those rows while it
+// writes them).  A row that fails the check (an "NA", a wider sample, ...) flags the call,
+// which is then redone with the sweeping walk; an input that failed once keeps the sweeping
+// walk until the next load.  VCFXG_DOSE_HEAD=0 always sweeps.
+static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *L_out, bool *overflow, bool head);
+static int dosage_region_once(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out, bool head, bool *redo);
 
 int vcfxg_dosage_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
+    static const bool head_ok = [] {
+        const char *e = getenv("VCFXG_DOSE_HEAD");
+        return !(e && e[0] == '0');
+    }();
+    bool redo = false;
+    int r = dosage_region_once(c, data_start, mode, out, head_ok && !c->dose_head_failed, &redo);
+    if (r || !redo) return r;
+    c->dose_head_failed = true;
+    return dosage_region_once(c, data_start, mode, out, false, &redo);
+}
+
+static int dosage_region_once(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out, bool head, bool *redo) {
     static const bool walk_ok = [] {
         const char *e = getenv("VCFXG_DOSE_WALK");
         return !(e && e[0] == '0');
@@ -1466,12 +1490,14 @@ int vcfxg_dosage_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary
     uint64_t L = 0;
     int r;
     bool walked = false;
+    head = head && walk;
     if (walk) {
         bool ovf = false;
-        r = dose_walk_index(c, data_start, mode, &L, &ovf);
+        r = dose_walk_index(c, data_start, mode, &L, &ovf, head);
         if (r) return r;
         walked = !ovf;
     }
+    head = head && walked;
     if (!walked) {
         r = vcfxg_index(c, data_start, &L);
         if (r) return r;
@@ -1497,20 +1523,31 @@ int vcfxg_dosage_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary
     r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)L + 1);
     if (r) return r;
     prof_end(c, "dose_rows");
-    static thread_local uint64_t tail[5];
+    static thread_local uint64_t tail[6];
     HIPCHK(c, hipMemcpyAsync(&tail[0], P<uint64_t>(c->rowoff) + L, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&tail[1], c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tail[1], c->counters.p, 40, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const uint64_t text = tail[0];
     r = ensure(c, c->text, text + 1);
     if (r) return r;
+    // (the head walk's rows are checked by the formatting pass: a failed check flags the call)
+    unsigned *bad = head ? reinterpret_cast<unsigned *>(P<uint64_t>(c->wk_small) + 4) : nullptr;
+    static thread_local unsigned bad_h;
+    bad_h = 0;
+    if (bad) HIPCHK(c, hipMemsetAsync(bad, 0, 4, c->stream));
     prof_begin(c, "dose_fmt");
     HIPCHK(c, vcfxg::launch_dose_fmt(buf, (int64_t)data_start, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L,
                                      P<uint8_t>(c->status), c->dose_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
-                                     ~0ull, tail[2], c->stream));
+                                     ~0ull, tail[2], c->stream, bad, tail[5]));
     prof_end(c, "dose_fmt");
+    if (bad) HIPCHK(c, hipMemcpyAsync(&bad_h, bad, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
+    if (bad_h) {  // some row the head walk took is not a fixed-stride row without "NA": redo
+        *redo = true;
+        c->text_bytes = 0;
+        return VCFXG_OK;
+    }
     c->text_bytes = text;
     if (out) {
         out->n_lines = L;

@@ -21,6 +21,8 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
 // compress a 0x80-per-byte mask to 4 bits (bit j = byte j)
 __device__ __forceinline__ uint32_t pack4(uint32_t m) { return (((m >> 7) * 0x00204081u) >> 21) & 0xFu; }
 
+// bytes of a 4-bit mask (bit j -> byte j = 0xFF)
+__device__ __forceinline__ uint32_t nib_bytes(uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu; }
 // 16-bit mask of the bytes of v equal to the byte replicated in rep
 __device__ __forceinline__ uint32_t eq_mask16(const uint4 v, uint32_t rep) {
     return pack4(zero_bytes(v.x ^ rep)) | (pack4(zero_bytes(v.y ^ rep)) << 4) |

@@ -104,7 +104,8 @@ struct DoseMeta {
     int32_t gi;     // GT index in FORMAT
     uint8_t kind;   // kDose*
     uint8_t plain;  // kDoseFast without an "NA": 2 output bytes per sample
-    uint8_t pad[2];
+    uint8_t sep;    // kDoseFast: the separator (the byte at S + 1)
+    uint8_t pad;
 };
 
 // kFast: the first pass -- fixed-stride records (and the head-only kinds) only; any other
@@ -118,12 +119,12 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
                                                            DoseMeta *__restrict__ meta,
                                                            unsigned long long *__restrict__ counters) {
     __shared__ int64_t scratch[kDoseWaves][16];
-    __shared__ uint32_t red[4][kDoseWaves];
+    __shared__ uint32_t red[5][kDoseWaves];
     int64_t *lds = scratch[threadIdx.x / kWave];
     const uint64_t n_lines = *n_lines_p;
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
-    uint32_t rows = 0, warns = 0, gen = 0, slow = 0;  // (wave-uniform; slow: rows not kDoseFast)
+    uint32_t rows = 0, warns = 0, gen = 0, slow = 0, napl = 0;  // (wave-uniform; slow: rows not kDoseFast)
     for (uint64_t li = wid; li < n_lines; li += nw) {
         if (!kFast && status[li] != kDosePend) continue;  // (wave-uniform)
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
                     bool fast = gi == 0 && gt_fast(buf, S, ae, op);
                     m.kind = kDoseFast;
                     m.plain = fast && op.na == 0;
+                    m.sep = fast ? (uint8_t)byte_at(buf, S + 1) : 0;
                     if (kFast && !fast) st = kDosePend;
                     else if (!fast) {
                         m.kind = kDoseGeneral;
@@ -171,6 +173,7 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
         }
         rows += st == kDoseRow;
         slow += st == kDoseRow && m.kind != kDoseFast;
+        napl += st == kDoseRow && m.kind == kDoseFast && !m.plain;
         warns += st == kDoseWarn;
         if (lane() == 0) {
             status[li] = st;
@@ -184,12 +187,13 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_len(const char *__restric
         red[1][threadIdx.x / kWave] = warns;
         red[2][threadIdx.x / kWave] = gen;
         red[3][threadIdx.x / kWave] = slow;
+        red[4][threadIdx.x / kWave] = napl;
     }
     __syncthreads();
-    if (threadIdx.x < 4) {  // counters: rows, rows k_dose_fmt<false> writes, warnings, general
+    if (threadIdx.x < 5) {  // counters: rows, rows of k_dose_fmt<kFmtOther>, warnings, general, rows of kFmtNa
         uint32_t t = 0;
         for (int k = 0; k < kDoseWaves; k++) t += red[threadIdx.x][k];
-        const int slot = threadIdx.x == 0 ? 0 : threadIdx.x == 1 ? 2 : threadIdx.x == 2 ? 3 : 1;
+        const int slot = threadIdx.x == 0 ? 0 : threadIdx.x == 1 ? 2 : threadIdx.x == 2 ? 3 : threadIdx.x == 3 ? 1 : 4;
         if (t) atomicAdd(&counters[slot], (unsigned long long)t);
     }
 }
@@ -205,16 +209,19 @@ __device__ __forceinline__ void put_dose(char *o, int d, bool last) {
     }
 }
 
-// kFast: the fixed-stride records only (m.kind == kDoseFast); the other launch takes every
-// other row kind, so the fixed-stride pass carries none of the general placement's registers
-template <bool kFast>
+// one launch per row kind, so each carries only its own registers and code: kFmtPlain the
+// fixed-stride rows without "NA" (every row of a clean GT-only input), kFmtNa the fixed-stride
+// rows with some "NA" (launched when k_dose_len / k_dose_from_walk counted any), kFmtOther every
+// other row kind (likewise)
+enum : int { kFmtOther = 0, kFmtNa = 1, kFmtPlain = 2 };
+template <int kMode>
 __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restrict__ buf, int64_t data_start,
                                                            const uint64_t *__restrict__ line_end,
                                                            const uint64_t *n_lines_p,
                                                            const uint8_t *__restrict__ status,
                                                            const DoseMeta *__restrict__ meta,
                                                            const uint64_t *__restrict__ off, char *__restrict__ out,
-                                                           uint64_t cap) {
+                                                           uint64_t cap, unsigned *__restrict__ bad) {
     const uint64_t n_lines = *n_lines_p;
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
@@ -222,7 +229,7 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
         if (status[li] != kDoseRow || off[li + 1] > cap) continue;  // (wave-uniform)
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
         const DoseMeta m = meta[li];
-        if ((m.kind == kDoseFast) != kFast) continue;  // (wave-uniform)
+        if ((m.kind != kDoseFast ? kFmtOther : m.plain ? kFmtPlain : kFmtNa) != kMode) continue;  // (wave-uniform)
         char *o = out + off[li];
         for (uint32_t k = lane(); k < m.pre; k += kWave) o[k] = buf[ls + k];
         o += m.pre;
@@ -243,45 +250,56 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
         // bytes end there is the last, and ends with '\n' instead of ','
         const uint64_t tot = off[li + 1] - off[li] - m.pre;
         uint64_t run = 0;  // output bytes of the samples before this wave-step
-        if (m.kind == kDoseFast && m.plain) {
+        if (kMode == kFmtPlain) {
             // fixed-stride, no "NA": sample k ("a s b\t" at S + 4k) is output bytes 2k, 2k + 1
-            // of the dosage text (the digit, then ',' or the final '\n').  Lane c takes samples
-            // 8c..8c+7 (32 input bytes, realigned from three 16 B loads by S mod 16) and builds
-            // the aligned 16 B output block that starts inside its 16 bytes' span: the previous
-            // lane's last (ob mod 16) bytes, then its own first ones -- one store per block
+            // of the dosage text (the digit, then ',' -- the row's last byte '\n').  Lane c takes
+            // samples 8c..8c+7 (32 input bytes, realigned by S mod 4 from 36 bytes at a 4-aligned address) and
+            // builds the aligned 16 B output block that starts inside its 16 bytes' span: the
+            // previous lane's last (ob mod 16) bytes, then its own first ones -- one store per block.
+            // Every sample is checked while it is read (a row the head walk took on its predicted
+            // end alone may turn out otherwise -- the call is then redone): with e = dword ^
+            // "0 s 0 \t" (s = m.sep), the separator and tab bytes of e are 0 and each allele
+            // field of e is below 10; the dosage is the number of non-zero allele fields.
             const int64_t ns = (E - S + 1) / 4;
             const uint64_t ob = (uint64_t)(o - out), oe = ob + 2 * (uint64_t)ns;
-            const uint32_t ish = (uint32_t)(S & 15), osh = (uint32_t)(ob & 15);
-            const uint32_t iq = ish >> 2, ib = ish & 3, wq = (16u - osh) >> 2, wb = (16u - osh) & 3;
+            const uint32_t osh = (uint32_t)(ob & 15);
+            const uint32_t ib = (uint32_t)(S & 3), wq = (16u - osh) >> 2, wb = (16u - osh) & 3;
             const int64_t nch = (ns + 7) / 8;  // chunks of 8 samples; chunk nch holds only the tail block
             uint32_t carry[4] = {0u, 0u, 0u, 0u};  // the previous wave-step's last chunk
+            const uint32_t exp = 0x09300030u | ((uint32_t)m.sep << 8);
+            uint32_t err = m.sep == '/' || m.sep == '|' ? 0u : 1u;
             for (int64_t c0 = 0; c0 <= nch; c0 += kWave) {
                 const int64_t c = c0 + lane(), k0 = 8 * c;
+                const bool edge = c0 + kWave > nch - 1;  // (wave-uniform) the step holds the last sample
                 uint32_t od[4] = {0u, 0u, 0u, 0u};
                 if (c < nch) {
-                    const char *ip = buf + ((S + 4 * k0) & ~(int64_t)15);
-                    const uint4 v0 = load16(ip, 0), v1 = load16(ip, 16), v2 = load16(ip, 32);
-                    const uint32_t w[12] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, v2.x, v2.y, v2.z, v2.w};
-                    uint32_t r[8];
+                    // 36 bytes from the 4-aligned address at or before the lane's first sample:
+                    // the samples are then the byte rotation ib (= S mod 4) of consecutive words,
+                    // with no word-level select (a select on the uniform word offset compiled to
+                    // branches around the loads: 1.38 -> 1.58 ms for this pass with the checks)
+                    typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+                    const uint32_t *ip = reinterpret_cast<const uint32_t *>(buf + ((S + 4 * k0) & ~(int64_t)3));
+                    const u32x4a4 v0 = *reinterpret_cast<const u32x4a4 *>(ip), v1 = *reinterpret_cast<const u32x4a4 *>(ip + 4);
+                    const uint32_t w[9] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, ip[8]};
+                    uint32_t e[8];
 #pragma unroll
-                    for (int i = 0; i < 8; i++) {  // (iq wave-uniform)
-                        const uint32_t lo_ = iq == 0 ? w[i] : iq == 1 ? w[i + 1] : iq == 2 ? w[i + 2] : w[i + 3];
-                        const uint32_t hi_ = iq == 0 ? w[i + 1] : iq == 1 ? w[i + 2] : iq == 2 ? w[i + 3] : w[i + 4];
-                        r[i] = __builtin_amdgcn_alignbyte(hi_, lo_, ib);
+                    for (int i = 0; i < 8; i++) e[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], ib);
+#pragma unroll
+                    for (int t = 0; t < 8; t++) e[t] ^= exp;
+                    if (edge) {  // samples past the record: nothing; the last one's tab byte is the line end
+                        const int rem = (int)std::min<int64_t>(ns - k0, 8);
+#pragma unroll
+                        for (int t = 0; t < 8; t++) e[t] = t < rem ? (t == rem - 1 ? e[t] & 0x00FFFFFFu : e[t]) : 0u;
+                    }
+                    uint32_t dd[8];
+#pragma unroll
+                    for (int t = 0; t < 8; t++) {
+                        const uint32_t f = e[t] & 0x00FF00FFu;
+                        err |= (e[t] & 0xFF00FF00u) | ((f + 0x00F600F6u) & 0x01000100u);  // field >= 10
+                        dd[t] = __popc((f + 0x00FF00FFu) & 0x01000100u);                  // field >= 1
                     }
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        uint32_t v = 0;
-#pragma unroll
-                        for (int h = 0; h < 2; h++) {
-                            const int t = 2 * j + h;
-                            const uint32_t a = r[t] & 0xFFu, b = (r[t] >> 16) & 0xFFu;
-                            const uint32_t d = (a != '0') + (b != '0');
-                            const uint32_t sep = k0 + t == ns - 1 ? (uint32_t)'\n' : (uint32_t)',';
-                            v |= (('0' + d) | (sep << 8)) << (16 * h);
-                        }
-                        od[j] = v;
-                    }
+                    for (int j = 0; j < 4; j++) od[j] = 0x2C302C30u + dd[2 * j] + (dd[2 * j + 1] << 16);  // "d,d,"
                 }
                 // the previous chunk's bytes: the lane before, or the carry for lane 0
                 uint32_t pv[4];
@@ -291,7 +309,7 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
                     pv[j] = lane() ? up : carry[j];
                     carry[j] = (uint32_t)__shfl((int)od[j], kWave - 1);
                 }
-                // the block = bytes [16 - osh, 32 - osh) of (pv ++ od)
+                // the block = bytes [16 - osh, 32 - osh) of (pv ++ od): word wq + i, byte wb
                 const uint32_t X[9] = {pv[0], pv[1], pv[2], pv[3], od[0], od[1], od[2], od[3], 0u};
                 uint32_t bw[4];
 #pragma unroll
@@ -301,6 +319,12 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
                     bw[i] = __builtin_amdgcn_alignbyte(hi_, lo_, wb);
                 }
                 const uint64_t base = (ob & ~15ull) + 16ull * (uint64_t)c;
+                if (edge && oe - 1 >= base && oe - 1 < base + 16) {  // the row's last byte: '\n'
+                    const uint32_t q = (uint32_t)(oe - 1 - base);
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if ((q >> 2) == (uint32_t)i) bw[i] = (bw[i] & ~(0xFFu << (8 * (q & 3)))) | (0x0Au << (8 * (q & 3)));
+                }
                 if (c <= nch && base < oe) {
                     if (base >= ob && base + 16 <= oe)
                         *reinterpret_cast<uint4 *>(out + base) = make_uint4(bw[0], bw[1], bw[2], bw[3]);
@@ -310,9 +334,10 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
                             if (base + j >= ob && base + j < oe) out[base + j] = (char)(bw[j >> 2] >> (8 * (j & 3)));
                 }
             }
+            if (__any(err != 0u) && lane() == 0 && bad) atomicOr(bad, 1u);
             continue;
         }
-        if (m.kind == kDoseFast) {
+        if (kMode == kFmtNa) {
             // the fixed-stride layout: samples "a s b\t" on the 4-byte grid from S, the last
             // without its tab; lane l of a wave-step takes 4 consecutive samples
             const int64_t ns = (E - S + 1) / 4;
@@ -394,7 +419,7 @@ __global__ void k_dose_from_walk(const uint64_t *__restrict__ line_end, const ui
                                  uint64_t *__restrict__ len, DoseMeta *__restrict__ meta,
                                  unsigned long long *__restrict__ counters) {
     const uint64_t n_lines = *n_lines_p;
-    uint32_t rows = 0;
+    uint32_t rows = 0, napl = 0;
     for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < n_lines;
          li += (uint64_t)gridDim.x * blockDim.x) {
         const LineMeta w = wm[li];
@@ -410,6 +435,8 @@ __global__ void k_dose_from_walk(const uint64_t *__restrict__ line_end, const ui
             m.gi = 0;
             m.kind = kDoseFast;
             m.plain = na[li] == 0;
+            m.sep = w.sep;
+            napl += !m.plain;
             st = kDoseRow;
             L = (uint64_t)m.pre + 2u * (uint64_t)ns[li] + (uint64_t)na[li];
             rows++;
@@ -419,7 +446,9 @@ __global__ void k_dose_from_walk(const uint64_t *__restrict__ line_end, const ui
         meta[li] = m;
     }
     rows = wave_sum(rows);
+    napl = wave_sum(napl);
     if (lane() == 0 && rows) atomicAdd(&counters[0], (unsigned long long)rows);
+    if (lane() == 0 && napl) atomicAdd(&counters[4], (unsigned long long)napl);
 }
 
 hipError_t launch_dose_from_walk(const uint64_t *line_end, const uint64_t *n_lines_dev, uint64_t n_lines_host,
@@ -448,14 +477,19 @@ hipError_t launch_dose_len(const char *buf, int64_t data_start, const uint64_t *
 
 hipError_t launch_dose_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, const uint8_t *status, const void *meta, const uint64_t *off,
-                           char *out, uint64_t cap, uint64_t slow_rows, hipStream_t s) {
+                           char *out, uint64_t cap, uint64_t slow_rows, hipStream_t s, unsigned *bad,
+                           uint64_t na_rows) {
     if (!n_lines_host) return hipSuccess;
     const dim3 g(dose_grid((int64_t)n_lines_host, kDoseWaves, 2048));
-    hipLaunchKernelGGL(k_dose_fmt<true>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev, status,
-                       static_cast<const DoseMeta *>(meta), off, out, cap);
-    if (slow_rows)  // (k_dose_len counted them: no pass over every line for nothing)
-        hipLaunchKernelGGL(k_dose_fmt<false>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev,
-                           status, static_cast<const DoseMeta *>(meta), off, out, cap);
+    hipLaunchKernelGGL(k_dose_fmt<kFmtPlain>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                       status, static_cast<const DoseMeta *>(meta), off, out, cap, bad);
+    // (k_dose_len / k_dose_from_walk counted these rows: no pass over every line for nothing)
+    if (na_rows)
+        hipLaunchKernelGGL(k_dose_fmt<kFmtNa>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                           status, static_cast<const DoseMeta *>(meta), off, out, cap, bad);
+    if (slow_rows)
+        hipLaunchKernelGGL(k_dose_fmt<kFmtOther>, g, dim3(kDoseThreads), 0, s, buf, data_start, line_end, n_lines_dev,
+                           status, static_cast<const DoseMeta *>(meta), off, out, cap, bad);
     return hipGetLastError();
 }
 

@@ -318,9 +318,6 @@ struct AfOp {
     }
 };
 
-// bytes of a 4-bit mask (bit j -> byte j = 0xFF)
-__device__ __forceinline__ uint32_t nib_bytes(uint32_t nib) { return ((nib * 0x00204081u) & 0x01010101u) * 0xFFu; }
-
 // ---------------------------------------------------------------------------------------
 // af_fixed: gt_fast + AfOp (the same record test and the same counts) on the raw 16 B
 // blocks, without realigning them to the sample grid.  In a fixed-stride record every byte's
@@ -646,6 +643,13 @@ struct DoseWalkOp {
         na = wave_sum(na);
     }
 };
+
+// the dosage HEAD walk (k_af_walk<DoseHeadOp>): a GT-only record whose end the walk predicts
+// from the previous fixed-stride record (and whose predicted end byte is the '\n') is taken
+// as fixed-stride without "NA" and without its samples being read; k_dose_fmt checks every
+// sample byte of such a row while it writes it and flags the call when one fails (the call is
+// then redone with DoseWalkOp).  Records the walk sweeps anyway count as DoseWalkOp does.
+struct DoseHeadOp : DoseWalkOp {};
 
 struct HweOp {
     const char *buf;

@@ -66,7 +66,7 @@ hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk
                           uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
                           uint8_t *status_b, void *meta_b, uint64_t *wcount, uint32_t *wgt, unsigned *overflow,
                           hipStream_t s, int32_t *hwe_aux_b = nullptr, const WalkTail *tail = nullptr,
-                          bool dose = false, bool gt_first_walk = false);
+                          bool dose = false, bool gt_first_walk = false, bool dose_head = false);
 // AF region tail without the dense per-line arrays (vcfxg_kernels.hip):
 //   launch_af_cx       the walk's leftover slots: af_line / the general sweep, new rows' bytes
 //                      added to their walker's total (counters as k_af_complex)
@@ -157,7 +157,8 @@ hipError_t launch_dose_from_walk(const uint64_t *line_end, const uint64_t *n_lin
                                  uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s);
 hipError_t launch_dose_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, const uint8_t *status, const void *meta, const uint64_t *off,
-                           char *out, uint64_t cap, uint64_t slow_rows, hipStream_t s);
+                           char *out, uint64_t cap, uint64_t slow_rows, hipStream_t s, unsigned *bad = nullptr,
+                           uint64_t na_rows = ~0ull);
 // VCFX_missing_detector (vcfxg_md.hip) over the indexed lines: per line status (0 empty, 4 '#',
 // 1 kept as is, kMdFlag flagged) and the flagged lines' INFO span relative to the line start;
 // counters [0] data lines, [1] flagged, [2] lines ending in '\n' with a '.' in their samples;
