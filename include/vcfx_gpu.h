@@ -65,6 +65,9 @@ const char *vcfxg_last_error(const vcfxg_ctx *ctx);
 void *vcfxg_stream(vcfxg_ctx *ctx);
 /* record HIP events around each kernel launch (see vcfxg_kernel_ms) */
 int vcfxg_set_profiling(vcfxg_ctx *ctx, int enable);
+/* time only the named kernel (nullptr or "": every kernel); the launches' events are read
+   when the figures are asked for, so a profiled loop makes no event queries between calls */
+int vcfxg_set_profiling_only(vcfxg_ctx *ctx, const char *kernel);
 /* elapsed ms of the last launch of the named kernel ("af_records", "line_index", ...) */
 int vcfxg_kernel_ms(vcfxg_ctx *ctx, const char *kernel, float *ms);
 /* accumulated event time and launch count of the named kernel since the last reset */

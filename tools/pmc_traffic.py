@@ -25,8 +25,10 @@ KERNELS = {
     "line_emit": r"vcfxg::k_idx_sweep<true>\(",
     "line_compact": r"vcfxg::k_nl_compact\(",
     "af_records": r"vcfxg::k_(line_meta|af_sweep|af_complex)\(",
-    "af_walk": r"vcfxg::k_af_walk<vcfxg::AfOp>\(",
-    "hwe_walk": r"vcfxg::k_af_walk<vcfxg::HweOp>\(",
+    "af_walk": r"vcfxg::k_af_walk<vcfxg::AfOp(, false)?>\(",
+    "hwe_walk": r"vcfxg::k_af_walk<vcfxg::HweOp(, false)?>\(",
+    "dose_walk": r"vcfxg::k_af_walk<vcfxg::Dose(Walk|Head)Op(, false)?>\(",
+    "dose_fmt": r"vcfxg::k_dose_fmt<",
     "walk_compact": r"vcfxg::k_walk_compact\(",
     "af_complex": r"vcfxg::k_af_(complex|cx)\(",
     "af_rows": r"vcfxg::k_(walker_scan|af_rowlen|af_summary)\(",
@@ -60,6 +62,7 @@ TIMED = {
             "line_compact"),
     "pipeline": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "rf_records", "gq_records"),
     "nonref": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "nr_records"),
+    "dose": ("dose_walk", "walk_compact", "dose_fmt"),
     "ld": ("line_count", "line_emit", "line_compact", "ld_parse", "ld_count", "ld_emit", "ld_count_gen",
            "ld_emit_gen", "ld_matrix", "ld_pack_vq", "ld_count_mask", "ld_emit_mask"),
 }

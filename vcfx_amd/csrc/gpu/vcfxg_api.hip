@@ -118,12 +118,18 @@ struct vcfxg_ctx {
     std::vector<uint32_t> ld_cid_host, ld_blocks_host;
     uint64_t text_bytes = 0;
     uint64_t text_hint = 0;  // AF walk: text bytes of the previous call (the next call's capacity)
-    // profiling
+    // profiling: an event pair per launch from a pool, harvested only when the figures are
+    // read (or the pending list is long): no event queries between the calls of a timed loop
     bool profiling = false;
-    std::map<std::string, std::pair<hipEvent_t, hipEvent_t>> ev;
+    std::string prof_only;  // non-empty: only this kernel is timed
+    struct ProfRec {
+        const char *name;
+        hipEvent_t a, b;
+    };
+    std::vector<hipEvent_t> ev_free;
+    std::vector<ProfRec> ev_open, pending;
     std::map<std::string, float> ms;           // last launch
     std::map<std::string, std::pair<double, uint64_t>> acc;  // sum ms, launches
-    std::vector<std::string> pending;
 };
 
 namespace {
@@ -160,33 +166,57 @@ T *P(DevBuf &b) {
     return reinterpret_cast<T *>(b.p);
 }
 
-void prof_begin(vcfxg_ctx *c, const char *name) {
-    if (!c->profiling) return;
-    auto &e = c->ev[name];
-    if (!e.first) {
-        (void)hipEventCreate(&e.first);
-        (void)hipEventCreate(&e.second);
+static hipEvent_t prof_event(vcfxg_ctx *c) {
+    hipEvent_t e = nullptr;
+    if (!c->ev_free.empty()) {
+        e = c->ev_free.back();
+        c->ev_free.pop_back();
+    } else {
+        (void)hipEventCreate(&e);
     }
-    (void)hipEventRecord(e.first, c->stream);
+    return e;
+}
+static bool prof_on(vcfxg_ctx *c, const char *name) {
+    return c->profiling && (c->prof_only.empty() || c->prof_only == name);
+}
+void prof_begin(vcfxg_ctx *c, const char *name) {
+    if (!prof_on(c, name)) return;
+    hipEvent_t e = prof_event(c);
+    (void)hipEventRecord(e, c->stream);
+    c->ev_open.push_back({name, e, nullptr});
 }
 void prof_end(vcfxg_ctx *c, const char *name) {
-    if (!c->profiling) return;
-    (void)hipEventRecord(c->ev[name].second, c->stream);
-    c->pending.push_back(name);
+    if (!prof_on(c, name)) return;
+    for (size_t k = c->ev_open.size(); k-- > 0;) {
+        if (strcmp(c->ev_open[k].name, name)) continue;
+        vcfxg_ctx::ProfRec r = c->ev_open[k];
+        c->ev_open.erase(c->ev_open.begin() + k);
+        r.b = prof_event(c);
+        (void)hipEventRecord(r.b, c->stream);
+        c->pending.push_back(r);
+        return;
+    }
 }
-// after a stream sync: harvest elapsed times
-void prof_collect(vcfxg_ctx *c) {
-    for (auto &nm : c->pending) {
-        auto &e = c->ev[nm];
+// elapsed times of the recorded launches (synchronises with the stream first)
+static void prof_harvest(vcfxg_ctx *c) {
+    if (c->pending.empty()) return;
+    (void)hipStreamSynchronize(c->stream);
+    for (auto &r : c->pending) {
         float t = 0.f;
-        if (hipEventElapsedTime(&t, e.first, e.second) == hipSuccess) {
-            c->ms[nm] = t;
-            auto &a = c->acc[nm];
+        if (hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+            c->ms[r.name] = t;
+            auto &a = c->acc[r.name];
             a.first += t;
             a.second += 1;
         }
+        c->ev_free.push_back(r.a);
+        c->ev_free.push_back(r.b);
     }
     c->pending.clear();
+}
+// after a call: harvest only when many launches are pending (bounded event pool)
+void prof_collect(vcfxg_ctx *c) {
+    if (c->pending.size() >= 4096) prof_harvest(c);
 }
 
 template <typename InT>
@@ -255,10 +285,12 @@ void vcfxg_close(vcfxg_ctx *c) {
         if (b->p) (void)hipFree(b->p);
     for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
     for (hipEvent_t e : c->ingest_ev_free) (void)hipEventDestroy(e);
-    for (auto &kv : c->ev) {
-        (void)hipEventDestroy(kv.second.first);
-        (void)hipEventDestroy(kv.second.second);
+    for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
+    for (auto &r : c->pending) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
     }
+    for (auto &r : c->ev_open) (void)hipEventDestroy(r.a);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -272,8 +304,15 @@ int vcfxg_set_profiling(vcfxg_ctx *c, int enable) {
     return VCFXG_OK;
 }
 
+int vcfxg_set_profiling_only(vcfxg_ctx *c, const char *kernel) {
+    if (!c) return VCFXG_E_ARG;
+    c->prof_only = kernel ? kernel : "";
+    return VCFXG_OK;
+}
+
 int vcfxg_kernel_ms(vcfxg_ctx *c, const char *kernel, float *ms) {
     if (!c || !kernel || !ms) return VCFXG_E_ARG;
+    prof_harvest(c);
     auto it = c->ms.find(kernel);
     if (it == c->ms.end()) return VCFXG_E_STATE;
     *ms = it->second;
@@ -282,6 +321,7 @@ int vcfxg_kernel_ms(vcfxg_ctx *c, const char *kernel, float *ms) {
 
 int vcfxg_kernel_stats(vcfxg_ctx *c, const char *kernel, double *total_ms, uint64_t *launches) {
     if (!c || !kernel) return VCFXG_E_ARG;
+    prof_harvest(c);
     auto it = c->acc.find(kernel);
     if (total_ms) *total_ms = it == c->acc.end() ? 0.0 : it->second.first;
     if (launches) *launches = it == c->acc.end() ? 0 : it->second.second;
@@ -290,6 +330,7 @@ int vcfxg_kernel_stats(vcfxg_ctx *c, const char *kernel, double *total_ms, uint6
 
 int vcfxg_reset_kernel_stats(vcfxg_ctx *c) {
     if (!c) return VCFXG_E_ARG;
+    prof_harvest(c);
     c->acc.clear();
     return VCFXG_OK;
 }
@@ -630,10 +671,7 @@ static int af_region_async(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summ
                                       P<int32_t>(c->alt), P<int32_t>(c->tot), P<uint32_t>(c->rowpre),
                                       P<uint8_t>(c->status), P<uint64_t>(c->rowoff), P<char>(c->text), c->stream));
     prof_end(c, "af_format");
-    if (c->profiling) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        prof_collect(c);
-    }
+    prof_collect(c);
     c->data_start = data_start;
     c->n_lines = L;
     c->indexed = true;
@@ -753,10 +791,7 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
                                             P<uint8_t>(c->wk_status), P<char>(c->text), ~0ull, c->stream));
         prof_end(c, "af_format");
     }
-    if (c->profiling) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        prof_collect(c);
-    }
+    prof_collect(c);
     c->data_start = data_start;
     c->n_lines = L;
     c->indexed = true;
@@ -1344,10 +1379,7 @@ static int hwe_region_impl(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summ
         HIPCHK(c, hipMemcpyAsync(&sm[7], rc_n, 8, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    if (c->profiling) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        prof_collect(c);
-    }
+    prof_collect(c);
     c->data_start = data_start;
     c->n_lines = L;
     c->indexed = true;

@@ -43,6 +43,7 @@ SIGNATURES = {
     "vcfxg_last_error": (_P, [_VP]),
     "vcfxg_stream": (_VP, [_VP]),
     "vcfxg_set_profiling": (_I, [_VP, _I]),
+    "vcfxg_set_profiling_only": (_I, [_VP, _P]),
     "vcfxg_kernel_ms": (_I, [_VP, _P, ctypes.POINTER(ctypes.c_float)]),
     "vcfxg_kernel_stats": (_I, [_VP, _P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_U64)]),
     "vcfxg_reset_kernel_stats": (_I, [_VP]),
@@ -102,6 +103,8 @@ def lib():
             raise RuntimeError("libvcfx_gpu.so not built (run `make` or __graft_entry__.build())")
         _lib = ctypes.CDLL(GPU_LIB)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("VCFXG_GPU_LIB") and not hasattr(_lib, name):
+                continue  # an older experiment build (A/B runs): its missing entries are not called
             f = getattr(_lib, name)
             f.restype = res
             f.argtypes = args
@@ -145,6 +148,12 @@ class Engine:
 
     def set_profiling(self, on=True):
         self._chk(self.L.vcfxg_set_profiling(self.h, int(on)), "set_profiling")
+
+    def set_profiling_only(self, name=None):
+        """time only the named kernel (None: every kernel)"""
+        if not hasattr(self.L, "vcfxg_set_profiling_only"):  # (an older experiment build: every kernel)
+            return
+        self._chk(self.L.vcfxg_set_profiling_only(self.h, name.encode() if name else None), "set_profiling_only")
 
     def kernel_ms(self, name):
         v = ctypes.c_float()
