@@ -105,3 +105,50 @@ def test_af_gt_ad_dp_region_matches_oracle(eng, oracle, cfg, tmp_path):
         want = oracle.run(argv, stdin)
         assert b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes) == want[0]
         assert tools.run(argv, stdin) == want
+
+
+def _mutate_gtadp(buf, edits):
+    """replace sample k of data record r (0-based) with the given bytes; (r, None, tail) appends
+    tail bytes to the record's end instead (before its newline)"""
+    lines = buf.split(b"\n")
+    first = next(i for i, l in enumerate(lines) if l.startswith(b"#CHROM")) + 1
+    for r, k, new in edits:
+        f = lines[first + r].split(b"\t")
+        if k is None:
+            lines[first + r] = lines[first + r] + new
+            continue
+        f[9 + k] = new
+        lines[first + r] = b"\t".join(f)
+    return b"\n".join(lines)
+
+
+def test_af_gt_first_flag_sweep_edge_samples(eng, oracle, tmp_path):
+    """the GT-first walk's per-byte-flag sweep (gt_first_af) against the oracle on GT:AD:DP
+    records holding every sample shape it must either count as a quick 'c0 s c2' GT or hand to
+    the exact path: letters, haploid and multi-digit GTs, spaces, empty samples, a non-ASCII
+    byte, a CRLF line end, a bare last GT ('0|1' then the line end), a sample cut to 1-2 bytes
+    at the line end, a GT at a lane / step boundary"""
+    buf = synth.generate(n_records=400, n_samples=600, seed=41, missing_rate=0.01, format_mode=1)
+    edits = [
+        (3, 5, b"A|1:3,4:7"), (7, 0, b"0:3,4:7"), (11, 599, b"10|1:2,2:4"), (13, 100, b"0 |1:2,2:4"),
+        (17, 200, b""), (19, 300, b"0|1:\xc3\xa9,4:7"), (23, 599, b"0|1"), (29, 599, b"0"), (31, 599, b"0|"),
+        (37, 42, b"0|1:1,2:3:4:5"), (41, 63, b".|1:1,1:2"), (43, 64, b"1/.:1,1:2"), (47, 1, b"|0:1,1:2"),
+        (53, 2, b"0||:1,1:2"), (59, 77, b"0|1\t"), (61, 599, b"1|1:"), (67, 5, b"0/1:"), (71, 9, b"-|1:1,1:2"),
+    ]
+    buf = _mutate_gtadp(buf, edits)
+    # one CRLF record
+    lines = buf.split(b"\n")
+    first = next(i for i, l in enumerate(lines) if l.startswith(b"#CHROM")) + 1
+    lines[first + 79] += b"\r"
+    buf = b"\n".join(lines)
+    for mode in (engine.MODE_FILE, engine.MODE_STDIN):
+        ds = engine.data_start_of(buf, strip_cr=(mode == engine.MODE_FILE))
+        eng.load(buf)
+        s = eng.allele_freq_region(ds, mode)
+        p = tmp_path / "in.vcf"
+        p.write_bytes(buf)
+        argv = ["VCFX_allele_freq_calc", "-q"] + (["-i", str(p)] if mode == engine.MODE_FILE else [])
+        stdin = b"" if mode == engine.MODE_FILE else buf
+        want = oracle.run(argv, stdin)
+        assert b"CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n" + eng.text(s.text_bytes) == want[0]
+        assert tools.run(argv, stdin) == want

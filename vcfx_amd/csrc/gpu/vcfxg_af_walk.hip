@@ -44,6 +44,17 @@ namespace vcfxg {
 #define VCFXG_WALK_UNROLL 6
 #endif
 constexpr int kWalkUnroll = VCFXG_WALK_UNROLL;  // wave-steps (KiB) of a record in flight per sweep step
+// the GT-first walk's allele counts on per-byte flags (gt_first_af) rather than gt_first's loop
+// over each lane's sample starts (VCFXG_GF_FLAGS=0: the loop, for A/B)
+#ifndef VCFXG_GF_FLAGS
+#define VCFXG_GF_FLAGS 1
+#endif
+constexpr bool kGfFlags = VCFXG_GF_FLAGS != 0;
+// wave-steps in flight in the GT-first walk's sweeps (its flags take more registers per step)
+#ifndef VCFXG_GF_UNROLL
+#define VCFXG_GF_UNROLL 4
+#endif
+constexpr int kGfUnroll = VCFXG_GF_UNROLL;
 
 // the walk's per-record reducer: AF allele counts (alt, total) or, for VCFX_hwe_tester, the
 // genotype classes (hom-ref, het, hom-alt; the third in aux_o)
@@ -251,7 +262,10 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                     An = std::max<int64_t>(e - 1, 0) & ~(int64_t)15;
                     pre();
                 };
-                ok = gt_first<kWalkUnroll>(buf, S, hi, strip_cr, op, pre_e, Eo, cro);
+                if constexpr (std::is_same<Op, AfOp>::value && kGfFlags)
+                    ok = gt_first_af<kGfUnroll>(buf, S, hi, strip_cr, op, pre_e, Eo, cro);
+                else
+                    ok = gt_first<kWalkUnroll>(buf, S, hi, strip_cr, op, pre_e, Eo, cro);
                 E = Eo;
                 cr = cro;
                 const int64_t ae = E - cr;
@@ -280,7 +294,8 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                       : t8 + 2 < wend ? (uint8_t)sep_w
                                       : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
                 Op op = R::make(buf, ae);
-                if constexpr (std::is_same<Op, AfOp>::value) ok = af_fixed<kWalkUnroll>(buf, S, ae, op, sep, pre);
+                if constexpr (std::is_same<Op, AfOp>::value)
+                    ok = af_fixed < kGF ? kGfUnroll : kWalkUnroll > (buf, S, ae, op, sep, pre);
                 else if constexpr (std::is_same<Op, DoseHeadOp>::value) {
                     if (skip) {  // samples (ae - S + 1) / 4, none "NA" (checked by k_dose_fmt)
                         ok = (sep == '/' || sep == '|') && ae - S >= 3 && ((ae - S + 1) & 3) == 0;

@@ -69,6 +69,22 @@ struct vcfxg_ctx {
     DevBuf wk_tabs, rf_tabs;    // filter / query walk: per-line tab offsets (per walker, dense)
     // AF walk region tail: per walker row bytes, text offsets, first line start; leftover list
     DevBuf wk_text, wk_toff, wk_start, wk_cx, wk_bs, scratch_small;
+    // AF walk: flags / counters that k_walker_scan zeroes after reading them (af_small_dirty: a
+    // call did not get that far, so the next one clears them first), and the call summary the
+    // same kernel writes straight into mapped host memory (no copy before the synchronisation)
+    DevBuf af_small;
+    bool af_small_dirty = true;
+    uint64_t *sum_host = nullptr, *sum_dev = nullptr;
+    uint64_t cx_hint = ~0ull;  // leftover lines of the previous AF walk (sizes k_af_cx's grid)
+    // filter / query walk: overflow slot + 8 counters, zeroed by k_fq_done after each call
+    // (fq_small_dirty as af_small_dirty); its summary goes to sum_host[8..17]
+    DevBuf fq_small;
+    bool fq_small_dirty = true;
+    uint64_t fq_lines_hint = 0;  // lines of the previous filter / query walk (sizes k_fq_finish's grid)
+    // the bytes last uploaded to query / crit / pool and the buffer they went to: an unchanged
+    // query or criteria list is not copied again (any other writer resets the pointer)
+    std::string query_dev, crit_dev, pool_dev;
+    void *query_dev_p = nullptr, *crit_dev_p = nullptr, *pool_dev_p = nullptr;
     // the last AF walk left its per-line results in walker regions only (ensure_dense)
     bool dense_pending = false;
     int64_t dense_nw = 0;
@@ -283,6 +299,9 @@ void vcfxg_close(vcfxg_ctx *c) {
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
                       &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
         if (b->p) (void)hipFree(b->p);
+    if (c->af_small.p) (void)hipFree(c->af_small.p);
+    if (c->fq_small.p) (void)hipFree(c->fq_small.p);
+    if (c->sum_host) (void)hipHostFree(c->sum_host);
     for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
     for (hipEvent_t e : c->ingest_ev_free) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_free) (void)hipEventDestroy(e);
@@ -697,6 +716,16 @@ static int af_region_async(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summ
 // statuses) are compacted from the regions only when a later call asks for them
 // (ensure_dense).  A walker over its line capacity, or an overlong leftover list, reruns the
 // call on the two-sweep schedule (and later calls on this input use it directly).
+// the mapped host words the tail kernels write the call summaries into (AF walk [0..7],
+// filter / query walk [8..17])
+static int ensure_sum_host(vcfxg_ctx *c) {
+    if (c->sum_host) return VCFXG_OK;
+    HIPCHK(c, hipHostMalloc(reinterpret_cast<void **>(&c->sum_host), 256, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(c->sum_host, 0, 256);
+    HIPCHK(c, hipHostGetDevicePointer(reinterpret_cast<void **>(&c->sum_dev), c->sum_host, 0));
+    return VCFXG_OK;
+}
+
 static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summary *out, bool gf = false) {
     if (c) c->dense_pending = false;  // a new index / regions replace the pending ones
     HIPCHK(c, hipSetDevice(c->device));
@@ -724,17 +753,20 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     if (!r) r = ensure(c, c->wk_cx, 8 * cap);
     const int64_t nbs = (nw + vcfxg::kWalkerScanBlock - 1) / vcfxg::kWalkerScanBlock;
     if (!r) r = ensure(c, c->wk_bs, 8 * (size_t)(5 * nbs + 4));
-    if (!r) r = ensure(c, c->wk_small, 128);
+    if (!r) r = ensure(c, c->af_small, 128);
+    if (r) return r;
+    r = ensure_sum_host(c);
     if (r) return r;
     const char *buf = P<char>(c->input);
-    // [0] walk overflow flag (u32), [1] leftover count, [2..5] counters, [6] walker-scan
-    // arrivals (u32), [8..14] call summary
+    // [0] walk overflow flag (u32), [1] leftover count, [2..5] counters: zero on entry (k_walker_scan
+    // clears them for the next call); [6] walker-scan arrivals (u32, reset by its last block)
     uint64_t *bpre_a = P<uint64_t>(c->wk_bs), *bpre_b = bpre_a + nbs + 1, *bsum = bpre_b + nbs + 1;
-    uint64_t *small = P<uint64_t>(c->wk_small);
+    uint64_t *small = P<uint64_t>(c->af_small);
     unsigned *ovf = reinterpret_cast<unsigned *>(small);
     unsigned long long *cx_n = reinterpret_cast<unsigned long long *>(small + 1);
     unsigned long long *cnt = reinterpret_cast<unsigned long long *>(small + 2);
-    HIPCHK(c, hipMemsetAsync(small, 0, 128, c->stream));
+    if (c->af_small_dirty) HIPCHK(c, hipMemsetAsync(small, 0, 128, c->stream));
+    c->af_small_dirty = true;  // until the call has synchronised
     vcfxg::WalkTail tail;
     tail.wtext = P<uint64_t>(c->wk_text);
     tail.wstart = P<uint64_t>(c->wk_start);
@@ -748,15 +780,18 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
                                     P<uint32_t>(c->wk_gt), ovf, c->stream, nullptr, &tail, false, gf));
     prof_end(c, "af_walk");
     prof_begin(c, "af_complex");
-    HIPCHK(c, vcfxg::launch_af_cx(buf, mode, cap_w, tail.cx_list, cx_n, cap, cap, tail.wstart, P<uint64_t>(c->wk_le),
-                                  c->wk_meta.p, P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot),
+    // the grid: a wave per leftover line of the previous call (usually none; 16 blocks at least)
+    const uint64_t cx_grid_lines = std::min<uint64_t>(cap, std::max<uint64_t>(c->cx_hint, 64));
+    HIPCHK(c, vcfxg::launch_af_cx(buf, mode, cap_w, tail.cx_list, cx_n, cap, cx_grid_lines, tail.wstart,
+                                  P<uint64_t>(c->wk_le), c->wk_meta.p, P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot),
                                   P<uint32_t>(c->wk_rowpre), P<uint8_t>(c->wk_status), tail.wtext, cnt, c->stream));
     prof_end(c, "af_complex");
     prof_begin(c, "af_rows");
+    uint64_t *sm = c->sum_host;  // lines, text bytes, counters[0..3], walk overflow, leftovers
     HIPCHK(c, vcfxg::launch_walker_scan(nw, P<uint64_t>(c->wk_count), tail.wtext, P<uint32_t>(c->wk_gt),
                                         P<uint64_t>(c->wk_offs), P<uint64_t>(c->wk_toff), bpre_a, bpre_b, bsum,
                                         reinterpret_cast<unsigned *>(small + 6), cnt, ovf, P<uint64_t>(c->d_nlines),
-                                        small + 8, c->stream));
+                                        c->sum_dev, c->stream, small));
     prof_end(c, "af_rows");
     // the rows go out before the host has seen their total: into the text capacity of the
     // previous call (rows past it are skipped, and all are written again below once it has
@@ -771,9 +806,9 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
                                         P<char>(c->text), tcap, c->stream));
     prof_end(c, "af_format");
     // (the leftover list holds every slot at most once: it cannot overflow its capacity)
-    static thread_local uint64_t sm[7];  // lines, text bytes, counters[0..3], walk overflow
-    HIPCHK(c, hipMemcpyAsync(sm, small + 8, sizeof sm, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->af_small_dirty = false;
+    c->cx_hint = sm[7];
     if (sm[6]) {  // a walker ran out of line slots (short lines): the two-sweep schedule
         prof_collect(c);
         c->walk_overflowed = true;
@@ -1033,10 +1068,16 @@ static int compile_criteria(vcfxg_ctx *c, const vcfxg_criterion *crit, int n) {
     if (r) return r;
     c->crit_host.assign((const char *)dev.data(), sizeof(vcfxg::RfCrit) * (size_t)n);
     c->pool_host = pool;
-    if (n)
+    if (n && !(c->crit_dev_p == c->crit.p && c->crit_dev == c->crit_host)) {
         HIPCHK(c, hipMemcpyAsync(c->crit.p, c->crit_host.data(), c->crit_host.size(), hipMemcpyHostToDevice, c->stream));
-    if (!pool.empty())
+        c->crit_dev = c->crit_host;
+        c->crit_dev_p = c->crit.p;
+    }
+    if (!pool.empty() && !(c->pool_dev_p == c->pool.p && c->pool_dev == c->pool_host)) {
         HIPCHK(c, hipMemcpyAsync(c->pool.p, c->pool_host.data(), pool.size(), hipMemcpyHostToDevice, c->stream));
+        c->pool_dev = c->pool_host;
+        c->pool_dev_p = c->pool.p;
+    }
     return VCFXG_OK;
 }
 
@@ -1155,7 +1196,7 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
     if (!r && rf) r = ensure(c, c->rf_tabs, 16 * (cap + 1));
     if (!r) r = ensure(c, c->wk_count, 8 * (size_t)(nw + 1));
     if (!r) r = ensure(c, c->wk_offs, 8 * (size_t)(nw + 1));
-    if (!r) r = ensure(c, c->wk_small, 128);
+    if (!r) r = ensure(c, c->fq_small, 128);
     if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
     if (!r) r = ensure(c, c->status, cap + 1);
     if (!r && gq) r = ensure(c, c->af_meta, mb * (cap + 1));
@@ -1166,19 +1207,25 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
     if (gq) {
         if (!strict) gq_parse_query(query, qlen, qa, qb);
         c->query_host.assign(query, qlen);
-        if (qlen)
+        if (qlen && !(c->query_dev_p == c->query.p && c->query_dev == c->query_host)) {
             HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), qlen, hipMemcpyHostToDevice, c->stream));
+            c->query_dev = c->query_host;
+            c->query_dev_p = c->query.p;
+        }
     }
     const char *buf = P<char>(c->input);
-    unsigned *ovf = P<unsigned>(c->wk_small);
-    unsigned long long *cnt = P<unsigned long long>(c->counters);
+    r = ensure_sum_host(c);
+    if (r) return r;
+    unsigned *ovf = P<unsigned>(c->fq_small);
+    unsigned long long *cnt = P<unsigned long long>(c->fq_small) + 1;
     unsigned long long *gq_cnt = what == vcfxg::kFqBoth ? cnt + 4 : cnt;
     const int strip_cr = rf ? 1 : gq_strip_cr;  // the pipeline's query sees record_filter's output
     const int pool_len = (int)c->pool_host.size();
     const vcfxg::RfArgs ra{P<vcfxg::RfCrit>(c->crit), n, and_logic ? 1 : 0, P<char>(c->pool), pool_len};
-    HIPCHK(c, hipMemsetAsync(ovf, 0, 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(cnt, 0, 64, c->stream));
-    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->wk_count) + nw, 0, 8, c->stream));
+    // (k_fq_done zeroed the slot and the counters after the last call; k_fq_walk zeroes
+    // wk_count[nw], the scan's last entry)
+    if (c->fq_small_dirty) HIPCHK(c, hipMemsetAsync(c->fq_small.p, 0, 128, c->stream));
+    c->fq_small_dirty = true;  // until the call has synchronised
     prof_begin(c, "fq_walk");
     HIPCHK(c, vcfxg::launch_fq_walk(what, buf, lo, hi, C, strip_cr, c->hint_span, cap_w, ra, P<char>(c->query),
                                     (int)qlen, strict, qa, qb, P<uint64_t>(c->wk_le), P<uint8_t>(c->wk_status),
@@ -1196,20 +1243,22 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
                                            strip_cr ? VCFXG_MODE_FILE : VCFXG_MODE_STDIN, P<uint8_t>(c->status), cnt,
                                            c->stream));
     else
-        HIPCHK(c, vcfxg::launch_fq_finish(what, buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap,
-                                          ra, P<uint8_t>(c->status), c->af_meta.p, c->rf_tabs.p, cnt, gq_cnt,
-                                          c->stream));
+        // (a thread per line of the previous call, at most cap: the kernel grid-strides over the
+        // device count, so fewer threads than lines is still exact)
+        HIPCHK(c, vcfxg::launch_fq_finish(what, buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines),
+                                          c->fq_lines_hint ? std::min<uint64_t>(cap, c->fq_lines_hint) : cap, ra,
+                                          P<uint8_t>(c->status), c->af_meta.p, c->rf_tabs.p, cnt, gq_cnt, c->stream));
     if (gq && !nr)
         HIPCHK(c, vcfxg::launch_gq_complex(buf, lo, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap, strip_cr,
                                            P<char>(c->query), (int)qlen, strict, qa, qb, c->af_meta.p,
                                            P<uint8_t>(c->status), gq_cnt,
                                            what == vcfxg::kFqBoth ? P<uint8_t>(c->status) : nullptr, c->stream));
     prof_end(c, "fq_rest");
-    static thread_local uint64_t host[10];
-    HIPCHK(c, hipMemcpyAsync(host, cnt, 64, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(host + 8, c->d_nlines.p, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(host + 9, ovf, 8, hipMemcpyDeviceToHost, c->stream));
+    uint64_t *host = c->sum_host + 8;  // counters[0..7], lines, overflow (k_fq_done)
+    HIPCHK(c, vcfxg::launch_fq_done(cnt, P<uint64_t>(c->d_nlines), P<uint64_t>(c->fq_small), c->sum_dev + 8, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->fq_small_dirty = false;
+    c->fq_lines_hint = host[8];
     prof_collect(c);
     if (host[9]) {  // a walker ran out of line slots (short lines): index + the per-tool kernels
         c->walk_overflowed = true;
@@ -1785,17 +1834,19 @@ static int md_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     if (!r) r = ensure(c, c->wk_meta, mb * cap);
     if (!r) r = ensure(c, c->wk_count, 8 * (size_t)(nw + 1));
     if (!r) r = ensure(c, c->wk_offs, 8 * (size_t)(nw + 1));
-    if (!r) r = ensure(c, c->wk_small, 128);
+    if (!r) r = ensure(c, c->fq_small, 128);
+    if (!r) r = ensure_sum_host(c);
     if (!r) r = ensure(c, c->line_end, 8 * (cap + 1));
     if (!r) r = ensure(c, c->af_meta, mb * (cap + 1));
     if (!r) r = af_buffers(c, cap);
     if (r) return r;
     const char *buf = P<char>(c->input);
-    unsigned *ovf = P<unsigned>(c->wk_small);
+    // the filter / query walk's slot and counters (zeroed by k_fq_done after the last call)
+    unsigned *ovf = P<unsigned>(c->fq_small);
+    unsigned long long *cnt = P<unsigned long long>(c->fq_small) + 1;
     const vcfxg::RfArgs ra{nullptr, 0, 1, nullptr, 0};
-    HIPCHK(c, hipMemsetAsync(ovf, 0, 8, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
-    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->wk_count) + nw, 0, 8, c->stream));
+    if (c->fq_small_dirty) HIPCHK(c, hipMemsetAsync(c->fq_small.p, 0, 128, c->stream));
+    c->fq_small_dirty = true;
     prof_begin(c, "md_walk");
     HIPCHK(c, vcfxg::launch_fq_walk(vcfxg::kFqMD, buf, lo, hi, C, mode == VCFXG_MODE_FILE ? 1 : 0, c->hint_span, cap_w, ra,
                                     nullptr, 0, 0, -1, -1, P<uint64_t>(c->wk_le), P<uint8_t>(c->wk_status),
@@ -1810,13 +1861,12 @@ static int md_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
                                        c->stream));
     HIPCHK(c, vcfxg::launch_md_lines(buf, lo, (int64_t)c->n, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), cap,
                                      mode, P<uint8_t>(c->status), P<int32_t>(c->alt), P<int32_t>(c->tot),
-                                     P<unsigned long long>(c->counters), c->stream, 1));
+                                     cnt, c->stream, 1));
     prof_end(c, "md_rest");
-    static thread_local uint64_t h[5];
-    HIPCHK(c, hipMemcpyAsync(h, c->counters.p, 24, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(h + 3, c->d_nlines.p, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(h + 4, ovf, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, vcfxg::launch_fq_done(cnt, P<uint64_t>(c->d_nlines), P<uint64_t>(c->fq_small), c->sum_dev + 8, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->fq_small_dirty = false;
+    uint64_t h[5] = {c->sum_host[8], c->sum_host[9], c->sum_host[10], c->sum_host[16], c->sum_host[17]};
     prof_collect(c);
     if (h[4] & 0xFFFFFFFFu) {  // a walker ran out of line slots (short lines): no walk
         c->walk_overflowed = true;
@@ -1919,6 +1969,7 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
     if (r) return r;
     c->query_host.assign(rchrom ? rchrom : "", rlen);
     if (rlen)
+        c->query_dev_p = nullptr;
         HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), rlen, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->ld_G.p, 0xFF, (size_t)L * kpad + 64, c->stream));
     vcfxg::LdParseArgs a{n_samples, kpad, has_region, rstart, rend, (int64_t)rlen, P<char>(c->query), parse_mode};

@@ -222,6 +222,9 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
                                                            const DoseMeta *__restrict__ meta,
                                                            const uint64_t *__restrict__ off, char *__restrict__ out,
                                                            uint64_t cap, unsigned *__restrict__ bad) {
+    // kFmtNa: a wave-step's text (512 samples, at most 3 bytes each) composed in LDS
+    __shared__ __attribute__((aligned(16))) unsigned char na_tile[kMode == kFmtNa ? kDoseThreads / kWave : 1]
+                                                                 [kMode == kFmtNa ? 3 * 8 * kWave + 32 : 16];
     const uint64_t n_lines = *n_lines_p;
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
@@ -338,33 +341,77 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
             continue;
         }
         if (kMode == kFmtNa) {
-            // the fixed-stride layout: samples "a s b\t" on the 4-byte grid from S, the last
-            // without its tab; lane l of a wave-step takes 4 consecutive samples
+            // the fixed-stride layout with some "NA" (k_dose_len / the walk validated it: every
+            // allele a digit or '.'): lane c of a wave-step reads samples 8c..8c+7 as the plain
+            // rows do (36 bytes from the 4-aligned address, rotated by S mod 4); a sample is "NA"
+            // when an allele field of e = dword ^ "0 s 0 \t" is >= 10 ('.'), else its dosage is the
+            // number of non-zero allele fields.  The lanes' texts (2 or 3 bytes per sample) are
+            // placed by a wave scan of their lengths into the wave's LDS tile (offset = output
+            // offset - the 16 B boundary below the step's first byte) and the tile goes out as
+            // aligned 16 B stores -- byte stores only for its two partial blocks.
             const int64_t ns = (E - S + 1) / 4;
-            for (int64_t k0 = 0; k0 < ns; k0 += 4 * kWave) {
-                const int64_t k = k0 + 4 * lane();
-                int d[4];
-                uint32_t bytes = 0;
+            const int64_t nch = (ns + 7) / 8;
+            const uint32_t ib = (uint32_t)(S & 3);
+            const uint32_t exp = 0x09300030u | ((uint32_t)m.sep << 8);
+            unsigned char *tile = na_tile[threadIdx.x / kWave];
+            const uint64_t ob = (uint64_t)(o - out);
+            for (int64_t c0 = 0; c0 < nch; c0 += kWave) {
+                const int64_t c = c0 + lane(), k0 = 8 * c;
+                uint32_t na = 0, dg = 0, bytes = 0;  // bit t: sample k0 + t is "NA" / its dosage digit (2 bits)
+                const int rem = c < nch ? (int)std::min<int64_t>(ns - k0, 8) : 0;
+                if (rem > 0) {
+                    typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+                    const uint32_t *ip = reinterpret_cast<const uint32_t *>(buf + ((S + 4 * k0) & ~(int64_t)3));
+                    const u32x4a4 v0 = *reinterpret_cast<const u32x4a4 *>(ip), v1 = *reinterpret_cast<const u32x4a4 *>(ip + 4);
+                    const uint32_t w[9] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w, ip[8]};
 #pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    d[i] = 0;
-                    if (k + i < ns) {
-                        const int64_t p = S + 4 * (k + i);
-                        const uint32_t a = byte_at(buf, p), b = byte_at(buf, p + 2);
-                        d[i] = (is_digit(a) && is_digit(b)) ? (a != '0') + (b != '0') : -1;
-                        bytes += d[i] < 0 ? 3u : 2u;
+                    for (int t = 0; t < 8; t++) {
+                        const uint32_t f = (__builtin_amdgcn_alignbyte(w[t + 1], w[t], ib) ^ exp) & 0x00FF00FFu;
+                        const bool isna = ((f + 0x00F600F6u) & 0x01000100u) != 0u;  // an allele field >= 10: '.'
+                        const uint32_t d = __popc((f + 0x00FF00FFu) & 0x01000100u);
+                        if (t < rem) {
+                            na |= (isna ? 1u : 0u) << t;
+                            dg |= d << (2 * t);
+                            bytes += isna ? 3u : 2u;
+                        }
                     }
                 }
                 const uint32_t incl = wave_incl_scan(bytes);
-                uint64_t pos = run + incl - bytes;
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-                    if (k + i < ns) {
-                        const uint32_t nb = d[i] < 0 ? 3u : 2u;
-                        put_dose(o + pos, d[i], pos + nb == tot);
-                        pos += nb;
+                const uint32_t step = (uint32_t)wave_bcast(incl, kWave - 1);
+                const uint64_t sb = ob + run;  // the step's first output byte
+                const uint64_t tb = sb & ~15ull;
+                uint32_t q = (uint32_t)(sb - tb) + incl - bytes;  // this lane's tile offset
+                for (int t = 0; t < rem; t++) {
+                    const unsigned char sepc = k0 + t == ns - 1 ? '\n' : ',';
+                    if ((na >> t) & 1u) {
+                        tile[q] = 'N';
+                        tile[q + 1] = 'A';
+                        tile[q + 2] = sepc;
+                        q += 3;
+                    } else {
+                        tile[q] = (unsigned char)('0' + ((dg >> (2 * t)) & 3u));
+                        tile[q + 1] = sepc;
+                        q += 2;
                     }
-                run += wave_bcast(incl, kWave - 1);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint64_t se = sb + step;
+                const int nblk = (int)((se - tb + 15) >> 4);
+                for (int j = lane(); j < nblk; j += kWave) {
+                    const uint64_t gb = tb + 16u * (uint64_t)j;
+                    if (gb >= sb && gb + 16 <= se) {
+                        *reinterpret_cast<uint4 *>(out + gb) = reinterpret_cast<const uint4 *>(tile)[j];
+                    } else {
+                        const uint64_t b0 = gb > sb ? gb : sb, b1 = gb + 16 < se ? gb + 16 : se;
+                        for (uint64_t b = b0; b < b1; b++) out[b] = (char)tile[b - tb];
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                run += step;
             }
             continue;
         }

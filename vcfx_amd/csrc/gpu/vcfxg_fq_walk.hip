@@ -75,6 +75,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
                                                           uint64_t *__restrict__ wcount, unsigned *overflow) {
     __shared__ uint4 win[kWalkWaves][2][kWave];  // two window slots per wave (double buffer)
     const int wv = threadIdx.x / kWave;
+    if (blockIdx.x == 0 && threadIdx.x == 0) wcount[n_walkers] = 0;  // the scan's last entry (no memset)
     const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + wv);
     if (wk >= n_walkers) return;
     const int64_t cs = lo + wk * chunk;
@@ -425,6 +426,26 @@ hipError_t launch_fq_compact(int what, int64_t n_walkers, uint64_t cap_w, const 
     else
         hipLaunchKernelGGL((k_fq_compact<true, true>), dim3((unsigned)blocks), dim3(256), 0, s, n_walkers, cap_w, offs,
                            le_b, status_b, mb, tb, line_end, status, m, t, n_lines);
+    return hipGetLastError();
+}
+
+// the call's counters, line count and overflow flag into mapped host memory (out[0..7],
+// out[8], out[9]), each zeroed once read: the next call needs no memset or copy
+__global__ void k_fq_done(unsigned long long *cnt, const uint64_t *n_lines, uint64_t *ovf, uint64_t *out) {
+    const int t = threadIdx.x;
+    if (t < 8) {
+        out[t] = cnt[t];
+        cnt[t] = 0;
+    } else if (t == 8) {
+        out[8] = *n_lines;
+    } else if (t == 9) {
+        out[9] = *ovf;
+        *ovf = 0;
+    }
+}
+hipError_t launch_fq_done(unsigned long long *cnt, const uint64_t *n_lines, uint64_t *ovf, uint64_t *out,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(k_fq_done, dim3(1), dim3(64), 0, s, cnt, n_lines, ovf, out);
     return hipGetLastError();
 }
 

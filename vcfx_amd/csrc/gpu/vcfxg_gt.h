@@ -319,6 +319,125 @@ struct AfOp {
 };
 
 // ---------------------------------------------------------------------------------------
+// gt_first_af: gt_first for the allele counts, on per-byte flags instead of a loop over each
+// lane's sample starts.  Bytes are classified SWAR on the lane's 16 B and the 4 B after them
+// (bit 7 of each byte; every byte must be ASCII -- else the record goes to the exact path):
+// for a byte b < 0x80, (b ^ c) + 0x7F has bit 7 set iff b != c, and b + (0x80 - c) iff b >= c.
+// A sample start p (S, and the byte after a tab) is accepted when p+1 is '/' or '|', p+3 is
+// ':', a tab or the line's '\n', and p, p+2 are digits or '.': the quick GT c0 s c2, whose
+// tokens are c0 and c2 alone (letters and the like at p or p+2 go to the exact path, as do
+// CRLF line ends).  The flags of p+1..p+3 are lined up with p's by v_alignbyte over
+// neighbouring dwords; tot and alt are popcounts of the accepted starts' digit and
+// nonzero-digit flags at p and p+2.  Same contract as gt_first: the record end E (first '\n'
+// at or after S, else hi), pre(E) as soon as it is known, false (wave-uniform) -> the
+// caller's exact path; on true op.alt / op.tot hold the record's counts.
+// ---------------------------------------------------------------------------------------
+template <int kU, class Pre>
+__device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi, int strip_cr, AfOp &op, Pre pre,
+                            int64_t &E_out, uint8_t &cr_out) {
+    S = uniform64(S);
+    constexpr uint32_t M = 0x80808080u, K = 0x7F7F7F7Fu;
+    int64_t E = hi, ae = hi;
+    bool found = false;
+    uint32_t bad = 0, asc = 0, tot = 0, alt = 0;
+    uint32_t carry = 0;  // tab flags of the previous step's last lane (byte 3: the byte before this step)
+    const int64_t b0 = S & ~(int64_t)15;
+    const int lo16 = lane() * kBlockBytes;
+    for (int64_t w0 = b0; w0 < hi && !found; w0 += kU * kWaveStep) {
+        uint4 v[kU];
+        uint32_t x4[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {  // branch-free: lanes past hi re-read the last block
+            const int64_t blk = w0 + u * kWaveStep + lo16;
+            const int64_t bl = blk < hi ? blk : ((hi - 1) & ~(int64_t)15);
+            v[u] = load16(buf, bl);
+            x4[u] = load4(buf, bl + 16);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            if (found) break;
+            const int64_t ws = w0 + u * kWaveStep, blk = ws + lo16;
+            const uint32_t W[5] = {v[u].x, v[u].y, v[u].z, v[u].w, x4[u]};
+            asc |= W[0] | W[1] | W[2] | W[3] | W[4];
+            // ---- the record end: the first '\n' at or after S (the first step may hold bytes
+            // before S, the last lanes of the input's last step re-read its last block)
+            const bool first = ws == b0, edge = first || ws + kWaveStep > hi;  // wave-uniform
+            uint32_t nlm = 0;
+            if (edge) nlm = blk < hi ? eq_mask16(v[u], kRepNl) & range_mask16(blk, S, hi) : 0u;
+            else  // exact per byte whatever the bytes are (the ASCII shortcut below is not)
+                nlm = zero_bytes(W[0] ^ kRepNl) | zero_bytes(W[1] ^ kRepNl) | zero_bytes(W[2] ^ kRepNl) |
+                      zero_bytes(W[3] ^ kRepNl);
+            const uint64_t anyn = __ballot(nlm != 0u);
+            if (anyn) {
+                const int k = __builtin_ctzll(anyn);
+                if (!edge) nlm = eq_mask16(v[u], kRepNl);  // lane k's exact mask
+                E = uniform64(ws + 16 * k + __builtin_ctz((uint32_t)__shfl((int)nlm, k)));
+                found = true;
+                const uint32_t cr = strip_cr && E > S ? __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r' : 0u;
+                cr_out = (uint8_t)cr;
+                ae = E - cr;
+                pre(E);
+            }
+            // ---- sample starts: the byte after a tab (the byte before the lane's block: the
+            // previous lane's, or the previous step's last), S, and only inside [S, ae)
+            const uint32_t tab3 = ~((W[3] ^ kRepTab) + K);
+            const uint32_t up = (uint32_t)__shfl_up((int)tab3, 1);
+            uint32_t tprev = lane() ? up : carry;
+            carry = (uint32_t)__shfl((int)tab3, kWave - 1);
+            uint32_t rm = 0xFFFFu;
+            if (edge || found) {
+                rm = blk < hi ? range_mask16(blk, S, ae) : 0u;
+                rm |= ((S >= blk && S < blk + 16) ? 1u << (S - blk) : 0u) << 16;  // S: a start
+            }
+            // ---- dword by dword (classes of W[i] and W[i+1] live at a time): each start
+            // needs c1 separator, c3 terminator, c0 / c2 digit or '.'; then the counts
+            auto classes = [&](uint32_t x, uint32_t &tab, uint32_t &sep, uint32_t &trm, uint32_t &vv, uint32_t &dg,
+                               uint32_t &nz) {
+                const uint32_t nt = (x ^ kRepTab) + K, nn = (x ^ kRepNl) + K, nc = (x ^ kRepColon) + K;
+                tab = ~nt;
+                trm = ~(nt & nn & nc);
+                sep = ~(((x ^ 0x2F2F2F2Fu) + K) & ((x ^ 0x7C7C7C7Cu) + K));
+                const uint32_t g9 = x + 0x46464646u;  // >= ':'
+                dg = (x + 0x50505050u) & ~g9;         // '0'..'9'
+                nz = (x + 0x4F4F4F4Fu) & ~g9;         // '1'..'9'
+                vv = dg | ~((x ^ 0x2E2E2E2Eu) + K);
+            };
+            uint32_t tab0, sep0, trm0, v0, dg0, nz0;
+            classes(W[0], tab0, sep0, trm0, v0, dg0, nz0);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                uint32_t tab1, sep1, trm1, v1, dg1, nz1;
+                classes(W[i + 1], tab1, sep1, trm1, v1, dg1, nz1);
+                uint32_t st = __builtin_amdgcn_alignbyte(tab0, tprev, 3) & M;
+                if (edge || found)
+                    st = (st | nib_bytes((rm >> (16 + 4 * i)) & 0xFu)) & nib_bytes((rm >> (4 * i)) & 0xFu) & M;
+                const uint32_t s1 = __builtin_amdgcn_alignbyte(sep1, sep0, 1);
+                const uint32_t c3 = __builtin_amdgcn_alignbyte(trm1, trm0, 3);
+                const uint32_t v2 = __builtin_amdgcn_alignbyte(v1, v0, 2);
+                const uint32_t d2 = __builtin_amdgcn_alignbyte(dg1, dg0, 2);
+                const uint32_t n2 = __builtin_amdgcn_alignbyte(nz1, nz0, 2);
+                bad |= st & ~(s1 & c3 & v0 & v2);
+                tot += __popc(st & dg0) + __popc(st & d2);
+                alt += __popc(st & nz0) + __popc(st & n2);
+                tprev = tab0;
+                tab0 = tab1, sep0 = sep1, trm0 = trm1, v0 = v1, dg0 = dg1, nz0 = nz1;
+            }
+        }
+    }
+    if (!found) {
+        E = hi;
+        const uint32_t cr = strip_cr && E > S ? __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r' : 0u;
+        cr_out = (uint8_t)cr;
+        pre(E);
+    }
+    E_out = E;
+    if (__any((bad | (asc & M)) != 0u)) return false;
+    op.alt = wave_sum(alt);
+    op.tot = wave_sum(tot);
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------
 // af_fixed: gt_fast + AfOp (the same record test and the same counts) on the raw 16 B
 // blocks, without realigning them to the sample grid.  In a fixed-stride record every byte's
 // role -- allele, separator or tab -- is (offset - S) mod 4, so a raw aligned dword holds the

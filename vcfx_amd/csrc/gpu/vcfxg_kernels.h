@@ -72,7 +72,8 @@ hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk
 //                      added to their walker's total (counters as k_af_complex)
 //   launch_walker_scan one block: exclusive scans of the walkers' line counts and row bytes,
 //                      GT-line totals into counters[0..1], the line count to *n_lines and the
-//                      7-value call summary (lines, text bytes, counters[0..3], *fail)
+//                      7-value call summary (lines, text bytes, counters[0..3], *fail); with
+//                      reset: summary[7] = reset[1] (the leftover count), then reset[0..5] = 0
 //   launch_af_format_w one wave per walker region: rows into out (rows ending past cap skipped)
 hipError_t launch_af_cx(const char *buf, int mode, uint64_t cap_w, const uint64_t *list, const unsigned long long *list_n,
                         uint64_t list_cap, uint64_t list_cap_host, const uint64_t *wstart, const uint64_t *le_b,
@@ -84,7 +85,7 @@ constexpr int kWalkerScanBlock = 1024;
 hipError_t launch_walker_scan(int64_t nw, const uint64_t *wcount, const uint64_t *wtext, const uint32_t *wgt,
                               uint64_t *woff, uint64_t *wtoff, uint64_t *bpre_a, uint64_t *bpre_b, uint64_t *bsum,
                               unsigned *done, unsigned long long *counters, const unsigned *fail, uint64_t *n_lines,
-                              uint64_t *summary, hipStream_t s);
+                              uint64_t *summary, hipStream_t s, uint64_t *reset = nullptr);
 hipError_t launch_af_format_w(const char *buf, int mode, int64_t nw, uint64_t cap_w, const uint64_t *wcount,
                               const uint64_t *wtoff, const uint64_t *bpre_b, const uint64_t *wstart,
                               const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b, const uint32_t *rowpre_b,

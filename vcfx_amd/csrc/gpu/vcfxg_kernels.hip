@@ -831,7 +831,8 @@ __global__ __launch_bounds__(kWScan) void k_walker_scan(int64_t nw, const uint64
                                                         uint64_t *__restrict__ wtoff, uint64_t *bpre_a, uint64_t *bpre_b,
                                                         uint64_t *bsum, unsigned *done,
                                                         unsigned long long *counters, const unsigned *fail,
-                                                        uint64_t *n_lines, uint64_t *__restrict__ summary) {
+                                                        uint64_t *n_lines, uint64_t *__restrict__ summary,
+                                                        uint64_t *reset) {
     __shared__ uint64_t sa[kWScan / kWave], sb[kWScan / kWave];
     __shared__ bool last;
     const int t = threadIdx.x;
@@ -864,16 +865,26 @@ __global__ __launch_bounds__(kWScan) void k_walker_scan(int64_t nw, const uint64
     }
     __syncthreads();
     if (!last) return;
-    // the last block: prefix of the block totals (atomic loads: other CUs' stores)
-    if (t == 0) {
-        uint64_t ra = 0, rb = 0, G = 0;
-        for (int64_t k = 0; k < nb; k++) {
-            bpre_a[k] = ra;
-            bpre_b[k] = rb;
-            ra += __hip_atomic_load(&bsum[3 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            rb += __hip_atomic_load(&bsum[3 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            G += __hip_atomic_load(&bsum[3 * k + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the last block: prefix of the block totals (atomic loads: other CUs' stores), 64 blocks
+    // per step by wave 0 (a serial loop paid one L2 round trip per block)
+    if (t >= kWave) return;
+    uint64_t ra = 0, rb = 0, G = 0;
+    for (int64_t k0 = 0; k0 < nb; k0 += kWave) {
+        const int64_t k = k0 + lane();
+        const bool in = k < nb;
+        const uint64_t x = in ? __hip_atomic_load(&bsum[3 * k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0,
+                       y = in ? __hip_atomic_load(&bsum[3 * k + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0,
+                       z = in ? __hip_atomic_load(&bsum[3 * k + 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        const uint64_t xi = wave_incl_scan(x), yi = wave_incl_scan(y);
+        if (in) {
+            bpre_a[k] = ra + xi - x;
+            bpre_b[k] = rb + yi - y;
         }
+        ra += wave_bcast(xi, kWave - 1);
+        rb += wave_bcast(yi, kWave - 1);
+        G += wave_sum(z);
+    }
+    if (lane() == 0) {
         bpre_a[nb] = ra;
         bpre_b[nb] = rb;
         if (nw % kWScan == 0) {  // no thread stood at w == nw
@@ -889,23 +900,48 @@ __global__ __launch_bounds__(kWScan) void k_walker_scan(int64_t nw, const uint64
         summary[1] = rb;
         for (int k = 0; k < 4; k++) summary[2 + k] = counters[k];
         summary[6] = *fail;
+        if (reset) {  // the call's flags and counters, zeroed once read: no memset before the next call
+            summary[7] = reset[1];
+            for (int k = 0; k < 6; k++) reset[k] = 0;
+        }
     }
 }
 
 // one wave per walker region: row offsets = the walker's text offset + a wave scan of its
-// rows' lengths; each lane writes its line's row (rows ending past cap are skipped)
-__global__ __launch_bounds__(256) void k_af_format_w(const char *__restrict__ buf, int mode, int64_t nw, uint64_t cap_w,
-                                                     const uint64_t *__restrict__ wcount,
-                                                     const uint64_t *__restrict__ wtoff,
-                                                     const uint64_t *__restrict__ bpre_b,
-                                                     const uint64_t *__restrict__ wstart,
-                                                     const uint64_t *__restrict__ le_b, const int32_t *__restrict__ alt_b,
-                                                     const int32_t *__restrict__ tot_b,
-                                                     const uint32_t *__restrict__ rowpre_b,
-                                                     const uint8_t *__restrict__ status_b, char *__restrict__ out,
-                                                     uint64_t cap) {
-    const int64_t nwv = (int64_t)gridDim.x * (256 / kWave);
-    for (int64_t w = (int64_t)blockIdx.x * (256 / kWave) + threadIdx.x / kWave; w < nw; w += nwv) {
+// rows' lengths.  Up to 64 rows at a time are composed in the wave's LDS tile: each lane brings
+// its row's CHROM..ALT bytes as three 16 B loads (one load instruction per 16 B of a row, not
+// one per byte) through a per-lane LDS stage, places them and the frequency at the row's tile
+// offset (tile offset = text offset - the 16 B boundary below the first row), and the wave
+// writes the tile as aligned 16 B stores -- byte stores only for the two blocks it shares with
+// the neighbouring walkers.  Rows past cap, tiles over kFmtTile bytes and heads longer than
+// the three loads fall back to the row-per-lane byte path.
+constexpr int kFmtWaves = 4, kFmtTile = 4096, kFmtStage = 48;
+__device__ __forceinline__ void af_freq_text(int mode, int32_t a, int32_t t, uint32_t &lo, uint32_t &hi) {
+    const double f = t > 0 ? __ddiv_rn((double)a, (double)t) : 0.0;
+    const uint32_t k4 = mode == 0 ? fixed4_mmap(f) : fixed4_printf(f);
+    const uint32_t ip = k4 / 10000u, fp = k4 % 10000u;
+    // "i.dddd\n": bytes 0..3 in lo, 4..6 in hi
+    lo = ('0' + ip) | ((uint32_t)'.' << 8) | (('0' + fp / 1000u) << 16) | (('0' + (fp / 100u) % 10u) << 24);
+    hi = ('0' + (fp / 10u) % 10u) | (('0' + fp % 10u) << 8) | ((uint32_t)'\n' << 16);
+}
+__global__ __launch_bounds__(kFmtWaves *kWave) void k_af_format_w(const char *__restrict__ buf, int mode, int64_t nw,
+                                                                   uint64_t cap_w, const uint64_t *__restrict__ wcount,
+                                                                   const uint64_t *__restrict__ wtoff,
+                                                                   const uint64_t *__restrict__ bpre_b,
+                                                                   const uint64_t *__restrict__ wstart,
+                                                                   const uint64_t *__restrict__ le_b,
+                                                                   const int32_t *__restrict__ alt_b,
+                                                                   const int32_t *__restrict__ tot_b,
+                                                                   const uint32_t *__restrict__ rowpre_b,
+                                                                   const uint8_t *__restrict__ status_b,
+                                                                   char *__restrict__ out, uint64_t cap) {
+    __shared__ uint4 tile_s[kFmtWaves][kFmtTile / 16];
+    __shared__ uint4 stage_s[kFmtWaves][kWave * kFmtStage / 16];
+    const int wv = threadIdx.x / kWave;
+    unsigned char *tile = reinterpret_cast<unsigned char *>(tile_s[wv]);
+    const unsigned char *stage = reinterpret_cast<const unsigned char *>(stage_s[wv]) + kFmtStage * lane();
+    const int64_t nwv = (int64_t)gridDim.x * kFmtWaves;
+    for (int64_t w = (int64_t)blockIdx.x * kFmtWaves + wv; w < nw; w += nwv) {
         const uint64_t n = wcount[w], s0 = (uint64_t)w * cap_w;
         uint64_t run = wtoff[w] + bpre_b[w / kWScan];
         for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
@@ -915,23 +951,65 @@ __global__ __launch_bounds__(256) void k_af_format_w(const char *__restrict__ bu
             const uint32_t len = in && status_b[sl] == 1 ? pl + 7u : 0u;
             const uint32_t incl = wave_incl_scan(len);
             const uint64_t off = run + incl - len;
-            run += wave_bcast(incl, kWave - 1);
-            if (!len || off + len > cap) continue;
-            const int64_t ls = i ? (int64_t)le_b[sl - 1] + 1 : (int64_t)wstart[w];
-            char *o = out + off;
-            for (uint32_t k = 0; k < pl; k++) o[k] = buf[ls + k];
-            const int a = alt_b[sl], t = tot_b[sl];
-            const double f = t > 0 ? __ddiv_rn((double)a, (double)t) : 0.0;
-            const uint32_t k4 = mode == 0 ? fixed4_mmap(f) : fixed4_printf(f);
-            const uint32_t ip = k4 / 10000u, fp = k4 % 10000u;
-            o += pl;
-            o[0] = (char)('0' + ip);
-            o[1] = '.';
-            o[2] = (char)('0' + fp / 1000u);
-            o[3] = (char)('0' + (fp / 100u) % 10u);
-            o[4] = (char)('0' + (fp / 10u) % 10u);
-            o[5] = (char)('0' + fp % 10u);
-            o[6] = '\n';
+            const uint64_t end = run + wave_bcast(incl, kWave - 1);
+            const int64_t ls = len ? (i ? (int64_t)le_b[sl - 1] + 1 : (int64_t)wstart[w]) : 0;
+            uint32_t flo = 0, fhi = 0;
+            if (len) af_freq_text(mode, alt_b[sl], tot_b[sl], flo, fhi);
+            const uint64_t tb = run & ~(uint64_t)15;
+            if (end == run) continue;
+            if (end > cap || end - tb > (uint64_t)kFmtTile) {  // row per lane, byte stores
+                if (len && off + len <= cap) {
+                    char *o = out + off;
+                    for (uint32_t k = 0; k < pl; k++) o[k] = buf[ls + k];
+                    for (int k = 0; k < 7; k++) o[pl + k] = (char)((k < 4 ? flo >> (8 * k) : fhi >> (8 * (k - 4))) & 0xFFu);
+                }
+                run = end;
+                continue;
+            }
+            // this lane's CHROM..ALT bytes: [ls, ls + pl) inside the 48 B from a16 (else bytes)
+            const int64_t a16 = ls & ~(int64_t)15;
+            const int sh = (int)(ls - a16);
+            const bool wide = len && sh + (int)pl <= kFmtStage;
+            if (wide) {
+                const uint4 q0 = load16(buf, a16), q1 = load16(buf, a16 + 16), q2 = load16(buf, a16 + 32);
+                uint4 *st = const_cast<uint4 *>(reinterpret_cast<const uint4 *>(stage));
+                st[0] = q0;
+                st[1] = q1;
+                st[2] = q2;
+            }
+            unsigned char *o = tile + (off - tb);
+            if (len) {
+                if (wide)
+                    for (uint32_t k = 0; k < pl; k++) o[k] = stage[sh + k];
+                else
+                    for (uint32_t k = 0; k < pl; k++) o[k] = (unsigned char)buf[ls + k];
+                o += pl;
+                o[0] = (unsigned char)flo;
+                o[1] = (unsigned char)(flo >> 8);
+                o[2] = (unsigned char)(flo >> 16);
+                o[3] = (unsigned char)(flo >> 24);
+                o[4] = (unsigned char)fhi;
+                o[5] = (unsigned char)(fhi >> 8);
+                o[6] = (unsigned char)(fhi >> 16);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // the tile [tb, end) as 16 B blocks; the first and last may hold other walkers' bytes
+            const int nblk = (int)((end - tb + 15) >> 4);
+            for (int j = lane(); j < nblk; j += kWave) {
+                const uint64_t gb = tb + 16u * (uint64_t)j;
+                if (gb >= run && gb + 16 <= end) {
+                    *reinterpret_cast<uint4 *>(out + gb) = tile_s[wv][j];
+                } else {
+                    const uint64_t b0 = gb > run ? gb : run, b1 = gb + 16 < end ? gb + 16 : end;
+                    for (uint64_t b = b0; b < b1; b++) out[b] = (char)tile[b - tb];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            run = end;
         }
     }
 }
@@ -1126,10 +1204,10 @@ hipError_t launch_af_cx(const char *buf, int mode, uint64_t cap_w, const uint64_
 hipError_t launch_walker_scan(int64_t nw, const uint64_t *wcount, const uint64_t *wtext, const uint32_t *wgt,
                               uint64_t *woff, uint64_t *wtoff, uint64_t *bpre_a, uint64_t *bpre_b, uint64_t *bsum,
                               unsigned *done, unsigned long long *counters, const unsigned *fail, uint64_t *n_lines,
-                              uint64_t *summary, hipStream_t s) {
+                              uint64_t *summary, hipStream_t s, uint64_t *reset) {
     const int64_t nb = std::max<int64_t>((nw + kWScan - 1) / kWScan, 1);
     hipLaunchKernelGGL(k_walker_scan, dim3((unsigned)nb), dim3(kWScan), 0, s, nw, wcount, wtext, wgt, woff, wtoff,
-                       bpre_a, bpre_b, bsum, done, counters, fail, n_lines, summary);
+                       bpre_a, bpre_b, bsum, done, counters, fail, n_lines, summary, reset);
     return hipGetLastError();
 }
 hipError_t launch_af_format_w(const char *buf, int mode, int64_t nw, uint64_t cap_w, const uint64_t *wcount,
@@ -1137,7 +1215,7 @@ hipError_t launch_af_format_w(const char *buf, int mode, int64_t nw, uint64_t ca
                               const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b, const uint32_t *rowpre_b,
                               const uint8_t *status_b, char *out, uint64_t cap, hipStream_t s) {
     if (nw <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_af_format_w, dim3(grid_for(nw, 256 / kWave, 16384)), dim3(256), 0, s, buf, mode, nw, cap_w,
+    hipLaunchKernelGGL(k_af_format_w, dim3(grid_for(nw, kFmtWaves, 16384)), dim3(kFmtWaves * kWave), 0, s, buf, mode, nw, cap_w,
                        wcount, wtoff, bpre_b, wstart, le_b, alt_b, tot_b, rowpre_b, status_b, out, cap);
     return hipGetLastError();
 }

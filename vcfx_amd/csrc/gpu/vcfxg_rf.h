@@ -150,6 +150,10 @@ hipError_t launch_fq_walk(int what, const char *buf, int64_t lo, int64_t hi, int
 hipError_t launch_fq_compact(int what, int64_t n_walkers, uint64_t cap_w, const uint64_t *offs, const uint64_t *le_b,
                              const uint8_t *status_b, const void *meta_b, const void *tabs_b, uint64_t *line_end,
                              uint8_t *status, void *meta, void *tabs, uint64_t *n_lines, hipStream_t s);
+// k_fq_done: counters [0..7], *n_lines and the 8-byte overflow slot into out[0..9] (mapped
+// host memory), the counters and the slot zeroed after being read
+hipError_t launch_fq_done(unsigned long long *cnt, const uint64_t *n_lines, uint64_t *ovf, uint64_t *out,
+                          hipStream_t s);
 hipError_t launch_fq_finish(int what, const char *buf, int64_t data_start, const uint64_t *line_end,
                             const uint64_t *n_lines_dev, uint64_t n_lines_host, const RfArgs &rf, uint8_t *status,
                             void *meta, const void *tabs, unsigned long long *rf_cnt, unsigned long long *gq_cnt,
