@@ -124,6 +124,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     uint8_t cr_prev = 0;   // and the '\r' state of that record
     uint64_t n = 0;
     uint32_t ngt = 0, ngf = 0;  // GT-first lines; of them, swept whole by gt_first (kGF)
+    bool dirty = false;         // AfOp staged rows: some row of this walker is not in its stage
     const uint64_t base = (uint64_t)wk * cap_w;
     // per-line results held by lane (n & 63), written out 64 lines at a time (no stores --
     // and no waits for their completion -- on the per-record path)
@@ -351,6 +352,29 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             r_pre = rowpre;
             r_k = (uint32_t)kind | ((uint32_t)sep << 8) | ((uint32_t)cr << 16) | ((uint32_t)st << 24);
         }
+        if constexpr (std::is_same<Op, AfOp>::value) {
+            // the row's text into the walker's stage (lanes = bytes): CHROM..ALT and its tab from
+            // the head window, which still holds the line (the next window went to the other slot),
+            // then the frequency; a line left to k_af_cx (or a stage too small) marks the walker
+            if (tail.stage) {
+                if (kind == kMetaGt && ok && wtext + rowpre + 7u <= tail.stage_cap) {
+                    uint32_t flo, fhi;
+                    af_freq_text(mode, (int32_t)alt, (int32_t)tot, flo, fhi);
+                    char *dst = tail.stage + (uint64_t)wk * tail.stage_cap + wtext;
+                    const unsigned char *src = reinterpret_cast<const unsigned char *>(cw) + (L - A);
+                    for (uint32_t j0 = 0; j0 < rowpre + 7u; j0 += kWave) {
+                        const uint32_t j = j0 + (uint32_t)lane();
+                        if (j < rowpre) dst[j] = (char)src[j];
+                        else if (j < rowpre + 7u) {
+                            const uint32_t q = j - rowpre;
+                            dst[j] = (char)((q < 4u ? flo >> (8u * q) : fhi >> (8u * (q - 4u))) & 0xFFu);
+                        }
+                    }
+                } else if (kind == kMetaGt || kind == kMetaFull) {
+                    dirty = true;
+                }
+            }
+        }
         ngt += kind == kMetaGt ? 1u : 0u;
         if constexpr (kGF) ngf += gf && kind == kMetaGt && ok ? 1u : 0u;
         if (tail.wtext) {
@@ -378,6 +402,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             tail.wstart[wk] = (uint64_t)L0;
         }
         wgt[wk] = ngt | (ngf << 16);
+        if (tail.wdirty) tail.wdirty[wk] = dirty || n >= cap_w ? 1 : 0;
     }
 }
 

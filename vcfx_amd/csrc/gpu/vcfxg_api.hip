@@ -74,6 +74,7 @@ struct vcfxg_ctx {
     // same kernel writes straight into mapped host memory (no copy before the synchronisation)
     DevBuf af_small;
     bool af_small_dirty = true;
+    DevBuf wk_stage, wk_dirty;  // AF walk: each walker's rows as text (kStageCap bytes), its clean flag
     uint64_t *sum_host = nullptr, *sum_dev = nullptr;
     uint64_t cx_hint = ~0ull;  // leftover lines of the previous AF walk (sizes k_af_cx's grid)
     // filter / query walk: overflow slot + 8 counters, zeroed by k_fq_done after each call
@@ -300,6 +301,8 @@ void vcfxg_close(vcfxg_ctx *c) {
                       &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
         if (b->p) (void)hipFree(b->p);
     if (c->af_small.p) (void)hipFree(c->af_small.p);
+    if (c->wk_stage.p) (void)hipFree(c->wk_stage.p);
+    if (c->wk_dirty.p) (void)hipFree(c->wk_dirty.p);
     if (c->fq_small.p) (void)hipFree(c->fq_small.p);
     if (c->sum_host) (void)hipHostFree(c->sum_host);
     for (auto &pe : c->ingest_ev) (void)hipEventDestroy(pe.second);
@@ -754,6 +757,11 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     const int64_t nbs = (nw + vcfxg::kWalkerScanBlock - 1) / vcfxg::kWalkerScanBlock;
     if (!r) r = ensure(c, c->wk_bs, 8 * (size_t)(5 * nbs + 4));
     if (!r) r = ensure(c, c->af_small, 128);
+    // a walker's rows as text: ~ 13 rows x 31 B on the config 2 shard; a walker whose rows
+    // outgrow its stage is formatted from the arrays instead
+    constexpr uint32_t kStageCap = 2048;
+    if (!r) r = ensure(c, c->wk_stage, (size_t)kStageCap * (size_t)nw);
+    if (!r) r = ensure(c, c->wk_dirty, (size_t)nw);
     if (r) return r;
     r = ensure_sum_host(c);
     if (r) return r;
@@ -773,6 +781,9 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     tail.cx_list = P<uint64_t>(c->wk_cx);
     tail.cx_n = cx_n;
     tail.cx_cap = cap;
+    tail.stage = P<char>(c->wk_stage);
+    tail.stage_cap = kStageCap;
+    tail.wdirty = P<uint8_t>(c->wk_dirty);
     prof_begin(c, "af_walk");
     HIPCHK(c, vcfxg::launch_af_walk(buf, lo, hi, C, mode, c->hint_span, cap_w, P<uint64_t>(c->wk_le),
                                     P<int32_t>(c->wk_alt), P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre),
@@ -803,7 +814,7 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
     HIPCHK(c, vcfxg::launch_af_format_w(buf, mode, nw, cap_w, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_toff),
                                         bpre_b, tail.wstart, P<uint64_t>(c->wk_le), P<int32_t>(c->wk_alt),
                                         P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre), P<uint8_t>(c->wk_status),
-                                        P<char>(c->text), tcap, c->stream));
+                                        P<char>(c->text), tcap, c->stream, &tail));
     prof_end(c, "af_format");
     // (the leftover list holds every slot at most once: it cannot overflow its capacity)
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -823,7 +834,7 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
         HIPCHK(c, vcfxg::launch_af_format_w(buf, mode, nw, cap_w, P<uint64_t>(c->wk_count), P<uint64_t>(c->wk_toff),
                                             bpre_b, tail.wstart, P<uint64_t>(c->wk_le), P<int32_t>(c->wk_alt),
                                             P<int32_t>(c->wk_tot), P<uint32_t>(c->wk_rowpre),
-                                            P<uint8_t>(c->wk_status), P<char>(c->text), ~0ull, c->stream));
+                                            P<uint8_t>(c->wk_status), P<char>(c->text), ~0ull, c->stream, &tail));
         prof_end(c, "af_format");
     }
     prof_collect(c);

@@ -318,6 +318,40 @@ struct AfOp {
     }
 };
 
+// the row's frequency text (VCFX_allele_freq_calc.cpp: writeDouble4 in file mode, printf "%.4f"
+// on stdin) -- shared by the walk's staged rows and k_af_format_w
+// writeDouble4 (VCFX_allele_freq_calc.cpp:119-143): (ull)(v*10000.0+0.5), no FMA contraction
+__device__ __forceinline__ uint32_t fixed4_mmap(double v) {
+    double sc = __dadd_rn(__dmul_rn(v, 10000.0), 0.5);
+    return (uint32_t)(unsigned long long)sc;
+}
+// printf("%.4f") of v in [0, 1]: exact binary value, round half to even (glibc)
+__device__ __forceinline__ uint32_t fixed4_printf(double v) {
+    if (v == 0.0) return 0u;
+    uint64_t bits = __double_as_longlong(v);
+    int ex = (int)((bits >> 52) & 0x7FF);
+    uint64_t m = bits & ((1ull << 52) - 1);
+    int q;  // v = m * 2^-q
+    if (ex == 0) q = 1074;
+    else { m |= 1ull << 52; q = 1075 - ex; }
+    if (q <= 0) return 10000u * (uint32_t)(m << -q);  // v >= 2^52: not reachable for freqs
+    unsigned __int128 num = (unsigned __int128)m * 10000u;
+    if (q >= 100) return 0u;
+    unsigned __int128 k = num >> q;
+    unsigned __int128 rem = num - (k << q);
+    unsigned __int128 half = (unsigned __int128)1 << (q - 1);
+    if (rem > half || (rem == half && (k & 1))) k += 1;
+    return (uint32_t)k;
+}
+
+__device__ __forceinline__ void af_freq_text(int mode, int32_t a, int32_t t, uint32_t &lo, uint32_t &hi) {
+    const double f = t > 0 ? __ddiv_rn((double)a, (double)t) : 0.0;
+    const uint32_t k4 = mode == 0 ? fixed4_mmap(f) : fixed4_printf(f);
+    const uint32_t ip = k4 / 10000u, fp = k4 % 10000u;
+    // "i.dddd\n": bytes 0..3 in lo, 4..6 in hi
+    lo = ('0' + ip) | ((uint32_t)'.' << 8) | (('0' + fp / 1000u) << 16) | (('0' + (fp / 100u) % 10u) << 24);
+    hi = ('0' + (fp / 10u) % 10u) | (('0' + fp % 10u) << 8) | ((uint32_t)'\n' << 16);
+}
 // ---------------------------------------------------------------------------------------
 // gt_first_af: gt_first for the allele counts, on per-byte flags instead of a loop over each
 // lane's sample starts.  Bytes are classified SWAR on the lane's 16 B and the 4 B after them

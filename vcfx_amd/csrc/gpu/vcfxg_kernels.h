@@ -61,6 +61,12 @@ struct WalkTail {
     uint64_t *cx_list = nullptr;
     unsigned long long *cx_n = nullptr;
     uint64_t cx_cap = 0;
+    // AF: each walker's rows as text, composed by the walk itself into its stage_cap bytes of
+    // stage (k_af_format_w then copies them out whole); wdirty[w] = 1 when the walker left a
+    // line to k_af_cx or its rows outgrew its stage (its rows are formatted from the arrays)
+    char *stage = nullptr;
+    uint32_t stage_cap = 0;
+    uint8_t *wdirty = nullptr;
 };
 hipError_t launch_af_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int mode, int64_t span0,
                           uint64_t cap_w, uint64_t *le_b, int32_t *alt_b, int32_t *tot_b, uint32_t *rowpre_b,
@@ -89,7 +95,7 @@ hipError_t launch_walker_scan(int64_t nw, const uint64_t *wcount, const uint64_t
 hipError_t launch_af_format_w(const char *buf, int mode, int64_t nw, uint64_t cap_w, const uint64_t *wcount,
                               const uint64_t *wtoff, const uint64_t *bpre_b, const uint64_t *wstart,
                               const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b, const uint32_t *rowpre_b,
-                              const uint8_t *status_b, char *out, uint64_t cap, hipStream_t s);
+                              const uint8_t *status_b, char *out, uint64_t cap, hipStream_t s, const WalkTail *tail = nullptr);
 hipError_t launch_walk_compact(int64_t n_walkers, uint64_t cap_w, const uint64_t *offs, const uint32_t *wgt,
                                const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b,
                                const uint32_t *rowpre_b, const uint8_t *status_b, const void *meta_b,

@@ -683,30 +683,6 @@ __global__ void k_af_rowlen(const uint32_t *__restrict__ rowpre, const uint8_t *
         len[i] = status[i] == 1 ? (uint64_t)rowpre[i] + 7u : 0u;
 }
 
-// writeDouble4 (VCFX_allele_freq_calc.cpp:119-143): (ull)(v*10000.0+0.5), no FMA contraction
-__device__ __forceinline__ uint32_t fixed4_mmap(double v) {
-    double sc = __dadd_rn(__dmul_rn(v, 10000.0), 0.5);
-    return (uint32_t)(unsigned long long)sc;
-}
-// printf("%.4f") of v in [0, 1]: exact binary value, round half to even (glibc)
-__device__ __forceinline__ uint32_t fixed4_printf(double v) {
-    if (v == 0.0) return 0u;
-    uint64_t bits = __double_as_longlong(v);
-    int ex = (int)((bits >> 52) & 0x7FF);
-    uint64_t m = bits & ((1ull << 52) - 1);
-    int q;  // v = m * 2^-q
-    if (ex == 0) q = 1074;
-    else { m |= 1ull << 52; q = 1075 - ex; }
-    if (q <= 0) return 10000u * (uint32_t)(m << -q);  // v >= 2^52: not reachable for freqs
-    unsigned __int128 num = (unsigned __int128)m * 10000u;
-    if (q >= 100) return 0u;
-    unsigned __int128 k = num >> q;
-    unsigned __int128 rem = num - (k << q);
-    unsigned __int128 half = (unsigned __int128)1 << (q - 1);
-    if (rem > half || (rem == half && (k & 1))) k += 1;
-    return (uint32_t)k;
-}
-
 __global__ void k_af_format(const char *__restrict__ buf, int64_t data_start, const uint64_t *__restrict__ line_end,
                             const uint64_t *n_lines_p, int mode, const int32_t *__restrict__ alt,
                             const int32_t *__restrict__ tot, const uint32_t *__restrict__ rowpre,
@@ -907,23 +883,13 @@ __global__ __launch_bounds__(kWScan) void k_walker_scan(int64_t nw, const uint64
     }
 }
 
-// one wave per walker region: row offsets = the walker's text offset + a wave scan of its
-// rows' lengths.  Up to 64 rows at a time are composed in the wave's LDS tile: each lane brings
-// its row's CHROM..ALT bytes as three 16 B loads (one load instruction per 16 B of a row, not
-// one per byte) through a per-lane LDS stage, places them and the frequency at the row's tile
-// offset (tile offset = text offset - the 16 B boundary below the first row), and the wave
-// writes the tile as aligned 16 B stores -- byte stores only for the two blocks it shares with
-// the neighbouring walkers.  Rows past cap, tiles over kFmtTile bytes and heads longer than
-// the three loads fall back to the row-per-lane byte path.
-constexpr int kFmtWaves = 4, kFmtTile = 4096, kFmtStage = 48;
-__device__ __forceinline__ void af_freq_text(int mode, int32_t a, int32_t t, uint32_t &lo, uint32_t &hi) {
-    const double f = t > 0 ? __ddiv_rn((double)a, (double)t) : 0.0;
-    const uint32_t k4 = mode == 0 ? fixed4_mmap(f) : fixed4_printf(f);
-    const uint32_t ip = k4 / 10000u, fp = k4 % 10000u;
-    // "i.dddd\n": bytes 0..3 in lo, 4..6 in hi
-    lo = ('0' + ip) | ((uint32_t)'.' << 8) | (('0' + fp / 1000u) << 16) | (('0' + (fp / 100u) % 10u) << 24);
-    hi = ('0' + (fp / 10u) % 10u) | (('0' + fp % 10u) << 8) | ((uint32_t)'\n' << 16);
-}
+// one wave per walker region.  A clean walker (the walk composed every row of it into its
+// stage: wdirty[w] == 0) is copied out whole (its text, usually a
+// few hundred bytes, from its stage to its text offset): loads issued 4 x 64 bytes at a time,
+// then the stores.  Any other walker: row offsets = the walker's text offset + a wave scan of
+// its rows' lengths, each lane writes its line's row.  Rows / walkers ending past cap are
+// skipped (the host writes all again once the text has grown).
+constexpr int kFmtWaves = 4;
 __global__ __launch_bounds__(kFmtWaves *kWave) void k_af_format_w(const char *__restrict__ buf, int mode, int64_t nw,
                                                                    uint64_t cap_w, const uint64_t *__restrict__ wcount,
                                                                    const uint64_t *__restrict__ wtoff,
@@ -934,16 +900,34 @@ __global__ __launch_bounds__(kFmtWaves *kWave) void k_af_format_w(const char *__
                                                                    const int32_t *__restrict__ tot_b,
                                                                    const uint32_t *__restrict__ rowpre_b,
                                                                    const uint8_t *__restrict__ status_b,
-                                                                   char *__restrict__ out, uint64_t cap) {
-    __shared__ uint4 tile_s[kFmtWaves][kFmtTile / 16];
-    __shared__ uint4 stage_s[kFmtWaves][kWave * kFmtStage / 16];
-    const int wv = threadIdx.x / kWave;
-    unsigned char *tile = reinterpret_cast<unsigned char *>(tile_s[wv]);
-    const unsigned char *stage = reinterpret_cast<const unsigned char *>(stage_s[wv]) + kFmtStage * lane();
+                                                                   char *__restrict__ out, uint64_t cap,
+                                                                   const char *__restrict__ stage, uint32_t stage_cap,
+                                                                   const uint8_t *__restrict__ wdirty,
+                                                                   const uint64_t *__restrict__ wtext) {
     const int64_t nwv = (int64_t)gridDim.x * kFmtWaves;
-    for (int64_t w = (int64_t)blockIdx.x * kFmtWaves + wv; w < nw; w += nwv) {
-        const uint64_t n = wcount[w], s0 = (uint64_t)w * cap_w;
+    for (int64_t w = (int64_t)blockIdx.x * kFmtWaves + threadIdx.x / kWave; w < nw; w += nwv) {
         uint64_t run = wtoff[w] + bpre_b[w / kWScan];
+        if (stage && !wdirty[w]) {
+            const uint64_t len = wtext[w];
+            if (run + len > cap) continue;
+            const char *__restrict__ src = stage + (uint64_t)w * stage_cap;
+            char *__restrict__ dst = out + run;
+            for (uint64_t j0 = 0; j0 < len; j0 += 4 * kWave) {
+                char b[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint64_t j = j0 + u * kWave + lane();
+                    b[u] = j < len ? src[j] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint64_t j = j0 + u * kWave + lane();
+                    if (j < len) dst[j] = b[u];
+                }
+            }
+            continue;
+        }
+        const uint64_t n = wcount[w], s0 = (uint64_t)w * cap_w;
         for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
             const uint64_t i = i0 + lane(), sl = s0 + i;
             const bool in = i < n;
@@ -951,65 +935,16 @@ __global__ __launch_bounds__(kFmtWaves *kWave) void k_af_format_w(const char *__
             const uint32_t len = in && status_b[sl] == 1 ? pl + 7u : 0u;
             const uint32_t incl = wave_incl_scan(len);
             const uint64_t off = run + incl - len;
-            const uint64_t end = run + wave_bcast(incl, kWave - 1);
-            const int64_t ls = len ? (i ? (int64_t)le_b[sl - 1] + 1 : (int64_t)wstart[w]) : 0;
-            uint32_t flo = 0, fhi = 0;
-            if (len) af_freq_text(mode, alt_b[sl], tot_b[sl], flo, fhi);
-            const uint64_t tb = run & ~(uint64_t)15;
-            if (end == run) continue;
-            if (end > cap || end - tb > (uint64_t)kFmtTile) {  // row per lane, byte stores
-                if (len && off + len <= cap) {
-                    char *o = out + off;
-                    for (uint32_t k = 0; k < pl; k++) o[k] = buf[ls + k];
-                    for (int k = 0; k < 7; k++) o[pl + k] = (char)((k < 4 ? flo >> (8 * k) : fhi >> (8 * (k - 4))) & 0xFFu);
-                }
-                run = end;
-                continue;
-            }
-            // this lane's CHROM..ALT bytes: [ls, ls + pl) inside the 48 B from a16 (else bytes)
-            const int64_t a16 = ls & ~(int64_t)15;
-            const int sh = (int)(ls - a16);
-            const bool wide = len && sh + (int)pl <= kFmtStage;
-            if (wide) {
-                const uint4 q0 = load16(buf, a16), q1 = load16(buf, a16 + 16), q2 = load16(buf, a16 + 32);
-                uint4 *st = const_cast<uint4 *>(reinterpret_cast<const uint4 *>(stage));
-                st[0] = q0;
-                st[1] = q1;
-                st[2] = q2;
-            }
-            unsigned char *o = tile + (off - tb);
-            if (len) {
-                if (wide)
-                    for (uint32_t k = 0; k < pl; k++) o[k] = stage[sh + k];
-                else
-                    for (uint32_t k = 0; k < pl; k++) o[k] = (unsigned char)buf[ls + k];
-                o += pl;
-                o[0] = (unsigned char)flo;
-                o[1] = (unsigned char)(flo >> 8);
-                o[2] = (unsigned char)(flo >> 16);
-                o[3] = (unsigned char)(flo >> 24);
-                o[4] = (unsigned char)fhi;
-                o[5] = (unsigned char)(fhi >> 8);
-                o[6] = (unsigned char)(fhi >> 16);
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // the tile [tb, end) as 16 B blocks; the first and last may hold other walkers' bytes
-            const int nblk = (int)((end - tb + 15) >> 4);
-            for (int j = lane(); j < nblk; j += kWave) {
-                const uint64_t gb = tb + 16u * (uint64_t)j;
-                if (gb >= run && gb + 16 <= end) {
-                    *reinterpret_cast<uint4 *>(out + gb) = tile_s[wv][j];
-                } else {
-                    const uint64_t b0 = gb > run ? gb : run, b1 = gb + 16 < end ? gb + 16 : end;
-                    for (uint64_t b = b0; b < b1; b++) out[b] = (char)tile[b - tb];
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            run = end;
+            run += wave_bcast(incl, kWave - 1);
+            if (!len || off + len > cap) continue;
+            const int64_t ls = i ? (int64_t)le_b[sl - 1] + 1 : (int64_t)wstart[w];
+            char *o = out + off;
+            for (uint32_t k = 0; k < pl; k++) o[k] = buf[ls + k];
+            uint32_t flo, fhi;
+            af_freq_text(mode, alt_b[sl], tot_b[sl], flo, fhi);
+            o += pl;
+#pragma unroll
+            for (int k = 0; k < 7; k++) o[k] = (char)((k < 4 ? flo >> (8 * k) : fhi >> (8 * (k - 4))) & 0xFFu);
         }
     }
 }
@@ -1213,10 +1148,12 @@ hipError_t launch_walker_scan(int64_t nw, const uint64_t *wcount, const uint64_t
 hipError_t launch_af_format_w(const char *buf, int mode, int64_t nw, uint64_t cap_w, const uint64_t *wcount,
                               const uint64_t *wtoff, const uint64_t *bpre_b, const uint64_t *wstart,
                               const uint64_t *le_b, const int32_t *alt_b, const int32_t *tot_b, const uint32_t *rowpre_b,
-                              const uint8_t *status_b, char *out, uint64_t cap, hipStream_t s) {
+                              const uint8_t *status_b, char *out, uint64_t cap, hipStream_t s, const WalkTail *tail) {
     if (nw <= 0) return hipSuccess;
+    const WalkTail t = tail ? *tail : WalkTail{};
     hipLaunchKernelGGL(k_af_format_w, dim3(grid_for(nw, kFmtWaves, 16384)), dim3(kFmtWaves * kWave), 0, s, buf, mode, nw, cap_w,
-                       wcount, wtoff, bpre_b, wstart, le_b, alt_b, tot_b, rowpre_b, status_b, out, cap);
+                       wcount, wtoff, bpre_b, wstart, le_b, alt_b, tot_b, rowpre_b, status_b, out, cap, t.stage,
+                       t.stage_cap, t.wdirty, t.wtext);
     return hipGetLastError();
 }
 
