@@ -1,0 +1,32 @@
+#!/bin/bash
+# r03 (session 3): both backward boundary scans in one loop -- parity, A/B against build_base
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+    local name=$1 secs=$2; shift 2
+    echo "=== $name ($(date +%T))"
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc"
+    grep '^{' "gpurun_out/$name.log" | python3 -c "
+import json,sys
+for l in sys.stdin:
+    d=json.loads(l); r=d.get('roofline',{}); print('VAL', d.get('value'), d.get('ms_per_step'), r.get('kernel'), round(r.get('avg_launch_ms') or 0,4), (d.get('output_check') or {}).get('match'), {k: round(v,3) for k,v in d.get('kernels_ms').items()})" 2>/dev/null
+    tail -2 "gpurun_out/$name.log" | cut -c1-300
+    return $rc
+}
+step t_walk 700 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_af.py tests/test_gpu_fq_walk.py tests/test_gpu_rf.py tests/test_gpu_gq.py tests/test_gpu_nr.py tests/test_gpu_md.py tests/test_gpu_dose.py tests/test_gpu_hwe.py tests/test_gpu_ngpu.py tests/test_gpu_stream.py tests/test_gpu_gzip.py || exit $?
+step t_scale 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_scale.py -k "af_ or pipeline or general or irregular or miss" || exit $?
+B="--no-cpu-baseline --no-e2e --steps 20 --warmup 3"
+for i in 1 2 3; do
+    step af_$i 300 python -u bench.py $B || exit $?
+    VCFXG_GPU_LIB=build_base/libvcfx_gpu.so step af_base_$i 300 python -u bench.py $B || exit $?
+    step pipe_$i 300 python -u bench.py --workload pipeline $B || exit $?
+    VCFXG_GPU_LIB=build_base/libvcfx_gpu.so step pipe_base_$i 300 python -u bench.py --workload pipeline $B || exit $?
+done
+step nonref 300 python -u bench.py --workload nonref $B || exit $?
+VCFXG_GPU_LIB=build_base/libvcfx_gpu.so step nonref_base 300 python -u bench.py --workload nonref $B || exit $?
+step hwe 300 python -u bench.py --workload hwe $B || exit $?
+VCFXG_GPU_LIB=build_base/libvcfx_gpu.so step hwe_base 300 python -u bench.py --workload hwe $B || exit $?
+echo "=== done"

@@ -1,9 +1,9 @@
 // vcfxg_af_walk.hip -- VCFX_allele_freq_calc's record pass without a separate line index.
 //
-// The data region is cut into C-byte chunks, one wave ("walker") each.  A line belongs to
-// the chunk holding its first byte.  A walker finds the first line start of its chunk (the
-// byte after the first '\n' at or after chunk start - 1: a short scan over the tail of the
-// previous chunk's last line) and then walks its lines one after the other:
+// The data region is cut into C-byte chunks, one wave ("walker") each.  A walker's lines are
+// those starting in [b(chunk start), b(chunk end)), b(x) the byte after the last '\n' before x
+// (vcfxg_walk.h walker_lines: two short backward scans; the line across a chunk boundary goes
+// to the walker after it, which reads it first).  It walks its lines one after the other:
 //
 //   1. one 1 KiB window at the line start (16 B per lane) gives the first '\n' if the line
 //      is short, the first 9 tabs and the FORMAT bytes (ballots + a wave scan);
@@ -21,9 +21,8 @@
 //   4. the line's end offset, counts, status and head record go to the walker's region;
 //      the next line starts at E + 1 (its window is loaded before this line's sweep).
 //
-// So every input byte is read from HBM about once (the tail of each chunk's last line is
-// read twice, the second time mostly from the Infinity Cache), against twice for the
-// separate index sweep.  k_walk_compact concatenates the regions in file order and
+// So every input byte is read from HBM about once (the backward scans' bytes are the next
+// walker's first line, read right after them), against twice for the separate index sweep.  k_walk_compact concatenates the regions in file order and
 // k_af_complex runs the exact per-line path for everything that is not a fixed-stride
 // GT-first record (kMetaFull lines, kAfPending lines), exactly as after the two-sweep
 // schedule.  A walker over its line capacity raises `overflow` and the caller reruns the
@@ -117,7 +116,8 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     const int strip_cr = mode == 0 ? 1 : 0;
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
-    int64_t L = wk == 0 ? lo : scan_nl<kFirstScanU>(buf, cs - 1, hi) + 1;
+    int64_t L, ce2;  // this walker's lines start in [L, ce2)
+    walker_lines(buf, lo, hi, cs, ce, L, ce2);
     const int64_t L0 = L;
     uint64_t wtext = 0;  // region tail (tail.wtext): bytes of this walker's GT-line rows
     int64_t span = span0;  // predicted '\n' distance from the sample start
@@ -155,8 +155,8 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     };
     int cur = 0;
     int64_t A = L & ~(int64_t)15;  // window base of the current line (L - A < 32)
-    if (L < ce) prefetch_window(buf, A, hi, win[wv][cur]);
-    while (L < ce) {
+    if (L < ce2) prefetch_window(buf, A, hi, win[wv][cur]);
+    while (L < ce2) {
         if (n >= cap_w) {
             if (lane() == 0) atomicOr(overflow, 1u);
             break;

@@ -80,7 +80,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
     if (wk >= n_walkers) return;
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
-    int64_t L = wk == 0 ? lo : scan_nl<kFirstScanU>(buf, cs - 1, hi) + 1;
+    int64_t L, ce2;  // this walker's lines start in [L, ce2)
+    walker_lines(buf, lo, hi, cs, ce, L, ce2);
     int64_t span = kGQ ? span0 : 0;  // predicted '\n' distance from the sample start
     uint8_t cr_prev = 0;             // and the '\r' state of that record
     uint64_t n = 0;
@@ -109,8 +110,8 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
     };
     int cur = 0;
     int64_t A = L & ~(int64_t)15;  // window base of the current line (L - A < 16)
-    if (L < ce) prefetch_window(buf, A, hi, win[wv][cur]);
-    while (L < ce) {
+    if (L < ce2) prefetch_window(buf, A, hi, win[wv][cur]);
+    while (L < ce2) {
         if (n >= cap_w) {
             if (lane() == 0) atomicOr(overflow, 1u);
             break;

@@ -396,15 +396,21 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
             // ---- the record end: the first '\n' at or after S (the first step may hold bytes
             // before S, the last lanes of the input's last step re-read its last block)
             const bool first = ws == b0, edge = first || ws + kWaveStep > hi;  // wave-uniform
+            // interior steps: the ASCII shortcut (the same sums as the classes below), exact only
+            // where it flags a byte: it can flag bytes >= 0x80 (such a record goes to the exact
+            // path anyway, but its end must still be the true '\n')
             uint32_t nlm = 0;
             if (edge) nlm = blk < hi ? eq_mask16(v[u], kRepNl) & range_mask16(blk, S, hi) : 0u;
-            else  // exact per byte whatever the bytes are (the ASCII shortcut below is not)
-                nlm = zero_bytes(W[0] ^ kRepNl) | zero_bytes(W[1] ^ kRepNl) | zero_bytes(W[2] ^ kRepNl) |
-                      zero_bytes(W[3] ^ kRepNl);
-            const uint64_t anyn = __ballot(nlm != 0u);
+            else
+                nlm = ~(((W[0] ^ kRepNl) + K) & ((W[1] ^ kRepNl) + K) & ((W[2] ^ kRepNl) + K) &
+                        ((W[3] ^ kRepNl) + K)) & M;
+            uint64_t anyn = __ballot(nlm != 0u);
+            if (anyn && !edge) {  // (rare: the step holding the record end) exact masks
+                nlm = eq_mask16(v[u], kRepNl);
+                anyn = __ballot(nlm != 0u);
+            }
             if (anyn) {
-                const int k = __builtin_ctzll(anyn);
-                if (!edge) nlm = eq_mask16(v[u], kRepNl);  // lane k's exact mask
+                const int k = __builtin_ctzll(anyn);  // (lane k's mask is exact and nonzero)
                 E = uniform64(ws + 16 * k + __builtin_ctz((uint32_t)__shfl((int)nlm, k)));
                 found = true;
                 const uint32_t cr = strip_cr && E > S ? __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r' : 0u;

@@ -49,6 +49,88 @@ __device__ __forceinline__ int64_t scan_nl(const char *__restrict__ buf, int64_t
     return hi;
 }
 
+// last '\n' in [lo, p), else lo - 1 (wave-uniform; kU KiB per step, backwards from p: lane 0
+// holds the highest block of a step, so the first lane with a '\n' holds the last one)
+template <int kU = 4>
+__device__ __forceinline__ int64_t scan_nl_back(const char *__restrict__ buf, int64_t p, int64_t lo) {
+    if (p <= lo) return lo - 1;
+    const int64_t tb = (p - 1) & ~(int64_t)15, lb = lo & ~(int64_t)15;
+    for (int64_t top = tb; top >= lb; top -= (int64_t)kU * kWaveStep) {
+        uint4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {  // branch-free: lanes below lo re-read the lowest block
+            const int64_t bb = top - (int64_t)kBlockBytes * (u * kWave + lane());
+            v[u] = load16(buf, bb >= lb ? bb : lb);
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int64_t bb = top - (int64_t)kBlockBytes * (u * kWave + lane());
+            const uint32_t m = bb >= lb ? eq_mask16(v[u], kRepNl) & range_mask16(bb, lo, p) : 0u;
+            const uint64_t any = __ballot(m != 0u);
+            if (any) {
+                const int k = __builtin_ctzll(any);
+                const uint32_t mk = (uint32_t)__shfl((int)m, k);  // (nonzero: lane k's exact mask)
+                return uniform64(top - (int64_t)kBlockBytes * (u * kWave + k) + 31 - __builtin_clz(mk));
+            }
+        }
+    }
+    return lo - 1;
+}
+
+// A walker's lines: those starting in [b(cs), b(ce)), b(x) = the byte after the last '\n'
+// before x (b = lo for the first chunk, hi past the last): the line across a chunk boundary
+// belongs to the walker after it, which reads that line first, right after its backward
+// scans over the line's head (the walker before stops at the same b).  With lines owned by the
+// chunk of their first byte, a walker's forward search for its first line read the tail of
+// the previous chunk's last line, which that chunk's walker read again only at its end (from
+// HBM: the walk's 3.9 % over-fetch).
+__device__ __forceinline__ void walker_lines(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t cs,
+                                             int64_t ce, int64_t &b0, int64_t &b1) {
+    // both backward scans in one loop: each step issues the loads of both before either is
+    // examined (one round trip for the two where two scans in sequence took two)
+    constexpr int kU = 3;  // (4: the prologue pushed the walks over an occupancy step)
+    bool da = cs <= lo, db = ce >= hi;
+    int64_t ra = lo - 1, rb = lo - 1;
+    const int64_t lb = lo & ~(int64_t)15;
+    int64_t ta = (cs - 1) & ~(int64_t)15, tb = (ce - 1) & ~(int64_t)15;
+    if (ta < lb) da = true;
+    if (tb < lb) db = true;
+    while (!(da && db)) {
+        uint4 va[kU], vb[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {  // (a finished scan re-reads the lowest block: cached)
+            const int64_t pa = ta - (int64_t)kBlockBytes * (u * kWave + lane());
+            const int64_t pb = tb - (int64_t)kBlockBytes * (u * kWave + lane());
+            va[u] = load16(buf, !da && pa >= lb ? pa : lb);
+            vb[u] = load16(buf, !db && pb >= lb ? pb : lb);
+        }
+        auto look = [&](const uint4 *v, int64_t top, int64_t p, bool &done, int64_t &r) {
+            if (done) return;
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const int64_t bb = top - (int64_t)kBlockBytes * (u * kWave + lane());
+                const uint32_t m = bb >= lb ? eq_mask16(v[u], kRepNl) & range_mask16(bb, lo, p) : 0u;
+                const uint64_t any = __ballot(m != 0u);
+                if (any) {
+                    const int k = __builtin_ctzll(any);
+                    const uint32_t mk = (uint32_t)__shfl((int)m, k);  // (nonzero: lane k's exact mask)
+                    r = uniform64(top - (int64_t)kBlockBytes * (u * kWave + k) + 31 - __builtin_clz(mk));
+                    done = true;
+                    return;
+                }
+            }
+        };
+        look(va, ta, cs, da, ra);
+        look(vb, tb, ce, db, rb);
+        ta -= (int64_t)kU * kWaveStep;
+        tb -= (int64_t)kU * kWaveStep;
+        if (ta < lb) da = true;
+        if (tb < lb) db = true;
+    }
+    b0 = cs <= lo ? lo : ra + 1;
+    b1 = ce >= hi ? hi : rb + 1;
+}
+
 // relative position of the tab with 0-based rank r (< total) given per-lane tab masks and
 // their exclusive per-lane counts (wave-uniform result)
 __device__ __forceinline__ int tab_at(uint32_t tm, uint32_t excl, uint32_t c, int r, int b) {
