@@ -883,13 +883,20 @@ __global__ __launch_bounds__(kWScan) void k_walker_scan(int64_t nw, const uint64
     }
 }
 
-// one wave per walker region.  A clean walker (the walk composed every row of it into its
-// stage: wdirty[w] == 0) is copied out whole (its text, usually a
-// few hundred bytes, from its stage to its text offset): loads issued 4 x 64 bytes at a time,
-// then the stores.  Any other walker: row offsets = the walker's text offset + a wave scan of
-// its rows' lengths, each lane writes its line's row.  Rows / walkers ending past cap are
-// skipped (the host writes all again once the text has grown).
-constexpr int kFmtWaves = 4;
+// k_af_format_w.  A clean walker (the walk composed every row of it into its stage:
+// wdirty[w] == 0) is copied out whole by a 16-lane group, four walkers per wave: lane l of the
+// group writes the aligned 16 B blocks l, l + 16, ... of the walker's text span, each the byte
+// rotation (uniform per walker: the span's offset mod 16) of two aligned stage blocks; the
+// span's first and last blocks, shared with the neighbouring walkers, by byte stores.  One
+// round trip for the offsets, one for the stage, and a quarter of the waves a wave per walker
+// took.  The other walkers (a line left to k_af_cx, a stage too small) take the whole wave one
+// at a time: row offsets = the walker's text offset + a wave scan of its rows' lengths, each
+// lane writes its line's row.  Rows / walkers ending past cap are skipped (the host writes all
+// again once the text has grown).
+constexpr int kFmtWaves = 4, kFmtGroup = 16, kFmtPerWave = kWave / kFmtGroup;
+__device__ __forceinline__ uint32_t sel4(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t i) {
+    return i == 0 ? a : i == 1 ? b : i == 2 ? c : d;
+}
 __global__ __launch_bounds__(kFmtWaves *kWave) void k_af_format_w(const char *__restrict__ buf, int mode, int64_t nw,
                                                                    uint64_t cap_w, const uint64_t *__restrict__ wcount,
                                                                    const uint64_t *__restrict__ wtoff,
@@ -904,47 +911,75 @@ __global__ __launch_bounds__(kFmtWaves *kWave) void k_af_format_w(const char *__
                                                                    const char *__restrict__ stage, uint32_t stage_cap,
                                                                    const uint8_t *__restrict__ wdirty,
                                                                    const uint64_t *__restrict__ wtext) {
-    const int64_t nwv = (int64_t)gridDim.x * kFmtWaves;
-    for (int64_t w = (int64_t)blockIdx.x * kFmtWaves + threadIdx.x / kWave; w < nw; w += nwv) {
-        uint64_t run = wtoff[w] + bpre_b[w / kWScan];
-        if (stage && !wdirty[w]) {
-            const uint64_t len = wtext[w];
-            if (run + len > cap) continue;
-            const char *__restrict__ src = stage + (uint64_t)w * stage_cap;
-            char *__restrict__ dst = out + run;
-            for (uint64_t j0 = 0; j0 < len; j0 += 4 * kWave) {
-                char b[4];
+    const int64_t step = (int64_t)gridDim.x * kFmtWaves * kFmtPerWave;
+    const int g = lane() / kFmtGroup, gl = lane() % kFmtGroup;
+    const int64_t qmax = (int64_t)(stage_cap / 16) - 1;
+    for (int64_t w0 = ((int64_t)blockIdx.x * kFmtWaves + threadIdx.x / kWave) * kFmtPerWave; w0 < nw; w0 += step) {
+        const int64_t w = w0 + g;
+        const bool have = w < nw;
+        const bool clean = have && stage && !wdirty[w];
+        const uint64_t run = have ? wtoff[w] + bpre_b[w / kWScan] : 0, len = clean ? wtext[w] : 0;
+        if (clean && len && run + len <= cap) {
+            const uint4 *__restrict__ src = reinterpret_cast<const uint4 *>(stage + (uint64_t)w * stage_cap);
+            const uint64_t d0 = run & ~15ull, dend = run + len;
+            const int nblk = (int)(((dend + 15) >> 4) - (d0 >> 4));
+            const int s = (int)(run & 15);
+            const uint32_t r = (uint32_t)(16 - s) & 15u, rq = r >> 2, rb = r & 3u;
+            for (int j0 = 0; j0 < nblk; j0 += 2 * kFmtGroup) {
+                uint4 a[2], b[2];
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint64_t j = j0 + u * kWave + lane();
-                    b[u] = j < len ? src[j] : 0;
+                for (int u = 0; u < 2; u++) {  // dst block j <- stage blocks q, q + 1 (q = j - 1 when s > 0)
+                    const int64_t q = (int64_t)(j0 + u * kFmtGroup + gl) - (s ? 1 : 0);
+                    a[u] = src[q < 0 ? 0 : (q > qmax ? qmax : q)];
+                    b[u] = src[q + 1 > qmax ? qmax : q + 1];
                 }
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint64_t j = j0 + u * kWave + lane();
-                    if (j < len) dst[j] = b[u];
+                for (int u = 0; u < 2; u++) {
+                    const int j = j0 + u * kFmtGroup + gl;
+                    if (j >= nblk) continue;
+                    const uint32_t W[8] = {a[u].x, a[u].y, a[u].z, a[u].w, b[u].x, b[u].y, b[u].z, b[u].w};
+                    uint32_t o[4];
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        o[i] = __builtin_amdgcn_alignbyte(sel4(W[i + 1], W[i + 2], W[i + 3], W[i + 4], rq),
+                                                          sel4(W[i], W[i + 1], W[i + 2], W[i + 3], rq), rb);
+                    const uint64_t D = d0 + 16u * (uint64_t)j;
+                    if (D >= run && D + 16 <= dend) {
+                        *reinterpret_cast<uint4 *>(out + D) = make_uint4(o[0], o[1], o[2], o[3]);
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < 16; t++)
+                            if (D + t >= run && D + t < dend) out[D + t] = (char)((o[t >> 2] >> (8 * (t & 3))) & 0xFFu);
+                    }
                 }
             }
-            continue;
         }
-        const uint64_t n = wcount[w], s0 = (uint64_t)w * cap_w;
-        for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
-            const uint64_t i = i0 + lane(), sl = s0 + i;
-            const bool in = i < n;
-            const uint32_t pl = in ? rowpre_b[sl] : 0u;
-            const uint32_t len = in && status_b[sl] == 1 ? pl + 7u : 0u;
-            const uint32_t incl = wave_incl_scan(len);
-            const uint64_t off = run + incl - len;
-            run += wave_bcast(incl, kWave - 1);
-            if (!len || off + len > cap) continue;
-            const int64_t ls = i ? (int64_t)le_b[sl - 1] + 1 : (int64_t)wstart[w];
-            char *o = out + off;
-            for (uint32_t k = 0; k < pl; k++) o[k] = buf[ls + k];
-            uint32_t flo, fhi;
-            af_freq_text(mode, alt_b[sl], tot_b[sl], flo, fhi);
-            o += pl;
+        // the group's other walkers, the whole wave each
+        uint64_t dm = __ballot(gl == 0 && have && !clean);
+        while (dm) {
+            const int k = __builtin_ctzll(dm);
+            dm &= dm - 1ull;
+            const int64_t wd = w0 + k / kFmtGroup;
+            uint64_t rw = wtoff[wd] + bpre_b[wd / kWScan];
+            const uint64_t n = wcount[wd], s0 = (uint64_t)wd * cap_w;
+            for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
+                const uint64_t i = i0 + lane(), sl = s0 + i;
+                const bool in = i < n;
+                const uint32_t pl = in ? rowpre_b[sl] : 0u;
+                const uint32_t ln = in && status_b[sl] == 1 ? pl + 7u : 0u;
+                const uint32_t incl = wave_incl_scan(ln);
+                const uint64_t off = rw + incl - ln;
+                rw += wave_bcast(incl, kWave - 1);
+                if (!ln || off + ln > cap) continue;
+                const int64_t ls = i ? (int64_t)le_b[sl - 1] + 1 : (int64_t)wstart[wd];
+                char *o = out + off;
+                for (uint32_t k2 = 0; k2 < pl; k2++) o[k2] = buf[ls + k2];
+                uint32_t flo, fhi;
+                af_freq_text(mode, alt_b[sl], tot_b[sl], flo, fhi);
+                o += pl;
 #pragma unroll
-            for (int k = 0; k < 7; k++) o[k] = (char)((k < 4 ? flo >> (8 * k) : fhi >> (8 * (k - 4))) & 0xFFu);
+                for (int k2 = 0; k2 < 7; k2++) o[k2] = (char)((k2 < 4 ? flo >> (8 * k2) : fhi >> (8 * (k2 - 4))) & 0xFFu);
+            }
         }
     }
 }
@@ -1151,7 +1186,7 @@ hipError_t launch_af_format_w(const char *buf, int mode, int64_t nw, uint64_t ca
                               const uint8_t *status_b, char *out, uint64_t cap, hipStream_t s, const WalkTail *tail) {
     if (nw <= 0) return hipSuccess;
     const WalkTail t = tail ? *tail : WalkTail{};
-    hipLaunchKernelGGL(k_af_format_w, dim3(grid_for(nw, kFmtWaves, 16384)), dim3(kFmtWaves * kWave), 0, s, buf, mode, nw, cap_w,
+    hipLaunchKernelGGL(k_af_format_w, dim3(grid_for(nw, kFmtWaves * kFmtPerWave, 16384)), dim3(kFmtWaves * kWave), 0, s, buf, mode, nw, cap_w,
                        wcount, wtoff, bpre_b, wstart, le_b, alt_b, tot_b, rowpre_b, status_b, out, cap, t.stage,
                        t.stage_cap, t.wdirty, t.wtext);
     return hipGetLastError();
