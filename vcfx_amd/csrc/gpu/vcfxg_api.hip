@@ -1045,6 +1045,24 @@ static vcfxg::DecRef put_dec(const vcfxg::DecHost &d, std::string &pool) {
     return r;
 }
 
+// threshold_bounds memoised by the value's bits: the exact decimal expansion of a boundary
+// (up to ~750 digits for the subnormal neighbours of 0.0, which every FILTER criterion asks
+// for) cost tens of microseconds per call, paid again for every region call with the same
+// criteria (a bounded per-thread table; the result is a pure function of the value)
+static void cached_threshold_bounds(double t, vcfxg::ThresholdHost &out) {
+    static thread_local std::map<uint64_t, vcfxg::ThresholdHost> memo;
+    uint64_t key;
+    std::memcpy(&key, &t, sizeof key);
+    auto it = memo.find(key);
+    if (it != memo.end()) {
+        out = it->second;
+        return;
+    }
+    vcfxg::threshold_bounds(t, out);
+    if (memo.size() >= 64) memo.clear();
+    memo.emplace(key, out);
+}
+
 static int compile_criteria(vcfxg_ctx *c, const vcfxg_criterion *crit, int n) {
     std::vector<vcfxg::RfCrit> dev((size_t)n);
     std::string pool;
@@ -1065,7 +1083,7 @@ static int compile_criteria(vcfxg_ctx *c, const vcfxg_criterion *crit, int n) {
         // FILTER and string INFO criteria never compare numbers: no boundary digits (they
         // would only lengthen the pool the filter walk keeps in registers)
         const bool cmp_num = h.target != vcfxg::RF_FILTER && (h.target != vcfxg::RF_INFO || h.numeric);
-        vcfxg::threshold_bounds(cmp_num && h.numeric ? h.value : 0.0, th);
+        cached_threshold_bounds(cmp_num && h.numeric ? h.value : 0.0, th);
         if (!cmp_num) th.lo.digits.clear(), th.hi.digits.clear();
         d.T.t = h.numeric ? h.value : 0.0;
         d.T.kind = th.kind;
