@@ -133,6 +133,12 @@ struct vcfxg_ctx {
     int ld_kpad = 64, ld_ns = 0, ld_kp4 = 64;
     bool ld_chrom_ids = false;
     std::vector<uint32_t> ld_cid_host, ld_blocks_host;
+    // the last streaming call's block lists: key (j0, j1, window, M, masked kernel), group
+    // flags, list sizes (fast, masked, int8), the ld_blocks buffer they were copied to
+    uint64_t ld_plan_key[5] = {0, 0, 0, 0, 0};
+    std::vector<uint8_t> ld_plan_gf;
+    uint32_t ld_plan_n[3] = {0, 0, 0};
+    void *ld_plan_dev = nullptr;
     uint64_t text_bytes = 0;
     uint64_t text_hint = 0;  // AF walk: text bytes of the previous call (the next call's capacity)
     // profiling: an event pair per launch from a pool, harvested only when the figures are
@@ -2136,85 +2142,107 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     const std::vector<uint8_t> &gf = c->ld_gflag_host;
     constexpr uint64_t kSub = vcfxg::kLdFastBlock / BM;  // 64-blocks per fast group
     auto gcomp = [&](uint64_t b64) { return gf[b64 / kSub] != 0; };
-    std::vector<uint32_t> blocks;
-    uint64_t nb = 1;
-    // fast list first, in kSuper x kSuper super-tiles (row blocks J x column blocks I): the
-    // kernel maps contiguous list ranges to one XCD, so the blocks an XCD runs at once share
-    // 2*kSuper operand tiles through its L2 instead of streaming distinct ones
-    static const uint64_t kSuper = [] {
-        const char *e = getenv("VCFXG_LD_SUPER");
-        const long v = e ? atol(e) : 0;
-        return (uint64_t)(v > 0 ? v : 4);
-    }();
-    const uint64_t Jb = j0 / FB, Je = (j1 + FB - 1) / FB;
-    for (uint64_t J0 = Jb; J0 < Je; J0 += kSuper) {
-        const uint64_t J1 = std::min(Je, J0 + kSuper);
-        const uint64_t Ilo = ifirst(kSub * J0) / kSub;
-        for (uint64_t I0 = Ilo; I0 < J1; I0 += kSuper)
-            for (uint64_t J = J0; J < J1; J++) {
-                if (!gf[J]) continue;
-                const uint64_t Imin = std::max(I0, ifirst(kSub * J) / kSub), Imax = std::min(I0 + kSuper, J + 1);
-                for (uint64_t I = Imin; I < Imax; I++)
-                    if (gf[I]) {
-                        blocks.push_back((uint32_t)I);
-                        blocks.push_back((uint32_t)J);
-                    }
-            }
-    }
-    const uint32_t nfast = (uint32_t)(blocks.size() / 2);
-    // the missing-data tiles (k_ld_mask, default): every 128 x 128 tile pair in the window
-    // whose 256-groups are not both complete (those are k_ld_fast's); VCFXG_LD_MASK=0 keeps the
-    // previous int8 kernel (k_ld_block) over every 64-block pair with an incomplete side
     static const bool use_mask = [] {
         const char *e = getenv("VCFXG_LD_MASK");
         return !(e && e[0] == '0');
     }();
+    // the block lists are a pure function of (j0, j1, window, M, the kernel choice, the
+    // per-group complete flags): a call with the same ones reuses the last lists and their
+    // device copy (building 77 K tile pairs and copying them cost ~0.13 ms of host time per call)
+    const bool mask_on = use_mask && c->ld_vq;
+    const uint64_t pkey[5] = {j0, j1, window, M, mask_on ? 1u : 0u};
+    const bool hit = c->ld_plan_dev != nullptr && c->ld_plan_dev == c->ld_blocks.p &&
+                     std::equal(pkey, pkey + 5, c->ld_plan_key) && c->ld_plan_gf == gf;
+    std::vector<uint32_t> blocks;
+    uint64_t nb = 1;
+    uint32_t nfast = 0, nmask = 0, nbl = 0;
     for (uint64_t J = j0 / BM; J * BM < j1; J++) nb = std::max<uint64_t>(nb, J - ifirst(J) + 1);
-    uint32_t nmask = 0, nbl = 0;
-    if (use_mask && c->ld_vq) {
-        constexpr uint64_t TM = vcfxg::kLdMaskTile, kPerG = vcfxg::kLdFastBlock / vcfxg::kLdMaskTile;
-        for (uint64_t J2 = j0 / TM; J2 * TM < j1; J2++) {
-            const uint64_t I2lo = ifirst(J2 * (TM / BM)) / (TM / BM);  // the first 64-row's window start
-            const bool jc = gf[J2 / kPerG] != 0;
-            for (uint64_t I2 = I2lo; I2 <= J2; I2++) {
-                if (jc && gf[I2 / kPerG]) continue;  // a complete group pair: k_ld_fast
-                blocks.push_back((uint32_t)I2);
-                blocks.push_back((uint32_t)J2);
-            }
-        }
-        nmask = (uint32_t)(blocks.size() / 2) - nfast;
+    if (hit) {
+        nfast = c->ld_plan_n[0];
+        nmask = c->ld_plan_n[1];
+        nbl = c->ld_plan_n[2];
     } else {
-        // for a complete row block J only the incomplete column blocks, found in the sorted list
-        // of them (no scan over the whole window triangle on the host)
-        const uint64_t Jlast = (j1 + BM - 1) / BM;
-        std::vector<uint32_t> inc;
-        for (uint64_t b = ifirst(j0 / BM); b < Jlast; b++)
-            if (!gcomp(b)) inc.push_back((uint32_t)b);
-        for (uint64_t J = j0 / BM; J * BM < j1; J++) {
-            const uint64_t I0 = ifirst(J);
-            if (!gcomp(J)) {
-                for (uint64_t I = I0; I <= J; I++) {
-                    blocks.push_back((uint32_t)I);
+        // fast list first, in kSuper x kSuper super-tiles (row blocks J x column blocks I): the
+        // kernel maps contiguous list ranges to one XCD, so the blocks an XCD runs at once share
+        // 2*kSuper operand tiles through its L2 instead of streaming distinct ones
+        static const uint64_t kSuper = [] {
+            const char *e = getenv("VCFXG_LD_SUPER");
+            const long v = e ? atol(e) : 0;
+            return (uint64_t)(v > 0 ? v : 4);
+        }();
+        const uint64_t Jb = j0 / FB, Je = (j1 + FB - 1) / FB;
+        for (uint64_t J0 = Jb; J0 < Je; J0 += kSuper) {
+            const uint64_t J1 = std::min(Je, J0 + kSuper);
+            const uint64_t Ilo = ifirst(kSub * J0) / kSub;
+            for (uint64_t I0 = Ilo; I0 < J1; I0 += kSuper)
+                for (uint64_t J = J0; J < J1; J++) {
+                    if (!gf[J]) continue;
+                    const uint64_t Imin = std::max(I0, ifirst(kSub * J) / kSub), Imax = std::min(I0 + kSuper, J + 1);
+                    for (uint64_t I = Imin; I < Imax; I++)
+                        if (gf[I]) {
+                            blocks.push_back((uint32_t)I);
+                            blocks.push_back((uint32_t)J);
+                        }
+                }
+        }
+        nfast = (uint32_t)(blocks.size() / 2);
+        // the missing-data tiles (k_ld_mask, default): every 128 x 128 tile pair in the window
+        // whose 256-groups are not both complete (those are k_ld_fast's); VCFXG_LD_MASK=0 keeps the
+        // previous int8 kernel (k_ld_block) over every 64-block pair with an incomplete side
+
+        if (use_mask && c->ld_vq) {
+            constexpr uint64_t TM = vcfxg::kLdMaskTile, kPerG = vcfxg::kLdFastBlock / vcfxg::kLdMaskTile;
+            for (uint64_t J2 = j0 / TM; J2 * TM < j1; J2++) {
+                const uint64_t I2lo = ifirst(J2 * (TM / BM)) / (TM / BM);  // the first 64-row's window start
+                const bool jc = gf[J2 / kPerG] != 0;
+                for (uint64_t I2 = I2lo; I2 <= J2; I2++) {
+                    if (jc && gf[I2 / kPerG]) continue;  // a complete group pair: k_ld_fast
+                    blocks.push_back((uint32_t)I2);
+                    blocks.push_back((uint32_t)J2);
+                }
+            }
+            nmask = (uint32_t)(blocks.size() / 2) - nfast;
+        } else {
+            // for a complete row block J only the incomplete column blocks, found in the sorted list
+            // of them (no scan over the whole window triangle on the host)
+            const uint64_t Jlast = (j1 + BM - 1) / BM;
+            std::vector<uint32_t> inc;
+            for (uint64_t b = ifirst(j0 / BM); b < Jlast; b++)
+                if (!gcomp(b)) inc.push_back((uint32_t)b);
+            for (uint64_t J = j0 / BM; J * BM < j1; J++) {
+                const uint64_t I0 = ifirst(J);
+                if (!gcomp(J)) {
+                    for (uint64_t I = I0; I <= J; I++) {
+                        blocks.push_back((uint32_t)I);
+                        blocks.push_back((uint32_t)J);
+                    }
+                    continue;
+                }
+                for (auto it = std::lower_bound(inc.begin(), inc.end(), (uint32_t)I0); it != inc.end() && *it <= J; ++it) {
+                    blocks.push_back(*it);
                     blocks.push_back((uint32_t)J);
                 }
-                continue;
             }
-            for (auto it = std::lower_bound(inc.begin(), inc.end(), (uint32_t)I0); it != inc.end() && *it <= J; ++it) {
-                blocks.push_back(*it);
-                blocks.push_back((uint32_t)J);
-            }
+            nbl = (uint32_t)(blocks.size() / 2) - nfast;
         }
-        nbl = (uint32_t)(blocks.size() / 2) - nfast;
     }
     const uint64_t rows = j1 - j0;
-    int r = ensure(c, c->ld_blocks, 4 * blocks.size() + 8);
+    int r = hit ? VCFXG_OK : ensure(c, c->ld_blocks, 4 * blocks.size() + 8);
     if (!r) r = ensure(c, c->ld_cnt, 2 * rows * nb + 16);
     if (!r) r = ensure(c, c->ld_off, 4 * (rows * nb + 1));  // u32 offsets inside each row
     if (!r) r = ensure(c, c->ld_rowoff, 16 * (rows + 1));      // row totals, then row starts
     if (r) return r;
-    c->ld_blocks_host.swap(blocks);
-    HIPCHK(c, hipMemcpyAsync(c->ld_blocks.p, c->ld_blocks_host.data(), 4 * c->ld_blocks_host.size(),
-                             hipMemcpyHostToDevice, c->stream));
+    if (!hit) {
+        c->ld_blocks_host.swap(blocks);
+        HIPCHK(c, hipMemcpyAsync(c->ld_blocks.p, c->ld_blocks_host.data(), 4 * c->ld_blocks_host.size(),
+                                 hipMemcpyHostToDevice, c->stream));
+        std::copy(pkey, pkey + 5, c->ld_plan_key);
+        c->ld_plan_gf = gf;
+        c->ld_plan_n[0] = nfast;
+        c->ld_plan_n[1] = nmask;
+        c->ld_plan_n[2] = nbl;
+        c->ld_plan_dev = c->ld_blocks.p;
+    }
     // (no clearing of ld_cnt: the count kernels write every window slot the row scan reads)
     vcfxg::LdWindowArgs a{M, c->ld_kpad, c->ld_ns, window, threshold, max_dist, j0, j1, nb, 0.0, 0};
     // prefilter margin: |fp64 r^2 - exact r^2| of the reference's sequence is < ~1.2e-14 * n
@@ -2345,6 +2373,7 @@ int vcfxg_ld_matrix(vcfxg_ctx *c, int gate, int printf4, uint64_t *cell_bytes) {
     if (!r) r = ensure(c, c->text, cells + 16);
     if (r) return r;
     c->ld_blocks_host.swap(blocks);
+    c->ld_plan_dev = nullptr;  // (the streaming lists' device copy is overwritten)
     HIPCHK(c, hipMemcpyAsync(c->ld_blocks.p, c->ld_blocks_host.data(), 4 * c->ld_blocks_host.size(),
                              hipMemcpyHostToDevice, c->stream));
     prof_begin(c, "ld_matrix");
