@@ -302,6 +302,9 @@ __global__ __launch_bounds__(256) void k_fq_compact(int64_t n_walkers, uint64_t 
 // record_filter: kept, data lines; genotype_query: the GT-first lines it matched and examined
 // (k_gq_complex adds the ones it takes)
 template <bool kRF, bool kGQ>
+#ifdef VCFXG_FIN_WAVES  // (A/B knob: a minimum occupancy for the latency-bound filter pass)
+__attribute__((amdgpu_waves_per_eu(VCFXG_FIN_WAVES, 8)))
+#endif
 __global__ __launch_bounds__(256) void k_fq_finish(const char *__restrict__ buf, int64_t data_start,
                                                    const uint64_t *__restrict__ line_end, const uint64_t *n_lines_p,
                                                    RfArgs rf, uint8_t *__restrict__ status, LineMeta *__restrict__ meta,
