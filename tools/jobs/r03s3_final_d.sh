@@ -1,0 +1,21 @@
+#!/bin/bash
+# r03 session-3 round end, part D: the full GPU suite, smoke and the default AF bench line on
+# the final tree
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 1
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() {
+    local name=$1 secs=$2; shift 2
+    echo "=== $name ($(date +%T))"
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc"
+    tail -2 "gpurun_out/$name.log" | cut -c1-300
+    return $rc
+}
+step pytest_gpu_d 1000 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 300 --timeout-method thread || exit $?
+step smoke_d 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit $?
+step bench_af_d 600 python -u bench.py || exit $?
+step bench_ld_d 600 python -u bench.py --workload ld --no-e2e || exit $?
+for f in gpurun_out/bench_af_d.log gpurun_out/bench_ld_d.log; do grep '^{' "$f" | tail -1 > "${f%.log}.json"; done
+echo "=== done"
