@@ -230,6 +230,32 @@ _CHECK_CASES = {
     "md": ("md_file",), "ph": ("ph_file",),
     "ld": ("ld20k_bench", "ld3000_bench", "ld20k_miss_bench"),
 }
+# LD: the reference's output on the header + variants [a, n) of the shard (a "slice" input) is
+# the full run's lines whose VAR1 is variant >= a (W >= n - a: every pair of the slice is in the
+# window; each variant's pairs stream oldest -> newest)
+_LD_TAIL_CASES = ("ld100k_tail_bench", "ld100k_miss_tail_bench")
+
+
+def ld_tail_lines(text, pos0):
+    """the pair lines of `text` whose VAR1_POS >= pos0 (positions strictly increase in the shard)"""
+    out = []
+    for ln in text.split(b"\n"):
+        if ln and int(ln.split(b"\t", 2)[1]) >= pos0:
+            out.append(ln)
+    return b"".join(x + b"\n" for x in out)
+
+
+def record_pos(arr, k):
+    """POS of data record k of a synthetic shard (numpy uint8 array of the file bytes)"""
+    import numpy as np
+    nl = np.flatnonzero(arr == 10)
+    # the data records follow the '#' lines: the first data line starts after the last header '\n'
+    starts = np.concatenate([[0], nl[:-1] + 1])
+    first = int(np.searchsorted(starts, 0, "left"))
+    while arr[starts[first]] == ord("#"):
+        first += 1
+    s0 = int(starts[first + k])
+    return int(bytes(arr[s0:s0 + 64]).split(b"\t")[1])
 
 
 def output_check(workload, eng, s, a, rank, arr=None):
@@ -331,6 +357,22 @@ def output_check(workload, eng, s, a, rank, arr=None):
         want = c["stdout"]["sha256"]
         what = "sha256 of the first %d variants' pair lines vs VCFX_ld_calculator -w 100000 -t 0.5 (reference)" % (
             dig["inputs"][c["input"]]["n_records"])
+        # and the shard's tail: the lines whose VAR1 is past the slice start
+        for nm in _LD_TAIL_CASES:
+            t = dig["cases"].get(nm)
+            if t is None or got != want:
+                continue
+            tin = dict(dig["inputs"][t["input"]])
+            lo, hi = tin.pop("slice")
+            if hi != a.records or a.window < hi - lo or a.threshold != 0.5 or not _same_input(mine, tin) or arr is None:
+                continue
+            tail = ld_tail_lines(text, record_pos(arr, lo))
+            got_t = hashlib.sha256(head + tail).hexdigest()
+            case += "+" + nm
+            what += "; sha256 of the pair lines with VAR1 >= variant %d vs the reference on variants [%d, %d)" % (
+                lo, lo, hi)
+            if got_t != t["stdout"]["sha256"]:
+                got, want = got_t, t["stdout"]["sha256"]
     if got != want:
         if os.environ.get("VCFX_BENCH_ABLATION"):  # diagnostic builds (results invalid by design)
             return {"checked": True, "match": False, "case": case, "what": what}

@@ -340,6 +340,10 @@ int vcfxg_ld_matrix(vcfxg_ctx *ctx, int gate, int printf4, uint64_t *cell_bytes)
  * loop of computeLDStreamingMmap :616-646 / computeLDStreaming :954-983. */
 int vcfxg_ld_stream_chunk(vcfxg_ctx *ctx, uint64_t j0, uint64_t j1, uint64_t window, double threshold, int max_dist,
                           uint64_t *n_pairs, uint64_t *text_bytes);
+/* pairs [first, first + count) of the last vcfxg_ld_stream_chunk call, in output order: variant
+ * indices (i < j, into the prepared variants) and the fp64 r^2 each line's text was formatted
+ * from (the value computeRsqFast returns, VCFX_ld_calculator.cpp:352-401); any pointer may be NULL */
+int vcfxg_ld_fetch_pairs(vcfxg_ctx *ctx, uint64_t first, uint64_t count, uint32_t *vi, uint32_t *vj, double *r2);
 /* checks the int8 MFMA operand layout the LD kernels assume (0 mismatches expected) */
 int vcfxg_selftest_mfma_i8(vcfxg_ctx *ctx, int *mismatches);
 /* checks the FP4 (e2m1, block-scaled) MFMA operand layout of the fast LD kernel */
@@ -358,13 +362,23 @@ int vcfxg_shard_cuts(const char *data, size_t n, size_t lo, int world, uint64_t 
  * include/vcfx_tools.h: one host thread per rank).  On n distinct devices the reductions run
  * over RCCL (librccl loaded at run time; ncclCommInitAll + ncclAllReduce on each rank's stream,
  * over xGMI); ranks sharing a device (a rehearsal on one GPU) reduce on the host.  VCFX_RCCL=0
- * forces the host reduction.  vcfxg_comm_allreduce_u64: every rank calls it from its own
- * thread with the same count (<= 64); on return vals holds the sums over all ranks. */
+ * forces the host reduction; VCFX_RCCL=1 forms an RCCL clique for n = 1 too (the one-GPU check of
+ * the RCCL path).  vcfxg_comm_allreduce_u64: every rank calls it from its own thread with the
+ * same count (<= 64); on return vals holds the sums over all ranks (the host reduction's when the
+ * status is not VCFXG_OK). */
 typedef struct vcfxg_comm vcfxg_comm;
 int vcfxg_comm_init(vcfxg_ctx *const *ctxs, int n, vcfxg_comm **out);
 int vcfxg_comm_allreduce_u64(vcfxg_comm *comm, int rank, uint64_t *vals, size_t count);
 int vcfxg_comm_uses_rccl(const vcfxg_comm *comm);
+/* RCCL all-reduces run by the clique, and how many of them disagreed with the host reduction
+ * every call also performs (the vote before the collective: no rank enters it unless every rank
+ * staged its values; on any failure all ranks get the host sums and a non-zero status) */
+int vcfxg_comm_rccl_stats(vcfxg_comm *comm, uint64_t *calls, uint64_t *mismatches);
 void vcfxg_comm_destroy(vcfxg_comm *comm);
+
+/* the schedule the last region call took ("af_walk", "af_walk_gt_first", "af_two_sweep", "fq_walk",
+ * "fq_two_sweep", ...): a diagnostic for tests; VCFXG_SCHEDULE_LOG=path appends one line per call */
+const char *vcfxg_last_schedule(const vcfxg_ctx *ctx);
 
 /* device-formatted output text (without the column header line) */
 int vcfxg_fetch_text(vcfxg_ctx *ctx, char *host, size_t cap);

@@ -14,7 +14,7 @@ output check.  The synthetic inputs are regenerated from their parameters (vcfx_
 counter-based: the bytes do not depend on thread count or host), so only digests are
 committed.  Needs ~10 GB of /tmp and a few minutes of CPU.
 
-    python tests/golden/make_full_digests.py [case-name ...]
+    python tests/golden/make_full_digests.py [--out PATH] [case-name ...]
 """
 import hashlib
 import json
@@ -23,6 +23,7 @@ import subprocess
 import sys
 import tempfile
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -63,6 +64,14 @@ INPUTS = {
     # config 3's annotated shard with sparse missing calls
     "annot_gtadp": dict(n_records=427409, n_samples=2504, seed=20251227, info_mode=1, format_mode=1),
     "annot_miss": dict(n_records=427409, n_samples=2504, seed=20251227, info_mode=1, missing_rate=5e-4),
+    # config 5 past its first 20 K variants: the header + variants [80,000, 100,000) of the bench's
+    # 100 K LD shard (complete, and with 0.1 % missing calls).  With W = 100 K every pair of the
+    # slice is in the window, and the reference streams each variant's pairs oldest -> newest, so
+    # its output on the slice is exactly the full 100 K run's lines whose VAR1 is variant >= 80,000
+    # (tests/test_gpu_scale.py filters the GPU's full run by VAR1_POS: positions strictly increase)
+    "ld100k_tail": dict(n_records=100000, n_samples=2504, seed=20251226, hap_blocks=1, slice=[80000, 100000]),
+    "ld100k_miss_tail": dict(n_records=100000, n_samples=2504, seed=20251226, hap_blocks=1, missing_rate=0.001,
+                             slice=[80000, 100000]),
 }
 
 AF, RF, GQ, LD, NR, HWE = ("VCFX_allele_freq_calc", "VCFX_record_filter", "VCFX_genotype_query",
@@ -106,6 +115,8 @@ CASES = {
     "ld3000_bench": ("ld3000", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
     "ld20k_bench": ("ld20k", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
     "ld20k_miss_bench": ("ld20k_miss", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
+    "ld100k_tail_bench": ("ld100k_tail", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
+    "ld100k_miss_tail_bench": ("ld100k_miss_tail", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
     "af_file_miss": ("chr21_miss", [[AF, "-q", "-i", "{F}"]], False),
     "af_stdin_miss": ("chr21_miss", [[AF, "-q"]], False),
     "af_file_gtadp": ("chr21_gtadp", [[AF, "-q", "-i", "{F}"]], False),
@@ -119,8 +130,19 @@ CASES = {
 
 
 def generate(params):
+    """(bytes, data-record offsets) of an input; a "slice": [a, b) input is the header of the
+    generated file followed by its data records a .. b-1 (offsets rebased to the slice)."""
     from vcfx_amd import synth
-    return synth.generate_array(rec_offsets=True, **params)
+    params = dict(params)
+    sl = params.pop("slice", None)
+    arr, offs = synth.generate_array(rec_offsets=True, **params)
+    if sl is None:
+        return arr, offs
+    a, b = sl
+    h = int(offs[0])
+    out = np.concatenate([arr[:h], arr[int(offs[a]):int(offs[b])]])
+    o2 = offs[a:b + 1] - offs[a] + np.uint64(h)
+    return out, o2
 
 
 def keep_mask(arr, offs, out):
@@ -163,9 +185,9 @@ def run_chain(bindir_fn, stages, path):
     return data, rc_all
 
 
-def main(names):
+def main(names, out_path=OUT):
     try:
-        with open(OUT) as f:
+        with open(out_path) as f:
             doc = json.load(f)
     except OSError:
         doc = {"inputs": {}, "cases": {}}
@@ -187,9 +209,12 @@ def main(names):
             for nm in nms:
                 _, stages, want_mask = CASES[nm]
                 t0 = time.time()
-                ref_out, ref_rc = run_chain(lambda t: os.path.join(REF, t), stages, f.name)
-                t_ref = time.time() - t0
-                ora_out, ora_rc = run_chain_oracle(stages, f.name)
+                # the reference and the oracle run side by side (subprocesses: no GIL contention)
+                with ThreadPoolExecutor(2) as ex:
+                    fo = ex.submit(run_chain_oracle, stages, f.name)
+                    ref_out, ref_rc = run_chain(lambda t: os.path.join(REF, t), stages, f.name)
+                    t_ref = time.time() - t0
+                    ora_out, ora_rc = fo.result()
                 assert ref_rc == ora_rc, (nm, ref_rc, ora_rc)
                 assert ref_out == ora_out, "%s: the C oracle differs from the reference at full size" % nm
                 c = {"input": inp, "stages": stages, "rc": ref_rc, "stdout": digest(ref_out),
@@ -201,7 +226,7 @@ def main(names):
                 doc["cases"][nm] = c
                 print("  %s: %s (%.1fs ref)" % (nm, c["stdout"], t_ref), flush=True)
         del arr, offs
-    with open(OUT, "w") as f:
+    with open(out_path, "w") as f:
         json.dump(doc, f, indent=1, sort_keys=True)
         f.write("\n")
 
@@ -222,4 +247,10 @@ def run_chain_oracle(stages, path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:])
+    # --out PATH: write (and read) another digest file, so long cases can run in parallel
+    # processes and be merged into full_digests.json afterwards
+    a = sys.argv[1:]
+    out = OUT
+    if a[:1] == ["--out"]:
+        out, a = a[1], a[2:]
+    main(a, out)

@@ -62,22 +62,57 @@ def test_ld_matrix_matches_oracle(oracle, cfg):
                 assert got == want, (a, cfg)
 
 
-def test_ld_r2_values_bitexact(oracle):
-    """Pair r^2 doubles (not only their 4-dp text) equal the oracle's computeRsqFast."""
+def _codes(buf, oracle):
+    """int8 genotype codes per data line (parseGenotypeRaw on the GT prefix, -1 missing)."""
     import ctypes
 
     import numpy as np
-    buf = synth.generate(200, 300, 57, 0, 0.03, 1, 0.0, 0)
+    f = oracle.lib.oracle_ld_parse_gt_raw
+    f.argtypes, f.restype = [ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int
+    rows = []
+    for ln in buf.split(b"\n"):
+        if not ln or ln[:1] == b"#":
+            continue
+        gts = [s.split(b":", 1)[0] for s in ln.split(b"\t")[9:]]
+        rows.append(np.array([f(g, len(g)) if g else -1 for g in gts], np.int8))
+    return rows
+
+
+@pytest.mark.parametrize("cfg,knock", [((200, 300, 57, 0, 0.03, 1, 0.0, 0), None),   # masked tiles only
+                                       ((600, 300, 63, 0, 0.0, 1, 0.0, 0), None),    # complete: FP4 fast blocks
+                                       ((600, 300, 63, 0, 0.0, 1, 0.0, 0), 300)])    # fast + masked mix
+def test_ld_r2_values_bitexact(oracle, cfg, knock):
+    """Every window pair's fp64 r^2 on the device (vcfxg_ld_fetch_pairs: the value each output line
+    was formatted from) equals the oracle's computeRsqFast on the same two genotype vectors, bit
+    for bit -- north_star's "r^2 within 1e-6" pinned at 0 ulp, not only through the 4-dp text."""
+    import ctypes
+
+    import numpy as np
+    buf = synth.generate(*cfg)
+    if knock is not None:
+        buf = _knock_out(buf, knock)
+    g = _codes(buf, oracle)
+    m, ns = len(g), cfg[1]
     e = engine.Engine(0)
-    e.load(buf)
-    e.index(engine.data_start_of(buf, strip_cr=False))
-    m = e.ld_prepare(300)
-    assert m == 200
-    # threshold 0: every window pair, text carries 4 dp; compare the epilogue via formatted
-    # output at full window and via the oracle's per-pair function on random pairs
-    np_, tb = e.ld_stream_chunk(0, m, m, 0.0)
-    assert np_ == m * (m - 1) // 2
-    e.close()
+    try:
+        e.load(buf)
+        e.index(engine.data_start_of(buf, strip_cr=False))
+        assert e.ld_prepare(ns) == m
+        # threshold 0: every window pair is written (r^2 >= 0 always), in (j, i ascending) order
+        np_, _ = e.ld_stream_chunk(0, m, m, 0.0)
+        assert np_ == m * (m - 1) // 2
+        vi, vj, r2 = e.ld_pairs(0, np_)
+    finally:
+        e.close()
+    want_i = np.concatenate([np.arange(j, dtype=np.uint32) for j in range(1, m)])
+    want_j = np.concatenate([np.full(j, j, np.uint32) for j in range(1, m)])
+    assert (vi == want_i).all() and (vj == want_j).all()
+    rs = oracle.lib.oracle_ld_rsq_fast
+    ptr = [x.ctypes.data_as(ctypes.c_void_p) for x in g]
+    want = np.array([rs(ptr[i], ptr[j], ns) for i, j in zip(want_i.tolist(), want_j.tolist())], np.float64)
+    bad = np.flatnonzero(r2.view(np.uint64) != want.view(np.uint64))
+    assert bad.size == 0, [(int(want_i[k]), int(want_j[k]), r2[k], want[k]) for k in bad[:5]]
+    assert (want > 0.0).sum() > np_ // 4  # the values are not all the gate's 0.0
 
 
 def _knock_out(buf, line_no):

@@ -128,6 +128,19 @@ def test_chr21_shard_matches_reference(inputs, case, stdin):
     _check(case, inputs, stdin)
 
 
+@pytest.mark.parametrize("case", ["af_file", "pipeline_bench", "pipeline_annot"])
+def test_ngpu8_drop_in_at_full_size(inputs, case):
+    """The in-process multi-GPU drop-in (VCFX_NGPU=8 on the first stage: eight rank contexts,
+    round robin over the box's devices) on the full 427 K-record shard; stdout must hash to the
+    reference's digest (AF: the ranks' rows in order; the RF|GQ pipeline: RF's ranks feeding GQ)."""
+    c = DIG["cases"][case]
+    path = inputs.path(c["input"])
+    cmd = "VCFX_NGPU=8 " + _cmd(c["stages"], path)
+    got, rc, err = _hash_cmd(cmd)
+    assert rc == 0, err[-2000:]
+    assert got == c["stdout"], (case, got, c["stdout"], err[-2000:])
+
+
 @pytest.mark.parametrize("case,stdin", [("pipeline_annot", "none"), ("rf_stdin_annot", "pipe"),
                                         ("gq_strict_annot", "none")])
 def test_annotated_shard_matches_reference(inputs, case, stdin):
@@ -195,6 +208,44 @@ def test_bgzf_chr21_matches_reference(inputs, case):
                                   "ld20k_bench", "ld20k_miss_bench"])
 def test_ld_matches_reference(inputs, case):
     _check(case, inputs)
+
+
+@pytest.mark.parametrize("case", ["ld100k_tail_bench", "ld100k_miss_tail_bench"])
+def test_ld_tail_matches_reference(case):
+    """Config 5 past its first 20 K variants.  The reference ran on the header + variants
+    [80,000, 100,000) of the bench's 100 K LD shard (complete, and with 0.1 % missing calls);
+    the drop-in runs on the WHOLE 100 K shard (every tile row up to 100 K, the count table and
+    the row offsets far from the origin) and its lines whose VAR1 is variant >= 80,000 must hash
+    to the reference's output: with W = 100 K each variant's pairs stream oldest -> newest, so
+    that subsequence is the reference's output on the slice."""
+    if case not in DIG["cases"]:
+        pytest.skip("no reference digest for %s" % case)
+    c = DIG["cases"][case]
+    params = dict(DIG["inputs"][c["input"]])
+    lo, hi = params.pop("slice")
+    assert hi == params["n_records"]
+    arr, offs = synth.generate_array(rec_offsets=True, **params)
+    pos0 = int(bytes(arr[int(offs[lo]):int(offs[lo]) + 64]).split(b"\t")[1])
+    d = tempfile.mkdtemp(prefix="vcfx_ldtail_")
+    path = os.path.join(d, "ld100k.vcf")
+    try:
+        arr.tofile(path)
+        del arr, offs
+        argv = [tool_binary("VCFX_ld_calculator")] + [a.replace("{F}", path) for a in c["stages"][0][1:]]
+        r = subprocess.run(argv, capture_output=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = r.stdout.split(b"\n")
+        head, keep = lines[0], []
+        for ln in lines[1:]:
+            if ln and int(ln.split(b"\t", 2)[1]) >= pos0:
+                keep.append(ln)
+        out = head + b"\n" + b"".join(x + b"\n" for x in keep)
+        got = {"sha256": hashlib.sha256(out).hexdigest(), "len": len(out), "lines": out.count(b"\n")}
+        assert got == c["stdout"], (case, got, c["stdout"])
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+        os.rmdir(d)
 
 
 def _mask_sha(st, n_records):

@@ -2,8 +2,11 @@
 // and the host-side sequencing of the record kernels on one HIP stream.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>  // declarations only: librccl is dlopen'd by the rank cliques
 
 #include <dlfcn.h>
+#include <fcntl.h>
+#include <unistd.h>
 
 #include <condition_variable>
 #include <cstdio>
@@ -41,8 +44,8 @@ struct vcfxg_ctx {
     int last_byte = -1;  // input[n-1] (host copy), -1 if empty
     bool loaded = false;
     bool ingesting = false;               // between vcfxg_ingest_begin and the final chunk
-    const char *ingest_first = nullptr;   // the first ingested chunk (load-time hints)
-    size_t ingest_first_n = 0;
+    bool hints_pending = false;           // no ingested chunk has held a data line yet
+    const char *last_schedule = "";       // the schedule of the last region call (note_schedule)
     std::vector<std::pair<size_t, hipEvent_t>> ingest_ev;  // (input bytes copied once it fires, event)
     std::vector<hipEvent_t> ingest_ev_free;
     // index
@@ -104,7 +107,12 @@ struct vcfxg_ctx {
     // ulps either side of the device p-value that must print the same digits (test hook: a
     // huge value sends every exp()-derived row to the host)
     int64_t hwe_ulps = getenv("VCFXG_HWE_ULPS") ? atoll(getenv("VCFXG_HWE_ULPS")) : 16;
-    int64_t walk_chunk = getenv("VCFXG_WALK_CHUNK") ? atol(getenv("VCFXG_WALK_CHUNK")) : 128 * 1024;
+    // (an override is clamped to [4 KiB, 8 MiB]: the AF walk packs a walker's GT-line count in
+    // 16 bits, and its line capacity 2 * chunk / hint_line + 16 stays below 2^15 for the
+    // >= 512 B records the walk takes)
+    int64_t walk_chunk = getenv("VCFXG_WALK_CHUNK")
+                             ? std::min<int64_t>(std::max<int64_t>(atol(getenv("VCFXG_WALK_CHUNK")), 4096), 8 << 20)
+                             : 128 * 1024;
     bool walk_overflowed = false;  // the last walk run overflowed: two-sweep schedule
     bool dose_head_failed = false;  // a dosage head walk's rows failed the check (this input)
     // host hints taken at load time from the first data line: its '\n' distance from the
@@ -129,7 +137,7 @@ struct vcfxg_ctx {
     // the first records average >= 512 B, 1 = the walk always, -1 = index + per-tool kernels
     int fq_path = getenv("VCFXG_FQ_WALK") ? atoi(getenv("VCFXG_FQ_WALK")) : 0;
     std::vector<uint8_t> ld_gflag_host;  // per 128-variant group: all complete
-    uint64_t ld_m = 0, ld_prefix_bytes = 0;
+    uint64_t ld_m = 0, ld_prefix_bytes = 0, ld_np = 0;
     int ld_kpad = 64, ld_ns = 0, ld_kp4 = 64;
     bool ld_chrom_ids = false;
     std::vector<uint32_t> ld_cid_host, ld_blocks_host;
@@ -363,21 +371,43 @@ int vcfxg_reset_kernel_stats(vcfxg_ctx *c) {
     return VCFXG_OK;
 }
 
-// the walk AF path's hints from the host copy: skip '#' lines, then the first data line's
-// '\n' distance from the byte after its 9th tab and the mean length of up to 256 lines
-static void load_hints(vcfxg_ctx *c, const char *h, size_t n) {
+// the walk paths' hints from the host bytes of the input's first chunk holding data lines:
+// skip '#' lines, then the first data line's '\n' distance from the byte after its 9th tab and
+// the mean length of up to 256 lines.  Called on each ingested chunk until one holds data: a
+// chunk of '#' lines only that ends at a line end (a shard view's header [0, H), a pipe's head)
+// returns false and the next chunk is looked at.  Chunks are read while the caller still owns
+// them (a pipe's staging slot is reused after the call).
+static void reset_hints(vcfxg_ctx *c) {
     c->hint_span = 0;
     c->hint_line = 0;
     c->hint_gt_only = false;
     c->hint_gt_first = false;
     c->walk_overflowed = false;
     c->dose_head_failed = false;
+    if (!getenv("VCFXG_WALK_CHUNK")) c->walk_chunk = 128 * 1024;
+}
+
+// the schedule a region call took (vcfxg_last_schedule; VCFXG_SCHEDULE_LOG=path appends one
+// line per call: tests check which path sharded ranks and fresh contexts run)
+static void note_schedule(vcfxg_ctx *c, const char *what) {
+    c->last_schedule = what;
+    static const char *log = getenv("VCFXG_SCHEDULE_LOG");
+    if (!log) return;
+    const int fd = ::open(log, O_WRONLY | O_APPEND | O_CREAT | O_CLOEXEC, 0644);
+    if (fd < 0) return;
+    const std::string l = std::string(what) + "\n";
+    (void)!::write(fd, l.data(), l.size());
+    ::close(fd);
+}
+
+static bool load_hints(vcfxg_ctx *c, const char *h, size_t n) {
     size_t p = 0;
     while (p < n && h[p] == '#') {
         const void *q = memchr(h + p, '\n', n - p);
-        if (!q) return;
+        if (!q) return true;  // a '#' line cut by the chunk end: no hints
         p = (size_t)((const char *)q - h) + 1;
     }
+    if (p >= n) return false;  // header lines only: the data starts in a later chunk
     const size_t first = p;
     int lines = 0;
     while (p < n && lines < 256) {
@@ -411,6 +441,7 @@ static void load_hints(vcfxg_ctx *c, const char *h, size_t n) {
         c->walk_chunk = c->hint_line > 16 * 1024
                             ? std::min<int64_t>(((16 * c->hint_line + 65535) / 65536) * 65536, 4 << 20)
                             : 128 * 1024;
+    return true;
 }
 
 int vcfxg_load_host(vcfxg_ctx *c, const char *host, size_t n) {
@@ -430,8 +461,8 @@ int vcfxg_ingest_begin(vcfxg_ctx *c, size_t size_hint) {
     c->indexed = false;
     c->n = 0;
     c->ingesting = true;
-    c->ingest_first = nullptr;
-    c->ingest_first_n = 0;
+    reset_hints(c);
+    c->hints_pending = true;
     return VCFXG_OK;
 }
 
@@ -465,10 +496,7 @@ int vcfxg_ingest(vcfxg_ctx *c, const char *host, size_t n, int is_final_chunk) {
         HIPCHK(c, hipEventRecord(e, c->stream));
         c->ingest_ev.push_back({c->n + n, e});
     }
-    if (n && !c->ingest_first) {
-        c->ingest_first = host;
-        c->ingest_first_n = n;
-    }
+    if (n && c->hints_pending) c->hints_pending = !load_hints(c, host, n);
     c->n += n;
     if (n) c->last_byte = (unsigned char)host[n - 1];
     if (!is_final_chunk) return VCFXG_OK;
@@ -477,8 +505,7 @@ int vcfxg_ingest(vcfxg_ctx *c, const char *host, size_t n, int is_final_chunk) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (auto &pe : c->ingest_ev) c->ingest_ev_free.push_back(pe.second);
     c->ingest_ev.clear();
-    load_hints(c, c->ingest_first, c->ingest_first_n);
-    c->ingest_first = nullptr;
+    c->hints_pending = false;
     c->ingesting = false;
     c->loaded = true;
     c->indexed = false;
@@ -754,6 +781,10 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
         return r ? r : vcfxg_allele_freq(c, mode, out);
     }
     const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
+    if (cap_w > 0xFFFF) {  // (wgt packs the GT-line count in 16 bits; see walk_chunk)
+        c->err = "af walk: walker line capacity over 65535";
+        return VCFXG_E_ARG;
+    }
     const uint64_t cap = (uint64_t)nw * cap_w;
     int r = ensure(c, c->wk_le, 8 * cap);
     if (!r) r = ensure(c, c->wk_alt, 4 * cap);
@@ -895,22 +926,24 @@ int vcfxg_allele_freq_region(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_su
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
-    if (c->af_path == 7) return af_region_walk(c, data_start, mode, out);
-    if (c->af_path == 8) return af_region_async(c, data_start, mode, out);
+    if (c->af_path == 7) return note_schedule(c, "af_walk"), af_region_walk(c, data_start, mode, out);
+    if (c->af_path == 8) return note_schedule(c, "af_two_sweep"), af_region_async(c, data_start, mode, out);
     if (c->af_path == 3) {  // synchronous two-sweep schedule: index + record kernels
+        note_schedule(c, "af_two_sweep_sync");
         int r = vcfxg_index(c, data_start, nullptr);
         return r ? r : vcfxg_allele_freq(c, mode, out);
     }
     // records of >= 512 B on average (a GT-dense VCF): the walk schedule, no index sweep; the
     // GT-first walk for "GT:..." records (VCFXG_AF_GF_WALK=0: the index sweep + per-line sweep)
-    if (c->hint_line >= 512 && c->hint_gt_only && !c->walk_overflowed) return af_region_walk(c, data_start, mode, out);
+    if (c->hint_line >= 512 && c->hint_gt_only && !c->walk_overflowed)
+        return note_schedule(c, "af_walk"), af_region_walk(c, data_start, mode, out);
     static const bool gf_ok = [] {
         const char *e = getenv("VCFXG_AF_GF_WALK");
         return !(e && e[0] == '0');
     }();
     if (gf_ok && c->hint_line >= 512 && c->hint_gt_first && !c->walk_overflowed)
-        return af_region_walk(c, data_start, mode, out, true);
-    return af_region_async(c, data_start, mode, out);
+        return note_schedule(c, "af_walk_gt_first"), af_region_walk(c, data_start, mode, out, true);
+    return note_schedule(c, "af_two_sweep"), af_region_async(c, data_start, mode, out);
 }
 
 static int af_rows(vcfxg_ctx *c, int mode, vcfxg_summary *out) {
@@ -1220,6 +1253,7 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
     const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n, C = c->walk_chunk;
     const int64_t nw = vcfxg::af_walkers(lo, hi, C);
     if (!nw || c->fq_path < 0 || c->walk_overflowed || (c->fq_path == 0 && c->hint_line < 512)) {
+        note_schedule(c, "fq_two_sweep");
         int r = vcfxg_index(c, data_start, nullptr);
         if (r) return r;
         if (what == vcfxg::kFqRF) return vcfxg_record_filter(c, crit, n, and_logic, out);
@@ -1227,6 +1261,7 @@ static int fq_region(vcfxg_ctx *c, size_t data_start, int what, const vcfxg_crit
         if (what == vcfxg::kFqNR) return vcfxg_nonref_filter(c, gq_strip_cr ? VCFXG_MODE_FILE : VCFXG_MODE_STDIN, out);
         return vcfxg_filter_query(c, crit, n, and_logic, query, qlen, strict, out);
     }
+    note_schedule(c, "fq_walk");
     const bool nr = what == vcfxg::kFqNR;  // nonref_filter: the query's walk with its own reducer
     const bool rf = !nr && (what & vcfxg::kFqRF) != 0, gq = nr || (what & vcfxg::kFqGQ) != 0;
     const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
@@ -1521,6 +1556,10 @@ static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *
     const int64_t C = c->walk_chunk;
     const int64_t nw = vcfxg::af_walkers(lo, hi, C);
     const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
+    if (cap_w > 0xFFFF) {  // (wgt packs the GT-line count in 16 bits; see walk_chunk)
+        c->err = "af walk: walker line capacity over 65535";
+        return VCFXG_E_ARG;
+    }
     const uint64_t cap = (uint64_t)nw * cap_w;
     int r = ensure(c, c->wk_le, 8 * cap);
     if (!r) r = ensure(c, c->wk_alt, 4 * cap);
@@ -2350,8 +2389,25 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     HIPCHK(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
     c->text_bytes = tb;
+    c->ld_np = np;
     if (n_pairs) *n_pairs = np;
     if (text_bytes) *text_bytes = tb;
+    return VCFXG_OK;
+}
+
+int vcfxg_ld_fetch_pairs(vcfxg_ctx *c, uint64_t first, uint64_t count, uint32_t *vi, uint32_t *vj, double *r2) {
+    if (!c || first > c->ld_np || count > c->ld_np - first) return VCFXG_E_ARG;
+    if (!count) return VCFXG_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<vcfxg::LdPair> h(count);
+    HIPCHK(c, hipMemcpyAsync(h.data(), P<vcfxg::LdPair>(c->ld_pairs) + first, sizeof(vcfxg::LdPair) * count,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (uint64_t k = 0; k < count; ++k) {
+        if (vi) vi[k] = h[k].i;
+        if (vj) vj[k] = h[k].j;
+        if (r2) r2[k] = h[k].r2;
+    }
     return VCFXG_OK;
 }
 
@@ -2484,15 +2540,14 @@ int vcfxg_shard_cuts(const char *data, size_t n, size_t lo, int world, uint64_t 
 }
 
 // ---- rank cliques: the count all-reduce of the in-process multi-GPU drop-in ------------------
-// RCCL comes from librccl at run time (dlopen: a single-GPU process never loads it); its symbols
-// are the ones of rccl.h (ncclCommInitAll, ncclAllReduce, ncclCommDestroy).
+// RCCL comes from librccl at run time (dlopen: a single-GPU process never loads it).  rccl.h is
+// included for its declarations only: the function pointer types and the enum values below are
+// checked against it at compile time (no link dependency).
 namespace {
-typedef void *nccl_comm_t;
-typedef int (*nccl_init_all_f)(nccl_comm_t *, int, const int *);
-typedef int (*nccl_allreduce_f)(const void *, void *, size_t, int, int, nccl_comm_t, hipStream_t);
-typedef int (*nccl_destroy_f)(nccl_comm_t);
-typedef const char *(*nccl_errstr_f)(int);
-constexpr int kNcclUint64 = 5, kNcclSum = 0;
+typedef decltype(&ncclCommInitAll) nccl_init_all_f;
+typedef decltype(&ncclAllReduce) nccl_allreduce_f;
+typedef decltype(&ncclCommDestroy) nccl_destroy_f;
+static_assert(ncclUint64 == 5 && ncclSum == 0 && ncclSuccess == 0, "rccl.h enum values");
 constexpr size_t kCommSlots = 64;  // u64 values per all-reduce
 }  // namespace
 
@@ -2503,14 +2558,17 @@ struct vcfxg_comm {
     void *lib = nullptr;
     nccl_allreduce_f allreduce = nullptr;
     nccl_destroy_f destroy = nullptr;
-    std::vector<nccl_comm_t> comms;
+    std::vector<ncclComm_t> comms;
     std::vector<uint64_t *> dbuf;  // per rank: kCommSlots u64 on its device
-    // host reduction (several ranks on one device)
+    // host side: every all-reduce is first a host reduction + vote of all ranks (the RCCL result
+    // is checked against it, and no rank enters the collective unless every rank staged its values)
     std::mutex mu;
     std::condition_variable cv;
     uint64_t gen = 0;
-    int arrived = 0;
+    int arrived = 0, failed = 0;
+    bool result_failed = false;
     std::vector<uint64_t> acc, result;
+    uint64_t rccl_calls = 0, rccl_mismatch = 0;
 };
 
 int vcfxg_comm_init(vcfxg_ctx *const *ctxs, int n, vcfxg_comm **out) {
@@ -2528,15 +2586,19 @@ int vcfxg_comm_init(vcfxg_ctx *const *ctxs, int n, vcfxg_comm **out) {
         dev[r] = ctxs[r]->device;
         for (int q = 0; q < r; q++) distinct = distinct && dev[q] != dev[r];
     }
+    // RCCL over n distinct devices; VCFX_RCCL=1 also forms a one-rank clique (a one-GPU box runs
+    // the whole RCCL path: init, the collective on the rank's stream, destroy); VCFX_RCCL=0 never.
+    // RCCL cannot put two ranks on one device, so ranks sharing one reduce on the host.
     const char *e = getenv("VCFX_RCCL");
-    if (distinct && !(e && e[0] == '0')) {
+    const bool want = (distinct && !(e && e[0] == '0')) || (n == 1 && e && e[0] == '1');
+    if (want) {
         c->lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
         if (!c->lib) c->lib = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
         nccl_init_all_f init = c->lib ? (nccl_init_all_f)dlsym(c->lib, "ncclCommInitAll") : nullptr;
         c->allreduce = c->lib ? (nccl_allreduce_f)dlsym(c->lib, "ncclAllReduce") : nullptr;
         c->destroy = c->lib ? (nccl_destroy_f)dlsym(c->lib, "ncclCommDestroy") : nullptr;
         c->comms.assign(n, nullptr);
-        if (!init || !c->allreduce || !c->destroy || init(c->comms.data(), n, dev.data()) != 0) {
+        if (!init || !c->allreduce || !c->destroy || init(c->comms.data(), n, dev.data()) != ncclSuccess) {
             if (c->lib) dlclose(c->lib);
             c->lib = nullptr;
             c->allreduce = nullptr;
@@ -2547,8 +2609,11 @@ int vcfxg_comm_init(vcfxg_ctx *const *ctxs, int n, vcfxg_comm **out) {
         }
         c->dbuf.assign(n, nullptr);
         for (int r = 0; r < n; r++) {
-            HIPCHK(ctxs[r], hipSetDevice(dev[r]));
-            HIPCHK(ctxs[r], hipMalloc((void **)&c->dbuf[r], kCommSlots * 8));
+            if (hipSetDevice(dev[r]) != hipSuccess || hipMalloc((void **)&c->dbuf[r], kCommSlots * 8) != hipSuccess) {
+                ctxs[r]->err = "vcfxg_comm_init: no device buffer for the all-reduce";
+                vcfxg_comm_destroy(c);
+                return VCFXG_E_HIP;
+            }
         }
     }
     c->acc.assign(kCommSlots, 0);
@@ -2559,34 +2624,82 @@ int vcfxg_comm_init(vcfxg_ctx *const *ctxs, int n, vcfxg_comm **out) {
 
 int vcfxg_comm_uses_rccl(const vcfxg_comm *c) { return c && c->allreduce ? 1 : 0; }
 
+const char *vcfxg_last_schedule(const vcfxg_ctx *c) { return c ? c->last_schedule : ""; }
+
+int vcfxg_comm_rccl_stats(vcfxg_comm *c, uint64_t *calls, uint64_t *mismatches) {
+    if (!c) return VCFXG_E_ARG;
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (calls) *calls = c->rccl_calls;
+    if (mismatches) *mismatches = c->rccl_mismatch;
+    return VCFXG_OK;
+}
+
 int vcfxg_comm_allreduce_u64(vcfxg_comm *c, int rank, uint64_t *vals, size_t count) {
     if (!c || rank < 0 || rank >= c->n || (!vals && count) || count > kCommSlots) return VCFXG_E_ARG;
-    if (c->allreduce) {  // RCCL over the devices (xGMI), on the rank's own stream
-        vcfxg_ctx *x = c->ctx[rank];
-        HIPCHK(x, hipSetDevice(x->device));
-        HIPCHK(x, hipMemcpyAsync(c->dbuf[rank], vals, 8 * count, hipMemcpyHostToDevice, x->stream));
-        if (c->allreduce(c->dbuf[rank], c->dbuf[rank], count, kNcclUint64, kNcclSum, c->comms[rank], x->stream) != 0) {
-            x->err = "ncclAllReduce failed";
-            return VCFXG_E_HIP;
+    vcfxg_ctx *x = c->ctx[rank];
+    // 1. stage the values on the rank's device (RCCL); a rank whose device call fails votes "no"
+    bool ok = true;
+    if (c->allreduce) {
+        ok = hipSetDevice(x->device) == hipSuccess &&
+             hipMemcpyAsync(c->dbuf[rank], vals, 8 * count, hipMemcpyHostToDevice, x->stream) == hipSuccess &&
+             hipStreamSynchronize(x->stream) == hipSuccess;
+        if (!ok) x->err = "vcfxg_comm_allreduce_u64: staging the values on the device failed";
+    }
+    // 2. host reduction + vote: the last rank to arrive publishes the sums of this generation
+    std::vector<uint64_t> host(count);
+    bool any_failed;
+    {
+        std::unique_lock<std::mutex> lk(c->mu);
+        const uint64_t g = c->gen;
+        for (size_t k = 0; k < count; k++) c->acc[k] += vals[k];
+        if (!ok) c->failed++;
+        if (++c->arrived == c->n) {
+            c->result = c->acc;
+            c->result_failed = c->failed != 0;
+            std::fill(c->acc.begin(), c->acc.end(), 0);
+            c->arrived = c->failed = 0;
+            c->gen++;
+            c->cv.notify_all();
+        } else {
+            c->cv.wait(lk, [&] { return c->gen != g; });
         }
-        HIPCHK(x, hipMemcpyAsync(vals, c->dbuf[rank], 8 * count, hipMemcpyDeviceToHost, x->stream));
-        HIPCHK(x, hipStreamSynchronize(x->stream));
+        std::copy(c->result.begin(), c->result.begin() + (long)count, host.begin());
+        any_failed = c->result_failed;
+    }
+    if (!c->allreduce) {
+        std::copy(host.begin(), host.end(), vals);
         return VCFXG_OK;
     }
-    // host: the last rank to arrive publishes the sums of this generation
-    std::unique_lock<std::mutex> lk(c->mu);
-    const uint64_t g = c->gen;
-    for (size_t k = 0; k < count; k++) c->acc[k] += vals[k];
-    if (++c->arrived == c->n) {
-        c->result = c->acc;
-        std::fill(c->acc.begin(), c->acc.end(), 0);
-        c->arrived = 0;
-        c->gen++;
-        c->cv.notify_all();
-    } else {
-        c->cv.wait(lk, [&] { return c->gen != g; });
+    if (any_failed) {  // no rank enters the collective; the host sums stand, the failure is reported
+        std::copy(host.begin(), host.end(), vals);
+        if (ok) x->err = "vcfxg_comm_allreduce_u64: another rank failed to stage its values";
+        return VCFXG_E_HIP;
     }
-    for (size_t k = 0; k < count; k++) vals[k] = c->result[k];
+    // 3. RCCL over the devices (xGMI), on the rank's own stream; checked against the host sums
+    std::vector<uint64_t> dv(count);
+    if (c->allreduce(c->dbuf[rank], c->dbuf[rank], count, ncclUint64, ncclSum, c->comms[rank], x->stream) !=
+        ncclSuccess) {
+        x->err = "ncclAllReduce failed";
+        std::copy(host.begin(), host.end(), vals);
+        return VCFXG_E_HIP;
+    }
+    if (hipMemcpyAsync(dv.data(), c->dbuf[rank], 8 * count, hipMemcpyDeviceToHost, x->stream) != hipSuccess ||
+        hipStreamSynchronize(x->stream) != hipSuccess) {
+        x->err = "vcfxg_comm_allreduce_u64: reading the RCCL sums back failed";
+        std::copy(host.begin(), host.end(), vals);
+        return VCFXG_E_HIP;
+    }
+    const bool same = dv == host;
+    {
+        std::lock_guard<std::mutex> lk(c->mu);
+        c->rccl_calls++;
+        if (!same) c->rccl_mismatch++;
+    }
+    std::copy(host.begin(), host.end(), vals);
+    if (!same) {
+        x->err = "vcfxg_comm_allreduce_u64: the RCCL sums differ from the host reduction";
+        return VCFXG_E_HIP;
+    }
     return VCFXG_OK;
 }
 

@@ -5,8 +5,9 @@
 // the cuts; each rank thread runs the tool itself on its VIEW of the file -- the header bytes
 // [0, H) (through the '#CHROM' line) and its records [cut_r, cut_r+1) -- cut at i*size/N and
 // advanced past the next '\n', the reference's own split (VCFX_allele_counter.cpp:889-901,
-// computed by vcfxg_shard_cuts).  The ranks' stdout goes to per-rank memory files and is
-// written in rank order (in parallel at exclusive-scan offsets when stdout is a regular file);
+// computed by vcfxg_shard_cuts).  Rank 0 writes its stdout straight to the output; ranks > 0
+// write per-rank memory files that follow in rank order (on a pipe each as soon as it and the
+// ranks before it are done; on a regular file in parallel at exclusive-scan offsets);
 // their stderr too, ranks > 0 from the point where their record phase began (the argument and
 // header messages are rank 0's).  Each rank leaves its counters (AF's "Processed V variants
 // from L data lines", missing_detector's totals) in its ShardRank; they are all-reduced over
@@ -306,11 +307,22 @@ extern "C" int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, i
             return 1;
         }
     }
+    // rank 0 writes its stdout straight to out_fd (its bytes come first whatever the other ranks
+    // do); ranks > 0 write memory files that follow it in rank order
+    struct stat ost;
+    const int ofl = fcntl(out_fd, F_GETFL);
+    const off_t start = lseek(out_fd, 0, SEEK_CUR);
+    const bool regular = fstat(out_fd, &ost) == 0 && S_ISREG(ost.st_mode) && start >= 0 && ofl >= 0 &&
+                         !(ofl & O_APPEND);
+    ::close(outs[0]);
+    outs[0] = -1;
     // ranks: open the context (in parallel), wait for the clique, run the tool, reduce
     std::mutex mu;
     std::condition_variable cv;
     int opened = 0;
     bool go = false;
+    std::vector<char> done((size_t)W, 0);
+    std::vector<int> red_rc((size_t)W, VCFXG_OK);
     vcfxg_comm *comm = nullptr;
     std::vector<std::thread> th;
     for (int r = 0; r < W; r++)
@@ -332,10 +344,17 @@ extern "C" int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, i
             }
             av.push_back(nullptr);
             t_shard = &s;
-            rc[(size_t)r] = vcfx_tool_main(tool, (int)av.size() - 1, av.data(), in_fd, outs[(size_t)r], s.err_fd);
+            rc[(size_t)r] = vcfx_tool_main(tool, (int)av.size() - 1, av.data(), in_fd, r ? outs[(size_t)r] : out_fd,
+                                           s.err_fd);
             t_shard = nullptr;
-            // every rank takes part, whatever its run did (no rank can be left waiting)
-            if (comm) vcfxg_comm_allreduce_u64(comm, r, s.cnt, 8);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                done[(size_t)r] = 1;
+                cv.notify_all();
+            }
+            // every rank takes part, whatever its run did (no rank can be left waiting: the clique
+            // votes on the host before any rank enters the collective)
+            if (comm) red_rc[(size_t)r] = vcfxg_comm_allreduce_u64(comm, r, s.cnt, 8);
         });
     {
         std::unique_lock<std::mutex> lk(mu);
@@ -346,11 +365,27 @@ extern "C" int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, i
         go = true;
         cv.notify_all();
     }
+    // a pipe / terminal: each rank's bytes as soon as it and every rank before it are done
+    bool streamed_ok = true;
+    int streamed = 0;
+    if (!regular) {
+        for (int r = 1; r < W; r++) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return done[0] && done[(size_t)r]; });
+            }
+            if (sr[0].err_mark < 0) break;  // rank 0 stopped before its records: its streams alone
+            streamed_ok = copy_range(outs[(size_t)r], 0, fd_size(outs[(size_t)r]), out_fd) && streamed_ok;
+            streamed = r;
+        }
+    }
     for (auto &t : th) t.join();
     phase("ranks done");
     uint64_t sum[8] = {};
+    bool red_ok = true;
     if (comm) {
         for (int k = 0; k < 8; k++) sum[k] = sr[0].cnt[k];  // (every rank holds the sums)
+        for (int r = 0; r < W; r++) red_ok = red_ok && red_rc[(size_t)r] == VCFXG_OK;
     } else {
         for (int r = 0; r < W; r++)
             for (int k = 0; k < 8; k++) sum[k] += sr[(size_t)r].cnt[k];
@@ -359,24 +394,20 @@ extern "C" int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, i
     const ShardRank &s0 = sr[0];
     int ret = 0;
     if (s0.err_mark < 0) {  // rank 0 stopped before its records (arguments, open): its streams alone
-        copy_range(outs[0], 0, fd_size(outs[0]), out_fd);
         copy_range(s0.err_fd, 0, fd_size(s0.err_fd), err_fd);
         ret = rc[0];
     } else {
-        std::vector<size_t> osz((size_t)W), ooff((size_t)W + 1, 0);
-        for (int r = 0; r < W; r++) {
-            osz[(size_t)r] = fd_size(outs[(size_t)r]);
-            ooff[(size_t)r + 1] = ooff[(size_t)r] + osz[(size_t)r];
-        }
-        struct stat st;
-        const int fl = fcntl(out_fd, F_GETFL);
-        const off_t start = lseek(out_fd, 0, SEEK_CUR);
-        const bool regular = fstat(out_fd, &st) == 0 && S_ISREG(st.st_mode) && start >= 0 && fl >= 0 &&
-                             !(fl & O_APPEND);
-        if (regular && W > 1) {  // every rank's bytes at their offset, in parallel
+        if (regular && W > 1) {  // ranks > 0: their bytes at their offsets after rank 0's, in parallel
+            const off_t end0 = lseek(out_fd, 0, SEEK_CUR);
+            std::vector<size_t> osz((size_t)W, 0), ooff((size_t)W + 1, 0);
+            ooff[1] = end0 >= start ? (size_t)(end0 - start) : 0;
+            for (int r = 1; r < W; r++) {
+                osz[(size_t)r] = fd_size(outs[(size_t)r]);
+                ooff[(size_t)r + 1] = ooff[(size_t)r] + osz[(size_t)r];
+            }
             std::vector<std::thread> wt;
-            std::atomic<bool> ok{true};
-            for (int r = 0; r < W; r++)
+            std::atomic<bool> ok{end0 >= start};
+            for (int r = 1; r < W; r++)
                 wt.emplace_back([&, r] {
                     const size_t n = osz[(size_t)r];
                     if (!n) return;
@@ -402,19 +433,45 @@ extern "C" int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, i
             lseek(out_fd, start + (off_t)ooff[(size_t)W], SEEK_SET);
             if (!ok) ret = 1;
         } else {
-            for (int r = 0; r < W; r++) copy_range(outs[(size_t)r], 0, osz[(size_t)r], out_fd);
+            for (int r = streamed + 1; r < W; r++)
+                streamed_ok = copy_range(outs[(size_t)r], 0, fd_size(outs[(size_t)r]), out_fd) && streamed_ok;
+            if (!streamed_ok) ret = 1;
         }
         for (int r = 0; r < W; r++) {
             const ShardRank &s = sr[(size_t)r];
-            const size_t from = r == 0 ? 0 : (size_t)std::max<long long>(s.err_mark, 0);
             const size_t n = fd_size(s.err_fd);
+            if (r > 0 && s.err_mark < 0) {
+                // a rank that stopped before its records where rank 0 did not: its argument /
+                // header messages are rank 0's already; only its last line (the error) is its own
+                std::string e(n, '\0');
+                if (n && pread(s.err_fd, &e[0], n, 0) == (ssize_t)n) {
+                    size_t end = e.size();
+                    while (end && e[end - 1] == '\n') end--;
+                    const size_t b = e.rfind('\n', end ? end - 1 : 0);
+                    const size_t from = (b == std::string::npos || end == 0) ? 0 : b + 1;
+                    if (end > from) write_str(err_fd, e.substr(from, end - from) + "\n");
+                }
+                continue;
+            }
+            const size_t from = r == 0 ? 0 : (size_t)s.err_mark;
             if (n > from) copy_range(s.err_fd, from, n - from, err_fd);
+        }
+        if (!red_ok) {
+            // the summary below is the host reduction's (always computed); the RCCL path failed
+            std::string e = "Error: vcfx_amd: the ranks' count all-reduce failed";
+            for (int r = 0; r < W; r++)
+                if (red_rc[(size_t)r] != VCFXG_OK && ctx[(size_t)r]) {
+                    e += std::string(": ") + vcfxg_last_error(ctx[(size_t)r]);
+                    break;
+                }
+            write_str(err_fd, e + "\n");
+            ret = 1;
         }
         if (s0.summary) write_str(err_fd, s0.summary(sum));
         for (int r = 0; r < W && !ret; r++) ret = rc[(size_t)r];
     }
     for (int r = 0; r < W; r++) {
-        ::close(outs[(size_t)r]);
+        if (outs[(size_t)r] >= 0) ::close(outs[(size_t)r]);
         ::close(sr[(size_t)r].err_fd);
     }
     if (!g_process_exit_fast) {  // (an executable ends right after: the runtime drops them)

@@ -76,6 +76,8 @@ SIGNATURES = {
     "vcfxg_comm_allreduce_u64": (_I, [_VP, _I, _VP, _S]),
     "vcfxg_comm_uses_rccl": (_I, [_VP]),
     "vcfxg_comm_destroy": (None, [_VP]),
+    "vcfxg_comm_rccl_stats": (_I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
+    "vcfxg_last_schedule": (_P, [_VP]),
     "vcfxg_haplotype_phaser": (_I, [_VP, _S, _I, ctypes.c_double, ctypes.c_uint32, ctypes.POINTER(Summary)]),
     "vcfxg_phaser_variants": (_I, [_VP, _VP, _VP, _VP]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
@@ -83,6 +85,7 @@ SIGNATURES = {
     "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_stream_chunk": (_I, [_VP, _U64, _U64, _U64, ctypes.c_double, _I, ctypes.POINTER(_U64),
                                    ctypes.POINTER(_U64)]),
+    "vcfxg_ld_fetch_pairs": (_I, [_VP, _U64, _U64, _VP, _VP, _VP]),
     "vcfxg_selftest_mfma_i8": (_I, [_VP, ctypes.POINTER(_I)]),
     "vcfxg_selftest_mfma_fp4": (_I, [_VP, ctypes.POINTER(_I)]),
     "vcfxg_filter_query": (_I, [_VP, _VP, _I, _I, _P, _S, _I, ctypes.POINTER(Summary)]),
@@ -354,6 +357,16 @@ class Engine:
         self._chk(self.L.vcfxg_ld_stream_chunk(self.h, j0, j1, window, threshold, max_dist, ctypes.byref(npairs),
                                                ctypes.byref(tb)), "ld_stream_chunk")
         return npairs.value, tb.value
+
+    def ld_pairs(self, first, count):
+        """(i, j, r2) numpy arrays of pairs [first, first + count) of the last ld_stream_chunk."""
+        import numpy as np
+        vi = np.zeros(count, np.uint32)
+        vj = np.zeros(count, np.uint32)
+        r2 = np.zeros(count, np.float64)
+        self._chk(self.L.vcfxg_ld_fetch_pairs(self.h, first, count, vi.ctypes.data, vj.ctypes.data, r2.ctypes.data),
+                  "ld_fetch_pairs")
+        return vi, vj, r2
 
     def selftest_mfma_i8(self):
         m = ctypes.c_int()
