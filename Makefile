@@ -89,7 +89,7 @@ clean:
 SAN := $(B)/san
 SANFLAGS := -O1 -g -fno-omit-frame-pointer -std=c++17 -Iinclude -I$(HOST_SRC)
 SAN_HOST_SRC := tests/host_san_test.cpp $(HOST_SRC)/hostio.cpp $(HOST_SRC)/gz.cpp
-sanitize: $(SAN)/host_san_asan $(SAN)/host_san_tsan $(SAN)/core_api_asan
+sanitize: $(SAN)/host_san_asan $(SAN)/host_san_tsan $(SAN)/core_api_asan $(SAN)/shard_tsan $(SAN)/shard_asan
 $(SAN)/host_san_asan: $(SAN_HOST_SRC) $(wildcard $(HOST_SRC)/*.h) $(B)/libvcfx_gpu.so
 	@mkdir -p $(dir $@)
 	$(CXX) $(SANFLAGS) -fsanitize=address,undefined -fno-sanitize-recover=undefined -o $@ $(SAN_HOST_SRC) \
@@ -101,4 +101,15 @@ $(SAN)/core_api_asan: tests/core_api_test.cpp $(HOST_SRC)/vcfx_core.cpp include/
 	@mkdir -p $(dir $@)
 	$(CXX) $(SANFLAGS) -fsanitize=address,undefined -fno-sanitize-recover=undefined \
 	    -o $@ tests/core_api_test.cpp $(HOST_SRC)/vcfx_core.cpp -lz
+# the in-process multi-GPU runner's host side (rank threads, getopt lock, thread-local ShardRank,
+# the ordered output writer, the clique) with vcfxg_* replaced by a host stand-in
+SHARD_SAN_SRC := tests/shard_tsan_stub.cpp vcfx_amd/csrc/tools/tool_shard_main.cpp \
+    vcfx_amd/csrc/tools/tool_allele_freq_calc.cpp $(HOST_SRC)/hostio.cpp $(HOST_SRC)/gz.cpp
+$(SAN)/shard_tsan: $(SHARD_SAN_SRC) $(wildcard $(HOST_SRC)/*.h) vcfx_amd/csrc/tools/tools.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(SANFLAGS) -Ivcfx_amd/csrc/tools -fsanitize=thread -o $@ $(SHARD_SAN_SRC) -lz -lpthread
+$(SAN)/shard_asan: $(SHARD_SAN_SRC) $(wildcard $(HOST_SRC)/*.h) vcfx_amd/csrc/tools/tools.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(SANFLAGS) -Ivcfx_amd/csrc/tools -fsanitize=address,undefined -fno-sanitize-recover=undefined \
+	    -o $@ $(SHARD_SAN_SRC) -lz -lpthread
 .PHONY: sanitize

@@ -88,3 +88,42 @@ def test_core_api_under_asan_ubsan(built, tmp_path):
     assert r.returncode == 0, err[-3000:]
     assert "Sanitizer" not in err and "runtime error" not in err, err[-3000:]
     assert r.stdout.decode() == open(GOLD).read()
+
+
+@pytest.mark.parametrize("kind", ["tsan", "asan"])
+def test_shard_runner_under_sanitizer(built, tmp_path, kind):
+    """The in-process multi-GPU runner's host side (tool_shard_main.cpp: rank threads, the getopt
+    lock, the thread-local ShardRank overrides, rank 0 writing straight to stdout and the ordered
+    writer of the other ranks, the clique's reduction) with the real AF tool and input layer and
+    vcfxg_* replaced by a host stand-in (tests/shard_tsan_stub.cpp): VCFX_NGPU = 2..8 ranks over
+    2 stub devices, stdout a regular file and a pipe, equal to the one-context run; a rank whose
+    context fails to open reports its rank and device, exits 1 and prints no partial summary."""
+    p = str(tmp_path / "a.vcf")
+    open(p, "wb").write(synth.generate(3000, 50, 7, 0, 0.01, 0, 0.1, 0))
+    exe = os.path.join(built, "shard_" + kind)
+    env = _env({"TSAN_OPTIONS": "halt_on_error=1:second_deadlock_stack=1",
+                "ASAN_OPTIONS": "detect_leaks=0", "UBSAN_OPTIONS": "print_stacktrace=1"})
+
+    def run(ngpu, pipe=False, **extra):
+        e = dict(env, VCFX_NGPU=str(ngpu), **extra)
+        if pipe:
+            r = subprocess.run([exe, "VCFX_allele_freq_calc", "-i", p], capture_output=True, env=e, timeout=300)
+            return r.stdout, r.stderr, r.returncode
+        out = str(tmp_path / ("o%d" % ngpu))
+        with open(out, "wb") as fo:
+            r = subprocess.run([exe, "VCFX_allele_freq_calc", "-i", p], stdout=fo, stderr=subprocess.PIPE, env=e,
+                               timeout=300)
+        return open(out, "rb").read(), r.stderr, r.returncode
+
+    want = run(1)
+    assert want[2] == 0 and want[1].endswith(b"Processed 3000 variants from 3000 data lines\n"), want[1][-2000:]
+    for n in (2, 3, 8):
+        for pipe in (False, True):
+            got = run(n, pipe)
+            assert b"Sanitizer" not in got[1] and b"runtime error" not in got[1], got[1][-3000:]
+            assert got == want, (n, pipe, got[1][-500:])
+    got = run(4, True, VCFX_STUB_DEVICES="4", VCFX_STUB_FAIL_RANK="2")
+    assert b"Sanitizer" not in got[1], got[1][-3000:]
+    assert got[2] == 1
+    assert b"rank 2 of 4: no usable MI355X (gfx950) device 2" in got[1]
+    assert b"Processed" not in got[1].split(b"\n", 1)[1]

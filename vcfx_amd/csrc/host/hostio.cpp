@@ -126,7 +126,12 @@ vcfxg_ctx *gpu_quiet() {
 
 vcfxg_ctx *gpu(int err_fd) {
     vcfxg_ctx *c = gpu_quiet();
-    if (!c)
+    if (!c && t_shard)
+        write_str(err_fd, std::string("Error: vcfx_amd: rank ") + std::to_string(t_shard->rank) + " of " +
+                              std::to_string(t_shard->world) + ": no usable MI355X (gfx950) device " +
+                              std::to_string(t_shard->device) + " (vcfxg_open rc=" + std::to_string(t_shard->open_rc) +
+                              "); this build has no CPU path.\n");
+    else if (!c)
         write_str(err_fd, std::string("Error: vcfx_amd: no usable MI355X (gfx950) device ") + std::to_string(g_dev) +
                               " (vcfxg_open rc=" + std::to_string(g_rc) + "); this build has no CPU path.\n");
     return c;

@@ -85,6 +85,7 @@ struct Input {
 struct ShardRank {
     int rank = 0, world = 1;
     vcfxg_ctx *g = nullptr;                          // this rank's context
+    int device = 0, open_rc = 0;                     // its device and vcfxg_open's status
     unsigned long long h = 0, lo = 0, hi = 0;        // view: header [0, h) + records [lo, hi)
     size_t whole_bytes = 0;                          // the whole input file's size
     int err_fd = -1;                                 // this rank's stderr (a memfd)

@@ -328,7 +328,9 @@ extern "C" int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, i
     for (int r = 0; r < W; r++)
         th.emplace_back([&, r] {
             ShardRank &s = sr[(size_t)r];
-            open_rc[(size_t)r] = vcfxg_open(r % ndev, &ctx[(size_t)r]);
+            s.device = r % ndev;
+            open_rc[(size_t)r] = vcfxg_open(s.device, &ctx[(size_t)r]);
+            s.open_rc = open_rc[(size_t)r];
             {
                 std::unique_lock<std::mutex> lk(mu);
                 opened++;
@@ -467,7 +469,9 @@ extern "C" int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, i
             write_str(err_fd, e + "\n");
             ret = 1;
         }
-        if (s0.summary) write_str(err_fd, s0.summary(sum));
+        bool all_ok = true;  // (a failed rank's counts are missing: no summary of partial sums)
+        for (int r = 0; r < W; r++) all_ok = all_ok && rc[(size_t)r] == 0;
+        if (s0.summary && all_ok) write_str(err_fd, s0.summary(sum));
         for (int r = 0; r < W && !ret; r++) ret = rc[(size_t)r];
     }
     for (int r = 0; r < W; r++) {
