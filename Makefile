@@ -19,7 +19,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wno-unused-result -Iinclude -I$(HOST_SRC
 TOOL_OBJS := $(sort $(B)/obj/hostio.o $(B)/obj/gz.o $(patsubst $(TOOL_SRC)/%.cpp,$(B)/obj/%.o,$(wildcard $(TOOL_SRC)/tool_*.cpp)))
 TOOL_BINS := $(foreach t,$(TOOLS),$(B)/src/$(t)/$(t))
 
-all: $(B)/bin/vcfx_bgzf $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so \
+all: $(B)/bin/vcfx_bgzf $(B)/bin/vcfx_drain $(B)/bin/vcfx_pipe $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so \
      $(B)/libvcfx_core.so $(B)/libvcfx_core.a $(B)/libvcfx_record_filter.so $(B)/libvcfx_genotype_query.so
 
 $(B)/obj/%.o: $(HOST_SRC)/%.cpp $(wildcard $(HOST_SRC)/*.h) include/vcfx_gpu.h
@@ -56,6 +56,10 @@ $(B)/src/%: $(TOOL_SRC)/binary_main.cpp $(B)/libvcfx_tools.so
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -DVCFX_TOOL_NAME='"$(notdir $@)"' -o $@ $< -L$(B) -lvcfx_tools -lvcfx_gpu -Wl,-rpath,'$$ORIGIN/../..'
 
+$(B)/bin/vcfx_pipe: $(TOOL_SRC)/pipe_main.cpp $(B)/libvcfx_tools.so
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(B) -lvcfx_tools -lvcfx_gpu -Wl,-rpath,'$$ORIGIN/..'
+
 $(B)/obj/vcfxg_%.o: $(GPU_SRC)/vcfxg_%.hip $(wildcard $(GPU_SRC)/*.h) include/vcfx_gpu.h
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -74,6 +78,10 @@ $(B)/bin/vcfx_synth: vcfx_amd/csrc/synth/vcfx_synth.c
 $(B)/bin/vcfx_bgzf: vcfx_amd/csrc/synth/vcfx_bgzf.c
 	@mkdir -p $(dir $@)
 	$(CC) -O2 -o $@ $< -lz -lpthread
+
+$(B)/bin/vcfx_drain: tools/microbench/pipe_drain.c
+	@mkdir -p $(dir $@)
+	$(CC) -O2 -o $@ $<
 
 $(B)/libvcfx_synth.so: vcfx_amd/csrc/synth/vcfx_synth.c
 	$(CC) -O2 -fPIC -shared -o $@ $< -lpthread

@@ -376,6 +376,9 @@ int vcfxg_comm_uses_rccl(const vcfxg_comm *comm);
 int vcfxg_comm_rccl_stats(vcfxg_comm *comm, uint64_t *calls, uint64_t *mismatches);
 void vcfxg_comm_destroy(vcfxg_comm *comm);
 
+/* occurrences of `byte` in the device input's bytes [from, n) (one HBM sweep; the fused chain
+ * of vcfx_pipe checks the records for '\r' with it) */
+int vcfxg_count_byte(vcfxg_ctx *ctx, uint64_t from, int byte, uint64_t *count);
 /* the schedule the last region call took ("af_walk", "af_walk_gt_first", "af_two_sweep", "fq_walk",
  * "fq_two_sweep", ...): a diagnostic for tests; VCFXG_SCHEDULE_LOG=path appends one line per call */
 const char *vcfxg_last_schedule(const vcfxg_ctx *ctx);

@@ -64,6 +64,15 @@ int vcfx_shard_plan(const char *tool, int argc, char **argv, int ngpu, uint64_t 
 int vcfx_pipeline_filter_query(const char *filter, const char *logic, const char *input, const char *query, int strict,
                                int gq_quiet, int in_fd, int out_fd, int err_fd);
 
+/* `vcfx_pipe 'VCFX_<t> [args] | VCFX_<t> [args] | ...'` (argc == 2: one chain string with shell
+ * quoting; argc > 2: the words, "|" separating stages): the reference's stdin -> stdout chaining
+ * (README.md:60-66) in one process on one device context, stdout byte-identical to the shell
+ * pipeline.  record_filter / genotype_query / nonref_filter stages ending in allele_freq_calc
+ * or a filter run fused (the input in HBM once, one walk per stage, decisions AND-ed); other
+ * chains run stage by stage in-process.  Exit code: the last stage's (VCFX_PIPEFAIL=1: the last
+ * non-zero); VCFX_PIPE_FUSED=0 forces the stage-by-stage schedule. */
+int vcfx_pipe_main(int argc, char **argv, int in_fd, int out_fd, int err_fd);
+
 #ifdef __cplusplus
 }
 #endif

@@ -115,6 +115,10 @@ CASES = {
     "ld3000_bench": ("ld3000", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
     "ld20k_bench": ("ld20k", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
     "ld20k_miss_bench": ("ld20k_miss", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
+    # a three-stage chain (vcfx_pipe's fused schedule): config 3's filter and query feeding AF
+    "pipeline_annot_af": ("annot", [[RF, "--filter", "FILTER==PASS;AF>=0.01", "-i", "{F}"], [GQ, "-g", "0/1"], [AF]],
+                          False),
+    "pipeline_annot_nr_af": ("annot", [[GQ, "-g", "0/1", "-i", "{F}"], [NR], [AF, "-q"]], False),
     "ld100k_tail_bench": ("ld100k_tail", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
     "ld100k_miss_tail_bench": ("ld100k_miss_tail", [[LD, "-q", "-w", "100000", "-t", "0.5", "-i", "{F}"]], False),
     "af_file_miss": ("chr21_miss", [[AF, "-q", "-i", "{F}"]], False),

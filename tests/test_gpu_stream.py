@@ -42,3 +42,48 @@ def test_golden_stdin_cases_through_a_pipe(monkeypatch, tool, knobs):
             bad.append((c["name"], rc, c["rc"], matches(c["out"], out), matches(c["err"], err)))
     assert n > 20
     assert not bad, "%d/%d %s cases differ, first: %s" % (len(bad), n, tool, bad[:8])
+
+
+FILE_KNOBS = [
+    # (first head read, ring slot, slots): the head grows by doubling until it holds '#CHROM'
+    {"VCFX_FILE_STREAM_MIN": "1", "VCFX_FILE_HEAD": "64", "VCFX_FILE_SLOT": "4096", "VCFX_FILE_SLOTS": "4"},
+    {"VCFX_FILE_STREAM_MIN": "1", "VCFX_FILE_HEAD": "1000", "VCFX_FILE_SLOT": "777", "VCFX_FILE_SLOTS": "5"},
+    {"VCFX_FILE_STREAM_MIN": "1", "VCFX_FILE_HEAD": "4096", "VCFX_FILE_SLOT": "65536", "VCFX_FILE_SLOTS": "12"},
+]
+
+
+@pytest.mark.parametrize("knobs", range(len(FILE_KNOBS)))
+def test_golden_af_file_cases_streamed_from_the_file(monkeypatch, knobs):
+    """VCFX_allele_freq_calc -i FILE on every golden file case with the device-only file path
+    forced on small files (Input::open_file_device: the head read into host memory, the rest
+    by reader threads into a pinned ring of tiny slots and copied to the device in order,
+    many ring wraps): stdout, stderr and exit code byte-identical to the reference's."""
+    for k, v in FILE_KNOBS[knobs].items():
+        monkeypatch.setenv(k, v)
+    bad = []
+    n = 0
+    for c in CASES:
+        if c["tool"] != "VCFX_allele_freq_calc" or c["stdin"] or not any(a in ("-i", "--input") for a in c["argv"]):
+            continue
+        n += 1
+        out, err, rc = tools.run(list(c["argv"]), b"", cwd=GOLDEN)
+        if rc != c["rc"] or not matches(c["out"], out) or not matches(c["err"], err):
+            bad.append((c["name"], rc, c["rc"], matches(c["out"], out), matches(c["err"], err)))
+    assert n > 20
+    assert not bad, "%d/%d cases differ, first: %s" % (len(bad), n, bad[:8])
+
+
+def test_af_streamed_file_larger_input(monkeypatch, tmp_path):
+    """A 40 MB synthetic input through the streamed file path (16 slots of 256 KiB: ~160 chunks,
+    ten ring wraps, six reader threads) equals the mapped path's output."""
+    from vcfx_amd import synth
+    p = str(tmp_path / "s.vcf")
+    open(p, "wb").write(synth.generate(6000, 2504, 91, 1, 0.001, 0, 0.02, 0))
+    argv = ["VCFX_allele_freq_calc", "-i", p]
+    monkeypatch.setenv("VCFX_FILE_STREAM", "0")
+    want = tools.run(argv)
+    monkeypatch.delenv("VCFX_FILE_STREAM")
+    for k, v in {"VCFX_FILE_STREAM_MIN": "1", "VCFX_FILE_SLOT": str(256 << 10), "VCFX_FILE_SLOTS": "16"}.items():
+        monkeypatch.setenv(k, v)
+    got = tools.run(argv)
+    assert want[2] == 0 and got == want

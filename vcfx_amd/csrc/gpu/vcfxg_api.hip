@@ -71,7 +71,7 @@ struct vcfxg_ctx {
     DevBuf wk_le, wk_alt, wk_tot, wk_rowpre, wk_status, wk_meta, wk_count, wk_offs, wk_gt, wk_small;
     DevBuf wk_tabs, rf_tabs;    // filter / query walk: per-line tab offsets (per walker, dense)
     // AF walk region tail: per walker row bytes, text offsets, first line start; leftover list
-    DevBuf wk_text, wk_toff, wk_start, wk_cx, wk_bs, scratch_small;
+    DevBuf wk_text, wk_toff, wk_start, wk_cx, wk_bs, scratch_small, byte_cnt;
     // AF walk: flags / counters that k_walker_scan zeroes after reading them (af_small_dirty: a
     // call did not get that far, so the next one clears them first), and the call summary the
     // same kernel writes straight into mapped host memory (no copy before the synchronisation)
@@ -312,7 +312,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt})
         if (b->p) (void)hipFree(b->p);
     if (c->af_small.p) (void)hipFree(c->af_small.p);
     if (c->wk_stage.p) (void)hipFree(c->wk_stage.p);
@@ -520,6 +520,27 @@ int vcfxg_ingest_wait(vcfxg_ctx *c, size_t upto) {
     HIPCHK(c, hipEventSynchronize(c->ingest_ev[k - 1].second));
     for (size_t i = 0; i < k; i++) c->ingest_ev_free.push_back(c->ingest_ev[i].second);
     c->ingest_ev.erase(c->ingest_ev.begin(), c->ingest_ev.begin() + (long)k);
+    return VCFXG_OK;
+}
+
+int vcfxg_count_byte(vcfxg_ctx *c, uint64_t from, int byte, uint64_t *count) {
+    if (!c || !count || byte < 0 || byte > 255) return VCFXG_E_ARG;
+    if (!c->loaded) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    *count = 0;
+    if (from >= c->n) return VCFXG_OK;
+    int r = ensure(c, c->byte_cnt, 8);
+    if (r) return r;
+    HIPCHK(c, hipMemsetAsync(c->byte_cnt.p, 0, 8, c->stream));
+    prof_begin(c, "count_byte");
+    HIPCHK(c, vcfxg::launch_count_byte(P<uint8_t>(c->input), from, c->n, (uint8_t)byte,
+                                       P<unsigned long long>(c->byte_cnt), c->stream));
+    prof_end(c, "count_byte");
+    static thread_local uint64_t h;
+    HIPCHK(c, hipMemcpyAsync(&h, c->byte_cnt.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    *count = h;
     return VCFXG_OK;
 }
 

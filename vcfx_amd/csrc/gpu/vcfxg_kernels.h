@@ -27,6 +27,9 @@ constexpr uint8_t kHweAltComma = 1, kHweEmptyField = 2;
 // idx_pos_cap() newline offsets per chunk, then a compaction into line_end (overflow != 0:
 // some chunk needs the emit sweep launch_idx_emit instead)
 int idx_pos_cap();
+// occurrences of `byte` in buf[lo, hi) added to *out (k_count_byte)
+hipError_t launch_count_byte(const uint8_t *buf, uint64_t lo, uint64_t hi, uint8_t byte, unsigned long long *out,
+                             hipStream_t s);
 int64_t idx_wchunks(int64_t lo, int64_t hi);
 hipError_t launch_idx_count(const char *buf, int64_t lo, int64_t hi, uint32_t *counts, uint64_t *pos,
                             unsigned *overflow, hipStream_t s);

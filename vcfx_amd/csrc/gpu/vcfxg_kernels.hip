@@ -1192,4 +1192,43 @@ hipError_t launch_af_format_w(const char *buf, int mode, int64_t nw, uint64_t ca
     return hipGetLastError();
 }
 
+// occurrences of one byte value in input bytes [lo, hi): 16 B per lane and step (aligned
+// loads; the input buffer is padded past n), exact zero-byte counts of x ^ pattern per dword,
+// a wave reduction and one atomic per wave.  HBM-bound; used by the fused chain's checks.
+__global__ void __launch_bounds__(256) k_count_byte(const uint8_t *__restrict__ buf, uint64_t lo, uint64_t hi,
+                                                    uint32_t pat, unsigned long long *out) {
+    const uint64_t a0 = lo & ~15ull;
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x * 16;
+    uint32_t cnt = 0;
+    for (uint64_t b = a0 + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; b < hi; b += step) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(buf + b);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const uint32_t x = w[d] ^ pat;
+            uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // 0x80 per zero byte
+            const uint64_t base = b + 4 * (uint64_t)d;
+            if (base < lo || base + 4 > hi) {  // a partial dword at either end
+                uint32_t keep = 0;
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+                    if (base + k >= lo && base + k < hi) keep |= 0x80u << (8 * k);
+                z &= keep;
+            }
+            cnt += __popc(z);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(out, (unsigned long long)cnt);
+}
+
+hipError_t launch_count_byte(const uint8_t *buf, uint64_t lo, uint64_t hi, uint8_t byte, unsigned long long *out,
+                             hipStream_t s) {
+    if (hi <= lo) return hipSuccess;
+    const uint64_t blocks16 = ((hi - (lo & ~15ull)) + 15) / 16;
+    const unsigned grid = (unsigned)std::min<uint64_t>((blocks16 + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_count_byte, dim3(grid), dim3(256), 0, s, buf, lo, hi, 0x01010101u * byte, out);
+    return hipGetLastError();
+}
+
 }  // namespace vcfxg

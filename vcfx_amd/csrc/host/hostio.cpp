@@ -156,6 +156,7 @@ Input::~Input() {
     if (ring_ctx)
         for (void *r : ring) vcfxg_host_free(ring_ctx, r);
     if (map_base && map_len) munmap(map_base, map_len);
+    phase("input released");
 }
 
 bool Input::open_file(const char *path) {
@@ -183,6 +184,7 @@ bool Input::open_file(const char *path) {
     // populated by helper threads instead of read-ahead (WILLNEED walks every cached page
     // on this thread first: ~30 ms at 4 GB)
     madvise(m, n, n < ((size_t)64 << 20) ? (MADV_SEQUENTIAL | MADV_WILLNEED) : MADV_SEQUENTIAL);
+    phase("file mapped");
     p = (const char *)m;
     mapped = true;
     map_base = m;
@@ -190,6 +192,189 @@ bool Input::open_file(const char *path) {
     source_n = n;
     if (gzip_ok && is_gzip(p, n) && gzip_enabled()) return true;  // decompress() takes it from here
     apply_view();
+    return true;
+}
+
+namespace {
+// the pinned staging ring of device-only file reads: allocated once per context and kept for
+// the process (a warm in-process context reuses it; hipHostMalloc of 192 MiB costs ~20 ms)
+struct FileRing {
+    vcfxg_ctx *ctx = nullptr;
+    size_t slot = 0;
+    std::vector<void *> slots;
+};
+std::mutex g_ring_mu;
+FileRing g_file_ring;
+
+size_t file_slot() { return env_bytes("VCFX_FILE_SLOT", (size_t)16 << 20); }
+size_t file_slots() { return std::max<size_t>(2, env_bytes("VCFX_FILE_SLOTS", 12)); }
+
+// pread of [off, off + len) into dst, whole (short reads continued); false on an error
+bool pread_full(int fd, char *dst, size_t len, size_t off, int *err) {
+    size_t got = 0;
+    while (got < len) {
+        ssize_t k = ::pread(fd, dst + got, len - got, (off_t)(off + got));
+        if (k < 0 && errno == EINTR) continue;
+        if (k < 0) *err = errno;
+        if (k <= 0) return false;
+        got += (size_t)k;
+    }
+    return true;
+}
+}  // namespace
+
+bool Input::open_file_device(const char *path) {
+    // where the mapped path stays: views (a shard rank, VCFX_INPUT_VIEW), VCFX_FILE_STREAM=0
+    const char *fs = getenv("VCFX_FILE_STREAM");
+    if (t_shard || getenv("VCFX_INPUT_VIEW") || (fs && fs[0] == '0')) return open_file(path);
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return false;
+    struct stat st;
+    if (fstat(fd, &st) < 0 || !S_ISREG(st.st_mode) || (size_t)st.st_size < env_bytes("VCFX_FILE_STREAM_MIN", (size_t)256 << 20)) {
+        ::close(fd);
+        return open_file(path);
+    }
+    const size_t total = (size_t)st.st_size;
+    gpu_prefetch();  // (a fresh process: the HIP runtime starts while the head is read)
+    // the head (until it holds the '#CHROM' line: the host's gate runs on it) into host memory
+    const size_t kSlot = file_slot(), kHeadMax = std::min(total, (size_t)256 << 20);
+    void *hm = mmap(nullptr, kHeadMax, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (hm == MAP_FAILED) {
+        ::close(fd);
+        return open_file(path);
+    }
+    char *head = (char *)hm;
+    size_t hn = 0;
+    bool chrom = false;
+    size_t scanned = 0;
+    while (!chrom && hn < kHeadMax) {
+        const size_t want = std::min(kHeadMax - hn, hn ? hn : env_bytes("VCFX_FILE_HEAD", (size_t)1 << 20));
+        if (!pread_full(fd, head + hn, want, hn, &read_errno)) break;
+        hn += want;
+        if (hn >= 2 && (unsigned char)head[0] == 0x1f && (unsigned char)head[1] == 0x8b) break;  // gzip
+        while (!chrom && scanned < hn) {
+            const char *s0 = head + scanned;
+            const char *nl = (const char *)memchr(s0, '\n', hn - scanned);
+            if (!nl) break;
+            chrom = is_chrom_line(s0, (size_t)(nl - s0));
+            scanned = (size_t)(nl - head) + 1;
+        }
+    }
+    vcfxg_ctx *g = chrom ? gpu_quiet() : nullptr;
+    if (!g) {  // gzip, no '#CHROM' in the first 256 MiB, a read error, or no device: the mapping
+        munmap(hm, kHeadMax);
+        ::close(fd);
+        read_errno = 0;
+        return open_file(path);
+    }
+    phase("file head read");
+    // the ring (this context's, kept for the process)
+    std::vector<void *> ring_;
+    {
+        std::lock_guard<std::mutex> lk(g_ring_mu);
+        if (g_file_ring.ctx != g || g_file_ring.slot != kSlot || g_file_ring.slots.size() != file_slots()) {
+            if (g_file_ring.ctx)
+                for (void *r : g_file_ring.slots) vcfxg_host_free(g_file_ring.ctx, r);
+            g_file_ring = FileRing{};
+            bool ok = true;
+            for (size_t i = 0; i < file_slots() && ok; i++) {
+                void *r = nullptr;
+                ok = vcfxg_host_alloc(g, kSlot, &r) == VCFXG_OK;
+                if (ok) g_file_ring.slots.push_back(r);
+            }
+            if (ok) {
+                g_file_ring.ctx = g;
+                g_file_ring.slot = kSlot;
+            } else {
+                for (void *r : g_file_ring.slots) vcfxg_host_free(g, r);
+                g_file_ring.slots.clear();
+            }
+        }
+        ring_ = g_file_ring.slots;
+    }
+    if (ring_.empty() || vcfxg_ingest_begin(g, total) != VCFXG_OK || vcfxg_ingest(g, head, hn, 0) != VCFXG_OK) {
+        munmap(hm, kHeadMax);
+        ::close(fd);
+        return open_file(path);
+    }
+    phase("file ring ready");
+    // the rest: chunk i = [hn + i*slot, ...) into slot i % S, read by T reader threads (reader
+    // t takes chunks t, t + T, ...), handed to the device in order by this thread; at most S/2
+    // chunks are in DMA flight, the other slots are being filled
+    const size_t S = ring_.size(), inflight = std::max<size_t>(1, S / 2);
+    const size_t nchunks = (total - hn + kSlot - 1) / kSlot;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t T = std::max<size_t>(1, std::min<size_t>({S - inflight, (size_t)8, hw ? (size_t)hw : 1}));
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<long long> filled(S, -1), freed(S, -1);  // chunk index held / released per slot
+    bool stop = false, ok = true;
+    std::atomic<int> rerr{0};
+    std::vector<std::thread> readers;
+    for (size_t t = 0; t < T; t++)
+        readers.emplace_back([&, t] {
+            for (size_t i = t; i < nchunks; i += T) {
+                const size_t s = i % S;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop || i < S || freed[s] >= (long long)(i - S); });
+                    if (stop) return;
+                }
+                const size_t off = hn + i * kSlot, len = std::min(kSlot, total - off);
+                int e = 0;
+                const bool r = pread_full(fd, (char *)ring_[s], len, off, &e);
+                std::lock_guard<std::mutex> lk(mu);
+                if (!r) {
+                    rerr = e ? e : EIO;
+                    stop = true;
+                } else {
+                    filled[s] = (long long)i;
+                }
+                cv.notify_all();
+                if (!r) return;
+            }
+        });
+    std::vector<size_t> ends(nchunks);
+    for (size_t i = 0; i < nchunks && ok; i++) {
+        const size_t s = i % S, off = hn + i * kSlot, len = std::min(kSlot, total - off);
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || filled[s] == (long long)i; });
+            if (stop) {
+                ok = false;
+                break;
+            }
+        }
+        ok = vcfxg_ingest(g, (const char *)ring_[s], len, 0) == VCFXG_OK;
+        ends[i] = off + len;
+        if (ok && i >= inflight) {  // the chunk inflight places back: its DMA done, its slot free
+            const size_t j = i - inflight;
+            ok = vcfxg_ingest_wait(g, ends[j]) == VCFXG_OK;
+            std::lock_guard<std::mutex> lk(mu);
+            freed[j % S] = (long long)j;
+            cv.notify_all();
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!ok) stop = true;
+        cv.notify_all();
+    }
+    for (auto &t : readers) t.join();
+    ::close(fd);
+    // every DMA from the ring finished before the slots are reused (the next call's readers)
+    if (ok && vcfxg_ingest_wait(g, total) != VCFXG_OK) ok = false;
+    if (rerr) read_errno = rerr;
+    phase("file streamed to the device");
+    p = head;
+    host_n = hn;
+    n = total;
+    source_n = total;
+    map_base = hm;
+    map_len = kHeadMax;
+    mapped = false;
+    stream_ctx = g;
+    streamed = ok ? total : 0;  // a failure is reported when the input is used (load_input)
     return true;
 }
 
@@ -540,6 +725,7 @@ void Input::read_fd(int fd, bool host_copy) {
 
 bool load_input(vcfxg_ctx *g, const Input &in, int err_fd) {
     in.join_populate();
+    phase("page population joined");
     if (in.tail) {  // a shard view: header + record range, straight from the mapping
         int rc = vcfxg_ingest_begin(g, in.n);
         if (!rc) rc = vcfxg_ingest(g, in.p, in.host_n, 0);

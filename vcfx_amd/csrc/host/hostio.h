@@ -53,6 +53,14 @@ struct Input {
     // fails; a 0-byte file is a successful empty map.  Inputs of 1 MiB and more start the
     // GPU context opening on a background thread (gpu_prefetch).
     bool open_file(const char *path);
+    // open_file for a tool that needs only the header on the host (AF: the device formats every
+    // row).  A regular file of 256 MiB and more (VCFX_FILE_STREAM_MIN) is not mapped: its head
+    // (through the '#CHROM' line) is read into host memory, the rest by reader threads into a
+    // pinned staging ring (kept per context) from which it is copied to the device in order
+    // (vcfxg_ingest, DMA overlapping the reads): no page-table population, no unmapping of the
+    // whole input afterwards.  Views, gzip input, smaller files and VCFX_FILE_STREAM=0 take
+    // open_file.  Afterwards host_n < n and load_input completes the device input.
+    bool open_file_device(const char *path);
     // VCFX_INPUT_VIEW="H:LO:HI" in the environment (set by the multi-GPU runner,
     // vcfx_amd/shard.py): the input is the file's header bytes [0, H) followed by its records
     // [LO, HI) -- one rank's shard, without a copy.  The device input is ingested from those

@@ -113,7 +113,7 @@ extern "C" int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int 
     uint64_t v = 0, l = 0;
     if (input) {
         phase("start");
-        if (!in.open_file(input)) {
+        if (!in.open_file_device(input)) {
             err.put(std::string("Error: Cannot open file: ") + input + "\n");
             return 1;
         }

@@ -78,6 +78,7 @@ SIGNATURES = {
     "vcfxg_comm_destroy": (None, [_VP]),
     "vcfxg_comm_rccl_stats": (_I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     "vcfxg_last_schedule": (_P, [_VP]),
+    "vcfxg_count_byte": (_I, [_VP, _U64, _I, ctypes.POINTER(_U64)]),
     "vcfxg_haplotype_phaser": (_I, [_VP, _S, _I, ctypes.c_double, ctypes.c_uint32, ctypes.POINTER(Summary)]),
     "vcfxg_phaser_variants": (_I, [_VP, _VP, _VP, _VP]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
@@ -357,6 +358,11 @@ class Engine:
         self._chk(self.L.vcfxg_ld_stream_chunk(self.h, j0, j1, window, threshold, max_dist, ctypes.byref(npairs),
                                                ctypes.byref(tb)), "ld_stream_chunk")
         return npairs.value, tb.value
+
+    def count_byte(self, from_, byte):
+        n = ctypes.c_uint64()
+        self._chk(self.L.vcfxg_count_byte(self.h, from_, byte, ctypes.byref(n)), "count_byte")
+        return n.value
 
     def ld_pairs(self, first, count):
         """(i, j, r2) numpy arrays of pairs [first, first + count) of the last ld_stream_chunk."""
