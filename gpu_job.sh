@@ -44,7 +44,8 @@ MODE=${1:-test}
 shift
 case "$MODE" in
 test)
-    step pytest_gpu 1100 python -u -m pytest ${*:-tests} -m gpu -q -x --timeout 300 --timeout-method thread ;;
+    [ $# -eq 0 ] && set -- tests
+    step pytest_gpu 1100 python -u -m pytest "$@" -m gpu -q -x --timeout 300 --timeout-method thread ;;
 scale)
     step pytest_scale 1100 python -u -m pytest tests/test_gpu_scale.py -v -x --timeout 900 --timeout-method thread "$@" ;;
 smoke)

@@ -19,9 +19,26 @@ done
 for i in 1 2 3; do
     echo -n "fresh_file "; time (VCFX_TIMING=$((i == 1)) timeout -k 5 60 $AF -q -i $F > /dev/null) || exit 1
 done
+for cfg in "33554432 4" "4194304 8" "2097152 8" "1048576 16" "8388608 4"; do
+    set -- $cfg
+    echo -n "cat_pipe_drain_ring $1x$2 "; time (cat $F | $DRAIN $1 $2)
+    echo -n "fresh_pipe ring $1x$2 "
+    time (cat $F | VCFX_RING_SLOT=$1 VCFX_RING_SLOTS=$2 VCFX_TIMING=1 timeout -k 5 60 $AF -q 2>&1 > /dev/null | grep "streamed") || exit 1
+done
 for i in 1 2 3; do
     echo -n "fresh_pipe "; time (cat $F | VCFX_TIMING=$((i == 1)) timeout -k 5 60 $AF -q > /dev/null) || exit 1
 done
 echo -n "fresh_file_mapped "; time (VCFX_FILE_STREAM=0 timeout -k 5 60 $AF -q -i $F > /dev/null) || exit 1
 VCFX_TIMING=1 timeout -k 5 120 python tools/e2e_warm.py $F || exit 1
+# ring shapes (warm context, the last of three runs each)
+for cfg in "16777216 12" "16777216 8" "8388608 16" "33554432 8" "16777216 20"; do
+    set -- $cfg
+    echo "ring slot=$1 slots=$2"
+    VCFX_FILE_SLOT=$1 VCFX_FILE_SLOTS=$2 VCFX_TIMING=1 timeout -k 5 120 python tools/e2e_warm.py $F 2>&1 | \
+        grep -E "^--- run 2|start|streamed|released" | tail -3 || exit 1
+done
+for cfg in "16777216 12" "8388608 8"; do
+    set -- $cfg
+    echo -n "fresh_file slot=$1 slots=$2 "; time (VCFX_FILE_SLOT=$1 VCFX_FILE_SLOTS=$2 timeout -k 5 60 $AF -q -i $F > /dev/null) || exit 1
+done
 rm -f $F

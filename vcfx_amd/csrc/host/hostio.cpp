@@ -628,7 +628,7 @@ void Input::read_fd(int fd, bool host_copy) {
             host_n = got;
             stream_ctx = g;
             ring_ctx = g;
-            constexpr int kSlots = 4;
+            const int kSlots = (int)std::min<size_t>(64, std::max<size_t>(2, env_bytes("VCFX_RING_SLOTS", 4)));
             const size_t kSlot = ring_slot();
             bool ok = true;
             for (int i = 0; i < kSlots && ok; i++) {
@@ -638,19 +638,36 @@ void Input::read_fd(int fd, bool host_copy) {
             }
             size_t total = got;
             std::vector<size_t> slot_end(kSlots, 0);  // input offset where the slot's last chunk ended
+            phase("stdin head ingested");
+            using clk = std::chrono::steady_clock;
+            double t_wait = 0, t_read = 0, t_ing = 0;
             for (int k = 0; ok; k = (k + 1) % kSlots) {
+                const auto a0 = clk::now();
                 ok = vcfxg_ingest_wait(g, slot_end[k]) == VCFXG_OK;
                 if (!ok) break;
+                const auto a1 = clk::now();
                 ssize_t r = read_full(fd, (char *)ring[k], kSlot, &read_errno);
+                const auto a2 = clk::now();
                 if (r <= 0) break;
                 ok = vcfxg_ingest(g, (const char *)ring[k], (size_t)r, 0) == VCFXG_OK;
+                const auto a3 = clk::now();
+                t_wait += std::chrono::duration<double, std::milli>(a1 - a0).count();
+                t_read += std::chrono::duration<double, std::milli>(a2 - a1).count();
+                t_ing += std::chrono::duration<double, std::milli>(a3 - a2).count();
                 total += (size_t)r;
                 slot_end[k] = total;
                 if ((size_t)r < kSlot) break;
             }
             n = total;
             streamed = ok ? total : 0;  // a failure is reported when the input is used
-            phase("stdin streamed to the device");
+            if (timing_on) {
+                char b[160];
+                snprintf(b, sizeof b, "stdin streamed to the device (head %zu MB; ring: wait %.1f, read %.1f, ingest %.1f ms)",
+                         got >> 20, t_wait, t_read, t_ing);
+                phase(b);
+            } else {
+                phase("stdin streamed to the device");
+            }
             return;
         }
     }
@@ -721,6 +738,35 @@ void Input::read_fd(int fd, bool host_copy) {
     ing.join();
     pre.join();
     n = host_n = got;
+}
+
+bool write_device_text(vcfxg_ctx *g, uint64_t bytes, Out &out, int err_fd) {
+    out.flush();
+    if (!bytes) return true;
+    std::vector<void *> slots;
+    size_t slot = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_ring_mu);
+        if (g_file_ring.ctx == g) {
+            slots = g_file_ring.slots;
+            slot = g_file_ring.slot;
+        }
+    }
+    if (slots.empty()) {  // no pinned ring on this context: one pageable copy
+        std::string text(bytes, '\0');
+        if (!gpu_ok(g, vcfxg_fetch_text(g, &text[0], text.size()), "fetch", err_fd)) return false;
+        write_all(out.fd, text.data(), text.size());
+        return true;
+    }
+    // through the pinned staging slots (the input's DMAs are complete): no page faults on a
+    // fresh host buffer, DMA-rate copies
+    for (uint64_t o = 0, k = 0; o < bytes; o += slot, k++) {
+        const size_t n = (size_t)std::min<uint64_t>(slot, bytes - o);
+        void *b = slots[k % slots.size()];
+        if (!gpu_ok(g, vcfxg_fetch_text_range(g, o, n, b), "fetch", err_fd)) return false;
+        write_all(out.fd, (const char *)b, n);
+    }
+    return true;
 }
 
 bool load_input(vcfxg_ctx *g, const Input &in, int err_fd) {

@@ -166,6 +166,10 @@ bool gpu_ok(vcfxg_ctx *c, int rc, const char *what, int err_fd);
 // was read, or copies the whole input (vcfxg_load_host)
 bool load_input(vcfxg_ctx *g, const Input &in, int err_fd);
 
+// the device-formatted text of the last call (bytes of it) written to out's fd after out's
+// buffer: through the context's pinned file ring when it has one, else one host copy
+bool write_device_text(vcfxg_ctx *g, uint64_t bytes, Out &out, int err_fd);
+
 const void *memchr_(const char *p, const char *end);
 
 // iterate lines of [p, end): returns false at end; [ls, le) excludes '\n'

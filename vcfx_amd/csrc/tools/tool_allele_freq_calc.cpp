@@ -72,10 +72,8 @@ bool run_af(const Input &in, int mode, bool quiet, Out &out, Out &err, uint64_t 
     vcfxg_summary s;  // index + counts + rows in one device sweep
     if (!gpu_ok(g, vcfxg_allele_freq_region(g, data_start, mode, &s), "allele_freq", err.fd)) return false;
     phase("allele_freq_region");
-    std::string text(s.text_bytes, '\0');
-    if (!gpu_ok(g, vcfxg_fetch_text(g, &text[0], text.size()), "fetch", err.fd)) return false;
-    phase("rows fetched");
-    out.put(text);
+    if (!write_device_text(g, s.text_bytes, out, err.fd)) return false;
+    phase("rows written");
     if (!quiet)
         for (uint64_t k = 0; k < s.warn_lines; k++) err.put(kWarnFields);
     *variants = s.rows;

@@ -330,7 +330,8 @@ int run_fused(const std::vector<Stage> &P, const std::string &path, int in_fd, i
         phase("pipe: allele_freq rows");
         // the rows of the kept records: the AF rows follow the ROW lines in order
         LineEmitter em(text.data(), text.size(), out_fd);
-        em.raw("CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n", 41);
+        static const char kHead[] = "CHROM\tPOS\tID\tREF\tALT\tAllele_Frequency\n";
+        em.raw(kHead, sizeof kHead - 1);
         const char *r = text.data(), *te = text.data() + text.size();
         for (uint64_t i = 0; i < nl && r < te; i++) {
             if (st[i] != VCFXG_LINE_ROW) continue;
