@@ -113,6 +113,12 @@ int vcfxg_fetch_text(vcfxg_ctx *c, char *host, size_t cap) {
     return VCFXG_OK;
 }
 
+int vcfxg_fetch_text_range(vcfxg_ctx *c, uint64_t offset, size_t n, void *host) {
+    if (offset > c->text.size() || n > c->text.size() - offset) return VCFXG_E_ARG;
+    memcpy(host, c->text.data() + offset, n);
+    return VCFXG_OK;
+}
+
 int vcfxg_shard_cuts(const char *data, size_t n, size_t lo, int world, uint64_t *cuts) {
     if (world < 1 || lo > n) return VCFXG_E_ARG;
     cuts[0] = lo;

@@ -69,3 +69,45 @@ def test_phaser_pair_r2_matches_oracle(oracle):
         assert r2[v] == rr.value, (v, r2[v], rr.value)
         assert bool(flags[v] & 1) == (rr.value >= 0.5)
         prev = cur
+
+
+def _mutate(buf, rec, sample, new):
+    lines = buf.split(b"\n")
+    k = next(i for i, l in enumerate(lines) if l.startswith(b"#CHROM")) + 1 + rec
+    f = lines[k].split(b"\t")
+    f[9 + sample] = new
+    lines[k] = b"\t".join(f)
+    return b"\n".join(lines)
+
+
+# the phaser's line index from the dosage HEAD walk: records taken on their predicted '\n' alone
+# must be validated by k_ph_lines' fixed-stride sweep; each way such a record can differ (a
+# missing allele -- valid for the sweep --, a non-digit allele, another separator, a wider
+# sample, a '\n' inside a record of the predicted length, a non-digit POS) against the oracle
+PH_MUTATIONS = [None, (7, 100, b".|0"), (11, 0, b"x|1"), (12, 5, b"1/0"), (13, 9, b"11|"), (14, 1000, b"0\n0"),
+                (300, 2503, b"0|\n")]
+
+
+@pytest.mark.parametrize("mut", PH_MUTATIONS)
+def test_phaser_head_walk_index(oracle, mut, tmp_path):
+    import os
+    buf = synth.generate(600, 2504, 116, 0, 0.0, 1, 0.0, 0)
+    if mut:
+        buf = _mutate(buf, *mut)
+    path = tmp_path / "in.vcf"
+    path.write_bytes(buf)
+    T = "VCFX_haplotype_phaser"
+    log = str(tmp_path / "sched.log")
+    os.environ["VCFXG_SCHEDULE_LOG"] = log
+    try:
+        for args in (["-l", "0.5"], ["-s", "-w", "3", "-l", "0.3"]):
+            for argv, stdin in (([T] + args + ["-i", str(path)], b""), ([T] + args, buf)):
+                want = oracle.run(argv, stdin)
+                got = tools.run(argv, stdin)
+                assert got == want, (mut, argv[1:], got[1][-300:], want[1][-300:])
+    finally:
+        del os.environ["VCFXG_SCHEDULE_LOG"]
+    sched = open(log).read().split()
+    assert sched and sched[0] == "ph_head_walk", sched
+    if mut is None:
+        assert set(sched) == {"ph_head_walk"}, sched

@@ -138,7 +138,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             LineMeta m{};
             m.kind = kind;
             m.cr = (uint8_t)(r_k >> 16);
-            m.pad = R::kAux ? (uint8_t)r_h : 0;
+            m.pad = (R::kAux || std::is_same<Op, DoseHeadOp>::value) ? (uint8_t)r_h : 0;
             if (kind == kMetaGt) {
                 m.S = r_S;
                 m.rowpre = r_pre;
@@ -332,6 +332,10 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                 // else: true bounds, not fixed-stride
             }
         }
+        // DoseHeadOp: a record taken on its predicted end without a sweep (its interior bytes are
+        // unread: the consumer checks them, k_dose_fmt / k_ph_lines)
+        if constexpr (std::is_same<Op, DoseHeadOp>::value)
+            if (skip && kind == kMetaGt) hflags |= kWalkUnswept;
         if (kind == kMetaGt) {
             if (ok) {
                 st = 1;

@@ -115,6 +115,7 @@ struct vcfxg_ctx {
                              : 128 * 1024;
     bool walk_overflowed = false;  // the last walk run overflowed: two-sweep schedule
     bool dose_head_failed = false;  // a dosage head walk's rows failed the check (this input)
+    bool ph_head_failed = false;    // a phaser head-walk index failed the parse's check (this input)
     // host hints taken at load time from the first data line: its '\n' distance from the
     // sample start (the walk's first prediction) and the mean length of the first lines
     int64_t hint_span = 0, hint_line = 0;
@@ -384,6 +385,7 @@ static void reset_hints(vcfxg_ctx *c) {
     c->hint_gt_first = false;
     c->walk_overflowed = false;
     c->dose_head_failed = false;
+    c->ph_head_failed = false;
     if (!getenv("VCFXG_WALK_CHUNK")) c->walk_chunk = 128 * 1024;
 }
 
@@ -1833,14 +1835,53 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
 // VCFX_haplotype_phaser over [data_start, n): index, the per-line parse into genotype rows, the
 // variant compaction (one host synchronisation for the variant count), the pair pass, a scan
 // and the entries (a second synchronisation)
+// VCFX_haplotype_phaser.  Records of >= 512 B, GT-only (a GT-dense VCF): the line index comes
+// from the dosage HEAD walk (record heads only; a GT-only record whose '\n' is where the
+// previous fixed-stride record predicts it is taken unswept), and k_ph_lines' fixed-stride
+// sweep, which reads every record anyway, validates the unswept records' interiors; a record it
+// cannot validate flags the call, which is redone on vcfxg_index (and this input keeps the
+// index).  VCFXG_PH_WALK=0: always the index.
+static int phaser_once(vcfxg_ctx *c, size_t data_start, int mode, double thr, uint32_t hint, vcfxg_summary *out,
+                       bool walk, bool *redo);
+
 int vcfxg_haplotype_phaser(vcfxg_ctx *c, size_t data_start, int mode, double thr, uint32_t hint, vcfxg_summary *out) {
     if (!c || (mode != VCFXG_MODE_FILE && mode != VCFXG_MODE_STDIN)) return VCFXG_E_ARG;
     if (!c->loaded) return VCFXG_E_STATE;
     if (data_start > c->n) data_start = c->n;
+    static const bool walk_ok = [] {
+        const char *e = getenv("VCFXG_PH_WALK");
+        return !(e && e[0] == '0');
+    }();
+    const bool walk = walk_ok && !c->ph_head_failed && c->af_path != 3 && c->af_path != 8 && c->hint_line >= 512 &&
+                      c->hint_gt_only && !c->walk_overflowed &&
+                      vcfxg::af_walkers((int64_t)data_start, (int64_t)c->n, c->walk_chunk) > 0;
+    bool redo = false;
+    int r = phaser_once(c, data_start, mode, thr, hint, out, walk, &redo);
+    if (r || !redo) return r;
+    c->ph_head_failed = true;
+    return phaser_once(c, data_start, mode, thr, hint, out, false, &redo);
+}
+
+static int phaser_once(vcfxg_ctx *c, size_t data_start, int mode, double thr, uint32_t hint, vcfxg_summary *out,
+                       bool walk, bool *redo) {
+    *redo = false;
     uint64_t L = 0;
-    int r = vcfxg_index(c, data_start, &L);
-    if (r) return r;
+    int r;
+    bool walked = false;
+    if (walk) {
+        bool ovf = false;
+        note_schedule(c, "ph_head_walk");
+        r = dose_walk_index(c, data_start, mode, &L, &ovf, true);
+        if (r) return r;
+        walked = !ovf;
+    }
+    if (!walked) {
+        note_schedule(c, "ph_index");
+        r = vcfxg_index(c, data_start, &L);
+        if (r) return r;
+    }
     HIPCHK(c, hipSetDevice(c->device));
+    unsigned *bad = walked ? reinterpret_cast<unsigned *>(P<uint64_t>(c->wk_small) + 4) : nullptr;
     const char *buf = P<char>(c->input);
     uint64_t kpad = ((uint64_t)std::max<uint32_t>(hint, 16) + 15) & ~15ull;
     static thread_local uint64_t h[2];
@@ -1854,11 +1895,12 @@ int vcfxg_haplotype_phaser(vcfxg_ctx *c, size_t data_start, int mode, double thr
         if (r) return r;
         HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
         HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->counters) + 4, 0, 8, c->stream));
+        if (bad) HIPCHK(c, hipMemsetAsync(bad, 0, 4, c->stream));
         prof_begin(c, "ph_lines");
         HIPCHK(c, vcfxg::launch_ph_lines(buf, (int64_t)data_start, P<uint64_t>(c->line_end), P<uint64_t>(c->d_nlines), L,
                                          mode, (uint32_t)kpad, P<int8_t>(c->ph_G), P<uint8_t>(c->status),
                                          P<uint32_t>(c->ph_isvar), c->ph_info.p, P<unsigned long long>(c->counters),
-                                         c->stream));
+                                         c->stream, walked ? c->af_meta.p : nullptr, bad));
         prof_end(c, "ph_lines");
         if (L) {
             r = exclusive_scan(c, P<uint32_t>(c->ph_isvar), P<uint64_t>(c->ph_vnum), (size_t)L);
@@ -1867,7 +1909,14 @@ int vcfxg_haplotype_phaser(vcfxg_ctx *c, size_t data_start, int mode, double thr
                                                L, P<uint64_t>(c->ph_vline), P<uint64_t>(c->counters) + 4, c->stream));
         }
         HIPCHK(c, hipMemcpyAsync(h, P<uint64_t>(c->counters) + 3, 16, hipMemcpyDeviceToHost, c->stream));
+        static thread_local unsigned bad_h;
+        bad_h = 0;
+        if (bad) HIPCHK(c, hipMemcpyAsync(&bad_h, bad, 4, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (bad_h) {  // an unswept record the parse could not validate: the call again on the index
+            *redo = true;
+            return VCFXG_OK;
+        }
         if (h[0] > kpad && pass == 0) {  // a record wider than the rows: once more with rows that fit
             kpad = (h[0] + 15) & ~15ull;
             continue;

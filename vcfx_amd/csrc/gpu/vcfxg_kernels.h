@@ -22,6 +22,8 @@ constexpr uint8_t kRfPending = 0xFD;  // RF walk: head beyond the window (k_fq_f
 constexpr uint8_t kGqFull = 0xFC;     // GQ walk: a kMetaFull line for k_gq_complex's gq_line
 // HWE walk: LineMeta::pad of a kMetaGt line -- ALT holds a ',' / CHROM, POS or ALT is empty
 constexpr uint8_t kHweAltComma = 1, kHweEmptyField = 2;
+// dosage HEAD walk: LineMeta::pad of a GT-only record taken on its predicted end, unswept
+constexpr uint8_t kWalkUnswept = 4;
 
 // single-sweep index over 16 KiB wave-chunks (idx_wchunks of them): counts + the first
 // idx_pos_cap() newline offsets per chunk, then a compaction into line_end (overflow != 0:
@@ -200,9 +202,12 @@ hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *li
 // passes, bit 1 same CHROM) + r^2 + entry length, and the entries "v:(chrom:pos)"
 enum : uint8_t { kPhSkip = 0, kPhVar = 1, kPhFew = 3, kPhHeader = 4, kPhPos = 7, kPhNoGt = 8 };
 size_t ph_line_bytes();
+// walk_meta (nullable): the head walk's LineMeta per line (its index); a line taken unswept
+// (kWalkUnswept) that the parse does not validate by the fixed-stride sweep sets *bad
 hipError_t launch_ph_lines(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, int mode, uint32_t kpad, int8_t *G, uint8_t *status, uint32_t *isvar,
-                           void *info, unsigned long long *counters, hipStream_t s);
+                           void *info, unsigned long long *counters, hipStream_t s, const void *walk_meta = nullptr,
+                           unsigned *bad = nullptr);
 hipError_t launch_ph_compact(const uint32_t *isvar, const uint64_t *vnum, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, uint64_t *vline, uint64_t *n_var, hipStream_t s);
 hipError_t launch_ph_pairs(const char *buf, const uint64_t *vline, const uint64_t *n_var_dev, uint64_t n_var_host,

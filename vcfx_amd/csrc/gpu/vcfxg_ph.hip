@@ -118,7 +118,8 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
                                                          const uint64_t *n_lines_p, int mode, uint32_t kpad,
                                                          int8_t *__restrict__ G, uint8_t *__restrict__ status,
                                                          uint32_t *__restrict__ isvar, PhLine *__restrict__ info,
-                                                         unsigned long long *__restrict__ counters) {
+                                                         unsigned long long *__restrict__ counters,
+                                                         const LineMeta *__restrict__ wmeta, unsigned *__restrict__ bad) {
     __shared__ int64_t scratch[kPhWaves][16];
     // a GT-only fixed-stride record's codes are composed in the wave's LDS row (byte writes)
     // and leave in 16 B stores: a byte store per sample to HBM would be 4 store instructions
@@ -133,6 +134,7 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
         if (!kFast && status[li] != kPhPend) continue;  // (wave-uniform)
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
         uint8_t st = kPhSkip;
+        bool swept_fixed = false;
         PhLine m{};
         if (!(mode == 1 && le == ls)) {  // stdin: an empty line before the '\r' strip
             int64_t ae = le;
@@ -190,6 +192,7 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
                             PhOp op{row, S};
                             swept = gt_fast(buf, S, ae, op);
                         }
+                        swept_fixed = swept;
                         if (swept)
                             m.ns = (uint32_t)((L + 1) / 4);
                         else if (kFast)
@@ -225,6 +228,11 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
                 }
             }
         }
+        // a record the head walk took on its predicted end: its bounds hold only if the fixed-stride
+        // sweep validated [S, ae) (no '\n' inside); any other outcome redoes the call on the index
+        if (wmeta && st != kPhPend && !(st == kPhVar && swept_fixed) && (wmeta[li].pad & kWalkUnswept) &&
+            wmeta[li].kind == kMetaGt && lane() == 0)
+            atomicOr(bad, 1u);
         if (lane() == 0) {
             status[li] = st;
             isvar[li] = st == kPhVar;
@@ -378,16 +386,19 @@ size_t ph_line_bytes() { return sizeof(PhLine); }
 
 hipError_t launch_ph_lines(const char *buf, int64_t data_start, const uint64_t *line_end, const uint64_t *n_lines_dev,
                            uint64_t n_lines_host, int mode, uint32_t kpad, int8_t *G, uint8_t *status, uint32_t *isvar,
-                           void *info, unsigned long long *counters, hipStream_t s) {
+                           void *info, unsigned long long *counters, hipStream_t s, const void *walk_meta,
+                           unsigned *bad) {
     if (!n_lines_host) return hipSuccess;
+    if (walk_meta && !bad) return hipErrorInvalidValue;
+    const LineMeta *wm = static_cast<const LineMeta *>(walk_meta);
     int64_t g = ((int64_t)n_lines_host + kPhWaves - 1) / kPhWaves;
     if (g > 4096) g = 4096;
     // (a record's sweep with 8 KiB-steps in flight per wave measured the same as 4: r02)
     hipLaunchKernelGGL(k_ph_lines<true>, dim3((unsigned)g), dim3(kPhThreads), 0, s, buf, data_start, line_end,
-                       n_lines_dev, mode, kpad, G, status, isvar, static_cast<PhLine *>(info), counters);
+                       n_lines_dev, mode, kpad, G, status, isvar, static_cast<PhLine *>(info), counters, wm, bad);
     hipLaunchKernelGGL(k_ph_lines<false>, dim3((unsigned)std::min<int64_t>(g, 2048)), dim3(kPhThreads), 0, s, buf,
                        data_start, line_end, n_lines_dev, mode, kpad, G, status, isvar,
-                       static_cast<PhLine *>(info), counters);
+                       static_cast<PhLine *>(info), counters, wm, bad);
     return hipGetLastError();
 }
 
