@@ -79,6 +79,7 @@ def _codes(buf, oracle):
 
 
 @pytest.mark.parametrize("cfg,knock", [((200, 300, 57, 0, 0.03, 1, 0.0, 0), None),   # masked tiles only
+                                       ((700, 2504, 64, 0, 0.001, 1, 0.0, 0), None),  # sparse-missing tiles (kSp)
                                        ((600, 300, 63, 0, 0.0, 1, 0.0, 0), None),    # complete: FP4 fast blocks
                                        ((600, 300, 63, 0, 0.0, 1, 0.0, 0), 300)])    # fast + masked mix
 def test_ld_r2_values_bitexact(oracle, cfg, knock):
@@ -226,3 +227,35 @@ def test_ld_mask_tiles_missing_calls(oracle, rate):
 def tools_binary(t):
     from vcfx_amd import tool_binary
     return tool_binary(t)
+
+
+@pytest.mark.parametrize("rate,ns", [(0.001, 2504), (0.004, 1000), (0.0005, 4100)])
+def test_ld_sparse_missing_tiles(oracle, rate, ns):
+    """The sparse-missing form of the 256 x 256 FP4 kernel (every variant of both groups misses
+    <= 15 calls): X.X^T from the MFMA, the other five sums of computeRsqSIMD corrected at the
+    missing samples (LDS contribution tables), the k_ld_mask prefilter and fp64 sequence.
+    Against the oracle over windows / thresholds / distance caps (threshold 0: every pair a
+    candidate), the count pass's staging both roomy and overflowing (the emit pass recomputes),
+    and against the dense masked kernel (VCFXG_LD_SPARSE=0, a fresh process)."""
+    import os
+    import subprocess
+    buf = synth.generate(1100, ns, 66, 0, rate, 1, 0.0, 0)
+    with tempfile.NamedTemporaryFile(suffix=".vcf") as f:
+        f.write(buf)
+        f.flush()
+        for a in (["-w", "1100", "-t", "0.5"], ["-w", "300", "-t", "0.2"], ["-w", "129", "-t", "0.0"],
+                  ["-w", "700", "-t", "0.35", "-d", "5000"], ["-w", "64", "-t", "0.05"]):
+            argv = ["VCFX_ld_calculator"] + a + ["-i", f.name]
+            want = oracle.run(argv, b"")
+            got = tools.run(argv, b"")
+            assert got == want, (a, rate, len(got[0]), len(want[0]))
+        argv = ["VCFX_ld_calculator", "-w", "1100", "-t", "0.3", "-i", f.name]
+        want = oracle.run(argv, b"")
+        os.environ["VCFXG_LD_STAGE_CAP"] = "7"
+        try:
+            assert tools.run(argv, b"") == want
+        finally:
+            del os.environ["VCFXG_LD_STAGE_CAP"]
+        old = subprocess.run([tools_binary("VCFX_ld_calculator")] + argv[1:], capture_output=True,
+                             env=dict(os.environ, VCFXG_LD_SPARSE="0"), timeout=300)
+        assert (old.stdout, old.returncode) == (want[0], 0)

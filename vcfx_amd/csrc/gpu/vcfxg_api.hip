@@ -146,7 +146,12 @@ struct vcfxg_ctx {
     // flags, list sizes (fast, masked, int8), the ld_blocks buffer they were copied to
     uint64_t ld_plan_key[5] = {0, 0, 0, 0, 0};
     std::vector<uint8_t> ld_plan_gf;
-    uint32_t ld_plan_n[3] = {0, 0, 0};
+    uint32_t ld_plan_n[4] = {0, 0, 0, 0};
+    // the sparse-missing LD kernel's data (ld_sp: some 256-group qualifies): CSR of each
+    // variant's missing samples and the sample-major contribution plane
+    bool ld_sp = false;
+    uint64_t ld_mp = 0;
+    DevBuf ld_moff, ld_midx, ld_mvar, ld_gt16;
     void *ld_plan_dev = nullptr;
     uint64_t text_bytes = 0;
     uint64_t text_hint = 0;  // AF walk: text bytes of the previous call (the next call's capacity)
@@ -313,7 +318,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16})
         if (b->p) (void)hipFree(b->p);
     if (c->af_small.p) (void)hipFree(c->af_small.p);
     if (c->wk_stage.p) (void)hipFree(c->wk_stage.p);
@@ -2165,7 +2170,14 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
                                        P<vcfxg::LdVar>(c->ld_vars), P<vcfxg::LdFast>(c->ld_fast), c->stream));
     HIPCHK(c, vcfxg::launch_ld_pack4(P<int8_t>(c->ld_Gc), M, kpad, n_samples, P<uint8_t>(c->ld_Gp), kp4, c->stream));
     prof_end(c, "ld_compact");
-    HIPCHK(c, vcfxg::launch_ld_groups(P<vcfxg::LdVar>(c->ld_vars), M, P<uint8_t>(c->ld_gflag), c->stream));
+    // VCFXG_LD_SPARSE=0: no sparse-missing groups (their tiles take k_ld_mask)
+    static const bool sparse_env = [] {
+        const char *e = getenv("VCFXG_LD_SPARSE");
+        return !(e && e[0] == '0');
+    }();
+    const int sparse = sparse_env && n_samples > 0 && n_samples <= 16383 ? 1 : 0;  // (Sxy as u16 in the epilogue)
+    HIPCHK(c, vcfxg::launch_ld_groups(P<vcfxg::LdVar>(c->ld_vars), M, n_samples, sparse, P<uint8_t>(c->ld_gflag),
+                                      c->stream));
     c->ld_gflag_host.assign(M / vcfxg::kLdFastBlock + 1, 0);
     if (M)
         HIPCHK(c, hipMemcpyAsync(c->ld_gflag_host.data(), c->ld_gflag.p, (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock,
@@ -2184,7 +2196,50 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
     // a group with a missing genotype: the valid-mask and squared-dosage planes of the
     // missing-data kernel (k_ld_mask), next to the dosage plane ld_Gp
     c->ld_vq = false;
-    for (uint64_t g = 0; g * vcfxg::kLdFastBlock < M && !c->ld_vq; g++) c->ld_vq = !c->ld_gflag_host[g];
+    c->ld_sp = false;
+    for (uint64_t g = 0; g * vcfxg::kLdFastBlock < M; g++) {
+        c->ld_vq = c->ld_vq || c->ld_gflag_host[g] == 0;
+        c->ld_sp = c->ld_sp || c->ld_gflag_host[g] == 2;
+    }
+    if (c->ld_sp) {
+        // the missing samples of every variant (CSR) and the contribution plane of the
+        // sparse-missing kernel (vcfxg_ld_fast.hip, kSp)
+        prof_begin(c, "ld_sparse_prep");
+        r = ensure(c, c->ld_moff, 8 * (M + 1));
+        if (r) return r;
+        struct MissOf {
+            int ns;
+            __host__ __device__ uint64_t operator()(const vcfxg::LdVar &v) const { return (uint64_t)(ns - v.cnt); }
+        };
+        hipcub::TransformInputIterator<uint64_t, MissOf, const vcfxg::LdVar *> min(P<vcfxg::LdVar>(c->ld_vars),
+                                                                                   MissOf{n_samples});
+        size_t tmp2 = 0;
+        HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp2, min, P<uint64_t>(c->ld_moff), (int)M + 1, c->stream));
+        r = ensure(c, c->scan_tmp, tmp2);
+        if (r) return r;
+        // (entry M of the input is vars[M]: its cnt is written as ns below, so moff[M] = total)
+        static thread_local vcfxg::LdVar pad_var;
+        pad_var = vcfxg::LdVar{};
+        pad_var.cnt = n_samples;
+        HIPCHK(c, hipMemcpyAsync(P<vcfxg::LdVar>(c->ld_vars) + M, &pad_var, sizeof pad_var, hipMemcpyHostToDevice,
+                                 c->stream));
+        HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp2, min, P<uint64_t>(c->ld_moff), (int)M + 1,
+                                                   c->stream));
+        static thread_local uint64_t entries;
+        HIPCHK(c, hipMemcpyAsync(&entries, P<uint64_t>(c->ld_moff) + M, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const uint64_t mp = (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock * vcfxg::kLdFastBlock;
+        r = ensure(c, c->ld_midx, 2 * entries + 16);
+        if (!r) r = ensure(c, c->ld_mvar, 4 * entries + 16);
+        if (!r) r = ensure(c, c->ld_gt16, 2 * (size_t)n_samples * mp + 64);
+        if (r) return r;
+        HIPCHK(c, vcfxg::launch_ld_miss_fill(P<int8_t>(c->ld_Gc), M, kpad, n_samples, P<uint64_t>(c->ld_moff),
+                                             P<uint16_t>(c->ld_midx), P<uint32_t>(c->ld_mvar), c->stream));
+        HIPCHK(c, vcfxg::launch_ld_gt16(P<int8_t>(c->ld_Gc), M, kpad, n_samples, mp, P<uint16_t>(c->ld_gt16),
+                                        c->stream));
+        c->ld_mp = mp;
+        prof_end(c, "ld_sparse_prep");
+    }
     if (c->ld_vq) {
         r = ensure(c, c->ld_Gv, (size_t)(M + 1) * kp4 + 64);
         if (!r) r = ensure(c, c->ld_Gq, (size_t)(M + 1) * kp4 + 64);
@@ -2258,7 +2313,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     auto ifirst = [&](uint64_t J) { const uint64_t jr0 = J * BM; return jr0 > window ? (jr0 - window) / BM : 0; };
     const std::vector<uint8_t> &gf = c->ld_gflag_host;
     constexpr uint64_t kSub = vcfxg::kLdFastBlock / BM;  // 64-blocks per fast group
-    auto gcomp = [&](uint64_t b64) { return gf[b64 / kSub] != 0; };
+    auto gcomp = [&](uint64_t b64) { return gf[b64 / kSub] == 1; };
     static const bool use_mask = [] {
         const char *e = getenv("VCFXG_LD_MASK");
         return !(e && e[0] == '0');
@@ -2267,17 +2322,19 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     // per-group complete flags): a call with the same ones reuses the last lists and their
     // device copy (building 77 K tile pairs and copying them cost ~0.13 ms of host time per call)
     const bool mask_on = use_mask && c->ld_vq;
-    const uint64_t pkey[5] = {j0, j1, window, M, mask_on ? 1u : 0u};
+    const bool sp_on = c->ld_sp;
+    const uint64_t pkey[5] = {j0, j1, window, M, (mask_on ? 1u : 0u) | (sp_on ? 2u : 0u)};
     const bool hit = c->ld_plan_dev != nullptr && c->ld_plan_dev == c->ld_blocks.p &&
                      std::equal(pkey, pkey + 5, c->ld_plan_key) && c->ld_plan_gf == gf;
     std::vector<uint32_t> blocks;
     uint64_t nb = 1;
-    uint32_t nfast = 0, nmask = 0, nbl = 0;
+    uint32_t nfast = 0, nmask = 0, nbl = 0, nsp = 0;
     for (uint64_t J = j0 / BM; J * BM < j1; J++) nb = std::max<uint64_t>(nb, J - ifirst(J) + 1);
     if (hit) {
         nfast = c->ld_plan_n[0];
         nmask = c->ld_plan_n[1];
         nbl = c->ld_plan_n[2];
+        nsp = c->ld_plan_n[3];
     } else {
         // fast list first, in kSuper x kSuper super-tiles (row blocks J x column blocks I): the
         // kernel maps contiguous list ranges to one XCD, so the blocks an XCD runs at once share
@@ -2288,21 +2345,29 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
             return (uint64_t)(v > 0 ? v : 4);
         }();
         const uint64_t Jb = j0 / FB, Je = (j1 + FB - 1) / FB;
-        for (uint64_t J0 = Jb; J0 < Je; J0 += kSuper) {
-            const uint64_t J1 = std::min(Je, J0 + kSuper);
-            const uint64_t Ilo = ifirst(kSub * J0) / kSub;
-            for (uint64_t I0 = Ilo; I0 < J1; I0 += kSuper)
-                for (uint64_t J = J0; J < J1; J++) {
-                    if (!gf[J]) continue;
-                    const uint64_t Imin = std::max(I0, ifirst(kSub * J) / kSub), Imax = std::min(I0 + kSuper, J + 1);
-                    for (uint64_t I = Imin; I < Imax; I++)
-                        if (gf[I]) {
-                            blocks.push_back((uint32_t)I);
-                            blocks.push_back((uint32_t)J);
-                        }
-                }
+        // pass 0: both groups complete (k_ld_fast); pass 1: both complete or sparse-missing, not
+        // both complete (the sparse-missing form, kSp)
+        for (int pass = 0; pass < (sp_on ? 2 : 1); pass++) {
+            auto take = [&](uint64_t I, uint64_t J) {
+                return pass == 0 ? gf[I] == 1 && gf[J] == 1 : gf[I] && gf[J] && (gf[I] == 2 || gf[J] == 2);
+            };
+            for (uint64_t J0 = Jb; J0 < Je; J0 += kSuper) {
+                const uint64_t J1 = std::min(Je, J0 + kSuper);
+                const uint64_t Ilo = ifirst(kSub * J0) / kSub;
+                for (uint64_t I0 = Ilo; I0 < J1; I0 += kSuper)
+                    for (uint64_t J = J0; J < J1; J++) {
+                        if (!gf[J]) continue;
+                        const uint64_t Imin = std::max(I0, ifirst(kSub * J) / kSub), Imax = std::min(I0 + kSuper, J + 1);
+                        for (uint64_t I = Imin; I < Imax; I++)
+                            if (take(I, J)) {
+                                blocks.push_back((uint32_t)I);
+                                blocks.push_back((uint32_t)J);
+                            }
+                    }
+            }
+            if (pass == 0) nfast = (uint32_t)(blocks.size() / 2);
+            else nsp = (uint32_t)(blocks.size() / 2) - nfast;
         }
-        nfast = (uint32_t)(blocks.size() / 2);
         // the missing-data tiles (k_ld_mask, default): every 128 x 128 tile pair in the window
         // whose 256-groups are not both complete (those are k_ld_fast's); VCFXG_LD_MASK=0 keeps the
         // previous int8 kernel (k_ld_block) over every 64-block pair with an incomplete side
@@ -2311,14 +2376,16 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
             constexpr uint64_t TM = vcfxg::kLdMaskTile, kPerG = vcfxg::kLdFastBlock / vcfxg::kLdMaskTile;
             for (uint64_t J2 = j0 / TM; J2 * TM < j1; J2++) {
                 const uint64_t I2lo = ifirst(J2 * (TM / BM)) / (TM / BM);  // the first 64-row's window start
-                const bool jc = gf[J2 / kPerG] != 0;
+                const uint8_t gj = gf[J2 / kPerG];
                 for (uint64_t I2 = I2lo; I2 <= J2; I2++) {
-                    if (jc && gf[I2 / kPerG]) continue;  // a complete group pair: k_ld_fast
+                    const uint8_t gi = gf[I2 / kPerG];
+                    if (gi == 1 && gj == 1) continue;           // a complete group pair: k_ld_fast
+                    if (sp_on && gi && gj) continue;            // complete / sparse: the kSp kernel
                     blocks.push_back((uint32_t)I2);
                     blocks.push_back((uint32_t)J2);
                 }
             }
-            nmask = (uint32_t)(blocks.size() / 2) - nfast;
+            nmask = (uint32_t)(blocks.size() / 2) - nfast - nsp;
         } else {
             // for a complete row block J only the incomplete column blocks, found in the sorted list
             // of them (no scan over the whole window triangle on the host)
@@ -2340,7 +2407,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
                     blocks.push_back((uint32_t)J);
                 }
             }
-            nbl = (uint32_t)(blocks.size() / 2) - nfast;
+            nbl = (uint32_t)(blocks.size() / 2) - nfast - nsp;
         }
     }
     const uint64_t rows = j1 - j0;
@@ -2358,6 +2425,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
         c->ld_plan_n[0] = nfast;
         c->ld_plan_n[1] = nmask;
         c->ld_plan_n[2] = nbl;
+        c->ld_plan_n[3] = nsp;
         c->ld_plan_dev = c->ld_blocks.p;
     }
     // (no clearing of ld_cnt: the count kernels write every window slot the row scan reads)
@@ -2368,12 +2436,24 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     a.all_pass = a.tm <= 0.0;
     a.kp4 = c->ld_kp4;
     const uint32_t *cid = max_dist > 0 ? P<uint32_t>(c->ld_cid) : nullptr;
-    const uint32_t *fbl = P<uint32_t>(c->ld_blocks), *gbl = fbl + 2 * (size_t)nfast;
+    const uint32_t *fbl = P<uint32_t>(c->ld_blocks), *sbl = fbl + 2 * (size_t)nfast,
+                   *gbl = sbl + 2 * (size_t)nsp;
+    vcfxg::LdSparse spa;
+    if (nsp) {
+        spa.vars = P<vcfxg::LdVar>(c->ld_vars);
+        spa.gt16 = P<uint16_t>(c->ld_gt16);
+        spa.mp = c->ld_mp;
+        spa.moff = P<uint64_t>(c->ld_moff);
+        spa.midx = P<uint16_t>(c->ld_midx);
+        spa.mvar = P<uint32_t>(c->ld_mvar);
+        const double big = 4.0 * (double)c->ld_ns * (double)c->ld_ns;  // (k_ld_mask's bound)
+        spa.pe = (float)(big * std::ldexp(1.0, -23) + 1.0);
+    }
     // staging for the pairs the count pass finds (capacity: what the last chunk needed, at
     // least 4 M pairs; a larger chunk overflows once and the emit pass recomputes)
     vcfxg::LdStage stg;
     {
-        const uint64_t qcap = 16ull * nfast + 16;
+        const uint64_t qcap = 16ull * (nfast + nsp) + 16;
         const uint64_t tcap = c->ld_stage_cap_fixed ? c->ld_stage_cap_fixed : std::max<uint64_t>(c->ld_temp_cap, 4ull << 20);
         int r0 = ensure(c, c->ld_temp, sizeof(vcfxg::LdPair) * tcap);
         if (!r0) r0 = ensure(c, c->ld_quarters, sizeof(vcfxg::LdQuarter) * qcap);
@@ -2392,6 +2472,10 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     HIPCHK(c, vcfxg::launch_ld_fast(1, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
                                     P<uint16_t>(c->ld_cnt), vcfxg::LdOffsets{}, nullptr, stg, c->stream));
     prof_end(c, "ld_count");
+    prof_begin(c, "ld_count_sparse");
+    HIPCHK(c, vcfxg::launch_ld_sparse(1, P<uint8_t>(c->ld_Gp), spa, cid, a, sbl, nsp, P<uint16_t>(c->ld_cnt),
+                                      vcfxg::LdOffsets{}, nullptr, stg, c->stream));
+    prof_end(c, "ld_count_sparse");
     prof_begin(c, "ld_count_gen");
     HIPCHK(c, vcfxg::launch_ld_block(1, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,
                                      P<uint16_t>(c->ld_cnt), vcfxg::LdOffsets{}, nullptr, c->stream));
@@ -2427,10 +2511,13 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
         HIPCHK(c, vcfxg::launch_ld_scatter(P<vcfxg::LdQuarter>(c->ld_quarters), P<unsigned long long>(c->ld_stage_ctr),
                                            sctr[1], a, P<uint16_t>(c->ld_cnt), offs,
                                            P<vcfxg::LdPair>(c->ld_temp), P<vcfxg::LdPair>(c->ld_pairs), c->stream));
-    else
+    else {
         HIPCHK(c, vcfxg::launch_ld_fast(2, P<uint8_t>(c->ld_Gp), P<vcfxg::LdFast>(c->ld_fast), cid, a, fbl, nfast,
                                         P<uint16_t>(c->ld_cnt), offs, P<vcfxg::LdPair>(c->ld_pairs),
                                         vcfxg::LdStage{}, c->stream));
+        HIPCHK(c, vcfxg::launch_ld_sparse(2, P<uint8_t>(c->ld_Gp), spa, cid, a, sbl, nsp, P<uint16_t>(c->ld_cnt), offs,
+                                          P<vcfxg::LdPair>(c->ld_pairs), vcfxg::LdStage{}, c->stream));
+    }
     prof_end(c, "ld_emit");
     prof_begin(c, "ld_emit_gen");
     HIPCHK(c, vcfxg::launch_ld_block(2, P<int8_t>(c->ld_Gc), P<vcfxg::LdVar>(c->ld_vars), cid, a, gbl, nbl,

@@ -54,6 +54,38 @@ __device__ __forceinline__ double ld_fast_r2(const LdFast &fi, const LdFast &fj,
     return __dmul_rn(r, r);
 }
 
+// The prefilter.  With n, Sx, Sy, Sxy, Sxx, Syy exact integers (fp32 accumulators, < 2^24):
+//   C = n Sxy - Sx Sy,  Vx = n Sxx - Sx^2,  Vy = n Syy - Sy^2,  exact r^2 = C^2 / (Vx Vy).
+// c = fma(n, Sxy, -fl(Sx Sy)) errs from C by at most ulp(Sx Sy)/2 + ulp(c)/2 <= pe, where pe
+// (host: 2^-23 * 4 ns^2 + 1, twice the ulp of the largest magnitude 4 ns^2, plus one) bounds
+// both; the same for vx, vy.  So |C| <= |c| + pe, Vx >= vx - pe, Vy >= vy - pe, and a pair is a
+// candidate when (|c| + pe)^2 >= tm' max(vx - pe, 0) max(vy - pe, 0), tm' = tm (1 - 1e-5)
+// absorbing the fp32 roundings of these three products (< 1e-6 relative).  Every pair whose
+// exact r^2 reaches tm (threshold less the fp64 sequence's error margin, LdWindowArgs::tm) is a
+// candidate; candidates run the reference's fp64 sequence.
+__device__ __forceinline__ bool mask_candidate(float n, float sx, float sy, float sxy, float sxx, float syy, float pe,
+                                               float tmf) {
+    const float c = fabsf(__builtin_fmaf(n, sxy, -(sx * sy))) + pe;
+    const float vx = fmaxf(__builtin_fmaf(n, sxx, -(sx * sx)) - pe, 0.f);
+    const float vy = fmaxf(__builtin_fmaf(n, syy, -(sy * sy)) - pe, 0.f);
+    return c * c >= tmf * (vx * vy);
+}
+
+// computeRsqFast (:397-401) on the pair's sums: the own-variance gate of both variants, then
+// computeRsqSIMD's fp64 sequence (:383-392) with correctly rounded operations
+__device__ __forceinline__ double mask_r2(double gi, double gj, int n, int sx, int sy, int sxy, int sxx, int syy) {
+    if (gi <= 0.0 || gj <= 0.0) return 0.0;
+    if (n < 2) return 0.0;
+    const double dn = (double)n;
+    const double mx = __ddiv_rn((double)sx, dn), my = __ddiv_rn((double)sy, dn);
+    const double cov = __dsub_rn(__ddiv_rn((double)sxy, dn), __dmul_rn(mx, my));
+    const double vx = __dsub_rn(__ddiv_rn((double)sxx, dn), __dmul_rn(mx, mx));
+    const double vy = __dsub_rn(__ddiv_rn((double)syy, dn), __dmul_rn(my, my));
+    if (vx <= 0.0 || vy <= 0.0) return 0.0;
+    const double r = __ddiv_rn(cov, __dmul_rn(__dsqrt_rn(vx), __dsqrt_rn(vy)));
+    return __dmul_rn(r, r);
+}
+
 struct LdPair {
     uint32_t i, j;          // variant indices, i < j
     double r2;
@@ -109,7 +141,29 @@ hipError_t launch_ld_scatter(const LdQuarter *quarters, const unsigned long long
 hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const uint32_t *chrom_id,
                           const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
                           LdOffsets off, LdPair *pairs, const LdStage &st, hipStream_t s);
-hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, uint8_t *gflag, hipStream_t s);
+// per 256-group: 1 = every variant complete; 2 = (sparse != 0) every variant has at most
+// kLdSparseMax missing calls (the sparse-correction kernel's groups); 0 = other
+constexpr int kLdSparseMax = 15;
+hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, int ns, int sparse, uint8_t *gflag, hipStream_t s);
+
+// the sparse-missing form of k_ld_fast (vcfxg_ld_fast.hip, kSp): per variant its missing samples
+// (CSR: moff[v] .. moff[v + 1] into midx = sample, mvar = v) and the sample-major contribution
+// plane gt16[s * mp + v] = c(code): x | x^2 << 5 | missing << 11 (x = 0 for a missing call)
+struct LdSparse {
+    const LdVar *vars = nullptr;
+    const uint16_t *gt16 = nullptr;
+    uint64_t mp = 0;           // gt16 row stride (variants, a multiple of 256, zero past m)
+    const uint64_t *moff = nullptr;
+    const uint16_t *midx = nullptr;
+    const uint32_t *mvar = nullptr;
+    float pe = 0.f;            // the fp32 prefilter's error bound (as k_ld_mask)
+};
+hipError_t launch_ld_miss_fill(const int8_t *Gc, uint64_t m, int kpad, int ns, const uint64_t *moff, uint16_t *midx,
+                               uint32_t *mvar, hipStream_t s);
+hipError_t launch_ld_gt16(const int8_t *Gc, uint64_t m, int kpad, int ns, uint64_t mp, uint16_t *gt16, hipStream_t s);
+hipError_t launch_ld_sparse(int pass, const uint8_t *Gp, const LdSparse &sp, const uint32_t *chrom_id,
+                            const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
+                            LdOffsets off, LdPair *pairs, const LdStage &st, hipStream_t s);
 hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s);
 hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C, hipStream_t s);
 // FP4 row bytes for ns samples: two per byte, whole 64-byte k-slices

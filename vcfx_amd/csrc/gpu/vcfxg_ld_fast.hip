@@ -206,14 +206,303 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
     qtot[1] = wave_sum(nc[2] + nc[3]);
 }
 
+// ---- the sparse-missing epilogue (kSp) ------------------------------------------------------
+// computeRsqSIMD (VCFX_ld_calculator.cpp:352-393) sums over the samples valid in BOTH variants.
+// With a missing call coded 0 in the FP4 plane, the k-loop's X_i . X_j is already Sxy over them;
+// the other five sums differ from the per-variant ones only at the few missing samples
+// (M_i: the samples variant i misses, |M_i| <= kLdSparseMax in these groups):
+//   n   = ns - |M_i| - |M_j| + |M_i n M_j|
+//   Sx  = SX_i - sum_{s in M_j} x_is       Sxx = SQ_i - sum_{s in M_j} x_is^2
+//   Sy  = SX_j - sum_{s in M_i} x_js       Syy = SQ_j - sum_{s in M_i} x_js^2
+// (x = 0 where missing).  Per column half hp (128 columns) the block adds, for every missing
+// entry (i, s) of its rows, the 128 contributions gt16[s][J-half] into R[i][.] and, for every
+// entry (j, s) of the half's columns, the 256 contributions gt16[s][I] into C[j][.]: packed u16
+// c = x | x^2 << 5 | missing << 11, whose sums stay in their fields for <= 15 entries (LDS
+// atomic adds of u16 pairs).  So R[i][j] = (Sum x_js, Sum x_js^2, |M_i n M_j|) over s in M_i and
+// C[j][i] = (Sum x_is, Sum x_is^2, .) over s in M_j.  Then the half's waves run the exact
+// prefilter and fp64 sequence of k_ld_mask on each pair.
+constexpr int kSpR = 0;                           // R: [256 rows][128 cols] u16
+constexpr int kSpCStride = 260;                   // C: [128 cols][256 rows + 4 pad] u16
+constexpr int kSpC = 256 * 128 * 2;
+constexpr int kSpRC = kSpC + 128 * kSpCStride * 2;  // 132,096 B (the ring and the dense terms)
+constexpr int kSpInts = kRing + kFB * 32;         // per row / column packed sums (the records' area)
+static_assert(kSpRC <= kSpInts, "R and C must not reach the packed sums");
+static_assert(kSpInts + 2 * kFB * 8 <= kRing + kFB * 32 + 2 * kFvBytes, "packed sums fit the records' area");
+
+// a row's / column's (missing count, Sx, Sx2) packed for one 64-bit LDS read
+__device__ __forceinline__ uint64_t sp_pack(int m, int sx, int sx2) {
+    return (uint64_t)(uint32_t)m | ((uint64_t)(uint32_t)sx << 8) | ((uint64_t)(uint32_t)sx2 << 32);
+}
+
 template <int P>
+__device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8_t *lds, const LdWindowArgs &a,
+                                                   const LdSparse &sp, const uint32_t *__restrict__ chrom_id,
+                                                   uint32_t I4, uint32_t J4, uint16_t *__restrict__ cnt,
+                                                   LdOffsets off, LdPair *__restrict__ pairs, const LdStage &st) {
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
+    const int wi = w >> 1, wj = w & 1;
+    const int64_t M = (int64_t)a.m;
+    const int64_t ibase = (int64_t)I4 * kFB, jbase = (int64_t)J4 * kFB;
+    // Sxy <= 4 ns < 2^16 (ns <= 16383, launch_ld_sparse): the accumulators as u16 pairs, half the
+    // registers through the epilogue
+    uint32_t accp[2][4][8];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                accp[x][y][q] = (uint32_t)(int)acc[x][y][2 * q] | ((uint32_t)(int)acc[x][y][2 * q + 1] << 16);
+    uint64_t *pk = reinterpret_cast<uint64_t *>(lds + kSpInts);  // [256 rows][256 columns]
+    {
+        const int64_t v = t < kFB ? ibase + t : jbase + (t - kFB);
+        uint64_t q = 0;
+        if (v < M) {
+            const LdVar x = sp.vars[v];
+            q = sp_pack(a.ns - x.cnt, x.sx, x.sx2);
+        }
+        pk[t] = q;
+    }
+    uint32_t *R32 = reinterpret_cast<uint32_t *>(lds + kSpR);
+    uint32_t *C32 = reinterpret_cast<uint32_t *>(lds + kSpC);
+    const uint16_t *R16 = reinterpret_cast<const uint16_t *>(lds + kSpR);
+    const uint16_t *C16 = reinterpret_cast<const uint16_t *>(lds + kSpC);
+    const float tmf = a.all_pass ? 0.f : (float)(a.tm * (1.0 - 1e-5));
+    const uint64_t bI = 4ull * I4 + wi;
+    const int64_t i0 = (int64_t)bI * kLdBlock;
+    // the row entries are contiguous in the CSR (rows ibase .. ibase + 255)
+    const uint64_t re0 = sp.moff[ibase], re1 = sp.moff[ibase + kFB < M ? ibase + kFB : M];
+    for (int hp = 0; hp < 2; hp++) {
+        const int64_t jb = jbase + 128 * hp;  // this half's first column
+        for (int k = t * 16; k < kSpRC; k += kWaves * kWave * 16) *reinterpret_cast<uint4 *>(lds + k) = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        // row side: entry (i, s) adds gt16[s][jb + 0..127] into R[i][.]: lane l, columns 2l, 2l + 1
+        {
+            const uint16_t *col = sp.gt16 + jb + 2 * l;
+            uint64_t e = re0 + w;
+            for (; e + 3 * kWaves < re1; e += 4 * kWaves) {  // four entries' loads in flight
+                uint32_t vv[4], ii[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint64_t eu = e + u * kWaves;
+                    ii[u] = sp.mvar[eu] - (uint32_t)ibase;
+                    vv[u] = *reinterpret_cast<const uint32_t *>(col + (uint64_t)sp.midx[eu] * sp.mp);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) atomicAdd(&R32[ii[u] * 64 + l], vv[u]);
+            }
+            for (; e < re1; e += kWaves) {
+                const uint32_t ii = sp.mvar[e] - (uint32_t)ibase;
+                atomicAdd(&R32[ii * 64 + l], *reinterpret_cast<const uint32_t *>(col + (uint64_t)sp.midx[e] * sp.mp));
+            }
+        }
+        // column side: entry (j, s) adds gt16[s][ibase + 0..255] into C[j][.]: lane l, rows 4l..4l+3
+        if (jb < M) {
+            const uint64_t ce0 = sp.moff[jb], ce1 = sp.moff[jb + 128 < M ? jb + 128 : M];
+            const uint16_t *col = sp.gt16 + ibase + 4 * l;
+            uint64_t e = ce0 + w;
+            for (; e + 3 * kWaves < ce1; e += 4 * kWaves) {
+                uint32_t jj[4];
+                uint2 vv[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint64_t eu = e + u * kWaves;
+                    jj[u] = sp.mvar[eu] - (uint32_t)jb;
+                    vv[u] = *reinterpret_cast<const uint2 *>(col + (uint64_t)sp.midx[eu] * sp.mp);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    atomicAdd(&C32[jj[u] * (kSpCStride / 2) + 2 * l], vv[u].x);
+                    atomicAdd(&C32[jj[u] * (kSpCStride / 2) + 2 * l + 1], vv[u].y);
+                }
+            }
+            for (; e < ce1; e += kWaves) {
+                const uint32_t jj = sp.mvar[e] - (uint32_t)jb;
+                const uint2 vv = *reinterpret_cast<const uint2 *>(col + (uint64_t)sp.midx[e] * sp.mp);
+                atomicAdd(&C32[jj * (kSpCStride / 2) + 2 * l], vv.x);
+                atomicAdd(&C32[jj * (kSpCStride / 2) + 2 * l + 1], vv.y);
+            }
+        }
+        __syncthreads();
+        if (wj == hp) {
+            // the pairs of this wave: column j = jb + 32y + r, rows i0 + 32x + 8g + 4h + e; per
+            // (y, x) a 16-bit mask over k = 4g + e.  Pass A: the fp32 prefilter on every pair of
+            // the window (short-lived temporaries: one pair at a time); pass B, only where some
+            // pair is a candidate: the exact fp64 decision
+            uint32_t pass[4][2];
+            int64_t jv[4];
+            bool jokv[4];
+            // one pair's six sums, k a run-time index (Sxy picked from the packed accumulators by a
+            // select chain: no dynamic register indexing), for the rare per-candidate loops
+            auto sums_rt = [&](int x, int y, int k, int &n, int &sx, int &sy, int &sxy, int &sxx, int &syy) {
+                const int jj = 32 * y + r;
+                const int il = wi * 64 + 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
+                const uint64_t pi = pk[il], pj = pk[kFB + 128 * hp + jj];
+                const uint32_t rv = R16[il * 128 + jj];
+                const uint32_t cv = C16[jj * kSpCStride + il];
+                n = a.ns - (int)(pi & 0xFF) - (int)(pj & 0xFF) + (int)(rv >> 11);
+                sx = (int)((pi >> 8) & 0xFFFFFF) - (int)(cv & 31);
+                sxx = (int)(pi >> 32) - (int)((cv >> 5) & 63);
+                sy = (int)((pj >> 8) & 0xFFFFFF) - (int)(rv & 31);
+                syy = (int)(pj >> 32) - (int)((rv >> 5) & 63);
+                uint32_t v = accp[x][y][0];
+#pragma unroll
+                for (int q = 1; q < 8; q++) v = (k >> 1) == q ? accp[x][y][q] : v;
+                sxy = (int)((v >> (16 * (k & 1))) & 0xFFFFu);
+            };
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                const int64_t j = jb + 32 * y + r;
+                jv[y] = j;
+                const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
+                jokv[y] = jok;
+                const int64_t lo_i = j - (int64_t)a.window;
+#pragma unroll
+                for (int x = 0; x < 2; x++) {
+                    uint32_t cb = 0;
+                    if (jok) {
+                        // a run-time loop over g (the four-row groups; their two packed Sxy words by
+                        // a select chain): an unrolled loop over all 16 rows kept too much live
+#pragma unroll 1
+                        for (int g = 0; g < 4; g++) {
+                            uint32_t lo = accp[x][y][0], hi = accp[x][y][1];
+#pragma unroll
+                            for (int q = 1; q < 4; q++) {
+                                lo = g == q ? accp[x][y][2 * q] : lo;
+                                hi = g == q ? accp[x][y][2 * q + 1] : hi;
+                            }
+                            const int il0 = wi * 64 + 32 * x + 8 * g + 4 * h;
+                            const uint64_t pj = pk[kFB + 128 * hp + 32 * y + r];
+                            const uint2 cq = *reinterpret_cast<const uint2 *>(C16 + (32 * y + r) * kSpCStride + il0);
+#pragma unroll
+                            for (int e = 0; e < 4; e++) {
+                                const int64_t i = i0 + 32 * x + 8 * g + 4 * h + e;
+                                if (!(i < j && i >= lo_i)) continue;
+                                bool c = true;
+                                if (!a.all_pass) {
+                                    const int il = il0 + e;
+                                    const uint64_t pi = pk[il];
+                                    const uint32_t rv = R16[il * 128 + 32 * y + r];
+                                    const uint32_t cv = ((e < 2 ? cq.x : cq.y) >> (16 * (e & 1))) & 0xFFFFu;
+                                    const int n = a.ns - (int)(pi & 0xFF) - (int)(pj & 0xFF) + (int)(rv >> 11);
+                                    const int sx = (int)((pi >> 8) & 0xFFFFFF) - (int)(cv & 31);
+                                    const int sxx = (int)(pi >> 32) - (int)((cv >> 5) & 63);
+                                    const int sy = (int)((pj >> 8) & 0xFFFFFF) - (int)(rv & 31);
+                                    const int syy = (int)(pj >> 32) - (int)((rv >> 5) & 63);
+                                    const int sxy = (int)(((e < 2 ? lo : hi) >> (16 * (e & 1))) & 0xFFFFu);
+                                    c = mask_candidate((float)n, (float)sx, (float)sy, (float)sxy, (float)sxx,
+                                                       (float)syy, sp.pe, tmf);
+                                }
+                                cb |= c ? 1u << (4 * g + e) : 0u;
+                            }
+                        }
+                    }
+                    uint32_t pb = 0;
+                    for (uint32_t mm = cb; mm; mm &= mm - 1u) {  // (rare at useful thresholds)
+                        const int k = __builtin_ctz(mm);
+                        const int64_t i = i0 + 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
+                        if (a.max_dist > 0 && chrom_id[i] == chrom_id[j]) {
+                            int d = sp.vars[j].pos - sp.vars[i].pos;
+                            if (d < 0) d = -d;
+                            if (d > a.max_dist) continue;
+                        }
+                        int n, sx, sy, sxy, sxx, syy;
+                        sums_rt(x, y, k, n, sx, sy, sxy, sxx, syy);
+                        if (mask_r2(sp.vars[i].varx, sp.vars[j].varx, n, sx, sy, sxy, sxx, syy) >= a.threshold)
+                            pb |= 1u << k;
+                    }
+                    pass[y][x] = pb;
+                }
+            }
+            // the column's 64-row mask (both lanes h of column r hold it): row = 32x + 8g + 4h + e
+            auto full_of = [&](int y) {
+                uint64_t m64 = 0;
+#pragma unroll
+                for (int x = 0; x < 2; x++)
+#pragma unroll
+                    for (int k = 0; k < 16; k++)
+                        if ((pass[y][x] >> k) & 1u) m64 |= 1ull << (32 * x + 8 * (k >> 2) + 4 * h + (k & 3));
+                return m64 | (uint64_t)__shfl_xor((long long)m64, 32);
+            };
+            // every passing pair of this lane to dst + its rank among the column's passing rows
+            auto emit = [&](int y, uint64_t fm, LdPair *dst) {
+                const int64_t j = jv[y];
+#pragma unroll
+                for (int x = 0; x < 2; x++)
+                    for (uint32_t mm = pass[y][x]; mm; mm &= mm - 1u) {
+                        const int k = __builtin_ctz(mm);
+                        const int row = 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
+                        int n, sx, sy, sxy, sxx, syy;
+                        sums_rt(x, y, k, n, sx, sy, sxy, sxx, syy);
+                        const int64_t i = i0 + row;
+                        LdPair pr;
+                        pr.i = (uint32_t)i;
+                        pr.j = (uint32_t)j;
+                        pr.r2 = mask_r2(sp.vars[i].varx, sp.vars[j].varx, n, sx, sy, sxy, sxx, syy);
+                        dst[__popcll(fm & ((1ull << row) - 1ull))] = pr;
+                    }
+            };
+            auto slot_of = [&](int y, uint64_t &slot) {  // the count-table slot of (bI, column j's 64-block)
+                const uint64_t bJ = 4ull * J4 + 2 * hp + (y >> 1);
+                const uint64_t jrow0 = bJ * kLdBlock;
+                const uint64_t ifirst = jrow0 > a.window ? (jrow0 - a.window) / kLdBlock : 0;
+                slot = bI - ifirst;
+                return bI >= ifirst && bI <= bJ;
+            };
+            int nc[4];
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                uint64_t slot;
+                const bool in = jokv[y] && slot_of(y, slot);
+                const uint64_t fm = full_of(y);
+                nc[y] = in ? __popcll(fm) : 0;
+                if (P == 1 && h == 0 && in) cnt[(uint64_t)(jv[y] - (int64_t)a.j_lo) * a.nb + slot] = (uint16_t)nc[y];
+                if (P == 2 && nc[y]) emit(y, fm, pairs + off.at((uint64_t)(jv[y] - (int64_t)a.j_lo), a.nb, slot));
+            }
+            if (P == 1 && st.temp) {
+                // quarters (64 columns: y = 2hy, 2hy + 1) holding pairs, staged as k_ld_fast's count
+                // pass stages them: lane l <-> column l of the quarter (its own mask, y = 2hy + h)
+#pragma unroll
+                for (int hy = 0; hy < 2; hy++) {
+                    const int qt = wave_sum(h == 0 ? nc[2 * hy] + nc[2 * hy + 1] : 0);
+                    if (!qt) continue;  // wave-uniform
+                    const uint32_t c = (uint32_t)(h ? nc[2 * hy + 1] : nc[2 * hy]);
+                    const uint32_t incl = wave_incl_scan(c);
+                    const uint32_t total = wave_bcast(incl, kWave - 1);
+                    unsigned long long base = 0;
+                    if (l == 0) base = atomicAdd(st.ctr, (unsigned long long)total);
+                    base = __shfl(base, 0);
+                    if (base + total > st.cap) {
+                        if (l == 0) atomicOr(st.overflow, 1u);
+                        continue;
+                    }
+#pragma unroll
+                    for (int yy = 0; yy < 2; yy++) {
+                        const int y = 2 * hy + yy;
+                        const uint32_t run = (uint32_t)__shfl((int)(incl - c), 32 * yy + r);  // column 32yy + r
+                        if (nc[y]) emit(y, full_of(y), st.temp + base + run);
+                    }
+                    if (l == 0) {
+                        const unsigned long long q = atomicAdd(st.ctr + 1, 1ull);
+                        const uint32_t bJ = (uint32_t)(4ull * J4 + 2 * hp + hy);
+                        if (q < st.qcap) st.quarters[q] = LdQuarter{(uint32_t)bI, bJ, (uint64_t)base};
+                        else atomicOr(st.overflow, 1u);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // R and C are zeroed again for the next half
+    }
+}
+
+template <int P, bool kSp>
 __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__restrict__ Gp,
                                                             const LdFast *__restrict__ fv,
                                                             const uint32_t *__restrict__ chrom_id, LdWindowArgs a,
                                                             const uint32_t *__restrict__ blocks, uint32_t nblocks,
                                                             uint16_t *__restrict__ cnt,
                                                             LdOffsets off,
-                                                            LdPair *__restrict__ pairs, LdStage st) {
+                                                            LdPair *__restrict__ pairs, LdStage st, LdSparse sp) {
     // ONE LDS array (a second __shared__ object makes hipcc drain vmcnt before the k-loop's
     // ds_reads): the staging ring during the k-loop, then the waves' epilogue tiles over it;
     // the per-row prefilter terms after that
@@ -256,7 +545,7 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
         }
         if (!__syncthreads_or(any != 0)) return;
     }
-    {  // the I and J records: kFvBytes each, 1 KiB per wave-instruction.  A lane whose 16 B
+    if (!kSp) {  // the I and J records: kFvBytes each, 1 KiB per wave-instruction.  A lane whose 16 B
         // start past the array re-reads its last 16 B (rows / columns outside the matrix, never
         // used); a lane straddling the end reads < 16 B past it, inside the M + 1 records the
         // array is allocated with (vcfxg_ld_prepare)
@@ -369,6 +658,12 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
 #pragma unroll
                 for (int k = 0; k < 16; k++) z ^= (int)acc[x][y][k];
         if (z == 0x7fffffff) cnt[0] = 1;
+        return;
+    }
+    if constexpr (kSp) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave is done with the ring
+        ld_sparse_epilogue<P>(acc, lds, a, sp, chrom_id, I4, J4, cnt, off, pairs, st);
         return;
     }
     // the row and column terms from the DMA'd records (every wave's loads done, then visible)
@@ -550,11 +845,25 @@ hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const u
     if (!nblocks) return hipSuccess;
     if (a.kp4 % kBK || a.kp4 <= 0) return hipErrorInvalidValue;
     if (pass == 1)
-        hipLaunchKernelGGL(k_ld_fast<1>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
-                           nblocks, cnt, off, pairs, st);
+        hipLaunchKernelGGL((k_ld_fast<1, false>), dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
+                           nblocks, cnt, off, pairs, st, LdSparse{});
     else
-        hipLaunchKernelGGL(k_ld_fast<2>, dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
-                           nblocks, cnt, off, pairs, st);
+        hipLaunchKernelGGL((k_ld_fast<2, false>), dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, fv, chrom_id, a, blocks,
+                           nblocks, cnt, off, pairs, st, LdSparse{});
+    return hipGetLastError();
+}
+
+hipError_t launch_ld_sparse(int pass, const uint8_t *Gp, const LdSparse &sp, const uint32_t *chrom_id,
+                            const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
+                            LdOffsets off, LdPair *pairs, const LdStage &st, hipStream_t s) {
+    if (!nblocks) return hipSuccess;
+    if (a.kp4 % kBK || a.kp4 <= 0 || a.ns > 16383 || !sp.gt16 || !sp.vars || sp.mp % kFB) return hipErrorInvalidValue;
+    if (pass == 1)
+        hipLaunchKernelGGL((k_ld_fast<1, true>), dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, nullptr, chrom_id, a,
+                           blocks, nblocks, cnt, off, pairs, st, sp);
+    else
+        hipLaunchKernelGGL((k_ld_fast<2, true>), dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, nullptr, chrom_id, a,
+                           blocks, nblocks, cnt, off, pairs, st, LdSparse(sp));
     return hipGetLastError();
 }
 
@@ -648,25 +957,123 @@ hipError_t launch_ld_rowscan(const uint16_t *cnt, uint64_t rows, uint64_t nb, ui
     return hipGetLastError();
 }
 
-// per kLdFastBlock-variant group: 1 if every variant of the group is complete
-__global__ void k_ld_groups(const LdVar *__restrict__ vars, uint64_t m, uint8_t *__restrict__ gflag) {
+// per kLdFastBlock-variant group: 1 if every variant of the group is complete; 2 (sparse) if
+// every variant misses at most kLdSparseMax calls; else 0
+__global__ void k_ld_groups(const LdVar *__restrict__ vars, uint64_t m, int ns, int sparse, uint8_t *__restrict__ gflag) {
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x / 64 + threadIdx.x / 64;
     const uint64_t ng = (m + kFB - 1) / kFB;
     if (g >= ng) return;
     const int l = threadIdx.x & 63;
-    bool ok = true;
+    bool ok = true, sp = true;
     for (int k = l; k < kFB; k += 64) {
         const uint64_t v = g * kFB + k;
-        if (v < m) ok = ok && vars[v].complete;
+        if (v < m) {
+            ok = ok && vars[v].complete;
+            sp = sp && ns - vars[v].cnt <= kLdSparseMax;
+        }
     }
     ok = __all(ok);
-    if (l == 0) gflag[g] = ok ? 1 : 0;
+    sp = __all(sp);
+    if (l == 0) gflag[g] = ok ? 1 : (sparse && sp) ? 2 : 0;
 }
 
-hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, uint8_t *gflag, hipStream_t s) {
+hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, int ns, int sparse, uint8_t *gflag, hipStream_t s) {
     const uint64_t ng = (m + kFB - 1) / kFB;
     if (!ng) return hipSuccess;
-    hipLaunchKernelGGL(k_ld_groups, dim3((unsigned)((ng + 3) / 4)), dim3(256), 0, s, vars, m, gflag);
+    hipLaunchKernelGGL(k_ld_groups, dim3((unsigned)((ng + 3) / 4)), dim3(256), 0, s, vars, m, ns, sparse, gflag);
+    return hipGetLastError();
+}
+
+// per variant (one wave each): its missing samples (codes < 0 among the first ns) in sample
+// order into midx / mvar from moff[v] (16 codes per lane per step, ballot-free: a wave scan of
+// the per-lane counts)
+__global__ __launch_bounds__(256) void k_ld_miss_fill(const int8_t *__restrict__ Gc, uint64_t m, int kpad, int ns,
+                                                      const uint64_t *__restrict__ moff, uint16_t *__restrict__ midx,
+                                                      uint32_t *__restrict__ mvar) {
+    const int l = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t v = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 64; v < m; v += nw) {
+        const int8_t *row = Gc + v * (uint64_t)kpad;
+        uint64_t at = moff[v];
+        for (int s0 = 0; s0 < ns; s0 += 16 * 64) {
+            const int b = s0 + 16 * l;
+            uint32_t bits = 0;
+            if (b < kpad) {
+                const uint4 q = *reinterpret_cast<const uint4 *>(row + b);
+                const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if ((int8_t)(w[k >> 2] >> (8 * (k & 3))) < 0 && b + k < ns) bits |= 1u << k;
+            }
+            const uint32_t c = (uint32_t)__popc(bits);
+            const uint32_t incl = wave_incl_scan(c);
+            uint64_t o = at + incl - c;
+            while (bits) {
+                const int k = __builtin_ctz(bits);
+                bits &= bits - 1u;
+                midx[o] = (uint16_t)(b + k);
+                mvar[o] = (uint32_t)v;
+                o++;
+            }
+            at += wave_bcast(incl, 63);
+        }
+    }
+}
+
+hipError_t launch_ld_miss_fill(const int8_t *Gc, uint64_t m, int kpad, int ns, const uint64_t *moff, uint16_t *midx,
+                               uint32_t *mvar, hipStream_t s) {
+    if (!m) return hipSuccess;
+    if (kpad % 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ld_miss_fill, dim3((unsigned)std::min<uint64_t>((m + 3) / 4, 16384)), dim3(256), 0, s, Gc, m,
+                       kpad, ns, moff, midx, mvar);
+    return hipGetLastError();
+}
+
+// the sample-major contribution plane: 64 variants x 64 samples per block through LDS (rows of
+// Gc in, rows of gt16 out, both coalesced); variants past m and samples past ns are zero
+__global__ __launch_bounds__(256) void k_ld_gt16(const int8_t *__restrict__ Gc, uint64_t m, int kpad, int ns,
+                                                 uint64_t mp, uint16_t *__restrict__ gt16) {
+    __shared__ int8_t tile[64][68];
+    const uint64_t v0 = (uint64_t)blockIdx.x * 64;
+    const int s0 = blockIdx.y * 64;
+    const int t = threadIdx.x;
+    // load: 64 rows x 64 codes, 16 B per thread
+    {
+        const int rr = t >> 2, cc = (t & 3) * 16;
+        const uint64_t v = v0 + rr;
+        uint4 q = make_uint4(0, 0, 0, 0);
+        if (v < m && s0 + cc < kpad) q = *reinterpret_cast<const uint4 *>(Gc + v * (uint64_t)kpad + s0 + cc);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+        for (int k = 0; k < 16; k++) tile[rr][cc + k] = (int8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
+    __syncthreads();
+    // store: 64 sample rows x 64 variants as u16, 16 per thread (two 16 B stores)
+    const int ss = t >> 2, vv = (t & 3) * 16;
+    if (s0 + ss >= ns) return;
+    uint32_t o[8];
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        uint32_t pr = 0;
+#pragma unroll
+        for (int e = 0; e < 2; e++) {
+            const uint64_t v = v0 + vv + k + e;
+            const int g = v < m ? (int)tile[vv + k + e][ss] : 0;
+            const uint32_t c = g < 0 ? 2048u : g == 1 ? 33u : g == 2 ? 130u : 0u;
+            pr |= c << (16 * e);
+        }
+        o[k >> 1] = pr;
+    }
+    uint4 *dst = reinterpret_cast<uint4 *>(gt16 + (uint64_t)(s0 + ss) * mp + v0 + vv);
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+hipError_t launch_ld_gt16(const int8_t *Gc, uint64_t m, int kpad, int ns, uint64_t mp, uint16_t *gt16, hipStream_t s) {
+    if (!m || ns <= 0) return hipSuccess;
+    if (mp % 256 || mp < m || kpad % 64) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ld_gt16, dim3((unsigned)(mp / 64), (unsigned)((ns + 63) / 64)), dim3(256), 0, s, Gc, m, kpad,
+                       ns, mp, gt16);
     return hipGetLastError();
 }
 

@@ -67,37 +67,7 @@ __device__ __forceinline__ v16f mfma4(const v4i &a, const v4i &b, const v16f &c)
 }
 }  // namespace
 
-// The prefilter.  With n, Sx, Sy, Sxy, Sxx, Syy exact integers (fp32 accumulators, < 2^24):
-//   C = n Sxy - Sx Sy,  Vx = n Sxx - Sx^2,  Vy = n Syy - Sy^2,  exact r^2 = C^2 / (Vx Vy).
-// c = fma(n, Sxy, -fl(Sx Sy)) errs from C by at most ulp(Sx Sy)/2 + ulp(c)/2 <= pe, where pe
-// (host: 2^-23 * 4 ns^2 + 1, twice the ulp of the largest magnitude 4 ns^2, plus one) bounds
-// both; the same for vx, vy.  So |C| <= |c| + pe, Vx >= vx - pe, Vy >= vy - pe, and a pair is a
-// candidate when (|c| + pe)^2 >= tm' max(vx - pe, 0) max(vy - pe, 0), tm' = tm (1 - 1e-5)
-// absorbing the fp32 roundings of these three products (< 1e-6 relative).  Every pair whose
-// exact r^2 reaches tm (threshold less the fp64 sequence's error margin, LdWindowArgs::tm) is a
-// candidate; candidates run the reference's fp64 sequence.
-__device__ __forceinline__ bool mask_candidate(float n, float sx, float sy, float sxy, float sxx, float syy, float pe,
-                                               float tmf) {
-    const float c = fabsf(__builtin_fmaf(n, sxy, -(sx * sy))) + pe;
-    const float vx = fmaxf(__builtin_fmaf(n, sxx, -(sx * sx)) - pe, 0.f);
-    const float vy = fmaxf(__builtin_fmaf(n, syy, -(sy * sy)) - pe, 0.f);
-    return c * c >= tmf * (vx * vy);
-}
-
-// computeRsqFast (:397-401) on the pair's sums: the own-variance gate of both variants, then
-// computeRsqSIMD's fp64 sequence (:383-392) with correctly rounded operations
-__device__ __forceinline__ double mask_r2(double gi, double gj, int n, int sx, int sy, int sxy, int sxx, int syy) {
-    if (gi <= 0.0 || gj <= 0.0) return 0.0;
-    if (n < 2) return 0.0;
-    const double dn = (double)n;
-    const double mx = __ddiv_rn((double)sx, dn), my = __ddiv_rn((double)sy, dn);
-    const double cov = __dsub_rn(__ddiv_rn((double)sxy, dn), __dmul_rn(mx, my));
-    const double vx = __dsub_rn(__ddiv_rn((double)sxx, dn), __dmul_rn(mx, mx));
-    const double vy = __dsub_rn(__ddiv_rn((double)syy, dn), __dmul_rn(my, my));
-    if (vx <= 0.0 || vy <= 0.0) return 0.0;
-    const double r = __ddiv_rn(cov, __dmul_rn(__dsqrt_rn(vx), __dsqrt_rn(vy)));
-    return __dmul_rn(r, r);
-}
+// mask_candidate / mask_r2: vcfxg_ld.h (shared with the sparse-missing kernel)
 
 template <int P>
 __global__ __launch_bounds__(kWaves * kWave) void k_ld_mask(const uint8_t *__restrict__ Gx,
