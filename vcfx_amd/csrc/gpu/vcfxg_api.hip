@@ -398,7 +398,7 @@ static void reset_hints(vcfxg_ctx *c) {
 // line per call: tests check which path sharded ranks and fresh contexts run)
 static void note_schedule(vcfxg_ctx *c, const char *what) {
     c->last_schedule = what;
-    static const char *log = getenv("VCFXG_SCHEDULE_LOG");
+    const char *log = getenv("VCFXG_SCHEDULE_LOG");  // (read per call: tests set it in-process)
     if (!log) return;
     const int fd = ::open(log, O_WRONLY | O_APPEND | O_CREAT | O_CLOEXEC, 0644);
     if (fd < 0) return;
@@ -2313,7 +2313,8 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     auto ifirst = [&](uint64_t J) { const uint64_t jr0 = J * BM; return jr0 > window ? (jr0 - window) / BM : 0; };
     const std::vector<uint8_t> &gf = c->ld_gflag_host;
     constexpr uint64_t kSub = vcfxg::kLdFastBlock / BM;  // 64-blocks per fast group
-    auto gcomp = [&](uint64_t b64) { return gf[b64 / kSub] == 1; };
+    // a 64-block whose 256-group the fast or the sparse-missing kernel covers (with another such)
+    auto gcomp = [&](uint64_t b64) { const uint8_t g = gf[b64 / kSub]; return g == 1 || (g == 2 && c->ld_sp); };
     static const bool use_mask = [] {
         const char *e = getenv("VCFXG_LD_MASK");
         return !(e && e[0] == '0');

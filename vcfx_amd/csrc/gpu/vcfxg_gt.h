@@ -12,6 +12,11 @@
 #pragma once
 #include "vcfxg_device.h"
 
+// af_fixed's rolling loads (VCFXG_AF_ROLL=0: batch loads, for A/B)
+#ifndef VCFXG_AF_ROLL
+#define VCFXG_AF_ROLL 1
+#endif
+
 namespace vcfxg {
 
 struct DwordView {
@@ -515,7 +520,20 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
     const int lastblk = (Er - 1) & ~15;
     const int lo16 = lane() * kBlockBytes;
     uint32_t alt = 0, dots = 0, err = 0;
+#if VCFXG_AF_ROLL
+    // rolling loads: as soon as a wave-step's registers are read, the same step of the next batch
+    // is issued into them, so kUnroll steps stay in flight across batches (no bubble between a
+    // record's batches) at no register cost
+    uint4 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; u++) {  // branch-free: lanes past the record re-read its last block
+        const int blk = u * kWaveStep + lo16;
+        v[u] = load16(base, blk < Er ? blk : lastblk);
+    }
+    pre();
+#endif
     for (int w0 = 0; w0 < Er; w0 += kUnroll * kWaveStep) {
+#if !VCFXG_AF_ROLL
         uint4 v[kUnroll];
 #pragma unroll
         for (int u = 0; u < kUnroll; u++) {  // branch-free: lanes past the record re-read its last block
@@ -523,6 +541,8 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
             v[u] = load16(base, blk < Er ? blk : lastblk);
         }
         if (w0 == 0) pre();
+#endif
+        const int wn = w0 + kUnroll * kWaveStep;  // the next batch (wave-uniform)
         // the step's dwords, bytes outside [S, E) replaced by the expected ones (edge steps only)
         auto dwords = [&](int u, const uint4 &x, uint32_t(&d)[4]) {
             d[0] = x.x, d[1] = x.y, d[2] = x.z, d[3] = x.w;
@@ -541,6 +561,12 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
         for (int u = 0; u < kUnroll; u++) {
             uint32_t d[4];
             dwords(u, v[u], d);
+#if VCFXG_AF_ROLL
+            if (wn < Er) {
+                const int blk = wn + u * kWaveStep + lo16;
+                v[u] = load16(base, blk < Er ? blk : lastblk);
+            }
+#endif
             uint32_t berr = 0, balt = 0;
 #pragma unroll
             for (int i = 0; i < 4; i++) {
