@@ -141,6 +141,26 @@ def test_ngpu8_drop_in_at_full_size(inputs, case):
     assert got == c["stdout"], (case, got, c["stdout"], err[-2000:])
 
 
+@pytest.mark.parametrize("case,fused", [("pipeline_annot_af", True), ("pipeline_annot_nr_af", True),
+                                        ("pipeline_annot", True), ("pipeline_annot_af", False)])
+def test_vcfx_pipe_at_full_size(inputs, case, fused):
+    """vcfx_pipe (one process, one device context) on the 4.3 GB annotated shard: the fused
+    schedule (the input in HBM once, a walk per filter stage, AF rows gathered) and the
+    stage-by-stage one, against the reference's digest of the shell pipeline; the same chain
+    through the drop-in executables piped by the shell"""
+    import shlex
+    from vcfx_amd import BUILD
+    c = DIG["cases"][case]
+    path = inputs.path(c["input"])
+    chain = " | ".join(" ".join(shlex.quote(a.replace("{F}", path)) for a in st) for st in c["stages"])
+    env = "" if fused else "VCFX_PIPE_FUSED=0 "
+    got, rc, err = _hash_cmd(env + shlex.quote(os.path.join(BUILD, "bin", "vcfx_pipe")) + " " + shlex.quote(chain))
+    assert rc == 0, err[-2000:]
+    assert got == c["stdout"], (case, fused, got, c["stdout"], err[-2000:])
+    if not fused:
+        _check(case, inputs)
+
+
 @pytest.mark.parametrize("case,stdin", [("pipeline_annot", "none"), ("rf_stdin_annot", "pipe"),
                                         ("gq_strict_annot", "none")])
 def test_annotated_shard_matches_reference(inputs, case, stdin):
