@@ -479,6 +479,21 @@ def e2e_rates(workload, arr, a, offs=None):
                 runs["small_input_latency"] = lat
             finally:
                 os.unlink(small)
+        # the pipe-ingest ceiling on this host: `cat F | vcfx_drain` (reads the way the device-only
+        # stdin path does, F_SETPIPE_SZ 1 MiB, 32 MiB reads; one hot buffer, and rotating over
+        # four 32 MiB buffers -- the staging ring's cache footprint), best of 3
+        drain = os.path.join(REPO, "build", "bin", "vcfx_drain")
+        if os.access(drain, os.X_OK):
+            for name, extra in (("pipe_ceiling", ""), ("pipe_ceiling_ring4x32M", " 33554432 4")):
+                walls = []
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    subprocess.run(["bash", "-o", "pipefail", "-c", "cat '%s' | '%s'%s" % (path, drain, extra)],
+                                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=300, check=True)
+                    walls.append(time.perf_counter() - t0)
+                runs[name] = {"value": a.records / min(walls), "wall_s": [round(w, 4) for w in walls]}
+            runs["process_stdin_pipe"]["frac_of_pipe_ceiling"] = round(
+                runs["process_stdin_pipe"]["value"] / runs["pipe_ceiling"]["value"], 3)
         runs["pcie_ceiling"] = a.records / (arr.size / (PCIE_H2D_GBS * 1e9))
         runs["unit"] = "records/s"
         runs["cmd"] = "%s %s -i FILE > /dev/null (page-cache-warm %.2f GB file)" % (tool, " ".join(args), arr.size / 1e9)
