@@ -54,6 +54,11 @@ constexpr bool kGfFlags = VCFXG_GF_FLAGS != 0;
 #define VCFXG_GF_UNROLL 4
 #endif
 constexpr int kGfUnroll = VCFXG_GF_UNROLL;
+// the GT-only AF walk carries the next record's first wave-steps across records (af_fixed_x);
+// VCFXG_AF_XREC=0: each record's sweep issues its own first loads after its head's analysis
+#ifndef VCFXG_AF_XREC
+#define VCFXG_AF_XREC 1
+#endif
 
 // the walk's per-record reducer: AF allele counts (alt, total) or, for VCFX_hwe_tester, the
 // genotype classes (hom-ref, het, hom-alt; the third in aux_o)
@@ -153,6 +158,10 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             meta_o[o] = m;
         }
     };
+    // (AfOp, GT-only walk) the next record's first wave-steps, issued during this record's sweep
+    constexpr bool kXrec = VCFXG_AF_XREC && std::is_same<Op, AfOp>::value && !kGF;
+    uint4 xv[kXrec ? kWalkUnroll : 1];
+    int64_t xvb = -1;  // their base (-1: none)
     int cur = 0;
     int64_t A = L & ~(int64_t)15;  // window base of the current line (L - A < 32)
     if (L < ce2) prefetch_window(buf, A, hi, win[wv][cur]);
@@ -252,6 +261,10 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         bool ok = false;
         // DoseHeadOp: a predicted GT-only record is not swept (k_dose_fmt checks its bytes)
         bool skip = std::is_same<Op, DoseHeadOp>::value && predicted;
+        // the carried wave-steps are this record's only if its sweep is the first af_fixed_x call
+        // since they were issued (any other record or a re-sweep drops them)
+        int64_t xuse = xvb;
+        xvb = -1;
         auto sweep = [&]() {
             if constexpr (kGF) {
               if (gf) {  // gt_first from the sample start: the counts and the record end
@@ -295,7 +308,14 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                       : t8 + 2 < wend ? (uint8_t)sep_w
                                       : (uint8_t)__builtin_amdgcn_readfirstlane(byte_at(buf, t8 + 2));
                 Op op = R::make(buf, ae);
-                if constexpr (std::is_same<Op, AfOp>::value)
+                if constexpr (kXrec) {
+                    const int64_t use = xuse >= 0 && xuse <= S ? xuse : -1;
+                    xuse = -1;
+                    const int64_t nb = E + 1 < ce2 ? (E + 1) & ~(int64_t)15 : -1;  // this walker's next line
+                    int64_t vbo;
+                    ok = af_fixed_x<kWalkUnroll>(buf, S, ae, hi, op, sep, pre, xv, use, nb, vbo);
+                    xvb = vbo;
+                } else if constexpr (std::is_same<Op, AfOp>::value)
                     ok = af_fixed < kGF ? kGfUnroll : kWalkUnroll > (buf, S, ae, op, sep, pre);
                 else if constexpr (std::is_same<Op, DoseHeadOp>::value) {
                     if (skip) {  // samples (ae - S + 1) / 4, none "NA" (checked by k_dose_fmt)

@@ -598,6 +598,103 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
     return true;
 }
 
+// af_fixed on the walk's carried loads (VCFXG_AF_XREC): the same test and counts, with the
+// sweep's grid based at vb (16-aligned, <= S; the bytes before S are masked like those past E)
+// when v already holds the wave-steps [vb, vb + kUnroll KiB) (lane l: vb + 1 KiB u + 16 l),
+// or at S & ~15 with its own first loads when vb < 0.  Its rolling loads continue past the
+// record into the next line's first wave-steps, from nb (16-aligned) when nb >= 0: on a true
+// return v holds [nb, nb + kUnroll KiB) and vb_out = nb, so the next record's sweep starts
+// with its first KiBs already in flight -- issued before this record's last steps were read,
+// not after the next head's analysis.  vb_out = -1 otherwise.
+template <int kUnroll, class Pre>
+__device__ bool af_fixed_x(const char *__restrict__ buf, int64_t S, int64_t E, int64_t hi, AfOp &op, uint32_t sep_hint,
+                           Pre pre, uint4 (&v)[kUnroll], int64_t vb, int64_t nb, int64_t &vb_out) {
+    S = uniform64(S);
+    E = uniform64(E);
+    vb_out = -1;
+    const int64_t L = E - S;
+    if (L < 3 || ((L + 1) & 3)) return false;
+    uint32_t sepc = sep_hint ? sep_hint : byte_at(buf, S + 1);
+    sepc = __builtin_amdgcn_readfirstlane(sepc);
+    if (sepc != '/' && sepc != '|') return false;
+    const uint32_t sh = 8u * (uint32_t)(S & 3);
+    auto rot = [&](uint32_t x) { return sh ? (x << sh) | (x >> (32u - sh)) : x; };
+    const uint32_t exp = rot(0x09300030u | (sepc << 8));  // '0' s '0' \t
+    const uint32_t mbin = rot(0xFFFEFFFEu);
+    const uint32_t msep = rot(0xFF00FF00u);
+    const uint32_t fsh = (S & 1) ? 8u : 0u;
+    const int64_t b0 = vb >= 0 ? uniform64(vb) : S & ~(int64_t)15;
+    const char *__restrict__ base = buf + b0;
+    const int Sr = (int)(S - b0), Er = (int)(E - b0);
+    const int lastblk = (Er - 1) & ~15;
+    const int lo16 = lane() * kBlockBytes;
+    const int64_t hlast = (hi - 1) & ~(int64_t)15;
+    uint32_t alt = 0, dots = 0, err = 0;
+    if (vb < 0) {
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            const int blk = u * kWaveStep + lo16;
+            v[u] = load16(base, blk < Er ? blk : lastblk);
+        }
+    }
+    pre();
+    for (int w0 = 0; w0 < Er; w0 += kUnroll * kWaveStep) {
+        const int wn = w0 + kUnroll * kWaveStep;  // the next batch (wave-uniform)
+        auto dwords = [&](int u, const uint4 &x, uint32_t(&d)[4]) {
+            d[0] = x.x, d[1] = x.y, d[2] = x.z, d[3] = x.w;
+            const int w = w0 + u * kWaveStep;
+            if (!(w >= Sr && w + kWaveStep <= Er)) {  // wave-uniform
+                const int blk = w + lo16;
+                const uint32_t rm = blk < Er ? range16(blk, Sr, Er) : 0u;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t bm = nib_bytes((rm >> (4 * i)) & 0xFu);
+                    d[i] = (d[i] & bm) | (exp & ~bm);
+                }
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < kUnroll; u++) {
+            uint32_t d[4];
+            dwords(u, v[u], d);
+            if (wn < Er) {
+                const int blk = wn + u * kWaveStep + lo16;
+                v[u] = load16(base, blk < Er ? blk : lastblk);
+            } else if (nb >= 0) {  // the next line's first wave-steps
+                const int64_t g = nb + u * kWaveStep + lo16;
+                v[u] = load16(buf, g < hi ? g : hlast);
+            }
+            uint32_t berr = 0, balt = 0;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t e = d[i] ^ exp;
+                berr |= e & mbin;
+                balt += __popc(e);
+            }
+            if (!__any(berr != 0u)) {
+                alt += balt;
+                continue;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t e = d[i] ^ exp;
+                err |= e & msep;
+                const uint32_t f = (e >> fsh) & 0x00FF00FFu;
+                const uint32_t notdig = (f + 0x00F600F6u) & 0x01000100u;
+                const uint32_t notdot = ((f ^ 0x001E001Eu) + 0x00FF00FFu) & 0x01000100u;
+                err |= notdig & notdot;
+                dots += __popc(notdig);
+                alt += __popc((f + 0x00FF00FFu) & (notdig ^ 0x01000100u));
+            }
+        }
+        if (__any(err != 0u)) return false;
+    }
+    op.alt = wave_sum(alt);
+    op.tot = (uint32_t)(2 * ((L + 1) >> 2)) - wave_sum(dots);
+    vb_out = nb;
+    return true;
+}
+
 // ---------------------------------------------------------------------------------------
 // genotype-match reducer: genotypeMatchesFast (VCFX_genotype_query.cpp:275-316) over
 // extractNthField (:199-218); "any sample matches" (checkAnySampleMatches :322-345)
