@@ -2,6 +2,7 @@
 # End-to-end probe (measurement tool): AF on the 427,409 x 2,504 shard written to /tmp --
 # the pipe ceiling (`cat F | drain`), a fresh process per run (file and pipe), and the
 # in-process warm-context phase breakdown (VCFX_TIMING=1).  Output under gpurun_out/.
+#   bash tools/e2e_probe.sh [all|pipe]     pipe: the ceiling and the pipe runs only
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 F=/tmp/e2e_chr21.vcf
 python -c "
@@ -16,10 +17,12 @@ for i in 1 2 3; do
     echo -n "cat_pipe_cat "; time (cat $F | cat > /dev/null)
     [ -x $DRAIN ] && { echo -n "cat_pipe_drain "; time (cat $F | $DRAIN); }
 done
+MODE=${1:-all}
 for i in 1 2 3; do
+    [ $MODE = pipe ] && break
     echo -n "fresh_file "; time (VCFX_TIMING=$((i == 1)) timeout -k 5 60 $AF -q -i $F > /dev/null) || exit 1
 done
-for cfg in "33554432 4" "4194304 8" "2097152 8" "1048576 16" "8388608 4"; do
+for cfg in "1048576 16" "2097152 8" "524288 32" "1048576 8"; do
     set -- $cfg
     echo -n "cat_pipe_drain_ring $1x$2 "; time (cat $F | $DRAIN $1 $2)
     echo -n "fresh_pipe ring $1x$2 "
@@ -27,7 +30,9 @@ for cfg in "33554432 4" "4194304 8" "2097152 8" "1048576 16" "8388608 4"; do
 done
 for i in 1 2 3; do
     echo -n "fresh_pipe "; time (cat $F | VCFX_TIMING=$((i == 1)) timeout -k 5 60 $AF -q > /dev/null) || exit 1
+    echo -n "cat_pipe_drain_ring 1048576x16 "; time (cat $F | $DRAIN 1048576 16)
 done
+[ $MODE = pipe ] && { rm -f $F; exit 0; }
 echo -n "fresh_file_mapped "; time (VCFX_FILE_STREAM=0 timeout -k 5 60 $AF -q -i $F > /dev/null) || exit 1
 VCFX_TIMING=1 timeout -k 5 120 python tools/e2e_warm.py $F || exit 1
 # ring shapes (warm context, the last of three runs each)

@@ -42,8 +42,9 @@ KERNELS = {
     "nr_records": r"vcfxg::k_nr_records\(",
     "gq_records": r"vcfxg::k_(line_meta|gq_sweep|gq_complex)\(",
     "ld_parse": r"vcfxg::k_ld_parse\(",
-    "ld_count": r"vcfxg::k_ld_fast<1>\(",
-    "ld_emit": r"vcfxg::k_ld_fast<2>\(",
+    "ld_count": r"vcfxg::k_ld_fast<1, ?false>\(",
+    "ld_count_sparse": r"vcfxg::k_ld_fast<1, ?true>\(",
+    "ld_emit": r"vcfxg::k_ld_fast<2, ?(false|true)>\(",
     "ld_count_gen": r"vcfxg::k_ld_block<1>\(",
     "ld_emit_gen": r"vcfxg::k_ld_block<2>\(",
     "ld_matrix": r"vcfxg::k_ld_matrix\(",
@@ -64,7 +65,7 @@ TIMED = {
     "nonref": ("fq_walk", "fq_rest", "line_count", "line_emit", "line_compact", "nr_records"),
     "dose": ("dose_walk", "walk_compact", "dose_fmt"),
     "ld": ("line_count", "line_emit", "line_compact", "ld_parse", "ld_count", "ld_emit", "ld_count_gen",
-           "ld_emit_gen", "ld_matrix", "ld_pack_vq", "ld_count_mask", "ld_emit_mask"),
+           "ld_emit_gen", "ld_matrix", "ld_pack_vq", "ld_count_mask", "ld_emit_mask", "ld_count_sparse"),
 }
 
 

@@ -54,10 +54,13 @@ constexpr bool kGfFlags = VCFXG_GF_FLAGS != 0;
 #define VCFXG_GF_UNROLL 4
 #endif
 constexpr int kGfUnroll = VCFXG_GF_UNROLL;
-// the GT-only AF walk carries the next record's first wave-steps across records (af_fixed_x);
-// VCFXG_AF_XREC=0: each record's sweep issues its own first loads after its head's analysis
+// VCFXG_AF_XREC=1: the GT-only AF walk carries the next record's first wave-steps across
+// records (af_fixed_x).  Measured slower (r04 A/B: af_walk 1.010-1.016 ms at 6 steps, 1.001 at
+// 3, against 0.896-0.904 for the default, 112 VGPRs / occupancy 4 against 95 / 5): the
+// per-record gap it hides is smaller than the occupancy it costs.  Default 0: each record's
+// sweep issues its own first loads after its head's analysis
 #ifndef VCFXG_AF_XREC
-#define VCFXG_AF_XREC 1
+#define VCFXG_AF_XREC 0
 #endif
 
 // the walk's per-record reducer: AF allele counts (alt, total) or, for VCFX_hwe_tester, the

@@ -12,9 +12,12 @@
 #pragma once
 #include "vcfxg_device.h"
 
-// af_fixed's rolling loads (VCFXG_AF_ROLL=0: batch loads, for A/B)
+// af_fixed's loads: a batch of kUnroll wave-steps per sweep step (default), or rolling
+// (VCFXG_AF_ROLL=1: a step's loads re-issued as soon as it is consumed).  r04 A/B on one box,
+// 2 alternations each (af_walk ms): batch 0.896-0.904, rolling 0.969-0.970, rolling at 5 steps
+// 0.916-0.919 -- the rolling variant's extra VGPRs cost occupancy
 #ifndef VCFXG_AF_ROLL
-#define VCFXG_AF_ROLL 1
+#define VCFXG_AF_ROLL 0
 #endif
 
 namespace vcfxg {
@@ -542,7 +545,9 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
         }
         if (w0 == 0) pre();
 #endif
+#if VCFXG_AF_ROLL
         const int wn = w0 + kUnroll * kWaveStep;  // the next batch (wave-uniform)
+#endif
         // the step's dwords, bytes outside [S, E) replaced by the expected ones (edge steps only)
         auto dwords = [&](int u, const uint4 &x, uint32_t(&d)[4]) {
             d[0] = x.x, d[1] = x.y, d[2] = x.z, d[3] = x.w;

@@ -32,7 +32,8 @@
 #include <type_traits>
 
 // VCFXG_LD_EXPT (diagnostic builds only, results invalid): bit 0 skips the epilogue, bit 3
-// stages k-slice 0 every step, bit 4 reads rows 0..255 for every block
+// stages k-slice 0 every step, bit 4 reads rows 0..255 for every block; sparse epilogue: bit 5
+// skips the missing-entry gathers, bit 6 the per-pair prefilter
 #ifndef VCFXG_LD_EXPT
 #define VCFXG_LD_EXPT 0
 #endif
@@ -221,6 +222,13 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
 // atomic adds of u16 pairs).  So R[i][j] = (Sum x_js, Sum x_js^2, |M_i n M_j|) over s in M_i and
 // C[j][i] = (Sum x_is, Sum x_is^2, .) over s in M_j.  Then the half's waves run the exact
 // prefilter and fp64 sequence of k_ld_mask on each pair.
+#ifndef VCFXG_LD_SP_ROWU
+#define VCFXG_LD_SP_ROWU 16
+#endif
+#ifndef VCFXG_LD_SP_COLU
+#define VCFXG_LD_SP_COLU 8
+#endif
+constexpr int kSpRowU = VCFXG_LD_SP_ROWU, kSpColU = VCFXG_LD_SP_COLU;
 constexpr int kSpR = 0;                           // R: [256 rows][128 cols] u16
 constexpr int kSpCStride = 260;                   // C: [128 cols][256 rows + 4 pad] u16
 constexpr int kSpC = 256 * 128 * 2;
@@ -239,7 +247,8 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                                                    const LdSparse &sp, const uint32_t *__restrict__ chrom_id,
                                                    uint32_t I4, uint32_t J4, uint16_t *__restrict__ cnt,
                                                    LdOffsets off, LdPair *__restrict__ pairs, const LdStage &st) {
-    const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
+    // (w wave-uniform: the CSR entry indices and their sample / variant loads are scalar)
+    const int t = threadIdx.x, w = __builtin_amdgcn_readfirstlane(t >> 6), l = t & 63, r = l & 31, h = l >> 5;
     const int wi = w >> 1, wj = w & 1;
     const int64_t M = (int64_t)a.m;
     const int64_t ibase = (int64_t)I4 * kFB, jbase = (int64_t)J4 * kFB;
@@ -276,20 +285,22 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
         const int64_t jb = jbase + 128 * hp;  // this half's first column
         for (int k = t * 16; k < kSpRC; k += kWaves * kWave * 16) *reinterpret_cast<uint4 *>(lds + k) = make_uint4(0, 0, 0, 0);
         __syncthreads();
-        // row side: entry (i, s) adds gt16[s][jb + 0..127] into R[i][.]: lane l, columns 2l, 2l + 1
-        {
+        // row side: entry (i, s) adds gt16[s][jb + 0..127] into R[i][.]: lane l, columns 2l, 2l + 1.
+        // The gathers are latency-bound (one 256 / 512 B row piece per entry, gt16 is not L2-
+        // resident): kSpRowU / kSpColU entries' loads in flight per wave
+        if (!(VCFXG_LD_EXPT & 32)) {
             const uint16_t *col = sp.gt16 + jb + 2 * l;
             uint64_t e = re0 + w;
-            for (; e + 3 * kWaves < re1; e += 4 * kWaves) {  // four entries' loads in flight
-                uint32_t vv[4], ii[4];
+            for (; e + (kSpRowU - 1) * kWaves < re1; e += kSpRowU * kWaves) {
+                uint32_t vv[kSpRowU], ii[kSpRowU];
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < kSpRowU; u++) {
                     const uint64_t eu = e + u * kWaves;
                     ii[u] = sp.mvar[eu] - (uint32_t)ibase;
                     vv[u] = *reinterpret_cast<const uint32_t *>(col + (uint64_t)sp.midx[eu] * sp.mp);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; u++) atomicAdd(&R32[ii[u] * 64 + l], vv[u]);
+                for (int u = 0; u < kSpRowU; u++) atomicAdd(&R32[ii[u] * 64 + l], vv[u]);
             }
             for (; e < re1; e += kWaves) {
                 const uint32_t ii = sp.mvar[e] - (uint32_t)ibase;
@@ -297,21 +308,21 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
             }
         }
         // column side: entry (j, s) adds gt16[s][ibase + 0..255] into C[j][.]: lane l, rows 4l..4l+3
-        if (jb < M) {
+        if (jb < M && !(VCFXG_LD_EXPT & 32)) {
             const uint64_t ce0 = sp.moff[jb], ce1 = sp.moff[jb + 128 < M ? jb + 128 : M];
             const uint16_t *col = sp.gt16 + ibase + 4 * l;
             uint64_t e = ce0 + w;
-            for (; e + 3 * kWaves < ce1; e += 4 * kWaves) {
-                uint32_t jj[4];
-                uint2 vv[4];
+            for (; e + (kSpColU - 1) * kWaves < ce1; e += kSpColU * kWaves) {
+                uint32_t jj[kSpColU];
+                uint2 vv[kSpColU];
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < kSpColU; u++) {
                     const uint64_t eu = e + u * kWaves;
                     jj[u] = sp.mvar[eu] - (uint32_t)jb;
                     vv[u] = *reinterpret_cast<const uint2 *>(col + (uint64_t)sp.midx[eu] * sp.mp);
                 }
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < kSpColU; u++) {
                     atomicAdd(&C32[jj[u] * (kSpCStride / 2) + 2 * l], vv[u].x);
                     atomicAdd(&C32[jj[u] * (kSpCStride / 2) + 2 * l + 1], vv[u].y);
                 }
@@ -360,7 +371,7 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
 #pragma unroll
                 for (int x = 0; x < 2; x++) {
                     uint32_t cb = 0;
-                    if (jok) {
+                    if (jok && !(VCFXG_LD_EXPT & 64)) {
                         // a run-time loop over g (the four-row groups; their two packed Sxy words by
                         // a select chain): an unrolled loop over all 16 rows kept too much live
 #pragma unroll 1

@@ -54,7 +54,10 @@ size_t prefetch_bytes() { return env_bytes("VCFX_PREFETCH_BYTES", (size_t)1 << 2
 // the pipe path streams to the device in chunks of this size
 size_t stream_chunk() { return env_bytes("VCFX_STREAM_CHUNK", (size_t)64 << 20); }
 // pinned staging slots of a device-only stream (4 of them)
-size_t ring_slot() { return env_bytes("VCFX_RING_SLOT", (size_t)32 << 20); }
+// the pipe ring: 16 slots of 1 MiB (r04 e2e probe, 4.30 GB through `cat F |`: ring read rate 9.0
+// GB/s at 1 MiB x 16, 8.2 at 2 MiB x 8, 7.1 at 4 MiB x 8, 6.3 at 32 MiB x 4 -- slots that stay in
+// the host's caches between the reader's write and the DMA's read)
+size_t ring_slot() { return env_bytes("VCFX_RING_SLOT", (size_t)1 << 20); }
 // the host window through which pass-through tools read a device-only input back
 size_t window_bytes() { return env_bytes("VCFX_WINDOW_BYTES", (size_t)64 << 20); }
 
@@ -518,6 +521,46 @@ ssize_t read_full(int fd, char *dst, size_t want, int *err) {
 }
 }  // namespace
 
+// The device-only pipe path's head copy: the head (read into host memory while the context
+// opened, often 0.5-2 GB) is copied to the device from pageable memory on a helper thread (~22
+// GB/s) while this thread keeps reading the pipe into the region behind it; repeated until the
+// bytes left are few, so the pipe never waits for the copy.  eof: the stream ended meanwhile
+// (everything then is on the device except the final-chunk marker).  false: a copy failed.
+static bool catch_up(vcfxg_ctx *g, int fd, char *base, size_t cap, size_t &got, bool &eof, int *read_errno) {
+    const size_t kRest = (size_t)8 << 20;
+    size_t at = 0;
+    for (;;) {
+        const size_t upto = got;
+        if (upto - at <= kRest || eof) {
+            if (upto > at && vcfxg_ingest(g, base + at, upto - at, 0) != VCFXG_OK) return false;
+            return true;
+        }
+        std::atomic<bool> fin{false};
+        bool ok = true;
+        std::thread t([&] {
+            ok = vcfxg_ingest(g, base + at, upto - at, 0) == VCFXG_OK;
+            fin.store(true, std::memory_order_release);
+        });
+        while (!fin.load(std::memory_order_acquire)) {
+            if (cap - got < ((size_t)8 << 20)) {
+                eof = true;  // the reservation is exhausted: treated as the end (as read_fd does)
+                break;
+            }
+            ssize_t k = ::read(fd, base + got, (size_t)8 << 20);
+            if (k < 0 && errno == EINTR) continue;
+            if (k < 0) *read_errno = errno;
+            if (k <= 0) {
+                eof = true;
+                break;
+            }
+            got += (size_t)k;
+        }
+        t.join();
+        if (!ok) return false;
+        at = upto;
+    }
+}
+
 void Input::read_fd(int fd, bool host_copy) {
     p = "";
     n = host_n = 0;
@@ -624,11 +667,17 @@ void Input::read_fd(int fd, bool host_copy) {
         // the caller needs only the header on the host (VCFX_allele_freq_calc): the rest goes
         // straight to the device through a pinned staging ring -- no host copy, no page faults
         vcfxg_ctx *g = gpu_quiet();
-        if (g && vcfxg_ingest_begin(g, (size_t)1 << 30) == VCFXG_OK && vcfxg_ingest(g, base, got, 0) == VCFXG_OK) {
+        bool eof = false;
+        if (g && vcfxg_ingest_begin(g, (size_t)1 << 30) == VCFXG_OK && catch_up(g, fd, base, cap, got, eof, &read_errno)) {
             host_n = got;
             stream_ctx = g;
             ring_ctx = g;
-            const int kSlots = (int)std::min<size_t>(64, std::max<size_t>(2, env_bytes("VCFX_RING_SLOTS", 4)));
+            if (eof) {  // all of it arrived while the head was copied
+                n = streamed = got;
+                phase("stdin streamed to the device (during the head copy)");
+                return;
+            }
+            const int kSlots = (int)std::min<size_t>(64, std::max<size_t>(2, env_bytes("VCFX_RING_SLOTS", 16)));
             const size_t kSlot = ring_slot();
             bool ok = true;
             for (int i = 0; i < kSlots && ok; i++) {
