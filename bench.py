@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the CPU baseline leg")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end CLI timings")
+    ap.add_argument("--no-output-check", action="store_true",
+                    help="skip the reference-digest check (diagnostic builds whose results are invalid)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL, default) or gloo (rehearsal on one GPU)")
     a = ap.parse_args()
     if a.records is None:
@@ -841,7 +843,8 @@ def main():
         if ld:
             out["pairs_per_gpu"] = pairs
             out["pairs_emitted"] = np_
-        out["output_check"] = output_check(a.workload, eng, s, a, rank, arr)
+        out["output_check"] = ({"checked": False, "match": None, "what": "--no-output-check (diagnostic run)"}
+                           if a.no_output_check else output_check(a.workload, eng, s, a, rank, arr))
         if world == 1 and not a.no_e2e and not general:
             out["e2e"] = e2e_rates(a.workload, arr, a, offs)
         if world == 1 and not a.no_cpu_baseline:

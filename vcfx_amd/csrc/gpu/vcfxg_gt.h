@@ -368,9 +368,10 @@ __device__ __forceinline__ void af_freq_text(int mode, int32_t a, int32_t t, uin
 // A sample start p (S, and the byte after a tab) is accepted when p+1 is '/' or '|', p+3 is
 // ':', a tab or the line's '\n', and p, p+2 are digits or '.': the quick GT c0 s c2, whose
 // tokens are c0 and c2 alone (letters and the like at p or p+2 go to the exact path, as do
-// CRLF line ends).  The flags of p+1..p+3 are lined up with p's by v_alignbyte over
-// neighbouring dwords; tot and alt are popcounts of the accepted starts' digit and
-// nonzero-digit flags at p and p+2.  Same contract as gt_first: the record end E (first '\n'
+// CRLF line ends).  The flags of p+1 and p+3 are lined up with p's by v_alignbyte over
+// neighbouring dwords, and the start flags are moved to p+2 the same way, so the allele bytes
+// (p and p+2) are one flag word: tot and alt are popcounts of its digit and nonzero-digit
+// flags (r04: 8 fewer VALU per dword than aligning the digit flags of p+2 to p).  Same contract as gt_first: the record end E (first '\n'
 // at or after S, else hi), pre(E) as soon as it is known, false (wave-uniform) -> the
 // caller's exact path; on true op.alt / op.tot hold the record's counts.
 // ---------------------------------------------------------------------------------------
@@ -383,6 +384,7 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
     bool found = false;
     uint32_t bad = 0, asc = 0, tot = 0, alt = 0;
     uint32_t carry = 0;  // tab flags of the previous step's last lane (byte 3: the byte before this step)
+    uint32_t scarry = 0;  // its last dword's starts
     const int64_t b0 = S & ~(int64_t)15;
     const int lo16 = lane() * kBlockBytes;
     for (int64_t w0 = b0; w0 < hi && !found; w0 += kU * kWaveStep) {
@@ -437,12 +439,32 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
                 rm = blk < hi ? range_mask16(blk, S, ae) : 0u;
                 rm |= ((S >= blk && S < blk + 16) ? 1u << (S - blk) : 0u) << 16;  // S: a start
             }
-            // ---- dword by dword (classes of W[i] and W[i+1] live at a time): each start
-            // needs c1 separator, c3 terminator, c0 / c2 digit or '.'; then the counts
-            auto classes = [&](uint32_t x, uint32_t &tab, uint32_t &sep, uint32_t &trm, uint32_t &vv, uint32_t &dg,
-                               uint32_t &nz) {
+            // ---- the starts of the lane's 4 dwords (bit 7 of each byte), then the starts two
+            // bytes back (s2: the c2 position of a start; dword 0's first two bytes are the
+            // previous lane's, or the previous step's last lane's, last two starts).  A byte is
+            // never both (a start two bytes after a start has a tab at the earlier start's
+            // separator: that start is bad), so u = st | s2 marks every allele byte once.
+            uint32_t st[4];
+            {
+                uint32_t tp = tprev;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const uint32_t tb = i == 3 ? tab3 : ~((W[i] ^ kRepTab) + K);
+                    uint32_t x = __builtin_amdgcn_alignbyte(tb, tp, 3) & M;
+                    if (edge || found)
+                        x = (x | nib_bytes((rm >> (16 + 4 * i)) & 0xFu)) & nib_bytes((rm >> (4 * i)) & 0xFu) & M;
+                    st[i] = x;
+                    tp = tb;
+                }
+            }
+            const uint32_t sup = (uint32_t)__shfl_up((int)st[3], 1);
+            const uint32_t sprev = lane() ? sup : scarry;
+            scarry = (uint32_t)__shfl((int)st[3], kWave - 1);
+            // ---- dword by dword (classes of W[i] and W[i+1] live at a time): each start needs
+            // c1 separator and c3 terminator, each allele byte (c0, c2) a digit or '.'; the counts
+            // are the allele bytes' digit / nonzero-digit flags
+            auto classes = [&](uint32_t x, uint32_t &sep, uint32_t &trm, uint32_t &vv, uint32_t &dg, uint32_t &nz) {
                 const uint32_t nt = (x ^ kRepTab) + K, nn = (x ^ kRepNl) + K, nc = (x ^ kRepColon) + K;
-                tab = ~nt;
                 trm = ~(nt & nn & nc);
                 sep = ~(((x ^ 0x2F2F2F2Fu) + K) & ((x ^ 0x7C7C7C7Cu) + K));
                 const uint32_t g9 = x + 0x46464646u;  // >= ':'
@@ -450,25 +472,20 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
                 nz = (x + 0x4F4F4F4Fu) & ~g9;         // '1'..'9'
                 vv = dg | ~((x ^ 0x2E2E2E2Eu) + K);
             };
-            uint32_t tab0, sep0, trm0, v0, dg0, nz0;
-            classes(W[0], tab0, sep0, trm0, v0, dg0, nz0);
+            uint32_t sep0, trm0, v0, dg0, nz0;
+            classes(W[0], sep0, trm0, v0, dg0, nz0);
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                uint32_t tab1, sep1, trm1, v1, dg1, nz1;
-                classes(W[i + 1], tab1, sep1, trm1, v1, dg1, nz1);
-                uint32_t st = __builtin_amdgcn_alignbyte(tab0, tprev, 3) & M;
-                if (edge || found)
-                    st = (st | nib_bytes((rm >> (16 + 4 * i)) & 0xFu)) & nib_bytes((rm >> (4 * i)) & 0xFu) & M;
+                uint32_t sep1, trm1, v1, dg1, nz1;
+                classes(W[i + 1], sep1, trm1, v1, dg1, nz1);
                 const uint32_t s1 = __builtin_amdgcn_alignbyte(sep1, sep0, 1);
                 const uint32_t c3 = __builtin_amdgcn_alignbyte(trm1, trm0, 3);
-                const uint32_t v2 = __builtin_amdgcn_alignbyte(v1, v0, 2);
-                const uint32_t d2 = __builtin_amdgcn_alignbyte(dg1, dg0, 2);
-                const uint32_t n2 = __builtin_amdgcn_alignbyte(nz1, nz0, 2);
-                bad |= st & ~(s1 & c3 & v0 & v2);
-                tot += __popc(st & dg0) + __popc(st & d2);
-                alt += __popc(st & nz0) + __popc(st & n2);
-                tprev = tab0;
-                tab0 = tab1, sep0 = sep1, trm0 = trm1, v0 = v1, dg0 = dg1, nz0 = nz1;
+                const uint32_t s2 = __builtin_amdgcn_alignbyte(st[i], i ? st[i - 1] : sprev, 2);
+                const uint32_t u = st[i] | s2;
+                bad |= (st[i] & ~(s1 & c3)) | (u & ~v0);
+                tot += __popc(u & dg0);
+                alt += __popc(u & nz0);
+                sep0 = sep1, trm0 = trm1, v0 = v1, dg0 = dg1, nz0 = nz1;
             }
         }
     }
