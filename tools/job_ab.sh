@@ -1,13 +1,7 @@
 #!/bin/bash
-# r04 job: LD sparse-missing kernel (gather batching / ablations), pipe-path exit cost
-for v in build_ldu4 build_ldu2 build_ldu8 build_lde32 build_lde64 build_lde96; do
-    export VCFXG_GPU_LIB=$v/libvcfx_gpu.so
-    x=""; case $v in *e32|*e64|*e96) x=--no-output-check;; esac
-    bash gpu_job.sh run ldmiss_${v#build_} 300 python -u bench.py --workload ld --missing-rate 0.001 --no-cpu-baseline --no-e2e --steps 3 $x || exit $?
-done
-unset VCFXG_GPU_LIB
-TIMEFORMAT="%R s"
-for m in 0 1 2 3 4; do
-    echo "teardown mode $m"; time (timeout -k 5 60 build/bin/teardown 1800000000 $m) || exit $?
-done > gpurun_out/teardown.log 2>&1
-cat gpurun_out/teardown.log
+# r04 job: sparse-missing LD with the per-block prefilter (parity + bench), pipe head release
+bash gpu_job.sh test tests/test_gpu_ld.py tests/test_gpu_stream.py tests/test_gpu_pipe.py || exit $?
+bash gpu_job.sh run ldmiss 300 python -u bench.py --workload ld --missing-rate 0.001 --no-cpu-baseline --no-e2e --steps 3 || exit $?
+bash gpu_job.sh run ldmiss4 300 python -u bench.py --workload ld --missing-rate 0.004 --no-cpu-baseline --no-e2e --steps 3 --no-output-check || exit $?
+bash gpu_job.sh run ld 300 python -u bench.py --workload ld --no-cpu-baseline --no-e2e --steps 3 || exit $?
+bash gpu_job.sh run e2e_pipe 300 bash tools/e2e_probe.sh pipe || exit $?

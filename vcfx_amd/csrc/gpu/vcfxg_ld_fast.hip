@@ -223,10 +223,10 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
 // C[j][i] = (Sum x_is, Sum x_is^2, .) over s in M_j.  Then the half's waves run the exact
 // prefilter and fp64 sequence of k_ld_mask on each pair.
 #ifndef VCFXG_LD_SP_ROWU
-#define VCFXG_LD_SP_ROWU 16
+#define VCFXG_LD_SP_ROWU 8
 #endif
 #ifndef VCFXG_LD_SP_COLU
-#define VCFXG_LD_SP_COLU 8
+#define VCFXG_LD_SP_COLU 4
 #endif
 constexpr int kSpRowU = VCFXG_LD_SP_ROWU, kSpColU = VCFXG_LD_SP_COLU;
 constexpr int kSpR = 0;                           // R: [256 rows][128 cols] u16
@@ -236,10 +236,141 @@ constexpr int kSpRC = kSpC + 128 * kSpCStride * 2;  // 132,096 B (the ring and t
 constexpr int kSpInts = kRing + kFB * 32;         // per row / column packed sums (the records' area)
 static_assert(kSpRC <= kSpInts, "R and C must not reach the packed sums");
 static_assert(kSpInts + 2 * kFB * 8 <= kRing + kFB * 32 + 2 * kFvBytes, "packed sums fit the records' area");
+// the prefilter's per-row (5) and per-column (3) fp32 terms and the block maxima, after them
+constexpr int kSpTerms = kSpInts + 2 * kFB * 8;
+static_assert(kSpTerms + 8 * kFB * 4 + 16 <= kRing + kFB * 32 + 2 * kFvBytes, "prefilter terms fit the records' area");
 
 // a row's / column's (missing count, Sx, Sx2) packed for one 64-bit LDS read
 __device__ __forceinline__ uint64_t sp_pack(int m, int sx, int sx2) {
     return (uint64_t)(uint32_t)m | ((uint64_t)(uint32_t)sx << 8) | ((uint64_t)(uint32_t)sx2 << 32);
+}
+
+// The sparse epilogue's prefilter (every wave, on its own accumulators, before any table).
+// Per variant, over its own present samples: N = ns - m, S, Q, V = N Q - S^2, xs its largest
+// dosage (1 when Q == S).  The pair's common samples drop k_i <= m_j of variant i's, whose sums
+// a_i <= min(k_i xs_i, S_i) and b_i <= min(k_i xs_i^2, Q_i) leave (MI / MJ the block's largest
+// missing counts over its rows / columns, am = min(M_other xs, S), AI / AJ the largest am over
+// the rows / columns):
+//   |C| <= |N_i Sxy - S_i S_j| + MJ Sxy + AJ (S_i + am_i) + AI S_j + E
+//   Vx  >= V_i - N_i min(MJ xs_i^2, Q_i) - MJ Q_i           (Vy alike, with MI)
+// (C - (N_i Sxy - S_i S_j) = (m_ij - m_j) Sxy + S_i a_j + S_j a_i - a_i a_j with n = N_i - k_i,
+// k_i = m_j - m_ij, Sx = S_i - a_i, Sy = S_j - a_j; E = 16 ulps of 4 ns^2 covers the fp32 roundings), so a
+// pair whose exact r^2 reaches tm has |C| >= sqrt(tm' Vxmin Vymin): it is a candidate.  A
+// variant that fails mask_r2's own-variance gate never is.  Per two rows of a column: five
+// packed fp32 instructions and two compares (the dense register epilogue's form).
+__device__ __forceinline__ void ld_sparse_prefilter(const v16f (&acc)[2][4], int8_t *lds, const LdWindowArgs &a,
+                                                    const LdSparse &sp, uint32_t I4, uint32_t J4,
+                                                    uint32_t (&cbm)[4][2]) {
+    const int t = threadIdx.x, w = t >> 6, l = t & 63, r = l & 31, h = l >> 5;
+    const int wi = w >> 1, wj = w & 1;
+    const int64_t M = (int64_t)a.m;
+    const int64_t ibase = (int64_t)I4 * kFB, jbase = (int64_t)J4 * kFB;
+    float *tS = reinterpret_cast<float *>(lds + kSpTerms);
+    float *tN = tS + kFB, *tU = tN + kFB, *tM = tU + kFB, *tD = tM + kFB;
+    float *cS = tD + kFB, *cV = cS + kFB, *cE = cV + kFB;
+    int *mx = reinterpret_cast<int *>(cE + kFB);  // MI, MJ, AI, AJ
+    if (t < 4) mx[t] = 0;
+    __syncthreads();
+    {
+        const bool row = t < kFB;
+        const int64_t v = row ? ibase + t : jbase + (t - kFB);
+        const bool vok = v < M;
+        LdVar x{};
+        if (vok) x = sp.vars[v];
+        const int mv = vok ? a.ns - x.cnt : 0;
+        const int xs = x.sx2 != x.sx ? 2 : 1;
+        atomicMax(&mx[row ? 0 : 1], mv);
+        __syncthreads();
+        const int Mo = row ? mx[1] : mx[0];  // the other side's largest missing count
+        const int am = vok ? min(Mo * xs, x.sx) : 0;
+        atomicMax(&mx[row ? 2 : 3], am);
+        __syncthreads();
+        const int AI = mx[2], AJ = mx[3];
+        const double N = x.cnt, S = x.sx, Q = x.sx2;
+        const double vmin = N * Q - S * S - N * fmin((double)(Mo * xs * xs), Q) - (double)Mo * Q;
+        const bool live = vok && x.varx > 0.0;
+        if (row) {
+            const float tmf = (float)(a.tm * (1.0 - 1e-5));
+            const float E = (float)(4.0 * a.ns * (double)a.ns * 0x1p-18);
+            tS[t] = (float)x.sx;
+            tN[t] = (float)x.cnt;
+            tU[t] = live ? sqrtf(tmf * (float)fmax(vmin, 0.0)) : INFINITY;
+            tM[t] = -(float)Mo;
+            tD[t] = -((float)AJ * (float)(x.sx + am) + E);
+        } else {
+            const int c = t - kFB;
+            cS[c] = (float)x.sx;
+            cV[c] = live ? sqrtf((float)fmax(vmin, 0.0)) : INFINITY;
+            cE[c] = -(float)AI * (float)x.sx;
+        }
+    }
+    __syncthreads();
+    const int64_t i0 = (int64_t)(4ull * I4 + wi) * kLdBlock;
+    float Sj[4], Vj[4], Ej[4];
+    int lo[4], span[4];
+    bool full = true;
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+        const int cj = 128 * wj + 32 * y + r;
+        const int64_t j = jbase + cj;
+        Sj[y] = cS[cj], Vj[y] = cV[cj], Ej[y] = cE[cj];
+        const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
+        // valid rows [lo, lo + span) of the wave's 64: i in [j - window, j)
+        const int64_t l0 = j - (int64_t)a.window - i0, h0 = j - i0;
+        const int lw = (int)(l0 > 0 ? (l0 < 64 ? l0 : 64) : 0);
+        const int hw = (int)(h0 > 0 ? (h0 < 64 ? h0 : 64) : 0);
+        lo[y] = lw;
+        span[y] = jok && hw > lw ? hw - lw : 0;
+        full = full && span[y] == 64;
+#pragma unroll
+        for (int x = 0; x < 2; x++) cbm[y][x] = a.all_pass ? 0xFFFFu : 0u;
+    }
+    if (!a.all_pass) {
+#pragma unroll
+        for (int x = 0; x < 2; x++)
+#pragma unroll
+            for (int g = 0; g < 4; g++) {
+                const int lr = wi * 64 + 32 * x + 8 * g + 4 * h;
+                const float4 S4 = *reinterpret_cast<const float4 *>(tS + lr);
+                const float4 N4 = *reinterpret_cast<const float4 *>(tN + lr);
+                const float4 U4 = *reinterpret_cast<const float4 *>(tU + lr);
+                const float4 M4 = *reinterpret_cast<const float4 *>(tM + lr);
+                const float4 D4 = *reinterpret_cast<const float4 *>(tD + lr);
+#pragma unroll
+                for (int e2 = 0; e2 < 4; e2 += 2) {
+                    const f2 Si = e2 ? f2{S4.z, S4.w} : f2{S4.x, S4.y};
+                    const f2 Ni = e2 ? f2{N4.z, N4.w} : f2{N4.x, N4.y};
+                    const f2 Ui = e2 ? f2{U4.z, U4.w} : f2{U4.x, U4.y};
+                    const f2 Mi = e2 ? f2{M4.z, M4.w} : f2{M4.x, M4.y};
+                    const f2 Di = e2 ? f2{D4.z, D4.w} : f2{D4.x, D4.y};
+                    const int k = 4 * g + e2;
+#pragma unroll
+                    for (int y = 0; y < 4; y++) {
+                        const f2 A = f2{acc[x][y][k], acc[x][y][k + 1]};
+                        const f2 Pp = Si * f2{Sj[y], Sj[y]};
+                        const f2 C = __builtin_elementwise_fma(Ni, A, -Pp);
+                        const f2 R = __builtin_elementwise_fma(Ui, f2{Vj[y], Vj[y]}, f2{Ej[y], Ej[y]});
+                        const f2 T = __builtin_elementwise_fma(Mi, A, R) + Di;
+                        cbm[y][x] |= (fabsf(C.x) >= T.x ? 1u << k : 0u) | (fabsf(C.y) >= T.y ? 2u << k : 0u);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);  // (one row group's terms live at a time)
+            }
+    }
+    if (!__all(full)) {
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+#pragma unroll
+            for (int x = 0; x < 2; x++) {
+                uint32_t vm = 0;
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const int row = 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
+                    vm |= (unsigned)(row - lo[y]) < (unsigned)span[y] ? 1u << k : 0u;
+                }
+                cbm[y][x] &= vm;
+            }
+    }
 }
 
 template <int P>
@@ -252,16 +383,6 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
     const int wi = w >> 1, wj = w & 1;
     const int64_t M = (int64_t)a.m;
     const int64_t ibase = (int64_t)I4 * kFB, jbase = (int64_t)J4 * kFB;
-    // Sxy <= 4 ns < 2^16 (ns <= 16383, launch_ld_sparse): the accumulators as u16 pairs, half the
-    // registers through the epilogue
-    uint32_t accp[2][4][8];
-#pragma unroll
-    for (int x = 0; x < 2; x++)
-#pragma unroll
-        for (int y = 0; y < 4; y++)
-#pragma unroll
-            for (int q = 0; q < 8; q++)
-                accp[x][y][q] = (uint32_t)(int)acc[x][y][2 * q] | ((uint32_t)(int)acc[x][y][2 * q + 1] << 16);
     uint64_t *pk = reinterpret_cast<uint64_t *>(lds + kSpInts);  // [256 rows][256 columns]
     {
         const int64_t v = t < kFB ? ibase + t : jbase + (t - kFB);
@@ -276,13 +397,34 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
     uint32_t *C32 = reinterpret_cast<uint32_t *>(lds + kSpC);
     const uint16_t *R16 = reinterpret_cast<const uint16_t *>(lds + kSpR);
     const uint16_t *C16 = reinterpret_cast<const uint16_t *>(lds + kSpC);
-    const float tmf = a.all_pass ? 0.f : (float)(a.tm * (1.0 - 1e-5));
     const uint64_t bI = 4ull * I4 + wi;
     const int64_t i0 = (int64_t)bI * kLdBlock;
+    // ---- the prefilter, on every wave's own accumulators (before the tables): a bound on the
+    // pair's r^2 from the per-variant sums and the block's largest missing counts, in the
+    // register epilogue's packed form; only halves holding a candidate build the tables
+    uint32_t cbm[4][2];
+    ld_sparse_prefilter(acc, lds, a, sp, I4, J4, cbm);
+    // Sxy <= 4 ns < 2^16 (ns <= 16383, launch_ld_sparse): the accumulators as u16 pairs, half the
+    // registers through the rest of the epilogue
+    uint32_t accp[2][4][8];
+#pragma unroll
+    for (int x = 0; x < 2; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++)
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                accp[x][y][q] = (uint32_t)(int)acc[x][y][2 * q] | ((uint32_t)(int)acc[x][y][2 * q + 1] << 16);
     // the row entries are contiguous in the CSR (rows ibase .. ibase + 255)
     const uint64_t re0 = sp.moff[ibase], re1 = sp.moff[ibase + kFB < M ? ibase + kFB : M];
     for (int hp = 0; hp < 2; hp++) {
         const int64_t jb = jbase + 128 * hp;  // this half's first column
+        uint32_t anyc = 0;
+        if (wj == hp)
+#pragma unroll
+            for (int y = 0; y < 4; y++) anyc |= cbm[y][0] | cbm[y][1];
+        // (no candidate in the half: no tables; its counts are written as 0 below)
+        const bool tables = __syncthreads_or(anyc != 0u);
+        if (tables) {
         for (int k = t * 16; k < kSpRC; k += kWaves * kWave * 16) *reinterpret_cast<uint4 *>(lds + k) = make_uint4(0, 0, 0, 0);
         __syncthreads();
         // row side: entry (i, s) adds gt16[s][jb + 0..127] into R[i][.]: lane l, columns 2l, 2l + 1.
@@ -335,11 +477,11 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
             }
         }
         __syncthreads();
+        }
         if (wj == hp) {
             // the pairs of this wave: column j = jb + 32y + r, rows i0 + 32x + 8g + 4h + e; per
-            // (y, x) a 16-bit mask over k = 4g + e.  Pass A: the fp32 prefilter on every pair of
-            // the window (short-lived temporaries: one pair at a time); pass B, only where some
-            // pair is a candidate: the exact fp64 decision
+            // (y, x) the prefilter's 16-bit candidate mask over k = 4g + e, and on its candidates
+            // the exact decision (the six sums from the tables, mask_r2's fp64 sequence)
             uint32_t pass[4][2];
             int64_t jv[4];
             bool jokv[4];
@@ -365,49 +507,10 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
             for (int y = 0; y < 4; y++) {
                 const int64_t j = jb + 32 * y + r;
                 jv[y] = j;
-                const bool jok = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
-                jokv[y] = jok;
-                const int64_t lo_i = j - (int64_t)a.window;
+                jokv[y] = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
 #pragma unroll
                 for (int x = 0; x < 2; x++) {
-                    uint32_t cb = 0;
-                    if (jok && !(VCFXG_LD_EXPT & 64)) {
-                        // a run-time loop over g (the four-row groups; their two packed Sxy words by
-                        // a select chain): an unrolled loop over all 16 rows kept too much live
-#pragma unroll 1
-                        for (int g = 0; g < 4; g++) {
-                            uint32_t lo = accp[x][y][0], hi = accp[x][y][1];
-#pragma unroll
-                            for (int q = 1; q < 4; q++) {
-                                lo = g == q ? accp[x][y][2 * q] : lo;
-                                hi = g == q ? accp[x][y][2 * q + 1] : hi;
-                            }
-                            const int il0 = wi * 64 + 32 * x + 8 * g + 4 * h;
-                            const uint64_t pj = pk[kFB + 128 * hp + 32 * y + r];
-                            const uint2 cq = *reinterpret_cast<const uint2 *>(C16 + (32 * y + r) * kSpCStride + il0);
-#pragma unroll
-                            for (int e = 0; e < 4; e++) {
-                                const int64_t i = i0 + 32 * x + 8 * g + 4 * h + e;
-                                if (!(i < j && i >= lo_i)) continue;
-                                bool c = true;
-                                if (!a.all_pass) {
-                                    const int il = il0 + e;
-                                    const uint64_t pi = pk[il];
-                                    const uint32_t rv = R16[il * 128 + 32 * y + r];
-                                    const uint32_t cv = ((e < 2 ? cq.x : cq.y) >> (16 * (e & 1))) & 0xFFFFu;
-                                    const int n = a.ns - (int)(pi & 0xFF) - (int)(pj & 0xFF) + (int)(rv >> 11);
-                                    const int sx = (int)((pi >> 8) & 0xFFFFFF) - (int)(cv & 31);
-                                    const int sxx = (int)(pi >> 32) - (int)((cv >> 5) & 63);
-                                    const int sy = (int)((pj >> 8) & 0xFFFFFF) - (int)(rv & 31);
-                                    const int syy = (int)(pj >> 32) - (int)((rv >> 5) & 63);
-                                    const int sxy = (int)(((e < 2 ? lo : hi) >> (16 * (e & 1))) & 0xFFFFu);
-                                    c = mask_candidate((float)n, (float)sx, (float)sy, (float)sxy, (float)sxx,
-                                                       (float)syy, sp.pe, tmf);
-                                }
-                                cb |= c ? 1u << (4 * g + e) : 0u;
-                            }
-                        }
-                    }
+                    const uint32_t cb = cbm[y][x];
                     uint32_t pb = 0;
                     for (uint32_t mm = cb; mm; mm &= mm - 1u) {  // (rare at useful thresholds)
                         const int k = __builtin_ctz(mm);

@@ -155,6 +155,10 @@ void Input::join_populate() const {
 
 Input::~Input() {
     join_populate();
+    if (releasing.joinable()) {  // (the process ends next: whatever is left goes with it)
+        if (g_process_exit_fast) releasing.detach();
+        else releasing.join();
+    }
     if (g_process_exit_fast) return;  // the process ends next: let exit() drop the mappings
     if (ring_ctx)
         for (void *r : ring) vcfxg_host_free(ring_ctx, r);
@@ -669,7 +673,9 @@ void Input::read_fd(int fd, bool host_copy) {
         vcfxg_ctx *g = gpu_quiet();
         bool eof = false;
         if (g && vcfxg_ingest_begin(g, (size_t)1 << 30) == VCFXG_OK && catch_up(g, fd, base, cap, got, eof, &read_errno)) {
-            host_n = got;
+            // the host keeps the header only (the records are on the device); the head's other
+            // pages are released once the stream is in (below)
+            host_n = scanned;
             stream_ctx = g;
             ring_ctx = g;
             if (eof) {  // all of it arrived while the head was copied
@@ -709,6 +715,12 @@ void Input::read_fd(int fd, bool host_copy) {
             }
             n = total;
             streamed = ok ? total : 0;  // a failure is reported when the input is used
+            // the head's record pages: freed by a helper thread while the device computes (1-2 GB
+            // of anonymous memory take ~40 ms/GB to free, at process exit otherwise: r04
+            // teardown probe; freed while the ring streams, they slowed its DMA: r04 e2e probe)
+            const size_t keep = (scanned + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+            if (got > keep + ((size_t)64 << 20))
+                releasing = std::thread([b = base + keep, len = got - keep] { madvise(b, len, MADV_DONTNEED); });
             if (timing_on) {
                 char b[160];
                 snprintf(b, sizeof b, "stdin streamed to the device (head %zu MB; ring: wait %.1f, read %.1f, ingest %.1f ms)",
