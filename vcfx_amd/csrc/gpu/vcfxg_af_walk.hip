@@ -113,7 +113,10 @@ __attribute__((amdgpu_waves_per_eu(1, VCFXG_WALK_MAXW)))
 #else
 // the GT-first walk at <= 128 VGPRs (4 waves per SIMD; it needs 129 unconstrained, which
 // rounds to 136 and 3 waves)
-__attribute__((amdgpu_waves_per_eu(kGF ? 4 : 1)))
+#ifndef VCFXG_AF_MINW
+#define VCFXG_AF_MINW 1
+#endif
+__attribute__((amdgpu_waves_per_eu(kGF ? 4 : VCFXG_AF_MINW)))
 #endif
 void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chunk, int64_t n_walkers, int mode,
                int64_t span0, uint64_t cap_w, uint64_t *__restrict__ le_o, int32_t *__restrict__ alt_o,

@@ -73,6 +73,12 @@ __device__ __forceinline__ T wave_sum(T v) {
 }
 template <typename T>
 __device__ __forceinline__ T wave_bcast(T v, int src) { return __shfl(v, src); }
+// lane i gets lane i - 1's x, lane 0 gets 0: one DPP move (wave_shr:1), no LDS permute
+__device__ __forceinline__ uint32_t lane_prev(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);
+}
+// the last lane's x, wave-uniform (v_readlane into a scalar register)
+__device__ __forceinline__ uint32_t lane_last(uint32_t x) { return __builtin_amdgcn_readlane(x, 63); }
 
 // a value known to be equal in all lanes, moved to scalar registers
 __device__ __forceinline__ int64_t uniform64(int64_t v) {

@@ -308,9 +308,9 @@ __global__ __launch_bounds__(kDoseThreads) void k_dose_fmt(const char *__restric
                 uint32_t pv[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const uint32_t up = (uint32_t)__shfl_up((int)od[j], 1);
+                    const uint32_t up = lane_prev(od[j]);
                     pv[j] = lane() ? up : carry[j];
-                    carry[j] = (uint32_t)__shfl((int)od[j], kWave - 1);
+                    carry[j] = lane_last(od[j]);
                 }
                 // the block = bytes [16 - osh, 32 - osh) of (pv ++ od): word wq + i, byte wb
                 const uint32_t X[9] = {pv[0], pv[1], pv[2], pv[3], od[0], od[1], od[2], od[3], 0u};

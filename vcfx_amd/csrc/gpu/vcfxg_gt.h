@@ -221,9 +221,9 @@ __device__ bool gt_first(const char *__restrict__ buf, int64_t S, int64_t hi, in
             }
             // sample starts: S, and the byte after every tab, in [S, ae)
             const uint32_t tm = eq_mask16(v[u], kRepTab);
-            const uint32_t last = (uint32_t)__shfl_up((int)(v[u].w >> 24), 1);
+            const uint32_t last = lane_prev(v[u].w >> 24);
             const uint32_t prev = lane() ? last : carry;
-            carry = (uint32_t)__shfl((int)(v[u].w >> 24), kWave - 1);
+            carry = lane_last(v[u].w >> 24);
             uint32_t starts = ((tm << 1) & 0xFFFFu) | (prev == '\t' ? 1u : 0u);
             if (S >= blk && S < blk + 16) starts |= 1u << (S - blk);
             starts &= range_mask16(blk, S, ae);
@@ -431,9 +431,9 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
             // ---- sample starts: the byte after a tab (the byte before the lane's block: the
             // previous lane's, or the previous step's last), S, and only inside [S, ae)
             const uint32_t tab3 = ~((W[3] ^ kRepTab) + K);
-            const uint32_t up = (uint32_t)__shfl_up((int)tab3, 1);
+            const uint32_t up = lane_prev(tab3);
             uint32_t tprev = lane() ? up : carry;
-            carry = (uint32_t)__shfl((int)tab3, kWave - 1);
+            carry = lane_last(tab3);
             uint32_t rm = 0xFFFFu;
             if (edge || found) {
                 rm = blk < hi ? range_mask16(blk, S, ae) : 0u;
@@ -457,9 +457,9 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
                     tp = tb;
                 }
             }
-            const uint32_t sup = (uint32_t)__shfl_up((int)st[3], 1);
+            const uint32_t sup = lane_prev(st[3]);
             const uint32_t sprev = lane() ? sup : scarry;
-            scarry = (uint32_t)__shfl((int)st[3], kWave - 1);
+            scarry = lane_last(st[3]);
             // ---- dword by dword (classes of W[i] and W[i+1] live at a time): each start needs
             // c1 separator and c3 terminator, each allele byte (c0, c2) a digit or '.'; the counts
             // are the allele bytes' digit / nonzero-digit flags

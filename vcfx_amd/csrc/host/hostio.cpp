@@ -16,6 +16,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <memory>
 #include <mutex>
 #include <thread>
 
@@ -155,10 +156,6 @@ void Input::join_populate() const {
 
 Input::~Input() {
     join_populate();
-    if (releasing.joinable()) {  // (the process ends next: whatever is left goes with it)
-        if (g_process_exit_fast) releasing.detach();
-        else releasing.join();
-    }
     if (g_process_exit_fast) return;  // the process ends next: let exit() drop the mappings
     if (ring_ctx)
         for (void *r : ring) vcfxg_host_free(ring_ctx, r);
@@ -530,7 +527,36 @@ ssize_t read_full(int fd, char *dst, size_t want, int *err) {
 // GB/s) while this thread keeps reading the pipe into the region behind it; repeated until the
 // bytes left are few, so the pipe never waits for the copy.  eof: the stream ended meanwhile
 // (everything then is on the device except the final-chunk marker).  false: a copy failed.
-static bool catch_up(vcfxg_ctx *g, int fd, char *base, size_t cap, size_t &got, bool &eof, int *read_errno) {
+// Faults a reserved region in ahead of a reader (on another core), so read() lands on
+// populated pages: 32 MiB steps up to 256 MiB ahead of the reader's position.  Without
+// MADV_POPULATE_WRITE (Linux < 5.14) it just stops.
+struct Prefaulter {
+    std::atomic<size_t> rd;
+    std::atomic<bool> done{false};
+    std::thread th;
+    Prefaulter(char *base, size_t cap, size_t from) : rd(from) {
+        const size_t kStep = (size_t)32 << 20, kAhead = (size_t)256 << 20;
+        th = std::thread([this, base, cap, from, kStep, kAhead] {
+            size_t pop = from & ~(((size_t)2 << 20) - 1);  // (madvise wants page-aligned ranges)
+            while (!done.load(std::memory_order_acquire)) {
+                if (pop < rd.load(std::memory_order_acquire) + kAhead && pop + kStep <= cap) {
+                    if (madvise(base + pop, kStep, kMadvPopulateWrite) != 0) return;
+                    pop += kStep;
+                } else {
+                    std::this_thread::sleep_for(std::chrono::microseconds(50));
+                }
+            }
+        });
+    }
+    void at(size_t got) { rd.store(got, std::memory_order_release); }
+    ~Prefaulter() {
+        done.store(true, std::memory_order_release);
+        th.join();
+    }
+};
+
+static bool catch_up(vcfxg_ctx *g, int fd, char *base, size_t cap, size_t &got, bool &eof, int *read_errno,
+                     Prefaulter *pf) {
     const size_t kRest = (size_t)8 << 20;
     size_t at = 0;
     for (;;) {
@@ -558,6 +584,7 @@ static bool catch_up(vcfxg_ctx *g, int fd, char *base, size_t cap, size_t &got, 
                 break;
             }
             got += (size_t)k;
+            if (pf) pf->at(got);
         }
         t.join();
         if (!ok) return false;
@@ -630,6 +657,7 @@ void Input::read_fd(int fd, bool host_copy) {
         n = host_n = source_n = got;
         return;
     }
+    std::unique_ptr<Prefaulter> head_pf;  // the device-only path's head reader's helper
     bool chrom = false;  // the head holds the complete '#CHROM' line
     size_t scanned = 0;
     auto scan = [&] {
@@ -647,6 +675,9 @@ void Input::read_fd(int fd, bool host_copy) {
         // waited for the open would stall the writer for ~0.2 s); a device-only stream also
         // needs the whole header in it
         const size_t head_cap = std::max<size_t>(2 * kChunk, (size_t)256 << 20);
+        // (the pages ahead of the reader faulted in on another core: the head arrives at the
+        // pipe's rate, not the page-fault rate)
+        if (!host_copy) head_pf.reset(new Prefaulter(base, cap, got));
         for (;;) {
             if (!host_copy) scan();
             const bool enough = got >= 2 * kChunk &&
@@ -661,6 +692,7 @@ void Input::read_fd(int fd, bool host_copy) {
                 return;  // EOF: everything is on the host
             }
             got += (size_t)k;
+            if (head_pf) head_pf->at(got);
         }
     }
     if (got < 2 * kChunk) {
@@ -672,9 +704,9 @@ void Input::read_fd(int fd, bool host_copy) {
         // straight to the device through a pinned staging ring -- no host copy, no page faults
         vcfxg_ctx *g = gpu_quiet();
         bool eof = false;
-        if (g && vcfxg_ingest_begin(g, (size_t)1 << 30) == VCFXG_OK && catch_up(g, fd, base, cap, got, eof, &read_errno)) {
-            // the host keeps the header only (the records are on the device); the head's other
-            // pages are released once the stream is in (below)
+        if (g && vcfxg_ingest_begin(g, (size_t)1 << 30) == VCFXG_OK && catch_up(g, fd, base, cap, got, eof, &read_errno, head_pf.get())) {
+            head_pf.reset();
+            // the host keeps the header only (the records are on the device)
             host_n = scanned;
             stream_ctx = g;
             ring_ctx = g;
@@ -715,12 +747,10 @@ void Input::read_fd(int fd, bool host_copy) {
             }
             n = total;
             streamed = ok ? total : 0;  // a failure is reported when the input is used
-            // the head's record pages: freed by a helper thread while the device computes (1-2 GB
-            // of anonymous memory take ~40 ms/GB to free, at process exit otherwise: r04
-            // teardown probe; freed while the ring streams, they slowed its DMA: r04 e2e probe)
-            const size_t keep = (scanned + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
-            if (got > keep + ((size_t)64 << 20))
-                releasing = std::thread([b = base + keep, len = got - keep] { madvise(b, len, MADV_DONTNEED); });
+            // (the head's record pages stay mapped until exit: freeing them early with
+            // MADV_DONTNEED on a helper thread -- 1-2 GB, ~40 ms/GB -- slowed the ring's DMA when
+            // it overlapped the stream and the device work when it came after, more than the
+            // exit saves: r04 e2e probes)
             if (timing_on) {
                 char b[160];
                 snprintf(b, sizeof b, "stdin streamed to the device (head %zu MB; ring: wait %.1f, read %.1f, ingest %.1f ms)",
@@ -734,22 +764,8 @@ void Input::read_fd(int fd, bool host_copy) {
     }
     n = host_n = got;
 
-    // a helper thread faults the region in ahead of the reader (on another core), so read()
-    // lands on populated pages; without MADV_POPULATE_WRITE (Linux < 5.14) it just stops
-    std::atomic<size_t> rd{got};
-    std::atomic<bool> done{false};
-    const size_t kStep = (size_t)32 << 20, kAhead = (size_t)256 << 20;
-    std::thread pre([&, got0 = got] {  // (got itself keeps changing on this thread: by value)
-        size_t pop = got0;
-        while (!done.load(std::memory_order_acquire)) {
-            if (pop < rd.load(std::memory_order_acquire) + kAhead && pop + kStep <= cap) {
-                if (madvise(base + pop, kStep, kMadvPopulateWrite) != 0) return;
-                pop += kStep;
-            } else {
-                std::this_thread::sleep_for(std::chrono::microseconds(50));
-            }
-        }
-    });
+    head_pf.reset();
+    std::unique_ptr<Prefaulter> pre(new Prefaulter(base, cap, got));
     // device ingest of complete chunks on its own thread, overlapping the pipe read (the
     // context comes from the background open; a failed open here is silent)
     std::mutex mu;
@@ -784,12 +800,12 @@ void Input::read_fd(int fd, bool host_copy) {
         if (k < 0) read_errno = errno;
         if (k <= 0) break;
         got += (size_t)k;
-        rd.store(got, std::memory_order_release);
+        pre->at(got);
         std::lock_guard<std::mutex> lk(mu);
         avail = got;
         cv.notify_one();
     }
-    done.store(true, std::memory_order_release);
+    pre.reset();
     {
         std::lock_guard<std::mutex> lk(mu);
         avail = got;
@@ -797,7 +813,6 @@ void Input::read_fd(int fd, bool host_copy) {
         cv.notify_one();
     }
     ing.join();
-    pre.join();
     n = host_n = got;
 }
 

@@ -82,8 +82,6 @@ struct Input {
     bool decompress(int err_fd);
     // mapped inputs of 64 MiB and more: page-table population running on helper threads
     mutable std::vector<std::thread> populating;
-    // the device-only pipe path: the head's record pages being released (joined by ~Input)
-    std::thread releasing;
     void populate(void *m, size_t len);
     void join_populate() const;
 };
