@@ -17,6 +17,8 @@
 //               reference's fp64 sequence in correctly rounded operations, the decision, the
 //               CHROM compare and the entry length;
 //   k_ph_fmt    the entries at their scanned offsets.
+#include <algorithm>
+
 #include "vcfxg_device.h"
 #include "vcfxg_gt.h"
 #include "vcfxg_kernels.h"
@@ -241,15 +243,176 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
     }
 }
 
-__device__ __forceinline__ uint32_t ph_digits(uint64_t v) {
+__device__ __forceinline__ uint32_t ph_digits(uint64_t v) {  // (compares, no 64-bit division)
     uint32_t d = 1;
-    while (v >= 10) {
-        v /= 10;
-        d++;
-    }
+    for (uint64_t p = 10; d < 20 && v >= p; p *= 10) d++;
     return d;
 }
 __device__ __forceinline__ uint32_t ph_int_len(int64_t v) { return v < 0 ? 1u + ph_digits((uint64_t)-v) : ph_digits((uint64_t)v); }
+
+// 16 codes per lane of two rows (x, y; a negative code is missing) into the six sums' lane parts:
+// four codes per dword, valid where both are >= 0 (bit 7 clear) and the sample is below n; the
+// sums by byte dot products of the codes masked to the valid bytes (v_dot4_u32_u8, v_sad_u8),
+// not a loop over the 16 codes.  Fields: (valid, Sx) | (Sy, Sxy) | (Sx2, Sy2), 32 bits each.
+__device__ __forceinline__ void ph_acc16(const uint4 &va, const uint4 &vb, uint32_t k0, uint32_t n, uint64_t &p0,
+                                         uint64_t &p1, uint64_t &p2) {
+    const uint32_t wa[4] = {va.x, va.y, va.z, va.w}, wb[4] = {vb.x, vb.y, vb.z, vb.w};
+    uint32_t vn = 0, sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int rem = (int)n - (int)(k0 + 4 * i);
+        const uint32_t lim = rem >= 4 ? 0xFFFFFFFFu : rem <= 0 ? 0u : (1u << (8 * rem)) - 1u;
+        const uint32_t m = ~(wa[i] | wb[i]) & 0x80808080u & lim;
+        const uint32_t mb = (m - (m >> 7)) | m;  // 0xFF per valid byte
+        const uint32_t xs = wa[i] & mb, ys = wb[i] & mb;
+        vn += __popc(m);
+        sx = __builtin_amdgcn_sad_u8(xs, 0u, sx);
+        sy = __builtin_amdgcn_sad_u8(ys, 0u, sy);
+        sxy = __builtin_amdgcn_udot4(xs, ys, sxy, false);
+        sx2 = __builtin_amdgcn_udot4(xs, xs, sx2, false);
+        sy2 = __builtin_amdgcn_udot4(ys, ys, sy2, false);
+    }
+    p0 += (uint64_t)vn | (uint64_t)sx << 32;
+    p1 += (uint64_t)sy | (uint64_t)sxy << 32;
+    p2 += (uint64_t)sx2 | (uint64_t)sy2 << 32;
+}
+
+// calculateLDFast's fp64 tail (:440-470) on the pair's six sums, correctly rounded, and the block
+// rule (r^2 >= thr, and r > 0 on CHROM "1"); flags as k_ph_pairs writes them
+__device__ __forceinline__ uint8_t ph_pair_flags(const PhLine &, const PhLine &, bool one, bool same, int64_t N,
+                                                 int64_t SX, int64_t SY, int64_t SXY, int64_t SX2, int64_t SY2,
+                                                 double thr, double &r2v) {
+    double r = 0.0;
+    r2v = 0.0;
+    if (N > 0) {
+        const double dn = (double)N;
+        const double mx = __ddiv_rn((double)SX, dn), my = __ddiv_rn((double)SY, dn);
+        const double cov = __dsub_rn(__ddiv_rn((double)SXY, dn), __dmul_rn(mx, my));
+        const double vx = __dsub_rn(__ddiv_rn((double)SX2, dn), __dmul_rn(mx, mx));
+        const double vy = __dsub_rn(__ddiv_rn((double)SY2, dn), __dmul_rn(my, my));
+        if (vx > 0.0 && vy > 0.0) {
+            r = __ddiv_rn(cov, __dmul_rn(__dsqrt_rn(vx), __dsqrt_rn(vy)));
+            r2v = __dmul_rn(r, r);
+        }
+    }
+    const bool pass = one ? (r2v >= thr && r > 0.0) : (r2v >= thr);
+    return (uint8_t)((pass ? 1u : 0u) | (same ? 2u : 0u));
+}
+
+// k_ph_pairs for rows of at most kU KiB: a wave takes kPhRun consecutive variants, each row
+// loaded once into registers (the next two rows' loads in flight while a pair reduces) and kept
+// as the next pair's first row -- every code read once, not twice
+constexpr uint64_t kPhRun = 32;
+template <int kU>
+__global__ __launch_bounds__(kPhThreads) void k_ph_pairs_run(const char *__restrict__ buf,
+                                                             const uint64_t *__restrict__ vline,
+                                                             const uint64_t *n_var_p, const PhLine *__restrict__ info,
+                                                             const int8_t *__restrict__ G, uint32_t kpad, double thr,
+                                                             uint8_t *__restrict__ flags, uint64_t *__restrict__ len,
+                                                             double *__restrict__ r2_out) {
+    const uint64_t nv = *n_var_p;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    auto load_row = [&](uint64_t line, uint4(&r)[kU]) {
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            uint32_t k0 = 16u * (lane() + kWave * u);
+            k0 = k0 < kpad ? k0 : kpad - 16u;  // (bytes past the row are masked by n)
+            r[u] = *reinterpret_cast<const uint4 *>(G + line * (uint64_t)kpad + k0);
+        }
+    };
+    // a PhLine field of variant lane k of the run (preloaded by lane k), wave-uniform
+    // (readlane returns int: each half goes through uint32_t, or the low half would sign-extend
+    // into the high one -- offsets past 2 GiB)
+    auto rd64 = [](uint64_t x, int k) {
+        return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), k) << 32) |
+               (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)x, k);
+    };
+    for (uint64_t v0 = wid * kPhRun; v0 < nv; v0 += nw * kPhRun) {
+        const uint64_t v1 = std::min<uint64_t>(nv, v0 + kPhRun);
+        // lane k < run length: variant v0 - 1 + k's line and PhLine (one load each, all lanes at
+        // once, instead of a dependent chain per variant)
+        const int64_t vk = (int64_t)v0 - 1 + lane();
+        uint64_t mline = 0, mchrom = 0;
+        uint32_t mclen = 0, mns = 0;
+        int32_t mpos = 0;
+        if (vk >= 0 && (uint64_t)vk < v1) {
+            mline = vline[vk];
+            const PhLine q = info[mline];
+            mchrom = q.chrom, mclen = q.clen, mns = q.ns, mpos = q.pos;
+        }
+        auto line_of = [&](uint64_t v) { return rd64(mline, (int)(v + 1 - v0)); };
+        auto info_of = [&](uint64_t v) {
+            const int k = (int)(v + 1 - v0);
+            PhLine q{};
+            q.chrom = rd64(mchrom, k);
+            q.clen = __builtin_amdgcn_readlane(mclen, k);
+            q.ns = __builtin_amdgcn_readlane(mns, k);
+            q.pos = (int32_t)__builtin_amdgcn_readlane((uint32_t)mpos, k);
+            return q;
+        };
+        // a CHROM's bytes, one per lane (CHROMs of up to 64 bytes; longer ones compared in a loop)
+        auto chrom_bytes = [&](const PhLine &q) {
+            return (uint32_t)lane() < q.clen ? (uint32_t)(uint8_t)buf[q.chrom + lane()] : 0u;
+        };
+        uint4 ra[kU], rb[kU];
+        PhLine a{};
+        uint32_t ca = 0;
+        if (v0 > 0) {
+            a = info_of(v0 - 1);
+            ca = chrom_bytes(a);
+            load_row(line_of(v0 - 1), ra);
+        }
+        uint64_t lb = line_of(v0);
+        load_row(lb, rb);
+        // the next two rows in flight while a pair reduces (one ahead left every iteration waiting
+        // on its row)
+        uint4 rn[kU], rm[kU];
+        if (v0 + 1 < v1) load_row(line_of(v0 + 1), rn);
+        // lane j keeps variant v0 + j's six sums and CHROM flags; the fp64 tails, the entry
+        // lengths and the stores then run once for the whole run, a variant per lane
+        uint64_t s0 = 0, s1 = 0, s2 = 0;
+        uint32_t sf = 0;  // bit 0: a pair, bit 1: CHROM "1", bit 2: same CHROM
+        for (uint64_t v = v0; v < v1; v++) {
+            const PhLine b = info_of(v);
+            const uint32_t cb = chrom_bytes(b);
+            if (v + 2 < v1) load_row(line_of(v + 2), rm);
+            if (v > 0) {
+                const uint32_t n = min(a.ns, b.ns);
+                uint64_t p0 = 0, p1 = 0, p2 = 0;
+#pragma unroll
+                for (int u = 0; u < kU; u++) ph_acc16(ra[u], rb[u], 16u * (lane() + kWave * u), n, p0, p1, p2);
+                const uint64_t q0 = (uint64_t)wave_sum((int64_t)p0), q1 = (uint64_t)wave_sum((int64_t)p1),
+                               q2 = (uint64_t)wave_sum((int64_t)p2);
+                const bool one = b.clen == 1 && __builtin_amdgcn_readfirstlane(cb) == '1';
+                bool same = a.clen == b.clen && !__any(ca != cb);
+                for (uint32_t k = kWave; same && k < a.clen; k++) same = buf[a.chrom + k] == buf[b.chrom + k];
+                if ((uint64_t)lane() == v - v0) {
+                    s0 = q0, s1 = q1, s2 = q2;
+                    sf = 1u | (one ? 2u : 0u) | (same ? 4u : 0u);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++) ra[u] = rb[u], rb[u] = rn[u], rn[u] = rm[u];
+            a = b;
+            ca = cb;
+        }
+        const uint64_t v = v0 + lane();
+        // variant v0 + j's CHROM length and POS: lane j + 1's preloaded ones
+        const uint32_t vclen = (uint32_t)__shfl_down((int)mclen, 1);
+        const int32_t vpos = __shfl_down(mpos, 1);
+        if (v < v1) {
+            uint8_t f = 0;
+            double r2v = 0.0;
+            if (sf & 1u)
+                f = ph_pair_flags(a, a, (sf & 2u) != 0, (sf & 4u) != 0, (uint32_t)s0, s0 >> 32, (uint32_t)s1,
+                                  s1 >> 32, (uint32_t)s2, s2 >> 32, thr, r2v);
+            flags[v] = f;
+            r2_out[v] = r2v;
+            len[v] = ph_digits(v) + 2u + vclen + 1u + ph_int_len(vpos) + 1u;
+        }
+    }
+}
 
 // per variant v: vline[v] = its line.  flags: bit 0 the pair (v - 1, v) passes the block rule,
 // bit 1 the two share CHROM.  len: bytes of the entry "v:(chrom:pos)".
@@ -287,26 +450,7 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_pairs(const char *__restrict_
                 }
                 uint64_t p0 = 0, p1 = 0, p2 = 0;
 #pragma unroll
-                for (int u = 0; u < kPhUnroll; u++) {
-                    const uint32_t k0 = b0 + 16u * (lane() + kWave * u);
-                    const uint32_t wa[4] = {va[u].x, va[u].y, va[u].z, va[u].w}, wb[4] = {vb[u].x, vb[u].y, vb[u].z, vb[u].w};
-                    uint32_t vn = 0, sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;
-#pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        const int x = (int)(int8_t)(wa[j >> 2] >> (8 * (j & 3)));
-                        const int y = (int)(int8_t)(wb[j >> 2] >> (8 * (j & 3)));
-                        if (k0 + j >= n || x < 0 || y < 0) continue;
-                        vn++;
-                        sx += x;
-                        sy += y;
-                        sxy += x * y;
-                        sx2 += x * x;
-                        sy2 += y * y;
-                    }
-                    p0 += (uint64_t)vn | (uint64_t)sx << 32;
-                    p1 += (uint64_t)sy | (uint64_t)sxy << 32;
-                    p2 += (uint64_t)sx2 | (uint64_t)sy2 << 32;
-                }
+                for (int u = 0; u < kPhUnroll; u++) ph_acc16(va[u], vb[u], b0 + 16u * (lane() + kWave * u), n, p0, p1, p2);
                 const uint64_t q0 = (uint64_t)wave_sum((int64_t)p0), q1 = (uint64_t)wave_sum((int64_t)p1),
                                q2 = (uint64_t)wave_sum((int64_t)p2);
                 N += (uint32_t)q0;
@@ -316,23 +460,10 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_pairs(const char *__restrict_
                 SX2 += (uint32_t)q2;
                 SY2 += q2 >> 32;
             }
-            double r = 0.0;
-            if (N > 0) {
-                const double dn = (double)N;
-                const double mx = __ddiv_rn((double)SX, dn), my = __ddiv_rn((double)SY, dn);
-                const double cov = __dsub_rn(__ddiv_rn((double)SXY, dn), __dmul_rn(mx, my));
-                const double vx = __dsub_rn(__ddiv_rn((double)SX2, dn), __dmul_rn(mx, mx));
-                const double vy = __dsub_rn(__ddiv_rn((double)SY2, dn), __dmul_rn(my, my));
-                if (vx > 0.0 && vy > 0.0) {
-                    r = __ddiv_rn(cov, __dmul_rn(__dsqrt_rn(vx), __dsqrt_rn(vy)));
-                    r2v = __dmul_rn(r, r);
-                }
-            }
             const bool one = b.clen == 1 && byte_at(buf, (int64_t)b.chrom) == '1';
-            const bool pass = one ? (r2v >= thr && r > 0.0) : (r2v >= thr);
             bool same = a.clen == b.clen;
             for (uint32_t k = 0; same && k < a.clen; k++) same = buf[a.chrom + k] == buf[b.chrom + k];
-            f = (uint8_t)((pass ? 1u : 0u) | (same ? 2u : 0u));
+            f = ph_pair_flags(a, b, one, same, N, SX, SY, SXY, SX2, SY2, thr, r2v);
         }
         if (lane() == 0) {
             flags[v] = f;
@@ -417,8 +548,26 @@ hipError_t launch_ph_pairs(const char *buf, const uint64_t *vline, const uint64_
     if (!n_var_host) return hipSuccess;
     int64_t g = ((int64_t)n_var_host + kPhWaves - 1) / kPhWaves;
     if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(k_ph_pairs, dim3((unsigned)g), dim3(kPhThreads), 0, s, buf, vline, n_var_dev,
-                       static_cast<const PhLine *>(info), G, kpad, thr, flags, len, r2);
+    const PhLine *in = static_cast<const PhLine *>(info);
+    // rows of up to 4 KiB: consecutive variants per wave, each row read once
+    const int ku = (int)((kpad + 1023) / 1024);
+    const unsigned gr = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(4096, (n_var_host + kPhWaves * kPhRun - 1) /
+                                                                                      (kPhWaves * kPhRun)));
+    if (ku == 1)
+        hipLaunchKernelGGL(k_ph_pairs_run<1>, dim3(gr), dim3(kPhThreads), 0, s, buf, vline, n_var_dev, in, G, kpad, thr,
+                           flags, len, r2);
+    else if (ku == 2)
+        hipLaunchKernelGGL(k_ph_pairs_run<2>, dim3(gr), dim3(kPhThreads), 0, s, buf, vline, n_var_dev, in, G, kpad, thr,
+                           flags, len, r2);
+    else if (ku == 3)
+        hipLaunchKernelGGL(k_ph_pairs_run<3>, dim3(gr), dim3(kPhThreads), 0, s, buf, vline, n_var_dev, in, G, kpad, thr,
+                           flags, len, r2);
+    else if (ku == 4)
+        hipLaunchKernelGGL(k_ph_pairs_run<4>, dim3(gr), dim3(kPhThreads), 0, s, buf, vline, n_var_dev, in, G, kpad, thr,
+                           flags, len, r2);
+    else
+        hipLaunchKernelGGL(k_ph_pairs, dim3((unsigned)g), dim3(kPhThreads), 0, s, buf, vline, n_var_dev, in, G, kpad,
+                           thr, flags, len, r2);
     return hipGetLastError();
 }
 
