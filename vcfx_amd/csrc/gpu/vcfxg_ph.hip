@@ -135,6 +135,7 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
     for (uint64_t li = wid; li < n_lines; li += nw) {
         if (!kFast && status[li] != kPhPend) continue;  // (wave-uniform)
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
+        const LineMeta wm = wmeta ? wmeta[li] : LineMeta{};
         uint8_t st = kPhSkip;
         bool swept_fixed = false;
         PhLine m{};
@@ -144,30 +145,61 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
             if (ae == ls) st = mode == 0 ? kPhSkip : kPhFew;  // (stdin: a lone '\r' is a 1-field line)
             else if (byte_at(buf, ls) == '#') st = kPhHeader;
             else {
-                int64_t t[9];
-                const int nt = head_tabs(buf, ls, ae, 9, t, lds);
+                int64_t t0 = 0, t8 = 0;
+                int nt = 0, gi = -1;
+                bool ok = true;  // POS: every byte a digit (an empty POS is 0), int accumulation
+                uint32_t pos = 0;
+                bool head = false;
+                if (kFast && wmeta && wm.kind == kMetaGt && (int64_t)wm.S > ls) {
+                    // a record of the head walk: its 9 tabs were found (S = the 9th + 1) and its
+                    // FORMAT starts "GT" (index 0), so CHROM and POS come from one 64-byte load --
+                    // no head sweep, no byte-by-byte POS loop of dependent loads
+                    const int64_t q = ls + lane();
+                    const uint32_t c = q < ae ? byte_at(buf, q) : 0u;
+                    const uint64_t tb = __ballot(c == '\t');
+                    if (__popcll(tb) >= 2) {
+                        t0 = ls + __builtin_ctzll(tb);
+                        const int64_t t1 = ls + __builtin_ctzll(tb & (tb - 1));
+                        t8 = (int64_t)wm.S - 1;
+                        nt = 9;
+                        gi = 0;
+                        head = true;
+                        // POS = sum of digit * 10^(place), mod 2^32 like the serial accumulation
+                        const bool in = q > t0 && q < t1;
+                        ok = !__any(in && c - '0' >= 10u);
+                        uint32_t pw = 1;
+                        for (int64_t k = t1 - 1 - q; in && k > 0; k--) pw *= 10u;
+                        pos = wave_sum(in && ok ? (c - '0') * pw : 0u);
+                        if (!ok) gi = -1;
+                    }
+                }
+                if (!head) {
+                    int64_t t[9];
+                    nt = head_tabs(buf, ls, ae, 9, t, lds);
+                    if (nt >= 9) {
+                        t0 = t[0];
+                        t8 = t[8];
+                        for (int64_t q = t[0] + 1; q < t[1]; q++) {
+                            const uint32_t c = byte_at(buf, q);
+                            if (c - '0' >= 10u) {
+                                ok = false;
+                                break;
+                            }
+                            pos = pos * 10u + (c - '0');
+                        }
+                        gi = ok ? gt_index(buf, t[7] + 1, t[8]) : -1;
+                    }
+                }
                 if (nt < 9) st = kPhFew;
                 else {
-                    // POS: every byte a digit (an empty POS is 0), int accumulation
-                    bool ok = true;
-                    uint32_t pos = 0;
-                    for (int64_t q = t[0] + 1; q < t[1]; q++) {
-                        const uint32_t c = byte_at(buf, q);
-                        if (c - '0' >= 10u) {
-                            ok = false;
-                            break;
-                        }
-                        pos = pos * 10u + (c - '0');
-                    }
-                    const int gi = ok ? gt_index(buf, t[7] + 1, t[8]) : -1;
                     if (!ok) st = kPhPos;
                     else if (gi < 0) st = kPhNoGt;
                     else {
                         st = kPhVar;
                         m.chrom = (uint64_t)ls;
-                        m.clen = (uint32_t)(t[0] - ls);
+                        m.clen = (uint32_t)(t0 - ls);
                         m.pos = (int32_t)pos;
-                        const int64_t S = t[8] + 1;
+                        const int64_t S = t8 + 1;
                         int8_t *row = G + li * (uint64_t)kpad;
                         const int64_t L = ae - S;
                         const bool fixed = gi == 0 && L >= 3 && ((L + 1) & 3) == 0 && (uint64_t)((L + 1) / 4) <= kpad;
@@ -232,8 +264,8 @@ __global__ __launch_bounds__(kPhThreads) void k_ph_lines(const char *__restrict_
         }
         // a record the head walk took on its predicted end: its bounds hold only if the fixed-stride
         // sweep validated [S, ae) (no '\n' inside); any other outcome redoes the call on the index
-        if (wmeta && st != kPhPend && !(st == kPhVar && swept_fixed) && (wmeta[li].pad & kWalkUnswept) &&
-            wmeta[li].kind == kMetaGt && lane() == 0)
+        if (wmeta && st != kPhPend && !(st == kPhVar && swept_fixed) && (wm.pad & kWalkUnswept) &&
+            wm.kind == kMetaGt && lane() == 0)
             atomicOr(bad, 1u);
         if (lane() == 0) {
             status[li] = st;
