@@ -1,7 +1,7 @@
 #!/bin/bash
-# r04 job: PH pair sums by byte dot products
-bash gpu_job.sh test tests/test_gpu_ph.py || exit $?
-bash gpu_job.sh scale -k "ph" || exit $?
+# r04 job: AC rows with counts hoisted per 32 tiles
+bash gpu_job.sh test tests/test_gpu_ac.py || exit $?
+bash gpu_job.sh scale -k "ac_" || exit $?
 for i in 1 2; do
-    bash gpu_job.sh run ph_$i 300 python -u bench.py --workload ph --no-cpu-baseline --no-e2e --steps 20 || exit $?
+bash gpu_job.sh run ac_$i 300 python -u bench.py --workload ac --no-cpu-baseline --no-e2e --steps 5 || exit $?
 done

@@ -28,6 +28,11 @@
 
 namespace vcfxg {
 
+// VCFXG_AC_EXPT (diagnostic builds only, output invalid): bit 0 skips the text rows' composition
+// in LDS, bit 1 their copy to the output
+#ifndef VCFXG_AC_EXPT
+#define VCFXG_AC_EXPT 0
+#endif
 constexpr int kAcThreads = 512;  // 8 waves share one LDS copy of the selection (r02: 256 -> 512)
 constexpr int kAcWaves = kAcThreads / kWave;
 constexpr int kAcTile = 3072;  // LDS bytes per wave for one tile of 64 text rows (longer: straight out)
@@ -199,19 +204,25 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_len(const char *__restrict__ 
                     m.kind = kAcFast;
                     const uint32_t ns = (uint32_t)((le - S + 1) / 4);
                     m.ns = ns;
-                    uint32_t cnt = 0;
-                    for (uint32_t i = lane(); i < A.m; i += kWave) {
-                        const uint32_t e = A.eff[i];
-                        const bool valid = !A.seq || e < ns;
-                        cnt += valid;
-                        if (A.kind == 1 && valid) {
-                            int r, a;
-                            ac_slot_fast(buf, S, ns, e, r, a);
-                            sr += (uint64_t)r;
-                            sa += (uint64_t)a;
+                    if (A.kind != 1 && (!A.seq || A.ident)) {
+                        // no per-slot work: every slot is a row, or (seq, slot i reads sample i)
+                        // the slots below the record's sample count
+                        rows = A.seq ? min(A.m, ns) : A.m;
+                    } else {
+                        uint32_t cnt = 0;
+                        for (uint32_t i = lane(); i < A.m; i += kWave) {
+                            const uint32_t e = A.eff[i];
+                            const bool valid = !A.seq || e < ns;
+                            cnt += valid;
+                            if (A.kind == 1 && valid) {
+                                int r, a;
+                                ac_slot_fast(buf, S, ns, e, r, a);
+                                sr += (uint64_t)r;
+                                sa += (uint64_t)a;
+                            }
                         }
+                        rows = wave_sum(cnt);
                     }
-                    rows = wave_sum(cnt);
                     if (A.kind == 0) text = (uint64_t)rows * (m.P + 5u) + A.noff[rows];
                 } else {
                     m.kind = kAcGeneral;
@@ -387,18 +398,40 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const uint64_t rl = P + 5u;
-        // the first tile's counts; each iteration loads the next tile's before writing its own
-        int rn = 0, an = 0;
-        if ((uint32_t)lane() < m.rows) ac_slot_fast(buf, S, m.ns, EFF(lane()), rn, an);
+        // the counts of 32 tiles at a time (a nibble r | a << 2 per tile in pk0 / pk1), loaded
+        // before any of those tiles' rows is stored: a count loaded between two tiles' stores made
+        // every tile wait for the previous tile's stores (loads and stores share vmcnt, and the
+        // varying store count leaves the compiler vmcnt(0))
+        uint64_t pk0 = 0, pk1 = 0;
+        bool lo_valid = false;  // tile[0, ga & 15) holds the previous tile's last partial block
         for (uint32_t i0 = 0; i0 < m.rows; i0 += kWave) {
             const uint32_t i1 = min(m.rows, i0 + (uint32_t)kWave);
             const uint64_t g0 = (uint64_t)i0 * rl + NOFF(i0);                // tile start in the line's text
             const uint64_t B = (uint64_t)(i1 - i0) * rl + NOFF(i1) - NOFF(i0);  // tile bytes
             const uint32_t i = i0 + lane();
-            const int r = rn, a = an;
-            if (i + kWave < m.rows) ac_slot_fast(buf, S, m.ns, EFF(i + kWave), rn, an);
+            const uint32_t t = i0 / kWave;
+            if ((t & 31) == 0) {
+                pk0 = pk1 = 0;
+#pragma unroll 4
+                for (uint32_t kk = 0; kk < 32; kk++) {
+                    const uint32_t ii = i + kk * kWave;
+                    uint32_t nib = 0;
+                    if (ii < m.rows) {
+                        int rr, aa;
+                        ac_slot_fast(buf, S, m.ns, EFF(ii), rr, aa);
+                        nib = (uint32_t)rr | ((uint32_t)aa << 2);
+                    }
+                    if (kk < 16) pk0 |= (uint64_t)nib << (4 * kk);
+                    else pk1 |= (uint64_t)nib << (4 * (kk - 16));
+                }
+            }
+            const uint32_t nib = (uint32_t)(((t & 16) ? pk1 : pk0) >> (4 * (t & 15))) & 15u;
+            const int r = (int)(nib & 3u), a = (int)(nib >> 2);
             const uint64_t ga = (uint64_t)(o - out) + g0;  // absolute text offset of the tile
-            if (B + 16 > (uint64_t)kAcTile) {             // long names: straight to global memory
+            const uint64_t lo = lo_valid ? (ga & ~(uint64_t)15) : ga;  // first byte this tile stores
+            if (B + 32 > (uint64_t)kAcTile) {             // long names: straight to global memory
+                if (lo_valid && (uint32_t)lane() < (uint32_t)(ga - lo)) out[lo + lane()] = tile[lane()];  // the carry
+                lo_valid = false;
                 if (i < i1) {
                     char *q = o + (uint64_t)i * rl + NOFF(i);
                     for (uint32_t k = 0; k < P; k++) q[k] = pre[k];
@@ -413,7 +446,7 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
                 continue;
             }
             const uint32_t sh = (uint32_t)(ga & 15);  // LDS position = text position mod 16
-            if (i < i1) {
+            if (i < i1 && !(VCFXG_AC_EXPT & 1)) {
                 char *q = tile + sh + ((uint64_t)i * rl + NOFF(i) - g0);
                 for (uint32_t k = 0; k < P; k++) q[k] = pre[k];
                 q += P;
@@ -427,17 +460,32 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // copy out: aligned 16 B blocks of [ga, ga + B)
+            // copy out: the aligned 16 B blocks of [lo, ga + B); a tile's last partial block is
+            // not stored but carried to the front of the next tile's LDS image (text position mod
+            // 16 again), so only the record's first and last blocks take byte stores (a block
+            // holding another record's bytes is never written whole)
             const uint64_t a0 = ga & ~(uint64_t)15, aend = ga + B;
-            for (uint64_t blk = a0 + 16ull * lane(); blk < aend; blk += 16ull * kWave) {
+            const bool last = i1 == m.rows;
+            const uint64_t cend = last ? aend : (aend & ~(uint64_t)15);
+            for (uint64_t blk = a0 + 16ull * lane(); blk < cend && !(VCFXG_AC_EXPT & 2); blk += 16ull * kWave) {
                 const char *src = tile + (blk - a0);
-                if (blk >= ga && blk + 16 <= aend)
+                if (blk >= lo && blk + 16 <= cend)
                     *reinterpret_cast<uint4 *>(out + blk) = *reinterpret_cast<const uint4 *>(src);
                 else
                     for (int k = 0; k < 16; k++)
-                        if (blk + k >= ga && blk + k < aend) out[blk + k] = src[k];
+                        if (blk + k >= lo && blk + k < cend) out[blk + k] = src[k];
             }
             __builtin_amdgcn_wave_barrier();  // the tile is rewritten by the next iteration
+            lo_valid = !last;
+            if (!last) {  // the carry: bytes [cend, aend) to the front
+                const uint32_t nc = (uint32_t)(aend - cend);
+                const uint32_t cv = (uint32_t)lane() < nc ? (uint32_t)(uint8_t)tile[(cend - a0) + lane()] : 0u;
+                __builtin_amdgcn_wave_barrier();
+                if ((uint32_t)lane() < nc) tile[lane()] = (char)cv;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
         }
     }
 }
@@ -462,11 +510,11 @@ static AcArgs ac_args(const uint32_t *eff, const uint64_t *noff, const char *nam
 
 hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
-                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint8_t *status,
+                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, int ident, uint8_t *status,
                          uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s) {
     if (l1 <= l0) return hipSuccess;
     hipLaunchKernelGGL(k_ac_len, dim3(blocks), dim3(kAcThreads), 0, s, buf, data_start, line_end, l0, l1,
-                       ac_args(eff, noff, names, scratch, m, scap, seq, kind), status, len,
+                       ac_args(eff, noff, names, scratch, m, scap, seq, kind, 0, ident), status, len,
                        static_cast<AcMeta *>(meta), counters);
     return hipGetLastError();
 }

@@ -1802,7 +1802,7 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
     HIPCHK(c, vcfxg::launch_ac_len(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, (unsigned)blocks,
                                    P<uint32_t>(c->ac_eff), P<uint64_t>(c->ac_noff), P<char>(c->ac_names),
                                    P<uint32_t>(c->ac_scratch), (uint32_t)m, (uint32_t)scap, p->seq, p->kind,
-                                   P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->af_meta.p,
+                                   ident ? 1 : 0, P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->af_meta.p,
                                    P<unsigned long long>(c->counters), c->stream));
     prof_end(c, "ac_len");
     r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)n + 1);

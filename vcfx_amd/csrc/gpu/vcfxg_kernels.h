@@ -189,7 +189,7 @@ size_t ac_meta_bytes();
 int ac_threads();
 hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
-                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint8_t *status,
+                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, int ident, uint8_t *status,
                          uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s);
 hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,

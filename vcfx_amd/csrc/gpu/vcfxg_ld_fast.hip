@@ -498,9 +498,15 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                 sxx = (int)(pi >> 32) - (int)((cv >> 5) & 63);
                 sy = (int)((pj >> 8) & 0xFFFFFF) - (int)(rv & 31);
                 syy = (int)(pj >> 32) - (int)((rv >> 5) & 63);
-                uint32_t v = accp[x][y][0];
-#pragma unroll
-                for (int q = 1; q < 8; q++) v = (k >> 1) == q ? accp[x][y][q] : v;
+                // (a select tree on the bits of k >> 1: a select chain on its value was turned
+                // into an indexed load, the packed accumulators moved to scratch -- 256 B per lane
+                // per block written to memory)
+                const int q = k >> 1;
+                const bool q1 = (q & 1) != 0, q2 = (q & 2) != 0, q4 = (q & 4) != 0;
+                const uint32_t a0 = q1 ? accp[x][y][1] : accp[x][y][0], a1 = q1 ? accp[x][y][3] : accp[x][y][2];
+                const uint32_t a2 = q1 ? accp[x][y][5] : accp[x][y][4], a3 = q1 ? accp[x][y][7] : accp[x][y][6];
+                const uint32_t b0 = q2 ? a1 : a0, b1 = q2 ? a3 : a2;
+                const uint32_t v = q4 ? b1 : b0;
                 sxy = (int)((v >> (16 * (k & 1))) & 0xFFFFu);
             };
 #pragma unroll
