@@ -18,6 +18,16 @@ for i in 1 2 3; do
     [ -x $DRAIN ] && { echo -n "cat_pipe_drain "; time (cat $F | $DRAIN); }
 done
 MODE=${1:-all}
+if [ $MODE = warm ]; then  # warm-context file ring shapes: slot bytes, slots, reader threads
+    for cfg in "16777216 12 8" "16777216 20 8" "16777216 24 12" "8388608 32 16" "16777216 32 16" "33554432 16 8"; do
+        set -- $cfg
+        echo "ring slot=$1 slots=$2 threads=$3"
+        VCFX_FILE_SLOT=$1 VCFX_FILE_SLOTS=$2 VCFX_FILE_THREADS=$3 VCFX_TIMING=1 timeout -k 5 120 python tools/e2e_warm.py $F 2>&1 | \
+            grep -E "^--- run|start|streamed|released" | tail -6 || exit 1
+    done
+    rm -f $F
+    exit 0
+fi
 for i in 1 2 3; do
     [ $MODE = pipe ] && break
     echo -n "fresh_file "; time (VCFX_TIMING=$((i == 1)) timeout -k 5 60 $AF -q -i $F > /dev/null) || exit 1

@@ -308,7 +308,8 @@ bool Input::open_file_device(const char *path) {
     const size_t S = ring_.size(), inflight = std::max<size_t>(1, S / 2);
     const size_t nchunks = (total - hn + kSlot - 1) / kSlot;
     const unsigned hw = std::thread::hardware_concurrency();
-    const size_t T = std::max<size_t>(1, std::min<size_t>({S - inflight, (size_t)8, hw ? (size_t)hw : 1}));
+    const size_t T = std::max<size_t>(1, std::min<size_t>({S - inflight, env_bytes("VCFX_FILE_THREADS", 8),
+                                                           hw ? (size_t)hw : 1}));
     std::mutex mu;
     std::condition_variable cv;
     std::vector<long long> filled(S, -1), freed(S, -1);  // chunk index held / released per slot
