@@ -19,6 +19,10 @@ for i in 1 2 3; do
 done
 MODE=${1:-all}
 if [ $MODE = warm ]; then  # warm-context file ring shapes: slot bytes, slots, reader threads
+    for i in 1 2; do
+        timeout -k 5 120 python tools/e2e_warm.py $F 2>/dev/null || exit 1
+        timeout -k 5 120 python tools/e2e_warm.py --torch $F 2>/dev/null || exit 1
+    done
     for cfg in "16777216 12 8" "16777216 20 8" "16777216 24 12" "8388608 32 16" "16777216 32 16" "33554432 16 8"; do
         set -- $cfg
         echo "ring slot=$1 slots=$2 threads=$3"

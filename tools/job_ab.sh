@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04 job: AC rows with counts hoisted per 32 tiles
+# r04 job: AC rows' prefix by aligned dword LDS writes
 bash gpu_job.sh test tests/test_gpu_ac.py || exit $?
 bash gpu_job.sh scale -k "ac_" || exit $?
 for i in 1 2; do
