@@ -33,7 +33,8 @@
 
 // VCFXG_LD_EXPT (diagnostic builds only, results invalid): bit 0 skips the epilogue, bit 3
 // stages k-slice 0 every step, bit 4 reads rows 0..255 for every block; sparse epilogue: bit 5
-// skips the missing-entry gathers, bit 6 the per-pair prefilter
+// skips the missing-entry gathers, bit 6 the per-pair prefilter, bit 7 the tables and exact
+// pairs after the prefilter
 #ifndef VCFXG_LD_EXPT
 #define VCFXG_LD_EXPT 0
 #endif
@@ -134,50 +135,57 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
         nc[y] = 0;
     }
     auto body = [&](auto check) {
+        // x outer, then the row groups g: a group's terms (4 rows) are read from LDS once for
+        // the four column tiles (r04: inside the (y, x) loop they were read four times, 64
+        // ds_read_b128 per lane per block); the rare exact path re-reads them
+        auto test2 = [&](int x, int y, int k, const float *rs, const float *uu, float wjj, float vjj, float a0,
+                         float a1, bool &c0, bool &c1) {
+            const f2 c = __builtin_elementwise_fma(f2{rs[0], rs[1]}, f2{wjj, wjj}, f2{a0, a1});
+            const f2 tt = __builtin_elementwise_fma(f2{uu[0], uu[1]}, f2{vjj, vjj}, f2{negE, negE});
+            c0 = fabsf(c.x) >= tt.x;
+            c1 = fabsf(c.y) >= tt.y;
+            if (decltype(check)::value) {
+                const int row = 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
+                c0 = c0 & ((unsigned)(row - lo[y]) < (unsigned)span[y]);
+                c1 = c1 & ((unsigned)(row + 1 - lo[y]) < (unsigned)span[y]);
+            }
+        };
 #pragma unroll
-        for (int y = 0; y < 4; y++) {
+        for (int x = 0; x < 2; x++) {
+            bool any[4] = {false, false, false, false};
 #pragma unroll
-            for (int x = 0; x < 2; x++) {
-                float rs[16], uu[16];
+            for (int g = 0; g < 4; g++) {
+                const int lr = wi * 64 + 32 * x + 8 * g + 4 * h;
+                const float4 a4 = *reinterpret_cast<const float4 *>(rsf + lr);
+                const float4 u4 = *reinterpret_cast<const float4 *>(ru + lr);
+                const float rsg[4] = {a4.x, a4.y, a4.z, a4.w}, uug[4] = {u4.x, u4.y, u4.z, u4.w};
 #pragma unroll
-                for (int g = 0; g < 4; g++) {
-                    const int lr = wi * 64 + 32 * x + 8 * g + 4 * h;
-                    const float4 a4 = *reinterpret_cast<const float4 *>(rsf + lr);
-                    const float4 u4 = *reinterpret_cast<const float4 *>(ru + lr);
-                    rs[4 * g] = a4.x, rs[4 * g + 1] = a4.y, rs[4 * g + 2] = a4.z, rs[4 * g + 3] = a4.w;
-                    uu[4 * g] = u4.x, uu[4 * g + 1] = u4.y, uu[4 * g + 2] = u4.z, uu[4 * g + 3] = u4.w;
-                }
-                auto cand2 = [&](int k, float wjj, float vjj, float a0, float a1, bool &c0, bool &c1) {
-                    const f2 c = __builtin_elementwise_fma(f2{rs[k], rs[k + 1]}, f2{wjj, wjj}, f2{a0, a1});
-                    const f2 tt = __builtin_elementwise_fma(f2{uu[k], uu[k + 1]}, f2{vjj, vjj}, f2{negE, negE});
-                    c0 = fabsf(c.x) >= tt.x;
-                    c1 = fabsf(c.y) >= tt.y;
-                    if (decltype(check)::value) {
-                        const int row = 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
-                        c0 = c0 & ((unsigned)(row - lo[y]) < (unsigned)span[y]);
-                        c1 = c1 & ((unsigned)(row + 1 - lo[y]) < (unsigned)span[y]);
+                for (int y = 0; y < 4; y++)
+#pragma unroll
+                    for (int e2 = 0; e2 < 4; e2 += 2) {
+                        const int k = 4 * g + e2;
+                        bool c0, c1;
+                        test2(x, y, k, rsg + e2, uug + e2, wv[y], vj[y], acc[x][y][k], acc[x][y][k + 1], c0, c1);
+                        any[y] = any[y] | c0 | c1;
+                        __builtin_amdgcn_sched_barrier(0);  // keep the pairs' temporaries short-lived
                     }
-                };
-                bool any = false;
+            }
 #pragma unroll
-                for (int k = 0; k < 16; k += 2) {
-                    bool c0, c1;
-                    cand2(k, wv[y], vj[y], acc[x][y][k], acc[x][y][k + 1], c0, c1);
-                    any = any | c0 | c1;
-                    __builtin_amdgcn_sched_barrier(0);  // keep the pairs' temporaries short-lived
-                }
+            for (int y = 0; y < 4; y++) {
                 // only lanes holding a candidate: exact fp64 r^2 (out of line)
-                if (any) {
-                    // recomputed from laundered operands: sharing pass A's temporaries would
-                    // keep them live (and spilled) across pass A for this rare path
+                if (any[y]) {
+                    // recomputed from laundered operands and re-read terms: sharing the test's
+                    // temporaries would keep them live (and spilled) across it for this rare path
                     float wjj = wv[y], vjj = vj[y];
                     asm volatile("" : "+v"(wjj), "+v"(vjj));
 #pragma unroll
                     for (int k = 0; k < 16; k += 2) {
                         float a0 = acc[x][y][k], a1 = acc[x][y][k + 1];
                         asm volatile("" : "+v"(a0), "+v"(a1));
+                        const int lr = wi * 64 + 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
+                        const float rs2[2] = {rsf[lr], rsf[lr + 1]}, uu2[2] = {ru[lr], ru[lr + 1]};
                         bool c[2];
-                        cand2(k, wjj, vjj, a0, a1, c[0], c[1]);
+                        test2(x, y, k, rs2, uu2, wjj, vjj, a0, a1, c[0], c[1]);
 #pragma unroll
                         for (int e = 0; e < 2; e++)
                             if (c[e])
@@ -423,7 +431,7 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
 #pragma unroll
             for (int y = 0; y < 4; y++) anyc |= cbm[y][0] | cbm[y][1];
         // (no candidate in the half: no tables; its counts are written as 0 below)
-        const bool tables = __syncthreads_or(anyc != 0u);
+        const bool tables = __syncthreads_or(anyc != 0u) && !(VCFXG_LD_EXPT & 128);
         if (tables) {
         for (int k = t * 16; k < kSpRC; k += kWaves * kWave * 16) *reinterpret_cast<uint4 *>(lds + k) = make_uint4(0, 0, 0, 0);
         __syncthreads();
@@ -516,7 +524,7 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                 jokv[y] = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
 #pragma unroll
                 for (int x = 0; x < 2; x++) {
-                    const uint32_t cb = cbm[y][x];
+                    const uint32_t cb = (VCFXG_LD_EXPT & 128) ? 0u : cbm[y][x];
                     uint32_t pb = 0;
                     for (uint32_t mm = cb; mm; mm &= mm - 1u) {  // (rare at useful thresholds)
                         const int k = __builtin_ctz(mm);
