@@ -62,6 +62,11 @@ constexpr int kGfUnroll = VCFXG_GF_UNROLL;
 #ifndef VCFXG_AF_XREC
 #define VCFXG_AF_XREC 0
 #endif
+// VCFXG_AF_EXPT (diagnostic builds only, rows invalid): bit 0 skips the rows' staging, bit 1
+// only their frequency text
+#ifndef VCFXG_AF_EXPT
+#define VCFXG_AF_EXPT 0
+#endif
 
 // the walk's per-record reducer: AF allele counts (alt, total) or, for VCFX_hwe_tester, the
 // genotype classes (hom-ref, het, hom-alt; the third in aux_o)
@@ -390,10 +395,10 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
             // the row's text into the walker's stage (lanes = bytes): CHROM..ALT and its tab from
             // the head window, which still holds the line (the next window went to the other slot),
             // then the frequency; a line left to k_af_cx (or a stage too small) marks the walker
-            if (tail.stage) {
+            if (tail.stage && !(VCFXG_AF_EXPT & 1)) {
                 if (kind == kMetaGt && ok && wtext + rowpre + 7u <= tail.stage_cap) {
-                    uint32_t flo, fhi;
-                    af_freq_text(mode, (int32_t)alt, (int32_t)tot, flo, fhi);
+                    uint32_t flo = 0x30303030u, fhi = 0x0A3030u;
+                    if (!(VCFXG_AF_EXPT & 2)) af_freq_text(mode, (int32_t)alt, (int32_t)tot, flo, fhi);
                     char *dst = tail.stage + (uint64_t)wk * tail.stage_cap + wtext;
                     const unsigned char *src = reinterpret_cast<const unsigned char *>(cw) + (L - A);
                     for (uint32_t j0 = 0; j0 < rowpre + 7u; j0 += kWave) {
