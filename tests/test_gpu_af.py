@@ -126,14 +126,18 @@ def test_af_gt_first_flag_sweep_edge_samples(eng, oracle, tmp_path):
     """the GT-first walk's per-byte-flag sweep (gt_first_af) against the oracle on GT:AD:DP
     records holding every sample shape it must either count as a quick 'c0 s c2' GT or hand to
     the exact path: letters, haploid and multi-digit GTs, spaces, empty samples, a non-ASCII
-    byte, a CRLF line end, a bare last GT ('0|1' then the line end), a sample cut to 1-2 bytes
-    at the line end, a GT at a lane / step boundary"""
+    byte (also right before the line end), a CRLF line end, a bare last GT ('0|1' then the line
+    end), a sample cut to 1-2 bytes at the line end, a GT at a lane / step boundary"""
     buf = synth.generate(n_records=400, n_samples=600, seed=41, missing_rate=0.01, format_mode=1)
     edits = [
         (3, 5, b"A|1:3,4:7"), (7, 0, b"0:3,4:7"), (11, 599, b"10|1:2,2:4"), (13, 100, b"0 |1:2,2:4"),
         (17, 200, b""), (19, 300, b"0|1:\xc3\xa9,4:7"), (23, 599, b"0|1"), (29, 599, b"0"), (31, 599, b"0|"),
         (37, 42, b"0|1:1,2:3:4:5"), (41, 63, b".|1:1,1:2"), (43, 64, b"1/.:1,1:2"), (47, 1, b"|0:1,1:2"),
         (53, 2, b"0||:1,1:2"), (59, 77, b"0|1\t"), (61, 599, b"1|1:"), (67, 5, b"0/1:"), (71, 9, b"-|1:1,1:2"),
+        # a non-ASCII byte right before the line end, at each offset in a dword (its SWAR carry
+        # must not hide the '\n' from the end search)
+        (83, 599, b"0|1:3,4:\xc3\xa9"), (85, 599, b"0|1:3,4:7\xc3\xa9"), (87, 599, b"0|1:3,4:77\xc3\xa9"),
+        (89, 599, b"0|1:3,4:777\xc3\xa9"),
     ]
     buf = _mutate_gtadp(buf, edits)
     # one CRLF record

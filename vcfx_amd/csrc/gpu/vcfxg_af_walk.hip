@@ -5,8 +5,10 @@
 // (vcfxg_walk.h walker_lines: two short backward scans; the line across a chunk boundary goes
 // to the walker after it, which reads it first).  It walks its lines one after the other:
 //
-//   1. one 1 KiB window at the line start (16 B per lane) gives the first '\n' if the line
-//      is short, the first 9 tabs and the FORMAT bytes (ballots + a wave scan);
+//   1. one kWin (256 B) window at the line start (4 B per lane, LDS-DMA'd during the previous
+//      line's sweep) gives the first '\n' if the line is short, the first 9 tabs and the
+//      FORMAT bytes (SWAR masks, one ballot, then scalar code over the matching lanes; a head
+//      longer than the window gets a 1 KiB one);
 //   2. the line end E: the window's '\n'; or, for a GT-only record (FORMAT == "GT"), the
 //      PREDICTED end S + span (span = the '\n' distance from the sample start of the
 //      walker's previous fixed-stride record, first the header's 4 * samples - 1), accepted
@@ -117,9 +119,10 @@ __global__ __launch_bounds__(kWalkThreads)
 __attribute__((amdgpu_waves_per_eu(1, VCFXG_WALK_MAXW)))
 #else
 // the GT-first walk at <= 128 VGPRs (4 waves per SIMD; it needs 129 unconstrained, which
-// rounds to 136 and 3 waves)
+// rounds to 136 and 3 waves); the others at <= 96 (5 waves: the HWE walk took 100 without
+// the bound, 4 waves; no spills at 96)
 #ifndef VCFXG_AF_MINW
-#define VCFXG_AF_MINW 1
+#define VCFXG_AF_MINW 5
 #endif
 __attribute__((amdgpu_waves_per_eu(kGF ? 4 : VCFXG_AF_MINW)))
 #endif
@@ -187,53 +190,58 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         }
         // ---- 1. window analysis (offsets relative to A); a head that does not fit the short
         // window (no '\n' and fewer than 9 tabs in it) gets the 1 KiB window
-        const int b = 16 * lane();
         const int Lr = (int)(L - A);
         const uint4 *cw = win[wv][cur];
         int hr, N1r, r4 = 0, r7 = 0, r8 = 0;
         uint32_t ntab, first, hflags = 0;
-        auto analyze = [&](int ws) {
-            const uint4 W = read_window(cw);
-            hr = (int)std::min<int64_t>(hi - A, ws);
-            const uint32_t nlm = eq_mask16(W, kRepNl) & range16(b, Lr, hr);
-            const uint64_t anyn = __ballot(nlm != 0u);
-            N1r = -1;
-            if (anyn) {
-                const int k = __builtin_ctzll(anyn);
-                N1r = __builtin_amdgcn_readfirstlane(16 * k + __builtin_ctz((uint32_t)__shfl((int)nlm, k)));
-            }
-            const uint32_t tm = eq_mask16(W, kRepTab) & range16(b, Lr, N1r >= 0 ? N1r : hr);
-            const uint32_t tc = __popc(tm);
-            const uint32_t tinc = wave_incl_scan(tc);
-            ntab = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tinc, kWave - 1));
-            first = slot_byte(cw, Lr);
-            if (ntab >= 9) {
-                r4 = tab_at(tm, tinc - tc, tc, 4, b);
-                r7 = tab_at(tm, tinc - tc, tc, 7, b);
-                r8 = tab_at(tm, tinc - tc, tc, 8, b);
-                if (R::kAux) {  // HWE row rules on CHROM..ALT (VCFX_hwe_tester.cpp:497-506)
-                    const int r0 = tab_at(tm, tinc - tc, tc, 0, b), r1 = tab_at(tm, tinc - tc, tc, 1, b),
-                              r3 = tab_at(tm, tinc - tc, tc, 3, b);
-                    const bool comma = __ballot((eq_mask16(W, 0x2C2C2C2Cu) & range16(b, r3 + 1, r4)) != 0u) != 0ull;
-                    const bool empty = r0 == Lr || r1 == r0 + 1 || r4 == r3 + 1;
-                    hflags = (comma ? kHweAltComma : 0u) | (empty ? kHweEmptyField : 0u);
-                }
+        // the tab positions -> r4, r7, r8 (and HWE's row rules on CHROM..ALT,
+        // VCFX_hwe_tester.cpp:497-506: an ALT with a comma, an empty CHROM / POS / ALT)
+        auto take = [&](const int(&rt)[9], bool comma) {
+            r4 = rt[4];
+            r7 = rt[7];
+            r8 = rt[8];
+            if (R::kAux) {
+                const bool empty = rt[0] == Lr || rt[1] == rt[0] + 1 || r4 == rt[3] + 1;
+                hflags = (comma ? kHweAltComma : 0u) | (empty ? kHweEmptyField : 0u);
             }
         };
-        analyze(kWin);
-        if (N1r < 0 && ntab < 9 && first != '#' && hr == kWin) {  // (rare) a long head
-            prefetch_window(buf, A, hi, win[wv][cur], kWaveStep);
-            analyze(kWaveStep);
+        // the kWin window, four bytes per lane (the lane's dword stays in w4 for the byte reads
+        // below: a v_readlane each instead of an LDS round trip)
+        uint32_t w4 = 0;
+        bool long_head = false;
+        {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            w4 = reinterpret_cast<const uint32_t *>(cw)[lane()];
+            hr = (int)std::min<int64_t>(hi - A, kWin);
+            const uint32_t rg = range4(Lr, hr);
+            N1r = first_match<4>(zero_bytes(w4 ^ kRepNl) & rg);
+            int rt[9] = {};
+            ntab = first_tabs<4>(zero_bytes(w4 ^ kRepTab) & rg, N1r >= 0 ? N1r : hr, rt);
+            first = dword_byte(w4, Lr);
+            if (ntab >= 9) take(rt, R::kAux && __ballot((zero_bytes(w4 ^ 0x2C2C2C2Cu) & range4(rt[3] + 1, rt[4])) != 0u));
         }
+        if (N1r < 0 && ntab < 9 && first != '#' && hr == kWin) {  // (rare) a long head: the 1 KiB window
+            prefetch_window(buf, A, hi, win[wv][cur], kWaveStep);
+            long_head = true;
+            const uint4 W = read_window(cw);
+            const int b = 16 * lane();
+            hr = (int)std::min<int64_t>(hi - A, kWaveStep);
+            N1r = first_match<16>(eq_mask16(W, kRepNl) & range16(b, Lr, hr));
+            int rt[9] = {};
+            ntab = first_tabs<16>(eq_mask16(W, kRepTab) & range16(b, Lr, hr), N1r >= 0 ? N1r : hr, rt);
+            if (ntab >= 9) take(rt, R::kAux && __ballot((eq_mask16(W, 0x2C2C2C2Cu) & range16(b, rt[3] + 1, rt[4])) != 0u));
+        }
+        // window byte o (wave-uniform, < hr)
+        auto wbyte = [&](int o) { return long_head ? slot_byte(cw, o) : dword_byte(w4, o); };
         const int64_t wend = A + hr;
         int64_t t4 = -1, t8 = -1;
         bool gt_head = false, gt_only = false;
         if (ntab >= 9 && first != '#') {
             t4 = A + r4;
             t8 = A + r8;
-            if (r8 - r7 >= 3 && slot_byte(cw, r7 + 1) == 'G' && slot_byte(cw, r7 + 2) == 'T') {
+            if (r8 - r7 >= 3 && wbyte(r7 + 1) == 'G' && wbyte(r7 + 2) == 'T') {
                 gt_only = r8 - r7 == 3;
-                gt_head = gt_only || slot_byte(cw, r7 + 3) == ':';
+                gt_head = gt_only || wbyte(r7 + 3) == ':';
             }
         }
         // ---- 2. line end (and its '\r' in file mode)
@@ -243,7 +251,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         const bool gf = kGF && N1r < 0 && gt_head && !gt_only;  // the end comes with the sweep
         if (N1r >= 0) {
             E = A + N1r;
-            cr = strip_cr && E > L && slot_byte(cw, N1r - 1) == '\r';
+            cr = strip_cr && E > L && wbyte(N1r - 1) == '\r';
         } else if (gf) {
             E = hi;  // (until gt_first finds the '\n')
         } else if (gt_only && span > 0 && t8 + 1 + span <= hi) {
@@ -258,7 +266,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         }
         // every read of the current slot happens before the next prefetch is issued (an LDS
         // read after it would make the compiler wait for the LDS-DMA)
-        const uint32_t sep_w = gt_head && t8 + 2 < wend ? slot_byte(cw, (int)(t8 + 2 - A)) : 0u;
+        const uint32_t sep_w = gt_head && t8 + 2 < wend ? wbyte((int)(t8 + 2 - A)) : 0u;
         // the next window (the next line's head, and bytes E - 1 and E): issued right after
         // the sweep's first loads (issued before them, the sweep loop's head wait would
         // hold its loads back until the window landed)

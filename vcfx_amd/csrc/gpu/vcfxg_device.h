@@ -49,6 +49,19 @@ __device__ __forceinline__ uint32_t range16(int b, int lo, int hi) {
 __device__ __forceinline__ uint4 load16(const char *buf, int64_t off) {
     return *reinterpret_cast<const uint4 *>(buf + off);
 }
+// a raw buffer resource over [p, p + bytes) (bytes < 2^31, p wave-uniform): a load whose
+// offset is past the end returns 0 without touching memory, so a sweep's lanes past its
+// record need no clamped addresses -- the load is one instruction on a per-lane 32-bit offset
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, int off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return uint4{v[0], v[1], v[2], v[3]};
+}
+__device__ __forceinline__ uint32_t bload4(__amdgpu_buffer_rsrc_t r, int off) {
+    return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
 __device__ __forceinline__ uint32_t load4(const char *buf, int64_t off) {
     return *reinterpret_cast<const uint32_t *>(buf + off);
 }
@@ -56,6 +69,30 @@ __device__ __forceinline__ uint32_t byte_at(const char *buf, int64_t off) {
     return (uint32_t)(uint8_t)buf[off];
 }
 
+// DPP move of x within the wave (lanes the pattern gives no source, or rows row_mask leaves
+// out, read 0): the building block of the 32-bit scans and sums below, which take six DPP
+// adds where the shuffle forms took six LDS permutes, each a round trip the wave waits for
+template <int kCtrl, int kRowMask = 0xF>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, kCtrl, kRowMask, 0xF, false);
+}
+// inclusive prefix sum over the 64 lanes: Hillis-Steele inside each row of 16 (row_shr 1, 2,
+// 4, 8), then row 0's total into row 1 and row 2's into row 3 (row_bcast:15), then rows
+// 0..1's total into rows 2 and 3 (row_bcast:31).  EVERY LANE MUST BE ACTIVE (a DPP source
+// lane outside EXEC holds a stale value): the walkers' uniform per-record code calls it.
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t x) {
+    x += dpp0<0x111>(x);
+    x += dpp0<0x112>(x);
+    x += dpp0<0x114>(x);
+    x += dpp0<0x118>(x);
+    x += dpp0<0x142, 0xA>(x);
+    x += dpp0<0x143, 0xC>(x);
+    return x;
+}
+// the sum over the wave (every lane active), wave-uniform in scalar registers
+__device__ __forceinline__ uint32_t wave_sum32(uint32_t x) {
+    return __builtin_amdgcn_readlane(wave_incl_scan32(x), kWave - 1);
+}
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T v) {
 #pragma unroll
@@ -73,6 +110,8 @@ __device__ __forceinline__ T wave_sum(T v) {
 }
 template <typename T>
 __device__ __forceinline__ T wave_bcast(T v, int src) { return __shfl(v, src); }
+// lane k's 32-bit x (k wave-uniform), in scalar registers
+__device__ __forceinline__ uint32_t lane_get(uint32_t x, int k) { return __builtin_amdgcn_readlane(x, k); }
 // lane i gets lane i - 1's x, lane 0 gets 0: one DPP move (wave_shr:1), no LDS permute
 __device__ __forceinline__ uint32_t lane_prev(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xF, 0xF, false);

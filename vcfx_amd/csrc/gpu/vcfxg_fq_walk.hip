@@ -117,43 +117,42 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
             break;
         }
         // ---- 1. window analysis (offsets relative to A): the first '\n', the first 9 tabs
-        const int b = 16 * lane();
         const int Lr = (int)(L - A);
         const uint4 *cw = win[wv][cur];
-        int hr, N1r, rt[9];
+        int hr, N1r, rt[9] = {};
         uint32_t ntab, first;
-        uint4 W;  // this lane's 16 window bytes
-        auto analyze = [&](int ws) {
-            W = read_window(cw);
-            hr = (int)std::min<int64_t>(hi - A, ws);
-            const uint32_t nlm = eq_mask16(W, kRepNl) & range16(b, Lr, hr);
-            const uint64_t anyn = __ballot(nlm != 0u);
-            N1r = -1;
-            if (anyn) {
-                const int k = __builtin_ctzll(anyn);
-                N1r = __builtin_amdgcn_readfirstlane(16 * k + __builtin_ctz((uint32_t)__shfl((int)nlm, k)));
-            }
-            const uint32_t tm = eq_mask16(W, kRepTab) & range16(b, Lr, N1r >= 0 ? N1r : hr);
-            const uint32_t tc = __popc(tm);
-            const uint32_t tinc = wave_incl_scan(tc);
-            ntab = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)tinc, kWave - 1));
-            first = slot_byte(cw, Lr);
-#pragma unroll
-            for (int r = kRF ? 0 : 7; r < 9; r++) rt[r] = (uint32_t)r < ntab ? tab_at(tm, tinc - tc, tc, r, b) : 0;
-        };
-        analyze(kWin);
-        if (N1r < 0 && ntab < 9 && first != '#' && hr == kWin) {  // (rare) a long head
-            prefetch_window(buf, A, hi, win[wv][cur], kWaveStep);
-            analyze(kWaveStep);
+        // the kWin window, four bytes per lane (vcfxg_walk.h first_tabs; the lane's dword stays
+        // in w4 for the byte reads below)
+        uint32_t w4 = 0;
+        bool long_head = false;
+        {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            w4 = reinterpret_cast<const uint32_t *>(cw)[lane()];
+            hr = (int)std::min<int64_t>(hi - A, kWin);
+            const uint32_t rg = range4(Lr, hr);
+            N1r = first_match<4>(zero_bytes(w4 ^ kRepNl) & rg);
+            ntab = first_tabs<4>(zero_bytes(w4 ^ kRepTab) & rg, N1r >= 0 ? N1r : hr, rt);
+            first = dword_byte(w4, Lr);
         }
+        if (N1r < 0 && ntab < 9 && first != '#' && hr == kWin) {  // (rare) a long head: the 1 KiB window
+            prefetch_window(buf, A, hi, win[wv][cur], kWaveStep);
+            long_head = true;
+            const uint4 W = read_window(cw);
+            const int b = 16 * lane();
+            hr = (int)std::min<int64_t>(hi - A, kWaveStep);
+            N1r = first_match<16>(eq_mask16(W, kRepNl) & range16(b, Lr, hr));
+            ntab = first_tabs<16>(eq_mask16(W, kRepTab) & range16(b, Lr, hr), N1r >= 0 ? N1r : hr, rt);
+        }
+        // window byte o (wave-uniform, < hr)
+        auto wbyte = [&](int o) { return long_head ? slot_byte(cw, o) : dword_byte(w4, o); };
         const int64_t wend = A + hr;
         const int64_t t8 = ntab >= 9 ? A + rt[8] : -1;
         bool gt_head = false, gt_only = false;
         if (ntab >= 9 && first != '#') {
             const int r7 = rt[7], r8 = rt[8];
-            if (r8 - r7 >= 3 && slot_byte(cw, r7 + 1) == 'G' && slot_byte(cw, r7 + 2) == 'T') {
+            if (r8 - r7 >= 3 && wbyte(r7 + 1) == 'G' && wbyte(r7 + 2) == 'T') {
                 gt_only = r8 - r7 == 3;
-                gt_head = gt_only || slot_byte(cw, r7 + 3) == ':';
+                gt_head = gt_only || wbyte(r7 + 3) == ':';
             }
         }
         // fields 0-7 inside the window: the whole line, or its first 8 tabs (and criteria and
@@ -165,7 +164,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
         bool predicted = false;
         if (N1r >= 0) {
             E = A + N1r;
-            cr = strip_cr && E > L && slot_byte(cw, N1r - 1) == '\r';
+            cr = strip_cr && E > L && wbyte(N1r - 1) == '\r';
         } else if (kGQ && gt_only && span > 0 && t8 + 1 + span <= hi) {
             E = t8 + 1 + span;  // checked after the sweep (its end bytes come with the next window)
             cr = cr_prev;
@@ -174,7 +173,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
             E = scan_nl(buf, wend, hi);
             cr = strip_cr && E > L && __builtin_amdgcn_readfirstlane(byte_at(buf, E - 1)) == '\r';
         }
-        const uint32_t sep_w = gt_head && t8 + 2 < wend ? slot_byte(cw, (int)(t8 + 2 - A)) : 0u;
+        const uint32_t sep_w = gt_head && t8 + 2 < wend ? wbyte((int)(t8 + 2 - A)) : 0u;
         // ---- 3. kind and the query sweep; the next
         // window's prefetch is issued right after the sweep's first loads
         const int nxt = cur ^ 1;

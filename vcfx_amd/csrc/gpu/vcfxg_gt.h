@@ -10,6 +10,8 @@
 // deviates anywhere returns false (wave-uniform) and the caller runs gt_general, which
 // restates the reference's per-sample loop exactly.
 #pragma once
+#include <algorithm>
+
 #include "vcfxg_device.h"
 
 // af_fixed's loads: a batch of kUnroll wave-steps per sweep step (default), or rolling
@@ -77,31 +79,37 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
     const int64_t b0 = S & ~(int64_t)15;
     const char *__restrict__ base = buf + b0;
     const int Sr = (int)(S - b0), Er = (int)(E - b0);  // record bounds relative to b0
-    const int lastblk = (Er - 1) & ~15;                 // block holding the record's last byte
+#if VCFXG_NT_SWEEP
+    const int lastblk = (Er - 1) & ~15;  // block holding the record's last byte
+#endif
     uint32_t err = 0;
     if (swept) *swept = E;
     // kUnroll wave-steps per iteration: their loads are all issued before any is consumed
     const int lo16 = lane() * kBlockBytes;
+#if !VCFXG_NT_SWEEP
+    // the record's 16 B blocks as a buffer: a lane past the record reads zeros (its bytes are
+    // masked below) with no clamped address, and the loads issue back to back in one basic
+    // block (per-lane branches around them made the compiler wait for each before the next)
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(base, (uint32_t)((Er + 15) & ~15));
+#endif
     for (int w0 = 0; w0 < Er; w0 += kUnroll * kWaveStep) {
         uint4 v[kUnroll];
         uint32_t x4[kUnroll];
-        // branch-free loads: a lane past the record re-reads the record's last block (its
-        // bytes are masked below), so the loads issue back to back in one basic block
-        // (per-lane branches around them made the compiler wait for each before the next)
 #pragma unroll
         for (int u = 0; u < kUnroll; u++) {
             const int blk = w0 + u * kWaveStep + lo16;
-            const int bl = blk < Er ? blk : lastblk;
 #if VCFXG_NT_SWEEP  // streaming (non-temporal) loads for the read-once sample bytes
+            const int bl = blk < Er ? blk : lastblk;  // (a lane past the record re-reads its last block)
             {
                 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
                 const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u *>(base + bl));
                 v[u] = make_uint4(t.x, t.y, t.z, t.w);
             }
-#else
-            v[u] = load16(base, bl);
-#endif
             x4[u] = load4(base, bl + 16);
+#else
+            v[u] = bload16(rs, blk);
+            x4[u] = bload4(rs, blk + 16);
+#endif
         }
         if (w0 == 0) pre();  // e.g. a prefetch that must not hold up these loads
 #pragma unroll
@@ -387,15 +395,18 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
     uint32_t scarry = 0;  // its last dword's starts
     const int64_t b0 = S & ~(int64_t)15;
     const int lo16 = lane() * kBlockBytes;
+    const int64_t hend = (hi + 15) & ~(int64_t)15;  // (the block holding hi - 1 is read whole)
     for (int64_t w0 = b0; w0 < hi && !found; w0 += kU * kWaveStep) {
         uint4 v[kU];
         uint32_t x4[kU];
+        // the batch's bytes as a buffer based at w0: lanes past hi read zeros (masked below),
+        // no per-lane 64-bit address or clamp
+        const __amdgpu_buffer_rsrc_t rs =
+            buf_rsrc(buf + w0, (uint32_t)std::min<int64_t>(hend - w0, (int64_t)kU * kWaveStep + 16));
 #pragma unroll
-        for (int u = 0; u < kU; u++) {  // branch-free: lanes past hi re-read the last block
-            const int64_t blk = w0 + u * kWaveStep + lo16;
-            const int64_t bl = blk < hi ? blk : ((hi - 1) & ~(int64_t)15);
-            v[u] = load16(buf, bl);
-            x4[u] = load4(buf, bl + 16);
+        for (int u = 0; u < kU; u++) {
+            v[u] = bload16(rs, u * kWaveStep + lo16);
+            x4[u] = bload4(rs, u * kWaveStep + lo16 + 16);
         }
 #pragma unroll
         for (int u = 0; u < kU; u++) {
@@ -406,16 +417,19 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
             // ---- the record end: the first '\n' at or after S (the first step may hold bytes
             // before S, the last lanes of the input's last step re-read its last block)
             const bool first = ws == b0, edge = first || ws + kWaveStep > hi;  // wave-uniform
-            // interior steps: the ASCII shortcut (the same sums as the classes below), exact only
-            // where it flags a byte: it can flag bytes >= 0x80 (such a record goes to the exact
-            // path anyway, but its end must still be the true '\n')
+            // interior steps of ASCII bytes: the shortcut (the same sums as the classes below),
+            // exact only where it flags a byte.  A byte >= 0x80 can carry into the next byte's
+            // sum and hide a '\n' there (and such a record goes to the exact path, which needs
+            // the true end): a step holding one takes the exact masks.
+            const bool exact = edge || __ballot(((W[0] | W[1] | W[2] | W[3]) & M) != 0u) != 0ull;
             uint32_t nlm = 0;
             if (edge) nlm = blk < hi ? eq_mask16(v[u], kRepNl) & range_mask16(blk, S, hi) : 0u;
+            else if (exact) nlm = eq_mask16(v[u], kRepNl);
             else
                 nlm = ~(((W[0] ^ kRepNl) + K) & ((W[1] ^ kRepNl) + K) & ((W[2] ^ kRepNl) + K) &
                         ((W[3] ^ kRepNl) + K)) & M;
             uint64_t anyn = __ballot(nlm != 0u);
-            if (anyn && !edge) {  // (rare: the step holding the record end) exact masks
+            if (anyn && !exact) {  // (rare: the step holding the record end) exact masks
                 nlm = eq_mask16(v[u], kRepNl);
                 anyn = __ballot(nlm != 0u);
             }
@@ -497,8 +511,8 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
     }
     E_out = E;
     if (__any((bad | (asc & M)) != 0u)) return false;
-    op.alt = wave_sum(alt);
-    op.tot = wave_sum(tot);
+    op.alt = wave_sum32(alt);  // (every lane active: the walk's uniform per-record path)
+    op.tot = wave_sum32(tot);
     return true;
 }
 
@@ -537,29 +551,26 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
     const int64_t b0 = S & ~(int64_t)15;
     const char *__restrict__ base = buf + b0;
     const int Sr = (int)(S - b0), Er = (int)(E - b0);  // record bounds relative to b0
-    const int lastblk = (Er - 1) & ~15;
+    // the record's 16 B blocks as a buffer: lanes past it read zeros (masked like the bytes
+    // past E, below), with no clamped address per load
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(base, (uint32_t)((Er + 15) & ~15));
     const int lo16 = lane() * kBlockBytes;
-    uint32_t alt = 0, dots = 0, err = 0;
+    uint32_t alt = 0, dots = 0, err = 0, alt8 = 0;
+    static_assert(4 * kUnroll <= 255, "af_fixed: bytewise allele sums");
 #if VCFXG_AF_ROLL
     // rolling loads: as soon as a wave-step's registers are read, the same step of the next batch
     // is issued into them, so kUnroll steps stay in flight across batches (no bubble between a
     // record's batches) at no register cost
     uint4 v[kUnroll];
 #pragma unroll
-    for (int u = 0; u < kUnroll; u++) {  // branch-free: lanes past the record re-read its last block
-        const int blk = u * kWaveStep + lo16;
-        v[u] = load16(base, blk < Er ? blk : lastblk);
-    }
+    for (int u = 0; u < kUnroll; u++) v[u] = bload16(rs, u * kWaveStep + lo16);
     pre();
 #endif
     for (int w0 = 0; w0 < Er; w0 += kUnroll * kWaveStep) {
 #if !VCFXG_AF_ROLL
         uint4 v[kUnroll];
 #pragma unroll
-        for (int u = 0; u < kUnroll; u++) {  // branch-free: lanes past the record re-read its last block
-            const int blk = w0 + u * kWaveStep + lo16;
-            v[u] = load16(base, blk < Er ? blk : lastblk);
-        }
+        for (int u = 0; u < kUnroll; u++) v[u] = bload16(rs, w0 + u * kWaveStep + lo16);
         if (w0 == 0) pre();
 #endif
 #if VCFXG_AF_ROLL
@@ -584,20 +595,15 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
             uint32_t d[4];
             dwords(u, v[u], d);
 #if VCFXG_AF_ROLL
-            if (wn < Er) {
-                const int blk = wn + u * kWaveStep + lo16;
-                v[u] = load16(base, blk < Er ? blk : lastblk);
-            }
+            if (wn < Er) v[u] = bload16(rs, wn + u * kWaveStep + lo16);
 #endif
-            uint32_t berr = 0, balt = 0;
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const uint32_t e = d[i] ^ exp;
-                berr |= e & mbin;
-                balt += __popc(e);
-            }
+            // a clean step (berr = 0) has e = bit 0 of the '1' allele bytes alone: its count is
+            // the byte sum of the e's, added bytewise (at most 4 kUnroll <= 255 per byte) and
+            // folded into alt once per batch (v_sad_u8) -- two adds a step, not four popcounts
+            const uint32_t e0 = d[0] ^ exp, e1 = d[1] ^ exp, e2 = d[2] ^ exp, e3 = d[3] ^ exp;
+            const uint32_t berr = (e0 | e1 | e2 | e3) & mbin;
             if (!__any(berr != 0u)) {
-                alt += balt;
+                alt8 += e0 + e1 + e2 + e3;
                 continue;
             }
             // some allele of the step is neither '0' nor '1': gt_fast's per-allele rules
@@ -614,9 +620,11 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
             }
         }
         if (__any(err != 0u)) return false;  // not fixed-stride: stop reading the record
+        alt = __builtin_amdgcn_sad_u8(alt8, 0u, alt);
+        alt8 = 0;
     }
-    op.alt = wave_sum(alt);
-    op.tot = (uint32_t)(2 * ((L + 1) >> 2)) - wave_sum(dots);
+    op.alt = wave_sum32(alt);  // (every lane active)
+    op.tot = (uint32_t)(2 * ((L + 1) >> 2)) - wave_sum32(dots);
     return true;
 }
 
@@ -711,8 +719,8 @@ __device__ bool af_fixed_x(const char *__restrict__ buf, int64_t S, int64_t E, i
         }
         if (__any(err != 0u)) return false;
     }
-    op.alt = wave_sum(alt);
-    op.tot = (uint32_t)(2 * ((L + 1) >> 2)) - wave_sum(dots);
+    op.alt = wave_sum32(alt);  // (every lane active)
+    op.tot = (uint32_t)(2 * ((L + 1) >> 2)) - wave_sum32(dots);
     vb_out = nb;
     return true;
 }

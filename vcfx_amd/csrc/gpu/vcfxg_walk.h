@@ -41,7 +41,7 @@ __device__ __forceinline__ int64_t scan_nl(const char *__restrict__ buf, int64_t
             const uint64_t any = __ballot(m != 0u);
             if (any) {
                 const int k = __builtin_ctzll(any);
-                const uint32_t mk = (uint32_t)__shfl((int)m, k);
+                const uint32_t mk = lane_get(m, k);
                 return uniform64(w + (int64_t)u * kWaveStep + 16 * k + __builtin_ctz(mk));
             }
         }
@@ -69,7 +69,7 @@ __device__ __forceinline__ int64_t scan_nl_back(const char *__restrict__ buf, in
             const uint64_t any = __ballot(m != 0u);
             if (any) {
                 const int k = __builtin_ctzll(any);
-                const uint32_t mk = (uint32_t)__shfl((int)m, k);  // (nonzero: lane k's exact mask)
+                const uint32_t mk = lane_get(m, k);  // (nonzero: lane k's exact mask)
                 return uniform64(top - (int64_t)kBlockBytes * (u * kWave + k) + 31 - __builtin_clz(mk));
             }
         }
@@ -95,25 +95,41 @@ __device__ __forceinline__ void walker_lines(const char *__restrict__ buf, int64
     int64_t ta = (cs - 1) & ~(int64_t)15, tb = (ce - 1) & ~(int64_t)15;
     if (ta < lb) da = true;
     if (tb < lb) db = true;
+    // a step's blocks descend from top: block (u, lane) at top - 16 (64 u + lane).  Each scan's
+    // loads go through a buffer based at its iteration's lowest block (no lower than lb), so a
+    // block below lb -- or any block of a finished scan (an empty buffer) -- reads zeros with
+    // no clamped 64-bit address: its offset is negative, i.e. far past the buffer's end.
+    constexpr int kSpan = kU * kWave * kBlockBytes;
+    const int off16 = kBlockBytes * lane();
     while (!(da && db)) {
+        const int64_t ba = std::max<int64_t>(lb, ta + kBlockBytes - kSpan), bb0 = std::max<int64_t>(lb, tb + kBlockBytes - kSpan);
+        const __amdgpu_buffer_rsrc_t rsa = buf_rsrc(buf + ba, da ? 0u : (uint32_t)(ta + kBlockBytes - ba));
+        const __amdgpu_buffer_rsrc_t rsb = buf_rsrc(buf + bb0, db ? 0u : (uint32_t)(tb + kBlockBytes - bb0));
         uint4 va[kU], vb[kU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) {  // (a finished scan re-reads the lowest block: cached)
-            const int64_t pa = ta - (int64_t)kBlockBytes * (u * kWave + lane());
-            const int64_t pb = tb - (int64_t)kBlockBytes * (u * kWave + lane());
-            va[u] = load16(buf, !da && pa >= lb ? pa : lb);
-            vb[u] = load16(buf, !db && pb >= lb ? pb : lb);
+        for (int u = 0; u < kU; u++) {
+            va[u] = bload16(rsa, (int)(ta - ba) - (u * kWaveStep + off16));
+            vb[u] = bload16(rsb, (int)(tb - bb0) - (u * kWaveStep + off16));
         }
+        // per step: any '\n' at all (exact per byte: ((x & 0x7F..) + 0x7F..) | x has bit 7 clear
+        // only in a zero byte; the four dwords' words ANDed), then, in the rare step that has
+        // one, the exact masks inside [lo, p) (a hit outside them -- header bytes below lo, bytes
+        // at or past p in the top block -- is dropped there and the scan goes on)
         auto look = [&](const uint4 *v, int64_t top, int64_t p, bool &done, int64_t &r) {
             if (done) return;
 #pragma unroll
             for (int u = 0; u < kU; u++) {
+                const uint32_t x0 = v[u].x ^ kRepNl, x1 = v[u].y ^ kRepNl, x2 = v[u].z ^ kRepNl, x3 = v[u].w ^ kRepNl;
+                const uint32_t K = 0x7F7F7F7Fu;
+                const uint32_t t = (((x0 & K) + K) | x0) & (((x1 & K) + K) | x1) & (((x2 & K) + K) | x2) &
+                                   (((x3 & K) + K) | x3);
+                if (!__ballot((~t & 0x80808080u) != 0u)) continue;
                 const int64_t bb = top - (int64_t)kBlockBytes * (u * kWave + lane());
                 const uint32_t m = bb >= lb ? eq_mask16(v[u], kRepNl) & range_mask16(bb, lo, p) : 0u;
                 const uint64_t any = __ballot(m != 0u);
                 if (any) {
                     const int k = __builtin_ctzll(any);
-                    const uint32_t mk = (uint32_t)__shfl((int)m, k);  // (nonzero: lane k's exact mask)
+                    const uint32_t mk = lane_get(m, k);  // (nonzero: lane k's exact mask)
                     r = uniform64(top - (int64_t)kBlockBytes * (u * kWave + k) + 31 - __builtin_clz(mk));
                     done = true;
                     return;
@@ -131,14 +147,56 @@ __device__ __forceinline__ void walker_lines(const char *__restrict__ buf, int64
     b1 = ce >= hi ? hi : rb + 1;
 }
 
-// relative position of the tab with 0-based rank r (< total) given per-lane tab masks and
-// their exclusive per-lane counts (wave-uniform result)
-__device__ __forceinline__ int tab_at(uint32_t tm, uint32_t excl, uint32_t c, int r, int b) {
-    const bool mine = (uint32_t)r >= excl && (uint32_t)r < excl + c;
-    const uint64_t who = __ballot(mine);
-    const int k = __builtin_ctzll(who);
-    const int p = mine ? b + nth_bit(tm, r - (int)excl) : 0;
-    return __builtin_amdgcn_readfirstlane(__shfl(p, k));
+// The head analysis classifies the window SWAR and then walks the matches in scalar code:
+// the lanes holding a match come from one ballot, each one's mask from one v_readlane, and
+// the positions in ascending order from s_ff1 -- no wave scan, no LDS permute, no per-lane
+// bit loop.  Two lane layouts: kBytes = 4 (lane l holds window bytes [4l, 4l + 4), a mask
+// with 0x80 per matching byte; the kWin window) or 16 (bytes [16l, 16l + 16), one bit per
+// byte; the 1 KiB window of a long head).
+template <int kBytes>
+__device__ __forceinline__ int match_pos(int k, uint32_t m) {
+    return kBytes == 4 ? 4 * k + (__builtin_ctz(m) >> 3) : 16 * k + __builtin_ctz(m);
+}
+// the first match of the per-lane masks (relative position, wave-uniform), -1 if none
+template <int kBytes>
+__device__ __forceinline__ int first_match(uint32_t mk) {
+    const uint64_t any = __ballot(mk != 0u);
+    if (!any) return -1;
+    const int k = __builtin_ctzll(any);
+    return match_pos<kBytes>(k, lane_get(mk, k));
+}
+// the first (up to) 9 tabs of the per-lane masks below position lim: rt[0..n), returns n
+template <int kBytes>
+__device__ __forceinline__ uint32_t first_tabs(uint32_t tm, int lim, int (&rt)[9]) {
+    uint64_t lanes = __ballot(tm != 0u);
+    uint32_t m = 0, n = 0;
+    int k = 0;
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+        if (m == 0u) {
+            if (lanes == 0ull) break;
+            k = __builtin_ctzll(lanes);
+            lanes &= lanes - 1ull;
+            m = lane_get(tm, k);
+        }
+        const int p = match_pos<kBytes>(k, m);
+        if (p >= lim) break;
+        rt[r] = p;
+        n = (uint32_t)r + 1u;
+        m &= m - 1u;
+    }
+    return n;
+}
+// the window bytes [lo, hi) among this lane's four (kBytes = 4 layout), 0x80 per byte
+__device__ __forceinline__ uint32_t range4(int lo, int hi) {
+    const int b = 4 * lane(), t = lo - b, u = hi - b;
+    const uint32_t mlo = t <= 0 ? 0x80808080u : t >= 4 ? 0u : (0x80808080u << (8 * t));
+    const uint32_t mhi = u >= 4 ? 0x80808080u : u <= 0 ? 0u : (0x80808080u >> (32 - 8 * u));
+    return mlo & mhi;
+}
+// window byte o (wave-uniform) out of the kBytes = 4 layout's registers
+__device__ __forceinline__ uint32_t dword_byte(uint32_t w, int o) {
+    return (lane_get(w, o >> 2) >> (8 * (o & 3))) & 0xFFu;
 }
 
 // the window at A (16 B per lane) -> the wave's LDS slot by LDS-DMA: issued before the
