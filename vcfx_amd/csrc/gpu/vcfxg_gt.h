@@ -21,6 +21,10 @@
 #ifndef VCFXG_AF_ROLL
 #define VCFXG_AF_ROLL 0
 #endif
+// gt_first_af's loads through a per-batch buffer resource (1) or clamped global addresses (0)
+#ifndef VCFXG_GF_BUF
+#define VCFXG_GF_BUF 1
+#endif
 
 namespace vcfxg {
 
@@ -399,6 +403,7 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
     for (int64_t w0 = b0; w0 < hi && !found; w0 += kU * kWaveStep) {
         uint4 v[kU];
         uint32_t x4[kU];
+#if VCFXG_GF_BUF
         // the batch's bytes as a buffer based at w0: lanes past hi read zeros (masked below),
         // no per-lane 64-bit address or clamp
         const __amdgpu_buffer_rsrc_t rs =
@@ -408,6 +413,15 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
             v[u] = bload16(rs, u * kWaveStep + lo16);
             x4[u] = bload4(rs, u * kWaveStep + lo16 + 16);
         }
+#else
+#pragma unroll
+        for (int u = 0; u < kU; u++) {  // branch-free: lanes past hi re-read the last block
+            const int64_t blk = w0 + u * kWaveStep + lo16;
+            const int64_t bl = blk < hi ? blk : hend - 16;
+            v[u] = load16(buf, bl);
+            x4[u] = load4(buf, bl + 16);
+        }
+#endif
 #pragma unroll
         for (int u = 0; u < kU; u++) {
             if (found) break;
@@ -417,19 +431,17 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
             // ---- the record end: the first '\n' at or after S (the first step may hold bytes
             // before S, the last lanes of the input's last step re-read its last block)
             const bool first = ws == b0, edge = first || ws + kWaveStep > hi;  // wave-uniform
-            // interior steps of ASCII bytes: the shortcut (the same sums as the classes below),
-            // exact only where it flags a byte.  A byte >= 0x80 can carry into the next byte's
-            // sum and hide a '\n' there (and such a record goes to the exact path, which needs
-            // the true end): a step holding one takes the exact masks.
-            const bool exact = edge || __ballot(((W[0] | W[1] | W[2] | W[3]) & M) != 0u) != 0ull;
+            // interior steps: the ASCII shortcut (the same sums as the classes below), exact only
+            // where it flags a byte.  A byte >= 0x80 can carry into the next byte's sum and hide
+            // a '\n' there (and such a record goes to the exact path, which needs the true end):
+            // the shortcut flags every such byte too, so its step takes the exact masks.
             uint32_t nlm = 0;
             if (edge) nlm = blk < hi ? eq_mask16(v[u], kRepNl) & range_mask16(blk, S, hi) : 0u;
-            else if (exact) nlm = eq_mask16(v[u], kRepNl);
             else
-                nlm = ~(((W[0] ^ kRepNl) + K) & ((W[1] ^ kRepNl) + K) & ((W[2] ^ kRepNl) + K) &
-                        ((W[3] ^ kRepNl) + K)) & M;
+                nlm = (~(((W[0] ^ kRepNl) + K) & ((W[1] ^ kRepNl) + K) & ((W[2] ^ kRepNl) + K) &
+                         ((W[3] ^ kRepNl) + K)) | W[0] | W[1] | W[2] | W[3]) & M;
             uint64_t anyn = __ballot(nlm != 0u);
-            if (anyn && !exact) {  // (rare: the step holding the record end) exact masks
+            if (anyn && !edge) {  // (rare: the step holding the record end) exact masks
                 nlm = eq_mask16(v[u], kRepNl);
                 anyn = __ballot(nlm != 0u);
             }
