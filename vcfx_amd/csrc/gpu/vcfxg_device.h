@@ -110,6 +110,12 @@ __device__ __forceinline__ T wave_sum(T v) {
 }
 template <typename T>
 __device__ __forceinline__ T wave_bcast(T v, int src) { return __shfl(v, src); }
+// acc + popcount(x) as the one v_bcnt_u32_b32 with its accumulator operand
+__device__ __forceinline__ uint32_t popc_acc(uint32_t x, uint32_t acc) {
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(acc));
+    return r;
+}
 // lane k's 32-bit x (k wave-uniform), in scalar registers
 __device__ __forceinline__ uint32_t lane_get(uint32_t x, int k) { return __builtin_amdgcn_readlane(x, k); }
 // lane i gets lane i - 1's x, lane 0 gets 0: one DPP move (wave_shr:1), no LDS permute

@@ -492,11 +492,12 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
             auto classes = [&](uint32_t x, uint32_t &sep, uint32_t &trm, uint32_t &vv, uint32_t &dg, uint32_t &nz) {
                 const uint32_t nt = (x ^ kRepTab) + K, nn = (x ^ kRepNl) + K, nc = (x ^ kRepColon) + K;
                 trm = ~(nt & nn & nc);
-                sep = ~(((x ^ 0x2F2F2F2Fu) + K) & ((x ^ 0x7C7C7C7Cu) + K));
+                const uint32_t ns = (x ^ 0x2F2F2F2Fu) + K;  // bit 7 clear: '/'
+                sep = ~(ns & ((x ^ 0x7C7C7C7Cu) + K));
                 const uint32_t g9 = x + 0x46464646u;  // >= ':'
                 dg = (x + 0x50505050u) & ~g9;         // '0'..'9'
                 nz = (x + 0x4F4F4F4Fu) & ~g9;         // '1'..'9'
-                vv = dg | ~((x ^ 0x2E2E2E2Eu) + K);
+                vv = (x + 0x52525252u) & ~g9 & ns;    // '.'..'9' but '/': '.' or a digit
             };
             uint32_t sep0, trm0, v0, dg0, nz0;
             classes(W[0], sep0, trm0, v0, dg0, nz0);
@@ -509,8 +510,8 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
                 const uint32_t s2 = __builtin_amdgcn_alignbyte(st[i], i ? st[i - 1] : sprev, 2);
                 const uint32_t u = st[i] | s2;
                 bad |= (st[i] & ~(s1 & c3)) | (u & ~v0);
-                tot += __popc(u & dg0);
-                alt += __popc(u & nz0);
+                tot = popc_acc(u & dg0, tot);  // (one v_bcnt each: the compiler split them into
+                alt = popc_acc(u & nz0, alt);  // a bcnt and a share of an add3)
                 sep0 = sep1, trm0 = trm1, v0 = v1, dg0 = dg1, nz0 = nz1;
             }
         }
