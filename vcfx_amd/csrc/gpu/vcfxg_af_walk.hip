@@ -69,6 +69,14 @@ constexpr int kGfUnroll = VCFXG_GF_UNROLL;
 #ifndef VCFXG_AF_EXPT
 #define VCFXG_AF_EXPT 0
 #endif
+// VCFXG_AF_EARLY=1: the GT-only AF walk issues a record's first sweep batch from its line start
+// (16-aligned) before analysing its head, so the batch's latency overlaps the analysis (the
+// head bytes ride along and are masked like the bytes before S)
+#ifndef VCFXG_AF_EARLY
+#define VCFXG_AF_EARLY 0
+#endif
+#define VCFXG_STR2(x) #x
+#define VCFXG_STR(x) VCFXG_STR2(x)
 
 // the walk's per-record reducer: AF allele counts (alt, total) or, for VCFX_hwe_tester, the
 // genotype classes (hom-ref, het, hom-alt; the third in aux_o)
@@ -183,11 +191,22 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     int cur = 0;
     int64_t A = L & ~(int64_t)15;  // window base of the current line (L - A < 32)
     if (L < ce2) prefetch_window(buf, A, hi, win[wv][cur]);
+    constexpr bool kEarly = VCFXG_AF_EARLY && std::is_same<Op, AfOp>::value && !kGF && !kXrec;
+    uint4 ev[kEarly ? kWalkUnroll : 1];
+    const int64_t hlast = (hi - 1) & ~(int64_t)15;
     while (L < ce2) {
         if (n >= cap_w) {
             if (lane() == 0) atomicOr(overflow, 1u);
             break;
         }
+        if constexpr (kEarly) {  // the first batch from the line start (= the window base A)
+#pragma unroll
+            for (int u = 0; u < kWalkUnroll; u++) {
+                const int64_t g = A + u * kWaveStep + kBlockBytes * lane();
+                ev[u] = load16(buf, g < hi ? g : hlast);
+            }
+        }
+        int64_t eA = kEarly ? A : -1;  // the early batch's base (-1: used or none)
         // ---- 1. window analysis (offsets relative to A); a head that does not fit the short
         // window (no '\n' and fewer than 9 tabs in it) gets the 1 KiB window
         const int Lr = (int)(L - A);
@@ -210,7 +229,9 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
         uint32_t w4 = 0;
         bool long_head = false;
         {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // the window's LDS-DMA landed (kEarly: all but the early batch, issued after it)
+            if constexpr (kEarly) asm volatile("s_waitcnt vmcnt(" VCFXG_STR(VCFXG_WALK_UNROLL) ")" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             w4 = reinterpret_cast<const uint32_t *>(cw)[lane()];
             hr = (int)std::min<int64_t>(hi - A, kWin);
             const uint32_t rg = range4(Lr, hr);
@@ -338,6 +359,12 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                     int64_t vbo;
                     ok = af_fixed_x<kWalkUnroll>(buf, S, ae, hi, op, sep, pre, xv, use, nb, vbo);
                     xvb = vbo;
+                } else if constexpr (kEarly) {
+                    // the early batch is this sweep's first when it covers S's block (a re-sweep
+                    // after a failed prediction loads its own)
+                    const bool mine = eA >= 0 && eA <= S;
+                    ok = af_fixed<kWalkUnroll>(buf, S, ae, op, sep, pre, mine ? ev : nullptr, mine ? eA : -1);
+                    eA = -1;
                 } else if constexpr (std::is_same<Op, AfOp>::value)
                     ok = af_fixed < kGF ? kGfUnroll : kWalkUnroll > (buf, S, ae, op, sep, pre);
                 else if constexpr (std::is_same<Op, DoseHeadOp>::value) {

@@ -546,8 +546,11 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
 // Returns false (wave-uniform) where gt_fast returns false; op.alt / op.tot as gt_fast leaves
 // them after op.finish().
 // ---------------------------------------------------------------------------------------
+// (first / vb: the walk's early loads -- the first kUnroll wave-steps from vb (16-aligned, <= S),
+// issued before the record's head was analysed; vb < 0: none)
 template <int kUnroll, class Pre>
-__device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfOp &op, uint32_t sep_hint, Pre pre) {
+__device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfOp &op, uint32_t sep_hint, Pre pre,
+                         const uint4 *first = nullptr, int64_t vb = -1) {
     S = uniform64(S);
     E = uniform64(E);
     const int64_t L = E - S;
@@ -561,7 +564,7 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
     const uint32_t mbin = rot(0xFFFEFFFEu);               // separator / tab bytes whole, allele bits 1..7
     const uint32_t msep = rot(0xFF00FF00u);               // separator / tab bytes
     const uint32_t fsh = (S & 1) ? 8u : 0u;               // allele bytes -> bytes 0 and 2
-    const int64_t b0 = S & ~(int64_t)15;
+    const int64_t b0 = vb >= 0 ? uniform64(vb) : S & ~(int64_t)15;
     const char *__restrict__ base = buf + b0;
     const int Sr = (int)(S - b0), Er = (int)(E - b0);  // record bounds relative to b0
     // the record's 16 B blocks as a buffer: lanes past it read zeros (masked like the bytes
@@ -583,7 +586,7 @@ __device__ bool af_fixed(const char *__restrict__ buf, int64_t S, int64_t E, AfO
 #if !VCFXG_AF_ROLL
         uint4 v[kUnroll];
 #pragma unroll
-        for (int u = 0; u < kUnroll; u++) v[u] = bload16(rs, w0 + u * kWaveStep + lo16);
+        for (int u = 0; u < kUnroll; u++) v[u] = first && w0 == 0 ? first[u] : bload16(rs, w0 + u * kWaveStep + lo16);
         if (w0 == 0) pre();
 #endif
 #if VCFXG_AF_ROLL
