@@ -45,6 +45,12 @@ namespace vcfxg {
 #define VCFXG_WALK_UNROLL 6
 #endif
 constexpr int kWalkUnroll = VCFXG_WALK_UNROLL;  // wave-steps (KiB) of a record in flight per sweep step
+// the HWE walk's sweep: 5 wave-steps (its clean-step genotype classes need the registers of the
+// sixth under the 96-VGPR bound; at 6 the record loop spilled)
+#ifndef VCFXG_HWE_UNROLL
+#define VCFXG_HWE_UNROLL 5
+#endif
+constexpr int kHweUnroll = VCFXG_HWE_UNROLL;
 // the GT-first walk's allele counts on per-byte flags (gt_first_af) rather than gt_first's loop
 // over each lane's sample starts (VCFXG_GF_FLAGS=0: the loop, for A/B)
 #ifndef VCFXG_GF_FLAGS
@@ -375,7 +381,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
                     } else {
                         ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
                     }
-                } else ok = gt_fast<kWalkUnroll>(buf, S, ae, op, sep, pre);
+                } else ok = gt_fast < std::is_same<Op, HweOp>::value ? kHweUnroll : kWalkUnroll > (buf, S, ae, op, sep, pre);
                 R::out(op, alt, tot, aux);
             }
         };

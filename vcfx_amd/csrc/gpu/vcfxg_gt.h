@@ -11,6 +11,7 @@
 // restates the reference's per-sample loop exactly.
 #pragma once
 #include <algorithm>
+#include <type_traits>
 
 #include "vcfxg_device.h"
 
@@ -62,6 +63,12 @@ __device__ __forceinline__ void fast_dword(uint32_t d, uint32_t exp_xor, uint32_
 struct NoPre {
     __device__ void operator()() const {}
 };
+// reducers with a clean-step form: op.clean(e0..e3), four sample dwords whose alleles are all
+// '0' / '1' (e = dword ^ the expected "0 s 0 \t": bit 0 = first allele '1', bit 16 = second)
+template <class T, class = void>
+struct HasClean : std::false_type {};
+template <class T>
+struct HasClean<T, std::void_t<decltype(&T::clean)>> : std::true_type {};
 // pre(): called once, right after the record's first batch of loads is issued.
 // swept (optional): the end of the bytes the sweep examined -- E, or on an early exit
 // (op.done()) the end of the last batch of loads
@@ -127,6 +134,17 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
                                  __builtin_amdgcn_alignbyte(v[u].z, v[u].y, s),
                                  __builtin_amdgcn_alignbyte(v[u].w, v[u].z, s),
                                  __builtin_amdgcn_alignbyte(x4[u], v[u].w, s)};
+                bool clean = false;
+                if constexpr (HasClean<Op>::value) {
+                    // an interior step whose every allele is '0' / '1' (e = d ^ exp has only
+                    // bits 0 and 16): the reducer's SWAR form on the four e's at once
+                    if (interior) {
+                        const uint32_t e0 = d[0] ^ exp_xor, e1 = d[1] ^ exp_xor, e2 = d[2] ^ exp_xor,
+                                       e3 = d[3] ^ exp_xor;
+                        clean = !__any(((e0 | e1 | e2 | e3) & ~0x00010001u) != 0u);
+                        if (clean) op.clean(e0, e1, e2, e3);
+                    }
+                }
                 bool real[4] = {true, true, true, true};
                 if (!interior) {
                     const int q0 = blk + s - Sr, last = Er - Sr - 3;  // dword i starts at S + q0 + 4i
@@ -139,8 +157,10 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
                         } else if (q == last) d[i] = (d[i] & 0x00FFFFFFu) | 0x09000000u;
                     }
                 }
+                if (!clean) {
 #pragma unroll
-                for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op, real[i], b0 + blk + s + 4 * i);
+                    for (int i = 0; i < 4; i++) fast_dword(d[i], exp_xor, err, op, real[i], b0 + blk + s + 4 * i);
+                }
             }
         }
         if (op.done()) {  // wave-uniform early exit (e.g. a match was found)
@@ -993,6 +1013,11 @@ struct HweOp {
         const bool ok = (v.f & 0x00FE00FEu) == 0u;
         nv_alt += ok ? (uint32_t)__popc(v.f) + 0x10000u : 0u;
         two += v.f == 0x00010001u;
+    }
+    // four valid samples: their ALT alleles (popcounts) and hom-alt ones (both bits)
+    __device__ void clean(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3) {
+        nv_alt = popc_acc(e3, popc_acc(e2, popc_acc(e1, popc_acc(e0, nv_alt + 0x40000u))));
+        two += (e0 & (e0 >> 16)) + (e1 & (e1 >> 16)) + (e2 & (e2 >> 16)) + (e3 & (e3 >> 16));
     }
     __device__ void gt3(uint32_t c0, uint32_t c2) {  // both '0' or '1': the class a + b
         const bool ok = (c0 - '0' < 2u) && (c2 - '0' < 2u);
