@@ -1,7 +1,7 @@
 #!/bin/bash
-# r04 job: HWE clean-step genotype classes in gt_fast (HweOp::clean), 5 wave-steps (build/) and
-# 4 (build_hu4), against the previous build (build_hweprev); the gt_fast users' tests first
-bash gpu_job.sh test tests/test_gpu_hwe.py tests/test_gpu_dose.py tests/test_gpu_gq.py tests/test_gpu_nr.py tests/test_gpu_pipe.py || exit $?
-bash gpu_job.sh ab hwe build_hweprev/libvcfx_gpu.so 2 --steps 20 --workload hwe || exit $?
-bash gpu_job.sh ab hu4 build_hu4/libvcfx_gpu.so 2 --steps 20 --workload hwe || exit $?
-bash gpu_job.sh ab af build_hweprev/libvcfx_gpu.so 1 --steps 20 || exit $?
+# r04 job: clean-step forms for the NR, MD and DOSE sweeps (NrOp / MdOp / DoseWalkOp::clean),
+# their tests, then A/B against the previous build (build_cprev)
+bash gpu_job.sh test tests/test_gpu_nr.py tests/test_gpu_md.py tests/test_gpu_dose.py tests/test_gpu_hwe.py || exit $?
+bash gpu_job.sh ab md build_cprev/libvcfx_gpu.so 2 --steps 20 --workload md || exit $?
+bash gpu_job.sh ab nr build_cprev/libvcfx_gpu.so 2 --steps 20 --workload nonref || exit $?
+bash gpu_job.sh ab dose build_cprev/libvcfx_gpu.so 1 --steps 20 --workload dose || exit $?
