@@ -1,6 +1,5 @@
 #!/bin/bash
-# r04 job: GT-first sweep batch depth (5 / 3 wave-steps against the default 4) on GT:AD:DP, and
-# the AF early first batch at 5 wave-steps again ('old' rows = the variant)
-bash gpu_job.sh ab gu5 build_gu5/libvcfx_gpu.so 2 --steps 20 --format gt:ad:dp || exit $?
-bash gpu_job.sh ab gu3 build_gu3/libvcfx_gpu.so 1 --steps 20 --format gt:ad:dp || exit $?
-bash gpu_job.sh ab eu5 build_eu5/libvcfx_gpu.so 3 --steps 20 || exit $?
+# r04 job: GT-first sweep sharing the OR of a lane's words between the ASCII check and the
+# newline shortcut: the AF tests, then GT:AD:DP A/B against the previous build (build_gfprev2)
+bash gpu_job.sh test tests/test_gpu_af.py tests/test_gpu_af_fused.py || exit $?
+bash gpu_job.sh ab gtadp build_gfprev2/libvcfx_gpu.so 2 --steps 20 --format gt:ad:dp || exit $?

@@ -447,7 +447,8 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
             if (found) break;
             const int64_t ws = w0 + u * kWaveStep, blk = ws + lo16;
             const uint32_t W[5] = {v[u].x, v[u].y, v[u].z, v[u].w, x4[u]};
-            asc |= W[0] | W[1] | W[2] | W[3] | W[4];
+            const uint32_t wor = W[0] | W[1] | W[2] | W[3];  // (bit 7: a byte >= 0x80)
+            asc |= wor | W[4];
             // ---- the record end: the first '\n' at or after S (the first step may hold bytes
             // before S, the last lanes of the input's last step re-read its last block)
             const bool first = ws == b0, edge = first || ws + kWaveStep > hi;  // wave-uniform
@@ -459,7 +460,7 @@ __device__ bool gt_first_af(const char *__restrict__ buf, int64_t S, int64_t hi,
             if (edge) nlm = blk < hi ? eq_mask16(v[u], kRepNl) & range_mask16(blk, S, hi) : 0u;
             else
                 nlm = (~(((W[0] ^ kRepNl) + K) & ((W[1] ^ kRepNl) + K) & ((W[2] ^ kRepNl) + K) &
-                         ((W[3] ^ kRepNl) + K)) | W[0] | W[1] | W[2] | W[3]) & M;
+                         ((W[3] ^ kRepNl) + K)) | wor) & M;
             uint64_t anyn = __ballot(nlm != 0u);
             if (anyn && !edge) {  // (rare: the step holding the record end) exact masks
                 nlm = eq_mask16(v[u], kRepNl);
