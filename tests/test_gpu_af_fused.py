@@ -14,17 +14,19 @@ from vcfx_amd import engine, synth
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module", params=["default", "sync", "walk", "walk4k", "walk1k", "twosweep"])
+@pytest.fixture(scope="module", params=["default", "sync", "walk", "walk4k", "walk1k", "walk8m", "twosweep"])
 def eng(request):
     """every region schedule: default (the walk for long records, else the two-sweep
     schedule), two-sweep = index + head pass + sweep with one host synchronisation;
     sync: the same kernels with the line count read back after the index; walk (no index
     sweep: predicted record ends validated by the sweep; chunks of 128 KiB, 4 KiB and 1 KiB,
-    so lines start in, span and skip over many walkers' chunks)"""
+    so lines start in, span and skip over many walkers' chunks; 8 MiB: short records would
+    overflow a walker's 16-bit line count, so the forced walk takes the two-sweep schedule)"""
     import os
     env = {"VCFXG_AF_FUSED": {"default": "0", "sync": "3", "walk": "7", "walk4k": "7", "walk1k": "7",
-                              "twosweep": "8"}[request.param],
-           "VCFXG_WALK_CHUNK": {"walk4k": "4096", "walk1k": "1024"}.get(request.param, str(128 * 1024))}
+                              "walk8m": "7", "twosweep": "8"}[request.param],
+           "VCFXG_WALK_CHUNK": {"walk4k": "4096", "walk1k": "1024",
+                                "walk8m": str(8 << 20)}.get(request.param, str(128 * 1024))}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:

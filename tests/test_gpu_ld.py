@@ -2,6 +2,7 @@
 256-variant groups, the six masked sums for 128-variant tiles with missing calls) + the exact
 fp64 epilogue against the C oracle's computeRsqFast / computeRsq, streaming and matrix modes,
 both input paths."""
+import os
 import tempfile
 
 import pytest
@@ -10,6 +11,8 @@ from tests._golden import Oracle
 from vcfx_amd import engine, synth, tools
 
 pytestmark = pytest.mark.gpu
+REF_LD_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                         "libref_ld_rsq.so")
 
 
 @pytest.fixture(scope="module")
@@ -108,12 +111,20 @@ def test_ld_r2_values_bitexact(oracle, cfg, knock):
     want_i = np.concatenate([np.arange(j, dtype=np.uint32) for j in range(1, m)])
     want_j = np.concatenate([np.full(j, j, np.uint32) for j in range(1, m)])
     assert (vi == want_i).all() and (vj == want_j).all()
-    rs = oracle.lib.oracle_ld_rsq_fast
     ptr = [x.ctypes.data_as(ctypes.c_void_p) for x in g]
-    want = np.array([rs(ptr[i], ptr[j], ns) for i, j in zip(want_i.tolist(), want_j.tolist())], np.float64)
-    bad = np.flatnonzero(r2.view(np.uint64) != want.view(np.uint64))
-    assert bad.size == 0, [(int(want_i[k]), int(want_j[k]), r2[k], want[k]) for k in bad[:5]]
-    assert (want > 0.0).sum() > np_ // 4  # the values are not all the gate's 0.0
+    # first the reference's own computeRsqFast (its source compiled into oracle/_ref by
+    # oracle/Makefile.ref, shipped with the tree), then the oracle's restatement of it
+    checkers = []
+    if os.path.exists(REF_LD_SO):
+        ref = ctypes.CDLL(REF_LD_SO).ref_rsq_fast
+        ref.argtypes, ref.restype = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_double
+        checkers.append(("reference", ref))
+    checkers.append(("oracle", oracle.lib.oracle_ld_rsq_fast))
+    for name, rs in checkers:
+        want = np.array([rs(ptr[i], ptr[j], ns) for i, j in zip(want_i.tolist(), want_j.tolist())], np.float64)
+        bad = np.flatnonzero(r2.view(np.uint64) != want.view(np.uint64))
+        assert bad.size == 0, (name, [(int(want_i[k]), int(want_j[k]), r2[k], want[k]) for k in bad[:5]])
+        assert (want > 0.0).sum() > np_ // 4  # the values are not all the gate's 0.0
 
 
 def _knock_out(buf, line_no):
@@ -259,3 +270,80 @@ def test_ld_sparse_missing_tiles(oracle, rate, ns):
         old = subprocess.run([tools_binary("VCFX_ld_calculator")] + argv[1:], capture_output=True,
                              env=dict(os.environ, VCFXG_LD_SPARSE="0"), timeout=300)
         assert (old.stdout, old.returncode) == (want[0], 0)
+        # the sparse planes' allocation failing (test hook): the sparse groups go back to the
+        # masked kernel and the call still succeeds with the same bytes
+        nomem = subprocess.run([tools_binary("VCFX_ld_calculator")] + argv[1:], capture_output=True,
+                               env=dict(os.environ, VCFXG_LD_SPARSE_NOMEM="1"), timeout=300)
+        assert (nomem.stdout, nomem.returncode) == (want[0], 0)
+
+
+def _wide_sparse_vcf(m, ns, seed):
+    """m variants x ns samples, dosage 2 (1|1) on ~95 % of the calls (Sxy close to the u16 limit
+    4 ns of the sparse epilogue's packed accumulators at ns = 16383), and exactly 15 missing calls
+    per variant (the most a sparse group allows): on odd variants the first 15 samples where the
+    previous variant's dosage is not 2 (the other variant's informative samples missing), on even
+    ones random samples.  Rows share one carrier pattern, so many pairs sit near every threshold."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    head = (b"##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" +
+            b"\t".join(b"S%d" % i for i in range(ns)) + b"\n")
+    codes = np.frombuffer(b"0|0\t0|1\t1|1\t.|.\t", dtype="<u4")
+    base = rng.random(ns) < 0.05
+    prev = None
+    out = [head]
+    for v in range(m):
+        d = np.full(ns, 2, np.int64)
+        alt = np.where(rng.random(ns) < 0.9, base, rng.random(ns) < 0.05)
+        d[alt] = rng.integers(0, 2, int(alt.sum()))
+        if v % 2 and prev is not None:
+            miss = np.flatnonzero(prev != 2)[:15]
+            if miss.size < 15:
+                miss = np.concatenate([miss, np.setdiff1d(np.arange(ns), miss)[:15 - miss.size]])
+        else:
+            miss = rng.choice(ns, 15, replace=False)
+        d[miss] = 3
+        prev = np.where(d == 3, 2, d)
+        row = bytearray(codes[d].tobytes())
+        row[-1:] = b"\n"
+        out.append(b"1\t%d\trs%d\tA\tG\t.\tPASS\t.\tGT\t" % (1000 + v, v) + bytes(row))
+    return b"".join(out)
+
+
+def test_ld_sparse_at_the_sample_limit(oracle):
+    """the sparse epilogue's fp32 prefilter and its u16 packed sums where they are
+    tightest -- ns = 16,383 (the largest the sparse groups take), 15 missing calls per variant,
+    adversarial patterns (a variant missing the other's informative samples) and Sxy near 2^16 --
+    against the oracle, with the reference's own r^2 doubles on every pair at threshold 0."""
+    import ctypes
+
+    import numpy as np
+    ns, m = 16383, 512
+    buf = _wide_sparse_vcf(m, ns, 71)
+    with tempfile.NamedTemporaryFile(suffix=".vcf") as f:
+        f.write(buf)
+        f.flush()
+        for a in (["-w", "512", "-t", "0.5"], ["-w", "512", "-t", "0.55"], ["-w", "512", "-t", "0.57"],
+                  ["-w", "300", "-t", "0.2"]):
+            argv = ["VCFX_ld_calculator"] + a + ["-i", f.name]
+            got = tools.run(argv, b"")
+            want = oracle.run(argv, b"")
+            assert got == want, (a, len(got[0]), len(want[0]))
+            assert want[0].count(b"\n") > 300, a  # pairs pass: the prefilter decided real cases
+    g = _codes(buf, oracle)
+    e = engine.Engine(0)
+    try:
+        e.load(buf)
+        e.index(engine.data_start_of(buf, strip_cr=False))
+        assert e.ld_prepare(ns) == m
+        np_, _ = e.ld_stream_chunk(0, m, m, 0.0)
+        vi, vj, r2 = e.ld_pairs(0, np_)
+    finally:
+        e.close()
+    rs = oracle.lib.oracle_ld_rsq_fast
+    if os.path.exists(REF_LD_SO):
+        rs = ctypes.CDLL(REF_LD_SO).ref_rsq_fast
+        rs.argtypes, rs.restype = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_double
+    ptr = [x.ctypes.data_as(ctypes.c_void_p) for x in g]
+    want = np.array([rs(ptr[i], ptr[j], ns) for i, j in zip(vi.tolist(), vj.tolist())], np.float64)
+    assert np_ == m * (m - 1) // 2
+    assert (r2.view(np.uint64) == want.view(np.uint64)).all()

@@ -107,6 +107,9 @@ def _check(case, inputs, stdin="none"):
     cmd = _cmd(c["stages"], path)
     stdin_path = None
     first_reads_stdin = not any("{F}" in a for a in c["stages"][0])
+    if stdin == "ngpu8":  # the in-process multi-GPU drop-in: 8 rank contexts on the first stage
+        assert not first_reads_stdin
+        cmd = "VCFX_NGPU=8 " + cmd
     if first_reads_stdin:
         if stdin == "pipe":
             cmd = "cat '%s' | %s" % (path, cmd)   # a pipe: the streaming ingest path
@@ -178,10 +181,11 @@ def test_missing_shard_matches_reference(inputs, case, stdin):
         inputs.drop("chr21_miss")
 
 
-@pytest.mark.parametrize("case,stdin", [("af_file_miss", "none"), ("af_stdin_miss", "pipe"), ("af_stdin_miss", "file")])
+@pytest.mark.parametrize("case,stdin", [("af_file_miss", "none"), ("af_file_miss", "ngpu8"), ("af_stdin_miss", "pipe"),
+                                        ("af_stdin_miss", "file")])
 def test_af_missing_shard_matches_reference(inputs, case, stdin):
     """AF where ~70 % of the records carry a missing call ('.|.'): the walk's fixed-stride
-    sweep with missing alleles at BASELINE scale"""
+    sweep with missing alleles at BASELINE scale (also as 8 ranks, VCFX_NGPU=8)"""
     _check(case, inputs, stdin)
 
 
@@ -192,10 +196,10 @@ def test_af_irregular_shard_matches_reference(inputs):
     inputs.drop("chr21_irreg")
 
 
-@pytest.mark.parametrize("case,stdin", [("af_file_gtadp", "none"), ("af_stdin_gtadp", "file")])
+@pytest.mark.parametrize("case,stdin", [("af_file_gtadp", "none"), ("af_file_gtadp", "ngpu8"), ("af_stdin_gtadp", "file")])
 def test_af_gtadp_shard_matches_reference(inputs, case, stdin):
-    """AF on the 13.2 GB shard with every record GT:AD:DP (the general GT path: index sweep +
-    gt_first) at BASELINE scale"""
+    """AF on the 13.2 GB shard with every record GT:AD:DP (the general GT path: the GT-first
+    walk) at BASELINE scale (also as 8 ranks, VCFX_NGPU=8)"""
     _check(case, inputs, stdin)
     if stdin == "file":
         inputs.drop("chr21_gtadp")
@@ -228,6 +232,51 @@ def test_bgzf_chr21_matches_reference(inputs, case):
                                   "ld20k_bench", "ld20k_miss_bench"])
 def test_ld_matches_reference(inputs, case):
     _check(case, inputs)
+
+
+@pytest.mark.parametrize("case,prefix", [("ld100k_tail_bench", "ld20k_bench"),
+                                         ("ld100k_miss_tail_bench", "ld20k_miss_bench")])
+def test_ngpu8_ld_at_full_size(case, prefix):
+    """Config 5 at 8 ranks (VCFX_NGPU=8: eight rank contexts, each parsing the 100 K shard and
+    writing the pair lines of its --shard r/8 share -- equal window-pair counts, row cuts at
+    j_k ~ M sqrt(k/8) -- rank 0's stdout first, the others' after it in rank order) on the whole
+    100 K x 2,504 bench shard, complete and with 0.1 % missing calls: its first 20 K variants'
+    lines against the reference's output on those variants, and its lines with VAR1 >= 80,000
+    against the reference's output on that slice (the same digests the one-rank run is held to)"""
+    for k in (case, prefix):
+        if k not in DIG["cases"]:
+            pytest.skip("no reference digest for %s" % k)
+    c, cp = DIG["cases"][case], DIG["cases"][prefix]
+    params = dict(DIG["inputs"][c["input"]])
+    lo, hi = params.pop("slice")
+    pin = dict(DIG["inputs"][cp["input"]])
+    assert pin.pop("n_records") <= lo and pin == {k: v for k, v in params.items() if k != "n_records"}
+    assert c["stages"] == cp["stages"]
+    arr, offs = synth.generate_array(rec_offsets=True, **params)
+    pos0 = int(bytes(arr[int(offs[lo]):int(offs[lo]) + 64]).split(b"\t")[1])
+    d = tempfile.mkdtemp(prefix="vcfx_ld8_")
+    path = os.path.join(d, "ld100k.vcf")
+    try:
+        arr.tofile(path)
+        del arr, offs
+        argv = [tool_binary("VCFX_ld_calculator")] + [a.replace("{F}", path) for a in c["stages"][0][1:]]
+        r = subprocess.run(argv, capture_output=True, timeout=600, env=dict(os.environ, VCFX_NGPU="8"))
+        assert r.returncode == 0, r.stderr[-2000:]
+        out = r.stdout
+        n = cp["stdout"]["len"]
+        got = {"sha256": hashlib.sha256(out[:n]).hexdigest(), "len": n, "lines": out[:n].count(b"\n")}
+        assert got == cp["stdout"], (prefix, got, cp["stdout"])
+        head = out[:out.index(b"\n") + 1]
+        tail = head
+        for ln in out[len(head):].split(b"\n"):
+            if ln and int(ln.split(b"\t", 2)[1]) >= pos0:
+                tail += ln + b"\n"
+        got = {"sha256": hashlib.sha256(tail).hexdigest(), "len": len(tail), "lines": tail.count(b"\n")}
+        assert got == c["stdout"], (case, got, c["stdout"])
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+        os.rmdir(d)
 
 
 @pytest.mark.parametrize("case", ["ld100k_tail_bench", "ld100k_miss_tail_bench"])

@@ -156,3 +156,39 @@ def test_af_tie_modes_differ(oracle):
     out_s, _, _ = oracle.run(["VCFX_allele_freq_calc"], data)
     out_m, _, _ = oracle.run(["VCFX_allele_freq_calc", "-q", "-i", "data/ties.vcf"], b"", cwd=GOLDEN)
     assert out_s.splitlines()[1].endswith(b"0.0312") and out_m.splitlines()[1].endswith(b"0.0313")
+
+
+REF_LD_SO = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref",
+                         "libref_ld_rsq.so")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_LD_SO), reason="oracle/_ref not built (no /root/reference here)")
+def test_oracle_rsq_equals_reference_doubles(oracle):
+    """The oracle's computeRsqFast restatement against the reference's own function (its source
+    compiled into oracle/_ref/libref_ld_rsq.so by oracle/Makefile.ref), bit for bit on the fp64
+    value: random dosage vectors with missing calls, monomorphic and all-missing vectors, rare
+    variants and the sample counts the GPU tests use."""
+    import ctypes
+
+    import numpy as np
+    ref = ctypes.CDLL(REF_LD_SO).ref_rsq_fast
+    ref.argtypes, ref.restype = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t], ctypes.c_double
+    mine = oracle.lib.oracle_ld_rsq_fast
+    rng = np.random.default_rng(5)
+    checked = nonzero = 0
+    for ns in (1, 2, 3, 17, 33, 300, 2504, 16383):
+        for _ in range(40 if ns < 5000 else 6):
+            p = rng.uniform(0.0, 0.6, 2)
+            miss = rng.choice([0.0, 0.001, 0.05, 0.5, 1.0], p=[0.4, 0.25, 0.2, 0.1, 0.05])
+            base = rng.binomial(2, p[0], ns)
+            g = []
+            for k in range(2):
+                x = np.where(rng.random(ns) < rng.uniform(0, 1), base, rng.binomial(2, p[k], ns)).astype(np.int8)
+                x[rng.random(ns) < miss] = -1
+                g.append(np.ascontiguousarray(x))
+            a, b = (x.ctypes.data_as(ctypes.c_void_p) for x in g)
+            want, got = ref(a, b, ns), mine(a, b, ns)
+            assert np.float64(want).view(np.uint64) == np.float64(got).view(np.uint64), (ns, want, got)
+            checked += 1
+            nonzero += want > 0
+    assert checked > 250 and nonzero > 100

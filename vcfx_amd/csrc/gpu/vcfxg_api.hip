@@ -809,9 +809,11 @@ static int af_region_walk(vcfxg_ctx *c, size_t data_start, int mode, vcfxg_summa
         return r ? r : vcfxg_allele_freq(c, mode, out);
     }
     const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
-    if (cap_w > 0xFFFF) {  // (wgt packs the GT-line count in 16 bits; see walk_chunk)
-        c->err = "af walk: walker line capacity over 65535";
-        return VCFXG_E_ARG;
+    if (cap_w > 0xFFFF) {
+        // (wgt packs the GT-line count in 16 bits: short records in a large VCFXG_WALK_CHUNK, or a
+        // forced walk on them) the two-sweep schedule, as after a walk that ran out of line slots
+        c->walk_overflowed = true;
+        return note_schedule(c, "af_two_sweep"), af_region_async(c, data_start, mode, out);
     }
     const uint64_t cap = (uint64_t)nw * cap_w;
     int r = ensure(c, c->wk_le, 8 * cap);
@@ -1584,9 +1586,10 @@ static int dose_walk_index(vcfxg_ctx *c, size_t data_start, int mode, uint64_t *
     const int64_t C = c->walk_chunk;
     const int64_t nw = vcfxg::af_walkers(lo, hi, C);
     const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
-    if (cap_w > 0xFFFF) {  // (wgt packs the GT-line count in 16 bits; see walk_chunk)
-        c->err = "af walk: walker line capacity over 65535";
-        return VCFXG_E_ARG;
+    if (cap_w > 0xFFFF) {  // (the walk's 16-bit GT-line count): the caller's index path
+        c->walk_overflowed = true;
+        *overflow = true;
+        return VCFXG_OK;
     }
     const uint64_t cap = (uint64_t)nw * cap_w;
     int r = ensure(c, c->wk_le, 8 * cap);
@@ -2201,12 +2204,40 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
         c->ld_vq = c->ld_vq || c->ld_gflag_host[g] == 0;
         c->ld_sp = c->ld_sp || c->ld_gflag_host[g] == 2;
     }
+    // the sparse-missing kernel's extra planes (CSR + the [sample][variant] u16 plane, about twice
+    // the int8 plane) must not make an input fail that the masked kernel alone fits: when they do
+    // not fit, every sparse group goes back to k_ld_mask (VCFXG_LD_SPARSE_NOMEM=1: a test hook
+    // that takes this way as if the allocation had failed)
+    static const bool sparse_nomem_hook = [] {
+        const char *e = getenv("VCFXG_LD_SPARSE_NOMEM");
+        return e && e[0] == '1';
+    }();
+    auto sparse_to_mask = [&]() -> int {
+        (void)hipGetLastError();  // (a failed hipMalloc leaves its error to be read once)
+        prof_end(c, "ld_sparse_prep");
+        c->ld_sp = false;
+        c->ld_vq = true;
+        for (auto &f : c->ld_gflag_host)
+            if (f == 2) f = 0;
+        if (M)
+            HIPCHK(c, hipMemcpyAsync(c->ld_gflag.p, c->ld_gflag_host.data(),
+                                     (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock, hipMemcpyHostToDevice, c->stream));
+        c->err.clear();
+        return VCFXG_OK;
+    };
+    if (c->ld_sp && sparse_nomem_hook) {
+        r = sparse_to_mask();
+        if (r) return r;
+    }
     if (c->ld_sp) {
         // the missing samples of every variant (CSR) and the contribution plane of the
         // sparse-missing kernel (vcfxg_ld_fast.hip, kSp)
         prof_begin(c, "ld_sparse_prep");
         r = ensure(c, c->ld_moff, 8 * (M + 1));
+        if (r == VCFXG_E_NOMEM) r = sparse_to_mask();
         if (r) return r;
+    }
+    if (c->ld_sp) {
         struct MissOf {
             int ns;
             __host__ __device__ uint64_t operator()(const vcfxg::LdVar &v) const { return (uint64_t)(ns - v.cnt); }
@@ -2232,7 +2263,11 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
         r = ensure(c, c->ld_midx, 2 * entries + 16);
         if (!r) r = ensure(c, c->ld_mvar, 4 * entries + 16);
         if (!r) r = ensure(c, c->ld_gt16, 2 * (size_t)n_samples * mp + 64);
+        if (r == VCFXG_E_NOMEM) r = sparse_to_mask();
         if (r) return r;
+    }
+    if (c->ld_sp) {
+        const uint64_t mp = (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock * vcfxg::kLdFastBlock;
         HIPCHK(c, vcfxg::launch_ld_miss_fill(P<int8_t>(c->ld_Gc), M, kpad, n_samples, P<uint64_t>(c->ld_moff),
                                              P<uint16_t>(c->ld_midx), P<uint32_t>(c->ld_mvar), c->stream));
         HIPCHK(c, vcfxg::launch_ld_gt16(P<int8_t>(c->ld_Gc), M, kpad, n_samples, mp, P<uint16_t>(c->ld_gt16),

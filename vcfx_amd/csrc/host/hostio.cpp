@@ -206,6 +206,7 @@ struct FileRing {
     vcfxg_ctx *ctx = nullptr;
     size_t slot = 0;
     std::vector<void *> slots;
+    bool busy = false;  // a caller is reading into / copying out of the slots (under g_ring_mu)
 };
 std::mutex g_ring_mu;
 FileRing g_file_ring;
@@ -276,6 +277,11 @@ bool Input::open_file_device(const char *path) {
     std::vector<void *> ring_;
     {
         std::lock_guard<std::mutex> lk(g_ring_mu);
+        if (g_file_ring.busy) {  // another caller holds the slots: this one maps the file
+            munmap(hm, kHeadMax);
+            ::close(fd);
+            return open_file(path);
+        }
         if (g_file_ring.ctx != g || g_file_ring.slot != kSlot || g_file_ring.slots.size() != file_slots()) {
             if (g_file_ring.ctx)
                 for (void *r : g_file_ring.slots) vcfxg_host_free(g_file_ring.ctx, r);
@@ -295,7 +301,16 @@ bool Input::open_file_device(const char *path) {
             }
         }
         ring_ = g_file_ring.slots;
+        g_file_ring.busy = !ring_.empty();
     }
+    struct RingRelease {  // the slots are free again once every DMA from them has finished
+        bool on;
+        ~RingRelease() {
+            if (!on) return;
+            std::lock_guard<std::mutex> lk(g_ring_mu);
+            g_file_ring.busy = false;
+        }
+    } ring_release{!ring_.empty()};
     if (ring_.empty() || vcfxg_ingest_begin(g, total) != VCFXG_OK || vcfxg_ingest(g, head, hn, 0) != VCFXG_OK) {
         munmap(hm, kHeadMax);
         ::close(fd);
@@ -367,8 +382,9 @@ bool Input::open_file_device(const char *path) {
     }
     for (auto &t : readers) t.join();
     ::close(fd);
-    // every DMA from the ring finished before the slots are reused (the next call's readers)
-    if (ok && vcfxg_ingest_wait(g, total) != VCFXG_OK) ok = false;
+    // every DMA from the ring finished before the slots are reused (the next call's readers),
+    // on the failure path too (the chunks queued before it may still be reading their slots)
+    if (vcfxg_ingest_wait(g, ok ? total : ~(size_t)0) != VCFXG_OK) ok = false;
     if (rerr) read_errno = rerr;
     phase("file streamed to the device");
     p = head;
@@ -824,12 +840,21 @@ bool write_device_text(vcfxg_ctx *g, uint64_t bytes, Out &out, int err_fd) {
     size_t slot = 0;
     {
         std::lock_guard<std::mutex> lk(g_ring_mu);
-        if (g_file_ring.ctx == g) {
+        if (g_file_ring.ctx == g && !g_file_ring.busy) {
             slots = g_file_ring.slots;
             slot = g_file_ring.slot;
+            g_file_ring.busy = !slots.empty();
         }
     }
-    if (slots.empty()) {  // no pinned ring on this context: one pageable copy
+    struct RingRelease {
+        bool on;
+        ~RingRelease() {
+            if (!on) return;
+            std::lock_guard<std::mutex> lk(g_ring_mu);
+            g_file_ring.busy = false;
+        }
+    } ring_release{!slots.empty()};
+    if (slots.empty()) {  // no pinned ring on this context (or it is in use): one pageable copy
         std::string text(bytes, '\0');
         if (!gpu_ok(g, vcfxg_fetch_text(g, &text[0], text.size()), "fetch", err_fd)) return false;
         write_all(out.fd, text.data(), text.size());
@@ -848,6 +873,10 @@ bool write_device_text(vcfxg_ctx *g, uint64_t bytes, Out &out, int err_fd) {
 
 bool load_input(vcfxg_ctx *g, const Input &in, int err_fd) {
     in.join_populate();
+    if (in.read_errno) {  // a read(2) error is not the end of the input (nor is a full reservation)
+        write_str(err_fd, std::string("Error: vcfx_amd: reading the input failed: ") + strerror(in.read_errno) + "\n");
+        return false;
+    }
     phase("page population joined");
     if (in.tail) {  // a shard view: header + record range, straight from the mapping
         int rc = vcfxg_ingest_begin(g, in.n);
