@@ -8,7 +8,7 @@ ARCH ?= gfx950
 B := build
 GPU_SRC := vcfx_amd/csrc/gpu
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Iinclude -I$(GPU_SRC) $(EXTRA_HIPFLAGS)
-GPU_OBJS := $(B)/obj/vcfxg_kernels.o $(B)/obj/vcfxg_rf.o $(B)/obj/vcfxg_ld.o $(B)/obj/vcfxg_ld_fast.o $(B)/obj/vcfxg_ld_mask.o $(B)/obj/vcfxg_af_walk.o $(B)/obj/vcfxg_fq_walk.o $(B)/obj/vcfxg_hwe.o $(B)/obj/vcfxg_dose.o $(B)/obj/vcfxg_md.o $(B)/obj/vcfxg_ac.o $(B)/obj/vcfxg_ph.o $(B)/obj/vcfxg_api.o $(B)/obj/vcfxg_decimal.o
+GPU_OBJS := $(B)/obj/vcfxg_kernels.o $(B)/obj/vcfxg_rf.o $(B)/obj/vcfxg_ld.o $(B)/obj/vcfxg_ld_fast.o $(B)/obj/vcfxg_ld_mask.o $(B)/obj/vcfxg_af_walk.o $(B)/obj/vcfxg_fq_walk.o $(B)/obj/vcfxg_hwe.o $(B)/obj/vcfxg_dose.o $(B)/obj/vcfxg_md.o $(B)/obj/vcfxg_ac.o $(B)/obj/vcfxg_ph.o $(B)/obj/vcfxg_inflate.o $(B)/obj/vcfxg_api.o $(B)/obj/vcfxg_decimal.o
 
 TOOLS := VCFX_allele_freq_calc VCFX_genotype_query VCFX_record_filter VCFX_variant_counter VCFX_ld_calculator \
          VCFX_nonref_filter VCFX_hwe_tester VCFX_dosage_calculator VCFX_missing_detector VCFX_allele_counter \

@@ -443,20 +443,45 @@ def e2e_rates(workload, arr, a, offs=None):
             os.close(dn)
         runs["warm_context_file"] = {"value": a.records / min(walls[1:]), "wall_s": [round(w, 4) for w in walls[1:]],
                                      "note": "in-process vcfx_tool_main with the device context already open"}
-        # the BGZF (.vcf.gz) form of the same file: inflated on the host threads, then the device path
+        # the BGZF (.vcf.gz) form of the same file: the compressed bytes cross PCIe and every member
+        # is inflated on the device (vcfxg_ingest_bgzf); the host-inflate path beside it
+        # (VCFX_BGZF_DEVICE=0: members inflated on <= 16 host threads, the text crosses PCIe)
         bgz = path + ".bgz"
         subprocess.check_call([os.path.join(REPO, "build", "bin", "vcfx_bgzf"), path, bgz, "16", "1"])
         try:
+            import hashlib
+            plain_sha = hashlib.sha256(subprocess.run([exe] + args + ["-i", path], capture_output=True,
+                                                      timeout=300).stdout).hexdigest()
+            for name, env in (("process_file_bgzf", {}), ("process_file_bgzf_host_inflate", {"VCFX_BGZF_DEVICE": "0"})):
+                walls = []
+                for _ in range(3):
+                    t0 = time.perf_counter()
+                    r = subprocess.run([exe] + args + ["-i", bgz], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                       timeout=300, env=dict(os.environ, **env))
+                    walls.append(time.perf_counter() - t0)
+                    assert r.returncode == 0, r.stderr[-500:]
+                out = subprocess.run([exe] + args + ["-i", bgz], capture_output=True, timeout=300,
+                                     env=dict(os.environ, **env)).stdout
+                runs[name] = {"value": a.records / min(walls), "wall_s": [round(w, 4) for w in walls],
+                              "compressed_bytes": os.path.getsize(bgz),
+                              "stdout_equals_plain_input": hashlib.sha256(out).hexdigest() == plain_sha,
+                              "note": "BGZF level 1 (build/bin/vcfx_bgzf); " + (
+                                  "members inflated on the host (<= 16 threads)" if env else
+                                  "members inflated on the device (vcfxg_ingest_bgzf)")}
+            argv = [tool] + args + ["-i", bgz]
+            carr = (ctypes.c_char_p * (len(argv) + 1))(*[x.encode() for x in argv], None)
+            dn = os.open(os.devnull, os.O_RDWR)
             walls = []
-            for _ in range(3):
-                t0 = time.perf_counter()
-                r = subprocess.run([exe] + args + ["-i", bgz], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                                   timeout=300)
-                walls.append(time.perf_counter() - t0)
-                assert r.returncode == 0, r.stderr[-500:]
-            runs["process_file_bgzf"] = {"value": a.records / min(walls), "wall_s": [round(w, 4) for w in walls],
-                                         "compressed_bytes": os.path.getsize(bgz),
-                                         "note": "BGZF level 1 (build/bin/vcfx_bgzf); inflate on <= 16 host threads"}
+            try:
+                for _ in range(4):
+                    t0 = time.perf_counter()
+                    rc = L.vcfx_tool_main(tool.encode(), len(argv), carr, dn, dn, dn)
+                    walls.append(time.perf_counter() - t0)
+                    assert rc == 0, rc
+            finally:
+                os.close(dn)
+            runs["warm_context_bgzf"] = {"value": a.records / min(walls[1:]), "wall_s": [round(w, 4) for w in walls[1:]],
+                                         "note": "in-process vcfx_tool_main on the BGZF file, device context open"}
         finally:
             os.unlink(bgz)
         # per-invocation start-up: the drop-in process on a small input (the first 100 records),
@@ -486,7 +511,10 @@ def e2e_rates(workload, arr, a, offs=None):
         # four 32 MiB buffers -- the staging ring's cache footprint), best of 3
         drain = os.path.join(REPO, "build", "bin", "vcfx_drain")
         if os.access(drain, os.X_OK):
-            for name, extra in (("pipe_ceiling", ""), ("pipe_ceiling_ring4x32M", " 33554432 4")):
+            # (the first: the pipe ring's own shape, 16 x 1 MiB buffers that stay in the host's
+            # caches; the ceiling is the best of the three)
+            for name, extra in (("pipe_ceiling_ring16x1M", " 1048576 16"), ("pipe_ceiling_32M", ""),
+                                ("pipe_ceiling_ring4x32M", " 33554432 4")):
                 walls = []
                 for _ in range(3):
                     t0 = time.perf_counter()
@@ -494,6 +522,7 @@ def e2e_rates(workload, arr, a, offs=None):
                                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=300, check=True)
                     walls.append(time.perf_counter() - t0)
                 runs[name] = {"value": a.records / min(walls), "wall_s": [round(w, 4) for w in walls]}
+            runs["pipe_ceiling"] = max((runs[k] for k in runs if k.startswith("pipe_ceiling_")), key=lambda r: r["value"])
             runs["process_stdin_pipe"]["frac_of_pipe_ceiling"] = round(
                 runs["process_stdin_pipe"]["value"] / runs["pipe_ceiling"]["value"], 3)
         runs["pcie_ceiling"] = a.records / (arr.size / (PCIE_H2D_GBS * 1e9))

@@ -14,6 +14,11 @@
 #   bash gpu_job.sh mfma NAME [bench args...]    one MFMA-utilisation pass
 #   bash gpu_job.sh rehearse                     bench.py --gpus 2 over gloo (both ranks on this GPU)
 #   bash gpu_job.sh run NAME SECS CMD...         any command as a timed step
+#   bash gpu_job.sh final                        validation: whole -m gpu suite, smoke, AF bench line,
+#                                                its kernel trace and PMC passes
+#   bash gpu_job.sh workloads                    one bench line per workload (configs 3 and 5 and the
+#                                                8(f) tools, LD with missing calls, GT:AD:DP AF)
+#   bash gpu_job.sh bgzf [NAME]                  device BGZF inflate at full size (tools/bgzf_probe.py)
 #
 # bench args default to the AF workload (config 2); e.g. `bench ld --workload ld`.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")}" || exit 1
@@ -90,6 +95,22 @@ rehearse)
 run)
     n=$1 secs=$2; shift 2
     step "$n" "$secs" "$@" ;;
+final)
+    bash "$0" test || exit $?
+    cp gpurun_out/pytest_gpu.log gpurun_out/pytest_gpu_full.log
+    bash "$0" smoke || exit $?
+    bash "$0" bench af || exit $?
+    bash "$0" prof af || exit $?
+    bash "$0" pmc af || exit $? ;;
+workloads)
+    for w in pipeline nonref hwe dose ac md ph ld; do
+        bash "$0" bench $w --workload $w --no-e2e || exit $?
+    done
+    bash "$0" bench ldmiss --workload ld --missing-rate 0.001 --no-e2e || exit $?
+    bash "$0" bench gtadp --format gt:ad:dp --no-e2e || exit $? ;;
+bgzf)
+    n=${1:-probe}
+    step bgzf_$n 400 python -u tools/bgzf_probe.py --out gpurun_out/bgzf_$n.json || exit $? ;;
 *)
     echo "unknown mode $MODE"; exit 2 ;;
 esac

@@ -30,7 +30,8 @@ enum vcfxg_status {
     VCFXG_E_ARG = -3,     /* bad argument */
     VCFXG_E_NOMEM = -4,   /* device or host allocation failed */
     VCFXG_E_STATE = -5,   /* call out of order (e.g. no input loaded / not indexed) */
-    VCFXG_E_CAP = -6      /* caller buffer too small */
+    VCFXG_E_CAP = -6,     /* caller buffer too small */
+    VCFXG_E_DATA = -7     /* the input data is invalid (a BGZF member that does not inflate as zlib would) */
 };
 
 /* input semantics of the reference tools: file = the mmap path, stdin = the getline path */
@@ -92,6 +93,25 @@ int vcfxg_ingest(vcfxg_ctx *ctx, const char *host, size_t n, int is_final_chunk)
 /* wait until the copies of the ingested bytes [0, upto) have completed (their host buffers
  * may then be reused: a pinned staging ring) */
 int vcfxg_ingest_wait(vcfxg_ctx *ctx, size_t upto);
+/* BGZF (.vcf.gz) input inflated on the device (the reference reads it through zlib,
+ * StreamingGzipReader, src/vcfx_core.cpp:144-354, members inflated in sequence with inflateReset
+ * at each, :270-277).  Appends the inflated bytes of n_members consecutive BGZF members to the
+ * input being ingested: comp[0, comp_n) holds them (host memory), member i = the gzip member at
+ * comp[src_off, src_off + src_len) (BSIZE + 1 bytes; the caller has checked its header: gzip magic,
+ * CM 8, FLG exactly FEXTRA, the 'BC' subfield) whose trailer's ISIZE is out_len (<= 65536).  The
+ * compressed bytes are copied to the device and each member is inflated by one wave, its CRC-32
+ * checked against the trailer.  head[0, head_n): the first inflated bytes as the caller has them on
+ * the host (the load-time hints are taken from them; may be NULL).  A member whose deflate stream
+ * zlib would refuse, that does not end at its trailer, or whose size or CRC-32 differs, fails the
+ * call with VCFXG_E_DATA (*bad_member = the first such member) and the ingest is abandoned: the
+ * caller then inflates on the host, where zlib reports the damage as the reference does. */
+typedef struct {
+    uint64_t src_off;  /* the member's first byte in comp */
+    uint32_t src_len;  /* the member's bytes (BSIZE + 1) */
+    uint32_t out_len;  /* its ISIZE */
+} vcfxg_bgzf_member;
+int vcfxg_ingest_bgzf(vcfxg_ctx *ctx, const void *comp, size_t comp_n, const vcfxg_bgzf_member *members,
+                      size_t n_members, const char *head, size_t head_n, uint64_t *bad_member);
 /* page-locked host memory (H2D at the full PCIe rate, asynchronous), for staging rings */
 int vcfxg_host_alloc(vcfxg_ctx *ctx, size_t n, void **out);
 void vcfxg_host_free(vcfxg_ctx *ctx, void *p);

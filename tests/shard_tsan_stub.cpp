@@ -66,6 +66,11 @@ int vcfxg_ingest(vcfxg_ctx *c, const char *host, size_t n, int is_final_chunk) {
 }
 
 int vcfxg_ingest_wait(vcfxg_ctx *, size_t) { return VCFXG_OK; }
+// (no device inflate in the stand-in: the runner's gzip inputs are unsharded anyway)
+int vcfxg_ingest_bgzf(vcfxg_ctx *, const void *, size_t, const vcfxg_bgzf_member *, size_t, const char *, size_t,
+                      uint64_t *) {
+    return VCFXG_E_STATE;
+}
 
 int vcfxg_load_host(vcfxg_ctx *c, const char *host, size_t n) {
     vcfxg_ingest_begin(c, n);

@@ -152,6 +152,9 @@ struct vcfxg_ctx {
     bool ld_sp = false;
     uint64_t ld_mp = 0;
     DevBuf ld_moff, ld_midx, ld_mvar, ld_gt16;
+    // device BGZF inflate (vcfxg_ingest_bgzf): compressed bytes, member table, output offsets,
+    // per-member status, first bad member
+    DevBuf bgz_in, bgz_mem, bgz_off, bgz_stat, bgz_small;
     void *ld_plan_dev = nullptr;
     uint64_t text_bytes = 0;
     uint64_t text_hint = 0;  // AF walk: text bytes of the previous call (the next call's capacity)
@@ -318,7 +321,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16, &c->bgz_in, &c->bgz_mem, &c->bgz_off, &c->bgz_stat, &c->bgz_small})
         if (b->p) (void)hipFree(b->p);
     if (c->af_small.p) (void)hipFree(c->af_small.p);
     if (c->wk_stage.p) (void)hipFree(c->wk_stage.p);
@@ -516,6 +519,89 @@ int vcfxg_ingest(vcfxg_ctx *c, const char *host, size_t n, int is_final_chunk) {
     c->ingesting = false;
     c->loaded = true;
     c->indexed = false;
+    return VCFXG_OK;
+}
+
+static_assert(sizeof(vcfxg_bgzf_member) == sizeof(vcfxg::BgzfMember), "BGZF member layout");
+
+int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg_bgzf_member *mem, size_t nm,
+                      const char *head, size_t head_n, uint64_t *bad_member) {
+    if (!c || (!comp && comp_n) || (!mem && nm) || (!head && head_n)) return VCFXG_E_ARG;
+    if (!c->ingesting) return VCFXG_E_STATE;
+    if (bad_member) *bad_member = ~0ull;
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<uint64_t> off(nm + 1);
+    uint64_t tot = 0;
+    for (size_t i = 0; i < nm; i++) {
+        // (the kernel reads the header's XLEN and the trailer inside the member)
+        if (mem[i].src_off > comp_n || mem[i].src_len > comp_n - mem[i].src_off || mem[i].src_len < 20 ||
+            mem[i].out_len > 65536) {
+            c->err = "vcfxg_ingest_bgzf: member " + std::to_string(i) + " out of range";
+            return VCFXG_E_ARG;
+        }
+        off[i] = tot;
+        tot += mem[i].out_len;
+    }
+    off[nm] = tot;
+    if (c->n + tot + kPad > c->input.cap) {  // grow as vcfxg_ingest does
+        size_t ncap = std::max(c->input.cap * 2, c->n + tot + kPad);
+        void *np = nullptr;
+        HIPCHK(c, hipMalloc(&np, ncap));
+        if (c->n) HIPCHK(c, hipMemcpyAsync(np, c->input.p, c->n, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, hipFree(c->input.p));
+        c->input.p = np;
+        c->input.cap = ncap;
+    }
+    constexpr size_t kCompPad = 8192;  // the inflate reader's ring loads run up to 3 KiB past a stream
+    int r = ensure(c, c->bgz_in, comp_n + kCompPad);
+    if (!r) r = ensure(c, c->bgz_mem, sizeof(vcfxg_bgzf_member) * (nm + 1));
+    if (!r) r = ensure(c, c->bgz_off, 8 * (nm + 1));
+    if (!r) r = ensure(c, c->bgz_stat, 4 * (nm + 1));
+    if (!r) r = ensure(c, c->bgz_small, 64);
+    if (r) return r;
+    static vcfxg::Crc1k z1k = [] {
+        vcfxg::Crc1k z;
+        vcfxg::crc32_zero1k_basis(&z);
+        return z;
+    }();
+    prof_begin(c, "bgzf_h2d");
+    if (comp_n) HIPCHK(c, hipMemcpyAsync(c->bgz_in.p, comp, comp_n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_in) + comp_n, 0, kCompPad, c->stream));
+    if (nm) {
+        HIPCHK(c, hipMemcpyAsync(c->bgz_mem.p, mem, sizeof(vcfxg_bgzf_member) * nm, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->bgz_off.p, off.data(), 8 * nm, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
+    prof_end(c, "bgzf_h2d");
+    for (int which = 0; which < 2; which++) {  // k_inflate, then k_crc32
+        const char *nm_k = which ? "bgzf_crc32" : "bgzf_inflate";
+        prof_begin(c, nm_k);
+        HIPCHK(c, vcfxg::launch_inflate(which, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem),
+                                        P<uint64_t>(c->bgz_off), nm, P<uint8_t>(c->input) + c->n,
+                                        P<uint32_t>(c->bgz_stat), P<unsigned long long>(c->bgz_small), z1k, c->stream));
+        prof_end(c, nm_k);
+    }
+    static thread_local uint64_t bad;
+    static thread_local uint8_t lastb;
+    HIPCHK(c, hipMemcpyAsync(&bad, c->bgz_small.p, 8, hipMemcpyDeviceToHost, c->stream));
+    if (tot) HIPCHK(c, hipMemcpyAsync(&lastb, P<uint8_t>(c->input) + c->n + tot - 1, 1, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    prof_collect(c);
+    if (bad != ~0ull) {
+        uint32_t why = 0;
+        (void)hipMemcpy(&why, P<uint32_t>(c->bgz_stat) + bad, 4, hipMemcpyDeviceToHost);
+        if (bad_member) *bad_member = bad;
+        c->err = "BGZF member " + std::to_string(bad) + " does not inflate (check " + std::to_string(why) + ")";
+        c->ingesting = false;
+        c->loaded = false;
+        c->n = 0;
+        return VCFXG_E_DATA;
+    }
+    if (head_n && c->hints_pending) c->hints_pending = !load_hints(c, head, head_n);
+    note_schedule(c, "bgzf_inflate");
+    c->n += tot;
+    if (tot) c->last_byte = lastb;
     return VCFXG_OK;
 }
 

@@ -1,0 +1,687 @@
+// vcfxg_inflate.hip -- BGZF members inflated on the device (the GPU form).
+//
+// The reference reads .vcf.gz through zlib (StreamingGzipReader, src/vcfx_core.cpp:144-354: one
+// inflate stream, inflateReset at each gzip member).  A BGZF file is a chain of independent gzip
+// members of <= 64 KiB output each, whose sizes are in their headers (BSIZE) and trailers (ISIZE),
+// so the host knows every member's input span and output offset before a byte is inflated: one
+// wave per member inflates it straight into the device input buffer, and the record kernels then
+// run on it unchanged.  The compressed file crosses PCIe instead of the text (17x less on the
+// bench shard).
+//
+// k_inflate (one 64-lane wave per member; the DEFLATE decode of RFC 1951 is serial per stream, so
+// the wave's scalar path decodes and its lanes do the parallel parts):
+//   - the compressed bytes stream through a 4 KiB LDS ring (1 KiB coalesced refills) into a 64-bit
+//     bit buffer;
+//   - each block's Huffman codes (fixed, or the dynamic header's) are built by the whole wave:
+//     per-length counts and each symbol's canonical rank from ballots, then lookup tables of 2^10
+//     (literal/length), 2^9 (distance) and 2^7 (code-length code) entries filled by all lanes,
+//     each entry decoded canonically; the rare longer codes take a per-length canonical walk;
+//   - literals go to a 32 KiB LDS window (deflate's largest distance), a match is copied by the
+//     64 lanes at once (distance < 64: the period-d pattern, out[p + i] = out[p - d + i mod d]);
+//   - the window is written to HBM in aligned 16 B blocks as it fills (byte stores only at the
+//     member's two ends, which neighbouring members share).
+// Every condition under which zlib's inflate fails (zlib inflate.c / inftrees.c: invalid block
+// type, stored LEN != ~NLEN, more than 286 / 30 symbols, an over-subscribed or incomplete code --
+// incomplete only allowed for a single code of length 1, and never for the code-length code --,
+// a bit-length repeat with nothing before it or past the end, no end-of-block code, literal /
+// length symbols 286-287 and distance symbols 30-31, a distance past the member's start) marks the
+// member bad; so does a stream that does not end exactly before the member's 8-byte trailer or
+// whose output is not ISIZE bytes.  k_crc32 then checks each member's CRC-32 against its trailer
+// (zlib's gzip check).  A bad member makes the whole ingest fail and the caller inflates on the
+// host, which reproduces the reference's behaviour on a damaged stream.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "vcfxg_kernels.h"
+
+namespace vcfxg {
+namespace {
+
+// the LDS output window: the last 8 KiB (deflate reaches back 32 KiB: a match from further back
+// than kFar reads the member's own output, already written to HBM, instead)
+constexpr uint32_t kWin = 1u << 13, kWinMask = kWin - 1;
+constexpr uint32_t kFar = 4096;
+constexpr int kLB = 10, kDB = 9, kCB = 7;                 // lookup-table bits: lit/len, dist, code lengths
+constexpr uint32_t kFlushStep = 1024;                     // HBM writes in 1 KiB-aligned steps
+
+// table entries: bits 0-15 value (literal, length base, distance base, code-length symbol), 16-19 code
+// length, 20-23 extra bits; flags
+constexpr uint32_t kLit = 1u << 24, kEob = 1u << 25, kBad = 1u << 26, kSlow = 1u << 27;
+
+// RFC 1951 §3.2.5: length codes 257..285 and distance codes 0..29 (base, extra bits)
+__constant__ uint16_t c_lbase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                     31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t c_lext[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t c_dbase[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
+                                     193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dext[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+// the order of the code-length code's lengths in a dynamic block header (RFC 1951 §3.2.7)
+__constant__ uint8_t c_clorder[19] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// three codes per block: 0 literal/length (288 symbols), 1 distance (32), 2 code-length code (19)
+constexpr int kLensOff[3] = {0, 288, 320};
+constexpr int kNsym[3] = {288, 32, 19};
+constexpr int kBits[3] = {kLB, kDB, kCB};
+
+struct InfLds {
+    uint8_t win[kWin];
+    uint32_t far[80];  // a far match's source dwords (staging)
+    uint32_t lim[3][16];  // per code and length L: end of the length-L codes, left-justified to 15 bits
+    int32_t base[3][16];  // per code and length: sorted index = base + (the code's L-bit value)
+    int32_t offs[3][16];  // per code and length: first sorted index of that length
+    uint16_t sorted[340];  // per code: its symbols ordered by (length, symbol)
+    uint8_t lens[340];     // code lengths: lit/len [0, 288), dist [288, 320), code-length code [320, 339)
+};
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ uint32_t make_entry(int k, uint32_t sym, uint32_t L) {
+    const uint32_t l = L << 16;
+    if (k == 0) {
+        if (sym < 256) return kLit | l | sym;
+        if (sym == 256) return kEob | l;
+        if (sym < 286) return l | c_lbase[sym - 257] | ((uint32_t)c_lext[sym - 257] << 20);
+        return kBad | l;  // 286, 287: "invalid literal/length code"
+    }
+    if (k == 1) return sym < 30 ? (l | c_dbase[sym] | ((uint32_t)c_dext[sym] << 20)) : (kBad | l);
+    return l | sym;
+}
+
+// Builds code k from S.lens (wave-wide): the sorted symbol list, the per-length limits and the
+// lookup table.  false: zlib's inflate_table would refuse the lengths (over-subscribed, or
+// incomplete other than one code of length 1; the code-length code must be complete and non-empty).
+template <int NR>
+__device__ bool build_code(InfLds &S, int k, uint32_t (&lut)[NR]) {
+    const int lane = threadIdx.x;
+    const int nsym = kNsym[k], bits = kBits[k];
+    const uint8_t *lens = S.lens + kLensOff[k];
+    uint32_t cnt[16];
+#pragma unroll
+    for (int L = 0; L < 16; L++) cnt[L] = 0;
+    int rk[5], ln[5];
+#pragma unroll
+    for (int ch = 0; ch < 5; ch++) {
+        rk[ch] = 0;
+        ln[ch] = 0;
+        if (ch * 64 >= nsym) continue;
+        const int s = ch * 64 + lane;
+        const int l = s < nsym ? lens[s] : 0;
+        int r = 0;
+#pragma unroll
+        for (int L = 1; L < 16; L++) {
+            const uint64_t m = __ballot(l == L);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (l == L) r = (int)(cnt[L] + below);
+            cnt[L] += (uint32_t)__popcll(m);
+        }
+        rk[ch] = r;
+        ln[ch] = l;
+    }
+    int left = 1, maxl = 0;
+    bool over = false;
+#pragma unroll
+    for (int L = 1; L < 16; L++) {
+        left = 2 * left - (int)cnt[L];
+        over = over || left < 0;
+        if (cnt[L]) maxl = L;
+    }
+    if (over) return false;
+    if (k == 2 && (maxl == 0 || left > 0)) return false;
+    if (maxl > 1 && left > 0) return false;
+    // canonical first codes (RFC 1951 §3.2.2), limits, offsets
+    uint32_t first = 0, o = 0;
+    uint32_t limv[16];
+    if (lane < 16) {
+        S.lim[k][lane] = 0;
+        S.base[k][lane] = 0;
+        S.offs[k][lane] = 0;
+    }
+    limv[0] = 0;
+#pragma unroll
+    for (int L = 1; L < 16; L++) {
+        first = (first + cnt[L - 1]) << 1;
+        if (L == 1) first = 0;
+        limv[L] = (first + cnt[L]) << (15 - L);
+        if (lane == L) {
+            S.lim[k][L] = limv[L];
+            S.base[k][L] = (int32_t)o - (int32_t)first;
+            S.offs[k][L] = (int32_t)o;
+        }
+        o += cnt[L];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ch = 0; ch < 5; ch++) {
+        if (ch * 64 >= nsym) continue;
+        if (ln[ch] > 0) S.sorted[kLensOff[k] + S.offs[k][ln[ch]] + rk[ch]] = (uint16_t)(ch * 64 + lane);
+    }
+    __syncthreads();
+    // the lookup table, held in VGPRs: entry e = the next `bits` stream bits (first bit in bit 0)
+    // is register e >> 6 of lane e & 63 (a lookup is a uniform-indexed register move + readlane)
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+        const int e = 64 * r + lane;
+        const uint32_t rev = __brev((uint32_t)e) >> (32 - bits);  // the bits MSB-first (code order)
+        int Lf = 0;
+#pragma unroll
+        for (int L = 1; L < 16; L++)
+            if (L <= bits && Lf == 0 && rev < (limv[L] >> (15 - bits))) Lf = L;
+        uint32_t ent;
+        if (Lf == 0) {
+            ent = maxl > bits ? kSlow : kBad;  // a longer code, or none (incomplete code / empty)
+        } else {
+            const int idx = S.base[k][Lf] + (int)(rev >> (bits - Lf));
+            ent = make_entry(k, S.sorted[kLensOff[k] + idx], (uint32_t)Lf);
+        }
+        lut[r] = ent;
+    }
+    __syncthreads();
+    return true;
+}
+
+// a code longer than the table's bits: the canonical walk over lengths bits+1 .. 15
+__device__ __forceinline__ uint32_t slow_decode(InfLds &S, int k, uint64_t bb) {
+    const uint32_t rev = __brev((uint32_t)bb) >> 17;  // next 15 bits, code order
+    for (int L = kBits[k] + 1; L < 16; L++) {
+        if (rev < S.lim[k][L]) {
+            const int idx = S.base[k][L] + (int)(rev >> (15 - L));
+            return make_entry(k, S.sorted[kLensOff[k] + idx], (uint32_t)L);
+        }
+    }
+    return kBad | (1u << 16);
+}
+
+__global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
+                                                const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
+                                                uint32_t *__restrict__ mstat, unsigned long long *__restrict__ first_bad) {
+    __shared__ InfLds S;
+    const int lane = threadIdx.x;
+    const uint32_t m = blockIdx.x;
+    const BgzfMember M = mem[m];
+    const uint64_t src = M.src_off;
+    const uint32_t olen = M.out_len;
+    uint32_t why = 0;  // 0 ok, else the first failing check (diagnostic)
+    // gzip header: 10 bytes + XLEN + the extra field (the host checked FLG == FEXTRA)
+    // (byte loads land in VGPRs: readfirstlane keeps every offset derived from them -- the whole
+    // reader state -- in scalar registers and the decode loop in scalar branches)
+    const uint32_t xlen = uni((uint32_t)comp[src + 10] | ((uint32_t)comp[src + 11] << 8));
+    const uint64_t pay0 = src + 12 + xlen;
+    const uint64_t pend = src + M.src_len - 8;  // the deflate stream ends where the trailer starts
+    uint8_t *const dst = out + out_off[m];
+    const uint64_t A = (uint64_t)(uintptr_t)dst;  // absolute output address of byte 0
+    const uint64_t Ab = A & ~15ull;               // the window holds byte p at (A - Ab + p) & mask
+    const uint32_t ph = (uint32_t)(A - Ab);
+    uint32_t pos = 0;      // output bytes produced
+    uint32_t fl = ph;      // output written to HBM up to x = fl (x = ph + byte index)
+    if (pay0 + 2 > pend || olen > 65536) {
+        why = 1;
+    }
+    // the bit reader: the stream's dwords (relative to gb, 16-aligned) reach the bit buffer from
+    // two 256-byte windows held in VGPRs, a dword per lane: dword q from lane q - qa of wa (q in
+    // [qa, qa + 64)) or of wb (the next 64); entering wb shifts the windows and loads the next one,
+    // whose latency the 256 bytes before it is needed hide.  bb holds bn >= 33 bits after refill().
+    // The stream may run past its end into the trailer and the next member (the checks catch it);
+    // past plen_end + 1 KiB the reader feeds zeros and sets ovr, so loads stay within the buffer's
+    // pad (>= 8 KiB) and every loop ends.
+    const uint64_t gb = pay0 & ~15ull;
+    const uint32_t plen_end = (uint32_t)(pend - gb);  // stream end, relative to gb
+    uint32_t qa = 0, rq = 0, bn = 0;
+    uint64_t bb = 0;
+    uint32_t wa = 0, wb = 0;
+    bool ovr = false;  // the reader ran more than 1 KiB past the stream's end (a corrupt stream)
+    auto wload = [&](uint32_t q0) -> uint32_t {
+        return 4 * q0 < plen_end + 2048 ? *reinterpret_cast<const uint32_t *>(comp + gb + 4ull * (q0 + lane)) : 0u;
+    };
+    auto refill = [&]() {
+        if (bn <= 32) {
+            if (rq >= qa + 64) {
+                wa = wb;
+                qa += 64;
+                wb = wload(qa + 64);
+            }
+            ovr = ovr || 4 * rq > plen_end + 1024;
+            const uint32_t w = ovr ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)wa, (int)(rq - qa));
+            bb |= (uint64_t)w << bn;
+            bn += 32;
+            rq++;
+        }
+    };
+    auto seek = [&](uint32_t byte) {  // the reader restarts at stream byte `byte`
+        rq = byte >> 2;
+        qa = rq & ~63u;
+        wa = wload(qa);
+        wb = wload(qa + 64);
+        bb = 0;
+        bn = 0;
+        refill();
+        bb >>= 8 * (byte & 3);
+        bn -= 8 * (byte & 3);
+    };
+    if (!why) seek((uint32_t)(pay0 - gb));
+    auto drop = [&](uint32_t n) {
+        bb >>= n;
+        bn -= n;
+    };
+    auto getb = [&](uint32_t n) -> uint32_t {
+        const uint32_t v = (uint32_t)bb & ((1u << n) - 1);
+        drop(n);
+        return v;
+    };
+    auto consumed_bytes = [&]() -> uint32_t {  // stream bytes used so far (a partial byte counts)
+        return (rq * 32 - bn + 7) / 8;
+    };
+    // the window up to x = `to` (x = ph + the member's byte index; global address Ab + x) goes to
+    // HBM: the member's first partial 16 B block (shared with the previous member) by byte stores,
+    // aligned 16 B blocks from LDS, the last partial block only when `fin`
+    uint8_t *const gout = dst - ph;  // (from the kernel argument: global, not flat, accesses)
+    // A match of <= 64 bytes is read from the window into a register (pv, a byte per lane) and
+    // written only after the next symbol is decoded: the read's LDS latency hides behind that
+    // decode, which needs no LDS (register tables, register input).  Every window access commits
+    // the pending bytes first, so the window sees the writes in stream order.
+    uint32_t pend_n = 0, pend_x = 0, pv = 0;
+    auto commit = [&]() {
+        if (pend_n) {
+            if ((uint32_t)lane < pend_n) S.win[(pend_x + lane) & kWinMask] = (uint8_t)pv;
+            pend_n = 0;
+        }
+    };
+    auto flush = [&](uint32_t to, bool fin) {
+        if (to <= fl) return;
+        commit();
+        uint32_t a = fl;
+        const uint32_t a16 = (a + 15) & ~15u;
+        if (a != a16) {
+            const uint32_t e = a16 < to ? a16 : to;
+            if ((uint32_t)lane < e - a) gout[a + lane] = S.win[(a + lane) & kWinMask];
+            a = e;
+        }
+        const uint32_t b16 = to & ~15u;
+        for (uint32_t x = a + 16 * lane; x + 16 <= b16; x += 16 * 64)
+            *reinterpret_cast<uint4 *>(gout + x) = *reinterpret_cast<const uint4 *>(S.win + (x & kWinMask));
+        if (fin && b16 >= a && to > b16)
+            if ((uint32_t)lane < to - b16) gout[b16 + lane] = S.win[(b16 + lane) & kWinMask];
+        fl = fin ? to : (b16 > a ? b16 : a);
+    };
+    auto maybe_flush = [&]() {
+        const uint32_t x = ph + pos;
+        if (x >= (fl & ~(kFlushStep - 1)) + 2 * kFlushStep) flush(x & ~(kFlushStep - 1), false);
+    };
+    uint32_t lut_ll[(1 << kLB) / 64], lut_d[(1 << kDB) / 64], lut_cl[(1 << kCB) / 64];
+    auto look = [&](const auto &t, uint32_t e) -> uint32_t {  // entry e of a register table
+        return (uint32_t)__builtin_amdgcn_readlane((int)t[e >> 6], (int)(e & 63));
+    };
+    bool fixed_built = false;
+    bool last = false;
+    // (the decoder state is wave-uniform and lives in scalar registers: the code builder's verdict
+    // is readfirstlane'd -- the compiler cannot see it is uniform, and one divergent `why` made the
+    // whole decode loop run on exec masks and VGPR copies of its state, 2.5x the instructions)
+    while (!why && !last) {
+        refill();
+        if (ovr) {
+            why = 17;
+            break;
+        }
+        last = getb(1) != 0;
+        const uint32_t bt = getb(2);
+        commit();
+        if (bt == 0) {  // stored block: to a byte boundary, LEN, NLEN, LEN raw bytes
+            drop(bn & 7);
+            refill();
+            const uint32_t ln = getb(16);
+            refill();
+            const uint32_t nl = getb(16);
+            if (ln != (~nl & 0xFFFFu)) {
+                why = 2;
+                break;
+            }
+            uint32_t q = rq * 4 - bn / 8;  // the next stream byte (relative to gb)
+            if ((uint64_t)q + ln > plen_end) {
+                why = 3;
+                break;
+            }
+            if (pos + ln > olen) {
+                why = 4;
+                break;
+            }
+            for (uint32_t c = 0; c < ln; c += 1024) {  // through the window, 1 KiB at a time
+                const uint32_t take = ln - c < 1024 ? ln - c : 1024;
+                for (uint32_t i = lane; i < take; i += 64)
+                    S.win[(ph + pos + i) & kWinMask] = comp[gb + q + c + i];
+                __syncthreads();
+                pos += take;
+                maybe_flush();
+            }
+            seek(q + ln);
+            continue;
+        }
+        if (bt == 3) {
+            why = 5;
+            break;
+        }
+        if (bt == 1) {  // fixed codes (RFC 1951 §3.2.6)
+            if (!fixed_built) {
+                for (int s = lane; s < 320; s += 64) S.lens[s] = s < 144 ? 8 : (s < 256 ? 9 : (s < 280 ? 7 : (s < 288 ? 8 : 5)));
+                __syncthreads();
+                build_code(S, 0, lut_ll);
+                build_code(S, 1, lut_d);
+                fixed_built = true;
+            }
+        } else {  // dynamic: HLIT, HDIST, HCLEN, the code-length code, then the two codes' lengths
+            fixed_built = false;
+            refill();
+            const uint32_t nlen = getb(5) + 257, ndist = getb(5) + 1, ncl = getb(4) + 4;
+            if (nlen > 286 || ndist > 30) {
+                why = 6;
+                break;
+            }
+            for (int s = lane; s < 340; s += 64) S.lens[s] = 0;
+            __syncthreads();
+            for (uint32_t i = 0; i < ncl; i++) {
+                refill();
+                const uint32_t v = getb(3);
+                if (lane == 0) S.lens[320 + c_clorder[i]] = (uint8_t)v;
+            }
+            __syncthreads();
+            if (!uni((uint32_t)build_code(S, 2, lut_cl))) {
+                why = 7;
+                break;
+            }
+            const uint32_t tot = nlen + ndist;
+            uint32_t n = 0, prev = 0;
+            while (n < tot) {
+                refill();
+                if (ovr) {
+                    why = 17;
+                    break;
+                }
+                const uint32_t e = look(lut_cl, (uint32_t)bb & ((1u << kCB) - 1));
+                if (e & (kBad | kSlow)) {
+                    why = 8;
+                    break;
+                }
+                drop((e >> 16) & 15);
+                const uint32_t sym = e & 31;
+                uint32_t rep = 1, val = sym;
+                if (sym == 16) {
+                    if (n == 0) {
+                        why = 9;
+                        break;
+                    }
+                    rep = 3 + getb(2);
+                    val = prev;
+                } else if (sym == 17) {
+                    rep = 3 + getb(3);
+                    val = 0;
+                } else if (sym == 18) {
+                    rep = 11 + getb(7);
+                    val = 0;
+                }
+                if (n + rep > tot) {
+                    why = 9;
+                    break;
+                }
+                for (uint32_t i = lane; i < rep; i += 64) {
+                    const uint32_t at = n + i;
+                    S.lens[at < nlen ? at : 288 + (at - nlen)] = (uint8_t)val;
+                }
+                n += rep;
+                prev = val;
+            }
+            if (why) break;
+            __syncthreads();
+            if (uni(S.lens[256]) == 0) {  // "invalid code -- missing end-of-block"
+                why = 10;
+                break;
+            }
+            if (!uni((uint32_t)build_code(S, 0, lut_ll))) {
+                why = 11;
+                break;
+            }
+            if (!uni((uint32_t)build_code(S, 1, lut_d))) {
+                why = 12;
+                break;
+            }
+        }
+        // the block's symbols
+        for (;;) {
+            refill();
+            if (ovr) {
+                why = 17;
+                break;
+            }
+            uint32_t e = look(lut_ll, (uint32_t)bb & ((1u << kLB) - 1));
+            if (e & kSlow) e = uni(slow_decode(S, 0, bb));
+            if (e & kBad) {
+                why = 13;
+                break;
+            }
+            drop((e >> 16) & 15);
+            if (e & kLit) {
+                if (pos >= olen) {
+                    why = 14;
+                    break;
+                }
+                commit();
+                if (lane == 0) S.win[(ph + pos) & kWinMask] = (uint8_t)e;
+                pos++;
+                maybe_flush();
+                continue;
+            }
+            if (e & kEob) {
+                commit();
+                break;
+            }
+            const uint32_t len = (e & 0xFFFF) + getb((e >> 20) & 15);
+            refill();
+            uint32_t d = look(lut_d, (uint32_t)bb & ((1u << kDB) - 1));
+            if (d & kSlow) d = uni(slow_decode(S, 1, bb));
+            if (d & kBad) {
+                why = 15;
+                break;
+            }
+            drop((d >> 16) & 15);
+            const uint32_t dist = (d & 0xFFFF) + getb((d >> 20) & 15);
+            if (dist > pos) {  // "invalid distance too far back"
+                why = 16;
+                break;
+            }
+            if (pos + len > olen) {
+                why = 14;
+                break;
+            }
+            if (dist > kFar) {
+                // further back than the window keeps: the member's own output, already in HBM (x - fl
+                // stays <= 2,306 between flushes, so every source byte went out >= 1.5 KiB ago).  Every
+                // store of this wave has completed (s_waitcnt 0); the dwords are read at agent scope
+                // (from L2, never an older L1 line), staged in LDS, then placed bytewise.
+                commit();
+                __builtin_amdgcn_s_waitcnt(0);
+                const uint32_t sx = ph + pos - dist, s4 = sx & ~3u, nb = len + (sx - s4);
+                uint32_t *const src32 = reinterpret_cast<uint32_t *>(gout + s4);
+                for (uint32_t k = lane; 4 * k < nb; k += 64)
+                    S.far[k] = __hip_atomic_load(src32 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __syncthreads();
+                const uint8_t *far8 = reinterpret_cast<const uint8_t *>(S.far) + (sx - s4);
+                for (uint32_t i = lane; i < len; i += 64) S.win[(ph + pos + i) & kWinMask] = far8[i];
+                __syncthreads();
+                pos += len;
+                maybe_flush();
+                continue;
+            }
+            commit();  // (this match may read the previous one's bytes)
+            const float rd = __builtin_amdgcn_rcpf((float)dist);  // (approximate: corrected below)
+            const uint32_t sbase = ph + pos - dist, dx = ph + pos;
+            auto src_of = [&](uint32_t i) -> uint32_t {
+                uint32_t si = i;
+                if (dist < 64) {  // the period-d pattern: i mod d
+                    const uint32_t qd = (uint32_t)((float)i * rd);
+                    int r = (int)i - (int)(qd * dist);
+                    if (r < 0) r += (int)dist;
+                    if (r >= (int)dist) r -= (int)dist;
+                    si = (uint32_t)r;
+                }
+                return (sbase + si) & kWinMask;
+            };
+            if (len <= 64) {  // read now, written after the next symbol's decode
+                if ((uint32_t)lane < len) pv = S.win[src_of((uint32_t)lane)];
+                pend_n = len;
+                pend_x = dx;
+            } else {
+                for (uint32_t c = 0; c < len; c += 64) {
+                    const uint32_t i = c + lane;
+                    if (i < len) {
+                        const uint8_t v = S.win[src_of(i)];
+                        S.win[(dx + i) & kWinMask] = v;
+                    }
+                }
+            }
+            pos += len;
+            maybe_flush();
+        }
+        if (!why && consumed_bytes() > plen_end) why = 17;  // (a block ran into the trailer)
+    }
+    if (!why && (uint64_t)consumed_bytes() != plen_end) why = 18;  // the trailer follows the stream
+    if (!why && pos != olen) why = 19;                               // ISIZE
+    if (!why) {
+        commit();
+        __syncthreads();
+        flush(ph + pos, true);
+    }
+    if (lane == 0) {
+        mstat[m] = why;
+        if (why) atomicMin(first_bad, (unsigned long long)m);
+    }
+}
+
+// ---- CRC-32 (zlib's gzip trailer check) ----------------------------------------------------------
+// Per member (one wave): the output is cut at its end into 1 KiB segments, the first one partial;
+// lane j computes the raw CRC register of segment j (slice-by-4 tables in LDS; the first segment
+// starts from 0xFFFFFFFF, the others from 0), then lane 0 folds them in order with the linear map
+// "through 1 KiB of zero bytes" (four 256-entry tables built from its 32 basis images, which the
+// host computes): acc = Z(acc) ^ R_j.  ~acc is the member's CRC-32.
+__global__ void __launch_bounds__(64) k_crc32(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
+                                              const uint64_t *__restrict__ out_off, const uint8_t *__restrict__ out,
+                                              Crc1k z1k, uint32_t *__restrict__ mstat,
+                                              unsigned long long *__restrict__ first_bad) {
+    __shared__ uint32_t T[4][256];
+    __shared__ uint32_t Z[4][256];
+    const int lane = threadIdx.x;
+    const uint32_t m = blockIdx.x;
+    for (int i = lane; i < 256; i += 64) {
+        uint32_t c = (uint32_t)i;
+#pragma unroll
+        for (int b = 0; b < 8; b++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1)));
+        T[0][i] = c;
+        uint32_t zz[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int b = 0; b < 8; b++)
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                if ((i >> b) & 1) zz[t] ^= z1k.v[8 * t + b];
+#pragma unroll
+        for (int t = 0; t < 4; t++) Z[t][i] = zz[t];
+    }
+    __syncthreads();
+    for (int i = lane; i < 256; i += 64) {
+        const uint32_t c0 = T[0][i];
+        const uint32_t c1 = (c0 >> 8) ^ T[0][c0 & 0xFF];
+        const uint32_t c2 = (c1 >> 8) ^ T[0][c1 & 0xFF];
+        const uint32_t c3 = (c2 >> 8) ^ T[0][c2 & 0xFF];
+        T[1][i] = c1;
+        T[2][i] = c2;
+        T[3][i] = c3;
+    }
+    __syncthreads();
+    const BgzfMember M = mem[m];
+    const uint32_t n = M.out_len;
+    const uint8_t *p = out + out_off[m];
+    const uint32_t head = n & 1023u, nseg = (n >> 10) + (head ? 1 : 0);
+    uint32_t r = 0;
+    if ((uint32_t)lane < nseg) {
+        const uint32_t s0 = lane == 0 ? 0 : head + ((uint32_t)lane - (head ? 1 : 0)) * 1024;
+        const uint32_t s1 = lane == 0 ? (head ? head : 1024) : s0 + 1024;
+        uint32_t c = lane == 0 ? 0xFFFFFFFFu : 0u;
+        const uint8_t *q = p + s0, *qe = p + s1;
+        auto step4 = [&](uint32_t w) {
+            c ^= w;
+            c = T[3][c & 0xFF] ^ T[2][(c >> 8) & 0xFF] ^ T[1][(c >> 16) & 0xFF] ^ T[0][c >> 24];
+        };
+        while (q < qe && (((uintptr_t)q) & 15)) c = (c >> 8) ^ T[0][(c ^ *q++) & 0xFF];
+        // 64 B per step from 16 B-aligned loads, the next step's four loads in flight while this
+        // step's 16 dwords go through the tables (a serial chain of loads was the kernel's cost)
+        if (q + 64 <= qe) {
+            uint4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) v[k] = reinterpret_cast<const uint4 *>(q)[k];
+            for (; q + 64 <= qe; q += 64) {
+                uint4 nx[4];
+                const bool more = q + 128 <= qe;
+#pragma unroll
+                for (int k = 0; k < 4; k++) nx[k] = more ? reinterpret_cast<const uint4 *>(q + 64)[k] : v[k];
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    step4(v[k].x);
+                    step4(v[k].y);
+                    step4(v[k].z);
+                    step4(v[k].w);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; k++) v[k] = nx[k];
+            }
+        }
+        for (; q + 4 <= qe; q += 4) step4(*reinterpret_cast<const uint32_t *>(q));
+        while (q < qe) c = (c >> 8) ^ T[0][(c ^ *q++) & 0xFF];
+        r = c;
+    }
+    // fold in order on lane 0 (the other lanes' registers through LDS)
+    __shared__ uint32_t R[64];
+    R[lane] = r;
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t acc = n ? R[0] : 0xFFFFFFFFu;
+        for (uint32_t j = 1; j < nseg; j++)
+            acc = Z[0][acc & 0xFF] ^ Z[1][(acc >> 8) & 0xFF] ^ Z[2][(acc >> 16) & 0xFF] ^ Z[3][acc >> 24] ^ R[j];
+        const uint64_t t = M.src_off + M.src_len - 8;
+        const uint32_t want = (uint32_t)comp[t] | ((uint32_t)comp[t + 1] << 8) | ((uint32_t)comp[t + 2] << 16) |
+                              ((uint32_t)comp[t + 3] << 24);
+        if (~acc != want && mstat[m] == 0) {
+            mstat[m] = 20;
+            atomicMin(first_bad, (unsigned long long)m);
+        }
+    }
+}
+
+}  // namespace
+
+void crc32_zero1k_basis(Crc1k *z) {
+    uint32_t t[256];
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int b = 0; b < 8; b++) c = (c >> 1) ^ (0xEDB88320u & (0u - (c & 1)));
+        t[i] = c;
+    }
+    for (int k = 0; k < 32; k++) {
+        uint32_t c = 1u << k;
+        for (int i = 0; i < 1024; i++) c = (c >> 8) ^ t[c & 0xFF];
+        z->v[k] = c;
+    }
+}
+
+hipError_t launch_inflate(int which, const uint8_t *comp, const BgzfMember *mem, const uint64_t *out_off,
+                          uint64_t n_members, uint8_t *out, uint32_t *mstat, unsigned long long *first_bad,
+                          const Crc1k &z1k, hipStream_t s) {
+    for (uint64_t m0 = 0; m0 < n_members; m0 += (1u << 30)) {
+        const uint64_t nm = n_members - m0 < (1u << 30) ? n_members - m0 : (1u << 30);
+        if (which == 0)
+            hipLaunchKernelGGL(k_inflate, dim3((unsigned)nm), dim3(64), 0, s, comp, mem + m0, out_off + m0, out,
+                               mstat + m0, first_bad);
+        else
+            hipLaunchKernelGGL(k_crc32, dim3((unsigned)nm), dim3(64), 0, s, comp, mem + m0, out_off + m0, out, z1k,
+                               mstat + m0, first_bad);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace vcfxg

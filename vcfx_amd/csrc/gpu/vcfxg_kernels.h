@@ -29,6 +29,23 @@ constexpr uint8_t kWalkUnswept = 4;
 // idx_pos_cap() newline offsets per chunk, then a compaction into line_end (overflow != 0:
 // some chunk needs the emit sweep launch_idx_emit instead)
 int idx_pos_cap();
+// BGZF members inflated on the device (vcfxg_inflate.hip): one wave per member into
+// out + out_off[m]; mstat[m] = 0 or the first failing check, *first_bad = the lowest bad member
+// (initialise to ~0); then each member's CRC-32 against its trailer.  z1k: the images of the 32
+// CRC register bits through 1 KiB of zero bytes (crc32_zero1k_basis).
+struct BgzfMember {  // = vcfxg_bgzf_member
+    uint64_t src_off;
+    uint32_t src_len;
+    uint32_t out_len;
+};
+struct Crc1k {
+    uint32_t v[32];
+};
+void crc32_zero1k_basis(Crc1k *z);
+// which: 0 = k_inflate, 1 = k_crc32
+hipError_t launch_inflate(int which, const uint8_t *comp, const BgzfMember *mem, const uint64_t *out_off,
+                          uint64_t n_members, uint8_t *out, uint32_t *mstat, unsigned long long *first_bad,
+                          const Crc1k &z1k, hipStream_t s);
 // occurrences of `byte` in buf[lo, hi) added to *out (k_count_byte)
 hipError_t launch_count_byte(const uint8_t *buf, uint64_t lo, uint64_t hi, uint8_t byte, unsigned long long *out,
                              hipStream_t s);

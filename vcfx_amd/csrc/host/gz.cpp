@@ -61,6 +61,31 @@ bool inflate_member(const uint8_t *src, size_t n, char *dst, size_t cap, size_t 
 
 }  // namespace
 
+bool bgzf_chain(const char *src_c, size_t n, std::vector<BgzfSpan> &ms, uint64_t *total) {
+    const uint8_t *src = (const uint8_t *)src_c;
+    ms.clear();
+    uint64_t out = 0;
+    size_t p = 0;
+    while (p < n) {
+        const uint8_t *h = src + p;
+        if (n - p < 18 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 4) return false;
+        const size_t xlen = le16(h + 10);
+        const size_t bs = bgzf_bsize(h, n - p);
+        if (!bs || bs > n - p || bs < 12 + xlen + 8 || bs > 65536) return false;
+        const uint32_t olen = le32(h + bs - 4);
+        if (olen > 65536) return false;
+        ms.push_back({(uint64_t)p, (uint32_t)bs, olen});
+        out += olen;
+        p += bs;
+    }
+    *total = out;
+    return !ms.empty();
+}
+
+bool gz_inflate_member(const char *src, size_t n, char *dst, size_t cap, size_t *got) {
+    return inflate_member((const uint8_t *)src, n, dst, cap, got);
+}
+
 bool is_gzip(const char *p, size_t n) { return n >= 2 && (unsigned char)p[0] == 0x1f && (unsigned char)p[1] == 0x8b; }
 
 GzResult gz_inflate(const char *src_c, size_t n, char *dst, size_t cap, int threads) {

@@ -1,6 +1,9 @@
 // gz.h -- gzip / BGZF input (see gz.cpp)
 #pragma once
 #include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
 
 namespace vcfxh {
 
@@ -15,5 +18,18 @@ struct GzResult {
 bool is_gzip(const char *p, size_t n);
 // inflate the gzip / BGZF stream [src, src+n) into [dst, dst+cap) on up to `threads` threads
 GzResult gz_inflate(const char *src, size_t n, char *dst, size_t cap, int threads);
+
+// The member chain of [src, src+n) when all of it is BGZF in the form the device inflates
+// (vcfxg_ingest_bgzf): each member a gzip member with CM 8 and FLG exactly FEXTRA, a 'BC'
+// subfield (BSIZE), ISIZE <= 64 KiB, the members ending exactly at n.  members[i] = {offset,
+// bytes, ISIZE}; *total = the sum of ISIZE.  false: not such a chain (the host path inflates it).
+struct BgzfSpan {
+    uint64_t off;
+    uint32_t len, olen;
+};
+bool bgzf_chain(const char *src, size_t n, std::vector<BgzfSpan> &members, uint64_t *total);
+// one gzip member [src, src+n) inflated into [dst, dst+cap) by zlib (CRC and ISIZE checked);
+// *got = its bytes; false on any error
+bool gz_inflate_member(const char *src, size_t n, char *dst, size_t cap, size_t *got);
 
 }  // namespace vcfxh

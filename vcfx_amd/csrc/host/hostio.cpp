@@ -436,6 +436,7 @@ bool Input::decompress(int err_fd) {
     }
     if (!gzip_ok || gz || host_n != n || !is_gzip(p, n) || !gzip_enabled()) return true;
     join_populate();
+    if (bgzf_device && device_bgzf()) return true;
     size_t cap = 0;
     void *m = reserve_region(&cap);
     if (!m) {
@@ -463,6 +464,66 @@ bool Input::decompress(int err_fd) {
     gz = true;
     tail = nullptr;
     if (n >= prefetch_bytes()) gpu_prefetch();
+    return true;
+}
+
+bool Input::device_bgzf() {
+    const char *e = getenv("VCFX_BGZF_DEVICE");
+    if ((e && e[0] == '0') || t_shard) return false;
+    const char *em = getenv("VCFX_BGZF_DEVICE_MIN");
+    const uint64_t min_out = em && *em ? strtoull(em, nullptr, 10) : (uint64_t)64 << 20;
+    // the member chain (its headers touch every page of the mapping: fault them in first)
+    if (mapped && map_base) {
+        populate(map_base, map_len);
+        join_populate();
+    }
+    std::vector<BgzfSpan> ms;
+    uint64_t total = 0;
+    if (!bgzf_chain(p, n, ms, &total) || total < min_out) return false;
+    phase("bgzf chain");
+    // the head: members inflated here, in order, until the output holds the complete '#CHROM'
+    // line (the host's gate and the tools' header output run on it); at most 64 MiB
+    const size_t kHeadMax = std::min<uint64_t>(total, (uint64_t)64 << 20) + 65536;
+    void *hm = mmap(nullptr, kHeadMax, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (hm == MAP_FAILED) return false;
+    char *head = (char *)hm;
+    size_t hn = 0, scanned = 0;
+    bool chrom = false;
+    for (size_t i = 0; i < ms.size() && !chrom; i++) {
+        if (hn + ms[i].olen > kHeadMax) break;
+        size_t got = 0;
+        if (!gz_inflate_member(p + ms[i].off, ms[i].len, head + hn, ms[i].olen, &got) || got != ms[i].olen) break;
+        hn += got;
+        while (!chrom && scanned < hn) {
+            const char *s0 = head + scanned;
+            const char *nl = (const char *)memchr(s0, '\n', hn - scanned);
+            if (!nl) break;
+            chrom = is_chrom_line(s0, (size_t)(nl - s0));
+            scanned = (size_t)(nl - head) + 1;
+        }
+    }
+    vcfxg_ctx *g = chrom ? gpu_quiet() : nullptr;
+    uint64_t bad = ~0ull;
+    static_assert(sizeof(BgzfSpan) == sizeof(vcfxg_bgzf_member), "member layout");
+    if (!g || vcfxg_ingest_begin(g, total) != VCFXG_OK ||
+        vcfxg_ingest_bgzf(g, p, n, reinterpret_cast<const vcfxg_bgzf_member *>(ms.data()), ms.size(), head, hn, &bad) !=
+            VCFXG_OK) {
+        munmap(hm, kHeadMax);
+        phase(bad != ~0ull ? "bgzf device inflate refused a member: host inflate" : "bgzf device path not taken");
+        return false;
+    }
+    phase("bgzf inflated on the device");
+    if (map_base && map_len) munmap(map_base, map_len);  // the compressed bytes
+    map_base = hm;
+    map_len = kHeadMax;
+    p = head;
+    host_n = hn;
+    n = (size_t)total;
+    stream_ctx = g;
+    streamed = (size_t)total;
+    mapped = false;
+    gz = true;
+    tail = nullptr;
     return true;
 }
 

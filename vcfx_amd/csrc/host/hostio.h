@@ -42,6 +42,10 @@ struct Input {
     // tools; not VCFX_variant_counter, whose own gzip handling is the reference's) before
     // open_file / read_fd; decompress() then inflates gzip / BGZF input in place
     bool gzip_ok = false;
+    // BGZF input may be inflated on the device (vcfxg_ingest_bgzf) into a device-only input (the
+    // host keeps the inflated head through the '#CHROM' line): set by the tools whose record
+    // phase reads only the header on the host and fetches kept records from the device
+    bool bgzf_device = false;
     bool gz = false;          // the input was inflated
     int read_errno = 0;       // read_fd stopped on a read(2) error (decompress() reports it)
     size_t source_n = 0;      // bytes of the file / stream as read (compressed size for gz)
@@ -80,6 +84,9 @@ struct Input {
     // on every host thread) into a reserved region that becomes the input.  false (after an
     // "Error: ..." line on err_fd) when the stream is truncated or corrupt.
     bool decompress(int err_fd);
+    // decompress()'s device path (bgzf_device, a BGZF chain of >= VCFX_BGZF_DEVICE_MIN inflated
+    // bytes, 64 MiB by default; VCFX_BGZF_DEVICE=0 turns it off): false leaves the input as it was
+    bool device_bgzf();
     // mapped inputs of 64 MiB and more: page-table population running on helper threads
     mutable std::vector<std::thread> populating;
     void populate(void *m, size_t len);

@@ -108,6 +108,7 @@ extern "C" int vcfx_tool_allele_freq_calc(int argc, char **argv, int in_fd, int 
     if (!input && gs.next < argc) input = argv[gs.next];
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
+    in.bgzf_device = true;  // BGZF members inflated on the device (the records stay there)
     uint64_t v = 0, l = 0;
     if (input) {
         phase("start");

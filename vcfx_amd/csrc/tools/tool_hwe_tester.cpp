@@ -161,6 +161,7 @@ extern "C" int vcfx_tool_hwe_tester(int argc, char **argv, int in_fd, int out_fd
     }
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
+    in.bgzf_device = true;  // BGZF members inflated on the device (the records stay there)
     if (input) {
         phase("start");
         if (!in.open_file(input)) {

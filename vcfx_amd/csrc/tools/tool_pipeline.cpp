@@ -26,6 +26,7 @@ extern "C" int vcfx_pipeline_filter_query(const char *filter, const char *logic,
     const bool and_logic = strcmp(logic, "or") != 0;
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
+    in.bgzf_device = true;  // BGZF members inflated on the device (the records stay there)
     bool stdin_mode = !input;
     if (input) {
         if (!in.open_file(input)) {

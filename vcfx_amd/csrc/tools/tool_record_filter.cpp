@@ -244,6 +244,7 @@ extern "C" int vcfx_tool_record_filter(int argc, char **argv, int in_fd, int out
     }
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
+    in.bgzf_device = true;  // BGZF members inflated on the device (the records stay there)
     out.flush();
     if (!input.empty() && input != "-") {
         if (!in.open_file(input.c_str())) {

@@ -51,6 +51,7 @@ SIGNATURES = {
     "vcfxg_ingest_begin": (_I, [_VP, _S]),
     "vcfxg_ingest": (_I, [_VP, _VP, _S, _I]),
     "vcfxg_ingest_wait": (_I, [_VP, _S]),
+    "vcfxg_ingest_bgzf": (_I, [_VP, _VP, _S, _VP, _S, _VP, _S, ctypes.POINTER(_U64)]),
     "vcfxg_host_alloc": (_I, [_VP, _S, ctypes.POINTER(_VP)]),
     "vcfxg_host_free": (None, [_VP, _VP]),
     "vcfxg_input_device_ptr": (_VP, [_VP]),
@@ -191,6 +192,34 @@ class Engine:
             self._chk(self.L.vcfxg_ingest(self.h, None, 0, 1), "ingest")
         for i, a in enumerate(arrs):
             self._chk(self.L.vcfxg_ingest(self.h, a.ctypes.data, a.size, int(i == len(arrs) - 1)), "ingest")
+
+    def load_bgzf(self, comp, members=None, head=b""):
+        """vcfxg_ingest_begin + vcfxg_ingest_bgzf + the final vcfxg_ingest: the BGZF members of
+        `comp` inflated on the device into the input.  members: bgzf_members(comp) by default.
+        Returns None, or (first bad member, error text) when the device refused a member (the
+        input is then not loaded)."""
+        import numpy as np
+        arr = np.frombuffer(comp, np.uint8) if not isinstance(comp, np.ndarray) else comp
+        mem = bgzf_members(arr) if members is None else members
+        hd = np.frombuffer(head, np.uint8) if head else None
+        self._buf = (arr, mem, hd)
+        total = int(mem["out_len"].sum()) if len(mem) else 0
+        self._chk(self.L.vcfxg_ingest_begin(self.h, total), "ingest_begin")
+        bad = ctypes.c_uint64()
+        rc = self.L.vcfxg_ingest_bgzf(self.h, arr.ctypes.data, arr.size, mem.ctypes.data if len(mem) else None,
+                                      len(mem), hd.ctypes.data if hd is not None else None,
+                                      0 if hd is None else hd.size, ctypes.byref(bad))
+        if rc == -7:  # VCFXG_E_DATA
+            return bad.value, self.L.vcfxg_last_error(self.h).decode()
+        self._chk(rc, "ingest_bgzf")
+        self._chk(self.L.vcfxg_ingest(self.h, None, 0, 1), "ingest")
+        return None
+
+    def input_bytes(self, offset, n):
+        """bytes [offset, offset + n) of the loaded device input (vcfxg_input_fetch)"""
+        b = ctypes.create_string_buffer(max(1, n))
+        self._chk(self.L.vcfxg_input_fetch(self.h, offset, n, b), "input_fetch")
+        return b.raw[:n]
 
     def index(self, data_start):
         n = ctypes.c_uint64()
@@ -410,6 +439,39 @@ class Engine:
         out = np.zeros(n, np.uint64)
         self._chk(self.L.vcfxg_line_ends(self.h, 0, n, out.ctypes.data), "line_ends")
         return out
+
+
+BGZF_MEMBER = None
+
+
+def bgzf_members(buf):
+    """The BGZF member table of buf (numpy uint8) for vcfxg_ingest_bgzf: every member a gzip
+    member with FLG exactly FEXTRA and a 'BC' subfield (SAM/BAM spec §4.1), ISIZE <= 65536;
+    raises ValueError otherwise (not a complete BGZF chain: the host inflates it)."""
+    import numpy as np
+    global BGZF_MEMBER
+    if BGZF_MEMBER is None:
+        BGZF_MEMBER = np.dtype([("src_off", "<u8"), ("src_len", "<u4"), ("out_len", "<u4")])
+    b = bytes(buf) if not isinstance(buf, (bytes, bytearray)) else buf
+    out, p, n = [], 0, len(b)
+    while p < n:
+        if n - p < 18 or b[p] != 0x1F or b[p + 1] != 0x8B or b[p + 2] != 8 or b[p + 3] != 4:
+            raise ValueError("not a BGZF member at %d" % p)
+        xlen = b[p + 10] | b[p + 11] << 8
+        k, bs = 12, 0
+        while k + 4 <= 12 + xlen and p + k + 4 <= n:
+            slen = b[p + k + 2] | b[p + k + 3] << 8
+            if b[p + k] == 66 and b[p + k + 1] == 67 and slen == 2:
+                bs = (b[p + k + 4] | b[p + k + 5] << 8) + 1
+            k += 4 + slen
+        if not bs or p + bs > n or bs < 12 + xlen + 8:
+            raise ValueError("bad BGZF member at %d" % p)
+        isize = int.from_bytes(b[p + bs - 4:p + bs], "little")
+        if isize > 65536:
+            raise ValueError("ISIZE over 64 KiB at %d" % p)
+        out.append((p, bs, isize))
+        p += bs
+    return np.array(out, dtype=BGZF_MEMBER)
 
 
 def shard_cuts(buf, lo, world):
