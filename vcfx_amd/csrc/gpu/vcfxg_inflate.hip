@@ -9,17 +9,26 @@
 // bench shard).
 //
 // k_inflate (one 64-lane wave per member; the DEFLATE decode of RFC 1951 is serial per stream, so
-// the wave's scalar path decodes and its lanes do the parallel parts):
-//   - the compressed bytes stream through a 4 KiB LDS ring (1 KiB coalesced refills) into a 64-bit
-//     bit buffer;
+// the wave's scalar unit decodes and its lanes do the parallel parts).  Every CU's scalar unit
+// issues one instruction per cycle for all its waves, so the decode is built to spend as few
+// scalar instructions per symbol as it can:
+//   - the input is a 64-byte window held in one VGPR, lane i holding the 32 stream bits that start
+//     at byte B + i: the next bits at bit position bp are one v_readlane + one shift (>= 25 valid
+//     bits), consuming bits is one add to bp, and the window moves (one unaligned dword load per
+//     lane) only when a symbol could reach past it;
 //   - each block's Huffman codes (fixed, or the dynamic header's) are built by the whole wave:
-//     per-length counts and each symbol's canonical rank from ballots, then lookup tables of 2^10
-//     (literal/length), 2^9 (distance) and 2^7 (code-length code) entries filled by all lanes,
-//     each entry decoded canonically; the rare longer codes take a per-length canonical walk;
-//   - literals go to a 32 KiB LDS window (deflate's largest distance), a match is copied by the
-//     64 lanes at once (distance < 64: the period-d pattern, out[p + i] = out[p - d + i mod d]);
-//   - the window is written to HBM in aligned 16 B blocks as it fills (byte stores only at the
-//     member's two ends, which neighbouring members share).
+//     per-length counts and each symbol's canonical rank from ballots, then lookup tables of 2^9
+//     (literal/length) and 2^8 (distance) entries held in VGPRs (entry e is register e >> 6 of lane
+//     e & 63: a uniform-indexed register move and a v_readlane), filled by all lanes and decoded
+//     canonically; a length or distance code whose extra bits fit in the table's index carries its
+//     final value, so most matches need no extra-bit reads; the rare longer codes take a per-length
+//     canonical walk over LDS tables; the code-length code's table is in LDS;
+//   - the output goes through an 8 KiB LDS window: a match of <= 64 bytes is one LDS read (all 64
+//     lanes, the period-d pattern out[p + i] = out[p - d + i mod d] for overlapping copies) whose
+//     write waits until after the next symbol's decode; a match from further back than 4 KiB reads
+//     the member's own output, already in HBM;
+//   - the window goes to HBM in aligned 16 B blocks as it fills (byte stores only at the member's
+//     two ends, which neighbouring members share).
 // Every condition under which zlib's inflate fails (zlib inflate.c / inftrees.c: invalid block
 // type, stored LEN != ~NLEN, more than 286 / 30 symbols, an over-subscribed or incomplete code --
 // incomplete only allowed for a single code of length 1, and never for the code-length code --,
@@ -41,12 +50,17 @@ namespace {
 // than kFar reads the member's own output, already written to HBM, instead)
 constexpr uint32_t kWin = 1u << 13, kWinMask = kWin - 1;
 constexpr uint32_t kFar = 4096;
-constexpr int kLB = 10, kDB = 9, kCB = 7;                 // lookup-table bits: lit/len, dist, code lengths
-constexpr uint32_t kFlushStep = 1024;                     // HBM writes in 1 KiB-aligned steps
+// lookup-table bits: lit/len, distance, code lengths.  The VGPR tables are one 16-register array
+// (the compiler keeps one such array in registers with uniform-indexed moves; a second array went
+// to scratch): lit/len entries in registers 0-7, distance entries in 8-11, distance values in 12-15
+constexpr int kLB = 9, kDB = 8, kCB = 7;
+constexpr uint32_t kFlushStep = 1024;  // HBM writes in 1 KiB-aligned steps
 
-// table entries: bits 0-15 value (literal, length base, distance base, code-length symbol), 16-19 code
-// length, 20-23 extra bits; flags
-constexpr uint32_t kLit = 1u << 24, kEob = 1u << 25, kBad = 1u << 26, kSlow = 1u << 27;
+// table entries: bits 0-4 `cons` (bits the entry consumes: the code, plus its extra bits when they
+// were folded into the value), 5-8 flags, 9-13 `tot` (cons + the extra bits still to read), 16-19
+// `unf` (those extra bits; with cons this is the s_bfe field of the extra value), 23-31 the value
+// (literal byte, length, code-length symbol; a distance value is in the value table)
+constexpr uint32_t kLit = 1u << 5, kEob = 1u << 6, kExc = 1u << 7, kBad = 1u << 8;
 
 // RFC 1951 §3.2.5: length codes 257..285 and distance codes 0..29 (base, extra bits)
 __constant__ uint16_t c_lbase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -66,6 +80,7 @@ constexpr int kBits[3] = {kLB, kDB, kCB};
 struct InfLds {
     uint8_t win[kWin];
     uint32_t far[80];  // a far match's source dwords (staging)
+    uint32_t cl[1 << kCB];  // the code-length code's table (dynamic headers only)
     uint32_t lim[3][16];  // per code and length L: end of the length-L codes, left-justified to 15 bits
     int32_t base[3][16];  // per code and length: sorted index = base + (the code's L-bit value)
     int32_t offs[3][16];  // per code and length: first sorted index of that length
@@ -75,26 +90,55 @@ struct InfLds {
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-__device__ __forceinline__ uint32_t make_entry(int k, uint32_t sym, uint32_t L) {
-    const uint32_t l = L << 16;
+// s_bfe_u32 with the entry as the field spec: the `unf` extra bits that follow the entry's `cons`
+__device__ __forceinline__ uint32_t sbfe(uint32_t p, uint32_t e) {
+    uint32_t r;
+    asm volatile("s_bfe_u32 %0, %1, %2" : "=s"(r) : "s"(p), "s"(e) : "scc");
+    return r;
+}
+__device__ __forceinline__ uint32_t tot_of(uint32_t e) { return (e >> 9) & 31; }
+
+__device__ __forceinline__ uint32_t make(uint32_t cons, uint32_t unf, uint32_t v9, uint32_t flags) {
+    return cons | flags | ((cons + unf) << 9) | (unf << 16) | (v9 << 23);
+}
+
+// the entry of symbol `sym` with an L-bit code; idx = the table index (stream bits, first in bit
+// 0) when the entry is a table slot (the extra bits after the code are idx >> L when L + extra <=
+// bits), bits = 0 for the canonical walk (no folding).  k 1: the distance value goes to `val`
+__device__ __forceinline__ uint32_t make_entry(int k, uint32_t sym, uint32_t L, uint32_t idx, int bits, uint32_t &val) {
+    val = 0;
     if (k == 0) {
-        if (sym < 256) return kLit | l | sym;
-        if (sym == 256) return kEob | l;
-        if (sym < 286) return l | c_lbase[sym - 257] | ((uint32_t)c_lext[sym - 257] << 20);
-        return kBad | l;  // 286, 287: "invalid literal/length code"
+        if (sym < 256) return make(L, 0, sym, kLit);
+        if (sym == 256) return make(L, 0, 0, kEob);
+        if (sym < 286) {
+            const uint32_t b = c_lbase[sym - 257], ex = c_lext[sym - 257];
+            if (L + ex <= (uint32_t)bits) return make(L + ex, 0, b + ((idx >> L) & ((1u << ex) - 1)), 0);
+            return make(L, ex, b, 0);
+        }
+        return make(L, 0, 0, kExc | kBad);  // 286, 287: "invalid literal/length code"
     }
-    if (k == 1) return sym < 30 ? (l | c_dbase[sym] | ((uint32_t)c_dext[sym] << 20)) : (kBad | l);
-    return l | sym;
+    if (k == 1) {
+        if (sym >= 30) return make(L, 0, 0, kExc | kBad);  // "invalid distance code"
+        const uint32_t b = c_dbase[sym], ex = c_dext[sym];
+        if (L + ex <= (uint32_t)bits) {
+            val = b + ((idx >> L) & ((1u << ex) - 1));
+            return make(L + ex, 0, 0, 0);
+        }
+        val = b;
+        return make(L, ex, 0, 0);
+    }
+    return make(L, 0, sym, 0);
 }
 
 // Builds code k from S.lens (wave-wide): the sorted symbol list, the per-length limits and the
 // lookup table.  false: zlib's inflate_table would refuse the lengths (over-subscribed, or
 // incomplete other than one code of length 1; the code-length code must be complete and non-empty).
-template <int NR>
-__device__ bool build_code(InfLds &S, int k, uint32_t (&lut)[NR]) {
+// k 0: the table goes to registers 0-7 of lut; k 1: entries to 8-11, values to 12-15; k 2: to S.cl
+template <int K>
+__device__ bool build_code(InfLds &S, uint32_t (&lut)[16]) {
     const int lane = threadIdx.x;
-    const int nsym = kNsym[k], bits = kBits[k];
-    const uint8_t *lens = S.lens + kLensOff[k];
+    constexpr int nsym = kNsym[K], bits = kBits[K];
+    const uint8_t *lens = S.lens + kLensOff[K];
     uint32_t cnt[16];
 #pragma unroll
     for (int L = 0; L < 16; L++) cnt[L] = 0;
@@ -126,15 +170,15 @@ __device__ bool build_code(InfLds &S, int k, uint32_t (&lut)[NR]) {
         if (cnt[L]) maxl = L;
     }
     if (over) return false;
-    if (k == 2 && (maxl == 0 || left > 0)) return false;
+    if (K == 2 && (maxl == 0 || left > 0)) return false;
     if (maxl > 1 && left > 0) return false;
     // canonical first codes (RFC 1951 §3.2.2), limits, offsets
     uint32_t first = 0, o = 0;
     uint32_t limv[16];
     if (lane < 16) {
-        S.lim[k][lane] = 0;
-        S.base[k][lane] = 0;
-        S.offs[k][lane] = 0;
+        S.lim[K][lane] = 0;
+        S.base[K][lane] = 0;
+        S.offs[K][lane] = 0;
     }
     limv[0] = 0;
 #pragma unroll
@@ -143,9 +187,9 @@ __device__ bool build_code(InfLds &S, int k, uint32_t (&lut)[NR]) {
         if (L == 1) first = 0;
         limv[L] = (first + cnt[L]) << (15 - L);
         if (lane == L) {
-            S.lim[k][L] = limv[L];
-            S.base[k][L] = (int32_t)o - (int32_t)first;
-            S.offs[k][L] = (int32_t)o;
+            S.lim[K][L] = limv[L];
+            S.base[K][L] = (int32_t)o - (int32_t)first;
+            S.offs[K][L] = (int32_t)o;
         }
         o += cnt[L];
     }
@@ -153,42 +197,50 @@ __device__ bool build_code(InfLds &S, int k, uint32_t (&lut)[NR]) {
 #pragma unroll
     for (int ch = 0; ch < 5; ch++) {
         if (ch * 64 >= nsym) continue;
-        if (ln[ch] > 0) S.sorted[kLensOff[k] + S.offs[k][ln[ch]] + rk[ch]] = (uint16_t)(ch * 64 + lane);
+        if (ln[ch] > 0) S.sorted[kLensOff[K] + S.offs[K][ln[ch]] + rk[ch]] = (uint16_t)(ch * 64 + lane);
     }
     __syncthreads();
-    // the lookup table, held in VGPRs: entry e = the next `bits` stream bits (first bit in bit 0)
-    // is register e >> 6 of lane e & 63 (a lookup is a uniform-indexed register move + readlane)
+    // the lookup table: entry e = the next `bits` stream bits (first bit in bit 0) is register
+    // e >> 6 of lane e & 63 (a lookup is a uniform-indexed register move + readlane)
+    constexpr int NR = (1 << bits) / 64;
 #pragma unroll
     for (int r = 0; r < NR; r++) {
-        const int e = 64 * r + lane;
-        const uint32_t rev = __brev((uint32_t)e) >> (32 - bits);  // the bits MSB-first (code order)
+        const uint32_t e = 64 * r + lane;
+        const uint32_t rev = __brev(e) >> (32 - bits);  // the bits MSB-first (code order)
         int Lf = 0;
 #pragma unroll
         for (int L = 1; L < 16; L++)
             if (L <= bits && Lf == 0 && rev < (limv[L] >> (15 - bits))) Lf = L;
-        uint32_t ent;
+        uint32_t ent, val = 0;
         if (Lf == 0) {
-            ent = maxl > bits ? kSlow : kBad;  // a longer code, or none (incomplete code / empty)
+            ent = maxl > bits ? kExc : (kExc | kBad);  // a longer code, or none (incomplete code / empty)
         } else {
-            const int idx = S.base[k][Lf] + (int)(rev >> (bits - Lf));
-            ent = make_entry(k, S.sorted[kLensOff[k] + idx], (uint32_t)Lf);
+            const int idx = S.base[K][Lf] + (int)(rev >> (bits - Lf));
+            ent = make_entry(K, S.sorted[kLensOff[K] + idx], (uint32_t)Lf, e, bits, val);
         }
-        lut[r] = ent;
+        if (K == 2) S.cl[e] = ent;
+        else if (K == 0) lut[r] = ent;
+        else {
+            lut[8 + r] = ent;
+            lut[12 + r] = val;
+        }
     }
     __syncthreads();
     return true;
 }
 
-// a code longer than the table's bits: the canonical walk over lengths bits+1 .. 15
-__device__ __forceinline__ uint32_t slow_decode(InfLds &S, int k, uint64_t bb) {
-    const uint32_t rev = __brev((uint32_t)bb) >> 17;  // next 15 bits, code order
+// a code longer than the table's bits: the canonical walk over lengths bits+1 .. 15 (p: the next
+// >= 15 stream bits); the entry carries the code's length as cons and its extra bits as unf
+__device__ __forceinline__ uint32_t slow_decode(InfLds &S, int k, uint32_t p, uint32_t &val) {
+    const uint32_t rev = __brev(p) >> 17;  // next 15 bits, code order
     for (int L = kBits[k] + 1; L < 16; L++) {
         if (rev < S.lim[k][L]) {
             const int idx = S.base[k][L] + (int)(rev >> (15 - L));
-            return make_entry(k, S.sorted[kLensOff[k] + idx], (uint32_t)L);
+            return make_entry(k, S.sorted[kLensOff[k] + idx], (uint32_t)L, 0, 0, val);
         }
     }
-    return kBad | (1u << 16);
+    val = 0;
+    return kExc | kBad;
 }
 
 __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
@@ -211,83 +263,56 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
     const uint64_t A = (uint64_t)(uintptr_t)dst;  // absolute output address of byte 0
     const uint64_t Ab = A & ~15ull;               // the window holds byte p at (A - Ab + p) & mask
     const uint32_t ph = (uint32_t)(A - Ab);
-    uint32_t pos = 0;      // output bytes produced
-    uint32_t fl = ph;      // output written to HBM up to x = fl (x = ph + byte index)
-    if (pay0 + 2 > pend || olen > 65536) {
-        why = 1;
-    }
-    // the bit reader: the stream's dwords (relative to gb, 16-aligned) reach the bit buffer from
-    // two 256-byte windows held in VGPRs, a dword per lane: dword q from lane q - qa of wa (q in
-    // [qa, qa + 64)) or of wb (the next 64); entering wb shifts the windows and loads the next one,
-    // whose latency the 256 bytes before it is needed hide.  bb holds bn >= 33 bits after refill().
-    // The stream may run past its end into the trailer and the next member (the checks catch it);
-    // past plen_end + 1 KiB the reader feeds zeros and sets ovr, so loads stay within the buffer's
-    // pad (>= 8 KiB) and every loop ends.
-    const uint64_t gb = pay0 & ~15ull;
+    // output position x = ph + the member's byte index; xend = ph + ISIZE
+    uint32_t x = ph;
+    const uint32_t xend = ph + olen;
+    uint32_t fl = ph;  // output written to HBM up to x = fl
+    uint32_t fnext = (ph & ~(kFlushStep - 1)) + 2 * kFlushStep;  // flush when x reaches this
+    if (pay0 + 2 > pend || olen > 65536) why = 1;
+    // the bit reader: stream bytes relative to gb; lane i of pk holds the dword at byte B + i (past
+    // plen_end + 2 KiB it holds zeros, so loads stay within the buffer's pad; a stream that runs
+    // past its end is caught at its block's end, and every loop ends since each symbol consumes
+    // bits and adds output or ends its block)
+    const uint64_t gb = pay0;
     const uint32_t plen_end = (uint32_t)(pend - gb);  // stream end, relative to gb
-    uint32_t qa = 0, rq = 0, bn = 0;
-    uint64_t bb = 0;
-    uint32_t wa = 0, wb = 0;
-    bool ovr = false;  // the reader ran more than 1 KiB past the stream's end (a corrupt stream)
-    auto wload = [&](uint32_t q0) -> uint32_t {
-        return 4 * q0 < plen_end + 2048 ? *reinterpret_cast<const uint32_t *>(comp + gb + 4ull * (q0 + lane)) : 0u;
+    uint32_t bp = 0, B = 0;
+    uint32_t pk = 0;
+    auto advance = [&]() {  // the window to start at the byte holding bit bp
+        B = bp >> 3;
+        uint32_t v = 0;
+        if (B + (uint32_t)lane < plen_end + 2048) __builtin_memcpy(&v, comp + gb + B + lane, 4);
+        pk = v;
     };
-    auto refill = [&]() {
-        if (bn <= 32) {
-            if (rq >= qa + 64) {
-                wa = wb;
-                qa += 64;
-                wb = wload(qa + 64);
-            }
-            ovr = ovr || 4 * rq > plen_end + 1024;
-            const uint32_t w = ovr ? 0u : (uint32_t)__builtin_amdgcn_readlane((int)wa, (int)(rq - qa));
-            bb |= (uint64_t)w << bn;
-            bn += 32;
-            rq++;
-        }
+    auto peek = [&]() -> uint32_t {  // >= 25 valid stream bits from bp (the window must hold them)
+        return (uint32_t)__builtin_amdgcn_readlane((int)pk, (int)((bp >> 3) - B)) >> (bp & 7);
     };
-    auto seek = [&](uint32_t byte) {  // the reader restarts at stream byte `byte`
-        rq = byte >> 2;
-        qa = rq & ~63u;
-        wa = wload(qa);
-        wb = wload(qa + 64);
-        bb = 0;
-        bn = 0;
-        refill();
-        bb >>= 8 * (byte & 3);
-        bn -= 8 * (byte & 3);
+    auto room = [&]() {  // the window holds >= 6 more bytes past bp's byte (a whole match)
+        if ((bp >> 3) - B > 57) advance();
     };
-    if (!why) seek((uint32_t)(pay0 - gb));
-    auto drop = [&](uint32_t n) {
-        bb >>= n;
-        bn -= n;
-    };
-    auto getb = [&](uint32_t n) -> uint32_t {
-        const uint32_t v = (uint32_t)bb & ((1u << n) - 1);
-        drop(n);
+    auto getb = [&](uint32_t n) -> uint32_t {  // n <= 16 bits
+        room();
+        const uint32_t v = peek() & ((1u << n) - 1);
+        bp += n;
         return v;
     };
-    auto consumed_bytes = [&]() -> uint32_t {  // stream bytes used so far (a partial byte counts)
-        return (rq * 32 - bn + 7) / 8;
-    };
-    // the window up to x = `to` (x = ph + the member's byte index; global address Ab + x) goes to
-    // HBM: the member's first partial 16 B block (shared with the previous member) by byte stores,
-    // aligned 16 B blocks from LDS, the last partial block only when `fin`
+    auto consumed_bytes = [&]() -> uint32_t { return (bp + 7) >> 3; };  // (a partial byte counts)
+    if (!why) advance();
+    // the window up to x = `to` goes to HBM: the member's first partial 16 B block (shared with the
+    // previous member) by byte stores, aligned 16 B blocks from LDS, the last partial block only
+    // when `fin`
     uint8_t *const gout = dst - ph;  // (from the kernel argument: global, not flat, accesses)
-    // A match of <= 64 bytes is read from the window into a register (pv, a byte per lane) and
-    // written only after the next symbol is decoded: the read's LDS latency hides behind that
-    // decode, which needs no LDS (register tables, register input).  Every window access commits
-    // the pending bytes first, so the window sees the writes in stream order.
-    uint32_t pend_n = 0, pend_x = 0, pv = 0;
-    auto commit = [&]() {
-        if (pend_n) {
-            if ((uint32_t)lane < pend_n) S.win[(pend_x + lane) & kWinMask] = (uint8_t)pv;
-            pend_n = 0;
-        }
-    };
+    // The pending write: the bytes of the last literal or match of <= 64 bytes, read into pv (a byte
+    // per lane) and written at x0 + lane only after the next symbol's decode, whose table lookups
+    // need no LDS, hides the read's latency.  All 64 lanes write: the lanes past the symbol's length
+    // write bytes ahead of the output, which later symbols overwrite before anything reads or
+    // flushes them (and which land on window slots that are flushed and out of match reach).  Every
+    // window access commits the pending write first, so the window sees the writes in stream order.
+    uint32_t pv = 0, pa = 0;  // pending byte and window slot (per lane)
+    auto commit = [&]() { S.win[pa] = (uint8_t)pv; };
+    pa = (x + lane) & kWinMask;
+    pv = 0;  // (the first commit writes zeros ahead of the output)
     auto flush = [&](uint32_t to, bool fin) {
         if (to <= fl) return;
-        commit();
         uint32_t a = fl;
         const uint32_t a16 = (a + 15) & ~15u;
         if (a != a16) {
@@ -296,62 +321,65 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
             a = e;
         }
         const uint32_t b16 = to & ~15u;
-        for (uint32_t x = a + 16 * lane; x + 16 <= b16; x += 16 * 64)
-            *reinterpret_cast<uint4 *>(gout + x) = *reinterpret_cast<const uint4 *>(S.win + (x & kWinMask));
+        for (uint32_t y = a + 16 * lane; y + 16 <= b16; y += 16 * 64)
+            *reinterpret_cast<uint4 *>(gout + y) = *reinterpret_cast<const uint4 *>(S.win + (y & kWinMask));
         if (fin && b16 >= a && to > b16)
             if ((uint32_t)lane < to - b16) gout[b16 + lane] = S.win[(b16 + lane) & kWinMask];
         fl = fin ? to : (b16 > a ? b16 : a);
+        fnext = (fl & ~(kFlushStep - 1)) + 2 * kFlushStep;
     };
     auto maybe_flush = [&]() {
-        const uint32_t x = ph + pos;
-        if (x >= (fl & ~(kFlushStep - 1)) + 2 * kFlushStep) flush(x & ~(kFlushStep - 1), false);
+        if (x >= fnext) {
+            commit();
+            flush(x & ~(kFlushStep - 1), false);
+        }
     };
-    uint32_t lut_ll[(1 << kLB) / 64], lut_d[(1 << kDB) / 64], lut_cl[(1 << kCB) / 64];
-    auto look = [&](const auto &t, uint32_t e) -> uint32_t {  // entry e of a register table
-        return (uint32_t)__builtin_amdgcn_readlane((int)t[e >> 6], (int)(e & 63));
+    uint32_t lut[16];  // lit/len entries in registers 0-7, distance entries 8-11, distance values 12-15
+    auto lookL = [&](uint32_t p) -> uint32_t {  // entry p & 511 (readlane takes the lane as p & 63)
+        return (uint32_t)__builtin_amdgcn_readlane((int)lut[(p >> 6) & 7], (int)(p & 63));
     };
+    auto lookD = [&](uint32_t p, uint32_t &val) -> uint32_t {
+        const uint32_t r = (p >> 6) & 3;
+        val = (uint32_t)__builtin_amdgcn_readlane((int)lut[12 + r], (int)(p & 63));
+        return (uint32_t)__builtin_amdgcn_readlane((int)lut[8 + r], (int)(p & 63));
+    };
+    const float lanef = (float)lane + 0.5f;
     bool fixed_built = false;
     bool last = false;
     // (the decoder state is wave-uniform and lives in scalar registers: the code builder's verdict
     // is readfirstlane'd -- the compiler cannot see it is uniform, and one divergent `why` made the
     // whole decode loop run on exec masks and VGPR copies of its state, 2.5x the instructions)
     while (!why && !last) {
-        refill();
-        if (ovr) {
-            why = 17;
-            break;
-        }
         last = getb(1) != 0;
         const uint32_t bt = getb(2);
         commit();
         if (bt == 0) {  // stored block: to a byte boundary, LEN, NLEN, LEN raw bytes
-            drop(bn & 7);
-            refill();
+            bp = (bp + 7) & ~7u;
             const uint32_t ln = getb(16);
-            refill();
             const uint32_t nl = getb(16);
             if (ln != (~nl & 0xFFFFu)) {
                 why = 2;
                 break;
             }
-            uint32_t q = rq * 4 - bn / 8;  // the next stream byte (relative to gb)
+            const uint32_t q = bp >> 3;  // the next stream byte (relative to gb)
             if ((uint64_t)q + ln > plen_end) {
                 why = 3;
                 break;
             }
-            if (pos + ln > olen) {
+            if (x + ln > xend) {
                 why = 4;
                 break;
             }
             for (uint32_t c = 0; c < ln; c += 1024) {  // through the window, 1 KiB at a time
                 const uint32_t take = ln - c < 1024 ? ln - c : 1024;
-                for (uint32_t i = lane; i < take; i += 64)
-                    S.win[(ph + pos + i) & kWinMask] = comp[gb + q + c + i];
+                for (uint32_t i = lane; i < take; i += 64) S.win[(x + i) & kWinMask] = comp[gb + q + c + i];
                 __syncthreads();
-                pos += take;
+                x += take;
+                pa = (x + lane) & kWinMask;  // (the next commit writes ahead of the output)
                 maybe_flush();
             }
-            seek(q + ln);
+            bp = (q + ln) * 8;
+            advance();
             continue;
         }
         if (bt == 3) {
@@ -362,13 +390,12 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
             if (!fixed_built) {
                 for (int s = lane; s < 320; s += 64) S.lens[s] = s < 144 ? 8 : (s < 256 ? 9 : (s < 280 ? 7 : (s < 288 ? 8 : 5)));
                 __syncthreads();
-                build_code(S, 0, lut_ll);
-                build_code(S, 1, lut_d);
+                build_code<0>(S, lut);
+                build_code<1>(S, lut);
                 fixed_built = true;
             }
         } else {  // dynamic: HLIT, HDIST, HCLEN, the code-length code, then the two codes' lengths
             fixed_built = false;
-            refill();
             const uint32_t nlen = getb(5) + 257, ndist = getb(5) + 1, ncl = getb(4) + 4;
             if (nlen > 286 || ndist > 30) {
                 why = 6;
@@ -377,30 +404,26 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
             for (int s = lane; s < 340; s += 64) S.lens[s] = 0;
             __syncthreads();
             for (uint32_t i = 0; i < ncl; i++) {
-                refill();
                 const uint32_t v = getb(3);
                 if (lane == 0) S.lens[320 + c_clorder[i]] = (uint8_t)v;
             }
             __syncthreads();
-            if (!uni((uint32_t)build_code(S, 2, lut_cl))) {
+            if (!uni((uint32_t)build_code<2>(S, lut))) {
                 why = 7;
                 break;
             }
             const uint32_t tot = nlen + ndist;
             uint32_t n = 0, prev = 0;
             while (n < tot) {
-                refill();
-                if (ovr) {
-                    why = 17;
-                    break;
-                }
-                const uint32_t e = look(lut_cl, (uint32_t)bb & ((1u << kCB) - 1));
-                if (e & (kBad | kSlow)) {
+                room();
+                const uint32_t p = peek();
+                const uint32_t e = uni(S.cl[p & ((1u << kCB) - 1)]);
+                if (e & kExc) {
                     why = 8;
                     break;
                 }
-                drop((e >> 16) & 15);
-                const uint32_t sym = e & 31;
+                bp += e & 31;
+                const uint32_t sym = e >> 23;
                 uint32_t rep = 1, val = sym;
                 if (sym == 16) {
                     if (n == 0) {
@@ -433,119 +456,137 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
                 why = 10;
                 break;
             }
-            if (!uni((uint32_t)build_code(S, 0, lut_ll))) {
+            if (!uni((uint32_t)build_code<0>(S, lut))) {
                 why = 11;
                 break;
             }
-            if (!uni((uint32_t)build_code(S, 1, lut_d))) {
+            if (!uni((uint32_t)build_code<1>(S, lut))) {
                 why = 12;
                 break;
             }
         }
         // the block's symbols
         for (;;) {
-            refill();
-            if (ovr) {
-                why = 17;
-                break;
-            }
-            uint32_t e = look(lut_ll, (uint32_t)bb & ((1u << kLB) - 1));
-            if (e & kSlow) e = uni(slow_decode(S, 0, bb));
-            if (e & kBad) {
-                why = 13;
-                break;
-            }
-            drop((e >> 16) & 15);
-            if (e & kLit) {
-                if (pos >= olen) {
-                    why = 14;
+            room();
+            uint32_t p = peek();
+            uint32_t e = lookL(p);
+            if (e & (kLit | kEob | kExc)) {
+                if (e & kExc) {
+                    if (e & kBad) {
+                        why = 13;
+                        break;
+                    }
+                    uint32_t unused;
+                    e = uni(slow_decode(S, 0, p, unused));
+                    if (e & kBad) {
+                        why = 13;
+                        break;
+                    }
+                }
+                if (e & kLit) {
+                    if (x >= xend) {
+                        why = 14;
+                        break;
+                    }
+                    commit();
+                    pv = e >> 23;
+                    pa = (x + lane) & kWinMask;
+                    x++;
+                    bp += tot_of(e);
+                    maybe_flush();
+                    continue;
+                }
+                if (e & kEob) {
+                    bp += tot_of(e);
+                    commit();
                     break;
                 }
-                commit();
-                if (lane == 0) S.win[(ph + pos) & kWinMask] = (uint8_t)e;
-                pos++;
-                maybe_flush();
-                continue;
             }
-            if (e & kEob) {
-                commit();
-                break;
+            const uint32_t len = (e >> 23) + sbfe(p, e);
+            bp += tot_of(e);
+            p = peek();
+            uint32_t dv;
+            uint32_t d = lookD(p, dv);
+            uint32_t dist;
+            if (d & kExc) {
+                if (d & kBad) {
+                    why = 15;
+                    break;
+                }
+                d = uni(slow_decode(S, 1, p, dv));
+                if (d & kBad) {
+                    why = 15;
+                    break;
+                }
+                dv = uni(dv);
+                bp += d & 31;  // the code, then its extra bits from a fresh peek (they may be 13)
+                dist = dv + (peek() & ((1u << ((d >> 16) & 15)) - 1));
+                bp += (d >> 16) & 15;
+            } else {
+                dist = dv + sbfe(p, d);
+                bp += tot_of(d);
             }
-            const uint32_t len = (e & 0xFFFF) + getb((e >> 20) & 15);
-            refill();
-            uint32_t d = look(lut_d, (uint32_t)bb & ((1u << kDB) - 1));
-            if (d & kSlow) d = uni(slow_decode(S, 1, bb));
-            if (d & kBad) {
-                why = 15;
-                break;
-            }
-            drop((d >> 16) & 15);
-            const uint32_t dist = (d & 0xFFFF) + getb((d >> 20) & 15);
-            if (dist > pos) {  // "invalid distance too far back"
+            if (dist > x - ph) {  // "invalid distance too far back"
                 why = 16;
                 break;
             }
-            if (pos + len > olen) {
+            if (x + len > xend) {
                 why = 14;
                 break;
             }
+            commit();  // (this match may read the previous symbol's bytes)
             if (dist > kFar) {
                 // further back than the window keeps: the member's own output, already in HBM (x - fl
-                // stays <= 2,306 between flushes, so every source byte went out >= 1.5 KiB ago).  Every
+                // stays below 3.3 KiB between flushes, so every source byte went out earlier).  Every
                 // store of this wave has completed (s_waitcnt 0); the dwords are read at agent scope
                 // (from L2, never an older L1 line), staged in LDS, then placed bytewise.
-                commit();
                 __builtin_amdgcn_s_waitcnt(0);
-                const uint32_t sx = ph + pos - dist, s4 = sx & ~3u, nb = len + (sx - s4);
+                const uint32_t sx = x - dist, s4 = sx & ~3u, nb = len + (sx - s4);
                 uint32_t *const src32 = reinterpret_cast<uint32_t *>(gout + s4);
                 for (uint32_t k = lane; 4 * k < nb; k += 64)
                     S.far[k] = __hip_atomic_load(src32 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 __syncthreads();
                 const uint8_t *far8 = reinterpret_cast<const uint8_t *>(S.far) + (sx - s4);
-                for (uint32_t i = lane; i < len; i += 64) S.win[(ph + pos + i) & kWinMask] = far8[i];
+                for (uint32_t i = lane; i < len; i += 64) S.win[(x + i) & kWinMask] = far8[i];
                 __syncthreads();
-                pos += len;
+                x += len;
+                pa = (x + lane) & kWinMask;
+                pv = 0;
                 maybe_flush();
                 continue;
             }
-            commit();  // (this match may read the previous one's bytes)
-            const float rd = __builtin_amdgcn_rcpf((float)dist);  // (approximate: corrected below)
-            const uint32_t sbase = ph + pos - dist, dx = ph + pos;
-            auto src_of = [&](uint32_t i) -> uint32_t {
-                uint32_t si = i;
-                if (dist < 64) {  // the period-d pattern: i mod d
-                    const uint32_t qd = (uint32_t)((float)i * rd);
-                    int r = (int)i - (int)(qd * dist);
-                    if (r < 0) r += (int)dist;
-                    if (r >= (int)dist) r -= (int)dist;
-                    si = (uint32_t)r;
-                }
-                return (sbase + si) & kWinMask;
-            };
+            // source byte of output byte i: sbase + (i mod dist) (the period-dist pattern, which is
+            // also the plain copy when dist > i); (i + 0.5) / dist through an approximate reciprocal
+            // stays within 0.5 / dist of the exact quotient's distance to an integer, so the floor
+            // is exact for i < 258 and dist <= 4096
+            const float rd = __builtin_amdgcn_rcpf((float)dist);
+            const uint32_t sbase = x - dist;
+            const uint32_t q0 = (uint32_t)(lanef * rd);
+            const uint32_t s0 = (sbase + (uint32_t)lane - q0 * dist) & kWinMask;
             if (len <= 64) {  // read now, written after the next symbol's decode
-                if ((uint32_t)lane < len) pv = S.win[src_of((uint32_t)lane)];
-                pend_n = len;
-                pend_x = dx;
+                pv = S.win[s0];
+                pa = (x + lane) & kWinMask;
             } else {
                 for (uint32_t c = 0; c < len; c += 64) {
                     const uint32_t i = c + lane;
-                    if (i < len) {
-                        const uint8_t v = S.win[src_of(i)];
-                        S.win[(dx + i) & kWinMask] = v;
-                    }
+                    const uint32_t q = (uint32_t)(((float)c + lanef) * rd);
+                    const uint8_t v = S.win[(sbase + i - q * dist) & kWinMask];
+                    if (i < len) S.win[(x + i) & kWinMask] = v;
                 }
+                pa = (x + len + lane) & kWinMask;
+                pv = 0;
             }
-            pos += len;
+            x += len;
             maybe_flush();
         }
         if (!why && consumed_bytes() > plen_end) why = 17;  // (a block ran into the trailer)
     }
     if (!why && (uint64_t)consumed_bytes() != plen_end) why = 18;  // the trailer follows the stream
-    if (!why && pos != olen) why = 19;                               // ISIZE
+    if (!why && x != xend) why = 19;                                 // ISIZE
     if (!why) {
         commit();
         __syncthreads();
-        flush(ph + pos, true);
+        flush(x, true);
     }
     if (lane == 0) {
         mstat[m] = why;
@@ -609,24 +650,21 @@ __global__ void __launch_bounds__(64) k_crc32(const uint8_t *__restrict__ comp, 
         while (q < qe && (((uintptr_t)q) & 15)) c = (c >> 8) ^ T[0][(c ^ *q++) & 0xFF];
         // 64 B per step from 16 B-aligned loads, the next step's four loads in flight while this
         // step's 16 dwords go through the tables (a serial chain of loads was the kernel's cost)
+        // (named registers, not arrays: the arrays' loop-carried copies went to scratch)
         if (q + 64 <= qe) {
-            uint4 v[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) v[k] = reinterpret_cast<const uint4 *>(q)[k];
+            const uint4 *q4 = reinterpret_cast<const uint4 *>(q);
+            uint4 v0 = q4[0], v1 = q4[1], v2 = q4[2], v3 = q4[3];
             for (; q + 64 <= qe; q += 64) {
-                uint4 nx[4];
-                const bool more = q + 128 <= qe;
-#pragma unroll
-                for (int k = 0; k < 4; k++) nx[k] = more ? reinterpret_cast<const uint4 *>(q + 64)[k] : v[k];
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    step4(v[k].x);
-                    step4(v[k].y);
-                    step4(v[k].z);
-                    step4(v[k].w);
+                uint4 n0 = v0, n1 = v1, n2 = v2, n3 = v3;
+                if (q + 128 <= qe) {
+                    const uint4 *p4 = reinterpret_cast<const uint4 *>(q + 64);
+                    n0 = p4[0], n1 = p4[1], n2 = p4[2], n3 = p4[3];
                 }
-#pragma unroll
-                for (int k = 0; k < 4; k++) v[k] = nx[k];
+                step4(v0.x), step4(v0.y), step4(v0.z), step4(v0.w);
+                step4(v1.x), step4(v1.y), step4(v1.z), step4(v1.w);
+                step4(v2.x), step4(v2.y), step4(v2.z), step4(v2.w);
+                step4(v3.x), step4(v3.y), step4(v3.z), step4(v3.w);
+                v0 = n0, v1 = n1, v2 = n2, v3 = n3;
             }
         }
         for (; q + 4 <= qe; q += 4) step4(*reinterpret_cast<const uint32_t *>(q));
