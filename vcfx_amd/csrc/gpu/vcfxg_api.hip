@@ -151,7 +151,7 @@ struct vcfxg_ctx {
     // variant's missing samples and the sample-major contribution plane
     bool ld_sp = false;
     uint64_t ld_mp = 0;
-    DevBuf ld_moff, ld_midx, ld_mvar, ld_gt16;
+    DevBuf ld_moff, ld_midx, ld_mvar, ld_gt16, ld_sprec;
     // device BGZF inflate (vcfxg_ingest_bgzf): compressed bytes, member table, output offsets,
     // per-member status, first bad member
     DevBuf bgz_in, bgz_mem, bgz_off, bgz_stat, bgz_small;
@@ -321,7 +321,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16, &c->bgz_in, &c->bgz_mem, &c->bgz_off, &c->bgz_stat, &c->bgz_small})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16, &c->ld_sprec, &c->bgz_in, &c->bgz_mem, &c->bgz_off, &c->bgz_stat, &c->bgz_small})
         if (b->p) (void)hipFree(b->p);
     if (c->af_small.p) (void)hipFree(c->af_small.p);
     if (c->wk_stage.p) (void)hipFree(c->wk_stage.p);
@@ -2348,6 +2348,7 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
         const uint64_t mp = (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock * vcfxg::kLdFastBlock;
         r = ensure(c, c->ld_midx, 2 * entries + 16);
         if (!r) r = ensure(c, c->ld_mvar, 4 * entries + 16);
+        if (!r) r = ensure(c, c->ld_sprec, sizeof(vcfxg::LdSpRec) * (M + 1));
         if (!r) r = ensure(c, c->ld_gt16, 2 * (size_t)n_samples * mp + 64);
         if (r == VCFXG_E_NOMEM) r = sparse_to_mask();
         if (r) return r;
@@ -2358,6 +2359,8 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
                                              P<uint16_t>(c->ld_midx), P<uint32_t>(c->ld_mvar), c->stream));
         HIPCHK(c, vcfxg::launch_ld_gt16(P<int8_t>(c->ld_Gc), M, kpad, n_samples, mp, P<uint16_t>(c->ld_gt16),
                                         c->stream));
+        HIPCHK(c, vcfxg::launch_ld_sprec(P<vcfxg::LdVar>(c->ld_vars), M, n_samples, P<vcfxg::LdSpRec>(c->ld_sprec),
+                                         c->stream));
         c->ld_mp = mp;
         prof_end(c, "ld_sparse_prep");
     }
@@ -2568,6 +2571,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
         spa.moff = P<uint64_t>(c->ld_moff);
         spa.midx = P<uint16_t>(c->ld_midx);
         spa.mvar = P<uint32_t>(c->ld_mvar);
+        spa.rec = P<vcfxg::LdSpRec>(c->ld_sprec);
         const double big = 4.0 * (double)c->ld_ns * (double)c->ld_ns;  // (k_ld_mask's bound)
         spa.pe = (float)(big * std::ldexp(1.0, -23) + 1.0);
     }
@@ -2621,6 +2625,12 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     HIPCHK(c, hipMemcpyAsync(&tot, rowbase + rows, 8, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipMemcpyAsync(sctr, c->ld_stage_ctr.p, 24, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (getenv("VCFXG_LD_DEBUG")) {  // (with a VCFXG_LD_EXPT & 256 build: the sparse kernel's half counts)
+        uint64_t dbg[3] = {0, 0, 0};
+        (void)hipMemcpy(dbg, P<unsigned long long>(c->ld_stage_ctr) + 4, 24, hipMemcpyDeviceToHost);
+        fprintf(stderr, "ld_sparse: halves %llu, with tables %llu, prefilter candidates %llu\n",
+                (unsigned long long)dbg[0], (unsigned long long)dbg[1], (unsigned long long)dbg[2]);
+    }
     const uint64_t np = tot;
     const bool staged = stg.temp && (sctr[2] & 0xFFFFFFFFull) == 0;  // staged, no overflow
     c->ld_temp_cap = std::max<uint64_t>(c->ld_temp_cap, sctr[0] + sctr[0] / 4);

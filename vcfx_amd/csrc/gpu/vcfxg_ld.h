@@ -149,6 +149,10 @@ hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, int ns, int sparse, u
 // the sparse-missing form of k_ld_fast (vcfxg_ld_fast.hip, kSp): per variant its missing samples
 // (CSR: moff[v] .. moff[v + 1] into midx = sample, mvar = v) and the sample-major contribution
 // plane gt16[s * mp + v] = c(code): x | x^2 << 5 | missing << 11 (x = 0 for a missing call)
+struct LdSpRec {
+    uint64_t pk;   // missing count | Sx << 8 | Sx2 << 32
+    double varx;   // LdVar::varx
+};
 struct LdSparse {
     const LdVar *vars = nullptr;
     const uint16_t *gt16 = nullptr;
@@ -157,9 +161,13 @@ struct LdSparse {
     const uint16_t *midx = nullptr;
     const uint32_t *mvar = nullptr;
     float pe = 0.f;            // the fp32 prefilter's error bound (as k_ld_mask)
+    // per variant (m + 1 entries, the last zero): the packed (missing count, Sx, Sx2) and the own
+    // variance, DMA'd into LDS with the first k-slices (k_ld_sprec)
+    const LdSpRec *rec = nullptr;
 };
 hipError_t launch_ld_miss_fill(const int8_t *Gc, uint64_t m, int kpad, int ns, const uint64_t *moff, uint16_t *midx,
                                uint32_t *mvar, hipStream_t s);
+hipError_t launch_ld_sprec(const LdVar *vars, uint64_t m, int ns, LdSpRec *rec, hipStream_t s);
 hipError_t launch_ld_gt16(const int8_t *Gc, uint64_t m, int kpad, int ns, uint64_t mp, uint16_t *gt16, hipStream_t s);
 hipError_t launch_ld_sparse(int pass, const uint8_t *Gp, const LdSparse &sp, const uint32_t *chrom_id,
                             const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,

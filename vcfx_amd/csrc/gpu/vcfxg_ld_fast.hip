@@ -34,7 +34,9 @@
 // VCFXG_LD_EXPT (diagnostic builds only, results invalid): bit 0 skips the epilogue, bit 3
 // stages k-slice 0 every step, bit 4 reads rows 0..255 for every block; sparse epilogue: bit 5
 // skips the missing-entry gathers, bit 6 the per-pair prefilter, bit 7 the tables and exact
-// pairs after the prefilter
+// pairs after the prefilter, bit 8 counts halves / halves with tables / candidates (VCFXG_LD_DEBUG),
+// bit 9 skips the exact pass on the candidates, bit 10 the tables (zeroing and gathers), bit 11 both
+// behind a run-time test (the code stays in the kernel)
 #ifndef VCFXG_LD_EXPT
 #define VCFXG_LD_EXPT 0
 #endif
@@ -243,9 +245,16 @@ constexpr int kSpC = 256 * 128 * 2;
 constexpr int kSpRC = kSpC + 128 * kSpCStride * 2;  // 132,096 B (the ring and the dense terms)
 constexpr int kSpInts = kRing + kFB * 32;         // per row / column packed sums (the records' area)
 static_assert(kSpRC <= kSpInts, "R and C must not reach the packed sums");
-static_assert(kSpInts + 2 * kFB * 8 <= kRing + kFB * 32 + 2 * kFvBytes, "packed sums fit the records' area");
+// (the tile's 512 LdSpRec records, 16 B each: 8 KiB, DMA'd with the first k-slices as the dense
+// kernel's LdFast records, so the epilogue starts without a global load)
+constexpr int kSpRecBytes = 2 * kFB * (int)sizeof(LdSpRec);
+static_assert(kSpRecBytes == 8 * 1024, "one 1 KiB piece per wave");
 // the prefilter's per-row (5) and per-column (3) fp32 terms and the block maxima, after them
-constexpr int kSpTerms = kSpInts + 2 * kFB * 8;
+constexpr int kSpTerms = kSpInts + kSpRecBytes;
+// the exact pass's per-wave work list over the terms once the prefilter is done: 4 waves per half,
+// kSpList 8 B entries (then, for the emit, kSpList destinations after them)
+constexpr int kSpList = 128;
+static_assert(4 * kSpList * 16 <= 8 * kFB * 4, "the work lists fit the prefilter terms");
 static_assert(kSpTerms + 8 * kFB * 4 + 16 <= kRing + kFB * 32 + 2 * kFvBytes, "prefilter terms fit the records' area");
 
 // a row's / column's (missing count, Sx, Sx2) packed for one 64-bit LDS read
@@ -283,8 +292,15 @@ __device__ __forceinline__ void ld_sparse_prefilter(const v16f (&acc)[2][4], int
         const bool row = t < kFB;
         const int64_t v = row ? ibase + t : jbase + (t - kFB);
         const bool vok = v < M;
-        LdVar x{};
-        if (vok) x = sp.vars[v];
+        const LdSpRec rc = reinterpret_cast<const LdSpRec *>(lds + kSpInts)[t];  // (zero past M)
+        struct {
+            int cnt, sx, sx2;
+            double varx;
+        } x;
+        x.cnt = a.ns - (int)(rc.pk & 0xFF);
+        x.sx = (int)((rc.pk >> 8) & 0xFFFFFF);
+        x.sx2 = (int)(rc.pk >> 32);
+        x.varx = rc.varx;
         const int mv = vok ? a.ns - x.cnt : 0;
         const int xs = x.sx2 != x.sx ? 2 : 1;
         atomicMax(&mx[row ? 0 : 1], mv);
@@ -391,22 +407,13 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
     const int wi = w >> 1, wj = w & 1;
     const int64_t M = (int64_t)a.m;
     const int64_t ibase = (int64_t)I4 * kFB, jbase = (int64_t)J4 * kFB;
-    uint64_t *pk = reinterpret_cast<uint64_t *>(lds + kSpInts);  // [256 rows][256 columns]
-    {
-        const int64_t v = t < kFB ? ibase + t : jbase + (t - kFB);
-        uint64_t q = 0;
-        if (v < M) {
-            const LdVar x = sp.vars[v];
-            q = sp_pack(a.ns - x.cnt, x.sx, x.sx2);
-        }
-        pk[t] = q;
-    }
+    // the tile's records ([256 rows][256 columns], DMA'd): packed sums and own variances
+    const LdSpRec *rec = reinterpret_cast<const LdSpRec *>(lds + kSpInts);
     uint32_t *R32 = reinterpret_cast<uint32_t *>(lds + kSpR);
     uint32_t *C32 = reinterpret_cast<uint32_t *>(lds + kSpC);
     const uint16_t *R16 = reinterpret_cast<const uint16_t *>(lds + kSpR);
     const uint16_t *C16 = reinterpret_cast<const uint16_t *>(lds + kSpC);
     const uint64_t bI = 4ull * I4 + wi;
-    const int64_t i0 = (int64_t)bI * kLdBlock;
     // ---- the prefilter, on every wave's own accumulators (before the tables): a bound on the
     // pair's r^2 from the per-variant sums and the block's largest missing counts, in the
     // register epilogue's packed form; only halves holding a candidate build the tables
@@ -414,14 +421,20 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
     ld_sparse_prefilter(acc, lds, a, sp, I4, J4, cbm);
     // Sxy <= 4 ns < 2^16 (ns <= 16383, launch_ld_sparse): the accumulators as u16 pairs, half the
     // registers through the rest of the epilogue
+    // (only a wave holding a candidate reads them: nearly every wave of a tile away from the
+    // diagonal holds none and skips the packing, as it skips every per-pair step below)
     uint32_t accp[2][4][8];
+    uint32_t cor = 0;
 #pragma unroll
-    for (int x = 0; x < 2; x++)
+    for (int y = 0; y < 4; y++) cor |= cbm[y][0] | cbm[y][1];
+    if (__builtin_amdgcn_ballot_w64(cor != 0u) != 0)
 #pragma unroll
-        for (int y = 0; y < 4; y++)
+        for (int x = 0; x < 2; x++)
 #pragma unroll
-            for (int q = 0; q < 8; q++)
-                accp[x][y][q] = (uint32_t)(int)acc[x][y][2 * q] | ((uint32_t)(int)acc[x][y][2 * q + 1] << 16);
+            for (int y = 0; y < 4; y++)
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    accp[x][y][q] = (uint32_t)(int)acc[x][y][2 * q] | ((uint32_t)(int)acc[x][y][2 * q + 1] << 16);
     // the row entries are contiguous in the CSR (rows ibase .. ibase + 255)
     const uint64_t re0 = sp.moff[ibase], re1 = sp.moff[ibase + kFB < M ? ibase + kFB : M];
     for (int hp = 0; hp < 2; hp++) {
@@ -431,7 +444,18 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
 #pragma unroll
             for (int y = 0; y < 4; y++) anyc |= cbm[y][0] | cbm[y][1];
         // (no candidate in the half: no tables; its counts are written as 0 below)
-        const bool tables = __syncthreads_or(anyc != 0u) && !(VCFXG_LD_EXPT & 128);
+        const bool tables = __syncthreads_or(anyc != 0u) && !(VCFXG_LD_EXPT & (128 | 1024)) &&
+                            !((VCFXG_LD_EXPT & 2048) && a.ns >= 0);
+        if ((VCFXG_LD_EXPT & 256) && P == 1) {  // (diagnostic: halves, halves with tables, candidates)
+            if (t == 0) {
+                atomicAdd(st.ctr + 4, 1ull);
+                if (tables) atomicAdd(st.ctr + 5, 1ull);
+            }
+            const int nca = wave_sum(wj == hp ? (int)(__popc(cbm[0][0]) + __popc(cbm[0][1]) + __popc(cbm[1][0]) +
+                                                      __popc(cbm[1][1]) + __popc(cbm[2][0]) + __popc(cbm[2][1]) +
+                                                      __popc(cbm[3][0]) + __popc(cbm[3][1])) : 0);
+            if (l == 0 && nca) atomicAdd(st.ctr + 6, (unsigned long long)nca);
+        }
         if (tables) {
         for (int k = t * 16; k < kSpRC; k += kWaves * kWave * 16) *reinterpret_cast<uint4 *>(lds + k) = make_uint4(0, 0, 0, 0);
         __syncthreads();
@@ -488,59 +512,155 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
         }
         if (wj == hp) {
             // the pairs of this wave: column j = jb + 32y + r, rows i0 + 32x + 8g + 4h + e; per
-            // (y, x) the prefilter's 16-bit candidate mask over k = 4g + e, and on its candidates
-            // the exact decision (the six sums from the tables, mask_r2's fp64 sequence)
-            uint32_t pass[4][2];
+            // (y, x) the prefilter's 16-bit candidate mask over k = 4g + e.  The exact work (the six
+            // sums from the tables, mask_r2's fp64 sequence) is spread over the wave's 64 lanes: a
+            // lane's candidates are listed in LDS (row, column, Sxy) in rank order and every lane
+            // takes every 64th entry, so a half whose candidates crowd a few columns (pairs inside an
+            // LD block) costs total / 64 sequences, not the busiest lane's count
+            uint2 *lst = reinterpret_cast<uint2 *>(lds + kSpTerms + wi * kSpList * 16);  // (the dead terms)
             int64_t jv[4];
             bool jokv[4];
-            // one pair's six sums, k a run-time index (Sxy picked from the packed accumulators by a
-            // select chain: no dynamic register indexing), for the rare per-candidate loops
-            auto sums_rt = [&](int x, int y, int k, int &n, int &sx, int &sy, int &sxy, int &sxx, int &syy) {
-                const int jj = 32 * y + r;
-                const int il = wi * 64 + 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
-                const uint64_t pi = pk[il], pj = pk[kFB + 128 * hp + jj];
-                const uint32_t rv = R16[il * 128 + jj];
-                const uint32_t cv = C16[jj * kSpCStride + il];
-                n = a.ns - (int)(pi & 0xFF) - (int)(pj & 0xFF) + (int)(rv >> 11);
-                sx = (int)((pi >> 8) & 0xFFFFFF) - (int)(cv & 31);
-                sxx = (int)(pi >> 32) - (int)((cv >> 5) & 63);
-                sy = (int)((pj >> 8) & 0xFFFFFF) - (int)(rv & 31);
-                syy = (int)(pj >> 32) - (int)((rv >> 5) & 63);
-                // (a select tree on the bits of k >> 1: a select chain on its value was turned
-                // into an indexed load, the packed accumulators moved to scratch -- 256 B per lane
-                // per block written to memory)
-                const int q = k >> 1;
-                const bool q1 = (q & 1) != 0, q2 = (q & 2) != 0, q4 = (q & 4) != 0;
-                const uint32_t a0 = q1 ? accp[x][y][1] : accp[x][y][0], a1 = q1 ? accp[x][y][3] : accp[x][y][2];
-                const uint32_t a2 = q1 ? accp[x][y][5] : accp[x][y][4], a3 = q1 ? accp[x][y][7] : accp[x][y][6];
-                const uint32_t b0 = q2 ? a1 : a0, b1 = q2 ? a3 : a2;
-                const uint32_t v = q4 ? b1 : b0;
-                sxy = (int)((v >> (16 * (k & 1))) & 0xFFFFu);
-            };
 #pragma unroll
             for (int y = 0; y < 4; y++) {
-                const int64_t j = jb + 32 * y + r;
-                jv[y] = j;
-                jokv[y] = j < M && j >= (int64_t)a.j_lo && j < (int64_t)a.j_hi;
+                jv[y] = jb + 32 * y + r;
+                jokv[y] = jv[y] < M && jv[y] >= (int64_t)a.j_lo && jv[y] < (int64_t)a.j_hi;
+            }
+            // Sxy of (x, y, k) from the packed accumulators, all three run-time indices (a select tree
+            // on their bits: a select chain on a value was once turned into an indexed load, the packed
+            // accumulators moved to scratch -- 256 B per lane per block written to memory)
+            auto sxy_of = [&](int x, int y, int k) -> uint32_t {
+                const int q = k >> 1;
+                uint32_t v4[2][4];
 #pragma unroll
-                for (int x = 0; x < 2; x++) {
-                    const uint32_t cb = (VCFXG_LD_EXPT & 128) ? 0u : cbm[y][x];
-                    uint32_t pb = 0;
-                    for (uint32_t mm = cb; mm; mm &= mm - 1u) {  // (rare at useful thresholds)
-                        const int k = __builtin_ctz(mm);
-                        const int64_t i = i0 + 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
-                        if (a.max_dist > 0 && chrom_id[i] == chrom_id[j]) {
-                            int d = sp.vars[j].pos - sp.vars[i].pos;
-                            if (d < 0) d = -d;
-                            if (d > a.max_dist) continue;
-                        }
-                        int n, sx, sy, sxy, sxx, syy;
-                        sums_rt(x, y, k, n, sx, sy, sxy, sxx, syy);
-                        if (mask_r2(sp.vars[i].varx, sp.vars[j].varx, n, sx, sy, sxy, sxx, syy) >= a.threshold)
-                            pb |= 1u << k;
+                for (int xx = 0; xx < 2; xx++)
+#pragma unroll
+                    for (int yy = 0; yy < 4; yy++) {
+                        const uint32_t a0 = (q & 1) ? accp[xx][yy][1] : accp[xx][yy][0];
+                        const uint32_t a1 = (q & 1) ? accp[xx][yy][3] : accp[xx][yy][2];
+                        const uint32_t a2 = (q & 1) ? accp[xx][yy][5] : accp[xx][yy][4];
+                        const uint32_t a3 = (q & 1) ? accp[xx][yy][7] : accp[xx][yy][6];
+                        const uint32_t b0 = (q & 2) ? a1 : a0, b1 = (q & 2) ? a3 : a2;
+                        v4[xx][yy] = (q & 4) ? b1 : b0;
                     }
-                    pass[y][x] = pb;
+                uint32_t vx[4];
+#pragma unroll
+                for (int yy = 0; yy < 4; yy++) vx[yy] = x ? v4[1][yy] : v4[0][yy];
+                const uint32_t c0 = (y & 1) ? vx[1] : vx[0], c1 = (y & 1) ? vx[3] : vx[2];
+                const uint32_t v = (y & 2) ? c1 : c0;
+                return (v >> (16 * (k & 1))) & 0xFFFFu;
+            };
+            // a listed pair (il: row in the tile, jl: column in the half, Sxy): its r^2 (mask_r2) and
+            // whether it is kept (max_dist, threshold)
+            auto exact = [&](uint32_t d0, double &r2) -> bool {
+                const int il = (int)(d0 & 0xFF), jl = (int)((d0 >> 8) & 0x7F), sxy = (int)(d0 >> 16);
+                const int jt = kFB + 128 * hp + jl;
+                const LdSpRec ri = rec[il], rj = rec[jt];
+                const uint32_t rv = R16[il * 128 + jl];
+                const uint32_t cv = C16[jl * kSpCStride + il];
+                const int n = a.ns - (int)(ri.pk & 0xFF) - (int)(rj.pk & 0xFF) + (int)(rv >> 11);
+                const int sx = (int)((ri.pk >> 8) & 0xFFFFFF) - (int)(cv & 31);
+                const int sxx = (int)(ri.pk >> 32) - (int)((cv >> 5) & 63);
+                const int sy = (int)((rj.pk >> 8) & 0xFFFFFF) - (int)(rv & 31);
+                const int syy = (int)(rj.pk >> 32) - (int)((rv >> 5) & 63);
+                if (a.max_dist > 0) {
+                    const int64_t i = ibase + il, j = jb + jl;
+                    if (chrom_id[i] == chrom_id[j]) {
+                        int d = sp.vars[j].pos - sp.vars[i].pos;
+                        if (d < 0) d = -d;
+                        if (d > a.max_dist) return false;
+                    }
                 }
+                r2 = mask_r2(ri.varx, rj.varx, n, sx, sy, sxy, sxx, syy);
+                return r2 >= a.threshold;
+            };
+            // (the row of bit k of mask (y, x) in the wave's 64)
+            auto row_of = [&](int x, int k) { return 32 * x + 8 * (k >> 2) + 4 * h + (k & 3); };
+            // Lane-parallel passes over per-lane pair sets, one 32-bit word per column y (bit b: x = b
+            // >> 4, k = b & 15).  In rounds, every lane with a pair left lists its next one (slot from
+            // a ballot), so the list fills kWave entries per round however unevenly the lanes hold
+            // pairs; put(y, b, slot) lists a pair, run(e) handles entry e on lane e % 64, get(y, b,
+            // slot) replays the rounds on the owning lanes to read the outcome back
+            auto spread = [&](const uint32_t (&W)[4], auto put, auto run, auto get) {
+                if (__builtin_amdgcn_ballot_w64((W[0] | W[1] | W[2] | W[3]) != 0u) == 0) return;  // (usual)
+                auto word = [&](int y) {
+                    const uint32_t c0 = (y & 1) ? W[1] : W[0], c1 = (y & 1) ? W[3] : W[2];
+                    return (y & 2) ? c1 : c0;
+                };
+                auto adv = [&](int &y, uint32_t &rm) {
+                    while (rm == 0u && y < 3) rm = word(++y);
+                };
+                auto rounds = [&](int &y, uint32_t &rm, auto fn) {
+                    int n = 0;
+#pragma unroll
+                    for (int rd = 0; rd < kSpList / kWave; rd++) {
+                        const uint64_t bl = __builtin_amdgcn_ballot_w64(rm != 0u);
+                        if (bl == 0) break;  // (wave-uniform)
+                        if (rm != 0u) {
+                            const int e = n + (int)__builtin_amdgcn_mbcnt_hi(
+                                                  (uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+                            fn(y, __builtin_ctz(rm), e);
+                            rm &= rm - 1u;
+                            adv(y, rm);
+                        }
+                        n += __popcll(bl);
+                    }
+                    return n;
+                };
+                int y = 0;
+                uint32_t rm = W[0];
+                adv(y, rm);
+                for (;;) {
+                    int yr = y;
+                    uint32_t rr = rm;
+                    const int n = rounds(y, rm, put);
+                    if (n == 0) break;  // (wave-uniform)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    for (int e = l; e < n; e += kWave) run(e);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    rounds(yr, rr, get);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();  // (the list is rewritten by the next chunk)
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                }
+            };
+            // the exact decision on every candidate
+            uint32_t passW[4];
+            {
+                uint32_t candW[4];
+#pragma unroll
+                for (int y = 0; y < 4; y++) {
+                    candW[y] = (VCFXG_LD_EXPT & (128 | 512)) || ((VCFXG_LD_EXPT & 2048) && a.ns >= 0)
+                                   ? 0u
+                                   : cbm[y][0] | cbm[y][1] << 16;
+                    passW[y] = 0;
+                }
+                spread(
+                    candW,
+                    [&](int y, int b, int e) {
+                        const int x = b >> 4, k = b & 15;
+                        lst[e] = make_uint2((uint32_t)(wi * 64 + row_of(x, k)) | (uint32_t)(32 * y + r) << 8 |
+                                                sxy_of(x, y, k) << 16,
+                                            0u);
+                    },
+                    [&](int e) {
+                        double r2;
+                        lst[e].y = exact(lst[e].x, r2) ? 1u : 0u;
+                    },
+                    [&](int y, int b, int e) {
+                        const uint32_t bit = lst[e].y ? 1u << b : 0u;
+#pragma unroll
+                        for (int yy = 0; yy < 4; yy++) passW[yy] |= yy == y ? bit : 0u;
+                    });
+            }
+            uint32_t pass[4][2];
+#pragma unroll
+            for (int y = 0; y < 4; y++) {
+                pass[y][0] = passW[y] & 0xFFFFu;
+                pass[y][1] = passW[y] >> 16;
             }
             // the column's 64-row mask (both lanes h of column r hold it): row = 32x + 8g + 4h + e
             auto full_of = [&](int y) {
@@ -549,26 +669,8 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                 for (int x = 0; x < 2; x++)
 #pragma unroll
                     for (int k = 0; k < 16; k++)
-                        if ((pass[y][x] >> k) & 1u) m64 |= 1ull << (32 * x + 8 * (k >> 2) + 4 * h + (k & 3));
+                        if ((pass[y][x] >> k) & 1u) m64 |= 1ull << row_of(x, k);
                 return m64 | (uint64_t)__shfl_xor((long long)m64, 32);
-            };
-            // every passing pair of this lane to dst + its rank among the column's passing rows
-            auto emit = [&](int y, uint64_t fm, LdPair *dst) {
-                const int64_t j = jv[y];
-#pragma unroll
-                for (int x = 0; x < 2; x++)
-                    for (uint32_t mm = pass[y][x]; mm; mm &= mm - 1u) {
-                        const int k = __builtin_ctz(mm);
-                        const int row = 32 * x + 8 * (k >> 2) + 4 * h + (k & 3);
-                        int n, sx, sy, sxy, sxx, syy;
-                        sums_rt(x, y, k, n, sx, sy, sxy, sxx, syy);
-                        const int64_t i = i0 + row;
-                        LdPair pr;
-                        pr.i = (uint32_t)i;
-                        pr.j = (uint32_t)j;
-                        pr.r2 = mask_r2(sp.vars[i].varx, sp.vars[j].varx, n, sx, sy, sxy, sxx, syy);
-                        dst[__popcll(fm & ((1ull << row) - 1ull))] = pr;
-                    }
             };
             auto slot_of = [&](int y, uint64_t &slot) {  // the count-table slot of (bI, column j's 64-block)
                 const uint64_t bJ = 4ull * J4 + 2 * hp + (y >> 1);
@@ -577,15 +679,22 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                 slot = bI - ifirst;
                 return bI >= ifirst && bI <= bJ;
             };
+            // each passing pair's destination: dst[y] + its rank among the column's passing rows
             int nc[4];
+            LdPair *dst[4] = {nullptr, nullptr, nullptr, nullptr};
+            uint64_t fmv[4];
+            uint32_t por = 0;
+#pragma unroll
+            for (int y = 0; y < 4; y++) por |= pass[y][0] | pass[y][1];
+            const bool wpass = __builtin_amdgcn_ballot_w64(por != 0u) != 0;  // (wave-uniform)
 #pragma unroll
             for (int y = 0; y < 4; y++) {
                 uint64_t slot;
                 const bool in = jokv[y] && slot_of(y, slot);
-                const uint64_t fm = full_of(y);
-                nc[y] = in ? __popcll(fm) : 0;
+                fmv[y] = wpass ? full_of(y) : 0ull;
+                nc[y] = in ? __popcll(fmv[y]) : 0;
                 if (P == 1 && h == 0 && in) cnt[(uint64_t)(jv[y] - (int64_t)a.j_lo) * a.nb + slot] = (uint16_t)nc[y];
-                if (P == 2 && nc[y]) emit(y, fm, pairs + off.at((uint64_t)(jv[y] - (int64_t)a.j_lo), a.nb, slot));
+                if (P == 2 && nc[y]) dst[y] = pairs + off.at((uint64_t)(jv[y] - (int64_t)a.j_lo), a.nb, slot);
             }
             if (P == 1 && st.temp) {
                 // quarters (64 columns: y = 2hy, 2hy + 1) holding pairs, staged as k_ld_fast's count
@@ -608,7 +717,7 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                     for (int yy = 0; yy < 2; yy++) {
                         const int y = 2 * hy + yy;
                         const uint32_t run = (uint32_t)__shfl((int)(incl - c), 32 * yy + r);  // column 32yy + r
-                        if (nc[y]) emit(y, full_of(y), st.temp + base + run);
+                        if (nc[y]) dst[y] = st.temp + base + run;
                     }
                     if (l == 0) {
                         const unsigned long long q = atomicAdd(st.ctr + 1, 1ull);
@@ -617,6 +726,37 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                         else atomicOr(st.overflow, 1u);
                     }
                 }
+            }
+            if (P == 2 || st.temp) {
+                // the passing pairs with a destination, their r^2 recomputed lane-parallel and written
+                uint32_t emitW[4];
+#pragma unroll
+                for (int y = 0; y < 4; y++) emitW[y] = dst[y] ? passW[y] : 0u;
+                uint64_t *dl = reinterpret_cast<uint64_t *>(lst) + kSpList;  // (the list's second half)
+                spread(
+                    emitW,
+                    [&](int y, int b, int e) {
+                        const int x = b >> 4, k = b & 15;
+                        const int row = row_of(x, k);
+                        LdPair *const d0 = (y & 1) ? dst[1] : dst[0], *const d1 = (y & 1) ? dst[3] : dst[2];
+                        const uint64_t f0 = (y & 1) ? fmv[1] : fmv[0], f1 = (y & 1) ? fmv[3] : fmv[2];
+                        LdPair *const d = ((y & 2) ? d1 : d0) + __popcll(((y & 2) ? f1 : f0) & ((1ull << row) - 1ull));
+                        lst[e] = make_uint2((uint32_t)(wi * 64 + row) | (uint32_t)(32 * y + r) << 8 |
+                                                sxy_of(x, y, k) << 16,
+                                            0u);
+                        dl[e] = (uint64_t)(uintptr_t)d;
+                    },
+                    [&](int e) {
+                        const uint32_t d0 = lst[e].x;
+                        double r2 = 0.0;
+                        (void)exact(d0, r2);
+                        LdPair pr;
+                        pr.i = (uint32_t)(ibase + (d0 & 0xFF));
+                        pr.j = (uint32_t)(jb + ((d0 >> 8) & 0x7F));
+                        pr.r2 = r2;
+                        *reinterpret_cast<LdPair *>((uintptr_t)dl[e]) = pr;
+                    },
+                    [&](int, int, int) {});
             }
         }
         __syncthreads();  // R and C are zeroed again for the next half
@@ -683,6 +823,12 @@ __global__ __launch_bounds__(kWaves * kWave) void k_ld_fast(const uint8_t *__res
             const char *s = reinterpret_cast<const char *>(fv + (side ? jbase : ibase)) + part * 1024 + l * 16;
             glds16(s < fv_end ? s : fv_end - 16, lds + kRing + kFB * 32 + side * kFvBytes + part * 1024);
         }
+    }
+    if (kSp) {  // the I and J sparse records: 8 KiB, one 1 KiB piece per wave (clamped to the zero
+        // record at M: rows / columns outside the matrix)
+        const int side = w >> 2, part = w & 3;
+        const int64_t v = (side ? jbase : ibase) + part * 64 + l;
+        glds16(reinterpret_cast<const char *>(sp.rec + (v < M ? v : M)), lds + kSpInts + w * 1024);
     }
     const int kpad = a.kp4;  // FP4 row bytes
     // staging: 32 wave-instructions of 1 KiB per stage, kGlds per wave; instruction q of
@@ -985,7 +1131,7 @@ hipError_t launch_ld_sparse(int pass, const uint8_t *Gp, const LdSparse &sp, con
                             const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
                             LdOffsets off, LdPair *pairs, const LdStage &st, hipStream_t s) {
     if (!nblocks) return hipSuccess;
-    if (a.kp4 % kBK || a.kp4 <= 0 || a.ns > 16383 || !sp.gt16 || !sp.vars || sp.mp % kFB) return hipErrorInvalidValue;
+    if (a.kp4 % kBK || a.kp4 <= 0 || a.ns > 16383 || !sp.gt16 || !sp.vars || !sp.rec || sp.mp % kFB) return hipErrorInvalidValue;
     if (pass == 1)
         hipLaunchKernelGGL((k_ld_fast<1, true>), dim3(nblocks), dim3(kWaves * kWave), 0, s, Gp, nullptr, chrom_id, a,
                            blocks, nblocks, cnt, off, pairs, st, sp);
@@ -1195,6 +1341,26 @@ __global__ __launch_bounds__(256) void k_ld_gt16(const int8_t *__restrict__ Gc, 
     uint4 *dst = reinterpret_cast<uint4 *>(gt16 + (uint64_t)(s0 + ss) * mp + v0 + vv);
     dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
     dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+// the sparse kernel's per-variant records (entry m: zeros, the rows / columns past the matrix)
+__global__ __launch_bounds__(256) void k_ld_sprec(const LdVar *__restrict__ vars, uint64_t m, int ns,
+                                                  LdSpRec *__restrict__ rec) {
+    for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v <= m; v += (uint64_t)gridDim.x * 256) {
+        LdSpRec r{0, 0.0};
+        if (v < m) {
+            const LdVar x = vars[v];
+            r.pk = sp_pack(ns - x.cnt, x.sx, x.sx2);
+            r.varx = x.varx;
+        }
+        rec[v] = r;
+    }
+}
+
+hipError_t launch_ld_sprec(const LdVar *vars, uint64_t m, int ns, LdSpRec *rec, hipStream_t s) {
+    hipLaunchKernelGGL(k_ld_sprec, dim3((unsigned)std::min<uint64_t>(m / 256 + 1, 4096)), dim3(256), 0, s, vars, m, ns,
+                       rec);
+    return hipGetLastError();
 }
 
 hipError_t launch_ld_gt16(const int8_t *Gc, uint64_t m, int kpad, int ns, uint64_t mp, uint16_t *gt16, hipStream_t s) {
