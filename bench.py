@@ -660,13 +660,13 @@ def main():
         W = a.window
 
         def step():
-            eng.index(ds)
-            m = eng.ld_prepare(a.samples)
+            m = eng.ld_prepare_region(ds, a.samples)  # (the LD walk: no separate index sweep)
             np_, tb = eng.ld_stream_chunk(0, m, W, a.threshold)
             if red is not None:
                 allreduce_counts([m, np_, tb, 0])
             return m, np_, tb
-        kern_names = ("line_count", "line_emit", "line_compact", "ld_parse", "ld_compact", "ld_pack_vq", "ld_count",
+        kern_names = ("line_count", "line_emit", "line_compact", "ld_walk", "ld_parse", "ld_compact", "ld_pack", "ld_gather",
+                      "ld_sparse_prep", "ld_pack_vq", "ld_count",
                       "ld_emit", "ld_count_sparse", "ld_count_mask", "ld_emit_mask", "ld_count_gen", "ld_emit_gen",
                       "ld_text")
 

@@ -112,6 +112,13 @@ typedef struct {
 } vcfxg_bgzf_member;
 int vcfxg_ingest_bgzf(vcfxg_ctx *ctx, const void *comp, size_t comp_n, const vcfxg_bgzf_member *members,
                       size_t n_members, const char *head, size_t head_n, uint64_t *bad_member);
+/* The compressed bytes for vcfxg_ingest_bgzf copied to the device piece by piece while the caller
+ * still reads the file (a pinned staging ring): bytes [offset, offset + n) of a comp_total-byte
+ * stream, in order (offset 0 first; each piece starts where the last ended), asynchronous;
+ * vcfxg_ingest_wait(ctx, offset + n) waits for the copy (the host buffer may then be reused).
+ * Between vcfxg_ingest_begin and vcfxg_ingest_bgzf, which then takes comp = NULL and
+ * comp_n = comp_total. */
+int vcfxg_bgzf_stage(vcfxg_ctx *ctx, const void *host, size_t n, size_t offset, size_t comp_total);
 /* page-locked host memory (H2D at the full PCIe rate, asynchronous), for staging rings */
 int vcfxg_host_alloc(vcfxg_ctx *ctx, size_t n, void **out);
 void vcfxg_host_free(vcfxg_ctx *ctx, void *p);
@@ -342,6 +349,15 @@ int vcfxg_variant_count(vcfxg_ctx *ctx, int strip_cr, vcfxg_summary *out);
  * LDVariantOpt::computeStats :243-258. */
 int vcfxg_ld_prepare(vcfxg_ctx *ctx, int n_samples, int id_dot_to_pos, const char *region_chrom, size_t region_len,
                      int has_region, int region_start, int region_end, int parse_mode, uint64_t *n_variants);
+/* vcfxg_index(data_start) + vcfxg_ld_prepare in one call, with the same variants, codes, sums and
+ * prefixes.  For records averaging >= 512 B and n_samples <= 4096 the device walks the records
+ * without a separate index sweep (one HBM pass) and synchronises with the host once; other
+ * inputs take the two calls.  The context is NOT indexed afterwards (call vcfxg_index before
+ * vcfxg_line_ends or a per-line call); vcfxg_ld_stream_chunk / vcfxg_ld_fetch_pairs follow as
+ * after vcfxg_ld_prepare.  Replaces the same reference code as the two calls it fuses. */
+int vcfxg_ld_prepare_region(vcfxg_ctx *ctx, size_t data_start, int n_samples, int id_dot_to_pos,
+                            const char *region_chrom, size_t region_len, int has_region, int region_start,
+                            int region_end, int parse_mode, uint64_t *n_variants);
 /* parse_mode: 0 = fastParseInt POS + parseGenotypeRaw on the GT prefix (file paths, stdin
  * streaming); 1 = the stdin matrix path's std::stoi POS + parseGenotype on the whole
  * sample field (computeLD :1021-1045, parseGenotype :468-482). */

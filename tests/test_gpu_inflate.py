@@ -378,3 +378,55 @@ def test_tools_on_device_bgzf(argv):
         for x in os.listdir(d):
             os.unlink(os.path.join(d, x))
         os.rmdir(d)
+
+
+# ---- the streamed form (VCFX_allele_freq_calc -i F.gz): the compressed file through the pinned file
+# ring, the member chain parsed from the ring's slots, every member inflated on the device -------------
+@pytest.mark.parametrize("slot", ["4096", "65536", "default"])
+def test_af_streams_bgzf_through_the_ring(slot):
+    """Slots far smaller than a member (a member's header and trailer in different slots), about one
+    member, and the default 16 MiB: the same rows as the oracle on the plain text, with the schedule
+    log showing the staged inflate ran; a plain (single-member) gzip file, a truncated BGZF file and
+    one with a zeroed tail are not a BGZF chain to the stream and take the mapped path (its host
+    inflate output, or the reference's "truncated or corrupt" failure)."""
+    import gzip
+    oracle = Oracle()
+    buf = synth.generate(900, 350, 97, 0, 0.004, 1, 0.02, 0)
+    d = tempfile.mkdtemp(prefix="vcfx_bgzs_")
+    plain, bg, gz, log = (os.path.join(d, x) for x in ("in.vcf", "in.vcf.gz", "in1.vcf.gz", "sched.log"))
+    try:
+        with open(plain, "wb") as f:
+            f.write(buf)
+        comp = B.bgzf(buf, level=6)
+        with open(bg, "wb") as f:
+            f.write(comp)
+        with open(gz, "wb") as f:
+            f.write(gzip.compress(buf, 6))
+        want = oracle.run(["VCFX_allele_freq_calc", "-i", plain], b"")
+        env = dict(os.environ, VCFX_BGZF_STREAM_MIN="0", VCFXG_SCHEDULE_LOG=log)
+        if slot != "default":
+            env["VCFX_FILE_SLOT"] = slot
+
+        def run(path):
+            if os.path.exists(log):
+                os.unlink(log)
+            r = subprocess.run([tool_binary("VCFX_allele_freq_calc"), "-i", path], capture_output=True, env=env,
+                               timeout=120)
+            return r, (open(log).read() if os.path.exists(log) else "")
+
+        r, sch = run(bg)
+        assert (r.stdout, r.returncode) == (want[0], want[2]), r.stderr[-500:]
+        assert "bgzf_inflate_staged" in sch, sch
+        r, sch = run(gz)  # one gzip member: the mapped path's sequential host inflate
+        assert (r.stdout, r.returncode) == (want[0], want[2]), r.stderr[-500:]
+        assert "bgzf_inflate_staged" not in sch
+        for cut in (comp[:len(comp) // 2], comp[:len(comp) - 3000] + bytes(3000)):
+            with open(bg, "wb") as f:
+                f.write(cut)
+            r, sch = run(bg)
+            assert r.returncode == 1 and b"truncated or corrupt" in r.stderr, r.stderr[-300:]
+            assert "bgzf_inflate_staged" not in sch
+    finally:
+        for x in os.listdir(d):
+            os.unlink(os.path.join(d, x))
+        os.rmdir(d)

@@ -2,7 +2,8 @@
 # End-to-end probe (measurement tool): AF on the 427,409 x 2,504 shard written to /tmp --
 # the pipe ceiling (`cat F | drain`), a fresh process per run (file and pipe), and the
 # in-process warm-context phase breakdown (VCFX_TIMING=1).  Output under gpurun_out/.
-#   bash tools/e2e_probe.sh [all|pipe]     pipe: the ceiling and the pipe runs only
+#   bash tools/e2e_probe.sh [all|pipe|warm|bgzf]     pipe: the ceiling and the pipe runs only; bgzf: the
+#   BGZF copy (fresh process and warm context)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 F=/tmp/e2e_chr21.vcf
 python -c "
@@ -18,6 +19,18 @@ for i in 1 2 3; do
     [ -x $DRAIN ] && { echo -n "cat_pipe_drain "; time (cat $F | $DRAIN); }
 done
 MODE=${1:-all}
+if [ $MODE = bgzf ]; then  # the BGZF copy: fresh process and warm context, phase breakdowns
+    G=/tmp/e2e_chr21.vcf.gz
+    build/bin/vcfx_bgzf $F $G 16 1 || exit 1
+    ls -l $G
+    cat $G > /dev/null
+    for i in 1 2 3; do
+        echo -n "fresh_bgzf "; time (VCFX_TIMING=$((i == 1)) timeout -k 5 60 $AF -q -i $G > /dev/null) || exit 1
+    done
+    VCFX_TIMING=1 timeout -k 5 120 python tools/e2e_warm.py $G || exit 1
+    rm -f $F $G
+    exit 0
+fi
 if [ $MODE = warm ]; then  # warm-context file ring shapes: slot bytes, slots, reader threads
     for i in 1 2; do
         timeout -k 5 120 python tools/e2e_warm.py $F 2>/dev/null || exit 1

@@ -59,6 +59,13 @@ struct vcfxg_ctx {
     // LD
     DevBuf ld_G, ld_lines, ld_vidx, ld_valid, ld_Gc, ld_vars, ld_plen, ld_poff, ld_prefix, ld_cid, ld_blocks, ld_cnt,
         ld_off, ld_pairs, ld_fast, ld_gflag, ld_Gp, ld_rowoff, ld_Gv, ld_Gq, dose_meta;
+    // LD walk (vcfxg_ld_prepare_region): walker counts, valid-line counts and their scan, flags +
+    // summary; ld_gc_ready: ld_Gc holds the compact int8 rows (the walk gathers them only when
+    // some variant misses a call)
+    DevBuf ld_wcnt, ld_wval, ld_vbase, ld_small, ld_pend;
+    // vcfxg_bgzf_stage: the compressed stream's size and the bytes staged so far (into bgz_in)
+    size_t bgz_total = 0, bgz_staged = 0;
+    bool ld_gc_ready = false;
     bool ld_vq = false;  // ld_Gv / ld_Gq (valid-mask and squared-dosage FP4 planes) are current
     int n_cu = 0;
     DevBuf async_small;         // asynchronous AF path: line range {0, n}, failure flags, summary
@@ -300,6 +307,7 @@ int vcfxg_open(int device, vcfxg_ctx **out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return VCFXG_E_NODEV;
     vcfxg_ctx *c = new vcfxg_ctx();
     c->device = device;
+    c->n_cu = prop.multiProcessorCount;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return VCFXG_E_HIP;
@@ -320,7 +328,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
-                      &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
+                      &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_wcnt, &c->ld_wval, &c->ld_vbase, &c->ld_small, &c->ld_pend, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
                       &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16, &c->ld_sprec, &c->bgz_in, &c->bgz_mem, &c->bgz_off, &c->bgz_stat, &c->bgz_small})
         if (b->p) (void)hipFree(b->p);
     if (c->af_small.p) (void)hipFree(c->af_small.p);
@@ -476,6 +484,8 @@ int vcfxg_ingest_begin(vcfxg_ctx *c, size_t size_hint) {
     return VCFXG_OK;
 }
 
+static int ingest_mark(vcfxg_ctx *c, size_t upto);
+
 int vcfxg_ingest(vcfxg_ctx *c, const char *host, size_t n, int is_final_chunk) {
     if (!c || (!host && n)) return VCFXG_E_ARG;
     if (!c->ingesting) return VCFXG_E_STATE;
@@ -496,15 +506,8 @@ int vcfxg_ingest(vcfxg_ctx *c, const char *host, size_t n, int is_final_chunk) {
     // up to its staging depth
     if (n) HIPCHK(c, hipMemcpyAsync(static_cast<char *>(c->input.p) + c->n, host, n, hipMemcpyHostToDevice, c->stream));
     if (n && !is_final_chunk) {  // completion marker for vcfxg_ingest_wait
-        hipEvent_t e = nullptr;
-        if (!c->ingest_ev_free.empty()) {
-            e = c->ingest_ev_free.back();
-            c->ingest_ev_free.pop_back();
-        } else {
-            HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
-        HIPCHK(c, hipEventRecord(e, c->stream));
-        c->ingest_ev.push_back({c->n + n, e});
+        int r = ingest_mark(c, c->n + n);
+        if (r) return r;
     }
     if (n && c->hints_pending) c->hints_pending = !load_hints(c, host, n);
     c->n += n;
@@ -523,10 +526,46 @@ int vcfxg_ingest(vcfxg_ctx *c, const char *host, size_t n, int is_final_chunk) {
 }
 
 static_assert(sizeof(vcfxg_bgzf_member) == sizeof(vcfxg::BgzfMember), "BGZF member layout");
+constexpr size_t kCompPad = 8192;  // the inflate reader's ring loads run up to 3 KiB past a stream
+
+// a completion marker for vcfxg_ingest_wait at stream offset `upto`
+static int ingest_mark(vcfxg_ctx *c, size_t upto) {
+    hipEvent_t e = nullptr;
+    if (!c->ingest_ev_free.empty()) {
+        e = c->ingest_ev_free.back();
+        c->ingest_ev_free.pop_back();
+    } else {
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    HIPCHK(c, hipEventRecord(e, c->stream));
+    c->ingest_ev.push_back({upto, e});
+    return VCFXG_OK;
+}
+
+int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, size_t comp_total) {
+    if (!c || (!host && n) || offset > comp_total || n > comp_total - offset) return VCFXG_E_ARG;
+    if (!c->ingesting) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (offset == 0) {
+        int r = ensure(c, c->bgz_in, comp_total + kCompPad);
+        if (r) return r;
+        c->bgz_total = comp_total;
+        c->bgz_staged = 0;
+    }
+    if (comp_total != c->bgz_total || offset != c->bgz_staged) return VCFXG_E_ARG;  // (in order)
+    if (!n) return VCFXG_OK;
+    HIPCHK(c, hipMemcpyAsync(P<uint8_t>(c->bgz_in) + offset, host, n, hipMemcpyHostToDevice, c->stream));
+    c->bgz_staged = offset + n;
+    return ingest_mark(c, offset + n);
+}
 
 int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg_bgzf_member *mem, size_t nm,
                       const char *head, size_t head_n, uint64_t *bad_member) {
-    if (!c || (!comp && comp_n) || (!mem && nm) || (!head && head_n)) return VCFXG_E_ARG;
+    // comp = NULL: the compressed bytes were staged by vcfxg_bgzf_stage (all comp_n of them)
+    const bool staged = !comp;
+    if (!c || (staged && comp_n && (c->bgz_total != comp_n || c->bgz_staged != comp_n)) || (!mem && nm) ||
+        (!head && head_n))
+        return VCFXG_E_ARG;
     if (!c->ingesting) return VCFXG_E_STATE;
     if (bad_member) *bad_member = ~0ull;
     HIPCHK(c, hipSetDevice(c->device));
@@ -553,8 +592,7 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         c->input.p = np;
         c->input.cap = ncap;
     }
-    constexpr size_t kCompPad = 8192;  // the inflate reader's ring loads run up to 3 KiB past a stream
-    int r = ensure(c, c->bgz_in, comp_n + kCompPad);
+    int r = staged ? VCFXG_OK : ensure(c, c->bgz_in, comp_n + kCompPad);
     if (!r) r = ensure(c, c->bgz_mem, sizeof(vcfxg_bgzf_member) * (nm + 1));
     if (!r) r = ensure(c, c->bgz_off, 8 * (nm + 1));
     if (!r) r = ensure(c, c->bgz_stat, 4 * (nm + 1));
@@ -566,7 +604,7 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         return z;
     }();
     prof_begin(c, "bgzf_h2d");
-    if (comp_n) HIPCHK(c, hipMemcpyAsync(c->bgz_in.p, comp, comp_n, hipMemcpyHostToDevice, c->stream));
+    if (comp_n && !staged) HIPCHK(c, hipMemcpyAsync(c->bgz_in.p, comp, comp_n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_in) + comp_n, 0, kCompPad, c->stream));
     if (nm) {
         HIPCHK(c, hipMemcpyAsync(c->bgz_mem.p, mem, sizeof(vcfxg_bgzf_member) * nm, hipMemcpyHostToDevice, c->stream));
@@ -599,7 +637,8 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         return VCFXG_E_DATA;
     }
     if (head_n && c->hints_pending) c->hints_pending = !load_hints(c, head, head_n);
-    note_schedule(c, "bgzf_inflate");
+    note_schedule(c, staged ? "bgzf_inflate_staged" : "bgzf_inflate");
+    c->bgz_total = c->bgz_staged = 0;
     c->n += tot;
     if (tot) c->last_byte = lastb;
     return VCFXG_OK;
@@ -2199,87 +2238,16 @@ struct U16ToU64 {
     __host__ __device__ uint64_t operator()(const uint16_t &x) const { return x; }
 };
 
-int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char *rchrom, size_t rlen, int has_region,
-                     int rstart, int rend, int parse_mode, uint64_t *n_variants) {
-    if (!c || n_samples < 0 || (has_region && !rchrom && rlen)) return VCFXG_E_ARG;
-    if (!c->indexed) return VCFXG_E_STATE;
-    DENSE(c);
-    HIPCHK(c, hipSetDevice(c->device));
-    const uint64_t L = c->n_lines;
-    const int kpad = n_samples > 0 ? ((n_samples + 63) / 64) * 64 : 64;  // MFMA k-steps of 32 B
-    int r = ensure(c, c->ld_G, (size_t)L * kpad + 64);
-    if (!r) r = ensure(c, c->ld_lines, sizeof(vcfxg::LdLine) * (L + 1));
-    if (!r) r = ensure(c, c->ld_vidx, 8 * (L + 1));
-    if (!r) r = ensure(c, c->ld_valid, 4 * (L + 1));
-    if (!r) r = ensure(c, c->query, rlen + 1);
-    if (r) return r;
-    c->query_host.assign(rchrom ? rchrom : "", rlen);
-    if (rlen)
-        c->query_dev_p = nullptr;
-        HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), rlen, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->ld_G.p, 0xFF, (size_t)L * kpad + 64, c->stream));
-    vcfxg::LdParseArgs a{n_samples, kpad, has_region, rstart, rend, (int64_t)rlen, P<char>(c->query), parse_mode};
-    prof_begin(c, "ld_parse");
-    HIPCHK(c, vcfxg::launch_ld_parse(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
-                                     P<uint64_t>(c->d_nlines), L, a, P<int8_t>(c->ld_G), P<vcfxg::LdLine>(c->ld_lines),
-                                     c->stream));
-    prof_end(c, "ld_parse");
-    // compact order: exclusive scan of the valid flags (first member of LdLine)
-    struct ValidOf {
-        __host__ __device__ uint64_t operator()(const vcfxg::LdLine &x) const { return x.valid; }
-    };
-    hipcub::TransformInputIterator<uint64_t, ValidOf, const vcfxg::LdLine *> vin(P<vcfxg::LdLine>(c->ld_lines),
-                                                                                 ValidOf());
-    size_t tmp = 0;
-    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, vin, P<uint64_t>(c->ld_vidx), (int)L, c->stream));
-    r = ensure(c, c->scan_tmp, tmp);
-    if (r) return r;
-    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, vin, P<uint64_t>(c->ld_vidx), (int)L, c->stream));
-    static thread_local uint64_t last[2];
-    static thread_local vcfxg::LdLine lastline;
-    if (L) {
-        HIPCHK(c, hipMemcpyAsync(&last[0], P<uint64_t>(c->ld_vidx) + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(c, hipMemcpyAsync(&lastline, P<vcfxg::LdLine>(c->ld_lines) + L - 1, sizeof lastline,
-                                 hipMemcpyDeviceToHost, c->stream));
+// the shared tail of the LD prepare paths: M variants with ld_vars / ld_fast / ld_Gp, the
+// prefix offsets ld_poff (pbytes in all) and the per-group flags ld_gflag_host in place (and
+// ld_Gc when ld_gc_ready): the sparse-missing / masked planes the groups need, the prefixes
+static int ld_prepare_finish(vcfxg_ctx *c, uint64_t M, int n_samples, int kpad, int kp4, int id_dot_to_pos,
+                             uint64_t pbytes, bool sync_end, uint64_t *n_variants) {
+    int r = VCFXG_OK;
+    if (!c->ld_gc_ready) {
+        for (uint64_t g = 0; g * vcfxg::kLdFastBlock < M; g++)
+            if (c->ld_gflag_host[g] != 1) return VCFXG_E_STATE;  // (the walk gathers Gc for these)
     }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    const uint64_t M = L ? last[0] + lastline.valid : 0;
-    r = ensure(c, c->ld_Gc, (size_t)(M + 1) * kpad + 64);
-    if (!r) r = ensure(c, c->ld_vars, sizeof(vcfxg::LdVar) * (M + 1));
-    if (!r) r = ensure(c, c->ld_fast, sizeof(vcfxg::LdFast) * (M + 1));
-    const int kp4 = vcfxg::ld_kp4(n_samples);
-    if (!r) r = ensure(c, c->ld_Gp, (size_t)(M + 1) * kp4 + 64);
-    if (!r) r = ensure(c, c->ld_gflag, M / vcfxg::kLdFastBlock + 2);
-    if (!r) r = ensure(c, c->ld_plen, 8 * (M + 2));
-    if (!r) r = ensure(c, c->ld_poff, 8 * (M + 2));
-    if (r) return r;
-    prof_begin(c, "ld_compact");
-    HIPCHK(c, vcfxg::launch_ld_compact(P<vcfxg::LdLine>(c->ld_lines), P<uint64_t>(c->ld_vidx), P<uint64_t>(c->d_nlines),
-                                       L, kpad, n_samples, P<int8_t>(c->ld_G), P<int8_t>(c->ld_Gc),
-                                       P<vcfxg::LdVar>(c->ld_vars), P<vcfxg::LdFast>(c->ld_fast), c->stream));
-    HIPCHK(c, vcfxg::launch_ld_pack4(P<int8_t>(c->ld_Gc), M, kpad, n_samples, P<uint8_t>(c->ld_Gp), kp4, c->stream));
-    prof_end(c, "ld_compact");
-    // VCFXG_LD_SPARSE=0: no sparse-missing groups (their tiles take k_ld_mask)
-    static const bool sparse_env = [] {
-        const char *e = getenv("VCFXG_LD_SPARSE");
-        return !(e && e[0] == '0');
-    }();
-    const int sparse = sparse_env && n_samples > 0 && n_samples <= 16383 ? 1 : 0;  // (Sxy as u16 in the epilogue)
-    HIPCHK(c, vcfxg::launch_ld_groups(P<vcfxg::LdVar>(c->ld_vars), M, n_samples, sparse, P<uint8_t>(c->ld_gflag),
-                                      c->stream));
-    c->ld_gflag_host.assign(M / vcfxg::kLdFastBlock + 1, 0);
-    if (M)
-        HIPCHK(c, hipMemcpyAsync(c->ld_gflag_host.data(), c->ld_gflag.p, (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock,
-                                 hipMemcpyDeviceToHost, c->stream));
-    // per-variant "chrom\tpos\tid" prefixes
-    HIPCHK(c, vcfxg::launch_ld_prefix(0, P<vcfxg::LdVar>(c->ld_vars), M, P<char>(c->input), id_dot_to_pos,
-                                      P<uint64_t>(c->ld_plen), nullptr, c->stream));
-    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->ld_plen) + M, 0, 8, c->stream));
-    r = exclusive_scan(c, P<uint64_t>(c->ld_plen), P<uint64_t>(c->ld_poff), (size_t)M + 1);
-    if (r) return r;
-    static thread_local uint64_t pbytes;
-    HIPCHK(c, hipMemcpyAsync(&pbytes, P<uint64_t>(c->ld_poff) + M, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     r = ensure(c, c->ld_prefix, pbytes + 16);
     if (r) return r;
     // a group with a missing genotype: the valid-mask and squared-dosage planes of the
@@ -2375,7 +2343,7 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
     }
     HIPCHK(c, vcfxg::launch_ld_prefix(1, P<vcfxg::LdVar>(c->ld_vars), M, P<char>(c->input), id_dot_to_pos,
                                       P<uint64_t>(c->ld_poff), P<char>(c->ld_prefix), c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (sync_end) HIPCHK(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
     c->ld_m = M;
     c->ld_kpad = kpad;
@@ -2385,6 +2353,225 @@ int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char 
     c->ld_chrom_ids = false;
     if (n_variants) *n_variants = M;
     return VCFXG_OK;
+}
+
+int vcfxg_ld_prepare(vcfxg_ctx *c, int n_samples, int id_dot_to_pos, const char *rchrom, size_t rlen, int has_region,
+                     int rstart, int rend, int parse_mode, uint64_t *n_variants) {
+    if (!c || n_samples < 0 || (has_region && !rchrom && rlen)) return VCFXG_E_ARG;
+    if (!c->indexed) return VCFXG_E_STATE;
+    DENSE(c);
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t L = c->n_lines;
+    const int kpad = n_samples > 0 ? ((n_samples + 63) / 64) * 64 : 64;  // MFMA k-steps of 32 B
+    int r = ensure(c, c->ld_G, (size_t)L * kpad + 64);
+    if (!r) r = ensure(c, c->ld_lines, sizeof(vcfxg::LdLine) * (L + 1));
+    if (!r) r = ensure(c, c->ld_vidx, 8 * (L + 1));
+    if (!r) r = ensure(c, c->ld_valid, 4 * (L + 1));
+    if (!r) r = ensure(c, c->query, rlen + 1);
+    if (r) return r;
+    c->query_host.assign(rchrom ? rchrom : "", rlen);
+    if (rlen) {
+        c->query_dev_p = nullptr;
+        HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), rlen, hipMemcpyHostToDevice, c->stream));
+    }
+    HIPCHK(c, hipMemsetAsync(c->ld_G.p, 0xFF, (size_t)L * kpad + 64, c->stream));
+    vcfxg::LdParseArgs a{n_samples, kpad, has_region, rstart, rend, (int64_t)rlen, P<char>(c->query), parse_mode};
+    prof_begin(c, "ld_parse");
+    HIPCHK(c, vcfxg::launch_ld_parse(P<char>(c->input), (int64_t)c->data_start, P<uint64_t>(c->line_end),
+                                     P<uint64_t>(c->d_nlines), L, a, P<int8_t>(c->ld_G), P<vcfxg::LdLine>(c->ld_lines),
+                                     c->stream));
+    prof_end(c, "ld_parse");
+    // compact order: exclusive scan of the valid flags (first member of LdLine)
+    struct ValidOf {
+        __host__ __device__ uint64_t operator()(const vcfxg::LdLine &x) const { return x.valid; }
+    };
+    hipcub::TransformInputIterator<uint64_t, ValidOf, const vcfxg::LdLine *> vin(P<vcfxg::LdLine>(c->ld_lines),
+                                                                                 ValidOf());
+    size_t tmp = 0;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, vin, P<uint64_t>(c->ld_vidx), (int)L, c->stream));
+    r = ensure(c, c->scan_tmp, tmp);
+    if (r) return r;
+    HIPCHK(c, hipcub::DeviceScan::ExclusiveSum(c->scan_tmp.p, tmp, vin, P<uint64_t>(c->ld_vidx), (int)L, c->stream));
+    static thread_local uint64_t last[2];
+    static thread_local vcfxg::LdLine lastline;
+    if (L) {
+        HIPCHK(c, hipMemcpyAsync(&last[0], P<uint64_t>(c->ld_vidx) + L - 1, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(c, hipMemcpyAsync(&lastline, P<vcfxg::LdLine>(c->ld_lines) + L - 1, sizeof lastline,
+                                 hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const uint64_t M = L ? last[0] + lastline.valid : 0;
+    r = ensure(c, c->ld_Gc, (size_t)(M + 1) * kpad + 64);
+    if (!r) r = ensure(c, c->ld_vars, sizeof(vcfxg::LdVar) * (M + 1));
+    if (!r) r = ensure(c, c->ld_fast, sizeof(vcfxg::LdFast) * (M + 1));
+    const int kp4 = vcfxg::ld_kp4(n_samples);
+    if (!r) r = ensure(c, c->ld_Gp, (size_t)(M + 1) * kp4 + 64);
+    if (!r) r = ensure(c, c->ld_gflag, M / vcfxg::kLdFastBlock + 2);
+    if (!r) r = ensure(c, c->ld_plen, 8 * (M + 2));
+    if (!r) r = ensure(c, c->ld_poff, 8 * (M + 2));
+    if (r) return r;
+    prof_begin(c, "ld_compact");
+    HIPCHK(c, vcfxg::launch_ld_compact(P<vcfxg::LdLine>(c->ld_lines), P<uint64_t>(c->ld_vidx), P<uint64_t>(c->d_nlines),
+                                       L, kpad, n_samples, P<int8_t>(c->ld_G), P<int8_t>(c->ld_Gc),
+                                       P<vcfxg::LdVar>(c->ld_vars), P<vcfxg::LdFast>(c->ld_fast), c->stream));
+    HIPCHK(c, vcfxg::launch_ld_pack4(P<int8_t>(c->ld_Gc), M, kpad, n_samples, P<uint8_t>(c->ld_Gp), kp4, c->stream));
+    prof_end(c, "ld_compact");
+    // VCFXG_LD_SPARSE=0: no sparse-missing groups (their tiles take k_ld_mask)
+    static const bool sparse_env = [] {
+        const char *e = getenv("VCFXG_LD_SPARSE");
+        return !(e && e[0] == '0');
+    }();
+    const int sparse = sparse_env && n_samples > 0 && n_samples <= 16383 ? 1 : 0;  // (Sxy as u16 in the epilogue)
+    HIPCHK(c, vcfxg::launch_ld_groups(P<vcfxg::LdVar>(c->ld_vars), M, n_samples, sparse, P<uint8_t>(c->ld_gflag),
+                                      c->stream));
+    c->ld_gflag_host.assign(M / vcfxg::kLdFastBlock + 1, 0);
+    if (M)
+        HIPCHK(c, hipMemcpyAsync(c->ld_gflag_host.data(), c->ld_gflag.p, (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock,
+                                 hipMemcpyDeviceToHost, c->stream));
+    // per-variant "chrom\tpos\tid" prefixes
+    HIPCHK(c, vcfxg::launch_ld_prefix(0, P<vcfxg::LdVar>(c->ld_vars), M, P<char>(c->input), id_dot_to_pos,
+                                      P<uint64_t>(c->ld_plen), nullptr, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->ld_plen) + M, 0, 8, c->stream));
+    r = exclusive_scan(c, P<uint64_t>(c->ld_plen), P<uint64_t>(c->ld_poff), (size_t)M + 1);
+    if (r) return r;
+    static thread_local uint64_t pbytes;
+    HIPCHK(c, hipMemcpyAsync(&pbytes, P<uint64_t>(c->ld_poff) + M, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->ld_gc_ready = true;
+    return ld_prepare_finish(c, M, n_samples, kpad, kp4, id_dot_to_pos, pbytes, true, n_variants);
+}
+
+// vcfxg_index(data_start) + vcfxg_ld_prepare in one call, with the same variants, rows, sums and
+// prefixes.  The default for records averaging >= 512 B with n_samples <= 4096: the LD walk
+// (vcfxg_ld.hip k_ld_walk: one HBM pass over the records, no line index), then one compaction
+// that writes the variant records, the FP4 rows and the prefix lengths, and ONE host
+// synchronisation for the variant count, the prefix bytes and the group flags.  The int8 rows in
+// variant order (ld_Gc) are gathered only when some variant misses a call (the sparse-missing and
+// masked kernels read them).  A walker over its line capacity, or an input the walk does not
+// take, runs vcfxg_index + vcfxg_ld_prepare (VCFXG_LD_WALK=0: always).  The context is not
+// indexed afterwards (vcfxg_line_ends and the per-line calls need vcfxg_index).
+int vcfxg_ld_prepare_region(vcfxg_ctx *c, size_t data_start, int n_samples, int id_dot_to_pos, const char *rchrom,
+                            size_t rlen, int has_region, int rstart, int rend, int parse_mode, uint64_t *n_variants) {
+    if (!c || n_samples < 0 || (has_region && !rchrom && rlen)) return VCFXG_E_ARG;
+    if (!c->loaded) return VCFXG_E_STATE;
+    if (data_start > c->n) data_start = c->n;
+    c->dense_pending = false;  // a new index / regions replace the pending ones
+    HIPCHK(c, hipSetDevice(c->device));
+    static const bool walk_env = [] {
+        const char *e = getenv("VCFXG_LD_WALK");
+        return !(e && e[0] == '0');
+    }();
+    const int64_t lo = (int64_t)data_start, hi = (int64_t)c->n;
+    // the walkers' chunk: the record walks' (128 KiB for ~10 KB records), halved while the input
+    // would give fewer than about 2 rounds of walkers over the chip (a 1 GB LD shard: 64 KiB;
+    // each walker's last round otherwise runs with the chip half empty); VCFXG_LD_WALK_CHUNK
+    // overrides
+    static const int64_t ld_chunk_env = getenv("VCFXG_LD_WALK_CHUNK") ? atol(getenv("VCFXG_LD_WALK_CHUNK")) : 0;
+    int64_t C = c->walk_chunk;
+    if (ld_chunk_env >= 4096) C = ld_chunk_env;
+    else
+        while (C > 32768 && (hi - lo) / C < 2 * 20 * (int64_t)std::max(c->n_cu, 1)) C /= 2;
+    const int64_t nw = hi > lo ? (hi - lo + C - 1) / C : 0;
+    const uint64_t cap_w = (uint64_t)(2 * C / std::max<int64_t>(c->hint_line, 64)) + 16;
+    const bool walk = walk_env && nw > 0 && n_samples > 0 && n_samples <= 4096 && c->hint_line >= 512 &&
+                      !c->walk_overflowed && cap_w <= 0xFFFF;
+    auto indexed_path = [&]() -> int {
+        note_schedule(c, "ld_index");
+        int r = vcfxg_index(c, data_start, nullptr);
+        return r ? r : vcfxg_ld_prepare(c, n_samples, id_dot_to_pos, rchrom, rlen, has_region, rstart, rend, parse_mode,
+                                        n_variants);
+    };
+    if (!walk) return indexed_path();
+    const uint64_t cap = (uint64_t)nw * cap_w;
+    const int kpad = ((n_samples + 63) / 64) * 64;
+    const int kp4 = vcfxg::ld_kp4(n_samples);
+    int r = ensure(c, c->ld_G, (size_t)cap * kpad + 64);
+    if (!r) r = ensure(c, c->ld_lines, sizeof(vcfxg::LdLine) * (cap + 1));
+    if (!r) r = ensure(c, c->ld_wcnt, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->ld_wval, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->ld_vbase, 8 * (size_t)(nw + 1));
+    if (!r) r = ensure(c, c->ld_small, 64);
+    if (!r) r = ensure(c, c->ld_pend, 8 * (cap + 1));
+    if (!r) r = ensure(c, c->ld_vars, sizeof(vcfxg::LdVar) * (cap + 1));
+    if (!r) r = ensure(c, c->ld_fast, sizeof(vcfxg::LdFast) * (cap + 1));
+    if (!r) r = ensure(c, c->ld_Gp, (size_t)(cap + 1) * kp4 + 64);
+    if (!r) r = ensure(c, c->ld_gflag, cap / vcfxg::kLdFastBlock + 2);
+    if (!r) r = ensure(c, c->ld_plen, 8 * (cap + 2));
+    if (!r) r = ensure(c, c->ld_poff, 8 * (cap + 2));
+    if (!r) r = ensure(c, c->query, rlen + 1);
+    if (r) return r;
+    if (rlen) {
+        c->query_host.assign(rchrom, rlen);
+        c->query_dev_p = nullptr;
+        HIPCHK(c, hipMemcpyAsync(c->query.p, c->query_host.data(), rlen, hipMemcpyHostToDevice, c->stream));
+    }
+    const char *buf = P<char>(c->input);
+    // small: [0] walk overflow (u32) | flags (u32: bit 0 = an incomplete variant), [1] M,
+    // [2] pending lines
+    uint64_t *small = P<uint64_t>(c->ld_small);
+    unsigned *ovf = reinterpret_cast<unsigned *>(small), *flags = ovf + 1;
+    HIPCHK(c, hipMemsetAsync(small, 0, 24, c->stream));
+    HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->ld_wval) + nw, 0, 8, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->ld_plen.p, 0, 8 * (cap + 1), c->stream));
+    vcfxg::LdParseArgs a{n_samples, kpad, has_region, rstart, rend, (int64_t)rlen, P<char>(c->query), parse_mode};
+    prof_begin(c, "ld_walk");
+    HIPCHK(c, vcfxg::launch_ld_walk(buf, lo, hi, C, c->hint_span, cap_w, a, P<int8_t>(c->ld_G),
+                                    P<vcfxg::LdLine>(c->ld_lines), P<uint64_t>(c->ld_wcnt), P<uint64_t>(c->ld_wval),
+                                    ovf, reinterpret_cast<unsigned long long *>(small + 2), P<uint64_t>(c->ld_pend),
+                                    c->stream));
+    prof_end(c, "ld_walk");
+    prof_begin(c, "ld_compact");
+    r = exclusive_scan(c, P<uint64_t>(c->ld_wval), P<uint64_t>(c->ld_vbase), (size_t)nw + 1);
+    if (r) return r;
+    HIPCHK(c, vcfxg::launch_ld_wcompact(nw, cap_w, P<uint64_t>(c->ld_wcnt), P<uint64_t>(c->ld_vbase),
+                                        P<vcfxg::LdLine>(c->ld_lines), n_samples, buf, id_dot_to_pos,
+                                        P<vcfxg::LdVar>(c->ld_vars), P<vcfxg::LdFast>(c->ld_fast),
+                                        P<uint64_t>(c->ld_plen), flags, small + 1, c->stream));
+    prof_end(c, "ld_compact");
+    static const bool sparse_env = [] {
+        const char *e = getenv("VCFXG_LD_SPARSE");
+        return !(e && e[0] == '0');
+    }();
+    const int sparse = sparse_env && n_samples <= 16383 ? 1 : 0;
+    HIPCHK(c, vcfxg::launch_ld_groups(P<vcfxg::LdVar>(c->ld_vars), cap, n_samples, sparse, P<uint8_t>(c->ld_gflag),
+                                      c->stream, small + 1));
+    r = exclusive_scan(c, P<uint64_t>(c->ld_plen), P<uint64_t>(c->ld_poff), (size_t)cap + 1);
+    if (r) return r;
+    // one synchronisation: overflow, flags, M, the prefix bytes (plen is 0 past M) and the
+    // group flags (computed for every group below cap; the first ceil(M / 256) are M's)
+    static thread_local uint64_t sm[3];
+    const uint64_t ng = (cap + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock;
+    c->ld_gflag_host.assign(ng + 1, 0);
+    HIPCHK(c, hipMemcpyAsync(sm, small, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(sm + 2, P<uint64_t>(c->ld_poff) + cap, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->ld_gflag_host.data(), c->ld_gflag.p, ng, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((uint32_t)sm[0]) {  // a walker ran out of line slots (short lines): the index path
+        prof_collect(c);
+        c->walk_overflowed = true;
+        return indexed_path();
+    }
+    note_schedule(c, "ld_walk");
+    const uint64_t M = sm[1], pbytes = sm[2];
+    prof_begin(c, "ld_pack");  // the FP4 rows, from the walk's slots
+    HIPCHK(c, vcfxg::launch_ld_pack4(P<int8_t>(c->ld_G), M, kpad, n_samples, P<uint8_t>(c->ld_Gp), kp4, c->stream,
+                                     P<vcfxg::LdVar>(c->ld_vars)));
+    prof_end(c, "ld_pack");
+    c->ld_gflag_host.resize(M / vcfxg::kLdFastBlock + 1);
+    for (uint64_t g = (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock; g < c->ld_gflag_host.size(); g++)
+        c->ld_gflag_host[g] = 0;  // (past M: as the indexed path leaves them)
+    c->ld_gc_ready = false;
+    if ((sm[0] >> 32) & 1u) {  // some variant misses a call: its group's kernels read ld_Gc
+        r = ensure(c, c->ld_Gc, (size_t)(M + 1) * kpad + 64);
+        if (r) return r;
+        prof_begin(c, "ld_gather");
+        HIPCHK(c, vcfxg::launch_ld_gather(P<vcfxg::LdVar>(c->ld_vars), M, P<int8_t>(c->ld_G), kpad,
+                                          P<int8_t>(c->ld_Gc), c->stream));
+        prof_end(c, "ld_gather");
+        c->ld_gc_ready = true;
+    }
+    c->indexed = false;  // (no line index: vcfxg_index before any per-line call)
+    return ld_prepare_finish(c, M, n_samples, kpad, kp4, id_dot_to_pos, pbytes, false, n_variants);
 }
 
 // exact chrom equality ids (for max_dist): strings are the first field of each prefix
@@ -2455,6 +2642,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
     uint64_t nb = 1;
     uint32_t nfast = 0, nmask = 0, nbl = 0, nsp = 0;
     for (uint64_t J = j0 / BM; J * BM < j1; J++) nb = std::max<uint64_t>(nb, J - ifirst(J) + 1);
+    nb = (nb + 7) & ~(uint64_t)7;  // (k_ld_rowscan reads a row's counts 8 slots per 16 B load)
     if (hit) {
         nfast = c->ld_plan_n[0];
         nmask = c->ld_plan_n[1];

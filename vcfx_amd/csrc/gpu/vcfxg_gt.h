@@ -69,6 +69,12 @@ template <class T, class = void>
 struct HasClean : std::false_type {};
 template <class T>
 struct HasClean<T, std::void_t<decltype(&T::clean)>> : std::true_type {};
+// ... or op.clean_at(e0..e3, p): the same with the offset p of the first of the four dwords
+// (reducers that place per-sample results: the LD walk's genotype codes)
+template <class T, class = void>
+struct HasCleanAt : std::false_type {};
+template <class T>
+struct HasCleanAt<T, std::void_t<decltype(&T::clean_at)>> : std::true_type {};
 // pre(): called once, right after the record's first batch of loads is issued.
 // swept (optional): the end of the bytes the sweep examined -- E, or on an early exit
 // (op.done()) the end of the last batch of loads
@@ -135,14 +141,17 @@ __device__ bool gt_fast(const char *__restrict__ buf, int64_t S, int64_t E, Op &
                                  __builtin_amdgcn_alignbyte(v[u].w, v[u].z, s),
                                  __builtin_amdgcn_alignbyte(x4[u], v[u].w, s)};
                 bool clean = false;
-                if constexpr (HasClean<Op>::value) {
+                if constexpr (HasClean<Op>::value || HasCleanAt<Op>::value) {
                     // an interior step whose every allele is '0' / '1' (e = d ^ exp has only
                     // bits 0 and 16): the reducer's SWAR form on the four e's at once
                     if (interior) {
                         const uint32_t e0 = d[0] ^ exp_xor, e1 = d[1] ^ exp_xor, e2 = d[2] ^ exp_xor,
                                        e3 = d[3] ^ exp_xor;
                         clean = !__any(((e0 | e1 | e2 | e3) & ~0x00010001u) != 0u);
-                        if (clean) op.clean(e0, e1, e2, e3);
+                        if (clean) {
+                            if constexpr (HasCleanAt<Op>::value) op.clean_at(e0, e1, e2, e3, b0 + blk + s);
+                            else op.clean(e0, e1, e2, e3);
+                        }
                     }
                 }
                 bool real[4] = {true, true, true, true};

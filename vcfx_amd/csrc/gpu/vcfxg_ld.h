@@ -109,6 +109,20 @@ hipError_t launch_ld_parse(const char *buf, int64_t data_start, const uint64_t *
 hipError_t launch_ld_compact(const LdLine *lines, const uint64_t *vidx, const uint64_t *n_lines_dev,
                              uint64_t n_lines_host, int kpad, int ns, const int8_t *G, int8_t *Gc, LdVar *vars,
                              LdFast *fv, hipStream_t s);
+// the LD walk (the parse without vcfxg_index; n_samples <= 4096): walker wk's lines to slots
+// wk * cap_w + n (LdLine + int8 row of kpad bytes in G); wcount / wvalid per walker; overflow
+// when a walker has more than cap_w lines; then the lines off the walk's fast path (pend_n
+// zeroed by the caller; pend: capacity nw * cap_w) parsed on their own (k_ld_pending)
+hipError_t launch_ld_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int64_t span0, uint64_t cap_w,
+                          const LdParseArgs &a, int8_t *G, LdLine *lines, uint64_t *wcount, uint64_t *wvalid,
+                          unsigned *overflow, unsigned long long *pend_n, uint64_t *pend, hipStream_t s);
+// slots -> compact variants (vbase: exclusive scan of wvalid, nw + 1 entries): vars (line = the
+// slot), fv, prefix lengths plen; flags bit 0 = some variant incomplete; *m_out = M
+hipError_t launch_ld_wcompact(int64_t nw, uint64_t cap_w, const uint64_t *wcount, const uint64_t *vbase,
+                              const LdLine *lines, int ns, const char *buf, int id_dot_to_pos, LdVar *vars, LdFast *fv,
+                              uint64_t *plen, unsigned *flags, uint64_t *m_out, hipStream_t s);
+// Gc[v] = the walk row of variant v (vars[v].line = its slot)
+hipError_t launch_ld_gather(const LdVar *vars, uint64_t m, const int8_t *G, int kpad, int8_t *Gc, hipStream_t s);
 // ordered output offset of pair slot (row j - j_lo, column block slot): the row's first
 // pair (exclusive scan over rows) + the slot's offset inside the row (per-row scan, u32)
 struct LdOffsets {
@@ -144,7 +158,9 @@ hipError_t launch_ld_fast(int pass, const uint8_t *Gp, const LdFast *fv, const u
 // per 256-group: 1 = every variant complete; 2 = (sparse != 0) every variant has at most
 // kLdSparseMax missing calls (the sparse-correction kernel's groups); 0 = other
 constexpr int kLdSparseMax = 15;
-hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, int ns, int sparse, uint8_t *gflag, hipStream_t s);
+// (m_dev: the variant count on the device, m its upper bound)
+hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, int ns, int sparse, uint8_t *gflag, hipStream_t s,
+                            const uint64_t *m_dev = nullptr);
 
 // the sparse-missing form of k_ld_fast (vcfxg_ld_fast.hip, kSp): per variant its missing samples
 // (CSR: moff[v] .. moff[v + 1] into midx = sample, mvar = v) and the sample-major contribution
@@ -172,7 +188,9 @@ hipError_t launch_ld_gt16(const int8_t *Gc, uint64_t m, int kpad, int ns, uint64
 hipError_t launch_ld_sparse(int pass, const uint8_t *Gp, const LdSparse &sp, const uint32_t *chrom_id,
                             const LdWindowArgs &a, const uint32_t *blocks, uint32_t nblocks, uint16_t *cnt,
                             LdOffsets off, LdPair *pairs, const LdStage &st, hipStream_t s);
-hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s);
+// (vars: the rows of variant v are Gc + vars[v].line * kpad -- the walk's slots -- instead of v * kpad)
+hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s,
+                           const LdVar *vars = nullptr);
 hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C, hipStream_t s);
 // FP4 row bytes for ns samples: two per byte, whole 64-byte k-slices
 inline int ld_kp4(int ns) { return ns > 0 ? ((ns + 127) / 128) * 64 : 64; }

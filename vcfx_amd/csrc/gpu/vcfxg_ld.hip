@@ -15,11 +15,35 @@
 #include "vcfxg_device.h"
 #include "vcfxg_gt.h"
 #include "vcfxg_ld.h"
+#include "vcfxg_walk.h"
 
 namespace vcfxg {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int int_len(int v) {
+    unsigned u = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+    int n = v < 0 ? 1 : 0;
+    do {
+        n++;
+        u /= 10u;
+    } while (u);
+    return n;
+}
+__device__ __forceinline__ char *put_int(char *o, int v) {  // formatInt :214-225 / to_string
+    unsigned u = v < 0 ? 0u - (unsigned)v : (unsigned)v;
+    if (v < 0) *o++ = '-';
+    char t[12];
+    int k = 0;
+    do {
+        t[k++] = (char)('0' + u % 10u);
+        u /= 10u;
+    } while (u);
+    while (k) *o++ = t[--k];
+    return o;
+}
+
 
 // ---------------------------------------------------------------------------------------
 // parse
@@ -167,6 +191,44 @@ struct LdOpL {
 };
 constexpr int kLdLdsRow = 4096;  // samples per record composed in LDS (more: byte stores to HBM)
 
+// LdOpL with the clean-step form (vcfxg_gt.h HasCleanAt): four samples whose alleles are all
+// '0' / '1' (e = dword ^ "0 s 0 \t", bits 0 and 16 only) -> their four codes as one dword
+// into the LDS row (k is congruent mod 4 across the wave: one store shape per record)
+struct LdOpW : LdOpL {
+    __device__ void clean_at(uint32_t e0, uint32_t e1, uint32_t e2, uint32_t e3, int64_t p) {
+        const int64_t k = (p - S) >> 2;
+        const uint32_t c0 = (e0 + (e0 >> 16)) & 3u, c1 = (e1 + (e1 >> 16)) & 3u, c2 = (e2 + (e2 >> 16)) & 3u,
+                       c3 = (e3 + (e3 >> 16)) & 3u;
+        if (k + 3 < ns) {
+            const uint32_t w = c0 | (c1 << 8) | (c2 << 16) | (c3 << 24);
+            auto *r = row + k;
+            if ((k & 3) == 0) {
+                *reinterpret_cast<__attribute__((address_space(3))) uint32_t *>(r) = w;
+            } else if ((k & 1) == 0) {
+                reinterpret_cast<__attribute__((address_space(3))) uint16_t *>(r)[0] = (uint16_t)w;
+                reinterpret_cast<__attribute__((address_space(3))) uint16_t *>(r)[1] = (uint16_t)(w >> 16);
+            } else {
+                r[0] = (int8_t)c0;
+                r[1] = (int8_t)c1;
+                r[2] = (int8_t)c2;
+                r[3] = (int8_t)c3;
+            }
+            const uint32_t sum = c0 + c1 + c2 + c3;
+            st.cnt += 4u;
+            st.sx += sum;
+            st.sx2 += sum + 2u * ((c0 >> 1) + (c1 >> 1) + (c2 >> 1) + (c3 >> 1));
+        } else {
+            const uint32_t c[4] = {c0, c1, c2, c3};
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+                if (k + i < ns) {
+                    row[k + i] = (int8_t)c[i];
+                    st.add((int)c[i]);
+                }
+        }
+    }
+};
+
 // general path: samples numbered by a running count of starts (sampleIdx, :598-611)
 __device__ void ld_general(const char *__restrict__ buf, int64_t S, int64_t E, int ns, int8_t *row, LdStats &st,
                            int stoi_mode) {
@@ -208,6 +270,99 @@ __device__ void ld_general(const char *__restrict__ buf, int64_t S, int64_t E, i
     }
 }
 
+// one line [ls, le) -> its LdLine; a valid line's codes into row (kpad bytes, global; composed
+// in the wave's LDS row lrow when ns <= kLdLdsRow).  pad: also write -1 over the row's bytes
+// past the codes (the walk's rows are not cleared beforehand; k_ld_parse's are, by a memset)
+__device__ __forceinline__ LdLine ld_line(const char *__restrict__ buf, int64_t ls, int64_t le, const LdParseArgs &a,
+                          int8_t *__restrict__ row, int8_t *lrow, int64_t *lds, bool pad) {
+    LdLine out;
+    out.valid = 0;
+    if (le > ls && byte_at(buf, ls) != '#') {
+        int64_t t[10];
+        const int nt = head_tabs(buf, ls, le, 9, t, lds);
+        bool ok = nt >= 9;
+        int pos = 0;
+        if (ok && !a.stoi_mode) {  // fastParseInt(field 1)
+            const int64_t p0 = t[0] + 1, p1 = t[1];
+            ok = p1 > p0;
+            if (ok && p1 - p0 <= kWave) {
+                // lane k holds digit k: one round of loads instead of a dependent byte
+                // chain; sum of d_k * 10^(len-1-k) mod 2^32 = the wrapping Horner loop
+                const int len = (int)(p1 - p0), k = lane();
+                const uint32_t c = k < len ? byte_at(buf, p0 + k) : (uint32_t)'0';
+                ok = !__any(c - '0' >= 10u);
+                uint32_t pw = 1u;
+                for (int e = k; e < len - 1; e++) pw *= 10u;
+                pos = (int)wave_sum(k < len ? (c - '0') * pw : 0u);
+            } else if (ok) {
+                uint32_t v = 0;
+                for (int64_t p = p0; ok && p < p1; p++) {
+                    uint32_t c = byte_at(buf, p);
+                    if (c - '0' >= 10u) ok = false;
+                    else v = v * 10u + (c - '0');
+                }
+                pos = (int)v;
+            }
+        } else if (ok) {  // std::stoi(fields[1]) (computeLD :1026)
+            ok = cxx_stoi(buf, t[0] + 1, t[1], &pos);
+        }
+        if (ok && a.has_region) {
+            int64_t cl = t[0] - ls;
+            ok = cl == a.rlen && pos >= a.rstart && pos <= a.rend;
+            for (int64_t k = 0; ok && k < cl; k++) ok = buf[ls + k] == a.rchrom[k];
+        }
+        if (ok) {
+            const int64_t S = t[8] + 1;
+            LdStats st;
+            bool fast;
+            if (a.ns <= kLdLdsRow) {  // codes composed in LDS, then 16 B stores
+                LdOpL op{(__attribute__((address_space(3))) int8_t *)lrow, S, a.ns};
+                fast = gt_fast<6>(buf, S, le, op);  // (six 1 KiB steps in flight, as the walks)
+                if (fast) {
+                    st = op.st;
+                    const int64_t nr = (le - S + 1) / 4;
+                    const uint32_t nout = (uint32_t)(nr < a.ns ? nr : a.ns);
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    for (uint32_t o = (uint32_t)lane() * 16; o < nout; o += kWave * 16) {
+                        if (o + 16 <= nout)
+                            *reinterpret_cast<uint4 *>(row + o) = *reinterpret_cast<const uint4 *>(lrow + o);
+                        else
+                            for (uint32_t q = o; q < nout; q++) row[q] = lrow[q];
+                    }
+                    if (pad)
+                        for (uint32_t q = nout + (uint32_t)lane(); q < (uint32_t)a.kpad; q += kWave) row[q] = -1;
+                    // the next line's byte writes must not pass these reads
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                }
+            } else {
+                if (pad)
+                    for (int k = lane(); k < a.kpad; k += kWave) row[k] = -1;
+                LdOp op{row, S, a.ns};
+                fast = gt_fast<6>(buf, S, le, op);
+                if (fast) st = op.st;
+            }
+            if (!fast) {
+                // rewrite the row: the failed fast sweep may have stored codes
+                for (int k = lane(); k < a.kpad; k += kWave) row[k] = -1;
+                ld_general(buf, S, le, a.ns, row, st, a.stoi_mode);
+            }
+            out.valid = 1;
+            out.pos = pos;
+            out.cnt = wave_sum(st.cnt);
+            out.sx = wave_sum(st.sx);
+            out.sx2 = wave_sum(st.sx2);
+            out.chrom = (uint64_t)ls;
+            out.chrom_len = (uint32_t)(t[0] - ls);
+            out.id = (uint64_t)(t[1] + 1);
+            out.id_len = (uint32_t)(t[2] - t[1] - 1);
+        }
+    }
+    return out;
+}
+
 __global__ __launch_bounds__(256) void k_ld_parse(const char *__restrict__ buf, int64_t data_start,
                                                   const uint64_t *__restrict__ line_end, const uint64_t *n_lines_p,
                                                   LdParseArgs a, int8_t *__restrict__ G, LdLine *__restrict__ lines) {
@@ -221,93 +376,47 @@ __global__ __launch_bounds__(256) void k_ld_parse(const char *__restrict__ buf, 
     for (uint64_t li = wid; li < n_lines; li += nw) {
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
         const int64_t le = (int64_t)line_end[li];
-        LdLine out;
-        out.valid = 0;
-        if (le > ls && byte_at(buf, ls) != '#') {
-            int64_t t[10];
-            const int nt = head_tabs(buf, ls, le, 9, t, lds);
-            bool ok = nt >= 9;
-            int pos = 0;
-            if (ok && !a.stoi_mode) {  // fastParseInt(field 1)
-                const int64_t p0 = t[0] + 1, p1 = t[1];
-                ok = p1 > p0;
-                if (ok && p1 - p0 <= kWave) {
-                    // lane k holds digit k: one round of loads instead of a dependent byte
-                    // chain; sum of d_k * 10^(len-1-k) mod 2^32 = the wrapping Horner loop
-                    const int len = (int)(p1 - p0), k = lane();
-                    const uint32_t c = k < len ? byte_at(buf, p0 + k) : (uint32_t)'0';
-                    ok = !__any(c - '0' >= 10u);
-                    uint32_t pw = 1u;
-                    for (int e = k; e < len - 1; e++) pw *= 10u;
-                    pos = (int)wave_sum(k < len ? (c - '0') * pw : 0u);
-                } else if (ok) {
-                    uint32_t v = 0;
-                    for (int64_t p = p0; ok && p < p1; p++) {
-                        uint32_t c = byte_at(buf, p);
-                        if (c - '0' >= 10u) ok = false;
-                        else v = v * 10u + (c - '0');
-                    }
-                    pos = (int)v;
-                }
-            } else if (ok) {  // std::stoi(fields[1]) (computeLD :1026)
-                ok = cxx_stoi(buf, t[0] + 1, t[1], &pos);
-            }
-            if (ok && a.has_region) {
-                int64_t cl = t[0] - ls;
-                ok = cl == a.rlen && pos >= a.rstart && pos <= a.rend;
-                for (int64_t k = 0; ok && k < cl; k++) ok = buf[ls + k] == a.rchrom[k];
-            }
-            if (ok) {
-                int8_t *row = G + li * (uint64_t)a.kpad;
-                const int64_t S = t[8] + 1;
-                LdStats st;
-                bool fast;
-                if (a.ns <= kLdLdsRow) {  // codes composed in LDS, then 16 B stores
-                    LdOpL op{(__attribute__((address_space(3))) int8_t *)lrow, S, a.ns};
-                    fast = gt_fast<6>(buf, S, le, op);  // (six 1 KiB steps in flight, as the walks)
-                    if (fast) {
-                        st = op.st;
-                        const int64_t nr = (le - S + 1) / 4;
-                        const uint32_t nout = (uint32_t)(nr < a.ns ? nr : a.ns);
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                        for (uint32_t o = (uint32_t)lane() * 16; o < nout; o += kWave * 16) {
-                            if (o + 16 <= nout)
-                                *reinterpret_cast<uint4 *>(row + o) = *reinterpret_cast<const uint4 *>(lrow + o);
-                            else
-                                for (uint32_t q = o; q < nout; q++) row[q] = lrow[q];
-                        }
-                        // the next line's byte writes must not pass these reads
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                } else {
-                    LdOp op{row, S, a.ns};
-                    fast = gt_fast<6>(buf, S, le, op);
-                    if (fast) st = op.st;
-                }
-                if (!fast) {
-                    // rewrite the row: the failed fast sweep may have stored codes
-                    for (int k = lane(); k < a.kpad; k += kWave) row[k] = -1;
-                    ld_general(buf, S, le, a.ns, row, st, a.stoi_mode);
-                }
-                out.valid = 1;
-                out.pos = pos;
-                out.cnt = wave_sum(st.cnt);
-                out.sx = wave_sum(st.sx);
-                out.sx2 = wave_sum(st.sx2);
-                out.chrom = (uint64_t)ls;
-                out.chrom_len = (uint32_t)(t[0] - ls);
-                out.id = (uint64_t)(t[1] + 1);
-                out.id_len = (uint32_t)(t[2] - t[1] - 1);
-            }
-        }
+        const LdLine out = ld_line(buf, ls, le, a, G + li * (uint64_t)a.kpad, lrow, lds, false);
         if (lane() == 0) lines[li] = out;
     }
 }
 
-// gather valid variants into compact order; stats -> fp64 varX exactly as computeStats
+// a valid line's variant record and fast-kernel terms: stats -> fp64 varX exactly as
+// computeStats (:243-258); `line` = the line's index (its slot, for the walk)
+__device__ __forceinline__ void ld_var_of(const LdLine &L, uint64_t line, int ns, LdVar &o, LdFast &f) {
+    o.pos = L.pos;
+    o.cnt = (int)L.cnt;
+    o.sx = (int)L.sx;
+    o.sx2 = (int)L.sx2;
+    double varx = 0.0;
+    if (L.cnt > 0) {
+        double mean = __ddiv_rn((double)L.sx, (double)L.cnt);
+        varx = __dsub_rn(__ddiv_rn((double)L.sx2, (double)L.cnt), __dmul_rn(mean, mean));
+    }
+    o.varx = varx;
+    o.complete = L.cnt == (uint32_t)ns;
+    o.chrom = L.chrom;
+    o.chrom_len = L.chrom_len;
+    o.id = L.id;
+    o.id_len = L.id_len;
+    o.line = line;
+    f.mx = 0.0;
+    f.vx = 0.0;
+    f.sq = 0.0;
+    f.vxp = __longlong_as_double(0x7FF0000000000000ll);  // +inf: never a prefilter candidate
+    if (L.cnt > 0) {
+        const double dn = (double)L.cnt;
+        f.mx = __ddiv_rn((double)L.sx, dn);
+        f.vx = __dsub_rn(__ddiv_rn((double)L.sx2, dn), __dmul_rn(f.mx, f.mx));
+        f.sq = f.vx > 0.0 ? __dsqrt_rn(f.vx) : 0.0;
+        const int64_t V = (int64_t)L.cnt * (int64_t)L.sx2 - (int64_t)L.sx * (int64_t)L.sx;
+        if (V > 0) f.vxp = (double)V;
+    }
+    f.sx = (int)L.sx;
+    f.pos = L.pos;
+}
+
+// gather valid variants into compact order
 __global__ void k_ld_compact(const LdLine *__restrict__ lines, const uint64_t *__restrict__ vidx,
                              const uint64_t *n_lines_p, int kpad, int ns, const int8_t *__restrict__ G,
                              int8_t *__restrict__ Gc, LdVar *__restrict__ vars, LdFast *__restrict__ fv) {
@@ -322,40 +431,256 @@ __global__ void k_ld_compact(const LdLine *__restrict__ lines, const uint64_t *_
         for (int k = threadIdx.x; k < kpad / 16; k += blockDim.x) dst[k] = src[k];
         if (threadIdx.x == 0) {
             LdVar o;
-            o.pos = L.pos;
-            o.cnt = (int)L.cnt;
-            o.sx = (int)L.sx;
-            o.sx2 = (int)L.sx2;
-            double varx = 0.0;
-            if (L.cnt > 0) {
-                double mean = __ddiv_rn((double)L.sx, (double)L.cnt);
-                varx = __dsub_rn(__ddiv_rn((double)L.sx2, (double)L.cnt), __dmul_rn(mean, mean));
-            }
-            o.varx = varx;
-            o.complete = L.cnt == (uint32_t)ns;
-            o.chrom = L.chrom;
-            o.chrom_len = L.chrom_len;
-            o.id = L.id;
-            o.id_len = L.id_len;
-            o.line = li;
-            vars[v] = o;
             LdFast f;
-            f.mx = 0.0;
-            f.vx = 0.0;
-            f.sq = 0.0;
-            f.vxp = __longlong_as_double(0x7FF0000000000000ll);  // +inf: never a prefilter candidate
-            if (L.cnt > 0) {
-                const double dn = (double)L.cnt;
-                f.mx = __ddiv_rn((double)L.sx, dn);
-                f.vx = __dsub_rn(__ddiv_rn((double)L.sx2, dn), __dmul_rn(f.mx, f.mx));
-                f.sq = f.vx > 0.0 ? __dsqrt_rn(f.vx) : 0.0;
-                const int64_t V = (int64_t)L.cnt * (int64_t)L.sx2 - (int64_t)L.sx * (int64_t)L.sx;
-                if (V > 0) f.vxp = (double)V;
-            }
-            f.sx = (int)L.sx;
-            f.pos = L.pos;
+            ld_var_of(L, li, ns, o, f);
+            vars[v] = o;
             fv[v] = f;
         }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// the LD walk: the parse without a separate line index (vcfxg_af_walk.hip's scheme).  Walker
+// wk's lines -- those starting in [b(chunk start), b(chunk end)), vcfxg_walk.h walker_lines --
+// go to slots wk * cap_w + n: each one's LdLine and int8 code row (kpad bytes, every byte
+// written: codes, then -1).  Per line: the kWin window (LDS-DMA'd during the previous line's
+// sweep) gives the first '\n' if the line is short, the first 9 tabs and POS; the end is the
+// window's '\n', or predicted from the previous fixed-stride record (S + span, accepted when
+// the sweep validates [S, E) and the byte at E is the '\n'), or searched for; the fixed-stride
+// sweep (gt_fast + LdOpW) composes the codes in LDS.  Every other line (a head past the
+// window, a POS of more than 10 digits or not all digits, a record off the fixed stride, the
+// region filter, the stoi parse mode: kGen) goes to the pending list, and k_ld_pending runs
+// ld_line on its exact bounds (the k_ld_parse path).  k_ld_wcompact then gathers the valid
+// lines in file order.
+// ---------------------------------------------------------------------------------------
+#ifndef VCFXG_LD_WALK_MINW
+#define VCFXG_LD_WALK_MINW 5
+#endif
+template <bool kGen>
+__global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(VCFXG_LD_WALK_MINW))) void k_ld_walk(const char *__restrict__ buf, int64_t lo, int64_t hi,
+                                                          int64_t chunk, int64_t n_walkers, int64_t span0,
+                                                          uint64_t cap_w, LdParseArgs a, int8_t *__restrict__ G,
+                                                          LdLine *__restrict__ lines, uint64_t *__restrict__ wcount,
+                                                          uint64_t *__restrict__ wvalid, unsigned *overflow,
+                                                          unsigned long long *pend_n, uint64_t *__restrict__ pend) {
+    __shared__ uint4 win[kWalkWaves][2][kWave];  // two window slots per wave (double buffer)
+    __shared__ __attribute__((aligned(16))) int8_t lrows[kWalkWaves][kLdLdsRow];
+    const int wv = threadIdx.x / kWave;
+    const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + wv);
+    if (wk >= n_walkers) return;
+    int8_t *lrow = lrows[wv];
+    const auto lrow3 = (__attribute__((address_space(3))) int8_t *)lrow;
+    const int64_t cs = lo + wk * chunk;
+    const int64_t ce = std::min<int64_t>(cs + chunk, hi);
+    int64_t L, ce2;
+    walker_lines(buf, lo, hi, cs, ce, L, ce2);
+    int64_t span = span0;  // predicted '\n' distance from the sample start
+    uint64_t n = 0, nv = 0;
+    const uint64_t base = (uint64_t)wk * cap_w;
+    int cur = 0;
+    int64_t A = L & ~(int64_t)15;
+    if (L < ce2) prefetch_window(buf, A, hi, win[wv][cur]);
+    while (L < ce2) {
+        if (n >= cap_w) {
+            if (lane() == 0) atomicOr(overflow, 1u);
+            break;
+        }
+        // ---- 1. the window: first '\n', 9 tabs, POS
+        const int Lr = (int)(L - A);
+        const uint4 *cw = win[wv][cur];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t w4 = reinterpret_cast<const uint32_t *>(cw)[lane()];
+        const int hr = (int)std::min<int64_t>(hi - A, kWin);
+        const uint32_t rg = range4(Lr, hr);
+        const int N1r = first_match<4>(zero_bytes(w4 ^ kRepNl) & rg);
+        int rt[9] = {};
+        const uint32_t ntab = first_tabs<4>(zero_bytes(w4 ^ kRepTab) & rg, N1r >= 0 ? N1r : hr, rt);
+        const uint32_t first = dword_byte(w4, Lr);
+        const int64_t wend = A + hr;
+        bool head = !kGen && ntab >= 9 && first != '#';
+        int pos = 0;
+        if (head) {  // fastParseInt (:188-197) on <= 10 digits (longer ones: ld_line's wrapping loop)
+            const int p0 = rt[0] + 1, p1 = rt[1];
+            head = p1 > p0 && p1 - p0 <= 10;
+            uint32_t v = 0;
+            for (int o = p0; head && o < p1; o++) {
+                const uint32_t ch = dword_byte(w4, o);
+                head = ch - '0' < 10u;
+                v = v * 10u + (ch - '0');
+            }
+            pos = (int)v;
+        }
+        // ---- 2. the line end
+        const int64_t S = head ? A + rt[8] + 1 : 0;
+        int64_t E;
+        bool predicted = false;
+        if (N1r >= 0) E = A + N1r;
+        else if (head && span > 0 && S + span <= hi) {
+            E = S + span;
+            predicted = true;
+        } else E = scan_nl(buf, wend, hi);
+        const uint32_t sep_w = head && rt[8] + 2 < hr ? dword_byte(w4, rt[8] + 2) : 0u;
+        const int nxt = cur ^ 1;
+        int64_t An = std::max<int64_t>(E - 1, 0) & ~(int64_t)15;
+        bool pending = true;  // the next window's prefetch is still to be issued
+        auto pre = [&]() {
+            prefetch_window(buf, An, hi, win[wv][nxt]);
+            pending = false;
+        };
+        // ---- 3. the fixed-stride sweep into the LDS row
+        LdOpW op{{lrow3, S, a.ns}};
+        bool ok = head && gt_fast<6>(buf, S, E, op, sep_w, pre);
+        if (pending) pre();
+        if (predicted) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t be = slot_byte(win[wv][nxt], (int)(E - An));
+            const bool endok = E < hi ? be == '\n' : true;
+            if (!(ok && endok)) {
+                const int64_t Et = scan_nl(buf, wend, hi);
+                ok = false;
+                if (Et != E) {  // the line again with its true bounds
+                    E = Et;
+                    An = std::max<int64_t>(E - 1, 0) & ~(int64_t)15;
+                    pending = true;
+                    op = LdOpW{{lrow3, S, a.ns}};
+                    ok = gt_fast<6>(buf, S, E, op, sep_w, pre);
+                    if (pending) pre();
+                }
+            }
+        }
+        int8_t *row = G + (base + n) * (uint64_t)a.kpad;
+        LdLine out;
+        if (ok) {
+            // ---- 4. the row: codes [0, nout) from LDS, -1 up to kpad (16 B stores)
+            const int64_t nr = (E - S + 1) / 4;
+            const uint32_t nout = (uint32_t)(nr < a.ns ? nr : a.ns);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            for (uint32_t o = (uint32_t)lane() * 16; o < (uint32_t)a.kpad; o += kWave * 16) {
+                uint4 val = make_uint4(~0u, ~0u, ~0u, ~0u);
+                if (o < nout) {
+                    val = *reinterpret_cast<const uint4 *>(lrow + o);
+                    if (o + 16 > nout) {  // the codes' last block: -1 past them
+                        const int j = (int)(nout - o);
+                        auto fill = [&](uint32_t x, int q) {
+                            const int kq = j - 4 * q;
+                            const uint32_t keep = kq >= 4 ? ~0u : kq <= 0 ? 0u : ((1u << (8 * kq)) - 1u);
+                            return (x & keep) | ~keep;
+                        };
+                        val = make_uint4(fill(val.x, 0), fill(val.y, 1), fill(val.z, 2), fill(val.w, 3));
+                    }
+                }
+                *reinterpret_cast<uint4 *>(row + o) = val;
+            }
+            // the next record's LDS writes must not pass these reads
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            out.valid = 1;
+            out.pos = pos;
+            out.cnt = wave_sum32(op.st.cnt);
+            out.sx = wave_sum32(op.st.sx);
+            out.sx2 = wave_sum32(op.st.sx2);
+            out.chrom = (uint64_t)L;
+            out.chrom_len = (uint32_t)(rt[0] - Lr);
+            out.id = (uint64_t)(A + rt[1] + 1);
+            out.id_len = (uint32_t)(rt[2] - rt[1] - 1);
+            span = E - S;
+        } else {  // k_ld_pending parses the line on its exact bounds [L, E)
+            out.valid = 0;
+            out.chrom = (uint64_t)L;
+            out.id = (uint64_t)E;
+            if (lane() == 0) pend[atomicAdd(pend_n, 1ull)] = base + n;
+        }
+        if (lane() == 0) lines[base + n] = out;
+        nv += out.valid;
+        n++;
+        L = E + 1;
+        A = An;
+        cur = nxt;
+    }
+    if (lane() == 0) {
+        wcount[wk] = n;
+        wvalid[wk] = nv;
+    }
+}
+
+// the walk's pending lines (bounds [chrom, id) in their LdLine): one wave each, ld_line on the
+// exact bounds into the slot's row; a valid one counts in its walker's wvalid (before the scan)
+__global__ __launch_bounds__(256) void k_ld_pending(const char *__restrict__ buf, LdParseArgs a, uint64_t cap_w,
+                                                    const unsigned long long *pend_n, const uint64_t *__restrict__ pend,
+                                                    int8_t *__restrict__ G, LdLine *__restrict__ lines,
+                                                    uint64_t *wvalid) {
+    __shared__ int64_t scratch[4][16];
+    __shared__ __attribute__((aligned(16))) int8_t lrows[4][kLdLdsRow];
+    int64_t *lds = scratch[threadIdx.x / kWave];
+    int8_t *lrow = lrows[threadIdx.x / kWave];
+    const uint64_t np = *pend_n;
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t k = wid; k < np; k += nw) {
+        const uint64_t slot = uniform64((int64_t)pend[k]);
+        const LdLine b = lines[slot];
+        const LdLine out = ld_line(buf, (int64_t)b.chrom, (int64_t)b.id, a, G + slot * (uint64_t)a.kpad, lrow, lds, true);
+        if (lane() == 0) {
+            lines[slot] = out;
+            if (out.valid) atomicAdd(reinterpret_cast<unsigned long long *>(wvalid + slot / cap_w), 1ull);
+        }
+    }
+}
+
+// walk slots -> variants in file order, one wave per walker (vbase: exclusive scan of the
+// walkers' valid-line counts): each valid line's LdVar (line = its slot) / LdFast / prefix
+// length (k_ld_prefix_len); flags bit 0: some variant misses a call (its rows are gathered into
+// Gc, k_ld_gather); m_out = M.  The FP4 rows follow once M is known (k_ld_pack4, slots through
+// vars[v].line: every row in parallel)
+__global__ __launch_bounds__(256) void k_ld_wcompact(int64_t n_walkers, uint64_t cap_w,
+                                                     const uint64_t *__restrict__ wcount,
+                                                     const uint64_t *__restrict__ vbase,
+                                                     const LdLine *__restrict__ lines, int ns,
+                                                     const char *__restrict__ buf, int id_dot_to_pos,
+                                                     LdVar *__restrict__ vars, LdFast *__restrict__ fv,
+                                                     uint64_t *__restrict__ plen, unsigned *flags, uint64_t *m_out) {
+    const int64_t nwaves = (int64_t)gridDim.x * (256 / kWave);
+    const int l = lane();
+    bool incomplete = false;
+    for (int64_t w = (int64_t)blockIdx.x * (256 / kWave) + threadIdx.x / kWave; w < n_walkers; w += nwaves) {
+        const uint64_t n = wcount[w], v0 = vbase[w], s0 = (uint64_t)w * cap_w;
+        uint64_t run = 0;
+        for (uint64_t i0 = 0; i0 < n; i0 += kWave) {
+            const uint64_t i = i0 + l;
+            LdLine x;
+            x.valid = 0;
+            if (i < n) x = lines[s0 + i];
+            const uint64_t bal = __ballot(x.valid != 0);
+            if (x.valid) {
+                const uint64_t v = v0 + run + (uint64_t)__popcll(bal & ((1ull << l) - 1ull));
+                LdVar o;
+                LdFast f;
+                ld_var_of(x, s0 + i, ns, o, f);
+                vars[v] = o;
+                fv[v] = f;
+                uint64_t len = o.chrom_len + 1 + int_len(o.pos) + 1;
+                if (id_dot_to_pos && o.id_len == 1 && buf[o.id] == '.') len += o.chrom_len + 1 + int_len(o.pos);
+                else len += o.id_len;
+                plen[v] = len;
+                incomplete = incomplete || !o.complete;
+            }
+            run += (uint64_t)__popcll(bal);
+        }
+    }
+    if (__any(incomplete) && lane() == 0) atomicOr(flags, 1u);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *m_out = vbase[n_walkers];
+}
+
+// the int8 rows of the walk's variants in compact order (when some variant misses a call: the
+// sparse-missing and masked kernels' planes are built from Gc)
+__global__ void k_ld_gather(const LdVar *__restrict__ vars, uint64_t m, const int8_t *__restrict__ G, int kpad,
+                            int8_t *__restrict__ Gc) {
+    for (uint64_t v = blockIdx.x; v < m; v += gridDim.x) {
+        const uint4 *src = reinterpret_cast<const uint4 *>(G + vars[v].line * (uint64_t)kpad);
+        uint4 *dst = reinterpret_cast<uint4 *>(Gc + v * (uint64_t)kpad);
+        for (int k = threadIdx.x; k < kpad / 16; k += blockDim.x) dst[k] = src[k];
     }
 }
 
@@ -601,28 +926,6 @@ __global__ void k_ld_matrix_diag(uint64_t m, char *__restrict__ cells) {
 // ---------------------------------------------------------------------------------------
 // text: per-variant "chrom\tpos\tid" prefixes, then pair lines
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int int_len(int v) {
-    unsigned u = v < 0 ? 0u - (unsigned)v : (unsigned)v;
-    int n = v < 0 ? 1 : 0;
-    do {
-        n++;
-        u /= 10u;
-    } while (u);
-    return n;
-}
-__device__ __forceinline__ char *put_int(char *o, int v) {  // formatInt :214-225 / to_string
-    unsigned u = v < 0 ? 0u - (unsigned)v : (unsigned)v;
-    if (v < 0) *o++ = '-';
-    char t[12];
-    int k = 0;
-    do {
-        t[k++] = (char)('0' + u % 10u);
-        u /= 10u;
-    } while (u);
-    while (k) *o++ = t[--k];
-    return o;
-}
-
 __global__ void k_ld_prefix_len(const LdVar *__restrict__ vars, uint64_t m, const char *__restrict__ buf,
                                 int id_dot_to_pos, uint64_t *__restrict__ len) {
     for (uint64_t v = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; v < m; v += gridDim.x * (uint64_t)blockDim.x) {
@@ -763,6 +1066,38 @@ hipError_t launch_ld_parse(const char *buf, int64_t data_start, const uint64_t *
     if (!n_lines_host) return hipSuccess;
     hipLaunchKernelGGL(k_ld_parse, dim3(gridfor(n_lines_host, 4, 8192)), dim3(256), 0, s, buf, data_start, line_end,
                        n_lines_dev, a, G, lines);
+    return hipGetLastError();
+}
+hipError_t launch_ld_walk(const char *buf, int64_t lo, int64_t hi, int64_t chunk, int64_t span0, uint64_t cap_w,
+                          const LdParseArgs &a, int8_t *G, LdLine *lines, uint64_t *wcount, uint64_t *wvalid,
+                          unsigned *overflow, unsigned long long *pend_n, uint64_t *pend, hipStream_t s) {
+    if (hi <= lo || chunk <= 0 || a.ns > kLdLdsRow) return hipErrorInvalidValue;
+    const int64_t nw = (hi - lo + chunk - 1) / chunk;
+    const unsigned grid = (unsigned)((nw + kWalkWaves - 1) / kWalkWaves);
+    if (a.has_region || a.stoi_mode)
+        hipLaunchKernelGGL(k_ld_walk<true>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, span0, cap_w,
+                           a, G, lines, wcount, wvalid, overflow, pend_n, pend);
+    else
+        hipLaunchKernelGGL(k_ld_walk<false>, dim3(grid), dim3(kWalkThreads), 0, s, buf, lo, hi, chunk, nw, span0, cap_w,
+                           a, G, lines, wcount, wvalid, overflow, pend_n, pend);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // the pending lines: a grid-stride loop over the device count (none: every wave exits)
+    hipLaunchKernelGGL(k_ld_pending, dim3(256), dim3(256), 0, s, buf, a, cap_w, pend_n, pend, G, lines, wvalid);
+    return hipGetLastError();
+}
+hipError_t launch_ld_wcompact(int64_t nw, uint64_t cap_w, const uint64_t *wcount, const uint64_t *vbase,
+                              const LdLine *lines, int ns, const char *buf, int id_dot_to_pos, LdVar *vars, LdFast *fv,
+                              uint64_t *plen, unsigned *flags, uint64_t *m_out, hipStream_t s) {
+    if (nw <= 0) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)std::min<int64_t>((nw + 3) / 4, 4096);
+    hipLaunchKernelGGL(k_ld_wcompact, dim3(grid), dim3(256), 0, s, nw, cap_w, wcount, vbase, lines, ns, buf,
+                       id_dot_to_pos, vars, fv, plen, flags, m_out);
+    return hipGetLastError();
+}
+hipError_t launch_ld_gather(const LdVar *vars, uint64_t m, const int8_t *G, int kpad, int8_t *Gc, hipStream_t s) {
+    if (!m) return hipSuccess;
+    hipLaunchKernelGGL(k_ld_gather, dim3(gridfor(m, 1, 65536)), dim3(256), 0, s, vars, m, G, kpad, Gc);
     return hipGetLastError();
 }
 hipError_t launch_ld_compact(const LdLine *lines, const uint64_t *vidx, const uint64_t *n_lines_dev,

@@ -1145,13 +1145,13 @@ hipError_t launch_ld_sparse(int pass, const uint8_t *Gp, const LdSparse &sp, con
 // 0x0/0x2/0x4, two per byte (element 2b low nibble), zero from ns on; an incomplete row's
 // missing code packs as 0 (such rows never reach k_ld_fast)
 __global__ void k_ld_pack4(const int8_t *__restrict__ Gc, uint64_t m, int kpad, int ns, uint8_t *__restrict__ Gp,
-                           int kp4) {
+                           int kp4, const LdVar *__restrict__ vars) {
     const int per = kp4 / 16;  // 16 output bytes per thread
     const uint64_t total = m * (uint64_t)per;
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t v = t / per;
         const int c = (int)(t - v * per);
-        const int8_t *row = Gc + v * (uint64_t)kpad;
+        const int8_t *row = Gc + (vars ? vars[v].line : v) * (uint64_t)kpad;
         uint32_t in[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // 32 codes, 4 per dword
         if (c * 32 + 32 <= kpad) {
             const uint4 u0 = reinterpret_cast<const uint4 *>(row)[2 * c];
@@ -1170,12 +1170,13 @@ __global__ void k_ld_pack4(const int8_t *__restrict__ Gc, uint64_t m, int kpad, 
     }
 }
 
-hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s) {
+hipError_t launch_ld_pack4(const int8_t *Gc, uint64_t m, int kpad, int ns, uint8_t *Gp, int kp4, hipStream_t s,
+                           const LdVar *vars) {
     if (!m) return hipSuccess;
     if (kp4 % 64 || 2 * (int64_t)kp4 < ns) return hipErrorInvalidValue;
     const uint64_t total = m * (uint64_t)(kp4 / 16);
     const unsigned grid = (unsigned)std::min<uint64_t>((total + 255) / 256, 65536);
-    hipLaunchKernelGGL(k_ld_pack4, dim3(grid), dim3(256), 0, s, Gc, m, kpad, ns, Gp, kp4);
+    hipLaunchKernelGGL(k_ld_pack4, dim3(grid), dim3(256), 0, s, Gc, m, kpad, ns, Gp, kp4, vars);
     return hipGetLastError();
 }
 
@@ -1198,7 +1199,10 @@ hipError_t launch_mfma_f4_selftest(const uint8_t *A, const uint8_t *B, float *C,
 
 // per-row scan of the pair-count table: one wave per output row j, the u16 counts of its
 // window slots (column blocks ifirst(J) .. J, every one written by the count kernels; the
-// table is not cleared) -> u32 offsets inside the row + the row's total
+// table is not cleared; nb is a multiple of 8, so each lane reads 8 slots as one 16 B load)
+// -> the row's total and the u32 offsets inside the row of the slots that HOLD pairs (the
+// emit passes read no other slot's offset).  Almost every slot is empty: a 512-slot step
+// whose counts are all zero costs its loads and one ballot, and writes nothing
 __global__ __launch_bounds__(256) void k_ld_rowscan(const uint16_t *__restrict__ cnt, uint64_t rows, uint64_t nb,
                                                     uint64_t j_lo, uint64_t window, uint32_t *__restrict__ in_row,
                                                     uint64_t *__restrict__ rowtot) {
@@ -1207,16 +1211,37 @@ __global__ __launch_bounds__(256) void k_ld_rowscan(const uint16_t *__restrict__
     for (uint64_t j = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 64; j < rows; j += nw) {
         const uint64_t J = (j_lo + j) / kLdBlock, jr0 = J * kLdBlock;
         const uint64_t I0 = jr0 > window ? (jr0 - window) / kLdBlock : 0;
-        const uint64_t ns = J - I0 + 1 < nb ? J - I0 + 1 : nb;
+        const uint32_t ns = (uint32_t)(J - I0 + 1 < nb ? J - I0 + 1 : nb);
         const uint16_t *c = cnt + j * nb;
         uint32_t *o = in_row + j * nb;
         uint32_t run = 0;
-        for (uint64_t s0 = 0; s0 < ns; s0 += 64) {
-            const uint64_t sl = s0 + l;
-            const uint32_t v = sl < ns ? c[sl] : 0u;
-            const uint32_t incl = wave_incl_scan(v);
-            if (sl < ns) o[sl] = run + incl - v;
-            run += wave_bcast(incl, 63);
+        for (uint32_t s0 = 0; s0 < ns; s0 += 512) {
+            const uint32_t sl = s0 + 8u * (uint32_t)l;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (sl < ns) v = *reinterpret_cast<const uint4 *>(c + sl);
+            // slots past the row's window (the table's padding, never written) read as 0
+            const uint32_t past = sl + 8u > ns ? (sl < ns ? sl + 8u - ns : 8u) : 0u;
+            uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int lo_e = 2 * q, hi_e = 2 * q + 1;  // elements of dword q
+                if (8 - (int)past <= lo_e) w[q] = 0u;
+                else if (8 - (int)past <= hi_e) w[q] &= 0xFFFFu;
+            }
+            const uint32_t t = (w[0] & 0xFFFFu) + (w[0] >> 16) + (w[1] & 0xFFFFu) + (w[1] >> 16) + (w[2] & 0xFFFFu) +
+                               (w[2] >> 16) + (w[3] & 0xFFFFu) + (w[3] >> 16);
+            if (!__ballot(t != 0u)) continue;
+            const uint32_t incl = wave_incl_scan32(t);
+            uint32_t acc = run + incl - t;
+            if (t) {
+#pragma unroll
+                for (int e = 0; e < 8; e++) {
+                    const uint32_t x = (w[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+                    if (x) o[sl + e] = acc;
+                    acc += x;
+                }
+            }
+            run += __builtin_amdgcn_readlane(incl, 63);
         }
         if (l == 0) rowtot[j] = run;
     }
@@ -1233,7 +1258,9 @@ hipError_t launch_ld_rowscan(const uint16_t *cnt, uint64_t rows, uint64_t nb, ui
 
 // per kLdFastBlock-variant group: 1 if every variant of the group is complete; 2 (sparse) if
 // every variant misses at most kLdSparseMax calls; else 0
-__global__ void k_ld_groups(const LdVar *__restrict__ vars, uint64_t m, int ns, int sparse, uint8_t *__restrict__ gflag) {
+__global__ void k_ld_groups(const LdVar *__restrict__ vars, uint64_t m, int ns, int sparse, uint8_t *__restrict__ gflag,
+                            const uint64_t *m_dev) {
+    if (m_dev) m = *m_dev;
     const uint64_t g = blockIdx.x * (uint64_t)blockDim.x / 64 + threadIdx.x / 64;
     const uint64_t ng = (m + kFB - 1) / kFB;
     if (g >= ng) return;
@@ -1251,10 +1278,11 @@ __global__ void k_ld_groups(const LdVar *__restrict__ vars, uint64_t m, int ns, 
     if (l == 0) gflag[g] = ok ? 1 : (sparse && sp) ? 2 : 0;
 }
 
-hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, int ns, int sparse, uint8_t *gflag, hipStream_t s) {
+hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, int ns, int sparse, uint8_t *gflag, hipStream_t s,
+                            const uint64_t *m_dev) {
     const uint64_t ng = (m + kFB - 1) / kFB;
     if (!ng) return hipSuccess;
-    hipLaunchKernelGGL(k_ld_groups, dim3((unsigned)((ng + 3) / 4)), dim3(256), 0, s, vars, m, ns, sparse, gflag);
+    hipLaunchKernelGGL(k_ld_groups, dim3((unsigned)((ng + 3) / 4)), dim3(256), 0, s, vars, m, ns, sparse, gflag, m_dev);
     return hipGetLastError();
 }
 

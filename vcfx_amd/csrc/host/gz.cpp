@@ -82,6 +82,64 @@ bool bgzf_chain(const char *src_c, size_t n, std::vector<BgzfSpan> &ms, uint64_t
     return !ms.empty();
 }
 
+// one member at h (n bytes available): 1 = a member of *bs bytes (validated as bgzf_chain does),
+// 0 = more bytes needed, -1 = not a BGZF member
+static int chain_member(const uint8_t *h, size_t n, size_t *bs, uint32_t *olen) {
+    if (n < 4) return 0;
+    if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || h[3] != 4) return -1;
+    if (n < 18) return 0;
+    const size_t xlen = le16(h + 10);
+    if (n < 12 + xlen) return 0;
+    const size_t b = bgzf_bsize(h, n);
+    if (!b || b < 12 + xlen + 8 || b > 65536) return -1;
+    if (b > n) return 0;
+    *bs = b;
+    *olen = le32(h + b - 4);
+    return *olen > 65536 ? -1 : 1;
+}
+
+void BgzfStream::feed(const char *d_c, size_t len) {
+    const uint8_t *d = (const uint8_t *)d_c;
+    const uint64_t off = fed;
+    fed += len;
+    if (bad) return;
+    size_t r = 0;  // the next unread byte of d
+    if (!carry.empty()) {  // complete the member at pos from this piece (a member is <= 64 KiB)
+        const size_t had = carry.size(), take = std::min<size_t>(len, 65536 + 64 - had);
+        carry.insert(carry.end(), d_c, d_c + take);
+        size_t bs = 0;
+        uint32_t olen = 0;
+        const int k = chain_member((const uint8_t *)carry.data(), carry.size(), &bs, &olen);
+        if (k < 0 || (k == 0 && take < len)) {
+            bad = true;
+            return;
+        }
+        if (k == 0) return;  // (the whole piece went to the carry: more to come)
+        members.push_back({pos, (uint32_t)bs, olen});
+        out += olen;
+        r = pos + bs - off;  // (bs > had: the member ends inside this piece)
+        pos += bs;
+        carry.clear();
+    }
+    while (r < len) {
+        size_t bs = 0;
+        uint32_t olen = 0;
+        const int k = chain_member(d + r, len - r, &bs, &olen);
+        if (k < 0) {
+            bad = true;
+            return;
+        }
+        if (k == 0) {  // the member continues in the next piece
+            carry.assign(d_c + r, d_c + len);
+            return;
+        }
+        members.push_back({pos, (uint32_t)bs, olen});
+        out += olen;
+        pos += bs;
+        r += bs;
+    }
+}
+
 bool gz_inflate_member(const char *src, size_t n, char *dst, size_t cap, size_t *got) {
     return inflate_member((const uint8_t *)src, n, dst, cap, got);
 }

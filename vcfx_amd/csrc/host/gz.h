@@ -28,6 +28,19 @@ struct BgzfSpan {
     uint32_t len, olen;
 };
 bool bgzf_chain(const char *src, size_t n, std::vector<BgzfSpan> &members, uint64_t *total);
+// bgzf_chain on a stream fed in order, piece by piece (a staging ring's slots): feed(d, len) takes
+// the next len bytes; a member whose bytes span pieces is completed from a carry of at most
+// 64 KiB.  ok(total) after the last piece: the same chain bgzf_chain returns on the whole stream.
+struct BgzfStream {
+    std::vector<BgzfSpan> members;
+    uint64_t out = 0;   // the sum of ISIZE so far
+    uint64_t pos = 0;   // the next member's first byte
+    uint64_t fed = 0;   // bytes fed so far
+    bool bad = false;   // not a BGZF chain
+    std::vector<char> carry;  // bytes [pos, fed) of a member not yet complete
+    void feed(const char *d, size_t len);
+    bool ok(uint64_t total) const { return !bad && carry.empty() && pos == total && fed == total && !members.empty(); }
+};
 // one gzip member [src, src+n) inflated into [dst, dst+cap) by zlib (CRC and ISIZE checked);
 // *got = its bytes; false on any error
 bool gz_inflate_member(const char *src, size_t n, char *dst, size_t cap, size_t *got);

@@ -228,6 +228,188 @@ bool pread_full(int fd, char *dst, size_t len, size_t off, int *err) {
 }
 }  // namespace
 
+// A BGZF file (open_file_device's gzip branch; the tools that take device BGZF, bgzf_device):
+// the compressed bytes go through the pinned file ring to the device as they are read
+// (vcfxg_bgzf_stage, DMA overlapping the reads), the member chain is parsed from the ring's
+// slots in order (BgzfStream), the head -- members inflated here until the output holds the
+// '#CHROM' line and 64 KiB after it -- comes from the first bytes read (first[0, fn)), then every
+// member is inflated on the device (vcfxg_ingest_bgzf).  No mapping of the file, no page
+// population, no pageable copy.  false (nothing changed): the caller maps the file instead
+// (decompress() then takes the host inflate, or device_bgzf on the mapping).
+bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t fn) {
+    const char *e = getenv("VCFX_BGZF_DEVICE");
+    if ((e && e[0] == '0') || t_shard || !bgzf_device || !gzip_ok || !gzip_enabled()) return false;
+    // the head
+    const size_t kHeadMax = ((size_t)64 << 20) + 65536;
+    void *hm = mmap(nullptr, kHeadMax, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (hm == MAP_FAILED) return false;
+    char *head = (char *)hm;
+    size_t hn = 0, scanned = 0, at = 0;
+    bool chrom = false;
+    size_t chrom_end = 0;
+    {
+        BgzfStream hs;  // (members wholly inside first[0, fn))
+        hs.feed(first, fn);
+        for (const BgzfSpan &m : hs.members) {
+            if (chrom && hn - chrom_end >= 65536) break;
+            if (hn + m.olen > kHeadMax) break;
+            size_t got = 0;
+            if (!gz_inflate_member(first + m.off, m.len, head + hn, m.olen, &got) || got != m.olen) break;
+            hn += got;
+            at = m.off + m.len;
+            while (!chrom && scanned < hn) {
+                const char *s0 = head + scanned;
+                const char *nl = (const char *)memchr(s0, '\n', hn - scanned);
+                if (!nl) break;
+                chrom = is_chrom_line(s0, (size_t)(nl - s0));
+                scanned = (size_t)(nl - head) + 1;
+                if (chrom) chrom_end = scanned;
+            }
+        }
+    }
+    (void)at;
+    vcfxg_ctx *g = chrom ? gpu_quiet() : nullptr;
+    if (!g) {
+        munmap(hm, kHeadMax);
+        return false;
+    }
+    phase("bgzf head inflated");
+    const size_t kSlot = file_slot();
+    std::vector<void *> ring_;
+    {
+        std::lock_guard<std::mutex> lk(g_ring_mu);
+        if (g_file_ring.busy) {
+            munmap(hm, kHeadMax);
+            return false;
+        }
+        if (g_file_ring.ctx != g || g_file_ring.slot != kSlot || g_file_ring.slots.size() != file_slots()) {
+            if (g_file_ring.ctx)
+                for (void *r : g_file_ring.slots) vcfxg_host_free(g_file_ring.ctx, r);
+            g_file_ring = FileRing{};
+            bool ok = true;
+            for (size_t i = 0; i < file_slots() && ok; i++) {
+                void *r = nullptr;
+                ok = vcfxg_host_alloc(g, kSlot, &r) == VCFXG_OK;
+                if (ok) g_file_ring.slots.push_back(r);
+            }
+            if (ok) {
+                g_file_ring.ctx = g;
+                g_file_ring.slot = kSlot;
+            } else {
+                for (void *r : g_file_ring.slots) vcfxg_host_free(g, r);
+                g_file_ring.slots.clear();
+            }
+        }
+        ring_ = g_file_ring.slots;
+        g_file_ring.busy = !ring_.empty();
+    }
+    struct RingRelease {
+        bool on;
+        ~RingRelease() {
+            if (!on) return;
+            std::lock_guard<std::mutex> lk(g_ring_mu);
+            g_file_ring.busy = false;
+        }
+    } ring_release{!ring_.empty()};
+    if (ring_.empty() || vcfxg_ingest_begin(g, 0) != VCFXG_OK) {
+        munmap(hm, kHeadMax);
+        return false;
+    }
+    // chunk i = [i*slot, ...) into slot i % S, read by T reader threads, staged in order by this
+    // thread (which parses the member chain from the slot before its DMA is waited for)
+    const size_t S = ring_.size(), inflight = std::max<size_t>(1, S / 2);
+    const size_t nchunks = (total + kSlot - 1) / kSlot;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t T = std::max<size_t>(1, std::min<size_t>({S - inflight, env_bytes("VCFX_FILE_THREADS", 8),
+                                                           hw ? (size_t)hw : 1}));
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<long long> filled(S, -1), freed(S, -1);
+    bool stop = false, ok = true;
+    std::atomic<int> rerr{0};
+    std::vector<std::thread> readers;
+    for (size_t t = 0; t < T; t++)
+        readers.emplace_back([&, t] {
+            for (size_t i = t; i < nchunks; i += T) {
+                const size_t s = i % S;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop || i < S || freed[s] >= (long long)(i - S); });
+                    if (stop) return;
+                }
+                const size_t off = i * kSlot, len = std::min(kSlot, total - off);
+                int er = 0;
+                const bool r = pread_full(fd, (char *)ring_[s], len, off, &er);
+                std::lock_guard<std::mutex> lk(mu);
+                if (!r) {
+                    rerr = er ? er : EIO;
+                    stop = true;
+                } else {
+                    filled[s] = (long long)i;
+                }
+                cv.notify_all();
+                if (!r) return;
+            }
+        });
+    BgzfStream chain;
+    std::vector<size_t> ends(nchunks);
+    for (size_t i = 0; i < nchunks && ok; i++) {
+        const size_t s = i % S, off = i * kSlot, len = std::min(kSlot, total - off);
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return stop || filled[s] == (long long)i; });
+            if (stop) {
+                ok = false;
+                break;
+            }
+        }
+        ok = vcfxg_bgzf_stage(g, ring_[s], len, off, total) == VCFXG_OK;
+        chain.feed((const char *)ring_[s], len);
+        ok = ok && !chain.bad;
+        ends[i] = off + len;
+        if (ok && i >= inflight) {
+            const size_t j = i - inflight;
+            ok = vcfxg_ingest_wait(g, ends[j]) == VCFXG_OK;
+            std::lock_guard<std::mutex> lk(mu);
+            freed[j % S] = (long long)j;
+            cv.notify_all();
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!ok) stop = true;
+        cv.notify_all();
+    }
+    for (auto &t : readers) t.join();
+    // every DMA from the ring finished before the slots are reused, on the failure path too
+    if (vcfxg_ingest_wait(g, ok ? total : ~(size_t)0) != VCFXG_OK) ok = false;
+    phase("bgzf streamed to the device");
+    ok = ok && !rerr && chain.ok(total) && chain.out >= hn;
+    uint64_t bad = ~0ull;
+    static_assert(sizeof(BgzfSpan) == sizeof(vcfxg_bgzf_member), "member layout");
+    if (!ok || vcfxg_ingest_bgzf(g, nullptr, total, reinterpret_cast<const vcfxg_bgzf_member *>(chain.members.data()),
+                                 chain.members.size(), head, hn, &bad) != VCFXG_OK) {
+        // (a read error, not a BGZF chain, or a member the device refused: the mapped path decides,
+        // the host inflate reporting damage as the reference does)
+        munmap(hm, kHeadMax);
+        phase("bgzf stream not taken");
+        return false;
+    }
+    phase("bgzf inflated on the device");
+    p = head;
+    host_n = hn;
+    n = (size_t)chain.out;
+    source_n = total;
+    map_base = hm;
+    map_len = kHeadMax;
+    mapped = false;
+    gz = true;
+    tail = nullptr;
+    stream_ctx = g;
+    streamed = n;
+    return true;
+}
+
 bool Input::open_file_device(const char *path) {
     // where the mapped path stays: views (a shard rank, VCFX_INPUT_VIEW), VCFX_FILE_STREAM=0
     const char *fs = getenv("VCFX_FILE_STREAM");
@@ -235,11 +417,22 @@ bool Input::open_file_device(const char *path) {
     const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return false;
     struct stat st;
-    if (fstat(fd, &st) < 0 || !S_ISREG(st.st_mode) || (size_t)st.st_size < env_bytes("VCFX_FILE_STREAM_MIN", (size_t)256 << 20)) {
+    if (fstat(fd, &st) < 0 || !S_ISREG(st.st_mode)) {
         ::close(fd);
         return open_file(path);
     }
     const size_t total = (size_t)st.st_size;
+    if (total < env_bytes("VCFX_FILE_STREAM_MIN", (size_t)256 << 20)) {
+        // (BGZF input streams from VCFX_BGZF_STREAM_MIN compressed bytes, 16 MiB by default)
+        unsigned char mg[2] = {0, 0};
+        int e = 0;
+        const bool gzf = total >= env_bytes("VCFX_BGZF_STREAM_MIN", (size_t)16 << 20) && total >= 2 &&
+                         pread_full(fd, (char *)mg, 2, 0, &e) && mg[0] == 0x1f && mg[1] == 0x8b;
+        if (!gzf) {
+            ::close(fd);
+            return open_file(path);
+        }
+    }
     gpu_prefetch();  // (a fresh process: the HIP runtime starts while the head is read)
     // the head (until it holds the '#CHROM' line: the host's gate runs on it) into host memory
     const size_t kSlot = file_slot(), kHeadMax = std::min(total, (size_t)256 << 20);
@@ -264,6 +457,11 @@ bool Input::open_file_device(const char *path) {
             chrom = is_chrom_line(s0, (size_t)(nl - s0));
             scanned = (size_t)(nl - head) + 1;
         }
+    }
+    if (!chrom && hn >= 2 && is_gzip(head, hn) && stream_bgzf_device(fd, total, head, hn)) {
+        munmap(hm, kHeadMax);
+        ::close(fd);
+        return true;
     }
     vcfxg_ctx *g = chrom ? gpu_quiet() : nullptr;
     if (!g) {  // gzip, no '#CHROM' in the first 256 MiB, a read error, or no device: the mapping

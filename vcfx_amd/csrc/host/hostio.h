@@ -65,6 +65,9 @@ struct Input {
     // whole input afterwards.  Views, gzip input, smaller files and VCFX_FILE_STREAM=0 take
     // open_file.  Afterwards host_n < n and load_input completes the device input.
     bool open_file_device(const char *path);
+    // open_file_device's BGZF branch (bgzf_device tools): the compressed file through the pinned
+    // ring to the device, the members inflated there; first[0, fn): its first bytes as read
+    bool stream_bgzf_device(int fd, size_t total, const char *first, size_t fn);
     // VCFX_INPUT_VIEW="H:LO:HI" in the environment (set by the multi-GPU runner,
     // vcfx_amd/shard.py): the input is the file's header bytes [0, H) followed by its records
     // [LO, HI) -- one rank's shard, without a copy.  The device input is ingested from those

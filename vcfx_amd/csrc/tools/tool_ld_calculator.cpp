@@ -129,9 +129,10 @@ bool run_stream(const Input &in, bool mmap_mode, const LdOpts &o, const std::str
     vcfxg_ctx *g = gpu(err.fd);
     if (!g) return false;
     uint64_t nl = 0, M = 0;
+    (void)nl;
     if (!load_input(g, in, err.fd) ||
-        !gpu_ok(g, vcfxg_index(g, data_start, &nl), "index", err.fd) ||
-        !gpu_ok(g, vcfxg_ld_prepare(g, ns, 1, rchrom.data(), rchrom.size(), has_region ? 1 : 0, rs, re, 0, &M),
+        !gpu_ok(g, vcfxg_ld_prepare_region(g, data_start, ns, 1, rchrom.data(), rchrom.size(), has_region ? 1 : 0, rs,
+                                           re, 0, &M),
                 "ld_prepare", err.fd))
         return false;
     const uint64_t W = std::min<uint64_t>(o.window, M ? M : 1);

@@ -83,6 +83,7 @@ SIGNATURES = {
     "vcfxg_haplotype_phaser": (_I, [_VP, _S, _I, ctypes.c_double, ctypes.c_uint32, ctypes.POINTER(Summary)]),
     "vcfxg_phaser_variants": (_I, [_VP, _VP, _VP, _VP]),
     "vcfxg_ld_prepare": (_I, [_VP, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
+    "vcfxg_ld_prepare_region": (_I, [_VP, _S, _I, _I, _P, _S, _I, _I, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_prefixes": (_I, [_VP, _VP, _S, _VP]),
     "vcfxg_ld_matrix": (_I, [_VP, _I, _I, ctypes.POINTER(_U64)]),
     "vcfxg_ld_stream_chunk": (_I, [_VP, _U64, _U64, _U64, ctypes.c_double, _I, ctypes.POINTER(_U64),
@@ -381,6 +382,14 @@ class Engine:
                                           re_, 0, ctypes.byref(n)), "ld_prepare")
         return n.value
 
+    def ld_prepare_region(self, data_start, n_samples, id_dot_to_pos=True, region=None):
+        """vcfxg_index + vcfxg_ld_prepare in one call (the LD walk for long records)."""
+        n = ctypes.c_uint64()
+        rc, rs, re_ = (region[0].encode(), region[1], region[2]) if region else (b"", 0, 0)
+        self._chk(self.L.vcfxg_ld_prepare_region(self.h, data_start, n_samples, int(id_dot_to_pos), rc, len(rc),
+                                                 int(bool(region)), rs, re_, 0, ctypes.byref(n)), "ld_prepare_region")
+        return n.value
+
     def ld_stream_chunk(self, j0, j1, window, threshold, max_dist=0):
         npairs = ctypes.c_uint64()
         tb = ctypes.c_uint64()
@@ -392,6 +401,17 @@ class Engine:
         n = ctypes.c_uint64()
         self._chk(self.L.vcfxg_count_byte(self.h, from_, byte, ctypes.byref(n)), "count_byte")
         return n.value
+
+    def ld_prefixes(self, m):
+        """The m variants' "CHROM\tPOS\tID" prefixes of the last LD prepare, as a list of bytes."""
+        import numpy as np
+        offs = np.zeros(m + 1, np.uint64)
+        self._chk(self.L.vcfxg_ld_prefixes(self.h, None, 0, offs.ctypes.data) if m == 0 else
+                  self.L.vcfxg_ld_prefixes(self.h, None, 1 << 62, offs.ctypes.data), "ld_prefixes")
+        text = ctypes.create_string_buffer(int(offs[m]) + 1)
+        self._chk(self.L.vcfxg_ld_prefixes(self.h, text, int(offs[m]) + 1, None), "ld_prefixes")
+        raw = text.raw
+        return [raw[int(offs[k]):int(offs[k + 1])] for k in range(m)]
 
     def ld_pairs(self, first, count):
         """(i, j, r2) numpy arrays of pairs [first, first + count) of the last ld_stream_chunk."""
