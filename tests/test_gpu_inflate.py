@@ -403,7 +403,7 @@ def test_af_streams_bgzf_through_the_ring(slot):
         with open(gz, "wb") as f:
             f.write(gzip.compress(buf, 6))
         want = oracle.run(["VCFX_allele_freq_calc", "-i", plain], b"")
-        env = dict(os.environ, VCFX_BGZF_STREAM_MIN="0", VCFXG_SCHEDULE_LOG=log)
+        env = dict(os.environ, VCFX_BGZF_STREAM_MIN="1", VCFXG_SCHEDULE_LOG=log)  # (0 reads as unset)
         if slot != "default":
             env["VCFX_FILE_SLOT"] = slot
 

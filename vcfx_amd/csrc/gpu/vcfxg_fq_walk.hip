@@ -222,7 +222,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
             const uint32_t be = slot_byte(nw, (int)(E - An)), be1 = slot_byte(nw, (int)(E - 1 - An));
             const bool endok = (E < hi ? be == '\n' : true) && ((strip_cr && be1 == '\r') == (cr != 0));
             // after an early exit the bytes past the sweep hold no '\n' only once scanned
-            const bool good = ok && endok && (swept >= ae || scan_nl(buf, swept, E) == E);
+            const bool good = ok && endok && (swept >= ae || nl_free(buf, swept, E));
             if (!good) {
                 const int64_t Et = scan_nl(buf, wend, hi);
                 if (Et != E || !endok) {  // the line again with its true bounds

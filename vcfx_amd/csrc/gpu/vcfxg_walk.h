@@ -49,6 +49,39 @@ __device__ __forceinline__ int64_t scan_nl(const char *__restrict__ buf, int64_t
     return hi;
 }
 
+// true iff [a, b) holds no '\n' (a 16-aligned, a < b, wave-uniform): the rest of a record whose
+// sweep stopped early (a match), checked before a predicted end is accepted.  A step of kU KiB
+// through a buffer resource, tested with the exact zero-byte test ANDed over the lane's dwords
+// (one ballot a step); only the last step, whose blocks may hold bytes at or past b, takes the
+// exact per-byte masks
+template <int kU = 4>
+__device__ __forceinline__ bool nl_free(const char *__restrict__ buf, int64_t a, int64_t b) {
+    const int lo16 = kBlockBytes * lane();
+    constexpr uint32_t K = 0x7F7F7F7Fu;
+    for (int64_t w = a; w < b; w += (int64_t)kU * kWaveStep) {
+        const int hr = (int)std::min<int64_t>(b - w, (int64_t)kU * kWaveStep);
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(buf + w, (uint32_t)((hr + 15) & ~15));
+        uint4 v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) v[u] = bload16(rs, u * kWaveStep + lo16);
+        if (hr == kU * kWaveStep) {  // every byte of the step is below b
+            uint32_t t = ~0u;
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const uint32_t x0 = v[u].x ^ kRepNl, x1 = v[u].y ^ kRepNl, x2 = v[u].z ^ kRepNl, x3 = v[u].w ^ kRepNl;
+                t &= (((x0 & K) + K) | x0) & (((x1 & K) + K) | x1) & (((x2 & K) + K) | x2) & (((x3 & K) + K) | x3);
+            }
+            if (__ballot((~t & 0x80808080u) != 0u)) return false;
+        } else {
+            uint32_t m = 0;
+#pragma unroll
+            for (int u = 0; u < kU; u++) m |= eq_mask16(v[u], kRepNl) & range16(u * kWaveStep + lo16, 0, hr);
+            if (__ballot(m != 0u)) return false;
+        }
+    }
+    return true;
+}
+
 // last '\n' in [lo, p), else lo - 1 (wave-uniform; kU KiB per step, backwards from p: lane 0
 // holds the highest block of a step, so the first lane with a '\n' holds the last one)
 template <int kU = 4>
