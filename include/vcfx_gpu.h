@@ -119,6 +119,13 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *ctx, const void *comp, size_t comp_n, const vcf
  * Between vcfxg_ingest_begin and vcfxg_ingest_bgzf, which then takes comp = NULL and
  * comp_n = comp_total. */
 int vcfxg_bgzf_stage(vcfxg_ctx *ctx, const void *host, size_t n, size_t offset, size_t comp_total);
+/* While staging: launch the inflate of the stream's next `count` members (in chain order from the
+ * first; every byte of them already staged), overlapping the copies still to come.  VCFXG_E_CAP:
+ * their output does not fit the input buffer as allocated (vcfxg_ingest_begin's size hint) --
+ * nothing launched; vcfxg_ingest_bgzf inflates them after growing it.  vcfxg_ingest_bgzf(comp =
+ * NULL) then takes the whole member list, launches the members not launched yet and checks every
+ * member's CRC-32. */
+int vcfxg_bgzf_inflate(vcfxg_ctx *ctx, const vcfxg_bgzf_member *members, size_t count);
 /* page-locked host memory (H2D at the full PCIe rate, asynchronous), for staging rings */
 int vcfxg_host_alloc(vcfxg_ctx *ctx, size_t n, void **out);
 void vcfxg_host_free(vcfxg_ctx *ctx, void *p);

@@ -71,6 +71,8 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *, const void *, size_t, const vcfxg_bgzf_member
                       uint64_t *) {
     return VCFXG_E_STATE;
 }
+int vcfxg_bgzf_stage(vcfxg_ctx *, const void *, size_t, size_t, size_t) { return VCFXG_E_STATE; }
+int vcfxg_bgzf_inflate(vcfxg_ctx *, const vcfxg_bgzf_member *, size_t) { return VCFXG_E_STATE; }
 
 int vcfxg_load_host(vcfxg_ctx *c, const char *host, size_t n) {
     vcfxg_ingest_begin(c, n);

@@ -382,10 +382,11 @@ def test_tools_on_device_bgzf(argv):
 
 # ---- the streamed form (VCFX_allele_freq_calc -i F.gz): the compressed file through the pinned file
 # ring, the member chain parsed from the ring's slots, every member inflated on the device -------------
-@pytest.mark.parametrize("slot", ["4096", "65536", "default"])
-def test_af_streams_bgzf_through_the_ring(slot):
+@pytest.mark.parametrize("slot,batch", [("4096", "1"), ("65536", "1"), ("65536", "0"), ("default", "1024")])
+def test_af_streams_bgzf_through_the_ring(slot, batch):
     """Slots far smaller than a member (a member's header and trailer in different slots), about one
-    member, and the default 16 MiB: the same rows as the oracle on the plain text, with the schedule
+    member, and the default 16 MiB; inflate batches launched per slot, or none until the end: the
+    same rows as the oracle on the plain text, with the schedule
     log showing the staged inflate ran; a plain (single-member) gzip file, a truncated BGZF file and
     one with a zeroed tail are not a BGZF chain to the stream and take the mapped path (its host
     inflate output, or the reference's "truncated or corrupt" failure)."""
@@ -404,6 +405,12 @@ def test_af_streams_bgzf_through_the_ring(slot):
             f.write(gzip.compress(buf, 6))
         want = oracle.run(["VCFX_allele_freq_calc", "-i", plain], b"")
         env = dict(os.environ, VCFX_BGZF_STREAM_MIN="1", VCFXG_SCHEDULE_LOG=log)  # (0 reads as unset)
+        # the members inflate in batches launched while later slots are still copied (batch 1: one
+        # launch per slot that completes a member; "0": all at the end)
+        if batch == "0":
+            env["VCFX_BGZF_BATCH"] = "0"
+        else:
+            env["VCFX_BGZF_BATCH_MIN"] = batch
         if slot != "default":
             env["VCFX_FILE_SLOT"] = slot
 

@@ -63,8 +63,18 @@ struct vcfxg_ctx {
     // summary; ld_gc_ready: ld_Gc holds the compact int8 rows (the walk gathers them only when
     // some variant misses a call)
     DevBuf ld_wcnt, ld_wval, ld_vbase, ld_small, ld_pend;
-    // vcfxg_bgzf_stage: the compressed stream's size and the bytes staged so far (into bgz_in)
+    // vcfxg_bgzf_stage: the compressed stream's size and the bytes staged so far (into bgz_in, on
+    // copy_stream); vcfxg_bgzf_inflate: members already launched and their output bytes
     size_t bgz_total = 0, bgz_staged = 0;
+    uint64_t bgz_launched = 0, bgz_out = 0;
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t bgz_copy_ev = nullptr;  // the latest staged copy
+    // the inflate batches run round robin on their own streams (a batch is a few waves per CU:
+    // one stream would serialise each batch's tail), joined before the CRC pass
+    static constexpr int kBgzStreams = 3;
+    hipStream_t bgz_stream[kBgzStreams] = {};
+    hipEvent_t bgz_ev[kBgzStreams] = {};
+    int bgz_next = 0;
     bool ld_gc_ready = false;
     bool ld_vq = false;  // ld_Gv / ld_Gq (valid-mask and squared-dosage FP4 planes) are current
     int n_cu = 0;
@@ -345,6 +355,12 @@ void vcfxg_close(vcfxg_ctx *c) {
     }
     for (auto &r : c->ev_open) (void)hipEventDestroy(r.a);
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++) {
+        if (c->bgz_stream[k]) (void)hipStreamDestroy(c->bgz_stream[k]);
+        if (c->bgz_ev[k]) (void)hipEventDestroy(c->bgz_ev[k]);
+    }
+    if (c->bgz_copy_ev) (void)hipEventDestroy(c->bgz_copy_ev);
     delete c;
 }
 
@@ -473,6 +489,12 @@ int vcfxg_ingest_begin(vcfxg_ctx *c, size_t size_hint) {
     if (c) c->dense_pending = false;  // a new index / regions replace the pending ones
     if (!c) return VCFXG_E_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    // (a staged BGZF stream abandoned before vcfxg_ingest_bgzf may still have copies and inflate
+    // batches in flight on their own streams: they finish before the input is written again)
+    if (c->copy_stream) HIPCHK(c, hipStreamSynchronize(c->copy_stream));
+    for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++)
+        if (c->bgz_stream[k]) HIPCHK(c, hipStreamSynchronize(c->bgz_stream[k]));
+    c->bgz_total = c->bgz_staged = 0;
     int r = ensure(c, c->input, size_hint + kPad);
     if (r) return r;
     c->loaded = false;
@@ -542,26 +564,111 @@ static int ingest_mark(vcfxg_ctx *c, size_t upto) {
     return VCFXG_OK;
 }
 
+// (a member holds >= 20 compressed bytes: the member tables of a staged stream are sized once)
+static uint64_t bgz_max_members(size_t comp_total) { return comp_total / 20 + 2; }
+
 int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, size_t comp_total) {
     if (!c || (!host && n) || offset > comp_total || n > comp_total - offset) return VCFXG_E_ARG;
     if (!c->ingesting) return VCFXG_E_STATE;
     HIPCHK(c, hipSetDevice(c->device));
     if (offset == 0) {
+        const uint64_t mm = bgz_max_members(comp_total);
         int r = ensure(c, c->bgz_in, comp_total + kCompPad);
+        if (!r) r = ensure(c, c->bgz_mem, sizeof(vcfxg_bgzf_member) * mm);
+        if (!r) r = ensure(c, c->bgz_off, 8 * mm);
+        if (!r) r = ensure(c, c->bgz_stat, 4 * mm);
+        if (!r) r = ensure(c, c->bgz_small, 64);
         if (r) return r;
+        if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+        if (!c->bgz_copy_ev) HIPCHK(c, hipEventCreateWithFlags(&c->bgz_copy_ev, hipEventDisableTiming));
+        for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++) {
+            if (!c->bgz_stream[k]) HIPCHK(c, hipStreamCreateWithFlags(&c->bgz_stream[k], hipStreamNonBlocking));
+            if (!c->bgz_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&c->bgz_ev[k], hipEventDisableTiming));
+        }
+        c->bgz_next = 0;
+        // (the stream's earlier work -- buffers just reallocated, the last call's kernels -- first)
+        HIPCHK(c, hipEventRecord(c->bgz_copy_ev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->bgz_copy_ev, 0));
+        HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
         c->bgz_total = comp_total;
         c->bgz_staged = 0;
+        c->bgz_launched = 0;
+        c->bgz_out = 0;
     }
     if (comp_total != c->bgz_total || offset != c->bgz_staged) return VCFXG_E_ARG;  // (in order)
     if (!n) return VCFXG_OK;
-    HIPCHK(c, hipMemcpyAsync(P<uint8_t>(c->bgz_in) + offset, host, n, hipMemcpyHostToDevice, c->stream));
+    // the copies on their own stream, so they overlap the inflate batches (vcfxg_bgzf_inflate)
+    HIPCHK(c, hipMemcpyAsync(P<uint8_t>(c->bgz_in) + offset, host, n, hipMemcpyHostToDevice, c->copy_stream));
     c->bgz_staged = offset + n;
-    return ingest_mark(c, offset + n);
+    if (c->bgz_staged == comp_total)
+        HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_in) + comp_total, 0, kCompPad, c->copy_stream));
+    HIPCHK(c, hipEventRecord(c->bgz_copy_ev, c->copy_stream));
+    // (the completion marker for vcfxg_ingest_wait: recorded on the copy stream)
+    hipEvent_t e = nullptr;
+    if (!c->ingest_ev_free.empty()) {
+        e = c->ingest_ev_free.back();
+        c->ingest_ev_free.pop_back();
+    } else {
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    HIPCHK(c, hipEventRecord(e, c->copy_stream));
+    c->ingest_ev.push_back({offset + n, e});
+    return VCFXG_OK;
+}
+
+// launch the inflate of members [first, first + count) of the staged stream: their table entries
+// and output offsets (from the running output count) to the device, k_inflate after the copies
+// staged so far
+static int bgz_launch(vcfxg_ctx *c, const vcfxg_bgzf_member *mem, uint64_t first, uint64_t count,
+                      hipStream_t st) {
+    if (!count) return VCFXG_OK;
+    std::vector<uint64_t> off(count);
+    uint64_t o = c->bgz_out;
+    for (uint64_t i = 0; i < count; i++) {
+        off[i] = o;
+        o += mem[i].out_len;
+    }
+    HIPCHK(c, hipMemcpyAsync(P<vcfxg_bgzf_member>(c->bgz_mem) + first, mem, sizeof(vcfxg_bgzf_member) * count,
+                             hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipMemcpyAsync(P<uint64_t>(c->bgz_off) + first, off.data(), 8 * count, hipMemcpyHostToDevice, st));
+    HIPCHK(c, hipStreamWaitEvent(st, c->bgz_copy_ev, 0));
+    static vcfxg::Crc1k z1k_unused{};
+    HIPCHK(c, vcfxg::launch_inflate(0, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem) + first,
+                                    P<uint64_t>(c->bgz_off) + first, count, P<uint8_t>(c->input) + c->n,
+                                    P<uint32_t>(c->bgz_stat) + first, P<unsigned long long>(c->bgz_small), z1k_unused,
+                                    st, first));
+    c->bgz_launched = first + count;
+    c->bgz_out = o;
+    return VCFXG_OK;
+}
+
+int vcfxg_bgzf_inflate(vcfxg_ctx *c, const vcfxg_bgzf_member *mem, size_t count) {
+    if (!c || (!mem && count)) return VCFXG_E_ARG;
+    if (!c->ingesting || !c->bgz_total) return VCFXG_E_STATE;
+    HIPCHK(c, hipSetDevice(c->device));
+    uint64_t out = 0;
+    for (size_t i = 0; i < count; i++) {
+        if (mem[i].src_off > c->bgz_staged || mem[i].src_len > c->bgz_staged - mem[i].src_off || mem[i].src_len < 20 ||
+            mem[i].out_len > 65536)
+            return VCFXG_E_ARG;  // (not staged yet, or out of range)
+        out += mem[i].out_len;
+    }
+    if (c->bgz_launched + count > bgz_max_members(c->bgz_total)) return VCFXG_E_ARG;
+    // the output must fit the input buffer as it is (growing it here would move the bytes the
+    // launched batches are writing): the rest waits for vcfxg_ingest_bgzf, which grows it
+    if (c->n + c->bgz_out + out + kPad > c->input.cap) return VCFXG_E_CAP;
+    const int k = c->bgz_next;
+    c->bgz_next = (k + 1) % vcfxg_ctx::kBgzStreams;
+    int r = bgz_launch(c, mem, c->bgz_launched, count, c->bgz_stream[k]);
+    if (r) return r;
+    HIPCHK(c, hipEventRecord(c->bgz_ev[k], c->bgz_stream[k]));
+    return VCFXG_OK;
 }
 
 int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg_bgzf_member *mem, size_t nm,
                       const char *head, size_t head_n, uint64_t *bad_member) {
-    // comp = NULL: the compressed bytes were staged by vcfxg_bgzf_stage (all comp_n of them)
+    // comp = NULL: the compressed bytes were staged by vcfxg_bgzf_stage (all comp_n of them), and
+    // members [0, bgz_launched) were launched by vcfxg_bgzf_inflate (mem[] must begin with them)
     const bool staged = !comp;
     if (!c || (staged && comp_n && (c->bgz_total != comp_n || c->bgz_staged != comp_n)) || (!mem && nm) ||
         (!head && head_n))
@@ -569,6 +676,8 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
     if (!c->ingesting) return VCFXG_E_STATE;
     if (bad_member) *bad_member = ~0ull;
     HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t done = staged ? c->bgz_launched : 0;  // members launched already
+    if (done > nm || (staged && nm > bgz_max_members(comp_n))) return VCFXG_E_ARG;
     std::vector<uint64_t> off(nm + 1);
     uint64_t tot = 0;
     for (size_t i = 0; i < nm; i++) {
@@ -582,50 +691,71 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         tot += mem[i].out_len;
     }
     off[nm] = tot;
-    if (c->n + tot + kPad > c->input.cap) {  // grow as vcfxg_ingest does
+    if (staged && done && off[done] != c->bgz_out) return VCFXG_E_ARG;  // (not the launched members)
+    if (c->n + tot + kPad > c->input.cap) {  // grow as vcfxg_ingest does (keeping launched output)
+        const size_t keep = c->n + (size_t)(staged ? c->bgz_out : 0);
         size_t ncap = std::max(c->input.cap * 2, c->n + tot + kPad);
         void *np = nullptr;
         HIPCHK(c, hipMalloc(&np, ncap));
-        if (c->n) HIPCHK(c, hipMemcpyAsync(np, c->input.p, c->n, hipMemcpyDeviceToDevice, c->stream));
+        if (keep) HIPCHK(c, hipMemcpyAsync(np, c->input.p, keep, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
         HIPCHK(c, hipFree(c->input.p));
         c->input.p = np;
         c->input.cap = ncap;
     }
-    int r = staged ? VCFXG_OK : ensure(c, c->bgz_in, comp_n + kCompPad);
-    if (!r) r = ensure(c, c->bgz_mem, sizeof(vcfxg_bgzf_member) * (nm + 1));
-    if (!r) r = ensure(c, c->bgz_off, 8 * (nm + 1));
-    if (!r) r = ensure(c, c->bgz_stat, 4 * (nm + 1));
-    if (!r) r = ensure(c, c->bgz_small, 64);
-    if (r) return r;
+    int r = VCFXG_OK;
+    if (!staged) {
+        r = ensure(c, c->bgz_in, comp_n + kCompPad);
+        if (!r) r = ensure(c, c->bgz_mem, sizeof(vcfxg_bgzf_member) * (nm + 1));
+        if (!r) r = ensure(c, c->bgz_off, 8 * (nm + 1));
+        if (!r) r = ensure(c, c->bgz_stat, 4 * (nm + 1));
+        if (!r) r = ensure(c, c->bgz_small, 64);
+        if (r) return r;
+    }
     static vcfxg::Crc1k z1k = [] {
         vcfxg::Crc1k z;
         vcfxg::crc32_zero1k_basis(&z);
         return z;
     }();
-    prof_begin(c, "bgzf_h2d");
-    if (comp_n && !staged) HIPCHK(c, hipMemcpyAsync(c->bgz_in.p, comp, comp_n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_in) + comp_n, 0, kCompPad, c->stream));
-    if (nm) {
-        HIPCHK(c, hipMemcpyAsync(c->bgz_mem.p, mem, sizeof(vcfxg_bgzf_member) * nm, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->bgz_off.p, off.data(), 8 * nm, hipMemcpyHostToDevice, c->stream));
-    }
-    HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
-    prof_end(c, "bgzf_h2d");
-    for (int which = 0; which < 2; which++) {  // k_inflate, then k_crc32
-        const char *nm_k = which ? "bgzf_crc32" : "bgzf_inflate";
-        prof_begin(c, nm_k);
-        HIPCHK(c, vcfxg::launch_inflate(which, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem),
+    if (staged) {
+        // every staged copy and every launched batch before the kernels below; the members not
+        // launched yet
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->bgz_copy_ev, 0));
+        if (done)
+            for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->bgz_ev[k], 0));
+        prof_begin(c, "bgzf_inflate");
+        r = bgz_launch(c, mem + done, done, nm - done, c->stream);
+        prof_end(c, "bgzf_inflate");
+        if (r) return r;
+    } else {
+        prof_begin(c, "bgzf_h2d");
+        if (comp_n) HIPCHK(c, hipMemcpyAsync(c->bgz_in.p, comp, comp_n, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_in) + comp_n, 0, kCompPad, c->stream));
+        if (nm) {
+            HIPCHK(c, hipMemcpyAsync(c->bgz_mem.p, mem, sizeof(vcfxg_bgzf_member) * nm, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(c, hipMemcpyAsync(c->bgz_off.p, off.data(), 8 * nm, hipMemcpyHostToDevice, c->stream));
+        }
+        HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
+        prof_end(c, "bgzf_h2d");
+        prof_begin(c, "bgzf_inflate");
+        HIPCHK(c, vcfxg::launch_inflate(0, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem),
                                         P<uint64_t>(c->bgz_off), nm, P<uint8_t>(c->input) + c->n,
                                         P<uint32_t>(c->bgz_stat), P<unsigned long long>(c->bgz_small), z1k, c->stream));
-        prof_end(c, nm_k);
+        prof_end(c, "bgzf_inflate");
     }
+    prof_begin(c, "bgzf_crc32");
+    HIPCHK(c, vcfxg::launch_inflate(1, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem), P<uint64_t>(c->bgz_off),
+                                    nm, P<uint8_t>(c->input) + c->n, P<uint32_t>(c->bgz_stat),
+                                    P<unsigned long long>(c->bgz_small), z1k, c->stream));
+    prof_end(c, "bgzf_crc32");
     static thread_local uint64_t bad;
     static thread_local uint8_t lastb;
     HIPCHK(c, hipMemcpyAsync(&bad, c->bgz_small.p, 8, hipMemcpyDeviceToHost, c->stream));
     if (tot) HIPCHK(c, hipMemcpyAsync(&lastb, P<uint8_t>(c->input) + c->n + tot - 1, 1, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
+    c->bgz_total = c->bgz_staged = 0;
+    c->bgz_launched = c->bgz_out = 0;
     if (bad != ~0ull) {
         uint32_t why = 0;
         (void)hipMemcpy(&why, P<uint32_t>(c->bgz_stat) + bad, 4, hipMemcpyDeviceToHost);
@@ -638,7 +768,6 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
     }
     if (head_n && c->hints_pending) c->hints_pending = !load_hints(c, head, head_n);
     note_schedule(c, staged ? "bgzf_inflate_staged" : "bgzf_inflate");
-    c->bgz_total = c->bgz_staged = 0;
     c->n += tot;
     if (tot) c->last_byte = lastb;
     return VCFXG_OK;

@@ -27,6 +27,10 @@
 #define VCFXG_GF_BUF 1
 #endif
 
+#ifndef VCFXG_FQ_EXPT
+#define VCFXG_FQ_EXPT 0
+#endif
+
 namespace vcfxg {
 
 struct DwordView {
@@ -856,7 +860,8 @@ struct GqOp {
         } else pmask = 0;
         (void)sepc;
     }
-    __device__ bool done() { return found = found || __any(any); }
+    // (VCFXG_FQ_EXPT & 1, diagnostic builds: no early exit -- every record swept whole)
+    __device__ bool done() { return (VCFXG_FQ_EXPT & 1) ? false : (found = found || __any(any)); }
     __device__ void dword(const DwordView &v) {
         uint32_t x = v.d & pmask;
         any = any || (v.real && pmask && (x == p1 || x == p2));

@@ -245,7 +245,8 @@ __device__ __forceinline__ uint32_t slow_decode(InfLds &S, int k, uint32_t p, ui
 
 __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
                                                 const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
-                                                uint32_t *__restrict__ mstat, unsigned long long *__restrict__ first_bad) {
+                                                uint32_t *__restrict__ mstat, unsigned long long *__restrict__ first_bad,
+                                                uint64_t mbase) {
     __shared__ InfLds S;
     const int lane = threadIdx.x;
     const uint32_t m = blockIdx.x;
@@ -590,7 +591,7 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
     }
     if (lane == 0) {
         mstat[m] = why;
-        if (why) atomicMin(first_bad, (unsigned long long)m);
+        if (why) atomicMin(first_bad, (unsigned long long)(mbase + m));
     }
 }
 
@@ -603,7 +604,7 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
 __global__ void __launch_bounds__(64) k_crc32(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
                                               const uint64_t *__restrict__ out_off, const uint8_t *__restrict__ out,
                                               Crc1k z1k, uint32_t *__restrict__ mstat,
-                                              unsigned long long *__restrict__ first_bad) {
+                                              unsigned long long *__restrict__ first_bad, uint64_t mbase) {
     __shared__ uint32_t T[4][256];
     __shared__ uint32_t Z[4][256];
     const int lane = threadIdx.x;
@@ -684,7 +685,7 @@ __global__ void __launch_bounds__(64) k_crc32(const uint8_t *__restrict__ comp, 
                               ((uint32_t)comp[t + 3] << 24);
         if (~acc != want && mstat[m] == 0) {
             mstat[m] = 20;
-            atomicMin(first_bad, (unsigned long long)m);
+            atomicMin(first_bad, (unsigned long long)(mbase + m));
         }
     }
 }
@@ -707,15 +708,16 @@ void crc32_zero1k_basis(Crc1k *z) {
 
 hipError_t launch_inflate(int which, const uint8_t *comp, const BgzfMember *mem, const uint64_t *out_off,
                           uint64_t n_members, uint8_t *out, uint32_t *mstat, unsigned long long *first_bad,
-                          const Crc1k &z1k, hipStream_t s) {
+                          const Crc1k &z1k, hipStream_t s, uint64_t mbase) {
+    // (mem, out_off, mstat: the arrays' entries for members mbase ..; first_bad: a global index)
     for (uint64_t m0 = 0; m0 < n_members; m0 += (1u << 30)) {
         const uint64_t nm = n_members - m0 < (1u << 30) ? n_members - m0 : (1u << 30);
         if (which == 0)
             hipLaunchKernelGGL(k_inflate, dim3((unsigned)nm), dim3(64), 0, s, comp, mem + m0, out_off + m0, out,
-                               mstat + m0, first_bad);
+                               mstat + m0, first_bad, mbase + m0);
         else
             hipLaunchKernelGGL(k_crc32, dim3((unsigned)nm), dim3(64), 0, s, comp, mem + m0, out_off + m0, out, z1k,
-                               mstat + m0, first_bad);
+                               mstat + m0, first_bad, mbase + m0);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

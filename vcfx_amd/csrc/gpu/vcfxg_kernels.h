@@ -45,7 +45,7 @@ void crc32_zero1k_basis(Crc1k *z);
 // which: 0 = k_inflate, 1 = k_crc32
 hipError_t launch_inflate(int which, const uint8_t *comp, const BgzfMember *mem, const uint64_t *out_off,
                           uint64_t n_members, uint8_t *out, uint32_t *mstat, unsigned long long *first_bad,
-                          const Crc1k &z1k, hipStream_t s);
+                          const Crc1k &z1k, hipStream_t s, uint64_t mbase = 0);
 // occurrences of `byte` in buf[lo, hi) added to *out (k_count_byte)
 hipError_t launch_count_byte(const uint8_t *buf, uint64_t lo, uint64_t hi, uint8_t byte, unsigned long long *out,
                              hipStream_t s);

@@ -311,7 +311,9 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
             g_file_ring.busy = false;
         }
     } ring_release{!ring_.empty()};
-    if (ring_.empty() || vcfxg_ingest_begin(g, 0) != VCFXG_OK) {
+    // (the input buffer sized for ~24x the compressed bytes, a VCF's usual BGZF ratio, so the
+    // inflate batches launched during the stream have their room; more grows it at the end)
+    if (ring_.empty() || vcfxg_ingest_begin(g, 24 * total) != VCFXG_OK) {
         munmap(hm, kHeadMax);
         return false;
     }
@@ -352,6 +354,9 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
             }
         });
     BgzfStream chain;
+    size_t launched = 0;
+    bool batching = !(getenv("VCFX_BGZF_BATCH") && getenv("VCFX_BGZF_BATCH")[0] == '0');
+    const size_t batch_min = env_bytes("VCFX_BGZF_BATCH_MIN", 16384);  // (~64 MB compressed; tests: 1)
     std::vector<size_t> ends(nchunks);
     for (size_t i = 0; i < nchunks && ok; i++) {
         const size_t s = i % S, off = i * kSlot, len = std::min(kSlot, total - off);
@@ -366,6 +371,16 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
         ok = vcfxg_bgzf_stage(g, ring_[s], len, off, total) == VCFXG_OK;
         chain.feed((const char *)ring_[s], len);
         ok = ok && !chain.bad;
+        // the members complete so far inflate on the device while the next chunks are read and
+        // copied (batches of >= 16384 members, about 64 MB compressed, round robin on three streams:
+        // 35 ms against 41 ms unbatched and 36.5 ms at 1024 on the bench shard; the rest at the end)
+        if (ok && batching && chain.members.size() - launched >= batch_min) {
+            const int br = vcfxg_bgzf_inflate(g, reinterpret_cast<const vcfxg_bgzf_member *>(chain.members.data()) +
+                                                     launched,
+                                              chain.members.size() - launched);
+            if (br == VCFXG_OK) launched = chain.members.size();
+            else batching = false;  // (E_CAP: the output outgrew the hint; the rest at the end)
+        }
         ends[i] = off + len;
         if (ok && i >= inflight) {
             const size_t j = i - inflight;

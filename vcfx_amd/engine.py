@@ -52,6 +52,8 @@ SIGNATURES = {
     "vcfxg_ingest": (_I, [_VP, _VP, _S, _I]),
     "vcfxg_ingest_wait": (_I, [_VP, _S]),
     "vcfxg_ingest_bgzf": (_I, [_VP, _VP, _S, _VP, _S, _VP, _S, ctypes.POINTER(_U64)]),
+    "vcfxg_bgzf_stage": (_I, [_VP, _VP, _S, _S, _S]),
+    "vcfxg_bgzf_inflate": (_I, [_VP, _VP, _S]),
     "vcfxg_host_alloc": (_I, [_VP, _S, ctypes.POINTER(_VP)]),
     "vcfxg_host_free": (None, [_VP, _VP]),
     "vcfxg_input_device_ptr": (_VP, [_VP]),
