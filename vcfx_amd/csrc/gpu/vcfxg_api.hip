@@ -168,7 +168,7 @@ struct vcfxg_ctx {
     // variant's missing samples and the sample-major contribution plane
     bool ld_sp = false;
     uint64_t ld_mp = 0;
-    DevBuf ld_moff, ld_midx, ld_mvar, ld_gt16, ld_sprec;
+    DevBuf ld_moff, ld_midx, ld_mvar, ld_gt16, ld_sprec, ld_midx16;
     // device BGZF inflate (vcfxg_ingest_bgzf): compressed bytes, member table, output offsets,
     // per-member status, first bad member
     DevBuf bgz_in, bgz_mem, bgz_off, bgz_stat, bgz_small;
@@ -339,7 +339,7 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_wcnt, &c->ld_wval, &c->ld_vbase, &c->ld_small, &c->ld_pend, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16, &c->ld_sprec, &c->bgz_in, &c->bgz_mem, &c->bgz_off, &c->bgz_stat, &c->bgz_small})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16, &c->ld_sprec, &c->ld_midx16, &c->bgz_in, &c->bgz_mem, &c->bgz_off, &c->bgz_stat, &c->bgz_small})
         if (b->p) (void)hipFree(b->p);
     if (c->af_small.p) (void)hipFree(c->af_small.p);
     if (c->wk_stage.p) (void)hipFree(c->wk_stage.p);
@@ -2445,6 +2445,7 @@ static int ld_prepare_finish(vcfxg_ctx *c, uint64_t M, int n_samples, int kpad, 
         const uint64_t mp = (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock * vcfxg::kLdFastBlock;
         r = ensure(c, c->ld_midx, 2 * entries + 16);
         if (!r) r = ensure(c, c->ld_mvar, 4 * entries + 16);
+        if (!r) r = ensure(c, c->ld_midx16, 32 * (M + 1));
         if (!r) r = ensure(c, c->ld_sprec, sizeof(vcfxg::LdSpRec) * (M + 1));
         if (!r) r = ensure(c, c->ld_gt16, 2 * (size_t)n_samples * mp + 64);
         if (r == VCFXG_E_NOMEM) r = sparse_to_mask();
@@ -2453,7 +2454,8 @@ static int ld_prepare_finish(vcfxg_ctx *c, uint64_t M, int n_samples, int kpad, 
     if (c->ld_sp) {
         const uint64_t mp = (M + vcfxg::kLdFastBlock - 1) / vcfxg::kLdFastBlock * vcfxg::kLdFastBlock;
         HIPCHK(c, vcfxg::launch_ld_miss_fill(P<int8_t>(c->ld_Gc), M, kpad, n_samples, P<uint64_t>(c->ld_moff),
-                                             P<uint16_t>(c->ld_midx), P<uint32_t>(c->ld_mvar), c->stream));
+                                             P<uint16_t>(c->ld_midx), P<uint32_t>(c->ld_mvar), P<uint16_t>(c->ld_midx16),
+                                             c->stream));
         HIPCHK(c, vcfxg::launch_ld_gt16(P<int8_t>(c->ld_Gc), M, kpad, n_samples, mp, P<uint16_t>(c->ld_gt16),
                                         c->stream));
         HIPCHK(c, vcfxg::launch_ld_sprec(P<vcfxg::LdVar>(c->ld_vars), M, n_samples, P<vcfxg::LdSpRec>(c->ld_sprec),
@@ -2888,6 +2890,7 @@ int vcfxg_ld_stream_chunk(vcfxg_ctx *c, uint64_t j0, uint64_t j1, uint64_t windo
         spa.moff = P<uint64_t>(c->ld_moff);
         spa.midx = P<uint16_t>(c->ld_midx);
         spa.mvar = P<uint32_t>(c->ld_mvar);
+        spa.midx16 = P<uint16_t>(c->ld_midx16);
         spa.rec = P<vcfxg::LdSpRec>(c->ld_sprec);
         const double big = 4.0 * (double)c->ld_ns * (double)c->ld_ns;  // (k_ld_mask's bound)
         spa.pe = (float)(big * std::ldexp(1.0, -23) + 1.0);

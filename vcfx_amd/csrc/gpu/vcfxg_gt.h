@@ -862,9 +862,9 @@ struct GqOp {
     }
     // (VCFXG_FQ_EXPT & 1, diagnostic builds: no early exit -- every record swept whole)
     __device__ bool done() { return (VCFXG_FQ_EXPT & 1) ? false : (found = found || __any(any)); }
-    __device__ void dword(const DwordView &v) {
-        uint32_t x = v.d & pmask;
-        any = any || (v.real && pmask && (x == p1 || x == p2));
+    __device__ void dword(const DwordView &v) {  // (bitwise on the flags: no lane branches)
+        const uint32_t x = v.d & pmask;
+        any |= v.real & (pmask != 0u) & ((x == p1) | (x == p2));
     }
     __device__ void sample(int64_t st) {
         if (any) return;

@@ -176,13 +176,14 @@ struct LdSparse {
     const uint64_t *moff = nullptr;
     const uint16_t *midx = nullptr;
     const uint32_t *mvar = nullptr;
+    const uint16_t *midx16 = nullptr;  // per variant its first 16 missing samples ([v][16], the rest unset)
     float pe = 0.f;            // the fp32 prefilter's error bound (as k_ld_mask)
     // per variant (m + 1 entries, the last zero): the packed (missing count, Sx, Sx2) and the own
     // variance, DMA'd into LDS with the first k-slices (k_ld_sprec)
     const LdSpRec *rec = nullptr;
 };
 hipError_t launch_ld_miss_fill(const int8_t *Gc, uint64_t m, int kpad, int ns, const uint64_t *moff, uint16_t *midx,
-                               uint32_t *mvar, hipStream_t s);
+                               uint32_t *mvar, uint16_t *midx16, hipStream_t s);
 hipError_t launch_ld_sprec(const LdVar *vars, uint64_t m, int ns, LdSpRec *rec, hipStream_t s);
 hipError_t launch_ld_gt16(const int8_t *Gc, uint64_t m, int kpad, int ns, uint64_t mp, uint16_t *gt16, hipStream_t s);
 hipError_t launch_ld_sparse(int pass, const uint8_t *Gp, const LdSparse &sp, const uint32_t *chrom_id,

@@ -239,6 +239,36 @@ __device__ __forceinline__ void ld_count_regs(const v16f (&acc)[2][4], const LdW
 #define VCFXG_LD_SP_COLU 4
 #endif
 constexpr int kSpRowU = VCFXG_LD_SP_ROWU, kSpColU = VCFXG_LD_SP_COLU;
+// VCFXG_LD_SP_TABLES=1: the R / C tables (every missing entry's plane row gathered into LDS by
+// atomic adds, for every half holding a candidate); 0 (default, r05): each candidate's two
+// corrections summed straight from the CSR and the plane (sp_corr)
+#ifndef VCFXG_LD_SP_TABLES
+#define VCFXG_LD_SP_TABLES 0
+#endif
+constexpr bool kSpTables = VCFXG_LD_SP_TABLES != 0;
+
+// sum over s in M_u (variant u's missing samples, CSR) of the plane's packed c(x_vs): (Sum x,
+// Sum x^2, the count of s where v misses too) in their u16 fields; mu = |M_u| (<= kLdSparseMax).
+// The sample indices of a step of 4 are loaded together, then their plane entries: two round trips
+// per step, the steps up to the active lanes' largest count
+__device__ __forceinline__ uint32_t sp_corr(const LdSparse &sp, uint64_t u, uint64_t v, int mu) {
+    // u's missing samples from its padded 16-entry list (two 16 B loads), then their plane entries
+    const uint4 *ml = reinterpret_cast<const uint4 *>(sp.midx16 + u * 16);
+    const uint4 m0 = ml[0];
+    const uint4 m1 = mu > 8 ? ml[1] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t w[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+    uint32_t acc = 0;
+#pragma unroll
+    for (int b = 0; b < 16; b += 4) {
+        if (!__ballot(b < mu)) break;  // (the active lanes' largest count reached)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t si = (w[(b + q) >> 1] >> (16 * ((b + q) & 1))) & 0xFFFFu;
+            acc += b + q < mu ? (uint32_t)sp.gt16[(uint64_t)si * sp.mp + v] : 0u;
+        }
+    }
+    return acc;
+}
 constexpr int kSpR = 0;                           // R: [256 rows][128 cols] u16
 constexpr int kSpCStride = 260;                   // C: [128 cols][256 rows + 4 pad] u16
 constexpr int kSpC = 256 * 128 * 2;
@@ -444,7 +474,7 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
 #pragma unroll
             for (int y = 0; y < 4; y++) anyc |= cbm[y][0] | cbm[y][1];
         // (no candidate in the half: no tables; its counts are written as 0 below)
-        const bool tables = __syncthreads_or(anyc != 0u) && !(VCFXG_LD_EXPT & (128 | 1024)) &&
+        const bool tables = __syncthreads_or(anyc != 0u) && kSpTables && !(VCFXG_LD_EXPT & (128 | 1024)) &&
                             !((VCFXG_LD_EXPT & 2048) && a.ns >= 0);
         if ((VCFXG_LD_EXPT & 256) && P == 1) {  // (diagnostic: halves, halves with tables, candidates)
             if (t == 0) {
@@ -555,8 +585,15 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                 const int il = (int)(d0 & 0xFF), jl = (int)((d0 >> 8) & 0x7F), sxy = (int)(d0 >> 16);
                 const int jt = kFB + 128 * hp + jl;
                 const LdSpRec ri = rec[il], rj = rec[jt];
-                const uint32_t rv = R16[il * 128 + jl];
-                const uint32_t cv = C16[jl * kSpCStride + il];
+                uint32_t rv, cv;
+                if constexpr (kSpTables) {
+                    rv = R16[il * 128 + jl];
+                    cv = C16[jl * kSpCStride + il];
+                } else {  // R[i][j] = over M_i of c(x_js), C[j][i] = over M_j of c(x_is)
+                    const uint64_t i = (uint64_t)(ibase + il), j = (uint64_t)(jb + jl);
+                    rv = sp_corr(sp, i, j, (int)(ri.pk & 0xFF));
+                    cv = sp_corr(sp, j, i, (int)(rj.pk & 0xFF));
+                }
                 const int n = a.ns - (int)(ri.pk & 0xFF) - (int)(rj.pk & 0xFF) + (int)(rv >> 11);
                 const int sx = (int)((ri.pk >> 8) & 0xFFFFFF) - (int)(cv & 31);
                 const int sxx = (int)(ri.pk >> 32) - (int)((cv >> 5) & 63);
@@ -1291,12 +1328,13 @@ hipError_t launch_ld_groups(const LdVar *vars, uint64_t m, int ns, int sparse, u
 // the per-lane counts)
 __global__ __launch_bounds__(256) void k_ld_miss_fill(const int8_t *__restrict__ Gc, uint64_t m, int kpad, int ns,
                                                       const uint64_t *__restrict__ moff, uint16_t *__restrict__ midx,
-                                                      uint32_t *__restrict__ mvar) {
+                                                      uint32_t *__restrict__ mvar, uint16_t *__restrict__ midx16) {
     const int l = threadIdx.x & 63;
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
     for (uint64_t v = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 64; v < m; v += nw) {
         const int8_t *row = Gc + v * (uint64_t)kpad;
-        uint64_t at = moff[v];
+        const uint64_t at0 = moff[v];
+        uint64_t at = at0;
         for (int s0 = 0; s0 < ns; s0 += 16 * 64) {
             const int b = s0 + 16 * l;
             uint32_t bits = 0;
@@ -1315,6 +1353,7 @@ __global__ __launch_bounds__(256) void k_ld_miss_fill(const int8_t *__restrict__
                 bits &= bits - 1u;
                 midx[o] = (uint16_t)(b + k);
                 mvar[o] = (uint32_t)v;
+                if (o - at0 < 16) midx16[v * 16 + (o - at0)] = (uint16_t)(b + k);  // (the first 16)
                 o++;
             }
             at += wave_bcast(incl, 63);
@@ -1323,11 +1362,11 @@ __global__ __launch_bounds__(256) void k_ld_miss_fill(const int8_t *__restrict__
 }
 
 hipError_t launch_ld_miss_fill(const int8_t *Gc, uint64_t m, int kpad, int ns, const uint64_t *moff, uint16_t *midx,
-                               uint32_t *mvar, hipStream_t s) {
+                               uint32_t *mvar, uint16_t *midx16, hipStream_t s) {
     if (!m) return hipSuccess;
     if (kpad % 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_ld_miss_fill, dim3((unsigned)std::min<uint64_t>((m + 3) / 4, 16384)), dim3(256), 0, s, Gc, m,
-                       kpad, ns, moff, midx, mvar);
+                       kpad, ns, moff, midx, mvar, midx16);
     return hipGetLastError();
 }
 
