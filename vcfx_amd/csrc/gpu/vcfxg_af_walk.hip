@@ -154,7 +154,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     constexpr uint32_t kStgCap = kStageLds ? 2048u : 16u;
     __shared__ __attribute__((aligned(16))) char stg[kStageLds ? kWalkWaves : 1][kStgCap];
     const int wv = threadIdx.x / kWave;
-    const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + wv);
+    const int64_t wk = uniform64((int64_t)walk_block() * kWalkWaves + wv);
     if (wk >= n_walkers) return;
     const int strip_cr = mode == 0 ? 1 : 0;
     const int64_t cs = lo + wk * chunk;

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
     __shared__ uint4 win[kWalkWaves][2][kWave];  // two window slots per wave (double buffer)
     const int wv = threadIdx.x / kWave;
     if (blockIdx.x == 0 && threadIdx.x == 0) wcount[n_walkers] = 0;  // the scan's last entry (no memset)
-    const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + wv);
+    const int64_t wk = uniform64((int64_t)walk_block() * kWalkWaves + wv);
     if (wk >= n_walkers) return;
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);

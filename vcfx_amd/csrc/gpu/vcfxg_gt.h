@@ -843,9 +843,17 @@ struct GqOp {
     int gi;
     GqQuery Q;
     uint32_t p1 = 0, p2 = 0, pmask = 0;  // fast-path dword pattern(s)
-    bool any = false;                    // this lane
+    // fast path: the least of (x ^ p1, x ^ p2) over this lane's dwords -- 0 iff one matched
+    // (VALU min / xor: as lane booleans the match tests had cost three scalar mask ops each)
+    uint32_t mn = ~0u;
+    bool any = false;                    // this lane (general path)
     bool found = false;                  // wave
     __device__ void begin(uint32_t sepc, uint32_t) {
+        begin_patterns();
+        if (!pmask) p1 = p2 = ~0u;  // (no fast-path match: x never has bit 31)
+        (void)sepc;
+    }
+    __device__ void begin_patterns() {
         // on the fixed-stride layout a GT is "a s b"; flexible: match <=> a, b digits with
         // sorted (a, b) == (qa, qb); strict: the 3 bytes equal the query
         if (Q.strict) {
@@ -858,13 +866,14 @@ struct GqOp {
             p2 = (uint32_t)('0' + Q.qb) | ((uint32_t)('0' + Q.qa) << 16);
             pmask = 0x00FF00FFu;
         } else pmask = 0;
-        (void)sepc;
     }
     // (VCFXG_FQ_EXPT & 1, diagnostic builds: no early exit -- every record swept whole)
-    __device__ bool done() { return (VCFXG_FQ_EXPT & 1) ? false : (found = found || __any(any)); }
-    __device__ void dword(const DwordView &v) {  // (bitwise on the flags: no lane branches)
-        const uint32_t x = v.d & pmask;
-        any |= v.real & (pmask != 0u) & ((x == p1) | (x == p2));
+    __device__ bool done() {
+        return (VCFXG_FQ_EXPT & 1) ? false : (found = found || __any(any || mn == 0u));
+    }
+    __device__ void dword(const DwordView &v) {
+        const uint32_t x = (v.d & pmask) | (v.real ? 0u : 0x01000000u);  // (padding never matches)
+        mn = std::min(mn, std::min(x ^ p1, x ^ p2));
     }
     __device__ void sample(int64_t st) {
         if (any) return;
@@ -884,7 +893,7 @@ struct GqOp {
         int64_t n = p - fs;
         if (n > 0 && gt_matches(buf, fs, n, Q)) any = true;
     }
-    __device__ void finish() { found = __any(any); }
+    __device__ void finish() { found = __any(any || mn == 0u); }
 };
 
 // ---------------------------------------------------------------------------------------

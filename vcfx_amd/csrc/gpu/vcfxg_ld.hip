@@ -466,7 +466,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(VC
     __shared__ uint4 win[kWalkWaves][2][kWave];  // two window slots per wave (double buffer)
     __shared__ __attribute__((aligned(16))) int8_t lrows[kWalkWaves][kLdLdsRow];
     const int wv = threadIdx.x / kWave;
-    const int64_t wk = uniform64((int64_t)blockIdx.x * kWalkWaves + wv);
+    const int64_t wk = uniform64((int64_t)walk_block() * kWalkWaves + wv);
     if (wk >= n_walkers) return;
     int8_t *lrow = lrows[wv];
     const auto lrow3 = (__attribute__((address_space(3))) int8_t *)lrow;

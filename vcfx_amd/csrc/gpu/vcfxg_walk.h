@@ -21,6 +21,21 @@ constexpr int kWalkWaves = kWalkThreads / kWave;
 #endif
 constexpr int kFirstScanU = VCFXG_FIRST_SCAN_U;
 
+// The walker block of this workgroup.  The dispatcher hands workgroup b to XCD b mod 8; with
+// VCFXG_WALK_XCD each XCD takes one contiguous eighth of the blocks instead, in order, so the
+// two walkers either side of a block boundary run at about the same time on one XCD and the
+// bytes both read at their starts (the straddling line's head, the backward scans) come from
+// one L2 rather than from HBM twice.  Bijective for any grid.
+#ifndef VCFXG_WALK_XCD
+#define VCFXG_WALK_XCD 1
+#endif
+__device__ __forceinline__ uint32_t walk_block() {
+    const uint32_t b = blockIdx.x;
+    if (!VCFXG_WALK_XCD) return b;
+    const uint32_t n = gridDim.x, q = n / 8, r = n % 8, x = b % 8, k = b / 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + k;
+}
+
 // first '\n' in [p, hi), else hi (wave-uniform; kU KiB per step, lane offsets 32-bit)
 template <int kU = 4>
 __device__ __forceinline__ int64_t scan_nl(const char *__restrict__ buf, int64_t p, int64_t hi) {
@@ -198,9 +213,54 @@ __device__ __forceinline__ int first_match(uint32_t mk) {
     const int k = __builtin_ctzll(any);
     return match_pos<kBytes>(k, lane_get(mk, k));
 }
+// the window bytes [lo, hi) among this lane's four (kBytes = 4 layout), 0x80 per byte
+__device__ __forceinline__ uint32_t range4(int lo, int hi) {
+    const int b = 4 * lane(), t = lo - b, u = hi - b;
+    const uint32_t mlo = t <= 0 ? 0x80808080u : t >= 4 ? 0u : (0x80808080u << (8 * t));
+    const uint32_t mhi = u >= 4 ? 0x80808080u : u <= 0 ? 0u : (0x80808080u >> (32 - 8 * u));
+    return mlo & mhi;
+}
 // the first (up to) 9 tabs of the per-lane masks below position lim: rt[0..n), returns n
+// (entries past n are unspecified).
+// kBytes = 4, VCFXG_TABS_LANE (default): lane-parallel -- each lane's tab index from the four
+// byte-slot ballots (v_mbcnt), its tabs' byte slots as 2-bit fields; tab r is then one ballot
+// ("r falls in my range"), one s_ff1 and one v_readlane.  The scalar form walked the matches
+// with a branch and an early break per tab, and the compiler copied the whole rt[] array of
+// SGPRs at every exit (~40 SALU per tab: with the sweep's mask logic, 856 SALU per record in
+// the pipeline walk, r05 SQ pass, against one scalar issue per CU per cycle).
+#ifndef VCFXG_TABS_LANE
+#define VCFXG_TABS_LANE 1
+#endif
+__device__ __forceinline__ uint32_t first_tabs_lane4(uint32_t tm, int lim, int (&rt)[9]) {
+    tm &= range4(0, lim);
+    uint32_t P = 0, t = tm;  // byte slot of this lane's j-th tab in bits [2j, 2j + 2)
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        P |= ((uint32_t)__builtin_ctz(t | 0x80000000u) >> 3) << (2 * j);
+        t &= t - 1u;
+    }
+    P |= 3u << 6;  // (a fourth tab can only be in slot 3)
+    const uint32_t cnt = (uint32_t)__builtin_popcount(tm);
+    uint32_t excl = 0, total = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint64_t bj = __ballot((tm & (0x80u << (8 * j))) != 0u);
+        excl = __builtin_amdgcn_mbcnt_hi((uint32_t)(bj >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bj, excl));
+        total += (uint32_t)__builtin_popcountll(bj);
+    }
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+        const uint32_t d = (uint32_t)r - excl;  // (wraps for lanes past tab r: d >= cnt)
+        const uint64_t own = __ballot(d < cnt);
+        const int k = (int)__builtin_ctzll(own | (1ull << 63));
+        const uint32_t slot = lane_get((P >> (2 * (d & 3u))) & 3u, k);
+        rt[r] = 4 * k + (int)slot;
+    }
+    return total < 9u ? total : 9u;
+}
 template <int kBytes>
 __device__ __forceinline__ uint32_t first_tabs(uint32_t tm, int lim, int (&rt)[9]) {
+    if constexpr (kBytes == 4 && VCFXG_TABS_LANE) return first_tabs_lane4(tm, lim, rt);
     uint64_t lanes = __ballot(tm != 0u);
     uint32_t m = 0, n = 0;
     int k = 0;
@@ -219,13 +279,6 @@ __device__ __forceinline__ uint32_t first_tabs(uint32_t tm, int lim, int (&rt)[9
         m &= m - 1u;
     }
     return n;
-}
-// the window bytes [lo, hi) among this lane's four (kBytes = 4 layout), 0x80 per byte
-__device__ __forceinline__ uint32_t range4(int lo, int hi) {
-    const int b = 4 * lane(), t = lo - b, u = hi - b;
-    const uint32_t mlo = t <= 0 ? 0x80808080u : t >= 4 ? 0u : (0x80808080u << (8 * t));
-    const uint32_t mhi = u >= 4 ? 0x80808080u : u <= 0 ? 0u : (0x80808080u >> (32 - 8 * u));
-    return mlo & mhi;
 }
 // window byte o (wave-uniform) out of the kBytes = 4 layout's registers
 __device__ __forceinline__ uint32_t dword_byte(uint32_t w, int o) {
