@@ -4,11 +4,10 @@
 Workloads (BASELINE.json configs; the default is the headline one):
   af        configs[1] / configs[3]: VCFX_allele_freq_calc -i on a device-resident
             427,409-record x 2,504-sample chr21-like shard per GPU.  A step =
-            vcfxg_allele_freq_region: the line index in one sweep (line_count keeps each 16 KiB
-            chunk's newline offsets; line_compact places them), per-record allele counts
-            (af_records = head pass + fixed-stride sample sweep + rare full-path lines) and
-            device formatted output rows (af_rows + af_format); for N > 1 ranks also all-reduce
-            the step's global counts over RCCL.
+            vcfxg_allele_freq_region: the walk (af_walk: one wave per chunk walks its lines --
+            head from an LDS window, fixed-stride sample sweep, the record's output row composed
+            in LDS) and the region tail (rare full-path lines, rows placed in file order); for
+            N > 1 ranks also all-reduce the step's global counts over RCCL.
   pipeline  configs[2] as SURVEY §8(d) defines it: VCFX_record_filter --filter
             "FILTER==PASS;AF>=0.01" | VCFX_genotype_query -g 0/1 fused on the device (one walk:
             the filter's INFO key lookup + the genotype query), on the annotated shard

@@ -246,6 +246,14 @@ constexpr int kSpRowU = VCFXG_LD_SP_ROWU, kSpColU = VCFXG_LD_SP_COLU;
 #define VCFXG_LD_SP_TABLES 0
 #endif
 constexpr bool kSpTables = VCFXG_LD_SP_TABLES != 0;
+// VCFXG_LD_SP_R2CACHE=1 (default, r05): the emit writes a passing pair with the r^2 its decision
+// computed, kept in the staging ring (dead in the epilogue when no R / C tables overlay it):
+// kSpR2Cap doubles per wave, by the pair's position in the wave's list sequence; a wave with
+// more candidates recomputes them.  0: the emit recomputes every pair
+#ifndef VCFXG_LD_SP_R2CACHE
+#define VCFXG_LD_SP_R2CACHE 1
+#endif
+constexpr bool kSpR2Cache = VCFXG_LD_SP_R2CACHE != 0 && !kSpTables;
 
 // sum over s in M_u (variant u's missing samples, CSR) of the plane's packed c(x_vs): (Sum x,
 // Sum x^2, the count of s where v misses too) in their u16 fields; mu = |M_u| (<= kLdSparseMax).
@@ -284,6 +292,7 @@ constexpr int kSpTerms = kSpInts + kSpRecBytes;
 // the exact pass's per-wave work list over the terms once the prefilter is done: 4 waves per half,
 // kSpList 8 B entries (then, for the emit, kSpList destinations after them)
 constexpr int kSpList = 128;
+constexpr int kSpR2Cap = kRing / (kWaves * 8);  // 2,048 cached r^2 per wave
 static_assert(4 * kSpList * 16 <= 8 * kFB * 4, "the work lists fit the prefilter terms");
 static_assert(kSpTerms + 8 * kFB * 4 + 16 <= kRing + kFB * 32 + 2 * kFvBytes, "prefilter terms fit the records' area");
 
@@ -617,36 +626,38 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
             // a ballot), so the list fills kWave entries per round however unevenly the lanes hold
             // pairs; put(y, b, slot) lists a pair, run(e) handles entry e on lane e % 64, get(y, b,
             // slot) replays the rounds on the owning lanes to read the outcome back
+            auto word_of = [&](const uint32_t (&W)[4], int y) {
+                const uint32_t c0 = (y & 1) ? W[1] : W[0], c1 = (y & 1) ? W[3] : W[2];
+                return (y & 2) ? c1 : c0;
+            };
+            auto adv_of = [&](const uint32_t (&W)[4], int &y, uint32_t &rm) {
+                while (rm == 0u && y < 3) rm = word_of(W, ++y);
+            };
+            // one list's rounds from the state (y, rm): fn(y, b, e) per listed pair; returns the count
+            auto rounds_of = [&](const uint32_t (&W)[4], int &y, uint32_t &rm, auto fn) {
+                int n = 0;
+#pragma unroll
+                for (int rd = 0; rd < kSpList / kWave; rd++) {
+                    const uint64_t bl = __builtin_amdgcn_ballot_w64(rm != 0u);
+                    if (bl == 0) break;  // (wave-uniform)
+                    if (rm != 0u) {
+                        const int e = n + (int)__builtin_amdgcn_mbcnt_hi(
+                                              (uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
+                        fn(y, __builtin_ctz(rm), e);
+                        rm &= rm - 1u;
+                        adv_of(W, y, rm);
+                    }
+                    n += __popcll(bl);
+                }
+                return n;
+            };
             auto spread = [&](const uint32_t (&W)[4], auto put, auto run, auto get) {
                 if (__builtin_amdgcn_ballot_w64((W[0] | W[1] | W[2] | W[3]) != 0u) == 0) return;  // (usual)
-                auto word = [&](int y) {
-                    const uint32_t c0 = (y & 1) ? W[1] : W[0], c1 = (y & 1) ? W[3] : W[2];
-                    return (y & 2) ? c1 : c0;
-                };
-                auto adv = [&](int &y, uint32_t &rm) {
-                    while (rm == 0u && y < 3) rm = word(++y);
-                };
-                auto rounds = [&](int &y, uint32_t &rm, auto fn) {
-                    int n = 0;
-#pragma unroll
-                    for (int rd = 0; rd < kSpList / kWave; rd++) {
-                        const uint64_t bl = __builtin_amdgcn_ballot_w64(rm != 0u);
-                        if (bl == 0) break;  // (wave-uniform)
-                        if (rm != 0u) {
-                            const int e = n + (int)__builtin_amdgcn_mbcnt_hi(
-                                                  (uint32_t)(bl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bl, 0u));
-                            fn(y, __builtin_ctz(rm), e);
-                            rm &= rm - 1u;
-                            adv(y, rm);
-                        }
-                        n += __popcll(bl);
-                    }
-                    return n;
-                };
+                auto rounds = [&](int &y, uint32_t &rm, auto fn) { return rounds_of(W, y, rm, fn); };
                 int y = 0;
                 uint32_t rm = W[0];
-                adv(y, rm);
-                for (;;) {
+                adv_of(W, y, rm);
+                for (int base = 0;;) {
                     int yr = y;
                     uint32_t rr = rm;
                     const int n = rounds(y, rm, put);
@@ -654,7 +665,8 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                    for (int e = l; e < n; e += kWave) run(e);
+                    for (int e = l; e < n; e += kWave) run(e, base + e);
+                    base += n;
                     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -664,10 +676,13 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 }
             };
-            // the exact decision on every candidate
+            // the exact decision on every candidate; each listed pair's r^2 kept in the list's second
+            // half (free until the emit), so when the wave's candidates fit one list -- the usual
+            // case -- the emit writes the passing pairs from it instead of recomputing them
+            double *const r2c = reinterpret_cast<double *>(lds + w * kSpR2Cap * 8);
             uint32_t passW[4];
+            uint32_t candW[4];
             {
-                uint32_t candW[4];
 #pragma unroll
                 for (int y = 0; y < 4; y++) {
                     candW[y] = (VCFXG_LD_EXPT & (128 | 512)) || ((VCFXG_LD_EXPT & 2048) && a.ns >= 0)
@@ -683,9 +698,10 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
                                                 sxy_of(x, y, k) << 16,
                                             0u);
                     },
-                    [&](int e) {
-                        double r2;
+                    [&](int e, int eg) {
+                        double r2 = 0.0;
                         lst[e].y = exact(lst[e].x, r2) ? 1u : 0u;
+                        if (kSpR2Cache && eg < kSpR2Cap) r2c[eg] = r2;
                     },
                     [&](int y, int b, int e) {
                         const uint32_t bit = lst[e].y ? 1u << b : 0u;
@@ -767,23 +783,51 @@ __device__ __forceinline__ void ld_sparse_epilogue(const v16f (&acc)[2][4], int8
             if (P == 2 || st.temp) {
                 // the passing pairs with a destination, their r^2 recomputed lane-parallel and written
                 uint32_t emitW[4];
+                uint32_t ncand = 0;
 #pragma unroll
-                for (int y = 0; y < 4; y++) emitW[y] = dst[y] ? passW[y] : 0u;
+                for (int y = 0; y < 4; y++) {
+                    emitW[y] = dst[y] ? passW[y] : 0u;
+                    ncand += (uint32_t)__builtin_popcount(candW[y]);
+                }
+                auto dest = [&](int y, int row) {
+                    LdPair *const d0 = (y & 1) ? dst[1] : dst[0], *const d1 = (y & 1) ? dst[3] : dst[2];
+                    const uint64_t f0 = (y & 1) ? fmv[1] : fmv[0], f1 = (y & 1) ? fmv[3] : fmv[2];
+                    return ((y & 2) ? d1 : d0) + __popcll(((y & 2) ? f1 : f0) & ((1ull << row) - 1ull));
+                };
                 uint64_t *dl = reinterpret_cast<uint64_t *>(lst) + kSpList;  // (the list's second half)
+                if (kSpR2Cache && wave_sum(ncand) <= (uint32_t)kSpR2Cap) {  // (wave-uniform)
+                    // every candidate's r^2 is cached: replay the decision pass's list sequence (the
+                    // same rounds from the same masks give every pair its position again); a pair
+                    // that passed and has a destination is written from its owning lane
+                    int y = 0;
+                    uint32_t rm = candW[0];
+                    adv_of(candW, y, rm);
+                    for (int base = 0;;) {
+                        const int n = rounds_of(candW, y, rm, [&](int yy, int b, int e) {
+                            if (!((word_of(emitW, yy) >> b) & 1u)) return;
+                            const int row = row_of(b >> 4, b & 15);
+                            LdPair pr;
+                            pr.i = (uint32_t)(ibase + wi * 64 + row);
+                            pr.j = (uint32_t)(jb + 32 * yy + r);
+                            pr.r2 = r2c[base + e];
+                            *dest(yy, row) = pr;
+                        });
+                        if (n == 0) break;  // (wave-uniform)
+                        base += n;
+                    }
+                } else
                 spread(
                     emitW,
                     [&](int y, int b, int e) {
                         const int x = b >> 4, k = b & 15;
                         const int row = row_of(x, k);
-                        LdPair *const d0 = (y & 1) ? dst[1] : dst[0], *const d1 = (y & 1) ? dst[3] : dst[2];
-                        const uint64_t f0 = (y & 1) ? fmv[1] : fmv[0], f1 = (y & 1) ? fmv[3] : fmv[2];
-                        LdPair *const d = ((y & 2) ? d1 : d0) + __popcll(((y & 2) ? f1 : f0) & ((1ull << row) - 1ull));
+                        LdPair *const d = dest(y, row);
                         lst[e] = make_uint2((uint32_t)(wi * 64 + row) | (uint32_t)(32 * y + r) << 8 |
                                                 sxy_of(x, y, k) << 16,
                                             0u);
                         dl[e] = (uint64_t)(uintptr_t)d;
                     },
-                    [&](int e) {
+                    [&](int e, int) {
                         const uint32_t d0 = lst[e].x;
                         double r2 = 0.0;
                         (void)exact(d0, r2);
