@@ -19,7 +19,7 @@ CXXFLAGS := -O2 -std=c++17 -fPIC -Wall -Wno-unused-result -Iinclude -I$(HOST_SRC
 TOOL_OBJS := $(sort $(B)/obj/hostio.o $(B)/obj/gz.o $(patsubst $(TOOL_SRC)/%.cpp,$(B)/obj/%.o,$(wildcard $(TOOL_SRC)/tool_*.cpp)))
 TOOL_BINS := $(foreach t,$(TOOLS),$(B)/src/$(t)/$(t))
 
-all: $(B)/bin/vcfx_bgzf $(B)/bin/vcfx_drain $(B)/bin/vcfx_pipe $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so \
+all: $(B)/bin/vcfx_bgzf $(B)/bin/vcfx_drain $(B)/bin/vcfx_pipe_ceiling $(B)/bin/vcfx_pipe $(B)/libvcfx_gpu.so $(B)/libvcfx_tools.so $(TOOL_BINS) $(B)/bin/vcfx_synth $(B)/libvcfx_synth.so \
      $(B)/libvcfx_core.so $(B)/libvcfx_core.a $(B)/libvcfx_record_filter.so $(B)/libvcfx_genotype_query.so
 
 $(B)/obj/%.o: $(HOST_SRC)/%.cpp $(wildcard $(HOST_SRC)/*.h) include/vcfx_gpu.h
@@ -82,6 +82,12 @@ $(B)/bin/vcfx_bgzf: vcfx_amd/csrc/synth/vcfx_bgzf.c
 $(B)/bin/vcfx_drain: tools/microbench/pipe_drain.c
 	@mkdir -p $(dir $@)
 	$(CC) -O2 -o $@ $<
+
+# the drop-in's stdin reader with the device stage stubbed (the e2e leg's pipe ceiling)
+PIPE_CEIL_SRC := tools/microbench/pipe_ceiling.cpp tests/shard_tsan_stub.cpp $(HOST_SRC)/hostio.cpp $(HOST_SRC)/gz.cpp
+$(B)/bin/vcfx_pipe_ceiling: $(PIPE_CEIL_SRC) $(wildcard $(HOST_SRC)/*.h)
+	@mkdir -p $(dir $@)
+	$(CXX) -O2 -std=c++17 -DVCFX_STUB_DISCARD -Iinclude -I$(HOST_SRC) -Ivcfx_amd/csrc/tools -o $@ $(PIPE_CEIL_SRC) -lz -lpthread
 
 $(B)/libvcfx_synth.so: vcfx_amd/csrc/synth/vcfx_synth.c
 	$(CC) -O2 -fPIC -shared -o $@ $< -lpthread

@@ -14,6 +14,9 @@
 //   - the rank clique is the host reduction (last rank to arrive publishes the sums);
 //   - VCFX_STUB_DEVICES sets the device count (default 2), VCFX_STUB_FAIL_RANK=r makes the
 //     context of device r fail to open (a rank that stops before its records).
+// Built with -DVCFX_STUB_DISCARD (build/bin/vcfx_pipe_ceiling, tools/microbench/pipe_ceiling.cpp)
+// the ingest keeps nothing: the drop-in's own stdin reader with the device stage stubbed, the
+// pipe ceiling bench.py's e2e leg quotes.
 #include <stdlib.h>
 #include <string.h>
 
@@ -53,14 +56,22 @@ const char *vcfxg_last_error(const vcfxg_ctx *c) { return c ? c->err.c_str() : "
 
 int vcfxg_ingest_begin(vcfxg_ctx *c, size_t size_hint) {
     c->input.clear();
+#ifndef VCFX_STUB_DISCARD
     c->input.reserve(size_hint);
+#else
+    (void)size_hint;
+#endif
     c->ingesting = true;
     return VCFXG_OK;
 }
 
 int vcfxg_ingest(vcfxg_ctx *c, const char *host, size_t n, int is_final_chunk) {
     if (!c->ingesting) return VCFXG_E_STATE;
+#ifndef VCFX_STUB_DISCARD
     c->input.append(host, n);
+#else
+    (void)host, (void)n;
+#endif
     if (is_final_chunk) c->ingesting = false;
     return VCFXG_OK;
 }
@@ -188,6 +199,7 @@ std::recursive_mutex &getopt_mutex() {
 }
 }  // namespace vcfxh
 
+#ifndef VCFX_STUB_DISCARD  // (the pipe ceiling has its own main and no tool)
 extern "C" int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd) {
     const char *t = strrchr(tool, '/');
     t = t ? t + 1 : tool;
@@ -203,3 +215,4 @@ int main(int argc, char **argv) {
     if (ngpu > 1) return vcfx_tool_main_sharded(argv[1], argc - 1, argv + 1, 0, 1, 2, ngpu);
     return vcfx_tool_main(argv[1], argc - 1, argv + 1, 0, 1, 2);
 }
+#endif
