@@ -467,13 +467,14 @@ static bool load_hints(vcfxg_ctx *c, const char *h, size_t n) {
         p = e + 1;
     }
     if (lines) c->hint_line = (int64_t)((std::min(p, n) - first) / (size_t)lines);
-    // the walkers' chunk: 128 KiB, or about 16 records (rounded up to 64 KiB, at most 4 MiB) for
+    // the walkers' chunk: 128 KiB, or about 12 records (rounded up to 64 KiB, at most 4 MiB) for
     // records over 16 KiB: each walker's two backward boundary scans read about one record, so
     // long records want longer chunks (GT:AD:DP, 30 KB records: 128 KiB 5.03 ms, 512 KiB 4.76,
-    // 1 MiB 5.10; r03 sweep).  VCFXG_WALK_CHUNK overrides.
+    // 1 MiB 5.10; r03 sweep; r05, XCD-contiguous walker blocks: 256 KiB 3.73 ms, 384 KiB 3.65,
+    // 512 KiB 3.69, 768 KiB 3.89).  VCFXG_WALK_CHUNK overrides.
     if (!getenv("VCFXG_WALK_CHUNK"))
         c->walk_chunk = c->hint_line > 16 * 1024
-                            ? std::min<int64_t>(((16 * c->hint_line + 65535) / 65536) * 65536, 4 << 20)
+                            ? std::min<int64_t>(((12 * c->hint_line + 65535) / 65536) * 65536, 4 << 20)
                             : 128 * 1024;
     return true;
 }
