@@ -132,11 +132,14 @@ __device__ __forceinline__ int64_t scan_nl_back(const char *__restrict__ buf, in
 // chunk of their first byte, a walker's forward search for its first line read the tail of
 // the previous chunk's last line, which that chunk's walker read again only at its end (from
 // HBM: the walk's 3.9 % over-fetch).
+#ifndef VCFXG_WALK_SCAN_U
+#define VCFXG_WALK_SCAN_U 3  // KiB per backward-scan step
+#endif
 __device__ __forceinline__ void walker_lines(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t cs,
                                              int64_t ce, int64_t &b0, int64_t &b1) {
     // both backward scans in one loop: each step issues the loads of both before either is
     // examined (one round trip for the two where two scans in sequence took two)
-    constexpr int kU = 3;  // (4: the prologue pushed the walks over an occupancy step)
+    constexpr int kU = VCFXG_WALK_SCAN_U;  // (4: the prologue pushed the walks over an occupancy step)
     bool da = cs <= lo, db = ce >= hi;
     int64_t ra = lo - 1, rb = lo - 1;
     const int64_t lb = lo & ~(int64_t)15;
