@@ -133,7 +133,11 @@ __device__ __forceinline__ int64_t scan_nl_back(const char *__restrict__ buf, in
 // the previous chunk's last line, which that chunk's walker read again only at its end (from
 // HBM: the walk's 3.9 % over-fetch).
 #ifndef VCFXG_WALK_SCAN_U
-#define VCFXG_WALK_SCAN_U 3  // KiB per backward-scan step
+// KiB per backward-scan step.  r05: 1 (from 3): a step reads past the '\n' it finds into the
+// previous line, which that line's walker reads again much later -- PMC fetch 4.61 -> 4.56 GB per
+// AF walk launch (a plain stream of the same bytes: 4.45), walk time unchanged or 0.3 % better
+// (profiles/r05_walk_scan_step_ab.txt, r05_pmc_calibration.json)
+#define VCFXG_WALK_SCAN_U 1
 #endif
 __device__ __forceinline__ void walker_lines(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t cs,
                                              int64_t ce, int64_t &b0, int64_t &b1) {
