@@ -507,9 +507,15 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
 }
 
 // walker regions -> dense per-line arrays in file order (offs = exclusive scan of wcount):
-// one wave per walker region at a time (its lanes copy the region's lines, 64 at a time), so
-// no slot division and no work for the unused slots; the rows / data-line counters (every
-// GT-first record counts as both) are reduced per block (few blocks: few atomics)
+// kCompactSub walker regions per wave at a time, one per group of 64 / kCompactSub lanes (r05: a
+// region holds ~13 lines on the 10 KB-record shards, so one region per wave left 51 of 64 lanes
+// idle through every round trip), so no slot division and no work for the unused slots; the
+// rows / data-line counters (every GT-first record counts as both) are reduced per block (few
+// blocks: few atomics)
+#ifndef VCFXG_COMPACT_SUB
+#define VCFXG_COMPACT_SUB 4
+#endif
+constexpr int kCompactSub = VCFXG_COMPACT_SUB, kCompactLanes = kWave / kCompactSub;
 __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_t cap_w,
                                                       const uint64_t *__restrict__ offs,
                                                       const uint32_t *__restrict__ wgt,
@@ -526,12 +532,16 @@ __global__ __launch_bounds__(256) void k_walk_compact(int64_t n_walkers, uint64_
     __shared__ uint32_t red[256 / kWave];
     uint32_t g = 0;
     const int64_t nwaves = (int64_t)gridDim.x * (256 / kWave);
-    for (int64_t w = (int64_t)blockIdx.x * (256 / kWave) + threadIdx.x / kWave; w < n_walkers; w += nwaves) {
+    const int sub = lane() / kCompactLanes, sl = lane() % kCompactLanes;
+    for (int64_t w0 = ((int64_t)blockIdx.x * (256 / kWave) + threadIdx.x / kWave) * kCompactSub; w0 < n_walkers;
+         w0 += nwaves * kCompactSub) {
+        const int64_t w = w0 + sub;
+        if (w >= n_walkers) continue;
         // (bpre: block-local offsets of k_walker_scan)
         const uint64_t d0 = offs[w] + (bpre ? bpre[w / kWalkerScanBlock] : 0),
                        cnt = offs[w + 1] + (bpre ? bpre[(w + 1) / kWalkerScanBlock] : 0) - d0, s0 = (uint64_t)w * cap_w;
-        g += lane() == 0 ? (wgt[w] & 0xFFFFu) : 0u;
-        for (uint64_t i = lane(); i < cnt; i += kWave) {
+        g += sl == 0 ? (wgt[w] & 0xFFFFu) : 0u;
+        for (uint64_t i = sl; i < cnt; i += kCompactLanes) {
             const uint64_t sl = s0 + i, d = d0 + i;
             line_end[d] = le_b[sl];
             alt[d] = alt_b[sl];
