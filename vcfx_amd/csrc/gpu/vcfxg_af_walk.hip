@@ -160,7 +160,7 @@ void k_af_walk(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t chu
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
     int64_t L, ce2;  // this walker's lines start in [L, ce2)
-    walker_lines(buf, lo, hi, cs, ce, L, ce2);
+    walker_lines(buf, lo, hi, cs, ce, L, ce2, chunk);
     const int64_t L0 = L;
     uint64_t wtext = 0;  // region tail (tail.wtext): bytes of this walker's GT-line rows
     int64_t span = span0;  // predicted '\n' distance from the sample start

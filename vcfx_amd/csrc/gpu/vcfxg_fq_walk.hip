@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kWalkThreads) void k_fq_walk(const char *__restrict
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
     int64_t L, ce2;  // this walker's lines start in [L, ce2)
-    walker_lines(buf, lo, hi, cs, ce, L, ce2);
+    walker_lines(buf, lo, hi, cs, ce, L, ce2, chunk);
     int64_t span = kGQ ? span0 : 0;  // predicted '\n' distance from the sample start
     uint8_t cr_prev = 0;             // and the '\r' state of that record
     uint64_t n = 0;

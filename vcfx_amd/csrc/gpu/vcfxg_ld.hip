@@ -473,7 +473,7 @@ __global__ __launch_bounds__(kWalkThreads) __attribute__((amdgpu_waves_per_eu(VC
     const int64_t cs = lo + wk * chunk;
     const int64_t ce = std::min<int64_t>(cs + chunk, hi);
     int64_t L, ce2;
-    walker_lines(buf, lo, hi, cs, ce, L, ce2);
+    walker_lines(buf, lo, hi, cs, ce, L, ce2, chunk);
     int64_t span = span0;  // predicted '\n' distance from the sample start
     uint64_t n = 0, nv = 0;
     const uint64_t base = (uint64_t)wk * cap_w;

@@ -139,11 +139,12 @@ __device__ __forceinline__ int64_t scan_nl_back(const char *__restrict__ buf, in
 // (profiles/r05_walk_scan_step_ab.txt, r05_pmc_calibration.json)
 #define VCFXG_WALK_SCAN_U 1
 #endif
-__device__ __forceinline__ void walker_lines(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t cs,
-                                             int64_t ce, int64_t &b0, int64_t &b1) {
+template <int kU>
+__device__ __forceinline__ void walker_lines_u(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t cs,
+                                               int64_t ce, int64_t &b0, int64_t &b1) {
     // both backward scans in one loop: each step issues the loads of both before either is
     // examined (one round trip for the two where two scans in sequence took two)
-    constexpr int kU = VCFXG_WALK_SCAN_U;  // (4: the prologue pushed the walks over an occupancy step)
+    // (kU KiB per step; 4: the prologue pushed the walks over an occupancy step)
     bool da = cs <= lo, db = ce >= hi;
     int64_t ra = lo - 1, rb = lo - 1;
     const int64_t lb = lo & ~(int64_t)15;
@@ -200,6 +201,13 @@ __device__ __forceinline__ void walker_lines(const char *__restrict__ buf, int64
     }
     b0 = cs <= lo ? lo : ra + 1;
     b1 = ce >= hi ? hi : rb + 1;
+}
+// the step by chunk size: long-record chunks (> 256 KiB: ~12 records of > 16 KiB, the boundary
+// ~half a record back) take 3 KiB steps -- 1 KiB steps cost the GT:AD:DP walk 3 % (r05)
+__device__ __forceinline__ void walker_lines(const char *__restrict__ buf, int64_t lo, int64_t hi, int64_t cs,
+                                             int64_t ce, int64_t &b0, int64_t &b1, int64_t chunk) {
+    if (chunk > ((int64_t)256 << 10)) walker_lines_u<3>(buf, lo, hi, cs, ce, b0, b1);
+    else walker_lines_u<VCFXG_WALK_SCAN_U>(buf, lo, hi, cs, ce, b0, b1);
 }
 
 // The head analysis classifies the window SWAR and then walks the matches in scalar code:
