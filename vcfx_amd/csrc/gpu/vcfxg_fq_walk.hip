@@ -4,11 +4,10 @@
 // line's head analysed out of an LDS window fetched while the previous line was swept) with
 // the per-line work of the two tools:
 //
-//   * record_filter (kRF): evaluateLine (VCFX_record_filter.cpp:383-401) over fields 0-7
-//     (rf_eval, vcfxg_rf.h), given the first 8 tabs found in the line's window, evaluated
-//     lane-parallel for a batch of 64 lines when the batch is flushed.  A line whose first
-//     8 tabs are not inside the 1 KiB window is left to k_fq_finish (status kRfPending, the
-//     thread-per-line rf_line).
+//   * record_filter (kRF): the walk stores each line's first 8 tab offsets (found in its head
+//     window); k_fq_finish then runs evaluateLine (VCFX_record_filter.cpp:383-401, rf_eval in
+//     vcfxg_rf.h) thread-per-line from them.  A line whose first 8 tabs are not inside the
+//     1 KiB window gets status kRfPending and k_fq_finish finds its tabs itself.
 //   * genotype_query (kGQ): checkAnySampleMatches (VCFX_genotype_query.cpp:322-345) on a
 //     GT-first record as the fixed-stride sweep with the early exit at the first match
 //     (gt_fast + GqOp, vcfxg_gt.h); everything else goes to k_gq_complex (kGqPending: the
