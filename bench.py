@@ -825,8 +825,8 @@ def main():
         else:
             extra = ""
         workload = {
-            "af": "VCFX_allele_freq_calc -i (file path) on a device-resident %d x %d VCF shard per GPU: index + "
-                  "allele counts + formatted rows" % (a.records, a.samples),
+            "af": "VCFX_allele_freq_calc -i (file path) on a device-resident %d x %d VCF shard per GPU: the walk "
+                  "(line ends + allele counts + rows composed in LDS) + the rows in file order" % (a.records, a.samples),
             "pipeline": "VCFX_record_filter --filter '%s' | VCFX_genotype_query -g '%s' fused, device-resident "
                         "%d x %d annotated shard per GPU" % (PIPE_FILTER, PIPE_QUERY, a.records, a.samples),
             "nonref": "VCFX_nonref_filter -i (file path) on a device-resident %d x %d shard per GPU: the walk "
