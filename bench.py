@@ -381,6 +381,14 @@ def output_check(workload, eng, s, a, rank, arr=None):
     return {"checked": True, "match": True, "case": case, "what": what}
 
 
+def _walls(records, walls, skip=0):
+    """an e2e leg: the best wall's rate as `value` and the median wall's beside it"""
+    w = sorted(walls[skip:])
+    med = w[len(w) // 2] if len(w) % 2 else 0.5 * (w[len(w) // 2 - 1] + w[len(w) // 2])
+    return {"value": records / w[0], "value_median": records / med, "wall_s": [round(x, 4) for x in walls[skip:]],
+            "wall_median_s": round(med, 4)}
+
+
 PCIE_H2D_GBS = 56.0  # pinned H2D measured on MI355X (tools/microbench/h2d_ingest.cpp; spec Gen5 x16 63 GB/s)
 
 
@@ -423,7 +431,7 @@ def e2e_rates(workload, arr, a, offs=None):
                 r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=300)
                 walls.append(time.perf_counter() - t0)
                 assert r.returncode == 0, r.stderr[-500:]
-            runs[name] = {"value": a.records / min(walls), "wall_s": [round(w, 4) for w in walls]}
+            runs[name] = _walls(a.records, walls)
         # in-process (libvcfx_tools' vcfx_tool_main, stdout -> /dev/null): the first call opens
         # the context and is not counted
         import ctypes
@@ -440,8 +448,8 @@ def e2e_rates(workload, arr, a, offs=None):
                 assert rc == 0, rc
         finally:
             os.close(dn)
-        runs["warm_context_file"] = {"value": a.records / min(walls[1:]), "wall_s": [round(w, 4) for w in walls[1:]],
-                                     "note": "in-process vcfx_tool_main with the device context already open"}
+        runs["warm_context_file"] = dict(_walls(a.records, walls, 1),
+                                         note="in-process vcfx_tool_main with the device context already open")
         # the BGZF (.vcf.gz) form of the same file: the compressed bytes cross PCIe and every member
         # is inflated on the device (vcfxg_ingest_bgzf); the host-inflate path beside it
         # (VCFX_BGZF_DEVICE=0: members inflated on <= 16 host threads, the text crosses PCIe)
@@ -461,8 +469,7 @@ def e2e_rates(workload, arr, a, offs=None):
                     assert r.returncode == 0, r.stderr[-500:]
                 out = subprocess.run([exe] + args + ["-i", bgz], capture_output=True, timeout=300,
                                      env=dict(os.environ, **env)).stdout
-                runs[name] = {"value": a.records / min(walls), "wall_s": [round(w, 4) for w in walls],
-                              "compressed_bytes": os.path.getsize(bgz),
+                runs[name] = {**_walls(a.records, walls), "compressed_bytes": os.path.getsize(bgz),
                               "stdout_equals_plain_input": hashlib.sha256(out).hexdigest() == plain_sha,
                               "note": "BGZF level 1 (build/bin/vcfx_bgzf); " + (
                                   "members inflated on the host (<= 16 threads)" if env else
@@ -479,8 +486,8 @@ def e2e_rates(workload, arr, a, offs=None):
                     assert rc == 0, rc
             finally:
                 os.close(dn)
-            runs["warm_context_bgzf"] = {"value": a.records / min(walls[1:]), "wall_s": [round(w, 4) for w in walls[1:]],
-                                         "note": "in-process vcfx_tool_main on the BGZF file, device context open"}
+            runs["warm_context_bgzf"] = dict(_walls(a.records, walls, 1),
+                                             note="in-process vcfx_tool_main on the BGZF file, device context open")
         finally:
             os.unlink(bgz)
         # per-invocation start-up: the drop-in process on a small input (the first 100 records),
@@ -501,6 +508,7 @@ def e2e_rates(workload, arr, a, offs=None):
                         walls.append(time.perf_counter() - t0)
                         assert r.returncode == 0, r.stderr[-500:]
                     lat[name + "_s"] = round(min(walls), 4)
+                    lat[name + "_median_s"] = round(sorted(walls)[len(walls) // 2], 4)
                 lat["input"] = "first 100 records (%.1f MB)" % (os.path.getsize(small) / 1e6)
                 runs["small_input_latency"] = lat
             finally:
@@ -521,11 +529,14 @@ def e2e_rates(workload, arr, a, offs=None):
                 subprocess.run(["bash", "-o", "pipefail", "-c", "cat '%s' | '%s'%s" % (path, exe, extra)],
                                stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=300, check=True)
                 walls.append(time.perf_counter() - t0)
-            runs[name] = {"value": a.records / min(walls), "wall_s": [round(w, 4) for w in walls]}
+            runs[name] = _walls(a.records, walls)
         if "pipe_ceiling" in runs:
             runs["pipe_ceiling"]["what"] = "cat F | vcfx_pipe_ceiling (the tool's reader, device stage stubbed)"
             runs["process_stdin_pipe"]["frac_of_pipe_ceiling"] = round(
                 runs["process_stdin_pipe"]["value"] / runs["pipe_ceiling"]["value"], 3)
+        if "pipe_drain_ring16x1M" in runs:  # (r03-r04's ceiling: a bare read loop, comparable across rounds)
+            runs["process_stdin_pipe"]["frac_of_drain_ceiling"] = round(
+                runs["process_stdin_pipe"]["value"] / runs["pipe_drain_ring16x1M"]["value"], 3)
         runs["pcie_ceiling"] = a.records / (arr.size / (PCIE_H2D_GBS * 1e9))
         runs["unit"] = "records/s"
         runs["cmd"] = "%s %s -i FILE > /dev/null (page-cache-warm %.2f GB file)" % (tool, " ".join(args), arr.size / 1e9)

@@ -126,6 +126,10 @@ int vcfxg_bgzf_stage(vcfxg_ctx *ctx, const void *host, size_t n, size_t offset, 
  * NULL) then takes the whole member list, launches the members not launched yet and checks every
  * member's CRC-32. */
 int vcfxg_bgzf_inflate(vcfxg_ctx *ctx, const vcfxg_bgzf_member *members, size_t count);
+/* Members of the last vcfxg_ingest_bgzf that the lane decoder (one member per lane) handed to the
+ * wave decoder (one member per wave): stored and fixed-code blocks, codes zlib allows only as a
+ * special case, members under 384 bytes, damaged streams (diagnostic; the output is the same). */
+uint64_t vcfxg_bgzf_handed_over(const vcfxg_ctx *ctx);
 /* page-locked host memory (H2D at the full PCIe rate, asynchronous), for staging rings */
 int vcfxg_host_alloc(vcfxg_ctx *ctx, size_t n, void **out);
 void vcfxg_host_free(vcfxg_ctx *ctx, void *p);

@@ -54,9 +54,11 @@ def main():
                 del got
                 continue
             walls.append(w)
+            handed = eng.bgzf_handed_over()
             for k in ks:
                 ks[k].append(eng.kernel_stats(k)[0])
-            print("rep %d: wall %.2f ms, %s" % (r, 1e3 * w, {k: round(v[-1], 3) for k, v in ks.items()}), flush=True)
+            print("rep %d: wall %.2f ms, %s, handed over %d" % (r, 1e3 * w, {k: round(v[-1], 3) for k, v in ks.items()},
+                                                                handed), flush=True)
         eng.close()
         best = {k: min(v) for k, v in ks.items()}
         out = {"records": a.records, "samples": a.samples, "level": a.level, "members": len(mem),
@@ -65,6 +67,8 @@ def main():
                "inflate_GBps_output": round(arr.size / (best["bgzf_inflate"] * 1e-3) / 1e9, 1),
                "crc_GBps": round(arr.size / (best["bgzf_crc32"] * 1e-3) / 1e9, 1),
                "records_per_s_device_inflate": round(a.records / (best["bgzf_inflate"] + best["bgzf_crc32"]) * 1e3),
+               "members_handed_to_wave_decoder": handed,
+               "lane_decoder": os.environ.get("VCFX_INFLATE_LANES", "1") != "0",
                "output_sha256_matches_plain": True}
         print(json.dumps(out))
         if a.out:

@@ -66,6 +66,7 @@ struct vcfxg_ctx {
     // vcfxg_bgzf_stage: the compressed stream's size and the bytes staged so far (into bgz_in, on
     // copy_stream); vcfxg_bgzf_inflate: members already launched and their output bytes
     size_t bgz_total = 0, bgz_staged = 0;
+    uint64_t bgz_handed = 0;  // members of the last BGZF ingest the lane decoder handed over
     uint64_t bgz_launched = 0, bgz_out = 0;
     hipStream_t copy_stream = nullptr;
     hipEvent_t bgz_copy_ev = nullptr;  // the latest staged copy
@@ -171,7 +172,12 @@ struct vcfxg_ctx {
     DevBuf ld_moff, ld_midx, ld_mvar, ld_gt16, ld_sprec, ld_midx16;
     // device BGZF inflate (vcfxg_ingest_bgzf): compressed bytes, member table, output offsets,
     // per-member status, first bad member
-    DevBuf bgz_in, bgz_mem, bgz_off, bgz_stat, bgz_small;
+    DevBuf bgz_in, bgz_mem, bgz_off, bgz_stat, bgz_small, bgz_perm;
+    // the lane decoder's token buffers: one per inflate stream and one for `stream`; the stream the
+    // wave decoder takes the lane decoder's hand-overs on (beside the copy), and its events
+    DevBuf bgz_tok[kBgzStreams + 1];
+    hipStream_t bgz_aux = nullptr;
+    hipEvent_t bgz_aux_ev[2] = {};
     void *ld_plan_dev = nullptr;
     uint64_t text_bytes = 0;
     uint64_t text_hint = 0;  // AF walk: text bytes of the previous call (the next call's capacity)
@@ -339,8 +345,10 @@ void vcfxg_close(vcfxg_ctx *c) {
     for (DevBuf *b : {&c->input, &c->idx_counts, &c->idx_offs, &c->idx_pos, &c->line_end, &c->d_nlines, &c->scan_tmp, &c->alt,
                       &c->tot, &c->rowpre, &c->status, &c->rowlen, &c->rowoff, &c->text, &c->counters, &c->query, &c->crit, &c->pool, &c->ld_G, &c->ld_lines,
                       &c->ld_vidx, &c->ld_valid, &c->ld_Gc, &c->ld_wcnt, &c->ld_wval, &c->ld_vbase, &c->ld_small, &c->ld_pend, &c->ld_vars, &c->ld_plen, &c->ld_poff, &c->ld_prefix,
-                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16, &c->ld_sprec, &c->ld_midx16, &c->bgz_in, &c->bgz_mem, &c->bgz_off, &c->bgz_stat, &c->bgz_small})
+                      &c->ld_cid, &c->ld_blocks, &c->ld_cnt, &c->ld_off, &c->ld_pairs, &c->ld_fast, &c->ld_gflag, &c->ld_Gp, &c->ld_Gv, &c->ld_Gq, &c->dose_meta, &c->af_meta, &c->ld_temp, &c->ld_quarters, &c->ld_stage_ctr, &c->ld_rowoff, &c->async_small, &c->wk_le, &c->wk_alt, &c->wk_tot, &c->wk_rowpre, &c->wk_status, &c->wk_meta, &c->wk_count, &c->wk_offs, &c->wk_gt, &c->wk_small, &c->wk_tabs, &c->rf_tabs, &c->hwe_aux, &c->wk_aux, &c->hwe_rc, &c->wk_text, &c->wk_toff, &c->wk_start, &c->wk_cx, &c->wk_bs, &c->scratch_small, &c->byte_cnt, &c->ld_moff, &c->ld_midx, &c->ld_mvar, &c->ld_gt16, &c->ld_sprec, &c->ld_midx16, &c->bgz_in, &c->bgz_mem, &c->bgz_off, &c->bgz_stat, &c->bgz_small, &c->bgz_perm})
         if (b->p) (void)hipFree(b->p);
+    for (DevBuf &b : c->bgz_tok)
+        if (b.p) (void)hipFree(b.p);
     if (c->af_small.p) (void)hipFree(c->af_small.p);
     if (c->wk_stage.p) (void)hipFree(c->wk_stage.p);
     if (c->wk_dirty.p) (void)hipFree(c->wk_dirty.p);
@@ -361,6 +369,9 @@ void vcfxg_close(vcfxg_ctx *c) {
         if (c->bgz_ev[k]) (void)hipEventDestroy(c->bgz_ev[k]);
     }
     if (c->bgz_copy_ev) (void)hipEventDestroy(c->bgz_copy_ev);
+    if (c->bgz_aux) (void)hipStreamDestroy(c->bgz_aux);
+    for (hipEvent_t e : c->bgz_aux_ev)
+        if (e) (void)hipEventDestroy(e);
     delete c;
 }
 
@@ -495,6 +506,7 @@ int vcfxg_ingest_begin(vcfxg_ctx *c, size_t size_hint) {
     if (c->copy_stream) HIPCHK(c, hipStreamSynchronize(c->copy_stream));
     for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++)
         if (c->bgz_stream[k]) HIPCHK(c, hipStreamSynchronize(c->bgz_stream[k]));
+    if (c->bgz_aux) HIPCHK(c, hipStreamSynchronize(c->bgz_aux));
     c->bgz_total = c->bgz_staged = 0;
     int r = ensure(c, c->input, size_hint + kPad);
     if (r) return r;
@@ -579,6 +591,7 @@ int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, si
         if (!r) r = ensure(c, c->bgz_off, 8 * mm);
         if (!r) r = ensure(c, c->bgz_stat, 4 * mm);
         if (!r) r = ensure(c, c->bgz_small, 64);
+        if (!r) r = ensure(c, c->bgz_perm, 4 * mm);
         if (r) return r;
         if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
         if (!c->bgz_copy_ev) HIPCHK(c, hipEventCreateWithFlags(&c->bgz_copy_ev, hipEventDisableTiming));
@@ -587,10 +600,12 @@ int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, si
             if (!c->bgz_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&c->bgz_ev[k], hipEventDisableTiming));
         }
         c->bgz_next = 0;
-        // (the stream's earlier work -- buffers just reallocated, the last call's kernels -- first)
+        // (the first-bad marker and the hand-over count, then the stream's earlier work -- buffers
+        // just reallocated, the last call's kernels: every batch is ordered after this event)
+        HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
+        HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_small) + 8, 0, 8, c->stream));
         HIPCHK(c, hipEventRecord(c->bgz_copy_ev, c->stream));
         HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->bgz_copy_ev, 0));
-        HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
         c->bgz_total = comp_total;
         c->bgz_staged = 0;
         c->bgz_launched = 0;
@@ -620,9 +635,54 @@ int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, si
 // launch the inflate of members [first, first + count) of the staged stream: their table entries
 // and output offsets (from the running output count) to the device, k_inflate after the copies
 // staged so far
+// the token buffer of stream slot k (kBgzStreams: c->stream) for `count` members, at most 65,536 at
+// a time (1.6 GB: the bench shard's 65,834 members in one launch, all its copy waves resident at
+// once); 0 members when it cannot be had (every member then on the wave decoder)
+static uint64_t bgz_tokens(vcfxg_ctx *c, int k, uint64_t count, hipStream_t st) {
+    const uint64_t want = std::min<uint64_t>(count, 65536);
+    const size_t bytes = (size_t)want * vcfxg::kTokCap * 4;
+    DevBuf &b = c->bgz_tok[k];
+    if (b.cap >= bytes) return want;
+    if (b.p) {  // (the stream's earlier batches may still read it)
+        if (hipStreamSynchronize(st) != hipSuccess) return 0;
+        (void)hipFree(b.p);
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    if (hipMalloc(&b.p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        b.p = nullptr;
+        return 0;
+    }
+    b.cap = bytes;
+    return want;
+}
+
+// the lane decoder's member order for `count` members: largest compressed first (a counting sort
+// on 64-byte buckets: the lanes of a wave then decode similar amounts, and the largest go first)
+static std::vector<uint32_t> bgz_order(const vcfxg_bgzf_member *mem, uint64_t count) {
+    constexpr uint32_t kB = 1026;  // (src_len <= 65,536 + header slack: buckets of 64 B)
+    std::vector<uint32_t> cnt(kB + 1, 0), perm(count);
+    auto bucket = [&](uint64_t i) { return kB - 1 - std::min<uint32_t>(mem[i].src_len >> 6, kB - 1); };
+    for (uint64_t i = 0; i < count; i++) cnt[bucket(i) + 1]++;
+    for (uint32_t b = 0; b < kB; b++) cnt[b + 1] += cnt[b];
+    for (uint64_t i = 0; i < count; i++) perm[cnt[bucket(i)]++] = (uint32_t)i;
+    return perm;
+}
+
+// the hand-over stream and its events (created once)
+static int bgz_aux(vcfxg_ctx *c) {
+    if (!c->bgz_aux) HIPCHK(c, hipStreamCreateWithFlags(&c->bgz_aux, hipStreamNonBlocking));
+    for (hipEvent_t &e : c->bgz_aux_ev)
+        if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return VCFXG_OK;
+}
+
 static int bgz_launch(vcfxg_ctx *c, const vcfxg_bgzf_member *mem, uint64_t first, uint64_t count,
-                      hipStream_t st) {
+                      hipStream_t st, int slot) {
     if (!count) return VCFXG_OK;
+    const std::vector<uint32_t> perm = bgz_order(mem, count);
+    HIPCHK(c, hipMemcpyAsync(P<uint32_t>(c->bgz_perm) + first, perm.data(), 4 * count, hipMemcpyHostToDevice, st));
     std::vector<uint64_t> off(count);
     uint64_t o = c->bgz_out;
     for (uint64_t i = 0; i < count; i++) {
@@ -634,10 +694,13 @@ static int bgz_launch(vcfxg_ctx *c, const vcfxg_bgzf_member *mem, uint64_t first
     HIPCHK(c, hipMemcpyAsync(P<uint64_t>(c->bgz_off) + first, off.data(), 8 * count, hipMemcpyHostToDevice, st));
     HIPCHK(c, hipStreamWaitEvent(st, c->bgz_copy_ev, 0));
     static vcfxg::Crc1k z1k_unused{};
+    const uint64_t tm = bgz_tokens(c, slot, count, st);
+    if (int r = bgz_aux(c)) return r;
     HIPCHK(c, vcfxg::launch_inflate(0, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem) + first,
                                     P<uint64_t>(c->bgz_off) + first, count, P<uint8_t>(c->input) + c->n,
                                     P<uint32_t>(c->bgz_stat) + first, P<unsigned long long>(c->bgz_small), z1k_unused,
-                                    st, first));
+                                    st, first, P<uint32_t>(c->bgz_tok[slot]), tm, P<uint32_t>(c->bgz_perm) + first,
+                                    c->bgz_aux, c->bgz_aux_ev[0], c->bgz_aux_ev[1]));
     c->bgz_launched = first + count;
     c->bgz_out = o;
     return VCFXG_OK;
@@ -660,7 +723,7 @@ int vcfxg_bgzf_inflate(vcfxg_ctx *c, const vcfxg_bgzf_member *mem, size_t count)
     if (c->n + c->bgz_out + out + kPad > c->input.cap) return VCFXG_E_CAP;
     const int k = c->bgz_next;
     c->bgz_next = (k + 1) % vcfxg_ctx::kBgzStreams;
-    int r = bgz_launch(c, mem, c->bgz_launched, count, c->bgz_stream[k]);
+    int r = bgz_launch(c, mem, c->bgz_launched, count, c->bgz_stream[k], k);
     if (r) return r;
     HIPCHK(c, hipEventRecord(c->bgz_ev[k], c->bgz_stream[k]));
     return VCFXG_OK;
@@ -693,6 +756,13 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
     }
     off[nm] = tot;
     if (staged && done && off[done] != c->bgz_out) return VCFXG_E_ARG;  // (not the launched members)
+    if (staged) {
+        // every staged copy and every launched batch before anything below (the grow copies the
+        // batches' output; the kernels below read the staged bytes)
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->bgz_copy_ev, 0));
+        if (done)
+            for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->bgz_ev[k], 0));
+    }
     if (c->n + tot + kPad > c->input.cap) {  // grow as vcfxg_ingest does (keeping launched output)
         const size_t keep = c->n + (size_t)(staged ? c->bgz_out : 0);
         size_t ncap = std::max(c->input.cap * 2, c->n + tot + kPad);
@@ -711,6 +781,7 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         if (!r) r = ensure(c, c->bgz_off, 8 * (nm + 1));
         if (!r) r = ensure(c, c->bgz_stat, 4 * (nm + 1));
         if (!r) r = ensure(c, c->bgz_small, 64);
+        if (!r) r = ensure(c, c->bgz_perm, 4 * (nm + 1));
         if (r) return r;
     }
     static vcfxg::Crc1k z1k = [] {
@@ -719,13 +790,9 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         return z;
     }();
     if (staged) {
-        // every staged copy and every launched batch before the kernels below; the members not
-        // launched yet
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->bgz_copy_ev, 0));
-        if (done)
-            for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->bgz_ev[k], 0));
+        // the members not launched yet
         prof_begin(c, "bgzf_inflate");
-        r = bgz_launch(c, mem + done, done, nm - done, c->stream);
+        r = bgz_launch(c, mem + done, done, nm - done, c->stream, vcfxg_ctx::kBgzStreams);
         prof_end(c, "bgzf_inflate");
         if (r) return r;
     } else {
@@ -737,11 +804,18 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
             HIPCHK(c, hipMemcpyAsync(c->bgz_off.p, off.data(), 8 * nm, hipMemcpyHostToDevice, c->stream));
         }
         HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
+        HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_small) + 8, 0, 8, c->stream));
         prof_end(c, "bgzf_h2d");
+        const uint64_t tm = bgz_tokens(c, vcfxg_ctx::kBgzStreams, nm, c->stream);
+        if (int ra = bgz_aux(c)) return ra;
+        const std::vector<uint32_t> perm = bgz_order(mem, nm);
+        if (nm) HIPCHK(c, hipMemcpyAsync(c->bgz_perm.p, perm.data(), 4 * nm, hipMemcpyHostToDevice, c->stream));
         prof_begin(c, "bgzf_inflate");
         HIPCHK(c, vcfxg::launch_inflate(0, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem),
                                         P<uint64_t>(c->bgz_off), nm, P<uint8_t>(c->input) + c->n,
-                                        P<uint32_t>(c->bgz_stat), P<unsigned long long>(c->bgz_small), z1k, c->stream));
+                                        P<uint32_t>(c->bgz_stat), P<unsigned long long>(c->bgz_small), z1k, c->stream, 0,
+                                        P<uint32_t>(c->bgz_tok[vcfxg_ctx::kBgzStreams]), tm, P<uint32_t>(c->bgz_perm),
+                                        c->bgz_aux, c->bgz_aux_ev[0], c->bgz_aux_ev[1]));
         prof_end(c, "bgzf_inflate");
     }
     prof_begin(c, "bgzf_crc32");
@@ -749,14 +823,16 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
                                     nm, P<uint8_t>(c->input) + c->n, P<uint32_t>(c->bgz_stat),
                                     P<unsigned long long>(c->bgz_small), z1k, c->stream));
     prof_end(c, "bgzf_crc32");
-    static thread_local uint64_t bad;
+    static thread_local uint64_t small[2];  // the first bad member, the hand-over count
     static thread_local uint8_t lastb;
-    HIPCHK(c, hipMemcpyAsync(&bad, c->bgz_small.p, 8, hipMemcpyDeviceToHost, c->stream));
+    uint64_t &bad = small[0];
+    HIPCHK(c, hipMemcpyAsync(small, c->bgz_small.p, 16, hipMemcpyDeviceToHost, c->stream));
     if (tot) HIPCHK(c, hipMemcpyAsync(&lastb, P<uint8_t>(c->input) + c->n + tot - 1, 1, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
     c->bgz_total = c->bgz_staged = 0;
     c->bgz_launched = c->bgz_out = 0;
+    c->bgz_handed = (uint32_t)small[1];
     if (bad != ~0ull) {
         uint32_t why = 0;
         (void)hipMemcpy(&why, P<uint32_t>(c->bgz_stat) + bad, 4, hipMemcpyDeviceToHost);
@@ -3235,6 +3311,7 @@ int vcfxg_comm_init(vcfxg_ctx *const *ctxs, int n, vcfxg_comm **out) {
 int vcfxg_comm_uses_rccl(const vcfxg_comm *c) { return c && c->allreduce ? 1 : 0; }
 
 const char *vcfxg_last_schedule(const vcfxg_ctx *c) { return c ? c->last_schedule : ""; }
+uint64_t vcfxg_bgzf_handed_over(const vcfxg_ctx *c) { return c ? c->bgz_handed : 0; }
 
 int vcfxg_comm_rccl_stats(vcfxg_comm *c, uint64_t *calls, uint64_t *mismatches) {
     if (!c) return VCFXG_E_ARG;

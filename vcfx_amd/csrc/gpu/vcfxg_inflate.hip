@@ -40,6 +40,7 @@
 // host, which reproduces the reference's behaviour on a damaged stream.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "vcfxg_kernels.h"
 
@@ -243,13 +244,16 @@ __device__ __forceinline__ uint32_t slow_decode(InfLds &S, int k, uint32_t p, ui
     return kExc | kBad;
 }
 
-__global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
-                                                const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
-                                                uint32_t *__restrict__ mstat, unsigned long long *__restrict__ first_bad,
-                                                uint64_t mbase) {
-    __shared__ InfLds S;
+// the lane decoder's verdict for a member it hands to the wave decoder (mstat)
+constexpr uint32_t kDefer = 0xFFFFu;
+
+// One member inflated by the whole wave (the wave decoder): every member the lane decoder below
+// hands over (kDefer), which includes every member that zlib would refuse.
+__device__ __forceinline__ void inflate_wave(InfLds &S, const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
+                                             const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
+                                             uint32_t *__restrict__ mstat, unsigned long long *__restrict__ first_bad,
+                                             uint64_t mbase, const uint32_t m) {
     const int lane = threadIdx.x;
-    const uint32_t m = blockIdx.x;
     const BgzfMember M = mem[m];
     const uint64_t src = M.src_off;
     const uint32_t olen = M.out_len;
@@ -595,6 +599,515 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
     }
 }
 
+// the wave decoder over the members the lane decoder handed over (a grid-stride loop: the count
+// is known only on the device)
+__global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
+                                                const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
+                                                uint32_t *__restrict__ mstat, unsigned long long *__restrict__ first_bad,
+                                                uint64_t mbase, uint32_t n, int all) {
+    __shared__ InfLds S;
+    for (uint32_t m = blockIdx.x; m < n; m += gridDim.x) {
+        if (!all && uni(mstat[m]) != kDefer) continue;
+        __syncthreads();  // (the previous member's last reads of S)
+        inflate_wave(S, comp, mem, out_off, out, mstat, first_bad, mbase, m);
+    }
+}
+
+// ---- the lane decoder: one member per lane -------------------------------------------------------
+// The wave decoder above decodes on the CU's one scalar unit: on the bench shard (65,834 members of
+// level-1 bgzip output, each ~2,200 symbols, mostly matches of ~35 B) it spends ~23 ms.  The
+// Huffman decode moves to the vector lanes, one member per lane, and the copy keeps the wave:
+//   k_inflate_decode: the Huffman decode of a member per lane, to a token list per member (a
+//     literal byte, or a match's length and distance: 4 B each, in a per-launch token buffer).  The
+//     tables live in the lane's own 848-byte slice of LDS (three waves per CU): a 2^7-entry
+//     literal/length root table and a 2^6-entry distance root table of 16-bit entries, with zlib's
+//     sub-tables (inftrees.c: a root entry points to a table indexed by the bits past the root) for
+//     longer codes, built per lane from the code lengths (which the header decode writes into the
+//     token slot's spare tail).  The stream comes through a 64-byte LDS window per lane: a symbol's
+//     64 bits are one ds_read2 + ds_read and two funnel shifts.  The window is reloaded once per
+//     trip of four symbols from registers loaded a whole trip ahead, and every trip makes the same
+//     loads and one 16-byte token store whatever its lanes decoded: the vector-memory counter is
+//     per wave and in order, so a load one lane needs now must not sit behind loads other lanes
+//     issued just before.  The lanes of a wave take members of similar compressed size (the host
+//     orders them, largest first): a wave runs as long as its longest member.
+//   k_inflate_copy (below): the LZ77 copy of a member's tokens per wave.
+// Only what zlib accepts is accepted: dynamic-Huffman blocks whose codes are complete (no
+// over-subscribed or incomplete code, an end-of-block code), repeats within bounds, no distance
+// past the member's start, output exactly ISIZE and a stream ending exactly at the trailer.
+// Everything else -- stored and fixed blocks, the single-code and empty distance codes zlib allows,
+// tables past the slice, members over the token capacity, and every damaged stream -- is handed to
+// the wave decoder (mstat kDefer), which decides it exactly as before.  k_crc32 then checks every
+// member.
+constexpr int kLT = 424;         // 16-bit table entries per lane (848 B: 3 waves per CU in 160 KiB)
+constexpr int kCtr = kLT - 32;   // the builder's 16 32-bit counters at the slice's tail
+constexpr uint32_t kLitR = 7, kDistR = 6;
+constexpr uint32_t kTokNone = 0xFFFFFFFFu;  // a member's token count: handed over
+// the copy's window (k_inflate_copy): 8 KiB of LDS per wave; a match from further back than
+// kCReach, or longer than 64 bytes, takes its slow path
+constexpr uint32_t kCW = 8192, kCWMask = kCW - 1;
+constexpr uint32_t kCReach = kCW - 258;
+constexpr uint32_t kCFlush = 1024;  // the window goes out in 1 KiB steps
+// a token: bits 16-24 its length (a literal: 1), bits 0-14 a match's distance - 1 (a literal: its
+// byte), bit 15 the copy's slow path, bit 25 a literal
+constexpr uint32_t kTLit = 1u << 25, kTSlow = 1u << 15;
+
+// entries: bits 0-3 the code length, 4-12 the value (literal byte, length symbol - 257, distance
+// symbol, code-length symbol), 14-15 the kind; a root entry of kind kKPtr holds its sub-table's
+// offset in the slice (bits 0-8) and index bits (9-12)
+constexpr uint32_t kKLit = 0, kKLen = 1, kKPtr = 2, kKEob = 3;
+
+__device__ __forceinline__ uint32_t brev_n(uint32_t c, uint32_t n) { return __brev(c) >> (32 - n); }
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) {
+    uint4 v;
+    __builtin_memcpy(&v, p, 16);
+    return v;
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem, const uint64_t *__restrict__ out_off,
+                 uint8_t *__restrict__ out, uint32_t *__restrict__ mstat, uint32_t *__restrict__ ndefer,
+                 uint32_t *__restrict__ tok, uint32_t tok_cap, const uint32_t *__restrict__ perm, uint32_t n_lanes) {
+    __shared__ __attribute__((aligned(16))) uint16_t T[64 * kLT];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = blockIdx.x * 64 + lane;  // the lane's slot; its member perm[i]
+    if (i >= n_lanes) return;  // (no barrier below: lanes never share LDS)
+    const uint32_t m = perm[i];
+    const uint32_t lt = lane * kLT;
+    // the slice's last 64 bytes: the builder's counters, and otherwise the stream window
+    uint32_t *const C = reinterpret_cast<uint32_t *>(&T[lt + kCtr]);
+    uint32_t *const Wd = C;
+    uint32_t *const tk = tok + (size_t)i * tok_cap;  // [0] the count, then the tokens
+    const BgzfMember M = mem[m];
+    const uint32_t olen = M.out_len;
+    // the code lengths' scratch: the token slot's last 512 bytes (past every token)
+    uint8_t *const lp = reinterpret_cast<uint8_t *>(tk + tok_cap - 128);
+    const uint8_t *const cp = comp + M.src_off;
+    const uint32_t xlen = (uint32_t)cp[10] | ((uint32_t)cp[11] << 8);
+    const int64_t plen = (int64_t)M.src_len - 8 - 12 - (int64_t)xlen;  // the deflate stream's bytes
+    if (plen < 2 || olen > 65536) {
+        tk[0] = kTokNone;
+        mstat[m] = kDefer;
+        atomicAdd(ndefer, 1u);
+        return;
+    }
+    bool bad = false;
+    // The bit reader: bpos = the next stream bit, counted from qp (the stream's first byte rounded
+    // down to a dword; the first sh bits are not the stream's).  The window holds stream dwords
+    // [wb, wb + 16) in LDS: a symbol's 64 bits are one ds_read2 + ds_read and two funnel shifts.
+    const uint32_t a3 = (uint32_t)((uintptr_t)(cp + 12 + xlen) & 3);
+    const uint32_t *const qp = reinterpret_cast<const uint32_t *>(cp + 12 + xlen - a3);  // (global: no int casts)
+    const uint32_t sh = a3 * 8;
+    const uint32_t bend = (uint32_t)(plen * 8) + sh;  // the stream's end bit
+    uint32_t bpos = sh, wb = 0;
+    uint4 N0, N1, N2, N3;  // the next trip's window, loaded a trip ahead (from dword nbase)
+    uint32_t nbase = 0;
+    auto qdw = [&]() -> uint32_t {  // the dword a window load starts at (a stream run past its end stops)
+        return bad ? 0u : (bpos >> 5);
+    };
+    auto read64 = [&](uint32_t &lo, uint32_t &hi) {
+        const uint32_t k = (bpos >> 5) - wb;
+        const uint32_t d0 = Wd[k], d1 = Wd[k + 1], d2 = Wd[k + 2];
+        lo = __builtin_amdgcn_alignbit(d1, d0, bpos & 31);
+        hi = __builtin_amdgcn_alignbit(d2, d1, bpos & 31);
+    };
+    auto put_window = [&](const uint4 &a, const uint4 &b, const uint4 &c, const uint4 &d, uint32_t base) {
+        reinterpret_cast<uint4 *>(Wd)[0] = a;
+        reinterpret_cast<uint4 *>(Wd)[1] = b;
+        reinterpret_cast<uint4 *>(Wd)[2] = c;
+        reinterpret_cast<uint4 *>(Wd)[3] = d;
+        wb = base;
+    };
+    auto sync_window = [&]() {  // the window from the current dword, now (block headers)
+        const uint32_t q = qdw();
+        const uint4 *p = reinterpret_cast<const uint4 *>(qp + q);
+        put_window(p[0], p[1], p[2], p[3], q);
+    };
+    auto hread = [&](uint32_t &lo, uint32_t &hi) {  // a header's read: the window moved when needed
+        if ((bpos >> 5) - wb > 13) sync_window();
+        read64(lo, hi);
+    };
+
+    // Builds the code of `nsym` lengths at lens (bytes) into the slice at `base` with `R` root
+    // bits; kind 0 literal/length, 1 distance or code-length.  Returns the entries used, or -1: a
+    // code zlib refuses or allows only as a special case (incomplete, over-subscribed, empty), or
+    // one whose tables pass the counters.  (The counters overwrite the stream window.)
+    auto build = [&](uint32_t base, const uint8_t *lens, uint32_t nsym, uint32_t R, int kind) -> int {
+#pragma unroll
+        for (int L = 0; L < 16; L++) C[L] = 0;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        for (uint32_t s = 0; s < nsym; s++) {
+            if ((s & 15) == 0) v = ld16(lens + s);
+            atomicAdd(&C[v.x & 15], 1u);
+            v.x = __builtin_amdgcn_alignbit(v.y, v.x, 8);
+            v.y = __builtin_amdgcn_alignbit(v.z, v.y, 8);
+            v.z = __builtin_amdgcn_alignbit(v.w, v.z, 8);
+            v.w >>= 8;
+        }
+        uint32_t cnt[16];
+#pragma unroll
+        for (int L = 0; L < 16; L++) cnt[L] = C[L];
+        cnt[0] = 0;
+        int left = 1;
+        uint32_t maxl = 0;
+        bool over = false;
+#pragma unroll
+        for (int L = 1; L < 16; L++) {
+            left = 2 * left - (int)cnt[L];
+            over = over || left < 0;
+            if (cnt[L]) maxl = L;
+        }
+        if (over || left != 0) return -1;
+        uint32_t first[16];
+        uint32_t code = 0;
+        first[0] = 0;
+#pragma unroll
+        for (int L = 1; L < 16; L++) {
+            code = (code + cnt[L - 1]) << 1;
+            first[L] = code;
+        }
+        uint32_t size = 1u << R;
+        if (base + size > (uint32_t)kCtr) return -1;
+        if (maxl > R) {
+            // zlib's sub-tables, from the counts alone: the long codes in canonical order fill one
+            // root prefix after another; a prefix's table has the fewest index bits its codes fill
+            // (inftrees.c "determine length of next table"); C holds the counts not yet placed
+            uint32_t p = 0;
+#pragma unroll
+            for (int L = 1; L < 16; L++)
+                if ((uint32_t)L == R) p = first[L] + cnt[L];  // the first prefix of a long code
+            uint32_t len = R + 1;
+            while (C[len] == 0) len++;
+            while (len <= maxl) {
+                uint32_t curr = len - R;
+                int lf = 1 << curr;
+                while (curr + R < maxl) {
+                    lf -= (int)C[curr + R];
+                    if (lf <= 0) break;
+                    curr++;
+                    lf <<= 1;
+                }
+                if (base + size + (1u << curr) > (uint32_t)kCtr || p >= (1u << R)) return -1;
+                T[lt + base + brev_n(p, R)] = (uint16_t)((base + size) | (curr << 9) | (kKPtr << 14));
+                size += 1u << curr;
+                uint32_t space = 1u << curr;
+                while (space) {
+                    const uint32_t s2 = R + curr - len;
+                    const uint32_t r = C[len], k = min(r, space >> s2);
+                    C[len] = r - k;
+                    space -= k << s2;
+                    if (r == k) {
+                        do len++;
+                        while (len <= maxl && C[len] == 0);
+                        if (len > maxl) break;
+                    }
+                }
+                p++;
+            }
+        }
+#pragma unroll
+        for (int L = 0; L < 16; L++) C[L] = first[L];
+        for (uint32_t s = 0; s < nsym; s++) {
+            if ((s & 15) == 0) v = ld16(lens + s);
+            const uint32_t L = v.x & 15;
+            v.x = __builtin_amdgcn_alignbit(v.y, v.x, 8);
+            v.y = __builtin_amdgcn_alignbit(v.z, v.y, 8);
+            v.z = __builtin_amdgcn_alignbit(v.w, v.z, 8);
+            v.w >>= 8;
+            if (!L) continue;
+            const uint32_t c = atomicAdd(&C[L], 1u);
+            uint32_t e;
+            if (kind == 0)
+                e = s < 256 ? (L | (s << 4)) : (s == 256 ? (L | (kKEob << 14)) : (L | ((s - 257) << 4) | (kKLen << 14)));
+            else
+                e = L | (s << 4);
+            if (L <= R) {
+                for (uint32_t i = brev_n(c, L); i < (1u << R); i += 1u << L) T[lt + base + i] = (uint16_t)e;
+            } else {
+                const uint32_t pe = T[lt + base + brev_n(c >> (L - R), R)];
+                const uint32_t so = pe & 511, cb = (pe >> 9) & 15;
+                for (uint32_t i = brev_n(c & ((1u << (L - R)) - 1), L - R); i < (1u << cb); i += 1u << (L - R))
+                    T[lt + so + i] = (uint16_t)e;
+            }
+        }
+        return (int)size;
+    };
+    // a lookup: the root entry of the next R bits, or its sub-table's entry
+    auto look = [&](uint32_t tb, uint32_t R, uint32_t bits) -> uint32_t {
+        uint32_t e = T[lt + tb + (bits & ((1u << R) - 1))];
+        if ((e >> 14) == kKPtr) e = T[lt + (e & 511) + ((bits >> R) & ((1u << ((e >> 9) & 15)) - 1))];
+        return e;
+    };
+
+    uint32_t xd = 0;      // output bytes decoded so far
+    uint32_t st = 0;      // 0 block header next, 1 in a block, 2 after the last block
+    bool last = false;
+    uint32_t dbase = 0;   // the distance table's offset in the slice
+    // A block header: the code lengths into lp (the code-length code's at lp[320, 339)), then the
+    // tables; the window follows the reads.  Any refusal sets bad.
+    auto header = [&]() {
+        sync_window();
+        uint32_t lo, hi;
+        hread(lo, hi);
+        last = lo & 1;
+        const uint32_t bt = (lo >> 1) & 3;
+        if (bt != 2) {
+            bad = true;
+            return;
+        }
+        const uint32_t nlen = ((lo >> 3) & 31) + 257, ndist = ((lo >> 8) & 31) + 1, ncl = ((lo >> 13) & 15) + 4;
+        bpos += 17;
+        if (nlen > 286 || ndist > 30) {
+            bad = true;
+            return;
+        }
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        __builtin_memcpy(lp + 320, &z, 16);
+        __builtin_memcpy(lp + 336, &z, 16);
+        hread(lo, hi);  // (at most 19 x 3 = 57 bits: one read)
+        const uint64_t cl = (uint64_t)hi << 32 | lo;
+        for (uint32_t i = 0; i < ncl; i++) lp[320 + c_clorder[i]] = (uint8_t)((cl >> (3 * i)) & 7);
+        bpos += 3 * ncl;
+        if (bad || build(0, lp + 320, 19, 7, 1) < 0) {
+            bad = true;
+            return;
+        }
+        sync_window();  // (the counters took the window's place)
+        const uint32_t tot = nlen + ndist;
+        uint32_t n = 0, prev = 0;
+        while (!bad && n < tot) {
+            hread(lo, hi);
+            const uint32_t e = look(0, 7, lo);
+            const uint32_t L = e & 15, sym = (e >> 4) & 31;
+            if (sym < 16) {
+                bpos += L;
+                lp[n++] = (uint8_t)sym;
+                prev = sym;
+                continue;
+            }
+            uint32_t rep, val = 0;
+            if (sym == 16) {
+                rep = 3 + __builtin_amdgcn_ubfe(lo, L, 2);
+                bpos += L + 2;
+                val = prev;
+                if (n == 0) bad = true;
+            } else if (sym == 17) {
+                rep = 3 + __builtin_amdgcn_ubfe(lo, L, 3);
+                bpos += L + 3;
+            } else {
+                rep = 11 + __builtin_amdgcn_ubfe(lo, L, 7);
+                bpos += L + 7;
+            }
+            if (n + rep > tot) bad = true;
+            if (bad) break;
+            for (uint32_t i = 0; i < rep; i++) lp[n + i] = (uint8_t)val;
+            n += rep;
+            prev = val;
+        }
+        if (bad || lp[256] == 0) {  // (no end-of-block code)
+            bad = true;
+            return;
+        }
+        // (one loop for the two codes: one copy of the builder in the code)
+        int used = 0;
+#pragma nounroll
+        for (int j = 0; j < 2 && used >= 0; j++) {
+            const int r = build(j ? (uint32_t)used : 0u, j ? lp + nlen : lp, j ? ndist : nlen, j ? kDistR : kLitR, j);
+            if (j == 0) dbase = (uint32_t)r;
+            used = r;
+        }
+        if (used < 0) bad = true;
+        st = 1;
+        // the window from here, and the next trip's from here too
+        sync_window();
+        N0 = reinterpret_cast<uint4 *>(Wd)[0];
+        N1 = reinterpret_cast<uint4 *>(Wd)[1];
+        N2 = reinterpret_cast<uint4 *>(Wd)[2];
+        N3 = reinterpret_cast<uint4 *>(Wd)[3];
+        nbase = wb;
+    };
+
+    uint32_t ti = 0;  // tokens stored (the first trip starts with the first block's header)
+    // (a trip's store reaches 4 slots past the count; the code-length scratch is the last 128)
+    const uint32_t tmax = tok_cap - 1 - 128 - 8;
+    for (;;) {
+        const bool act = !bad && st != 2;
+        if (!__builtin_amdgcn_ballot_w64(act)) break;
+        // every lane makes a trip's window write, load and token store, decoding or not: the
+        // window loaded a trip ago into LDS, the next trip's from where this one starts
+        put_window(N0, N1, N2, N3, nbase);
+        {
+            const uint32_t q = qdw();
+            const uint4 *p = reinterpret_cast<const uint4 *>(qp + q);
+            N0 = p[0], N1 = p[1], N2 = p[2], N3 = p[3];
+            nbase = q;
+        }
+        uint4 tg = make_uint4(0, 0, 0, 0);
+        uint32_t pc = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (!bad && st == 1) {
+                uint32_t lo, hi;
+                read64(lo, hi);
+                const uint32_t e = look(0, kLitR, lo);
+                const uint32_t L = e & 15, kind = e >> 14;
+                uint32_t t = 0;
+                if (kind == kKLit) {
+                    bpos += L;
+                    if (xd >= olen) bad = true;
+                    t = kTLit | (1u << 16) | ((e >> 4) & 255);
+                    xd++;
+                } else if (kind == kKLen) {
+                    const uint32_t v = (e >> 4) & 31;
+                    uint32_t ext = 0, base = v + 3;
+                    if (v == 28) base = 258;
+                    else if (v >= 8) {
+                        ext = (v - 4) >> 2;
+                        base = ((4 + (v & 3)) << ext) + 3;
+                    }
+                    const uint32_t len = base + __builtin_amdgcn_ubfe(lo, L, ext);
+                    const uint32_t s1 = L + ext;
+                    const uint32_t db = __builtin_amdgcn_alignbit(hi, lo, s1);
+                    const uint32_t d = look(dbase, kDistR, db);
+                    const uint32_t dl = d & 15, ds = (d >> 4) & 31;
+                    const uint32_t dext = ds < 4 ? 0 : (ds >> 1) - 1;
+                    const uint32_t dbs = ds < 4 ? ds + 1 : ((2u | (ds & 1)) << dext) + 1;
+                    const uint32_t dist = dbs + __builtin_amdgcn_ubfe(db, dl, dext);
+                    bpos += s1 + dl + dext;
+                    if (dist > xd || xd + len > olen) bad = true;
+                    t = (len << 16) | (dist - 1) | (len > 64 || dist > kCReach ? kTSlow : 0u);
+                    xd += len;
+                } else {  // end of block
+                    bpos += L;
+                    st = last ? 2 : 0;
+                }
+                if (kind != kKEob) {
+                    tg.x = pc == 0 ? t : tg.x;
+                    tg.y = pc == 1 ? t : tg.y;
+                    tg.z = pc == 2 ? t : tg.z;
+                    tg.w = pc == 3 ? t : tg.w;
+                    pc++;
+                }
+                if (bpos > bend + 64) bad = true;  // (ran past the stream)
+            }
+            if (!bad && st == 0) header();  // (the first block's, or a block after it)
+        }
+        // the trip's tokens (slots past them are rewritten by the next trip)
+        const uint32_t at = ti <= tmax ? ti : tmax;
+        __builtin_memcpy(tk + 1 + at, &tg, 16);
+        ti += pc;
+        if (ti > tmax) bad = true;
+    }
+    if (!bad && (((bpos - sh) + 7) >> 3 != (uint32_t)plen || xd != olen)) bad = true;
+    tk[0] = bad ? kTokNone : ti;
+    mstat[m] = bad ? kDefer : 0u;
+    if (bad) atomicAdd(ndefer, 1u);
+}
+
+// k_inflate_copy: the LZ77 copy of the decoded tokens, one member per wave.  The lane decoder's
+// tokens make the copy a loop of wave-uniform steps (no Huffman work left in it):
+//   - the member's tokens come 64 at a time, one per lane (a coalesced load, the next group in
+//     flight behind the current), and each step broadcasts the next one (v_readlane);
+//   - the output goes through an 8 KiB LDS window: a token's bytes are one LDS read and one write
+//     per lane per 64 bytes (the period-d pattern out[x + i] = out[x - d + i mod d], which is also
+//     the plain copy when d > i: every byte read lies before the match);
+//   - the window goes to memory in aligned, coalesced 16-byte blocks every 1 KiB (byte stores only
+//     at the member's two ends, whose 16-byte blocks it shares with its neighbours);
+//   - a match further back than the window holds (7,934 bytes: 2 % of the bench shard's) reads
+//     the member's output in memory, already written (every store of the wave waited for, the
+//     dwords read at agent scope: from L2, never an older L1 line).
+// Eight KiB of LDS a wave: 20 waves on a CU hide each other's LDS round trips.
+
+__global__ void __launch_bounds__(64) k_inflate_copy(const BgzfMember *__restrict__ mem, const uint64_t *__restrict__ out_off,
+                                                     uint8_t *__restrict__ out, const uint32_t *__restrict__ tok,
+                                                     uint32_t tok_cap, const uint32_t *__restrict__ perm, uint32_t n_lanes) {
+    __shared__ __attribute__((aligned(16))) uint8_t W[kCW];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = blockIdx.x;  // the member's token slot (perm order)
+    if (i >= n_lanes) return;
+    const uint32_t *const tk = tok + (size_t)i * tok_cap;
+    const uint32_t ntok = uni(tk[0]);
+    if (ntok == kTokNone) return;  // (the wave decoder's)
+    const uint32_t m = uni(perm[i]);
+    uint8_t *const ob = out + out_off[m];
+    const uint32_t olen = uni(mem[m].out_len);
+    // output byte p is at window slot (ph + p) & mask, ph = its address mod 16: aligned 16-byte
+    // blocks of the window go to aligned 16-byte blocks of memory
+    const uint32_t ph = (uint32_t)((uintptr_t)ob & 15);
+    uint8_t *const gout = ob - ph;
+    uint32_t x = ph, fl = ph;  // the next byte (window coordinates), the first byte not yet out
+    const uint32_t xend = ph + olen;
+    auto flush = [&](uint32_t to, bool fin) {
+        if (to <= fl) return;
+        uint32_t a = fl;
+        const uint32_t a16 = (a + 15) & ~15u;
+        if (a != a16) {  // (the first block: shared with the member before)
+            const uint32_t e = a16 < to ? a16 : to;
+            if (lane < e - a) gout[a + lane] = W[(a + lane) & kCWMask];
+            a = e;
+        }
+        const uint32_t b16 = to & ~15u;
+        for (uint32_t y = a + 16 * lane; y + 16 <= b16; y += 16 * 64)
+            *reinterpret_cast<uint4 *>(gout + y) = *reinterpret_cast<const uint4 *>(W + (y & kCWMask));
+        if (fin && b16 >= a && to > b16)  // (the last block: shared with the member after)
+            if (lane < to - b16) gout[b16 + lane] = W[(b16 + lane) & kCWMask];
+        fl = fin ? to : (b16 > a ? b16 : a);
+    };
+    const float lanef = (float)lane + 0.5f;
+    // A token of at most 64 bytes from within the window (all literals, nearly all matches) is one
+    // branch-free step: every lane reads its byte of the period-d pattern (a literal's lanes take
+    // its byte) and writes it at x + lane; the lanes past the length write ahead of the output,
+    // into slots of bytes long flushed and out of reach, which the next tokens rewrite before
+    // anything reads or flushes them.  Longer or further matches take the loop below.
+    uint32_t nxt = tk[1 + lane];
+    for (uint32_t tb = 0; tb < ntok; tb += 64) {
+        const uint32_t cur = nxt;
+        {
+            const uint32_t q = tb + 64 + lane;  // (the next group: a token slot's spare tail past the count)
+            nxt = tk[1 + (q < tok_cap - 1 ? q : tok_cap - 2)];
+        }
+        const uint32_t nt = ntok - tb < 64 ? ntok - tb : 64;
+        auto token = [&](uint32_t j) {
+            const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)j);
+            const uint32_t len = (t >> 16) & 511, dist = (t & 0x7FFF) + 1;
+            const float rd = __builtin_amdgcn_rcpf((float)dist);
+            if (!(t & kTSlow)) {
+                const uint32_t q = (uint32_t)(lanef * rd);
+                uint32_t v = W[(x - dist + lane - __mul24(q, dist)) & kCWMask];
+                v = (t & kTLit) ? t : v;
+                W[(x + lane) & kCWMask] = (uint8_t)v;
+            } else if (dist <= kCReach) {
+                for (uint32_t c = 0; c < len; c += 64) {
+                    const uint32_t q = (uint32_t)(((float)c + lanef) * rd);
+                    const uint8_t v = W[(x - dist + c + lane - __mul24(q, dist)) & kCWMask];
+                    W[(x + c + lane) & kCWMask] = v;
+                }
+            } else {
+                // from memory: [x - dist, x - dist + len) went out long ago (no period: dist > len)
+                __builtin_amdgcn_s_waitcnt(0);
+                for (uint32_t c = 0; c < len; c += 64) {
+                    const uint32_t p = x - dist + c + lane;
+                    const uint32_t w = __hip_atomic_load(reinterpret_cast<uint32_t *>(gout + (p & ~3u)), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    W[(x + c + lane) & kCWMask] = (uint8_t)(w >> (8 * (p & 3)));
+                }
+            }
+            x += len;
+        };
+        // four tokens a flush check (x moves at most 4 x 258 bytes between checks)
+        uint32_t j = 0;
+        for (; j + 4 <= nt; j += 4) {
+            token(j);
+            token(j + 1);
+            token(j + 2);
+            token(j + 3);
+            if (x - fl >= 2 * kCFlush) flush(x & ~(kCFlush - 1), false);
+        }
+        for (; j < nt; j++) token(j);
+        if (x - fl >= 2 * kCFlush) flush(x & ~(kCFlush - 1), false);
+    }
+    flush(xend, true);
+}
+
 // ---- CRC-32 (zlib's gzip trailer check) ----------------------------------------------------------
 // Per member (one wave): the output is cut at its end into 1 KiB segments, the first one partial;
 // lane j computes the raw CRC register of segment j (slice-by-4 tables in LDS; the first segment
@@ -708,16 +1221,53 @@ void crc32_zero1k_basis(Crc1k *z) {
 
 hipError_t launch_inflate(int which, const uint8_t *comp, const BgzfMember *mem, const uint64_t *out_off,
                           uint64_t n_members, uint8_t *out, uint32_t *mstat, unsigned long long *first_bad,
-                          const Crc1k &z1k, hipStream_t s, uint64_t mbase) {
-    // (mem, out_off, mstat: the arrays' entries for members mbase ..; first_bad: a global index)
+                          const Crc1k &z1k, hipStream_t s, uint64_t mbase, uint32_t *tok, uint64_t tok_members,
+                          const uint32_t *perm, hipStream_t aux, hipEvent_t ev_dec, hipEvent_t ev_fb) {
+    // (mem, out_off, mstat: the arrays' entries for members mbase ..; first_bad: a global index,
+    // followed by the 32-bit count of members the lane decoder handed to the wave decoder)
+    static const int lanes_env = [] {
+        const char *e = getenv("VCFX_INFLATE_LANES");  // 0: every member on the wave decoder (A/B)
+        return e && *e == '0' ? 0 : 1;
+    }();
+    const int lanes = lanes_env && tok && tok_members && perm;
+    uint32_t *const ndefer = reinterpret_cast<uint32_t *>(first_bad + 1);
+    // the wave decoder: every member, or the lane decoder's hand-overs (a grid of at most 4,096
+    // waves walks the members' verdicts; beside the last copy on `aux` when there is one)
+    auto wave = [&](hipStream_t st) -> hipError_t {
+        for (uint64_t m0 = 0; m0 < n_members; m0 += (1u << 30)) {
+            const uint64_t nm = n_members - m0 < (1u << 30) ? n_members - m0 : (1u << 30);
+            const unsigned g = lanes ? (unsigned)(nm < 4096 ? nm : 4096) : (unsigned)nm;
+            hipLaunchKernelGGL(k_inflate, dim3(g), dim3(64), 0, st, comp, mem + m0, out_off + m0, out, mstat + m0,
+                               first_bad, mbase + m0, (uint32_t)nm, lanes ? 0 : 1);
+            const hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
+    if (which == 0) {
+        if (!lanes) return wave(s);
+        // the lane decoder in pieces of at most tok_members (the token buffer's members)
+        const bool side = aux && ev_dec && ev_fb;
+        for (uint64_t b = 0; b < n_members; b += tok_members) {
+            const uint32_t nb = (uint32_t)(n_members - b < tok_members ? n_members - b : tok_members);
+            hipLaunchKernelGGL(k_inflate_decode, dim3((nb + 63) / 64), dim3(64), 0, s, comp, mem, out_off, out, mstat,
+                               ndefer, tok, kTokCap, perm + b, nb);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+            if (side && b + nb == n_members) {  // (every verdict known: the hand-overs beside the copy)
+                if ((e = hipEventRecord(ev_dec, s)) != hipSuccess || (e = hipStreamWaitEvent(aux, ev_dec, 0)) != hipSuccess ||
+                    (e = wave(aux)) != hipSuccess || (e = hipEventRecord(ev_fb, aux)) != hipSuccess)
+                    return e;
+            }
+            hipLaunchKernelGGL(k_inflate_copy, dim3(nb), dim3(64), 0, s, mem, out_off, out, tok, kTokCap, perm + b, nb);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        return side ? hipStreamWaitEvent(s, ev_fb, 0) : wave(s);
+    }
     for (uint64_t m0 = 0; m0 < n_members; m0 += (1u << 30)) {
         const uint64_t nm = n_members - m0 < (1u << 30) ? n_members - m0 : (1u << 30);
-        if (which == 0)
-            hipLaunchKernelGGL(k_inflate, dim3((unsigned)nm), dim3(64), 0, s, comp, mem + m0, out_off + m0, out,
-                               mstat + m0, first_bad, mbase + m0);
-        else
-            hipLaunchKernelGGL(k_crc32, dim3((unsigned)nm), dim3(64), 0, s, comp, mem + m0, out_off + m0, out, z1k,
-                               mstat + m0, first_bad, mbase + m0);
+        hipLaunchKernelGGL(k_crc32, dim3((unsigned)nm), dim3(64), 0, s, comp, mem + m0, out_off + m0, out, z1k,
+                           mstat + m0, first_bad, mbase + m0);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

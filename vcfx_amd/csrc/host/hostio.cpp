@@ -311,9 +311,10 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
             g_file_ring.busy = false;
         }
     } ring_release{!ring_.empty()};
-    // (the input buffer sized for ~24x the compressed bytes, a VCF's usual BGZF ratio, so the
-    // inflate batches launched during the stream have their room; more grows it at the end)
-    if (ring_.empty() || vcfxg_ingest_begin(g, 24 * total) != VCFXG_OK) {
+    // (the input buffer sized for ~24x the compressed bytes, a genotype VCF's BGZF ratio, so the
+    // inflate batches launched during the stream have their room; more grows it at the end.  When
+    // the device cannot hold that, 6x: the batches that do not fit wait for the end, E_CAP)
+    if (ring_.empty() || (vcfxg_ingest_begin(g, 24 * total) != VCFXG_OK && vcfxg_ingest_begin(g, 6 * total) != VCFXG_OK)) {
         munmap(hm, kHeadMax);
         return false;
     }

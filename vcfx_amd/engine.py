@@ -81,6 +81,7 @@ SIGNATURES = {
     "vcfxg_comm_destroy": (None, [_VP]),
     "vcfxg_comm_rccl_stats": (_I, [_VP, ctypes.POINTER(_U64), ctypes.POINTER(_U64)]),
     "vcfxg_last_schedule": (_P, [_VP]),
+    "vcfxg_bgzf_handed_over": (_U64, [_VP]),
     "vcfxg_count_byte": (_I, [_VP, _U64, _I, ctypes.POINTER(_U64)]),
     "vcfxg_haplotype_phaser": (_I, [_VP, _S, _I, ctypes.c_double, ctypes.c_uint32, ctypes.POINTER(Summary)]),
     "vcfxg_phaser_variants": (_I, [_VP, _VP, _VP, _VP]),
@@ -217,6 +218,10 @@ class Engine:
         self._chk(rc, "ingest_bgzf")
         self._chk(self.L.vcfxg_ingest(self.h, None, 0, 1), "ingest")
         return None
+
+    def bgzf_handed_over(self):
+        """members of the last load_bgzf the lane decoder handed to the wave decoder"""
+        return int(self.L.vcfxg_bgzf_handed_over(self.h))
 
     def input_bytes(self, offset, n):
         """bytes [offset, offset + n) of the loaded device input (vcfxg_input_fetch)"""
