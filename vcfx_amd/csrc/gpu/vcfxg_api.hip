@@ -635,11 +635,11 @@ int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, si
 // launch the inflate of members [first, first + count) of the staged stream: their table entries
 // and output offsets (from the running output count) to the device, k_inflate after the copies
 // staged so far
-// the token buffer of stream slot k (kBgzStreams: c->stream) for `count` members, at most 65,536 at
-// a time (1.6 GB: the bench shard's 65,834 members in one launch, all its copy waves resident at
-// once); 0 members when it cannot be had (every member then on the wave decoder)
+// the token buffer of stream slot k (kBgzStreams: c->stream) for `count` members, at most 69,632 at
+// a time (1.7 GB: the bench shard's 65,834 members in one launch); 0 members when it cannot be had
+// (every member then on the wave decoder)
 static uint64_t bgz_tokens(vcfxg_ctx *c, int k, uint64_t count, hipStream_t st) {
-    const uint64_t want = std::min<uint64_t>(count, 65536);
+    const uint64_t want = std::min<uint64_t>(count, 69632);
     const size_t bytes = (size_t)want * vcfxg::kTokCap * 4;
     DevBuf &b = c->bgz_tok[k];
     if (b.cap >= bytes) return want;
