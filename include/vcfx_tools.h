@@ -56,7 +56,8 @@ int vcfx_tool_main(const char *tool, int argc, char **argv, int in_fd, int out_f
  * ranks than devices share devices round robin. */
 int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, int in_fd, int out_fd, int err_fd, int ngpu);
 /* host-only plan of that run (no device): the ranks used (1 = unsharded), *kind 0 unsharded /
- * 1 record views / 2 LD rows, and for kind 1 the world + 1 cut offsets into cuts */
+ * 1 record views / 2 LD rows / 3 record views of a BGZF file, and for kinds 1 and 3 the world + 1
+ * cut offsets into cuts (kind 3: offsets into the inflated bytes, cuts[0] = the header's end) */
 int vcfx_shard_plan(const char *tool, int argc, char **argv, int ngpu, uint64_t *cuts, int *kind);
 /* `VCFX_record_filter --filter F --logic L [-i input] | VCFX_genotype_query -g Q [--strict] [-q]`
  * fused in one device pass (BASELINE config 3); input = NULL reads in_fd.  The return value is

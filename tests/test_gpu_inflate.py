@@ -346,13 +346,23 @@ TOOL_CASES = [
     ["VCFX_record_filter", "--filter", "QUAL>=30", "-i", "{F}"], ["VCFX_record_filter", "--filter", "POS>9420000"],
     ["VCFX_genotype_query", "-g", "0|1", "-i", "{F}"], ["VCFX_genotype_query", "-g", "1|1", "--strict"],
     ["VCFX_nonref_filter", "-i", "{F}"], ["VCFX_hwe_tester", "-i", "{F}"], ["VCFX_hwe_tester"],
+    ["VCFX_ld_calculator", "-w", "60", "-t", "0.2", "-i", "{F}"], ["VCFX_ld_calculator", "-w", "40", "-t", "0.1"],
+    ["VCFX_dosage_calculator", "-i", "{F}"], ["VCFX_dosage_calculator"],
+    ["VCFX_missing_detector", "-i", "{F}"], ["VCFX_missing_detector"],
+    ["VCFX_missing_detector", "-i", "{F}", "(no missing)"],  # the pre-scan's fast path: the input as it is
+    ["VCFX_allele_counter", "-i", "{F}"], ["VCFX_allele_counter", "-q", "-a", "-i", "{F}"], ["VCFX_allele_counter"],
+    ["VCFX_haplotype_phaser", "-i", "{F}"], ["VCFX_haplotype_phaser", "--streaming"],
 ]
 
 
 @pytest.mark.parametrize("argv", TOOL_CASES)
 def test_tools_on_device_bgzf(argv):
     oracle = Oracle()
-    buf = synth.generate(800, 400, 93, 1, 0.005, 0, 0.05, 1)
+    if argv[-1] == "(no missing)":
+        argv = argv[:-1]
+        buf = synth.generate(800, 400, 93, 1, 0.0, 0, 0.0, 0)
+    else:
+        buf = synth.generate(800, 400, 93, 1, 0.005, 0, 0.05, 1)
     d = tempfile.mkdtemp(prefix="vcfx_bgz_")
     plain, gz, log = os.path.join(d, "in.vcf"), os.path.join(d, "in.vcf.gz"), os.path.join(d, "sched.log")
     try:
@@ -371,7 +381,7 @@ def test_tools_on_device_bgzf(argv):
                 stdin.close()
         assert (r.stdout, r.returncode) == (want[0], want[2]), (argv, r.stderr[-500:])
         # (the file modes' "Processing F (size)" line names the .gz file and its own size)
-        keep = lambda e: [x for x in e.split(b"\n") if not x.startswith(b"Processing ")]
+        keep = lambda e: [x.replace(gz.encode(), plain.encode()) for x in e.split(b"\n") if not x.startswith(b"Processing ")]
         assert keep(r.stderr) == keep(want[1]), argv
         assert "bgzf_inflate" in open(log).read(), argv
     finally:
@@ -437,3 +447,70 @@ def test_af_streams_bgzf_through_the_ring(slot, batch):
         for x in os.listdir(d):
             os.unlink(os.path.join(d, x))
         os.rmdir(d)
+
+
+# ---- BGZF input split across ranks in its inflated bytes ------------------------------------------
+NGPU_CASES = [
+    ["VCFX_allele_freq_calc", "-i", "{F}"], ["VCFX_record_filter", "--filter", "QUAL>=30", "-i", "{F}"],
+    ["VCFX_genotype_query", "-g", "0|1", "-i", "{F}"], ["VCFX_nonref_filter", "-i", "{F}"],
+    ["VCFX_dosage_calculator", "-i", "{F}"], ["VCFX_hwe_tester", "-i", "{F}"], ["VCFX_missing_detector", "-i", "{F}"],
+    ["VCFX_allele_counter", "-q", "-a", "-i", "{F}"], ["VCFX_ld_calculator", "-w", "60", "-t", "0.2", "-i", "{F}"],
+]
+
+
+@pytest.fixture(scope="module")
+def bgz_pair():
+    buf = synth.generate(1200, 300, 95, 1, 0.005, 0, 0.05, 1)
+    d = tempfile.mkdtemp(prefix="vcfx_bgzn_")
+    plain, gz = os.path.join(d, "in.vcf"), os.path.join(d, "in.vcf.gz")
+    with open(plain, "wb") as f:
+        f.write(buf)
+    with open(gz, "wb") as f:
+        f.write(B.bgzf(buf, level=6))
+    yield plain, gz, buf
+    for x in os.listdir(d):
+        os.unlink(os.path.join(d, x))
+    os.rmdir(d)
+
+
+def _keep(e, gz, plain):
+    return [x.replace(gz.encode(), plain.encode()) for x in e.split(b"\n") if not x.startswith(b"Processing ")]
+
+
+@pytest.mark.parametrize("argv", NGPU_CASES)
+def test_ngpu_ranks_on_bgzf(argv, bgz_pair):
+    """VCFX_NGPU=3 on a BGZF file (three rank contexts on the one GPU, round robin): the member
+    chain cut in the inflated bytes (vcfx_shard_plan kind 3; LD: rows, every rank inflating the
+    whole file), each rank inflating its members on its device; the reference's output on the
+    plain bytes"""
+    from vcfx_amd import tools
+    plain, gz, _ = bgz_pair
+    w, kind, _ = tools.shard_plan([a.replace("{F}", gz) for a in argv], 3)
+    assert w == 3 and kind == (2 if argv[0] == "VCFX_ld_calculator" else 3), (argv, w, kind)
+    want = Oracle().run([a.replace("{F}", plain) for a in argv], b"")
+    env = dict(os.environ, VCFX_NGPU="3", VCFX_BGZF_DEVICE_MIN="0")
+    r = subprocess.run([tool_binary(argv[0])] + [a.replace("{F}", gz) for a in argv[1:]], capture_output=True, env=env,
+                       timeout=120)
+    assert (r.stdout, r.returncode) == (want[0], want[2]), (argv, r.stderr[-500:])
+    assert _keep(r.stderr, gz, plain) == _keep(want[1], gz, plain), argv
+
+
+@pytest.mark.parametrize("tool", ["VCFX_allele_freq_calc", "VCFX_record_filter"])
+def test_env_bgzf_views(tool, bgz_pair):
+    """the per-process form vcfx_amd/shard.py uses (VCFX_INPUT_VIEW="bgzf:H:LO:HI" +
+    VCFX_VIEW_SKIP_HEADER on ranks > 0): the views' outputs in rank order are the whole run's"""
+    from vcfx_amd import shard
+    plain, gz, _ = bgz_pair
+    argv = [tool] + (["--filter", "QUAL>=30"] if tool == "VCFX_record_filter" else ["-q"]) + ["-i", gz]
+    cuts = shard.bgzf_cuts(argv, 4)
+    assert cuts is not None
+    want = Oracle().run([plain if a == gz else a for a in argv], b"")
+    out = b""
+    for r in range(4):
+        env = dict(os.environ, VCFX_INPUT_VIEW="bgzf:%d:%d:%d" % (cuts[0], cuts[r], cuts[r + 1]))
+        if r:
+            env["VCFX_VIEW_SKIP_HEADER"] = "1"
+        p = subprocess.run([tool_binary(tool)] + argv[1:], capture_output=True, env=env, timeout=120)
+        assert p.returncode == 0, p.stderr[-500:]
+        out += p.stdout
+    assert out == want[0]

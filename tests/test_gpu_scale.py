@@ -213,17 +213,32 @@ def test_pipeline_general_shards_match_reference(inputs, case, inp):
     inputs.drop(inp)
 
 
-@pytest.mark.parametrize("case", ["af_file", "pipeline_bench", "hwe_file"])
-def test_bgzf_chr21_matches_reference(inputs, case):
-    """the same shard as BGZF (.vcf.gz, made by build/bin/vcfx_bgzf): inflated on the host
-    threads, then the device path; output identical to the reference's on the plain bytes"""
+@pytest.mark.parametrize("case,how", [("af_file", "none"), ("af_file", "ngpu8"), ("af_stdin", "pipe"),
+                                      ("pipeline_bench", "none"), ("pipeline_bench", "ngpu8"), ("hwe_file", "none"),
+                                      ("nonref_file", "none"), ("dose_file", "none"), ("md_file", "none"),
+                                      ("md_file", "ngpu8"), ("ac_agg_file", "none"), ("ph_file", "none"),
+                                      ("ld20k_bench", "none"), ("ld20k_bench", "ngpu8")])
+def test_bgzf_chr21_matches_reference(inputs, case, how):
+    """the same shard as BGZF (.vcf.gz, made by build/bin/vcfx_bgzf at level 1): inflated on the
+    device (the lane decoder + copy kernels; AF's file form streamed through the pinned file ring,
+    a pipe read whole first), then the tool's device path; with VCFX_NGPU=8
+    each of the eight rank contexts inflates the members of its share of the inflated bytes (LD:
+    every rank the whole file, for its share of the pair rows).  Output identical to the
+    reference's on the plain bytes."""
     from vcfx_amd import BUILD
-    plain = inputs.path("chr21")
+    if case not in DIG["cases"]:
+        pytest.skip("no reference digest for %s" % case)
+    c = DIG["cases"][case]
+    plain = inputs.path(c["input"])
     bgz = plain + ".bgz"
     if not os.path.exists(bgz):
         subprocess.check_call([os.path.join(BUILD, "bin", "vcfx_bgzf"), plain, bgz, "16", "1"])
-    c = DIG["cases"][case]
-    got, rc, err = _hash_cmd(_cmd(c["stages"], bgz))
+    cmd = _cmd(c["stages"], bgz)
+    if how == "ngpu8":
+        cmd = "VCFX_NGPU=8 " + cmd
+    elif how == "pipe":
+        cmd = "cat '%s' | %s" % (bgz, cmd)
+    got, rc, err = _hash_cmd(cmd)
     assert rc == 0, err[-2000:]
     assert got == c["stdout"], (case, got, err[-2000:])
 

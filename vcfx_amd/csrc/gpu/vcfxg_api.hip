@@ -173,8 +173,9 @@ struct vcfxg_ctx {
     // device BGZF inflate (vcfxg_ingest_bgzf): compressed bytes, member table, output offsets,
     // per-member status, first bad member
     DevBuf bgz_in, bgz_mem, bgz_off, bgz_stat, bgz_small, bgz_perm;
-    // the lane decoder's token buffers: one per inflate stream and one for `stream`; the stream the
-    // wave decoder takes the lane decoder's hand-overs on (beside the copy), and its events
+    // the lane decoder's token buffers (and hand-over lists): one per inflate stream and one for
+    // `stream`; the stream the wave decoder takes the lane decoder's hand-overs on (beside the
+    // copy), and its events
     DevBuf bgz_tok[kBgzStreams + 1];
     hipStream_t bgz_aux = nullptr;
     hipEvent_t bgz_aux_ev[2] = {};
@@ -603,7 +604,7 @@ int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, si
         // (the first-bad marker and the hand-over count, then the stream's earlier work -- buffers
         // just reallocated, the last call's kernels: every batch is ordered after this event)
         HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
-        HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_small) + 8, 0, 8, c->stream));
+        HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_small) + 8, 0, 56, c->stream));
         HIPCHK(c, hipEventRecord(c->bgz_copy_ev, c->stream));
         HIPCHK(c, hipStreamWaitEvent(c->copy_stream, c->bgz_copy_ev, 0));
         c->bgz_total = comp_total;
@@ -635,27 +636,29 @@ int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, si
 // launch the inflate of members [first, first + count) of the staged stream: their table entries
 // and output offsets (from the running output count) to the device, k_inflate after the copies
 // staged so far
-// the token buffer of stream slot k (kBgzStreams: c->stream) for `count` members, at most 69,632 at
-// a time (1.7 GB: the bench shard's 65,834 members in one launch); 0 members when it cannot be had
-// (every member then on the wave decoder)
+// the token buffer of stream slot k (kBgzStreams: c->stream) for `count` members: at most 69,632 at
+// a time (2.3 GB: the bench shard's 65,834 members in one launch), fewer when the device cannot
+// spare that (down to 4,096; launches of more members run in pieces); 0 members when even that
+// cannot be had (every member then on the wave decoder)
 static uint64_t bgz_tokens(vcfxg_ctx *c, int k, uint64_t count, hipStream_t st) {
-    const uint64_t want = std::min<uint64_t>(count, 69632);
-    const size_t bytes = (size_t)want * vcfxg::kTokCap * 4;
     DevBuf &b = c->bgz_tok[k];
-    if (b.cap >= bytes) return want;
-    if (b.p) {  // (the stream's earlier batches may still read it)
-        if (hipStreamSynchronize(st) != hipSuccess) return 0;
-        (void)hipFree(b.p);
-        b.p = nullptr;
-        b.cap = 0;
-    }
-    if (hipMalloc(&b.p, bytes) != hipSuccess) {
+    const size_t per = (size_t)vcfxg::kTokCap * 4 + 4;  // (the tokens, and a hand-over list entry)
+    for (uint64_t want = std::min<uint64_t>(count, 69632);; want /= 2) {
+        if (b.cap >= want * per + 4) return want;
+        if (b.p) {  // (the stream's earlier batches may still read it)
+            if (hipStreamSynchronize(st) != hipSuccess) return 0;
+            (void)hipFree(b.p);
+            b.p = nullptr;
+            b.cap = 0;
+        }
+        if (hipMalloc(&b.p, want * per + 4) == hipSuccess) {
+            b.cap = want * per + 4;
+            return want;
+        }
         (void)hipGetLastError();
         b.p = nullptr;
-        return 0;
+        if (want <= 4096) return 0;
     }
-    b.cap = bytes;
-    return want;
 }
 
 // the lane decoder's member order for `count` members: largest compressed first (a counting sort
@@ -804,7 +807,7 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
             HIPCHK(c, hipMemcpyAsync(c->bgz_off.p, off.data(), 8 * nm, hipMemcpyHostToDevice, c->stream));
         }
         HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
-        HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_small) + 8, 0, 8, c->stream));
+        HIPCHK(c, hipMemsetAsync(P<uint8_t>(c->bgz_small) + 8, 0, 56, c->stream));
         prof_end(c, "bgzf_h2d");
         const uint64_t tm = bgz_tokens(c, vcfxg_ctx::kBgzStreams, nm, c->stream);
         if (int ra = bgz_aux(c)) return ra;
@@ -823,16 +826,23 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
                                     nm, P<uint8_t>(c->input) + c->n, P<uint32_t>(c->bgz_stat),
                                     P<unsigned long long>(c->bgz_small), z1k, c->stream));
     prof_end(c, "bgzf_crc32");
-    static thread_local uint64_t small[2];  // the first bad member, the hand-over count
+    // the first bad member, the hand-over count and its reasons (32-bit words 3..14)
+    static thread_local uint64_t small[8];
     static thread_local uint8_t lastb;
     uint64_t &bad = small[0];
-    HIPCHK(c, hipMemcpyAsync(small, c->bgz_small.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(small, c->bgz_small.p, 64, hipMemcpyDeviceToHost, c->stream));
     if (tot) HIPCHK(c, hipMemcpyAsync(&lastb, P<uint8_t>(c->input) + c->n + tot - 1, 1, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
     c->bgz_total = c->bgz_staged = 0;
     c->bgz_launched = c->bgz_out = 0;
     c->bgz_handed = (uint32_t)small[1];
+    if (c->bgz_handed && getenv("VCFX_BGZF_DIAG")) {  // (why the lane decoder handed members over)
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(small) + 2;
+        fprintf(stderr, "vcfxg: BGZF members handed to the wave decoder: %u (by reason 1-12:", w[0]);
+        for (int k = 1; k <= 12; k++) fprintf(stderr, " %u", w[k]);
+        fprintf(stderr, ")\n");
+    }
     if (bad != ~0ull) {
         uint32_t why = 0;
         (void)hipMemcpy(&why, P<uint32_t>(c->bgz_stat) + bad, 4, hipMemcpyDeviceToHost);

@@ -246,6 +246,8 @@ __device__ __forceinline__ uint32_t slow_decode(InfLds &S, int k, uint32_t p, ui
 
 // the lane decoder's verdict for a member it hands to the wave decoder (mstat)
 constexpr uint32_t kDefer = 0xFFFFu;
+// the lane decoder's token count of a member it hands over
+constexpr uint32_t kTokNone = 0xFFFFFFFFu;
 
 // One member inflated by the whole wave (the wave decoder): every member the lane decoder below
 // hands over (kDefer), which includes every member that zlib would refuse.
@@ -599,18 +601,33 @@ __device__ __forceinline__ void inflate_wave(InfLds &S, const uint8_t *__restric
     }
 }
 
-// the wave decoder over the members the lane decoder handed over (a grid-stride loop: the count
-// is known only on the device)
+// The members the lane decoder handed over (2.6 in 10,000 on the bench shard: a code whose tables
+// pass the lane's slice, a stored or fixed block, damage): the wave decoder, one member per wave,
+// from the list the lane decoder appends them to (hlist[0] their count, then their token slots),
+// on a second stream beside the copy, its waves at raised priority.  (A scan of the token slots
+// for them, one wave per 256 slots, serialised the members that sort together: 15 ms.)
+constexpr uint32_t kHandGrid = 256;
+__global__ void __launch_bounds__(64) k_inflate_handover(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
+                                                         const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
+                                                         uint32_t *__restrict__ mstat, unsigned long long *__restrict__ first_bad,
+                                                         uint64_t mbase, const uint32_t *__restrict__ perm,
+                                                         const uint32_t *__restrict__ hlist) {
+    __shared__ InfLds S;
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t cnt = uni(hlist[0]);
+    for (uint32_t k = blockIdx.x; k < cnt; k += gridDim.x) {
+        __syncthreads();  // (the previous member's last reads of S)
+        inflate_wave(S, comp, mem, out_off, out, mstat, first_bad, mbase, uni(perm[uni(hlist[1 + k])]));
+    }
+}
+
+// the wave decoder over every member, one per wave (VCFX_INFLATE_LANES=0: the A/B baseline)
 __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem,
                                                 const uint64_t *__restrict__ out_off, uint8_t *__restrict__ out,
                                                 uint32_t *__restrict__ mstat, unsigned long long *__restrict__ first_bad,
-                                                uint64_t mbase, uint32_t n, int all) {
+                                                uint64_t mbase) {
     __shared__ InfLds S;
-    for (uint32_t m = blockIdx.x; m < n; m += gridDim.x) {
-        if (!all && uni(mstat[m]) != kDefer) continue;
-        __syncthreads();  // (the previous member's last reads of S)
-        inflate_wave(S, comp, mem, out_off, out, mstat, first_bad, mbase, m);
-    }
+    inflate_wave(S, comp, mem, out_off, out, mstat, first_bad, mbase, blockIdx.x);
 }
 
 // ---- the lane decoder: one member per lane -------------------------------------------------------
@@ -620,7 +637,8 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
 //   k_inflate_decode: the Huffman decode of a member per lane, to a token list per member (a
 //     literal byte, or a match's length and distance: 4 B each, in a per-launch token buffer).  The
 //     tables live in the lane's own 848-byte slice of LDS (three waves per CU): a 2^7-entry
-//     literal/length root table and a 2^6-entry distance root table of 16-bit entries, with zlib's
+//     literal/length root table and a 2^6-entry distance root table of 16-bit entries (fewer root
+//     bits when the tables would not fit), with zlib's
 //     sub-tables (inftrees.c: a root entry points to a table indexed by the bits past the root) for
 //     longer codes, built per lane from the code lengths (which the header decode writes into the
 //     token slot's spare tail).  The stream comes through a 64-byte LDS window per lane: a symbol's
@@ -640,8 +658,6 @@ __global__ void __launch_bounds__(64) k_inflate(const uint8_t *__restrict__ comp
 // member.
 constexpr int kLT = 424;         // 16-bit table entries per lane (848 B: 3 waves per CU in 160 KiB)
 constexpr int kCtr = kLT - 32;   // the builder's 16 32-bit counters at the slice's tail
-constexpr uint32_t kLitR = 7, kDistR = 6;
-constexpr uint32_t kTokNone = 0xFFFFFFFFu;  // a member's token count: handed over
 // the copy's window (k_inflate_copy): 8 KiB of LDS per wave; a match from further back than
 // kCReach, or longer than 64 bytes, takes its slow path
 constexpr uint32_t kCW = 8192, kCWMask = kCW - 1;
@@ -666,7 +682,8 @@ __device__ __forceinline__ uint4 ld16(const uint8_t *p) {
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict__ mem, const uint64_t *__restrict__ out_off,
                  uint8_t *__restrict__ out, uint32_t *__restrict__ mstat, uint32_t *__restrict__ ndefer,
-                 uint32_t *__restrict__ tok, uint32_t tok_cap, const uint32_t *__restrict__ perm, uint32_t n_lanes) {
+                 uint32_t *__restrict__ tok, uint32_t tok_cap, const uint32_t *__restrict__ perm, uint32_t n_lanes,
+                 uint32_t *__restrict__ hlist) {
     __shared__ __attribute__((aligned(16))) uint16_t T[64 * kLT];
     const uint32_t lane = threadIdx.x;
     const uint32_t i = blockIdx.x * 64 + lane;  // the lane's slot; its member perm[i]
@@ -687,10 +704,13 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
     if (plen < 2 || olen > 65536) {
         tk[0] = kTokNone;
         mstat[m] = kDefer;
+        hlist[1 + atomicAdd(hlist, 1u)] = i;
         atomicAdd(ndefer, 1u);
+        atomicAdd(ndefer + 1, 1u);
         return;
     }
     bool bad = false;
+    uint32_t why = 0;  // the first refusal (a diagnostic: ndefer[1 + why - 1] counts them)
     // The bit reader: bpos = the next stream bit, counted from qp (the stream's first byte rounded
     // down to a dword; the first sh bits are not the stream's).  The window holds stream dwords
     // [wb, wb + 16) in LDS: a symbol's 64 bits are one ds_read2 + ds_read and two funnel shifts.
@@ -766,7 +786,7 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
             first[L] = code;
         }
         uint32_t size = 1u << R;
-        if (base + size > (uint32_t)kCtr) return -1;
+        if (base + size > (uint32_t)kCtr) return -2;
         if (maxl > R) {
             // zlib's sub-tables, from the counts alone: the long codes in canonical order fill one
             // root prefix after another; a prefix's table has the fewest index bits its codes fill
@@ -786,7 +806,8 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
                     curr++;
                     lf <<= 1;
                 }
-                if (base + size + (1u << curr) > (uint32_t)kCtr || p >= (1u << R)) return -1;
+                if (p >= (1u << R)) return -1;
+                if (base + size + (1u << curr) > (uint32_t)kCtr) return -2;
                 T[lt + base + brev_n(p, R)] = (uint16_t)((base + size) | (curr << 9) | (kKPtr << 14));
                 size += 1u << curr;
                 uint32_t space = 1u << curr;
@@ -842,6 +863,7 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
     uint32_t st = 0;      // 0 block header next, 1 in a block, 2 after the last block
     bool last = false;
     uint32_t dbase = 0;   // the distance table's offset in the slice
+    constexpr uint32_t kLR = 7, kDR = 6;  // the root bits of the two tables
     // A block header: the code lengths into lp (the code-length code's at lp[320, 339)), then the
     // tables; the window follows the reads.  Any refusal sets bad.
     auto header = [&]() {
@@ -851,13 +873,13 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
         last = lo & 1;
         const uint32_t bt = (lo >> 1) & 3;
         if (bt != 2) {
-            bad = true;
+            bad = true, why = why ? why : 2u;
             return;
         }
         const uint32_t nlen = ((lo >> 3) & 31) + 257, ndist = ((lo >> 8) & 31) + 1, ncl = ((lo >> 13) & 15) + 4;
         bpos += 17;
         if (nlen > 286 || ndist > 30) {
-            bad = true;
+            bad = true, why = why ? why : 3u;
             return;
         }
         const uint4 z = make_uint4(0, 0, 0, 0);
@@ -868,7 +890,7 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
         for (uint32_t i = 0; i < ncl; i++) lp[320 + c_clorder[i]] = (uint8_t)((cl >> (3 * i)) & 7);
         bpos += 3 * ncl;
         if (bad || build(0, lp + 320, 19, 7, 1) < 0) {
-            bad = true;
+            bad = true, why = why ? why : 4u;
             return;
         }
         sync_window();  // (the counters took the window's place)
@@ -889,7 +911,7 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
                 rep = 3 + __builtin_amdgcn_ubfe(lo, L, 2);
                 bpos += L + 2;
                 val = prev;
-                if (n == 0) bad = true;
+                if (n == 0) bad = true, why = why ? why : 5u;
             } else if (sym == 17) {
                 rep = 3 + __builtin_amdgcn_ubfe(lo, L, 3);
                 bpos += L + 3;
@@ -897,25 +919,25 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
                 rep = 11 + __builtin_amdgcn_ubfe(lo, L, 7);
                 bpos += L + 7;
             }
-            if (n + rep > tot) bad = true;
+            if (n + rep > tot) bad = true, why = why ? why : 5u;
             if (bad) break;
             for (uint32_t i = 0; i < rep; i++) lp[n + i] = (uint8_t)val;
             n += rep;
             prev = val;
         }
         if (bad || lp[256] == 0) {  // (no end-of-block code)
-            bad = true;
+            bad = true, why = why ? why : 6u;
             return;
         }
         // (one loop for the two codes: one copy of the builder in the code)
         int used = 0;
 #pragma nounroll
         for (int j = 0; j < 2 && used >= 0; j++) {
-            const int r = build(j ? (uint32_t)used : 0u, j ? lp + nlen : lp, j ? ndist : nlen, j ? kDistR : kLitR, j);
+            const int r = build(j ? (uint32_t)used : 0u, j ? lp + nlen : lp, j ? ndist : nlen, j ? kDR : kLR, j);
             if (j == 0) dbase = (uint32_t)r;
             used = r;
         }
-        if (used < 0) bad = true;
+        if (used < 0) bad = true, why = why ? why : 7u;
         st = 1;
         // the window from here, and the next trip's from here too
         sync_window();
@@ -948,12 +970,12 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
             if (!bad && st == 1) {
                 uint32_t lo, hi;
                 read64(lo, hi);
-                const uint32_t e = look(0, kLitR, lo);
+                const uint32_t e = look(0, kLR, lo);
                 const uint32_t L = e & 15, kind = e >> 14;
                 uint32_t t = 0;
                 if (kind == kKLit) {
                     bpos += L;
-                    if (xd >= olen) bad = true;
+                    if (xd >= olen) bad = true, why = why ? why : 8u;
                     t = kTLit | (1u << 16) | ((e >> 4) & 255);
                     xd++;
                 } else if (kind == kKLen) {
@@ -967,13 +989,13 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
                     const uint32_t len = base + __builtin_amdgcn_ubfe(lo, L, ext);
                     const uint32_t s1 = L + ext;
                     const uint32_t db = __builtin_amdgcn_alignbit(hi, lo, s1);
-                    const uint32_t d = look(dbase, kDistR, db);
+                    const uint32_t d = look(dbase, kDR, db);
                     const uint32_t dl = d & 15, ds = (d >> 4) & 31;
                     const uint32_t dext = ds < 4 ? 0 : (ds >> 1) - 1;
                     const uint32_t dbs = ds < 4 ? ds + 1 : ((2u | (ds & 1)) << dext) + 1;
                     const uint32_t dist = dbs + __builtin_amdgcn_ubfe(db, dl, dext);
                     bpos += s1 + dl + dext;
-                    if (dist > xd || xd + len > olen) bad = true;
+                    if (dist > xd || xd + len > olen) bad = true, why = why ? why : 8u;
                     t = (len << 16) | (dist - 1) | (len > 64 || dist > kCReach ? kTSlow : 0u);
                     xd += len;
                 } else {  // end of block
@@ -987,7 +1009,7 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
                     tg.w = pc == 3 ? t : tg.w;
                     pc++;
                 }
-                if (bpos > bend + 64) bad = true;  // (ran past the stream)
+                if (bpos > bend + 64) bad = true, why = why ? why : 9u;  // (ran past the stream)
             }
             if (!bad && st == 0) header();  // (the first block's, or a block after it)
         }
@@ -995,12 +1017,16 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
         const uint32_t at = ti <= tmax ? ti : tmax;
         __builtin_memcpy(tk + 1 + at, &tg, 16);
         ti += pc;
-        if (ti > tmax) bad = true;
+        if (ti > tmax) bad = true, why = why ? why : 10u;
     }
-    if (!bad && (((bpos - sh) + 7) >> 3 != (uint32_t)plen || xd != olen)) bad = true;
+    if (!bad && (((bpos - sh) + 7) >> 3 != (uint32_t)plen || xd != olen)) bad = true, why = why ? why : 11u;
     tk[0] = bad ? kTokNone : ti;
     mstat[m] = bad ? kDefer : 0u;
-    if (bad) atomicAdd(ndefer, 1u);
+    if (bad) {
+        hlist[1 + atomicAdd(hlist, 1u)] = i;
+        atomicAdd(ndefer, 1u);
+        atomicAdd(ndefer + (why ? why : 12u), 1u);
+    }
 }
 
 // k_inflate_copy: the LZ77 copy of the decoded tokens, one member per wave.  The lane decoder's
@@ -1016,7 +1042,6 @@ k_inflate_decode(const uint8_t *__restrict__ comp, const BgzfMember *__restrict_
 //     the member's output in memory, already written (every store of the wave waited for, the
 //     dwords read at agent scope: from L2, never an older L1 line).
 // Eight KiB of LDS a wave: 20 waves on a CU hide each other's LDS round trips.
-
 __global__ void __launch_bounds__(64) k_inflate_copy(const BgzfMember *__restrict__ mem, const uint64_t *__restrict__ out_off,
                                                      uint8_t *__restrict__ out, const uint32_t *__restrict__ tok,
                                                      uint32_t tok_cap, const uint32_t *__restrict__ perm, uint32_t n_lanes) {
@@ -1026,7 +1051,7 @@ __global__ void __launch_bounds__(64) k_inflate_copy(const BgzfMember *__restric
     if (i >= n_lanes) return;
     const uint32_t *const tk = tok + (size_t)i * tok_cap;
     const uint32_t ntok = uni(tk[0]);
-    if (ntok == kTokNone) return;  // (the wave decoder's)
+    if (ntok == kTokNone) return;  // (handed over: k_inflate_handover's)
     const uint32_t m = uni(perm[i]);
     uint8_t *const ob = out + out_off[m];
     const uint32_t olen = uni(mem[m].out_len);
@@ -1229,40 +1254,39 @@ hipError_t launch_inflate(int which, const uint8_t *comp, const BgzfMember *mem,
         const char *e = getenv("VCFX_INFLATE_LANES");  // 0: every member on the wave decoder (A/B)
         return e && *e == '0' ? 0 : 1;
     }();
-    const int lanes = lanes_env && tok && tok_members && perm;
+    const int lanes = lanes_env && tok && tok_members && perm && aux && ev_dec && ev_fb;
     uint32_t *const ndefer = reinterpret_cast<uint32_t *>(first_bad + 1);
-    // the wave decoder: every member, or the lane decoder's hand-overs (a grid of at most 4,096
-    // waves walks the members' verdicts; beside the last copy on `aux` when there is one)
-    auto wave = [&](hipStream_t st) -> hipError_t {
+    if (which == 0 && !lanes) {
         for (uint64_t m0 = 0; m0 < n_members; m0 += (1u << 30)) {
             const uint64_t nm = n_members - m0 < (1u << 30) ? n_members - m0 : (1u << 30);
-            const unsigned g = lanes ? (unsigned)(nm < 4096 ? nm : 4096) : (unsigned)nm;
-            hipLaunchKernelGGL(k_inflate, dim3(g), dim3(64), 0, st, comp, mem + m0, out_off + m0, out, mstat + m0,
-                               first_bad, mbase + m0, (uint32_t)nm, lanes ? 0 : 1);
+            hipLaunchKernelGGL(k_inflate, dim3((unsigned)nm), dim3(64), 0, s, comp, mem + m0, out_off + m0, out,
+                               mstat + m0, first_bad, mbase + m0);
             const hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
-    };
+    }
     if (which == 0) {
-        if (!lanes) return wave(s);
-        // the lane decoder in pieces of at most tok_members (the token buffer's members)
-        const bool side = aux && ev_dec && ev_fb;
+        // the lane decoder, then its hand-overs on `aux` beside the copy on `s`, in pieces of at
+        // most tok_members (the token buffer's members; its hand-over list follows the tokens)
+        uint32_t *const hlist = tok + (size_t)tok_members * kTokCap;
         for (uint64_t b = 0; b < n_members; b += tok_members) {
             const uint32_t nb = (uint32_t)(n_members - b < tok_members ? n_members - b : tok_members);
+            hipError_t e;
+            if (b && (e = hipStreamWaitEvent(s, ev_fb, 0)) != hipSuccess) return e;  // (the list is reused)
+            if ((e = hipMemsetAsync(hlist, 0, 4, s)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_inflate_decode, dim3((nb + 63) / 64), dim3(64), 0, s, comp, mem, out_off, out, mstat,
-                               ndefer, tok, kTokCap, perm + b, nb);
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
-            if (side && b + nb == n_members) {  // (every verdict known: the hand-overs beside the copy)
-                if ((e = hipEventRecord(ev_dec, s)) != hipSuccess || (e = hipStreamWaitEvent(aux, ev_dec, 0)) != hipSuccess ||
-                    (e = wave(aux)) != hipSuccess || (e = hipEventRecord(ev_fb, aux)) != hipSuccess)
-                    return e;
-            }
+                               ndefer, tok, kTokCap, perm + b, nb, hlist);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = hipEventRecord(ev_dec, s)) != hipSuccess || (e = hipStreamWaitEvent(aux, ev_dec, 0)) != hipSuccess)
+                return e;
+            hipLaunchKernelGGL(k_inflate_handover, dim3(kHandGrid), dim3(64), 0, aux, comp, mem, out_off, out, mstat,
+                               first_bad, mbase, perm + b, hlist);
+            if ((e = hipGetLastError()) != hipSuccess || (e = hipEventRecord(ev_fb, aux)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_inflate_copy, dim3(nb), dim3(64), 0, s, mem, out_off, out, tok, kTokCap, perm + b, nb);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        return side ? hipStreamWaitEvent(s, ev_fb, 0) : wave(s);
+        return hipStreamWaitEvent(s, ev_fb, 0);
     }
     for (uint64_t m0 = 0; m0 < n_members; m0 += (1u << 30)) {
         const uint64_t nm = n_members - m0 < (1u << 30) ? n_members - m0 : (1u << 30);

@@ -650,6 +650,24 @@ bool Input::decompress(int err_fd) {
     }
     if (!gzip_ok || gz || host_n != n || !is_gzip(p, n) || !gzip_enabled()) return true;
     join_populate();
+    if (t_shard && t_shard->bgz)
+        return bgzf_view(err_fd, *t_shard->bgz, t_shard->h, t_shard->lo, t_shard->hi,
+                         "rank " + std::to_string(t_shard->rank));
+    unsigned long long vh = 0, vlo = 0, vhi = 0;
+    const char *v = t_shard ? nullptr : getenv("VCFX_INPUT_VIEW");
+    if (v && sscanf(v, "bgzf:%llu:%llu:%llu", &vh, &vlo, &vhi) == 3) {
+        BgzfShard B;
+        uint64_t tot = 0;
+        if (!bgzf_chain(p, n, B.ms, &tot)) {
+            write_str(err_fd, "Error: vcfx_amd: VCFX_INPUT_VIEW=bgzf:...: the input is not a BGZF member chain\n");
+            return false;
+        }
+        B.comp = p;
+        B.comp_n = n;
+        B.off.assign(B.ms.size() + 1, 0);
+        for (size_t i = 0; i < B.ms.size(); i++) B.off[i + 1] = B.off[i] + B.ms[i].olen;
+        return bgzf_view(err_fd, B, vh, vlo, vhi, "view");
+    }
     if (bgzf_device && device_bgzf()) return true;
     size_t cap = 0;
     void *m = reserve_region(&cap);
@@ -683,7 +701,9 @@ bool Input::decompress(int err_fd) {
 
 bool Input::device_bgzf() {
     const char *e = getenv("VCFX_BGZF_DEVICE");
-    if ((e && e[0] == '0') || t_shard) return false;
+    // (a rank of a multi-GPU run: only one that takes the whole file, VCFX_ld_calculator's rows)
+    const bool view = t_shard && !(t_shard->h == 0 && t_shard->lo == 0 && t_shard->hi == n);
+    if ((e && e[0] == '0') || view) return false;
     const char *em = getenv("VCFX_BGZF_DEVICE_MIN");
     const uint64_t min_out = em && *em ? strtoull(em, nullptr, 10) : (uint64_t)64 << 20;
     // the member chain (its headers touch every page of the mapping: fault them in first)
@@ -696,14 +716,15 @@ bool Input::device_bgzf() {
     if (!bgzf_chain(p, n, ms, &total) || total < min_out) return false;
     phase("bgzf chain");
     // the head: members inflated here, in order, until the output holds the complete '#CHROM'
-    // line (the host's gate and the tools' header output run on it); at most 64 MiB
-    const size_t kHeadMax = std::min<uint64_t>(total, (uint64_t)64 << 20) + 65536;
+    // line and 64 KiB after it (the host's gate and the tools' header scans run on it: a scan
+    // that ends in the head sees the first record line start); at most 64 MiB
+    const size_t kHeadMax = std::min<uint64_t>(total, (uint64_t)64 << 20) + 3 * 65536;
     void *hm = mmap(nullptr, kHeadMax, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (hm == MAP_FAILED) return false;
     char *head = (char *)hm;
-    size_t hn = 0, scanned = 0;
+    size_t hn = 0, scanned = 0, chrom_end = 0;
     bool chrom = false;
-    for (size_t i = 0; i < ms.size() && !chrom; i++) {
+    for (size_t i = 0; i < ms.size() && !(chrom && hn - chrom_end >= 65536); i++) {
         if (hn + ms[i].olen > kHeadMax) break;
         size_t got = 0;
         if (!gz_inflate_member(p + ms[i].off, ms[i].len, head + hn, ms[i].olen, &got) || got != ms[i].olen) break;
@@ -714,6 +735,7 @@ bool Input::device_bgzf() {
             if (!nl) break;
             chrom = is_chrom_line(s0, (size_t)(nl - s0));
             scanned = (size_t)(nl - head) + 1;
+            if (chrom) chrom_end = scanned;
         }
     }
     vcfxg_ctx *g = chrom ? gpu_quiet() : nullptr;
@@ -742,6 +764,70 @@ bool Input::device_bgzf() {
 }
 
 thread_local ShardRank *t_shard = nullptr;
+
+bool Input::bgzf_view(int err_fd, const BgzfShard &B, uint64_t H, uint64_t lo, uint64_t hi, const std::string &who) {
+    const size_t nm = B.ms.size();
+    vcfxg_ctx *g = gpu(err_fd);
+    if (!g) return false;
+    auto fail = [&](const std::string &what) {
+        write_str(err_fd, "Error: vcfx_amd: " + who + ": the BGZF input: " + what + "\n");
+        return false;
+    };
+    if (H > lo || lo >= hi || hi > B.off[nm]) return fail("bad view");
+    // host memory: the head members' output (the header, then up to a member past it), and the two
+    // cut members' output
+    const size_t kM = 65536;
+    size_t hm_n = 0;
+    while (hm_n < nm && B.off[hm_n] < H) hm_n++;  // members [0, hm_n) hold the header
+    const size_t head_cap = (size_t)B.off[hm_n] + kM, len = head_cap + 2 * kM;
+    void *m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) return fail("no host memory");
+    char *head = (char *)m, *fa = head + head_cap, *fb = fa + kM;
+    auto inflate = [&](size_t i, char *dst) {
+        size_t got = 0;
+        return gz_inflate_member(B.comp + B.ms[i].off, B.ms[i].len, dst, kM, &got) && got == B.ms[i].olen;
+    };
+    bool ok = true;
+    for (size_t i = 0; i < hm_n && ok; i++) ok = inflate(i, head + B.off[i]);
+    // the members holding lo and hi - 1
+    const size_t mb = (size_t)(std::upper_bound(B.off.begin(), B.off.end(), lo) - B.off.begin()) - 1;
+    const size_t me = (size_t)(std::upper_bound(B.off.begin(), B.off.end(), hi - 1) - B.off.begin()) - 1;
+    ok = ok && inflate(mb, fa) && (me == mb || inflate(me, fb));
+    if (!ok) {
+        munmap(m, len);
+        return fail("a member does not inflate");
+    }
+    phase("bgzf shard: head and cut members inflated");
+    const uint64_t a0 = lo - B.off[mb], a1 = std::min<uint64_t>(hi, B.off[mb + 1]) - B.off[mb];
+    int rc = vcfxg_ingest_begin(g, (size_t)(H + (hi - lo)));
+    if (!rc) rc = vcfxg_ingest(g, head, (size_t)H, 0);
+    if (!rc) rc = vcfxg_ingest(g, fa + a0, (size_t)(a1 - a0), 0);
+    if (!rc && me > mb + 1) {  // the members between: inflated on the device
+        const uint64_t c0 = B.ms[mb + 1].off, c1 = B.ms[me - 1].off + B.ms[me - 1].len;
+        std::vector<vcfxg_bgzf_member> mm(me - mb - 1);
+        for (size_t i = mb + 1; i < me; i++) mm[i - mb - 1] = {B.ms[i].off - c0, B.ms[i].len, B.ms[i].olen};
+        uint64_t bad = ~0ull;
+        rc = vcfxg_ingest_bgzf(g, B.comp + c0, (size_t)(c1 - c0), mm.data(), mm.size(), head, (size_t)H, &bad);
+    }
+    if (!rc && me > mb) rc = vcfxg_ingest(g, fb, (size_t)(hi - B.off[me]), 0);
+    if (rc) {
+        munmap(m, len);
+        return gpu_ok(g, rc, "bgzf shard ingest", err_fd);
+    }
+    phase("bgzf shard on the device");
+    if (map_base && map_len) munmap(map_base, map_len);  // the compressed bytes (the planner maps them too)
+    map_base = m;
+    map_len = len;
+    p = head;
+    host_n = (size_t)H;
+    n = (size_t)(H + (hi - lo));
+    stream_ctx = g;
+    streamed = n;
+    mapped = false;
+    gz = true;
+    tail = nullptr;
+    return true;
+}
 
 void shard_records_begin(Out &err) {
     if (!t_shard) return;

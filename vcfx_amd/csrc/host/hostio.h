@@ -12,11 +12,13 @@
 #include <thread>
 #include <vector>
 
+#include "gz.h"
 #include "vcfx_gpu.h"
 
 namespace vcfxh {
 
 struct Out;
+struct BgzfShard;
 
 struct Input {
     // the input bytes [p, p + host_n) on the host; n = all input bytes.  host_n < n only for
@@ -90,6 +92,11 @@ struct Input {
     // decompress()'s device path (bgzf_device, a BGZF chain of >= VCFX_BGZF_DEVICE_MIN inflated
     // bytes, 64 MiB by default; VCFX_BGZF_DEVICE=0 turns it off): false leaves the input as it was
     bool device_bgzf();
+    // decompress() on a rank of a multi-GPU run over a BGZF file (ShardRank::bgz, or
+    // VCFX_INPUT_VIEW="bgzf:H:LO:HI" from vcfx_amd/shard.py): the header [0, h) and the rank's
+    // records [lo, hi) of the inflated stream, on the rank's device (the members wholly inside
+    // inflated there; the two cut members' parts on the host); false after an "Error: ..." line
+    bool bgzf_view(int err_fd, const BgzfShard &B, uint64_t h, uint64_t lo, uint64_t hi, const std::string &who);
     // mapped inputs of 64 MiB and more: page-table population running on helper threads
     mutable std::vector<std::thread> populating;
     void populate(void *m, size_t len);
@@ -97,6 +104,14 @@ struct Input {
 };
 
 // ---- one rank of an in-process multi-GPU run (tool_shard_main.cpp, VCFX_NGPU) -------------------
+// A BGZF input split across the ranks by output offset (the planner's, shared by the ranks): the
+// member chain of the mapped file and each member's first output byte (off[nm] = the total)
+struct BgzfShard {
+    const char *comp = nullptr;
+    size_t comp_n = 0;
+    std::vector<BgzfSpan> ms;
+    std::vector<uint64_t> off;
+};
 // The driver runs the tool once per rank, each on its own host thread with its own device
 // context and its own view of the input file; these thread-local settings replace the
 // process-wide ones (gpu(), VCFX_INPUT_VIEW, VCFX_VIEW_SKIP_HEADER) on that thread.
@@ -105,6 +120,7 @@ struct ShardRank {
     vcfxg_ctx *g = nullptr;                          // this rank's context
     int device = 0, open_rc = 0;                     // its device and vcfxg_open's status
     unsigned long long h = 0, lo = 0, hi = 0;        // view: header [0, h) + records [lo, hi)
+    const BgzfShard *bgz = nullptr;                  // a BGZF file: the view is of its inflated bytes
     size_t whole_bytes = 0;                          // the whole input file's size
     int err_fd = -1;                                 // this rank's stderr (a memfd)
     long long err_mark = -1;                         // its bytes before the record phase

@@ -183,8 +183,9 @@ size_t file_header(const Input &in, std::vector<std::string> &names) {
         if (is_chrom_line(ls, (size_t)(le - ls))) chrom_names(ls, le, names);
         p = q;
     }
-    // a shard view (VCFX_INPUT_VIEW / a multi-GPU rank): its records follow the header part
-    return in.tail && p >= end ? in.host_n : in.n;
+    // a shard view (VCFX_INPUT_VIEW / a multi-GPU rank) or a device-only input (BGZF inflated on
+    // the device): its records follow the header part
+    return (in.tail || in.host_n < in.n) && p >= end ? in.host_n : in.n;
 }
 
 int hw_threads() {
@@ -196,6 +197,7 @@ int hw_threads() {
 int run_file(const Args &A, int out_fd, Out &err) {
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
+    in.bgzf_device = true;  // BGZF members inflated on the device (the records stay there)
     phase("start");
     if (!in.open_file(A.input)) {
         err.put(std::string("Error: Cannot open file: ") + A.input + "\n");
@@ -265,6 +267,7 @@ int run_file(const Args &A, int out_fd, Out &err) {
 int run_stream(const Args &A, int in_fd, int out_fd, Out &err) {
     Input in;
     in.gzip_ok = true;
+    in.bgzf_device = true;
     phase("start");
     in.read_fd(in_fd, /*host_copy=*/false);  // the header on the host; records on the device
     if (!in.decompress(err.fd)) return 1;

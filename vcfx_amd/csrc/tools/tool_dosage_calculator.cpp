@@ -122,6 +122,7 @@ extern "C" int vcfx_tool_dosage_calculator(int argc, char **argv, int in_fd, int
     }
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
+    in.bgzf_device = true;  // BGZF members inflated on the device (the records stay there)
     int rc;
     if (input) {
         phase("start");

@@ -323,6 +323,7 @@ extern "C" int vcfx_tool_haplotype_phaser(int argc, char **argv, int in_fd, int 
     Phaser P{false, streaming, quiet, thr, (size_t)win, out, err};
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
+    in.bgzf_device = true;  // BGZF members inflated on the device (the records stay there)
     phase("start");
     if (!input.empty() && input != "-") {
         if (!in.open_file(input.c_str())) {

@@ -105,7 +105,7 @@ bool run_stream(const Input &in, bool mmap_mode, const LdOpts &o, const std::str
                 int re, int out_fd, Out &err) {
     static const char kHead[] = "#VAR1_CHROM\tVAR1_POS\tVAR1_ID\tVAR2_CHROM\tVAR2_POS\tVAR2_ID\tR2\n";
     if (o.shard_rank == 0) write_all(out_fd, kHead, sizeof kHead - 1);
-    const char *p = in.p, *end = in.p + in.n, *ls, *le;
+    const char *p = in.p, *end = in.p + in.host_n, *ls, *le;  // (device BGZF: the head on the host)
     bool found = false;
     int ns = 0;
     size_t data_start = in.n;
@@ -288,6 +288,9 @@ extern "C" int vcfx_tool_ld_calculator(int argc, char **argv, int in_fd, int out
     out.flush();
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
+    // BGZF members inflated on the device (the records stay there) in streaming mode; matrix mode
+    // reads the records' text on the host
+    in.bgzf_device = !o.matrix;
     if (!o.input.empty()) {
         if (!in.open_file(o.input.c_str()) || in.n == 0) {
             err.put("Error: cannot open file '" + o.input + "'\n");

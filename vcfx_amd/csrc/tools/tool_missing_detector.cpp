@@ -105,7 +105,14 @@ bool run_md(const Input &in, bool file, const char *path, bool quiet, int out_fd
     }
     // a multi-GPU rank: the summary over every rank (the fast path's message only when no rank
     // saw a '.'; a rank's own fast path writes the same bytes as its per-line pass in file mode)
-    const bool last_nl = in.n && (in.tail ? in.tail[in.n - in.host_n - 1] : in.p[in.n - 1]) == '\n';
+    // (the input's last byte: a shard view's tail, the host bytes, or -- a device-only input, the
+    // records of a pipe or of BGZF inflated on the device -- one byte fetched from the device)
+    char lastb = 0;
+    if (in.n == 0) {
+    } else if (in.tail) lastb = in.tail[in.n - in.host_n - 1];
+    else if (in.host_n == in.n) lastb = in.p[in.n - 1];
+    else if (!gpu_ok(g, vcfxg_input_fetch(g, in.n - 1, 1, &lastb), "input_fetch", err.fd)) return false;
+    const bool last_nl = lastb == '\n';
     const uint64_t lines = nl - (nl && !last_nl ? 1 : 0);
     if (file && t_shard) {
         t_shard->cnt[0] = lines;
@@ -120,6 +127,18 @@ bool run_md(const Input &in, bool file, const char *path, bool quiet, int out_fd
         em.bytes(in.p + ds, in.p + in.host_n);
         em.finish();
         if (in.tail) write_all(out_fd, in.tail, in.n - in.host_n);
+        else if (in.host_n < in.n) {  // a device-only input: read back window by window
+            LineSource src(in, g, em);
+            for (uint64_t a = in.host_n; a < in.n;) {
+                const uint64_t b = std::min<uint64_t>(in.n, a + window_bytes() - 1);
+                const char *q = src.at(a, b);
+                if (!q) break;
+                em.bytes(q, q + (b - a));
+                a = b;
+            }
+            em.finish();
+            if (!src.ok) return gpu_ok(g, VCFXG_E_HIP, "input_fetch", err.fd);
+        }
         if (!quiet && !t_shard) err.put(md_summary(true, lines, 0, 0));
         return true;
     }
@@ -195,6 +214,7 @@ extern "C" int vcfx_tool_missing_detector(int argc, char **argv, int in_fd, int 
     if (!input && gs.next < argc) input = argv[gs.next];
     Input in;
     in.gzip_ok = true;  // .vcf.gz / BGZF input is inflated (VCFX_GZIP=0: off)
+    in.bgzf_device = true;  // BGZF members inflated on the device (the records stay there)
     if (input) {
         phase("start");
         if (!in.open_file(input)) {

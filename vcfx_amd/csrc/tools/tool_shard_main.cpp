@@ -19,8 +19,13 @@
 //     VCFX_missing_detector, VCFX_allele_counter (not -z)
 //   VCFX_ld_calculator (streaming): every rank parses the file and writes the pair rows of its
 //     `--shard r/N` share (equal window-pair counts)
-// Anything else -- stdin input, gzip / BGZF input, data lines before '#CHROM', help / version,
-// LD matrix mode, other tools -- runs as the plain single-context tool.  VCFX_NGPU larger than
+// A BGZF file (.vcf.gz as bgzip writes it) is cut the same way in the coordinates of its inflated
+// bytes: the planner parses the member chain, inflates on the host the members up to the '#CHROM'
+// line and the W - 1 members that hold the cuts (the cut advanced past the next '\n' there), and
+// each rank inflates the members wholly inside its records on its own device (Input::bgzf_view);
+// for VCFX_ld_calculator every rank inflates the whole file on its device.
+// Anything else -- stdin input, a gzip file that is not such a chain, data lines before '#CHROM',
+// help / version, LD matrix mode, other tools -- runs as the plain single-context tool.  VCFX_NGPU larger than
 // the device count puts several ranks on a device (round robin): the one-GPU rehearsal.
 #include <errno.h>
 #include <fcntl.h>
@@ -33,6 +38,7 @@
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <string>
@@ -132,9 +138,10 @@ struct Mapping {
 };
 
 // the byte after the first '#CHROM' line (a trailing '\r' dropped first, as the file paths
-// do), n if none; pre = a data line (not empty, not '#') comes before it
-size_t header_end(const char *p, size_t n, bool *pre) {
+// do), n if none (*found: whether there is one); pre = a data line (not empty, not '#') comes before it
+size_t header_end(const char *p, size_t n, bool *pre, bool *found = nullptr) {
     *pre = false;
+    if (found) *found = false;
     size_t at = 0;
     while (at < n) {
         const char *nl = (const char *)memchr(p + at, '\n', n - at);
@@ -143,21 +150,97 @@ size_t header_end(const char *p, size_t n, bool *pre) {
         if (le > at && p[le - 1] == '\r') le--;
         if (le > at) {
             if (p[at] != '#') *pre = true;
-            else if (is_chrom_line(p + at, le - at)) return e < n ? e + 1 : n;
+            else if (is_chrom_line(p + at, le - at)) {
+                if (found) *found = e < n;  // (a '#CHROM' line cut by the end of p is not complete)
+                return e < n ? e + 1 : n;
+            }
         }
         at = e + 1;
     }
     return n;
 }
 
-// the plan: kind, input path, the world actually used and world + 1 cuts (view kind)
+// the plan: kind, input path, the world actually used and world + 1 cuts (view kind); a BGZF
+// file: its member chain, h and the cuts in the inflated bytes' coordinates
 struct Plan {
     Kind kind = kUnsharded;
     std::string path;
     size_t whole = 0, h = 0;
     std::vector<uint64_t> cuts;
     int world = 1;
+    std::shared_ptr<BgzfShard> bgz;
 };
+
+// the cuts of a BGZF file (map): false when it is not a chain the device inflates, has a data line
+// before '#CHROM' or no record after it.  The header end H is found in the inflated head; the cut
+// r is the byte after the first '\n' at or past H + r (total - H) / W (vcfxg_shard_cuts' rule on the
+// inflated bytes), found by inflating the member that holds it (and the next ones, for a line
+// longer than the member's rest).
+bool plan_bgzf(const Mapping &map, int ngpu, Plan &pl) {
+    const char *e = getenv("VCFX_BGZF_DEVICE");
+    if ((e && e[0] == '0') || !gzip_enabled()) return false;
+    auto B = std::make_shared<BgzfShard>();
+    uint64_t total = 0;
+    if (!bgzf_chain(map.p, map.n, B->ms, &total) || B->ms.empty()) return false;
+    const size_t nm = B->ms.size();
+    B->comp = map.p;
+    B->comp_n = map.n;
+    B->off.resize(nm + 1);
+    for (size_t i = 0; i < nm; i++) B->off[i + 1] = B->off[i] + B->ms[i].olen;
+    std::vector<char> buf;
+    auto inflate = [&](size_t i, std::vector<char> &dst) {  // member i appended to dst
+        const size_t at = dst.size();
+        dst.resize(at + B->ms[i].olen);
+        size_t got = 0;
+        return gz_inflate_member(map.p + B->ms[i].off, B->ms[i].len, dst.data() + at, B->ms[i].olen, &got) &&
+               got == B->ms[i].olen;
+    };
+    // the header end
+    bool pre = false;
+    size_t H = 0;
+    for (size_t i = 0;; i++) {
+        if (i == nm || buf.size() > ((size_t)64 << 20) || !inflate(i, buf)) return false;
+        bool found = false;
+        H = header_end(buf.data(), buf.size(), &pre, &found);
+        if (pre) return false;
+        if (found) break;
+    }
+    if (H >= total) return false;
+    std::vector<uint64_t> cuts((size_t)ngpu + 1);
+    cuts[0] = H;
+    cuts[(size_t)ngpu] = total;
+    for (int r = 1; r < ngpu; r++) {
+        // (t > H: a line starts at t when byte t - 1 is a '\n'; else the cut is past the next one)
+        const uint64_t t = H + (total - H) * (uint64_t)r / (uint64_t)ngpu;
+        if (t <= H || t <= cuts[(size_t)r - 1]) {
+            cuts[(size_t)r] = std::max<uint64_t>(t, cuts[(size_t)r - 1]);
+            continue;
+        }
+        size_t k = (size_t)(std::upper_bound(B->off.begin(), B->off.end(), t - 1) - B->off.begin()) - 1;
+        uint64_t cut = total, from = t - 1 - B->off[k];
+        for (; k < nm; k++, from = 0) {
+            std::vector<char> mb;
+            if (!inflate(k, mb)) return false;
+            const char *nl = from < mb.size() ? (const char *)memchr(mb.data() + from, '\n', mb.size() - from) : nullptr;
+            if (nl) {
+                cut = B->off[k] + (uint64_t)(nl - mb.data()) + 1;
+                break;
+            }
+        }
+        cuts[(size_t)r] = std::max(cut, cuts[(size_t)r - 1]);
+    }
+    std::vector<uint64_t> keep{cuts[0]};
+    for (int r = 1; r <= ngpu; r++)
+        if (cuts[(size_t)r] > keep.back() || r == ngpu) keep.push_back(cuts[(size_t)r]);
+    if (keep.size() > 2 && keep[keep.size() - 1] == keep[keep.size() - 2]) keep.pop_back();
+    if (keep.size() < 3) return false;
+    pl.h = H;
+    pl.cuts = keep;
+    pl.world = (int)keep.size() - 1;
+    pl.bgz = B;
+    pl.kind = kView;
+    return true;
+}
 
 Plan make_plan(const char *tool, int argc, char **argv, int ngpu, Mapping &map) {
     Plan pl;
@@ -199,9 +282,21 @@ Plan make_plan(const char *tool, int argc, char **argv, int ngpu, Mapping &map) 
     if (m == MAP_FAILED) return pl;
     map.p = (const char *)m;
     map.n = n;
-    if ((unsigned char)map.p[0] == 0x1f && (unsigned char)map.p[1] == 0x8b) return pl;  // gzip / BGZF
     pl.path = path;
     pl.whole = n;
+    if ((unsigned char)map.p[0] == 0x1f && (unsigned char)map.p[1] == 0x8b) {  // gzip / BGZF
+        Plan g = pl;
+        if (T->kind == kRows) {  // (every rank inflates the whole file on its device)
+            if (gzip_enabled()) {
+                g.kind = kRows;
+                g.world = ngpu;
+                return g;
+            }
+        } else if (plan_bgzf(map, ngpu, g)) {
+            return g;
+        }
+        return Plan{};
+    }
     if (T->kind == kRows) {
         pl.kind = kRows;
         pl.world = ngpu;
@@ -266,7 +361,7 @@ int memfd(const char *name) {
 extern "C" int vcfx_shard_plan(const char *tool, int argc, char **argv, int ngpu, uint64_t *cuts, int *kind) {
     Mapping map;
     const Plan pl = make_plan(tool, argc, argv, ngpu, map);
-    if (kind) *kind = (int)pl.kind;
+    if (kind) *kind = pl.bgz ? 3 : (int)pl.kind;
     if (pl.kind == kUnsharded) return 1;
     if (cuts && pl.kind == kView)
         for (int r = 0; r <= pl.world; r++) cuts[r] = pl.cuts[(size_t)r];
@@ -296,6 +391,7 @@ extern "C" int vcfx_tool_main_sharded(const char *tool, int argc, char **argv, i
             s.h = pl.h;
             s.lo = pl.cuts[(size_t)r];
             s.hi = pl.cuts[(size_t)r + 1];
+            s.bgz = pl.bgz.get();
         } else {
             s.h = 0, s.lo = 0, s.hi = pl.whole;
             shard_arg[(size_t)r] = std::to_string(r) + "/" + std::to_string(W);

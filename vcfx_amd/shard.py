@@ -22,6 +22,11 @@ the mapping and kept records are written from the mapping.
   rows of its `--shard r/N` share (equal window-pair counts); with a window as large as the
   file (BASELINE config 5) every row range needs every variant, so there is nothing to cut.
   Matrix mode runs on rank 0 only.
+* A BGZF file (.vcf.gz as bgzip writes it; the AF and filter tools): the same cuts in the
+  inflated bytes' coordinates, planned by the drop-in library (vcfx_shard_plan: the member chain
+  parsed, the header and the W - 1 members holding the cuts inflated on the host); rank r's
+  view is VCFX_INPUT_VIEW="bgzf:H:LO:HI" and its tool inflates the members inside [LO, HI) on
+  its own device (hostio.cpp Input::bgzf_view).  Other gzip files run unsharded on rank 0.
 
 Outputs move to rank 0 only -- the only writer of stdout/stderr, so pipes work -- as chunked
 point-to-point sends in rank order (64 MiB per message); rank 0 streams each chunk to the sink
@@ -173,6 +178,15 @@ def is_gzip(path):
         return False
 
 
+def bgzf_cuts(argv, world):
+    """world + 1 cuts of a BGZF input in its inflated bytes (cuts[0] = the header's end) as the
+    drop-in library plans them (vcfx_shard_plan kind 3), or None: not a BGZF member chain, data
+    before '#CHROM', no records, or fewer non-empty shares than ranks (then: unsharded)"""
+    from . import tools
+    w, kind, cuts = tools.shard_plan(argv, world)
+    return cuts if kind == 3 and w == world else None
+
+
 def _has_flag(tool, argv, *names):
     opts, _ = parse_args(tool, argv)
     return any(n in names for n, _ in opts)
@@ -246,8 +260,8 @@ def tool_runner(argv, stdin, view=None, skip_header=False):
     keys = ("VCFX_INPUT_VIEW", "VCFX_VIEW_SKIP_HEADER")
     saved = {k: os.environ.get(k) for k in keys}
     try:
-        if view is not None:
-            os.environ["VCFX_INPUT_VIEW"] = "%d:%d:%d" % view
+        if view is not None:  # (a 4th item "bgzf": offsets into the inflated bytes)
+            os.environ["VCFX_INPUT_VIEW"] = ("bgzf:" if len(view) > 3 else "") + "%d:%d:%d" % tuple(view[:3])
         if skip_header:
             os.environ["VCFX_VIEW_SKIP_HEADER"] = "1"
         return tools.run(argv, stdin)
@@ -288,13 +302,24 @@ class _Sink:
         return b"".join(self.parts)
 
 
+def _unsharded(argv, comm, runner):
+    if comm.rank:
+        return b"", b"", 0
+    return runner(argv, b"")
+
+
 def run_af(argv, comm, runner, path, sink):
     quiet = _has_flag("VCFX_allele_freq_calc", argv, "-q", "--quiet")
     buf = _memmap(path)
-    ds = header_end(buf)
-    cuts = record_cuts(buf, ds, comm.world)
+    if is_gzip(path):
+        cuts = bgzf_cuts(argv, comm.world)
+        if cuts is None:
+            return _unsharded(argv, comm, runner)
+        tag = ("bgzf",)
+    else:
+        cuts, tag = record_cuts(buf, header_end(buf), comm.world), ()
     lo, hi = cuts[comm.rank], cuts[comm.rank + 1]
-    out, err, rc = runner(argv, b"", view=(ds, lo, hi), skip_header=comm.rank > 0)
+    out, err, rc = runner(argv, b"", view=(cuts[0], lo, hi) + tag, skip_header=comm.rank > 0)
     m = _AF_PROCESSED.search(err)
     v, lines = (int(m.group(1)), int(m.group(2))) if m else (0, 0)
     tot = comm.allreduce([v, lines, rc])
@@ -357,15 +382,17 @@ def _pre_header_data(buf, ds):
 
 def run_filter(argv, comm, runner, path, sink):
     buf = _memmap(path)
-    ds = header_end(buf)
-    plain = ds < len(buf) and not _pre_header_data(buf, ds)
-    if not comm.allreduce([1 if plain else 0], op="min")[0]:  # unsharded on rank 0
-        if comm.rank:
-            return b"", b"", 0
-        return runner(argv, b"")
-    cuts = record_cuts(buf, ds, comm.world)
+    if is_gzip(path):
+        cuts, tag = bgzf_cuts(argv, comm.world), ("bgzf",)
+        ok = cuts is not None
+    else:
+        ds, tag = header_end(buf), ()
+        ok = ds < len(buf) and not _pre_header_data(buf, ds)
+        cuts = record_cuts(buf, ds, comm.world) if ok else None
+    if not comm.allreduce([1 if ok else 0], op="min")[0]:  # unsharded on rank 0
+        return _unsharded(argv, comm, runner)
     lo, hi = cuts[comm.rank], cuts[comm.rank + 1]
-    out, err, rc = runner(argv, b"", view=(ds, lo, hi), skip_header=comm.rank > 0)
+    out, err, rc = runner(argv, b"", view=(cuts[0], lo, hi) + tag, skip_header=comm.rank > 0)
     comm.to_root(out, sink)
     errs = _Sink()
     comm.to_root(err, errs)
@@ -404,10 +431,11 @@ def plan(argv):
     if tool == "VCFX_ld_calculator":
         # every rank parses the whole (inflated) input and takes a share of the pair rows
         return None if _has_flag(tool, argv, "-m", "--matrix") else "ld"
-    if is_gzip(path):
-        # gzip / BGZF: the byte cuts of the compressed file are not record cuts, and the tool
-        # inflates its whole input before a view could apply -- run it unsharded on rank 0
+    if is_gzip(path) and tool == "VCFX_variant_counter":
+        # its gzip input is the reference's own (the first member): unsharded on rank 0
         return None
+    # (gzip: a BGZF member chain shards in its inflated bytes, bgzf_cuts; other gzip files
+    # then run unsharded on rank 0)
     if tool == "VCFX_allele_freq_calc":
         return "af"
     if tool == "VCFX_variant_counter":

@@ -65,7 +65,7 @@ def shard_plan(argv, ngpu):
     cuts = (ctypes.c_uint64 * (ngpu + 1))()
     kind = ctypes.c_int(0)
     w = L.vcfx_shard_plan(argv[0].encode(), len(argv), arr, ngpu, cuts, ctypes.byref(kind))
-    return w, kind.value, list(cuts[:w + 1]) if kind.value == 1 else None
+    return w, kind.value, list(cuts[:w + 1]) if kind.value in (1, 3) else None
 
 
 def run_pipe(argv, stdin=b"", cwd=None):
