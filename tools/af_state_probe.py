@@ -3,7 +3,7 @@ config-2 shard into a fresh device input buffer `--trials` times (a fresh contex
 spacer allocation of a varying size kept alive between trials so the buffer lands at other
 physical / virtual placements) and times `af_walk` over `--steps` calls each (HIP events on the
 engine stream).  Prints one JSON line per trial: the walk's mean / min ms, the buffer's device
-address and its alignment, and the clock the GPU reports; a bimodal walk time that follows the
+address and its alignment (the clock: tools/af_state_clock.sh); a bimodal walk time that follows the
 placement (not the order) points at the allocation.
 
     python tools/af_state_probe.py [--trials 8] [--steps 20] [--out JSON]
@@ -12,20 +12,11 @@ import argparse
 import ctypes
 import json
 import os
-import subprocess
 import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-
-
-def sclk():
-    try:
-        out = subprocess.run(["rocm-smi", "--showclocks"], capture_output=True, text=True, timeout=20).stdout
-        return [l.strip() for l in out.splitlines() if "sclk" in l.lower() or "fclk" in l.lower() or "mclk" in l.lower()]
-    except Exception as e:  # (rocm-smi absent or refused)
-        return [str(e)]
 
 
 def main():
@@ -59,7 +50,7 @@ def main():
         tot, n = eng.kernel_stats("af_walk")
         eng.close()
         r = {"trial": t, "spacer_mb": sz >> 20, "walk_ms_mean": round(tot / max(n, 1), 4), "step_ms": round(wall, 4),
-             "input_ptr": hex(ptr), "ptr_mod_2M": ptr % (2 << 20), "ptr_mod_1G": ptr % (1 << 30), "clocks": sclk()}
+             "input_ptr": hex(ptr), "ptr_mod_2M": ptr % (2 << 20), "ptr_mod_1G": ptr % (1 << 30)}
         print(json.dumps(r), flush=True)
         res.append(r)
     if a.out:

@@ -174,11 +174,9 @@ struct vcfxg_ctx {
     // per-member status, first bad member
     DevBuf bgz_in, bgz_mem, bgz_off, bgz_stat, bgz_small, bgz_perm;
     // the lane decoder's token buffers (and hand-over lists): one per inflate stream and one for
-    // `stream`; the stream the wave decoder takes the lane decoder's hand-overs on (beside the
-    // copy), and its events
+    // `stream`; its side stream (the hand-overs') and events
     DevBuf bgz_tok[kBgzStreams + 1];
-    hipStream_t bgz_aux = nullptr;
-    hipEvent_t bgz_aux_ev[2] = {};
+    vcfxg::InflateSide bgz_side;
     void *ld_plan_dev = nullptr;
     uint64_t text_bytes = 0;
     uint64_t text_hint = 0;  // AF walk: text bytes of the previous call (the next call's capacity)
@@ -370,8 +368,8 @@ void vcfxg_close(vcfxg_ctx *c) {
         if (c->bgz_ev[k]) (void)hipEventDestroy(c->bgz_ev[k]);
     }
     if (c->bgz_copy_ev) (void)hipEventDestroy(c->bgz_copy_ev);
-    if (c->bgz_aux) (void)hipStreamDestroy(c->bgz_aux);
-    for (hipEvent_t e : c->bgz_aux_ev)
+    if (c->bgz_side.aux) (void)hipStreamDestroy(c->bgz_side.aux);
+    for (hipEvent_t e : c->bgz_side.ev)
         if (e) (void)hipEventDestroy(e);
     delete c;
 }
@@ -507,7 +505,7 @@ int vcfxg_ingest_begin(vcfxg_ctx *c, size_t size_hint) {
     if (c->copy_stream) HIPCHK(c, hipStreamSynchronize(c->copy_stream));
     for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++)
         if (c->bgz_stream[k]) HIPCHK(c, hipStreamSynchronize(c->bgz_stream[k]));
-    if (c->bgz_aux) HIPCHK(c, hipStreamSynchronize(c->bgz_aux));
+    if (c->bgz_side.aux) HIPCHK(c, hipStreamSynchronize(c->bgz_side.aux));
     c->bgz_total = c->bgz_staged = 0;
     int r = ensure(c, c->input, size_hint + kPad);
     if (r) return r;
@@ -673,10 +671,11 @@ static std::vector<uint32_t> bgz_order(const vcfxg_bgzf_member *mem, uint64_t co
     return perm;
 }
 
-// the hand-over stream and its events (created once)
+// the lane decoder's side stream and events (created once)
 static int bgz_aux(vcfxg_ctx *c) {
-    if (!c->bgz_aux) HIPCHK(c, hipStreamCreateWithFlags(&c->bgz_aux, hipStreamNonBlocking));
-    for (hipEvent_t &e : c->bgz_aux_ev)
+    vcfxg::InflateSide &d = c->bgz_side;
+    if (!d.aux) HIPCHK(c, hipStreamCreateWithFlags(&d.aux, hipStreamNonBlocking));
+    for (hipEvent_t &e : d.ev)
         if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return VCFXG_OK;
 }
@@ -702,8 +701,7 @@ static int bgz_launch(vcfxg_ctx *c, const vcfxg_bgzf_member *mem, uint64_t first
     HIPCHK(c, vcfxg::launch_inflate(0, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem) + first,
                                     P<uint64_t>(c->bgz_off) + first, count, P<uint8_t>(c->input) + c->n,
                                     P<uint32_t>(c->bgz_stat) + first, P<unsigned long long>(c->bgz_small), z1k_unused,
-                                    st, first, P<uint32_t>(c->bgz_tok[slot]), tm, P<uint32_t>(c->bgz_perm) + first,
-                                    c->bgz_aux, c->bgz_aux_ev[0], c->bgz_aux_ev[1]));
+                                    st, first, P<uint32_t>(c->bgz_tok[slot]), tm, P<uint32_t>(c->bgz_perm) + first, &c->bgz_side));
     c->bgz_launched = first + count;
     c->bgz_out = o;
     return VCFXG_OK;
@@ -817,8 +815,7 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         HIPCHK(c, vcfxg::launch_inflate(0, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem),
                                         P<uint64_t>(c->bgz_off), nm, P<uint8_t>(c->input) + c->n,
                                         P<uint32_t>(c->bgz_stat), P<unsigned long long>(c->bgz_small), z1k, c->stream, 0,
-                                        P<uint32_t>(c->bgz_tok[vcfxg_ctx::kBgzStreams]), tm, P<uint32_t>(c->bgz_perm),
-                                        c->bgz_aux, c->bgz_aux_ev[0], c->bgz_aux_ev[1]));
+                                        P<uint32_t>(c->bgz_tok[vcfxg_ctx::kBgzStreams]), tm, P<uint32_t>(c->bgz_perm), &c->bgz_side));
         prof_end(c, "bgzf_inflate");
     }
     prof_begin(c, "bgzf_crc32");

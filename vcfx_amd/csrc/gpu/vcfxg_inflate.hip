@@ -1082,7 +1082,11 @@ __global__ void __launch_bounds__(64) k_inflate_copy(const BgzfMember *__restric
     // branch-free step: every lane reads its byte of the period-d pattern (a literal's lanes take
     // its byte) and writes it at x + lane; the lanes past the length write ahead of the output,
     // into slots of bytes long flushed and out of reach, which the next tokens rewrite before
-    // anything reads or flushes them.  Longer or further matches take the loop below.
+    // anything reads or flushes them.  Longer or further matches (the slow flag) take the loops
+    // of slow() below.  The fields of a group's 64 tokens are unpacked once, a token per lane
+    // (length, distance, its reciprocal, a literal's byte); a fast step takes them by v_readlane,
+    // which is vector work: the CU's one scalar unit, which a step of scalar field extraction and
+    // branching kept busy (~15 scalar instructions a token), now counts steps only.
     uint32_t nxt = tk[1 + lane];
     for (uint32_t tb = 0; tb < ntok; tb += 64) {
         const uint32_t cur = nxt;
@@ -1091,16 +1095,26 @@ __global__ void __launch_bounds__(64) k_inflate_copy(const BgzfMember *__restric
             nxt = tk[1 + (q < tok_cap - 1 ? q : tok_cap - 2)];
         }
         const uint32_t nt = ntok - tb < 64 ? ntok - tb : 64;
-        auto token = [&](uint32_t j) {
+        const uint32_t tlen = (cur >> 16) & 511, tdist = (cur & 0x7FFF) + 1;
+        const float trcp = __builtin_amdgcn_rcpf((float)tdist);
+        const uint32_t tlit = (cur & kTLit) ? (cur & 255) : 256u;  // < 256: a literal's byte
+        uint64_t slowm = __builtin_amdgcn_ballot_w64(lane < nt && (cur & kTSlow));
+        auto fast = [&](uint32_t j) {
+            const uint32_t dist = (uint32_t)__builtin_amdgcn_readlane((int)tdist, (int)j);
+            const uint32_t lit = (uint32_t)__builtin_amdgcn_readlane((int)tlit, (int)j);
+            const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)tlen, (int)j);
+            const float rd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(trcp), (int)j));
+            const uint32_t q = (uint32_t)(lanef * rd);
+            uint32_t v = W[(x + lane - __umul24(q + 1u, dist)) & kCWMask];
+            v = lit < 256 ? lit : v;
+            W[(x + lane) & kCWMask] = (uint8_t)v;
+            x += len;
+        };
+        auto slow = [&](uint32_t j) {
             const uint32_t t = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)j);
             const uint32_t len = (t >> 16) & 511, dist = (t & 0x7FFF) + 1;
             const float rd = __builtin_amdgcn_rcpf((float)dist);
-            if (!(t & kTSlow)) {
-                const uint32_t q = (uint32_t)(lanef * rd);
-                uint32_t v = W[(x - dist + lane - __mul24(q, dist)) & kCWMask];
-                v = (t & kTLit) ? t : v;
-                W[(x + lane) & kCWMask] = (uint8_t)v;
-            } else if (dist <= kCReach) {
+            if (dist <= kCReach) {
                 for (uint32_t c = 0; c < len; c += 64) {
                     const uint32_t q = (uint32_t)(((float)c + lanef) * rd);
                     const uint8_t v = W[(x - dist + c + lane - __mul24(q, dist)) & kCWMask];
@@ -1118,17 +1132,28 @@ __global__ void __launch_bounds__(64) k_inflate_copy(const BgzfMember *__restric
             }
             x += len;
         };
-        // four tokens a flush check (x moves at most 4 x 258 bytes between checks)
+        // runs of fast tokens up to the next slow one; a flush check every 16 fast tokens (x moves
+        // at most 1 KiB between checks) and after each slow one
         uint32_t j = 0;
-        for (; j + 4 <= nt; j += 4) {
-            token(j);
-            token(j + 1);
-            token(j + 2);
-            token(j + 3);
-            if (x - fl >= 2 * kCFlush) flush(x & ~(kCFlush - 1), false);
+        while (j < nt) {
+            const uint32_t stop = slowm ? min((uint32_t)__builtin_ctzll(slowm), nt) : nt;
+            while (j < stop) {
+                const uint32_t e = min(stop, j + 16);
+                for (; j + 4 <= e; j += 4) {
+                    fast(j);
+                    fast(j + 1);
+                    fast(j + 2);
+                    fast(j + 3);
+                }
+                for (; j < e; j++) fast(j);
+                if (x - fl >= 2 * kCFlush) flush(x & ~(kCFlush - 1), false);
+            }
+            if (j < nt) {
+                slow(j++);
+                slowm &= slowm - 1;
+                if (x - fl >= 2 * kCFlush) flush(x & ~(kCFlush - 1), false);
+            }
         }
-        for (; j < nt; j++) token(j);
-        if (x - fl >= 2 * kCFlush) flush(x & ~(kCFlush - 1), false);
     }
     flush(xend, true);
 }
@@ -1247,14 +1272,14 @@ void crc32_zero1k_basis(Crc1k *z) {
 hipError_t launch_inflate(int which, const uint8_t *comp, const BgzfMember *mem, const uint64_t *out_off,
                           uint64_t n_members, uint8_t *out, uint32_t *mstat, unsigned long long *first_bad,
                           const Crc1k &z1k, hipStream_t s, uint64_t mbase, uint32_t *tok, uint64_t tok_members,
-                          const uint32_t *perm, hipStream_t aux, hipEvent_t ev_dec, hipEvent_t ev_fb) {
+                          const uint32_t *perm, const InflateSide *side) {
     // (mem, out_off, mstat: the arrays' entries for members mbase ..; first_bad: a global index,
     // followed by the 32-bit count of members the lane decoder handed to the wave decoder)
     static const int lanes_env = [] {
         const char *e = getenv("VCFX_INFLATE_LANES");  // 0: every member on the wave decoder (A/B)
         return e && *e == '0' ? 0 : 1;
     }();
-    const int lanes = lanes_env && tok && tok_members && perm && aux && ev_dec && ev_fb;
+    const int lanes = lanes_env && tok && tok_members && perm && side && side->aux;
     uint32_t *const ndefer = reinterpret_cast<uint32_t *>(first_bad + 1);
     if (which == 0 && !lanes) {
         for (uint64_t m0 = 0; m0 < n_members; m0 += (1u << 30)) {
@@ -1267,24 +1292,39 @@ hipError_t launch_inflate(int which, const uint8_t *comp, const BgzfMember *mem,
         return hipSuccess;
     }
     if (which == 0) {
+        hipStream_t aux = side->aux;
+        hipEvent_t ev_dec = side->ev[0], ev_fb = side->ev[1];
+        // the hand-over list follows the tokens
+        uint32_t *const hl0 = tok + (size_t)tok_members * kTokCap;
+        hipError_t e;
+        auto decode = [&](hipStream_t st, uint64_t b, uint32_t nb, uint32_t *hl) -> hipError_t {
+            hipError_t r;
+            if ((r = hipMemsetAsync(hl, 0, 4, st)) != hipSuccess) return r;
+            hipLaunchKernelGGL(k_inflate_decode, dim3((nb + 63) / 64), dim3(64), 0, st, comp, mem, out_off, out, mstat,
+                               ndefer, tok + (size_t)(b % tok_members) * kTokCap, kTokCap, perm + b, nb, hl);
+            return hipGetLastError();
+        };
+        auto handover = [&](uint64_t b, const uint32_t *hl) -> hipError_t {
+            hipLaunchKernelGGL(k_inflate_handover, dim3(kHandGrid), dim3(64), 0, aux, comp, mem, out_off, out, mstat,
+                               first_bad, mbase, perm + b, hl);
+            return hipGetLastError();
+        };
+        auto copy = [&](hipStream_t st, uint64_t b, uint32_t nb) -> hipError_t {
+            hipLaunchKernelGGL(k_inflate_copy, dim3(nb), dim3(64), 0, st, mem, out_off, out,
+                               tok + (size_t)(b % tok_members) * kTokCap, kTokCap, perm + b, nb);
+            return hipGetLastError();
+        };
         // the lane decoder, then its hand-overs on `aux` beside the copy on `s`, in pieces of at
-        // most tok_members (the token buffer's members; its hand-over list follows the tokens)
-        uint32_t *const hlist = tok + (size_t)tok_members * kTokCap;
+        // most tok_members (the token buffer's members).  (Two pieces on two streams -- one round of
+        // decode waves, the rest on a low-priority stream so that the first piece's copy starts
+        // while the rest decodes -- measured 8.64-8.75 ms against 8.70: not kept.)
         for (uint64_t b = 0; b < n_members; b += tok_members) {
             const uint32_t nb = (uint32_t)(n_members - b < tok_members ? n_members - b : tok_members);
-            hipError_t e;
             if (b && (e = hipStreamWaitEvent(s, ev_fb, 0)) != hipSuccess) return e;  // (the list is reused)
-            if ((e = hipMemsetAsync(hlist, 0, 4, s)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_inflate_decode, dim3((nb + 63) / 64), dim3(64), 0, s, comp, mem, out_off, out, mstat,
-                               ndefer, tok, kTokCap, perm + b, nb, hlist);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            if ((e = hipEventRecord(ev_dec, s)) != hipSuccess || (e = hipStreamWaitEvent(aux, ev_dec, 0)) != hipSuccess)
+            if ((e = decode(s, b, nb, hl0)) != hipSuccess || (e = hipEventRecord(ev_dec, s)) != hipSuccess ||
+                (e = hipStreamWaitEvent(aux, ev_dec, 0)) != hipSuccess || (e = handover(b, hl0)) != hipSuccess ||
+                (e = hipEventRecord(ev_fb, aux)) != hipSuccess || (e = copy(s, b, nb)) != hipSuccess)
                 return e;
-            hipLaunchKernelGGL(k_inflate_handover, dim3(kHandGrid), dim3(64), 0, aux, comp, mem, out_off, out, mstat,
-                               first_bad, mbase, perm + b, hlist);
-            if ((e = hipGetLastError()) != hipSuccess || (e = hipEventRecord(ev_fb, aux)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_inflate_copy, dim3(nb), dim3(64), 0, s, mem, out_off, out, tok, kTokCap, perm + b, nb);
-            if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         return hipStreamWaitEvent(s, ev_fb, 0);
     }

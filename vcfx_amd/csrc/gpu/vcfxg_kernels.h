@@ -42,20 +42,23 @@ struct Crc1k {
     uint32_t v[32];
 };
 void crc32_zero1k_basis(Crc1k *z);
+// the lane decoder's side stream (the hand-overs') and the events that join it
+struct InflateSide {
+    hipStream_t aux = nullptr;
+    hipEvent_t ev[2] = {};  // decoded, hand-overs done
+};
 // which: 0 = the inflate (k_inflate_decode; k_inflate_handover, the wave decoder on the members the
-// lane decoder hands over, on `aux` beside k_inflate_copy), 1 = k_crc32.  first_bad[0]: the first
-// bad member; the 32-bit word after it counts the hand-overs.
+// lane decoder hands over, on side->aux beside k_inflate_copy), 1 = k_crc32.  first_bad[0]: the
+// first bad member; the 32-bit word after it counts the hand-overs.
 hipError_t launch_inflate(int which, const uint8_t *comp, const BgzfMember *mem, const uint64_t *out_off,
                           uint64_t n_members, uint8_t *out, uint32_t *mstat, unsigned long long *first_bad,
                           const Crc1k &z1k, hipStream_t s, uint64_t mbase = 0, uint32_t *tok = nullptr,
-                          uint64_t tok_members = 0, const uint32_t *perm = nullptr, hipStream_t aux = nullptr,
-                          hipEvent_t ev_dec = nullptr, hipEvent_t ev_fb = nullptr);
+                          uint64_t tok_members = 0, const uint32_t *perm = nullptr, const InflateSide *side = nullptr);
 // the lane decoder's token buffer: kTokCap 32-bit slots per member, tok_members members (launches
-// of more members run in pieces), then tok_members + 1 words of the hand-over list; perm: the
+// of more members run in pieces), then the hand-over list of tok_members + 1 words; perm: the
 // members in the order the lanes take them (largest compressed first: a wave's lanes then decode
-// similar amounts); aux and two events: the hand-overs' stream.  None of them: every member on the
-// wave decoder.
-constexpr uint32_t kTokCap = 8192;
+// similar amounts).  No side: every member on the wave decoder.
+constexpr uint32_t kTokCap = 6144;
 // occurrences of `byte` in buf[lo, hi) added to *out (k_count_byte)
 hipError_t launch_count_byte(const uint8_t *buf, uint64_t lo, uint64_t hi, uint8_t byte, unsigned long long *out,
                              hipStream_t s);
