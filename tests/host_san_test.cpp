@@ -15,8 +15,10 @@
 #include <string.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <string>
 #include <thread>
+#include <vector>
 
 #include "hostio.h"
 
@@ -73,7 +75,43 @@ int main(int argc, char **argv) {
     open_and_inflate("gzip", argv[3], true);
     open_and_inflate("multi", argv[4], true);
     open_and_inflate("trunc", argv[5], true);
-    // 7. a pipe read whole into the head; 8. the same with a 1 MiB head and 4 MiB chunks: the
+    // 7. the BGZF chain walked piece by piece as the file ring does (BgzfStream::feed), and with
+    //    each piece's chain scanned beforehand (BgzfChunk::scan + adopt, the ring's readers): both
+    //    equal to bgzf_chain on the whole file, for pieces smaller than a member, about a member,
+    //    and larger (odd sizes: headers and trailers cut at every offset)
+    {
+        FILE *f = fopen(argv[2], "rb");
+        std::string z;
+        char b[1 << 16];
+        size_t k;
+        while (f && (k = fread(b, 1, sizeof b, f)) > 0) z.append(b, k);
+        if (f) fclose(f);
+        std::vector<vcfxh::BgzfSpan> whole;
+        uint64_t tot = 0;
+        const bool okw = vcfxh::bgzf_chain(z.data(), z.size(), whole, &tot);
+        bool same = okw;
+        for (size_t piece : {(size_t)1000, (size_t)4099, (size_t)65536, (size_t)70001, (size_t)1 << 20, (size_t)16 << 20}) {
+            vcfxh::BgzfStream fw, ad;
+            vcfxh::BgzfChunk c;
+            for (size_t o = 0; o < z.size(); o += piece) {
+                const size_t n = std::min(piece, z.size() - o);
+                fw.feed(z.data() + o, n);
+                c.scan(z.data() + o, n, o);
+                ad.adopt(z.data() + o, n, c);
+            }
+            auto eq = [&](const vcfxh::BgzfStream &s) {
+                if (!s.ok(z.size()) || s.members.size() != whole.size() || s.out != tot) return false;
+                for (size_t i = 0; i < whole.size(); i++)
+                    if (s.members[i].off != whole[i].off || s.members[i].len != whole[i].len ||
+                        s.members[i].olen != whole[i].olen)
+                        return false;
+                return true;
+            };
+            same = same && eq(fw) && eq(ad);
+        }
+        printf("chain %zu %s\n", whole.size(), same ? "same" : "differs");
+    }
+    // 8. a pipe read whole into the head; 9. the same with a 1 MiB head and 4 MiB chunks: the
     // reader, its pre-fault thread, the background device open and the ingest thread (no
     // device here: the open fails and the ingest thread leaves)
     for (int round = 0; round < 2; round++) {

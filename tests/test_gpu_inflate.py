@@ -392,8 +392,9 @@ def test_tools_on_device_bgzf(argv):
 
 # ---- the streamed form (VCFX_allele_freq_calc -i F.gz): the compressed file through the pinned file
 # ring, the member chain parsed from the ring's slots, every member inflated on the device -------------
-@pytest.mark.parametrize("slot,batch", [("4096", "1"), ("65536", "1"), ("65536", "0"), ("default", "1024")])
-def test_af_streams_bgzf_through_the_ring(slot, batch):
+@pytest.mark.parametrize("slot,batch,table", [("4096", "1", None), ("65536", "1", None), ("65536", "0", None),
+                                               ("default", "1024", None), ("65536", "1", "3")])
+def test_af_streams_bgzf_through_the_ring(slot, batch, table):
     """Slots far smaller than a member (a member's header and trailer in different slots), about one
     member, and the default 16 MiB; inflate batches launched per slot, or none until the end: the
     same rows as the oracle on the plain text, with the schedule
@@ -423,6 +424,8 @@ def test_af_streams_bgzf_through_the_ring(slot, batch):
             env["VCFX_BGZF_BATCH_MIN"] = batch
         if slot != "default":
             env["VCFX_FILE_SLOT"] = slot
+        if table:  # member tables sized for 3 members: the batches stop (E_CAP), the tables grow at the end
+            env["VCFXG_BGZF_TABLE"] = table
 
         def run(path):
             if os.path.exists(log):

@@ -507,6 +507,12 @@ int vcfxg_ingest_begin(vcfxg_ctx *c, size_t size_hint) {
         if (c->bgz_stream[k]) HIPCHK(c, hipStreamSynchronize(c->bgz_stream[k]));
     if (c->bgz_side.aux) HIPCHK(c, hipStreamSynchronize(c->bgz_side.aux));
     c->bgz_total = c->bgz_staged = 0;
+    // (a hint past half of the memory the input could take -- free memory plus its buffer now --
+    // is cut to that half: the walk's, LD's and the inflate's buffers keep the rest, and the
+    // ingest grows the buffer if the bytes need more)
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && size_hint > (fr + c->input.cap) / 2)
+        size_hint = (fr + c->input.cap) / 2;
     int r = ensure(c, c->input, size_hint + kPad);
     if (r) return r;
     c->loaded = false;
@@ -576,21 +582,53 @@ static int ingest_mark(vcfxg_ctx *c, size_t upto) {
     return VCFXG_OK;
 }
 
-// (a member holds >= 20 compressed bytes: the member tables of a staged stream are sized once)
+// (a member holds >= 20 compressed bytes: at most this many members in a stream)
 static uint64_t bgz_max_members(size_t comp_total) { return comp_total / 20 + 2; }
+
+// The member tables (members, output offsets, verdicts, the lane order) of a staged stream hold
+// `want` members, keeping the first `keep` (the entries the launched batches wrote; every batch
+// is complete -- the caller made `stream` wait for them).  Sized at the stage's start for members
+// of >= 1 KiB compressed (a genotype VCF's are ~4 KiB): 28 B a member where the worst case
+// (20-byte members) would be ~1.4x the compressed bytes; a stream of smaller members stops
+// batching (E_CAP) and grows them at the end.
+static int bgz_tables(vcfxg_ctx *c, uint64_t want, uint64_t keep) {
+    struct Tab {
+        DevBuf *b;
+        size_t w;
+    } t[] = {{&c->bgz_mem, sizeof(vcfxg_bgzf_member)}, {&c->bgz_off, 8}, {&c->bgz_stat, 4}, {&c->bgz_perm, 4}};
+    bool need = false;
+    for (const Tab &x : t) need = need || x.b->cap < x.w * want;
+    if (!need) return VCFXG_OK;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (const Tab &x : t) {
+        if (x.b->cap >= x.w * want) continue;
+        const size_t nc = x.w * want + x.w * want / 8;
+        void *np = nullptr;
+        HIPCHK(c, hipMalloc(&np, nc));
+        if (keep && x.b->p) HIPCHK(c, hipMemcpyAsync(np, x.b->p, x.w * keep, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (x.b->p) HIPCHK(c, hipFree(x.b->p));
+        x.b->p = np;
+        x.b->cap = nc;
+    }
+    return VCFXG_OK;
+}
+static uint64_t bgz_table_members(const vcfxg_ctx *c) { return c->bgz_mem.cap / sizeof(vcfxg_bgzf_member); }
 
 int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, size_t comp_total) {
     if (!c || (!host && n) || offset > comp_total || n > comp_total - offset) return VCFXG_E_ARG;
     if (!c->ingesting) return VCFXG_E_STATE;
     HIPCHK(c, hipSetDevice(c->device));
     if (offset == 0) {
-        const uint64_t mm = bgz_max_members(comp_total);
+        static const uint64_t tset = [] {  // (VCFXG_BGZF_TABLE: the members sized for; tests: tiny)
+            const char *e = getenv("VCFXG_BGZF_TABLE");
+            return e && *e ? std::max<uint64_t>(2, strtoull(e, nullptr, 10)) : (uint64_t)0;
+        }();
+        const uint64_t mm = std::min<uint64_t>(bgz_max_members(comp_total),
+                                               tset ? tset : std::max<uint64_t>(65536, comp_total / 1024));
         int r = ensure(c, c->bgz_in, comp_total + kCompPad);
-        if (!r) r = ensure(c, c->bgz_mem, sizeof(vcfxg_bgzf_member) * mm);
-        if (!r) r = ensure(c, c->bgz_off, 8 * mm);
-        if (!r) r = ensure(c, c->bgz_stat, 4 * mm);
+        if (!r) r = bgz_tables(c, mm, 0);
         if (!r) r = ensure(c, c->bgz_small, 64);
-        if (!r) r = ensure(c, c->bgz_perm, 4 * mm);
         if (r) return r;
         if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
         if (!c->bgz_copy_ev) HIPCHK(c, hipEventCreateWithFlags(&c->bgz_copy_ev, hipEventDisableTiming));
@@ -719,6 +757,7 @@ int vcfxg_bgzf_inflate(vcfxg_ctx *c, const vcfxg_bgzf_member *mem, size_t count)
         out += mem[i].out_len;
     }
     if (c->bgz_launched + count > bgz_max_members(c->bgz_total)) return VCFXG_E_ARG;
+    if (c->bgz_launched + count + 1 > bgz_table_members(c)) return VCFXG_E_CAP;  // (the rest at the end)
     // the output must fit the input buffer as it is (growing it here would move the bytes the
     // launched batches are writing): the rest waits for vcfxg_ingest_bgzf, which grows it
     if (c->n + c->bgz_out + out + kPad > c->input.cap) return VCFXG_E_CAP;
@@ -763,6 +802,7 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->bgz_copy_ev, 0));
         if (done)
             for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++) HIPCHK(c, hipStreamWaitEvent(c->stream, c->bgz_ev[k], 0));
+        if (int rt = bgz_tables(c, nm + 1, done)) return rt;  // (more members than the stage sized for)
     }
     if (c->n + tot + kPad > c->input.cap) {  // grow as vcfxg_ingest does (keeping launched output)
         const size_t keep = c->n + (size_t)(staged ? c->bgz_out : 0);

@@ -140,6 +140,70 @@ void BgzfStream::feed(const char *d_c, size_t len) {
     }
 }
 
+void BgzfChunk::scan(const char *d_c, size_t len, uint64_t off) {
+    const uint8_t *d = (const uint8_t *)d_c;
+    ms.clear();
+    first = end = ~0ull;
+    // the first position at which a member header validates (a guess: adopt() takes the chain
+    // only if the stream's own walk arrives exactly there)
+    size_t r = 0, bs = 0;
+    uint32_t olen = 0;
+    for (;;) {
+        const void *q = r < len ? memchr(d + r, 0x1f, len - r) : nullptr;
+        if (!q) return;
+        r = (size_t)((const uint8_t *)q - d);
+        if (chain_member(d + r, len - r, &bs, &olen) > 0) break;
+        r++;
+    }
+    first = off + r;
+    int k;
+    do {
+        ms.push_back({off + r, (uint32_t)bs, olen});
+        r += bs;
+    } while ((k = chain_member(d + r, len - r, &bs, &olen)) > 0);
+    end = off + r;  // (the member at end is cut by the chunk's end, or not a member: the walk decides)
+}
+
+void BgzfStream::adopt(const char *d_c, size_t len, const BgzfChunk &c) {
+    const uint64_t off = fed;
+    if (bad) {
+        fed += len;
+        return;
+    }
+    size_t r = 0;  // the bytes of d the carried member takes
+    if (!carry.empty()) {
+        const size_t had = carry.size(), take = std::min<size_t>(len, 65536 + 64 - had);
+        carry.insert(carry.end(), d_c, d_c + take);
+        size_t bs = 0;
+        uint32_t olen = 0;
+        const int k = chain_member((const uint8_t *)carry.data(), carry.size(), &bs, &olen);
+        if (k < 0 || (k == 0 && take < len)) {
+            bad = true;
+            fed += len;
+            return;
+        }
+        if (k == 0) {
+            fed += len;
+            return;
+        }
+        members.push_back({pos, (uint32_t)bs, olen});
+        out += olen;
+        r = pos + bs - off;
+        pos += bs;
+        carry.clear();
+    }
+    if (c.first != pos || c.end > off + len) {  // (the guess is not where the walk is: walk it here)
+        fed = off + r;
+        feed(d_c + r, len - r);
+        return;
+    }
+    for (const BgzfSpan &m : c.ms) out += m.olen;
+    members.insert(members.end(), c.ms.begin(), c.ms.end());
+    pos = c.end;
+    fed = c.end;
+    feed(d_c + (c.end - off), len - (size_t)(c.end - off));  // (the rest: the member the chunk cuts)
+}
+
 bool gz_inflate_member(const char *src, size_t n, char *dst, size_t cap, size_t *got) {
     return inflate_member((const uint8_t *)src, n, dst, cap, got);
 }

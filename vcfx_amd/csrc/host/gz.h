@@ -31,6 +31,15 @@ bool bgzf_chain(const char *src, size_t n, std::vector<BgzfSpan> &members, uint6
 // bgzf_chain on a stream fed in order, piece by piece (a staging ring's slots): feed(d, len) takes
 // the next len bytes; a member whose bytes span pieces is completed from a carry of at most
 // 64 KiB.  ok(total) after the last piece: the same chain bgzf_chain returns on the whole stream.
+// The members of one piece of the stream found without the walk before it (a reader thread's,
+// on the bytes it just read): the first offset at which a member header validates, the chain of
+// complete members from there and the offset past the last; BgzfStream::adopt takes them when the
+// stream's own walk arrives at `first`, else walks the piece itself.
+struct BgzfChunk {
+    std::vector<BgzfSpan> ms;
+    uint64_t first = ~0ull, end = ~0ull;
+    void scan(const char *d, size_t len, uint64_t off);  // d = stream bytes [off, off + len)
+};
 struct BgzfStream {
     std::vector<BgzfSpan> members;
     uint64_t out = 0;   // the sum of ISIZE so far
@@ -39,6 +48,8 @@ struct BgzfStream {
     bool bad = false;   // not a BGZF chain
     std::vector<char> carry;  // bytes [pos, fed) of a member not yet complete
     void feed(const char *d, size_t len);
+    // feed(d, len) with the piece's members scanned beforehand (the same chain, faster)
+    void adopt(const char *d, size_t len, const BgzfChunk &c);
     bool ok(uint64_t total) const { return !bad && carry.empty() && pos == total && fed == total && !members.empty(); }
 };
 // one gzip member [src, src+n) inflated into [dst, dst+cap) by zlib (CRC and ISIZE checked);

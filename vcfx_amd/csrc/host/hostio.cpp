@@ -312,8 +312,9 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
         }
     } ring_release{!ring_.empty()};
     // (the input buffer sized for ~24x the compressed bytes, a genotype VCF's BGZF ratio, so the
-    // inflate batches launched during the stream have their room; more grows it at the end.  When
-    // the device cannot hold that, 6x: the batches that do not fit wait for the end, E_CAP)
+    // inflate batches launched during the stream have their room; more grows it at the end.
+    // vcfxg_ingest_begin cuts a hint past half the device's free memory; when even the cut one
+    // cannot be had, 6x: the batches that do not fit wait for the end, E_CAP)
     if (ring_.empty() || (vcfxg_ingest_begin(g, 24 * total) != VCFXG_OK && vcfxg_ingest_begin(g, 6 * total) != VCFXG_OK)) {
         munmap(hm, kHeadMax);
         return false;
@@ -331,6 +332,10 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
     bool stop = false, ok = true;
     std::atomic<int> rerr{0};
     std::vector<std::thread> readers;
+    // (each reader walks the member chain of the chunk it just read, from the first header that
+    // validates -- the bytes still in its core's caches; the loop below takes that chain when its
+    // own walk arrives there: the walk was a dependent miss per member, 14-17 ms on the bench shard)
+    std::vector<BgzfChunk> scans(S);
     for (size_t t = 0; t < T; t++)
         readers.emplace_back([&, t] {
             for (size_t i = t; i < nchunks; i += T) {
@@ -343,6 +348,7 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
                 const size_t off = i * kSlot, len = std::min(kSlot, total - off);
                 int er = 0;
                 const bool r = pread_full(fd, (char *)ring_[s], len, off, &er);
+                if (r) scans[s].scan((const char *)ring_[s], len, off);
                 std::lock_guard<std::mutex> lk(mu);
                 if (!r) {
                     rerr = er ? er : EIO;
@@ -359,8 +365,16 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
     bool batching = !(getenv("VCFX_BGZF_BATCH") && getenv("VCFX_BGZF_BATCH")[0] == '0');
     const size_t batch_min = env_bytes("VCFX_BGZF_BATCH_MIN", 16384);  // (~64 MB compressed; tests: 1)
     std::vector<size_t> ends(nchunks);
+    // (VCFX_TIMING: where the loop's time goes -- waiting for the readers, the H2D stage call, the
+    // chain walk, the batch launches, waiting for a slot's DMA)
+    double t_fill = 0, t_stage = 0, t_stage0 = 0, t_feed = 0, t_batch = 0, t_dma = 0;
+    auto clk = [] { return std::chrono::steady_clock::now(); };
+    auto dms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
     for (size_t i = 0; i < nchunks && ok; i++) {
         const size_t s = i % S, off = i * kSlot, len = std::min(kSlot, total - off);
+        auto t0 = clk();
         {
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return stop || filled[s] == (long long)i; });
@@ -369,9 +383,14 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
                 break;
             }
         }
+        auto t1 = clk();
         ok = vcfxg_bgzf_stage(g, ring_[s], len, off, total) == VCFXG_OK;
-        chain.feed((const char *)ring_[s], len);
+        auto t2 = clk();
+        chain.adopt((const char *)ring_[s], len, scans[s]);
         ok = ok && !chain.bad;
+        auto t3 = clk();
+        t_fill += dms(t0, t1), t_stage += dms(t1, t2), t_feed += dms(t2, t3);
+        if (i == 0) t_stage0 = dms(t1, t2);
         // the members complete so far inflate on the device while the next chunks are read and
         // copied (batches of >= 16384 members, about 64 MB compressed, round robin on three streams:
         // 35 ms against 41 ms unbatched and 36.5 ms at 1024 on the bench shard; the rest at the end)
@@ -382,6 +401,8 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
             if (br == VCFXG_OK) launched = chain.members.size();
             else batching = false;  // (E_CAP: the output outgrew the hint; the rest at the end)
         }
+        auto t4 = clk();
+        t_batch += dms(t3, t4);
         ends[i] = off + len;
         if (ok && i >= inflight) {
             const size_t j = i - inflight;
@@ -390,6 +411,14 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
             freed[j % S] = (long long)j;
             cv.notify_all();
         }
+        t_dma += dms(t4, clk());
+    }
+    if (timing_on) {
+        char b[200];
+        snprintf(b, sizeof b,
+                 "bgzf stream loop: readers %.2f, stage %.2f (first %.2f), chain %.2f, batches %.2f, slot DMA %.2f ms",
+                 t_fill, t_stage, t_stage0, t_feed, t_batch, t_dma);
+        phase(b);
     }
     {
         std::lock_guard<std::mutex> lk(mu);
