@@ -8,6 +8,7 @@
 #include <fcntl.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
@@ -70,9 +71,10 @@ struct vcfxg_ctx {
     uint64_t bgz_launched = 0, bgz_out = 0;
     hipStream_t copy_stream = nullptr;
     hipEvent_t bgz_copy_ev = nullptr;  // the latest staged copy
-    // the inflate batches run round robin on their own streams (a batch is a few waves per CU:
-    // one stream would serialise each batch's tail), joined before the CRC pass
-    static constexpr int kBgzStreams = 3;
+    // the inflate batches run round robin on their own streams (one stream would serialise each
+    // batch's tail), joined before the device input completes; two: batches are 32,768 members
+    // (hostio.cpp), and a fresh context pays ~7 ms to create a stream
+    static constexpr int kBgzStreams = 2;
     hipStream_t bgz_stream[kBgzStreams] = {};
     hipEvent_t bgz_ev[kBgzStreams] = {};
     int bgz_next = 0;
@@ -433,6 +435,16 @@ static void reset_hints(vcfxg_ctx *c) {
 
 // the schedule a region call took (vcfxg_last_schedule; VCFXG_SCHEDULE_LOG=path appends one
 // line per call: tests check which path sharded ranks and fresh contexts run)
+// VCFX_TIMING=1: "[vcfxg-timing] <what> <ms>" on stderr at the steps of a fresh context's first
+// BGZF stage (ms since the library loaded; the host's own phases are hostio.cpp phase())
+static void lib_phase(const char *what) {
+    static const auto t0 = std::chrono::steady_clock::now();
+    static const bool on = getenv("VCFX_TIMING") && atoi(getenv("VCFX_TIMING")) > 0;
+    if (!on) return;
+    fprintf(stderr, "[vcfxg-timing] %s %.2f ms\n", what,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+}
+
 static void note_schedule(vcfxg_ctx *c, const char *what) {
     c->last_schedule = what;
     const char *log = getenv("VCFXG_SCHEDULE_LOG");  // (read per call: tests set it in-process)
@@ -626,10 +638,13 @@ int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, si
         }();
         const uint64_t mm = std::min<uint64_t>(bgz_max_members(comp_total),
                                                tset ? tset : std::max<uint64_t>(65536, comp_total / 1024));
+        lib_phase("bgzf stage: begin");
         int r = ensure(c, c->bgz_in, comp_total + kCompPad);
+        lib_phase("bgzf stage: compressed buffer");
         if (!r) r = bgz_tables(c, mm, 0);
         if (!r) r = ensure(c, c->bgz_small, 64);
         if (r) return r;
+        lib_phase("bgzf stage: member tables");
         if (!c->copy_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
         if (!c->bgz_copy_ev) HIPCHK(c, hipEventCreateWithFlags(&c->bgz_copy_ev, hipEventDisableTiming));
         for (int k = 0; k < vcfxg_ctx::kBgzStreams; k++) {
@@ -637,6 +652,7 @@ int vcfxg_bgzf_stage(vcfxg_ctx *c, const void *host, size_t n, size_t offset, si
             if (!c->bgz_ev[k]) HIPCHK(c, hipEventCreateWithFlags(&c->bgz_ev[k], hipEventDisableTiming));
         }
         c->bgz_next = 0;
+        lib_phase("bgzf stage: streams");
         // (the first-bad marker and the hand-over count, then the stream's earlier work -- buffers
         // just reallocated, the last call's kernels: every batch is ordered after this event)
         HIPCHK(c, hipMemsetAsync(c->bgz_small.p, 0xFF, 8, c->stream));
@@ -687,8 +703,10 @@ static uint64_t bgz_tokens(vcfxg_ctx *c, int k, uint64_t count, hipStream_t st) 
             b.p = nullptr;
             b.cap = 0;
         }
-        if (hipMalloc(&b.p, want * per + 4) == hipSuccess) {
-            b.cap = want * per + 4;
+        // (rounded up to 8,192 members: a batch a few members past the last one's size reuses it)
+        const uint64_t alloc = std::min<uint64_t>((want + 8191) / 8192 * 8192, std::max<uint64_t>(want, 69632));
+        if (hipMalloc(&b.p, alloc * per + 4) == hipSuccess) {
+            b.cap = alloc * per + 4;
             return want;
         }
         (void)hipGetLastError();
@@ -718,6 +736,18 @@ static int bgz_aux(vcfxg_ctx *c) {
     return VCFXG_OK;
 }
 
+// the CRC-32 pass's "1 KiB of zeros" basis
+static const vcfxg::Crc1k &crc_basis() {
+    static const vcfxg::Crc1k z = [] {
+        vcfxg::Crc1k b;
+        vcfxg::crc32_zero1k_basis(&b);
+        return b;
+    }();
+    return z;
+}
+
+// members [first, first + count) of a staged stream: the tables, the inflate and its CRC-32 pass
+// on `st` (so the last batch's check does not wait for a pass over every member)
 static int bgz_launch(vcfxg_ctx *c, const vcfxg_bgzf_member *mem, uint64_t first, uint64_t count,
                       hipStream_t st, int slot) {
     if (!count) return VCFXG_OK;
@@ -733,13 +763,14 @@ static int bgz_launch(vcfxg_ctx *c, const vcfxg_bgzf_member *mem, uint64_t first
                              hipMemcpyHostToDevice, st));
     HIPCHK(c, hipMemcpyAsync(P<uint64_t>(c->bgz_off) + first, off.data(), 8 * count, hipMemcpyHostToDevice, st));
     HIPCHK(c, hipStreamWaitEvent(st, c->bgz_copy_ev, 0));
-    static vcfxg::Crc1k z1k_unused{};
     const uint64_t tm = bgz_tokens(c, slot, count, st);
     if (int r = bgz_aux(c)) return r;
-    HIPCHK(c, vcfxg::launch_inflate(0, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem) + first,
-                                    P<uint64_t>(c->bgz_off) + first, count, P<uint8_t>(c->input) + c->n,
-                                    P<uint32_t>(c->bgz_stat) + first, P<unsigned long long>(c->bgz_small), z1k_unused,
-                                    st, first, P<uint32_t>(c->bgz_tok[slot]), tm, P<uint32_t>(c->bgz_perm) + first, &c->bgz_side));
+    for (int which = 0; which < 2; which++)
+        HIPCHK(c, vcfxg::launch_inflate(which, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem) + first,
+                                        P<uint64_t>(c->bgz_off) + first, count, P<uint8_t>(c->input) + c->n,
+                                        P<uint32_t>(c->bgz_stat) + first, P<unsigned long long>(c->bgz_small),
+                                        crc_basis(), st, first, P<uint32_t>(c->bgz_tok[slot]), tm,
+                                        P<uint32_t>(c->bgz_perm) + first, &c->bgz_side));
     c->bgz_launched = first + count;
     c->bgz_out = o;
     return VCFXG_OK;
@@ -825,11 +856,7 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         if (!r) r = ensure(c, c->bgz_perm, 4 * (nm + 1));
         if (r) return r;
     }
-    static vcfxg::Crc1k z1k = [] {
-        vcfxg::Crc1k z;
-        vcfxg::crc32_zero1k_basis(&z);
-        return z;
-    }();
+    const vcfxg::Crc1k &z1k = crc_basis();
     if (staged) {
         // the members not launched yet
         prof_begin(c, "bgzf_inflate");
@@ -859,9 +886,10 @@ int vcfxg_ingest_bgzf(vcfxg_ctx *c, const void *comp, size_t comp_n, const vcfxg
         prof_end(c, "bgzf_inflate");
     }
     prof_begin(c, "bgzf_crc32");
-    HIPCHK(c, vcfxg::launch_inflate(1, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem), P<uint64_t>(c->bgz_off),
-                                    nm, P<uint8_t>(c->input) + c->n, P<uint32_t>(c->bgz_stat),
-                                    P<unsigned long long>(c->bgz_small), z1k, c->stream));
+    if (!staged)  // (a staged stream's batches checked their own members, bgz_launch)
+        HIPCHK(c, vcfxg::launch_inflate(1, P<uint8_t>(c->bgz_in), P<vcfxg::BgzfMember>(c->bgz_mem),
+                                        P<uint64_t>(c->bgz_off), nm, P<uint8_t>(c->input) + c->n,
+                                        P<uint32_t>(c->bgz_stat), P<unsigned long long>(c->bgz_small), z1k, c->stream));
     prof_end(c, "bgzf_crc32");
     // the first bad member, the hand-over count and its reasons (32-bit words 3..14)
     static thread_local uint64_t small[8];

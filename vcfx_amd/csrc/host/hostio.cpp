@@ -274,7 +274,12 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
         return false;
     }
     phase("bgzf head inflated");
-    const size_t kSlot = file_slot();
+    bool batching = !(getenv("VCFX_BGZF_BATCH") && getenv("VCFX_BGZF_BATCH")[0] == '0');
+    const size_t batch_min = env_bytes("VCFX_BGZF_BATCH_MIN", 32768);  // (~128 MB compressed; tests: 1)
+    // (a ring of 8 x 8 MiB, a third of the text path's 12 x 16 MiB: pinning costs ~0.2 ms per MiB in
+    // a fresh process, and the compressed bytes are 17x fewer; VCFX_FILE_SLOT / _SLOTS override)
+    const size_t kSlot = env_bytes("VCFX_FILE_SLOT", (size_t)8 << 20);
+    const size_t kSlots = std::max<size_t>(2, env_bytes("VCFX_FILE_SLOTS", 8));
     std::vector<void *> ring_;
     {
         std::lock_guard<std::mutex> lk(g_ring_mu);
@@ -282,12 +287,12 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
             munmap(hm, kHeadMax);
             return false;
         }
-        if (g_file_ring.ctx != g || g_file_ring.slot != kSlot || g_file_ring.slots.size() != file_slots()) {
+        if (g_file_ring.ctx != g || g_file_ring.slot != kSlot || g_file_ring.slots.size() != kSlots) {
             if (g_file_ring.ctx)
                 for (void *r : g_file_ring.slots) vcfxg_host_free(g_file_ring.ctx, r);
             g_file_ring = FileRing{};
             bool ok = true;
-            for (size_t i = 0; i < file_slots() && ok; i++) {
+            for (size_t i = 0; i < kSlots && ok; i++) {
                 void *r = nullptr;
                 ok = vcfxg_host_alloc(g, kSlot, &r) == VCFXG_OK;
                 if (ok) g_file_ring.slots.push_back(r);
@@ -315,10 +320,12 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
     // inflate batches launched during the stream have their room; more grows it at the end.
     // vcfxg_ingest_begin cuts a hint past half the device's free memory; when even the cut one
     // cannot be had, 6x: the batches that do not fit wait for the end, E_CAP)
+    phase("bgzf ring ready");
     if (ring_.empty() || (vcfxg_ingest_begin(g, 24 * total) != VCFXG_OK && vcfxg_ingest_begin(g, 6 * total) != VCFXG_OK)) {
         munmap(hm, kHeadMax);
         return false;
     }
+    phase("bgzf input buffer ready");
     // chunk i = [i*slot, ...) into slot i % S, read by T reader threads, staged in order by this
     // thread (which parses the member chain from the slot before its DMA is waited for)
     const size_t S = ring_.size(), inflight = std::max<size_t>(1, S / 2);
@@ -362,8 +369,6 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
         });
     BgzfStream chain;
     size_t launched = 0;
-    bool batching = !(getenv("VCFX_BGZF_BATCH") && getenv("VCFX_BGZF_BATCH")[0] == '0');
-    const size_t batch_min = env_bytes("VCFX_BGZF_BATCH_MIN", 16384);  // (~64 MB compressed; tests: 1)
     std::vector<size_t> ends(nchunks);
     // (VCFX_TIMING: where the loop's time goes -- waiting for the readers, the H2D stage call, the
     // chain walk, the batch launches, waiting for a slot's DMA)
@@ -392,8 +397,9 @@ bool Input::stream_bgzf_device(int fd, size_t total, const char *first, size_t f
         t_fill += dms(t0, t1), t_stage += dms(t1, t2), t_feed += dms(t2, t3);
         if (i == 0) t_stage0 = dms(t1, t2);
         // the members complete so far inflate on the device while the next chunks are read and
-        // copied (batches of >= 16384 members, about 64 MB compressed, round robin on three streams:
-        // 35 ms against 41 ms unbatched and 36.5 ms at 1024 on the bench shard; the rest at the end)
+        // copied (batches of >= 32,768 members, about 128 MB compressed, round robin on two
+        // streams, each checking its own CRCs; the rest at the end.  r06, the bench shard with the
+        // context open: 21-25 ms against 24-36 at 16,384, 25 at 24,576 and 22-50 unbatched)
         if (ok && batching && chain.members.size() - launched >= batch_min) {
             const int br = vcfxg_bgzf_inflate(g, reinterpret_cast<const vcfxg_bgzf_member *>(chain.members.data()) +
                                                      launched,
@@ -1276,6 +1282,7 @@ bool load_input(vcfxg_ctx *g, const Input &in, int err_fd) {
     }
     if (in.stream_ctx == g && in.streamed == in.n) {
         // the bytes are on the device already (streamed while stdin was read); complete it
+        phase("completing the device input");
         return gpu_ok(g, vcfxg_ingest(g, nullptr, 0, 1), "ingest", err_fd);
     }
     if (in.host_n != in.n) {  // a device-only stream whose ingest failed: nothing to redo
