@@ -132,3 +132,35 @@ def test_allele_counter_long_rows_and_identity_selection(oracle, tmp_path):
     T = "VCFX_allele_counter"
     for argv in ([T, "-q", "-i", p], [T, "-q", "-s", " ".join(nm[::-1]), "-i", p], [T, "-q", "-s", " ".join(nm), "-i", p]):
         _check(oracle, argv)
+
+
+@pytest.mark.parametrize("L", [1, 6, 11, 12])
+def test_allele_counter_direct_rows(oracle, L, tmp_path, monkeypatch):
+    """k_ac_rows (text rows written straight from registers: names of one length L <= 11, record
+    prefixes of 16..64 bytes) beside k_ac_fmt for the other records: prefixes on both sides of
+    16 / 32 / 48 / 64 bytes, records with fewer samples than the selection (all: 0 / 0 past them;
+    seq: the rows stop), 130 samples (a partial last tile), the identity selection, a reordered
+    one and a limit; and the same calls with k_ac_rows off (VCFXG_AC_DIRECT=0)."""
+    import random
+    rnd = random.Random(L)
+    ns = 130
+    names = ["%0*d" % (L, k) if L > 1 else chr(65 + k % 26) for k in range(ns)]
+    head = "##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + "\t".join(names) + "\n"
+    rows = []
+    for k, P in enumerate([15, 16, 17, 31, 32, 33, 47, 48, 49, 63, 64, 65, 80, 20, 40, 60]):
+        rid = ("r%d_" % k + "x" * 80)[:P - 9]
+        for n in (ns, 100):
+            gts = "\t".join("%d%s%d" % (rnd.randint(0, 1), rnd.choice("|/"), rnd.randint(0, 2)) for _ in range(n))
+            rows.append("1\t%d\t%s\tA\tC\t.\t.\t.\tGT\t%s\n" % (k + 1, rid, gts))
+    buf = (head + "".join(rows)).encode()
+    path = tmp_path / "d.vcf"
+    path.write_bytes(buf)
+    p = str(path)
+    pick = " ".join(names[::-3])
+    T = "VCFX_allele_counter"
+    for direct in ("1", "0"):
+        monkeypatch.setenv("VCFXG_AC_DIRECT", direct)
+        for argv in ([T, "-q", "-i", p], [T, "-q", "-s", pick, "-i", p], [T, "-q", "-l", "7", "-i", p],
+                     [T, "-q", "-s", " ".join(names), "-a", p]):
+            _check(oracle, argv)
+        _check(oracle, [T, "-q"], buf)

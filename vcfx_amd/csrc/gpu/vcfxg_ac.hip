@@ -33,6 +33,7 @@ namespace vcfxg {
 #ifndef VCFXG_AC_EXPT
 #define VCFXG_AC_EXPT 0
 #endif
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 constexpr int kAcThreads = 512;  // 8 waves share one LDS copy of the selection (r02: 256 -> 512)
 constexpr int kAcWaves = kAcThreads / kWave;
 constexpr int kAcTile = 3072;  // LDS bytes per wave for one tile of 64 text rows (longer: straight out)
@@ -60,7 +61,15 @@ struct AcArgs {
     int seq, kind;
     uint32_t sel_lds;      // k_ac_fmt: the selection (eff, name offsets, names) copied to LDS (its bytes; 0: read from global memory)
     uint32_t ident;        // k_ac_fmt: eff[i] == i for every slot (no index array in LDS)
+    uint32_t direct;       // text rows: k_ac_rows writes the records ac_direct_rec accepts (k_ac_fmt skips them)
 };
+
+// the direct rows (k_ac_rows): a fixed-stride record whose prefix is 16..64 bytes, under a text
+// selection whose names all have one length L <= 11 (the host's check, A.direct)
+constexpr uint32_t kAcDirectP = 64;
+__device__ __forceinline__ bool ac_direct_rec(const AcArgs &A, const AcMeta &m) {
+    return A.direct && m.kind == kAcFast && m.P >= 16 && m.P <= kAcDirectP;
+}
 
 struct AcNullOp {
     __device__ void begin(uint32_t, uint32_t) {}
@@ -169,13 +178,13 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_len(const char *__restrict__ 
                                                        AcMeta *__restrict__ meta,
                                                        unsigned long long *__restrict__ counters) {
     __shared__ int64_t scratch[kAcWaves][16];
-    __shared__ unsigned long long red[4][kAcWaves];
+    __shared__ unsigned long long red[5][kAcWaves];
     int64_t *lds = scratch[threadIdx.x / kWave];
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
     uint32_t *tab = A.scratch + wid * (uint64_t)A.scap;
     unsigned long long rows_all = 0;
-    uint32_t data = 0, chrom = 0, gen = 0;  // (wave-uniform)
+    uint32_t data = 0, chrom = 0, gen = 0, slow = 0;  // (wave-uniform)
     for (uint64_t li = l0 + wid; li < l1; li += nw) {
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
         uint8_t st = 0;
@@ -248,6 +257,7 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_len(const char *__restrict__ 
                     text = wave_sum(text);
                 }
                 m.rows = rows;
+                slow += !ac_direct_rec(A, m);
                 if (A.kind == 1) {
                     sr = wave_sum(sr);
                     sa = wave_sum(sa);
@@ -271,9 +281,10 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_len(const char *__restrict__ 
         red[1][threadIdx.x / kWave] = data;
         red[2][threadIdx.x / kWave] = chrom;
         red[3][threadIdx.x / kWave] = gen;
+        red[4][threadIdx.x / kWave] = slow;
     }
     __syncthreads();
-    if (threadIdx.x < 4) {
+    if (threadIdx.x < 5) {
         unsigned long long t = 0;
         for (int k = 0; k < kAcWaves; k++) t += red[threadIdx.x][k];
         if (t) atomicAdd(&counters[threadIdx.x], t);
@@ -290,6 +301,10 @@ __device__ __forceinline__ void put_int(char *o, int64_t v, uint32_t nb) {
     }
 }
 
+// kSel: the selection sits in LDS (A.sel_lds != 0).  A compile-time choice: with both forms in one
+// body the tile loop's name offsets came from an LDS read or a global load, and the join waited
+// vmcnt(0) every tile -- on the previous tile's stores (loads and stores share vmcnt)
+template <bool kSel>
 __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ buf, int64_t data_start,
                                                        const uint64_t *__restrict__ line_end, uint64_t l0, uint64_t l1,
                                                        AcArgs A, const uint8_t *__restrict__ status,
@@ -302,7 +317,7 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
     extern __shared__ __attribute__((aligned(16))) char sel_all[];
     uint32_t *s_eff = reinterpret_cast<uint32_t *>(sel_all), *s_noff = s_eff + (A.ident ? 0u : A.m);
     char *s_names = reinterpret_cast<char *>(s_noff + A.m + 1);
-    if (A.sel_lds) {
+    if (kSel) {
         for (uint32_t k = threadIdx.x; k <= A.m; k += blockDim.x) {
             if (k < A.m && !A.ident) s_eff[k] = A.eff[k];
             s_noff[k] = (uint32_t)A.noff[k];
@@ -310,9 +325,9 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
         for (uint64_t k = threadIdx.x; k < A.noff[A.m]; k += blockDim.x) s_names[k] = A.names[k];
         __syncthreads();
     }
-    auto EFF = [&](uint32_t i) -> uint32_t { return A.ident ? i : A.sel_lds ? s_eff[i] : A.eff[i]; };
-    auto NOFF = [&](uint32_t i) -> uint64_t { return A.sel_lds ? (uint64_t)s_noff[i] : A.noff[i]; };
-    auto NAME = [&](uint64_t k) -> char { return A.sel_lds ? s_names[k] : A.names[k]; };
+    auto EFF = [&](uint32_t i) -> uint32_t { return A.ident ? i : kSel ? s_eff[i] : A.eff[i]; };
+    auto NOFF = [&](uint32_t i) -> uint64_t { return kSel ? (uint64_t)s_noff[i] : A.noff[i]; };
+    auto NAME = [&](uint64_t k) -> char { return kSel ? s_names[k] : A.names[k]; };
     char *tile = tile_all[threadIdx.x / kWave];
     char *pre = pre_all[threadIdx.x / kWave];
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
@@ -322,6 +337,7 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
         if (status[li] != 1) continue;  // (wave-uniform)
         const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start, le = (int64_t)line_end[li];
         const AcMeta m = meta[li];
+        if (ac_direct_rec(A, m)) continue;  // (k_ac_rows' record)
         char *o = out + off[li - l0];
         const int64_t S = (int64_t)m.S;
         const uint32_t P = m.P;
@@ -470,7 +486,7 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
             for (uint64_t blk = a0 + 16ull * lane(); blk < cend && !(VCFXG_AC_EXPT & 2); blk += 16ull * kWave) {
                 const char *src = tile + (blk - a0);
                 if (blk >= lo && blk + 16 <= cend)
-                    *reinterpret_cast<uint4 *>(out + blk) = *reinterpret_cast<const uint4 *>(src);
+                    *reinterpret_cast<v4u *>(out + blk) = *reinterpret_cast<const v4u *>(src);
                 else
                     for (int k = 0; k < 16; k++)
                         if (blk + k >= lo && blk + k < cend) out[blk + k] = src[k];
@@ -490,10 +506,132 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
     }
 }
 
+// k_ac_rows: the text rows of the records ac_direct_rec accepts, straight from registers to the
+// output -- no LDS image, no copy-out.  Every row is P + L + 5 bytes: the record's prefix, the
+// slot's name, "\t" r "\t" a "\n".  A lane per row writes it as unaligned 16 B stores:
+//   prefix [0, 16) (and [16, 32), [32, 48) when P exceeds them), prefix [P - 16, P), and the
+//   row's last 16 bytes: 11 - L prefix bytes, the name, '\t', r, '\t', a, '\n'.
+// The pieces overlap only where they carry the same bytes, so their order does not matter, and
+// none leaves the row (P >= 16).  The last piece comes from the slot's entry in LDS (etab: the
+// name right-aligned before "\t0\t0\n", zeros in front), the record's prefix bytes ORed into
+// its zeros and the counts into its last dword.  r02-r06 composed the rows in an LDS image and
+// copied it out; the image's round trips, not the stores, bounded that kernel (ablations in
+// DESIGN §3), and 16 B stores at any alignment sustain the store rate (tools/microbench).
+constexpr int kAcRowsThreads = 1024;  // 16 waves share one LDS copy of etab
+constexpr int kAcRowsWaves = kAcRowsThreads / kWave;
+template <bool kIdent>
+__global__ __launch_bounds__(kAcRowsThreads, 8) void k_ac_rows(const char *__restrict__ buf, int64_t data_start,
+                                                            const uint64_t *__restrict__ line_end, uint64_t l0,
+                                                            uint64_t l1, AcArgs A, const v4u *__restrict__ etab,
+                                                            uint32_t L, const uint8_t *__restrict__ status,
+                                                            const AcMeta *__restrict__ meta,
+                                                            const uint64_t *__restrict__ off, char *__restrict__ out) {
+    // dynamic LDS (ac_rows_lds): the m entries, (!kIdent) the m sample indices, and per wave the
+    // counts of its record, 16 tiles' nibbles per lane and uint64 (ceil(m / 1024) of them)
+    extern __shared__ v4u s_e[];
+    __shared__ __attribute__((aligned(16))) char pre_all[kAcRowsWaves][kAcDirectP + 16];
+    uint32_t *s_eff = reinterpret_cast<uint32_t *>(s_e + A.m);
+    const uint32_t nbat = (A.m + 1023u) / 1024u;
+    uint64_t *s_nib = reinterpret_cast<uint64_t *>(s_e + A.m + (kIdent ? 0u : (A.m + 3u) / 4u)) +
+                      (uint64_t)(threadIdx.x / kWave) * nbat * kWave + lane();
+    for (uint32_t k = threadIdx.x; k < A.m; k += blockDim.x) {
+        s_e[k] = etab[k];
+        if (!kIdent) s_eff[k] = A.eff[k];
+    }
+    __syncthreads();
+    char *pre = pre_all[threadIdx.x / kWave];
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    const uint32_t kp = 11u - L;  // prefix bytes in an entry's front
+    for (uint64_t li = l0 + wid; li < l1; li += nw) {
+        if (status[li] != 1) continue;  // (wave-uniform)
+        const AcMeta m = meta[li];
+        if (!ac_direct_rec(A, m)) continue;
+        const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
+        char *o = out + off[li - l0];
+        const int64_t S = (int64_t)m.S;
+        const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)m.P), rl = P + L + 5u;
+        if ((uint32_t)lane() < P) pre[lane()] = (uint32_t)lane() < m.lim ? buf[ls + lane()] : '\t';
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        v4u c0v, c1, c2v, cl, pm;
+        __builtin_memcpy(&c0v, pre, 16);
+        __builtin_memcpy(&c1, pre + 16, 16);
+        __builtin_memcpy(&c2v, pre + 32, 16);
+        __builtin_memcpy(&cl, pre + P - 16, 16);
+        __builtin_memcpy(&pm, pre + P - kp, 16);
+        pm.x &= kp >= 4 ? ~0u : (1u << (8 * kp)) - 1u;
+        pm.y &= kp >= 8 ? ~0u : kp <= 4 ? 0u : (1u << (8 * (kp - 4))) - 1u;
+        pm.z &= kp <= 8 ? 0u : (1u << (8 * (kp - 8))) - 1u;  // (kp <= 11)
+        const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane((int)m.rows);
+        const uint32_t ns = (uint32_t)__builtin_amdgcn_readfirstlane((int)m.ns);
+        if (R == 0) continue;
+        // the record's counts first, 16 tiles at a time as nibbles r | a << 2 in one uint64 per lane,
+        // into the wave's LDS: the 16 GT dwords ("a|b\t", the dword may be unaligned) are issued
+        // together and waited for once.  Loads and stores share vmcnt, so a load among the rows'
+        // stores would drain them (a load batch every 16 tiles: 8.9 -> 11.1 ms in
+        // tools/microbench/store_fronts.hip); here only the record's first batch waits behind the
+        // previous record's stores, as its metadata loads do anyway.  Relaxed wave-scope atomic
+        // loads: plain ones (a read-only input) were re-issued one by one at their uses.
+        auto counts16 = [&](uint32_t i0) -> uint64_t {
+            uint64_t pk = 0;
+#pragma unroll
+            for (int h = 0; h < 16; h += 8) {  // (8 loads at a time: 64 VGPRs for 2 blocks per CU)
+                uint32_t g[8];
+#pragma unroll
+                for (int kk = 0; kk < 8; kk++) {
+                    const uint32_t i = min(i0 + (h + kk) * kWave + (uint32_t)lane(), R - 1);
+                    const uint32_t e = kIdent ? i : s_eff[i];
+                    g[kk] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(buf + S + 4 * (uint64_t)(e < ns ? e : 0u)),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                }
+#pragma unroll
+                for (int kk = 0; kk < 8; kk++) {
+                    const uint32_t i = min(i0 + (h + kk) * kWave + (uint32_t)lane(), R - 1);
+                    const uint32_t gc = (kIdent ? i : s_eff[i]) < ns ? g[kk] : 0u;  // (a slot past the samples: 0 / 0)
+                    const uint32_t c0 = gc & 255u, c2 = (gc >> 16) & 255u;
+                    const uint32_t r = (c0 == '0') + (c2 == '0'), a = (c0 - '1' < 9u) + (c2 - '1' < 9u);
+                    pk |= (uint64_t)(r | a << 2) << (4 * (h + kk));
+                }
+            }
+            return pk;
+        };
+        // kNp: the prefix pieces before [P - 16, P) (1: P <= 32, 2: P <= 48, 3: P <= 64); a loop per
+        // count, so that no store in it is conditional; lanes past the last row repeat it (same
+        // bytes to the same places)
+        auto rows = [&](auto np) {
+            constexpr int kNp = decltype(np)::value;
+            uint64_t pk = 0;
+            for (uint32_t i0 = 0; i0 < R; i0 += kWave) {
+                const uint32_t t = i0 / kWave;
+                if ((t & 15) == 0) pk = s_nib[(t >> 4) * kWave];  // (this lane's own entry)
+                const uint32_t nib = (uint32_t)(pk >> (4 * (t & 15))) & 15u;
+                const uint32_t i = min(i0 + (uint32_t)lane(), R - 1);
+                char *q = o + (uint64_t)(i * rl);  // (a record's text is < 4 GiB)
+                __builtin_memcpy(q, &c0v, 16);
+                if (kNp > 1) __builtin_memcpy(q + 16, &c1, 16);
+                if (kNp > 2) __builtin_memcpy(q + 32, &c2v, 16);
+                __builtin_memcpy(q + P - 16, &cl, 16);
+                v4u e = s_e[i];
+                e.x |= pm.x;
+                e.y |= pm.y;
+                e.z |= pm.z;
+                e.w = 0x0A000900u | ('0' + (nib & 3u)) | (('0' + (nib >> 2)) << 16);
+                __builtin_memcpy(q + rl - 16, &e, 16);
+            }
+        };
+        for (uint32_t b = 0; b * 16u * kWave < R; b++) s_nib[b * kWave] = counts16(b * 16u * kWave);
+        if (P <= 32) rows(std::integral_constant<int, 1>{});
+        else if (P <= 48) rows(std::integral_constant<int, 2>{});
+        else rows(std::integral_constant<int, 3>{});
+    }
+}
+
 size_t ac_meta_bytes() { return sizeof(AcMeta); }
 
 static AcArgs ac_args(const uint32_t *eff, const uint64_t *noff, const char *names, uint32_t *scratch, uint32_t m,
-                      uint32_t scap, int seq, int kind, uint32_t sel_lds = 0, int ident = 0) {
+                      uint32_t scap, int seq, int kind, uint32_t sel_lds = 0, int ident = 0, int direct = 0) {
     AcArgs A;
     A.ident = ident ? 1u : 0u;
     A.eff = eff;
@@ -505,16 +643,17 @@ static AcArgs ac_args(const uint32_t *eff, const uint64_t *noff, const char *nam
     A.seq = seq;
     A.kind = kind;
     A.sel_lds = sel_lds;
+    A.direct = direct ? 1u : 0u;
     return A;
 }
 
 hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
-                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, int ident, uint8_t *status,
-                         uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s) {
+                         uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, int ident, int direct,
+                         uint8_t *status, uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s) {
     if (l1 <= l0) return hipSuccess;
     hipLaunchKernelGGL(k_ac_len, dim3(blocks), dim3(kAcThreads), 0, s, buf, data_start, line_end, l0, l1,
-                       ac_args(eff, noff, names, scratch, m, scap, seq, kind, 0, ident), status, len,
+                       ac_args(eff, noff, names, scratch, m, scap, seq, kind, 0, ident, direct), status, len,
                        static_cast<AcMeta *>(meta), counters);
     return hipGetLastError();
 }
@@ -522,15 +661,40 @@ hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *li
 hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
                          uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint32_t sel_lds,
-                         int ident, const uint8_t *status, const void *meta, const uint64_t *off, char *out,
-                         hipStream_t s) {
+                         int ident, int direct, const uint8_t *status, const void *meta, const uint64_t *off,
+                         char *out, hipStream_t s) {
     if (l1 <= l0) return hipSuccess;
-    hipLaunchKernelGGL(k_ac_fmt, dim3(blocks), dim3(kAcThreads), sel_lds, s, buf, data_start, line_end, l0, l1,
-                       ac_args(eff, noff, names, scratch, m, scap, seq, kind, sel_lds, ident), status,
-                       static_cast<const AcMeta *>(meta), off, out);
+    const AcArgs A = ac_args(eff, noff, names, scratch, m, scap, seq, kind, sel_lds, ident, direct);
+    if (sel_lds)
+        hipLaunchKernelGGL(k_ac_fmt<true>, dim3(blocks), dim3(kAcThreads), sel_lds, s, buf, data_start, line_end, l0,
+                           l1, A, status, static_cast<const AcMeta *>(meta), off, out);
+    else
+        hipLaunchKernelGGL(k_ac_fmt<false>, dim3(blocks), dim3(kAcThreads), 0, s, buf, data_start, line_end, l0, l1, A,
+                           status, static_cast<const AcMeta *>(meta), off, out);
     return hipGetLastError();
 }
 
+hipError_t launch_ac_rows(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
+                          unsigned blocks, const uint32_t *eff, uint32_t m, int ident, const void *etab, uint32_t L,
+                          const uint8_t *status, const void *meta, const uint64_t *off, char *out, hipStream_t s) {
+    if (l1 <= l0) return hipSuccess;
+    const size_t lds = ac_rows_lds(m, ident);
+    if (L > 11 || m > 4096 || lds > ac_rows_lds_max()) return hipErrorInvalidValue;
+    const AcArgs A = ac_args(eff, nullptr, nullptr, nullptr, m, 0, 0, 0, 0, ident, 1);
+    if (ident)
+        hipLaunchKernelGGL(k_ac_rows<true>, dim3(blocks), dim3(kAcRowsThreads), lds, s, buf, data_start, line_end, l0, l1,
+                           A, static_cast<const v4u *>(etab), L, status, static_cast<const AcMeta *>(meta), off, out);
+    else
+        hipLaunchKernelGGL(k_ac_rows<false>, dim3(blocks), dim3(kAcRowsThreads), lds, s, buf, data_start, line_end, l0,
+                           l1, A, static_cast<const v4u *>(etab), L, status, static_cast<const AcMeta *>(meta), off, out);
+    return hipGetLastError();
+}
+
+size_t ac_rows_lds(uint32_t m, int ident) {
+    return 16 * (size_t)m + (ident ? 0 : 16 * (((size_t)m + 3) / 4)) + (size_t)kAcRowsWaves * ((m + 1023) / 1024) * kWave * 8;
+}
+size_t ac_rows_lds_max() { return 131072; }
+int ac_rows_threads() { return kAcRowsThreads; }
 int ac_threads() { return kAcThreads; }
 
 }  // namespace vcfxg

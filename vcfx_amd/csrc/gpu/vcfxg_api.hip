@@ -116,10 +116,11 @@ struct vcfxg_ctx {
     // VCFX_hwe_tester: hom-alt counts (dense, per walker), the host-recheck list and its length
     DevBuf hwe_aux, wk_aux, hwe_rc;
     // VCFX_allele_counter: slots' sample indices, name offsets and bytes, per-wave sample tables
-    DevBuf ac_eff, ac_noff, ac_names, ac_scratch;
+    DevBuf ac_eff, ac_noff, ac_names, ac_scratch, ac_etab;
     std::vector<uint32_t> ac_eff_host;
     std::vector<uint64_t> ac_noff_host;
     std::string ac_names_host;
+    std::vector<uint8_t> ac_etab_host;
     // VCFX_haplotype_phaser: genotype rows (by line), per-line info, variant -> line, pair flags
     DevBuf ph_G, ph_isvar, ph_info, ph_vnum, ph_vline, ph_flags, ph_r2;
     uint64_t ph_nvar = 0;
@@ -2190,6 +2191,25 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
     for (uint64_t i = 0; i < m && ident; i++) ident = c->ac_eff_host[i] == i;
     const uint64_t sel_bytes = (((ident ? 0 : 4 * m) + 4 * (m + 1) + (p->name_off[m] - p->name_off[0]) + 15) / 16) * 16;
     const uint32_t sel_lds = sel_bytes <= 40960 && !getenv("VCFXG_AC_SEL_GLOBAL") ? (uint32_t)sel_bytes : 0u;
+    // text rows under a selection whose names share one length L <= 11: k_ac_rows writes the
+    // fixed-stride records straight from registers (vcfxg_ac.hip); VCFXG_AC_DIRECT=0 keeps every
+    // record on k_ac_fmt's LDS image (A/B and test hook)
+    static const bool direct_env = [] {
+        const char *e = getenv("VCFXG_AC_DIRECT");
+        return !(e && e[0] == '0');
+    }();
+    const uint64_t L0 = m ? p->name_off[1] - p->name_off[0] : 0;
+    bool direct = direct_env && p->kind == 0 && m > 0 && m <= 4096 && L0 <= 11 &&
+                  vcfxg::ac_rows_lds((uint32_t)m, ident ? 1 : 0) <= vcfxg::ac_rows_lds_max();
+    for (uint64_t i = 0; i < m && direct; i++) direct = p->name_off[i + 1] - p->name_off[i] == L0;
+    if (direct) {
+        c->ac_etab_host.assign(16 * m, 0);
+        for (uint64_t i = 0; i < m; i++) {
+            uint8_t *e = &c->ac_etab_host[16 * i];
+            std::memcpy(e + 11 - L0, c->ac_names_host.data() + p->name_off[i], (size_t)L0);
+            std::memcpy(e + 11, "\t0\t0\n", 5);
+        }
+    }
     // grid: a wave per line up to 2048 blocks, and at most 1 GiB of per-wave sample tables
     const uint64_t waves_per_block = (uint64_t)(vcfxg::ac_threads() / 64);
     uint64_t blocks = std::min<uint64_t>((n + waves_per_block - 1) / waves_per_block, 2048);
@@ -2198,12 +2218,15 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
     if (!r) r = ensure(c, c->ac_noff, 8 * (m + 1));
     if (!r) r = ensure(c, c->ac_names, nb + 1);
     if (!r) r = ensure(c, c->ac_scratch, 4 * scap * waves_per_block * blocks);
+    if (!r && direct) r = ensure(c, c->ac_etab, 16 * m);
     if (!r) r = af_buffers(c, L);
     if (!r) r = ensure(c, c->af_meta, vcfxg::ac_meta_bytes() * (L + 1));
     if (r) return r;
     HIPCHK(c, hipMemcpyAsync(c->ac_eff.p, c->ac_eff_host.data(), 4 * (m + 1), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->ac_noff.p, c->ac_noff_host.data(), 8 * (m + 1), hipMemcpyHostToDevice, c->stream));
     if (nb) HIPCHK(c, hipMemcpyAsync(c->ac_names.p, c->ac_names_host.data(), nb, hipMemcpyHostToDevice, c->stream));
+    if (direct)
+        HIPCHK(c, hipMemcpyAsync(c->ac_etab.p, c->ac_etab_host.data(), 16 * m, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 64, c->stream));
     HIPCHK(c, hipMemsetAsync(P<uint64_t>(c->rowlen) + n, 0, 8, c->stream));
     const char *buf = P<char>(c->input);
@@ -2211,25 +2234,33 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
     HIPCHK(c, vcfxg::launch_ac_len(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, (unsigned)blocks,
                                    P<uint32_t>(c->ac_eff), P<uint64_t>(c->ac_noff), P<char>(c->ac_names),
                                    P<uint32_t>(c->ac_scratch), (uint32_t)m, (uint32_t)scap, p->seq, p->kind,
-                                   ident ? 1 : 0, P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->af_meta.p,
+                                   ident ? 1 : 0, direct ? 1 : 0, P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->af_meta.p,
                                    P<unsigned long long>(c->counters), c->stream));
     prof_end(c, "ac_len");
     r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)n + 1);
     if (r) return r;
-    static thread_local uint64_t tail[5];
+    static thread_local uint64_t tail[6];
     HIPCHK(c, hipMemcpyAsync(&tail[0], P<uint64_t>(c->rowoff) + n, 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipMemcpyAsync(&tail[1], c->counters.p, 32, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&tail[1], c->counters.p, 40, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const uint64_t text = tail[0];
     r = ensure(c, c->text, text + 1);
     if (r) return r;
     prof_begin(c, "ac_fmt");
-    HIPCHK(c, vcfxg::launch_ac_fmt(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, (unsigned)blocks,
-                                   P<uint32_t>(c->ac_eff), P<uint64_t>(c->ac_noff), P<char>(c->ac_names),
-                                   P<uint32_t>(c->ac_scratch), (uint32_t)m, (uint32_t)scap, p->seq, p->kind, sel_lds,
-                                   ident ? 1 : 0, P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->rowoff),
-                                   P<char>(c->text),
-                                   c->stream));
+    if (direct) {
+        const uint64_t rw = (uint64_t)(vcfxg::ac_rows_threads() / 64);
+        const unsigned rb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + rw - 1) / rw, 1024));
+        HIPCHK(c, vcfxg::launch_ac_rows(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, rb,
+                                        P<uint32_t>(c->ac_eff), (uint32_t)m, ident ? 1 : 0, c->ac_etab.p, (uint32_t)L0,
+                                        P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
+                                        c->stream));
+    }
+    if (!direct || tail[5])  // (the records k_ac_rows does not take)
+        HIPCHK(c, vcfxg::launch_ac_fmt(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, (unsigned)blocks,
+                                       P<uint32_t>(c->ac_eff), P<uint64_t>(c->ac_noff), P<char>(c->ac_names),
+                                       P<uint32_t>(c->ac_scratch), (uint32_t)m, (uint32_t)scap, p->seq, p->kind, sel_lds,
+                                       ident ? 1 : 0, direct ? 1 : 0, P<uint8_t>(c->status), c->af_meta.p,
+                                       P<uint64_t>(c->rowoff), P<char>(c->text), c->stream));
     prof_end(c, "ac_fmt");
     HIPCHK(c, hipStreamSynchronize(c->stream));
     prof_collect(c);
