@@ -62,6 +62,7 @@ struct AcArgs {
     uint32_t sel_lds;      // k_ac_fmt: the selection (eff, name offsets, names) copied to LDS (its bytes; 0: read from global memory)
     uint32_t ident;        // k_ac_fmt: eff[i] == i for every slot (no index array in LDS)
     uint32_t direct;       // text rows: k_ac_rows writes the records ac_direct_rec accepts (k_ac_fmt skips them)
+    uint32_t ntile;        // direct: tiles per record in the nibble array (ceil(m / 64), 8 dwords each)
 };
 
 // the direct rows (k_ac_rows): a fixed-stride record whose prefix is 16..64 bytes, under a text
@@ -175,7 +176,7 @@ __device__ __forceinline__ void ac_slot_fast(const char *__restrict__ buf, int64
 __global__ __launch_bounds__(kAcThreads) void k_ac_len(const char *__restrict__ buf, int64_t data_start,
                                                        const uint64_t *__restrict__ line_end, uint64_t l0, uint64_t l1,
                                                        AcArgs A, uint8_t *__restrict__ status, uint64_t *__restrict__ len,
-                                                       AcMeta *__restrict__ meta,
+                                                       AcMeta *__restrict__ meta, uint32_t *__restrict__ nib,
                                                        unsigned long long *__restrict__ counters) {
     __shared__ int64_t scratch[kAcWaves][16];
     __shared__ unsigned long long red[5][kAcWaves];
@@ -257,7 +258,65 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_len(const char *__restrict__ 
                     text = wave_sum(text);
                 }
                 m.rows = rows;
-                slow += !ac_direct_rec(A, m);
+                const bool direct = ac_direct_rec(A, m);
+                slow += !direct;
+                if (direct && rows) {
+                    // k_ac_rows' counts: per tile of 64 rows 8 dwords, row i's nibble r | a << 2 at
+                    // bits 4 (i & 7) of dword (i & 63) / 8 (a lane past the last row: the last row's).
+                    // A lane makes one dword, rows 8 k .. 8 k + 7 of 512 (8 tiles' dwords are
+                    // contiguous: dword 8 t + j of the record is rows 64 t + 8 j ..): 8 loads, then a
+                    // store, no cross-lane step
+                    uint32_t *nb = nib + (li - l0) * (uint64_t)A.ntile * 8u;
+                    const uint32_t ns = m.ns;
+                    auto nib8 = [](const v4u &u) -> uint32_t {  // 4 GT dwords -> 4 nibbles
+                        uint32_t x = 0;
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const uint32_t c0 = u[q] & 255u, c2 = (u[q] >> 16) & 255u;
+                            const uint32_t r = (c0 == '0') + (c2 == '0'), a = (c0 - '1' < 9u) + (c2 - '1' < 9u);
+                            x |= (r | a << 2) << (4 * q);
+                        }
+                        return x;
+                    };
+                    // the identity selection over whole groups of 512 rows below the sample count:
+                    // a lane's 8 GT dwords are 32 contiguous bytes, 4 groups' loads in flight at once
+                    // (the memory parallelism this pass needs at 3 waves per SIMD)
+                    const uint32_t full = A.ident ? min(rows, ns) / (8 * kWave) * (8 * kWave) : 0u;
+                    uint32_t r0 = 0;
+                    for (; r0 + 4 * 8 * kWave <= full; r0 += 4 * 8 * kWave) {
+                        v4u u[8];
+#pragma unroll
+                        for (int h = 0; h < 4; h++) {
+                            const char *p = buf + S + 4 * (uint64_t)(r0 + h * 8 * kWave + 8u * lane());
+                            __builtin_memcpy(&u[2 * h], p, 16);  // (unaligned)
+                            __builtin_memcpy(&u[2 * h + 1], p + 16, 16);
+                        }
+#pragma unroll
+                        for (int h = 0; h < 4; h++)
+                            nb[(r0 + h * 8 * kWave) / 8u + lane()] = nib8(u[2 * h]) | nib8(u[2 * h + 1]) << 16;
+                    }
+                    for (; r0 < rows; r0 += 8 * kWave) {
+                        const uint32_t b = r0 + 8u * lane();
+                        uint32_t g[8], ev[8];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            const uint32_t i = min(b + q, rows - 1);
+                            ev[q] = A.ident ? i : A.eff[i];
+                            g[q] = __hip_atomic_load(
+                                reinterpret_cast<const uint32_t *>(buf + S + 4 * (uint64_t)(ev[q] < ns ? ev[q] : 0u)),
+                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);  // (unaligned: S + 4 e)
+                        }
+                        uint32_t x = 0;
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            const uint32_t gc = ev[q] < ns ? g[q] : 0u;  // (a slot past the samples: 0 / 0)
+                            const uint32_t c0 = gc & 255u, c2 = (gc >> 16) & 255u;
+                            const uint32_t r = (c0 == '0') + (c2 == '0'), a = (c0 - '1' < 9u) + (c2 - '1' < 9u);
+                            x |= (r | a << 2) << (4 * q);
+                        }
+                        if (b < ((rows + 63u) & ~63u)) nb[r0 / 8u + lane()] = x;  // (the last tile whole)
+                    }
+                }
                 if (A.kind == 1) {
                     sr = wave_sum(sr);
                     sa = wave_sum(sa);
@@ -514,44 +573,63 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
 // The pieces overlap only where they carry the same bytes, so their order does not matter, and
 // none leaves the row (P >= 16).  The last piece comes from the slot's entry in LDS (etab: the
 // name right-aligned before "\t0\t0\n", zeros in front), the record's prefix bytes ORed into
-// its zeros and the counts into its last dword.  r02-r06 composed the rows in an LDS image and
-// copied it out; the image's round trips, not the stores, bounded that kernel (ablations in
-// DESIGN §3), and 16 B stores at any alignment sustain the store rate (tools/microbench).
+// its zeros and the counts into its last dword.
+// The kernel issues no vector load: the record's metadata, prefix bytes and counts (k_ac_len's
+// nibbles, 32 B a tile) come by scalar loads (lgkmcnt).  Vector loads and stores share vmcnt, so
+// any vector load among the rows' stores waits for all of them: a load batch every 16 tiles made
+// the same stores 8.9 -> 11.1 ms (tools/microbench/store_fronts.hip), and this kernel with its
+// counts loaded per record 12.9 ms.  r02-r06 composed the rows in an LDS image and copied it
+// out; the image's round trips, not the stores, bounded that kernel.
 constexpr int kAcRowsThreads = 1024;  // 16 waves share one LDS copy of etab
 constexpr int kAcRowsWaves = kAcRowsThreads / kWave;
-template <bool kIdent>
+#define AC_CONST __attribute__((address_space(4)))  // (uniform loads through it are scalar loads)
+typedef unsigned int v8u __attribute__((ext_vector_type(8)));
+typedef unsigned int v16u __attribute__((ext_vector_type(16)));
+// (whole vectors: a select among the dwords of separate loads became one per-lane vector load)
 __global__ __launch_bounds__(kAcRowsThreads, 8) void k_ac_rows(const char *__restrict__ buf, int64_t data_start,
                                                             const uint64_t *__restrict__ line_end, uint64_t l0,
                                                             uint64_t l1, AcArgs A, const v4u *__restrict__ etab,
-                                                            uint32_t L, const uint8_t *__restrict__ status,
+                                                            uint32_t L, const uint32_t *__restrict__ nib,
                                                             const AcMeta *__restrict__ meta,
                                                             const uint64_t *__restrict__ off, char *__restrict__ out) {
-    // dynamic LDS (ac_rows_lds): the m entries, (!kIdent) the m sample indices, and per wave the
-    // counts of its record, 16 tiles' nibbles per lane and uint64 (ceil(m / 1024) of them)
-    extern __shared__ v4u s_e[];
-    __shared__ __attribute__((aligned(16))) char pre_all[kAcRowsWaves][kAcDirectP + 16];
-    uint32_t *s_eff = reinterpret_cast<uint32_t *>(s_e + A.m);
-    const uint32_t nbat = (A.m + 1023u) / 1024u;
-    uint64_t *s_nib = reinterpret_cast<uint64_t *>(s_e + A.m + (kIdent ? 0u : (A.m + 3u) / 4u)) +
-                      (uint64_t)(threadIdx.x / kWave) * nbat * kWave + lane();
-    for (uint32_t k = threadIdx.x; k < A.m; k += blockDim.x) {
-        s_e[k] = etab[k];
-        if (!kIdent) s_eff[k] = A.eff[k];
-    }
+    extern __shared__ v4u s_e[];  // (ac_rows_lds) the m entries
+    __shared__ __attribute__((aligned(16))) uint32_t pre_all[kAcRowsWaves][(kAcDirectP + 16) / 4 + 4];
+    for (uint32_t k = threadIdx.x; k < A.m; k += blockDim.x) s_e[k] = etab[k];
     __syncthreads();
-    char *pre = pre_all[threadIdx.x / kWave];
+    uint32_t *prew = pre_all[threadIdx.x / kWave];
     const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
     const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
     const uint32_t kp = 11u - L;  // prefix bytes in an entry's front
-    for (uint64_t li = l0 + wid; li < l1; li += nw) {
-        if (status[li] != 1) continue;  // (wave-uniform)
-        const AcMeta m = meta[li];
-        if (!ac_direct_rec(A, m)) continue;
-        const int64_t ls = li ? (int64_t)line_end[li - 1] + 1 : data_start;
-        char *o = out + off[li - l0];
-        const int64_t S = (int64_t)m.S;
-        const uint32_t P = (uint32_t)__builtin_amdgcn_readfirstlane((int)m.P), rl = P + L + 5u;
-        if ((uint32_t)lane() < P) pre[lane()] = (uint32_t)lane() < m.lim ? buf[ls + lane()] : '\t';
+    const uint32_t sub = lane() >> 3, shn = 4u * (lane() & 7u);  // this lane's nibble in a tile's 8 dwords
+    for (uint64_t lv = l0 + wid; lv < l1; lv += nw) {
+        const uint64_t li = (uint64_t)uniform64((int64_t)lv);  // (so that the loads below are scalar)
+        AcMeta m;  // (its dwords: a byte field alone would be a vector load)
+        {
+            const v8u a = *(const AC_CONST v8u *)(meta + li);
+            const v4u b = *(const AC_CONST v4u *)((const char *)(meta + li) + 32);
+            m.S = (uint64_t)a[0] | (uint64_t)a[1] << 32;
+            m.P = a[6];
+            m.rows = a[7];
+            m.ns = b[0];
+            m.lim = b[1];
+            m.kind = (uint8_t)b[2];
+        }
+        if (!ac_direct_rec(A, m)) continue;  // (every other line: k_ac_fmt or no row)
+        const uint32_t R = m.rows;
+        if (R == 0) continue;
+        const int64_t ls = li ? (int64_t)*(const AC_CONST uint64_t *)(line_end + li - 1) + 1 : data_start;
+        char *o = out + *(const AC_CONST uint64_t *)(off + li - l0);
+        const uint32_t P = m.P, rl = P + L + 5u;
+        // the prefix: 17 dwords from ls rounded down (P <= 64; the input has 256 zeroed bytes past
+        // its end) into the wave's LDS, tabs for the fields the line lacks, then the pieces
+        const AC_CONST uint32_t *pw = (const AC_CONST uint32_t *)(buf + (ls & ~(int64_t)3));
+        const v16u pv = *(const AC_CONST v16u *)pw;
+        uint32_t w = pw[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) w = lane() == j ? pv[j] : w;
+        if (lane() < 17) prew[lane()] = w;
+        char *pre = reinterpret_cast<char *>(prew) + (ls & 3);
+        if ((uint32_t)lane() >= m.lim && (uint32_t)lane() < P) pre[lane()] = '\t';
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -564,49 +642,18 @@ __global__ __launch_bounds__(kAcRowsThreads, 8) void k_ac_rows(const char *__res
         pm.x &= kp >= 4 ? ~0u : (1u << (8 * kp)) - 1u;
         pm.y &= kp >= 8 ? ~0u : kp <= 4 ? 0u : (1u << (8 * (kp - 4))) - 1u;
         pm.z &= kp <= 8 ? 0u : (1u << (8 * (kp - 8))) - 1u;  // (kp <= 11)
-        const uint32_t R = (uint32_t)__builtin_amdgcn_readfirstlane((int)m.rows);
-        const uint32_t ns = (uint32_t)__builtin_amdgcn_readfirstlane((int)m.ns);
-        if (R == 0) continue;
-        // the record's counts first, 16 tiles at a time as nibbles r | a << 2 in one uint64 per lane,
-        // into the wave's LDS: the 16 GT dwords ("a|b\t", the dword may be unaligned) are issued
-        // together and waited for once.  Loads and stores share vmcnt, so a load among the rows'
-        // stores would drain them (a load batch every 16 tiles: 8.9 -> 11.1 ms in
-        // tools/microbench/store_fronts.hip); here only the record's first batch waits behind the
-        // previous record's stores, as its metadata loads do anyway.  Relaxed wave-scope atomic
-        // loads: plain ones (a read-only input) were re-issued one by one at their uses.
-        auto counts16 = [&](uint32_t i0) -> uint64_t {
-            uint64_t pk = 0;
-#pragma unroll
-            for (int h = 0; h < 16; h += 8) {  // (8 loads at a time: 64 VGPRs for 2 blocks per CU)
-                uint32_t g[8];
-#pragma unroll
-                for (int kk = 0; kk < 8; kk++) {
-                    const uint32_t i = min(i0 + (h + kk) * kWave + (uint32_t)lane(), R - 1);
-                    const uint32_t e = kIdent ? i : s_eff[i];
-                    g[kk] = __hip_atomic_load(reinterpret_cast<const uint32_t *>(buf + S + 4 * (uint64_t)(e < ns ? e : 0u)),
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                }
-#pragma unroll
-                for (int kk = 0; kk < 8; kk++) {
-                    const uint32_t i = min(i0 + (h + kk) * kWave + (uint32_t)lane(), R - 1);
-                    const uint32_t gc = (kIdent ? i : s_eff[i]) < ns ? g[kk] : 0u;  // (a slot past the samples: 0 / 0)
-                    const uint32_t c0 = gc & 255u, c2 = (gc >> 16) & 255u;
-                    const uint32_t r = (c0 == '0') + (c2 == '0'), a = (c0 - '1' < 9u) + (c2 - '1' < 9u);
-                    pk |= (uint64_t)(r | a << 2) << (4 * (h + kk));
-                }
-            }
-            return pk;
-        };
+        const AC_CONST uint32_t *nt = (const AC_CONST uint32_t *)(nib + (li - l0) * (uint64_t)A.ntile * 8u);
         // kNp: the prefix pieces before [P - 16, P) (1: P <= 32, 2: P <= 48, 3: P <= 64); a loop per
         // count, so that no store in it is conditional; lanes past the last row repeat it (same
-        // bytes to the same places)
+        // bytes to the same places; k_ac_len gave them its nibble)
         auto rows = [&](auto np) {
             constexpr int kNp = decltype(np)::value;
-            uint64_t pk = 0;
-            for (uint32_t i0 = 0; i0 < R; i0 += kWave) {
-                const uint32_t t = i0 / kWave;
-                if ((t & 15) == 0) pk = s_nib[(t >> 4) * kWave];  // (this lane's own entry)
-                const uint32_t nib = (uint32_t)(pk >> (4 * (t & 15))) & 15u;
+            for (uint32_t i0 = 0, t = 0; i0 < R; i0 += kWave, t++) {
+                const v8u nd = *(const AC_CONST v8u *)(nt + 8u * t);
+                uint32_t d = nd[0];
+#pragma unroll
+                for (int j = 1; j < 8; j++) d = sub == (uint32_t)j ? nd[j] : d;
+                const uint32_t nb = (d >> shn) & 15u;
                 const uint32_t i = min(i0 + (uint32_t)lane(), R - 1);
                 char *q = o + (uint64_t)(i * rl);  // (a record's text is < 4 GiB)
                 __builtin_memcpy(q, &c0v, 16);
@@ -617,21 +664,23 @@ __global__ __launch_bounds__(kAcRowsThreads, 8) void k_ac_rows(const char *__res
                 e.x |= pm.x;
                 e.y |= pm.y;
                 e.z |= pm.z;
-                e.w = 0x0A000900u | ('0' + (nib & 3u)) | (('0' + (nib >> 2)) << 16);
+                e.w = 0x0A000900u | ('0' + (nb & 3u)) | (('0' + (nb >> 2)) << 16);
                 __builtin_memcpy(q + rl - 16, &e, 16);
             }
         };
-        for (uint32_t b = 0; b * 16u * kWave < R; b++) s_nib[b * kWave] = counts16(b * 16u * kWave);
         if (P <= 32) rows(std::integral_constant<int, 1>{});
         else if (P <= 48) rows(std::integral_constant<int, 2>{});
         else rows(std::integral_constant<int, 3>{});
+        __builtin_amdgcn_wave_barrier();  // (the prefix buffer is rewritten by the next record)
     }
 }
+#undef AC_CONST
 
 size_t ac_meta_bytes() { return sizeof(AcMeta); }
 
 static AcArgs ac_args(const uint32_t *eff, const uint64_t *noff, const char *names, uint32_t *scratch, uint32_t m,
                       uint32_t scap, int seq, int kind, uint32_t sel_lds = 0, int ident = 0, int direct = 0) {
+    // (direct: ntile for the nibble array)
     AcArgs A;
     A.ident = ident ? 1u : 0u;
     A.eff = eff;
@@ -644,17 +693,20 @@ static AcArgs ac_args(const uint32_t *eff, const uint64_t *noff, const char *nam
     A.kind = kind;
     A.sel_lds = sel_lds;
     A.direct = direct ? 1u : 0u;
+    A.ntile = (m + 63u) / 64u;
     return A;
 }
 
 hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
                          uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, int ident, int direct,
-                         uint8_t *status, uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s) {
+                         uint32_t *nib, uint8_t *status, uint64_t *len, void *meta, unsigned long long *counters,
+                         hipStream_t s) {
     if (l1 <= l0) return hipSuccess;
+    if (direct && !nib) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_ac_len, dim3(blocks), dim3(kAcThreads), 0, s, buf, data_start, line_end, l0, l1,
                        ac_args(eff, noff, names, scratch, m, scap, seq, kind, 0, ident, direct), status, len,
-                       static_cast<AcMeta *>(meta), counters);
+                       static_cast<AcMeta *>(meta), nib, counters);
     return hipGetLastError();
 }
 
@@ -676,23 +728,17 @@ hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *li
 
 hipError_t launch_ac_rows(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                           unsigned blocks, const uint32_t *eff, uint32_t m, int ident, const void *etab, uint32_t L,
-                          const uint8_t *status, const void *meta, const uint64_t *off, char *out, hipStream_t s) {
+                          const uint32_t *nib, const void *meta, const uint64_t *off, char *out, hipStream_t s) {
     if (l1 <= l0) return hipSuccess;
     const size_t lds = ac_rows_lds(m, ident);
     if (L > 11 || m > 4096 || lds > ac_rows_lds_max()) return hipErrorInvalidValue;
     const AcArgs A = ac_args(eff, nullptr, nullptr, nullptr, m, 0, 0, 0, 0, ident, 1);
-    if (ident)
-        hipLaunchKernelGGL(k_ac_rows<true>, dim3(blocks), dim3(kAcRowsThreads), lds, s, buf, data_start, line_end, l0, l1,
-                           A, static_cast<const v4u *>(etab), L, status, static_cast<const AcMeta *>(meta), off, out);
-    else
-        hipLaunchKernelGGL(k_ac_rows<false>, dim3(blocks), dim3(kAcRowsThreads), lds, s, buf, data_start, line_end, l0,
-                           l1, A, static_cast<const v4u *>(etab), L, status, static_cast<const AcMeta *>(meta), off, out);
+    hipLaunchKernelGGL(k_ac_rows, dim3(blocks), dim3(kAcRowsThreads), lds, s, buf, data_start, line_end, l0, l1,
+                       A, static_cast<const v4u *>(etab), L, nib, static_cast<const AcMeta *>(meta), off, out);
     return hipGetLastError();
 }
 
-size_t ac_rows_lds(uint32_t m, int ident) {
-    return 16 * (size_t)m + (ident ? 0 : 16 * (((size_t)m + 3) / 4)) + (size_t)kAcRowsWaves * ((m + 1023) / 1024) * kWave * 8;
-}
+size_t ac_rows_lds(uint32_t m, int) { return 16 * (size_t)m; }
 size_t ac_rows_lds_max() { return 131072; }
 int ac_rows_threads() { return kAcRowsThreads; }
 int ac_threads() { return kAcThreads; }

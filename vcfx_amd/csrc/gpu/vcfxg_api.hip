@@ -116,7 +116,7 @@ struct vcfxg_ctx {
     // VCFX_hwe_tester: hom-alt counts (dense, per walker), the host-recheck list and its length
     DevBuf hwe_aux, wk_aux, hwe_rc;
     // VCFX_allele_counter: slots' sample indices, name offsets and bytes, per-wave sample tables
-    DevBuf ac_eff, ac_noff, ac_names, ac_scratch, ac_etab;
+    DevBuf ac_eff, ac_noff, ac_names, ac_scratch, ac_etab, ac_nib;
     std::vector<uint32_t> ac_eff_host;
     std::vector<uint64_t> ac_noff_host;
     std::string ac_names_host;
@@ -2219,6 +2219,7 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
     if (!r) r = ensure(c, c->ac_names, nb + 1);
     if (!r) r = ensure(c, c->ac_scratch, 4 * scap * waves_per_block * blocks);
     if (!r && direct) r = ensure(c, c->ac_etab, 16 * m);
+    if (!r && direct) r = ensure(c, c->ac_nib, n * ((m + 63) / 64) * 32);  // (k_ac_len's counts for k_ac_rows)
     if (!r) r = af_buffers(c, L);
     if (!r) r = ensure(c, c->af_meta, vcfxg::ac_meta_bytes() * (L + 1));
     if (r) return r;
@@ -2234,7 +2235,8 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
     HIPCHK(c, vcfxg::launch_ac_len(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, (unsigned)blocks,
                                    P<uint32_t>(c->ac_eff), P<uint64_t>(c->ac_noff), P<char>(c->ac_names),
                                    P<uint32_t>(c->ac_scratch), (uint32_t)m, (uint32_t)scap, p->seq, p->kind,
-                                   ident ? 1 : 0, direct ? 1 : 0, P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->af_meta.p,
+                                   ident ? 1 : 0, direct ? 1 : 0, direct ? P<uint32_t>(c->ac_nib) : nullptr,
+                                   P<uint8_t>(c->status), P<uint64_t>(c->rowlen), c->af_meta.p,
                                    P<unsigned long long>(c->counters), c->stream));
     prof_end(c, "ac_len");
     r = exclusive_scan(c, P<uint64_t>(c->rowlen), P<uint64_t>(c->rowoff), (size_t)n + 1);
@@ -2252,7 +2254,7 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
         const unsigned rb = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + rw - 1) / rw, 1024));
         HIPCHK(c, vcfxg::launch_ac_rows(buf, (int64_t)c->data_start, P<uint64_t>(c->line_end), l0, l1, rb,
                                         P<uint32_t>(c->ac_eff), (uint32_t)m, ident ? 1 : 0, c->ac_etab.p, (uint32_t)L0,
-                                        P<uint8_t>(c->status), c->af_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
+                                        P<uint32_t>(c->ac_nib), c->af_meta.p, P<uint64_t>(c->rowoff), P<char>(c->text),
                                         c->stream));
     }
     if (!direct || tail[5])  // (the records k_ac_rows does not take)

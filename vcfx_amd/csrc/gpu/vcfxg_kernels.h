@@ -220,11 +220,13 @@ int ac_threads();
 hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
                          uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, int ident, int direct,
-                         uint8_t *status, uint64_t *len, void *meta, unsigned long long *counters, hipStream_t s);
+                         uint32_t *nib, uint8_t *status, uint64_t *len, void *meta, unsigned long long *counters,
+                         hipStream_t s);
 // direct != 0 (text rows, every name L <= 11 bytes, m <= 4096, ac_rows_lds <= ac_rows_lds_max()): k_ac_rows writes
 // the fixed-stride records whose prefix is 16..64 bytes (etab: per slot 16 B, the name at bytes
-// [11 - L, 11), then "\t0\t0\n", zeros in front) and k_ac_fmt the others; k_ac_len counts the
-// others' data lines in counters[4] (0: no k_ac_fmt launch needed)
+// [11 - L, 11), then "\t0\t0\n", zeros in front; nib: k_ac_len's counts, per line li - l0
+// ceil(m / 64) tiles of 8 dwords) and k_ac_fmt the others; k_ac_len counts the others' data lines
+// in counters[4] (0: no k_ac_fmt launch needed)
 hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                          unsigned blocks, const uint32_t *eff, const uint64_t *noff, const char *names,
                          uint32_t *scratch, uint32_t m, uint32_t scap, int seq, int kind, uint32_t sel_lds,
@@ -232,7 +234,7 @@ hipError_t launch_ac_fmt(const char *buf, int64_t data_start, const uint64_t *li
                          char *out, hipStream_t s);
 hipError_t launch_ac_rows(const char *buf, int64_t data_start, const uint64_t *line_end, uint64_t l0, uint64_t l1,
                           unsigned blocks, const uint32_t *eff, uint32_t m, int ident, const void *etab, uint32_t L,
-                          const uint8_t *status, const void *meta, const uint64_t *off, char *out, hipStream_t s);
+                          const uint32_t *nib, const void *meta, const uint64_t *off, char *out, hipStream_t s);
 size_t ac_rows_lds(uint32_t m, int ident);  // k_ac_rows' dynamic LDS bytes (m <= 4096)
 size_t ac_rows_lds_max();
 int ac_rows_threads();
