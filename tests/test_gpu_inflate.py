@@ -452,6 +452,37 @@ def test_af_streams_bgzf_through_the_ring(slot, batch, table):
         os.rmdir(d)
 
 
+def test_af_streams_bgzf_past_the_output_hint():
+    """A BGZF file that inflates to far more than the stream's 24x output hint (every genotype
+    0|0: deflate ratio ~100): batches launched per slot run until the output outgrows the buffer
+    (E_CAP), the rest inflates at the end after the buffer grows -- the grow waits for the
+    launched batches before it copies their output.  Same rows as the oracle on the
+    plain text, and the schedule log shows the staged inflate."""
+    oracle = Oracle()
+    names = "\t".join("S%d" % k for k in range(400))
+    rows = "".join("1\t%d\t.\tA\tC\t50\tPASS\t.\tGT\t%s\n" % (1000 + 7 * k, "\t".join(["0|0"] * 400)) for k in range(3000))
+    buf = ("##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" + names + "\n" + rows).encode()
+    comp = B.bgzf(buf, level=6)
+    assert len(buf) > 40 * len(comp), (len(buf), len(comp))
+    d = tempfile.mkdtemp(prefix="vcfx_bgzh_")
+    plain, bg, log = (os.path.join(d, x) for x in ("in.vcf", "in.vcf.gz", "sched.log"))
+    try:
+        with open(plain, "wb") as f:
+            f.write(buf)
+        with open(bg, "wb") as f:
+            f.write(comp)
+        want = oracle.run(["VCFX_allele_freq_calc", "-i", plain], b"")
+        env = dict(os.environ, VCFX_BGZF_STREAM_MIN="1", VCFXG_SCHEDULE_LOG=log, VCFX_BGZF_BATCH_MIN="1",
+                   VCFX_FILE_SLOT="4096")
+        r = subprocess.run([tool_binary("VCFX_allele_freq_calc"), "-i", bg], capture_output=True, env=env, timeout=120)
+        assert (r.stdout, r.returncode) == (want[0], want[2]), r.stderr[-500:]
+        assert "bgzf_inflate_staged" in open(log).read()
+    finally:
+        for x in os.listdir(d):
+            os.unlink(os.path.join(d, x))
+        os.rmdir(d)
+
+
 # ---- BGZF input split across ranks in its inflated bytes ------------------------------------------
 NGPU_CASES = [
     ["VCFX_allele_freq_calc", "-i", "{F}"], ["VCFX_record_filter", "--filter", "QUAL>=30", "-i", "{F}"],
