@@ -176,7 +176,7 @@ __device__ __forceinline__ void ac_slot_fast(const char *__restrict__ buf, int64
 __global__ __launch_bounds__(kAcThreads) void k_ac_len(const char *__restrict__ buf, int64_t data_start,
                                                        const uint64_t *__restrict__ line_end, uint64_t l0, uint64_t l1,
                                                        AcArgs A, uint8_t *__restrict__ status, uint64_t *__restrict__ len,
-                                                       AcMeta *__restrict__ meta, uint32_t *__restrict__ nib,
+                                                       AcMeta *__restrict__ meta,
                                                        unsigned long long *__restrict__ counters) {
     __shared__ int64_t scratch[kAcWaves][16];
     __shared__ unsigned long long red[5][kAcWaves];
@@ -258,65 +258,7 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_len(const char *__restrict__ 
                     text = wave_sum(text);
                 }
                 m.rows = rows;
-                const bool direct = ac_direct_rec(A, m);
-                slow += !direct;
-                if (direct && rows) {
-                    // k_ac_rows' counts: per tile of 64 rows 8 dwords, row i's nibble r | a << 2 at
-                    // bits 4 (i & 7) of dword (i & 63) / 8 (a lane past the last row: the last row's).
-                    // A lane makes one dword, rows 8 k .. 8 k + 7 of 512 (8 tiles' dwords are
-                    // contiguous: dword 8 t + j of the record is rows 64 t + 8 j ..): 8 loads, then a
-                    // store, no cross-lane step
-                    uint32_t *nb = nib + (li - l0) * (uint64_t)A.ntile * 8u;
-                    const uint32_t ns = m.ns;
-                    auto nib8 = [](const v4u &u) -> uint32_t {  // 4 GT dwords -> 4 nibbles
-                        uint32_t x = 0;
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const uint32_t c0 = u[q] & 255u, c2 = (u[q] >> 16) & 255u;
-                            const uint32_t r = (c0 == '0') + (c2 == '0'), a = (c0 - '1' < 9u) + (c2 - '1' < 9u);
-                            x |= (r | a << 2) << (4 * q);
-                        }
-                        return x;
-                    };
-                    // the identity selection over whole groups of 512 rows below the sample count:
-                    // a lane's 8 GT dwords are 32 contiguous bytes, 4 groups' loads in flight at once
-                    // (the memory parallelism this pass needs at 3 waves per SIMD)
-                    const uint32_t full = A.ident ? min(rows, ns) / (8 * kWave) * (8 * kWave) : 0u;
-                    uint32_t r0 = 0;
-                    for (; r0 + 4 * 8 * kWave <= full; r0 += 4 * 8 * kWave) {
-                        v4u u[8];
-#pragma unroll
-                        for (int h = 0; h < 4; h++) {
-                            const char *p = buf + S + 4 * (uint64_t)(r0 + h * 8 * kWave + 8u * lane());
-                            __builtin_memcpy(&u[2 * h], p, 16);  // (unaligned)
-                            __builtin_memcpy(&u[2 * h + 1], p + 16, 16);
-                        }
-#pragma unroll
-                        for (int h = 0; h < 4; h++)
-                            nb[(r0 + h * 8 * kWave) / 8u + lane()] = nib8(u[2 * h]) | nib8(u[2 * h + 1]) << 16;
-                    }
-                    for (; r0 < rows; r0 += 8 * kWave) {
-                        const uint32_t b = r0 + 8u * lane();
-                        uint32_t g[8], ev[8];
-#pragma unroll
-                        for (int q = 0; q < 8; q++) {
-                            const uint32_t i = min(b + q, rows - 1);
-                            ev[q] = A.ident ? i : A.eff[i];
-                            g[q] = __hip_atomic_load(
-                                reinterpret_cast<const uint32_t *>(buf + S + 4 * (uint64_t)(ev[q] < ns ? ev[q] : 0u)),
-                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);  // (unaligned: S + 4 e)
-                        }
-                        uint32_t x = 0;
-#pragma unroll
-                        for (int q = 0; q < 8; q++) {
-                            const uint32_t gc = ev[q] < ns ? g[q] : 0u;  // (a slot past the samples: 0 / 0)
-                            const uint32_t c0 = gc & 255u, c2 = (gc >> 16) & 255u;
-                            const uint32_t r = (c0 == '0') + (c2 == '0'), a = (c0 - '1' < 9u) + (c2 - '1' < 9u);
-                            x |= (r | a << 2) << (4 * q);
-                        }
-                        if (b < ((rows + 63u) & ~63u)) nb[r0 / 8u + lane()] = x;  // (the last tile whole)
-                    }
-                }
+                slow += !ac_direct_rec(A, m);  // (k_ac_nib then packs the direct records' counts)
                 if (A.kind == 1) {
                     sr = wave_sum(sr);
                     sa = wave_sum(sa);
@@ -565,6 +507,87 @@ __global__ __launch_bounds__(kAcThreads) void k_ac_fmt(const char *__restrict__ 
     }
 }
 
+// k_ac_nib: k_ac_rows' counts, for the records ac_direct_rec accepts (k_ac_len's meta), a wave per
+// line.  A kernel of its own: inside k_ac_len (149 VGPRs, 3 waves per SIMD) the pass cost 1.5 ms,
+// latency-bound per record; here a wave holds 4 groups' loads with few registers.
+constexpr int kAcNibThreads = 256;
+__global__ __launch_bounds__(kAcNibThreads) void k_ac_nib(const char *__restrict__ buf, uint64_t l0, uint64_t l1,
+                                                          AcArgs A, const AcMeta *__restrict__ meta,
+                                                          uint32_t *__restrict__ nib) {
+    const uint64_t wid = (uint64_t)uniform64((int64_t)((blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave));
+    const uint64_t nw = (gridDim.x * (uint64_t)blockDim.x) / kWave;
+    for (uint64_t lv = l0 + wid; lv < l1; lv += nw) {
+        const uint64_t li = (uint64_t)uniform64((int64_t)lv);
+        AcMeta m;
+        {
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(meta + li);
+            m.S = (uint64_t)w[0] | (uint64_t)w[1] << 32;
+            m.P = w[6];
+            m.rows = w[7];
+            m.ns = w[8];
+            m.lim = w[9];
+            m.kind = (uint8_t)w[10];
+        }
+        const uint32_t rows = (uint32_t)__builtin_amdgcn_readfirstlane((int)m.rows);
+        if (!ac_direct_rec(A, m) || rows == 0) continue;
+        const int64_t S = (int64_t)m.S;
+        // k_ac_rows' counts: per tile of 64 rows 8 dwords, row i's nibble r | a << 2 at
+        // bits 4 (i & 7) of dword (i & 63) / 8 (a lane past the last row: the last row's).
+        // A lane makes one dword, rows 8 k .. 8 k + 7 of 512 (8 tiles' dwords are
+        // contiguous: dword 8 t + j of the record is rows 64 t + 8 j ..): 8 loads, then a
+        // store, no cross-lane step
+        uint32_t *nb = nib + (li - l0) * (uint64_t)A.ntile * 8u;
+        const uint32_t ns = m.ns;
+        auto nib8 = [](const v4u &u) -> uint32_t {  // 4 GT dwords -> 4 nibbles
+            uint32_t x = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t c0 = u[q] & 255u, c2 = (u[q] >> 16) & 255u;
+                const uint32_t r = (c0 == '0') + (c2 == '0'), a = (c0 - '1' < 9u) + (c2 - '1' < 9u);
+                x |= (r | a << 2) << (4 * q);
+            }
+            return x;
+        };
+        // the identity selection over whole groups of 512 rows below the sample count:
+        // a lane's 8 GT dwords are 32 contiguous bytes, 4 groups' loads in flight at once
+        const uint32_t full = A.ident ? min(rows, ns) / (8 * kWave) * (8 * kWave) : 0u;
+        uint32_t r0 = 0;
+        for (; r0 + 4 * 8 * kWave <= full; r0 += 4 * 8 * kWave) {
+            v4u u[8];
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const char *p = buf + S + 4 * (uint64_t)(r0 + h * 8 * kWave + 8u * lane());
+                __builtin_memcpy(&u[2 * h], p, 16);  // (unaligned)
+                __builtin_memcpy(&u[2 * h + 1], p + 16, 16);
+            }
+#pragma unroll
+            for (int h = 0; h < 4; h++)
+                nb[(r0 + h * 8 * kWave) / 8u + lane()] = nib8(u[2 * h]) | nib8(u[2 * h + 1]) << 16;
+        }
+        for (; r0 < rows; r0 += 8 * kWave) {
+            const uint32_t b = r0 + 8u * lane();
+            uint32_t g[8], ev[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint32_t i = min(b + q, rows - 1);
+                ev[q] = A.ident ? i : A.eff[i];
+                g[q] = __hip_atomic_load(
+                    reinterpret_cast<const uint32_t *>(buf + S + 4 * (uint64_t)(ev[q] < ns ? ev[q] : 0u)),
+                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);  // (unaligned: S + 4 e)
+            }
+            uint32_t x = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint32_t gc = ev[q] < ns ? g[q] : 0u;  // (a slot past the samples: 0 / 0)
+                const uint32_t c0 = gc & 255u, c2 = (gc >> 16) & 255u;
+                const uint32_t r = (c0 == '0') + (c2 == '0'), a = (c0 - '1' < 9u) + (c2 - '1' < 9u);
+                x |= (r | a << 2) << (4 * q);
+            }
+            if (b < ((rows + 63u) & ~63u)) nb[r0 / 8u + lane()] = x;  // (the last tile whole)
+        }
+    }
+}
+
 // k_ac_rows: the text rows of the records ac_direct_rec accepts, straight from registers to the
 // output -- no LDS image, no copy-out.  Every row is P + L + 5 bytes: the record's prefix, the
 // slot's name, "\t" r "\t" a "\n".  A lane per row writes it as unaligned 16 B stores:
@@ -704,9 +727,14 @@ hipError_t launch_ac_len(const char *buf, int64_t data_start, const uint64_t *li
                          hipStream_t s) {
     if (l1 <= l0) return hipSuccess;
     if (direct && !nib) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ac_len, dim3(blocks), dim3(kAcThreads), 0, s, buf, data_start, line_end, l0, l1,
-                       ac_args(eff, noff, names, scratch, m, scap, seq, kind, 0, ident, direct), status, len,
-                       static_cast<AcMeta *>(meta), nib, counters);
+    const AcArgs A = ac_args(eff, noff, names, scratch, m, scap, seq, kind, 0, ident, direct);
+    hipLaunchKernelGGL(k_ac_len, dim3(blocks), dim3(kAcThreads), 0, s, buf, data_start, line_end, l0, l1, A, status,
+                       len, static_cast<AcMeta *>(meta), counters);
+    if (direct) {
+        const uint64_t w = (l1 - l0 + (kAcNibThreads / kWave) - 1) / (kAcNibThreads / kWave);
+        hipLaunchKernelGGL(k_ac_nib, dim3((unsigned)std::min<uint64_t>(w, 8192)), dim3(kAcNibThreads), 0, s, buf, l0,
+                           l1, A, static_cast<const AcMeta *>(meta), nib);
+    }
     return hipGetLastError();
 }
 
