@@ -2218,8 +2218,18 @@ int vcfxg_allele_counter(vcfxg_ctx *c, uint64_t l0, uint64_t l1, const vcfxg_ac_
     if (!r) r = ensure(c, c->ac_noff, 8 * (m + 1));
     if (!r) r = ensure(c, c->ac_names, nb + 1);
     if (!r) r = ensure(c, c->ac_scratch, 4 * scap * waves_per_block * blocks);
-    if (!r && direct) r = ensure(c, c->ac_etab, 16 * m);
-    if (!r && direct) r = ensure(c, c->ac_nib, n * ((m + 63) / 64) * 32);  // (k_ac_len's counts for k_ac_rows)
+    if (!r && direct) {
+        // the entries and k_ac_nib's counts for k_ac_rows (n x ceil(m / 64) x 32 B); without room
+        // for them every record takes k_ac_fmt
+        int rd = ensure(c, c->ac_etab, 16 * m);
+        if (!rd) rd = ensure(c, c->ac_nib, n * ((m + 63) / 64) * 32);
+        if (rd == VCFXG_E_NOMEM) {
+            (void)hipGetLastError();  // (a failed hipMalloc leaves its error to be read once)
+            c->err.clear();
+            direct = false;
+        } else
+            r = rd;
+    }
     if (!r) r = af_buffers(c, L);
     if (!r) r = ensure(c, c->af_meta, vcfxg::ac_meta_bytes() * (L + 1));
     if (r) return r;
